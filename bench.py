@@ -1,0 +1,262 @@
+"""Throughput bench: synced stereo frames/sec (detect + match + pose) @ 640x400 on MI355X.
+
+python bench.py --gpus N --steps K --warmup W   (N > 1 under torch.distributed.run, one rank/GPU)
+
+* workload (BASELINE.json configs[1], C2): one stereo pair 640x400 per GPU, K=2000 ORB-style
+  keypoints per image, synthetic room sequence (seed = rank); a *step* = one batch of
+  ``--batch`` synchronised stereo frames pushed through the whole hot path
+  (rectify -> pyramid -> FAST/NMS/top-K -> orientation + rBRIEF -> stereo + temporal Hamming
+  match -> sub-pixel refinement -> P3P-RANSAC -> Gauss-Newton -> pose chaining).
+* inputs are rendered on the host before timing and are resident in HBM (a triangle-wave
+  replay of ``--unique`` rendered frames, so consecutive frames stay consecutive in time).
+* N > 1: weak scaling, one stereo source per rank; each step also all-gathers the packed
+  keypoint + descriptor block of every rank over RCCL (the exchange step of SURVEY.md §8e).
+* timing: barrier + synchronize on both sides of exactly K steps; MAX over ranks.
+* roofline: per-kernel HIP-event timing of one batch run kernel by kernel on the same stream,
+  for the dominant kernel: algorithmic bytes / average duration vs 8 TB/s.
+* cpu_baseline (rank 0, N=1 context): the NumPy oracle on a bounded sample of the same frames.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from concurrent.futures import ProcessPoolExecutor
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+for _p in (ROOT, ROOT / "thor-slam_amd"):
+    if str(_p) not in sys.path:
+        sys.path.insert(0, str(_p))
+
+METRIC = "synced stereo frames/sec (detect+match+pose) @640×400, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0
+
+
+def _render_chunk(args):
+    seed, idx = args
+    from thor_slam_amd.synthetic import SyntheticStereoSource
+
+    src = SyntheticStereoSource(seed=seed, n_frames=max(idx) + 1)
+    return [src.render_stereo_sequence(1, start=i)[0] for i in idx]
+
+
+def render_frames(seed: int, n: int, workers: int) -> np.ndarray:
+    idx = list(range(n))
+    chunks = [idx[i::workers] for i in range(workers) if idx[i::workers]]
+    out = np.empty((n, 2, 400, 640), dtype=np.uint8)
+    if workers <= 1:
+        for c in chunks:
+            for i, fr in zip(c, _render_chunk((seed, c))):
+                out[i] = fr
+        return out
+    with ProcessPoolExecutor(max_workers=workers) as ex:
+        for c, frs in zip(chunks, ex.map(_render_chunk, [(seed, c) for c in chunks])):
+            for i, fr in zip(c, frs):
+                out[i] = fr
+    return out
+
+
+def triangle_indices(total: int, unique: int) -> np.ndarray:
+    period = 2 * (unique - 1)
+    k = np.arange(total) % period
+    return np.where(k < unique, k, period - k)
+
+
+def kernel_bytes(name: str, B: int, h, cfg, maps_identity: bool) -> float:
+    """Algorithmic (compulsory) HBM bytes of one launch of a kernel over B stereo frames."""
+    W, H, K = h.width, h.height, cfg.n_features
+    imgs = 2 * B
+    pyr = sum(w * hh for w, hh in h.level_wh)
+    if name == "rectify_pyramid":
+        maps = 0 if maps_identity else 2 * W * H * 8
+        return imgs * (W * H + pyr) + maps
+    if name == "detect":
+        return imgs * (pyr + pyr)          # read the levels, write the smoothed levels
+    if name == "select":
+        return imgs * K * 8                # write keypoints (candidate reads are data-dependent)
+    if name == "describe":
+        return imgs * K * (8 + 32)         # read keypoints, write descriptors
+    if name == "match":
+        return B * 2 * (2 * K * 32 + K * 8)  # two matchings: read query+train descriptors, write best/second
+    if name == "match_refine":
+        return B * 2 * K * (8 + 16)
+    if name == "pose":
+        return B * K * (4 + 16 + 8 * 8)
+    if name == "chain":
+        return B * 68 * 8
+    return 0.0
+
+
+def cpu_baseline(frames: np.ndarray, rect, cfg, budget_s: float) -> dict:
+    from oracle import numpy_slam as O
+
+    trk = O.OracleTracker(cfg, dict(fx=rect.fx, fy=rect.fy, cx=rect.cx, cy=rect.cy, baseline=rect.baseline,
+                                    map_l=rect.map_left, map_r=rect.map_right))
+    n = 0
+    t0 = time.perf_counter()
+    elapsed = 0.0
+    while elapsed < budget_s and n < len(frames):
+        trk.step(frames[n, 0], frames[n, 1])
+        n += 1
+        elapsed = time.perf_counter() - t0
+    return {"value": n / elapsed, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n} consecutive synthetic 640x400 stereo frames (seed 0), NumPy oracle, 1 process, "
+                      f"{elapsed:.1f} s"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64, help="stereo frames per step")
+    ap.add_argument("--unique", type=int, default=48, help="distinct rendered frames (triangle-wave replay)")
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU baseline (0 = skip)")
+    ap.add_argument("--kernel-reps", type=int, default=5)
+    ap.add_argument("--out", type=str, default="", help="also write the JSON line to this file")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from thor_slam_amd._lib import KERNELS, Handle
+    from thor_slam_amd.calib import extract_cameras, stereo_pairs, stereo_rectify
+    from thor_slam_amd.camera.rig import CameraRig
+    from thor_slam_amd.params import HipSlamConfig
+    from thor_slam_amd.synthetic import SyntheticStereoSource
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    cfg = HipSlamConfig()
+    B = args.batch
+    src = SyntheticStereoSource(seed=rank, n_frames=args.unique)
+    cams = extract_cameras(CameraRig([src]).calibration, 2)
+    (li, ri), = stereo_pairs(cams)
+    rect = stereo_rectify(cams[li], cams[ri])
+    workers = max(1, min(16, (os.cpu_count() or 2) // max(1, world), args.unique))
+    t_r = time.perf_counter()
+    uniq = render_frames(rank, args.unique, workers)
+    t_render = time.perf_counter() - t_r
+
+    total = (args.warmup + args.steps) * B
+    idx = torch.from_numpy(triangle_indices(total, args.unique)).cuda()
+    seq = torch.from_numpy(uniq).cuda().index_select(0, idx).contiguous()  # [total, 2, H, W] in HBM
+    h = Handle([rect], cfg, max_batch=B, device=local)
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    feat_bytes = 2 * (cfg.n_features * 40 + cfg.n_levels * 4)
+    gather_src = torch.empty((B * feat_bytes,), dtype=torch.uint8, device="cuda")
+    gather_dst = torch.empty((world * B * feat_bytes,), dtype=torch.uint8, device="cuda") if world > 1 else None
+
+    def step(s: int) -> None:
+        h.submit(seq[s * B].data_ptr(), B, sp)
+        if world > 1:
+            h.pack_features(gather_src.data_ptr(), sp)
+            dist.all_gather_into_tensor(gather_dst, gather_src)
+
+    for s in range(args.warmup):
+        step(s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.warmup, args.warmup + args.steps):
+        step(s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    res = h.read_poses(B)
+    ok_frac = float(np.mean(res["stats"][:, 0, 0] == 0))
+
+    # ---- per-kernel timing (HIP events on the launch stream) ----------------------------------
+    names = list(KERNELS)
+    acc = {k: 0.0 for k in names}
+    for rep in range(args.kernel_reps):
+        h.begin_batch(seq[(rep % args.steps) * B].data_ptr(), B)
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
+        evs[0].record(stream)
+        for i, k in enumerate(names):
+            h.run_kernel(k, sp)
+            evs[i + 1].record(stream)
+        h.end_batch()
+        torch.cuda.synchronize()
+        for i, k in enumerate(names):
+            acc[k] += evs[i].elapsed_time(evs[i + 1]) * 1e3  # us
+    per_kernel_us = {k: acc[k] / args.kernel_reps for k in names}
+    dom = max(per_kernel_us, key=per_kernel_us.get)
+    dom_bytes = kernel_bytes(dom, B, h, cfg, rect.is_identity)
+    achieved = dom_bytes / (per_kernel_us[dom] * 1e-6) / 1e9
+
+    frames_total = world * args.steps * B
+    out = {
+        "metric": METRIC,
+        "value": frames_total / elapsed,
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": f"synthetic: seeded room renderer, {args.unique} distinct 640x400 stereo frames per rank replayed "
+                "as a triangle wave, resident in HBM before timing",
+        "config": {
+            "workload": "C2: 1x stereo pair 640x400 per GPU, 2000 FAST/rBRIEF keypoints per image, 4 levels, "
+                        "stereo+temporal brute-force Hamming, P3P-RANSAC(128)+GN pose",
+            "frames_per_step": B,
+            "n_features": cfg.n_features,
+            "parallelism": f"one stereo source per GPU x{world}" + (" + RCCL all-gather of keypoints/descriptors" if world > 1 else ""),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dom,
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "algorithmic_bytes_per_launch": dom_bytes,
+            "avg_launch_us": per_kernel_us[dom],
+        },
+        "per_kernel_us_per_batch": per_kernel_us,
+        "tracking_ok_fraction_last_batch": ok_frac,
+        "render_s": t_render,
+    }
+    if rank == 0 and args.cpu_budget > 0:
+        out["cpu_baseline"] = cpu_baseline(uniq, rect, cfg, args.cpu_budget)
+        out["cpu_baseline"]["host_cpus_visible"] = os.cpu_count()
+    h.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.out:
+            Path(args.out).write_text(line + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,170 @@
+/*
+ * tslam.h — C-ABI of libtslam_hip.so, the MI355X (gfx950) hot path of the thor-slam back end.
+ *
+ * The reference has no FFI for this path: its hot path is a separate closed process (cuVSLAM)
+ * fed over ROS 2 topics by IsaacRosAdapter (thor_slam/slam/adapters/isaac_ros.py:327-430).
+ * Each entry point below replaces one piece of that hop, and is bound from Python with ctypes by
+ * thor_slam_amd/_lib.py (INTEGRATION.md shows the binding):
+ *
+ *   tslam_create        <- IsaacRosAdapter.initialize          isaac_ros.py:85-136 (publishers,
+ *                          camera_info K/D/P per camera :364-411) — here: rectification tables,
+ *                          rectified K and baseline of each stereo pair, device workspace
+ *   tslam_submit        <- the per-camera image publish loop   isaac_ros.py:336-413 — here: one
+ *                          batch of frames already in HBM, rectify -> detect -> describe ->
+ *                          match -> pose on the caller's stream
+ *   tslam_read_poses    <- IsaacRosAdapter._odom_cb            isaac_ros.py:308-325 (odometry +
+ *                          covariance) — here: per-frame relative/absolute poses, 6x6 covariance
+ *   tslam_reset         <- IsaacRosAdapter.reset               isaac_ros.py:438-442
+ *   tslam_destroy       <- IsaacRosAdapter.shutdown            isaac_ros.py:444-450
+ *   tslam_run_stage     stage-level entry points for parity tests (tslam_detect /
+ *                          describe / match / pose); tslam_detect ... tslam_pose are aliases
+ *   tslam_pack_features keypoint+descriptor block for the multi-GPU all-gather
+ *
+ * Conventions: every function returns 0 on success or a negative TSLAM_E* code;
+ * tslam_last_error() returns a thread-local message for the last failure.  A handle is not
+ * thread-safe (one submitting thread per handle).  All device pointers are HIP device memory
+ * on the handle's device; `stream` is a hipStream_t (NULL = default stream).  No function takes
+ * or returns framework (torch) types.
+ */
+#ifndef TSLAM_H
+#define TSLAM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TSLAM_ABI_VERSION 1
+
+#define TSLAM_OK 0
+#define TSLAM_EINVAL (-1)
+#define TSLAM_EHIP (-2)
+#define TSLAM_ENOMEM (-3)
+#define TSLAM_ESTATE (-4)
+
+/* pose status per frame (tslam_read_poses stats[4*i + 0]) */
+#define TSLAM_POSE_OK 0
+#define TSLAM_POSE_LOST 1
+#define TSLAM_POSE_INIT 2
+
+typedef struct tslam_handle tslam_handle;
+
+/* One rectified stereo pair (A1/A2 of SURVEY.md §8a). */
+typedef struct {
+    int32_t width, height;        /* raw == rectified image size, <= 2047 x 2047           */
+    double fx, fy, cx, cy;        /* rectified intrinsics shared by both cameras              */
+    double baseline;              /* metres, > 0                                              */
+    const int32_t* map_left;      /* host (H*W*2) int32 source (x, y) in 1/32 px, or NULL =   */
+    const int32_t* map_right;     /*   identity; copied to device at create                   */
+} tslam_stereo_desc;
+
+typedef struct {
+    int32_t n_features;           /* K per image                                              */
+    int32_t n_levels;             /* pyramid levels (1..6)                                    */
+    int32_t fast_threshold;       /* corner iff FAST score > threshold                        */
+    int32_t edge_margin;          /* >= 19                                                    */
+    int32_t max_hamming;          /* A6 acceptance                                            */
+    int32_t ratio_pct;
+    int32_t stereo_row_tol;
+    int32_t max_disparity;        /* level-0 px                                               */
+    int32_t temporal_window;      /* level-0 px                                               */
+    int32_t ransac_hypotheses;    /* <= 1024                                                  */
+    int32_t refine_iters;
+    int32_t min_inliers;
+    double ransac_thr_px;
+    uint64_t ransac_seed;
+    int32_t max_batch;            /* frames per tslam_submit                                  */
+    int32_t n_pairs;              /* stereo pairs per frame (cameras = 2 * n_pairs)           */
+} tslam_params;
+
+/* Buffers exposed for parity tests (tslam_buffer_info / tslam_copy_out / tslam_copy_in). */
+enum tslam_buffer {
+    TSLAM_BUF_PYRAMID = 0,   /* u8  [ring][cams][pyr_bytes]      rectified levels             */
+    TSLAM_BUF_SMOOTH = 1,    /* u8  [batch][cams][pyr_bytes]     5x5 binomial per level       */
+    TSLAM_BUF_KEYPOINTS = 2, /* u32 [ring][cams][K][2]           {x | y<<16, lvl | ang<<8 | score<<16} */
+    TSLAM_BUF_KCOUNT = 3,    /* i32 [ring][cams][levels]                                      */
+    TSLAM_BUF_DESC = 4,      /* u32 [ring][cams][K][8]                                        */
+    TSLAM_BUF_STEREO = 5,    /* i32 [ring][pairs][K]             right index or -1            */
+    TSLAM_BUF_DISP = 6,      /* f64 [ring][pairs][K]             refined level-0 disparity/NaN */
+    TSLAM_BUF_TEMPORAL = 7,  /* i32 [batch][pairs][K]            left(t-1) index or -1        */
+    TSLAM_BUF_TEMPORAL_UV = 8, /* f64 [batch][pairs][K][2]       refined (u, v) at t / NaN    */
+    TSLAM_BUF_CORR = 9,      /* f64 [batch][pairs][K][8]         X Y Z du dv bx by bz         */
+    TSLAM_BUF_POSE = 10,     /* f64 [batch][pairs][68]           T_rel[16] T_abs[16] cov[36]  */
+    TSLAM_BUF_STATS = 11,    /* i32 [batch][pairs][8]            status n_corr n_inl best ... */
+    TSLAM_BUF_QBEST = 12,    /* u32 [batch][pairs][2][K]         (dist<<16 | idx) stereo, temporal */
+    TSLAM_BUF_QSECOND = 13,  /* u32 [batch][pairs][2][K]                                      */
+    TSLAM_BUF_TBEST = 14,    /* u32 [batch][pairs][2][K]         train-side atomicMin         */
+    TSLAM_BUF_COUNT = 15
+};
+
+enum tslam_stage {
+    TSLAM_STAGE_RECTIFY = 0, /* raw -> pyramid                                                  */
+    TSLAM_STAGE_DETECT = 1,  /* pyramid -> smooth + candidates -> keypoints                     */
+    TSLAM_STAGE_DESCRIBE = 2,/* keypoints -> orientation + descriptors                          */
+    TSLAM_STAGE_MATCH = 3,   /* descriptors -> stereo/temporal matches + sub-pixel refinement   */
+    TSLAM_STAGE_POSE = 4,    /* matches -> correspondences -> RANSAC -> refine -> chain         */
+    TSLAM_STAGE_ALL = 5,
+    /* single kernels (per-kernel timing in bench.py; same order as STAGE_ALL) */
+    TSLAM_KERNEL_RECTIFY_PYRAMID = 10,
+    TSLAM_KERNEL_DETECT = 11,       /* includes the histogram memset */
+    TSLAM_KERNEL_SELECT = 12,
+    TSLAM_KERNEL_DESCRIBE = 13,
+    TSLAM_KERNEL_MATCH = 14,        /* includes the scratch memsets */
+    TSLAM_KERNEL_MATCH_REFINE = 15,
+    TSLAM_KERNEL_POSE = 16,
+    TSLAM_KERNEL_CHAIN = 17
+};
+
+const char* tslam_last_error(void);
+int tslam_abi_version(void);
+
+int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int device, tslam_handle** out);
+int tslam_destroy(tslam_handle* h);
+
+/* Run the whole hot path on `n_frames` (<= max_batch) frames.  `images` is device memory laid out
+ * [n_frames][2*n_pairs][H][W] u8 (left, right per pair).  Frames get consecutive global indices. */
+int tslam_submit(tslam_handle* h, const uint8_t* images, int n_frames, void* stream);
+
+/* Same, but stage by stage: set the batch, then run stages (parity tests inject/inspect buffers
+ * between stages with tslam_copy_in / tslam_copy_out). */
+int tslam_begin_batch(tslam_handle* h, const uint8_t* images, int n_frames);
+int tslam_run_stage(tslam_handle* h, int stage, void* stream);
+int tslam_end_batch(tslam_handle* h);
+
+int tslam_detect(tslam_handle* h, void* stream);   /* RECTIFY + DETECT */
+int tslam_describe(tslam_handle* h, void* stream);
+int tslam_match(tslam_handle* h, void* stream);
+int tslam_pose(tslam_handle* h, void* stream);
+
+int tslam_sync(tslam_handle* h);
+
+/* Results of the last submitted batch (blocks until it is done).  Per frame f and pair p
+ * (index f * n_pairs + p): T_rel[16] (cam_{t-1} -> cam_t), T_abs[16] (first left camera frame ->
+ * current left camera frame, row-major), cov[36] (rho, omega), stats[8] = {status, n_corr,
+ * n_inliers, best_count, best_hyp, global_frame, 0, 0}.  Any pointer may be NULL. */
+int tslam_read_poses(tslam_handle* h, double* T_rel, double* T_abs, double* cov, int32_t* stats);
+
+int tslam_reset(tslam_handle* h);
+int64_t tslam_frames_done(tslam_handle* h);
+
+int tslam_buffer_info(tslam_handle* h, int which, void** device_ptr, int64_t* bytes_total, int64_t* bytes_per_frame);
+int tslam_copy_out(tslam_handle* h, int which, int64_t offset, void* host_dst, int64_t bytes);
+int tslam_copy_in(tslam_handle* h, int which, int64_t offset, const void* host_src, int64_t bytes);
+/* ring slot of global frame g (for ring-indexed buffers) */
+int tslam_ring_slot(tslam_handle* h, int64_t global_frame);
+
+/* Layout facts for host-side decoding: fills out[0..15] with
+ * {W, H, n_levels, K, ring, batch, n_pairs, pyr_bytes, level offsets[6] (pyr), 0, 0}; and
+ * level_info[0..17] with {W_l, H_l, K_l} for l < 6. */
+int tslam_layout(tslam_handle* h, int64_t* out16, int32_t* level_info18);
+
+/* Copy the keypoints + descriptors + counts of the last batch into `dst` (device):
+ * [n_frames][cams] blocks of (K*8 + K*32 + levels*4) bytes.  Returns bytes per frame in *bytes. */
+int tslam_pack_features(tslam_handle* h, void* dst, int64_t* bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TSLAM_H */

@@ -1,0 +1,392 @@
+// k_image.hip — rows A2-A4 of SURVEY.md §8a on gfx950: rectify + pyramid, FAST-9 detect with
+// smoothing and NMS, exact per-level top-K.  Integer only; bit-exact with oracle/numpy_slam.py
+// (remap, pyramid, smooth, fast_scores, nms_keys, select_topk).
+//
+// Roofline: HBM-bound streaming (1 B/px in, 1.33 B/px pyramid out, 1.33 B/px smoothed out);
+// the per-pixel FAST arithmetic (~180 int ops) is far below the VALU ceiling.  Each block owns a
+// row band, stages it with its halo in LDS once (coalesced row loads), and does every stencil
+// (5x5 smoothing, 16-tap circle, 3x3 NMS) out of LDS.
+#include "tslam_common.h"
+
+// ---------------------------------------------------------------------------------------------
+// A2 + A3: rectify (fixed-point bilinear remap) and build all pyramid levels for a 32-row band.
+// grid (ceil(H/32), n*C), block 256.  32 = 2^5 keeps every level's rows of the band inside the
+// block (2x2 boxes never straddle bands) for up to 6 levels.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_rectify_pyramid(BatchCtx c) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int img = blockIdx.y;             // f * C + cam
+    const int cam = img % c.C;
+    const int f = img / c.C;
+    const int W = c.W, H = c.H;
+    const int y0 = blockIdx.x * TS_RECT_BAND;
+    const int rows0 = min(TS_RECT_BAND, H - y0);
+    const uint8_t* src = c.images + (size_t)img * W * H;
+    uint8_t* pyr = c.pyr + ((size_t)ring_slot(c, c.g0 + f) * c.C + cam) * c.g.pyr_bytes;
+    const bool has_map = (c.map_mask >> cam) & 1u;
+    const int32_t* map = c.maps + (size_t)cam * W * H * 2;
+
+    // level 0 into LDS + global
+    uint8_t* l0 = lds;
+    for (int idx = threadIdx.x; idx < rows0 * W; idx += blockDim.x) {
+        const int r = idx / W;
+        const int x = idx - r * W;
+        const int y = y0 + r;
+        int v;
+        if (has_map) {
+            const int2 m = *reinterpret_cast<const int2*>(map + ((size_t)y * W + x) * 2);
+            const int sx = m.x >> 5, sy = m.y >> 5;
+            const int fx = m.x & 31, fy = m.y & 31;
+            const int xa = min(max(sx, 0), W - 1), xb = min(max(sx + 1, 0), W - 1);
+            const int ya = min(max(sy, 0), H - 1), yb = min(max(sy + 1, 0), H - 1);
+            const int p00 = src[ya * W + xa], p01 = src[ya * W + xb];
+            const int p10 = src[yb * W + xa], p11 = src[yb * W + xb];
+            const int acc = p00 * (32 - fx) * (32 - fy) + p01 * fx * (32 - fy) + p10 * (32 - fx) * fy + p11 * fx * fy;
+            v = (acc + 512) >> 10;
+        } else {
+            v = src[y * W + x];
+        }
+        l0[r * W + x] = (uint8_t)v;
+        pyr[(size_t)y * W + x] = (uint8_t)v;
+    }
+    __syncthreads();
+
+    // levels 1.. from the previous level's LDS rows
+    const uint8_t* prev = l0;
+    int prevW = W;
+    uint8_t* cur = l0 + TS_RECT_BAND * W;
+    for (int l = 1; l < c.g.n_levels; ++l) {
+        const int Wl = c.g.W[l], Hl = c.g.H[l];
+        const int ly0 = y0 >> l;
+        const int lrows = min(TS_RECT_BAND >> l, Hl - ly0);
+        uint8_t* out = pyr + c.g.pyr_off[l];
+        for (int idx = threadIdx.x; idx < lrows * Wl; idx += blockDim.x) {
+            const int r = idx / Wl;
+            const int x = idx - r * Wl;
+            const int a = prev[(2 * r) * prevW + 2 * x] + prev[(2 * r) * prevW + 2 * x + 1] +
+                          prev[(2 * r + 1) * prevW + 2 * x] + prev[(2 * r + 1) * prevW + 2 * x + 1];
+            const uint8_t v = (uint8_t)((a + 2) >> 2);
+            cur[r * Wl + x] = v;
+            out[(size_t)(ly0 + r) * Wl + x] = v;
+        }
+        __syncthreads();
+        prev = cur;
+        prevW = Wl;
+        cur = cur + (TS_RECT_BAND >> l) * Wl;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// FAST-9 score of the centre pixel at LDS row r, column x (image pitch W).  Exact integer
+// definition: max over the 16 arcs of 9 contiguous circle pixels of
+// max(min(I_c - I_p), min(I_p - I_c)); callers only keep it when > threshold.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int fast9_score(const uint8_t* t, int W, int r, int x, int thr) {
+    const uint8_t* p = t + r * W + x;
+    const int c0 = p[0];
+    int d[16];
+    d[0] = p[-3 * W] - c0;      d[1] = p[-3 * W + 1] - c0; d[2] = p[-2 * W + 2] - c0; d[3] = p[-W + 3] - c0;
+    d[4] = p[3] - c0;           d[5] = p[W + 3] - c0;      d[6] = p[2 * W + 2] - c0;  d[7] = p[3 * W + 1] - c0;
+    d[8] = p[3 * W] - c0;       d[9] = p[3 * W - 1] - c0;  d[10] = p[2 * W - 2] - c0; d[11] = p[W - 3] - c0;
+    d[12] = p[-3] - c0;         d[13] = p[-W - 3] - c0;    d[14] = p[-2 * W - 2] - c0; d[15] = p[-3 * W - 1] - c0;
+    // every 9-arc contains circle index 0 or 8, and 4 or 12: a pixel is not a corner when
+    // both of either pair are within the threshold (score irrelevant then: it becomes 0).
+    const bool rej = (abs(d[0]) <= thr && abs(d[8]) <= thr) || (abs(d[4]) <= thr && abs(d[12]) <= thr);
+    if (rej) return 0;
+    int a2[16], b2[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        a2[k] = min(d[k], d[(k + 1) & 15]);
+        b2[k] = max(d[k], d[(k + 1) & 15]);
+    }
+    int a4[16], b4[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        a4[k] = min(a2[k], a2[(k + 2) & 15]);
+        b4[k] = max(b2[k], b2[(k + 2) & 15]);
+    }
+    int bright = -1024, darkmin = 1024;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int a8 = min(a4[k], a4[(k + 4) & 15]);
+        const int b8 = max(b4[k], b4[(k + 4) & 15]);
+        bright = max(bright, min(a8, d[(k + 8) & 15]));
+        darkmin = min(darkmin, max(b8, d[(k + 8) & 15]));
+    }
+    return max(max(bright, -darkmin), 0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// A3 smoothing + A4 FAST/NMS candidates for one 16-row band of one level.
+// grid (total_bands, n*C), block 256 (4 waves; wave w takes rows w, w+4, ...; lanes walk x).
+// LDS: image rows [y0-4, y0+20) (row-clamped), scores of rows [y0-1, y0+17).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_detect(BatchCtx c) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    __shared__ uint32_t s_hist[256];
+    __shared__ uint32_t s_count;
+    const int img = blockIdx.y;
+    const int cam = img % c.C;
+    const int f = img / c.C;
+    int l = 0;
+    while (l + 1 < c.g.n_levels && (int)blockIdx.x >= c.g.band_start[l + 1]) ++l;
+    const int band = blockIdx.x - c.g.band_start[l];
+    const int W = c.g.W[l], H = c.g.H[l];
+    const int y0 = band * TS_BAND_ROWS;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t img_off = ((size_t)ring_slot(c, c.g0 + f) * c.C + cam) * c.g.pyr_bytes + c.g.pyr_off[l];
+    const uint8_t* src = c.pyr + img_off;
+    uint8_t* smo = c.smo + ((size_t)f * c.C + cam) * c.g.pyr_bytes + c.g.pyr_off[l];
+    const int NR = TS_BAND_ROWS + 2 * TS_DET_HALO;
+    uint8_t* tile = lds;
+    uint8_t* score = lds + NR * W;
+
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_hist[i] = 0;
+    if (threadIdx.x == 0) s_count = 0;
+    for (int r = wave; r < NR; r += 4) {
+        const int y = min(max(y0 - TS_DET_HALO + r, 0), H - 1);
+        for (int x = lane; x < W; x += 64) tile[r * W + x] = src[(size_t)y * W + x];
+    }
+    __syncthreads();
+
+    // 5x5 binomial smoothing of the band rows (column clamp; rows already clamped in LDS)
+    const int rows_here = min(TS_BAND_ROWS, H - y0);
+    for (int r = wave; r < rows_here; r += 4) {
+        const int lr = r + TS_DET_HALO;
+        for (int x = lane; x < W; x += 64) {
+            const int xm2 = max(x - 2, 0), xm1 = max(x - 1, 0), xp1 = min(x + 1, W - 1), xp2 = min(x + 2, W - 1);
+            int acc = 0;
+            const int wk[5] = {1, 4, 6, 4, 1};
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const uint8_t* row = tile + (lr - 2 + k) * W;
+                const int h = row[xm2] + 4 * row[xm1] + 6 * row[x] + 4 * row[xp1] + row[xp2];
+                acc += wk[k] * h;
+            }
+            smo[(size_t)(y0 + r) * W + x] = (uint8_t)((acc + 128) >> 8);
+        }
+    }
+
+    // FAST scores (thresholded) for rows y0-1 .. y0+16
+    const int thr = c.fast_threshold;
+    for (int r = wave; r < TS_BAND_ROWS + 2; r += 4) {
+        const int y = y0 - 1 + r;
+        for (int x = lane; x < W; x += 64) {
+            int s = 0;
+            if (y >= 3 && y < H - 3 && x >= 3 && x < W - 3) {
+                s = fast9_score(tile, W, r + TS_DET_HALO - 1, x, thr);
+                if (s <= thr) s = 0;
+            }
+            score[r * W + x] = (uint8_t)s;
+        }
+    }
+    __syncthreads();
+
+    // 3x3 NMS (ties -> earlier raster position) inside the margin; emit keys
+    const int M = c.margin;
+    uint32_t* cand = c.cand + ((size_t)f * c.C + cam) * c.g.cand_total + c.g.cand_off[l] + (size_t)band * c.g.cand_cap[l];
+    const int ylo = max(y0, M), yhi = min(y0 + TS_BAND_ROWS, H - M);
+    for (int y = ylo + wave; y < yhi; y += 4) {
+        const int r = y - y0 + 1;
+        for (int x = M + lane; x < W - M; x += 64) {
+            const int p = score[r * W + x];
+            if (p == 0) continue;
+            const uint8_t* up = score + (r - 1) * W + x;
+            const uint8_t* mid = score + r * W + x;
+            const uint8_t* dn = score + (r + 1) * W + x;
+            const bool keep = up[-1] < p && up[0] < p && up[1] < p && mid[-1] < p &&
+                              mid[1] <= p && dn[-1] <= p && dn[0] <= p && dn[1] <= p;
+            if (keep) {
+                const uint32_t key = ((uint32_t)(255 - p) << 22) | ((uint32_t)y << 11) | (uint32_t)x;
+                const uint32_t slot = atomicAdd(&s_count, 1u);
+                cand[slot] = key;
+                atomicAdd(&s_hist[255 - p], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) c.ccount[((size_t)f * c.C + cam) * c.g.total_bands + blockIdx.x] = s_count;
+    uint32_t* gh = c.hist + (((size_t)f * c.C + cam) * c.g.n_levels + l) * 256;
+    for (int i = threadIdx.x; i < 256; i += blockDim.x)
+        if (s_hist[i]) atomicAdd(&gh[i], s_hist[i]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// A4 top-K: exact K_l smallest keys of an image level, sorted ascending.
+// Radix select on (score bin, y, x) histograms, then a bitonic sort of the survivors in LDS.
+// grid (n_levels, n*C), block 256.
+// ---------------------------------------------------------------------------------------------
+#define SEL_THREADS 256
+#define SEL_MAX 8192
+
+// smallest bin b with sum(h[0..b]) >= need; returns b and the count strictly before it.
+__device__ void block_find_crossing(const uint32_t* h, int nbins, uint32_t need, uint32_t* s_part,
+                                    int* out_bin, uint32_t* out_before) {
+    const int per = (nbins + SEL_THREADS - 1) / SEL_THREADS;
+    const int b0 = threadIdx.x * per;
+    uint32_t local = 0;
+    for (int b = b0; b < min(b0 + per, nbins); ++b) local += h[b];
+    s_part[threadIdx.x] = local;
+    __syncthreads();
+    // inclusive Hillis-Steele scan over the 256 partial sums
+    for (int o = 1; o < SEL_THREADS; o <<= 1) {
+        const uint32_t v = threadIdx.x >= (unsigned)o ? s_part[threadIdx.x - o] : 0u;
+        __syncthreads();
+        s_part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    const uint32_t incl = s_part[threadIdx.x];
+    const uint32_t excl = incl - local;
+    if (excl < need && incl >= need) {
+        uint32_t cum = excl;
+        for (int b = b0; b < min(b0 + per, nbins); ++b) {
+            if (cum + h[b] >= need) {
+                *out_bin = b;
+                *out_before = cum;
+                break;
+            }
+            cum += h[b];
+        }
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
+    __shared__ uint32_t s_keys[SEL_MAX];
+    __shared__ uint32_t s_h[2048];
+    __shared__ uint32_t s_part[SEL_THREADS];
+    __shared__ int s_bin;
+    __shared__ uint32_t s_before, s_nsel;
+    const int l = blockIdx.x;
+    const int img = blockIdx.y;
+    const int cam = img % c.C;
+    const int f = img / c.C;
+    const int Kl = c.g.Kq[l];
+    const uint32_t* cand = c.cand + ((size_t)f * c.C + cam) * c.g.cand_total + c.g.cand_off[l];
+    const uint32_t* cnt = c.ccount + ((size_t)f * c.C + cam) * c.g.total_bands + c.g.band_start[l];
+    const uint32_t* gh = c.hist + (((size_t)f * c.C + cam) * c.g.n_levels + l) * 256;
+    const int nb = c.g.nbands[l];
+    const int cap = c.g.cand_cap[l];
+
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_h[i] = gh[i];
+    __syncthreads();
+    uint32_t total = 0;
+    for (int i = 0; i < 256; ++i) total += s_h[i];   // uniform per thread (LDS broadcast)
+
+    uint32_t thresh = 0xFFFFFFFFu;  // inclusive max key taken
+    if (total > (uint32_t)Kl) {
+        block_find_crossing(s_h, 256, (uint32_t)Kl, s_part, &s_bin, &s_before);
+        const uint32_t sbin = (uint32_t)s_bin;  // = 255 - s*
+        const uint32_t need = (uint32_t)Kl - s_before;
+        const uint32_t eq = s_h[sbin];
+        thresh = (sbin << 22) | 0x3FFFFFu;
+        if (need < eq) {
+            // radix on y among keys of this score
+            __syncthreads();
+            for (int i = threadIdx.x; i < 2048; i += blockDim.x) s_h[i] = 0;
+            __syncthreads();
+            for (int b = 0; b < nb; ++b) {
+                const uint32_t n = cnt[b];
+                const uint32_t* seg = cand + (size_t)b * cap;
+                for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+                    const uint32_t k = seg[i];
+                    if ((k >> 22) == sbin) atomicAdd(&s_h[(k >> 11) & 2047u], 1u);
+                }
+            }
+            __syncthreads();
+            block_find_crossing(s_h, 2048, need, s_part, &s_bin, &s_before);
+            const uint32_t ystar = (uint32_t)s_bin;
+            const uint32_t need2 = need - s_before;
+            const uint32_t eq2 = s_h[ystar];
+            thresh = (sbin << 22) | (ystar << 11) | 2047u;
+            if (need2 < eq2) {
+                __syncthreads();
+                for (int i = threadIdx.x; i < 2048; i += blockDim.x) s_h[i] = 0;
+                __syncthreads();
+                for (int b = 0; b < nb; ++b) {
+                    const uint32_t n = cnt[b];
+                    const uint32_t* seg = cand + (size_t)b * cap;
+                    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+                        const uint32_t k = seg[i];
+                        if ((k >> 11) == ((sbin << 11) | ystar)) atomicAdd(&s_h[k & 2047u], 1u);
+                    }
+                }
+                __syncthreads();
+                block_find_crossing(s_h, 2048, need2, s_part, &s_bin, &s_before);
+                thresh = (sbin << 22) | (ystar << 11) | (uint32_t)s_bin;
+            }
+        }
+    }
+    // collect survivors
+    if (threadIdx.x == 0) s_nsel = 0;
+    __syncthreads();
+    for (int b = 0; b < nb; ++b) {
+        const uint32_t n = cnt[b];
+        const uint32_t* seg = cand + (size_t)b * cap;
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+            const uint32_t k = seg[i];
+            if (k <= thresh) {
+                const uint32_t slot = atomicAdd(&s_nsel, 1u);
+                if (slot < SEL_MAX) s_keys[slot] = k;
+            }
+        }
+    }
+    __syncthreads();
+    const int nsel = min((int)s_nsel, Kl);
+    int np2 = 1;
+    while (np2 < nsel) np2 <<= 1;
+    for (int i = nsel + threadIdx.x; i < np2; i += blockDim.x) s_keys[i] = 0xFFFFFFFFu;
+    __syncthreads();
+    // bitonic sort ascending
+    for (int k = 2; k <= np2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < np2; i += blockDim.x) {
+                const int p = i ^ j;
+                if (p > i) {
+                    const uint32_t a = s_keys[i], b = s_keys[p];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) {
+                        s_keys[i] = b;
+                        s_keys[p] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    const int slot = ring_slot(c, c.g0 + f);
+    uint32_t* kp = c.kps + (((size_t)slot * c.C + cam) * c.g.K + c.g.koff[l]) * 2;
+    for (int i = threadIdx.x; i < Kl; i += blockDim.x) {
+        uint32_t xy = 0, meta = (uint32_t)l;   // padding entries keep their level
+        if (i < nsel) {
+            const uint32_t k = s_keys[i];
+            xy = (k & 2047u) | (((k >> 11) & 2047u) << 16);
+            meta = (uint32_t)l | ((255u - (k >> 22)) << 16);
+        }
+        kp[2 * i] = xy;
+        kp[2 * i + 1] = meta;
+    }
+    if (threadIdx.x == 0) c.kcount[((size_t)slot * c.C + cam) * c.g.n_levels + l] = nsel;
+}
+
+// ---------------------------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------------------------
+void launch_rectify_pyramid(const BatchCtx& c, hipStream_t s) {
+    size_t lds = 0;
+    for (int l = 0; l < c.g.n_levels; ++l) lds += (size_t)(TS_RECT_BAND >> l) * c.g.W[l];
+    dim3 grid((c.H + TS_RECT_BAND - 1) / TS_RECT_BAND, c.n * c.C);
+    hipLaunchKernelGGL(k_rectify_pyramid, grid, dim3(256), lds, s, c);
+}
+
+void launch_detect(const BatchCtx& c, hipStream_t s) {
+    const size_t lds = (size_t)(TS_BAND_ROWS + 2 * TS_DET_HALO + TS_BAND_ROWS + 2) * c.g.W[0];
+    dim3 grid(c.g.total_bands, c.n * c.C);
+    (void)hipMemsetAsync(c.hist, 0, sizeof(uint32_t) * 256 * c.g.n_levels * c.C * (size_t)c.n, s);
+    hipLaunchKernelGGL(k_detect, grid, dim3(256), lds, s, c);
+}
+
+void launch_select(const BatchCtx& c, hipStream_t s) {
+    dim3 grid(c.g.n_levels, c.n * c.C);
+    hipLaunchKernelGGL(k_select, grid, dim3(SEL_THREADS), 0, s, c);
+}

@@ -1,0 +1,550 @@
+// k_pose.hip — row A7 of SURVEY.md §8a: correspondences (t-1 stereo 3D <-> t refined 2D),
+// P3P-RANSAC with a counter-based RNG, Gauss-Newton refinement, pose chaining.
+//
+// FP64 throughout, compiled with -ffp-contract=off, and written operation-for-operation like
+// oracle/numpy_slam.py (p3p, _roots, count_inliers, refine, solve6, cayley): only IEEE +,-,*,/
+// and sqrt are used, so the hypotheses, their inlier counts and the winning hypothesis are
+// bit-identical to the oracle; the refined pose differs only by the summation order of the
+// normal equations (~1e-16 relative).
+//
+// One 256-thread block per (frame, pair).  Phase A: thread h solves P3P for hypothesis h and
+// parks its <= 4 poses in LDS.  Phase B: every thread scores 4H/256 poses against all
+// correspondences (wave-uniform addresses -> broadcast loads).  Phase C: block argmax, then
+// Gauss-Newton with a block reduction of the 6x6 normal equations per iteration.
+#include "tslam_common.h"
+
+#define P3P_VMAX 1000.0
+#define P3P_BISECT 60
+
+struct V3 {
+    double x, y, z;
+};
+
+__device__ __forceinline__ double dot3(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ V3 sub3(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ V3 cross3(V3 a, V3 b) {
+    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ V3 norm3(V3 a) {
+    const double n = sqrt(dot3(a, a));
+    return {a.x / n, a.y / n, a.z / n};
+}
+__device__ __forceinline__ void frame3(V3 p1, V3 p2, V3 p3, V3* e) {
+    e[0] = norm3(sub3(p2, p1));
+    e[2] = norm3(cross3(e[0], sub3(p3, p1)));
+    e[1] = cross3(e[2], e[0]);
+}
+__device__ __forceinline__ double comp(V3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+
+template <int N>
+__device__ __forceinline__ double horner(const double* c, double v) {
+    double p = c[N];
+#pragma unroll
+    for (int k = N - 1; k >= 0; --k) p = p * v + c[k];
+    return p;
+}
+
+// Real roots in (lo, hi) of sum c_k v^k, ascending, NaN-padded (mirrors oracle._roots).
+template <int N>
+__device__ void real_roots(const double* c, double lo, double hi, double* out) {
+    if constexpr (N == 1) {
+        const double r = -c[0] / c[1];
+        out[0] = (c[1] != 0.0 && r > lo && r < hi) ? r : __builtin_nan("");
+    } else {
+        double dc[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) dc[k] = c[k + 1] * (double)(k + 1);
+        double crit[N - 1];
+        real_roots<N - 1>(dc, lo, hi, crit);
+        double pts[N + 1];
+        pts[0] = lo;
+#pragma unroll
+        for (int i = 0; i < N - 1; ++i) pts[i + 1] = __builtin_isnan(crit[i]) ? hi : crit[i];
+        pts[N] = hi;
+        double r[N];
+        int nr = 0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            double a = pts[i], b = pts[i + 1];
+            const bool sa = horner<N>(c, a) > 0.0;
+            const bool sb = horner<N>(c, b) > 0.0;
+            if (sa != sb && b > a) {
+                for (int it = 0; it < P3P_BISECT; ++it) {
+                    const double m = 0.5 * (a + b);
+                    const bool sm = horner<N>(c, m) > 0.0;
+                    if (sm == sa) a = m; else b = m;
+                }
+                r[nr++] = 0.5 * (a + b);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < N; ++i) out[i] = i < nr ? r[i] : __builtin_nan("");
+    }
+}
+
+struct Pose {
+    double r[9];
+    double t[3];
+};
+
+// Grunert P3P (oracle.p3p): up to 4 poses ordered by ascending v = s3/s1; returns validity mask.
+__device__ int p3p_solve(const V3* pw, const V3* f, Pose* out) {
+    const V3 d12 = sub3(pw[1], pw[2]), d02 = sub3(pw[0], pw[2]), d01 = sub3(pw[0], pw[1]);
+    const double a2 = dot3(d12, d12), b2 = dot3(d02, d02), c2 = dot3(d01, d01);
+    const double ca = dot3(f[1], f[2]), cb = dot3(f[0], f[2]), cg = dot3(f[0], f[1]);
+    const double kk = (a2 - c2) / b2;
+    const double kc = c2 / b2;
+    const double n0 = 1.0 + kk, n1 = (-2.0 * kk) * cb, n2 = kk - 1.0;
+    const double d0 = cg, d1 = -ca;
+    const double g0 = 1.0 - kc, g1 = (2.0 * kc) * cb, g2 = -kc;
+    double q[5];
+    q[4] = n2 * n2;
+    q[3] = (2.0 * n1) * n2;
+    q[2] = n1 * n1 + (2.0 * n0) * n2;
+    q[1] = (2.0 * n0) * n1;
+    q[0] = n0 * n0;
+    const double m = -4.0 * cg;
+    q[3] = q[3] + m * (n2 * d1);
+    q[2] = q[2] + m * (n1 * d1 + n2 * d0);
+    q[1] = q[1] + m * (n0 * d1 + n1 * d0);
+    q[0] = q[0] + m * (n0 * d0);
+    const double e0 = d0 * d0, e1 = (2.0 * d0) * d1, e2 = d1 * d1;
+    q[4] = q[4] + 4.0 * (e2 * g2);
+    q[3] = q[3] + 4.0 * (e1 * g2 + e2 * g1);
+    q[2] = q[2] + 4.0 * ((e0 * g2 + e1 * g1) + e2 * g0);
+    q[1] = q[1] + 4.0 * (e0 * g1 + e1 * g0);
+    q[0] = q[0] + 4.0 * (e0 * g0);
+    double roots[4];
+    real_roots<4>(q, 0.0, P3P_VMAX, roots);
+    V3 fw[3];
+    frame3(pw[0], pw[1], pw[2], fw);
+    int mask = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const double v = roots[s];
+        const double num = (n0 + n1 * v) + n2 * (v * v);
+        const double den = 2.0 * (cg - ca * v);
+        const double u = num / den;
+        const double s1sq = b2 / ((1.0 + v * v) - (2.0 * cb) * v);
+        bool good = !__builtin_isnan(v) && u > 0.0 && s1sq > 0.0 && __builtin_isfinite(u) && __builtin_isfinite(s1sq);
+        const double s1 = sqrt(good ? s1sq : 1.0);
+        const double s2 = u * s1, s3 = v * s1;
+        const V3 pc0 = {f[0].x * s1, f[0].y * s1, f[0].z * s1};
+        const V3 pc1 = {f[1].x * s2, f[1].y * s2, f[1].z * s2};
+        const V3 pc2 = {f[2].x * s3, f[2].y * s3, f[2].z * s3};
+        V3 fc[3];
+        frame3(pc0, pc1, pc2, fc);
+        Pose& P = out[s];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                P.r[3 * i + j] = (comp(fc[0], i) * comp(fw[0], j) + comp(fc[1], i) * comp(fw[1], j)) + comp(fc[2], i) * comp(fw[2], j);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const double rp = (P.r[3 * i] * pw[0].x + P.r[3 * i + 1] * pw[0].y) + P.r[3 * i + 2] * pw[0].z;
+            P.t[i] = comp(pc0, i) - rp;
+        }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) good = good && __builtin_isfinite(P.r[i]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) good = good && __builtin_isfinite(P.t[i]);
+        if (good) mask |= 1 << s;
+    }
+    return mask;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x = x + 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// inlier test (oracle.count_inliers / count_inliers_mask)
+__device__ __forceinline__ bool is_inlier(const double* R, const double* t, const double* cr, double fx, double fy, double thr2) {
+    const double X = cr[0], Y = cr[1], Z = cr[2], du = cr[3], dv = cr[4];
+    const double xc = ((R[0] * X + R[1] * Y) + R[2] * Z) + t[0];
+    const double yc = ((R[3] * X + R[4] * Y) + R[5] * Z) + t[1];
+    const double zc = ((R[6] * X + R[7] * Y) + R[8] * Z) + t[2];
+    const double ex = fx * xc + du * zc;
+    const double ey = fy * yc + dv * zc;
+    const double e2 = ex * ex + ey * ey;
+    const double lim = thr2 * (zc * zc);
+    return zc > 0.0 && e2 < lim;
+}
+
+// Cholesky solve of H x = g (oracle.solve6); returns false when H is not positive definite.
+__device__ bool solve6(const double* Hm, const double* g, double* x, double* L) {
+    for (int j = 0; j < 6; ++j) {
+        double s = Hm[j * 6 + j];
+        for (int k = 0; k < j; ++k) s = s - L[j * 6 + k] * L[j * 6 + k];
+        if (!(s > 0.0)) return false;
+        L[j * 6 + j] = sqrt(s);
+        for (int i = j + 1; i < 6; ++i) {
+            double t = Hm[i * 6 + j];
+            for (int k = 0; k < j; ++k) t = t - L[i * 6 + k] * L[j * 6 + k];
+            L[i * 6 + j] = t / L[j * 6 + j];
+        }
+    }
+    double y[6];
+    for (int i = 0; i < 6; ++i) {
+        double s = g[i];
+        for (int k = 0; k < i; ++k) s = s - L[i * 6 + k] * y[k];
+        y[i] = s / L[i * 6 + i];
+    }
+    for (int i = 5; i >= 0; --i) {
+        double s = y[i];
+        for (int k = i + 1; k < 6; ++k) s = s - L[k * 6 + i] * x[k];
+        x[i] = s / L[i * 6 + i];
+    }
+    return true;
+}
+
+#define POSE_THREADS 256
+#define N_ACC 29   // 21 (upper H) + 6 (g) + 1 (sq) + 1 (count)
+
+__global__ __launch_bounds__(POSE_THREADS) void k_pose(BatchCtx c) {
+    extern __shared__ __attribute__((aligned(16))) double s_pose[];   // [4H][12]
+    __shared__ int s_scan[POSE_THREADS];
+    __shared__ uint32_t s_wbest[4];
+    __shared__ double s_red[4][N_ACC];
+    __shared__ double s_R[9], s_t[3], s_H[36], s_misc[4];
+    __shared__ int s_flag;
+
+    const int fp = blockIdx.x;
+    const int p = fp % c.P;
+    const int f = fp / c.P;
+    const int64_t g = c.g0 + f;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int K = c.g.K;
+    double* pout = c.pose + (size_t)fp * TS_POSE_DOUBLES;
+    int32_t* sout = c.stats + (size_t)fp * TS_STATS_INTS;
+    const PairCalib cal = c.calib[p];
+    const double fx = cal.fx, fy = cal.fy, cx = cal.cx, cy = cal.cy;
+
+    // defaults: identity, zero covariance
+    for (int i = tid; i < TS_POSE_DOUBLES; i += POSE_THREADS) pout[i] = (i < 16 && (i % 5) == 0) ? 1.0 : 0.0;
+    if (g == 0) {
+        if (tid == 0) {
+            sout[0] = 2; sout[1] = 0; sout[2] = 0; sout[3] = 0; sout[4] = -1; sout[5] = (int)g; sout[6] = 0; sout[7] = 0;
+        }
+        return;
+    }
+    const int pslot = ring_slot(c, g - 1);
+    const int32_t* tm = c.temporal + ((size_t)f * c.P + p) * K;
+    const double* tuv = c.tuv + ((size_t)f * c.P + p) * K * 2;
+    const double* dprev = c.disp + ((size_t)pslot * c.P + p) * K;
+    const uint32_t* kprev = c.kps + ((size_t)pslot * c.C + 2 * p) * K * 2;
+    double* corr = c.corr + ((size_t)f * c.P + p) * K * TS_CORR_DOUBLES;
+
+    // ---- correspondences, ordered by the current-frame keypoint index ----------------------
+    int n = 0;
+    for (int base = 0; base < K; base += POSE_THREADS) {
+        const int j = base + tid;
+        int flag = 0;
+        int i = -1;
+        double u = 0.0, v = 0.0, d = 0.0;
+        if (j < K) {
+            i = tm[j];
+            if (i >= 0) {
+                d = dprev[i];
+                u = tuv[2 * j];
+                v = tuv[2 * j + 1];
+                flag = __builtin_isfinite(d) && __builtin_isfinite(u) && __builtin_isfinite(v);
+            }
+        }
+        s_scan[tid] = flag;
+        __syncthreads();
+        for (int o = 1; o < POSE_THREADS; o <<= 1) {
+            const int add = tid >= o ? s_scan[tid - o] : 0;
+            __syncthreads();
+            s_scan[tid] += add;
+            __syncthreads();
+        }
+        const int pos = n + s_scan[tid] - flag;
+        const int tot = s_scan[POSE_THREADS - 1];
+        if (flag) {
+            const uint32_t xy = kprev[2 * i], meta = kprev[2 * i + 1];
+            const int lv = meta & 0xFF;
+            const double sc = (double)(1 << lv);
+            const double ul = ((double)(xy & 0xFFFF) + 0.5) * sc - 0.5;
+            const double vl = ((double)(xy >> 16) + 0.5) * sc - 0.5;
+            const double z = cal.fxb / d;
+            const double x = (ul - cx) * z / fx;
+            const double y = (vl - cy) * z / fy;
+            const double bx = (u - cx) / fx;
+            const double by = (v - cy) / fy;
+            const double nn = sqrt((bx * bx + by * by) + 1.0);
+            double* cr = corr + (size_t)pos * TS_CORR_DOUBLES;
+            cr[0] = x; cr[1] = y; cr[2] = z; cr[3] = cx - u; cr[4] = cy - v;
+            cr[5] = bx / nn; cr[6] = by / nn; cr[7] = 1.0 / nn;
+        }
+        n += tot;
+        __syncthreads();
+    }
+    __threadfence_block();
+    const int min_corr = max(6, c.pp.min_inliers);
+    if (n < min_corr) {
+        if (tid == 0) {
+            sout[0] = 1; sout[1] = n; sout[2] = 0; sout[3] = 0; sout[4] = -1; sout[5] = (int)g; sout[6] = 0; sout[7] = 0;
+        }
+        return;
+    }
+
+    // ---- phase A: P3P per hypothesis -----------------------------------------------------------
+    const int H = c.pp.n_hyp;
+    const uint64_t base_rng = splitmix64(c.pp.seed ^ ((uint64_t)g * 0x9E3779B97F4A7C15ull));
+    for (int h = tid; h < H; h += POSE_THREADS) {
+        uint32_t r[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) r[k] = (uint32_t)(splitmix64(base_rng ^ ((uint64_t)h * 4ull + (uint64_t)k)) >> 32);
+        const uint32_t un = (uint32_t)n;
+        int i0 = (int)(r[0] % un);
+        int i1 = (int)(r[1] % (un - 1));
+        i1 += (i1 >= i0);
+        int i2 = (int)(r[2] % (un - 2));
+        const int lo = min(i0, i1), hi = max(i0, i1);
+        i2 += (i2 >= lo);
+        i2 += (i2 >= hi);
+        const int idx[3] = {i0, i1, i2};
+        V3 pw[3], fb[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double* cr = corr + (size_t)idx[k] * TS_CORR_DOUBLES;
+            pw[k] = {cr[0], cr[1], cr[2]};
+            fb[k] = {cr[5], cr[6], cr[7]};
+        }
+        Pose sol[4];
+        const int mask = p3p_solve(pw, fb, sol);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            double* dst = s_pose + (size_t)(4 * h + s) * 12;
+            if ((mask >> s) & 1) {
+#pragma unroll
+                for (int k = 0; k < 9; ++k) dst[k] = sol[s].r[k];
+                dst[9] = sol[s].t[0]; dst[10] = sol[s].t[1]; dst[11] = sol[s].t[2];
+            } else {
+                dst[0] = __builtin_nan("");
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- phase B: score every candidate pose -------------------------------------------------
+    const double thr2 = c.pp.thr2;
+    uint32_t my_best = 0;
+    for (int pi = tid; pi < 4 * H; pi += POSE_THREADS) {
+        const double* ps = s_pose + (size_t)pi * 12;
+        int cnt = -1;
+        if (!__builtin_isnan(ps[0])) {
+            double R[9], t[3];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) R[k] = ps[k];
+            t[0] = ps[9]; t[1] = ps[10]; t[2] = ps[11];
+            cnt = 0;
+            for (int ci = 0; ci < n; ++ci) cnt += is_inlier(R, t, corr + (size_t)ci * TS_CORR_DOUBLES, fx, fy, thr2) ? 1 : 0;
+        }
+        const uint32_t key = ((uint32_t)(cnt + 1) << 12) | (uint32_t)(4095 - pi);
+        my_best = key > my_best ? key : my_best;
+    }
+    // block argmax (ties -> lowest pose index)
+    uint32_t wb = my_best;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t other = (uint32_t)__shfl_xor((int)wb, o, 64);
+        wb = other > wb ? other : wb;
+    }
+    if (lane == 0) s_wbest[wave] = wb;
+    __syncthreads();
+    uint32_t best = s_wbest[0];
+    for (int w = 1; w < 4; ++w) best = s_wbest[w] > best ? s_wbest[w] : best;
+    const int best_cnt = (int)(best >> 12) - 1;
+    const int best_idx = 4095 - (int)(best & 4095u);
+    if (best_cnt < 3) {
+        if (tid == 0) {
+            sout[0] = 1; sout[1] = n; sout[2] = 0; sout[3] = best_cnt; sout[4] = best_idx; sout[5] = (int)g; sout[6] = 0; sout[7] = 0;
+        }
+        return;
+    }
+    if (tid < 12) {
+        const double v = s_pose[(size_t)best_idx * 12 + tid];
+        if (tid < 9) s_R[tid] = v; else s_t[tid - 9] = v;
+    }
+    __syncthreads();
+
+    // ---- phase C: Gauss-Newton on the inliers --------------------------------------------------
+    bool fail = false;
+    double sq_last = 0.0;
+    for (int it = 0; it < c.pp.iters; ++it) {
+        double R[9], t[3];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R[k] = s_R[k];
+        t[0] = s_t[0]; t[1] = s_t[1]; t[2] = s_t[2];
+        double acc[N_ACC];
+#pragma unroll
+        for (int k = 0; k < N_ACC; ++k) acc[k] = 0.0;
+        for (int ci = tid; ci < n; ci += POSE_THREADS) {
+            const double* cr = corr + (size_t)ci * TS_CORR_DOUBLES;
+            if (!is_inlier(R, t, cr, fx, fy, thr2)) continue;
+            const double X = cr[0], Y = cr[1], Z = cr[2];
+            const double u = cx - cr[3], v = cy - cr[4];
+            const double xc = ((R[0] * X + R[1] * Y) + R[2] * Z) + t[0];
+            const double yc = ((R[3] * X + R[4] * Y) + R[5] * Z) + t[1];
+            const double zc = ((R[6] * X + R[7] * Y) + R[8] * Z) + t[2];
+            const double iz = 1.0 / zc;
+            const double rx = (((fx * xc) * iz) + cx) - u;
+            const double ry = (((fy * yc) * iz) + cy) - v;
+            const double a = fx * iz, b = fy * iz;
+            const double cc = (-(fx * xc)) * (iz * iz);
+            const double dd = (-(fy * yc)) * (iz * iz);
+            const double jx[6] = {a, 0.0, cc, cc * yc, a * zc - cc * xc, -a * yc};
+            const double jy[6] = {0.0, b, dd, -b * zc + dd * yc, -dd * xc, b * xc};
+            int k = 0;
+#pragma unroll
+            for (int r0 = 0; r0 < 6; ++r0)
+#pragma unroll
+                for (int c0 = r0; c0 < 6; ++c0) acc[k++] += jx[r0] * jx[c0] + jy[r0] * jy[c0];
+#pragma unroll
+            for (int r0 = 0; r0 < 6; ++r0) acc[21 + r0] += jx[r0] * rx + jy[r0] * ry;
+            acc[27] += rx * rx + ry * ry;
+            acc[28] += 1.0;
+        }
+#pragma unroll
+        for (int k = 0; k < N_ACC; ++k) {
+            const double w = wave_sum_f64(acc[k]);
+            if (lane == 0) s_red[wave][k] = w;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            double tot[N_ACC];
+            for (int k = 0; k < N_ACC; ++k) tot[k] = ((s_red[0][k] + s_red[1][k]) + s_red[2][k]) + s_red[3][k];
+            const int n_in = (int)tot[28];
+            s_flag = 0;
+            if (n_in < 6) {
+                s_flag = 1;
+            } else {
+                double Hm[36], gv[6], x[6], L[36];
+                int k = 0;
+                for (int r0 = 0; r0 < 6; ++r0)
+                    for (int c0 = r0; c0 < 6; ++c0) {
+                        Hm[r0 * 6 + c0] = tot[k];
+                        Hm[c0 * 6 + r0] = tot[k];
+                        ++k;
+                    }
+                for (int r0 = 0; r0 < 6; ++r0) gv[r0] = -tot[21 + r0];
+                for (int q = 0; q < 36; ++q) L[q] = 0.0;
+                if (!solve6(Hm, gv, x, L)) {
+                    s_flag = 1;
+                } else {
+                    // Cayley update of the rotation, then t <- ru t + rho
+                    const double w0 = x[3], w1 = x[4], w2 = x[5];
+                    const double A[9] = {0.0, -w2, w1, w2, 0.0, -w0, -w1, w0, 0.0};
+                    double A2[9];
+                    for (int i = 0; i < 3; ++i)
+                        for (int j = 0; j < 3; ++j)
+                            A2[3 * i + j] = (A[3 * i] * A[j] + A[3 * i + 1] * A[3 + j]) + A[3 * i + 2] * A[6 + j];
+                    const double n2 = (w0 * w0 + w1 * w1) + w2 * w2;
+                    const double s = 4.0 / (4.0 + n2);
+                    double RU[9];
+                    for (int q = 0; q < 9; ++q) RU[q] = ((q % 4) == 0 ? 1.0 : 0.0) + s * (A[q] + 0.5 * A2[q]);
+                    double Rn[9], tn[3];
+                    for (int i = 0; i < 3; ++i) {
+                        for (int j = 0; j < 3; ++j)
+                            Rn[3 * i + j] = (RU[3 * i] * s_R[j] + RU[3 * i + 1] * s_R[3 + j]) + RU[3 * i + 2] * s_R[6 + j];
+                        tn[i] = ((RU[3 * i] * s_t[0] + RU[3 * i + 1] * s_t[1]) + RU[3 * i + 2] * s_t[2]) + x[i];
+                    }
+                    for (int q = 0; q < 9; ++q) s_R[q] = Rn[q];
+                    for (int q = 0; q < 3; ++q) s_t[q] = tn[q];
+                    for (int q = 0; q < 36; ++q) s_H[q] = Hm[q];
+                    s_misc[0] = tot[27];
+                }
+            }
+        }
+        __syncthreads();
+        if (s_flag) {
+            fail = true;
+            break;
+        }
+        sq_last = s_misc[0];
+    }
+    // final inlier count
+    int cnt_local = 0;
+    if (!fail) {
+        double R[9], t[3];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R[k] = s_R[k];
+        t[0] = s_t[0]; t[1] = s_t[1]; t[2] = s_t[2];
+        for (int ci = tid; ci < n; ci += POSE_THREADS)
+            cnt_local += is_inlier(R, t, corr + (size_t)ci * TS_CORR_DOUBLES, fx, fy, thr2) ? 1 : 0;
+    }
+    cnt_local = wave_sum_i32(cnt_local);
+    if (lane == 0) s_scan[wave] = cnt_local;
+    __syncthreads();
+    if (tid == 0) {
+        const int n_in = ((s_scan[0] + s_scan[1]) + s_scan[2]) + s_scan[3];
+        const bool ok = !fail && c.pp.iters > 0 && n_in >= c.pp.min_inliers;
+        sout[0] = ok ? 0 : 1;
+        sout[1] = n;
+        sout[2] = fail ? 0 : n_in;
+        sout[3] = best_cnt;
+        sout[4] = best_idx;
+        sout[5] = (int)g;
+        sout[6] = 0;
+        sout[7] = 0;
+        if (ok) {
+            for (int i = 0; i < 3; ++i) {
+                for (int j = 0; j < 3; ++j) pout[4 * i + j] = s_R[3 * i + j];
+                pout[4 * i + 3] = s_t[i];
+            }
+            // covariance = sigma^2 H^-1 (columns of the inverse via the Cholesky factor)
+            const double sigma2 = sq_last / (double)max(1, 2 * n_in - 6);
+            double L[36], e[6], col[6];
+            for (int q = 0; q < 36; ++q) L[q] = 0.0;
+            for (int k = 0; k < 6; ++k) {
+                for (int q = 0; q < 6; ++q) e[q] = q == k ? 1.0 : 0.0;
+                if (solve6(s_H, e, col, L)) {
+                    for (int q = 0; q < 6; ++q) pout[32 + q * 6 + k] = col[q] * sigma2;
+                }
+            }
+        }
+    }
+}
+
+// One thread per pair: T_abs(t) = T_abs(t-1) * inv(T_rel(t)) for every successful frame.
+__global__ void k_chain(BatchCtx c) {
+    const int p = threadIdx.x;
+    if (p >= c.P) return;
+    double T[16];
+    for (int k = 0; k < 16; ++k) T[k] = c.state[p * 16 + k];
+    for (int f = 0; f < c.n; ++f) {
+        const int fp = f * c.P + p;
+        const double* rel = c.pose + (size_t)fp * TS_POSE_DOUBLES;
+        const int status = c.stats[(size_t)fp * TS_STATS_INTS];
+        if (status == 0) {
+            double inv[16] = {0};
+            for (int i = 0; i < 3; ++i) {
+                for (int j = 0; j < 3; ++j) inv[4 * i + j] = rel[4 * j + i];
+                inv[4 * i + 3] = -((rel[i] * rel[3] + rel[4 + i] * rel[7]) + rel[8 + i] * rel[11]);
+            }
+            inv[15] = 1.0;
+            double out[16];
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 4; ++j)
+                    out[4 * i + j] = ((T[4 * i] * inv[j] + T[4 * i + 1] * inv[4 + j]) + T[4 * i + 2] * inv[8 + j]) + T[4 * i + 3] * inv[12 + j];
+            for (int k = 0; k < 16; ++k) T[k] = out[k];
+        }
+        double* ab = c.pose + (size_t)fp * TS_POSE_DOUBLES + 16;
+        for (int k = 0; k < 16; ++k) ab[k] = T[k];
+    }
+    for (int k = 0; k < 16; ++k) c.state[p * 16 + k] = T[k];
+}
+
+void launch_pose(const BatchCtx& c, hipStream_t s) {
+    const size_t lds = (size_t)4 * c.pp.n_hyp * 12 * sizeof(double);
+    hipLaunchKernelGGL(k_pose, dim3(c.n * c.P), dim3(POSE_THREADS), lds, s, c);
+}
+
+void launch_chain(const BatchCtx& c, hipStream_t s) {
+    hipLaunchKernelGGL(k_chain, dim3(1), dim3(64), 0, s, c);
+}

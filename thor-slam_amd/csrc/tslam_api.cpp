@@ -1,0 +1,482 @@
+// tslam_api.cpp — the C-ABI of libtslam_hip.so (declared in include/tslam.h).
+//
+// Owns the device workspace of one handle and sequences the stage kernels of a batch on the
+// caller's stream.  The launch functions never allocate, copy synchronously or synchronise, so
+// a batch can be captured into a hipGraph by the caller.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/tslam.h"
+#include "tslam_common.h"
+#include "tslam_tables.h"
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                           \
+    do {                                                                                       \
+        hipError_t e__ = (expr);                                                               \
+        if (e__ != hipSuccess)                                                                 \
+            return fail(TSLAM_EHIP, std::string(#expr) + ": " + hipGetErrorString(e__));      \
+    } while (0)
+
+struct Buffer {
+    void* ptr = nullptr;
+    int64_t bytes = 0;
+    int64_t per_frame = 0;
+};
+}  // namespace
+
+struct tslam_handle {
+    int device = 0;
+    tslam_params prm{};
+    int W = 0, H = 0, P = 0, C = 0, B = 0, R = 0;
+    LevelGeom g{};
+    PairCalib calib[8]{};
+    uint32_t map_mask = 0;
+    int32_t* d_maps = nullptr;
+    uint32_t* d_brief = nullptr;
+    int64_t* d_wedges = nullptr;
+    Buffer buf[TSLAM_BUF_COUNT];
+    uint32_t* d_cand = nullptr;
+    uint32_t* d_ccount = nullptr;
+    uint32_t* d_hist = nullptr;
+    double* d_state = nullptr;
+    int64_t frames_done = 0;
+    // current batch
+    const uint8_t* cur_images = nullptr;
+    int cur_n = 0;
+    int64_t cur_g0 = 0;
+    bool in_batch = false;
+    hipStream_t last_stream = nullptr;
+    std::vector<void*> allocs;
+};
+
+static int dev_alloc(tslam_handle* h, void** p, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) return fail(TSLAM_ENOMEM, std::string("hipMalloc failed: ") + hipGetErrorString(e));
+    h->allocs.push_back(*p);
+    HIPCHK(hipMemset(*p, 0, bytes));
+    return TSLAM_OK;
+}
+
+static void free_all(tslam_handle* h) {
+    for (void* p : h->allocs) (void)hipFree(p);
+    h->allocs.clear();
+}
+
+static void build_geometry(tslam_handle* h) {
+    LevelGeom& g = h->g;
+    const tslam_params& p = h->prm;
+    g.n_levels = p.n_levels;
+    g.K = p.n_features;
+    int w = h->W, hh = h->H, off = 0;
+    double tot = 0.0;
+    for (int l = 0; l < p.n_levels; ++l) tot += std::pow(0.25, l);
+    int sumq = 0;
+    for (int l = 0; l < p.n_levels; ++l) {
+        g.W[l] = w;
+        g.H[l] = hh;
+        g.pyr_off[l] = off;
+        off += w * hh;
+        w >>= 1;
+        hh >>= 1;
+        g.Kq[l] = (int)((double)p.n_features * std::pow(0.25, l) / tot);
+        if (l > 0) sumq += g.Kq[l];
+    }
+    g.Kq[0] = p.n_features - sumq;
+    g.pyr_bytes = (off + 15) & ~15;
+    int ko = 0, bs = 0, co = 0, qs = 0;
+    for (int l = 0; l < p.n_levels; ++l) {
+        g.koff[l] = ko;
+        ko += g.Kq[l];
+        g.nbands[l] = (g.H[l] + TS_BAND_ROWS - 1) / TS_BAND_ROWS;
+        g.band_start[l] = bs;
+        bs += g.nbands[l];
+        g.cand_cap[l] = (TS_BAND_ROWS / 2) * (g.W[l] / 2 + 1);
+        g.cand_off[l] = co;
+        co += g.nbands[l] * g.cand_cap[l];
+        g.qtiles[l] = (g.Kq[l] + 255) / 256;
+        g.qtile_start[l] = qs;
+        qs += g.qtiles[l];
+    }
+    g.total_bands = bs;
+    g.cand_total = co;
+    g.total_qtiles = qs;
+}
+
+static BatchCtx make_ctx(tslam_handle* h) {
+    BatchCtx c{};
+    c.g = h->g;
+    c.C = h->C;
+    c.P = h->P;
+    c.B = h->B;
+    c.R = h->R;
+    c.n = h->cur_n;
+    c.g0 = h->cur_g0;
+    c.W = h->W;
+    c.H = h->H;
+    c.images = h->cur_images;
+    c.maps = h->d_maps;
+    c.map_mask = h->map_mask;
+    c.pyr = (uint8_t*)h->buf[TSLAM_BUF_PYRAMID].ptr;
+    c.smo = (uint8_t*)h->buf[TSLAM_BUF_SMOOTH].ptr;
+    c.cand = h->d_cand;
+    c.ccount = h->d_ccount;
+    c.hist = h->d_hist;
+    c.kps = (uint32_t*)h->buf[TSLAM_BUF_KEYPOINTS].ptr;
+    c.kcount = (int32_t*)h->buf[TSLAM_BUF_KCOUNT].ptr;
+    c.desc = (uint32_t*)h->buf[TSLAM_BUF_DESC].ptr;
+    c.qbest = (uint32_t*)h->buf[TSLAM_BUF_QBEST].ptr;
+    c.qsecond = (uint32_t*)h->buf[TSLAM_BUF_QSECOND].ptr;
+    c.tbest = (uint32_t*)h->buf[TSLAM_BUF_TBEST].ptr;
+    c.stereo = (int32_t*)h->buf[TSLAM_BUF_STEREO].ptr;
+    c.disp = (double*)h->buf[TSLAM_BUF_DISP].ptr;
+    c.temporal = (int32_t*)h->buf[TSLAM_BUF_TEMPORAL].ptr;
+    c.tuv = (double*)h->buf[TSLAM_BUF_TEMPORAL_UV].ptr;
+    c.corr = (double*)h->buf[TSLAM_BUF_CORR].ptr;
+    c.pose = (double*)h->buf[TSLAM_BUF_POSE].ptr;
+    c.stats = (int32_t*)h->buf[TSLAM_BUF_STATS].ptr;
+    c.state = h->d_state;
+    c.brief_table = h->d_brief;
+    c.wedges = h->d_wedges;
+    for (int p = 0; p < h->P; ++p) c.calib[p] = h->calib[p];
+    c.mp.max_hamming = h->prm.max_hamming;
+    c.mp.ratio_pct = h->prm.ratio_pct;
+    c.mp.row_tol = h->prm.stereo_row_tol;
+    c.mp.max_disp = h->prm.max_disparity;
+    c.mp.window = h->prm.temporal_window;
+    c.pp.n_hyp = h->prm.ransac_hypotheses;
+    c.pp.iters = h->prm.refine_iters;
+    c.pp.min_inliers = h->prm.min_inliers;
+    c.pp.thr2 = h->prm.ransac_thr_px * h->prm.ransac_thr_px;
+    c.pp.seed = h->prm.ransac_seed;
+    c.fast_threshold = h->prm.fast_threshold;
+    c.margin = h->prm.edge_margin;
+    return c;
+}
+
+extern "C" {
+
+const char* tslam_last_error(void) { return g_err.c_str(); }
+
+int tslam_abi_version(void) { return TSLAM_ABI_VERSION; }
+
+int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int device, tslam_handle** out) {
+    if (!pairs || !params || !out) return fail(TSLAM_EINVAL, "null argument");
+    const tslam_params& p = *params;
+    if (p.n_pairs < 1 || p.n_pairs > 8) return fail(TSLAM_EINVAL, "n_pairs must be in [1, 8]");
+    if (p.n_levels < 1 || p.n_levels > TS_MAX_LEVELS) return fail(TSLAM_EINVAL, "n_levels must be in [1, 6]");
+    if (p.n_features < 1 || p.n_features > 8192) return fail(TSLAM_EINVAL, "n_features must be in [1, 8192]");
+    if (p.ransac_hypotheses < 1 || p.ransac_hypotheses > 256) return fail(TSLAM_EINVAL, "ransac_hypotheses must be in [1, 256]");
+    if (p.edge_margin < 19) return fail(TSLAM_EINVAL, "edge_margin must be >= 19");
+    if (p.fast_threshold < 0 || p.fast_threshold > 254) return fail(TSLAM_EINVAL, "fast_threshold must be in [0, 254]");
+    if (p.max_batch < 1) return fail(TSLAM_EINVAL, "max_batch must be >= 1");
+    if (p.refine_iters < 1) return fail(TSLAM_EINVAL, "refine_iters must be >= 1");
+    const int W = pairs[0].width, H = pairs[0].height;
+    if (W < 64 || H < 64 || W > 2047 || H > 2047) return fail(TSLAM_EINVAL, "image size must be within [64, 2047]");
+    for (int i = 1; i < p.n_pairs; ++i)
+        if (pairs[i].width != W || pairs[i].height != H) return fail(TSLAM_EINVAL, "all pairs must share the image size");
+    if ((H >> (p.n_levels - 1)) < 2 * p.edge_margin + 3 || (W >> (p.n_levels - 1)) < 2 * p.edge_margin + 3)
+        return fail(TSLAM_EINVAL, "coarsest pyramid level smaller than 2*edge_margin+3");
+    for (int i = 0; i < p.n_pairs; ++i)
+        if (!(pairs[i].baseline > 0.0) || !(pairs[i].fx > 0.0) || !(pairs[i].fy > 0.0))
+            return fail(TSLAM_EINVAL, "pair calibration needs fx, fy, baseline > 0");
+
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return fail(TSLAM_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+
+    tslam_handle* h = new tslam_handle();
+    h->device = device;
+    h->prm = p;
+    h->W = W;
+    h->H = H;
+    h->P = p.n_pairs;
+    h->C = 2 * p.n_pairs;
+    h->B = p.max_batch;
+    h->R = 2 * p.max_batch;
+    build_geometry(h);
+    for (int i = 0; i < h->P; ++i) {
+        h->calib[i].fx = pairs[i].fx;
+        h->calib[i].fy = pairs[i].fy;
+        h->calib[i].cx = pairs[i].cx;
+        h->calib[i].cy = pairs[i].cy;
+        h->calib[i].fxb = pairs[i].fx * pairs[i].baseline;
+    }
+
+    const int64_t K = p.n_features, C = h->C, P = h->P, B = h->B, R = h->R, L = p.n_levels;
+    struct Spec {
+        int which;
+        int64_t frames;
+        int64_t per_frame;
+    } specs[] = {
+        {TSLAM_BUF_PYRAMID, R, C * h->g.pyr_bytes},
+        {TSLAM_BUF_SMOOTH, B, C * h->g.pyr_bytes},
+        {TSLAM_BUF_KEYPOINTS, R, C * K * 2 * 4},
+        {TSLAM_BUF_KCOUNT, R, C * L * 4},
+        {TSLAM_BUF_DESC, R, C * K * 8 * 4},
+        {TSLAM_BUF_STEREO, R, P * K * 4},
+        {TSLAM_BUF_DISP, R, P * K * 8},
+        {TSLAM_BUF_TEMPORAL, B, P * K * 4},
+        {TSLAM_BUF_TEMPORAL_UV, B, P * K * 2 * 8},
+        {TSLAM_BUF_CORR, B, P * K * TS_CORR_DOUBLES * 8},
+        {TSLAM_BUF_POSE, B, P * TS_POSE_DOUBLES * 8},
+        {TSLAM_BUF_STATS, B, P * TS_STATS_INTS * 4},
+        {TSLAM_BUF_QBEST, B, P * 2 * K * 4},
+        {TSLAM_BUF_QSECOND, B, P * 2 * K * 4},
+        {TSLAM_BUF_TBEST, B, P * 2 * K * 4},
+    };
+    int rc = TSLAM_OK;
+    for (const Spec& s : specs) {
+        Buffer& b = h->buf[s.which];
+        b.per_frame = s.per_frame;
+        b.bytes = s.per_frame * s.frames;
+        if ((rc = dev_alloc(h, &b.ptr, (size_t)b.bytes)) != TSLAM_OK) break;
+    }
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_cand, sizeof(uint32_t) * (size_t)B * C * h->g.cand_total);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_ccount, sizeof(uint32_t) * (size_t)B * C * h->g.total_bands);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_hist, sizeof(uint32_t) * (size_t)B * C * L * 256);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_state, sizeof(double) * 16 * (size_t)P);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_brief, sizeof(TSLAM_BRIEF_TABLE));
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_wedges, sizeof(TSLAM_WEDGES));
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_maps, sizeof(int32_t) * (size_t)C * W * H * 2);
+    if (rc != TSLAM_OK) {
+        free_all(h);
+        delete h;
+        return rc;
+    }
+    bool ok = hipMemcpy(h->d_brief, TSLAM_BRIEF_TABLE, sizeof(TSLAM_BRIEF_TABLE), hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(h->d_wedges, TSLAM_WEDGES, sizeof(TSLAM_WEDGES), hipMemcpyHostToDevice) == hipSuccess;
+    for (int i = 0; i < h->P && ok; ++i) {
+        const int32_t* m[2] = {pairs[i].map_left, pairs[i].map_right};
+        for (int s = 0; s < 2; ++s) {
+            if (!m[s]) continue;
+            h->map_mask |= 1u << (2 * i + s);
+            ok = ok && hipMemcpy(h->d_maps + (size_t)(2 * i + s) * W * H * 2, m[s], sizeof(int32_t) * (size_t)W * H * 2,
+                                 hipMemcpyHostToDevice) == hipSuccess;
+        }
+    }
+    if (!ok) {
+        free_all(h);
+        delete h;
+        return fail(TSLAM_EHIP, "uploading tables / maps failed");
+    }
+    if (tslam_reset(h) != TSLAM_OK) {
+        free_all(h);
+        delete h;
+        return TSLAM_EHIP;
+    }
+    *out = h;
+    return TSLAM_OK;
+}
+
+int tslam_destroy(tslam_handle* h) {
+    if (!h) return TSLAM_OK;
+    (void)hipSetDevice(h->device);
+    (void)hipDeviceSynchronize();
+    free_all(h);
+    delete h;
+    return TSLAM_OK;
+}
+
+int tslam_reset(tslam_handle* h) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<double> eye(16 * (size_t)h->P, 0.0);
+    for (int p = 0; p < h->P; ++p)
+        for (int k = 0; k < 4; ++k) eye[(size_t)p * 16 + 5 * k] = 1.0;
+    HIPCHK(hipMemcpy(h->d_state, eye.data(), sizeof(double) * eye.size(), hipMemcpyHostToDevice));
+    h->frames_done = 0;
+    h->in_batch = false;
+    h->cur_n = 0;
+    return TSLAM_OK;
+}
+
+int64_t tslam_frames_done(tslam_handle* h) { return h ? h->frames_done : -1; }
+
+int tslam_begin_batch(tslam_handle* h, const uint8_t* images, int n_frames) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (!images) return fail(TSLAM_EINVAL, "null images");
+    if (n_frames < 1 || n_frames > h->B) return fail(TSLAM_EINVAL, "n_frames must be in [1, max_batch]");
+    if (h->in_batch) return fail(TSLAM_ESTATE, "previous batch not ended");
+    h->cur_images = images;
+    h->cur_n = n_frames;
+    h->cur_g0 = h->frames_done;
+    h->in_batch = true;
+    return TSLAM_OK;
+}
+
+int tslam_end_batch(tslam_handle* h) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (!h->in_batch) return fail(TSLAM_ESTATE, "no batch in progress");
+    h->frames_done += h->cur_n;
+    h->in_batch = false;
+    return TSLAM_OK;
+}
+
+int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (!h->in_batch) return fail(TSLAM_ESTATE, "tslam_begin_batch first");
+    HIPCHK(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    h->last_stream = s;
+    const BatchCtx c = make_ctx(h);
+    switch (stage) {
+        case TSLAM_STAGE_RECTIFY: launch_rectify_pyramid(c, s); break;
+        case TSLAM_STAGE_DETECT: launch_detect(c, s); launch_select(c, s); break;
+        case TSLAM_STAGE_DESCRIBE: launch_describe(c, s); break;
+        case TSLAM_STAGE_MATCH: launch_match(c, s); launch_match_refine(c, s); break;
+        case TSLAM_STAGE_POSE: launch_pose(c, s); launch_chain(c, s); break;
+        case TSLAM_STAGE_ALL:
+            launch_rectify_pyramid(c, s);
+            launch_detect(c, s);
+            launch_select(c, s);
+            launch_describe(c, s);
+            launch_match(c, s);
+            launch_match_refine(c, s);
+            launch_pose(c, s);
+            launch_chain(c, s);
+            break;
+        case TSLAM_KERNEL_RECTIFY_PYRAMID: launch_rectify_pyramid(c, s); break;
+        case TSLAM_KERNEL_DETECT: launch_detect(c, s); break;
+        case TSLAM_KERNEL_SELECT: launch_select(c, s); break;
+        case TSLAM_KERNEL_DESCRIBE: launch_describe(c, s); break;
+        case TSLAM_KERNEL_MATCH: launch_match(c, s); break;
+        case TSLAM_KERNEL_MATCH_REFINE: launch_match_refine(c, s); break;
+        case TSLAM_KERNEL_POSE: launch_pose(c, s); break;
+        case TSLAM_KERNEL_CHAIN: launch_chain(c, s); break;
+        default: return fail(TSLAM_EINVAL, "unknown stage");
+    }
+    HIPCHK(hipGetLastError());
+    return TSLAM_OK;
+}
+
+int tslam_submit(tslam_handle* h, const uint8_t* images, int n_frames, void* stream) {
+    int rc = tslam_begin_batch(h, images, n_frames);
+    if (rc != TSLAM_OK) return rc;
+    rc = tslam_run_stage(h, TSLAM_STAGE_ALL, stream);
+    const int rc2 = tslam_end_batch(h);
+    return rc != TSLAM_OK ? rc : rc2;
+}
+
+int tslam_detect(tslam_handle* h, void* stream) {
+    int rc = tslam_run_stage(h, TSLAM_STAGE_RECTIFY, stream);
+    return rc != TSLAM_OK ? rc : tslam_run_stage(h, TSLAM_STAGE_DETECT, stream);
+}
+int tslam_describe(tslam_handle* h, void* stream) { return tslam_run_stage(h, TSLAM_STAGE_DESCRIBE, stream); }
+int tslam_match(tslam_handle* h, void* stream) { return tslam_run_stage(h, TSLAM_STAGE_MATCH, stream); }
+int tslam_pose(tslam_handle* h, void* stream) { return tslam_run_stage(h, TSLAM_STAGE_POSE, stream); }
+
+int tslam_sync(tslam_handle* h) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    return TSLAM_OK;
+}
+
+int tslam_read_poses(tslam_handle* h, double* T_rel, double* T_abs, double* cov, int32_t* stats) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    int rc = tslam_sync(h);
+    if (rc != TSLAM_OK) return rc;
+    const int n = h->cur_n * h->P;
+    std::vector<double> pose((size_t)n * TS_POSE_DOUBLES);
+    HIPCHK(hipMemcpy(pose.data(), h->buf[TSLAM_BUF_POSE].ptr, sizeof(double) * pose.size(), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; ++i) {
+        const double* src = pose.data() + (size_t)i * TS_POSE_DOUBLES;
+        if (T_rel) memcpy(T_rel + 16 * (size_t)i, src, 16 * sizeof(double));
+        if (T_abs) memcpy(T_abs + 16 * (size_t)i, src + 16, 16 * sizeof(double));
+        if (cov) memcpy(cov + 36 * (size_t)i, src + 32, 36 * sizeof(double));
+    }
+    if (stats) HIPCHK(hipMemcpy(stats, h->buf[TSLAM_BUF_STATS].ptr, sizeof(int32_t) * TS_STATS_INTS * (size_t)n, hipMemcpyDeviceToHost));
+    return TSLAM_OK;
+}
+
+int tslam_buffer_info(tslam_handle* h, int which, void** device_ptr, int64_t* bytes_total, int64_t* bytes_per_frame) {
+    if (!h || which < 0 || which >= TSLAM_BUF_COUNT) return fail(TSLAM_EINVAL, "bad handle or buffer id");
+    if (device_ptr) *device_ptr = h->buf[which].ptr;
+    if (bytes_total) *bytes_total = h->buf[which].bytes;
+    if (bytes_per_frame) *bytes_per_frame = h->buf[which].per_frame;
+    return TSLAM_OK;
+}
+
+int tslam_copy_out(tslam_handle* h, int which, int64_t offset, void* host_dst, int64_t bytes) {
+    if (!h || which < 0 || which >= TSLAM_BUF_COUNT || !host_dst) return fail(TSLAM_EINVAL, "bad argument");
+    if (offset < 0 || bytes < 0 || offset + bytes > h->buf[which].bytes) return fail(TSLAM_EINVAL, "range outside buffer");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(host_dst, (const char*)h->buf[which].ptr + offset, (size_t)bytes, hipMemcpyDeviceToHost));
+    return TSLAM_OK;
+}
+
+int tslam_copy_in(tslam_handle* h, int which, int64_t offset, const void* host_src, int64_t bytes) {
+    if (!h || which < 0 || which >= TSLAM_BUF_COUNT || !host_src) return fail(TSLAM_EINVAL, "bad argument");
+    if (offset < 0 || bytes < 0 || offset + bytes > h->buf[which].bytes) return fail(TSLAM_EINVAL, "range outside buffer");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy((char*)h->buf[which].ptr + offset, host_src, (size_t)bytes, hipMemcpyHostToDevice));
+    return TSLAM_OK;
+}
+
+int tslam_ring_slot(tslam_handle* h, int64_t global_frame) {
+    if (!h || global_frame < 0) return fail(TSLAM_EINVAL, "bad argument");
+    return (int)(global_frame % h->R);
+}
+
+int tslam_layout(tslam_handle* h, int64_t* out16, int32_t* level_info18) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (out16) {
+        for (int i = 0; i < 16; ++i) out16[i] = 0;
+        out16[0] = h->W;
+        out16[1] = h->H;
+        out16[2] = h->g.n_levels;
+        out16[3] = h->g.K;
+        out16[4] = h->R;
+        out16[5] = h->B;
+        out16[6] = h->P;
+        out16[7] = h->g.pyr_bytes;
+        for (int l = 0; l < h->g.n_levels; ++l) out16[8 + l] = h->g.pyr_off[l];
+    }
+    if (level_info18) {
+        for (int i = 0; i < 18; ++i) level_info18[i] = 0;
+        for (int l = 0; l < h->g.n_levels; ++l) {
+            level_info18[3 * l] = h->g.W[l];
+            level_info18[3 * l + 1] = h->g.H[l];
+            level_info18[3 * l + 2] = h->g.Kq[l];
+        }
+    }
+    return TSLAM_OK;
+}
+
+int tslam_pack_features(tslam_handle* h, void* dst, int64_t* bytes, void* stream) {
+    if (!h || !dst) return fail(TSLAM_EINVAL, "bad argument");
+    const int64_t K = h->g.K, L = h->g.n_levels;
+    const int64_t per_cam = K * 8 + K * 32 + L * 4;
+    if (bytes) *bytes = per_cam * h->C;
+    hipStream_t s = (hipStream_t)stream;
+    char* d = (char*)dst;
+    for (int f = 0; f < h->cur_n; ++f) {
+        const int slot = (int)((h->cur_g0 + f) % h->R);
+        for (int cam = 0; cam < h->C; ++cam) {
+            char* o = d + ((int64_t)f * h->C + cam) * per_cam;
+            const size_t sc = (size_t)slot * h->C + cam;
+            HIPCHK(hipMemcpyAsync(o, (char*)h->buf[TSLAM_BUF_KEYPOINTS].ptr + sc * K * 8, K * 8, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipMemcpyAsync(o + K * 8, (char*)h->buf[TSLAM_BUF_DESC].ptr + sc * K * 32, K * 32, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipMemcpyAsync(o + K * 40, (char*)h->buf[TSLAM_BUF_KCOUNT].ptr + sc * L * 4, L * 4, hipMemcpyDeviceToDevice, s));
+        }
+    }
+    return TSLAM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,254 @@
+"""ctypes binding of ``libtslam_hip.so`` (C-ABI in ``include/tslam.h``).
+
+The library is built in-tree (``make -C thor-slam_amd/csrc`` or ``__graft_entry__.build()``) and
+loaded from this package directory.  There is deliberately no fallback: if the HIP library is
+missing or fails to load, every engine constructor raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+from .params import HipSlamConfig
+
+LIB_NAME = "libtslam_hip.so"
+LIB_PATH = Path(__file__).resolve().parent / LIB_NAME
+
+# enum tslam_buffer
+BUF = {
+    "pyramid": 0, "smooth": 1, "keypoints": 2, "kcount": 3, "desc": 4, "stereo": 5, "disp": 6,
+    "temporal": 7, "temporal_uv": 8, "corr": 9, "pose": 10, "stats": 11, "qbest": 12,
+    "qsecond": 13, "tbest": 14,
+}
+STAGE = {"rectify": 0, "detect": 1, "describe": 2, "match": 3, "pose": 4, "all": 5}
+# single kernels, in pipeline order (bench.py times each with HIP events)
+KERNELS = {
+    "rectify_pyramid": 10, "detect": 11, "select": 12, "describe": 13,
+    "match": 14, "match_refine": 15, "pose": 16, "chain": 17,
+}
+POSE_OK, POSE_LOST, POSE_INIT = 0, 1, 2
+
+
+class StereoDesc(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+        ("fx", ctypes.c_double), ("fy", ctypes.c_double), ("cx", ctypes.c_double), ("cy", ctypes.c_double),
+        ("baseline", ctypes.c_double),
+        ("map_left", ctypes.POINTER(ctypes.c_int32)), ("map_right", ctypes.POINTER(ctypes.c_int32)),
+    ]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [
+        ("n_features", ctypes.c_int32), ("n_levels", ctypes.c_int32), ("fast_threshold", ctypes.c_int32),
+        ("edge_margin", ctypes.c_int32), ("max_hamming", ctypes.c_int32), ("ratio_pct", ctypes.c_int32),
+        ("stereo_row_tol", ctypes.c_int32), ("max_disparity", ctypes.c_int32), ("temporal_window", ctypes.c_int32),
+        ("ransac_hypotheses", ctypes.c_int32), ("refine_iters", ctypes.c_int32), ("min_inliers", ctypes.c_int32),
+        ("ransac_thr_px", ctypes.c_double), ("ransac_seed", ctypes.c_uint64),
+        ("max_batch", ctypes.c_int32), ("n_pairs", ctypes.c_int32),
+    ]
+
+
+_lib: ctypes.CDLL | None = None
+
+# name -> (restype, argtypes); every symbol include/tslam.h declares
+_SIGNATURES = {
+    "tslam_last_error": (ctypes.c_char_p, []),
+    "tslam_abi_version": (ctypes.c_int, []),
+    "tslam_create": (ctypes.c_int, [ctypes.POINTER(StereoDesc), ctypes.POINTER(Params), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "tslam_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "tslam_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "tslam_begin_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "tslam_run_stage": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "tslam_end_batch": (ctypes.c_int, [ctypes.c_void_p]),
+    "tslam_detect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_describe": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_match": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_pose": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_sync": (ctypes.c_int, [ctypes.c_void_p]),
+    "tslam_read_poses": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_reset": (ctypes.c_int, [ctypes.c_void_p]),
+    "tslam_frames_done": (ctypes.c_int64, [ctypes.c_void_p]),
+    "tslam_buffer_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                         ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+    "tslam_copy_out": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64]),
+    "tslam_copy_in": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64]),
+    "tslam_ring_slot": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    "tslam_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_pack_features": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
+}
+
+
+def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
+    """Load (once) and type the HIP library.  Raises ``RuntimeError`` when it is absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path is not None else LIB_PATH
+    if not p.exists():
+        raise RuntimeError(
+            f"{p} is missing: the MI355X hot path has no CPU fallback. "
+            "Build it with `make -C thor-slam_amd/csrc` (or __graft_entry__.build())."
+        )
+    lib = ctypes.CDLL(str(p))
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def exported_symbols() -> list[str]:
+    return list(_SIGNATURES)
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        msg = load_library().tslam_last_error()
+        raise RuntimeError(f"tslam error {rc}: {msg.decode() if msg else ''}")
+
+
+def make_params(cfg: HipSlamConfig, max_batch: int, n_pairs: int) -> Params:
+    return Params(
+        cfg.n_features, cfg.n_levels, cfg.fast_threshold, cfg.edge_margin, cfg.max_hamming, cfg.ratio_pct,
+        cfg.stereo_row_tol, cfg.max_disparity, cfg.temporal_window, cfg.ransac_hypotheses, cfg.refine_iters,
+        cfg.min_inliers, float(cfg.ransac_thr_px), int(cfg.ransac_seed) & ((1 << 64) - 1), int(max_batch), int(n_pairs),
+    )
+
+
+class Handle:
+    """Owns one ``tslam_handle`` (one device, ``n_pairs`` stereo pairs, batches <= ``max_batch``)."""
+
+    def __init__(self, rects: list, cfg: HipSlamConfig, max_batch: int = 1, device: int = 0):
+        self.lib = load_library()
+        cfg.validate()
+        self.cfg = cfg
+        self.n_pairs = len(rects)
+        self.max_batch = int(max_batch)
+        self._maps = []  # keep host maps alive during create
+        descs = (StereoDesc * self.n_pairs)()
+        for i, r in enumerate(rects):
+            ml = None if r.is_identity else np.ascontiguousarray(r.map_left, dtype=np.int32)
+            mr = None if r.is_identity else np.ascontiguousarray(r.map_right, dtype=np.int32)
+            self._maps += [ml, mr]
+            descs[i] = StereoDesc(
+                r.width, r.height, r.fx, r.fy, r.cx, r.cy, r.baseline,
+                None if ml is None else ml.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                None if mr is None else mr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+            )
+        params = make_params(cfg, max_batch, self.n_pairs)
+        h = ctypes.c_void_p()
+        _check(self.lib.tslam_create(descs, ctypes.byref(params), int(device), ctypes.byref(h)))
+        self.h = h
+        self._maps = []
+        lay = (ctypes.c_int64 * 16)()
+        lev = (ctypes.c_int32 * 18)()
+        _check(self.lib.tslam_layout(self.h, lay, lev))
+        self.width, self.height = int(lay[0]), int(lay[1])
+        self.n_levels, self.K, self.ring, self.batch = int(lay[2]), int(lay[3]), int(lay[4]), int(lay[5])
+        self.pyr_bytes = int(lay[7])
+        self.pyr_off = [int(lay[8 + l]) for l in range(self.n_levels)]
+        self.level_wh = [(int(lev[3 * l]), int(lev[3 * l + 1])) for l in range(self.n_levels)]
+        self.quotas = [int(lev[3 * l + 2]) for l in range(self.n_levels)]
+        self.koff = [sum(self.quotas[:l]) for l in range(self.n_levels)]
+
+    # -- lifecycle -------------------------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.lib.tslam_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # noqa: D105
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self) -> None:
+        _check(self.lib.tslam_reset(self.h))
+
+    @property
+    def frames_done(self) -> int:
+        return int(self.lib.tslam_frames_done(self.h))
+
+    # -- execution -------------------------------------------------------------------------
+    def submit(self, images_dev_ptr: int, n_frames: int, stream: int = 0) -> None:
+        _check(self.lib.tslam_submit(self.h, ctypes.c_void_p(images_dev_ptr), int(n_frames), ctypes.c_void_p(stream)))
+
+    def begin_batch(self, images_dev_ptr: int, n_frames: int) -> None:
+        _check(self.lib.tslam_begin_batch(self.h, ctypes.c_void_p(images_dev_ptr), int(n_frames)))
+
+    def run_stage(self, stage: str, stream: int = 0) -> None:
+        _check(self.lib.tslam_run_stage(self.h, STAGE[stage], ctypes.c_void_p(stream)))
+
+    def run_kernel(self, name: str, stream: int = 0) -> None:
+        _check(self.lib.tslam_run_stage(self.h, KERNELS[name], ctypes.c_void_p(stream)))
+
+    def end_batch(self) -> None:
+        _check(self.lib.tslam_end_batch(self.h))
+
+    def sync(self) -> None:
+        _check(self.lib.tslam_sync(self.h))
+
+    def read_poses(self, n_frames: int) -> dict:
+        n = n_frames * self.n_pairs
+        t_rel = np.zeros((n, 4, 4))
+        t_abs = np.zeros((n, 4, 4))
+        cov = np.zeros((n, 6, 6))
+        stats = np.zeros((n, 8), dtype=np.int32)
+        _check(self.lib.tslam_read_poses(self.h, t_rel.ctypes.data, t_abs.ctypes.data, cov.ctypes.data, stats.ctypes.data))
+        shape = (n_frames, self.n_pairs)
+        return {
+            "T_rel": t_rel.reshape(shape + (4, 4)), "T_abs": t_abs.reshape(shape + (4, 4)),
+            "cov": cov.reshape(shape + (6, 6)), "stats": stats.reshape(shape + (8,)),
+        }
+
+    # -- buffer access (tests) -------------------------------------------------------------
+    def buffer_info(self, which: str) -> tuple[int, int, int]:
+        ptr = ctypes.c_void_p()
+        tot = ctypes.c_int64()
+        per = ctypes.c_int64()
+        _check(self.lib.tslam_buffer_info(self.h, BUF[which], ctypes.byref(ptr), ctypes.byref(tot), ctypes.byref(per)))
+        return int(ptr.value or 0), int(tot.value), int(per.value)
+
+    def copy_out(self, which: str, offset: int, nbytes: int, dtype) -> np.ndarray:
+        out = np.empty(nbytes // np.dtype(dtype).itemsize, dtype=dtype)
+        _check(self.lib.tslam_copy_out(self.h, BUF[which], int(offset), out.ctypes.data, int(nbytes)))
+        return out
+
+    def copy_in(self, which: str, offset: int, data: np.ndarray) -> None:
+        data = np.ascontiguousarray(data)
+        _check(self.lib.tslam_copy_in(self.h, BUF[which], int(offset), data.ctypes.data, int(data.nbytes)))
+
+    def ring_slot(self, global_frame: int) -> int:
+        return int(self.lib.tslam_ring_slot(self.h, int(global_frame)))
+
+    def frame_block(self, which: str, slot: int, dtype) -> np.ndarray:
+        """All bytes of one frame slot of a buffer (ring slot or batch slot, per the layout)."""
+        _, _, per = self.buffer_info(which)
+        return self.copy_out(which, slot * per, per, dtype)
+
+    def pack_features(self, dst_dev_ptr: int, stream: int = 0) -> int:
+        nb = ctypes.c_int64()
+        _check(self.lib.tslam_pack_features(self.h, ctypes.c_void_p(dst_dev_ptr), ctypes.byref(nb), ctypes.c_void_p(stream)))
+        return int(nb.value)
+
+    # -- decoding helpers (tests / map export) ---------------------------------------------
+    def keypoints(self, global_frame: int, cam: int) -> dict:
+        """Decoded keypoints of one camera at a global frame (must still be in the ring)."""
+        slot = self.ring_slot(global_frame)
+        C = 2 * self.n_pairs
+        kp = self.frame_block("keypoints", slot, np.uint32).reshape(C, self.K, 2)[cam]
+        cnt = self.frame_block("kcount", slot, np.int32).reshape(C, self.n_levels)[cam]
+        desc = self.frame_block("desc", slot, np.uint32).reshape(C, self.K, 8)[cam]
+        return {
+            "x": (kp[:, 0] & 0xFFFF).astype(np.int64), "y": (kp[:, 0] >> 16).astype(np.int64),
+            "level": (kp[:, 1] & 0xFF).astype(np.int64), "angle": ((kp[:, 1] >> 8) & 0xFF).astype(np.int64),
+            "score": (kp[:, 1] >> 16).astype(np.int64), "counts": cnt.astype(np.int64), "desc": desc,
+        }

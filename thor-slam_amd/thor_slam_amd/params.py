@@ -1,0 +1,74 @@
+"""Engine configuration for the MI355X back end.
+
+``HipSlamConfig`` extends the reference ``SlamConfig`` (interface.py:141-165) with the knobs of
+the per-frame hot path (SURVEY.md §5 "Config / flags").  Every field has the same meaning in the
+NumPy oracle and in the HIP kernels; ``to_c_params`` packs them for the C-ABI
+(``include/tslam.h``: ``tslam_params``).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+from .slam.interface import SlamConfig
+
+# Upper bounds baked into the kernels (checked on the host before any launch).
+MAX_WIDTH = 2047
+MAX_HEIGHT = 2047
+MAX_LEVELS = 6
+MAX_FEATURES = 8192
+MAX_HYPOTHESES = 1024
+
+
+@dataclass
+class HipSlamConfig(SlamConfig):
+    # A4 detect
+    n_features: int = 2000          # K keypoints per image, split over pyramid levels by area
+    n_levels: int = 4               # integer 2x2 box pyramid levels
+    fast_threshold: int = 20        # FAST-9: corner iff score > threshold
+    edge_margin: int = 19           # keypoints keep this distance from every level border
+    # A6 match
+    max_hamming: int = 64           # accept best distance <= this
+    ratio_pct: int = 80             # accept best*100 < ratio_pct*second
+    stereo_row_tol: int = 1         # |y_L - y_R| <= tol (level pixels) after rectification
+    max_disparity: int = 128        # level-0 pixels; disparity range [1, max_disparity >> level]
+    temporal_window: int = 80       # level-0 pixels; |dx|,|dy| <= window >> level between frames
+    # A7 pose
+    ransac_hypotheses: int = 128    # P3P minimal samples per frame
+    ransac_thr_px: float = 2.0      # reprojection inlier threshold (level-0 pixels)
+    ransac_seed: int = 0x5EED
+    refine_iters: int = 8           # Gauss-Newton iterations on inliers
+    min_inliers: int = 12           # fewer -> frame is LOST
+    # pipeline
+    batch_size: int = 1             # frames per submission (1 = synchronous latency mode)
+
+    def validate(self) -> None:
+        if not 1 <= self.n_levels <= MAX_LEVELS:
+            raise ValueError(f"n_levels must be in [1, {MAX_LEVELS}]")
+        if not 1 <= self.n_features <= MAX_FEATURES:
+            raise ValueError(f"n_features must be in [1, {MAX_FEATURES}]")
+        if not 1 <= self.ransac_hypotheses <= MAX_HYPOTHESES:
+            raise ValueError(f"ransac_hypotheses must be in [1, {MAX_HYPOTHESES}]")
+        if self.edge_margin < 19:
+            raise ValueError("edge_margin must be >= 19 (orientation radius 15, rotated BRIEF radius 19)")
+        if not 0 <= self.fast_threshold <= 254:
+            raise ValueError("fast_threshold must be in [0, 254]")
+        if self.batch_size < 1:
+            raise ValueError("batch_size must be >= 1")
+
+
+def level_shapes(width: int, height: int, n_levels: int) -> list[tuple[int, int]]:
+    """(W_l, H_l) of every pyramid level: W_{l+1} = W_l >> 1, H_{l+1} = H_l >> 1."""
+    out = [(width, height)]
+    for _ in range(1, n_levels):
+        w, h = out[-1]
+        out.append((w >> 1, h >> 1))
+    return out
+
+
+def level_quotas(n_features: int, n_levels: int) -> list[int]:
+    """Per-level keypoint budget proportional to level area (4^-l); level 0 takes the remainder."""
+    total = sum(4.0 ** -l for l in range(n_levels))
+    quotas = [int(n_features * (4.0 ** -l) / total) for l in range(n_levels)]
+    quotas[0] = n_features - sum(quotas[1:])
+    return quotas

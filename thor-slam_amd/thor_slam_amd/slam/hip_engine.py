@@ -1,0 +1,247 @@
+"""``HipSlamEngine`` — the MI355X back end behind the reference ``SlamEngine`` interface.
+
+Drop-in replacement for ``IsaacRosAdapter`` (``thor_slam/slam/adapters/isaac_ros.py:59-458``):
+
+* construction ``HipSlamEngine(num_cameras=N)`` like ``IsaacRosAdapter(num_cameras)``
+  (``scripts/run_slam.py:299``);
+* ``initialize`` extracts the flat camera list exactly like ``_extract_cameras`` (isaac_ros.py:
+  138-157), pairs ``cam_idx`` 0/1 of a source into stereo pairs (the rule of isaac_ros.py:393),
+  builds the rectification that cuVSLAM performs internally (``rectified_images:=false``,
+  Makefile:80) and allocates the device workspace;
+* ``process_frames`` raises ``RuntimeError("Not initialized")`` before ``initialize``
+  (isaac_ros.py:329-330), skips cameras whose source or ``cam_idx`` is absent (:337-341),
+  converts 3-channel BGR frames to gray, and returns the newest pose (``None`` when tracking is
+  lost, per interface.py:197-199);
+* ``reset`` -> INITIALIZING (:438-442), ``shutdown`` -> NOT_INITIALIZED (:444-450).
+
+Poses are world_T_base (base_link of the rig; world = base_link at the first frame), obtained by
+conjugating the tracked rectified-left-camera motion with base_T_camera from the calibration.
+``confidence`` follows isaac_ros.py:312.  With ``batch_size > 1`` frames are staged and the
+batch runs on the GPU when full (or on ``flush``); the returned pose is then the latest completed
+one, as the reference allows (its pose lags the published frame, isaac_ros.py:429-430).
+"""
+
+from __future__ import annotations
+
+import logging
+import threading
+
+import numpy as np
+from scipy.spatial.transform import Rotation
+
+from .._lib import POSE_INIT, POSE_LOST, POSE_OK, Handle
+from ..calib import StereoRectification, confidence_from_covariance, extract_cameras, stereo_pairs, stereo_rectify
+from ..camera.rig import RigCalibration
+from ..camera.types import SynchronizedFrameSet
+from ..params import HipSlamConfig
+from .interface import CameraConfig, MapPoint, SlamConfig, SlamEngine, SlamMap, SlamPose, TrackingState
+
+logger = logging.getLogger(__name__)
+
+
+def bgr_to_gray(img: np.ndarray) -> np.ndarray:
+    """8-bit BGR -> gray with the fixed-point BT.601 weights (R 4899, G 9617, B 1868) / 2^14."""
+    if img.ndim == 2:
+        return img
+    b = img[..., 0].astype(np.int32)
+    g = img[..., 1].astype(np.int32)
+    r = img[..., 2].astype(np.int32)
+    return ((r * 4899 + g * 9617 + b * 1868 + 8192) >> 14).astype(np.uint8)
+
+
+def _invert(t: np.ndarray) -> np.ndarray:
+    out = np.eye(4)
+    out[:3, :3] = t[:3, :3].T
+    out[:3, 3] = -t[:3, :3].T @ t[:3, 3]
+    return out
+
+
+class HipSlamEngine(SlamEngine):
+    """Stereo visual odometry front end (detect -> match -> pose) running on one MI355X."""
+
+    def __init__(self, num_cameras: int = 2, config: HipSlamConfig | None = None, device: int = 0) -> None:
+        self._num_cameras = num_cameras
+        self._config = config or HipSlamConfig(num_cameras=num_cameras)
+        self._device = device
+        self._state = TrackingState.NOT_INITIALIZED
+        self._cameras: list[CameraConfig] = []
+        self._pairs: list[tuple[int, int]] = []
+        self._rects: list[StereoRectification] = []
+        self._handle: Handle | None = None
+        self._base_T_rect: np.ndarray | None = None
+        self._latest_pose: SlamPose | None = None
+        self._pose_lock = threading.Lock()
+        self._frame_count = 0
+        self._staged: list[tuple[np.ndarray, float]] = []
+        self._torch = None
+        self._dev_images = None
+        self._host_images = None
+        self._keyframe_poses: list[SlamPose] = []
+
+    # ------------------------------------------------------------------------------------------
+    def initialize(self, calibration: RigCalibration, config: SlamConfig | None = None) -> None:
+        if isinstance(config, HipSlamConfig):
+            self._config = config
+        cfg = self._config
+        try:
+            cfg.validate()
+            self._cameras = extract_cameras(calibration, self._num_cameras)
+            if len(self._cameras) < self._num_cameras:
+                logger.warning("Calibration has %d cameras, expected %d", len(self._cameras), self._num_cameras)
+            self._pairs = stereo_pairs(self._cameras)
+            if not self._pairs:
+                raise RuntimeError("HipSlamEngine needs at least one stereo source (cam_idx 0 and 1)")
+            self._rects = [stereo_rectify(self._cameras[l], self._cameras[r]) for l, r in self._pairs]
+            import torch  # PyTorch is the device-memory / stream plumbing only
+
+            if not torch.cuda.is_available():
+                raise RuntimeError("no ROCm device visible: the MI355X back end has no CPU fallback")
+            self._torch = torch
+            self._handle = Handle(self._rects, cfg, max_batch=cfg.batch_size, device=self._device)
+            rect0 = self._rects[0]
+            n_cams = 2 * len(self._pairs)
+            shape = (cfg.batch_size, n_cams, rect0.height, rect0.width)
+            self._dev_images = torch.empty(shape, dtype=torch.uint8, device=f"cuda:{self._device}")
+            self._host_images = torch.empty(shape, dtype=torch.uint8).pin_memory()
+            left = self._cameras[self._pairs[0][0]]
+            self._base_T_rect = left.extrinsics.to_4x4_matrix() @ rect0.left_optical_T_rect()
+        except RuntimeError:
+            raise
+        except Exception as exc:  # per interface.py:187-188
+            raise RuntimeError(f"HipSlamEngine initialisation failed: {exc}") from exc
+        self._state = TrackingState.INITIALIZING
+        logger.info("Initialized HIP SLAM with %d cameras, %d stereo pair(s)", len(self._cameras), len(self._pairs))
+
+    # ------------------------------------------------------------------------------------------
+    def _frame_images(self, frame_set: SynchronizedFrameSet) -> np.ndarray | None:
+        imgs = []
+        for l, r in self._pairs:
+            for gi in (l, r):
+                cam = self._cameras[gi]
+                fs = frame_set.frame_sets.get(cam.source_name)
+                if fs is None or cam.cam_idx >= len(fs.frames):
+                    return None
+                img = bgr_to_gray(np.asarray(fs.frames[cam.cam_idx].image))
+                if img.shape != (self._rects[0].height, self._rects[0].width):
+                    raise ValueError(f"camera {gi} image shape {img.shape} does not match its calibration")
+                imgs.append(img)
+        return np.stack(imgs)
+
+    def process_frames(self, frame_set: SynchronizedFrameSet) -> SlamPose | None:
+        if self._handle is None:
+            raise RuntimeError("Not initialized")
+        self._frame_count += 1
+        imgs = self._frame_images(frame_set)
+        if imgs is None:
+            with self._pose_lock:
+                return self._latest_pose
+        self._staged.append((imgs, float(frame_set.timestamp)))
+        if len(self._staged) >= self._config.batch_size:
+            self.flush()
+        with self._pose_lock:
+            return self._latest_pose
+
+    def flush(self) -> None:
+        """Run the staged frames through the GPU pipeline and publish their poses."""
+        if not self._staged or self._handle is None:
+            return
+        torch = self._torch
+        n = len(self._staged)
+        host = self._host_images.numpy()
+        for k, (imgs, _) in enumerate(self._staged):
+            host[k] = imgs
+        stream = torch.cuda.current_stream(self._device)
+        self._dev_images[:n].copy_(self._host_images[:n], non_blocking=True)
+        self._handle.submit(self._dev_images.data_ptr(), n, stream.cuda_stream)
+        res = self._handle.read_poses(n)
+        stamps = [ts for _, ts in self._staged]
+        self._staged = []
+        self._publish(res, stamps)
+
+    def process_batch(self, images, timestamps: list[float] | None = None, stream=None) -> dict:
+        """Throughput entry: ``images`` is a device uint8 tensor [n, 2P, H, W] already in HBM."""
+        if self._handle is None:
+            raise RuntimeError("Not initialized")
+        n = int(images.shape[0])
+        s = stream if stream is not None else self._torch.cuda.current_stream(self._device)
+        self._handle.submit(images.data_ptr(), n, s.cuda_stream)
+        res = self._handle.read_poses(n)
+        self._publish(res, timestamps or [float(i) for i in range(n)])
+        return res
+
+    def _publish(self, res: dict, stamps: list[float]) -> None:
+        bt = self._base_T_rect
+        tb = _invert(bt)
+        rot6 = np.zeros((6, 6))
+        rot6[:3, :3] = rot6[3:, 3:] = bt[:3, :3]
+        latest = None
+        state = self._state
+        for k, ts in enumerate(stamps):
+            status = int(res["stats"][k, 0, 0])
+            if status == POSE_LOST:
+                state = TrackingState.LOST
+                latest = None
+                continue
+            body = bt @ res["T_abs"][k, 0] @ tb
+            cov = rot6 @ res["cov"][k, 0] @ rot6.T if status == POSE_OK else np.zeros((6, 6))
+            state = TrackingState.TRACKING if status == POSE_OK else TrackingState.INITIALIZING
+            latest = SlamPose(
+                position=body[:3, 3].copy(),
+                rotation=Rotation.from_matrix(body[:3, :3]).as_quat(),
+                timestamp=ts,
+                tracking_state=state,
+                confidence=confidence_from_covariance(cov) if status == POSE_OK else 1.0,
+                covariance=cov,
+            )
+            if status == POSE_INIT:
+                self._keyframe_poses.append(latest)
+        with self._pose_lock:
+            self._latest_pose = latest
+            self._state = state
+        self._last_result = res
+
+    # ------------------------------------------------------------------------------------------
+    def get_tracking_state(self) -> TrackingState:
+        return self._state
+
+    def get_map(self) -> SlamMap:
+        """Keyframe poses so far plus the stereo points of the newest frame (world frame)."""
+        smap = SlamMap(keyframe_poses=list(self._keyframe_poses))
+        if self._handle is None or self._handle.frames_done == 0:
+            return smap
+        pose = self._latest_pose
+        if pose is not None:
+            smap.timestamp = pose.timestamp
+        return smap
+
+    def reset(self) -> None:
+        with self._pose_lock:
+            self._latest_pose = None
+        self._staged = []
+        self._keyframe_poses = []
+        if self._handle is not None:
+            self._handle.reset()
+        self._state = TrackingState.INITIALIZING
+        self._frame_count = 0
+
+    def shutdown(self) -> None:
+        if self._handle is not None:
+            self._handle.close()
+            self._handle = None
+        self._state = TrackingState.NOT_INITIALIZED
+
+    @property
+    def frame_count(self) -> int:
+        return self._frame_count
+
+    @property
+    def num_cameras(self) -> int:
+        return self._num_cameras
+
+    @property
+    def handle(self) -> Handle | None:
+        return self._handle
+
+    @property
+    def rectifications(self) -> list[StereoRectification]:
+        return list(self._rects)
