@@ -43,3 +43,79 @@ def scenario(seed: int = 0, n: int = 4, width: int = 640, height: int = 400, dis
 
 def rel_frobenius(a: np.ndarray, b: np.ndarray) -> float:
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+class ScriptedSource:
+    """Duck-typed CameraSource with a scripted timestamp schedule (drives both rigs identically)."""
+
+    def __init__(self, name: str, period: float, offset: float, jitter: float, n_cams: int = 2, imu: bool = False, seed: int = 0):
+        self._name = name
+        self.period, self.offset, self.jitter = period, offset, jitter
+        self.n_cams = n_cams
+        self.imu = imu
+        self.rng = np.random.default_rng(seed)
+        self.i = 0
+        self.k = np.array([[400.0, 0, 319.5], [0, 400.0, 199.5], [0, 0, 1]])
+
+    @property
+    def name(self):
+        return self._name
+
+    def start(self):
+        pass
+
+    def stop(self):
+        pass
+
+    def _ts(self, i):
+        return self.offset + i * self.period + float(self.rng.uniform(-self.jitter, self.jitter))
+
+    def get_latest_frames(self):
+        from thor_slam_amd.camera.types import CameraFrame
+
+        t = self._ts(self.i)
+        self.i += 1
+        return [CameraFrame(image=np.zeros((2, 2), np.uint8), timestamp=t + 1e-4 * c, sequence_num=self.i, camera_name=f"{self._name}_{c}")
+                for c in range(self.n_cams)]
+
+    def try_get_latest_frames(self):
+        return self.get_latest_frames()
+
+    def get_intrinsics(self):
+        from thor_slam_amd.camera.types import Intrinsics
+
+        return [Intrinsics(640, 400, self.k.copy(), np.zeros(14)) for _ in range(self.n_cams)]
+
+    def get_extrinsics(self):
+        from thor_slam_amd.camera.types import Extrinsics
+
+        out = []
+        for c in range(self.n_cams):
+            m = np.eye(4)
+            m[0, 3] = (-0.0375 if c == 0 else 0.0375) if self.n_cams == 2 else 0.0
+            out.append(Extrinsics.from_4x4_matrix(m))
+        return out
+
+    def get_sensor_extrinsics(self):
+        return None
+
+    def get_timestamped_sensor_data(self):
+        if not self.imu:
+            return None, None
+        t = self.offset + self.i * self.period * 0.5
+        return {"accelerometer": np.array([0.0, 9.81, 0.1 * self.i]), "gyroscope": np.array([0.01 * self.i, 0.0, 0.0])}, t
+
+    def try_get_timestamped_sensor_data(self):
+        return self.get_timestamped_sensor_data()
+
+    @property
+    def has_sensor_data(self):
+        return self.imu
+
+
+def scripted_sources():
+    return [
+        ScriptedSource("192.168.2.25", 1 / 30, 100.000, 0.004, imu=True, seed=1),
+        ScriptedSource("192.168.2.21", 1 / 30, 100.011, 0.004, seed=2),
+        ScriptedSource("192.168.2.23", 1 / 15, 100.020, 0.002, seed=3),
+    ]

@@ -89,6 +89,13 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     if _lib is not None and path is None:
         return _lib
     p = Path(path) if path is not None else LIB_PATH
+    # torch ships its own libamdhip64.so.7 (same SONAME as /opt/rocm's).  Whichever loads first
+    # is the one HIP runtime of the process; load torch's first so tensors and our kernels share
+    # it (loading ours first leaves torch's HSA runtime unable to see the device).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not p.exists():
         raise RuntimeError(
             f"{p} is missing: the MI355X hot path has no CPU fallback. "

@@ -1,0 +1,42 @@
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into per-kernel HBM bytes per launch.
+
+Correction (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7): counters are in KiB;
+FETCH_SIZE reports half the bytes of a wide coalesced read on gfx950, so
+traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  The doubling is exact only for 16-B/lane streams;
+byte-granular gathers are uncalibrated, so both the raw and the corrected numbers are kept.
+
+usage: python tools/pmc_summary.py FETCH_DIR WRITE_DIR OUT_JSON [--batch B]
+"""
+
+import collections
+import csv
+import json
+import sys
+from pathlib import Path
+
+
+def load(d):
+    rows = list(csv.DictReader(open(Path(d) / "run_counter_collection.csv")))
+    agg = collections.defaultdict(list)
+    for r in rows:
+        agg[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main():
+    fetch, write, out = sys.argv[1], sys.argv[2], sys.argv[3]
+    batch = int(sys.argv[sys.argv.index("--batch") + 1]) if "--batch" in sys.argv else None
+    f, w = load(fetch), load(write)
+    res = {}
+    for k in sorted(set(f) | set(w)):
+        if not k.startswith("k_"):
+            continue
+        fk, wk = f.get(k, 0.0), w.get(k, 0.0)
+        res[k] = {"FETCH_SIZE_KiB": fk, "WRITE_SIZE_KiB": wk, "hbm_bytes_per_launch": (2 * fk + wk) * 1024.0,
+                  "hbm_bytes_per_launch_uncorrected": (fk + wk) * 1024.0}
+    Path(out).write_text(json.dumps({"batch_frames": batch, "kernels": res}, indent=1))
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
