@@ -76,6 +76,7 @@ typedef struct {
     uint64_t ransac_seed;
     int32_t max_batch;            /* frames per tslam_submit                                  */
     int32_t n_pairs;              /* stereo pairs per frame (cameras = 2 * n_pairs)           */
+    int32_t ransac_splits;        /* RANSAC blocks per frame (0 = auto); never changes results */
 } tslam_params;
 
 /* Buffers exposed for parity tests (tslam_buffer_info / tslam_copy_out / tslam_copy_in). */
@@ -95,7 +96,9 @@ enum tslam_buffer {
     TSLAM_BUF_QBEST = 12,    /* u32 [batch][pairs][2][K]         (dist<<16 | idx) stereo, temporal */
     TSLAM_BUF_QSECOND = 13,  /* u32 [batch][pairs][2][K]                                      */
     TSLAM_BUF_TBEST = 14,    /* u32 [batch][pairs][2][K]         train-side atomicMin         */
-    TSLAM_BUF_COUNT = 15
+    TSLAM_BUF_YPERM = 15,    /* u16 [ring][cams][K]              per level: kp indices sorted by (y, rank) */
+    TSLAM_BUF_ROWSTART = 16, /* u16 [ring][cams][sum(H_l+1)]     per level: first y-sorted position of row y */
+    TSLAM_BUF_COUNT = 17
 };
 
 enum tslam_stage {

@@ -21,14 +21,15 @@ N_FRAMES = 4
 
 
 @functools.lru_cache(maxsize=8)
-def hip_run(seed: int = 0, batch: int = N_FRAMES, distorted: bool = False, n: int = N_FRAMES, cfg_items: tuple = ()):
+def hip_run(seed: int = 0, batch: int = N_FRAMES, distorted: bool = False, n: int = N_FRAMES, cfg_items: tuple = (),
+            splits: int = 0):
     import torch
 
     from thor_slam_amd._lib import Handle
 
     sc = scenario(seed=seed, n=n, distorted=distorted, cfg_items=cfg_items)
     cfg = sc["cfg"]
-    h = Handle([sc["rect"]], cfg, max_batch=batch)
+    h = Handle([sc["rect"]], cfg, max_batch=batch, ransac_splits=splits)
     dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
     per = []
     K = cfg.n_features
@@ -148,3 +149,26 @@ def test_batch_size_invariance():
             np.testing.assert_array_equal(x[k], y[k], err_msg=f"frame {i} {k}")
         np.testing.assert_array_equal(x["stats"], y["stats"])
         np.testing.assert_array_equal(x["T_abs"], y["T_abs"])
+
+
+@pytest.mark.parametrize("splits", [1, 3, 32])
+def test_ransac_split_invariance(splits):
+    _, a = hip_run()
+    _, b = hip_run(splits=splits)
+    for i, (x, y) in enumerate(zip(a, b)):
+        np.testing.assert_array_equal(x["stats"], y["stats"], err_msg=f"frame {i}")
+        np.testing.assert_array_equal(x["T_abs"], y["T_abs"], err_msg=f"frame {i}")
+
+
+def test_other_seeds_and_config():
+    """Different scene seed and a smaller, single-level configuration stay bit-exact."""
+    items = (("n_features", 700), ("n_levels", 1), ("ransac_hypotheses", 64))
+    sc, per = hip_run(seed=5, n=3, cfg_items=items)
+    for i, rec in enumerate(per):
+        o = sc["oracle"][i]
+        _check_image_features(o["cur"]["left"], rec["kp"][0], sc["cfg"], f"frame {i} left")
+        np.testing.assert_array_equal(rec["stereo"], o["cur"]["stereo"])
+        np.testing.assert_array_equal(rec["temporal"], o["cur"]["temporal"])
+        if i:
+            assert rec["stats"][4] == o["best_hyp"] and rec["stats"][2] == o["n_inliers"]
+            assert rel_frobenius(rec["T_abs"], o["world_T_cam"]) < 1e-9

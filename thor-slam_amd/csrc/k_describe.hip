@@ -7,18 +7,21 @@
 
 __global__ __launch_bounds__(256) void k_describe(BatchCtx c) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int kp_idx = blockIdx.x * 4 + wave;
-    const int img = blockIdx.y;
+    int img, local;
+    if (!xcd_image_block(blockIdx.x, c.n * c.C, (c.g.K + 3) / 4, &img, &local)) return;
+    const int pos = local * 4 + wave;          // y-sorted walk of the image (L1/L2 locality)
     const int cam = img % c.C;
     const int f = img / c.C;
     const int slot = ring_slot(c, c.g0 + f);
-    if (kp_idx >= c.g.K) return;
+    if (pos >= c.g.K) return;
+    int l;
+    bool valid;
+    const int kp_idx = ysorted_kp(c, c.yperm + ((size_t)slot * c.C + cam) * c.g.K,
+                                  c.kcount + ((size_t)slot * c.C + cam) * c.g.n_levels, pos, &l, &valid);
     uint32_t* kp = c.kps + (((size_t)slot * c.C + cam) * c.g.K + kp_idx) * 2;
     const uint32_t meta = kp[1];
-    const int l = meta & 0xFF;
-    const int nvalid = c.kcount[((size_t)slot * c.C + cam) * c.g.n_levels + l];
     uint32_t* dst = c.desc + (((size_t)slot * c.C + cam) * c.g.K + kp_idx) * 8;
-    if (kp_idx - c.g.koff[l] >= nvalid) {
+    if (!valid) {
         if (lane < 8) dst[lane] = 0u;
         return;
     }
@@ -40,8 +43,10 @@ __global__ __launch_bounds__(256) void k_describe(BatchCtx c) {
             m01 += dy * v;
         }
     }
-    m10 = wave_sum_i32(m10);
-    m01 = wave_sum_i32(m01);
+    // integer sums are order-independent: DPP row sums + readlanes leave them in SGPRs, so the
+    // wedge search below runs on the scalar unit
+    m10 = __builtin_amdgcn_readfirstlane(wave_sum_dpp(m10));
+    m01 = __builtin_amdgcn_readfirstlane(wave_sum_dpp(m01));
     // bin b: cross(u_b, v) >= 0 and cross(u_{b+1}, v) < 0, v = (m10, m01)
     int bin = 0;
     {
@@ -80,6 +85,6 @@ __global__ __launch_bounds__(256) void k_describe(BatchCtx c) {
 }
 
 void launch_describe(const BatchCtx& c, hipStream_t s) {
-    dim3 grid((c.g.K + 3) / 4, c.n * c.C);
-    hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, s, c);
+    const int bpi = (c.g.K + 3) / 4;
+    hipLaunchKernelGGL(k_describe, dim3(xcd_grid(c.n * c.C, bpi)), dim3(256), 0, s, c);
 }

@@ -81,6 +81,12 @@ __global__ __launch_bounds__(256) void k_rectify_pyramid(BatchCtx c) {
 // definition: max over the 16 arcs of 9 contiguous circle pixels of
 // max(min(I_c - I_p), min(I_p - I_c)); callers only keep it when > threshold.
 // ---------------------------------------------------------------------------------------------
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ s16x2 pk_min(s16x2 a, s16x2 b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ s16x2 pk_max(s16x2 a, s16x2 b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ s16x2 swp(s16x2 a) { return __builtin_shufflevector(a, a, 1, 0); }
+
 __device__ __forceinline__ int fast9_score(const uint8_t* t, int W, int r, int x, int thr) {
     const uint8_t* p = t + r * W + x;
     const int c0 = p[0];
@@ -93,26 +99,34 @@ __device__ __forceinline__ int fast9_score(const uint8_t* t, int W, int r, int x
     // both of either pair are within the threshold (score irrelevant then: it becomes 0).
     const bool rej = (abs(d[0]) <= thr && abs(d[8]) <= thr) || (abs(d[4]) <= thr && abs(d[12]) <= thr);
     if (rej) return 0;
-    int a2[16], b2[16];
+    // packed pairs P[k] = (d[k], d[k+8]); circle index k+8 (k < 8) is the swapped pair.
+    s16x2 P[8];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        a2[k] = min(d[k], d[(k + 1) & 15]);
-        b2[k] = max(d[k], d[(k + 1) & 15]);
-    }
-    int a4[16], b4[16];
+    for (int k = 0; k < 8; ++k) P[k] = (s16x2){(short)d[k], (short)d[k + 8]};
+    // S(v, k) = pair for circle index k of a packed 16-array v
+#define SEL(v, k) ((k) < 8 ? (v)[(k)] : swp((v)[(k) - 8]))
+    s16x2 A2[8], B2[8], A4[8], B4[8];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        a4[k] = min(a2[k], a2[(k + 2) & 15]);
-        b4[k] = max(b2[k], b2[(k + 2) & 15]);
+    for (int k = 0; k < 8; ++k) {
+        A2[k] = pk_min(P[k], SEL(P, k + 1));
+        B2[k] = pk_max(P[k], SEL(P, k + 1));
     }
-    int bright = -1024, darkmin = 1024;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int a8 = min(a4[k], a4[(k + 4) & 15]);
-        const int b8 = max(b4[k], b4[(k + 4) & 15]);
-        bright = max(bright, min(a8, d[(k + 8) & 15]));
-        darkmin = min(darkmin, max(b8, d[(k + 8) & 15]));
+    for (int k = 0; k < 8; ++k) {
+        A4[k] = pk_min(A2[k], SEL(A2, k + 2));
+        B4[k] = pk_max(B2[k], SEL(B2, k + 2));
     }
+    s16x2 br = (s16x2){-1024, -1024}, dk = (s16x2){1024, 1024};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const s16x2 a8 = pk_min(A4[k], SEL(A4, k + 4));
+        const s16x2 b8 = pk_max(B4[k], SEL(B4, k + 4));
+        br = pk_max(br, pk_min(a8, swp(P[k])));   // a9 = min(a8, d[k+8])
+        dk = pk_min(dk, pk_max(b8, swp(P[k])));
+    }
+#undef SEL
+    const int bright = max((int)br.x, (int)br.y);
+    const int darkmin = min((int)dk.x, (int)dk.y);
     return max(max(bright, -darkmin), 0);
 }
 
@@ -149,21 +163,21 @@ __global__ __launch_bounds__(256) void k_detect(BatchCtx c) {
     }
     __syncthreads();
 
-    // 5x5 binomial smoothing of the band rows (column clamp; rows already clamped in LDS)
+    // 5x5 binomial smoothing of the band rows (column clamp; rows already clamped in LDS):
+    // each thread walks one column down the tile keeping the last five horizontal 1-4-6-4-1
+    // sums in registers (5 LDS reads per output pixel instead of 25).
     const int rows_here = min(TS_BAND_ROWS, H - y0);
-    for (int r = wave; r < rows_here; r += 4) {
-        const int lr = r + TS_DET_HALO;
-        for (int x = lane; x < W; x += 64) {
-            const int xm2 = max(x - 2, 0), xm1 = max(x - 1, 0), xp1 = min(x + 1, W - 1), xp2 = min(x + 2, W - 1);
-            int acc = 0;
-            const int wk[5] = {1, 4, 6, 4, 1};
-#pragma unroll
-            for (int k = 0; k < 5; ++k) {
-                const uint8_t* row = tile + (lr - 2 + k) * W;
-                const int h = row[xm2] + 4 * row[xm1] + 6 * row[x] + 4 * row[xp1] + row[xp2];
-                acc += wk[k] * h;
+    for (int x = threadIdx.x; x < W; x += blockDim.x) {
+        const int xm2 = max(x - 2, 0), xm1 = max(x - 1, 0), xp1 = min(x + 1, W - 1), xp2 = min(x + 2, W - 1);
+        int h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+        for (int r = TS_DET_HALO - 2; r < TS_DET_HALO + rows_here + 2; ++r) {
+            const uint8_t* row = tile + r * W;
+            const int h4 = row[xm2] + 4 * row[xm1] + 6 * row[x] + 4 * row[xp1] + row[xp2];
+            if (r >= TS_DET_HALO + 2) {
+                const int acc = h0 + 4 * h1 + 6 * h2 + 4 * h3 + h4;
+                smo[(size_t)(y0 + r - 2 - TS_DET_HALO) * W + x] = (uint8_t)((acc + 128) >> 8);
             }
-            smo[(size_t)(y0 + r) * W + x] = (uint8_t)((acc + 128) >> 8);
+            h0 = h1; h1 = h2; h2 = h3; h3 = h4;
         }
     }
 
@@ -367,6 +381,41 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
         kp[2 * i + 1] = meta;
     }
     if (threadIdx.x == 0) c.kcount[((size_t)slot * c.C + cam) * c.g.n_levels + l] = nsel;
+
+    // y-sorted order of this level (key y<<13 | rank) + row-start table, for band-limited matching
+    for (int i = threadIdx.x; i < nsel; i += blockDim.x) s_keys[i] = (((s_keys[i] >> 11) & 2047u) << 13) | (uint32_t)i;
+    for (int i = nsel + threadIdx.x; i < np2; i += blockDim.x) s_keys[i] = 0xFFFFFFFFu;
+    __syncthreads();
+    for (int k = 2; k <= np2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < np2; i += blockDim.x) {
+                const int p = i ^ j;
+                if (p > i) {
+                    const uint32_t a = s_keys[i], b = s_keys[p];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) {
+                        s_keys[i] = b;
+                        s_keys[p] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    uint16_t* yp = c.yperm + ((size_t)slot * c.C + cam) * c.g.K + c.g.koff[l];
+    for (int i = threadIdx.x; i < Kl; i += blockDim.x)
+        yp[i] = (uint16_t)(i < nsel ? c.g.koff[l] + (int)(s_keys[i] & 8191u) : 0);
+    uint16_t* rs = c.rowstart + ((size_t)slot * c.C + cam) * c.g.rs_total + c.g.rs_off[l];
+    const int Hl = c.g.H[l];
+    for (int y = threadIdx.x; y <= Hl; y += blockDim.x) {
+        const uint32_t target = (uint32_t)y << 13;
+        int lo = 0, hi = nsel;  // first position with key >= target
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_keys[mid] < target) lo = mid + 1; else hi = mid;
+        }
+        rs[y] = (uint16_t)lo;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -14,7 +14,10 @@
 __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     __shared__ uint4 s_desc[TS_MATCH_CHUNK * 2];
     __shared__ uint32_t s_xy[TS_MATCH_CHUNK];
+    __shared__ uint32_t s_idx[TS_MATCH_CHUNK];
     __shared__ uint32_t s_tmin[TS_MATCH_CHUNK];
+    __shared__ uint16_t s_tile[4][64][64];   // per wave: distance[train jj][query lane]
+    __shared__ uint32_t s_qi[4][64];
     const int z = blockIdx.y;                 // (f * P + p) * 2 + mode
     const int mode = z & 1;
     const int fp = z >> 1;
@@ -32,13 +35,21 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     const int K = c.g.K;
     const int qn = c.kcount[((size_t)slot * c.C + qcam) * c.g.n_levels + l];
     const int tn = c.kcount[((size_t)tslot * c.C + tcam) * c.g.n_levels + l];
-    const int qlocal = tile * 256 + threadIdx.x;
-    const bool active = qlocal < qn;
-    const int qi = c.g.koff[l] + qlocal;
+    const int q0 = tile * 256;
+    if (q0 >= qn || tn == 0) return;          // block-uniform
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const size_t qbase = ((size_t)slot * c.C + qcam) * K;
     const size_t tbase = ((size_t)tslot * c.C + tcam) * K;
     const size_t mbase = (((size_t)f * c.P + p) * 2 + mode) * K;
+    const uint16_t* qperm = c.yperm + qbase + c.g.koff[l];
+    const uint16_t* tperm = c.yperm + tbase + c.g.koff[l];
+    const uint16_t* trs = c.rowstart + ((size_t)tslot * c.C + tcam) * c.g.rs_total + c.g.rs_off[l];
+    const int Hl = c.g.H[l];
 
+    // queries in y-sorted order: this block holds positions q0 .. q0+255 of the level
+    const int qpos = q0 + threadIdx.x;
+    const bool active = qpos < qn;
+    const int qi = active ? (int)qperm[qpos] : 0;
     uint32_t q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int qx = 0, qy = 0;
     if (active) {
@@ -49,56 +60,97 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
         qx = xy & 0xFFFF;
         qy = xy >> 16;
     }
+    s_qi[wave][lane] = (uint32_t)qi;
     const int row_tol = c.mp.row_tol, dmax = c.mp.max_disp >> l, win = c.mp.window >> l;
-    int best_d = 1 << 20, best_j = -1, second_d = 1 << 20;
+    const int reach = mode == 0 ? row_tol : win;
+    // rows any query of the block / of this wave can match (queries are y-sorted)
+    const int qlast = min(qn, q0 + 256) - 1;
+    const int by0 = c.kps[(qbase + qperm[q0]) * 2] >> 16;
+    const int by1 = c.kps[(qbase + qperm[qlast]) * 2] >> 16;
+    const int t0 = trs[max(0, by0 - reach)];
+    const int t1 = trs[min(Hl - 1, by1 + reach) + 1];
+    int wy0, wy1;
+    {
+        int a = active ? qy : (1 << 20), b = active ? qy : -1;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            a = min(a, __shfl_xor(a, o, 64));
+            b = max(b, __shfl_xor(b, o, 64));
+        }
+        wy0 = a;
+        wy1 = b;
+    }
+    const bool wave_active = wy1 >= 0;
+    const int wt0 = wave_active ? (int)trs[max(0, wy0 - reach)] : 0;
+    const int wt1 = wave_active ? (int)trs[min(Hl - 1, wy1 + reach) + 1] : 0;
 
-    for (int j0 = 0; j0 < tn; j0 += TS_MATCH_CHUNK) {
-        const int jn = min(TS_MATCH_CHUNK, tn - j0);
+    int best_d = 1 << 20, best_j = 0x7FFFFFFF, second_d = 1 << 20;
+    for (int j0 = t0; j0 < t1; j0 += TS_MATCH_CHUNK) {
+        const int jn = min(TS_MATCH_CHUNK, t1 - j0);
         __syncthreads();
         for (int i = threadIdx.x; i < jn; i += blockDim.x) {
-            const size_t tj = tbase + c.g.koff[l] + j0 + i;
-            const uint4* d = reinterpret_cast<const uint4*>(c.desc + tj * 8);
+            const uint32_t tj = tperm[j0 + i];
+            const uint4* d = reinterpret_cast<const uint4*>(c.desc + (tbase + tj) * 8);
             s_desc[2 * i] = d[0];
             s_desc[2 * i + 1] = d[1];
-            s_xy[i] = c.kps[tj * 2];
+            s_xy[i] = c.kps[(tbase + tj) * 2];
+            s_idx[i] = tj;
             s_tmin[i] = 0xFFFFFFFFu;
         }
         __syncthreads();
-        for (int j = 0; j < jn; ++j) {
-            const uint32_t txy = s_xy[j];
-            const int tx = txy & 0xFFFF, ty = txy >> 16;
-            bool elig;
-            if (mode == 0) {
-                const int dd = qx - tx;
-                elig = abs(qy - ty) <= row_tol && dd >= 1 && dd <= dmax;
-            } else {
-                elig = abs(qx - tx) <= win && abs(qy - ty) <= win;
-            }
-            elig = elig && active;
-            if (__any(elig)) {
-                const uint4 a = s_desc[2 * j], b = s_desc[2 * j + 1];
-                int dist = __popc(q[0] ^ a.x) + __popc(q[1] ^ a.y) + __popc(q[2] ^ a.z) + __popc(q[3] ^ a.w) +
-                           __popc(q[4] ^ b.x) + __popc(q[5] ^ b.y) + __popc(q[6] ^ b.z) + __popc(q[7] ^ b.w);
-                if (elig) {
-                    if (dist < best_d) {
-                        second_d = best_d;
-                        best_d = dist;
-                        best_j = j0 + j;
-                    } else if (dist < second_d) {
-                        second_d = dist;
-                    }
+        const int ja = max(wt0, j0) - j0, jb = min(wt1, j0 + jn) - j0;
+        for (int jt = ja; jt < jb; jt += 64) {
+            const int jcount = min(64, jb - jt);
+            // phase 1: this lane's query against up to 64 train descriptors (LDS broadcasts).
+            // Straight-line and unrolled by 8 so the LDS loads of 8 descriptors are in flight together.
+            for (int jj0 = 0; jj0 < 64; jj0 += 8) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int jj = jj0 + u;
+                    const int j = min(jt + jj, jb - 1);
+                    const uint32_t txy = s_xy[j];
+                    const uint4 a = s_desc[2 * j], b = s_desc[2 * j + 1];
+                    const int tx = txy & 0xFFFF, ty = txy >> 16;
+                    const int dxy = qx - tx;
+                    const bool geo = mode == 0 ? (abs(qy - ty) <= row_tol && dxy >= 1 && dxy <= dmax)
+                                               : (abs(dxy) <= win && abs(qy - ty) <= win);
+                    const bool elig = geo && active && jj < jcount;
+                    const int dd = __popc(q[0] ^ a.x) + __popc(q[1] ^ a.y) + __popc(q[2] ^ a.z) + __popc(q[3] ^ a.w) +
+                                   __popc(q[4] ^ b.x) + __popc(q[5] ^ b.y) + __popc(q[6] ^ b.z) + __popc(q[7] ^ b.w);
+                    const int tj = (int)s_idx[j];
+                    // lexicographic (distance, train index) minimum; scan order is irrelevant
+                    const bool better = elig && (dd < best_d || (dd == best_d && tj < best_j));
+                    const bool sec = elig && !better && dd < second_d;
+                    second_d = better ? best_d : (sec ? dd : second_d);
+                    best_d = better ? dd : best_d;
+                    best_j = better ? tj : best_j;
+                    s_tile[wave][jj][lane] = (uint16_t)(elig ? dd : 0xFFFF);
                 }
-                uint32_t packed = elig ? (((uint32_t)dist << 16) | (uint32_t)qi) : 0xFFFFFFFFu;
-                packed = wave_min_u32(packed);
-                if ((threadIdx.x & 63) == 0 && packed != 0xFFFFFFFFu) atomicMin(&s_tmin[j], packed);
+                if (jj0 + 8 >= jcount) break;
             }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            // phase 2: transposed read, lane = train descriptor: (distance, query) minimum over
+            // the wave's 64 queries, no cross-lane reduction
+            if (lane < jcount) {
+                uint32_t best = 0xFFFFFFFFu;
+#pragma unroll 16
+                for (int r = 0; r < 64; ++r) {
+                    const uint32_t d = s_tile[wave][lane][r];
+                    const uint32_t key = (d << 16) | s_qi[wave][r];
+                    best = (d != 0xFFFFu && key < best) ? key : best;
+                }
+                if (best != 0xFFFFFFFFu) atomicMin(&s_tmin[jt + lane], best);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
         }
         __syncthreads();
         for (int i = threadIdx.x; i < jn; i += blockDim.x)
-            if (s_tmin[i] != 0xFFFFFFFFu) atomicMin(&c.tbest[mbase + c.g.koff[l] + j0 + i], s_tmin[i]);
+            if (s_tmin[i] != 0xFFFFFFFFu) atomicMin(&c.tbest[mbase + s_idx[i]], s_tmin[i]);
     }
     if (active) {
-        c.qbest[mbase + qi] = best_j >= 0 ? (((uint32_t)best_d << 16) | (uint32_t)(c.g.koff[l] + best_j)) : 0xFFFFFFFFu;
+        c.qbest[mbase + qi] = best_d < (1 << 20) ? (((uint32_t)best_d << 16) | (uint32_t)best_j) : 0xFFFFFFFFu;
         c.qsecond[mbase + qi] = second_d >= (1 << 20) ? 256u : (uint32_t)second_d;
     }
 }
@@ -109,16 +161,31 @@ __device__ __forceinline__ double parabola(int sm, int s0, int sp) {
     return den > 0 ? (double)(sm - sp) / (2.0 * (double)den) : 0.0;
 }
 
-// 11x11 integer SAD between patch a (centre ax, ay) and patch b (centre bx, by), pitch W.
+// The 11 bytes of row `y` starting at column `x0` as three dwords (byte 12 zeroed), from aligned
+// dword loads + v_alignbyte (any alignment of the level base, row pitch and x0).
+__device__ __forceinline__ void row11(const uint8_t* img, int W, int y, int x0, uint32_t* w) {
+    const uintptr_t addr = reinterpret_cast<uintptr_t>(img + (size_t)y * W + x0);
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(addr & 3u);
+    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3];
+    w[0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
+    w[1] = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    w[2] = __builtin_amdgcn_alignbyte(d3, d2, sh) & 0x00FFFFFFu;
+}
+
+// 11x11 integer SAD between patch a (centre ax, ay) and patch b (centre bx, by), pitch W:
+// 33 v_sad_u8 (4 |a-b| + accumulate per instruction).
 __device__ __forceinline__ int sad11(const uint8_t* a, int ax, int ay, const uint8_t* b, int bx, int by, int W) {
-    int s = 0;
+    uint32_t s = 0;
     for (int dy = -TS_SAD_HALF; dy <= TS_SAD_HALF; ++dy) {
-        const uint8_t* ra = a + (size_t)(ay + dy) * W + ax - TS_SAD_HALF;
-        const uint8_t* rb = b + (size_t)(by + dy) * W + bx - TS_SAD_HALF;
-#pragma unroll
-        for (int t = 0; t < 2 * TS_SAD_HALF + 1; ++t) s += abs((int)ra[t] - (int)rb[t]);
+        uint32_t ra[3], rb[3];
+        row11(a, W, ay + dy, ax - TS_SAD_HALF, ra);
+        row11(b, W, by + dy, bx - TS_SAD_HALF, rb);
+        s = __builtin_amdgcn_sad_u8(ra[0], rb[0], s);
+        s = __builtin_amdgcn_sad_u8(ra[1], rb[1], s);
+        s = __builtin_amdgcn_sad_u8(ra[2], rb[2], s);
     }
-    return s;
+    return (int)s;
 }
 
 // k_match_refine: validity (max distance, ratio, mutual) + sub-pixel refinement, one wave per
@@ -126,24 +193,25 @@ __device__ __forceinline__ int sad11(const uint8_t* a, int ax, int ay, const uin
 // no barriers).  grid (ceil(K/4), n*P*2).
 __global__ __launch_bounds__(256) void k_match_refine(BatchCtx c) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int qi = blockIdx.x * 4 + wave;
-    const int z = blockIdx.y;
+    const int K = c.g.K;
+    int z, local;
+    if (!xcd_image_block(blockIdx.x, c.n * c.P * 2, (K + 3) / 4, &z, &local)) return;
+    const int pos = local * 4 + wave;
     const int mode = z & 1;
     const int fp = z >> 1;
     const int p = fp % c.P;
     const int f = fp / c.P;
     const int64_t g = c.g0 + f;
-    const int K = c.g.K;
-    if (qi >= K) return;
+    if (pos >= K) return;
     const int slot = ring_slot(c, g);
     const size_t mbase = (((size_t)f * c.P + p) * 2 + mode) * K;
     int32_t* out_idx = mode == 0 ? c.stereo + ((size_t)slot * c.P + p) * K : c.temporal + ((size_t)f * c.P + p) * K;
     const int qcam = 2 * p;
     const size_t qkb = ((size_t)slot * c.C + qcam) * K;
-    const uint32_t meta = c.kps[(qkb + qi) * 2 + 1];
-    const int l = meta & 0xFF;
-    const int qn = c.kcount[((size_t)slot * c.C + qcam) * c.g.n_levels + l];
-    bool valid = (qi - c.g.koff[l]) < qn && !(mode == 1 && g == 0);
+    int l;
+    bool kvalid;
+    const int qi = ysorted_kp(c, c.yperm + qkb, c.kcount + ((size_t)slot * c.C + qcam) * c.g.n_levels, pos, &l, &kvalid);
+    bool valid = kvalid && !(mode == 1 && g == 0);
     int j = -1;
     if (valid) {
         const uint32_t qb = c.qbest[mbase + qi];
@@ -180,16 +248,16 @@ __global__ __launch_bounds__(256) void k_match_refine(BatchCtx c) {
         const uint8_t* R = c.pyr + ((size_t)slot * c.C + qcam + 1) * c.g.pyr_bytes + c.g.pyr_off[l];
         int cost = BIG;
         if (lane < 2 * TS_SAD_RANGE + 1) cost = sad11(L, qx, qy, R, xr + lane - TS_SAD_RANGE, qy, W);
-        int cs[5];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) cs[k] = __shfl(cost, k, 64);
+        // first minimum over k: min of (cost << 5 | k) across the wave (no dynamic register indexing)
+        const uint32_t key = wave_min_dpp(lane < 5 ? ((uint32_t)cost << 5) | (uint32_t)lane : 0xFFFFFFFFu);
+        const int ks = (int)(key & 31u);
+        const int c0 = __shfl(cost, ks, 64);
+        const int cm = __shfl(cost, max(ks - 1, 0), 64);
+        const int cp = __shfl(cost, min(ks + 1, 63), 64);
         if (lane == 0) {
-            int ks = 0;
-            for (int k = 1; k < 5; ++k)
-                if (cs[k] < cs[ks]) ks = k;
             double d0 = nanv;
             if (ks > 0 && ks < 4) {
-                const double delta = parabola(cs[ks - 1], cs[ks], cs[ks + 1]);
+                const double delta = parabola(cm, c0, cp);
                 const double sc = (double)(1 << l);
                 const double v = ((double)qx - ((double)(xr + (ks - TS_SAD_RANGE)) + delta)) * sc;
                 if (v > 0.0) d0 = v;
@@ -206,18 +274,17 @@ __global__ __launch_bounds__(256) void k_match_refine(BatchCtx c) {
         const uint8_t* B = c.pyr + ((size_t)slot * c.C + qcam) * c.g.pyr_bytes + c.g.pyr_off[l];
         int cost = BIG;
         if (lane < 25) cost = sad11(A, px, py, B, qx + lane % 5 - TS_SAD_RANGE, qy + lane / 5 - TS_SAD_RANGE, W);
-        int cs[25];
-#pragma unroll
-        for (int o = 0; o < 25; ++o) cs[o] = __shfl(cost, o, 64);
+        const uint32_t key = wave_min_dpp(lane < 25 ? ((uint32_t)cost << 5) | (uint32_t)lane : 0xFFFFFFFFu);
+        const int a = (int)(key & 31u);
+        const int c0 = __shfl(cost, a, 64);
+        const int cl = __shfl(cost, max(a - 1, 0), 64), cr = __shfl(cost, min(a + 1, 63), 64);
+        const int cu = __shfl(cost, max(a - 5, 0), 64), cd = __shfl(cost, min(a + 5, 63), 64);
         if (lane == 0) {
-            int a = 0;
-            for (int o = 1; o < 25; ++o)
-                if (cs[o] < cs[a]) a = o;
             const int ky = a / 5, kx = a % 5;
             double u = nanv, v = nanv;
             if (kx > 0 && kx < 4 && ky > 0 && ky < 4) {
-                const double ddx = parabola(cs[ky * 5 + kx - 1], cs[ky * 5 + kx], cs[ky * 5 + kx + 1]);
-                const double ddy = parabola(cs[(ky - 1) * 5 + kx], cs[ky * 5 + kx], cs[(ky + 1) * 5 + kx]);
+                const double ddx = parabola(cl, c0, cr);
+                const double ddy = parabola(cu, c0, cd);
                 const double sc = (double)(1 << l);
                 u = (((double)(qx + (kx - TS_SAD_RANGE)) + ddx) + 0.5) * sc - 0.5;
                 v = (((double)(qy + (ky - TS_SAD_RANGE)) + ddy) + 0.5) * sc - 0.5;
@@ -236,6 +303,6 @@ void launch_match(const BatchCtx& c, hipStream_t s) {
 }
 
 void launch_match_refine(const BatchCtx& c, hipStream_t s) {
-    dim3 grid((c.g.K + 3) / 4, c.n * c.P * 2);
-    hipLaunchKernelGGL(k_match_refine, grid, dim3(256), 0, s, c);
+    const int bpi = (c.g.K + 3) / 4;
+    hipLaunchKernelGGL(k_match_refine, dim3(xcd_grid(c.n * c.P * 2, bpi)), dim3(256), 0, s, c);
 }

@@ -61,24 +61,29 @@ __device__ void real_roots(const double* c, double lo, double hi, double* out) {
 #pragma unroll
         for (int i = 0; i < N - 1; ++i) pts[i + 1] = __builtin_isnan(crit[i]) ? hi : crit[i];
         pts[N] = hi;
-        double r[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) out[i] = __builtin_nan("");
         int nr = 0;
 #pragma unroll
         for (int i = 0; i < N; ++i) {
             double a = pts[i], b = pts[i + 1];
             const bool sa = horner<N>(c, a) > 0.0;
             const bool sb = horner<N>(c, b) > 0.0;
-            if (sa != sb && b > a) {
+            const bool has = sa != sb && b > a;
+            if (has) {
                 for (int it = 0; it < P3P_BISECT; ++it) {
                     const double m = 0.5 * (a + b);
                     const bool sm = horner<N>(c, m) > 0.0;
                     if (sm == sa) a = m; else b = m;
                 }
-                r[nr++] = 0.5 * (a + b);
             }
-        }
+            const double root = 0.5 * (a + b);
+            // compaction with compile-time register indices (no scratch)
 #pragma unroll
-        for (int i = 0; i < N; ++i) out[i] = i < nr ? r[i] : __builtin_nan("");
+            for (int k = 0; k < N; ++k)
+                if (has && nr == k) out[k] = root;
+            nr += has ? 1 : 0;
+        }
     }
 }
 
@@ -204,46 +209,38 @@ __device__ bool solve6(const double* Hm, const double* g, double* x, double* L) 
 #define POSE_THREADS 256
 #define N_ACC 29   // 21 (upper H) + 6 (g) + 1 (sq) + 1 (count)
 
-__global__ __launch_bounds__(POSE_THREADS) void k_pose(BatchCtx c) {
-    extern __shared__ __attribute__((aligned(16))) double s_pose[];   // [4H][12]
-    __shared__ int s_scan[POSE_THREADS];
-    __shared__ uint32_t s_wbest[4];
-    __shared__ double s_red[4][N_ACC];
-    __shared__ double s_R[9], s_t[3], s_H[36], s_misc[4];
-    __shared__ int s_flag;
+__device__ __forceinline__ void write_stats(int32_t* so, int status, int n, int n_in, int best_cnt, int best_idx, int64_t g) {
+    so[0] = status; so[1] = n; so[2] = n_in; so[3] = best_cnt; so[4] = best_idx; so[5] = (int)g; so[6] = 0; so[7] = 0;
+}
 
+// ---- k_corr: correspondences of one (frame, pair), ordered by the current keypoint index ------
+__global__ __launch_bounds__(POSE_THREADS) void k_corr(BatchCtx c) {
+    __shared__ int s_scan[POSE_THREADS];
     const int fp = blockIdx.x;
     const int p = fp % c.P;
     const int f = fp / c.P;
     const int64_t g = c.g0 + f;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x;
     const int K = c.g.K;
     double* pout = c.pose + (size_t)fp * TS_POSE_DOUBLES;
     int32_t* sout = c.stats + (size_t)fp * TS_STATS_INTS;
-    const PairCalib cal = c.calib[p];
-    const double fx = cal.fx, fy = cal.fy, cx = cal.cx, cy = cal.cy;
-
-    // defaults: identity, zero covariance
     for (int i = tid; i < TS_POSE_DOUBLES; i += POSE_THREADS) pout[i] = (i < 16 && (i % 5) == 0) ? 1.0 : 0.0;
     if (g == 0) {
-        if (tid == 0) {
-            sout[0] = 2; sout[1] = 0; sout[2] = 0; sout[3] = 0; sout[4] = -1; sout[5] = (int)g; sout[6] = 0; sout[7] = 0;
-        }
+        if (tid == 0) write_stats(sout, 2, 0, 0, 0, -1, g);
         return;
     }
+    const PairCalib cal = c.calib[p];
+    const double fx = cal.fx, fy = cal.fy, cx = cal.cx, cy = cal.cy;
     const int pslot = ring_slot(c, g - 1);
     const int32_t* tm = c.temporal + ((size_t)f * c.P + p) * K;
     const double* tuv = c.tuv + ((size_t)f * c.P + p) * K * 2;
     const double* dprev = c.disp + ((size_t)pslot * c.P + p) * K;
     const uint32_t* kprev = c.kps + ((size_t)pslot * c.C + 2 * p) * K * 2;
     double* corr = c.corr + ((size_t)f * c.P + p) * K * TS_CORR_DOUBLES;
-
-    // ---- correspondences, ordered by the current-frame keypoint index ----------------------
     int n = 0;
     for (int base = 0; base < K; base += POSE_THREADS) {
         const int j = base + tid;
-        int flag = 0;
-        int i = -1;
+        int flag = 0, i = -1;
         double u = 0.0, v = 0.0, d = 0.0;
         if (j < K) {
             i = tm[j];
@@ -266,8 +263,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_pose(BatchCtx c) {
         const int tot = s_scan[POSE_THREADS - 1];
         if (flag) {
             const uint32_t xy = kprev[2 * i], meta = kprev[2 * i + 1];
-            const int lv = meta & 0xFF;
-            const double sc = (double)(1 << lv);
+            const double sc = (double)(1 << (meta & 0xFF));
             const double ul = ((double)(xy & 0xFFFF) + 0.5) * sc - 0.5;
             const double vl = ((double)(xy >> 16) + 0.5) * sc - 0.5;
             const double z = cal.fxb / d;
@@ -283,19 +279,40 @@ __global__ __launch_bounds__(POSE_THREADS) void k_pose(BatchCtx c) {
         n += tot;
         __syncthreads();
     }
-    __threadfence_block();
-    const int min_corr = max(6, c.pp.min_inliers);
-    if (n < min_corr) {
-        if (tid == 0) {
-            sout[0] = 1; sout[1] = n; sout[2] = 0; sout[3] = 0; sout[4] = -1; sout[5] = (int)g; sout[6] = 0; sout[7] = 0;
-        }
+    if (tid == 0) write_stats(sout, n < max(6, c.pp.min_inliers) ? 1 : 3, n, 0, 0, -1, g);  // 3 = "to be solved"
+}
+
+// ---- k_ransac: one split of the hypotheses of one (frame, pair) -----------------------------
+// grid (n*P*S): block (fp, split) solves P3P for hypotheses [h0, h1) (one per thread), then
+// scores its 4*(h1-h0) poses with every thread taking one pose and 1/slices of the
+// correspondences; writes its best (count+1)<<12 | (4095 - pose index) key and that pose.
+__global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
+    extern __shared__ __attribute__((aligned(16))) double s_pose[];   // [4*Hs][12]
+    __shared__ int s_cnt[POSE_THREADS];
+    __shared__ uint32_t s_wbest[4];
+    const int fp = blockIdx.x / S;
+    const int split = blockIdx.x % S;
+    const int p = fp % c.P;
+    const int f = fp / c.P;
+    const int64_t g = c.g0 + f;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int32_t* sout = c.stats + (size_t)fp * TS_STATS_INTS;
+    uint32_t* kout = reinterpret_cast<uint32_t*>(c.ransac) + ((size_t)fp * S + split) * TS_RANSAC_WORDS;
+    if (sout[0] != 3) {
+        if (tid == 0) kout[0] = 0u;
         return;
     }
-
-    // ---- phase A: P3P per hypothesis -----------------------------------------------------------
+    const int n = sout[1];
     const int H = c.pp.n_hyp;
+    const int Hs = (H + S - 1) / S;
+    const int h0 = split * Hs, h1 = min(H, h0 + Hs);
+    const int nh = max(0, h1 - h0);
+    const PairCalib cal = c.calib[p];
+    const double fx = cal.fx, fy = cal.fy;
+    const double* corr = c.corr + ((size_t)f * c.P + p) * c.g.K * TS_CORR_DOUBLES;
     const uint64_t base_rng = splitmix64(c.pp.seed ^ ((uint64_t)g * 0x9E3779B97F4A7C15ull));
-    for (int h = tid; h < H; h += POSE_THREADS) {
+    for (int t = tid; t < nh; t += POSE_THREADS) {
+        const int h = h0 + t;
         uint32_t r[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) r[k] = (uint32_t)(splitmix64(base_rng ^ ((uint64_t)h * 4ull + (uint64_t)k)) >> 32);
@@ -318,37 +335,50 @@ __global__ __launch_bounds__(POSE_THREADS) void k_pose(BatchCtx c) {
         Pose sol[4];
         const int mask = p3p_solve(pw, fb, sol);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            double* dst = s_pose + (size_t)(4 * h + s) * 12;
-            if ((mask >> s) & 1) {
+        for (int s2 = 0; s2 < 4; ++s2) {
+            double* dst = s_pose + (size_t)(4 * t + s2) * 12;
+            if ((mask >> s2) & 1) {
 #pragma unroll
-                for (int k = 0; k < 9; ++k) dst[k] = sol[s].r[k];
-                dst[9] = sol[s].t[0]; dst[10] = sol[s].t[1]; dst[11] = sol[s].t[2];
+                for (int k = 0; k < 9; ++k) dst[k] = sol[s2].r[k];
+                dst[9] = sol[s2].t[0]; dst[10] = sol[s2].t[1]; dst[11] = sol[s2].t[2];
             } else {
                 dst[0] = __builtin_nan("");
             }
         }
     }
     __syncthreads();
-
-    // ---- phase B: score every candidate pose -------------------------------------------------
+    const int npose = 4 * nh;
+    const int slices = max(1, POSE_THREADS / max(1, npose));
     const double thr2 = c.pp.thr2;
     uint32_t my_best = 0;
-    for (int pi = tid; pi < 4 * H; pi += POSE_THREADS) {
-        const double* ps = s_pose + (size_t)pi * 12;
-        int cnt = -1;
-        if (!__builtin_isnan(ps[0])) {
-            double R[9], t[3];
+    for (int pi0 = 0; pi0 < npose; pi0 += POSE_THREADS / slices) {
+        const int pi = pi0 + tid / slices;
+        const int sl = tid % slices;
+        int cnt = 0;
+        bool valid = false;
+        if (tid / slices < POSE_THREADS / slices && pi < npose) {
+            const double* ps = s_pose + (size_t)pi * 12;
+            valid = !__builtin_isnan(ps[0]);
+            if (valid) {
+                double R[9], t[3];
 #pragma unroll
-            for (int k = 0; k < 9; ++k) R[k] = ps[k];
-            t[0] = ps[9]; t[1] = ps[10]; t[2] = ps[11];
-            cnt = 0;
-            for (int ci = 0; ci < n; ++ci) cnt += is_inlier(R, t, corr + (size_t)ci * TS_CORR_DOUBLES, fx, fy, thr2) ? 1 : 0;
+                for (int k = 0; k < 9; ++k) R[k] = ps[k];
+                t[0] = ps[9]; t[1] = ps[10]; t[2] = ps[11];
+                for (int ci = sl; ci < n; ci += slices)
+                    cnt += is_inlier(R, t, corr + (size_t)ci * TS_CORR_DOUBLES, fx, fy, thr2) ? 1 : 0;
+            }
         }
-        const uint32_t key = ((uint32_t)(cnt + 1) << 12) | (uint32_t)(4095 - pi);
-        my_best = key > my_best ? key : my_best;
+        s_cnt[tid] = cnt;
+        __syncthreads();
+        if (sl == 0 && tid / slices < POSE_THREADS / slices && pi < npose) {
+            int tot = 0;
+            for (int k = 0; k < slices; ++k) tot += s_cnt[tid + k];
+            const int gidx = 4 * h0 + pi;
+            const uint32_t key = valid ? ((uint32_t)(tot + 1) << 12) | (uint32_t)(4095 - gidx) : (uint32_t)(4095 - gidx);
+            my_best = key > my_best ? key : my_best;
+        }
+        __syncthreads();
     }
-    // block argmax (ties -> lowest pose index)
     uint32_t wb = my_best;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -359,21 +389,58 @@ __global__ __launch_bounds__(POSE_THREADS) void k_pose(BatchCtx c) {
     __syncthreads();
     uint32_t best = s_wbest[0];
     for (int w = 1; w < 4; ++w) best = s_wbest[w] > best ? s_wbest[w] : best;
-    const int best_cnt = (int)(best >> 12) - 1;
-    const int best_idx = 4095 - (int)(best & 4095u);
+    if (tid == 0) kout[0] = best;
+    if (tid < 12 && best != 0u) {
+        const int gidx = 4095 - (int)(best & 4095u);
+        const double v = s_pose[(size_t)(gidx - 4 * h0) * 12 + tid];
+        reinterpret_cast<double*>(kout + 2)[tid] = v;
+    }
+}
+
+// ---- k_refine: pick the best split, Gauss-Newton on the inliers, covariance -----------------
+__global__ __launch_bounds__(POSE_THREADS) void k_refine(BatchCtx c, int S) {
+    __shared__ int s_scan[4];
+    __shared__ double s_red[4][N_ACC];
+    __shared__ double s_R[9], s_t[3], s_H[36], s_misc[4];
+    __shared__ int s_flag, s_best;
+    const int fp = blockIdx.x;
+    const int p = fp % c.P;
+    const int f = fp / c.P;
+    const int64_t g = c.g0 + f;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int32_t* sout = c.stats + (size_t)fp * TS_STATS_INTS;
+    if (sout[0] != 3) return;
+    const int n = sout[1];
+    double* pout = c.pose + (size_t)fp * TS_POSE_DOUBLES;
+    const PairCalib cal = c.calib[p];
+    const double fx = cal.fx, fy = cal.fy, cx = cal.cx, cy = cal.cy;
+    const double thr2 = c.pp.thr2;
+    const double* corr = c.corr + ((size_t)f * c.P + p) * c.g.K * TS_CORR_DOUBLES;
+    const uint32_t* kin = reinterpret_cast<const uint32_t*>(c.ransac) + (size_t)fp * S * TS_RANSAC_WORDS;
+    if (tid == 0) {
+        uint32_t best = 0;
+        int bs = 0;
+        for (int s2 = 0; s2 < S; ++s2)
+            if (kin[s2 * TS_RANSAC_WORDS] > best) {
+                best = kin[s2 * TS_RANSAC_WORDS];
+                bs = s2;
+            }
+        s_best = bs;
+    }
+    __syncthreads();
+    const uint32_t bkey = kin[s_best * TS_RANSAC_WORDS];
+    const int best_cnt = (int)(bkey >> 12) - 1;
+    const int best_idx = 4095 - (int)(bkey & 4095u);
     if (best_cnt < 3) {
-        if (tid == 0) {
-            sout[0] = 1; sout[1] = n; sout[2] = 0; sout[3] = best_cnt; sout[4] = best_idx; sout[5] = (int)g; sout[6] = 0; sout[7] = 0;
-        }
+        if (tid == 0) write_stats(sout, 1, n, 0, best_cnt, best_idx, g);
         return;
     }
     if (tid < 12) {
-        const double v = s_pose[(size_t)best_idx * 12 + tid];
+        const double v = reinterpret_cast<const double*>(kin + s_best * TS_RANSAC_WORDS + 2)[tid];
         if (tid < 9) s_R[tid] = v; else s_t[tid - 9] = v;
     }
     __syncthreads();
 
-    // ---- phase C: Gauss-Newton on the inliers --------------------------------------------------
     bool fail = false;
     double sq_last = 0.0;
     for (int it = 0; it < c.pp.iters; ++it) {
@@ -437,7 +504,6 @@ __global__ __launch_bounds__(POSE_THREADS) void k_pose(BatchCtx c) {
                 if (!solve6(Hm, gv, x, L)) {
                     s_flag = 1;
                 } else {
-                    // Cayley update of the rotation, then t <- ru t + rho
                     const double w0 = x[3], w1 = x[4], w2 = x[5];
                     const double A[9] = {0.0, -w2, w1, w2, 0.0, -w0, -w1, w0, 0.0};
                     double A2[9];
@@ -445,9 +511,9 @@ __global__ __launch_bounds__(POSE_THREADS) void k_pose(BatchCtx c) {
                         for (int j = 0; j < 3; ++j)
                             A2[3 * i + j] = (A[3 * i] * A[j] + A[3 * i + 1] * A[3 + j]) + A[3 * i + 2] * A[6 + j];
                     const double n2 = (w0 * w0 + w1 * w1) + w2 * w2;
-                    const double s = 4.0 / (4.0 + n2);
+                    const double sc = 4.0 / (4.0 + n2);
                     double RU[9];
-                    for (int q = 0; q < 9; ++q) RU[q] = ((q % 4) == 0 ? 1.0 : 0.0) + s * (A[q] + 0.5 * A2[q]);
+                    for (int q = 0; q < 9; ++q) RU[q] = ((q % 4) == 0 ? 1.0 : 0.0) + sc * (A[q] + 0.5 * A2[q]);
                     double Rn[9], tn[3];
                     for (int i = 0; i < 3; ++i) {
                         for (int j = 0; j < 3; ++j)
@@ -468,7 +534,6 @@ __global__ __launch_bounds__(POSE_THREADS) void k_pose(BatchCtx c) {
         }
         sq_last = s_misc[0];
     }
-    // final inlier count
     int cnt_local = 0;
     if (!fail) {
         double R[9], t[3];
@@ -483,68 +548,84 @@ __global__ __launch_bounds__(POSE_THREADS) void k_pose(BatchCtx c) {
     __syncthreads();
     if (tid == 0) {
         const int n_in = ((s_scan[0] + s_scan[1]) + s_scan[2]) + s_scan[3];
-        const bool ok = !fail && c.pp.iters > 0 && n_in >= c.pp.min_inliers;
-        sout[0] = ok ? 0 : 1;
-        sout[1] = n;
-        sout[2] = fail ? 0 : n_in;
-        sout[3] = best_cnt;
-        sout[4] = best_idx;
-        sout[5] = (int)g;
-        sout[6] = 0;
-        sout[7] = 0;
+        const bool ok = !fail && n_in >= c.pp.min_inliers;
+        write_stats(sout, ok ? 0 : 1, n, fail ? 0 : n_in, best_cnt, best_idx, g);
         if (ok) {
             for (int i = 0; i < 3; ++i) {
                 for (int j = 0; j < 3; ++j) pout[4 * i + j] = s_R[3 * i + j];
                 pout[4 * i + 3] = s_t[i];
             }
-            // covariance = sigma^2 H^-1 (columns of the inverse via the Cholesky factor)
             const double sigma2 = sq_last / (double)max(1, 2 * n_in - 6);
             double L[36], e[6], col[6];
             for (int q = 0; q < 36; ++q) L[q] = 0.0;
             for (int k = 0; k < 6; ++k) {
                 for (int q = 0; q < 6; ++q) e[q] = q == k ? 1.0 : 0.0;
-                if (solve6(s_H, e, col, L)) {
+                if (solve6(s_H, e, col, L))
                     for (int q = 0; q < 6; ++q) pout[32 + q * 6 + k] = col[q] * sigma2;
-                }
             }
         }
     }
 }
 
-// One thread per pair: T_abs(t) = T_abs(t-1) * inv(T_rel(t)) for every successful frame.
-__global__ void k_chain(BatchCtx c) {
-    const int p = threadIdx.x;
-    if (p >= c.P) return;
-    double T[16];
-    for (int k = 0; k < 16; ++k) T[k] = c.state[p * 16 + k];
-    for (int f = 0; f < c.n; ++f) {
-        const int fp = f * c.P + p;
-        const double* rel = c.pose + (size_t)fp * TS_POSE_DOUBLES;
-        const int status = c.stats[(size_t)fp * TS_STATS_INTS];
-        if (status == 0) {
-            double inv[16] = {0};
-            for (int i = 0; i < 3; ++i) {
-                for (int j = 0; j < 3; ++j) inv[4 * i + j] = rel[4 * j + i];
-                inv[4 * i + 3] = -((rel[i] * rel[3] + rel[4 + i] * rel[7]) + rel[8 + i] * rel[11]);
-            }
-            inv[15] = 1.0;
-            double out[16];
-            for (int i = 0; i < 4; ++i)
-                for (int j = 0; j < 4; ++j)
-                    out[4 * i + j] = ((T[4 * i] * inv[j] + T[4 * i + 1] * inv[4 + j]) + T[4 * i + 2] * inv[8 + j]) + T[4 * i + 3] * inv[12 + j];
-            for (int k = 0; k < 16; ++k) T[k] = out[k];
+// Pose chaining: T_abs(t) = T_abs(t-1) * inv(T_rel(t)) for every successful frame.  The
+// relative poses of the batch are staged in LDS by the whole block first, so the sequential
+// composition (thread 0, one pair at a time) runs from LDS instead of dependent HBM loads.
+__global__ __launch_bounds__(256) void k_chain(BatchCtx c) {
+    extern __shared__ __attribute__((aligned(16))) double s_rel[];   // [n][12] + status
+    int* s_status = reinterpret_cast<int*>(s_rel + (size_t)c.n * 12);
+    for (int p = 0; p < c.P; ++p) {
+        for (int i = threadIdx.x; i < c.n * 12; i += blockDim.x) {
+            const int f = i / 12, k = i % 12;
+            s_rel[i] = c.pose[(size_t)(f * c.P + p) * TS_POSE_DOUBLES + k];
         }
-        double* ab = c.pose + (size_t)fp * TS_POSE_DOUBLES + 16;
-        for (int k = 0; k < 16; ++k) ab[k] = T[k];
+        for (int f = threadIdx.x; f < c.n; f += blockDim.x) s_status[f] = c.stats[(size_t)(f * c.P + p) * TS_STATS_INTS];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double T[16];
+            for (int k = 0; k < 16; ++k) T[k] = c.state[p * 16 + k];
+            for (int f = 0; f < c.n; ++f) {
+                const double* rel = s_rel + (size_t)f * 12;
+                if (s_status[f] == 0) {
+                    double inv[16] = {0};
+                    for (int i = 0; i < 3; ++i) {
+                        for (int j = 0; j < 3; ++j) inv[4 * i + j] = rel[4 * j + i];
+                        inv[4 * i + 3] = -((rel[i] * rel[3] + rel[4 + i] * rel[7]) + rel[8 + i] * rel[11]);
+                    }
+                    inv[15] = 1.0;
+                    double out[16];
+                    for (int i = 0; i < 4; ++i)
+                        for (int j = 0; j < 4; ++j)
+                            out[4 * i + j] = ((T[4 * i] * inv[j] + T[4 * i + 1] * inv[4 + j]) + T[4 * i + 2] * inv[8 + j]) + T[4 * i + 3] * inv[12 + j];
+                    for (int k = 0; k < 16; ++k) T[k] = out[k];
+                }
+                double* ab = c.pose + (size_t)(f * c.P + p) * TS_POSE_DOUBLES + 16;
+                for (int k = 0; k < 16; ++k) ab[k] = T[k];
+            }
+            for (int k = 0; k < 16; ++k) c.state[p * 16 + k] = T[k];
+        }
+        __syncthreads();
     }
-    for (int k = 0; k < 16; ++k) c.state[p * 16 + k] = T[k];
+}
+
+int ransac_splits(const BatchCtx& c) {
+    if (c.pp.splits > 0) return min(min(c.pp.splits, c.pp.n_hyp), TS_MAX_SPLITS);
+    // enough blocks to cover the chip (>= 512), at least 8 hypotheses per split
+    const int frames = c.n * c.P;
+    int S = (512 + frames - 1) / frames;
+    S = max(1, min(S, max(1, c.pp.n_hyp / 8)));
+    return min(S, TS_MAX_SPLITS);
 }
 
 void launch_pose(const BatchCtx& c, hipStream_t s) {
-    const size_t lds = (size_t)4 * c.pp.n_hyp * 12 * sizeof(double);
-    hipLaunchKernelGGL(k_pose, dim3(c.n * c.P), dim3(POSE_THREADS), lds, s, c);
+    const int S = ransac_splits(c);
+    const int hs = (c.pp.n_hyp + S - 1) / S;
+    const size_t lds = (size_t)4 * hs * 12 * sizeof(double);
+    hipLaunchKernelGGL(k_corr, dim3(c.n * c.P), dim3(POSE_THREADS), 0, s, c);
+    hipLaunchKernelGGL(k_ransac, dim3(c.n * c.P * S), dim3(POSE_THREADS), lds, s, c, S);
+    hipLaunchKernelGGL(k_refine, dim3(c.n * c.P), dim3(POSE_THREADS), 0, s, c, S);
 }
 
 void launch_chain(const BatchCtx& c, hipStream_t s) {
-    hipLaunchKernelGGL(k_chain, dim3(1), dim3(64), 0, s, c);
+    const size_t lds = (size_t)c.n * 12 * sizeof(double) + (size_t)c.n * sizeof(int) + 16;
+    hipLaunchKernelGGL(k_chain, dim3(1), dim3(256), lds, s, c);
 }

@@ -52,6 +52,7 @@ struct tslam_handle {
     uint32_t* d_ccount = nullptr;
     uint32_t* d_hist = nullptr;
     double* d_state = nullptr;
+    double* d_ransac = nullptr;
     int64_t frames_done = 0;
     // current batch
     const uint8_t* cur_images = nullptr;
@@ -114,6 +115,12 @@ static void build_geometry(tslam_handle* h) {
     g.total_bands = bs;
     g.cand_total = co;
     g.total_qtiles = qs;
+    int ro = 0;
+    for (int l = 0; l < p.n_levels; ++l) {
+        g.rs_off[l] = ro;
+        ro += g.H[l] + 1;
+    }
+    g.rs_total = (ro + 7) & ~7;
 }
 
 static BatchCtx make_ctx(tslam_handle* h) {
@@ -138,6 +145,8 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.kps = (uint32_t*)h->buf[TSLAM_BUF_KEYPOINTS].ptr;
     c.kcount = (int32_t*)h->buf[TSLAM_BUF_KCOUNT].ptr;
     c.desc = (uint32_t*)h->buf[TSLAM_BUF_DESC].ptr;
+    c.yperm = (uint16_t*)h->buf[TSLAM_BUF_YPERM].ptr;
+    c.rowstart = (uint16_t*)h->buf[TSLAM_BUF_ROWSTART].ptr;
     c.qbest = (uint32_t*)h->buf[TSLAM_BUF_QBEST].ptr;
     c.qsecond = (uint32_t*)h->buf[TSLAM_BUF_QSECOND].ptr;
     c.tbest = (uint32_t*)h->buf[TSLAM_BUF_TBEST].ptr;
@@ -149,6 +158,7 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.pose = (double*)h->buf[TSLAM_BUF_POSE].ptr;
     c.stats = (int32_t*)h->buf[TSLAM_BUF_STATS].ptr;
     c.state = h->d_state;
+    c.ransac = h->d_ransac;
     c.brief_table = h->d_brief;
     c.wedges = h->d_wedges;
     for (int p = 0; p < h->P; ++p) c.calib[p] = h->calib[p];
@@ -160,6 +170,7 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.pp.n_hyp = h->prm.ransac_hypotheses;
     c.pp.iters = h->prm.refine_iters;
     c.pp.min_inliers = h->prm.min_inliers;
+    c.pp.splits = h->prm.ransac_splits;
     c.pp.thr2 = h->prm.ransac_thr_px * h->prm.ransac_thr_px;
     c.pp.seed = h->prm.ransac_seed;
     c.fast_threshold = h->prm.fast_threshold;
@@ -184,6 +195,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     if (p.fast_threshold < 0 || p.fast_threshold > 254) return fail(TSLAM_EINVAL, "fast_threshold must be in [0, 254]");
     if (p.max_batch < 1) return fail(TSLAM_EINVAL, "max_batch must be >= 1");
     if (p.refine_iters < 1) return fail(TSLAM_EINVAL, "refine_iters must be >= 1");
+    if (p.ransac_splits < 0 || p.ransac_splits > TS_MAX_SPLITS) return fail(TSLAM_EINVAL, "ransac_splits must be in [0, 32]");
     const int W = pairs[0].width, H = pairs[0].height;
     if (W < 64 || H < 64 || W > 2047 || H > 2047) return fail(TSLAM_EINVAL, "image size must be within [64, 2047]");
     for (int i = 1; i < p.n_pairs; ++i)
@@ -236,6 +248,8 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
         {TSLAM_BUF_QBEST, B, P * 2 * K * 4},
         {TSLAM_BUF_QSECOND, B, P * 2 * K * 4},
         {TSLAM_BUF_TBEST, B, P * 2 * K * 4},
+        {TSLAM_BUF_YPERM, R, C * K * 2},
+        {TSLAM_BUF_ROWSTART, R, C * (int64_t)h->g.rs_total * 2},
     };
     int rc = TSLAM_OK;
     for (const Spec& s : specs) {
@@ -248,6 +262,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_ccount, sizeof(uint32_t) * (size_t)B * C * h->g.total_bands);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_hist, sizeof(uint32_t) * (size_t)B * C * L * 256);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_state, sizeof(double) * 16 * (size_t)P);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_ransac, sizeof(uint32_t) * TS_RANSAC_WORDS * TS_MAX_SPLITS * (size_t)B * P);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_brief, sizeof(TSLAM_BRIEF_TABLE));
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_wedges, sizeof(TSLAM_WEDGES));
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_maps, sizeof(int32_t) * (size_t)C * W * H * 2);

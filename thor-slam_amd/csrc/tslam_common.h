@@ -11,6 +11,7 @@
 //   kps      u32 [R][C][K][2]        {x | y<<16, level | angle<<8 | score<<16}
 //   kcount   i32 [R][C][L]
 //   desc     u32 [R][C][K][8]        rBRIEF-256
+//   yperm    u16 [R][C][K]  rowstart u16 [R][C][sum(H_l+1)]  per-level y-sorted order + row index
 //   qbest/qsecond/tbest u32 [B][P][2][K]   matching scratch (mode 0 stereo, 1 temporal)
 //   stereo   i32 [R][P][K]  disp f64 [R][P][K]        stereo match + refined disparity of left kps
 //   temporal i32 [B][P][K]  tuv  f64 [B][P][K][2]     temporal match + refined (u, v) at t
@@ -25,13 +26,15 @@
 #define TS_BAND_ROWS 16
 #define TS_DET_HALO 4
 #define TS_RECT_BAND 32
-#define TS_MATCH_CHUNK 1024
+#define TS_MATCH_CHUNK 512
 #define TS_SAD_HALF 5
 #define TS_SAD_RANGE 2
 #define TS_POSE_DOUBLES 68
 #define TS_STATS_INTS 8
 #define TS_CORR_DOUBLES 8
 #define TS_MAX_HYP 1024
+#define TS_MAX_SPLITS 32   // RANSAC blocks per frame
+#define TS_RANSAC_WORDS 26 // per split: key + pad + 12 doubles
 
 struct LevelGeom {
     int n_levels;
@@ -47,6 +50,8 @@ struct LevelGeom {
     int cand_total;                // u32 per image
     int qtiles[TS_MAX_LEVELS], qtile_start[TS_MAX_LEVELS];  // 256-query tiles per level
     int total_qtiles;
+    int rs_off[TS_MAX_LEVELS];     // u16 offset of level l's row-start table (H_l + 1 entries)
+    int rs_total;                  // u16 per image
 };
 
 struct PairCalib {
@@ -58,7 +63,7 @@ struct MatchParams {
 };
 
 struct PoseParams {
-    int n_hyp, iters, min_inliers;
+    int n_hyp, iters, min_inliers, splits;
     double thr2;
     uint64_t seed;
 };
@@ -83,6 +88,8 @@ struct BatchCtx {
     uint32_t* kps;
     int32_t* kcount;
     uint32_t* desc;
+    uint16_t* yperm;       // [R][C][K]
+    uint16_t* rowstart;    // [R][C][rs_total]
     uint32_t* qbest;
     uint32_t* qsecond;
     uint32_t* tbest;
@@ -92,6 +99,7 @@ struct BatchCtx {
     double* tuv;
     double* corr;
     double* pose;
+    double* ransac;        // [B][P][TS_MAX_SPLITS][13] split winners (key word + pose)
     int32_t* stats;
     double* state;
     const uint32_t* brief_table;  // [30][256] packed int8x4 (px, py, qx, qy)
@@ -134,8 +142,54 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return v;
 }
 
+// Wave-uniform minimum via DPP row reductions (quad perms, half-row and row mirrors: VALU
+// latency, no LDS crossbar) and four readlanes.  Requires all 64 lanes active.
+__device__ __forceinline__ uint32_t wave_min_dpp(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false));  // row_mirror
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+    return min(min(a, b), min(c, d));
+}
+
+// Wave-uniform sum via the same DPP row reduction (result in an SGPR).
+__device__ __forceinline__ int wave_sum_dpp(int v) {
+    v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
+    v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);
+    v += __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false);
+    v += __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false);
+    return (__builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16)) +
+           (__builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48));
+}
+
 __device__ __forceinline__ double wave_sum_f64(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
+}
+
+// XCD-aware 1-D block mapping: blocks are dealt round-robin over the 8 XCDs, so block b runs on the
+// XCD labelled b % 8.  Give all `bpi` blocks of one image the same label, so that image's pyramid
+// lines are fetched into one L2 only.  Speed only: correctness never depends on placement.
+// Launch with xcd_grid(n_img, bpi) blocks; returns false for the padding blocks.
+static inline __host__ int xcd_grid(int n_img, int bpi) { return ((n_img + 7) / 8) * 8 * bpi; }
+__device__ __forceinline__ bool xcd_image_block(int b, int n_img, int bpi, int* img, int* local) {
+    const int k = b >> 3;
+    *img = (k / bpi) * 8 + (b & 7);
+    *local = k % bpi;
+    return *img < n_img;
+}
+
+// Keypoint slot for position `pos` of an image walked level by level in y-sorted order (padding
+// positions map to themselves).  Returns the keypoint index and its level.
+__device__ __forceinline__ int ysorted_kp(const BatchCtx& c, const uint16_t* yperm_img, const int32_t* kcount_img,
+                                          int pos, int* level, bool* valid) {
+    int l = 0;
+    while (l + 1 < c.g.n_levels && pos >= c.g.koff[l + 1]) ++l;
+    *level = l;
+    const int r = pos - c.g.koff[l];
+    *valid = r < kcount_img[l];
+    return *valid ? (int)yperm_img[pos] : pos;
 }

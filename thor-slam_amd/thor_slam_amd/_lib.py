@@ -22,7 +22,7 @@ LIB_PATH = Path(__file__).resolve().parent / LIB_NAME
 BUF = {
     "pyramid": 0, "smooth": 1, "keypoints": 2, "kcount": 3, "desc": 4, "stereo": 5, "disp": 6,
     "temporal": 7, "temporal_uv": 8, "corr": 9, "pose": 10, "stats": 11, "qbest": 12,
-    "qsecond": 13, "tbest": 14,
+    "qsecond": 13, "tbest": 14, "yperm": 15, "rowstart": 16,
 }
 STAGE = {"rectify": 0, "detect": 1, "describe": 2, "match": 3, "pose": 4, "all": 5}
 # single kernels, in pipeline order (bench.py times each with HIP events)
@@ -49,7 +49,7 @@ class Params(ctypes.Structure):
         ("stereo_row_tol", ctypes.c_int32), ("max_disparity", ctypes.c_int32), ("temporal_window", ctypes.c_int32),
         ("ransac_hypotheses", ctypes.c_int32), ("refine_iters", ctypes.c_int32), ("min_inliers", ctypes.c_int32),
         ("ransac_thr_px", ctypes.c_double), ("ransac_seed", ctypes.c_uint64),
-        ("max_batch", ctypes.c_int32), ("n_pairs", ctypes.c_int32),
+        ("max_batch", ctypes.c_int32), ("n_pairs", ctypes.c_int32), ("ransac_splits", ctypes.c_int32),
     ]
 
 
@@ -121,18 +121,19 @@ def _check(rc: int) -> None:
         raise RuntimeError(f"tslam error {rc}: {msg.decode() if msg else ''}")
 
 
-def make_params(cfg: HipSlamConfig, max_batch: int, n_pairs: int) -> Params:
+def make_params(cfg: HipSlamConfig, max_batch: int, n_pairs: int, ransac_splits: int = 0) -> Params:
     return Params(
         cfg.n_features, cfg.n_levels, cfg.fast_threshold, cfg.edge_margin, cfg.max_hamming, cfg.ratio_pct,
         cfg.stereo_row_tol, cfg.max_disparity, cfg.temporal_window, cfg.ransac_hypotheses, cfg.refine_iters,
         cfg.min_inliers, float(cfg.ransac_thr_px), int(cfg.ransac_seed) & ((1 << 64) - 1), int(max_batch), int(n_pairs),
+        int(ransac_splits),
     )
 
 
 class Handle:
     """Owns one ``tslam_handle`` (one device, ``n_pairs`` stereo pairs, batches <= ``max_batch``)."""
 
-    def __init__(self, rects: list, cfg: HipSlamConfig, max_batch: int = 1, device: int = 0):
+    def __init__(self, rects: list, cfg: HipSlamConfig, max_batch: int = 1, device: int = 0, ransac_splits: int = 0):
         self.lib = load_library()
         cfg.validate()
         self.cfg = cfg
@@ -149,7 +150,7 @@ class Handle:
                 None if ml is None else ml.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
                 None if mr is None else mr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
             )
-        params = make_params(cfg, max_batch, self.n_pairs)
+        params = make_params(cfg, max_batch, self.n_pairs, ransac_splits)
         h = ctypes.c_void_p()
         _check(self.lib.tslam_create(descs, ctypes.byref(params), int(device), ctypes.byref(h)))
         self.h = h
