@@ -36,6 +36,10 @@ for _p in (ROOT, ROOT / "thor-slam_amd"):
 
 METRIC = "synced stereo frames/sec (detect+match+pose) @640×400, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0
+# bench kernel label -> device symbol (rocprofv3 / PMC summaries); "pose" is k_corr+k_ransac+k_refine
+KERNEL_SYMBOL = {"rectify_pyramid": "k_rectify_pyramid", "detect": "k_detect", "select": "k_select",
+                 "describe": "k_describe", "match": "k_match", "match_refine": "k_match_refine",
+                 "pose": "k_ransac", "chain": "k_chain"}
 
 
 def _render_chunk(args):
@@ -115,11 +119,14 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=64, help="stereo frames per step")
+    ap.add_argument("--batch", type=int, default=256, help="stereo frames per step")
     ap.add_argument("--unique", type=int, default=48, help="distinct rendered frames (triangle-wave replay)")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU baseline (0 = skip)")
     ap.add_argument("--kernel-reps", type=int, default=5)
     ap.add_argument("--out", type=str, default="", help="also write the JSON line to this file")
+    ap.add_argument("--dist-backend", type=str, default="nccl", help="nccl (RCCL) or gloo (rehearsal, host copy)")
+    ap.add_argument("--pmc", type=str, default=str(ROOT / "profiles" / "pmc_latest.json"),
+                    help="PMC summary (tools/pmc_summary.py) used for roofline.traffic when its batch matches")
     args = ap.parse_args()
 
     import torch
@@ -127,6 +134,7 @@ def main() -> None:
 
     from thor_slam_amd._lib import KERNELS, Handle
     from thor_slam_amd.calib import extract_cameras, stereo_pairs, stereo_rectify
+    from thor_slam_amd.dist import BlockLayout, FeatureExchange
     from thor_slam_amd.camera.rig import CameraRig
     from thor_slam_amd.params import HipSlamConfig
     from thor_slam_amd.synthetic import SyntheticStereoSource
@@ -136,9 +144,13 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
+    dev_index = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     cfg = HipSlamConfig()
     B = args.batch
@@ -154,18 +166,23 @@ def main() -> None:
     total = (args.warmup + args.steps) * B
     idx = torch.from_numpy(triangle_indices(total, args.unique)).cuda()
     seq = torch.from_numpy(uniq).cuda().index_select(0, idx).contiguous()  # [total, 2, H, W] in HBM
-    h = Handle([rect], cfg, max_batch=B, device=local)
+    h = Handle([rect], cfg, max_batch=B, device=dev_index)
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
-    feat_bytes = 2 * (cfg.n_features * 40 + cfg.n_levels * 4)
-    gather_src = torch.empty((B * feat_bytes,), dtype=torch.uint8, device="cuda")
-    gather_dst = torch.empty((world * B * feat_bytes,), dtype=torch.uint8, device="cuda") if world > 1 else None
+    layout = BlockLayout(n_frames=B, n_cams=2, K=cfg.n_features, L=cfg.n_levels)
+    on_device = args.dist_backend == "nccl"
+    exchange = FeatureExchange(layout, "cuda" if on_device else "cpu", world) if world > 1 else None
+    staging = torch.empty((layout.rank_bytes,), dtype=torch.uint8, device="cuda") if world > 1 and not on_device else None
 
     def step(s: int) -> None:
         h.submit(seq[s * B].data_ptr(), B, sp)
-        if world > 1:
-            h.pack_features(gather_src.data_ptr(), sp)
-            dist.all_gather_into_tensor(gather_dst, gather_src)
+        if exchange is not None:  # the exchange step: every rank's keypoints/descriptors/poses to all
+            if on_device:
+                h.pack_features(exchange.send.data_ptr(), sp)
+            else:
+                h.pack_features(staging.data_ptr(), sp)
+                exchange.send.copy_(staging.cpu())
+            exchange.all_gather()
 
     for s in range(args.warmup):
         step(s)
@@ -207,6 +224,14 @@ def main() -> None:
     dom_bytes = kernel_bytes(dom, B, h, cfg, rect.is_identity)
     achieved = dom_bytes / (per_kernel_us[dom] * 1e-6) / 1e9
 
+    traffic = None
+    pmc_path = Path(args.pmc)
+    if pmc_path.exists():
+        pmc = json.loads(pmc_path.read_text())
+        kern = pmc.get("kernels", {}).get(KERNEL_SYMBOL.get(dom, ""), None)
+        if kern is not None and pmc.get("batch_frames") == B:
+            traffic = kern["hbm_bytes_per_launch"]
+
     frames_total = world * args.steps * B
     out = {
         "metric": METRIC,
@@ -236,7 +261,7 @@ def main() -> None:
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": traffic,
             "algorithmic_bytes_per_launch": dom_bytes,
             "avg_launch_us": per_kernel_us[dom],
         },

@@ -163,7 +163,8 @@ int tslam_ring_slot(tslam_handle* h, int64_t global_frame);
 int tslam_layout(tslam_handle* h, int64_t* out16, int32_t* level_info18);
 
 /* Copy the keypoints + descriptors + counts of the last batch into `dst` (device):
- * [n_frames][cams] blocks of (K*8 + K*32 + levels*4) bytes.  Returns bytes per frame in *bytes. */
+ * [n_frames][cams] blocks of (K*8 + K*32 + levels*4) bytes, then a pose trailer per
+ * (frame, pair) of T_rel[16] + cov[36] f64 and stats[8] i32.  Returns the total in *bytes. */
 int tslam_pack_features(tslam_handle* h, void* dst, int64_t* bytes, void* stream);
 
 #ifdef __cplusplus

@@ -1,0 +1,140 @@
+"""End-to-end on the GPU: HipSlamEngine behind the SlamEngine contract driven by CameraRig, and
+multi-pair handles (P > 1) equal to independent single-pair runs."""
+
+from __future__ import annotations
+
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from helpers import make_source, rel_frobenius, scenario
+from oracle import numpy_slam as O
+from thor_slam_amd.calib import extract_cameras, stereo_pairs, stereo_rectify
+from thor_slam_amd.camera import CameraRig, Extrinsics
+from thor_slam_amd.dist import fuse_rig_motion
+from thor_slam_amd.params import HipSlamConfig
+from thor_slam_amd.slam import TrackingState
+from thor_slam_amd.synthetic import RoomScene, SyntheticStereoSource, circle_trajectory
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_handle(rects, frames, cfg, batch):
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    h = Handle(rects, cfg, max_batch=batch)
+    dev = torch.from_numpy(np.ascontiguousarray(frames)).cuda()
+    out = []
+    n = frames.shape[0]
+    for b0 in range(0, n, batch):
+        nb = min(batch, n - b0)
+        h.submit(dev[b0:].data_ptr(), nb, torch.cuda.current_stream().cuda_stream)
+        res = h.read_poses(nb)
+        for f in range(nb):
+            g = b0 + f
+            out.append({"kp": [h.keypoints(g, c) for c in range(2 * len(rects))], "stats": res["stats"][f], "T_abs": res["T_abs"][f]})
+    h.close()
+    return out
+
+
+def test_multi_pair_handle_equals_single_pairs():
+    a, b = scenario(seed=0, n=3), scenario(seed=7, n=3)
+    cfg = a["cfg"]
+    both = np.concatenate([a["frames"], b["frames"]], axis=1)  # [n][4][H][W]
+    multi = _run_handle([a["rect"], b["rect"]], both, cfg, batch=3)
+    sa = _run_handle([a["rect"]], a["frames"], cfg, batch=3)
+    sb = _run_handle([b["rect"]], b["frames"], cfg, batch=3)
+    for i in range(3):
+        for cam in range(4):
+            ref = (sa if cam < 2 else sb)[i]["kp"][cam % 2]
+            for k in ("x", "y", "score", "angle", "counts"):
+                np.testing.assert_array_equal(multi[i]["kp"][cam][k], ref[k], err_msg=f"frame {i} cam {cam} {k}")
+            np.testing.assert_array_equal(multi[i]["kp"][cam]["desc"], ref["desc"])
+        np.testing.assert_array_equal(multi[i]["stats"][0], sa[i]["stats"][0])
+        np.testing.assert_array_equal(multi[i]["stats"][1], sb[i]["stats"][0])
+        np.testing.assert_array_equal(multi[i]["T_abs"][1], sb[i]["T_abs"][0])
+
+
+def _engine_poses(cfg, n, batch):
+    from thor_slam_amd.slam.hip_engine import HipSlamEngine
+
+    src = make_source(0)
+    rig = CameraRig([src], rig_extrinsics={src.name: Extrinsics.from_4x4_matrix(src.rig_T_source)})
+    rig.start()
+    eng = HipSlamEngine(num_cameras=2, config=HipSlamConfig(batch_size=batch))
+    eng.initialize(rig.calibration)
+    poses, states = [], []
+    for _ in range(n):
+        poses.append(eng.process_frames(rig.get_synchronized_frames()))
+        states.append(eng.get_tracking_state())
+    eng.flush()
+    final = eng._latest_pose
+    eng.shutdown()
+    return src, poses, states, final
+
+
+def test_engine_end_to_end_matches_oracle():
+    n = 4
+    src, poses, states, _ = _engine_poses(HipSlamConfig(), n, batch=1)
+    sc = scenario(seed=0, n=n)
+    base_T_cam = src.rig_T_source @ src.get_extrinsics()[0].to_4x4_matrix() @ sc["rect"].left_optical_T_rect()
+    assert states[0] == TrackingState.INITIALIZING and all(s == TrackingState.TRACKING for s in states[1:])
+    for i, pose in enumerate(poses):
+        want = base_T_cam @ sc["oracle"][i]["world_T_cam"] @ np.linalg.inv(base_T_cam)
+        assert rel_frobenius(pose.to_4x4_matrix(), want) < 1e-9
+        assert 0.0 < pose.confidence <= 1.0
+        if i:
+            assert pose.covariance.shape == (6, 6) and pose.tracking_state == TrackingState.TRACKING
+    # the body-frame motion also agrees with the rendered ground truth (FLU base_link)
+    gt = np.linalg.inv(src.ground_truth_body(0)) @ src.ground_truth_body(n - 1)
+    assert np.linalg.norm(poses[-1].position - gt[:3, 3]) < 0.1 * np.linalg.norm(gt[:3, 3]) + 2e-3
+
+
+def test_engine_batched_mode_returns_completed_poses():
+    _, p1, _, f1 = _engine_poses(HipSlamConfig(), 5, batch=1)
+    _, p3, _, f3 = _engine_poses(HipSlamConfig(), 5, batch=3)
+    assert p3[0] is None and p3[1] is None and p3[2] is not None  # first batch completes at frame 3
+    assert rel_frobenius(p3[2].to_4x4_matrix(), p1[2].to_4x4_matrix()) < 1e-12
+    assert rel_frobenius(f3.to_4x4_matrix(), f1.to_4x4_matrix()) < 1e-12
+
+
+def test_engine_two_source_rig_fuses_motion():
+    from thor_slam_amd.slam.hip_engine import HipSlamEngine
+
+    mats = json.loads((Path(__file__).parent / "golden" / "brackets_joints.json").read_text())
+    names = ["192.168.2.21", "192.168.2.25"]
+    scene = RoomScene(seed=0)
+    traj = circle_trajectory(40)
+    srcs = [SyntheticStereoSource(name=nm, scene=scene, trajectory=traj, rig_T_source=np.array(mats[nm]), seed=k)
+            for k, nm in enumerate(names)]
+    rig = CameraRig(srcs, rig_extrinsics={nm: Extrinsics.from_4x4_matrix(np.array(mats[nm])) for nm in names})
+    rig.start()
+    eng = HipSlamEngine(num_cameras=4)
+    eng.initialize(rig.calibration)
+    n = 6
+    for _ in range(n):
+        pose = eng.process_frames(rig.get_synchronized_frames())
+    assert eng.get_tracking_state() == TrackingState.TRACKING
+    # oracle: track each pair on the CPU and fuse with the same host rule
+    cams = extract_cameras(rig.calibration, 4)
+    pairs = stereo_pairs(cams)
+    rects = [stereo_rectify(cams[l], cams[r]) for l, r in pairs]
+    bts = [cams[l].extrinsics.to_4x4_matrix() @ r.left_optical_T_rect() for (l, _), r in zip(pairs, rects)]
+    by_name = {s.name: s for s in srcs}
+    trks = [O.OracleTracker(HipSlamConfig(), dict(fx=r.fx, fy=r.fy, cx=r.cx, cy=r.cy, baseline=r.baseline,
+                                                  map_l=r.map_left, map_r=r.map_right)) for r in rects]
+    want = np.eye(4)
+    for i in range(n):
+        outs = [trk.step(by_name[cams[l].source_name].render_image(i, 0), by_name[cams[l].source_name].render_image(i, 1))
+                for trk, (l, _) in zip(trks, pairs)]
+        if i:
+            want = want @ fuse_rig_motion(bts, [o["T"] for o in outs], [o["cov"] for o in outs], [o["status"] == 0 for o in outs])
+    assert rel_frobenius(pose.to_4x4_matrix(), want) < 1e-9
+    gt = np.linalg.inv(traj[0]) @ traj[n - 1]
+    err = np.linalg.norm(pose.position - gt[:3, 3])
+    assert err < 0.15 * np.linalg.norm(gt[:3, 3]) + 3e-3, err
+    eng.shutdown()

@@ -33,6 +33,7 @@ from .._lib import POSE_INIT, POSE_LOST, POSE_OK, Handle
 from ..calib import StereoRectification, confidence_from_covariance, extract_cameras, stereo_pairs, stereo_rectify
 from ..camera.rig import RigCalibration
 from ..camera.types import SynchronizedFrameSet
+from ..dist import fuse_rig_motion
 from ..params import HipSlamConfig
 from .interface import CameraConfig, MapPoint, SlamConfig, SlamEngine, SlamMap, SlamPose, TrackingState
 
@@ -103,8 +104,10 @@ class HipSlamEngine(SlamEngine):
             shape = (cfg.batch_size, n_cams, rect0.height, rect0.width)
             self._dev_images = torch.empty(shape, dtype=torch.uint8, device=f"cuda:{self._device}")
             self._host_images = torch.empty(shape, dtype=torch.uint8).pin_memory()
-            left = self._cameras[self._pairs[0][0]]
-            self._base_T_rect = left.extrinsics.to_4x4_matrix() @ rect0.left_optical_T_rect()
+            self._base_T_rects = [self._cameras[l].extrinsics.to_4x4_matrix() @ r.left_optical_T_rect()
+                                  for (l, _), r in zip(self._pairs, self._rects)]
+            self._base_T_rect = self._base_T_rects[0]
+            self._world_T_base = np.eye(4)
         except RuntimeError:
             raise
         except Exception as exc:  # per interface.py:187-188
@@ -169,21 +172,38 @@ class HipSlamEngine(SlamEngine):
         self._publish(res, timestamps or [float(i) for i in range(n)])
         return res
 
-    def _publish(self, res: dict, stamps: list[float]) -> None:
+    def _body_pose(self, res: dict, k: int) -> tuple[int, np.ndarray, np.ndarray]:
+        """(status, world_T_base, 6x6 body covariance) of frame k of a batch result."""
         bt = self._base_T_rect
-        tb = _invert(bt)
         rot6 = np.zeros((6, 6))
         rot6[:3, :3] = rot6[3:, 3:] = bt[:3, :3]
+        stats = res["stats"][k, :, 0]
+        if len(self._pairs) == 1:
+            status = int(stats[0])
+            body = bt @ res["T_abs"][k, 0] @ _invert(bt)
+            cov = rot6 @ res["cov"][k, 0] @ rot6.T if status == POSE_OK else np.zeros((6, 6))
+            return status, body, cov
+        # multi-pair rig: information-weighted fusion of the per-pair body motions, chained here
+        if (stats == POSE_INIT).all():
+            self._world_T_base = np.eye(4)
+            return POSE_INIT, self._world_T_base.copy(), np.zeros((6, 6))
+        ok = [int(st) == POSE_OK for st in stats]
+        motion = fuse_rig_motion(self._base_T_rects, list(res["T_rel"][k]), list(res["cov"][k]), ok)
+        if motion is None:
+            return POSE_LOST, self._world_T_base.copy(), np.zeros((6, 6))
+        self._world_T_base = self._world_T_base @ motion
+        best = int(np.argmax([res["stats"][k, p, 2] if ok[p] else -1 for p in range(len(ok))]))
+        return POSE_OK, self._world_T_base.copy(), rot6 @ res["cov"][k, best] @ rot6.T
+
+    def _publish(self, res: dict, stamps: list[float]) -> None:
         latest = None
         state = self._state
         for k, ts in enumerate(stamps):
-            status = int(res["stats"][k, 0, 0])
+            status, body, cov = self._body_pose(res, k)
             if status == POSE_LOST:
                 state = TrackingState.LOST
                 latest = None
                 continue
-            body = bt @ res["T_abs"][k, 0] @ tb
-            cov = rot6 @ res["cov"][k, 0] @ rot6.T if status == POSE_OK else np.zeros((6, 6))
             state = TrackingState.TRACKING if status == POSE_OK else TrackingState.INITIALIZING
             latest = SlamPose(
                 position=body[:3, 3].copy(),
@@ -219,6 +239,7 @@ class HipSlamEngine(SlamEngine):
             self._latest_pose = None
         self._staged = []
         self._keyframe_poses = []
+        self._world_T_base = np.eye(4)
         if self._handle is not None:
             self._handle.reset()
         self._state = TrackingState.INITIALIZING
