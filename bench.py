@@ -38,7 +38,7 @@ METRIC = "synced stereo frames/sec (detect+match+pose) @640×400, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0
 # bench kernel label -> device symbol (rocprofv3 / PMC summaries); "pose" is k_corr+k_ransac+k_refine
 KERNEL_SYMBOL = {"rectify_pyramid": "k_rectify_pyramid", "detect": "k_detect", "select": "k_select",
-                 "describe": "k_describe", "match": "k_match", "match_refine": "k_match_refine",
+                 "describe": "k_describe", "match": "k_match", "match_refine": "k_refine_temporal",
                  "pose": "k_ransac", "chain": "k_chain"}
 
 

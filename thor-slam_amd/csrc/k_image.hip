@@ -87,8 +87,7 @@ __device__ __forceinline__ s16x2 pk_min(s16x2 a, s16x2 b) { return __builtin_ele
 __device__ __forceinline__ s16x2 pk_max(s16x2 a, s16x2 b) { return __builtin_elementwise_max(a, b); }
 __device__ __forceinline__ s16x2 swp(s16x2 a) { return __builtin_shufflevector(a, a, 1, 0); }
 
-__device__ __forceinline__ int fast9_score(const uint8_t* t, int W, int r, int x, int thr) {
-    const uint8_t* p = t + r * W + x;
+__device__ __forceinline__ int fast9_core(const uint8_t* p, int W, int thr, bool pretest) {
     const int c0 = p[0];
     int d[16];
     d[0] = p[-3 * W] - c0;      d[1] = p[-3 * W + 1] - c0; d[2] = p[-2 * W + 2] - c0; d[3] = p[-W + 3] - c0;
@@ -97,8 +96,10 @@ __device__ __forceinline__ int fast9_score(const uint8_t* t, int W, int r, int x
     d[12] = p[-3] - c0;         d[13] = p[-W - 3] - c0;    d[14] = p[-2 * W - 2] - c0; d[15] = p[-3 * W - 1] - c0;
     // every 9-arc contains circle index 0 or 8, and 4 or 12: a pixel is not a corner when
     // both of either pair are within the threshold (score irrelevant then: it becomes 0).
-    const bool rej = (abs(d[0]) <= thr && abs(d[8]) <= thr) || (abs(d[4]) <= thr && abs(d[12]) <= thr);
-    if (rej) return 0;
+    if (pretest) {
+        const bool rej = (abs(d[0]) <= thr && abs(d[8]) <= thr) || (abs(d[4]) <= thr && abs(d[12]) <= thr);
+        if (rej) return 0;
+    }
     // packed pairs P[k] = (d[k], d[k+8]); circle index k+8 (k < 8) is the swapped pair.
     s16x2 P[8];
 #pragma unroll
@@ -130,12 +131,145 @@ __device__ __forceinline__ int fast9_score(const uint8_t* t, int W, int r, int x
     return max(max(bright, -darkmin), 0);
 }
 
+__device__ __forceinline__ int fast9_score(const uint8_t* t, int W, int r, int x, int thr) {
+    return fast9_core(t + r * W + x, W, thr, true);
+}
+
+// FAST-9 scores of the 4 pixels x0..x0+3 of tile row `rc` (pitch W), thresholded (score > thr,
+// else 0), as 4 bytes.  Straight-line packed f16: the pixels travel as (x0, x0+2) / (x0+1, x0+3)
+// pairs; a byte b becomes the f16 1024 + b (0x64 as its high byte, one v_perm per pair), so
+// every difference, min and max below is exact.  The 16 circle windows come from 3 dword LDS reads per
+// circle row + v_alignbyte; each 9-arc minimum is min3(min3 of 3, 3, 3) (v_pk_minimum3_f16).
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ h16x2 hmin3(h16x2 a, h16x2 b, h16x2 c) {
+    return __builtin_elementwise_minimum(a, __builtin_elementwise_minimum(b, c));
+}
+__device__ __forceinline__ h16x2 hmax3(h16x2 a, h16x2 b, h16x2 c) {
+    return __builtin_elementwise_maximum(a, __builtin_elementwise_maximum(b, c));
+}
+
+__device__ __forceinline__ uint32_t fast4(const uint8_t* rc, int W, int x0, int thr) {
+    // circle index k -> (dx, dy): 0 (0,-3) 1 (1,-3) 2 (2,-2) 3 (3,-1) 4 (3,0) 5 (3,1) 6 (2,2)
+    // 7 (1,3) 8 (0,3) 9 (-1,3) 10 (-2,2) 11 (-3,1) 12 (-3,0) 13 (-3,-1) 14 (-2,-2) 15 (-1,-3)
+    uint32_t win[16], cen;
+    {
+        const uint32_t* p = (const uint32_t*)(rc - 3 * W + x0);   // rows walked by adding W
+        const int Wd = W >> 2;
+        uint32_t a, b, c;
+        auto rd = [&]() {
+            a = p[-1];
+            b = p[0];
+            c = p[1];
+            p += Wd;
+        };
+        rd();   // dy = -3
+        win[15] = __builtin_amdgcn_alignbyte(b, a, 3); win[0] = b; win[1] = __builtin_amdgcn_alignbyte(c, b, 1);
+        rd();   // dy = -2
+        win[14] = __builtin_amdgcn_alignbyte(b, a, 2); win[2] = __builtin_amdgcn_alignbyte(c, b, 2);
+        rd();   // dy = -1
+        win[13] = __builtin_amdgcn_alignbyte(b, a, 1); win[3] = __builtin_amdgcn_alignbyte(c, b, 3);
+        rd();   // dy = 0
+        win[12] = __builtin_amdgcn_alignbyte(b, a, 1); win[4] = __builtin_amdgcn_alignbyte(c, b, 3); cen = b;
+        rd();   // dy = 1
+        win[11] = __builtin_amdgcn_alignbyte(b, a, 1); win[5] = __builtin_amdgcn_alignbyte(c, b, 3);
+        rd();   // dy = 2
+        win[10] = __builtin_amdgcn_alignbyte(b, a, 2); win[6] = __builtin_amdgcn_alignbyte(c, b, 2);
+        rd();   // dy = 3
+        win[9] = __builtin_amdgcn_alignbyte(b, a, 3); win[8] = b; win[7] = __builtin_amdgcn_alignbyte(c, b, 1);
+    }
+    // Arc extrema are taken on the raw values (min over an arc of (p - c) = (min over it of p) - c),
+    // so the centre is subtracted once: score = max(max_k min9_k - c, c - min_k max9_k, 0).
+    uint32_t out = 0;
+    constexpr uint32_t k64 = 0x64646464u;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {   // h = 0: pixels x0, x0+2; h = 1: pixels x0+1, x0+3
+        // v_perm: bytes (h, 2+h) of the window into the low bytes of two f16 lanes, 0x64 above
+        const uint32_t sel = h ? 0x00070005u : 0x00060004u;
+        auto toh = [sel](uint32_t v) { return __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(v, k64, sel)); };
+        h16x2 p[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) p[k] = toh(win[k]);
+        h16x2 a3[16], b3[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            a3[k] = hmin3(p[k], p[(k + 1) & 15], p[(k + 2) & 15]);
+            b3[k] = hmax3(p[k], p[(k + 1) & 15], p[(k + 2) & 15]);
+        }
+        h16x2 a9[16], b9[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            a9[k] = hmin3(a3[k], a3[(k + 3) & 15], a3[(k + 6) & 15]);
+            b9[k] = hmax3(b3[k], b3[(k + 3) & 15], b3[(k + 6) & 15]);
+        }
+        h16x2 br = hmax3(a9[0], a9[1], a9[2]), dk = hmin3(b9[0], b9[1], b9[2]);
+#pragma unroll
+        for (int k = 3; k < 15; k += 2) {
+            br = hmax3(br, a9[k], a9[k + 1]);
+            dk = hmin3(dk, b9[k], b9[k + 1]);
+        }
+        br = __builtin_elementwise_maximum(br, a9[15]);
+        dk = __builtin_elementwise_minimum(dk, b9[15]);
+        const h16x2 cc = toh(cen);
+        const h16x2 zero = {(_Float16)0, (_Float16)0};
+        const h16x2 sc = hmax3(br - cc, cc - dk, zero) + (h16x2){(_Float16)1024, (_Float16)1024};
+        const uint32_t bits = __builtin_bit_cast(uint32_t, sc) & 0x03FF03FFu;   // (score, score) as u16
+        const uint32_t s0 = bits & 0xFFFFu, s1 = bits >> 16;
+        out |= (s0 > (uint32_t)thr ? s0 : 0u) << (8 * h);
+        out |= (s1 > (uint32_t)thr ? s1 : 0u) << (8 * h + 16);
+    }
+    return out;
+}
+
 // ---------------------------------------------------------------------------------------------
 // A3 smoothing + A4 FAST/NMS candidates for one 16-row band of one level.
-// grid (total_bands, n*C), block 256 (4 waves; wave w takes rows w, w+4, ...; lanes walk x).
-// LDS: image rows [y0-4, y0+20) (row-clamped), scores of rows [y0-1, y0+17).
+// grid (total_bands, n*C), block 512 (8 waves).  LDS: image rows [y0-4, y0+20) (row-clamped),
+// scores of rows [y0-1, y0+17).  ~36 KiB per block -> 4 blocks = 32 waves per CU (the kernel is
+// latency-bound, so occupancy is what hides the LDS and memory latencies).  Work inside each
+// phase is dealt to the 8 waves in equal (row, 64-lane chunk) items.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_detect(BatchCtx c) {
+#define TS_DET_THREADS 512
+#define TS_DET_WAVES (TS_DET_THREADS / 64)
+
+// 16-byte async global -> LDS copy; `wave_dst` is the wave-uniform LDS base, lane k lands at +16k
+__device__ __forceinline__ void glds16(const uint4* src, uint4* wave_dst) {
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)wave_dst, 16, 0, 0);
+}
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// Horizontal 1-4-6-4-1 of the 4 pixels x0..x0+3 of one tile row as two u16 pairs:
+// ev = (h[x0], h[x0+2]), od = (h[x0+1], h[x0+3]).  Byte windows D_k = row[x0-2+k .. x0+1+k];
+// (D_k & 0x00FF00FF) are the taps of the even pair, (D_k >> 8) & 0x00FF00FF of the odd pair.
+// Column clamp (x-2 < 0, x+2 > W-1) only for the first and last quad of a row.
+__device__ __forceinline__ void hsum4(const uint8_t* row, int x0, int W, u16x2* ev, u16x2* od) {
+    uint32_t D[5];
+    if (x0 >= 4 && x0 + 8 <= W) {
+        const uint32_t a = *(const uint32_t*)(row + x0 - 4), b = *(const uint32_t*)(row + x0),
+                       c2 = *(const uint32_t*)(row + x0 + 4);
+        D[0] = __builtin_amdgcn_alignbyte(b, a, 2);
+        D[1] = __builtin_amdgcn_alignbyte(b, a, 3);
+        D[2] = b;
+        D[3] = __builtin_amdgcn_alignbyte(c2, b, 1);
+        D[4] = __builtin_amdgcn_alignbyte(c2, b, 2);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w |= (uint32_t)row[min(max(x0 - 2 + k + j, 0), W - 1)] << (8 * j);
+            D[k] = w;
+        }
+    }
+    const u16x2 four = {4, 4}, six = {6, 6};
+    auto lo = [](uint32_t v) { return __builtin_bit_cast(u16x2, v & 0x00FF00FFu); };
+    auto hi = [](uint32_t v) { return __builtin_bit_cast(u16x2, (v >> 8) & 0x00FF00FFu); };
+    *ev = lo(D[0]) + four * lo(D[1]) + six * lo(D[2]) + four * lo(D[3]) + lo(D[4]);
+    *od = hi(D[0]) + four * hi(D[1]) + six * hi(D[2]) + four * hi(D[3]) + hi(D[4]);
+}
+
+__global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ uint32_t s_hist[256];
     __shared__ uint32_t s_count;
@@ -154,74 +288,147 @@ __global__ __launch_bounds__(256) void k_detect(BatchCtx c) {
     const int NR = TS_BAND_ROWS + 2 * TS_DET_HALO;
     uint8_t* tile = lds;
     uint8_t* score = lds + NR * W;
+    const int thr = c.fast_threshold;
+    // dword rows (W % 4 == 0: every config in BASELINE.json) take the packed paths; byte rows
+    // the scalar ones
+    const bool wide = ((W & 3) == 0) && ((img_off & 3) == 0);
+    const int rows_here = min(TS_BAND_ROWS, H - y0);
 
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_hist[i] = 0;
+    for (int i = threadIdx.x; i < 256; i += TS_DET_THREADS) s_hist[i] = 0;
     if (threadIdx.x == 0) s_count = 0;
-    for (int r = wave; r < NR; r += 4) {
-        const int y = min(max(y0 - TS_DET_HALO + r, 0), H - 1);
-        for (int x = lane; x < W; x += 64) tile[r * W + x] = src[(size_t)y * W + x];
+    if (((W & 15) == 0) && ((img_off & 15) == 0)) {
+        // LDS-DMA: each wave-instruction lands 1 KiB of the lane-linear tile, no VGPRs
+        const int W16 = W >> 4, n16 = NR * W16;
+        const uint4* s16 = (const uint4*)src;
+        for (int i0 = wave * 64; i0 < n16; i0 += TS_DET_THREADS) {
+            const int i = i0 + lane;
+            if (i < n16) {
+                const int r = i / W16, x = i - r * W16;
+                glds16(s16 + (size_t)min(max(y0 - TS_DET_HALO + r, 0), H - 1) * W16 + x, (uint4*)tile + i0);
+            }
+        }
+    } else {
+        for (int i = threadIdx.x; i < NR * W; i += TS_DET_THREADS) {
+            const int r = i / W, x = i - r * W;
+            tile[i] = src[(size_t)min(max(y0 - TS_DET_HALO + r, 0), H - 1) * W + x];
+        }
     }
     __syncthreads();
 
-    // 5x5 binomial smoothing of the band rows (column clamp; rows already clamped in LDS):
-    // each thread walks one column down the tile keeping the last five horizontal 1-4-6-4-1
-    // sums in registers (5 LDS reads per output pixel instead of 25).
-    const int rows_here = min(TS_BAND_ROWS, H - y0);
-    for (int x = threadIdx.x; x < W; x += blockDim.x) {
-        const int xm2 = max(x - 2, 0), xm1 = max(x - 1, 0), xp1 = min(x + 1, W - 1), xp2 = min(x + 2, W - 1);
-        int h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-        for (int r = TS_DET_HALO - 2; r < TS_DET_HALO + rows_here + 2; ++r) {
-            const uint8_t* row = tile + r * W;
-            const int h4 = row[xm2] + 4 * row[xm1] + 6 * row[x] + 4 * row[xp1] + row[xp2];
-            if (r >= TS_DET_HALO + 2) {
-                const int acc = h0 + 4 * h1 + 6 * h2 + 4 * h3 + h4;
-                smo[(size_t)(y0 + r - 2 - TS_DET_HALO) * W + x] = (uint8_t)((acc + 128) >> 8);
+    // 5x5 binomial smoothing of the band rows (column clamp; rows already clamped in LDS).
+#ifndef XP_SKIP_SMOOTH
+    if (wide) {
+        // item = (4-pixel quad, 8-row half): 12 horizontal sums (3 dword LDS reads each) slide
+        // through 5 registers; u16 pairs cannot overflow (16 * 16 * 255 + 128 < 2^16)
+        const int W4 = W >> 2;
+        const u16x2 four = {4, 4}, six = {6, 6}, rnd = {128, 128};
+        for (int it = threadIdx.x; it < 2 * W4; it += TS_DET_THREADS) {
+            const int half = it / W4, q = it - half * W4, x0 = 4 * q;
+            const int o0 = 8 * half, o1 = min(o0 + 8, rows_here);   // output rows (band-relative)
+            if (o0 >= o1) continue;
+            u16x2 e[5], d[5];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) hsum4(tile + (TS_DET_HALO - 2 + o0 + k) * W, x0, W, &e[k], &d[k]);
+            for (int o = o0; o < o1; ++o) {
+                hsum4(tile + (TS_DET_HALO + 2 + o) * W, x0, W, &e[4], &d[4]);
+                const u16x2 ve = (e[0] + four * e[1] + six * e[2] + four * e[3] + e[4] + rnd) >> 8;
+                const u16x2 vo = (d[0] + four * d[1] + six * d[2] + four * d[3] + d[4] + rnd) >> 8;
+                *(uint32_t*)(smo + (size_t)(y0 + o) * W + x0) =
+                    (uint32_t)ve.x | ((uint32_t)vo.x << 8) | ((uint32_t)ve.y << 16) | ((uint32_t)vo.y << 24);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    e[k] = e[k + 1];
+                    d[k] = d[k + 1];
+                }
             }
-            h0 = h1; h1 = h2; h2 = h3; h3 = h4;
+        }
+    } else {
+        for (int x = threadIdx.x; x < W; x += TS_DET_THREADS) {
+            const int xm2 = max(x - 2, 0), xm1 = max(x - 1, 0), xp1 = min(x + 1, W - 1), xp2 = min(x + 2, W - 1);
+            int h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+            for (int r = TS_DET_HALO - 2; r < TS_DET_HALO + rows_here + 2; ++r) {
+                const uint8_t* row = tile + r * W;
+                const int h4 = row[xm2] + 4 * row[xm1] + 6 * row[x] + 4 * row[xp1] + row[xp2];
+                if (r >= TS_DET_HALO + 2) {
+                    const int acc = h0 + 4 * h1 + 6 * h2 + 4 * h3 + h4;
+                    smo[(size_t)(y0 + r - 2 - TS_DET_HALO) * W + x] = (uint8_t)((acc + 128) >> 8);
+                }
+                h0 = h1; h1 = h2; h2 = h3; h3 = h4;
+            }
         }
     }
+#endif
 
     // FAST scores (thresholded) for rows y0-1 .. y0+16
-    const int thr = c.fast_threshold;
-    for (int r = wave; r < TS_BAND_ROWS + 2; r += 4) {
-        const int y = y0 - 1 + r;
-        for (int x = lane; x < W; x += 64) {
-            int s = 0;
-            if (y >= 3 && y < H - 3 && x >= 3 && x < W - 3) {
-                s = fast9_score(tile, W, r + TS_DET_HALO - 1, x, thr);
-                if (s <= thr) s = 0;
+#ifndef XP_SKIP_FAST
+    if (wide) {
+        // 4 pixels per lane (fast4): 21 dword LDS reads and ~250 packed-f16 ops per quad, no
+        // divergence; items (row, quad) dealt over the block
+        uint32_t* score32 = (uint32_t*)score;
+        const int W4 = W >> 2;
+        for (int it = threadIdx.x; it < (TS_BAND_ROWS + 2) * W4; it += TS_DET_THREADS) {
+            const int r = it / W4, x4 = it - r * W4;
+            const int y = y0 - 1 + r;
+            uint32_t sc4 = 0;
+            if (y >= 3 && y < H - 3) {
+                const int x0 = 4 * x4;
+                sc4 = fast4(tile + (r + TS_DET_HALO - 1) * W, W, x0, thr);
+                if (x0 < 3) sc4 &= 0xFFFFFFFFu << (8 * (3 - x0));                    // x >= 3
+                if (x0 + 4 > W - 3) {                                                // x < W-3
+                    const int keep = max(W - 3 - x0, 0);                             // pixels kept
+                    sc4 &= keep >= 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u);
+                }
             }
-            score[r * W + x] = (uint8_t)s;
+            score32[r * W4 + x4] = sc4;
+        }
+    } else {
+        for (int i = threadIdx.x; i < (TS_BAND_ROWS + 2) * W; i += TS_DET_THREADS) {
+            const int r = i / W, x = i - r * W;
+            const int y = y0 - 1 + r;
+            int sc = 0;
+            if (y >= 3 && y < H - 3 && x >= 3 && x < W - 3) {
+                sc = fast9_score(tile, W, r + TS_DET_HALO - 1, x, thr);
+                if (sc <= thr) sc = 0;
+            }
+            score[i] = (uint8_t)sc;
         }
     }
+#endif
     __syncthreads();
 
-    // 3x3 NMS (ties -> earlier raster position) inside the margin; emit keys
+    // 3x3 NMS (ties -> earlier raster position) inside the margin; emit keys.  Items = (row,
+    // 64-pixel chunk) dealt round-robin over the waves.
     const int M = c.margin;
     uint32_t* cand = c.cand + ((size_t)f * c.C + cam) * c.g.cand_total + c.g.cand_off[l] + (size_t)band * c.g.cand_cap[l];
+#ifdef XP_SKIP_NMS
+    const int ylo = 0, yhi = 0;
+#else
     const int ylo = max(y0, M), yhi = min(y0 + TS_BAND_ROWS, H - M);
-    for (int y = ylo + wave; y < yhi; y += 4) {
+#endif
+    const int xspan = W - 2 * M, nchx = (xspan + 63) >> 6;
+    for (int it = wave; it < (yhi - ylo) * nchx; it += TS_DET_WAVES) {
+        const int yy = it / nchx, ch = it - yy * nchx;
+        const int y = ylo + yy, x = M + ch * 64 + lane;
+        if (x >= W - M) continue;
         const int r = y - y0 + 1;
-        for (int x = M + lane; x < W - M; x += 64) {
-            const int p = score[r * W + x];
-            if (p == 0) continue;
-            const uint8_t* up = score + (r - 1) * W + x;
-            const uint8_t* mid = score + r * W + x;
-            const uint8_t* dn = score + (r + 1) * W + x;
-            const bool keep = up[-1] < p && up[0] < p && up[1] < p && mid[-1] < p &&
-                              mid[1] <= p && dn[-1] <= p && dn[0] <= p && dn[1] <= p;
-            if (keep) {
-                const uint32_t key = ((uint32_t)(255 - p) << 22) | ((uint32_t)y << 11) | (uint32_t)x;
-                const uint32_t slot = atomicAdd(&s_count, 1u);
-                cand[slot] = key;
-                atomicAdd(&s_hist[255 - p], 1u);
-            }
+        const int p = score[r * W + x];
+        if (p == 0) continue;
+        const uint8_t* up = score + (r - 1) * W + x;
+        const uint8_t* mid = score + r * W + x;
+        const uint8_t* dn = score + (r + 1) * W + x;
+        const bool keep = up[-1] < p && up[0] < p && up[1] < p && mid[-1] < p &&
+                          mid[1] <= p && dn[-1] <= p && dn[0] <= p && dn[1] <= p;
+        if (keep) {
+            const uint32_t key = ((uint32_t)(255 - p) << 22) | ((uint32_t)y << 11) | (uint32_t)x;
+            const uint32_t slot = atomicAdd(&s_count, 1u);
+            cand[slot] = key;
+            atomicAdd(&s_hist[255 - p], 1u);
         }
     }
     __syncthreads();
     if (threadIdx.x == 0) c.ccount[((size_t)f * c.C + cam) * c.g.total_bands + blockIdx.x] = s_count;
     uint32_t* gh = c.hist + (((size_t)f * c.C + cam) * c.g.n_levels + l) * 256;
-    for (int i = threadIdx.x; i < 256; i += blockDim.x)
+    for (int i = threadIdx.x; i < 256; i += TS_DET_THREADS)
         if (s_hist[i]) atomicAdd(&gh[i], s_hist[i]);
 }
 
@@ -432,7 +639,7 @@ void launch_detect(const BatchCtx& c, hipStream_t s) {
     const size_t lds = (size_t)(TS_BAND_ROWS + 2 * TS_DET_HALO + TS_BAND_ROWS + 2) * c.g.W[0];
     dim3 grid(c.g.total_bands, c.n * c.C);
     (void)hipMemsetAsync(c.hist, 0, sizeof(uint32_t) * 256 * c.g.n_levels * c.C * (size_t)c.n, s);
-    hipLaunchKernelGGL(k_detect, grid, dim3(256), lds, s, c);
+    hipLaunchKernelGGL(k_detect, grid, dim3(TS_DET_THREADS), lds, s, c);
 }
 
 void launch_select(const BatchCtx& c, hipStream_t s) {

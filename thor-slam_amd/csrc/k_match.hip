@@ -164,9 +164,9 @@ __device__ __forceinline__ double parabola(int sm, int s0, int sp) {
 // The 11 bytes of row `y` starting at column `x0` as three dwords (byte 12 zeroed), from aligned
 // dword loads + v_alignbyte (any alignment of the level base, row pitch and x0).
 __device__ __forceinline__ void row11(const uint8_t* img, int W, int y, int x0, uint32_t* w) {
-    const uintptr_t addr = reinterpret_cast<uintptr_t>(img + (size_t)y * W + x0);
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(addr & 3u);
+    const uint8_t* a = img + (size_t)y * W + x0;
+    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 3u);
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(a - sh);   // pointer arithmetic keeps global loads
     const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3];
     w[0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
     w[1] = __builtin_amdgcn_alignbyte(d2, d1, sh);
@@ -188,110 +188,206 @@ __device__ __forceinline__ int sad11(const uint8_t* a, int ax, int ay, const uin
     return (int)s;
 }
 
-// k_match_refine: validity (max distance, ratio, mutual) + sub-pixel refinement, one wave per
-// query keypoint (4 per block), one search offset per lane, costs gathered by shuffles (no LDS,
-// no barriers).  grid (ceil(K/4), n*P*2).
-__global__ __launch_bounds__(256) void k_match_refine(BatchCtx c) {
+// Validity of the match of query keypoint qi (max distance, ratio, mutual); returns the train
+// index or -1.
+__device__ __forceinline__ int match_valid(const BatchCtx& c, size_t mbase, int qi) {
+    const uint32_t qb = c.qbest[mbase + qi];
+    if (qb == 0xFFFFFFFFu) return -1;
+    const int bd = qb >> 16, j = qb & 0xFFFF;
+    const int sd = c.qsecond[mbase + qi];
+    const uint32_t tb = c.tbest[mbase + j];
+    return (bd <= c.mp.max_hamming && bd * 100 < c.mp.ratio_pct * sd && (int)(tb & 0xFFFF) == qi) ? j : -1;
+}
+
+// Stereo refinement (A6b): validity + disparity by 5-offset SAD + parabola.  One wave serves
+// 12 queries, 5 lanes each (lane = query slot * 5 + offset), so the index chain and the loads of
+// a query are issued once per 12 queries; the SAD rows are direct dword loads (the 5 lanes of a
+// query share the left patch lines).  grid xcd_grid(n*P, ceil(K/48)), block 256.
+#define TS_RS_Q 12
+__global__ __launch_bounds__(256) void k_refine_stereo(BatchCtx c) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int K = c.g.K;
     int z, local;
-    if (!xcd_image_block(blockIdx.x, c.n * c.P * 2, (K + 3) / 4, &z, &local)) return;
-    const int pos = local * 4 + wave;
-    const int mode = z & 1;
-    const int fp = z >> 1;
-    const int p = fp % c.P;
-    const int f = fp / c.P;
+    if (!xcd_image_block(blockIdx.x, c.n * c.P, (K + 4 * TS_RS_Q - 1) / (4 * TS_RS_Q), &z, &local)) return;
+    const int p = z % c.P, f = z / c.P;
     const int64_t g = c.g0 + f;
-    if (pos >= K) return;
     const int slot = ring_slot(c, g);
-    const size_t mbase = (((size_t)f * c.P + p) * 2 + mode) * K;
-    int32_t* out_idx = mode == 0 ? c.stereo + ((size_t)slot * c.P + p) * K : c.temporal + ((size_t)f * c.P + p) * K;
+    const int qs = lane / 5, k = lane - 5 * qs;
+    const int pos = (local * 4 + wave) * TS_RS_Q + qs;
+    const bool live = lane < 5 * TS_RS_Q && pos < K;
+    const size_t mbase = (((size_t)f * c.P + p) * 2 + 0) * K;
     const int qcam = 2 * p;
     const size_t qkb = ((size_t)slot * c.C + qcam) * K;
-    int l;
-    bool kvalid;
-    const int qi = ysorted_kp(c, c.yperm + qkb, c.kcount + ((size_t)slot * c.C + qcam) * c.g.n_levels, pos, &l, &kvalid);
-    bool valid = kvalid && !(mode == 1 && g == 0);
-    int j = -1;
-    if (valid) {
-        const uint32_t qb = c.qbest[mbase + qi];
-        if (qb == 0xFFFFFFFFu) {
-            valid = false;
-        } else {
-            const int bd = qb >> 16;
-            j = qb & 0xFFFF;
-            const int sd = c.qsecond[mbase + qi];
-            const uint32_t tb = c.tbest[mbase + j];
-            valid = bd <= c.mp.max_hamming && bd * 100 < c.mp.ratio_pct * sd && (int)(tb & 0xFFFF) == qi;
-        }
+    int l = 0, qi = 0, j = -1;
+    if (live) {
+        bool kvalid;
+        qi = ysorted_kp(c, c.yperm + qkb, c.kcount + ((size_t)slot * c.C + qcam) * c.g.n_levels, pos, &l, &kvalid);
+        if (kvalid) j = match_valid(c, mbase, qi);
     }
-    if (lane == 0) out_idx[qi] = valid ? j : -1;
-    double* out_val = mode == 0 ? c.disp + ((size_t)slot * c.P + p) * K + qi
-                                : c.tuv + (((size_t)f * c.P + p) * K + qi) * 2;
     const double nanv = __builtin_nan("");
-    if (!valid) {
-        if (lane == 0) {
-            out_val[0] = nanv;
-            if (mode == 1) out_val[1] = nanv;
-        }
-        return;
+    if (live && k == 0 && j < 0) {
+        c.stereo[((size_t)slot * c.P + p) * K + qi] = -1;
+        c.disp[((size_t)slot * c.P + p) * K + qi] = nanv;
     }
-    const int W = c.g.W[l];
-    const uint32_t qxy = c.kps[(qkb + qi) * 2];
-    const int qx = qxy & 0xFFFF, qy = qxy >> 16;
     const int BIG = 0x7FFFFFFF;
-    if (mode == 0) {
-        // left patch at (qx, qy) vs right row qy at xr + k, k in [-2, 2]
-        const size_t rkb = ((size_t)slot * c.C + qcam + 1) * K;
-        const int xr = c.kps[(rkb + j) * 2] & 0xFFFF;
+    int cost = BIG, qx = 0, xr = 0;
+    if (j >= 0) {
+        const int W = c.g.W[l];
+        const uint32_t qxy = c.kps[(qkb + qi) * 2];
+        qx = qxy & 0xFFFF;
+        const int qy = qxy >> 16;
+        xr = c.kps[(((size_t)slot * c.C + qcam + 1) * K + j) * 2] & 0xFFFF;
         const uint8_t* L = c.pyr + ((size_t)slot * c.C + qcam) * c.g.pyr_bytes + c.g.pyr_off[l];
         const uint8_t* R = c.pyr + ((size_t)slot * c.C + qcam + 1) * c.g.pyr_bytes + c.g.pyr_off[l];
-        int cost = BIG;
-        if (lane < 2 * TS_SAD_RANGE + 1) cost = sad11(L, qx, qy, R, xr + lane - TS_SAD_RANGE, qy, W);
-        // first minimum over k: min of (cost << 5 | k) across the wave (no dynamic register indexing)
-        const uint32_t key = wave_min_dpp(lane < 5 ? ((uint32_t)cost << 5) | (uint32_t)lane : 0xFFFFFFFFu);
+        cost = sad11(L, qx, qy, R, xr + k - TS_SAD_RANGE, qy, W);
+    }
+    // first minimum over the 5 offsets of each query: (cost << 5 | k) over the lane group
+    const int base = 5 * qs;
+    uint32_t key = 0xFFFFFFFFu;
+    int cs[5];
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+        cs[u] = __shfl(cost, min(base + u, 63), 64);
+        const uint32_t ku = cs[u] == BIG ? 0xFFFFFFFFu : (((uint32_t)cs[u] << 5) | (uint32_t)u);
+        key = ku < key ? ku : key;
+    }
+    if (j >= 0 && k == 0) {
         const int ks = (int)(key & 31u);
-        const int c0 = __shfl(cost, ks, 64);
-        const int cm = __shfl(cost, max(ks - 1, 0), 64);
-        const int cp = __shfl(cost, min(ks + 1, 63), 64);
-        if (lane == 0) {
-            double d0 = nanv;
-            if (ks > 0 && ks < 4) {
-                const double delta = parabola(cm, c0, cp);
-                const double sc = (double)(1 << l);
-                const double v = ((double)qx - ((double)(xr + (ks - TS_SAD_RANGE)) + delta)) * sc;
-                if (v > 0.0) d0 = v;
-            }
-            out_val[0] = d0;
+        double d0 = nanv;
+        if (ks > 0 && ks < 4) {
+            int c0 = cs[0], cm = cs[0], cp = cs[0];
+#pragma unroll
+            for (int u = 1; u < 4; ++u)
+                if (u == ks) {
+                    cm = cs[u - 1];
+                    c0 = cs[u];
+                    cp = cs[u + 1];
+                }
+            const double delta = parabola(cm, c0, cp);
+            const double sc = (double)(1 << l);
+            const double v = ((double)qx - ((double)(xr + (ks - TS_SAD_RANGE)) + delta)) * sc;
+            if (v > 0.0) d0 = v;
         }
-    } else {
-        // left(t-1) patch at kp j vs left(t) at (qx + kx, qy + ky), kx, ky in [-2, 2]
+        c.stereo[((size_t)slot * c.P + p) * K + qi] = j;
+        c.disp[((size_t)slot * c.P + p) * K + qi] = d0;
+    }
+}
+
+// Temporal refinement (A7a): validity + position by 5x5 SAD search + 2-D parabola.  Two queries
+// per wave (half-waves, 25 lanes each).  The query's 11x11 patch at t-1 and the 15x15 search
+// window at t are staged in LDS (a few coalesced loads per query instead of 88 gathers per lane),
+// rows padded to 16 bytes and read back as ds_read_b128.  grid xcd_grid(n*P, ceil(K/8)), block 256.
+#define TS_RT_AROWS 11
+#define TS_RT_BROWS 15
+__global__ __launch_bounds__(256) void k_refine_temporal(BatchCtx c) {
+    __shared__ uint4 s_a[8][TS_RT_AROWS];   // [query slot][row]: 11 bytes used (+ zero pad)
+    __shared__ uint4 s_b[8][TS_RT_BROWS];   // 15 bytes used
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int K = c.g.K;
+    int z, local;
+    if (!xcd_image_block(blockIdx.x, c.n * c.P, (K + 7) / 8, &z, &local)) return;
+    const int p = z % c.P, f = z / c.P;
+    const int64_t g = c.g0 + f;
+    const int slot = ring_slot(c, g);
+    const int half = lane >> 5, hl = lane & 31;
+    const int qslot = wave * 2 + half;
+    const int pos = local * 8 + qslot;
+    const bool live = pos < K;
+    const size_t mbase = (((size_t)f * c.P + p) * 2 + 1) * K;
+    const int qcam = 2 * p;
+    const size_t qkb = ((size_t)slot * c.C + qcam) * K;
+    int l = 0, qi = 0, j = -1;
+    if (live) {
+        bool kvalid;
+        qi = ysorted_kp(c, c.yperm + qkb, c.kcount + ((size_t)slot * c.C + qcam) * c.g.n_levels, pos, &l, &kvalid);
+        if (kvalid && g > 0) j = match_valid(c, mbase, qi);
+    }
+    int32_t* out_idx = c.temporal + ((size_t)f * c.P + p) * K;
+    double* out_uv = c.tuv + (((size_t)f * c.P + p) * K + qi) * 2;
+    const double nanv = __builtin_nan("");
+    if (live && hl == 0) out_idx[qi] = j;
+    if (live && hl == 0 && j < 0) {
+        out_uv[0] = nanv;
+        out_uv[1] = nanv;
+    }
+    int qx = 0, qy = 0, W = 0;
+    if (j >= 0) {
+        W = c.g.W[l];
+        const uint32_t qxy = c.kps[(qkb + qi) * 2];
+        qx = qxy & 0xFFFF;
+        qy = qxy >> 16;
         const int pslot = ring_slot(c, g - 1);
-        const size_t pkb = ((size_t)pslot * c.C + qcam) * K;
-        const uint32_t pxy = c.kps[(pkb + j) * 2];
+        const uint32_t pxy = c.kps[(((size_t)pslot * c.C + qcam) * K + j) * 2];
         const int px = pxy & 0xFFFF, py = pxy >> 16;
         const uint8_t* A = c.pyr + ((size_t)pslot * c.C + qcam) * c.g.pyr_bytes + c.g.pyr_off[l];
         const uint8_t* B = c.pyr + ((size_t)slot * c.C + qcam) * c.g.pyr_bytes + c.g.pyr_off[l];
-        int cost = BIG;
-        if (lane < 25) cost = sad11(A, px, py, B, qx + lane % 5 - TS_SAD_RANGE, qy + lane / 5 - TS_SAD_RANGE, W);
-        const uint32_t key = wave_min_dpp(lane < 25 ? ((uint32_t)cost << 5) | (uint32_t)lane : 0xFFFFFFFFu);
-        const int a = (int)(key & 31u);
-        const int c0 = __shfl(cost, a, 64);
-        const int cl = __shfl(cost, max(a - 1, 0), 64), cr = __shfl(cost, min(a + 1, 63), 64);
-        const int cu = __shfl(cost, max(a - 5, 0), 64), cd = __shfl(cost, min(a + 5, 63), 64);
-        if (lane == 0) {
-            const int ky = a / 5, kx = a % 5;
-            double u = nanv, v = nanv;
-            if (kx > 0 && kx < 4 && ky > 0 && ky < 4) {
-                const double ddx = parabola(cl, c0, cr);
-                const double ddy = parabola(cu, c0, cd);
-                const double sc = (double)(1 << l);
-                u = (((double)(qx + (kx - TS_SAD_RANGE)) + ddx) + 0.5) * sc - 0.5;
-                v = (((double)(qy + (ky - TS_SAD_RANGE)) + ddy) + 0.5) * sc - 0.5;
-            }
-            out_val[0] = u;
-            out_val[1] = v;
+        // stage: lanes 0..10 the patch rows (3 dwords via row11), lanes 11..25 the window rows
+        // (15 bytes from 5 aligned dwords + alignbyte)
+        uint4 v = {0u, 0u, 0u, 0u};
+        if (hl < TS_RT_AROWS) {
+            uint32_t w3[3];
+            row11(A, W, py - TS_SAD_HALF + hl, px - TS_SAD_HALF, w3);
+            v = {w3[0], w3[1], w3[2], 0u};
+            s_a[qslot][hl] = v;
+        } else if (hl < TS_RT_AROWS + TS_RT_BROWS) {
+            const int r = hl - TS_RT_AROWS;
+            const uint8_t* a = B + (size_t)(qy - TS_SAD_HALF - TS_SAD_RANGE + r) * W + (qx - TS_SAD_HALF - TS_SAD_RANGE);
+            const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 3u);
+            const uint32_t* q = reinterpret_cast<const uint32_t*>(a - sh);
+            const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
+            v = {__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                 __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh) & 0x00FFFFFFu};
+            s_b[qslot][r] = v;
         }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // staged rows before the reads (own wave)
+    const int BIG = 0x7FFFFFFF;
+    int cost = BIG;
+    if (j >= 0 && hl < 25) {
+        const int kx = hl % 5, ky = hl / 5;
+        uint32_t s = 0;
+#pragma unroll
+        for (int dy = 0; dy < TS_RT_AROWS; ++dy) {
+            const uint4 ra = s_a[qslot][dy];
+            const uint4 rb = s_b[qslot][dy + ky];
+            // window bytes kx .. kx+10 of the 15-byte row
+            const uint32_t b0 = __builtin_amdgcn_alignbyte(rb.y, rb.x, kx & 3);
+            const uint32_t b1 = __builtin_amdgcn_alignbyte(rb.z, rb.y, kx & 3);
+            const uint32_t b2 = __builtin_amdgcn_alignbyte(rb.w, rb.z, kx & 3);
+            const uint32_t b3 = rb.w >> (8 * (kx & 3));
+            const bool hi = kx >= 4;   // kx == 4: shift by a whole dword
+            const uint32_t w0 = hi ? b1 : b0, w1 = hi ? b2 : b1, w2 = (hi ? b3 : b2) & 0x00FFFFFFu;
+            s = __builtin_amdgcn_sad_u8(ra.x, w0, s);
+            s = __builtin_amdgcn_sad_u8(ra.y, w1, s);
+            s = __builtin_amdgcn_sad_u8(ra.z, w2, s);
+        }
+        cost = (int)s;
+    }
+    // first minimum of (cost << 5 | offset) inside each half-wave: DPP row minima + readlanes
+    uint32_t key = (j >= 0 && hl < 25) ? (((uint32_t)cost << 5) | (uint32_t)hl) : 0xFFFFFFFFu;
+    key = min(key, (uint32_t)__builtin_amdgcn_mov_dpp((int)key, 0xB1, 0xF, 0xF, false));
+    key = min(key, (uint32_t)__builtin_amdgcn_mov_dpp((int)key, 0x4E, 0xF, 0xF, false));
+    key = min(key, (uint32_t)__builtin_amdgcn_mov_dpp((int)key, 0x141, 0xF, 0xF, false));
+    key = min(key, (uint32_t)__builtin_amdgcn_mov_dpp((int)key, 0x140, 0xF, 0xF, false));
+    const uint32_t k0 = min((uint32_t)__builtin_amdgcn_readlane((int)key, 0), (uint32_t)__builtin_amdgcn_readlane((int)key, 16));
+    const uint32_t k1 = min((uint32_t)__builtin_amdgcn_readlane((int)key, 32), (uint32_t)__builtin_amdgcn_readlane((int)key, 48));
+    const int a = (int)((half ? k1 : k0) & 31u);
+    const int hb = half * 32;
+    const int c0 = __shfl(cost, hb + a, 64);
+    const int cl = __shfl(cost, hb + max(a - 1, 0), 64), cr = __shfl(cost, hb + min(a + 1, 31), 64);
+    const int cu = __shfl(cost, hb + max(a - 5, 0), 64), cd = __shfl(cost, hb + min(a + 5, 31), 64);
+    if (j >= 0 && hl == 0) {
+        const int ky = a / 5, kx = a % 5;
+        double u = nanv, v = nanv;
+        if (kx > 0 && kx < 4 && ky > 0 && ky < 4) {
+            const double ddx = parabola(cl, c0, cr);
+            const double ddy = parabola(cu, c0, cd);
+            const double sc = (double)(1 << l);
+            u = (((double)(qx + (kx - TS_SAD_RANGE)) + ddx) + 0.5) * sc - 0.5;
+            v = (((double)(qy + (ky - TS_SAD_RANGE)) + ddy) + 0.5) * sc - 0.5;
+        }
+        out_uv[0] = u;
+        out_uv[1] = v;
     }
 }
 
@@ -303,6 +399,7 @@ void launch_match(const BatchCtx& c, hipStream_t s) {
 }
 
 void launch_match_refine(const BatchCtx& c, hipStream_t s) {
-    const int bpi = (c.g.K + 3) / 4;
-    hipLaunchKernelGGL(k_match_refine, dim3(xcd_grid(c.n * c.P * 2, bpi)), dim3(256), 0, s, c);
+    const int K = c.g.K;
+    hipLaunchKernelGGL(k_refine_stereo, dim3(xcd_grid(c.n * c.P, (K + 4 * TS_RS_Q - 1) / (4 * TS_RS_Q))), dim3(256), 0, s, c);
+    hipLaunchKernelGGL(k_refine_temporal, dim3(xcd_grid(c.n * c.P, (K + 7) / 8)), dim3(256), 0, s, c);
 }

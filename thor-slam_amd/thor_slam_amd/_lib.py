@@ -88,7 +88,13 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path is not None else LIB_PATH
+    if path is None and os.environ.get("TSLAM_LIBRARY"):
+        path = os.environ["TSLAM_LIBRARY"]  # e.g. an experiment build; still cached as the one library
+        p = Path(path)
+        lib_is_default = True
+    else:
+        p = Path(path) if path is not None else LIB_PATH
+        lib_is_default = path is None
     # torch ships its own libamdhip64.so.7 (same SONAME as /opt/rocm's).  Whichever loads first
     # is the one HIP runtime of the process; load torch's first so tensors and our kernels share
     # it (loading ours first leaves torch's HSA runtime unable to see the device).
@@ -106,7 +112,7 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if path is None:
+    if lib_is_default:
         _lib = lib
     return lib
 

@@ -1,0 +1,77 @@
+"""Time single kernels back to back on resident data (profiling aid, not the bench).
+
+    python tools/kernel_probe.py [--batch 256] [--kernels rectify_pyramid,detect,detect,detect]
+
+Runs one full batch first (so every buffer holds real data), then launches the listed kernels in
+order inside one batch and prints each launch's duration from HIP events on the launch stream.
+Also times a device-to-device copy of the batch's pyramid slice as a bandwidth reference.
+"""
+
+from __future__ import annotations
+
+import argparse
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+for p in (ROOT, ROOT / "thor-slam_amd"):
+    sys.path.insert(0, str(p))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--kernels", default="rectify_pyramid,detect,detect,detect,select,describe,describe")
+    args = ap.parse_args()
+    import torch
+
+    from bench import render_frames, triangle_indices
+    from thor_slam_amd._lib import Handle
+    from thor_slam_amd.calib import extract_cameras, stereo_pairs, stereo_rectify
+    from thor_slam_amd.camera.rig import CameraRig
+    from thor_slam_amd.params import HipSlamConfig
+    from thor_slam_amd.synthetic import SyntheticStereoSource
+
+    src = SyntheticStereoSource(seed=0)
+    cams = extract_cameras(CameraRig([src]).calibration, 2)
+    (li, ri), = stereo_pairs(cams)
+    rect = stereo_rectify(cams[li], cams[ri])
+    B = args.batch
+    frames = render_frames(0, 48, 8)[triangle_indices(2 * B, 48)]
+    dev = torch.from_numpy(frames).cuda()
+    h = Handle([rect], HipSlamConfig(), max_batch=B)
+    stream = torch.cuda.current_stream()
+    s = stream.cuda_stream
+    h.submit(dev[:B].data_ptr(), B, s)
+    h.submit(dev[B:].data_ptr(), B, s)
+    torch.cuda.synchronize()
+    h.begin_batch(dev[:B].data_ptr(), B)
+    for name in args.kernels.split(","):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        h.run_kernel(name, s)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        print(f"{name:16s} {1000 * e0.elapsed_time(e1):9.1f} us")
+    h.end_batch()
+    # bandwidth reference: copy the pyramid slice of B frames (read + write)
+    import ctypes
+
+    ptr, total, per = h.buffer_info("pyramid") if hasattr(h, "buffer_info") else (None, None, None)
+    if ptr is not None:
+        nbytes = per * B
+        a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        b = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        for _ in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            b.copy_(a)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            us = 1000 * e0.elapsed_time(e1)
+            print(f"copy {nbytes / 1e6:.0f} MB  {us:9.1f} us  {2 * nbytes / us / 1e3:.0f} GB/s")
+    h.close()
+
+
+if __name__ == "__main__":
+    main()
