@@ -96,9 +96,10 @@ enum tslam_buffer {
     TSLAM_BUF_QBEST = 12,    /* u32 [batch][pairs][2][K]         (dist<<16 | idx) stereo, temporal */
     TSLAM_BUF_QSECOND = 13,  /* u32 [batch][pairs][2][K]                                      */
     TSLAM_BUF_TBEST = 14,    /* u32 [batch][pairs][2][K]         train-side atomicMin         */
-    TSLAM_BUF_YPERM = 15,    /* u16 [ring][cams][K]              per level: kp indices sorted by (y, rank) */
+    TSLAM_BUF_YSORTED = 15,  /* u32 [ring][cams][K][4]           per level, by (y, rank): {x | y<<16, lvl | score<<16, kp index, valid} */
     TSLAM_BUF_ROWSTART = 16, /* u16 [ring][cams][sum(H_l+1)]     per level: first y-sorted position of row y */
-    TSLAM_BUF_COUNT = 17
+    TSLAM_BUF_DESC_YS = 17,  /* u32 [ring][cams][K][8]           descriptors in the y-sorted order */
+    TSLAM_BUF_COUNT = 18
 };
 
 enum tslam_stage {

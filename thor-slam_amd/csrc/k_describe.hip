@@ -1,178 +1,222 @@
 // k_describe.hip — row A5 of SURVEY.md §8a: intensity-centroid orientation + rotated BRIEF-256.
 //
-// One wave64 handles TS_DESC_KPW consecutive keypoints of the y-sorted walk of one image.  The
-// kernel is latency-bound (each keypoint needs an index chain, then pixels, then the table row
-// of its orientation bin), so a wave resolves all its keypoints' indices in one round trip,
-// issues the pixel loads of all of them before using any, computes every orientation, then
-// loads all table rows at once: 3 exposed memory latencies per wave instead of ~5 per keypoint.
-// Only coalesced dword loads touch global memory (byte gathers cost one address cycle per cache
-// line): the orientation disc is reduced straight from registers, and the 37x37 BRIEF patch is
-// staged in the wave's own LDS slice, where the 512 rotated samples are byte reads.  The 256
-// binary tests are four wave ballots (lane i of ballot k = test 64k + i); no atomics, no block
-// barriers.  Bit-exact with oracle.orientation_bins / oracle.brief.
+// Tile-staged: a block owns a 128 x 32 tile of one level.  It copies the tile plus halo of the
+// raw level (orientation) and of the smoothed level (BRIEF) into LDS with 16-byte LDS-DMA loads,
+// then serves every keypoint inside the tile from LDS, one wave per keypoint.  A wave-per-
+// keypoint design that fetched each 37x37 patch from L2 issued ~10 cache-line requests per
+// wave-load and ran L2-request-bound; staging reads every line of the tile once (the patches of
+// neighbouring keypoints overlap ~3-4x).
+//  * keypoints of the tile: the y-sorted records of the tile's rows (rowstart), 64 at a time,
+//    filtered by x with a ballot;
+//  * orientation: lane (row, word) holds the realigned word at dx = 4w - 15 .. 4w - 12 of disc
+//    row dy = row - 15; m10 = dot4(wx, I) - 15 dot4(mask, I), m01 = dy dot4(mask, I) with
+//    per-lane constant byte weights (3 ops per word); bin by 30 wedge tests in parallel lanes;
+//  * BRIEF: the rotated pattern is a table of byte offsets for the tile pitch (built by the host),
+//    2 ds_read_u8 + 1 compare per test, four wave ballots per descriptor.
+// Bit-exact with oracle.orientation_bins / oracle.brief.
 #include "tslam_common.h"
 
-#define TS_BRIEF_ROWS 37   // rotated pattern offsets lie in [-18, 18]
-#define TS_BRIEF_WORDS 10  // 40 bytes per staged row (37 columns at any alignment)
-#define TS_ORIENT_WORDS 9  // 36 bytes per disc row (31 columns at any alignment)
-#define TS_DESC_KPW 4      // keypoints per wave
+// shared with the host (tslam_api.cpp builds the BRIEF offset table for TS_DT_P)
+#include "tslam_describe.h"
 
-// Round down to a dword boundary by pointer arithmetic (an integer round trip would turn the
-// loads into flat loads, which the compiler then drains together with every scalar load).
-__device__ __forceinline__ const uint8_t* align4(const uint8_t* p) { return p - ((uintptr_t)p & 3u); }
+#define TS_DT_G 4   // keypoints per orientation / table-load group
 
-__global__ __launch_bounds__(256) void k_describe(BatchCtx c) {
-    __shared__ uint32_t s_patch[4][TS_BRIEF_ROWS * TS_BRIEF_WORDS];
+__device__ __forceinline__ int dt_count(int W, int H, int* nx) {
+    *nx = (W + TS_DT_W - 1) / TS_DT_W;
+    return *nx * ((H + TS_DT_H - 1) / TS_DT_H);
+}
+
+// 16-byte async global -> LDS copy; `wave_dst` is the wave-uniform LDS base, lane k lands at +16k
+__device__ __forceinline__ void glds16d(const void* src, void* wave_dst) {
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)wave_dst, 16, 0, 0);
+}
+
+// Copy rows [r0, r0 + nrows) x columns [c0, c0 + TS_DT_P) of a level (pitch W, H rows) into an
+// LDS image of pitch TS_DT_P.  Rows outside the level and words outside [0, W) are skipped (the
+// keypoint margin guarantees no keypoint reads them).
+__device__ __forceinline__ void stage_tile(const uint8_t* level, int W, int H, int r0, int c0, int nrows,
+                                           uint8_t* lds, bool wide16) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int img, local;
-    const int bpi = (c.g.K + 4 * TS_DESC_KPW - 1) / (4 * TS_DESC_KPW);
-    if (!xcd_image_block(blockIdx.x, c.n * c.C, bpi, &img, &local)) return;
-    const int pos0 = (local * 4 + wave) * TS_DESC_KPW;   // y-sorted walk (L1/L2 locality)
-    if (pos0 >= c.g.K) return;
-    const int cam = img % c.C;
-    const int f = img / c.C;
-    const int slot = ring_slot(c, c.g0 + f);
-    const size_t ib = (size_t)slot * c.C + cam;
-    uint32_t* kps = c.kps + ib * c.g.K * 2;
-    uint32_t* desc = c.desc + ib * c.g.K * 8;
-
-    // (1) index chain: lane k resolves position pos0 + k
-    int my_idx = 0, my_lev = 0, my_ok = 0;
-    uint32_t my_xy = 0, my_meta = 0;
-    if (lane < TS_DESC_KPW && pos0 + lane < c.g.K) {
-        bool v;
-        my_idx = ysorted_kp(c, c.yperm + ib * c.g.K, c.kcount + ib * c.g.n_levels, pos0 + lane, &my_lev, &v);
-        my_ok = v ? 1 : 2;   // 2 = padding slot (zero descriptor)
-        if (v) {
-            const uint2 e = *reinterpret_cast<const uint2*>(kps + (size_t)my_idx * 2);
-            my_xy = e.x;
-            my_meta = e.y;
-        }
-    }
-    int kidx[TS_DESC_KPW], kok[TS_DESC_KPW], kx[TS_DESC_KPW], ky[TS_DESC_KPW], kW[TS_DESC_KPW];
-    uint32_t kmeta[TS_DESC_KPW];
-    const uint8_t* lev[TS_DESC_KPW];
-    const uint8_t* q0[TS_DESC_KPW];
-#pragma unroll
-    for (int k = 0; k < TS_DESC_KPW; ++k) {
-        kidx[k] = __builtin_amdgcn_readlane(my_idx, k);
-        kok[k] = __builtin_amdgcn_readlane(my_ok, k);
-        const uint32_t xy = (uint32_t)__builtin_amdgcn_readlane((int)my_xy, k);
-        kmeta[k] = (uint32_t)__builtin_amdgcn_readlane((int)my_meta, k);
-        const int l = __builtin_amdgcn_readlane(my_lev, k);
-        kx[k] = xy & 0xFFFF;
-        ky[k] = xy >> 16;
-        kW[k] = c.g.W[l];
-        lev[k] = c.pyr + ib * c.g.pyr_bytes + c.g.pyr_off[l] + (size_t)(ky[k] - 15) * kW[k] + (kx[k] - 15);
-        q0[k] = c.smo + ((size_t)f * c.C + cam) * c.g.pyr_bytes + c.g.pyr_off[l] + (size_t)(ky[k] - 18) * kW[k] + (kx[k] - 18);
-    }
-
-    // (2) every pixel load of the wave's keypoints before any use: the 31-row disc as 9 aligned
-    // words per row (5 wave loads) and the 37-row patch as 10 words per row (6 wave loads)
-    uint32_t od[TS_DESC_KPW][5], pd[TS_DESC_KPW][6];
-#pragma unroll
-    for (int k = 0; k < TS_DESC_KPW; ++k) {
-        if (kok[k] != 1) continue;
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            const int s = lane + 64 * i;
-            const int r = s / TS_ORIENT_WORDS, w = s - TS_ORIENT_WORDS * r;
-            od[k][i] = s < 31 * TS_ORIENT_WORDS ? *(const uint32_t*)(align4(lev[k] + (size_t)r * kW[k]) + 4 * w) : 0u;
-        }
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            const int s = lane + 64 * i;
-            const int r = s / TS_BRIEF_WORDS, w = s - TS_BRIEF_WORDS * r;
-            pd[k][i] = s < TS_BRIEF_ROWS * TS_BRIEF_WORDS ? *(const uint32_t*)(align4(q0[k] + (size_t)r * kW[k]) + 4 * w) : 0u;
-        }
-    }
-
-    // (3) orientation moments over dx^2 + dy^2 <= 225 from registers; the integer sums are
-    // order-independent (DPP row sums + readlanes leave them in SGPRs).  Bin b: cross(u_b, v) >= 0
-    // and cross(u_{b+1}, v) < 0 with v = (m10, m01); lane b tests wedge b, the lowest hit wins
-    // (== the sequential first-match scan), no hit -> bin 0.
-    int bin[TS_DESC_KPW];
-    const int64_t wa0 = lane < 30 ? c.wedges[2 * lane] : 0, wa1 = lane < 30 ? c.wedges[2 * lane + 1] : 0;
-    const int64_t wb0 = lane < 30 ? c.wedges[2 * lane + 2] : 0, wb1 = lane < 30 ? c.wedges[2 * lane + 3] : 0;
-#pragma unroll
-    for (int k = 0; k < TS_DESC_KPW; ++k) {
-        bin[k] = 0;
-        if (kok[k] != 1) continue;
-        int m10 = 0, m01 = 0;
-        const uintptr_t base = (uintptr_t)lev[k];
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            const int s = lane + 64 * i;
-            if (s < 31 * TS_ORIENT_WORDS) {
-                const int r = s / TS_ORIENT_WORDS, w = s - TS_ORIENT_WORDS * r;
-                const uintptr_t rp = base + (uintptr_t)r * kW[k];
-                const int dx0 = (int)(((rp & ~(uintptr_t)3) + 4 * w) - rp) - 15, dy = r - 15;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int dx = dx0 + j, v = (od[k][i] >> (8 * j)) & 0xFF;
-                    if (dx * dx + dy * dy <= 225) {
-                        m10 += dx * v;
-                        m01 += dy * v;
-                    }
-                }
+    if (wide16) {
+        const int per_row = TS_DT_P / 16, n = nrows * per_row;
+        for (int i0 = wave * 64; i0 < n; i0 += 256) {
+            const int i = i0 + lane;
+            if (i < n) {
+                const int r = i / per_row, q = i - r * per_row;
+                const int y = r0 + r, x = c0 + 16 * q;
+                if (y >= 0 && y < H && x >= 0 && x + 16 <= W) glds16d(level + (size_t)y * W + x, lds + 16 * i0);
             }
         }
-        m10 = __builtin_amdgcn_readfirstlane(wave_sum_dpp(m10));
-        m01 = __builtin_amdgcn_readfirstlane(wave_sum_dpp(m01));
-        const bool hit = lane < 30 && (wa0 * (int64_t)m01 - wa1 * (int64_t)m10) >= 0 &&
-                         (wb0 * (int64_t)m01 - wb1 * (int64_t)m10) < 0;
-        const uint64_t m = __ballot(hit);
-        bin[k] = m ? (int)__builtin_ctzll(m) : 0;
+    } else {
+        for (int i = threadIdx.x; i < nrows * TS_DT_P; i += 256) {
+            const int r = i / TS_DT_P, q = i - r * TS_DT_P;
+            const int y = r0 + r, x = c0 + q;
+            if (y >= 0 && y < H && x >= 0 && x < W) lds[i] = level[(size_t)y * W + x];
+        }
     }
+}
 
-    // (4) the table rows of all bins at once, then BRIEF per keypoint out of the LDS patch
-    uint32_t tab[TS_DESC_KPW][4];
-#pragma unroll
-    for (int k = 0; k < TS_DESC_KPW; ++k)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) tab[k][j] = kok[k] == 1 ? c.brief_table[bin[k] * 256 + 64 * j + lane] : 0u;
-    uint8_t* patch = (uint8_t*)s_patch[wave];
-#pragma unroll
-    for (int k = 0; k < TS_DESC_KPW; ++k) {
-        if (kok[k] == 0) continue;
-        uint32_t* dst = desc + (size_t)kidx[k] * 8;
-        if (kok[k] == 2) {
-            if (lane < 8) dst[lane] = 0u;
-            continue;
+__global__ __launch_bounds__(256) void k_describe(BatchCtx c) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_raw[TS_DT_RAW_ROWS * TS_DT_P];
+    __shared__ __attribute__((aligned(16))) uint8_t s_smo[TS_DT_SMO_ROWS * TS_DT_P];
+    __shared__ uint16_t s_list[TS_DT_W * TS_DT_H / 4];   // NMS keeps at most one per 2x2
+    __shared__ uint32_t s_n;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // block -> (image, level, tile); all tiles of one image on one XCD
+    int tiles = 0;
+    for (int l = 0; l < c.g.n_levels; ++l) {
+        int nx;
+        tiles += dt_count(c.g.W[l], c.g.H[l], &nx);
+    }
+    int img, local;
+    if (!xcd_image_block(blockIdx.x, c.n * c.C, tiles, &img, &local)) return;
+    int l = 0, nx = 1;
+    for (;; ++l) {
+        const int t = dt_count(c.g.W[l], c.g.H[l], &nx);
+        if (local < t || l + 1 == c.g.n_levels) break;
+        local -= t;
+    }
+    const int ty = local / nx, tx = local - ty * nx;
+    const int W = c.g.W[l], H = c.g.H[l];
+    const int x0 = tx * TS_DT_W, y0 = ty * TS_DT_H;
+    const int cam = img % c.C, f = img / c.C;
+    const int slot = ring_slot(c, c.g0 + f);
+    const size_t ib = (size_t)slot * c.C + cam;
+    const uint8_t* raw = c.pyr + ib * c.g.pyr_bytes + c.g.pyr_off[l];
+    const uint8_t* smo = c.smo + ((size_t)f * c.C + cam) * c.g.pyr_bytes + c.g.pyr_off[l];
+    uint32_t* kps = c.kps + ib * c.g.K * 2;
+    uint32_t* desc = c.desc + ib * c.g.K * 8;
+    uint32_t* desc_ys = c.desc_ys + ib * c.g.K * 8;
+    const uint4* ys = c.ys + ib * c.g.K + c.g.koff[l];
+    const uint16_t* rs = c.rowstart + ib * c.g.rs_total + c.g.rs_off[l];
+    const int kn = c.kcount[ib * c.g.n_levels + l];
+
+    // padding slots of the level get zero descriptors (first tile of the level does it)
+    if (local == 0) {
+        const int Kl = c.g.Kq[l];
+        for (int i = kn * 8 + threadIdx.x; i < Kl * 8; i += 256) {
+            desc[(size_t)(c.g.koff[l] + i / 8) * 8 + (i & 7)] = 0u;
+            desc_ys[(size_t)(c.g.koff[l] + i / 8) * 8 + (i & 7)] = 0u;
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // previous keypoint's reads first
+    }
+    const int pa = rs[y0], pb = rs[min(y0 + TS_DT_H, H)];
+    if (pa >= pb) return;   // no keypoint in the tile's rows (block-uniform)
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+
+    const bool wide16 = ((W & 15) == 0) && ((c.g.pyr_off[l] & 15) == 0) && ((c.g.pyr_bytes & 15) == 0);
+    const int c0 = x0 - TS_DT_HX;
+    stage_tile(raw, W, H, y0 - 15, c0, TS_DT_RAW_ROWS, s_raw, wide16);
+    stage_tile(smo, W, H, y0 - 18, c0, TS_DT_SMO_ROWS, s_smo, wide16);
+
+    // per-lane disc weights (pixel dx = 4w - 15 + j, dy = r - 15 of slot s = lane + 64 i)
+    uint32_t wx[5], mk[5];
+    int dyl[5], rofs[5];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            const int s = lane + 64 * i;
-            if (s < TS_BRIEF_ROWS * TS_BRIEF_WORDS) s_patch[wave][s] = pd[k][i];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // patch writes before reads
-        const uintptr_t base = (uintptr_t)q0[k];
-        uint32_t words[8];
+    for (int i = 0; i < 5; ++i) {
+        const int s = lane + 64 * i;
+        const int r = s / 9, w = s - 9 * r;
+        uint32_t a = 0, m = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t t = tab[k][j];
-            const int px = (int8_t)(t & 0xFF), py = (int8_t)((t >> 8) & 0xFF);
-            const int qx = (int8_t)((t >> 16) & 0xFF), qy = (int8_t)(t >> 24);
-            const uintptr_t ra = base + (uintptr_t)(py + 18) * kW[k], rb = base + (uintptr_t)(qy + 18) * kW[k];
-            const int a = patch[(py + 18) * (4 * TS_BRIEF_WORDS) + (int)(ra & 3) + px + 18];
-            const int b = patch[(qy + 18) * (4 * TS_BRIEF_WORDS) + (int)(rb & 3) + qx + 18];
-            const uint64_t m = __ballot(a < b);
-            words[2 * j] = (uint32_t)m;
-            words[2 * j + 1] = (uint32_t)(m >> 32);
+            const int dx = 4 * w - 15 + j, dy = r - 15;
+            if (r < 31 && dx <= 15 && dx * dx + dy * dy <= 225) {
+                a |= (uint32_t)(dx + 15) << (8 * j);
+                m |= 1u << (8 * j);
+            }
         }
-        if (lane < 8) {
-            uint32_t w = words[0];
+        wx[i] = a;
+        mk[i] = m;
+        dyl[i] = r - 15;
+        rofs[i] = min(r, 30) * TS_DT_P + 4 * w;   // LDS byte offset of the word (before the kp origin)
+    }
+    // wedge directions as doubles: |u| < 2^25 and |m| < 2^23, so every product and difference
+    // below is an exact integer in f64 (< 2^53) and the sign tests equal the int64 ones
+    const double wa0 = lane < 30 ? (double)c.wedges[2 * lane] : 0.0, wa1 = lane < 30 ? (double)c.wedges[2 * lane + 1] : 0.0;
+    const double wb0 = lane < 30 ? (double)c.wedges[2 * lane + 2] : 0.0, wb1 = lane < 30 ? (double)c.wedges[2 * lane + 3] : 0.0;
+
+    // keypoints of the tile: the records of its rows filtered by x, compacted into an LDS list
+    // so the 4 waves get equal shares (order is irrelevant: every keypoint is independent)
+    for (int p = pa + threadIdx.x; p < pb; p += 256) {
+        const int x = ys[p].x & 0xFFFF;
+        if (x >= x0 && x < x0 + TS_DT_W) s_list[atomicAdd(&s_n, 1u)] = (uint16_t)p;
+    }
+    __syncthreads();   // tiles landed (drains the LDS-DMA) and the list is complete
+    const int n = (int)s_n;
+    // groups of TS_DT_G keypoints per wave: all orientations, then all table rows (one exposed
+    // latency per group), then the descriptors
+    for (int g0 = wave * TS_DT_G; g0 < n; g0 += 4 * TS_DT_G) {
+        int bin[TS_DT_G], pos[TS_DT_G];
+        uint4 rec[TS_DT_G];
 #pragma unroll
-            for (int j = 1; j < 8; ++j)
-                if (lane == j) w = words[j];
-            dst[lane] = w;
+        for (int g = 0; g < TS_DT_G; ++g) {
+            pos[g] = g0 + g < n ? (int)s_list[g0 + g] : -1;
+            rec[g] = pos[g] >= 0 ? ys[pos[g]] : uint4{0u, 0u, 0u, 0u};
         }
-        if (lane == 0) kps[(size_t)kidx[k] * 2 + 1] = (kmeta[k] & ~0xFF00u) | ((uint32_t)bin[k] << 8);
+#pragma unroll
+        for (int g = 0; g < TS_DT_G; ++g) {
+            bin[g] = 0;
+            if (pos[g] < 0) continue;
+            const int x = rec[g].x & 0xFFFF, y = rec[g].x >> 16;
+            // orientation: disc origin (x - 15, y - 15) in the raw tile
+            const int ob = (y - y0) * TS_DT_P + (x - 15 - c0);
+            const uint32_t sh = (uint32_t)ob & 3u;
+            const uint8_t* obase = s_raw + (ob & ~3);
+            int sx = 0, s1 = 0, sy = 0;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                const uint32_t* wp = reinterpret_cast<const uint32_t*>(obase + rofs[i]);
+                const uint32_t v = __builtin_amdgcn_alignbyte(wp[1], wp[0], sh);
+                const int mm = (int)__builtin_amdgcn_udot4(mk[i], v, 0u, false);
+                sx = (int)__builtin_amdgcn_udot4(wx[i], v, (uint32_t)sx, false);
+                s1 += mm;
+                sy += dyl[i] * mm;
+            }
+            const int m10 = __builtin_amdgcn_readfirstlane(wave_sum_dpp(sx - 15 * s1));
+            const int m01 = __builtin_amdgcn_readfirstlane(wave_sum_dpp(sy));
+            const double d01 = (double)m01, d10 = (double)m10;
+            const bool hit = lane < 30 && (wa0 * d01 - wa1 * d10) >= 0.0 && (wb0 * d01 - wb1 * d10) < 0.0;
+            const uint64_t hm = __ballot(hit);
+            bin[g] = hm ? (int)__builtin_ctzll(hm) : 0;
+        }
+        uint32_t t[TS_DT_G][4];
+#pragma unroll
+        for (int g = 0; g < TS_DT_G; ++g)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) t[g][j] = pos[g] >= 0 ? c.brief_table[bin[g] * 256 + 64 * j + lane] : 0u;
+#pragma unroll
+        for (int g = 0; g < TS_DT_G; ++g) {
+            if (pos[g] < 0) continue;
+            const int x = rec[g].x & 0xFFFF, y = rec[g].x >> 16;
+            // BRIEF: patch origin (x - 18, y - 18) in the smoothed tile
+            const uint8_t* pbase = s_smo + (y - y0) * TS_DT_P + (x - 18 - c0);
+            uint32_t words[8];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int a = pbase[t[g][j] & 0xFFFFu];
+                const int b = pbase[t[g][j] >> 16];
+                const uint64_t bm = __ballot(a < b);
+                words[2 * j] = (uint32_t)bm;
+                words[2 * j + 1] = (uint32_t)(bm >> 32);
+            }
+            const int kidx = (int)rec[g].z;
+            if (lane < 8) {
+                uint32_t w = words[0];
+#pragma unroll
+                for (int j = 1; j < 8; ++j)
+                    if (lane == j) w = words[j];
+                desc[(size_t)kidx * 8 + lane] = w;
+                desc_ys[(size_t)(c.g.koff[l] + pos[g]) * 8 + lane] = w;
+            }
+            if (lane == 0) kps[(size_t)kidx * 2 + 1] = (rec[g].y & ~0xFF00u) | ((uint32_t)bin[g] << 8);
+        }
     }
 }
 
 void launch_describe(const BatchCtx& c, hipStream_t s) {
-    const int bpi = (c.g.K + 4 * TS_DESC_KPW - 1) / (4 * TS_DESC_KPW);
-    hipLaunchKernelGGL(k_describe, dim3(xcd_grid(c.n * c.C, bpi)), dim3(256), 0, s, c);
+    int tiles = 0;
+    for (int l = 0; l < c.g.n_levels; ++l)
+        tiles += ((c.g.W[l] + TS_DT_W - 1) / TS_DT_W) * ((c.g.H[l] + TS_DT_H - 1) / TS_DT_H);
+    hipLaunchKernelGGL(k_describe, dim3(xcd_grid(c.n * c.C, tiles)), dim3(256), 0, s, c);
 }

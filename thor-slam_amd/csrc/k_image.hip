@@ -472,12 +472,62 @@ __device__ void block_find_crossing(const uint32_t* h, int nbins, uint32_t need,
     __syncthreads();
 }
 
+#define TS_SEL_BUCKET_MAX 256   // larger score buckets -> bitonic fallback (O(n^2) ranking)
+
+// In-place exclusive scan of a[0..n) (n <= 8 * SEL_THREADS) by the whole block; ends synchronised.
+__device__ void block_exclusive_scan(uint32_t* a, int n, uint32_t* s_part) {
+    const int per = (n + SEL_THREADS - 1) / SEL_THREADS;
+    const int b0 = threadIdx.x * per;
+    uint32_t local = 0;
+    for (int b = b0; b < min(b0 + per, n); ++b) local += a[b];
+    s_part[threadIdx.x] = local;
+    __syncthreads();
+    for (int o = 1; o < SEL_THREADS; o <<= 1) {
+        const uint32_t v = threadIdx.x >= (unsigned)o ? s_part[threadIdx.x - o] : 0u;
+        __syncthreads();
+        s_part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = s_part[threadIdx.x] - local;
+    for (int b = b0; b < min(b0 + per, n); ++b) {
+        const uint32_t v = a[b];
+        a[b] = run;
+        run += v;
+    }
+    __syncthreads();
+}
+
+// Ascending bitonic sort of a[0..n) in place (pads to a power of two with 0xFFFFFFFF; n <= SEL_MAX).
+__device__ void bitonic_sort(uint32_t* a, int n) {
+    int np2 = 1;
+    while (np2 < n) np2 <<= 1;
+    for (int i = n + threadIdx.x; i < np2; i += SEL_THREADS) a[i] = 0xFFFFFFFFu;
+    __syncthreads();
+    for (int k = 2; k <= np2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < np2; i += SEL_THREADS) {
+                const int p = i ^ j;
+                if (p > i) {
+                    const uint32_t x = a[i], y = a[p];
+                    const bool up = (i & k) == 0;
+                    if ((x > y) == up) {
+                        a[i] = y;
+                        a[p] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
 __global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
     __shared__ uint32_t s_keys[SEL_MAX];
     __shared__ uint32_t s_h[2048];
     __shared__ uint32_t s_part[SEL_THREADS];
+    __shared__ uint32_t s_pref[SEL_THREADS + 1];
     __shared__ int s_bin;
-    __shared__ uint32_t s_before, s_nsel;
+    __shared__ uint32_t s_before, s_nsel, s_flag;
     const int l = blockIdx.x;
     const int img = blockIdx.y;
     const int cam = img % c.C;
@@ -489,8 +539,42 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
     const int nb = c.g.nbands[l];
     const int cap = c.g.cand_cap[l];
 
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_h[i] = gh[i];
+    // band counts -> exclusive prefix (flat candidate index i lives in band b with
+    // s_pref[b] <= i < s_pref[b+1]); every pass below is then one flat, independent-load sweep
+    // over the level's candidates (a per-band loop serialised ~25 dependent global round trips)
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        s_h[i] = gh[i];
+        s_part[i] = i < nb ? cnt[i] : 0u;
+    }
     __syncthreads();
+    for (int o = 1; o < SEL_THREADS; o <<= 1) {
+        const uint32_t v = threadIdx.x >= (unsigned)o ? s_part[threadIdx.x - o] : 0u;
+        __syncthreads();
+        s_part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    if (threadIdx.x <= (unsigned)nb) s_pref[threadIdx.x] = threadIdx.x == 0 ? 0u : s_part[threadIdx.x - 1];
+    __syncthreads();
+    const int ncand = (int)s_pref[nb];
+    auto fetch = [&](int i) -> uint32_t {
+        int lo = 0, hi = nb;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if ((int)s_pref[mid] <= i) lo = mid; else hi = mid;
+        }
+        return cand[(size_t)lo * cap + (i - (int)s_pref[lo])];
+    };
+    // sweep(fn): fn(key) for every candidate, 4 independent loads in flight per thread
+    auto sweep = [&](auto&& fn) {
+        for (int i0 = threadIdx.x; i0 < ncand; i0 += 4 * SEL_THREADS) {
+            uint32_t k[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) k[u] = i0 + u * SEL_THREADS < ncand ? fetch(i0 + u * SEL_THREADS) : 0u;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i0 + u * SEL_THREADS < ncand) fn(k[u]);
+        }
+    };
     uint32_t total = 0;
     for (int i = 0; i < 256; ++i) total += s_h[i];   // uniform per thread (LDS broadcast)
 
@@ -506,14 +590,9 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
             __syncthreads();
             for (int i = threadIdx.x; i < 2048; i += blockDim.x) s_h[i] = 0;
             __syncthreads();
-            for (int b = 0; b < nb; ++b) {
-                const uint32_t n = cnt[b];
-                const uint32_t* seg = cand + (size_t)b * cap;
-                for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-                    const uint32_t k = seg[i];
-                    if ((k >> 22) == sbin) atomicAdd(&s_h[(k >> 11) & 2047u], 1u);
-                }
-            }
+            sweep([&](uint32_t k) {
+                if ((k >> 22) == sbin) atomicAdd(&s_h[(k >> 11) & 2047u], 1u);
+            });
             __syncthreads();
             block_find_crossing(s_h, 2048, need, s_part, &s_bin, &s_before);
             const uint32_t ystar = (uint32_t)s_bin;
@@ -524,14 +603,9 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
                 __syncthreads();
                 for (int i = threadIdx.x; i < 2048; i += blockDim.x) s_h[i] = 0;
                 __syncthreads();
-                for (int b = 0; b < nb; ++b) {
-                    const uint32_t n = cnt[b];
-                    const uint32_t* seg = cand + (size_t)b * cap;
-                    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-                        const uint32_t k = seg[i];
-                        if ((k >> 11) == ((sbin << 11) | ystar)) atomicAdd(&s_h[k & 2047u], 1u);
-                    }
-                }
+                sweep([&](uint32_t k) {
+                    if ((k >> 11) == ((sbin << 11) | ystar)) atomicAdd(&s_h[k & 2047u], 1u);
+                });
                 __syncthreads();
                 block_find_crossing(s_h, 2048, need2, s_part, &s_bin, &s_before);
                 thresh = (sbin << 22) | (ystar << 11) | (uint32_t)s_bin;
@@ -541,43 +615,52 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
     // collect survivors
     if (threadIdx.x == 0) s_nsel = 0;
     __syncthreads();
-    for (int b = 0; b < nb; ++b) {
-        const uint32_t n = cnt[b];
-        const uint32_t* seg = cand + (size_t)b * cap;
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-            const uint32_t k = seg[i];
-            if (k <= thresh) {
-                const uint32_t slot = atomicAdd(&s_nsel, 1u);
-                if (slot < SEL_MAX) s_keys[slot] = k;
-            }
+    sweep([&](uint32_t k) {
+        if (k <= thresh) {
+            const uint32_t slot = atomicAdd(&s_nsel, 1u);
+            if (slot < SEL_MAX) s_keys[slot] = k;
         }
-    }
+    });
     __syncthreads();
     const int nsel = min((int)s_nsel, Kl);
-    int np2 = 1;
-    while (np2 < nsel) np2 <<= 1;
-    for (int i = nsel + threadIdx.x; i < np2; i += blockDim.x) s_keys[i] = 0xFFFFFFFFu;
-    __syncthreads();
-    // bitonic sort ascending
-    for (int k = 2; k <= np2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < np2; i += blockDim.x) {
-                const int p = i ^ j;
-                if (p > i) {
-                    const uint32_t a = s_keys[i], b = s_keys[p];
-                    const bool up = (i & k) == 0;
-                    if ((a > b) == up) {
-                        s_keys[i] = b;
-                        s_keys[p] = a;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    }
     const int slot = ring_slot(c, c.g0 + f);
     uint32_t* kp = c.kps + (((size_t)slot * c.C + cam) * c.g.K + c.g.koff[l]) * 2;
-    for (int i = threadIdx.x; i < Kl; i += blockDim.x) {
+    const int Hl = c.g.H[l];
+    // Counting sorts (few barriers) when the level fits a quarter of s_keys and no score
+    // bucket is huge; a bitonic network otherwise (66 barrier stages at 2048 keys).  Keys are
+    // unique, so "rank = bucket offset + #smaller keys in the bucket" is the sorted position.
+    uint32_t* s_tmp = s_keys + SEL_MAX / 2;
+    if (threadIdx.x == 0) s_flag = 0;
+    for (int i = threadIdx.x; i < 512; i += SEL_THREADS) s_h[i] = 0;
+    __syncthreads();
+    const bool counting = nsel <= SEL_MAX / 4;   // s_tmp = [4096, 6144), row fill = [6144, 8192)
+    if (counting) {
+        for (int i = threadIdx.x; i < nsel; i += SEL_THREADS) atomicAdd(&s_h[s_keys[i] >> 22], 1u);
+        __syncthreads();
+        const uint32_t cnt_b = s_h[threadIdx.x];   // one score bucket per thread
+        if (cnt_b > TS_SEL_BUCKET_MAX) s_flag = 1;
+        block_exclusive_scan(s_h, 256, s_part);      // s_h[b] = bucket offset
+    }
+    __syncthreads();
+    if (counting && s_flag == 0) {
+        uint32_t* fill = s_h + 256;
+        for (int i = threadIdx.x; i < nsel; i += SEL_THREADS) {
+            const uint32_t k = s_keys[i], b = k >> 22;
+            s_tmp[s_h[b] + atomicAdd(&fill[b], 1u)] = k;
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < nsel; i += SEL_THREADS) {
+            const uint32_t k = s_tmp[i], b = k >> 22;
+            const int lo = (int)s_h[b], n = (int)fill[b];
+            int r = 0;
+            for (int j = lo; j < lo + n; ++j) r += s_tmp[j] < k;
+            s_keys[lo + r] = k;
+        }
+        __syncthreads();
+    } else {
+        bitonic_sort(s_keys, nsel);
+    }
+    for (int i = threadIdx.x; i < Kl; i += SEL_THREADS) {
         uint32_t xy = 0, meta = (uint32_t)l;   // padding entries keep their level
         if (i < nsel) {
             const uint32_t k = s_keys[i];
@@ -589,39 +672,62 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
     }
     if (threadIdx.x == 0) c.kcount[((size_t)slot * c.C + cam) * c.g.n_levels + l] = nsel;
 
-    // y-sorted order of this level (key y<<13 | rank) + row-start table, for band-limited matching
-    for (int i = threadIdx.x; i < nsel; i += blockDim.x) s_keys[i] = (((s_keys[i] >> 11) & 2047u) << 13) | (uint32_t)i;
-    for (int i = nsel + threadIdx.x; i < np2; i += blockDim.x) s_keys[i] = 0xFFFFFFFFu;
-    __syncthreads();
-    for (int k = 2; k <= np2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < np2; i += blockDim.x) {
-                const int p = i ^ j;
-                if (p > i) {
-                    const uint32_t a = s_keys[i], b = s_keys[p];
-                    const bool up = (i & k) == 0;
-                    if ((a > b) == up) {
-                        s_keys[i] = b;
-                        s_keys[p] = a;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    }
-    uint16_t* yp = c.yperm + ((size_t)slot * c.C + cam) * c.g.K + c.g.koff[l];
-    for (int i = threadIdx.x; i < Kl; i += blockDim.x)
-        yp[i] = (uint16_t)(i < nsel ? c.g.koff[l] + (int)(s_keys[i] & 8191u) : 0);
+    // y-sorted order of this level (by y, then rank) + row-start table, for band-limited matching
+    uint4* ys = c.ys + ((size_t)slot * c.C + cam) * c.g.K + c.g.koff[l];
     uint16_t* rs = c.rowstart + ((size_t)slot * c.C + cam) * c.g.rs_total + c.g.rs_off[l];
-    const int Hl = c.g.H[l];
-    for (int y = threadIdx.x; y <= Hl; y += blockDim.x) {
-        const uint32_t target = (uint32_t)y << 13;
-        int lo = 0, hi = nsel;  // first position with key >= target
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (s_keys[mid] < target) lo = mid + 1; else hi = mid;
+    auto record = [&](int rank) -> uint4 {
+        const uint32_t k = s_keys[rank];
+        return {(k & 2047u) | (((k >> 11) & 2047u) << 16), (uint32_t)l | ((255u - (k >> 22)) << 16),
+                (uint32_t)(c.g.koff[l] + rank), 1u};
+    };
+    for (int i = nsel + threadIdx.x; i < Kl; i += SEL_THREADS) ys[i] = {0u, (uint32_t)l, (uint32_t)(c.g.koff[l] + i), 0u};
+    if (counting) {
+        // rows: counts -> exclusive offsets (= rowstart), bucket ranks by row, order by rank
+        uint32_t* fill = s_keys + SEL_MAX / 2 + SEL_MAX / 4;   // [2048] row fill counters
+        __syncthreads();
+        for (int i = threadIdx.x; i < 2048; i += SEL_THREADS) {
+            s_h[i] = 0;
+            fill[i] = 0;
         }
-        rs[y] = (uint16_t)lo;
+        __syncthreads();
+        for (int i = threadIdx.x; i < nsel; i += SEL_THREADS) atomicAdd(&s_h[(s_keys[i] >> 11) & 2047u], 1u);
+        __syncthreads();
+        block_exclusive_scan(s_h, 2048, s_part);
+        for (int y = threadIdx.x; y <= Hl; y += SEL_THREADS) rs[y] = (uint16_t)s_h[y];
+        for (int i = threadIdx.x; i < nsel; i += SEL_THREADS) {
+            const uint32_t y = (s_keys[i] >> 11) & 2047u;
+            s_tmp[s_h[y] + atomicAdd(&fill[y], 1u)] = (uint32_t)i;
+        }
+        __syncthreads();
+        for (int p = threadIdx.x; p < nsel; p += SEL_THREADS) {
+            const uint32_t i = s_tmp[p], y = (s_keys[i] >> 11) & 2047u;
+            const int lo = (int)s_h[y], n = (int)fill[y];
+            int r = 0;
+            for (int j = lo; j < lo + n; ++j) r += s_tmp[j] < i;
+            ys[lo + r] = record((int)i);
+        }
+    } else {
+        // bitonic on (y << 13 | rank) in the scratch half is not possible here (nsel > half):
+        // sort in place after the records are taken
+        __syncthreads();
+        uint32_t* yk = s_keys;   // reuse: keys are re-derived from kp[] below
+        for (int i = threadIdx.x; i < nsel; i += SEL_THREADS) yk[i] = (((yk[i] >> 11) & 2047u) << 13) | (uint32_t)i;
+        __syncthreads();
+        bitonic_sort(yk, nsel);
+        for (int i = threadIdx.x; i < nsel; i += SEL_THREADS) {
+            const int rank = (int)(yk[i] & 8191u);
+            const uint2 e = *reinterpret_cast<const uint2*>(kp + 2 * rank);
+            ys[i] = {e.x, e.y, (uint32_t)(c.g.koff[l] + rank), 1u};
+        }
+        for (int y = threadIdx.x; y <= Hl; y += SEL_THREADS) {
+            const uint32_t target = (uint32_t)y << 13;
+            int lo = 0, hi = nsel;  // first position with key >= target
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (yk[mid] < target) lo = mid + 1; else hi = mid;
+            }
+            rs[y] = (uint16_t)lo;
+        }
     }
 }
 

@@ -4,19 +4,25 @@
 // Bit-exact with oracle.match / oracle.stereo_subpixel / oracle.temporal_subpixel.
 //
 // k_match: one thread per query, 256 queries per block; the train descriptors of the same level
-// are staged in LDS in chunks of 1024 (32 KiB) and read as LDS broadcasts, so each pair costs
+// are staged in LDS in chunks of 512 (16 KiB) and read as LDS broadcasts, so each pair costs
 // 8 v_xor + 8 v_bcnt (popcount with accumulate) and a compare.  The train side's best query
-// (for the mutual check) is a wave min-reduction of (dist<<16 | query) per train descriptor,
+// (for the mutual check) comes from a per-wave distance tile read transposed (lane = train),
 // an LDS atomicMin per wave, and one global atomicMin per train descriptor per block: min is
 // order-independent, so the result is deterministic.
 #include "tslam_common.h"
+
+// Distances enter the mutual check as bytes: the train side's best query only matters when its
+// distance is <= the query's best <= max_hamming <= 253 (validated), so min(d, 254) keeps every
+// decision exact; 255 marks "not eligible".  Rows padded to 68 B for conflict-free transposed
+// reads.  Total LDS 40 KiB -> 4 blocks per CU.
+#define TS_TILE_PITCH 68
 
 __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     __shared__ uint4 s_desc[TS_MATCH_CHUNK * 2];
     __shared__ uint32_t s_xy[TS_MATCH_CHUNK];
     __shared__ uint32_t s_idx[TS_MATCH_CHUNK];
     __shared__ uint32_t s_tmin[TS_MATCH_CHUNK];
-    __shared__ uint16_t s_tile[4][64][64];   // per wave: distance[train jj][query lane]
+    __shared__ uint8_t s_tile[4][64][TS_TILE_PITCH];   // per wave: min(distance, 254)[train jj][query lane]
     __shared__ uint32_t s_qi[4][64];
     const int z = blockIdx.y;                 // (f * P + p) * 2 + mode
     const int mode = z & 1;
@@ -41,32 +47,33 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     const size_t qbase = ((size_t)slot * c.C + qcam) * K;
     const size_t tbase = ((size_t)tslot * c.C + tcam) * K;
     const size_t mbase = (((size_t)f * c.P + p) * 2 + mode) * K;
-    const uint16_t* qperm = c.yperm + qbase + c.g.koff[l];
-    const uint16_t* tperm = c.yperm + tbase + c.g.koff[l];
+    const uint4* qys = c.ys + qbase + c.g.koff[l];           // y-sorted records of the level
+    const uint4* tys = c.ys + tbase + c.g.koff[l];
+    const uint4* qdesc = reinterpret_cast<const uint4*>(c.desc_ys + (qbase + c.g.koff[l]) * 8);
+    const uint4* tdesc = reinterpret_cast<const uint4*>(c.desc_ys + (tbase + c.g.koff[l]) * 8);
     const uint16_t* trs = c.rowstart + ((size_t)tslot * c.C + tcam) * c.g.rs_total + c.g.rs_off[l];
     const int Hl = c.g.H[l];
 
     // queries in y-sorted order: this block holds positions q0 .. q0+255 of the level
     const int qpos = q0 + threadIdx.x;
     const bool active = qpos < qn;
-    const int qi = active ? (int)qperm[qpos] : 0;
     uint32_t q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    int qx = 0, qy = 0;
+    int qx = 0, qy = 0, qi = 0;
     if (active) {
-        const uint4* d = reinterpret_cast<const uint4*>(c.desc + (qbase + qi) * 8);
-        const uint4 a = d[0], b = d[1];
+        const uint4 rec = qys[qpos];
+        const uint4 a = qdesc[2 * qpos], b = qdesc[2 * qpos + 1];
         q[0] = a.x; q[1] = a.y; q[2] = a.z; q[3] = a.w; q[4] = b.x; q[5] = b.y; q[6] = b.z; q[7] = b.w;
-        const uint32_t xy = c.kps[(qbase + qi) * 2];
-        qx = xy & 0xFFFF;
-        qy = xy >> 16;
+        qi = (int)rec.z;
+        qx = rec.x & 0xFFFF;
+        qy = rec.x >> 16;
     }
     s_qi[wave][lane] = (uint32_t)qi;
     const int row_tol = c.mp.row_tol, dmax = c.mp.max_disp >> l, win = c.mp.window >> l;
     const int reach = mode == 0 ? row_tol : win;
     // rows any query of the block / of this wave can match (queries are y-sorted)
     const int qlast = min(qn, q0 + 256) - 1;
-    const int by0 = c.kps[(qbase + qperm[q0]) * 2] >> 16;
-    const int by1 = c.kps[(qbase + qperm[qlast]) * 2] >> 16;
+    const int by0 = qys[q0].x >> 16;
+    const int by1 = qys[qlast].x >> 16;
     const int t0 = trs[max(0, by0 - reach)];
     const int t1 = trs[min(Hl - 1, by1 + reach) + 1];
     int wy0, wy1;
@@ -88,13 +95,13 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     for (int j0 = t0; j0 < t1; j0 += TS_MATCH_CHUNK) {
         const int jn = min(TS_MATCH_CHUNK, t1 - j0);
         __syncthreads();
+        // contiguous y-sorted train records and descriptors (no index indirection)
         for (int i = threadIdx.x; i < jn; i += blockDim.x) {
-            const uint32_t tj = tperm[j0 + i];
-            const uint4* d = reinterpret_cast<const uint4*>(c.desc + (tbase + tj) * 8);
-            s_desc[2 * i] = d[0];
-            s_desc[2 * i + 1] = d[1];
-            s_xy[i] = c.kps[(tbase + tj) * 2];
-            s_idx[i] = tj;
+            const uint4 rec = tys[j0 + i];
+            s_desc[2 * i] = tdesc[2 * (j0 + i)];
+            s_desc[2 * i + 1] = tdesc[2 * (j0 + i) + 1];
+            s_xy[i] = rec.x;
+            s_idx[i] = rec.z;
             s_tmin[i] = 0xFFFFFFFFu;
         }
         __syncthreads();
@@ -124,21 +131,27 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
                     second_d = better ? best_d : (sec ? dd : second_d);
                     best_d = better ? dd : best_d;
                     best_j = better ? tj : best_j;
-                    s_tile[wave][jj][lane] = (uint16_t)(elig ? dd : 0xFFFF);
+                    s_tile[wave][jj][lane] = (uint8_t)(elig ? min(dd, 254) : 255);
                 }
                 if (jj0 + 8 >= jcount) break;
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
             // phase 2: transposed read, lane = train descriptor: (distance, query) minimum over
-            // the wave's 64 queries, no cross-lane reduction
+            // the wave's 64 queries, 4 queries per dword read (row pitch 68 B = 17 dwords, an
+            // odd stride, so the 64 lanes hit 64 different banks), no cross-lane reduction
             if (lane < jcount) {
                 uint32_t best = 0xFFFFFFFFu;
-#pragma unroll 16
-                for (int r = 0; r < 64; ++r) {
-                    const uint32_t d = s_tile[wave][lane][r];
-                    const uint32_t key = (d << 16) | s_qi[wave][r];
-                    best = (d != 0xFFFFu && key < best) ? key : best;
+                const uint32_t* row = reinterpret_cast<const uint32_t*>(&s_tile[wave][lane][0]);
+#pragma unroll 4
+                for (int r4 = 0; r4 < 16; ++r4) {
+                    const uint32_t d4 = row[r4];
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const uint32_t d = (d4 >> (8 * b)) & 0xFFu;
+                        const uint32_t key = (d << 16) | s_qi[wave][4 * r4 + b];
+                        best = (d != 0xFFu && key < best) ? key : best;
+                    }
                 }
                 if (best != 0xFFFFFFFFu) atomicMin(&s_tmin[jt + lane], best);
             }
@@ -219,10 +232,13 @@ __global__ __launch_bounds__(256) void k_refine_stereo(BatchCtx c) {
     const int qcam = 2 * p;
     const size_t qkb = ((size_t)slot * c.C + qcam) * K;
     int l = 0, qi = 0, j = -1;
+    uint32_t qxy = 0;
     if (live) {
-        bool kvalid;
-        qi = ysorted_kp(c, c.yperm + qkb, c.kcount + ((size_t)slot * c.C + qcam) * c.g.n_levels, pos, &l, &kvalid);
-        if (kvalid) j = match_valid(c, mbase, qi);
+        const uint4 rec = c.ys[qkb + pos];
+        qi = (int)rec.z;
+        l = (int)(rec.y & 0xFFu);
+        qxy = rec.x;
+        if (rec.w) j = match_valid(c, mbase, qi);
     }
     const double nanv = __builtin_nan("");
     if (live && k == 0 && j < 0) {
@@ -233,7 +249,6 @@ __global__ __launch_bounds__(256) void k_refine_stereo(BatchCtx c) {
     int cost = BIG, qx = 0, xr = 0;
     if (j >= 0) {
         const int W = c.g.W[l];
-        const uint32_t qxy = c.kps[(qkb + qi) * 2];
         qx = qxy & 0xFFFF;
         const int qy = qxy >> 16;
         xr = c.kps[(((size_t)slot * c.C + qcam + 1) * K + j) * 2] & 0xFFFF;
@@ -297,10 +312,13 @@ __global__ __launch_bounds__(256) void k_refine_temporal(BatchCtx c) {
     const int qcam = 2 * p;
     const size_t qkb = ((size_t)slot * c.C + qcam) * K;
     int l = 0, qi = 0, j = -1;
+    uint32_t qxy = 0;
     if (live) {
-        bool kvalid;
-        qi = ysorted_kp(c, c.yperm + qkb, c.kcount + ((size_t)slot * c.C + qcam) * c.g.n_levels, pos, &l, &kvalid);
-        if (kvalid && g > 0) j = match_valid(c, mbase, qi);
+        const uint4 rec = c.ys[qkb + pos];
+        qi = (int)rec.z;
+        l = (int)(rec.y & 0xFFu);
+        qxy = rec.x;
+        if (rec.w && g > 0) j = match_valid(c, mbase, qi);
     }
     int32_t* out_idx = c.temporal + ((size_t)f * c.P + p) * K;
     double* out_uv = c.tuv + (((size_t)f * c.P + p) * K + qi) * 2;
@@ -313,7 +331,6 @@ __global__ __launch_bounds__(256) void k_refine_temporal(BatchCtx c) {
     int qx = 0, qy = 0, W = 0;
     if (j >= 0) {
         W = c.g.W[l];
-        const uint32_t qxy = c.kps[(qkb + qi) * 2];
         qx = qxy & 0xFFFF;
         qy = qxy >> 16;
         const int pslot = ring_slot(c, g - 1);

@@ -13,6 +13,7 @@
 
 #include "../../include/tslam.h"
 #include "tslam_common.h"
+#include "tslam_describe.h"
 #include "tslam_tables.h"
 
 namespace {
@@ -145,7 +146,8 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.kps = (uint32_t*)h->buf[TSLAM_BUF_KEYPOINTS].ptr;
     c.kcount = (int32_t*)h->buf[TSLAM_BUF_KCOUNT].ptr;
     c.desc = (uint32_t*)h->buf[TSLAM_BUF_DESC].ptr;
-    c.yperm = (uint16_t*)h->buf[TSLAM_BUF_YPERM].ptr;
+    c.ys = (uint4*)h->buf[TSLAM_BUF_YSORTED].ptr;
+    c.desc_ys = (uint32_t*)h->buf[TSLAM_BUF_DESC_YS].ptr;
     c.rowstart = (uint16_t*)h->buf[TSLAM_BUF_ROWSTART].ptr;
     c.qbest = (uint32_t*)h->buf[TSLAM_BUF_QBEST].ptr;
     c.qsecond = (uint32_t*)h->buf[TSLAM_BUF_QSECOND].ptr;
@@ -194,6 +196,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     if (p.edge_margin < 19) return fail(TSLAM_EINVAL, "edge_margin must be >= 19");
     if (p.fast_threshold < 0 || p.fast_threshold > 254) return fail(TSLAM_EINVAL, "fast_threshold must be in [0, 254]");
     if (p.max_batch < 1) return fail(TSLAM_EINVAL, "max_batch must be >= 1");
+    if (p.max_hamming < 0 || p.max_hamming > 253) return fail(TSLAM_EINVAL, "max_hamming must be in [0, 253]");
     if (p.refine_iters < 1) return fail(TSLAM_EINVAL, "refine_iters must be >= 1");
     if (p.ransac_splits < 0 || p.ransac_splits > TS_MAX_SPLITS) return fail(TSLAM_EINVAL, "ransac_splits must be in [0, 32]");
     const int W = pairs[0].width, H = pairs[0].height;
@@ -248,7 +251,8 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
         {TSLAM_BUF_QBEST, B, P * 2 * K * 4},
         {TSLAM_BUF_QSECOND, B, P * 2 * K * 4},
         {TSLAM_BUF_TBEST, B, P * 2 * K * 4},
-        {TSLAM_BUF_YPERM, R, C * K * 2},
+        {TSLAM_BUF_YSORTED, R, C * K * 16},
+        {TSLAM_BUF_DESC_YS, R, C * K * 8 * 4},
         {TSLAM_BUF_ROWSTART, R, C * (int64_t)h->g.rs_total * 2},
     };
     int rc = TSLAM_OK;
@@ -271,7 +275,17 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
         delete h;
         return rc;
     }
-    bool ok = hipMemcpy(h->d_brief, TSLAM_BRIEF_TABLE, sizeof(TSLAM_BRIEF_TABLE), hipMemcpyHostToDevice) == hipSuccess &&
+    // the describe kernel reads the rotated pattern as byte offsets from the patch origin
+    // (x - 18, y - 18) in its LDS tile: (py + 18) * TS_DT_P + px + 18 for both points, packed
+    // low | high << 16
+    std::vector<uint32_t> brief_off(30 * 256);
+    for (int i = 0; i < 30 * 256; ++i) {
+        const uint32_t t = TSLAM_BRIEF_TABLE[i];
+        const int px = (int8_t)(t & 0xFF), py = (int8_t)((t >> 8) & 0xFF);
+        const int qx = (int8_t)((t >> 16) & 0xFF), qy = (int8_t)(t >> 24);
+        brief_off[i] = (uint32_t)((py + 18) * TS_DT_P + px + 18) | ((uint32_t)((qy + 18) * TS_DT_P + qx + 18) << 16);
+    }
+    bool ok = hipMemcpy(h->d_brief, brief_off.data(), sizeof(uint32_t) * brief_off.size(), hipMemcpyHostToDevice) == hipSuccess &&
               hipMemcpy(h->d_wedges, TSLAM_WEDGES, sizeof(TSLAM_WEDGES), hipMemcpyHostToDevice) == hipSuccess;
     for (int i = 0; i < h->P && ok; ++i) {
         const int32_t* m[2] = {pairs[i].map_left, pairs[i].map_right};

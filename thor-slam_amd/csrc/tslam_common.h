@@ -11,7 +11,9 @@
 //   kps      u32 [R][C][K][2]        {x | y<<16, level | angle<<8 | score<<16}
 //   kcount   i32 [R][C][L]
 //   desc     u32 [R][C][K][8]        rBRIEF-256
-//   yperm    u16 [R][C][K]  rowstart u16 [R][C][sum(H_l+1)]  per-level y-sorted order + row index
+//   ys       u32x4 [R][C][K]  desc_ys u32 [R][C][K][8]  per level, keypoints sorted by (y, rank):
+//            {xy, level | score<<16, kp index, valid} and their descriptors (contiguous match staging)
+//   rowstart u16 [R][C][sum(H_l+1)]  per level: first y-sorted position of row y
 //   qbest/qsecond/tbest u32 [B][P][2][K]   matching scratch (mode 0 stereo, 1 temporal)
 //   stereo   i32 [R][P][K]  disp f64 [R][P][K]        stereo match + refined disparity of left kps
 //   temporal i32 [B][P][K]  tuv  f64 [B][P][K][2]     temporal match + refined (u, v) at t
@@ -88,7 +90,8 @@ struct BatchCtx {
     uint32_t* kps;
     int32_t* kcount;
     uint32_t* desc;
-    uint16_t* yperm;       // [R][C][K]
+    uint4* ys;             // [R][C][K] y-sorted keypoint records
+    uint32_t* desc_ys;     // [R][C][K][8] y-sorted descriptors
     uint16_t* rowstart;    // [R][C][rs_total]
     uint32_t* qbest;
     uint32_t* qsecond;
@@ -102,7 +105,7 @@ struct BatchCtx {
     double* ransac;        // [B][P][TS_MAX_SPLITS][13] split winners (key word + pose)
     int32_t* stats;
     double* state;
-    const uint32_t* brief_table;  // [30][256] packed int8x4 (px, py, qx, qy)
+    const uint32_t* brief_table;  // [30][256] LDS patch byte offsets of the two points (lo | hi << 16)
     const int64_t* wedges;        // [31][2]
     PairCalib calib[8];
     MatchParams mp;
@@ -182,14 +185,9 @@ __device__ __forceinline__ bool xcd_image_block(int b, int n_img, int bpi, int* 
     return *img < n_img;
 }
 
-// Keypoint slot for position `pos` of an image walked level by level in y-sorted order (padding
-// positions map to themselves).  Returns the keypoint index and its level.
-__device__ __forceinline__ int ysorted_kp(const BatchCtx& c, const uint16_t* yperm_img, const int32_t* kcount_img,
-                                          int pos, int* level, bool* valid) {
+// Level of y-sorted position `pos` (levels are laid out back to back, koff[l] .. koff[l+1]).
+__device__ __forceinline__ int pos_level(const LevelGeom& g, int pos) {
     int l = 0;
-    while (l + 1 < c.g.n_levels && pos >= c.g.koff[l + 1]) ++l;
-    *level = l;
-    const int r = pos - c.g.koff[l];
-    *valid = r < kcount_img[l];
-    return *valid ? (int)yperm_img[pos] : pos;
+    while (l + 1 < g.n_levels && pos >= g.koff[l + 1]) ++l;
+    return l;
 }

@@ -55,6 +55,8 @@ class HipSlamConfig(SlamConfig):
             raise ValueError("fast_threshold must be in [0, 254]")
         if self.batch_size < 1:
             raise ValueError("batch_size must be >= 1")
+        if not 0 <= self.max_hamming <= 253:
+            raise ValueError("max_hamming must be in [0, 253] (the mutual check keeps distances as bytes)")
 
 
 def level_shapes(width: int, height: int, n_levels: int) -> list[tuple[int, int]]:
