@@ -13,6 +13,28 @@
 // grid (ceil(H/32), n*C), block 256.  32 = 2^5 keeps every level's rows of the band inside the
 // block (2x2 boxes never straddle bands) for up to 6 levels.
 // ---------------------------------------------------------------------------------------------
+// Bilinear sample of the source at a 1/32-px fixed-point map position (oracle.remap).
+__device__ __forceinline__ int remap_px(const uint8_t* src, int W, int H, int2 m) {
+    const int sx = m.x >> 5, sy = m.y >> 5;
+    const int fx = m.x & 31, fy = m.y & 31;
+    const int xa = min(max(sx, 0), W - 1), xb = min(max(sx + 1, 0), W - 1);
+    const int ya = min(max(sy, 0), H - 1), yb = min(max(sy + 1, 0), H - 1);
+    const int p00 = src[ya * W + xa], p01 = src[ya * W + xb];
+    const int p10 = src[yb * W + xa], p11 = src[yb * W + xb];
+    const int acc = p00 * (32 - fx) * (32 - fy) + p01 * fx * (32 - fy) + p10 * (32 - fx) * fy + p11 * fx * fy;
+    return (acc + 512) >> 10;
+}
+
+// 2x2 box of 8 bytes of two rows -> 4 output bytes: (a + b + c + d + 2) >> 2 per output, on u16
+// pairs (even / odd byte lanes), exact.
+__device__ __forceinline__ uint32_t box4(uint32_t r0a, uint32_t r0b, uint32_t r1a, uint32_t r1b) {
+    auto pairsum = [](uint32_t v) { return (v & 0x00FF00FFu) + ((v >> 8) & 0x00FF00FFu); };   // (b0+b1, b2+b3)
+    const uint32_t sa = pairsum(r0a) + pairsum(r1a) + 0x00020002u;   // outputs 0, 1 (u16 lanes)
+    const uint32_t sb = pairsum(r0b) + pairsum(r1b) + 0x00020002u;   // outputs 2, 3
+    const uint32_t qa = (sa >> 2) & 0x00FF00FFu, qb = (sb >> 2) & 0x00FF00FFu;
+    return __builtin_amdgcn_perm(qb, qa, 0x06040200u);   // bytes: qa.lo, qa.hi, qb.lo, qb.hi
+}
+
 __global__ __launch_bounds__(256) void k_rectify_pyramid(BatchCtx c) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int img = blockIdx.y;             // f * C + cam
@@ -25,33 +47,74 @@ __global__ __launch_bounds__(256) void k_rectify_pyramid(BatchCtx c) {
     uint8_t* pyr = c.pyr + ((size_t)ring_slot(c, c.g0 + f) * c.C + cam) * c.g.pyr_bytes;
     const bool has_map = (c.map_mask >> cam) & 1u;
     const int32_t* map = c.maps + (size_t)cam * W * H * 2;
+    // 16-byte rows everywhere (W % 64 == 0 keeps every level's rows 16-byte aligned for 4 levels;
+    // the configs in BASELINE.json have W = 640 / 1280): wide path; byte path otherwise
+    bool wide = (W & 63) == 0 && (c.g.pyr_bytes & 15) == 0;
+    for (int l = 1; l < c.g.n_levels; ++l) wide = wide && (c.g.pyr_off[l] & 15) == 0 && (c.g.W[l] & 15) == 0;
 
-    // level 0 into LDS + global
     uint8_t* l0 = lds;
+    if (wide) {
+        // level 0: 16 pixels per thread item
+        const int W16 = W >> 4, n16 = rows0 * W16;
+        for (int i = threadIdx.x; i < n16; i += blockDim.x) {
+            const int r = i / W16, x16 = i - r * W16;
+            const size_t off = (size_t)(y0 + r) * W + 16 * x16;
+            uint4 v;
+            if (has_map) {
+                uint32_t w[4];
+                const int2* mp = reinterpret_cast<const int2*>(map) + off;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    uint32_t acc = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) acc |= (uint32_t)remap_px(src, W, H, mp[4 * q + b]) << (8 * b);
+                    w[q] = acc;
+                }
+                v = {w[0], w[1], w[2], w[3]};
+            } else {
+                v = *reinterpret_cast<const uint4*>(src + off);
+            }
+            reinterpret_cast<uint4*>(l0)[i] = v;
+            *reinterpret_cast<uint4*>(pyr + off) = v;
+        }
+        __syncthreads();
+        // levels 1..: 4 output bytes per item from two 8-byte row pieces of the previous level
+        const uint8_t* prev = l0;
+        int prevW = W;
+        uint8_t* cur = l0 + TS_RECT_BAND * W;
+        for (int l = 1; l < c.g.n_levels; ++l) {
+            const int Wl = c.g.W[l], Hl = c.g.H[l];
+            const int ly0 = y0 >> l;
+            const int lrows = min(TS_RECT_BAND >> l, Hl - ly0);
+            const int W4 = Wl >> 2;
+            uint8_t* out = pyr + c.g.pyr_off[l];
+            for (int i = threadIdx.x; i < lrows * W4; i += blockDim.x) {
+                const int r = i / W4, x4 = i - r * W4;
+                const uint2 a = *reinterpret_cast<const uint2*>(prev + (2 * r) * prevW + 8 * x4);
+                const uint2 b = *reinterpret_cast<const uint2*>(prev + (2 * r + 1) * prevW + 8 * x4);
+                const uint32_t v = box4(a.x, a.y, b.x, b.y);
+                reinterpret_cast<uint32_t*>(cur)[i] = v;
+                *reinterpret_cast<uint32_t*>(out + (size_t)(ly0 + r) * Wl + 4 * x4) = v;
+            }
+            __syncthreads();
+            prev = cur;
+            prevW = Wl;
+            cur = cur + (TS_RECT_BAND >> l) * Wl;
+        }
+        return;
+    }
+
+    // byte path (any geometry)
     for (int idx = threadIdx.x; idx < rows0 * W; idx += blockDim.x) {
         const int r = idx / W;
         const int x = idx - r * W;
         const int y = y0 + r;
-        int v;
-        if (has_map) {
-            const int2 m = *reinterpret_cast<const int2*>(map + ((size_t)y * W + x) * 2);
-            const int sx = m.x >> 5, sy = m.y >> 5;
-            const int fx = m.x & 31, fy = m.y & 31;
-            const int xa = min(max(sx, 0), W - 1), xb = min(max(sx + 1, 0), W - 1);
-            const int ya = min(max(sy, 0), H - 1), yb = min(max(sy + 1, 0), H - 1);
-            const int p00 = src[ya * W + xa], p01 = src[ya * W + xb];
-            const int p10 = src[yb * W + xa], p11 = src[yb * W + xb];
-            const int acc = p00 * (32 - fx) * (32 - fy) + p01 * fx * (32 - fy) + p10 * (32 - fx) * fy + p11 * fx * fy;
-            v = (acc + 512) >> 10;
-        } else {
-            v = src[y * W + x];
-        }
+        const int v = has_map ? remap_px(src, W, H, *reinterpret_cast<const int2*>(map + ((size_t)y * W + x) * 2))
+                              : src[y * W + x];
         l0[r * W + x] = (uint8_t)v;
         pyr[(size_t)y * W + x] = (uint8_t)v;
     }
     __syncthreads();
-
-    // levels 1.. from the previous level's LDS rows
     const uint8_t* prev = l0;
     int prevW = W;
     uint8_t* cur = l0 + TS_RECT_BAND * W;

@@ -207,6 +207,8 @@ __device__ bool solve6(const double* Hm, const double* g, double* x, double* L) 
 }
 
 #define POSE_THREADS 256
+#define TS_RS_CPT 4            // correspondences per thread per scoring pass
+#define TS_MAX_HYP_SPLIT 256   // hypotheses per RANSAC block (n_hyp <= 256)
 #define N_ACC 29   // 21 (upper H) + 6 (g) + 1 (sq) + 1 (count)
 
 __device__ __forceinline__ void write_stats(int32_t* so, int status, int n, int n_in, int best_cnt, int best_idx, int64_t g) {
@@ -284,11 +286,12 @@ __global__ __launch_bounds__(POSE_THREADS) void k_corr(BatchCtx c) {
 
 // ---- k_ransac: one split of the hypotheses of one (frame, pair) -----------------------------
 // grid (n*P*S): block (fp, split) solves P3P for hypotheses [h0, h1) (one per thread), then
-// scores its 4*(h1-h0) poses with every thread taking one pose and 1/slices of the
-// correspondences; writes its best (count+1)<<12 | (4095 - pose index) key and that pose.
+// scores its 4*(h1-h0) poses: correspondences stay in registers (TS_RS_CPT per thread), poses
+// are LDS broadcasts, inlier counts are wave ballots (integer sums: order-independent); writes
+// its best (count+1)<<12 | (4095 - pose index) key and that pose.
 __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
     extern __shared__ __attribute__((aligned(16))) double s_pose[];   // [4*Hs][12]
-    __shared__ int s_cnt[POSE_THREADS];
+    __shared__ int s_cnt[4 * TS_MAX_HYP_SPLIT];
     __shared__ uint32_t s_wbest[4];
     const int fp = blockIdx.x / S;
     const int split = blockIdx.x % S;
@@ -346,38 +349,46 @@ __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
             }
         }
     }
-    __syncthreads();
+    // scoring: every thread holds TS_RS_CPT correspondences in registers and walks the poses
+    // (LDS broadcasts); per pose and wave the inliers are ballot popcounts, added into s_cnt
     const int npose = 4 * nh;
-    const int slices = max(1, POSE_THREADS / max(1, npose));
+    for (int i = tid; i < npose; i += POSE_THREADS) s_cnt[i] = 0;
+    __syncthreads();
     const double thr2 = c.pp.thr2;
-    uint32_t my_best = 0;
-    for (int pi0 = 0; pi0 < npose; pi0 += POSE_THREADS / slices) {
-        const int pi = pi0 + tid / slices;
-        const int sl = tid % slices;
-        int cnt = 0;
-        bool valid = false;
-        if (tid / slices < POSE_THREADS / slices && pi < npose) {
-            const double* ps = s_pose + (size_t)pi * 12;
-            valid = !__builtin_isnan(ps[0]);
-            if (valid) {
-                double R[9], t[3];
+    for (int c0 = 0; c0 < n; c0 += POSE_THREADS * TS_RS_CPT) {
+        double cx5[TS_RS_CPT][5];
+        bool have[TS_RS_CPT];
 #pragma unroll
-                for (int k = 0; k < 9; ++k) R[k] = ps[k];
-                t[0] = ps[9]; t[1] = ps[10]; t[2] = ps[11];
-                for (int ci = sl; ci < n; ci += slices)
-                    cnt += is_inlier(R, t, corr + (size_t)ci * TS_CORR_DOUBLES, fx, fy, thr2) ? 1 : 0;
+        for (int k = 0; k < TS_RS_CPT; ++k) {
+            const int ci = c0 + k * POSE_THREADS + tid;
+            have[k] = ci < n;
+            const double* cr = corr + (size_t)(have[k] ? ci : 0) * TS_CORR_DOUBLES;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) cx5[k][q] = cr[q];
+        }
+        for (int pi = 0; pi < npose; ++pi) {
+            const double* ps = s_pose + (size_t)pi * 12;
+            if (__builtin_isnan(ps[0])) continue;   // uniform
+            double R[9], t[3];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) R[k] = ps[k];
+            t[0] = ps[9]; t[1] = ps[10]; t[2] = ps[11];
+            int cnt = 0;
+#pragma unroll
+            for (int k = 0; k < TS_RS_CPT; ++k) {
+                const bool in = have[k] && is_inlier(R, t, cx5[k], fx, fy, thr2);
+                cnt += __popcll(__ballot(in));
             }
+            if (lane == 0 && cnt) atomicAdd(&s_cnt[pi], cnt);
         }
-        s_cnt[tid] = cnt;
-        __syncthreads();
-        if (sl == 0 && tid / slices < POSE_THREADS / slices && pi < npose) {
-            int tot = 0;
-            for (int k = 0; k < slices; ++k) tot += s_cnt[tid + k];
-            const int gidx = 4 * h0 + pi;
-            const uint32_t key = valid ? ((uint32_t)(tot + 1) << 12) | (uint32_t)(4095 - gidx) : (uint32_t)(4095 - gidx);
-            my_best = key > my_best ? key : my_best;
-        }
-        __syncthreads();
+    }
+    __syncthreads();
+    uint32_t my_best = 0;
+    for (int pi = tid; pi < npose; pi += POSE_THREADS) {
+        const bool valid = !__builtin_isnan(s_pose[(size_t)pi * 12]);
+        const int gidx = 4 * h0 + pi;
+        const uint32_t key = valid ? ((uint32_t)(s_cnt[pi] + 1) << 12) | (uint32_t)(4095 - gidx) : (uint32_t)(4095 - gidx);
+        my_best = key > my_best ? key : my_best;
     }
     uint32_t wb = my_best;
 #pragma unroll
@@ -567,42 +578,48 @@ __global__ __launch_bounds__(POSE_THREADS) void k_refine(BatchCtx c, int S) {
     }
 }
 
-// Pose chaining: T_abs(t) = T_abs(t-1) * inv(T_rel(t)) for every successful frame.  The
-// relative poses of the batch are staged in LDS by the whole block first, so the sequential
-// composition (thread 0, one pair at a time) runs from LDS instead of dependent HBM loads.
+// Pose chaining: T_abs(t) = T_abs(t-1) * inv(T_rel(t)) for every successful frame, in frame
+// order (the association is the oracle's, so results do not depend on the batch size).  The
+// block inverts all relative poses in parallel into LDS; then 16 lanes of wave 0 carry T, one
+// element each: per frame a lane gathers its row of T (4 quad DPP broadcasts) and computes its element
+// with the oracle's expression, so a frame costs one 4-term dot product of latency.
+#define TS_CHAIN_CHUNK 128
 __global__ __launch_bounds__(256) void k_chain(BatchCtx c) {
-    extern __shared__ __attribute__((aligned(16))) double s_rel[];   // [n][12] + status
-    int* s_status = reinterpret_cast<int*>(s_rel + (size_t)c.n * 12);
+    __shared__ double s_inv[TS_CHAIN_CHUNK][16];
+    __shared__ int s_status[TS_CHAIN_CHUNK];
+    const int tid = threadIdx.x, lane = tid & 63;
     for (int p = 0; p < c.P; ++p) {
-        for (int i = threadIdx.x; i < c.n * 12; i += blockDim.x) {
-            const int f = i / 12, k = i % 12;
-            s_rel[i] = c.pose[(size_t)(f * c.P + p) * TS_POSE_DOUBLES + k];
-        }
-        for (int f = threadIdx.x; f < c.n; f += blockDim.x) s_status[f] = c.stats[(size_t)(f * c.P + p) * TS_STATS_INTS];
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            double T[16];
-            for (int k = 0; k < 16; ++k) T[k] = c.state[p * 16 + k];
-            for (int f = 0; f < c.n; ++f) {
-                const double* rel = s_rel + (size_t)f * 12;
-                if (s_status[f] == 0) {
-                    double inv[16] = {0};
-                    for (int i = 0; i < 3; ++i) {
-                        for (int j = 0; j < 3; ++j) inv[4 * i + j] = rel[4 * j + i];
-                        inv[4 * i + 3] = -((rel[i] * rel[3] + rel[4 + i] * rel[7]) + rel[8 + i] * rel[11]);
-                    }
-                    inv[15] = 1.0;
-                    double out[16];
-                    for (int i = 0; i < 4; ++i)
-                        for (int j = 0; j < 4; ++j)
-                            out[4 * i + j] = ((T[4 * i] * inv[j] + T[4 * i + 1] * inv[4 + j]) + T[4 * i + 2] * inv[8 + j]) + T[4 * i + 3] * inv[12 + j];
-                    for (int k = 0; k < 16; ++k) T[k] = out[k];
-                }
-                double* ab = c.pose + (size_t)(f * c.P + p) * TS_POSE_DOUBLES + 16;
-                for (int k = 0; k < 16; ++k) ab[k] = T[k];
+        double T = 0.0;
+        if (tid < 16) T = c.state[p * 16 + tid];
+        for (int f0 = 0; f0 < c.n; f0 += TS_CHAIN_CHUNK) {
+            const int nf = min(TS_CHAIN_CHUNK, c.n - f0);
+            __syncthreads();
+            for (int i = tid; i < nf * 16; i += blockDim.x) {
+                const int fl = i / 16, e = i % 16, r = e / 4, q = e % 4;
+                const double* rel = c.pose + (size_t)((f0 + fl) * c.P + p) * TS_POSE_DOUBLES;
+                double v;
+                if (r == 3) v = q == 3 ? 1.0 : 0.0;
+                else if (q < 3) v = rel[4 * q + r];
+                else v = -((rel[r] * rel[3] + rel[4 + r] * rel[7]) + rel[8 + r] * rel[11]);
+                s_inv[fl][e] = v;
             }
-            for (int k = 0; k < 16; ++k) c.state[p * 16 + k] = T[k];
+            for (int fl = tid; fl < nf; fl += blockDim.x) s_status[fl] = c.stats[(size_t)((f0 + fl) * c.P + p) * TS_STATS_INTS];
+            __syncthreads();
+            if (tid < 64) {
+                const int j = lane & 3;
+                for (int fl = 0; fl < nf; ++fl) {
+                    // row i of T lives in this lane's quad: quad_perm broadcasts of lanes 0..3
+                    const double t0 = dpp_f64c<0x00>(T), t1 = dpp_f64c<0x55>(T);
+                    const double t2 = dpp_f64c<0xAA>(T), t3 = dpp_f64c<0xFF>(T);
+                    if (s_status[fl] == 0) {
+                        const double* inv = s_inv[fl];
+                        T = ((t0 * inv[j] + t1 * inv[4 + j]) + t2 * inv[8 + j]) + t3 * inv[12 + j];
+                    }
+                    if (lane < 16) c.pose[(size_t)((f0 + fl) * c.P + p) * TS_POSE_DOUBLES + 16 + lane] = T;
+                }
+            }
         }
+        if (tid < 16) c.state[p * 16 + tid] = T;
         __syncthreads();
     }
 }
@@ -626,6 +643,5 @@ void launch_pose(const BatchCtx& c, hipStream_t s) {
 }
 
 void launch_chain(const BatchCtx& c, hipStream_t s) {
-    const size_t lds = (size_t)c.n * 12 * sizeof(double) + (size_t)c.n * sizeof(int) + 16;
-    hipLaunchKernelGGL(k_chain, dim3(1), dim3(256), lds, s, c);
+    hipLaunchKernelGGL(k_chain, dim3(1), dim3(256), 0, s, c);
 }

@@ -167,10 +167,40 @@ __device__ __forceinline__ int wave_sum_dpp(int v) {
            (__builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48));
 }
 
+// f64 DPP move (both halves) for the row reductions below.
+__device__ __forceinline__ double dpp_f64(double v, int ctrl_sel) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    int lo = (int)(uint32_t)b, hi = (int)(uint32_t)(b >> 32);
+    switch (ctrl_sel) {   // constant after inlining
+        case 0: lo = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, false); break;
+        case 1: lo = __builtin_amdgcn_mov_dpp(lo, 0x4E, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x4E, 0xF, 0xF, false); break;
+        case 2: lo = __builtin_amdgcn_mov_dpp(lo, 0x141, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x141, 0xF, 0xF, false); break;
+        default: lo = __builtin_amdgcn_mov_dpp(lo, 0x140, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x140, 0xF, 0xF, false); break;
+    }
+    return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+// f64 DPP move with a compile-time control (e.g. quad_perm broadcasts 0x00/0x55/0xAA/0xFF).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64c(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), lane);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// Wave-uniform f64 sum: DPP row reductions (no LDS crossbar) + four readlanes.  Requires all 64
+// lanes active.  The summation order is fixed (deterministic run to run).
 __device__ __forceinline__ double wave_sum_f64(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v = v + dpp_f64(v, 0);
+    v = v + dpp_f64(v, 1);
+    v = v + dpp_f64(v, 2);
+    v = v + dpp_f64(v, 3);
+    return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
 }
 
 // XCD-aware 1-D block mapping: blocks are dealt round-robin over the 8 XCDs, so block b runs on the
