@@ -292,6 +292,8 @@ __device__ __forceinline__ uint32_t fast4(const uint8_t* rc, int W, int x0, int 
 // phase is dealt to the 8 waves in equal (row, 64-lane chunk) items.
 // ---------------------------------------------------------------------------------------------
 #define TS_DET_THREADS 512
+#define TS_SMOOTH_GROUPS 2                                // smoothing items = (quad, row group)
+#define TS_SMOOTH_ROWS (TS_BAND_ROWS / TS_SMOOTH_GROUPS)
 #define TS_DET_WAVES (TS_DET_THREADS / 64)
 
 // 16-byte async global -> LDS copy; `wave_dst` is the wave-uniform LDS base, lane k lands at +16k
@@ -379,15 +381,14 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
     __syncthreads();
 
     // 5x5 binomial smoothing of the band rows (column clamp; rows already clamped in LDS).
-#ifndef XP_SKIP_SMOOTH
     if (wide) {
-        // item = (4-pixel quad, 8-row half): 12 horizontal sums (3 dword LDS reads each) slide
+        // item = (4-pixel quad, 8-row group): 12 horizontal sums (3 dword LDS reads each) slide
         // through 5 registers; u16 pairs cannot overflow (16 * 16 * 255 + 128 < 2^16)
         const int W4 = W >> 2;
         const u16x2 four = {4, 4}, six = {6, 6}, rnd = {128, 128};
-        for (int it = threadIdx.x; it < 2 * W4; it += TS_DET_THREADS) {
+        for (int it = threadIdx.x; it < TS_SMOOTH_GROUPS * W4; it += TS_DET_THREADS) {
             const int half = it / W4, q = it - half * W4, x0 = 4 * q;
-            const int o0 = 8 * half, o1 = min(o0 + 8, rows_here);   // output rows (band-relative)
+            const int o0 = TS_SMOOTH_ROWS * half, o1 = min(o0 + TS_SMOOTH_ROWS, rows_here);   // output rows (band-relative)
             if (o0 >= o1) continue;
             u16x2 e[5], d[5];
 #pragma unroll
@@ -420,10 +421,8 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
             }
         }
     }
-#endif
 
     // FAST scores (thresholded) for rows y0-1 .. y0+16
-#ifndef XP_SKIP_FAST
     if (wide) {
         // 4 pixels per lane (fast4): 21 dword LDS reads and ~250 packed-f16 ops per quad, no
         // divergence; items (row, quad) dealt over the block
@@ -456,36 +455,102 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
             score[i] = (uint8_t)sc;
         }
     }
-#endif
     __syncthreads();
 
-    // 3x3 NMS (ties -> earlier raster position) inside the margin; emit keys.  Items = (row,
-    // 64-pixel chunk) dealt round-robin over the waves.
+    // 3x3 NMS (ties -> earlier raster position) inside the margin; emit keys.
     const int M = c.margin;
     uint32_t* cand = c.cand + ((size_t)f * c.C + cam) * c.g.cand_total + c.g.cand_off[l] + (size_t)band * c.g.cand_cap[l];
-#ifdef XP_SKIP_NMS
-    const int ylo = 0, yhi = 0;
-#else
     const int ylo = max(y0, M), yhi = min(y0 + TS_BAND_ROWS, H - M);
-#endif
-    const int xspan = W - 2 * M, nchx = (xspan + 63) >> 6;
-    for (int it = wave; it < (yhi - ylo) * nchx; it += TS_DET_WAVES) {
-        const int yy = it / nchx, ch = it - yy * nchx;
-        const int y = ylo + yy, x = M + ch * 64 + lane;
-        if (x >= W - M) continue;
-        const int r = y - y0 + 1;
-        const int p = score[r * W + x];
-        if (p == 0) continue;
-        const uint8_t* up = score + (r - 1) * W + x;
-        const uint8_t* mid = score + r * W + x;
-        const uint8_t* dn = score + (r + 1) * W + x;
-        const bool keep = up[-1] < p && up[0] < p && up[1] < p && mid[-1] < p &&
-                          mid[1] <= p && dn[-1] <= p && dn[0] <= p && dn[1] <= p;
-        if (keep) {
-            const uint32_t key = ((uint32_t)(255 - p) << 22) | ((uint32_t)y << 11) | (uint32_t)x;
-            const uint32_t slot = atomicAdd(&s_count, 1u);
-            cand[slot] = key;
-            atomicAdd(&s_hist[255 - p], 1u);
+    if (wide) {
+        // 4 pixels per lane: keep = p > max(4 earlier neighbours) && p >= max(4 later ones), on
+        // the two f16 pixel pairs (1024 + score, exact), no divergence; survivors are appended
+        // with one LDS atomic per wave and pixel slot
+        const int W4 = W >> 2;
+        const uint32_t* sc32 = (const uint32_t*)score;
+        constexpr uint32_t k64 = 0x64646464u;
+        const h16x2 half = {(_Float16)0.5, (_Float16)0.5};
+        for (int i0 = wave * 64; i0 < (yhi - ylo) * W4; i0 += TS_DET_THREADS) {
+            const int it = i0 + lane;
+            uint32_t kbits = 0;   // bit j: pixel x0 + j survives
+            int y = 0, x0 = 0;
+            uint32_t P = 0;
+            if (it < (yhi - ylo) * W4) {
+                const int yy = it / W4, q = it - yy * W4;
+                y = ylo + yy;
+                x0 = 4 * q;
+                const int r = y - y0 + 1;
+                const uint32_t* pm = sc32 + r * W4 + q;
+                P = pm[0];
+                if (P && x0 + 4 > M && x0 < W - M) {
+                    const uint32_t* pu = pm - W4;
+                    const uint32_t* pd = pm + W4;
+                    const uint32_t ua = pu[-1], ub = pu[0], uc = pu[1];
+                    const uint32_t ma = pm[-1], mc = pm[1];
+                    const uint32_t da = pd[-1], db = pd[0], dc = pd[1];
+                    const uint32_t ul = __builtin_amdgcn_alignbyte(ub, ua, 3), ur = __builtin_amdgcn_alignbyte(uc, ub, 1);
+                    const uint32_t ml = __builtin_amdgcn_alignbyte(P, ma, 3), mr = __builtin_amdgcn_alignbyte(mc, P, 1);
+                    const uint32_t dl = __builtin_amdgcn_alignbyte(db, da, 3), dr = __builtin_amdgcn_alignbyte(dc, db, 1);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const uint32_t sel = h ? 0x00070005u : 0x00060004u;
+                        auto toh = [sel](uint32_t v) { return __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(v, k64, sel)); };
+                        const h16x2 pp = toh(P);
+                        const h16x2 before = hmax3(hmax3(toh(ul), toh(ub), toh(ur)), toh(ml), toh(ml));
+                        const h16x2 after = hmax3(hmax3(toh(dl), toh(db), toh(dr)), toh(mr), toh(mr));
+                        const h16x2 k = __builtin_elementwise_minimum((pp - before) - half, pp - after);
+                        const uint32_t nb = ~__builtin_bit_cast(uint32_t, k);
+                        kbits |= ((nb >> 15) & 1u) << h;
+                        kbits |= ((nb >> 31) & 1u) << (h + 2);
+                    }
+                    // margin: M <= x < W - M
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (x0 + j < M || x0 + j >= W - M) kbits &= ~(1u << j);
+                }
+            }
+            // append: one LDS atomic per wave for its 4 pixel slots
+            uint64_t bm[4];
+            uint32_t tot = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                bm[j] = __ballot((kbits >> j) & 1u);
+                tot += (uint32_t)__popcll(bm[j]);
+            }
+            if (tot == 0) continue;   // wave-uniform
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&s_count, tot);
+            base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if ((kbits >> j) & 1u) {
+                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm[j], 0u));
+                    const uint32_t pv = (P >> (8 * j)) & 0xFFu;
+                    cand[base + rank] = ((255u - pv) << 22) | ((uint32_t)y << 11) | (uint32_t)(x0 + j);
+                    atomicAdd(&s_hist[255 - pv], 1u);
+                }
+                base += (uint32_t)__popcll(bm[j]);
+            }
+        }
+    } else {
+        const int xspan = W - 2 * M, nchx = (xspan + 63) >> 6;
+        for (int it = wave; it < (yhi - ylo) * nchx; it += TS_DET_WAVES) {
+            const int yy = it / nchx, ch = it - yy * nchx;
+            const int y = ylo + yy, x = M + ch * 64 + lane;
+            if (x >= W - M) continue;
+            const int r = y - y0 + 1;
+            const int p = score[r * W + x];
+            if (p == 0) continue;
+            const uint8_t* up = score + (r - 1) * W + x;
+            const uint8_t* mid = score + r * W + x;
+            const uint8_t* dn = score + (r + 1) * W + x;
+            const bool keep = up[-1] < p && up[0] < p && up[1] < p && mid[-1] < p &&
+                              mid[1] <= p && dn[-1] <= p && dn[0] <= p && dn[1] <= p;
+            if (keep) {
+                const uint32_t key = ((uint32_t)(255 - p) << 22) | ((uint32_t)y << 11) | (uint32_t)x;
+                const uint32_t slot = atomicAdd(&s_count, 1u);
+                cand[slot] = key;
+                atomicAdd(&s_hist[255 - p], 1u);
+            }
         }
     }
     __syncthreads();
