@@ -72,6 +72,13 @@ def triangle_indices(total: int, unique: int) -> np.ndarray:
     return np.where(k < unique, k, period - k)
 
 
+def frame_bytes(W: int, H: int, K: int, n_img: int = 2, n_pairs: int = 1, channels: int = 1) -> int:
+    """SURVEY.md §8d compulsory bytes per stereo frame: read the images, write keypoints (12 B) and
+    descriptors (32 B), write the match records (8 B per keypoint, for the stereo and the temporal
+    matching of each pair).  C2: 2 * (256,000 + 88,000) + 2 * 16,000 = 720,000 B."""
+    return n_img * (W * H * channels + K * (12 + 32)) + 2 * n_pairs * K * 8
+
+
 def kernel_bytes(name: str, B: int, h, cfg, maps_identity: bool) -> float:
     """Algorithmic (compulsory) HBM bytes of one launch of a kernel over B stereo frames."""
     W, H, K = h.width, h.height, cfg.n_features
@@ -97,21 +104,41 @@ def kernel_bytes(name: str, B: int, h, cfg, maps_identity: bool) -> float:
     return 0.0
 
 
-def cpu_baseline(frames: np.ndarray, rect, cfg, budget_s: float) -> dict:
+def _oracle_worker(args):
+    """One CPU process: the NumPy oracle tracking its contiguous frame chunk (replayed) for budget_s."""
+    frames, rect_d, cfg_d, budget_s = args
     from oracle import numpy_slam as O
+    from thor_slam_amd.params import HipSlamConfig
 
-    trk = O.OracleTracker(cfg, dict(fx=rect.fx, fy=rect.fy, cx=rect.cx, cy=rect.cy, baseline=rect.baseline,
-                                    map_l=rect.map_left, map_r=rect.map_right))
+    trk = O.OracleTracker(HipSlamConfig(**cfg_d), rect_d)
     n = 0
     t0 = time.perf_counter()
-    elapsed = 0.0
-    while elapsed < budget_s and n < len(frames):
-        trk.step(frames[n, 0], frames[n, 1])
+    while time.perf_counter() - t0 < budget_s:
+        i = n % len(frames)
+        trk.step(frames[i, 0], frames[i, 1])
         n += 1
-        elapsed = time.perf_counter() - t0
-    return {"value": n / elapsed, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{n} consecutive synthetic 640x400 stereo frames (seed 0), NumPy oracle, 1 process, "
-                      f"{elapsed:.1f} s"}
+    return n, time.perf_counter() - t0
+
+
+def cpu_baseline(frames: np.ndarray, rect, cfg, budget_s: float, procs: int) -> dict:
+    """The NumPy oracle on the host cores: `procs` processes, each tracking a contiguous chunk of the
+    same frames (relative-pose work is independent per frame pair)."""
+    import dataclasses
+
+    rect_d = dict(fx=rect.fx, fy=rect.fy, cx=rect.cx, cy=rect.cy, baseline=rect.baseline,
+                  map_l=rect.map_left, map_r=rect.map_right)
+    cfg_d = dataclasses.asdict(cfg)
+    chunks = [c for c in np.array_split(frames, procs) if len(c)]
+    if len(chunks) == 1:
+        results = [_oracle_worker((chunks[0], rect_d, cfg_d, budget_s))]
+    else:
+        with ProcessPoolExecutor(max_workers=len(chunks)) as ex:
+            results = list(ex.map(_oracle_worker, [(c, rect_d, cfg_d, budget_s) for c in chunks]))
+    n = sum(r[0] for r in results)
+    wall = max(r[1] for r in results)
+    return {"value": n / wall, "unit": "frames/s", "cores": len(chunks), "kind": "port",
+            "sample": f"{n} synthetic 640x400 stereo frames (seed 0, {len(frames)} distinct, replayed per process), "
+                      f"NumPy oracle, {len(chunks)} process(es) x {budget_s:.0f} s"}
 
 
 def main() -> None:
@@ -122,7 +149,8 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=256, help="stereo frames per step")
     ap.add_argument("--unique", type=int, default=48, help="distinct rendered frames (triangle-wave replay)")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU baseline (0 = skip)")
-    ap.add_argument("--kernel-reps", type=int, default=5)
+    ap.add_argument("--cpu-procs", type=int, default=8, help="oracle processes for the CPU baseline")
+    ap.add_argument("--latency-frames", type=int, default=20, help="B=1 submissions timed for latency_b1_ms")
     ap.add_argument("--out", type=str, default="", help="also write the JSON line to this file")
     ap.add_argument("--dist-backend", type=str, default="nccl", help="nccl (RCCL) or gloo (rehearsal, host copy)")
     ap.add_argument("--pmc", type=str, default=str(ROOT / "profiles" / "pmc_latest.json"),
@@ -174,8 +202,20 @@ def main() -> None:
     exchange = FeatureExchange(layout, "cuda" if on_device else "cpu", world) if world > 1 else None
     staging = torch.empty((layout.rank_bytes,), dtype=torch.uint8, device="cuda") if world > 1 and not on_device else None
 
-    def step(s: int) -> None:
-        h.submit(seq[s * B].data_ptr(), B, sp)
+    names = list(KERNELS)
+    n_ev = len(names) + 1
+
+    def step(s: int, evs=None) -> None:
+        # one batch = every kernel of the hot path in order on `stream`; in the timed steps HIP
+        # events bracket each kernel (the per-kernel durations below are from these launches)
+        h.begin_batch(seq[s * B].data_ptr(), B)
+        if evs is not None:
+            evs[0].record(stream)
+        for i, k in enumerate(names):
+            h.run_kernel(k, sp)
+            if evs is not None:
+                evs[i + 1].record(stream)
+        h.end_batch()
         if exchange is not None:  # the exchange step: every rank's keypoints/descriptors/poses to all
             if on_device:
                 h.pack_features(exchange.send.data_ptr(), sp)
@@ -184,6 +224,7 @@ def main() -> None:
                 exchange.send.copy_(staging.cpu())
             exchange.all_gather()
 
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_ev)] for _ in range(args.steps)]
     for s in range(args.warmup):
         step(s)
     torch.cuda.synchronize()
@@ -191,8 +232,8 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s in range(args.warmup, args.warmup + args.steps):
-        step(s)
+    for k in range(args.steps):
+        step(args.warmup + k, events[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -205,23 +246,14 @@ def main() -> None:
     res = h.read_poses(B)
     ok_frac = float(np.mean(res["stats"][:, 0, 0] == 0))
 
-    # ---- per-kernel timing (HIP events on the launch stream) ----------------------------------
-    names = list(KERNELS)
-    acc = {k: 0.0 for k in names}
-    for rep in range(args.kernel_reps):
-        h.begin_batch(seq[(rep % args.steps) * B].data_ptr(), B)
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
-        evs[0].record(stream)
+    # ---- per-kernel durations of the timed launches (HIP events on the launch stream) ----------
+    per_kernel_us = {k: 0.0 for k in names}
+    for evs in events:
         for i, k in enumerate(names):
-            h.run_kernel(k, sp)
-            evs[i + 1].record(stream)
-        h.end_batch()
-        torch.cuda.synchronize()
-        for i, k in enumerate(names):
-            acc[k] += evs[i].elapsed_time(evs[i + 1]) * 1e3  # us
-    per_kernel_us = {k: acc[k] / args.kernel_reps for k in names}
+            per_kernel_us[k] += evs[i].elapsed_time(evs[i + 1]) * 1e3 / args.steps  # us
     dom = max(per_kernel_us, key=per_kernel_us.get)
-    dom_bytes = kernel_bytes(dom, B, h, cfg, rect.is_identity)
+    unit_bytes = frame_bytes(rect.width, rect.height, cfg.n_features)
+    dom_bytes = unit_bytes * B          # §8d per-frame bytes x the frames one launch processes
     achieved = dom_bytes / (per_kernel_us[dom] * 1e-6) / 1e9
 
     traffic = None
@@ -231,6 +263,21 @@ def main() -> None:
         kern = pmc.get("kernels", {}).get(KERNEL_SYMBOL.get(dom, ""), None)
         if kern is not None and pmc.get("batch_frames") == B:
             traffic = kern["hbm_bytes_per_launch"]
+
+    # ---- B = 1 latency: one frame submitted and its pose read back -------------
+    lat_ms = None
+    if rank == 0 and args.latency_frames > 0:
+        h1 = Handle([rect], cfg, max_batch=1, device=dev_index)
+        lat = []
+        for i in range(args.latency_frames + 3):
+            torch.cuda.synchronize()
+            ta = time.perf_counter()
+            h1.submit(seq[i].data_ptr(), 1, sp)
+            h1.read_poses(1)
+            if i >= 3:
+                lat.append((time.perf_counter() - ta) * 1e3)
+        h1.close()
+        lat_ms = float(np.median(lat))
 
     frames_total = world * args.steps * B
     out = {
@@ -263,14 +310,19 @@ def main() -> None:
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "algorithmic_bytes_per_launch": dom_bytes,
+            "algorithmic_bytes_per_frame": unit_bytes,
+            "frames_per_launch": B,
             "avg_launch_us": per_kernel_us[dom],
+            "kernel_own_bytes_per_launch": kernel_bytes(dom, B, h, cfg, rect.is_identity),
+            "end_to_end_hbm_frac": unit_bytes * (frames_total / elapsed / world) / (HBM_PEAK_GBS * 1e9),
         },
+        "latency_b1_ms": lat_ms,
         "per_kernel_us_per_batch": per_kernel_us,
         "tracking_ok_fraction_last_batch": ok_frac,
         "render_s": t_render,
     }
     if rank == 0 and args.cpu_budget > 0:
-        out["cpu_baseline"] = cpu_baseline(uniq, rect, cfg, args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(uniq, rect, cfg, args.cpu_budget, args.cpu_procs)
         out["cpu_baseline"]["host_cpus_visible"] = os.cpu_count()
     h.close()
     if world > 1:
