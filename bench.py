@@ -199,9 +199,11 @@ def main() -> None:
     sp = stream.cuda_stream
     layout = BlockLayout(n_frames=B, n_cams=2, K=cfg.n_features, L=cfg.n_levels)
     on_device = args.dist_backend == "nccl"
-    exchange = FeatureExchange(layout, "cuda" if on_device else "cpu", world) if world > 1 else None
+    # two exchange buffers: batch s packs into buffer s % 2 and all-gathers it asynchronously over
+    # RCCL while batch s + 1 computes (the buffer is reused only after its gather has completed)
+    exchanges = [FeatureExchange(layout, "cuda" if on_device else "cpu", world) for _ in range(2)] if world > 1 else []
+    pending = [None, None]
     staging = torch.empty((layout.rank_bytes,), dtype=torch.uint8, device="cuda") if world > 1 and not on_device else None
-
     names = list(KERNELS)
     n_ev = len(names) + 1
 
@@ -216,17 +218,29 @@ def main() -> None:
             if evs is not None:
                 evs[i + 1].record(stream)
         h.end_batch()
-        if exchange is not None:  # the exchange step: every rank's keypoints/descriptors/poses to all
+        if exchanges:  # the exchange step: every rank's keypoints/descriptors/poses to all ranks
+            k = s % 2
+            ex = exchanges[k]
             if on_device:
-                h.pack_features(exchange.send.data_ptr(), sp)
+                if pending[k] is not None:
+                    pending[k].wait()
+                h.pack_features(ex.send.data_ptr(), sp)
+                pending[k] = ex.all_gather(async_op=True)
             else:
                 h.pack_features(staging.data_ptr(), sp)
-                exchange.send.copy_(staging.cpu())
-            exchange.all_gather()
+                ex.send.copy_(staging.cpu())
+                ex.all_gather()
+
+    def drain() -> None:
+        for k in range(2):
+            if pending[k] is not None:
+                pending[k].wait()
+                pending[k] = None
 
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_ev)] for _ in range(args.steps)]
     for s in range(args.warmup):
         step(s)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -234,6 +248,7 @@ def main() -> None:
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(args.warmup + k, events[k])
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -138,3 +138,40 @@ def test_engine_two_source_rig_fuses_motion():
     err = np.linalg.norm(pose.position - gt[:3, 3])
     assert err < 0.15 * np.linalg.norm(gt[:3, 3]) + 3e-3, err
     eng.shutdown()
+
+
+def test_pack_features_matches_host_block():
+    """tslam_pack_features (device gather) == dist.pack_block of the handle's own outputs."""
+    import torch
+
+    from thor_slam_amd._lib import Handle
+    from thor_slam_amd.dist import BlockLayout, pack_block, unpack_rank_block
+
+    sc = scenario(seed=0, n=3)
+    cfg, rect = sc["cfg"], sc["rect"]
+    n = 3
+    h = Handle([rect], cfg, max_batch=n)
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    h.submit(dev.data_ptr(), n, s)
+    res = h.read_poses(n)
+    layout = BlockLayout(n_frames=n, n_cams=2, K=cfg.n_features, L=cfg.n_levels)
+    out = torch.zeros(layout.rank_bytes, dtype=torch.uint8, device="cuda")
+    assert h.pack_features(out.data_ptr(), s) == layout.rank_bytes
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    kps = np.zeros((n, 2, layout.K, 2), np.uint32)
+    desc = np.zeros((n, 2, layout.K, 8), np.uint32)
+    counts = np.zeros((n, 2, layout.L), np.int32)
+    for f in range(n):
+        for cam in range(2):
+            k = h.keypoints(f, cam)
+            kps[f, cam, :, 0] = k["x"] | (k["y"] << 16)
+            kps[f, cam, :, 1] = k["level"] | (k["angle"] << 8) | (k["score"] << 16)
+            desc[f, cam] = k["desc"]
+            counts[f, cam] = k["counts"]
+    want = pack_block(layout, kps, desc, counts, res["T_rel"], res["cov"], res["stats"])
+    np.testing.assert_array_equal(got, want)
+    dec = unpack_rank_block(layout, got)
+    np.testing.assert_array_equal(dec["stats"], res["stats"])
+    h.close()

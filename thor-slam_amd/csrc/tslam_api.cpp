@@ -495,27 +495,10 @@ int tslam_pack_features(tslam_handle* h, void* dst, int64_t* bytes, void* stream
     const int64_t feat = (int64_t)h->cur_n * h->C * per_cam;
     const int64_t pose_bytes = (16 + 36) * 8 + TS_STATS_INTS * 4;
     if (bytes) *bytes = feat + (int64_t)h->cur_n * h->P * pose_bytes;
-    hipStream_t s = (hipStream_t)stream;
-    char* d = (char*)dst;
-    for (int f = 0; f < h->cur_n; ++f) {
-        const int slot = (int)((h->cur_g0 + f) % h->R);
-        for (int cam = 0; cam < h->C; ++cam) {
-            char* o = d + ((int64_t)f * h->C + cam) * per_cam;
-            const size_t sc = (size_t)slot * h->C + cam;
-            HIPCHK(hipMemcpyAsync(o, (char*)h->buf[TSLAM_BUF_KEYPOINTS].ptr + sc * K * 8, K * 8, hipMemcpyDeviceToDevice, s));
-            HIPCHK(hipMemcpyAsync(o + K * 8, (char*)h->buf[TSLAM_BUF_DESC].ptr + sc * K * 32, K * 32, hipMemcpyDeviceToDevice, s));
-            HIPCHK(hipMemcpyAsync(o + K * 40, (char*)h->buf[TSLAM_BUF_KCOUNT].ptr + sc * L * 4, L * 4, hipMemcpyDeviceToDevice, s));
-        }
-    }
-    // pose trailer per (frame, pair): T_rel[16], cov[36] (f64), stats[8] (i32)
-    for (int i = 0; i < h->cur_n * h->P; ++i) {
-        char* o = d + feat + (int64_t)i * pose_bytes;
-        const char* pz = (const char*)h->buf[TSLAM_BUF_POSE].ptr + (size_t)i * TS_POSE_DOUBLES * 8;
-        HIPCHK(hipMemcpyAsync(o, pz, 16 * 8, hipMemcpyDeviceToDevice, s));
-        HIPCHK(hipMemcpyAsync(o + 16 * 8, pz + 32 * 8, 36 * 8, hipMemcpyDeviceToDevice, s));
-        HIPCHK(hipMemcpyAsync(o + 52 * 8, (const char*)h->buf[TSLAM_BUF_STATS].ptr + (size_t)i * TS_STATS_INTS * 4,
-                              TS_STATS_INTS * 4, hipMemcpyDeviceToDevice, s));
-    }
+    HIPCHK(hipSetDevice(h->device));
+    const BatchCtx c = make_ctx(h);
+    launch_pack(c, (uint8_t*)dst, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
     return TSLAM_OK;
 }
 

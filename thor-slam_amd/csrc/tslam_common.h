@@ -124,6 +124,7 @@ void launch_match(const BatchCtx& c, hipStream_t s);
 void launch_match_refine(const BatchCtx& c, hipStream_t s);
 void launch_pose(const BatchCtx& c, hipStream_t s);
 void launch_chain(const BatchCtx& c, hipStream_t s);
+void launch_pack(const BatchCtx& c, uint8_t* dst, hipStream_t s);
 
 // ---------------------------------------------------------------------------------------------
 // small device helpers

@@ -97,18 +97,22 @@ class FeatureExchange:
         self.send = torch.zeros((layout.rank_bytes,), dtype=torch.uint8, device=device)
         self.recv = torch.zeros((world * layout.rank_bytes,), dtype=torch.uint8, device=device)
 
-    def all_gather(self):
-        """All-gather ``send`` from every rank into ``recv`` ([world][rank_bytes])."""
+    def all_gather(self, async_op: bool = False):
+        """All-gather ``send`` from every rank into ``recv`` ([world][rank_bytes]).
+
+        With ``async_op`` (RCCL) the collective is queued behind the current stream's work (the
+        pack kernel) and the call returns its work handle at once; ``handle.wait()`` makes the
+        current stream wait for it, so the next batch's kernels overlap the transfer."""
         import torch.distributed as dist
 
         if self.world == 1:
             self.recv.copy_(self.send)
-        elif dist.get_backend() == "nccl":
-            dist.all_gather_into_tensor(self.recv, self.send)
-        else:  # gloo (CPU tensors)
-            parts = list(self.recv.view(self.world, -1).unbind(0))
-            dist.all_gather(parts, self.send)
-        return self.recv
+            return None
+        if dist.get_backend() == "nccl":
+            return dist.all_gather_into_tensor(self.recv, self.send, async_op=async_op)
+        parts = list(self.recv.view(self.world, -1).unbind(0))  # gloo (CPU tensors)
+        dist.all_gather(parts, self.send)
+        return None
 
     def ranks(self) -> list[dict]:
         host = self.recv.view(self.world, -1).cpu().numpy()
