@@ -22,12 +22,12 @@ N_FRAMES = 4
 
 @functools.lru_cache(maxsize=8)
 def hip_run(seed: int = 0, batch: int = N_FRAMES, distorted: bool = False, n: int = N_FRAMES, cfg_items: tuple = (),
-            splits: int = 0):
+            splits: int = 0, width: int = 640, height: int = 400):
     import torch
 
     from thor_slam_amd._lib import Handle
 
-    sc = scenario(seed=seed, n=n, distorted=distorted, cfg_items=cfg_items)
+    sc = scenario(seed=seed, n=n, width=width, height=height, distorted=distorted, cfg_items=cfg_items)
     cfg = sc["cfg"]
     h = Handle([sc["rect"]], cfg, max_batch=batch, ransac_splits=splits)
     dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
@@ -167,6 +167,22 @@ def test_other_seeds_and_config():
     for i, rec in enumerate(per):
         o = sc["oracle"][i]
         _check_image_features(o["cur"]["left"], rec["kp"][0], sc["cfg"], f"frame {i} left")
+        np.testing.assert_array_equal(rec["stereo"], o["cur"]["stereo"])
+        np.testing.assert_array_equal(rec["temporal"], o["cur"]["temporal"])
+        if i:
+            assert rec["stats"][4] == o["best_hyp"] and rec["stats"][2] == o["n_inliers"]
+            assert rel_frobenius(rec["T_abs"], o["world_T_cam"]) < 1e-9
+
+
+def test_c4_size_bit_exact():
+    """Config C4 geometry (1280x800, K=4000: the level-0 quota exceeds the counting-sort capacity,
+    so select takes its bitonic path) stays bit-exact, with a distorted lens."""
+    items = (("n_features", 4000),)
+    sc, per = hip_run(seed=2, n=2, cfg_items=items, width=1280, height=800, distorted=True)
+    for i, rec in enumerate(per):
+        o = sc["oracle"][i]
+        _check_image_features(o["cur"]["left"], rec["kp"][0], sc["cfg"], f"frame {i} left")
+        _check_image_features(o["cur"]["right"], rec["kp"][1], sc["cfg"], f"frame {i} right")
         np.testing.assert_array_equal(rec["stereo"], o["cur"]["stereo"])
         np.testing.assert_array_equal(rec["temporal"], o["cur"]["temporal"])
         if i:

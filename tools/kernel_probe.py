@@ -22,6 +22,9 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--kernels", default="rectify_pyramid,detect,detect,detect,select,describe,describe")
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--height", type=int, default=400)
+    ap.add_argument("--features", type=int, default=2000)
     args = ap.parse_args()
     import torch
 
@@ -32,14 +35,18 @@ def main() -> None:
     from thor_slam_amd.params import HipSlamConfig
     from thor_slam_amd.synthetic import SyntheticStereoSource
 
-    src = SyntheticStereoSource(seed=0)
+    src = SyntheticStereoSource(seed=0, width=args.width, height=args.height)
     cams = extract_cameras(CameraRig([src]).calibration, 2)
     (li, ri), = stereo_pairs(cams)
     rect = stereo_rectify(cams[li], cams[ri])
     B = args.batch
-    frames = render_frames(0, 48, 8)[triangle_indices(2 * B, 48)]
+    if (args.width, args.height) == (640, 400):
+        uniq = render_frames(0, 48, 8)
+    else:
+        uniq = src.render_stereo_sequence(16)
+    frames = uniq[triangle_indices(2 * B, len(uniq))]
     dev = torch.from_numpy(frames).cuda()
-    h = Handle([rect], HipSlamConfig(), max_batch=B)
+    h = Handle([rect], HipSlamConfig(n_features=args.features), max_batch=B)
     stream = torch.cuda.current_stream()
     s = stream.cuda_stream
     h.submit(dev[:B].data_ptr(), B, s)
