@@ -18,6 +18,8 @@
  *   tslam_destroy       <- IsaacRosAdapter.shutdown            isaac_ros.py:444-450
  *   tslam_run_stage     stage-level entry points for parity tests (tslam_detect /
  *                          describe / match / pose); tslam_detect ... tslam_pose are aliases
+ *   tslam_ba_read       <- the map/keyframe side of cuVSLAM (SlamEngine.get_map, interface.py:207) —
+ *                          here: the A8 sliding keyframe window (poses, landmarks) of a pair
  *   tslam_pack_features keypoint+descriptor block for the multi-GPU all-gather
  *
  * Conventions: every function returns 0 on success or a negative TSLAM_E* code;
@@ -35,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 1
+#define TSLAM_ABI_VERSION 2
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -77,6 +79,14 @@ typedef struct {
     int32_t max_batch;            /* frames per tslam_submit                                  */
     int32_t n_pairs;              /* stereo pairs per frame (cameras = 2 * n_pairs)           */
     int32_t ransac_splits;        /* RANSAC blocks per frame (0 = auto); never changes results */
+    /* A8 local bundle adjustment (0 = off): keyframe window, frames between keyframes,
+     * Gauss-Newton steps per solve, Levenberg damping, initial outlier gate (px) */
+    int32_t ba_window;            /* keyframes in the sliding window (0 or 2..10)            */
+    int32_t ba_kf_interval;       /* frame g is a keyframe iff g % ba_kf_interval == 0        */
+    int32_t ba_iters;
+    int32_t ba_pad;               /* reserved, 0                                              */
+    double ba_lambda;
+    double ba_outlier_px;
 } tslam_params;
 
 /* Buffers exposed for parity tests (tslam_buffer_info / tslam_copy_out / tslam_copy_in). */
@@ -88,7 +98,7 @@ enum tslam_buffer {
     TSLAM_BUF_DESC = 4,      /* u32 [ring][cams][K][8]                                        */
     TSLAM_BUF_STEREO = 5,    /* i32 [ring][pairs][K]             right index or -1            */
     TSLAM_BUF_DISP = 6,      /* f64 [ring][pairs][K]             refined level-0 disparity/NaN */
-    TSLAM_BUF_TEMPORAL = 7,  /* i32 [batch][pairs][K]            left(t-1) index or -1        */
+    TSLAM_BUF_TEMPORAL = 7,  /* i32 [ring][pairs][K]             left(t-1) index or -1        */
     TSLAM_BUF_TEMPORAL_UV = 8, /* f64 [batch][pairs][K][2]       refined (u, v) at t / NaN    */
     TSLAM_BUF_CORR = 9,      /* f64 [batch][pairs][K][8]         X Y Z du dv bx by bz         */
     TSLAM_BUF_POSE = 10,     /* f64 [batch][pairs][68]           T_rel[16] T_abs[16] cov[36]  */
@@ -108,7 +118,8 @@ enum tslam_stage {
     TSLAM_STAGE_DESCRIBE = 2,/* keypoints -> orientation + descriptors                          */
     TSLAM_STAGE_MATCH = 3,   /* descriptors -> stereo/temporal matches + sub-pixel refinement   */
     TSLAM_STAGE_POSE = 4,    /* matches -> correspondences -> RANSAC -> refine -> chain         */
-    TSLAM_STAGE_ALL = 5,
+    TSLAM_STAGE_ALL = 5,     /* RECTIFY .. POSE, then BA when ba_window > 0                     */
+    TSLAM_STAGE_BA = 6,      /* A8: insert the batch's keyframes into each pair's window + solve */
     /* single kernels (per-kernel timing in bench.py; same order as STAGE_ALL) */
     TSLAM_KERNEL_RECTIFY_PYRAMID = 10,
     TSLAM_KERNEL_DETECT = 11,       /* includes the histogram memset */
@@ -166,6 +177,14 @@ int tslam_layout(tslam_handle* h, int64_t* out16, int32_t* level_info18);
 /* Copy the keypoints + descriptors + counts of the last batch into `dst` (device):
  * [n_frames][cams] blocks of (K*8 + K*32 + levels*4) bytes, then a pose trailer per
  * (frame, pair) of T_rel[16] + cov[36] f64 and stats[8] i32.  Returns the total in *bytes. */
+/* A8 window of stereo pair `pair` after the last enqueued solve (synchronises the device),
+ * indexed by slot (slot = keyframe number mod ba_window): frames[W] (global frame, -1 = empty),
+ * cam_T_world[W][16] (BA estimate), landmark[W][K] (id = home slot * K + keypoint, or -1),
+ * points[W*K][3] (world position by id), obs_uvd[3][W][K] (u, v, disparity; NaN = none),
+ * counts[4] (observations, landmarks, last solve ok, 0).  Any output pointer may be NULL. */
+int tslam_ba_read(tslam_handle* h, int pair, int64_t* frames, double* cam_T_world, int32_t* landmark,
+                  double* points, double* obs_uvd, int32_t* counts);
+
 int tslam_pack_features(tslam_handle* h, void* dst, int64_t* bytes, void* stream);
 
 #ifdef __cplusplus

@@ -1,0 +1,292 @@
+"""Row A8 of SURVEY.md §8a — sliding-window local bundle adjustment, CPU restatement.
+
+TEST INFRASTRUCTURE (see ``oracle/__init__.py``): the checker for the HIP back end's A8 kernels,
+never imported by the product.  cuVSLAM's BA is closed, so this file *is* the
+spec the kernels follow; parity against the reference is unpinned, like rows A2-A7.
+
+Spec (shared with ``thor-slam_amd/csrc/k_ba.hip``):
+
+* Keyframes: global frame g is a keyframe iff ``g % kf_interval == 0``; the window keeps the
+  newest ``window`` keyframes in ``window`` slots (slot = keyframe number mod window).
+* Observations of keyframe g: every valid keypoint k at its level-0 position
+  ``u = (x + 0.5) * 2^l - 0.5`` (same for v); its stereo disparity (refined, NaN when unmatched)
+  initialises new landmarks: ``Z = fx*B/d, X = (u-cx)Z/fx, Y = (v-cy)Z/fy`` in the camera,
+  mapped to the world with the keyframe's pose.
+* Association: ``link[k]`` = the keypoint of the previous keyframe reached by chaining the
+  per-frame temporal matches back over the frames in between (-1 when the chain breaks).  A
+  keypoint inherits its link's landmark; otherwise, with a finite disparity, it creates landmark
+  ``slot * K + k``; else it has none.
+* Eviction (a new keyframe reuses the oldest slot): every landmark homed in that slot moves to its
+  observation in the oldest remaining keyframe that sees it (new id ``slot' * K + k'``, position
+  copied, ids remapped in every keyframe); landmarks nobody else sees are dropped.
+* Solve (``iters`` Gauss-Newton steps with Levenberg damping ``lam``), camera 0 = oldest keyframe
+  held fixed (gauge):
+    - cameras are ``cam_T_world`` (R, t); residual ``r = pi(R X + t) - z`` with the stereo row
+      ``(fx (Xc - B) / Zc + cx) - (u - d)`` when the observation has a disparity (it fixes the scale
+      a monocular window would leave free), zero otherwise;
+    - ``J_c = dpi [I | -[Xc]x]`` (left update, translation first), ``J_p = dpi R``;
+    - observations with an initial reprojection error > ``outlier_px`` or a non-positive depth are
+      dropped; landmarks need >= 2 remaining observations;
+    - ``S = blockdiag(U_c + lam I) - sum_i sum_{o,o' in i} W_o V_i^-1 W_o'^T``,
+      ``b = -g_c + sum_i sum_{o in i} W_o V_i^-1 g_p,i`` with ``V_i = sum J_p^T J_p + lam I``;
+    - ``S' dc = b'`` without camera 0 (Cholesky), ``dp_i = V_i^-1 (-g_p,i - sum_o W_o^T dc_o)``;
+    - cameras ``R <- cayley(w) R, t <- cayley(w) t + rho``; points ``X += dp``.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from .numpy_slam import cayley, level0_coords
+
+
+@dataclass
+class BAParams:
+    window: int = 10
+    kf_interval: int = 5
+    iters: int = 5
+    lam: float = 1.0
+    outlier_px: float = 3.0
+
+
+def chain_links(temporal_maps: list[np.ndarray]) -> np.ndarray:
+    """Compose per-frame temporal maps (newest first: frame g, g-1, ...) into keypoint -> keypoint
+    of the frame before the last map (-1 where any step is unmatched)."""
+    idx = np.arange(temporal_maps[0].size)
+    out = idx.copy()
+    for tm in temporal_maps:
+        ok = out >= 0
+        out = np.where(ok, tm[np.where(ok, out, 0)], -1)
+    return out
+
+
+class KeyframeWindow:
+    """The keyframe slots, landmark table and solver of one stereo pair (restated spec)."""
+
+    def __init__(self, K: int, intr, params: BAParams):
+        self.K = K
+        self.fx, self.fy, self.cx, self.cy, self.fxb = intr
+        self.p = params
+        W = params.window
+        self.frame = np.full(W, -1, dtype=np.int64)       # global frame of each slot (-1 = empty)
+        self.T_cw = np.tile(np.eye(4), (W, 1, 1))
+        self.u = np.full((W, K), np.nan)
+        self.v = np.full((W, K), np.nan)
+        self.d = np.full((W, K), np.nan)
+        self.lm = np.full((W, K), -1, dtype=np.int64)
+        self.X = np.zeros((W * K, 3))
+        self.n_kf = 0
+
+    # -- window bookkeeping --------------------------------------------------------------------
+    def order(self) -> list[int]:
+        """Occupied slots, oldest keyframe first."""
+        occ = [s for s in range(self.p.window) if self.frame[s] >= 0]
+        return sorted(occ, key=lambda s: self.frame[s])
+
+    def _evict(self, slot: int) -> None:
+        K = self.K
+        lo, hi = slot * K, slot * K + K
+        rest = [s for s in self.order() if s != slot]
+        remap = np.full(K, -1, dtype=np.int64)
+        for s in rest:                       # oldest remaining keyframe first
+            lm = self.lm[s]
+            hit = (lm >= lo) & (lm < hi)
+            for k in np.nonzero(hit)[0]:
+                old = lm[k] - lo
+                if remap[old] < 0:
+                    remap[old] = s * K + k
+                    self.X[s * K + k] = self.X[lm[k]]
+        for s in rest:
+            lm = self.lm[s]
+            hit = (lm >= lo) & (lm < hi)
+            lm[hit] = remap[lm[hit] - lo]
+        self.lm[slot] = -1
+        self.frame[slot] = -1
+
+    def add_keyframe(self, g: int, T_cw: np.ndarray, u: np.ndarray, v: np.ndarray, disp: np.ndarray,
+                     link: np.ndarray | None) -> int:
+        """Insert keyframe g (u, v level-0 observations, NaN = invalid; disp refined, NaN = none;
+        link into the previous keyframe or None for the first)."""
+        K = self.K
+        slot = self.n_kf % self.p.window
+        prev = self.order()[-1] if self.n_kf else -1
+        if self.frame[slot] >= 0:
+            self._evict(slot)
+        self.frame[slot] = g
+        self.T_cw[slot] = T_cw
+        self.u[slot], self.v[slot] = u, v
+        self.d[slot] = np.where(np.isfinite(disp) & (disp > 0), disp, np.nan)
+        valid = np.isfinite(u)
+        lm = np.full(K, -1, dtype=np.int64)
+        if link is not None and prev >= 0:
+            has = valid & (link >= 0)
+            inh = np.where(has, self.lm[prev][np.where(has, link, 0)], -1)
+            lm = np.where(has, inh, -1)
+        new = valid & (lm < 0) & np.isfinite(disp) & (disp > 0)
+        ks = np.nonzero(new)[0]
+        lm[ks] = slot * K + ks
+        if ks.size:
+            z = self.fxb / disp[ks]
+            xc = np.stack([(u[ks] - self.cx) * z / self.fx, (v[ks] - self.cy) * z / self.fy, z], axis=1)
+            R, t = T_cw[:3, :3], T_cw[:3, 3]
+            self.X[slot * K + ks] = (xc - t) @ R       # R^T (xc - t)
+        self.lm[slot] = lm
+        self.n_kf += 1
+        return slot
+
+    # -- solve -----------------------------------------------------------------------------------
+    def observations(self):
+        """(camera index, landmark id, u, v, d) of every observation, cameras oldest first."""
+        cams, lms, us, vs, ds = [], [], [], [], []
+        for ci, s in enumerate(self.order()):
+            k = np.nonzero(self.lm[s] >= 0)[0]
+            cams.append(np.full(k.size, ci))
+            lms.append(self.lm[s][k])
+            us.append(self.u[s][k])
+            vs.append(self.v[s][k])
+            ds.append(self.d[s][k])
+        return (np.concatenate(cams), np.concatenate(lms), np.concatenate(us), np.concatenate(vs),
+                np.concatenate(ds))
+
+    def _project(self, R, t, X):
+        xc = np.einsum("nij,nj->ni", R, X) + t
+        return xc, self.fx * xc[:, 0] / xc[:, 2] + self.cx, self.fy * xc[:, 1] / xc[:, 2] + self.cy
+
+    def solve(self) -> dict:
+        p = self.p
+        slots = self.order()
+        n = len(slots)
+        if n < 2:
+            return {"n_obs": 0, "n_lm": 0}
+        cam, lm, uo, vo, do = self.observations()
+        T = self.T_cw[slots]
+        # outlier / depth gate at the initial estimate, then >= 2 observations per landmark
+        xc, pu, pv = self._project(T[cam, :3, :3], T[cam, :3, 3], self.X[lm])
+        keep = (xc[:, 2] > 0) & ((pu - uo) ** 2 + (pv - vo) ** 2 <= p.outlier_px * p.outlier_px)
+        cnt = np.bincount(lm[keep], minlength=self.X.shape[0])
+        keep &= cnt[lm] >= 2
+        cam, lm, uo, vo, do = cam[keep], lm[keep], uo[keep], vo[keep], do[keep]
+        st = np.isfinite(do)                           # observations with a stereo row
+        ur = np.where(st, uo - np.where(st, do, 0.0), 0.0)
+        base = self.fxb / self.fx
+        ids, li = np.unique(lm, return_inverse=True)   # compact landmark index per observation
+        L = ids.size
+        X = self.X[ids].copy()
+        Rs, ts = T[:, :3, :3].copy(), T[:, :3, 3].copy()
+        fx, fy = self.fx, self.fy
+        for _ in range(p.iters):
+            R = Rs[cam]
+            xc = np.einsum("nij,nj->ni", R, X[li]) + ts[cam]
+            iz = 1.0 / xc[:, 2]
+            r3 = np.where(st, fx * (xc[:, 0] - base) * iz + self.cx - ur, 0.0)
+            r = np.stack([fx * xc[:, 0] * iz + self.cx - uo, fy * xc[:, 1] * iz + self.cy - vo, r3], axis=1)
+            dpi = np.zeros((lm.size, 3, 3))
+            dpi[:, 0, 0] = fx * iz
+            dpi[:, 0, 2] = -fx * xc[:, 0] * iz * iz
+            dpi[:, 1, 1] = fy * iz
+            dpi[:, 1, 2] = -fy * xc[:, 1] * iz * iz
+            dpi[:, 2, 0] = np.where(st, fx * iz, 0.0)
+            dpi[:, 2, 2] = np.where(st, -fx * (xc[:, 0] - base) * iz * iz, 0.0)
+            skew = np.zeros((lm.size, 3, 3))
+            skew[:, 0, 1], skew[:, 0, 2] = -xc[:, 2], xc[:, 1]
+            skew[:, 1, 0], skew[:, 1, 2] = xc[:, 2], -xc[:, 0]
+            skew[:, 2, 0], skew[:, 2, 1] = -xc[:, 1], xc[:, 0]
+            Jc = np.concatenate([dpi, -np.einsum("nij,njk->nik", dpi, skew)], axis=2)   # n x 3 x 6
+            Jp = np.einsum("nij,njk->nik", dpi, R)                                        # n x 3 x 3
+            U = np.zeros((n, 6, 6))
+            gc = np.zeros((n, 6))
+            np.add.at(U, cam, np.einsum("nki,nkj->nij", Jc, Jc))
+            np.add.at(gc, cam, np.einsum("nki,nk->ni", Jc, r))
+            V = np.tile(np.eye(3) * p.lam, (L, 1, 1))
+            gp = np.zeros((L, 3))
+            np.add.at(V, li, np.einsum("nki,nkj->nij", Jp, Jp))
+            np.add.at(gp, li, np.einsum("nki,nk->ni", Jp, r))
+            Vinv = np.linalg.inv(V)
+            Wo = np.einsum("nki,nkj->nij", Jc, Jp)                                        # n x 6 x 3
+            S = np.zeros((6 * n, 6 * n))
+            for c in range(n):
+                S[6 * c:6 * c + 6, 6 * c:6 * c + 6] += U[c] + p.lam * np.eye(6)
+            b = -gc.reshape(-1).copy()
+            WV = np.einsum("nij,njk->nik", Wo, Vinv[li])                                   # W_o V_i^-1
+            np.add.at(b.reshape(n, 6), cam, np.einsum("nij,nj->ni", WV, gp[li]))
+            order = np.argsort(li, kind="stable")
+            starts = np.searchsorted(li[order], np.arange(L + 1))
+            for i in range(L):
+                obs = order[starts[i]:starts[i + 1]]
+                for a in obs:
+                    for bb in obs:
+                        ca, cb = cam[a], cam[bb]
+                        S[6 * ca:6 * ca + 6, 6 * cb:6 * cb + 6] -= WV[a] @ Wo[bb].T
+            dc = np.zeros(6 * n)
+            dc[6:] = np.linalg.solve(S[6:, 6:], b[6:])
+            dcc = dc.reshape(n, 6)
+            rhs = -gp.copy()
+            np.add.at(rhs, li, -np.einsum("nji,nj->ni", Wo, dcc[cam]))
+            dp = np.einsum("lij,lj->li", Vinv, rhs)
+            for c in range(1, n):
+                ru = cayley(dcc[c, 3:])
+                Rs[c] = ru @ Rs[c]
+                ts[c] = ru @ ts[c] + dcc[c, :3]
+            X = X + dp
+        for c, s in enumerate(slots):
+            self.T_cw[s, :3, :3], self.T_cw[s, :3, 3] = Rs[c], ts[c]
+        self.X[ids] = X
+        xc, pu, pv = self._project(Rs[cam], ts[cam], X[li])
+        rms = float(np.sqrt(np.mean((pu - uo) ** 2 + (pv - vo) ** 2))) if lm.size else 0.0
+        return {"n_obs": int(lm.size), "n_lm": int(L), "rms_px": rms}
+
+
+def keyframe_observations(left: dict, K: int):
+    """Level-0 (u, v) of every valid keypoint of one image (NaN for padding slots)."""
+    kp = left["kp"]
+    u, v = level0_coords(kp["x"], kp["y"], kp["level"])
+    u = np.where(left["valid"], u, np.nan)
+    v = np.where(left["valid"], v, np.nan)
+    return u[:K].astype(np.float64), v[:K].astype(np.float64)
+
+
+def _inv_rigid(T: np.ndarray) -> np.ndarray:
+    out = np.eye(4)
+    out[:3, :3] = T[:3, :3].T
+    out[:3, 3] = -(T[:3, :3].T @ T[:3, 3])
+    return out
+
+
+class BATracker:
+    """Drives one pair's ``KeyframeWindow`` from ``OracleTracker.step`` results (in frame order).
+
+    Keyframe g's initial pose composes the previous keyframe's BA estimate with the front end's
+    motion since then: ``world_T_cam = W_ba(prev) inv(W_fe(prev)) W_fe(g)`` (front end = the
+    tracking chain, ``res['world_T_cam']``), so a BA correction carries forward."""
+
+    def __init__(self, K: int, intr, params: BAParams):
+        self.win = KeyframeWindow(K, intr, params)
+        self.K = K
+        self.p = params
+        self.Tfe = np.tile(np.eye(4), (params.window, 1, 1))
+        self.temporal: list[np.ndarray] = []   # newest first, the last kf_interval frames
+        self.last_solve: dict | None = None
+
+    def step(self, res: dict) -> dict | None:
+        g = int(res["frame"])
+        cur = res["cur"]
+        self.temporal.insert(0, np.asarray(cur["temporal"], dtype=np.int64))
+        del self.temporal[self.p.kf_interval:]
+        if g % self.p.kf_interval:
+            return None
+        w = self.win
+        W_fe = res["world_T_cam"]
+        if w.n_kf == 0:
+            T_wc = W_fe.copy()
+            link = None
+        else:
+            prev = w.order()[-1]
+            T_wc = _inv_rigid(w.T_cw[prev]) @ _inv_rigid(self.Tfe[prev]) @ W_fe
+            link = chain_links(self.temporal[: self.p.kf_interval])
+        u, v = keyframe_observations(cur["left"], self.K)
+        slot = w.add_keyframe(g, _inv_rigid(T_wc), u, v, np.asarray(cur["disp"], dtype=np.float64), link)
+        self.Tfe[slot] = W_fe
+        self.last_solve = w.solve()
+        return self.last_solve

@@ -45,7 +45,7 @@ def hip_run(seed: int = 0, batch: int = N_FRAMES, distorted: bool = False, n: in
                 "kp": [h.keypoints(g, 0), h.keypoints(g, 1)],
                 "stereo": h.frame_block("stereo", slot, np.int32)[:K],
                 "disp": h.frame_block("disp", slot, np.float64)[:K],
-                "temporal": h.frame_block("temporal", f, np.int32)[:K],
+                "temporal": h.frame_block("temporal", slot, np.int32)[:K],
                 "tuv": h.frame_block("temporal_uv", f, np.float64)[: 2 * K].reshape(K, 2),
                 "corr": h.frame_block("corr", f, np.float64)[: 8 * K].reshape(K, 8),
                 "T_rel": res["T_rel"][f, 0], "T_abs": res["T_abs"][f, 0], "cov": res["cov"][f, 0],

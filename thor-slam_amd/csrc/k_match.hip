@@ -320,7 +320,7 @@ __global__ __launch_bounds__(256) void k_refine_temporal(BatchCtx c) {
         qxy = rec.x;
         if (rec.w && g > 0) j = match_valid(c, mbase, qi);
     }
-    int32_t* out_idx = c.temporal + ((size_t)f * c.P + p) * K;
+    int32_t* out_idx = c.temporal + ((size_t)slot * c.P + p) * K;
     double* out_uv = c.tuv + (((size_t)f * c.P + p) * K + qi) * 2;
     const double nanv = __builtin_nan("");
     if (live && hl == 0) out_idx[qi] = j;

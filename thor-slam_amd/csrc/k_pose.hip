@@ -234,7 +234,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_corr(BatchCtx c) {
     const PairCalib cal = c.calib[p];
     const double fx = cal.fx, fy = cal.fy, cx = cal.cx, cy = cal.cy;
     const int pslot = ring_slot(c, g - 1);
-    const int32_t* tm = c.temporal + ((size_t)f * c.P + p) * K;
+    const int32_t* tm = c.temporal + ((size_t)ring_slot(c, g) * c.P + p) * K;
     const double* tuv = c.tuv + ((size_t)f * c.P + p) * K * 2;
     const double* dprev = c.disp + ((size_t)pslot * c.P + p) * K;
     const uint32_t* kprev = c.kps + ((size_t)pslot * c.C + 2 * p) * K * 2;

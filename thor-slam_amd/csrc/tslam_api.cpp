@@ -5,6 +5,7 @@
 // a batch can be captured into a hipGraph by the caller.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -12,6 +13,7 @@
 #include <vector>
 
 #include "../../include/tslam.h"
+#include "tslam_ba.h"
 #include "tslam_common.h"
 #include "tslam_describe.h"
 #include "tslam_tables.h"
@@ -62,6 +64,11 @@ struct tslam_handle {
     bool in_batch = false;
     hipStream_t last_stream = nullptr;
     std::vector<void*> allocs;
+    // A8 keyframe window (slots shared by all pairs: keyframes are whole frames)
+    BaStore ba{};
+    int64_t ba_frame[TS_BA_MAXW]{};
+    int64_t ba_nkf = 0;
+    int64_t ba_last = -1;    // newest frame inserted
 };
 
 static int dev_alloc(tslam_handle* h, void** p, size_t bytes) {
@@ -122,6 +129,84 @@ static void build_geometry(tslam_handle* h) {
         ro += g.H[l] + 1;
     }
     g.rs_total = (ro + 7) & ~7;
+}
+
+static int alloc_ba(tslam_handle* h) {
+    const size_t W = h->prm.ba_window, K = h->g.K, P = h->P, WK = W * K;
+    BaStore& b = h->ba;
+    struct A {
+        void** p;
+        size_t bytes;
+    } list[] = {
+        {(void**)&b.T, 8 * P * W * 16},      {(void**)&b.Tfe, 8 * P * W * 16},   {(void**)&b.u, 8 * P * WK},
+        {(void**)&b.v, 8 * P * WK},          {(void**)&b.d, 8 * P * WK},         {(void**)&b.lm, 4 * P * WK},
+        {(void**)&b.X, 8 * P * WK * 3},      {(void**)&b.remap, 4 * K},          {(void**)&b.cnt, 4 * WK},
+        {(void**)&b.li, 4 * WK},             {(void**)&b.lm_id, 4 * WK},         {(void**)&b.lm_off, 4 * (WK + 1)},
+        {(void**)&b.fill, 4 * WK},           {(void**)&b.lm_obs, 4 * WK},        {(void**)&b.obs_cam, 4 * WK},
+        {(void**)&b.obs_k, 4 * WK},          {(void**)&b.obs_id, 4 * WK},        {(void**)&b.cam_off, 4 * (W + 1)},
+        {(void**)&b.counts, 4 * 4 * P},      {(void**)&b.obs_W, 8 * WK * 18},    {(void**)&b.obs_Ug, 8 * WK * 27},
+        {(void**)&b.lm_L, 8 * WK * 9},       {(void**)&b.lm_gp, 8 * WK * 3},     {(void**)&b.Qt, 8 * (3 * WK + 4) * 64},
+        {(void**)&b.part, 8 * (size_t)TS_BA_SPLIT * 64 * 64}, {(void**)&b.cam_U, 8 * W * 27}, {(void**)&b.dc, 8 * W * 6},
+    };
+    for (const A& a : list) {
+        const int rc = dev_alloc(h, a.p, a.bytes);
+        if (rc != TSLAM_OK) return rc;
+    }
+    return TSLAM_OK;
+}
+
+static BaArgs ba_args(tslam_handle* h) {
+    BaArgs a{};
+    a.st = h->ba;
+    a.W = h->prm.ba_window;
+    a.interval = h->prm.ba_kf_interval;
+    a.iters = h->prm.ba_iters;
+    a.nsplit = TS_BA_SPLIT;
+    a.lam = h->prm.ba_lambda;
+    a.outlier_px = h->prm.ba_outlier_px;
+    a.prev = -1;
+    return a;
+}
+
+// Occupied slots, oldest keyframe first, without `skip`.
+static int ba_order(const tslam_handle* h, int skip, int* out) {
+    int n = 0;
+    for (int s = 0; s < h->prm.ba_window; ++s)
+        if (h->ba_frame[s] >= 0 && s != skip) out[n++] = s;
+    std::sort(out, out + n, [h](int a, int b) { return h->ba_frame[a] < h->ba_frame[b]; });
+    return n;
+}
+
+static BatchCtx make_ctx(tslam_handle* h);
+
+// A8: every keyframe of the current batch (g % ba_kf_interval == 0) enters each pair's window,
+// evicting the oldest when the window is full, and the window is solved.  Host bookkeeping of
+// the slots only; nothing synchronises.
+static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s) {
+    const int W = h->prm.ba_window, iv = h->prm.ba_kf_interval;
+    for (int64_t g = c.g0; g < c.g0 + c.n; ++g) {
+        if (g % iv != 0 || g <= h->ba_last) continue;
+        BaArgs a = ba_args(h);
+        a.frame = g;
+        a.slot = (int)(h->ba_nkf % W);
+        int ord[TS_BA_MAXW];
+        const int nocc = ba_order(h, -1, ord);
+        a.prev = nocc ? ord[nocc - 1] : -1;
+        const bool evict = h->ba_frame[a.slot] >= 0;
+        if (evict) a.n_order = ba_order(h, a.slot, a.order);
+        for (int p = 0; p < h->P; ++p) {
+            a.pair = p;
+            launch_ba_keyframe(c, a, evict, s);
+        }
+        h->ba_frame[a.slot] = g;
+        h->ba_nkf += 1;
+        h->ba_last = g;
+        a.n_order = ba_order(h, -1, a.order);
+        for (int p = 0; p < h->P; ++p) {
+            a.pair = p;
+            launch_ba_solve(c, a, s);
+        }
+    }
 }
 
 static BatchCtx make_ctx(tslam_handle* h) {
@@ -197,6 +282,10 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     if (p.fast_threshold < 0 || p.fast_threshold > 254) return fail(TSLAM_EINVAL, "fast_threshold must be in [0, 254]");
     if (p.max_batch < 1) return fail(TSLAM_EINVAL, "max_batch must be >= 1");
     if (p.max_hamming < 0 || p.max_hamming > 253) return fail(TSLAM_EINVAL, "max_hamming must be in [0, 253]");
+    if (!(p.ba_window == 0 || (p.ba_window >= 2 && p.ba_window <= TS_BA_MAXW)))
+        return fail(TSLAM_EINVAL, "ba_window must be 0 (off) or in [2, 10]");
+    if (p.ba_window && (p.ba_kf_interval < 1 || p.ba_iters < 1 || !(p.ba_lambda >= 0.0) || !(p.ba_outlier_px > 0.0)))
+        return fail(TSLAM_EINVAL, "ba_kf_interval, ba_iters >= 1, ba_lambda >= 0, ba_outlier_px > 0");
     if (p.refine_iters < 1) return fail(TSLAM_EINVAL, "refine_iters must be >= 1");
     if (p.ransac_splits < 0 || p.ransac_splits > TS_MAX_SPLITS) return fail(TSLAM_EINVAL, "ransac_splits must be in [0, 32]");
     const int W = pairs[0].width, H = pairs[0].height;
@@ -220,7 +309,10 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     h->P = p.n_pairs;
     h->C = 2 * p.n_pairs;
     h->B = p.max_batch;
+    // the ring keeps frame t-1 of a batch's first frame; with BA it also keeps the frames a
+    // keyframe's temporal match chain walks back over
     h->R = 2 * p.max_batch;
+    if (p.ba_window) h->R = std::max(h->R, p.ba_kf_interval + 1);
     build_geometry(h);
     for (int i = 0; i < h->P; ++i) {
         h->calib[i].fx = pairs[i].fx;
@@ -243,7 +335,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
         {TSLAM_BUF_DESC, R, C * K * 8 * 4},
         {TSLAM_BUF_STEREO, R, P * K * 4},
         {TSLAM_BUF_DISP, R, P * K * 8},
-        {TSLAM_BUF_TEMPORAL, B, P * K * 4},
+        {TSLAM_BUF_TEMPORAL, R, P * K * 4},
         {TSLAM_BUF_TEMPORAL_UV, B, P * K * 2 * 8},
         {TSLAM_BUF_CORR, B, P * K * TS_CORR_DOUBLES * 8},
         {TSLAM_BUF_POSE, B, P * TS_POSE_DOUBLES * 8},
@@ -270,6 +362,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_brief, sizeof(TSLAM_BRIEF_TABLE));
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_wedges, sizeof(TSLAM_WEDGES));
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_maps, sizeof(int32_t) * (size_t)C * W * H * 2);
+    if (rc == TSLAM_OK && p.ba_window) rc = alloc_ba(h);
     if (rc != TSLAM_OK) {
         free_all(h);
         delete h;
@@ -328,6 +421,9 @@ int tslam_reset(tslam_handle* h) {
         for (int k = 0; k < 4; ++k) eye[(size_t)p * 16 + 5 * k] = 1.0;
     HIPCHK(hipMemcpy(h->d_state, eye.data(), sizeof(double) * eye.size(), hipMemcpyHostToDevice));
     h->frames_done = 0;
+    for (int i = 0; i < TS_BA_MAXW; ++i) h->ba_frame[i] = -1;
+    h->ba_nkf = 0;
+    h->ba_last = -1;
     h->in_batch = false;
     h->cur_n = 0;
     return TSLAM_OK;
@@ -377,6 +473,11 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
             launch_match_refine(c, s);
             launch_pose(c, s);
             launch_chain(c, s);
+            if (h->prm.ba_window) run_ba(h, c, s);
+            break;
+        case TSLAM_STAGE_BA:
+            if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
+            run_ba(h, c, s);
             break;
         case TSLAM_KERNEL_RECTIFY_PYRAMID: launch_rectify_pyramid(c, s); break;
         case TSLAM_KERNEL_DETECT: launch_detect(c, s); break;
@@ -499,6 +600,28 @@ int tslam_pack_features(tslam_handle* h, void* dst, int64_t* bytes, void* stream
     const BatchCtx c = make_ctx(h);
     launch_pack(c, (uint8_t*)dst, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
+    return TSLAM_OK;
+}
+
+int tslam_ba_read(tslam_handle* h, int pair, int64_t* frames, double* cam_T_world, int32_t* landmark,
+                  double* points, double* obs_uvd, int32_t* counts) {
+    if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
+    if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
+    int rc = tslam_sync(h);
+    if (rc != TSLAM_OK) return rc;
+    const size_t W = h->prm.ba_window, K = h->g.K, WK = W * K;
+    const BaStore& b = h->ba;
+    if (frames)
+        for (size_t s = 0; s < W; ++s) frames[s] = h->ba_frame[s];
+    if (cam_T_world) HIPCHK(hipMemcpy(cam_T_world, b.T + pair * W * 16, 8 * W * 16, hipMemcpyDeviceToHost));
+    if (landmark) HIPCHK(hipMemcpy(landmark, b.lm + pair * WK, 4 * WK, hipMemcpyDeviceToHost));
+    if (points) HIPCHK(hipMemcpy(points, b.X + pair * WK * 3, 8 * WK * 3, hipMemcpyDeviceToHost));
+    if (obs_uvd) {
+        HIPCHK(hipMemcpy(obs_uvd, b.u + pair * WK, 8 * WK, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(obs_uvd + WK, b.v + pair * WK, 8 * WK, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(obs_uvd + 2 * WK, b.d + pair * WK, 8 * WK, hipMemcpyDeviceToHost));
+    }
+    if (counts) HIPCHK(hipMemcpy(counts, b.counts + 4 * pair, 4 * 4, hipMemcpyDeviceToHost));
     return TSLAM_OK;
 }
 

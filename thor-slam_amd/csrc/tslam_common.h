@@ -16,7 +16,7 @@
 //   rowstart u16 [R][C][sum(H_l+1)]  per level: first y-sorted position of row y
 //   qbest/qsecond/tbest u32 [B][P][2][K]   matching scratch (mode 0 stereo, 1 temporal)
 //   stereo   i32 [R][P][K]  disp f64 [R][P][K]        stereo match + refined disparity of left kps
-//   temporal i32 [B][P][K]  tuv  f64 [B][P][K][2]     temporal match + refined (u, v) at t
+//   temporal i32 [R][P][K]  tuv  f64 [B][P][K][2]     temporal match + refined (u, v) at t
 //   corr     f64 [B][P][K][8]        X Y Z du dv bx by bz (ordered by t keypoint index)
 //   pose     f64 [B][P][68]          T_rel, T_abs, cov;  stats i32 [B][P][8];  state f64 [P][16]
 #pragma once
@@ -37,6 +37,7 @@
 #define TS_MAX_HYP 1024
 #define TS_MAX_SPLITS 32   // RANSAC blocks per frame
 #define TS_RANSAC_WORDS 26 // per split: key + pad + 12 doubles
+#define TS_BA_MAXW 10      // keyframes per BA window (6 camera rows each in the 64-wide system)
 
 struct LevelGeom {
     int n_levels;

@@ -24,7 +24,7 @@ BUF = {
     "temporal": 7, "temporal_uv": 8, "corr": 9, "pose": 10, "stats": 11, "qbest": 12,
     "qsecond": 13, "tbest": 14, "ysorted": 15, "rowstart": 16, "desc_ys": 17,
 }
-STAGE = {"rectify": 0, "detect": 1, "describe": 2, "match": 3, "pose": 4, "all": 5}
+STAGE = {"rectify": 0, "detect": 1, "describe": 2, "match": 3, "pose": 4, "all": 5, "ba": 6}
 # single kernels, in pipeline order (bench.py times each with HIP events)
 KERNELS = {
     "rectify_pyramid": 10, "detect": 11, "select": 12, "describe": 13,
@@ -50,6 +50,8 @@ class Params(ctypes.Structure):
         ("ransac_hypotheses", ctypes.c_int32), ("refine_iters", ctypes.c_int32), ("min_inliers", ctypes.c_int32),
         ("ransac_thr_px", ctypes.c_double), ("ransac_seed", ctypes.c_uint64),
         ("max_batch", ctypes.c_int32), ("n_pairs", ctypes.c_int32), ("ransac_splits", ctypes.c_int32),
+        ("ba_window", ctypes.c_int32), ("ba_kf_interval", ctypes.c_int32), ("ba_iters", ctypes.c_int32),
+        ("ba_pad", ctypes.c_int32), ("ba_lambda", ctypes.c_double), ("ba_outlier_px", ctypes.c_double),
     ]
 
 
@@ -80,6 +82,7 @@ _SIGNATURES = {
     "tslam_ring_slot": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "tslam_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_pack_features": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
+    "tslam_ba_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6),
 }
 
 
@@ -132,7 +135,8 @@ def make_params(cfg: HipSlamConfig, max_batch: int, n_pairs: int, ransac_splits:
         cfg.n_features, cfg.n_levels, cfg.fast_threshold, cfg.edge_margin, cfg.max_hamming, cfg.ratio_pct,
         cfg.stereo_row_tol, cfg.max_disparity, cfg.temporal_window, cfg.ransac_hypotheses, cfg.refine_iters,
         cfg.min_inliers, float(cfg.ransac_thr_px), int(cfg.ransac_seed) & ((1 << 64) - 1), int(max_batch), int(n_pairs),
-        int(ransac_splits),
+        int(ransac_splits), int(cfg.ba_window), int(cfg.ba_kf_interval), int(cfg.ba_iters), 0, float(cfg.ba_lambda),
+        float(cfg.ba_outlier_px),
     )
 
 
@@ -252,6 +256,20 @@ class Handle:
         nb = ctypes.c_int64()
         _check(self.lib.tslam_pack_features(self.h, ctypes.c_void_p(dst_dev_ptr), ctypes.byref(nb), ctypes.c_void_p(stream)))
         return int(nb.value)
+
+    def ba_read(self, pair: int = 0) -> dict:
+        """A8 keyframe window of one pair (synchronises): slot-indexed frames, cam_T_world,
+        landmark ids, landmark positions (by id), observations and the last solve's counts."""
+        W, K = self.cfg.ba_window, self.K
+        frames = np.zeros(W, dtype=np.int64)
+        T = np.zeros((W, 4, 4))
+        lm = np.zeros((W, K), dtype=np.int32)
+        X = np.zeros((W * K, 3))
+        uvd = np.zeros((3, W, K))
+        cnt = np.zeros(4, dtype=np.int32)
+        _check(self.lib.tslam_ba_read(self.h, int(pair), *(a.ctypes.data for a in (frames, T, lm, X, uvd, cnt))))
+        return {"frames": frames, "T_cw": T, "lm": lm.astype(np.int64), "X": X, "u": uvd[0], "v": uvd[1],
+                "d": uvd[2], "n_obs": int(cnt[0]), "n_lm": int(cnt[1]), "ok": bool(cnt[2])}
 
     # -- decoding helpers (tests / map export) ---------------------------------------------
     def keypoints(self, global_frame: int, cam: int) -> dict:

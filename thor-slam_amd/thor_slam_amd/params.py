@@ -39,6 +39,12 @@ class HipSlamConfig(SlamConfig):
     ransac_seed: int = 0x5EED
     refine_iters: int = 8           # Gauss-Newton iterations on inliers
     min_inliers: int = 12           # fewer -> frame is LOST
+    # A8 local bundle adjustment (config C4); ba_window = 0 disables it
+    ba_window: int = 0              # keyframes in the sliding window
+    ba_kf_interval: int = 5         # frame g is a keyframe iff g % ba_kf_interval == 0
+    ba_iters: int = 5               # Gauss-Newton steps per window solve
+    ba_lambda: float = 1.0          # Levenberg damping (px^2 units)
+    ba_outlier_px: float = 3.0      # observations farther than this at the start are dropped
     # pipeline
     batch_size: int = 1             # frames per submission (1 = synchronous latency mode)
 
@@ -55,6 +61,10 @@ class HipSlamConfig(SlamConfig):
             raise ValueError("fast_threshold must be in [0, 254]")
         if self.batch_size < 1:
             raise ValueError("batch_size must be >= 1")
+        if not (self.ba_window == 0 or 2 <= self.ba_window <= 10):
+            raise ValueError("ba_window must be 0 (off) or in [2, 10]")
+        if self.ba_kf_interval < 1 or self.ba_iters < 1:
+            raise ValueError("ba_kf_interval and ba_iters must be >= 1")
         if not 0 <= self.max_hamming <= 253:
             raise ValueError("max_hamming must be in [0, 253] (the mutual check keeps distances as bytes)")
 
