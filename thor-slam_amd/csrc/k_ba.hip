@@ -4,19 +4,25 @@
 // landmark homes slot*K + k with re-homing on eviction, stereo reprojection residuals, Schur
 // complement on the cameras, Gauss-Newton with Levenberg damping, gauge = oldest keyframe).
 //
-// Per window solve and iteration:
-//   k_ba_lin     one thread per landmark: Jacobians of its (<= window) observations, V_i, g_p,i,
-//                the Cholesky factor L_i of V_i, and the landmark's Schur columns
-//                Q_i = [W_o L_i^-T] (camera rows) with y_i = L_i^-1 g_p,i appended as row 60;
-//   k_ba_camred  one block per camera: U_c = sum J_c^T J_c, g_c = sum J_c^T r (fixed order);
-//   k_ba_gemm    the dense part of the Schur complement, C = Qe Qe^T over all 3L landmark columns,
-//                on the FP64 matrix cores (v_mfma_f64_16x16x4f64), split over blocks in K;
-//                C[0:60,0:60] = sum_i W V^-1 W^T and C[0:60, 60] = sum_i W V^-1 g_p;
-//   k_ba_solve   one block: fixed-order sum of the split partials, S = blockdiag(U + lam) - C,
-//                b = -g_c + C[:,60], camera 0 removed, Cholesky, camera updates (Cayley);
-//   k_ba_backsub one thread per landmark: dp = V^-1 (-g_p - sum W_o^T dc), X += dp.
+// Per window solve: k_ba_gate gates the observations at the current estimate and counts them per
+// landmark; a tiled scan (k_ba_tilecount / tilescan / tilescatter) keeps landmarks seen >= 2 times,
+// ranks them (compact index) and builds the observation list; k_ba_camobs the camera x landmark
+// table of observation indices.
+// Then per Gauss-Newton iteration:
+//   k_ba_jac     one thread per observation: J_c, J_p, r -> W_o = J_c^T J_p, J_c^T J_c | J_c^T r,
+//                J_p^T J_p | J_p^T r;
+//   k_ba_camred  one wave per (camera, element): U_c = sum J_c^T J_c, g_c = sum J_c^T r;
+//   k_ba_schur   per chunk of 32 landmarks: V_i = sum J_p^T J_p + lam I, g_p,i, L_i = chol(V_i),
+//                y_i = L_i^-1 g_p,i; the chunk's Schur columns Q_i = [W_o L_i^-T] (rows of the
+//                observing camera) with y_i in row 60 in an LDS tile; C += Q^T Q on the FP64
+//                matrix cores (v_mfma_f64_16x16x4f64).  C[0:60,0:60] = sum_i W V^-1 W^T and
+//                C[0:60, 60] = sum_i W V^-1 g_p; blocks stride the chunks (split-K partials);
+//   k_ba_reduce  fixed-order sum of the split partials;
+//   k_ba_solve   one block: S = blockdiag(U + lam) - C, b = -g_c + C[:,60] without camera 0,
+//                LDL^T elimination + back substitution, camera updates (Cayley);
+//   k_ba_backsub 16 lanes per landmark: dp = V^-1 (-g_p - sum W_o^T dc), X += dp.
 // Every reduction has a fixed order, so a solve is deterministic run to run.  Floating-point
-// results differ from the oracle's (LU solves, numpy summation order) at the 1e-12 level.
+// results differ from the oracle's (LU solves, numpy summation order) at the 1e-14 level.
 #include "tslam_ba.h"
 
 // ---------------------------------------------------------------------------------------------
@@ -51,34 +57,38 @@ __device__ __forceinline__ bool kp_obs(const BatchCtx& c, int slot, int cam, int
 // ---------------------------------------------------------------------------------------------
 // keyframe insertion (after the batch that contains frame g) and eviction
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_ba_evict(BatchCtx c, BaArgs a) {
+// Eviction of slot a.slot: each landmark homed there moves to its observation in the oldest
+// remaining keyframe (a.order, oldest first).  Pass 1 takes the minimum (rank, keypoint) key per
+// landmark (remap pre-filled with a large value), pass 2 rewrites the ids and copies the position.
+__global__ __launch_bounds__(256) void k_ba_evict_min(BatchCtx c, BaArgs a) {
     const int K = c.g.K;
     BaPair q = ba_pair(c, a, a.pair);
-    const int lo = a.slot * K;
-    for (int k = threadIdx.x; k < K; k += blockDim.x) q.remap[k] = -1;
-    __syncthreads();
-    for (int r = 0; r < a.n_order; ++r) {          // remaining keyframes, oldest first
-        const int s = a.order[r];
-        for (int k = threadIdx.x; k < K; k += blockDim.x) {
-            const int id = q.lm[(size_t)s * K + k];
-            if (id >= lo && id < lo + K && q.remap[id - lo] < 0) {   // ids are unique per keyframe
-                q.remap[id - lo] = s * K + k;
-                for (int e = 0; e < 3; ++e) q.X[(size_t)(s * K + k) * 3 + e] = q.X[(size_t)id * 3 + e];
-            }
-        }
-        __syncthreads();
-    }
-    for (int r = 0; r < a.n_order; ++r) {
-        const int s = a.order[r];
-        for (int k = threadIdx.x; k < K; k += blockDim.x) {
-            const int id = q.lm[(size_t)s * K + k];
-            if (id >= lo && id < lo + K) q.lm[(size_t)s * K + k] = q.remap[id - lo];
-        }
-    }
-    for (int k = threadIdx.x; k < K; k += blockDim.x) q.lm[(size_t)a.slot * K + k] = -1;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n_order * K) return;
+    const int r = i / K, k = i - r * K;
+    const int id = q.lm[(size_t)a.order[r] * K + k], lo = a.slot * K;
+    if (id >= lo && id < lo + K) atomicMin(&q.remap[id - lo], i);
 }
 
-__global__ __launch_bounds__(1024) void k_ba_insert(BatchCtx c, BaArgs a) {
+__global__ __launch_bounds__(256) void k_ba_evict_move(BatchCtx c, BaArgs a) {
+    const int K = c.g.K;
+    BaPair q = ba_pair(c, a, a.pair);
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n_order * K) return;
+    const int r = i / K, k = i - r * K;
+    const size_t o = (size_t)a.order[r] * K + k;
+    const int id = q.lm[o], lo = a.slot * K;
+    if (id < lo || id >= lo + K) return;
+    const int key = q.remap[id - lo];
+    const int hr = key / K;
+    const int nid = a.order[hr] * K + (key - hr * K);
+    q.lm[o] = nid;
+    if (key == i)   // the new home copies the position (sources lie in the evicted slot's range)
+        for (int e = 0; e < 3; ++e) q.X[(size_t)nid * 3 + e] = q.X[(size_t)id * 3 + e];
+}
+
+// Insertion of frame a.frame into slot a.slot (every block derives the pose; block 0 stores it).
+__global__ __launch_bounds__(256) void k_ba_insert(BatchCtx c, BaArgs a) {
     __shared__ double s_T[16];   // new keyframe's cam_T_world
     const int K = c.g.K, p = a.pair;
     BaPair q = ba_pair(c, a, p);
@@ -98,18 +108,19 @@ __global__ __launch_bounds__(1024) void k_ba_insert(BatchCtx c, BaArgs a) {
             mul4(Wba, ifp, tmp);
             mul4(tmp, Tfe, Twc);
         }
-        for (int e = 0; e < 16; ++e) q.Tfe[(size_t)a.slot * 16 + e] = Tfe[e];
         double Tcw[16];
         inv_rigid(Twc, Tcw);
-        for (int e = 0; e < 16; ++e) {
-            s_T[e] = Tcw[e];
-            q.T[(size_t)a.slot * 16 + e] = Tcw[e];
-        }
+        for (int e = 0; e < 16; ++e) s_T[e] = Tcw[e];
+        if (blockIdx.x == 0)
+            for (int e = 0; e < 16; ++e) {
+                q.Tfe[(size_t)a.slot * 16 + e] = Tfe[e];
+                q.T[(size_t)a.slot * 16 + e] = Tcw[e];
+            }
     }
     __syncthreads();
     const PairCalib cal = c.calib[p];
     const double* disp = c.disp + ((size_t)rslot * c.P + p) * K;
-    for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x) {
         double u = __builtin_nan(""), v = __builtin_nan("");
         const bool valid = kp_obs(c, rslot, 2 * p, k, &u, &v);
         const double dd = disp[k];
@@ -137,11 +148,13 @@ __global__ __launch_bounds__(1024) void k_ba_insert(BatchCtx c, BaArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// observation set of a solve (one block): gate at the initial estimate, >= 2 observations per
-// landmark, compact landmark index (sorted ids), landmark -> observations CSR, camera ranges
+// observation set of a solve (one block): gate at the current estimate, >= 2 observations per
+// landmark, compact landmark index (= rank of the id), camera x landmark observation table
 // ---------------------------------------------------------------------------------------------
+#define BA_SCAN_ITEMS 8
+
+// Exclusive scan of one int per thread over the block; *total = block sum.
 __device__ int block_scan_excl(int v, int* s_tmp, int* total) {
-    // exclusive scan of one int per thread over the block (1024 threads)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int x = v;
 #pragma unroll
@@ -167,129 +180,156 @@ __device__ int block_scan_excl(int v, int* s_tmp, int* total) {
     return r;
 }
 
-__global__ __launch_bounds__(1024) void k_ba_gather(BatchCtx c, BaArgs a) {
-    __shared__ int s_tmp[32];
+// Gate every observation of the window at the current estimate (positive depth, reprojection
+// error <= outlier_px); count the gated observations per landmark (cnt pre-zeroed).
+__global__ __launch_bounds__(256) void k_ba_gate(BatchCtx c, BaArgs a) {
     __shared__ double s_T[TS_BA_MAXW][12];
-    const int K = c.g.K, p = a.pair;
+    const int K = c.g.K, p = a.pair, n = a.n_order;
     BaPair q = ba_pair(c, a, p);
+    for (int i = threadIdx.x; i < n * 12; i += blockDim.x) s_T[i / 12][i % 12] = q.T[(size_t)a.order[i / 12] * 16 + i % 12];
+    __syncthreads();
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * K) return;
     const PairCalib cal = c.calib[p];
-    const int NID = a.W * K;
-    for (int i = threadIdx.x; i < NID; i += blockDim.x) q.cnt[i] = 0;
-    for (int i = threadIdx.x; i < a.n_order * 12; i += blockDim.x) {
-        const int ci = i / 12, e = i % 12;
-        s_T[ci][e] = q.T[(size_t)a.order[ci] * 16 + e];
-    }
-    __syncthreads();
     const double lim = a.outlier_px * a.outlier_px;
-    // pass 1: gated candidates in (camera, keypoint) order -> obs arrays, counts per landmark
-    int n1 = 0;
-    const int total1 = a.n_order * K;
-    for (int base = 0; base < total1; base += blockDim.x) {
-        const int i = base + threadIdx.x;
-        int keep = 0, id = -1, ci = 0, k = 0;
-        if (i < total1) {
-            ci = i / K;
-            k = i - ci * K;
-            const size_t o = (size_t)a.order[ci] * K + k;
-            id = q.lm[o];
-            if (id >= 0) {
-                const double* T = s_T[ci];
-                const double* X = q.X + (size_t)id * 3;
-                const double xc = ((T[0] * X[0] + T[1] * X[1]) + T[2] * X[2]) + T[3];
-                const double yc = ((T[4] * X[0] + T[5] * X[1]) + T[6] * X[2]) + T[7];
-                const double zc = ((T[8] * X[0] + T[9] * X[1]) + T[10] * X[2]) + T[11];
-                const double pu = cal.fx * xc / zc + cal.cx, pv = cal.fy * yc / zc + cal.cy;
-                const double du = pu - q.u[o], dv = pv - q.v[o];
-                keep = zc > 0.0 && du * du + dv * dv <= lim;
+    const int ci = i / K, k = i - ci * K;
+    const size_t o = (size_t)a.order[ci] * K + k;
+    const int id = q.lm[o];
+    int keep = 0;
+    if (id >= 0) {
+        const double* T = s_T[ci];
+        const double* X = q.X + (size_t)id * 3;
+        const double xc = ((T[0] * X[0] + T[1] * X[1]) + T[2] * X[2]) + T[3];
+        const double yc = ((T[4] * X[0] + T[5] * X[1]) + T[6] * X[2]) + T[7];
+        const double zc = ((T[8] * X[0] + T[9] * X[1]) + T[10] * X[2]) + T[11];
+        const double pu = cal.fx * xc / zc + cal.cx, pv = cal.fy * yc / zc + cal.cy;
+        const double du = pu - q.u[o], dv = pv - q.v[o];
+        keep = zc > 0.0 && du * du + dv * dv <= lim;
+        if (keep) atomicAdd(&q.cnt[id], 1);
+    }
+    q.keep[i] = (uint8_t)keep;
+}
+
+// Compaction after the gate, as a deterministic tiled scan (tiles of BA_TILE items):
+//   landmark tiles over the ids (flag: >= 2 gated observations) -> compact index li = rank of the
+//   id, lm_id = its inverse;  observation tiles per window camera over its keypoints (flag: gated
+//   and its landmark kept) -> the observation list in (camera, keypoint) order.
+// k_ba_tilecount counts every tile, k_ba_tilescan scans the counts (one block), k_ba_tilescatter
+// writes, k_ba_camobs fills the camera x landmark table.
+#define BA_TILE (256 * BA_SCAN_ITEMS)
+
+struct BaTiles {
+    int n_lm_tiles, per_cam;   // landmark tiles; observation tiles per camera
+};
+__device__ __forceinline__ BaTiles ba_tiles(const BatchCtx& c, const BaArgs& a) {
+    return BaTiles{(a.W * c.g.K + BA_TILE - 1) / BA_TILE, (c.g.K + BA_TILE - 1) / BA_TILE};
+}
+
+// Flags of the BA_SCAN_ITEMS items of this thread in tile b; *ids gets the landmark id of each
+// flagged observation (observation tiles) or the id itself (landmark tiles).
+__device__ __forceinline__ void ba_tile_flags(const BatchCtx& c, const BaArgs& a, const BaPair& q, int b, int* fl,
+                                              int* ids, int* ci_out, int* k0_out) {
+    const int K = c.g.K;
+    const BaTiles t = ba_tiles(c, a);
+    if (b < t.n_lm_tiles) {
+        const int NID = a.W * K;
+        const int i0 = b * BA_TILE + threadIdx.x * BA_SCAN_ITEMS;
+        *ci_out = -1;
+        *k0_out = i0;
+#pragma unroll
+        for (int it = 0; it < BA_SCAN_ITEMS; ++it) {
+            ids[it] = i0 + it;
+            fl[it] = i0 + it < NID && q.cnt[i0 + it] >= 2;
+        }
+    } else {
+        const int bb = b - t.n_lm_tiles, ci = bb / t.per_cam;
+        const int k0 = (bb - ci * t.per_cam) * BA_TILE + threadIdx.x * BA_SCAN_ITEMS;
+        *ci_out = ci;
+        *k0_out = k0;
+        const size_t base = (size_t)a.order[ci] * K;
+#pragma unroll
+        for (int it = 0; it < BA_SCAN_ITEMS; ++it) {
+            const int k = k0 + it;
+            ids[it] = -1;
+            fl[it] = 0;
+            if (k < K && q.keep[ci * K + k]) {
+                ids[it] = q.lm[base + k];
+                fl[it] = q.cnt[ids[it]] >= 2;
             }
         }
-        int tot;
-        const int pos = n1 + block_scan_excl(keep, s_tmp, &tot);
-        if (keep) {
-            q.obs_cam[pos] = ci;
-            q.obs_k[pos] = k;
-            q.obs_id[pos] = id;
-            atomicAdd(&q.cnt[id], 1);
-        }
-        n1 += tot;
     }
-    __syncthreads();
-    // pass 2: keep observations of landmarks seen >= 2 times (stable, in place)
-    int n2 = 0;
-    for (int base = 0; base < n1; base += blockDim.x) {
-        const int i = base + threadIdx.x;
-        int keep = 0, ci = 0, k = 0, id = 0;
-        if (i < n1) {
-            ci = q.obs_cam[i];
-            k = q.obs_k[i];
-            id = q.obs_id[i];
-            keep = q.cnt[id] >= 2;
-        }
-        int tot;
-        const int pos = n2 + block_scan_excl(keep, s_tmp, &tot);
-        __syncthreads();   // every read of this chunk before any in-place write
-        if (keep) {
-            q.obs_cam[pos] = ci;
-            q.obs_k[pos] = k;
-            q.obs_id[pos] = id;
-        }
-        n2 += tot;
-        __syncthreads();
-    }
-    // compact landmark index = rank among the ids with >= 2 observations (sorted ids)
-    int L = 0;
-    for (int base = 0; base < NID; base += blockDim.x) {
-        const int i = base + threadIdx.x;
-        const int fl = i < NID && q.cnt[i] >= 2;
-        int tot;
-        const int r = L + block_scan_excl(fl, s_tmp, &tot);
-        if (i < NID) q.li[i] = fl ? r : -1;
-        if (fl) q.lm_id[r] = i;
-        L += tot;
-    }
-    __syncthreads();
-    // CSR offsets (counts per compact landmark, exclusive scan)
+}
+
+__global__ __launch_bounds__(256) void k_ba_tilecount(BatchCtx c, BaArgs a) {
+    __shared__ int s_tmp[32];
+    BaPair q = ba_pair(c, a, a.pair);
+    int fl[BA_SCAN_ITEMS], ids[BA_SCAN_ITEMS], ci, k0, cnt = 0;
+    ba_tile_flags(c, a, q, blockIdx.x, fl, ids, &ci, &k0);
+#pragma unroll
+    for (int it = 0; it < BA_SCAN_ITEMS; ++it) cnt += fl[it];
+    int tot;
+    block_scan_excl(cnt, s_tmp, &tot);
+    if (threadIdx.x == 0) q.tiles[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(64) void k_ba_tilescan(BatchCtx c, BaArgs a) {
+    BaPair q = ba_pair(c, a, a.pair);
+    const BaTiles t = ba_tiles(c, a);
+    if (threadIdx.x != 0) return;
     int run = 0;
-    for (int base = 0; base < L; base += blockDim.x) {
-        const int r = base + threadIdx.x;
-        const int cn = r < L ? q.cnt[q.lm_id[r]] : 0;
-        int tot;
-        const int off = run + block_scan_excl(cn, s_tmp, &tot);
-        if (r < L) {
-            q.lm_off[r] = off;
-            q.fill[r] = 0;
+    for (int b = 0; b < t.n_lm_tiles; ++b) {
+        const int v = q.tiles[b];
+        q.tiles[TS_BA_TILES + b] = run;
+        run += v;
+    }
+    q.counts[1] = run;
+    run = 0;
+    for (int ci = 0; ci < a.n_order; ++ci) {
+        q.cam_off[ci] = run;
+        for (int tt = 0; tt < t.per_cam; ++tt) {
+            const int b = t.n_lm_tiles + ci * t.per_cam + tt;
+            const int v = q.tiles[b];
+            q.tiles[TS_BA_TILES + b] = run;
+            run += v;
         }
-        run += tot;
     }
-    if (threadIdx.x == 0) q.lm_off[L] = run;
-    __syncthreads();
-    for (int i = threadIdx.x; i < n2; i += blockDim.x) {
-        const int r = q.li[q.obs_id[i]];
-        q.lm_obs[q.lm_off[r] + atomicAdd(&q.fill[r], 1)] = i;
-    }
-    __syncthreads();
-    for (int r = threadIdx.x; r < L; r += blockDim.x) {   // each segment in observation order
-        const int o0 = q.lm_off[r], o1 = q.lm_off[r + 1];
-        for (int x = o0 + 1; x < o1; ++x)
-            for (int y = x; y > o0 && q.lm_obs[y - 1] > q.lm_obs[y]; --y) {
-                const int t = q.lm_obs[y];
-                q.lm_obs[y] = q.lm_obs[y - 1];
-                q.lm_obs[y - 1] = t;
+    q.cam_off[a.n_order] = run;
+    q.counts[0] = run;
+}
+
+__global__ __launch_bounds__(256) void k_ba_tilescatter(BatchCtx c, BaArgs a) {
+    __shared__ int s_tmp[32];
+    BaPair q = ba_pair(c, a, a.pair);
+    int fl[BA_SCAN_ITEMS], ids[BA_SCAN_ITEMS], ci, k0, cnt = 0;
+    ba_tile_flags(c, a, q, blockIdx.x, fl, ids, &ci, &k0);
+#pragma unroll
+    for (int it = 0; it < BA_SCAN_ITEMS; ++it) cnt += fl[it];
+    int tot;
+    int pos = q.tiles[TS_BA_TILES + blockIdx.x] + block_scan_excl(cnt, s_tmp, &tot);
+    if (ci < 0) {
+        const int NID = a.W * c.g.K;
+#pragma unroll
+        for (int it = 0; it < BA_SCAN_ITEMS; ++it) {
+            if (k0 + it < NID) q.li[k0 + it] = fl[it] ? pos : -1;
+            if (fl[it]) q.lm_id[pos++] = k0 + it;
+        }
+    } else {
+#pragma unroll
+        for (int it = 0; it < BA_SCAN_ITEMS; ++it)
+            if (fl[it]) {
+                q.obs_cam[pos] = ci;
+                q.obs_k[pos] = k0 + it;
+                q.obs_id[pos] = ids[it];
+                ++pos;
             }
     }
-    // camera ranges of the (camera-ordered) observations
-    for (int ci = threadIdx.x; ci <= a.n_order; ci += blockDim.x) {
-        int lo = 0, hi = n2;   // first observation with camera >= ci
-        while (lo < hi) {
-            const int m = (lo + hi) >> 1;
-            if (q.obs_cam[m] < ci) lo = m + 1; else hi = m;
-        }
-        q.cam_off[ci] = lo;
-    }
-    if (threadIdx.x == 0) {
-        q.counts[0] = n2;
-        q.counts[1] = L;
-    }
+}
+
+__global__ __launch_bounds__(256) void k_ba_camobs(BatchCtx c, BaArgs a) {
+    BaPair q = ba_pair(c, a, a.pair);
+    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= q.counts[0]) return;
+    q.camobs[(size_t)q.obs_cam[o] * a.W * c.g.K + q.li[q.obs_id[o]]] = o;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -322,124 +362,170 @@ __device__ __forceinline__ void ba_obs_jac(const double* T, const double* X, dou
     }
 }
 
-__global__ __launch_bounds__(256) void k_ba_lin(BatchCtx c, BaArgs a) {
-    const int K = c.g.K;
+// One thread per observation: W_o = J_c^T J_p and J_p^T J_p | J_p^T r (per observation, read back
+// per landmark), J_c^T J_c | J_c^T r (structure-of-arrays, summed per camera).
+__global__ __launch_bounds__(256) void k_ba_jac(BatchCtx c, BaArgs a) {
+    __shared__ double s_T[TS_BA_MAXW][12];
+    const int K = c.g.K, WK = a.W * K;
     BaPair q = ba_pair(c, a, a.pair);
-    const int L = q.counts[1];
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    const int kpad = (3 * L + 3) & ~3;
-    if (r >= L) {
-        // zero the padding columns up to a multiple of 4 (the MFMA k-step)
-        const int col = 3 * L + (r - L);
-        if (col < kpad)
-            for (int e = 0; e < 64; ++e) q.Qt[(size_t)col * 64 + e] = 0.0;
-        return;
-    }
+    for (int i = threadIdx.x; i < a.n_order * 12; i += blockDim.x) s_T[i / 12][i % 12] = q.T[(size_t)a.order[i / 12] * 16 + i % 12];
+    __syncthreads();
+    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= q.counts[0]) return;
     const PairCalib cal = c.calib[a.pair];
-    const int id = q.lm_id[r];
+    const int ci = q.obs_cam[o], id = q.obs_id[o];
+    const size_t so = (size_t)a.order[ci] * K + q.obs_k[o];
     const double X[3] = {q.X[(size_t)id * 3], q.X[(size_t)id * 3 + 1], q.X[(size_t)id * 3 + 2]};
-    double V[3][3] = {{a.lam, 0.0, 0.0}, {0.0, a.lam, 0.0}, {0.0, 0.0, a.lam}}, gp[3] = {0.0, 0.0, 0.0};
-    const int o0 = q.lm_off[r], o1 = q.lm_off[r + 1];
-    for (int oi = o0; oi < o1; ++oi) {
-        const int o = q.lm_obs[oi];
-        const int ci = q.obs_cam[o], k = q.obs_k[o];
-        const int s = a.order[ci];
-        const size_t so = (size_t)s * K + k;
-        double Jc[3][6], Jp[3][3], res[3];
-        ba_obs_jac(q.T + (size_t)s * 16, X, q.u[so], q.v[so], q.d[so], cal, Jc, Jp, res);
-        for (int i = 0; i < 3; ++i) {
-            for (int j = 0; j < 3; ++j) V[i][j] += (Jp[0][i] * Jp[0][j] + Jp[1][i] * Jp[1][j]) + Jp[2][i] * Jp[2][j];
-            gp[i] += (Jp[0][i] * res[0] + Jp[1][i] * res[1]) + Jp[2][i] * res[2];
-        }
-        double* W = q.obs_W + (size_t)o * 18;
-        for (int i = 0; i < 6; ++i)
-            for (int j = 0; j < 3; ++j) W[3 * i + j] = (Jc[0][i] * Jp[0][j] + Jc[1][i] * Jp[1][j]) + Jc[2][i] * Jp[2][j];
-        double* Ug = q.obs_Ug + (size_t)o * 27;   // upper-triangular J_c^T J_c (21) + J_c^T r (6)
-        int e = 0;
-        for (int i = 0; i < 6; ++i)
-            for (int j = i; j < 6; ++j) Ug[e++] = (Jc[0][i] * Jc[0][j] + Jc[1][i] * Jc[1][j]) + Jc[2][i] * Jc[2][j];
-        for (int i = 0; i < 6; ++i) Ug[21 + i] = (Jc[0][i] * res[0] + Jc[1][i] * res[1]) + Jc[2][i] * res[2];
-    }
-    // Cholesky V = L L^T
-    double Lm[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
-    for (int j = 0; j < 3; ++j) {
-        double sd = V[j][j];
-        for (int k = 0; k < j; ++k) sd -= Lm[j][k] * Lm[j][k];
-        Lm[j][j] = sqrt(sd > 1e-300 ? sd : 1e-300);
-        for (int i = j + 1; i < 3; ++i) {
-            double t = V[i][j];
-            for (int k = 0; k < j; ++k) t -= Lm[i][k] * Lm[j][k];
-            Lm[i][j] = t / Lm[j][j];
-        }
-    }
-    double* Ls = q.lm_L + (size_t)r * 9;
+    double Jc[3][6], Jp[3][3], res[3];
+    ba_obs_jac(s_T[ci], X, q.u[so], q.v[so], q.d[so], cal, Jc, Jp, res);
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 3; ++j) q.obs_W[(size_t)o * 18 + 3 * i + j] = (Jc[0][i] * Jp[0][j] + Jc[1][i] * Jp[1][j]) + Jc[2][i] * Jp[2][j];
+    int e = 0;
+    for (int i = 0; i < 6; ++i)
+        for (int j = i; j < 6; ++j) q.obs_Ug[(size_t)(e++) * WK + o] = (Jc[0][i] * Jc[0][j] + Jc[1][i] * Jc[1][j]) + Jc[2][i] * Jc[2][j];
+    for (int i = 0; i < 6; ++i) q.obs_Ug[(size_t)(21 + i) * WK + o] = (Jc[0][i] * res[0] + Jc[1][i] * res[1]) + Jc[2][i] * res[2];
+    e = 0;
     for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) Ls[3 * i + j] = Lm[i][j];
-    for (int i = 0; i < 3; ++i) q.lm_gp[(size_t)r * 3 + i] = gp[i];
-    // y = L^-1 g_p ; Q_o rows = L^-1 W_o[row]^T
-    double y[3];
-    for (int i = 0; i < 3; ++i) {
-        double t = gp[i];
-        for (int k = 0; k < i; ++k) t -= Lm[i][k] * y[k];
-        y[i] = t / Lm[i][i];
-    }
-    double* Q = q.Qt + (size_t)(3 * r) * 64;   // three k-columns of 64 rows
-    for (int e = 0; e < 3 * 64; ++e) Q[e] = 0.0;
-    for (int j = 0; j < 3; ++j) Q[j * 64 + 60] = y[j];
-    for (int oi = o0; oi < o1; ++oi) {
-        const int o = q.lm_obs[oi];
-        const int ci = q.obs_cam[o];
-        const double* W = q.obs_W + (size_t)o * 18;
-        for (int rr = 0; rr < 6; ++rr) {
-            double z[3];
-            for (int i = 0; i < 3; ++i) {
-                double t = W[3 * rr + i];
-                for (int k = 0; k < i; ++k) t -= Lm[i][k] * z[k];
-                z[i] = t / Lm[i][i];
-            }
-            for (int j = 0; j < 3; ++j) Q[j * 64 + 6 * ci + rr] = z[j];
-        }
-    }
+        for (int j = i; j < 3; ++j) q.obs_Vg[(size_t)o * 9 + (e++)] = (Jp[0][i] * Jp[0][j] + Jp[1][i] * Jp[1][j]) + Jp[2][i] * Jp[2][j];
+    for (int i = 0; i < 3; ++i) q.obs_Vg[(size_t)o * 9 + 6 + i] = (Jp[0][i] * res[0] + Jp[1][i] * res[1]) + Jp[2][i] * res[2];
 }
 
-__global__ __launch_bounds__(256) void k_ba_camred(BatchCtx c, BaArgs a) {
-    __shared__ double s_red[256];
+// One wave per (window camera, element): U_c = sum J_c^T J_c, g_c = sum J_c^T r over the camera's
+// observations (lanes stride them, 4 accumulators, DPP wave sum: a fixed order).
+__global__ __launch_bounds__(64) void k_ba_camred(BatchCtx c, BaArgs a) {
+    const int WK = a.W * c.g.K;
     BaPair q = ba_pair(c, a, a.pair);
-    const int ci = blockIdx.x;
+    const int ci = blockIdx.x / 27, e = blockIdx.x % 27;
+    const int lane = threadIdx.x;
     const int o0 = q.cam_off[ci], o1 = q.cam_off[ci + 1];
-    for (int e = 0; e < 27; ++e) {
-        double s = 0.0;
-        for (int o = o0 + (int)threadIdx.x; o < o1; o += blockDim.x) s += q.obs_Ug[(size_t)o * 27 + e];
-        s_red[threadIdx.x] = s;
-        __syncthreads();
-        for (int w = 128; w > 0; w >>= 1) {
-            if ((int)threadIdx.x < w) s_red[threadIdx.x] += s_red[threadIdx.x + w];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) q.cam_U[(size_t)ci * 27 + e] = s_red[0];
-        __syncthreads();
+    const double* src = q.obs_Ug + (size_t)e * WK;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int o = o0 + lane;
+    for (; o + 192 < o1; o += 256) {
+        s0 += src[o];
+        s1 += src[o + 64];
+        s2 += src[o + 128];
+        s3 += src[o + 192];
     }
+    for (; o < o1; o += 64) s0 += src[o];
+    const double s = wave_sum_f64((s0 + s1) + (s2 + s3));
+    if (lane == 0) q.cam_U[(size_t)ci * 27 + e] = s;
 }
 
 typedef double d4v __attribute__((ext_vector_type(4)));
+#define BA_CHUNK 32          // landmarks per LDS tile (96 Schur columns)
+#define BA_QPITCH 80         // doubles per tile column: 160 dwords = 32 mod 64 banks, so the four
+                             // columns one MFMA operand read touches fall in disjoint bank halves
 
-__global__ __launch_bounds__(256) void k_ba_gemm(BatchCtx c, BaArgs a) {
+// The landmark side of the Schur complement, fused: per chunk of BA_CHUNK landmarks,
+//   1. one thread per landmark: V = sum J_p^T J_p + lam I (camera order), g_p, L = chol(V),
+//      y = L^-1 g_p (L and g_p also go to HBM for the back substitution);
+//   2. the chunk's Schur columns into an LDS tile Q[3 * BA_CHUNK][64]: column 3l + j holds
+//      (W_o L^-T)[:, j] in the 6 rows of the observing camera (0 when unobserved) and y_j in row 60;
+//   3. C += Q^T Q on the FP64 matrix cores (v_mfma_f64_16x16x4f64): wave w owns rows 16w..16w+15.
+// Blocks stride the chunks; each block writes its 64 x 64 partial (summed by k_ba_reduce).
+__global__ __launch_bounds__(256) void k_ba_schur(BatchCtx c, BaArgs a) {
+    __shared__ double s_Q[3 * BA_CHUNK * BA_QPITCH];
+    __shared__ double s_L[BA_CHUNK][6];
+    __shared__ int s_co[BA_CHUNK][TS_BA_MAXW];
+    const int WK = a.W * c.g.K, n = a.n_order;
     BaPair q = ba_pair(c, a, a.pair);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int L = q.counts[1];
-    const int kt = ((3 * L + 3) & ~3) / 4;            // k-steps of 4
-    const int per = (kt + gridDim.x - 1) / gridDim.x;
-    const int s0 = blockIdx.x * per, s1 = min(kt, s0 + per);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int kk = lane >> 4, rc = lane & 15;
     d4v acc[4];
     for (int t = 0; t < 4; ++t) acc[t] = (d4v){0.0, 0.0, 0.0, 0.0};
-    const int a0 = 16 * wave, kk = lane >> 4, rc = lane & 15;
-    for (int st = s0; st < s1; ++st) {
-        const double* col = q.Qt + (size_t)(4 * st + kk) * 64;
-        const double av = col[a0 + rc];
+    for (int l0 = blockIdx.x * BA_CHUNK; l0 < L; l0 += gridDim.x * BA_CHUNK) {
+        const int nl = min(BA_CHUNK, L - l0);
+        // 1. per-landmark factor (loads issued unconditionally from clamped indices, then masked:
+        //    the kernel is latency bound, so every load of a thread is in flight at once)
+        if (threadIdx.x < BA_CHUNK) {
+            const int li = threadIdx.x, r = min(l0 + li, L - 1);
+            const bool live = li < nl;
+            int co[TS_BA_MAXW];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, col[16 * t + rc], acc[t], 0, 0, 0);
+            for (int ci = 0; ci < TS_BA_MAXW; ++ci) co[ci] = q.camobs[(size_t)min(ci, n - 1) * WK + r];
+            double vo[TS_BA_MAXW][9];
+#pragma unroll
+            for (int ci = 0; ci < TS_BA_MAXW; ++ci)
+#pragma unroll
+                for (int e = 0; e < 9; ++e) vo[ci][e] = q.obs_Vg[(size_t)max(co[ci], 0) * 9 + e];
+            double vg[9] = {a.lam, 0.0, 0.0, a.lam, 0.0, a.lam, 0.0, 0.0, 0.0};   // V00 V01 V02 V11 V12 V22 g
+#pragma unroll
+            for (int ci = 0; ci < TS_BA_MAXW; ++ci) {
+                const bool use = ci < n && co[ci] >= 0;
+                s_co[li][ci] = ci < n ? co[ci] : -1;
+#pragma unroll
+                for (int e = 0; e < 9; ++e) vg[e] += use ? vo[ci][e] : 0.0;
+            }
+            const double l00 = sqrt(vg[0] > 1e-300 ? vg[0] : 1e-300);
+            const double l10 = vg[1] / l00, l20 = vg[2] / l00;
+            const double d11 = vg[3] - l10 * l10;
+            const double l11 = sqrt(d11 > 1e-300 ? d11 : 1e-300);
+            const double l21 = (vg[4] - l20 * l10) / l11;
+            const double d22 = (vg[5] - l20 * l20) - l21 * l21;
+            const double l22 = sqrt(d22 > 1e-300 ? d22 : 1e-300);
+            const double y0 = vg[6] / l00, y1 = (vg[7] - l10 * y0) / l11, y2 = ((vg[8] - l20 * y0) - l21 * y1) / l22;
+            s_L[li][0] = 1.0 / l00; s_L[li][1] = l10; s_L[li][2] = 1.0 / l11; s_L[li][3] = l20; s_L[li][4] = l21;
+            s_L[li][5] = 1.0 / l22;
+            s_Q[(3 * li) * BA_QPITCH + 60] = live ? y0 : 0.0;
+            s_Q[(3 * li + 1) * BA_QPITCH + 60] = live ? y1 : 0.0;
+            s_Q[(3 * li + 2) * BA_QPITCH + 60] = live ? y2 : 0.0;
+            if (live) {
+                q.lm_L[r] = l00; q.lm_L[(size_t)WK + r] = l10; q.lm_L[(size_t)2 * WK + r] = l11;
+                q.lm_L[(size_t)3 * WK + r] = l20; q.lm_L[(size_t)4 * WK + r] = l21; q.lm_L[(size_t)5 * WK + r] = l22;
+                q.lm_gp[r] = vg[6]; q.lm_gp[(size_t)WK + r] = vg[7]; q.lm_gp[(size_t)2 * WK + r] = vg[8];
+            }
+        }
+        __syncthreads();
+        // 2. Schur columns: thread = (row, wave); items = landmarks wave, wave + 4, ...:
+        //    z = L^-1 W_o[row % 6, :]^T for the observation o of the row's camera (0 if none)
+        {
+            const int row = threadIdx.x & 63, ci = min(row / 6, TS_BA_MAXW - 1), rr = row - 6 * (row / 6);
+            constexpr int NU = BA_CHUNK / 4;
+            int o[NU];
+            double w[NU][3];
+#pragma unroll
+            for (int u = 0; u < NU; ++u) o[u] = s_co[wave + 4 * u][ci];
+#pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                const double* W = q.obs_W + (size_t)max(o[u], 0) * 18 + 3 * rr;
+                w[u][0] = W[0];
+                w[u][1] = W[1];
+                w[u][2] = W[2];
+            }
+            const bool row_ok = row < 6 * n && row != 60;
+#pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                const int li = wave + 4 * u;
+                const double* Lm = s_L[li];
+                const bool use = row_ok && li < nl && o[u] >= 0;
+                const double z0 = w[u][0] * Lm[0];
+                const double z1 = (w[u][1] - Lm[1] * z0) * Lm[2];
+                const double z2 = ((w[u][2] - Lm[3] * z0) - Lm[4] * z1) * Lm[5];
+                if (row != 60) {
+                    s_Q[(3 * li) * BA_QPITCH + row] = use ? z0 : 0.0;
+                    s_Q[(3 * li + 1) * BA_QPITCH + row] = use ? z1 : 0.0;
+                    s_Q[(3 * li + 2) * BA_QPITCH + row] = use ? z2 : 0.0;
+                }
+            }
+        }
+        __syncthreads();
+        // 3. C += Q^T Q over the chunk's columns (zero columns past nl contribute nothing)
+        const int ksteps = (3 * nl + 3) >> 2;
+        for (int st = 0; st < ksteps; ++st) {
+            const double* col = s_Q + (4 * st + kk) * BA_QPITCH;
+            const double b0 = col[rc], b1 = col[16 + rc], b2 = col[32 + rc], b3 = col[48 + rc];
+            const double av = wave == 0 ? b0 : wave == 1 ? b1 : wave == 2 ? b2 : b3;
+            acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b0, acc[0], 0, 0, 0);
+            acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b1, acc[1], 0, 0, 0);
+            acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b2, acc[2], 0, 0, 0);
+            acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b3, acc[3], 0, 0, 0);
+        }
+        __syncthreads();
     }
     double* out = q.part + (size_t)blockIdx.x * 64 * 64;
+    const int a0 = 16 * wave;
     // C/D layout of v_mfma_f64_16x16x4f64: col = lane & 15, row = (lane >> 4) + 4 * reg
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -447,74 +533,113 @@ __global__ __launch_bounds__(256) void k_ba_gemm(BatchCtx c, BaArgs a) {
         for (int rg = 0; rg < 4; ++rg) out[(size_t)(a0 + kk + 4 * rg) * 64 + 16 * t + rc] = acc[t][rg];
 }
 
+// Fixed-order sum of the split-K partials (one thread per element of C).
+__global__ __launch_bounds__(256) void k_ba_reduce(BatchCtx c, BaArgs a) {
+    BaPair q = ba_pair(c, a, a.pair);
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    double s = 0.0;
+#pragma unroll 16
+    for (int b = 0; b < a.nsplit; ++b) s += q.part[(size_t)b * 4096 + e];
+    q.C[e] = s;
+}
+
+// Reduced camera system (camera 0 = gauge): S = blockdiag(U + lam) - C, b = -g_c + C[:, 60].
+// LDL^T elimination with the right-hand side as an extra column (one barrier per pivot), then
+// the back substitution on one wave (lane = row); camera updates R <- cayley(w) R, t <- ... + rho.
 __global__ __launch_bounds__(1024) void k_ba_solve(BatchCtx c, BaArgs a) {
-    __shared__ double s_S[TS_BA_MAXD * TS_BA_MAXD];
-    __shared__ double s_b[TS_BA_MAXD], s_x[TS_BA_MAXD];
+    __shared__ double s_S[TS_BA_MAXD * (TS_BA_MAXD + 1)];
+    __shared__ double s_x[TS_BA_MAXD];
     __shared__ int s_ok;
     BaPair q = ba_pair(c, a, a.pair);
     const int n = a.n_order;
-    const int m = 6 * (n - 1);   // camera 0 is the gauge
+    const int m = 6 * (n - 1), mp = m + 1;
     if (q.counts[1] == 0 || n < 2) {
         if (threadIdx.x == 0) q.counts[2] = 0;
         return;
     }
-    for (int i = threadIdx.x; i < m * m; i += blockDim.x) {
-        const int rr = i / m, cc = i % m;
-        const int R = rr + 6, Cc = cc + 6;   // full-system indices
-        double sum = 0.0;
-        for (int bk = 0; bk < a.nsplit; ++bk) sum += q.part[(size_t)bk * 4096 + R * 64 + Cc];
-        double v = -sum;
-        if (R / 6 == Cc / 6) {
-            const int ci = R / 6, i0 = R % 6, j0 = Cc % 6;
-            const int lo = min(i0, j0), hi = max(i0, j0);
-            const int e = lo * 6 - lo * (lo - 1) / 2 + (hi - lo);   // upper-triangular index
-            v += q.cam_U[(size_t)ci * 27 + e] + (i0 == j0 ? a.lam : 0.0);
-        }
-        s_S[rr * m + cc] = v;
-    }
-    for (int rr = threadIdx.x; rr < m; rr += blockDim.x) {
+    for (int i = threadIdx.x; i < m * mp; i += blockDim.x) {
+        const int rr = i / mp, cc = i - rr * mp;
         const int R = rr + 6;
-        double sum = 0.0;
-        for (int bk = 0; bk < a.nsplit; ++bk) sum += q.part[(size_t)bk * 4096 + R * 64 + 60];
-        s_b[rr] = -q.cam_U[(size_t)(R / 6) * 27 + 21 + R % 6] + sum;
+        double v;
+        if (cc == m) {
+            v = -q.cam_U[(size_t)(R / 6) * 27 + 21 + R % 6] + q.C[R * 64 + 60];
+        } else {
+            const int Cc = cc + 6;
+            v = -q.C[R * 64 + Cc];
+            if (R / 6 == Cc / 6) {
+                const int i0 = R % 6, j0 = Cc % 6;
+                const int lo = min(i0, j0), hi = max(i0, j0);
+                v += q.cam_U[(size_t)(R / 6) * 27 + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)] + (i0 == j0 ? a.lam : 0.0);
+            }
+        }
+        s_S[i] = v;
     }
     if (threadIdx.x == 0) s_ok = 1;
     __syncthreads();
-    // right-looking Cholesky in LDS (lower triangle)
-    for (int j = 0; j < m; ++j) {
-        if (threadIdx.x == 0) {
-            const double dj = s_S[j * m + j];
-            if (!(dj > 0.0)) s_ok = 0;
-            s_S[j * m + j] = sqrt(dj > 0.0 ? dj : 1.0);
+    // S = L' D L'^T by 6-column blocks (one camera each).  For block J (columns c0..c0+5):
+    //  panel (wave 0, lane = row i >= c0): the unblocked steps j = c0..c0+5 restricted to the
+    //    block's columns and the rhs, S[i][k] -= (S[i][j] / d_j) S[k][j] (wave-synchronous);
+    //  trailing (all threads): S[i][k] -= sum_j (S[i][j] / d_j) S[k][j] for c0+6 <= k <= i.
+    // Column j below the pivot is left as L'[i][j] * d_j.
+#ifndef BA_XP_NOELIM
+    __shared__ double s_rd[6];
+    for (int c0 = 0; c0 < m; c0 += 6) {
+        if (threadIdx.x < 64) {
+            const int i = c0 + (int)threadIdx.x;
+            for (int j = c0; j < c0 + 6; ++j) {
+                const double dj = s_S[j * mp + j];
+                if (!(dj > 0.0)) {   // uniform across the wave
+                    if (threadIdx.x == 0) s_ok = 0;
+                    break;
+                }
+                const double rj = 1.0 / dj;
+                if (threadIdx.x == 0) s_rd[j - c0] = rj;
+                if (i > j && i < m) {
+                    const double sij = s_S[i * mp + j] * rj;
+                    for (int k = j + 1; k < c0 + 6 && k <= i; ++k) s_S[i * mp + k] -= sij * s_S[k * mp + j];
+                    s_S[i * mp + m] -= sij * s_S[j * mp + m];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+            }
         }
         __syncthreads();
-        const double ljj = s_S[j * m + j];
-        for (int i = j + 1 + (int)threadIdx.x; i < m; i += blockDim.x) s_S[i * m + j] /= ljj;
-        __syncthreads();
-        const int nt = m - j - 1;
+        if (!s_ok) break;
+        const int c1 = c0 + 6, nt = m - c1;
         for (int t = threadIdx.x; t < nt * nt; t += blockDim.x) {
-            const int i = j + 1 + t / nt, k = j + 1 + t % nt;
-            if (k <= i) s_S[i * m + k] -= s_S[i * m + j] * s_S[k * m + j];
+            const int i = c1 + t / nt, k = c1 + t % nt;
+            if (k > i) continue;
+            const double* si = s_S + i * mp + c0;
+            const double* sk = s_S + k * mp + c0;
+            double acc = 0.0;
+#pragma unroll
+            for (int e = 0; e < 6; ++e) acc += (si[e] * s_rd[e]) * sk[e];
+            s_S[i * mp + k] -= acc;
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
-        for (int i = 0; i < m; ++i) {   // L y = b
-            double t = s_b[i];
-            for (int k = 0; k < i; ++k) t -= s_S[i * m + k] * s_x[k];
-            s_x[i] = t / s_S[i * m + i];
+#endif
+    __syncthreads();
+    const bool ok = s_ok;
+#ifdef BA_XP_NOSUB
+    if (false) {
+#else
+    if (ok && threadIdx.x < 64) {
+#endif
+        // D L'^T x = b'':  x_k = b''_k / d_k - sum_{i > k} L'[i][k] x_i   (lane k, i descending)
+        const int k = threadIdx.x;
+        const double rk = k < m ? 1.0 / s_S[k * mp + k] : 1.0;
+        double r = k < m ? s_S[k * mp + m] * rk : 0.0;
+        for (int i = m - 1; i >= 0; --i) {
+            const double xi = __shfl(r, i, 64);
+            if (k < i) r -= (s_S[i * mp + k] * rk) * xi;
         }
-        for (int i = m - 1; i >= 0; --i) {   // L^T x = y
-            double t = s_x[i];
-            for (int k = i + 1; k < m; ++k) t -= s_S[k * m + i] * s_x[k];
-            s_x[i] = t / s_S[i * m + i];
-        }
-        q.counts[2] = s_ok;
+        if (k < m) s_x[k] = r;
     }
     __syncthreads();
-    // dc (camera 0: zero) and camera updates: R <- cayley(w) R, t <- cayley(w) t + rho
-    for (int i = threadIdx.x; i < 6 * n; i += blockDim.x) q.dc[i] = (i < 6 || !s_ok) ? 0.0 : s_x[i - 6];
-    if (s_ok && (int)threadIdx.x >= 1 && (int)threadIdx.x < n) {
+    if (threadIdx.x == 0) q.counts[2] = ok;
+    for (int i = threadIdx.x; i < 6 * n; i += blockDim.x) q.dc[i] = (i < 6 || !ok) ? 0.0 : s_x[i - 6];
+    if (ok && (int)threadIdx.x >= 1 && (int)threadIdx.x < n) {
         const int ci = threadIdx.x;
         const double* x = s_x + 6 * (ci - 1);
         const double w0 = x[3], w1 = x[4], w2 = x[5];
@@ -539,34 +664,51 @@ __global__ __launch_bounds__(1024) void k_ba_solve(BatchCtx c, BaArgs a) {
     }
 }
 
+// 16 lanes per landmark (lane = window camera): W_o^T dc_o of each observation, summed over the
+// 16 lanes by a fixed xor-butterfly; the first lane then solves dp = V^-1 (-g_p - sum) with the
+// stored Cholesky factor and moves the landmark, X += dp.
 __global__ __launch_bounds__(256) void k_ba_backsub(BatchCtx c, BaArgs a) {
+    const int WK = a.W * c.g.K;
     BaPair q = ba_pair(c, a, a.pair);
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = gid >> 4, ci = gid & 15;
     const int L = q.counts[1];
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= L || !q.counts[2]) return;
-    double rhs[3];
-    for (int i = 0; i < 3; ++i) rhs[i] = -q.lm_gp[(size_t)r * 3 + i];
-    for (int oi = q.lm_off[r]; oi < q.lm_off[r + 1]; ++oi) {
-        const int o = q.lm_obs[oi];
-        const double* W = q.obs_W + (size_t)o * 18;
-        const double* dc = q.dc + 6 * q.obs_cam[o];
-        for (int j = 0; j < 3; ++j) {
-            double t = 0.0;
-            for (int i = 0; i < 6; ++i) t += W[3 * i + j] * dc[i];
-            rhs[j] -= t;
-        }
+    if (!q.counts[2] || (r & ~15) >= L) return;   // whole 16-landmark groups exit together
+    const bool live = r < L;
+    const int rc = min(r, L - 1);
+    const int o = ci >= 1 && ci < a.n_order ? q.camobs[(size_t)ci * WK + rc] : -1;   // dc of camera 0 is zero
+    const double* W = q.obs_W + (size_t)max(o, 0) * 18;
+    double wv[18];
+#pragma unroll
+    for (int e = 0; e < 18; ++e) wv[e] = W[e];
+    const double* dc = q.dc + 6 * min(ci, TS_BA_MAXW - 1);
+    double t[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) acc += wv[3 * i + j] * dc[i];
+        t[j] = o >= 0 ? acc : 0.0;
     }
-    const double* Lm = q.lm_L + (size_t)r * 9;
+#pragma unroll
+    for (int sh = 8; sh > 0; sh >>= 1)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) t[j] += __shfl_xor(t[j], sh, 64);
+    if (ci != 0 || !live) return;
+    double rhs[3];
+    for (int i = 0; i < 3; ++i) rhs[i] = -q.lm_gp[(size_t)i * WK + r] - t[i];
+    double Lm[3][3] = {{q.lm_L[r], 0.0, 0.0}, {q.lm_L[(size_t)WK + r], q.lm_L[(size_t)2 * WK + r], 0.0},
+                       {q.lm_L[(size_t)3 * WK + r], q.lm_L[(size_t)4 * WK + r], q.lm_L[(size_t)5 * WK + r]}};
     double y[3], x[3];
     for (int i = 0; i < 3; ++i) {
-        double t = rhs[i];
-        for (int k = 0; k < i; ++k) t -= Lm[3 * i + k] * y[k];
-        y[i] = t / Lm[3 * i + i];
+        double v = rhs[i];
+        for (int k = 0; k < i; ++k) v -= Lm[i][k] * y[k];
+        y[i] = v / Lm[i][i];
     }
     for (int i = 2; i >= 0; --i) {
-        double t = y[i];
-        for (int k = i + 1; k < 3; ++k) t -= Lm[3 * k + i] * x[k];
-        x[i] = t / Lm[3 * i + i];
+        double v = y[i];
+        for (int k = i + 1; k < 3; ++k) v -= Lm[k][i] * x[k];
+        x[i] = v / Lm[i][i];
     }
     const int id = q.lm_id[r];
     for (int i = 0; i < 3; ++i) q.X[(size_t)id * 3 + i] += x[i];
@@ -576,18 +718,34 @@ __global__ __launch_bounds__(256) void k_ba_backsub(BatchCtx c, BaArgs a) {
 // host launchers
 // ---------------------------------------------------------------------------------------------
 void launch_ba_keyframe(const BatchCtx& c, const BaArgs& a, bool evict, hipStream_t s) {
-    if (evict) hipLaunchKernelGGL(k_ba_evict, dim3(1), dim3(1024), 0, s, c, a);
-    hipLaunchKernelGGL(k_ba_insert, dim3(1), dim3(1024), 0, s, c, a);
+    const int K = c.g.K;
+    if (evict) {
+        const int nb = (a.n_order * K + 255) / 256;
+        (void)hipMemsetAsync(a.st.remap, 0x7F, sizeof(int32_t) * K, s);
+        hipLaunchKernelGGL(k_ba_evict_min, dim3(nb), dim3(256), 0, s, c, a);
+        hipLaunchKernelGGL(k_ba_evict_move, dim3(nb), dim3(256), 0, s, c, a);
+    }
+    hipLaunchKernelGGL(k_ba_insert, dim3((K + 255) / 256), dim3(256), 0, s, c, a);
 }
 
 void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s) {
-    const int maxL = a.W * c.g.K;
-    hipLaunchKernelGGL(k_ba_gather, dim3(1), dim3(1024), 0, s, c, a);
+    // grids sized for the window's maximum (counts live on the device; threads past them exit)
+    const int WK = a.W * c.g.K;
+    const int nb = (WK + 255) / 256;
+    (void)hipMemsetAsync(a.st.cnt, 0, sizeof(int32_t) * WK, s);
+    (void)hipMemsetAsync(a.st.camobs, 0xFF, sizeof(int32_t) * (size_t)a.n_order * WK, s);
+    hipLaunchKernelGGL(k_ba_gate, dim3((a.n_order * c.g.K + 255) / 256), dim3(256), 0, s, c, a);
+    const int ntiles = (WK + BA_TILE - 1) / BA_TILE + a.n_order * ((c.g.K + BA_TILE - 1) / BA_TILE);
+    hipLaunchKernelGGL(k_ba_tilecount, dim3(ntiles), dim3(256), 0, s, c, a);
+    hipLaunchKernelGGL(k_ba_tilescan, dim3(1), dim3(64), 0, s, c, a);
+    hipLaunchKernelGGL(k_ba_tilescatter, dim3(ntiles), dim3(256), 0, s, c, a);
+    hipLaunchKernelGGL(k_ba_camobs, dim3(nb), dim3(256), 0, s, c, a);
     for (int it = 0; it < a.iters; ++it) {
-        hipLaunchKernelGGL(k_ba_lin, dim3((maxL + 4 + 255) / 256), dim3(256), 0, s, c, a);
-        hipLaunchKernelGGL(k_ba_camred, dim3(a.n_order), dim3(256), 0, s, c, a);
-        hipLaunchKernelGGL(k_ba_gemm, dim3(a.nsplit), dim3(256), 0, s, c, a);
+        hipLaunchKernelGGL(k_ba_jac, dim3(nb), dim3(256), 0, s, c, a);
+        hipLaunchKernelGGL(k_ba_camred, dim3(a.n_order * 27), dim3(64), 0, s, c, a);
+        hipLaunchKernelGGL(k_ba_schur, dim3(a.nsplit), dim3(256), 0, s, c, a);
+        hipLaunchKernelGGL(k_ba_reduce, dim3(16), dim3(256), 0, s, c, a);
         hipLaunchKernelGGL(k_ba_solve, dim3(1), dim3(1024), 0, s, c, a);
-        hipLaunchKernelGGL(k_ba_backsub, dim3((maxL + 255) / 256), dim3(256), 0, s, c, a);
+        hipLaunchKernelGGL(k_ba_backsub, dim3(16 * nb), dim3(256), 0, s, c, a);
     }
 }

@@ -141,11 +141,11 @@ static int alloc_ba(tslam_handle* h) {
         {(void**)&b.T, 8 * P * W * 16},      {(void**)&b.Tfe, 8 * P * W * 16},   {(void**)&b.u, 8 * P * WK},
         {(void**)&b.v, 8 * P * WK},          {(void**)&b.d, 8 * P * WK},         {(void**)&b.lm, 4 * P * WK},
         {(void**)&b.X, 8 * P * WK * 3},      {(void**)&b.remap, 4 * K},          {(void**)&b.cnt, 4 * WK},
-        {(void**)&b.li, 4 * WK},             {(void**)&b.lm_id, 4 * WK},         {(void**)&b.lm_off, 4 * (WK + 1)},
-        {(void**)&b.fill, 4 * WK},           {(void**)&b.lm_obs, 4 * WK},        {(void**)&b.obs_cam, 4 * WK},
+        {(void**)&b.li, 4 * WK},             {(void**)&b.lm_id, 4 * WK},         {(void**)&b.keep, WK},
+        {(void**)&b.camobs, 4 * W * WK},     {(void**)&b.obs_Vg, 8 * WK * 9},    {(void**)&b.obs_cam, 4 * WK},
         {(void**)&b.obs_k, 4 * WK},          {(void**)&b.obs_id, 4 * WK},        {(void**)&b.cam_off, 4 * (W + 1)},
-        {(void**)&b.counts, 4 * 4 * P},      {(void**)&b.obs_W, 8 * WK * 18},    {(void**)&b.obs_Ug, 8 * WK * 27},
-        {(void**)&b.lm_L, 8 * WK * 9},       {(void**)&b.lm_gp, 8 * WK * 3},     {(void**)&b.Qt, 8 * (3 * WK + 4) * 64},
+        {(void**)&b.counts, 4 * 4 * P},      {(void**)&b.tiles, 4 * 2 * TS_BA_TILES},      {(void**)&b.obs_W, 8 * WK * 18},    {(void**)&b.obs_Ug, 8 * WK * 27},
+        {(void**)&b.lm_L, 8 * WK * 6},       {(void**)&b.lm_gp, 8 * WK * 3},     {(void**)&b.C, 8 * 64 * 64},
         {(void**)&b.part, 8 * (size_t)TS_BA_SPLIT * 64 * 64}, {(void**)&b.cam_U, 8 * W * 27}, {(void**)&b.dc, 8 * W * 6},
     };
     for (const A& a : list) {

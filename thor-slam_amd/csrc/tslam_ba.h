@@ -7,15 +7,16 @@
 //   lm   i32 [P][W][K]      landmark id (home slot * K + keypoint) or -1
 //   X    f64 [P][W*K][3]    landmark positions (world), indexed by id
 // Per solve (scratch, shared by the pairs: their solves are ordered on one stream):
-//   observation lists, per-landmark CSR, Jacobian blocks, the Schur columns Qt [3L][64] and the
-//   split-K partials of C = Qt^T Qt.  The camera system is 64 wide: 6 rows per keyframe
+//   observation lists, the camera x landmark observation table, Jacobian blocks and the split-K
+//   partials of the 64 x 64 Schur product C.  The camera system is 64 wide: 6 rows per keyframe
 //   (<= 10 keyframes = 60 rows) and row 60 = the landmark right-hand side.
 #pragma once
 
 #include "tslam_common.h"
 
 #define TS_BA_MAXD 54   // 6 * (TS_BA_MAXW - 1): the reduced camera system without the gauge
-#define TS_BA_SPLIT 128 // split-K blocks of the Schur GEMM
+#define TS_BA_SPLIT 64  // split-K blocks of the Schur GEMM
+#define TS_BA_TILES 128 // scan tiles of a solve's compaction (landmark + observation tiles)
 
 static_assert(6 * TS_BA_MAXW + 1 <= 64, "the BA camera system (6 rows per keyframe + rhs) is 64 wide");
 
@@ -33,20 +34,21 @@ struct BaStore {
     int32_t* cnt;      // [WK] observations per landmark id (after the gate)
     int32_t* li;       // [WK] compact index per id or -1
     int32_t* lm_id;    // [WK] id per compact index
-    int32_t* lm_off;   // [WK+1] CSR offsets
-    int32_t* fill;     // [WK]
-    int32_t* lm_obs;   // [WK] observation indices grouped by landmark
+    uint8_t* keep;     // [W*K] gate result per (window camera, keypoint)
+    int32_t* camobs;   // [W][WK] observation index of (window camera, compact landmark) or -1
     int32_t* obs_cam;  // [WK] window position of the observing keyframe (0 = oldest)
     int32_t* obs_k;    // [WK]
     int32_t* obs_id;   // [WK]
     int32_t* cam_off;  // [W+1]
     int32_t* counts;   // [P][4] n_obs, L, solve ok, pad
-    double* obs_W;     // [WK][18]  W_o = J_c^T J_p (6x3)
-    double* obs_Ug;    // [WK][27]  J_c^T J_c (upper 21) | J_c^T r (6)
-    double* lm_L;      // [WK][9]   Cholesky factor of V_i
-    double* lm_gp;     // [WK][3]
-    double* Qt;        // [3WK+4][64]
+    int32_t* tiles;    // [2][TS_BA_TILES] tile counts, tile offsets
+    double* obs_W;     // [WK][18]  W_o = J_c^T J_p (6x3, row-major), gathered per landmark
+    double* obs_Ug;    // [27][WK]  J_c^T J_c (upper 21) | J_c^T r (6), structure-of-arrays
+    double* obs_Vg;    // [WK][9]   J_p^T J_p (upper 6) | J_p^T r (3), gathered per landmark
+    double* lm_L;      // [6][WK]   (structure-of-arrays)   Cholesky factor of V_i (L00 L10 L11 L20 L21 L22)
+    double* lm_gp;     // [3][WK]
     double* part;      // [TS_BA_SPLIT][64][64]
+    double* C;         // [64][64]
     double* cam_U;     // [W][27]
     double* dc;        // [W][6]
 };
@@ -74,8 +76,9 @@ struct BaPair {
     double* d;
     int32_t* lm;
     double* X;
-    int32_t *remap, *cnt, *li, *lm_id, *lm_off, *fill, *lm_obs, *obs_cam, *obs_k, *obs_id, *cam_off, *counts;
-    double *obs_W, *obs_Ug, *lm_L, *lm_gp, *Qt, *part, *cam_U, *dc;
+    int32_t *remap, *cnt, *li, *lm_id, *camobs, *obs_cam, *obs_k, *obs_id, *cam_off, *counts, *tiles;
+    uint8_t* keep;
+    double *obs_W, *obs_Ug, *obs_Vg, *lm_L, *lm_gp, *part, *C, *cam_U, *dc;
 };
 
 __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, int p) {
@@ -89,10 +92,11 @@ __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, in
     q.d = s.d + p * WK;
     q.lm = s.lm + p * WK;
     q.X = s.X + p * WK * 3;
-    q.remap = s.remap; q.cnt = s.cnt; q.li = s.li; q.lm_id = s.lm_id; q.lm_off = s.lm_off; q.fill = s.fill;
-    q.lm_obs = s.lm_obs; q.obs_cam = s.obs_cam; q.obs_k = s.obs_k; q.obs_id = s.obs_id; q.cam_off = s.cam_off;
+    q.remap = s.remap; q.cnt = s.cnt; q.li = s.li; q.lm_id = s.lm_id; q.keep = s.keep; q.camobs = s.camobs;
+    q.obs_cam = s.obs_cam; q.obs_k = s.obs_k; q.obs_id = s.obs_id; q.cam_off = s.cam_off;
     q.counts = s.counts + 4 * p;
-    q.obs_W = s.obs_W; q.obs_Ug = s.obs_Ug; q.lm_L = s.lm_L; q.lm_gp = s.lm_gp; q.Qt = s.Qt; q.part = s.part;
+    q.tiles = s.tiles;
+    q.obs_W = s.obs_W; q.obs_Ug = s.obs_Ug; q.obs_Vg = s.obs_Vg; q.lm_L = s.lm_L; q.lm_gp = s.lm_gp; q.part = s.part; q.C = s.C;
     q.cam_U = s.cam_U; q.dc = s.dc;
     return q;
 }
