@@ -103,3 +103,43 @@ def test_ba_stage_is_idempotent_per_batch():
         _compare(got, want[3], "frames 0-3, BA stage twice")
     finally:
         h.close()
+
+
+def test_engine_publishes_ba_poses_and_map():
+    """HipSlamEngine with local BA: each published pose is the front end carried by its newest
+    window keyframe's correction (the oracle's window at that frame), get_map returns every
+    keyframe and the window's landmarks, and the drift against ground truth shrinks."""
+    from thor_slam_amd.camera import CameraRig, Extrinsics
+    from thor_slam_amd.params import HipSlamConfig
+    from thor_slam_amd.slam.hip_engine import HipSlamEngine
+
+    from helpers import make_source
+
+    n = 12
+    sc, want = _scenario_and_oracle(n)
+    src = make_source(0)
+    rig = CameraRig([src], rig_extrinsics={src.name: Extrinsics.from_4x4_matrix(src.rig_T_source)})
+    rig.start()
+    eng = HipSlamEngine(num_cameras=2, config=HipSlamConfig(batch_size=1, **dict(BA_ITEMS)))
+    eng.initialize(rig.calibration)
+    bt = src.rig_T_source @ src.get_extrinsics()[0].to_4x4_matrix() @ sc["rect"].left_optical_T_rect()
+    inv = np.linalg.inv
+    poses = []
+    for g in range(n):
+        pose = eng.process_frames(rig.get_synchronized_frames())
+        poses.append(pose)
+        w = want[g]
+        live = {int(f): inv(w["T_cw"][s]) for s, f in enumerate(w["frames"]) if f >= 0}
+        kf = max(f for f in live if f <= g)
+        fe = sc["oracle"]
+        expect = bt @ live[kf] @ inv(fe[kf]["world_T_cam"]) @ fe[g]["world_T_cam"] @ inv(bt)
+        assert rel_frobenius(pose.to_4x4_matrix(), expect) < 1e-9, g
+    smap = eng.get_map()
+    assert [round(p.timestamp, 6) for p in smap.keyframe_poses] == sorted(round(p.timestamp, 6) for p in smap.keyframe_poses)
+    assert len(smap.keyframe_poses) == n // 2
+    assert len(smap.points) == np.unique(want[-1]["lm"][want[-1]["lm"] >= 0]).size
+    assert all(p.observations >= 1 for p in smap.points)
+    gt = inv(src.ground_truth_body(0)) @ src.ground_truth_body(n - 1)
+    fe_err = np.linalg.norm((bt @ sc["oracle"][n - 1]["world_T_cam"] @ inv(bt))[:3, 3] - gt[:3, 3])
+    assert np.linalg.norm(poses[-1].position - gt[:3, 3]) < fe_err
+    eng.shutdown()

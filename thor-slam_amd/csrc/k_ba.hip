@@ -585,22 +585,38 @@ __global__ __launch_bounds__(1024) void k_ba_solve(BatchCtx c, BaArgs a) {
     __shared__ double s_rd[6];
     for (int c0 = 0; c0 < m; c0 += 6) {
         if (threadIdx.x < 64) {
+            // panel in registers: lane = row i (>= c0) holds its 6 block entries and its rhs; the
+            // pivot row's entries come by readlane (lane j - c0), so the 6 steps need no LDS trip
             const int i = c0 + (int)threadIdx.x;
-            for (int j = c0; j < c0 + 6; ++j) {
-                const double dj = s_S[j * mp + j];
+            const bool row = i < m;
+            double pv[6], rh = row ? s_S[i * mp + m] : 0.0;
+#pragma unroll
+            for (int e = 0; e < 6; ++e) pv[e] = row ? s_S[i * mp + c0 + e] : 0.0;
+            bool good = true;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const double dj = readlane_f64(pv[j], j);
                 if (!(dj > 0.0)) {   // uniform across the wave
-                    if (threadIdx.x == 0) s_ok = 0;
+                    good = false;
                     break;
                 }
                 const double rj = 1.0 / dj;
-                if (threadIdx.x == 0) s_rd[j - c0] = rj;
-                if (i > j && i < m) {
-                    const double sij = s_S[i * mp + j] * rj;
-                    for (int k = j + 1; k < c0 + 6 && k <= i; ++k) s_S[i * mp + k] -= sij * s_S[k * mp + j];
-                    s_S[i * mp + m] -= sij * s_S[j * mp + m];
+                const double sij = pv[j] * rj;
+                const double rhj = readlane_f64(rh, j);
+                const bool below = (int)threadIdx.x > j && row;
+#pragma unroll
+                for (int k = j + 1; k < 6; ++k) {
+                    const double skj = readlane_f64(pv[j], k);   // S[c0 + k][c0 + j]
+                    if (below && k <= (int)threadIdx.x) pv[k] -= sij * skj;
                 }
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                __builtin_amdgcn_wave_barrier();
+                if (below) rh -= sij * rhj;
+                if (threadIdx.x == 0) s_rd[j] = rj;
+            }
+            if (!good && threadIdx.x == 0) s_ok = 0;
+            if (row) {
+#pragma unroll
+                for (int e = 0; e < 6; ++e) s_S[i * mp + c0 + e] = pv[e];
+                s_S[i * mp + m] = rh;
             }
         }
         __syncthreads();
@@ -631,8 +647,8 @@ __global__ __launch_bounds__(1024) void k_ba_solve(BatchCtx c, BaArgs a) {
         const double rk = k < m ? 1.0 / s_S[k * mp + k] : 1.0;
         double r = k < m ? s_S[k * mp + m] * rk : 0.0;
         for (int i = m - 1; i >= 0; --i) {
-            const double xi = __shfl(r, i, 64);
-            if (k < i) r -= (s_S[i * mp + k] * rk) * xi;
+            const double lik = k < i ? s_S[i * mp + k] * rk : 0.0;   // independent of the chain
+            r -= lik * readlane_f64(r, i);
         }
         if (k < m) s_x[k] = r;
     }

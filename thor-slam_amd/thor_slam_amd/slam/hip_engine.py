@@ -16,6 +16,12 @@ Drop-in replacement for ``IsaacRosAdapter`` (``thor_slam/slam/adapters/isaac_ros
 
 Poses are world_T_base (base_link of the rig; world = base_link at the first frame), obtained by
 conjugating the tracked rectified-left-camera motion with base_T_camera from the calibration.
+With local BA on (``ba_window > 0``, SURVEY.md §8a A8, one stereo pair) a frame's pose is the
+front-end pose carried by the correction of the newest keyframe at or before it that is still in
+the window, ``W_ba(kf) inv(W_fe(kf)) W_fe(g)`` (the oldest window keyframe's when the batch has
+already evicted it), and ``get_map`` returns the keyframes (BA estimates) and the window's
+landmarks.  With several pairs each keeps its own window (``handle.ba_read(p)``); the published
+pose stays the fused front end and ``get_map`` uses pair 0.
 ``confidence`` follows isaac_ros.py:312.  With ``batch_size > 1`` frames are staged and the
 batch runs on the GPU when full (or on ``flush``); the returned pose is then the latest completed
 one, as the reference allows (its pose lags the published frame, isaac_ros.py:429-430).
@@ -78,6 +84,10 @@ class HipSlamEngine(SlamEngine):
         self._dev_images = None
         self._host_images = None
         self._keyframe_poses: list[SlamPose] = []
+        self._fe_at: dict[int, np.ndarray] = {}      # front-end rect world_T_cam of BA keyframes
+        self._kf_final: dict[int, np.ndarray] = {}   # last BA estimate (rect world_T_cam) per keyframe
+        self._kf_stamp: dict[int, float] = {}
+        self._ba_window: dict | None = None
 
     # ------------------------------------------------------------------------------------------
     def initialize(self, calibration: RigCalibration, config: SlamConfig | None = None) -> None:
@@ -195,11 +205,43 @@ class HipSlamEngine(SlamEngine):
         best = int(np.argmax([res["stats"][k, p, 2] if ok[p] else -1 for p in range(len(ok))]))
         return POSE_OK, self._world_T_base.copy(), rot6 @ res["cov"][k, best] @ rot6.T
 
+    def _ba_corrections(self, res: dict, n: int):
+        """Per frame of the batch: the rect-frame correction W_ba(kf) inv(W_fe(kf)) (or None)."""
+        cfg = self._config
+        if cfg.ba_window <= 0:
+            return None
+        g0 = self._handle.frames_done - n
+        for k in range(n):
+            if (g0 + k) % cfg.ba_kf_interval == 0:
+                self._fe_at[g0 + k] = res["T_abs"][k, 0].copy()
+        win = self._handle.ba_read(0)
+        self._ba_window = win
+        live = {}
+        for s_, f in enumerate(win["frames"]):
+            if f >= 0:
+                live[int(f)] = _invert(win["T_cw"][s_])
+                self._kf_final[int(f)] = live[int(f)]
+        for f in [f for f in self._fe_at if f not in live and f < min(live, default=0)]:
+            del self._fe_at[f]   # evicted: its final estimate is kept in _kf_final
+        if not live or len(self._pairs) != 1:
+            return None
+        frames = sorted(live)
+        out = []
+        for k in range(n):
+            g = g0 + k
+            kf = max([f for f in frames if f <= g], default=frames[0])
+            out.append(live[kf] @ _invert(self._fe_at[kf]))
+        return out
+
     def _publish(self, res: dict, stamps: list[float]) -> None:
         latest = None
         state = self._state
+        corr = self._ba_corrections(res, len(stamps))
+        bt = self._base_T_rect
         for k, ts in enumerate(stamps):
             status, body, cov = self._body_pose(res, k)
+            if corr is not None and status != POSE_LOST:
+                body = bt @ corr[k] @ res["T_abs"][k, 0] @ _invert(bt)
             if status == POSE_LOST:
                 state = TrackingState.LOST
                 latest = None
@@ -215,6 +257,9 @@ class HipSlamEngine(SlamEngine):
             )
             if status == POSE_INIT:
                 self._keyframe_poses.append(latest)
+            g = self._handle.frames_done - len(stamps) + k
+            if self._config.ba_window > 0 and g % self._config.ba_kf_interval == 0:
+                self._kf_stamp[g] = ts
         with self._pose_lock:
             self._latest_pose = latest
             self._state = state
@@ -225,10 +270,27 @@ class HipSlamEngine(SlamEngine):
         return self._state
 
     def get_map(self) -> SlamMap:
-        """Keyframe poses so far plus the stereo points of the newest frame (world frame)."""
-        smap = SlamMap(keyframe_poses=list(self._keyframe_poses))
-        if self._handle is None or self._handle.frames_done == 0:
-            return smap
+        """Without BA: the (re)initialisation poses.  With BA: every keyframe so far at its latest
+        BA estimate (world_T_base) and the landmarks of pair 0's window (world frame, with their
+        observation counts)."""
+        if self._config.ba_window <= 0 or self._ba_window is None:
+            smap = SlamMap(keyframe_poses=list(self._keyframe_poses))
+        else:
+            bt = self._base_T_rect
+            kfs = []
+            for f in sorted(self._kf_final):
+                body = bt @ self._kf_final[f] @ _invert(bt)
+                kfs.append(SlamPose(position=body[:3, 3].copy(), rotation=Rotation.from_matrix(body[:3, :3]).as_quat(),
+                                    timestamp=self._kf_stamp.get(f, float(f)), tracking_state=TrackingState.TRACKING,
+                                    confidence=1.0))
+            win = self._ba_window
+            occ = win["frames"] >= 0
+            ids, counts = np.unique(win["lm"][occ], return_counts=True)
+            keep = ids >= 0
+            ids, counts = ids[keep], counts[keep]
+            pts = win["X"][ids] @ bt[:3, :3].T + bt[:3, 3]
+            smap = SlamMap(points=[MapPoint(position=p.copy(), observations=int(c)) for p, c in zip(pts, counts)],
+                           keyframe_poses=kfs)
         pose = self._latest_pose
         if pose is not None:
             smap.timestamp = pose.timestamp
@@ -239,6 +301,7 @@ class HipSlamEngine(SlamEngine):
             self._latest_pose = None
         self._staged = []
         self._keyframe_poses = []
+        self._fe_at, self._kf_final, self._kf_stamp, self._ba_window = {}, {}, {}, None
         self._world_T_base = np.eye(4)
         if self._handle is not None:
             self._handle.reset()
