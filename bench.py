@@ -1,6 +1,7 @@
 """Throughput bench: synced stereo frames/sec (detect + match + pose) @ 640x400 on MI355X.
 
 python bench.py --gpus N --steps K --warmup W   (N > 1 under torch.distributed.run, one rank/GPU)
+python bench.py --config c4                     (BASELINE.json configs[3]: 1280x800, K=4000, + local BA)
 
 * workload (BASELINE.json configs[1], C2): one stereo pair 640x400 per GPU, K=2000 ORB-style
   keypoints per image, synthetic room sequence (seed = rank); a *step* = one batch of
@@ -15,6 +16,9 @@ python bench.py --gpus N --steps K --warmup W   (N > 1 under torch.distributed.r
 * roofline: per-kernel HIP-event timing of one batch run kernel by kernel on the same stream,
   for the dominant kernel: algorithmic bytes / average duration vs 8 TB/s.
 * cpu_baseline (rank 0, N=1 context): the NumPy oracle on a bounded sample of the same frames.
+* --config c4: the same step plus the A8 stage (every 5th frame a keyframe of a 10-keyframe
+  window, 5 Gauss-Newton iterations per keyframe); the roofline is then that of the dominant
+  kernel of the step, the FP64-MFMA Schur product when it dominates (HIP events around its launches).
 """
 
 from __future__ import annotations
@@ -35,7 +39,9 @@ for _p in (ROOT, ROOT / "thor-slam_amd"):
         sys.path.insert(0, str(_p))
 
 METRIC = "synced stereo frames/sec (detect+match+pose) @640×400, 1/2/4/8 GPU"
+METRIC_C4 = "synced stereo frames/sec (detect+match+pose+10-keyframe local BA) @1280×800, 1 GPU"
 HBM_PEAK_GBS = 8000.0
+FP64_MFMA_PEAK_TFS = 78.6   # MI355X FP64 matrix peak (AMD spec; the microarch guide lists no FP64 row)
 # bench kernel label -> device symbol (rocprofv3 / PMC summaries); "pose" is k_corr+k_ransac+k_refine
 KERNEL_SYMBOL = {"rectify_pyramid": "k_rectify_pyramid", "detect": "k_detect", "select": "k_select",
                  "describe": "k_describe", "match": "k_match", "match_refine": "k_refine_temporal",
@@ -43,24 +49,24 @@ KERNEL_SYMBOL = {"rectify_pyramid": "k_rectify_pyramid", "detect": "k_detect", "
 
 
 def _render_chunk(args):
-    seed, idx = args
+    seed, idx, width, height = args
     from thor_slam_amd.synthetic import SyntheticStereoSource
 
-    src = SyntheticStereoSource(seed=seed, n_frames=max(idx) + 1)
+    src = SyntheticStereoSource(seed=seed, n_frames=max(idx) + 1, width=width, height=height)
     return [src.render_stereo_sequence(1, start=i)[0] for i in idx]
 
 
-def render_frames(seed: int, n: int, workers: int) -> np.ndarray:
+def render_frames(seed: int, n: int, workers: int, width: int = 640, height: int = 400) -> np.ndarray:
     idx = list(range(n))
     chunks = [idx[i::workers] for i in range(workers) if idx[i::workers]]
-    out = np.empty((n, 2, 400, 640), dtype=np.uint8)
+    out = np.empty((n, 2, height, width), dtype=np.uint8)
     if workers <= 1:
         for c in chunks:
-            for i, fr in zip(c, _render_chunk((seed, c))):
+            for i, fr in zip(c, _render_chunk((seed, c, width, height))):
                 out[i] = fr
         return out
     with ProcessPoolExecutor(max_workers=workers) as ex:
-        for c, frs in zip(chunks, ex.map(_render_chunk, [(seed, c) for c in chunks])):
+        for c, frs in zip(chunks, ex.map(_render_chunk, [(seed, c, width, height) for c in chunks])):
             for i, fr in zip(c, frs):
                 out[i] = fr
     return out
@@ -110,12 +116,22 @@ def _oracle_worker(args):
     from oracle import numpy_slam as O
     from thor_slam_amd.params import HipSlamConfig
 
-    trk = O.OracleTracker(HipSlamConfig(**cfg_d), rect_d)
+    cfg = HipSlamConfig(**cfg_d)
+    trk = O.OracleTracker(cfg, rect_d)
+    bat = None
+    if cfg.ba_window > 0:
+        from oracle.numpy_ba import BAParams, BATracker
+
+        bat = BATracker(cfg.n_features, (rect_d["fx"], rect_d["fy"], rect_d["cx"], rect_d["cy"],
+                                         rect_d["fx"] * rect_d["baseline"]),
+                        BAParams(cfg.ba_window, cfg.ba_kf_interval, cfg.ba_iters, cfg.ba_lambda, cfg.ba_outlier_px))
     n = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
         i = n % len(frames)
-        trk.step(frames[i, 0], frames[i, 1])
+        res = trk.step(frames[i, 0], frames[i, 1])
+        if bat is not None:
+            bat.step(res)
         n += 1
     return n, time.perf_counter() - t0
 
@@ -137,8 +153,9 @@ def cpu_baseline(frames: np.ndarray, rect, cfg, budget_s: float, procs: int) -> 
     n = sum(r[0] for r in results)
     wall = max(r[1] for r in results)
     return {"value": n / wall, "unit": "frames/s", "cores": len(chunks), "kind": "port",
-            "sample": f"{n} synthetic 640x400 stereo frames (seed 0, {len(frames)} distinct, replayed per process), "
-                      f"NumPy oracle, {len(chunks)} process(es) x {budget_s:.0f} s"}
+            "sample": f"{n} synthetic {frames.shape[3]}x{frames.shape[2]} stereo frames (seed 0, {len(frames)} distinct, "
+                      f"replayed per process), NumPy oracle{' + local BA' if cfg.ba_window else ''}, "
+                      f"{len(chunks)} process(es) x {budget_s:.0f} s"}
 
 
 def main() -> None:
@@ -146,8 +163,9 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="stereo frames per step")
-    ap.add_argument("--unique", type=int, default=48, help="distinct rendered frames (triangle-wave replay)")
+    ap.add_argument("--config", choices=["c2", "c4"], default="c2", help="BASELINE.json configs[1] (c2) or configs[3] (c4)")
+    ap.add_argument("--batch", type=int, default=0, help="stereo frames per step (0 = 256 for c2, 50 for c4)")
+    ap.add_argument("--unique", type=int, default=0, help="distinct rendered frames, triangle-wave replay (0 = 48 / 24)")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU baseline (0 = skip)")
     ap.add_argument("--cpu-procs", type=int, default=8, help="oracle processes for the CPU baseline")
     ap.add_argument("--latency-frames", type=int, default=20, help="B=1 submissions timed for latency_b1_ms")
@@ -180,15 +198,20 @@ def main() -> None:
         else:
             dist.init_process_group(args.dist_backend)
 
-    cfg = HipSlamConfig()
-    B = args.batch
-    src = SyntheticStereoSource(seed=rank, n_frames=args.unique)
+    c4 = args.config == "c4"
+    if c4 and world > 1:
+        raise SystemExit("--config c4 is a single-GPU configuration")
+    width, height = (1280, 800) if c4 else (640, 400)
+    cfg = HipSlamConfig(n_features=4000, ba_window=10, ba_kf_interval=5, ba_iters=5) if c4 else HipSlamConfig()
+    B = args.batch or (50 if c4 else 256)
+    args.unique = args.unique or (24 if c4 else 48)
+    src = SyntheticStereoSource(seed=rank, n_frames=args.unique, width=width, height=height)
     cams = extract_cameras(CameraRig([src]).calibration, 2)
     (li, ri), = stereo_pairs(cams)
     rect = stereo_rectify(cams[li], cams[ri])
     workers = max(1, min(16, (os.cpu_count() or 2) // max(1, world), args.unique))
     t_r = time.perf_counter()
-    uniq = render_frames(rank, args.unique, workers)
+    uniq = render_frames(rank, args.unique, workers, width, height)
     t_render = time.perf_counter() - t_r
 
     total = (args.warmup + args.steps) * B
@@ -204,7 +227,7 @@ def main() -> None:
     exchanges = [FeatureExchange(layout, "cuda" if on_device else "cpu", world) for _ in range(2)] if world > 1 else []
     pending = [None, None]
     staging = torch.empty((layout.rank_bytes,), dtype=torch.uint8, device="cuda") if world > 1 and not on_device else None
-    names = list(KERNELS)
+    names = list(KERNELS) + (["local_ba"] if c4 else [])
     n_ev = len(names) + 1
 
     def step(s: int, evs=None) -> None:
@@ -214,7 +237,10 @@ def main() -> None:
         if evs is not None:
             evs[0].record(stream)
         for i, k in enumerate(names):
-            h.run_kernel(k, sp)
+            if k == "local_ba":
+                h.run_stage("ba", sp)
+            else:
+                h.run_kernel(k, sp)
             if evs is not None:
                 evs[i + 1].record(stream)
         h.end_batch()
@@ -245,6 +271,8 @@ def main() -> None:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if c4:   # arm the Schur-kernel events (launches per step: keyframes x iterations)
+        h.ba_profile(max_launches=args.steps * (B // cfg.ba_kf_interval + 1) * cfg.ba_iters)
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(args.warmup + k, events[k])
@@ -266,10 +294,21 @@ def main() -> None:
     for evs in events:
         for i, k in enumerate(names):
             per_kernel_us[k] += evs[i].elapsed_time(evs[i + 1]) * 1e3 / args.steps  # us
-    dom = max(per_kernel_us, key=per_kernel_us.get)
     unit_bytes = frame_bytes(rect.width, rect.height, cfg.n_features)
     dom_bytes = unit_bytes * B          # §8d per-frame bytes x the frames one launch processes
+    schur = h.ba_profile(0) if c4 else None
+    front = {k: v for k, v in per_kernel_us.items() if k != "local_ba"}
+    dom = max(front, key=front.get)
     achieved = dom_bytes / (per_kernel_us[dom] * 1e-6) / 1e9
+    mfma = None
+    if schur and schur["launches"]:
+        avg_us = schur["ms"] * 1e3 / schur["launches"]
+        flops = schur["flops"] / schur["launches"]
+        mfma = {"bound": "mfma", "kernel": "k_ba_schur", "achieved": flops / (avg_us * 1e-6) / 1e12,
+                "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s", "traffic": None, "dtype": "f64",
+                "algorithmic_flops_per_launch": flops, "avg_launch_us": avg_us, "launches_timed": schur["launches"],
+                "time_per_step_us": schur["ms"] * 1e3 / args.steps}
+        mfma["frac"] = mfma["achieved"] / mfma["peak"]
 
     traffic = None
     pmc_path = Path(args.pmc)
@@ -295,8 +334,32 @@ def main() -> None:
         lat_ms = float(np.median(lat))
 
     frames_total = world * args.steps * B
+    roofline = {
+        "bound": "hbm",
+        "kernel": dom,
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "traffic": traffic,
+        "algorithmic_bytes_per_launch": dom_bytes,
+        "algorithmic_bytes_per_frame": unit_bytes,
+        "frames_per_launch": B,
+        "avg_launch_us": per_kernel_us[dom],
+        "kernel_own_bytes_per_launch": kernel_bytes(dom, B, h, cfg, rect.is_identity),
+        "end_to_end_hbm_frac": unit_bytes * (frames_total / elapsed / world) / (HBM_PEAK_GBS * 1e9),
+    }
+    if mfma is not None and mfma["time_per_step_us"] > per_kernel_us[dom]:
+        roofline, front_roofline = mfma, roofline   # the Schur product is the step's dominant kernel
+    else:
+        front_roofline = None
+    workload = ("C4: 1x stereo pair 1280x800, 4000 FAST/rBRIEF keypoints per image, 4 levels, stereo+temporal "
+                "brute-force Hamming, P3P-RANSAC(128)+GN pose, 10-keyframe local BA (keyframe every 5 frames, "
+                "5 Gauss-Newton iterations, Schur complement on FP64 MFMA)") if c4 else (
+                "C2: 1x stereo pair 640x400 per GPU, 2000 FAST/rBRIEF keypoints per image, 4 levels, "
+                "stereo+temporal brute-force Hamming, P3P-RANSAC(128)+GN pose")
     out = {
-        "metric": METRIC,
+        "metric": METRIC_C4 if c4 else METRIC,
         "value": frames_total / elapsed,
         "unit": "frames/s",
         "n_gpus": world,
@@ -306,36 +369,23 @@ def main() -> None:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u8",
-        "data": f"synthetic: seeded room renderer, {args.unique} distinct 640x400 stereo frames per rank replayed "
-                "as a triangle wave, resident in HBM before timing",
+        "dtype": "u8" + ("+f64" if c4 else ""),
+        "data": f"synthetic: seeded room renderer, {args.unique} distinct {width}x{height} stereo frames per rank "
+                "replayed as a triangle wave, resident in HBM before timing",
         "config": {
-            "workload": "C2: 1x stereo pair 640x400 per GPU, 2000 FAST/rBRIEF keypoints per image, 4 levels, "
-                        "stereo+temporal brute-force Hamming, P3P-RANSAC(128)+GN pose",
+            "workload": workload,
             "frames_per_step": B,
             "n_features": cfg.n_features,
             "parallelism": f"one stereo source per GPU x{world}" + (" + RCCL all-gather of keypoints/descriptors" if world > 1 else ""),
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": dom,
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "algorithmic_bytes_per_launch": dom_bytes,
-            "algorithmic_bytes_per_frame": unit_bytes,
-            "frames_per_launch": B,
-            "avg_launch_us": per_kernel_us[dom],
-            "kernel_own_bytes_per_launch": kernel_bytes(dom, B, h, cfg, rect.is_identity),
-            "end_to_end_hbm_frac": unit_bytes * (frames_total / elapsed / world) / (HBM_PEAK_GBS * 1e9),
-        },
+        "roofline": roofline,
         "latency_b1_ms": lat_ms,
         "per_kernel_us_per_batch": per_kernel_us,
         "tracking_ok_fraction_last_batch": ok_frac,
         "render_s": t_render,
     }
+    if front_roofline is not None:
+        out["front_end_roofline"] = front_roofline
     if rank == 0 and args.cpu_budget > 0:
         out["cpu_baseline"] = cpu_baseline(uniq, rect, cfg, args.cpu_budget, args.cpu_procs)
         out["cpu_baseline"]["host_cpus_visible"] = os.cpu_count()

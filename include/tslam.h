@@ -185,6 +185,12 @@ int tslam_layout(tslam_handle* h, int64_t* out16, int32_t* level_info18);
 int tslam_ba_read(tslam_handle* h, int pair, int64_t* frames, double* cam_T_world, int32_t* landmark,
                   double* points, double* obs_uvd, int32_t* counts);
 
+/* A8 profiling (synchronises): returns the total HIP-event time and count of the Schur-product
+ * kernel (k_ba_schur) launches timed since the previous call and their algorithmic flops
+ * (2 (6n+1)^2 3L per launch, n keyframes, L landmarks), then re-arms timing for up to
+ * `max_launches` further launches (0 = off). */
+int tslam_ba_profile(tslam_handle* h, int max_launches, double* schur_ms, int64_t* schur_launches, double* schur_flops);
+
 int tslam_pack_features(tslam_handle* h, void* dst, int64_t* bytes, void* stream);
 
 #ifdef __cplusplus

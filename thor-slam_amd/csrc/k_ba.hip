@@ -524,6 +524,10 @@ __global__ __launch_bounds__(256) void k_ba_schur(BatchCtx c, BaArgs a) {
         }
         __syncthreads();
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {   // algorithmic flops of the dense Schur product
+        const double rows = 6.0 * n + 1.0;
+        q.flops[0] += 2.0 * rows * rows * 3.0 * L;
+    }
     double* out = q.part + (size_t)blockIdx.x * 64 * 64;
     const int a0 = 16 * wave;
     // C/D layout of v_mfma_f64_16x16x4f64: col = lane & 15, row = (lane >> 4) + 4 * reg
@@ -744,7 +748,7 @@ void launch_ba_keyframe(const BatchCtx& c, const BaArgs& a, bool evict, hipStrea
     hipLaunchKernelGGL(k_ba_insert, dim3((K + 255) / 256), dim3(256), 0, s, c, a);
 }
 
-void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s) {
+void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing) {
     // grids sized for the window's maximum (counts live on the device; threads past them exit)
     const int WK = a.W * c.g.K;
     const int nb = (WK + 255) / 256;
@@ -759,7 +763,10 @@ void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s) {
     for (int it = 0; it < a.iters; ++it) {
         hipLaunchKernelGGL(k_ba_jac, dim3(nb), dim3(256), 0, s, c, a);
         hipLaunchKernelGGL(k_ba_camred, dim3(a.n_order * 27), dim3(64), 0, s, c, a);
+        const bool rec = timing && timing->used < timing->cap;
+        if (rec) (void)hipEventRecord(timing->ev[2 * timing->used], s);
         hipLaunchKernelGGL(k_ba_schur, dim3(a.nsplit), dim3(256), 0, s, c, a);
+        if (rec) (void)hipEventRecord(timing->ev[2 * timing->used++ + 1], s);
         hipLaunchKernelGGL(k_ba_reduce, dim3(16), dim3(256), 0, s, c, a);
         hipLaunchKernelGGL(k_ba_solve, dim3(1), dim3(1024), 0, s, c, a);
         hipLaunchKernelGGL(k_ba_backsub, dim3(16 * nb), dim3(256), 0, s, c, a);

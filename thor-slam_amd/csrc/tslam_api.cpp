@@ -69,6 +69,8 @@ struct tslam_handle {
     int64_t ba_frame[TS_BA_MAXW]{};
     int64_t ba_nkf = 0;
     int64_t ba_last = -1;    // newest frame inserted
+    BaTiming ba_timing{};    // k_ba_schur events while profiling is on
+    std::vector<hipEvent_t> ba_events;
 };
 
 static int dev_alloc(tslam_handle* h, void** p, size_t bytes) {
@@ -147,6 +149,7 @@ static int alloc_ba(tslam_handle* h) {
         {(void**)&b.counts, 4 * 4 * P},      {(void**)&b.tiles, 4 * 2 * TS_BA_TILES},      {(void**)&b.obs_W, 8 * WK * 18},    {(void**)&b.obs_Ug, 8 * WK * 27},
         {(void**)&b.lm_L, 8 * WK * 6},       {(void**)&b.lm_gp, 8 * WK * 3},     {(void**)&b.C, 8 * 64 * 64},
         {(void**)&b.part, 8 * (size_t)TS_BA_SPLIT * 64 * 64}, {(void**)&b.cam_U, 8 * W * 27}, {(void**)&b.dc, 8 * W * 6},
+        {(void**)&b.flops, 8},
     };
     for (const A& a : list) {
         const int rc = dev_alloc(h, a.p, a.bytes);
@@ -204,7 +207,7 @@ static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s) {
         a.n_order = ba_order(h, -1, a.order);
         for (int p = 0; p < h->P; ++p) {
             a.pair = p;
-            launch_ba_solve(c, a, s);
+            launch_ba_solve(c, a, s, h->ba_timing.ev ? &h->ba_timing : nullptr);
         }
     }
 }
@@ -407,6 +410,7 @@ int tslam_destroy(tslam_handle* h) {
     if (!h) return TSLAM_OK;
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();
+    for (hipEvent_t e : h->ba_events) (void)hipEventDestroy(e);
     free_all(h);
     delete h;
     return TSLAM_OK;
@@ -622,6 +626,40 @@ int tslam_ba_read(tslam_handle* h, int pair, int64_t* frames, double* cam_T_worl
         HIPCHK(hipMemcpy(obs_uvd + 2 * WK, b.d + pair * WK, 8 * WK, hipMemcpyDeviceToHost));
     }
     if (counts) HIPCHK(hipMemcpy(counts, b.counts + 4 * pair, 4 * 4, hipMemcpyDeviceToHost));
+    return TSLAM_OK;
+}
+
+int tslam_ba_profile(tslam_handle* h, int max_launches, double* schur_ms, int64_t* schur_launches, double* schur_flops) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
+    int rc = tslam_sync(h);
+    if (rc != TSLAM_OK) return rc;
+    BaTiming& t = h->ba_timing;
+    double ms = 0.0;
+    for (int i = 0; i < t.used; ++i) {
+        float e = 0.0f;
+        HIPCHK(hipEventElapsedTime(&e, t.ev[2 * i], t.ev[2 * i + 1]));
+        ms += e;
+    }
+    double fl = 0.0;
+    HIPCHK(hipMemcpy(&fl, h->ba.flops, sizeof(double), hipMemcpyDeviceToHost));
+    if (schur_ms) *schur_ms = ms;
+    if (schur_launches) *schur_launches = t.used;
+    if (schur_flops) *schur_flops = t.ev ? fl : 0.0;
+    // restart: (re)arm with room for max_launches timed launches, or disarm with 0
+    const double zero = 0.0;
+    HIPCHK(hipMemcpy(h->ba.flops, &zero, sizeof(double), hipMemcpyHostToDevice));
+    t.used = 0;
+    if (max_launches < 0) return fail(TSLAM_EINVAL, "max_launches must be >= 0");
+    if ((size_t)max_launches * 2 > h->ba_events.size()) {
+        while (h->ba_events.size() < (size_t)max_launches * 2) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreate(&e));
+            h->ba_events.push_back(e);
+        }
+    }
+    t.ev = max_launches ? h->ba_events.data() : nullptr;
+    t.cap = max_launches;
     return TSLAM_OK;
 }
 

@@ -51,6 +51,7 @@ struct BaStore {
     double* C;         // [64][64]
     double* cam_U;     // [W][27]
     double* dc;        // [W][6]
+    double* flops;     // [1] algorithmic Schur-product flops accumulated (profiling)
 };
 
 struct BaArgs {
@@ -78,7 +79,7 @@ struct BaPair {
     double* X;
     int32_t *remap, *cnt, *li, *lm_id, *camobs, *obs_cam, *obs_k, *obs_id, *cam_off, *counts, *tiles;
     uint8_t* keep;
-    double *obs_W, *obs_Ug, *obs_Vg, *lm_L, *lm_gp, *part, *C, *cam_U, *dc;
+    double *obs_W, *obs_Ug, *obs_Vg, *lm_L, *lm_gp, *part, *C, *cam_U, *dc, *flops;
 };
 
 __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, int p) {
@@ -97,9 +98,14 @@ __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, in
     q.counts = s.counts + 4 * p;
     q.tiles = s.tiles;
     q.obs_W = s.obs_W; q.obs_Ug = s.obs_Ug; q.obs_Vg = s.obs_Vg; q.lm_L = s.lm_L; q.lm_gp = s.lm_gp; q.part = s.part; q.C = s.C;
-    q.cam_U = s.cam_U; q.dc = s.dc;
+    q.cam_U = s.cam_U; q.dc = s.dc; q.flops = s.flops;
     return q;
 }
 
 void launch_ba_keyframe(const BatchCtx& c, const BaArgs& a, bool evict, hipStream_t s);
-void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s);
+// timing: when non-null, an event pair is recorded around every k_ba_schur launch (profiling)
+struct BaTiming {
+    hipEvent_t* ev;   // 2 * cap events
+    int cap, used;
+};
+void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing);

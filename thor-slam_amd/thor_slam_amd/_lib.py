@@ -83,6 +83,8 @@ _SIGNATURES = {
     "tslam_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_pack_features": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
     "tslam_ba_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6),
+    "tslam_ba_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
 }
 
 
@@ -270,6 +272,13 @@ class Handle:
         _check(self.lib.tslam_ba_read(self.h, int(pair), *(a.ctypes.data for a in (frames, T, lm, X, uvd, cnt))))
         return {"frames": frames, "T_cw": T, "lm": lm.astype(np.int64), "X": X, "u": uvd[0], "v": uvd[1],
                 "d": uvd[2], "n_obs": int(cnt[0]), "n_lm": int(cnt[1]), "ok": bool(cnt[2])}
+
+    def ba_profile(self, max_launches: int = 0) -> dict:
+        """Schur-kernel HIP-event time / launches / algorithmic flops since the last call; re-arms
+        timing for up to ``max_launches`` launches (0 = off).  Synchronises."""
+        ms, n, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        _check(self.lib.tslam_ba_profile(self.h, int(max_launches), ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl)))
+        return {"ms": ms.value, "launches": int(n.value), "flops": fl.value}
 
     # -- decoding helpers (tests / map export) ---------------------------------------------
     def keypoints(self, global_frame: int, cam: int) -> dict:
