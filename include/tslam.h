@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 2
+#define TSLAM_ABI_VERSION 3
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -87,6 +87,12 @@ typedef struct {
     int32_t ba_pad;               /* reserved, 0                                              */
     double ba_lambda;
     double ba_outlier_px;
+    /* RGB-D input (BASELINE configs[4]): each "pair" is one colour camera with a depth image
+     * aligned to it; per frame and camera the submitted record is [BGR u8 H*W*3 | depth u16 mm
+     * H*W] (images = [n][n_pairs][5*H*W] bytes; W*H even).  tslam_stereo_desc gives the colour
+     * camera (baseline ignored, map_right unused); the stereo stage becomes a depth lookup. */
+    int32_t rgbd;
+    int32_t rgbd_pad;             /* reserved, 0                                              */
 } tslam_params;
 
 /* Buffers exposed for parity tests (tslam_buffer_info / tslam_copy_out / tslam_copy_in). */

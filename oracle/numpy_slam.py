@@ -17,6 +17,11 @@ Stages for one stereo frame (left L, right R):
   A6 match     brute-force Hamming per level: stereo (row band, positive disparity) and temporal
                (window) with ratio test + mutual check
   A7 pose      triangulate t-1 stereo matches, P3P-RANSAC with a counter RNG, Gauss-Newton refine
+
+RGB-D frames (BASELINE configs[4], ``OracleTracker.step_rgbd``): the BGR colour image becomes
+gray with fixed-point BT.601 weights, is undistorted like A2, and instead of A6 stereo every
+keypoint reads the aligned depth (u16 mm) at its nearest raw pixel: disp = fx / Z, a virtual
+1 m baseline, so A7 triangulates exactly as for stereo.
 """
 
 from __future__ import annotations
@@ -163,6 +168,34 @@ def remap(img: np.ndarray, mp: np.ndarray) -> np.ndarray:
     acc = (tap(x0, y0) * (32 - fx) * (32 - fy) + tap(x0 + 1, y0) * fx * (32 - fy)
            + tap(x0, y0 + 1) * (32 - fx) * fy + tap(x0 + 1, y0 + 1) * fx * fy)
     return ((acc + 512) >> 10).astype(np.uint8)
+
+
+def bgr_to_gray(bgr: np.ndarray) -> np.ndarray:
+    """RGB-D input: (R*4899 + G*9617 + B*1868 + 8192) >> 14 on the BGR u8 image."""
+    b = bgr[..., 0].astype(np.int64)
+    g = bgr[..., 1].astype(np.int64)
+    r = bgr[..., 2].astype(np.int64)
+    return ((r * 4899 + g * 9617 + b * 1868 + 8192) >> 14).astype(np.uint8)
+
+
+def depth_disparity(feat: dict, depth_mm: np.ndarray, mp: np.ndarray | None, fx: float) -> np.ndarray:
+    """RGB-D stand-in for A6 stereo: per keypoint, the depth at the raw pixel nearest to its level-0
+    position (rounded, then through the undistortion table ``mp`` when given) as disp = fx / Z
+    (Z = mm * 0.001; NaN for padding keypoints and zero depth)."""
+    h, w = depth_mm.shape
+    kp = feat["kp"]
+    u, v = level0_coords(kp["x"], kp["y"], kp["level"])
+    ix = np.clip(np.floor(u + 0.5).astype(np.int64), 0, w - 1)
+    iy = np.clip(np.floor(v + 0.5).astype(np.int64), 0, h - 1)
+    if mp is not None:
+        m = mp[iy, ix].astype(np.int64)
+        ix = np.clip((m[:, 0] + 16) >> RECT_BITS, 0, w - 1)
+        iy = np.clip((m[:, 1] + 16) >> RECT_BITS, 0, h - 1)
+    mm = depth_mm[iy, ix].astype(np.int64)
+    ok = feat["valid"] & (mm > 0)
+    with np.errstate(divide="ignore"):
+        disp = fx / (mm.astype(np.float64) * 0.001)
+    return np.where(ok, disp, np.nan)
 
 
 # ----------------------------------------------------------------------------------------
@@ -790,13 +823,27 @@ class OracleTracker:
         disp = stereo_subpixel(fl, fr, sm[0], fl["levels"], fr["levels"])
         cur = {"left": fl, "right": fr, "stereo": sm[0], "stereo_full": sm, "disp": disp,
                "rect_left": left, "rect_right": right}
+        return self._advance(cur)
+
+    def step_rgbd(self, bgr: np.ndarray, depth_mm: np.ndarray) -> dict:
+        """One RGB-D frame: colour -> gray -> undistort -> features; depth -> disparity."""
+        cfg, rp = self.cfg, self.rect
+        left = remap(bgr_to_gray(bgr), rp["map_l"])
+        fl = extract(left, cfg)
+        disp = depth_disparity(fl, depth_mm, rp["map_l"], rp["fx"])
+        stereo = np.where(np.isfinite(disp), np.arange(cfg.n_features), -1)
+        cur = {"left": fl, "right": None, "stereo": stereo, "disp": disp, "rect_left": left}
+        return self._advance(cur)
+
+    def _advance(self, cur: dict) -> dict:
+        cfg, rp = self.cfg, self.rect
         intr = (rp["fx"], rp["fy"], rp["cx"], rp["cy"])
         res = {"frame": self.frame, "cur": cur}
         if self.prev is None:
             res.update(T=np.eye(4), cov=np.zeros((6, 6)), status=2, n_corr=0, n_inliers=0)
             cur["temporal"] = np.full(cfg.n_features, -1, dtype=np.int64)
         else:
-            tm = match(fl, self.prev["left"], cfg, "temporal")
+            tm = match(cur["left"], self.prev["left"], cfg, "temporal")
             cur["temporal"] = tm[0]
             cur["temporal_full"] = tm
             corr = build_correspondences(self.prev, cur, tm[0], (rp["fx"], rp["fy"], rp["cx"], rp["cy"], rp["fx"] * rp["baseline"]))

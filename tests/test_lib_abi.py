@@ -27,7 +27,7 @@ def test_library_exports_every_symbol():
     lib = _lib.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.tslam_abi_version() == 2
+    assert lib.tslam_abi_version() == 3
     out = subprocess.run(["nm", "-D", "--defined-only", str(_lib.LIB_PATH)], capture_output=True, text=True, check=True).stdout
     exported = set(re.findall(r" T (tslam_[a-z_]+)", out))
     assert declared_functions() <= exported
@@ -40,9 +40,9 @@ def test_struct_layouts_match_c(tmp_path):
 #include <stddef.h>
 #include "{HEADER}"
 int main(void) {{
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(tslam_params), offsetof(tslam_params, ransac_thr_px),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(tslam_params), offsetof(tslam_params, ransac_thr_px),
          offsetof(tslam_params, ransac_seed), offsetof(tslam_params, ransac_splits),
-         offsetof(tslam_params, ba_window), offsetof(tslam_params, ba_lambda),
+         offsetof(tslam_params, ba_window), offsetof(tslam_params, ba_lambda), offsetof(tslam_params, rgbd),
          sizeof(tslam_stereo_desc), offsetof(tslam_stereo_desc, map_left));
   return 0;
 }}""")
@@ -51,7 +51,7 @@ int main(void) {{
     got = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
     P, S = _lib.Params, _lib.StereoDesc
     assert got == [ctypes.sizeof(P), P.ransac_thr_px.offset, P.ransac_seed.offset, P.ransac_splits.offset,
-                   P.ba_window.offset, P.ba_lambda.offset, ctypes.sizeof(S), S.map_left.offset]
+                   P.ba_window.offset, P.ba_lambda.offset, P.rgbd.offset, ctypes.sizeof(S), S.map_left.offset]
 
 
 def test_invalid_arguments_fail_cleanly():

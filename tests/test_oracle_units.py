@@ -210,3 +210,41 @@ def test_tracker_follows_ground_truth():
         # ~5 % drift budget on a fronto-parallel scene (yaw / x-translation ambiguity)
         assert np.linalg.norm(gt[:3, 3] - res["world_T_cam"][:3, 3]) < 0.08 * np.linalg.norm(gt[:3, 3]) + 1e-3
         assert np.linalg.norm(gt[:3, :3] - res["world_T_cam"][:3, :3]) < 2e-3
+
+
+def test_rgbd_oracle_follows_ground_truth_and_record_layout():
+    """RGB-D oracle (configs[4]): gray conversion, depth -> disparity and tracking vs the renderer."""
+    from thor_slam_amd.calib import extract_cameras, rgbd_pairs, rgbd_undistort
+    from thor_slam_amd.camera.rig import CameraRig
+    from thor_slam_amd.params import HipSlamConfig
+    from thor_slam_amd.rgbd import pack_rgbd
+    from thor_slam_amd.synthetic import SyntheticRGBDSource
+
+    src = SyntheticRGBDSource(width=320, height=240)
+    bgr, depth = src.render_rgbd(0)
+    rec = pack_rgbd(bgr, depth)
+    assert rec.size == 5 * 320 * 240
+    np.testing.assert_array_equal(rec[: bgr.size].reshape(bgr.shape), bgr)
+    np.testing.assert_array_equal(rec[bgr.size:].view("<u2").reshape(depth.shape), depth)
+    g = O.bgr_to_gray(np.array([[[255, 255, 255], [0, 0, 0], [0, 0, 255]]], dtype=np.uint8))
+    assert g.tolist() == [[255, 0, (255 * 4899 + 8192) >> 14]]
+    cams = extract_cameras(CameraRig([src]).calibration, 2)
+    (ci, di), = rgbd_pairs(cams)
+    r = rgbd_undistort(cams[ci])
+    assert r.is_identity and r.baseline == 1.0
+    cfg = HipSlamConfig(rgbd=True, n_features=500, n_levels=3)
+    trk = O.OracleTracker(cfg, dict(fx=r.fx, fy=r.fy, cx=r.cx, cy=r.cy, baseline=r.baseline, map_l=r.map_left,
+                                    map_r=r.map_right))
+    for i in range(3):
+        res = trk.step_rgbd(*src.render_rgbd(i))
+    d = res["cur"]["disp"]
+    ok = np.isfinite(d)
+    assert ok.sum() > 100
+    # the disparity is fx / Z of the rendered depth at the keypoint
+    kp = res["cur"]["left"]["kp"]
+    u, v = O.level0_coords(kp["x"][ok], kp["y"][ok], kp["level"][ok])
+    _, dep = src.render_rgbd(2)
+    z = dep[np.floor(v + 0.5).astype(int), np.floor(u + 0.5).astype(int)] * 0.001
+    np.testing.assert_allclose(d[ok], r.fx / z, rtol=1e-12)
+    gt = np.linalg.inv(src.camera_pose(0, 0)) @ src.camera_pose(2, 0)
+    assert np.linalg.norm(res["world_T_cam"][:3, 3] - gt[:3, 3]) < 0.1 * np.linalg.norm(gt[:3, 3]) + 2e-3

@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void k_ba_insert(BatchCtx c, BaArgs a) {
     const double* disp = c.disp + ((size_t)rslot * c.P + p) * K;
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x) {
         double u = __builtin_nan(""), v = __builtin_nan("");
-        const bool valid = kp_obs(c, rslot, 2 * p, k, &u, &v);
+        const bool valid = kp_obs(c, rslot, c.cpp * p, k, &u, &v);
         const double dd = disp[k];
         const bool has_d = __builtin_isfinite(dd) && dd > 0.0;
         int lm = -1;

@@ -31,13 +31,14 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     const int f = fp / c.P;
     const int64_t g = c.g0 + f;
     if (mode == 1 && g == 0) return;          // no previous frame
+    if (mode == 0 && c.rgbd) return;          // RGB-D: depth replaces stereo matching
     int l = 0;
     while (l + 1 < c.g.n_levels && (int)blockIdx.x >= c.g.qtile_start[l + 1]) ++l;
     const int tile = blockIdx.x - c.g.qtile_start[l];
     const int slot = ring_slot(c, g);
-    const int qcam = 2 * p;
+    const int qcam = c.cpp * p;
     const int tslot = mode == 0 ? slot : ring_slot(c, g - 1);
-    const int tcam = mode == 0 ? 2 * p + 1 : 2 * p;
+    const int tcam = mode == 0 ? qcam + 1 : qcam;
     const int K = c.g.K;
     const int qn = c.kcount[((size_t)slot * c.C + qcam) * c.g.n_levels + l];
     const int tn = c.kcount[((size_t)tslot * c.C + tcam) * c.g.n_levels + l];
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(256) void k_refine_stereo(BatchCtx c) {
     const int pos = (local * 4 + wave) * TS_RS_Q + qs;
     const bool live = lane < 5 * TS_RS_Q && pos < K;
     const size_t mbase = (((size_t)f * c.P + p) * 2 + 0) * K;
-    const int qcam = 2 * p;
+    const int qcam = c.cpp * p;
     const size_t qkb = ((size_t)slot * c.C + qcam) * K;
     int l = 0, qi = 0, j = -1;
     uint32_t qxy = 0;
@@ -309,7 +310,7 @@ __global__ __launch_bounds__(256) void k_refine_temporal(BatchCtx c) {
     const int pos = local * 8 + qslot;
     const bool live = pos < K;
     const size_t mbase = (((size_t)f * c.P + p) * 2 + 1) * K;
-    const int qcam = 2 * p;
+    const int qcam = c.cpp * p;
     const size_t qkb = ((size_t)slot * c.C + qcam) * K;
     int l = 0, qi = 0, j = -1;
     uint32_t qxy = 0;
@@ -417,6 +418,9 @@ void launch_match(const BatchCtx& c, hipStream_t s) {
 
 void launch_match_refine(const BatchCtx& c, hipStream_t s) {
     const int K = c.g.K;
-    hipLaunchKernelGGL(k_refine_stereo, dim3(xcd_grid(c.n * c.P, (K + 4 * TS_RS_Q - 1) / (4 * TS_RS_Q))), dim3(256), 0, s, c);
+    if (c.rgbd)
+        launch_rgbd_depth(c, s);
+    else
+        hipLaunchKernelGGL(k_refine_stereo, dim3(xcd_grid(c.n * c.P, (K + 4 * TS_RS_Q - 1) / (4 * TS_RS_Q))), dim3(256), 0, s, c);
     hipLaunchKernelGGL(k_refine_temporal, dim3(xcd_grid(c.n * c.P, (K + 7) / 8)), dim3(256), 0, s, c);
 }

@@ -237,7 +237,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_corr(BatchCtx c) {
     const int32_t* tm = c.temporal + ((size_t)ring_slot(c, g) * c.P + p) * K;
     const double* tuv = c.tuv + ((size_t)f * c.P + p) * K * 2;
     const double* dprev = c.disp + ((size_t)pslot * c.P + p) * K;
-    const uint32_t* kprev = c.kps + ((size_t)pslot * c.C + 2 * p) * K * 2;
+    const uint32_t* kprev = c.kps + ((size_t)pslot * c.C + c.cpp * p) * K * 2;
     double* corr = c.corr + ((size_t)f * c.P + p) * K * TS_CORR_DOUBLES;
     int n = 0;
     for (int base = 0; base < K; base += POSE_THREADS) {

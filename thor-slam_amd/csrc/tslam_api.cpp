@@ -49,6 +49,7 @@ struct tslam_handle {
     uint32_t map_mask = 0;
     int32_t* d_maps = nullptr;
     uint32_t* d_brief = nullptr;
+    uint8_t* d_gray = nullptr;   // RGB-D: converted colour images [B][P][H][W]
     int64_t* d_wedges = nullptr;
     Buffer buf[TSLAM_BUF_COUNT];
     uint32_t* d_cand = nullptr;
@@ -223,7 +224,10 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.g0 = h->cur_g0;
     c.W = h->W;
     c.H = h->H;
-    c.images = h->cur_images;
+    c.cpp = h->prm.rgbd ? 1 : 2;
+    c.rgbd = h->prm.rgbd;
+    c.images = h->prm.rgbd ? h->d_gray : h->cur_images;
+    c.rgbd_in = h->prm.rgbd ? h->cur_images : nullptr;
     c.maps = h->d_maps;
     c.map_mask = h->map_mask;
     c.pyr = (uint8_t*)h->buf[TSLAM_BUF_PYRAMID].ptr;
@@ -298,8 +302,10 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     if ((H >> (p.n_levels - 1)) < 2 * p.edge_margin + 3 || (W >> (p.n_levels - 1)) < 2 * p.edge_margin + 3)
         return fail(TSLAM_EINVAL, "coarsest pyramid level smaller than 2*edge_margin+3");
     for (int i = 0; i < p.n_pairs; ++i)
-        if (!(pairs[i].baseline > 0.0) || !(pairs[i].fx > 0.0) || !(pairs[i].fy > 0.0))
+        if (!(p.rgbd || pairs[i].baseline > 0.0) || !(pairs[i].fx > 0.0) || !(pairs[i].fy > 0.0))
             return fail(TSLAM_EINVAL, "pair calibration needs fx, fy, baseline > 0");
+    if (p.rgbd != 0 && p.rgbd != 1) return fail(TSLAM_EINVAL, "rgbd must be 0 or 1");
+    if (p.rgbd && ((W * H) & 1)) return fail(TSLAM_EINVAL, "RGB-D needs an even pixel count (u16 depth alignment)");
 
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) return fail(TSLAM_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
@@ -310,7 +316,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     h->W = W;
     h->H = H;
     h->P = p.n_pairs;
-    h->C = 2 * p.n_pairs;
+    h->C = (p.rgbd ? 1 : 2) * p.n_pairs;
     h->B = p.max_batch;
     // the ring keeps frame t-1 of a batch's first frame; with BA it also keeps the frames a
     // keyframe's temporal match chain walks back over
@@ -322,7 +328,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
         h->calib[i].fy = pairs[i].fy;
         h->calib[i].cx = pairs[i].cx;
         h->calib[i].cy = pairs[i].cy;
-        h->calib[i].fxb = pairs[i].fx * pairs[i].baseline;
+        h->calib[i].fxb = pairs[i].fx * (p.rgbd ? 1.0 : pairs[i].baseline);   // RGB-D: virtual 1 m baseline
     }
 
     const int64_t K = p.n_features, C = h->C, P = h->P, B = h->B, R = h->R, L = p.n_levels;
@@ -366,6 +372,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_wedges, sizeof(TSLAM_WEDGES));
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_maps, sizeof(int32_t) * (size_t)C * W * H * 2);
     if (rc == TSLAM_OK && p.ba_window) rc = alloc_ba(h);
+    if (rc == TSLAM_OK && p.rgbd) rc = dev_alloc(h, (void**)&h->d_gray, (size_t)B * P * W * H);
     if (rc != TSLAM_OK) {
         free_all(h);
         delete h;
@@ -385,10 +392,11 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
               hipMemcpy(h->d_wedges, TSLAM_WEDGES, sizeof(TSLAM_WEDGES), hipMemcpyHostToDevice) == hipSuccess;
     for (int i = 0; i < h->P && ok; ++i) {
         const int32_t* m[2] = {pairs[i].map_left, pairs[i].map_right};
-        for (int s = 0; s < 2; ++s) {
+        const int cpp = p.rgbd ? 1 : 2;
+        for (int s = 0; s < cpp; ++s) {
             if (!m[s]) continue;
-            h->map_mask |= 1u << (2 * i + s);
-            ok = ok && hipMemcpy(h->d_maps + (size_t)(2 * i + s) * W * H * 2, m[s], sizeof(int32_t) * (size_t)W * H * 2,
+            h->map_mask |= 1u << (cpp * i + s);
+            ok = ok && hipMemcpy(h->d_maps + (size_t)(cpp * i + s) * W * H * 2, m[s], sizeof(int32_t) * (size_t)W * H * 2,
                                  hipMemcpyHostToDevice) == hipSuccess;
         }
     }
@@ -462,6 +470,8 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     h->last_stream = s;
     const BatchCtx c = make_ctx(h);
+    if (h->prm.rgbd && (stage == TSLAM_STAGE_RECTIFY || stage == TSLAM_STAGE_ALL || stage == TSLAM_KERNEL_RECTIFY_PYRAMID))
+        launch_rgbd_gray(c, h->d_gray, s);   // the colour images become the gray input of rectify
     switch (stage) {
         case TSLAM_STAGE_RECTIFY: launch_rectify_pyramid(c, s); break;
         case TSLAM_STAGE_DETECT: launch_detect(c, s); launch_select(c, s); break;

@@ -16,6 +16,7 @@
 //   rowstart u16 [R][C][sum(H_l+1)]  per level: first y-sorted position of row y
 //   qbest/qsecond/tbest u32 [B][P][2][K]   matching scratch (mode 0 stereo, 1 temporal)
 //   stereo   i32 [R][P][K]  disp f64 [R][P][K]        stereo match + refined disparity of left kps
+//            (RGB-D: disp = fx / Z from the aligned depth, a virtual 1 m baseline; stereo = k or -1)
 //   temporal i32 [R][P][K]  tuv  f64 [B][P][K][2]     temporal match + refined (u, v) at t
 //   corr     f64 [B][P][K][8]        X Y Z du dv bx by bz (ordered by t keypoint index)
 //   pose     f64 [B][P][68]          T_rel, T_abs, cov;  stats i32 [B][P][8];  state f64 [P][16]
@@ -75,11 +76,14 @@ struct PoseParams {
 struct BatchCtx {
     LevelGeom g;
     int C, P, B, R;
+    int cpp;               // cameras per pair: 2 (stereo), 1 (RGB-D: colour camera + aligned depth)
+    int rgbd;
     int n;                 // frames in this batch
     int64_t g0;            // global index of the batch's first frame
     int W, H;              // level-0 size
     // inputs
-    const uint8_t* images; // [n][C][H][W]
+    const uint8_t* images; // [n][C][H][W] gray (RGB-D: the converted staging buffer)
+    const uint8_t* rgbd_in; // RGB-D only: [n][P][BGR u8 H*W*3 | depth u16 mm H*W]
     const int32_t* maps;   // [C][H][W][2] or nullptr
     uint32_t map_mask;     // bit c set -> camera c has a map (else identity)
     // buffers
@@ -126,6 +130,8 @@ void launch_match_refine(const BatchCtx& c, hipStream_t s);
 void launch_pose(const BatchCtx& c, hipStream_t s);
 void launch_chain(const BatchCtx& c, hipStream_t s);
 void launch_pack(const BatchCtx& c, uint8_t* dst, hipStream_t s);
+void launch_rgbd_gray(const BatchCtx& c, uint8_t* gray, hipStream_t s);
+void launch_rgbd_depth(const BatchCtx& c, hipStream_t s);
 
 // ---------------------------------------------------------------------------------------------
 // small device helpers

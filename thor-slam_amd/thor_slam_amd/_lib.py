@@ -52,6 +52,7 @@ class Params(ctypes.Structure):
         ("max_batch", ctypes.c_int32), ("n_pairs", ctypes.c_int32), ("ransac_splits", ctypes.c_int32),
         ("ba_window", ctypes.c_int32), ("ba_kf_interval", ctypes.c_int32), ("ba_iters", ctypes.c_int32),
         ("ba_pad", ctypes.c_int32), ("ba_lambda", ctypes.c_double), ("ba_outlier_px", ctypes.c_double),
+        ("rgbd", ctypes.c_int32), ("rgbd_pad", ctypes.c_int32),
     ]
 
 
@@ -138,7 +139,7 @@ def make_params(cfg: HipSlamConfig, max_batch: int, n_pairs: int, ransac_splits:
         cfg.stereo_row_tol, cfg.max_disparity, cfg.temporal_window, cfg.ransac_hypotheses, cfg.refine_iters,
         cfg.min_inliers, float(cfg.ransac_thr_px), int(cfg.ransac_seed) & ((1 << 64) - 1), int(max_batch), int(n_pairs),
         int(ransac_splits), int(cfg.ba_window), int(cfg.ba_kf_interval), int(cfg.ba_iters), 0, float(cfg.ba_lambda),
-        float(cfg.ba_outlier_px),
+        float(cfg.ba_outlier_px), int(bool(cfg.rgbd)), 0,
     )
 
 
@@ -150,6 +151,8 @@ class Handle:
         cfg.validate()
         self.cfg = cfg
         self.n_pairs = len(rects)
+        self.cams_per_pair = 1 if cfg.rgbd else 2   # RGB-D: one colour camera (+ aligned depth) per "pair"
+        self.n_cams = self.cams_per_pair * self.n_pairs
         self.max_batch = int(max_batch)
         self._maps = []  # keep host maps alive during create
         descs = (StereoDesc * self.n_pairs)()
@@ -284,7 +287,7 @@ class Handle:
     def keypoints(self, global_frame: int, cam: int) -> dict:
         """Decoded keypoints of one camera at a global frame (must still be in the ring)."""
         slot = self.ring_slot(global_frame)
-        C = 2 * self.n_pairs
+        C = self.n_cams
         kp = self.frame_block("keypoints", slot, np.uint32).reshape(C, self.K, 2)[cam]
         cnt = self.frame_block("kcount", slot, np.int32).reshape(C, self.n_levels)[cam]
         desc = self.frame_block("desc", slot, np.uint32).reshape(C, self.K, 8)[cam]

@@ -215,3 +215,24 @@ def stereo_rectify(left: CameraConfig, right: CameraConfig) -> StereoRectificati
         map_right=map_r,
         is_identity=is_identity,
     )
+
+
+def rgbd_pairs(cams: list[CameraConfig]) -> list[tuple[int, int]]:
+    """(colour, depth) global indices of RGB-D sources: cam_idx 0 = the colour camera (BGR),
+    cam_idx 1 = the depth image aligned to it (``get_latest_rgbd_frames`` order, luxonis.py:876-919)."""
+    return stereo_pairs(cams)
+
+
+def rgbd_undistort(color: CameraConfig) -> StereoRectification:
+    """Undistortion of a colour camera whose depth image is aligned to it (same K and D,
+    luxonis.py:1018-1030): pinhole f = min(fx, fy) at the camera's principal point, no rotation.
+    The depth is sampled through the same table (nearest raw pixel).  ``baseline`` is the virtual
+    1 m the device uses to store depth as disparity fx / Z."""
+    k = np.asarray(color.intrinsics.matrix, dtype=np.float64)
+    f = float(min(k[0, 0], k[1, 1]))
+    cx, cy = float(k[0, 2]), float(k[1, 2])
+    mp = rectify_map(color.intrinsics, np.eye(3), f, f, cx, cy)
+    h, w = mp.shape[:2]
+    ident = np.stack(np.meshgrid(np.arange(w), np.arange(h)), axis=-1).astype(np.int32) * RECT_ONE
+    return StereoRectification(width=w, height=h, fx=f, fy=f, cx=cx, cy=cy, baseline=1.0, rect_left=np.eye(3),
+                               rect_right=np.eye(3), map_left=mp, map_right=mp, is_identity=bool(np.array_equal(mp, ident)))

@@ -45,6 +45,9 @@ class HipSlamConfig(SlamConfig):
     ba_iters: int = 5               # Gauss-Newton steps per window solve
     ba_lambda: float = 1.0          # Levenberg damping (px^2 units)
     ba_outlier_px: float = 3.0      # observations farther than this at the start are dropped
+    # input kind: RGB-D (BASELINE configs[4]) = per source a colour camera (cam_idx 0, BGR) and a
+    # depth image aligned to it (cam_idx 1, u16 mm); depth replaces stereo matching
+    rgbd: bool = False
     # pipeline
     batch_size: int = 1             # frames per submission (1 = synchronous latency mode)
 

@@ -36,11 +36,13 @@ import numpy as np
 from scipy.spatial.transform import Rotation
 
 from .._lib import POSE_INIT, POSE_LOST, POSE_OK, Handle
-from ..calib import StereoRectification, confidence_from_covariance, extract_cameras, stereo_pairs, stereo_rectify
+from ..calib import (StereoRectification, confidence_from_covariance, extract_cameras, rgbd_pairs, rgbd_undistort,
+                     stereo_pairs, stereo_rectify)
 from ..camera.rig import RigCalibration
 from ..camera.types import SynchronizedFrameSet
 from ..dist import fuse_rig_motion
 from ..params import HipSlamConfig
+from ..rgbd import pack_rgbd
 from .interface import CameraConfig, MapPoint, SlamConfig, SlamEngine, SlamMap, SlamPose, TrackingState
 
 logger = logging.getLogger(__name__)
@@ -99,10 +101,16 @@ class HipSlamEngine(SlamEngine):
             self._cameras = extract_cameras(calibration, self._num_cameras)
             if len(self._cameras) < self._num_cameras:
                 logger.warning("Calibration has %d cameras, expected %d", len(self._cameras), self._num_cameras)
-            self._pairs = stereo_pairs(self._cameras)
-            if not self._pairs:
-                raise RuntimeError("HipSlamEngine needs at least one stereo source (cam_idx 0 and 1)")
-            self._rects = [stereo_rectify(self._cameras[l], self._cameras[r]) for l, r in self._pairs]
+            if cfg.rgbd:   # per source: colour camera (cam_idx 0) + aligned depth (cam_idx 1)
+                self._pairs = rgbd_pairs(self._cameras)
+                if not self._pairs:
+                    raise RuntimeError("HipSlamEngine(rgbd) needs an RGB-D source (colour cam_idx 0, depth cam_idx 1)")
+                self._rects = [rgbd_undistort(self._cameras[l]) for l, _ in self._pairs]
+            else:
+                self._pairs = stereo_pairs(self._cameras)
+                if not self._pairs:
+                    raise RuntimeError("HipSlamEngine needs at least one stereo source (cam_idx 0 and 1)")
+                self._rects = [stereo_rectify(self._cameras[l], self._cameras[r]) for l, r in self._pairs]
             import torch  # PyTorch is the device-memory / stream plumbing only
 
             if not torch.cuda.is_available():
@@ -110,8 +118,10 @@ class HipSlamEngine(SlamEngine):
             self._torch = torch
             self._handle = Handle(self._rects, cfg, max_batch=cfg.batch_size, device=self._device)
             rect0 = self._rects[0]
-            n_cams = 2 * len(self._pairs)
-            shape = (cfg.batch_size, n_cams, rect0.height, rect0.width)
+            if cfg.rgbd:   # one [BGR | u16 depth] record of 5*H*W bytes per camera
+                shape = (cfg.batch_size, len(self._pairs), 5 * rect0.height * rect0.width)
+            else:
+                shape = (cfg.batch_size, 2 * len(self._pairs), rect0.height, rect0.width)
             self._dev_images = torch.empty(shape, dtype=torch.uint8, device=f"cuda:{self._device}")
             self._host_images = torch.empty(shape, dtype=torch.uint8).pin_memory()
             self._base_T_rects = [self._cameras[l].extrinsics.to_4x4_matrix() @ r.left_optical_T_rect()
@@ -128,6 +138,20 @@ class HipSlamEngine(SlamEngine):
     # ------------------------------------------------------------------------------------------
     def _frame_images(self, frame_set: SynchronizedFrameSet) -> np.ndarray | None:
         imgs = []
+        if self._config.rgbd:
+            for c, d in self._pairs:
+                cam = self._cameras[c]
+                fs = frame_set.frame_sets.get(cam.source_name)
+                if fs is None or max(cam.cam_idx, self._cameras[d].cam_idx) >= len(fs.frames):
+                    return None
+                bgr = np.asarray(fs.frames[cam.cam_idx].image)
+                depth = np.asarray(fs.frames[self._cameras[d].cam_idx].image)
+                if bgr.ndim == 2:
+                    bgr = np.repeat(bgr[..., None], 3, axis=-1)
+                if bgr.shape[:2] != (self._rects[0].height, self._rects[0].width) or depth.shape != bgr.shape[:2]:
+                    raise ValueError(f"RGB-D camera {c}: colour {bgr.shape} / depth {depth.shape} do not match its calibration")
+                imgs.append(pack_rgbd(bgr, depth.astype(np.uint16, copy=False)))
+            return np.stack(imgs)
         for l, r in self._pairs:
             for gi in (l, r):
                 cam = self._cameras[gi]
@@ -172,7 +196,8 @@ class HipSlamEngine(SlamEngine):
         self._publish(res, stamps)
 
     def process_batch(self, images, timestamps: list[float] | None = None, stream=None) -> dict:
-        """Throughput entry: ``images`` is a device uint8 tensor [n, 2P, H, W] already in HBM."""
+        """Throughput entry: ``images`` is a device uint8 tensor already in HBM: [n, 2P, H, W] gray
+        stereo pairs, or [n, P, 5*H*W] RGB-D records (``rgbd.pack_rgbd``)."""
         if self._handle is None:
             raise RuntimeError("Not initialized")
         n = int(images.shape[0])

@@ -26,6 +26,7 @@ import numpy as np
 
 from .calib import RDF_TO_FLU_MATRIX, undistort_normalized
 from .camera.types import CameraFrame, CameraSource, Extrinsics, Intrinsics
+from .rgbd import pack_rgbd
 
 TEXTURE_SIZE = 1024
 TEXEL_M = 0.01
@@ -270,3 +271,38 @@ class SyntheticStereoSource(CameraSource):
 
     def ground_truth_body(self, i: int) -> np.ndarray:
         return self.trajectory[i % len(self.trajectory)]
+
+
+class SyntheticRGBDSource(SyntheticStereoSource):
+    """An RGB-D source (BASELINE configs[4]): frames are [colour BGR u8, depth u16 mm] from one
+    camera, the depth aligned to the colour image (same K and D, as Luxonis ``depth_align_to_rgb``,
+    luxonis.py:1018-1030; frame order of ``get_latest_rgbd_frames``, :876-919).  Colour = the room
+    texture through fixed channel gains; depth = the optical-axis distance in mm (0 beyond 65.535 m)."""
+
+    def __init__(self, name: str = "192.168.2.21", width: int = 1280, height: int = 720, **kw) -> None:
+        super().__init__(name=name, width=width, height=height, **kw)
+        self._extr = [Extrinsics.from_4x4_matrix(np.eye(4)), Extrinsics.from_4x4_matrix(np.eye(4))]
+
+    def render_rgbd(self, i: int) -> tuple[np.ndarray, np.ndarray]:
+        rng = np.random.default_rng((self.seed, i, 0))
+        g, z = self.scene.render(self.camera_pose(i, 0), self._intr[0], rng, return_depth=True)
+        gf = g.astype(np.float64)
+        bgr = np.stack([np.clip(np.floor(0.8 * gf + 30.5), 0, 255), gf, np.clip(np.floor(1.1 * gf - 9.5), 0, 255)],
+                       axis=-1).astype(np.uint8)
+        mm = np.floor(z * 1000.0 + 0.5)
+        depth = np.where((mm > 0) & (mm <= 65535), mm, 0).astype(np.uint16)
+        return bgr, depth
+
+    def render_frames(self, i: int) -> list[CameraFrame]:
+        ts = self.timestamp(i)
+        bgr, depth = self.render_rgbd(i)
+        return [CameraFrame(image=bgr, timestamp=ts, sequence_num=i, camera_name=f"{self._name}_rgb"),
+                CameraFrame(image=depth, timestamp=ts, sequence_num=i, camera_name=f"{self._name}_depth")]
+
+    def render_rgbd_sequence(self, n: int, start: int = 0) -> np.ndarray:
+        """(n, 5*H*W) u8 device records: [BGR H*W*3 | depth u16 H*W little-endian] per frame."""
+        out = np.empty((n, 5 * self.height * self.width), dtype=np.uint8)
+        for k in range(n):
+            out[k] = pack_rgbd(*self.render_rgbd(start + k))
+        return out
+
