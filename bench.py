@@ -2,6 +2,7 @@
 
 python bench.py --gpus N --steps K --warmup W   (N > 1 under torch.distributed.run, one rank/GPU)
 python bench.py --config c4                     (BASELINE.json configs[3]: 1280x800, K=4000, + local BA)
+python bench.py --config c5 [--gpus 4]          (BASELINE.json configs[4]: RGB-D 1280x720, one camera per GPU)
 
 * workload (BASELINE.json configs[1], C2): one stereo pair 640x400 per GPU, K=2000 ORB-style
   keypoints per image, synthetic room sequence (seed = rank); a *step* = one batch of
@@ -19,6 +20,8 @@ python bench.py --config c4                     (BASELINE.json configs[3]: 1280x
 * --config c4: the same step plus the A8 stage (every 5th frame a keyframe of a 10-keyframe
   window, 5 Gauss-Newton iterations per keyframe); the roofline is then that of the dominant
   kernel of the step, the FP64-MFMA Schur product when it dominates (HIP events around its launches).
+* --config c5: RGB-D frames (BGR u8 + aligned u16 mm depth, 1280x720) of one camera per GPU; the
+  colour image is converted on the device and depth replaces the stereo matching.
 """
 
 from __future__ import annotations
@@ -40,6 +43,7 @@ for _p in (ROOT, ROOT / "thor-slam_amd"):
 
 METRIC = "synced stereo frames/sec (detect+match+pose) @640×400, 1/2/4/8 GPU"
 METRIC_C4 = "synced stereo frames/sec (detect+match+pose+10-keyframe local BA) @1280×800, 1 GPU"
+METRIC_C5 = "RGB-D frames/sec (BGR+depth, detect+match+pose) @1280×720, one camera per GPU, 1/2/4 GPU"
 HBM_PEAK_GBS = 8000.0
 FP64_MFMA_PEAK_TFS = 78.6   # MI355X FP64 matrix peak (AMD spec; the microarch guide lists no FP64 row)
 # bench kernel label -> device symbol (rocprofv3 / PMC summaries); "pose" is k_corr+k_ransac+k_refine
@@ -78,11 +82,12 @@ def triangle_indices(total: int, unique: int) -> np.ndarray:
     return np.where(k < unique, k, period - k)
 
 
-def frame_bytes(W: int, H: int, K: int, n_img: int = 2, n_pairs: int = 1, channels: int = 1) -> int:
+def frame_bytes(W: int, H: int, K: int, n_img: int = 2, n_pairs: int = 1, channels: int = 1, matchings: int = 2) -> int:
     """SURVEY.md §8d compulsory bytes per stereo frame: read the images, write keypoints (12 B) and
     descriptors (32 B), write the match records (8 B per keypoint, for the stereo and the temporal
-    matching of each pair).  C2: 2 * (256,000 + 88,000) + 2 * 16,000 = 720,000 B."""
-    return n_img * (W * H * channels + K * (12 + 32)) + 2 * n_pairs * K * 8
+    matching of each pair).  C2: 2 * (256,000 + 88,000) + 2 * 16,000 = 720,000 B.  RGB-D (C5): one
+    image of 5 bytes per pixel (BGR + u16 depth), temporal matching only."""
+    return n_img * (W * H * channels + K * (12 + 32)) + matchings * n_pairs * K * 8
 
 
 def kernel_bytes(name: str, B: int, h, cfg, maps_identity: bool) -> float:
@@ -113,6 +118,8 @@ def kernel_bytes(name: str, B: int, h, cfg, maps_identity: bool) -> float:
 def _oracle_worker(args):
     """One CPU process: the NumPy oracle tracking its contiguous frame chunk (replayed) for budget_s."""
     frames, rect_d, cfg_d, budget_s = args
+    if cfg_d.get("rgbd"):
+        return _oracle_worker_rgbd(args)
     from oracle import numpy_slam as O
     from thor_slam_amd.params import HipSlamConfig
 
@@ -134,6 +141,38 @@ def _oracle_worker(args):
             bat.step(res)
         n += 1
     return n, time.perf_counter() - t0
+
+
+def _oracle_worker_rgbd(args):
+    frames, rect_d, cfg_d, budget_s = args   # frames: (n, H, W, 3) BGR and (n, H, W) depth
+    from oracle import numpy_slam as O
+    from thor_slam_amd.params import HipSlamConfig
+
+    bgr, depth = frames
+    trk = O.OracleTracker(HipSlamConfig(**cfg_d), rect_d)
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        i = n % len(bgr)
+        trk.step_rgbd(bgr[i], depth[i])
+        n += 1
+    return n, time.perf_counter() - t0
+
+
+def cpu_baseline_rgbd(bgr: np.ndarray, depth: np.ndarray, rect, cfg, budget_s: float, procs: int) -> dict:
+    import dataclasses
+
+    rect_d = dict(fx=rect.fx, fy=rect.fy, cx=rect.cx, cy=rect.cy, baseline=rect.baseline,
+                  map_l=rect.map_left, map_r=rect.map_right)
+    cfg_d = dataclasses.asdict(cfg)
+    parts = [(b, d) for b, d in zip(np.array_split(bgr, procs), np.array_split(depth, procs)) if len(b)]
+    with ProcessPoolExecutor(max_workers=len(parts)) as ex:
+        results = list(ex.map(_oracle_worker, [(pt, rect_d, cfg_d, budget_s) for pt in parts]))
+    n = sum(r[0] for r in results)
+    wall = max(r[1] for r in results)
+    return {"value": n / wall, "unit": "frames/s", "cores": len(parts), "kind": "port",
+            "sample": f"{n} synthetic {bgr.shape[2]}x{bgr.shape[1]} RGB-D frames (seed 0, {len(bgr)} distinct, replayed "
+                      f"per process), NumPy oracle step_rgbd, {len(parts)} process(es) x {budget_s:.0f} s"}
 
 
 def cpu_baseline(frames: np.ndarray, rect, cfg, budget_s: float, procs: int) -> dict:
@@ -163,8 +202,9 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=["c2", "c4"], default="c2", help="BASELINE.json configs[1] (c2) or configs[3] (c4)")
-    ap.add_argument("--batch", type=int, default=0, help="stereo frames per step (0 = 256 for c2, 50 for c4)")
+    ap.add_argument("--config", choices=["c2", "c4", "c5"], default="c2",
+                    help="BASELINE.json configs[1] (c2), configs[3] (c4) or configs[4] (c5)")
+    ap.add_argument("--batch", type=int, default=0, help="frames per step (0 = 256 for c2, 50 for c4, 128 for c5)")
     ap.add_argument("--unique", type=int, default=0, help="distinct rendered frames, triangle-wave replay (0 = 48 / 24)")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU baseline (0 = skip)")
     ap.add_argument("--cpu-procs", type=int, default=8, help="oracle processes for the CPU baseline")
@@ -183,6 +223,7 @@ def main() -> None:
     from thor_slam_amd.dist import BlockLayout, FeatureExchange
     from thor_slam_amd.camera.rig import CameraRig
     from thor_slam_amd.params import HipSlamConfig
+    from thor_slam_amd.rgbd import pack_rgbd
     from thor_slam_amd.synthetic import SyntheticStereoSource
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -198,29 +239,41 @@ def main() -> None:
         else:
             dist.init_process_group(args.dist_backend)
 
-    c4 = args.config == "c4"
+    c4, c5 = args.config == "c4", args.config == "c5"
     if c4 and world > 1:
         raise SystemExit("--config c4 is a single-GPU configuration")
-    width, height = (1280, 800) if c4 else (640, 400)
-    cfg = HipSlamConfig(n_features=4000, ba_window=10, ba_kf_interval=5, ba_iters=5) if c4 else HipSlamConfig()
-    B = args.batch or (50 if c4 else 256)
-    args.unique = args.unique or (24 if c4 else 48)
-    src = SyntheticStereoSource(seed=rank, n_frames=args.unique, width=width, height=height)
-    cams = extract_cameras(CameraRig([src]).calibration, 2)
-    (li, ri), = stereo_pairs(cams)
-    rect = stereo_rectify(cams[li], cams[ri])
+    width, height = (1280, 800) if c4 else (1280, 720) if c5 else (640, 400)
+    cfg = (HipSlamConfig(n_features=4000, ba_window=10, ba_kf_interval=5, ba_iters=5) if c4 else
+           HipSlamConfig(rgbd=True) if c5 else HipSlamConfig())
+    B = args.batch or (50 if c4 else 128 if c5 else 256)
+    args.unique = args.unique or (24 if (c4 or c5) else 48)
     workers = max(1, min(16, (os.cpu_count() or 2) // max(1, world), args.unique))
     t_r = time.perf_counter()
-    uniq = render_frames(rank, args.unique, workers, width, height)
+    if c5:
+        from thor_slam_amd.calib import rgbd_pairs, rgbd_undistort
+        from thor_slam_amd.synthetic import SyntheticRGBDSource
+
+        src = SyntheticRGBDSource(seed=rank, n_frames=args.unique, width=width, height=height)
+        cams = extract_cameras(CameraRig([src]).calibration, 2)
+        (ci, _), = rgbd_pairs(cams)
+        rect = rgbd_undistort(cams[ci])
+        rgbd_frames = [src.render_rgbd(i) for i in range(args.unique)]
+        uniq = np.stack([pack_rgbd(b, d) for b, d in rgbd_frames])[:, None, :]   # [n][1][5HW]
+    else:
+        src = SyntheticStereoSource(seed=rank, n_frames=args.unique, width=width, height=height)
+        cams = extract_cameras(CameraRig([src]).calibration, 2)
+        (li, ri), = stereo_pairs(cams)
+        rect = stereo_rectify(cams[li], cams[ri])
+        uniq = render_frames(rank, args.unique, workers, width, height)
     t_render = time.perf_counter() - t_r
 
     total = (args.warmup + args.steps) * B
     idx = torch.from_numpy(triangle_indices(total, args.unique)).cuda()
-    seq = torch.from_numpy(uniq).cuda().index_select(0, idx).contiguous()  # [total, 2, H, W] in HBM
+    seq = torch.from_numpy(uniq).cuda().index_select(0, idx).contiguous()  # [total, 2, H, W] (c5: [total, 1, 5HW]) in HBM
     h = Handle([rect], cfg, max_batch=B, device=dev_index)
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
-    layout = BlockLayout(n_frames=B, n_cams=2, K=cfg.n_features, L=cfg.n_levels)
+    layout = BlockLayout(n_frames=B, n_cams=1 if c5 else 2, K=cfg.n_features, L=cfg.n_levels)
     on_device = args.dist_backend == "nccl"
     # two exchange buffers: batch s packs into buffer s % 2 and all-gathers it asynchronously over
     # RCCL while batch s + 1 computes (the buffer is reused only after its gather has completed)
@@ -294,7 +347,8 @@ def main() -> None:
     for evs in events:
         for i, k in enumerate(names):
             per_kernel_us[k] += evs[i].elapsed_time(evs[i + 1]) * 1e3 / args.steps  # us
-    unit_bytes = frame_bytes(rect.width, rect.height, cfg.n_features)
+    unit_bytes = (frame_bytes(rect.width, rect.height, cfg.n_features, n_img=1, channels=5, matchings=1) if c5 else
+                  frame_bytes(rect.width, rect.height, cfg.n_features))
     dom_bytes = unit_bytes * B          # §8d per-frame bytes x the frames one launch processes
     schur = h.ba_profile(0) if c4 else None
     front = {k: v for k, v in per_kernel_us.items() if k != "local_ba"}
@@ -346,20 +400,26 @@ def main() -> None:
         "algorithmic_bytes_per_frame": unit_bytes,
         "frames_per_launch": B,
         "avg_launch_us": per_kernel_us[dom],
-        "kernel_own_bytes_per_launch": kernel_bytes(dom, B, h, cfg, rect.is_identity),
+        "kernel_own_bytes_per_launch": None if c5 else kernel_bytes(dom, B, h, cfg, rect.is_identity),
         "end_to_end_hbm_frac": unit_bytes * (frames_total / elapsed / world) / (HBM_PEAK_GBS * 1e9),
     }
     if mfma is not None and mfma["time_per_step_us"] > per_kernel_us[dom]:
         roofline, front_roofline = mfma, roofline   # the Schur product is the step's dominant kernel
     else:
         front_roofline = None
-    workload = ("C4: 1x stereo pair 1280x800, 4000 FAST/rBRIEF keypoints per image, 4 levels, stereo+temporal "
-                "brute-force Hamming, P3P-RANSAC(128)+GN pose, 10-keyframe local BA (keyframe every 5 frames, "
-                "5 Gauss-Newton iterations, Schur complement on FP64 MFMA)") if c4 else (
-                "C2: 1x stereo pair 640x400 per GPU, 2000 FAST/rBRIEF keypoints per image, 4 levels, "
-                "stereo+temporal brute-force Hamming, P3P-RANSAC(128)+GN pose")
+    if c5:
+        workload = ("C5: one RGB-D camera per GPU, 1280x720 BGR u8 + aligned u16 mm depth, on-device gray conversion, "
+                    "2000 FAST/rBRIEF keypoints, 4 levels, temporal brute-force Hamming, depth-lookup 3D points, "
+                    "P3P-RANSAC(128)+GN pose")
+    elif c4:
+        workload = ("C4: 1x stereo pair 1280x800, 4000 FAST/rBRIEF keypoints per image, 4 levels, stereo+temporal "
+                    "brute-force Hamming, P3P-RANSAC(128)+GN pose, 10-keyframe local BA (keyframe every 5 frames, "
+                    "5 Gauss-Newton iterations, Schur complement on FP64 MFMA)")
+    else:
+        workload = ("C2: 1x stereo pair 640x400 per GPU, 2000 FAST/rBRIEF keypoints per image, 4 levels, "
+                    "stereo+temporal brute-force Hamming, P3P-RANSAC(128)+GN pose")
     out = {
-        "metric": METRIC_C4 if c4 else METRIC,
+        "metric": METRIC_C4 if c4 else METRIC_C5 if c5 else METRIC,
         "value": frames_total / elapsed,
         "unit": "frames/s",
         "n_gpus": world,
@@ -370,13 +430,14 @@ def main() -> None:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8" + ("+f64" if c4 else ""),
-        "data": f"synthetic: seeded room renderer, {args.unique} distinct {width}x{height} stereo frames per rank "
-                "replayed as a triangle wave, resident in HBM before timing",
+        "data": f"synthetic: seeded room renderer, {args.unique} distinct {width}x{height} "
+                f"{'RGB-D' if c5 else 'stereo'} frames per rank replayed as a triangle wave, resident in HBM before timing",
         "config": {
             "workload": workload,
             "frames_per_step": B,
             "n_features": cfg.n_features,
-            "parallelism": f"one stereo source per GPU x{world}" + (" + RCCL all-gather of keypoints/descriptors" if world > 1 else ""),
+            "parallelism": f"one {'RGB-D camera' if c5 else 'stereo source'} per GPU x{world}"
+                           + (" + RCCL all-gather of keypoints/descriptors" if world > 1 else ""),
         },
         "roofline": roofline,
         "latency_b1_ms": lat_ms,
@@ -387,7 +448,11 @@ def main() -> None:
     if front_roofline is not None:
         out["front_end_roofline"] = front_roofline
     if rank == 0 and args.cpu_budget > 0:
-        out["cpu_baseline"] = cpu_baseline(uniq, rect, cfg, args.cpu_budget, args.cpu_procs)
+        if c5:
+            out["cpu_baseline"] = cpu_baseline_rgbd(np.stack([b for b, _ in rgbd_frames]), np.stack([d for _, d in rgbd_frames]),
+                                                    rect, cfg, args.cpu_budget, args.cpu_procs)
+        else:
+            out["cpu_baseline"] = cpu_baseline(uniq, rect, cfg, args.cpu_budget, args.cpu_procs)
         out["cpu_baseline"]["host_cpus_visible"] = os.cpu_count()
     h.close()
     if world > 1:
