@@ -134,7 +134,8 @@ enum tslam_stage {
     TSLAM_KERNEL_MATCH = 14,        /* includes the scratch memsets */
     TSLAM_KERNEL_MATCH_REFINE = 15,
     TSLAM_KERNEL_POSE = 16,
-    TSLAM_KERNEL_CHAIN = 17
+    TSLAM_KERNEL_CHAIN = 17,
+    TSLAM_KERNEL_RIG = 18           /* rig pose + its chain (after tslam_set_rig) */
 };
 
 const char* tslam_last_error(void);
@@ -183,6 +184,18 @@ int tslam_layout(tslam_handle* h, int64_t* out16, int32_t* level_info18);
 /* Copy the keypoints + descriptors + counts of the last batch into `dst` (device):
  * [n_frames][cams] blocks of (K*8 + K*32 + levels*4) bytes, then a pose trailer per
  * (frame, pair) of T_rel[16] + cov[36] f64 and stats[8] i32.  Returns the total in *bytes. */
+/* Rig pose (replaces the multi-camera fusion cuVSLAM does for the rig of
+ * isaac_ros.py:364-411): base_T_rect[P][16] = the rectified-left frame of each pair in the rig's
+ * base frame (RigCalibration.get_world_extrinsics, rig.py:35-70, composed with the
+ * rectification).  Afterwards every POSE stage also solves one body motion per frame from ALL
+ * pairs' correspondences (generalised PnP: per-pair RANSAC winners as candidates scored on every
+ * pair, then a joint Gauss-Newton) and chains it. */
+int tslam_set_rig(tslam_handle* h, const double* base_T_rect);
+/* Body-frame results of the last batch (synchronises): per frame T_rel (body_{t-1} -> body_t
+ * point map), T_abs (world_T_base, world = base at frame 0), 6x6 covariance, stats
+ * {status, n_corr (all pairs), n_inliers, best candidate count, best candidate, frame, 0, 0}. */
+int tslam_read_rig_poses(tslam_handle* h, double* T_rel, double* T_abs, double* cov, int32_t* stats);
+
 /* A8 window of stereo pair `pair` after the last enqueued solve (synchronises the device),
  * indexed by slot (slot = keyframe number mod ba_window): frames[W] (global frame, -1 = empty),
  * cam_T_world[W][16] (BA estimate), landmark[W][K] (id = home slot * K + keypoint, or -1),

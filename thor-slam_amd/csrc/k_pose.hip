@@ -624,6 +624,268 @@ __global__ __launch_bounds__(256) void k_chain(BatchCtx c) {
     }
 }
 
+// ---- rig pose: generalised PnP over every pair of the rig ---------------
+// One block per frame.  Candidates: each tracked pair's motion moved to the body frame,
+// M_p = (E_p T_p) E_p^-1 with E_p = base_T_rect-left of pair p.  Each candidate is scored on the
+// correspondences of ALL pairs (pair q sees T_q = (E_q^-1 M) E_q, A7's inlier test in its own
+// camera); the most inliers wins (ties: lowest pair).  Gauss-Newton then refines M on the inliers
+// of all pairs together (re-selected every iteration, A7's left-multiplied Cayley update applied to
+// the body motion): with Y = E_q Xc the body point, d(res)/d(rho, omega) = [q, Y x q] where
+// q = dpi/dXc R_e^T.  Covariance sigma^2 H^-1 in the body frame.
+__device__ __forceinline__ void mul4_fixed(const double* A, const double* B, double* out) {
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            out[4 * i + j] = ((A[4 * i] * B[j] + A[4 * i + 1] * B[4 + j]) + A[4 * i + 2] * B[8 + j]) + A[4 * i + 3] * B[12 + j];
+}
+
+#define TS_RIG_MAXP 8
+__global__ __launch_bounds__(POSE_THREADS) void k_rig_pose(BatchCtx c) {
+    __shared__ double s_M[TS_RIG_MAXP][16];                  // candidates (body motions)
+    __shared__ double s_T[TS_RIG_MAXP][TS_RIG_MAXP][12];     // [candidate][pair] R | t
+    __shared__ int s_cnt[4][TS_RIG_MAXP];
+    __shared__ double s_red[4][N_ACC];
+    __shared__ double s_H[36], s_misc[2];
+    __shared__ int s_nc, s_flag, s_best;
+    const int f = blockIdx.x;
+    const int64_t g = c.g0 + f;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int P = c.P, K = c.g.K;
+    double* pout = c.rig_pose + (size_t)f * TS_POSE_DOUBLES;
+    int32_t* sout = c.rig_stats + (size_t)f * TS_STATS_INTS;
+    for (int i = tid; i < TS_POSE_DOUBLES; i += POSE_THREADS) pout[i] = (i < 16 && (i % 5) == 0) ? 1.0 : 0.0;
+    if (g == 0) {
+        if (tid == 0) write_stats(sout, 2, 0, 0, 0, -1, g);
+        return;
+    }
+    if (tid == 0) {
+        int nc = 0;
+        for (int p = 0; p < P; ++p) {
+            if (c.stats[(size_t)(f * P + p) * TS_STATS_INTS] != 0) continue;
+            double Tp[16], ET[16];
+            const double* rel = c.pose + (size_t)(f * P + p) * TS_POSE_DOUBLES;
+            for (int e = 0; e < 16; ++e) Tp[e] = rel[e];
+            mul4_fixed(c.rig_E + 16 * p, Tp, ET);
+            mul4_fixed(ET, c.rig_Einv + 16 * p, s_M[nc]);
+            ++nc;
+        }
+        s_nc = nc;
+    }
+    __syncthreads();
+    const int nc = s_nc;
+    int n_total = 0;
+    for (int q = 0; q < P; ++q) n_total += c.stats[(size_t)(f * P + q) * TS_STATS_INTS + 1];
+    if (nc == 0) {
+        if (tid == 0) write_stats(sout, 1, n_total, 0, 0, -1, g);
+        return;
+    }
+    // per (candidate, pair): T_q = (E_q^-1 M) E_q
+    for (int i = tid; i < nc * P; i += POSE_THREADS) {
+        const int m = i / P, q = i % P;
+        double A[16], T[16];
+        mul4_fixed(c.rig_Einv + 16 * q, s_M[m], A);
+        mul4_fixed(A, c.rig_E + 16 * q, T);
+        for (int r = 0; r < 3; ++r) {
+            for (int k = 0; k < 3; ++k) s_T[m][q][3 * r + k] = T[4 * r + k];
+            s_T[m][q][9 + r] = T[4 * r + 3];
+        }
+    }
+    __syncthreads();
+    // scoring: every candidate on every pair's correspondences (integer counts, order-free)
+    int cnt[TS_RIG_MAXP];
+    for (int m = 0; m < TS_RIG_MAXP; ++m) cnt[m] = 0;
+    const double thr2 = c.pp.thr2;
+    for (int q = 0; q < P; ++q) {
+        const int nq = c.stats[(size_t)(f * P + q) * TS_STATS_INTS + 1];
+        const double* corr = c.corr + ((size_t)f * P + q) * K * TS_CORR_DOUBLES;
+        const double fx = c.calib[q].fx, fy = c.calib[q].fy;
+        for (int ci = tid; ci < nq; ci += POSE_THREADS) {
+            const double* cr = corr + (size_t)ci * TS_CORR_DOUBLES;
+            for (int m = 0; m < nc; ++m) cnt[m] += is_inlier(s_T[m][q], s_T[m][q] + 9, cr, fx, fy, thr2) ? 1 : 0;
+        }
+    }
+    for (int m = 0; m < TS_RIG_MAXP; ++m) {
+        const int w = wave_sum_i32(cnt[m]);
+        if (lane == 0) s_cnt[wave][m] = w;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int best = 0, bc = -1;
+        for (int m = 0; m < nc; ++m) {
+            const int t = ((s_cnt[0][m] + s_cnt[1][m]) + s_cnt[2][m]) + s_cnt[3][m];
+            if (t > bc) {
+                bc = t;
+                best = m;
+            }
+        }
+        s_best = best;
+        s_misc[1] = (double)bc;
+    }
+    __syncthreads();
+    const int best_cnt = (int)s_misc[1], best_idx = s_best;
+    // Gauss-Newton on the body motion (s_M[0] holds the current estimate)
+    if (tid < 16) s_M[0][tid] = s_M[best_idx][tid];
+    __syncthreads();
+    bool fail = false;
+    double sq_last = 0.0;
+    for (int it = 0; it < c.pp.iters; ++it) {
+        for (int q = tid; q < P; q += POSE_THREADS) {
+            double A[16], T[16];
+            mul4_fixed(c.rig_Einv + 16 * q, s_M[0], A);
+            mul4_fixed(A, c.rig_E + 16 * q, T);
+            for (int r = 0; r < 3; ++r) {
+                for (int k = 0; k < 3; ++k) s_T[0][q][3 * r + k] = T[4 * r + k];
+                s_T[0][q][9 + r] = T[4 * r + 3];
+            }
+        }
+        __syncthreads();
+        double acc[N_ACC];
+#pragma unroll
+        for (int k = 0; k < N_ACC; ++k) acc[k] = 0.0;
+        for (int q = 0; q < P; ++q) {
+            const int nq = c.stats[(size_t)(f * P + q) * TS_STATS_INTS + 1];
+            const double* corr = c.corr + ((size_t)f * P + q) * K * TS_CORR_DOUBLES;
+            const PairCalib cal = c.calib[q];
+            const double fx = cal.fx, fy = cal.fy, cx = cal.cx, cy = cal.cy;
+            const double* R = s_T[0][q];
+            const double* t = R + 9;
+            const double* E = c.rig_E + 16 * q;
+            for (int ci = tid; ci < nq; ci += POSE_THREADS) {
+                const double* cr = corr + (size_t)ci * TS_CORR_DOUBLES;
+                if (!is_inlier(R, t, cr, fx, fy, thr2)) continue;
+                const double X = cr[0], Y = cr[1], Z = cr[2];
+                const double u = cx - cr[3], v = cy - cr[4];
+                const double xc = ((R[0] * X + R[1] * Y) + R[2] * Z) + t[0];
+                const double yc = ((R[3] * X + R[4] * Y) + R[5] * Z) + t[1];
+                const double zc = ((R[6] * X + R[7] * Y) + R[8] * Z) + t[2];
+                const double iz = 1.0 / zc;
+                const double rx = (((fx * xc) * iz) + cx) - u;
+                const double ry = (((fy * yc) * iz) + cy) - v;
+                const double a = fx * iz, b = fy * iz;
+                const double cc = (-(fx * xc)) * (iz * iz);
+                const double dd = (-(fy * yc)) * (iz * iz);
+                const double by0 = ((E[0] * xc + E[1] * yc) + E[2] * zc) + E[3];
+                const double by1 = ((E[4] * xc + E[5] * yc) + E[6] * zc) + E[7];
+                const double by2 = ((E[8] * xc + E[9] * yc) + E[10] * zc) + E[11];
+                // q = dpi/dXc R_e^T: q_j = sum_i p_i R_e[j][i]
+                const double qx0 = a * E[0] + cc * E[2], qx1 = a * E[4] + cc * E[6], qx2 = a * E[8] + cc * E[10];
+                const double qy0 = b * E[1] + dd * E[2], qy1 = b * E[5] + dd * E[6], qy2 = b * E[9] + dd * E[10];
+                const double jx[6] = {qx0, qx1, qx2, by1 * qx2 - by2 * qx1, by2 * qx0 - by0 * qx2, by0 * qx1 - by1 * qx0};
+                const double jy[6] = {qy0, qy1, qy2, by1 * qy2 - by2 * qy1, by2 * qy0 - by0 * qy2, by0 * qy1 - by1 * qy0};
+                int k = 0;
+#pragma unroll
+                for (int r0 = 0; r0 < 6; ++r0)
+#pragma unroll
+                    for (int c0 = r0; c0 < 6; ++c0) acc[k++] += jx[r0] * jx[c0] + jy[r0] * jy[c0];
+#pragma unroll
+                for (int r0 = 0; r0 < 6; ++r0) acc[21 + r0] += jx[r0] * rx + jy[r0] * ry;
+                acc[27] += rx * rx + ry * ry;
+                acc[28] += 1.0;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < N_ACC; ++k) {
+            const double w = wave_sum_f64(acc[k]);
+            if (lane == 0) s_red[wave][k] = w;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            double tot[N_ACC];
+            for (int k = 0; k < N_ACC; ++k) tot[k] = ((s_red[0][k] + s_red[1][k]) + s_red[2][k]) + s_red[3][k];
+            s_flag = 0;
+            double Hm[36], gv[6], x[6], L[36];
+            int k = 0;
+            for (int r0 = 0; r0 < 6; ++r0)
+                for (int c0 = r0; c0 < 6; ++c0) {
+                    Hm[r0 * 6 + c0] = tot[k];
+                    Hm[c0 * 6 + r0] = tot[k];
+                    ++k;
+                }
+            for (int r0 = 0; r0 < 6; ++r0) gv[r0] = -tot[21 + r0];
+            for (int q = 0; q < 36; ++q) L[q] = 0.0;
+            if ((int)tot[28] < 6 || !solve6(Hm, gv, x, L)) {
+                s_flag = 1;
+            } else {
+                const double w0 = x[3], w1 = x[4], w2 = x[5];
+                const double A[9] = {0.0, -w2, w1, w2, 0.0, -w0, -w1, w0, 0.0};
+                double A2[9];
+                for (int i = 0; i < 3; ++i)
+                    for (int j = 0; j < 3; ++j) A2[3 * i + j] = (A[3 * i] * A[j] + A[3 * i + 1] * A[3 + j]) + A[3 * i + 2] * A[6 + j];
+                const double n2 = (w0 * w0 + w1 * w1) + w2 * w2;
+                const double sc = 4.0 / (4.0 + n2);
+                double RU[9];
+                for (int q = 0; q < 9; ++q) RU[q] = ((q % 4) == 0 ? 1.0 : 0.0) + sc * (A[q] + 0.5 * A2[q]);
+                double* M = s_M[0];
+                double Rn[9], tn[3];
+                for (int i = 0; i < 3; ++i) {
+                    for (int j = 0; j < 3; ++j) Rn[3 * i + j] = (RU[3 * i] * M[j] + RU[3 * i + 1] * M[4 + j]) + RU[3 * i + 2] * M[8 + j];
+                    tn[i] = ((RU[3 * i] * M[3] + RU[3 * i + 1] * M[7]) + RU[3 * i + 2] * M[11]) + x[i];
+                }
+                for (int i = 0; i < 3; ++i) {
+                    for (int j = 0; j < 3; ++j) M[4 * i + j] = Rn[3 * i + j];
+                    M[4 * i + 3] = tn[i];
+                }
+                for (int q = 0; q < 36; ++q) s_H[q] = Hm[q];
+                s_misc[0] = tot[27];
+            }
+        }
+        __syncthreads();
+        if (s_flag) {
+            fail = true;
+            break;
+        }
+        sq_last = s_misc[0];
+    }
+    // final inliers of all pairs under M
+    for (int q = tid; q < P; q += POSE_THREADS) {
+        double A[16], T[16];
+        mul4_fixed(c.rig_Einv + 16 * q, s_M[0], A);
+        mul4_fixed(A, c.rig_E + 16 * q, T);
+        for (int r = 0; r < 3; ++r) {
+            for (int k = 0; k < 3; ++k) s_T[0][q][3 * r + k] = T[4 * r + k];
+            s_T[0][q][9 + r] = T[4 * r + 3];
+        }
+    }
+    __syncthreads();
+    int cnt_local = 0;
+    if (!fail)
+        for (int q = 0; q < P; ++q) {
+            const int nq = c.stats[(size_t)(f * P + q) * TS_STATS_INTS + 1];
+            const double* corr = c.corr + ((size_t)f * P + q) * K * TS_CORR_DOUBLES;
+            for (int ci = tid; ci < nq; ci += POSE_THREADS)
+                cnt_local += is_inlier(s_T[0][q], s_T[0][q] + 9, corr + (size_t)ci * TS_CORR_DOUBLES, c.calib[q].fx,
+                                       c.calib[q].fy, thr2) ? 1 : 0;
+        }
+    cnt_local = wave_sum_i32(cnt_local);
+    if (lane == 0) s_cnt[wave][0] = cnt_local;
+    __syncthreads();
+    if (tid == 0) {
+        const int n_in = ((s_cnt[0][0] + s_cnt[1][0]) + s_cnt[2][0]) + s_cnt[3][0];
+        const bool ok = !fail && n_in >= c.pp.min_inliers;
+        write_stats(sout, ok ? 0 : 1, n_total, fail ? 0 : n_in, best_cnt, best_idx, g);
+        if (ok) {
+            for (int e = 0; e < 12; ++e) pout[e] = s_M[0][e];
+            const double sigma2 = sq_last / (double)max(1, 2 * n_in - 6);
+            double L[36], e6[6], col[6];
+            for (int q = 0; q < 36; ++q) L[q] = 0.0;
+            for (int k = 0; k < 6; ++k) {
+                for (int q = 0; q < 6; ++q) e6[q] = q == k ? 1.0 : 0.0;
+                if (solve6(s_H, e6, col, L))
+                    for (int q = 0; q < 6; ++q) pout[32 + q * 6 + k] = col[q] * sigma2;
+            }
+        }
+    }
+}
+
+void launch_rig(const BatchCtx& c, hipStream_t s) {
+    hipLaunchKernelGGL(k_rig_pose, dim3(c.n), dim3(POSE_THREADS), 0, s, c);
+    BatchCtx r = c;   // chain the body motions with the pair chain kernel: one "pair", the rig
+    r.pose = c.rig_pose;
+    r.stats = c.rig_stats;
+    r.state = c.rig_state;
+    r.P = 1;
+    hipLaunchKernelGGL(k_chain, dim3(1), dim3(256), 0, s, r);
+}
+
 int ransac_splits(const BatchCtx& c) {
     if (c.pp.splits > 0) return min(min(c.pp.splits, c.pp.n_hyp), TS_MAX_SPLITS);
     // enough blocks to cover the chip (>= 512), at least 8 hypotheses per split

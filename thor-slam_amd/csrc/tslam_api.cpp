@@ -50,6 +50,12 @@ struct tslam_handle {
     int32_t* d_maps = nullptr;
     uint32_t* d_brief = nullptr;
     uint8_t* d_gray = nullptr;   // RGB-D: converted colour images [B][P][H][W]
+    // rig pose (tslam_set_rig): E = base_T_rect-left per pair, its inverse, body-frame results
+    bool rig = false;
+    double* d_rig_E = nullptr;
+    double* d_rig_pose = nullptr;
+    int32_t* d_rig_stats = nullptr;
+    double* d_rig_state = nullptr;
     int64_t* d_wedges = nullptr;
     Buffer buf[TSLAM_BUF_COUNT];
     uint32_t* d_cand = nullptr;
@@ -252,6 +258,11 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.pose = (double*)h->buf[TSLAM_BUF_POSE].ptr;
     c.stats = (int32_t*)h->buf[TSLAM_BUF_STATS].ptr;
     c.state = h->d_state;
+    c.rig_E = h->d_rig_E;
+    c.rig_Einv = h->d_rig_E ? h->d_rig_E + 16 * h->P : nullptr;
+    c.rig_pose = h->d_rig_pose;
+    c.rig_stats = h->d_rig_stats;
+    c.rig_state = h->d_rig_state;
     c.ransac = h->d_ransac;
     c.brief_table = h->d_brief;
     c.wedges = h->d_wedges;
@@ -432,6 +443,7 @@ int tslam_reset(tslam_handle* h) {
     for (int p = 0; p < h->P; ++p)
         for (int k = 0; k < 4; ++k) eye[(size_t)p * 16 + 5 * k] = 1.0;
     HIPCHK(hipMemcpy(h->d_state, eye.data(), sizeof(double) * eye.size(), hipMemcpyHostToDevice));
+    if (h->d_rig_state) HIPCHK(hipMemcpy(h->d_rig_state, eye.data(), sizeof(double) * 16, hipMemcpyHostToDevice));
     h->frames_done = 0;
     for (int i = 0; i < TS_BA_MAXW; ++i) h->ba_frame[i] = -1;
     h->ba_nkf = 0;
@@ -477,7 +489,11 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
         case TSLAM_STAGE_DETECT: launch_detect(c, s); launch_select(c, s); break;
         case TSLAM_STAGE_DESCRIBE: launch_describe(c, s); break;
         case TSLAM_STAGE_MATCH: launch_match(c, s); launch_match_refine(c, s); break;
-        case TSLAM_STAGE_POSE: launch_pose(c, s); launch_chain(c, s); break;
+        case TSLAM_STAGE_POSE:
+            launch_pose(c, s);
+            launch_chain(c, s);
+            if (h->rig) launch_rig(c, s);
+            break;
         case TSLAM_STAGE_ALL:
             launch_rectify_pyramid(c, s);
             launch_detect(c, s);
@@ -487,7 +503,12 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
             launch_match_refine(c, s);
             launch_pose(c, s);
             launch_chain(c, s);
+            if (h->rig) launch_rig(c, s);
             if (h->prm.ba_window) run_ba(h, c, s);
+            break;
+        case TSLAM_KERNEL_RIG:
+            if (!h->rig) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig)");
+            launch_rig(c, s);
             break;
         case TSLAM_STAGE_BA:
             if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
@@ -614,6 +635,55 @@ int tslam_pack_features(tslam_handle* h, void* dst, int64_t* bytes, void* stream
     const BatchCtx c = make_ctx(h);
     launch_pack(c, (uint8_t*)dst, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
+    return TSLAM_OK;
+}
+
+int tslam_set_rig(tslam_handle* h, const double* base_T_rect) {
+    if (!h || !base_T_rect) return fail(TSLAM_EINVAL, "bad argument");
+    if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_set_rig inside a batch");
+    HIPCHK(hipSetDevice(h->device));
+    const int P = h->P;
+    std::vector<double> e(32 * (size_t)P, 0.0);
+    for (int p = 0; p < P; ++p) {
+        const double* E = base_T_rect + 16 * p;
+        double* inv = e.data() + 16 * (P + p);
+        for (int i = 0; i < 16; ++i) e[16 * p + i] = E[i];
+        if (E[12] != 0.0 || E[13] != 0.0 || E[14] != 0.0 || E[15] != 1.0) return fail(TSLAM_EINVAL, "base_T_rect must be rigid 4x4");
+        for (int i = 0; i < 3; ++i) {   // [R^T | -R^T t]
+            for (int j = 0; j < 3; ++j) inv[4 * i + j] = E[4 * j + i];
+            inv[4 * i + 3] = -((E[i] * E[3] + E[4 + i] * E[7]) + E[8 + i] * E[11]);
+        }
+        inv[15] = 1.0;
+    }
+    if (!h->d_rig_E) {
+        int rc = dev_alloc(h, (void**)&h->d_rig_E, sizeof(double) * 32 * P);
+        if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rig_pose, sizeof(double) * TS_POSE_DOUBLES * h->B);
+        if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rig_stats, sizeof(int32_t) * TS_STATS_INTS * h->B);
+        if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rig_state, sizeof(double) * 16);
+        if (rc != TSLAM_OK) return rc;
+        const double eye[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+        HIPCHK(hipMemcpy(h->d_rig_state, eye, sizeof(eye), hipMemcpyHostToDevice));
+    }
+    HIPCHK(hipMemcpy(h->d_rig_E, e.data(), sizeof(double) * e.size(), hipMemcpyHostToDevice));
+    h->rig = true;
+    return TSLAM_OK;
+}
+
+int tslam_read_rig_poses(tslam_handle* h, double* T_rel, double* T_abs, double* cov, int32_t* stats) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (!h->rig) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig)");
+    int rc = tslam_sync(h);
+    if (rc != TSLAM_OK) return rc;
+    const int n = h->cur_n;
+    std::vector<double> pose((size_t)n * TS_POSE_DOUBLES);
+    HIPCHK(hipMemcpy(pose.data(), h->d_rig_pose, sizeof(double) * pose.size(), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; ++i) {
+        const double* src = pose.data() + (size_t)i * TS_POSE_DOUBLES;
+        if (T_rel) memcpy(T_rel + 16 * (size_t)i, src, 16 * sizeof(double));
+        if (T_abs) memcpy(T_abs + 16 * (size_t)i, src + 16, 16 * sizeof(double));
+        if (cov) memcpy(cov + 36 * (size_t)i, src + 32, 36 * sizeof(double));
+    }
+    if (stats) HIPCHK(hipMemcpy(stats, h->d_rig_stats, sizeof(int32_t) * TS_STATS_INTS * (size_t)n, hipMemcpyDeviceToHost));
     return TSLAM_OK;
 }
 

@@ -110,6 +110,12 @@ struct BatchCtx {
     double* ransac;        // [B][P][TS_MAX_SPLITS][13] split winners (key word + pose)
     int32_t* stats;
     double* state;
+    // rig: base_T_rect-left of each pair and its inverse, body-frame results
+    const double* rig_E;   // [P][16]
+    const double* rig_Einv;
+    double* rig_pose;      // [B][68]  body T_rel, T_abs, cov
+    int32_t* rig_stats;    // [B][8]
+    double* rig_state;     // [16]
     const uint32_t* brief_table;  // [30][256] LDS patch byte offsets of the two points (lo | hi << 16)
     const int64_t* wedges;        // [31][2]
     PairCalib calib[8];
@@ -130,6 +136,7 @@ void launch_match_refine(const BatchCtx& c, hipStream_t s);
 void launch_pose(const BatchCtx& c, hipStream_t s);
 void launch_chain(const BatchCtx& c, hipStream_t s);
 void launch_pack(const BatchCtx& c, uint8_t* dst, hipStream_t s);
+void launch_rig(const BatchCtx& c, hipStream_t s);
 void launch_rgbd_gray(const BatchCtx& c, uint8_t* gray, hipStream_t s);
 void launch_rgbd_depth(const BatchCtx& c, hipStream_t s);
 

@@ -83,6 +83,8 @@ _SIGNATURES = {
     "tslam_ring_slot": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "tslam_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_pack_features": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
+    "tslam_set_rig": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_read_rig_poses": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 4),
     "tslam_ba_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6),
     "tslam_ba_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
@@ -231,6 +233,22 @@ class Handle:
             "T_rel": t_rel.reshape(shape + (4, 4)), "T_abs": t_abs.reshape(shape + (4, 4)),
             "cov": cov.reshape(shape + (6, 6)), "stats": stats.reshape(shape + (8,)),
         }
+
+    def set_rig(self, base_T_rect: list) -> None:
+        """Enable the rig pose: base_T_rect-left (4x4) of every pair, in pair order."""
+        e = np.ascontiguousarray(np.stack([np.asarray(m, dtype=np.float64) for m in base_T_rect]))
+        if e.shape != (self.n_pairs, 4, 4):
+            raise ValueError(f"need {self.n_pairs} 4x4 matrices")
+        _check(self.lib.tslam_set_rig(self.h, e.ctypes.data))
+
+    def read_rig_poses(self, n_frames: int) -> dict:
+        """Body-frame rig motion of the last batch (synchronises)."""
+        t_rel = np.zeros((n_frames, 4, 4))
+        t_abs = np.zeros((n_frames, 4, 4))
+        cov = np.zeros((n_frames, 6, 6))
+        stats = np.zeros((n_frames, 8), dtype=np.int32)
+        _check(self.lib.tslam_read_rig_poses(self.h, t_rel.ctypes.data, t_abs.ctypes.data, cov.ctypes.data, stats.ctypes.data))
+        return {"T_rel": t_rel, "T_abs": t_abs, "cov": cov, "stats": stats}
 
     # -- buffer access (tests) -------------------------------------------------------------
     def buffer_info(self, which: str) -> tuple[int, int, int]:
