@@ -13,7 +13,7 @@ from helpers import make_source, rel_frobenius, scenario
 from oracle import numpy_slam as O
 from thor_slam_amd.calib import extract_cameras, stereo_pairs, stereo_rectify
 from thor_slam_amd.camera import CameraRig, Extrinsics
-from thor_slam_amd.dist import fuse_rig_motion
+from oracle.numpy_rig import RigChain, rig_pose
 from thor_slam_amd.params import HipSlamConfig
 from thor_slam_amd.slam import TrackingState
 from thor_slam_amd.synthetic import RoomScene, SyntheticStereoSource, circle_trajectory
@@ -102,7 +102,7 @@ def test_engine_batched_mode_returns_completed_poses():
     assert rel_frobenius(f3.to_4x4_matrix(), f1.to_4x4_matrix()) < 1e-12
 
 
-def test_engine_two_source_rig_fuses_motion():
+def test_engine_two_source_rig_solves_body_motion():
     from thor_slam_amd.slam.hip_engine import HipSlamEngine
 
     mats = json.loads((Path(__file__).parent / "golden" / "brackets_joints.json").read_text())
@@ -127,12 +127,15 @@ def test_engine_two_source_rig_fuses_motion():
     by_name = {s.name: s for s in srcs}
     trks = [O.OracleTracker(HipSlamConfig(), dict(fx=r.fx, fy=r.fy, cx=r.cx, cy=r.cy, baseline=r.baseline,
                                                   map_l=r.map_left, map_r=r.map_right)) for r in rects]
+    chain = RigChain()
     want = np.eye(4)
     for i in range(n):
         outs = [trk.step(by_name[cams[l].source_name].render_image(i, 0), by_name[cams[l].source_name].render_image(i, 1))
                 for trk, (l, _) in zip(trks, pairs)]
         if i:
-            want = want @ fuse_rig_motion(bts, [o["T"] for o in outs], [o["cov"] for o in outs], [o["status"] == 0 for o in outs])
+            items = [{"status": o["status"], "T": o["T"], "corr": o.get("corr"), "intr": (r.fx, r.fy, r.cx, r.cy)}
+                     for o, r in zip(outs, rects)]
+            want = chain.step(rig_pose(items, bts, HipSlamConfig()))
     assert rel_frobenius(pose.to_4x4_matrix(), want) < 1e-9
     gt = np.linalg.inv(traj[0]) @ traj[n - 1]
     err = np.linalg.norm(pose.position - gt[:3, 3])

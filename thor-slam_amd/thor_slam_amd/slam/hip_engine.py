@@ -40,7 +40,6 @@ from ..calib import (StereoRectification, confidence_from_covariance, extract_ca
                      stereo_pairs, stereo_rectify)
 from ..camera.rig import RigCalibration
 from ..camera.types import SynchronizedFrameSet
-from ..dist import fuse_rig_motion
 from ..params import HipSlamConfig
 from ..rgbd import pack_rgbd
 from .interface import CameraConfig, MapPoint, SlamConfig, SlamEngine, SlamMap, SlamPose, TrackingState
@@ -127,7 +126,8 @@ class HipSlamEngine(SlamEngine):
             self._base_T_rects = [self._cameras[l].extrinsics.to_4x4_matrix() @ r.left_optical_T_rect()
                                   for (l, _), r in zip(self._pairs, self._rects)]
             self._base_T_rect = self._base_T_rects[0]
-            self._world_T_base = np.eye(4)
+            if len(self._pairs) > 1:   # the rig's body motion is solved on the device from all pairs
+                self._handle.set_rig(self._base_T_rects)
         except RuntimeError:
             raise
         except Exception as exc:  # per interface.py:187-188
@@ -190,7 +190,7 @@ class HipSlamEngine(SlamEngine):
         stream = torch.cuda.current_stream(self._device)
         self._dev_images[:n].copy_(self._host_images[:n], non_blocking=True)
         self._handle.submit(self._dev_images.data_ptr(), n, stream.cuda_stream)
-        res = self._handle.read_poses(n)
+        res = self._read(n)
         stamps = [ts for _, ts in self._staged]
         self._staged = []
         self._publish(res, stamps)
@@ -203,8 +203,14 @@ class HipSlamEngine(SlamEngine):
         n = int(images.shape[0])
         s = stream if stream is not None else self._torch.cuda.current_stream(self._device)
         self._handle.submit(images.data_ptr(), n, s.cuda_stream)
-        res = self._handle.read_poses(n)
+        res = self._read(n)
         self._publish(res, timestamps or [float(i) for i in range(n)])
+        return res
+
+    def _read(self, n: int) -> dict:
+        res = self._handle.read_poses(n)
+        if len(self._pairs) > 1:
+            res["rig"] = self._handle.read_rig_poses(n)
         return res
 
     def _body_pose(self, res: dict, k: int) -> tuple[int, np.ndarray, np.ndarray]:
@@ -218,17 +224,12 @@ class HipSlamEngine(SlamEngine):
             body = bt @ res["T_abs"][k, 0] @ _invert(bt)
             cov = rot6 @ res["cov"][k, 0] @ rot6.T if status == POSE_OK else np.zeros((6, 6))
             return status, body, cov
-        # multi-pair rig: information-weighted fusion of the per-pair body motions, chained here
-        if (stats == POSE_INIT).all():
-            self._world_T_base = np.eye(4)
-            return POSE_INIT, self._world_T_base.copy(), np.zeros((6, 6))
-        ok = [int(st) == POSE_OK for st in stats]
-        motion = fuse_rig_motion(self._base_T_rects, list(res["T_rel"][k]), list(res["cov"][k]), ok)
-        if motion is None:
-            return POSE_LOST, self._world_T_base.copy(), np.zeros((6, 6))
-        self._world_T_base = self._world_T_base @ motion
-        best = int(np.argmax([res["stats"][k, p, 2] if ok[p] else -1 for p in range(len(ok))]))
-        return POSE_OK, self._world_T_base.copy(), rot6 @ res["cov"][k, best] @ rot6.T
+        # multi-pair rig: the device's generalised PnP over all pairs (k_rig_pose), already in the
+        # base frame and chained (world = base_link at the first frame)
+        rig = res["rig"]
+        status = int(rig["stats"][k, 0])
+        cov = rig["cov"][k] if status == POSE_OK else np.zeros((6, 6))
+        return status, rig["T_abs"][k].copy(), cov
 
     def _ba_corrections(self, res: dict, n: int):
         """Per frame of the batch: the rect-frame correction W_ba(kf) inv(W_fe(kf)) (or None)."""
@@ -327,7 +328,6 @@ class HipSlamEngine(SlamEngine):
         self._staged = []
         self._keyframe_poses = []
         self._fe_at, self._kf_final, self._kf_stamp, self._ba_window = {}, {}, {}, None
-        self._world_T_base = np.eye(4)
         if self._handle is not None:
             self._handle.reset()
         self._state = TrackingState.INITIALIZING
