@@ -210,6 +210,19 @@ int tslam_ba_read(tslam_handle* h, int pair, int64_t* frames, double* cam_T_worl
  * `max_launches` further launches (0 = off). */
 int tslam_ba_profile(tslam_handle* h, int max_launches, double* schur_ms, int64_t* schur_launches, double* schur_flops);
 
+/* Map side of A8 for persistence (synchronises): per landmark id of pair `pair`'s window the
+ * global landmark id (creation frame * K + keypoint; -1 / stale where no landmark lives) and the
+ * rBRIEF descriptor of the keyframe keypoint the id names: gid[W*K], desc[W*K][8]. */
+int tslam_ba_read_map(tslam_handle* h, int pair, int64_t* gid, uint32_t* desc);
+
+/* Relocalisation (SlamEngine.load_map / relocalize, interface.py:239-256): upload a map of n
+ * landmarks (world xyz f64 [n][3], rBRIEF-256 [n][8]; n < 2^20), then solve cam_T_world of a
+ * resident frame's left camera of `pair` by brute-force Hamming matching of its keypoints against
+ * the map (ratio + max_hamming as A6) and A7's P3P-RANSAC + Gauss-Newton.  stats as
+ * tslam_read_poses (status 0 = relocalised); cam_T_world = identity when it fails. */
+int tslam_map_upload(tslam_handle* h, const double* xyz, const uint32_t* desc, int64_t n);
+int tslam_relocalize(tslam_handle* h, int pair, int64_t frame, double* cam_T_world, double* cov, int32_t* stats);
+
 int tslam_pack_features(tslam_handle* h, void* dst, int64_t* bytes, void* stream);
 
 #ifdef __cplusplus

@@ -1,0 +1,62 @@
+"""SURVEY.md §8f item 3 — relocalisation in a saved map, CPU restatement.
+
+TEST INFRASTRUCTURE (see ``oracle/__init__.py``): the checker for ``k_reloc.hip``.  The map is a
+set of landmarks (world xyz + rBRIEF-256).  Spec:
+
+* every valid keypoint of the frame's left image is matched against ALL map descriptors:
+  best = lexicographic min of (Hamming distance, map index), second = min distance over the other
+  map points; accepted iff best <= max_hamming and (no second or 100 * best < ratio_pct * second);
+* the matches, in keypoint order, are 3D-2D correspondences (map point, level-0 keypoint
+  position) and A7's ``estimate_pose`` (RNG seeded by the frame index) gives cam_T_world.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from .numpy_slam import estimate_pose, level0_coords
+
+_POP8 = np.array([bin(i).count("1") for i in range(256)], dtype=np.int64)
+
+
+def hamming(q: np.ndarray, m: np.ndarray) -> np.ndarray:
+    """Distances between descriptor rows q [nq][8] u32 and m [nm][8] u32 -> [nq][nm]."""
+    x = (q[:, None, :] ^ m[None, :, :]).view(np.uint8)
+    return _POP8[x].sum(-1)
+
+
+def match_map(feat: dict, map_desc: np.ndarray, cfg, chunk: int = 256) -> np.ndarray:
+    K = feat["desc"].shape[0]
+    out = np.full(K, -1, dtype=np.int64)
+    qs = np.nonzero(feat["valid"])[0]
+    M = map_desc.shape[0]
+    if M == 0:
+        return out
+    for a in range(0, qs.size, chunk):
+        q = qs[a:a + chunk]
+        d = hamming(feat["desc"][q].astype(np.uint32), map_desc.astype(np.uint32))
+        best = np.argmin(d, axis=1)                   # first minimum = lowest index
+        bd = d[np.arange(q.size), best]
+        if M > 1:
+            d2 = d.copy()
+            d2[np.arange(q.size), best] = 1 << 30
+            sd = d2.min(axis=1)
+            ok = (bd <= cfg.max_hamming) & (100 * bd < cfg.ratio_pct * sd)
+        else:
+            ok = bd <= cfg.max_hamming
+        out[q[ok]] = best[ok]
+    return out
+
+
+def relocalize(feat: dict, map_xyz: np.ndarray, map_desc: np.ndarray, intr, cfg, frame: int) -> dict:
+    fx, fy, cx, cy = intr
+    m = match_map(feat, map_desc, cfg)
+    j = np.nonzero(m >= 0)[0]
+    kp = feat["kp"]
+    u, v = level0_coords(kp["x"][j], kp["y"][j], kp["level"][j])
+    xyz = map_xyz[m[j]]
+    corr = {"X": xyz[:, 0], "Y": xyz[:, 1], "Z": xyz[:, 2], "du": cx - u, "dv": cy - v, "u": u, "v": v,
+            "j": j, "i": m[j]}
+    res = estimate_pose(corr, intr, cfg, frame)
+    res["matches"] = m
+    return res

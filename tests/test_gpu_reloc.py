@@ -1,0 +1,79 @@
+"""Map persistence + relocalisation: the A8 window's landmarks carry the
+descriptors of their keyframe keypoints; a map built from them relocalises a frame of a fresh
+handle.  HIP ``k_reloc`` vs ``oracle/numpy_map.py``: matches, RANSAC winner and inlier counts
+identical, cam_T_world within 1e-9 relative Frobenius."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from helpers import rel_frobenius
+from oracle.numpy_map import relocalize
+from test_gpu_ba import _scenario_and_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_map(sc, want):
+    """Landmarks of the oracle's final window: world xyz (rect frame 0) + keyframe descriptors."""
+    K = sc["cfg"].n_features
+    w = want[-1]
+    ids = np.unique(w["lm"][w["frames"] >= 0])
+    ids = ids[ids >= 0]
+    desc = np.stack([sc["oracle"][int(w["frames"][i // K])]["cur"]["left"]["desc"][i % K] for i in ids])
+    return ids, w["X"][ids], desc.astype(np.uint32)
+
+
+def test_window_map_descriptors_and_relocalisation():
+    import torch
+
+    from thor_slam_amd._lib import Handle
+    from thor_slam_amd.params import HipSlamConfig
+
+    sc, want = _scenario_and_oracle(12)
+    ids, xyz, desc = _oracle_map(sc, want)
+    # 1. the device window exports the same map (descriptors bit-exact, positions to 1e-9)
+    h = Handle([sc["rect"]], sc["cfg"], max_batch=12)
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    h.submit(dev.data_ptr(), 12, torch.cuda.current_stream().cuda_stream)
+    win, mp = h.ba_read(0), h.ba_read_map(0)
+    h.close()
+    np.testing.assert_array_equal(mp["desc"][ids], desc)
+    assert np.abs(win["X"][ids] - xyz).max() < 1e-9 * np.abs(xyz).max()
+    gids = mp["gid"][ids]
+    assert np.unique(gids).size == gids.size and (gids >= 0).all()
+    # 2. relocalise frames of a fresh handle (no BA) against that map
+    cfg = HipSlamConfig()
+    rect = sc["rect"]
+    intr = (rect.fx, rect.fy, rect.cx, rect.cy)
+    h = Handle([rect], cfg, max_batch=4)
+    h.map_upload(xyz, desc)
+    h.submit(dev[8:].data_ptr(), 4, torch.cuda.current_stream().cuda_stream)   # frames 8..11 as 0..3
+    for f in range(4):
+        got = h.relocalize(f)
+        o = relocalize(sc["oracle"][8 + f]["cur"]["left"], xyz, desc, intr, cfg, f)
+        assert got["stats"][0] == o["status"] == 0, (f, got["stats"])
+        assert got["stats"][1] == o["n_corr"] and got["stats"][2] == o["n_inliers"] and got["stats"][4] == o["best_hyp"]
+        assert rel_frobenius(got["T"], o["T"]) < 1e-9
+        # the map frame is rect-left of frame 0: cam_T_world ~ inv(front-end world_T_cam)
+        fe = np.linalg.inv(sc["oracle"][8 + f]["world_T_cam"])
+        assert np.linalg.norm(got["T"][:3, 3] - fe[:3, 3]) < 0.02
+    h.close()
+
+
+def test_relocalise_fails_cleanly_on_an_unrelated_map():
+    import torch
+
+    from thor_slam_amd._lib import Handle
+    from thor_slam_amd.params import HipSlamConfig
+
+    sc, _ = _scenario_and_oracle(12)
+    rng = np.random.default_rng(0)
+    h = Handle([sc["rect"]], HipSlamConfig(), max_batch=1)
+    h.map_upload(rng.normal(size=(500, 3)), rng.integers(0, 2**32, size=(500, 8), dtype=np.uint32))
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    h.submit(dev.data_ptr(), 1, torch.cuda.current_stream().cuda_stream)
+    got = h.relocalize(0)
+    h.close()
+    assert got["stats"][0] != 0 and np.array_equal(got["T"], np.eye(4))

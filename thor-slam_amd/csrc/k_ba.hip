@@ -83,8 +83,10 @@ __global__ __launch_bounds__(256) void k_ba_evict_move(BatchCtx c, BaArgs a) {
     const int hr = key / K;
     const int nid = a.order[hr] * K + (key - hr * K);
     q.lm[o] = nid;
-    if (key == i)   // the new home copies the position (sources lie in the evicted slot's range)
+    if (key == i) {   // the new home copies the position and global id (sources: the evicted slot)
         for (int e = 0; e < 3; ++e) q.X[(size_t)nid * 3 + e] = q.X[(size_t)id * 3 + e];
+        q.gid[nid] = q.gid[id];
+    }
 }
 
 // Insertion of frame a.frame into slot a.slot (every block derives the pose; block 0 stores it).
@@ -134,12 +136,17 @@ __global__ __launch_bounds__(256) void k_ba_insert(BatchCtx c, BaArgs a) {
         }
         if (valid && lm < 0 && has_d) {
             lm = a.slot * K + k;
+            q.gid[lm] = g * K + k;
             const double z = cal.fxb / dd;
             const double xc[3] = {(u - cal.cx) * z / cal.fx, (v - cal.cy) * z / cal.fy, z};
             for (int e = 0; e < 3; ++e)   // R^T (xc - t)
                 q.X[(size_t)lm * 3 + e] = ((s_T[e] * (xc[0] - s_T[3]) + s_T[4 + e] * (xc[1] - s_T[7])) + s_T[8 + e] * (xc[2] - s_T[11]));
         }
         const size_t o = (size_t)a.slot * K + k;
+        const uint4* dsrc = reinterpret_cast<const uint4*>(c.desc + (((size_t)rslot * c.C + c.cpp * p) * K + k) * 8);
+        uint4* ddst = reinterpret_cast<uint4*>(q.kf_desc + o * 8);
+        ddst[0] = dsrc[0];
+        ddst[1] = dsrc[1];
         q.u[o] = valid ? u : __builtin_nan("");
         q.v[o] = valid ? v : __builtin_nan("");
         q.d[o] = has_d ? dd : __builtin_nan("");

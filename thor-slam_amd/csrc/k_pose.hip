@@ -904,6 +904,15 @@ void launch_pose(const BatchCtx& c, hipStream_t s) {
     hipLaunchKernelGGL(k_refine, dim3(c.n * c.P), dim3(POSE_THREADS), 0, s, c, S);
 }
 
+// RANSAC + refinement only, on correspondences another kernel wrote (relocalisation).
+void launch_pose_solve(const BatchCtx& c, hipStream_t s) {
+    const int S = ransac_splits(c);
+    const int hs = (c.pp.n_hyp + S - 1) / S;
+    const size_t lds = (size_t)4 * hs * 12 * sizeof(double);
+    hipLaunchKernelGGL(k_ransac, dim3(c.n * c.P * S), dim3(POSE_THREADS), lds, s, c, S);
+    hipLaunchKernelGGL(k_refine, dim3(c.n * c.P), dim3(POSE_THREADS), 0, s, c, S);
+}
+
 void launch_chain(const BatchCtx& c, hipStream_t s) {
     hipLaunchKernelGGL(k_chain, dim3(1), dim3(256), 0, s, c);
 }

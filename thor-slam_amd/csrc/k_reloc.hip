@@ -1,0 +1,137 @@
+// k_reloc.hip — relocalisation in a loaded map (SlamEngine.relocalize,
+// reference thor_slam/slam/interface.py:250-256).
+//
+// The map is a set of landmarks (world position f64 x3 + rBRIEF-256 descriptor), uploaded once.
+// For one resident frame: every valid left keypoint is matched against ALL map descriptors by
+// brute-force Hamming (best = lexicographic min of (distance, index), second = min over the
+// others; accepted iff best <= max_hamming and 100 * best < ratio_pct * second), the matches
+// become 3D-2D correspondences (world point, level-0 keypoint position) in keypoint order, and
+// A7's P3P-RANSAC + Gauss-Newton solve cam_T_world (RNG seeded by the frame index).
+#include "tslam_common.h"
+
+#define RL_CHUNK 512   // map descriptors staged per LDS pass (16 KB)
+
+// One thread per query keypoint; the block stages the map descriptors chunk by chunk (LDS
+// broadcasts: every thread reads the same descriptor) and keeps best / second per query.
+__global__ __launch_bounds__(256) void k_reloc_match(BatchCtx c, int cam, int slot, const uint32_t* map_desc, int M,
+                                                     int32_t* match) {
+    __shared__ uint4 s_d[RL_CHUNK][2];
+    const int K = c.g.K;
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t ib = (size_t)slot * c.C + cam;
+    bool valid = false;
+    uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (q < K) {
+        const uint32_t meta = c.kps[(ib * K + q) * 2 + 1];
+        const int l = (int)(meta & 0xFF);
+        valid = q - c.g.koff[l] < c.kcount[ib * c.g.n_levels + l];
+        const uint4* src = reinterpret_cast<const uint4*>(c.desc + (ib * K + q) * 8);
+        const uint4 a = src[0], b = src[1];
+        d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+    }
+    uint32_t best = 0xFFFFFFFFu, second = 0xFFFFFFFFu;   // (distance << 20) | index
+    for (int m0 = 0; m0 < M; m0 += RL_CHUNK) {
+        const int nm = min(RL_CHUNK, M - m0);
+        __syncthreads();
+        for (int i = threadIdx.x; i < nm * 2; i += blockDim.x)
+            s_d[i >> 1][i & 1] = reinterpret_cast<const uint4*>(map_desc + (size_t)(m0 + (i >> 1)) * 8)[i & 1];
+        __syncthreads();
+        if (!valid) continue;
+        for (int j = 0; j < nm; ++j) {
+            const uint4 a = s_d[j][0], b = s_d[j][1];
+            const uint32_t dist = __builtin_popcount(d[0] ^ a.x) + __builtin_popcount(d[1] ^ a.y) +
+                                  __builtin_popcount(d[2] ^ a.z) + __builtin_popcount(d[3] ^ a.w) +
+                                  __builtin_popcount(d[4] ^ b.x) + __builtin_popcount(d[5] ^ b.y) +
+                                  __builtin_popcount(d[6] ^ b.z) + __builtin_popcount(d[7] ^ b.w);
+            const uint32_t key = (dist << 20) | (uint32_t)(m0 + j);
+            if (key < best) {
+                second = best;
+                best = key;
+            } else if (key < second) {
+                second = key;
+            }
+        }
+    }
+    if (q >= K) return;
+    int out = -1;
+    if (valid && best != 0xFFFFFFFFu) {
+        const uint32_t bd = best >> 20, sd = second >> 20;   // second: 4095 when absent
+        if ((int)bd <= c.mp.max_hamming && (second == 0xFFFFFFFFu || 100u * bd < (uint32_t)c.mp.ratio_pct * sd))
+            out = (int)(best & 0xFFFFFu);
+    }
+    match[q] = out;
+}
+
+// One block: the matches in keypoint order -> correspondence rows (A7 layout) + stats.
+__global__ __launch_bounds__(256) void k_reloc_corr(BatchCtx c, int cam, int slot, int pair, const double* map_xyz,
+                                                    const int32_t* match, double* corr, int32_t* stats, int64_t frame) {
+    __shared__ int s_tmp[32];
+    const int K = c.g.K;
+    const size_t ib = (size_t)slot * c.C + cam;
+    const PairCalib cal = c.calib[pair];
+    const double fx = cal.fx, fy = cal.fy, cx = cal.cx, cy = cal.cy;
+    int n = 0;
+    for (int base = 0; base < K; base += blockDim.x) {
+        const int q = base + threadIdx.x;
+        const int m = q < K ? match[q] : -1;
+        const int flag = m >= 0;
+        // block exclusive scan of the flags
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        int x = flag;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_tmp[wave] = x;
+        __syncthreads();
+        int off = 0, tot = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+            if (w < wave) off += s_tmp[w];
+            tot += s_tmp[w];
+        }
+        if (flag) {
+            const uint32_t xy = c.kps[(ib * K + q) * 2], meta = c.kps[(ib * K + q) * 2 + 1];
+            const double sc = (double)(1 << (meta & 0xFF));
+            const double u = ((double)(xy & 0xFFFF) + 0.5) * sc - 0.5;
+            const double v = ((double)(xy >> 16) + 0.5) * sc - 0.5;
+            const double bx = (u - cx) / fx;
+            const double by = (v - cy) / fy;
+            const double nn = sqrt((bx * bx + by * by) + 1.0);
+            double* cr = corr + (size_t)(n + off + x - flag) * TS_CORR_DOUBLES;
+            cr[0] = map_xyz[(size_t)m * 3];
+            cr[1] = map_xyz[(size_t)m * 3 + 1];
+            cr[2] = map_xyz[(size_t)m * 3 + 2];
+            cr[3] = cx - u;
+            cr[4] = cy - v;
+            cr[5] = bx / nn;
+            cr[6] = by / nn;
+            cr[7] = 1.0 / nn;
+        }
+        n += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        stats[0] = n < max(6, c.pp.min_inliers) ? 1 : 3;   // 3 = "to be solved" (A7 convention)
+        stats[1] = n;
+        stats[2] = stats[3] = stats[6] = stats[7] = 0;
+        stats[4] = -1;
+        stats[5] = (int)frame;
+    }
+}
+
+void launch_reloc(const BatchCtx& c, int pair, int64_t frame, const double* map_xyz, const uint32_t* map_desc, int M,
+                  int32_t* match, double* corr, int32_t* stats, double* pose, double* ransac, hipStream_t s) {
+    const int slot = ring_slot(c, frame), cam = c.cpp * pair;
+    hipLaunchKernelGGL(k_reloc_match, dim3((c.g.K + 255) / 256), dim3(256), 0, s, c, cam, slot, map_desc, M, match);
+    hipLaunchKernelGGL(k_reloc_corr, dim3(1), dim3(256), 0, s, c, cam, slot, pair, map_xyz, match, corr, stats, frame);
+    BatchCtx r = c;   // A7's RANSAC + refinement on the relocalisation scratch: one frame, one "pair"
+    r.n = 1;
+    r.P = 1;
+    r.g0 = frame;
+    r.calib[0] = c.calib[pair];
+    r.corr = corr;
+    r.stats = stats;
+    r.pose = pose;
+    r.ransac = ransac;
+    launch_pose_solve(r, s);
+}

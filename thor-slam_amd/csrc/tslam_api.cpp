@@ -56,6 +56,15 @@ struct tslam_handle {
     double* d_rig_pose = nullptr;
     int32_t* d_rig_stats = nullptr;
     double* d_rig_state = nullptr;
+    // relocalisation map (tslam_map_upload) and scratch
+    double* d_map_xyz = nullptr;
+    uint32_t* d_map_desc = nullptr;
+    int64_t map_n = 0, map_cap = 0;
+    int32_t* d_rl_match = nullptr;
+    double* d_rl_corr = nullptr;
+    int32_t* d_rl_stats = nullptr;
+    double* d_rl_pose = nullptr;
+    double* d_rl_ransac = nullptr;
     int64_t* d_wedges = nullptr;
     Buffer buf[TSLAM_BUF_COUNT];
     uint32_t* d_cand = nullptr;
@@ -149,7 +158,7 @@ static int alloc_ba(tslam_handle* h) {
     } list[] = {
         {(void**)&b.T, 8 * P * W * 16},      {(void**)&b.Tfe, 8 * P * W * 16},   {(void**)&b.u, 8 * P * WK},
         {(void**)&b.v, 8 * P * WK},          {(void**)&b.d, 8 * P * WK},         {(void**)&b.lm, 4 * P * WK},
-        {(void**)&b.X, 8 * P * WK * 3},      {(void**)&b.remap, 4 * K},          {(void**)&b.cnt, 4 * WK},
+        {(void**)&b.X, 8 * P * WK * 3},      {(void**)&b.kf_desc, 32 * P * WK},   {(void**)&b.gid, 8 * P * WK},      {(void**)&b.remap, 4 * K},          {(void**)&b.cnt, 4 * WK},
         {(void**)&b.li, 4 * WK},             {(void**)&b.lm_id, 4 * WK},         {(void**)&b.keep, WK},
         {(void**)&b.camobs, 4 * W * WK},     {(void**)&b.obs_Vg, 8 * WK * 9},    {(void**)&b.obs_cam, 4 * WK},
         {(void**)&b.obs_k, 4 * WK},          {(void**)&b.obs_id, 4 * WK},        {(void**)&b.cam_off, 4 * (W + 1)},
@@ -684,6 +693,81 @@ int tslam_read_rig_poses(tslam_handle* h, double* T_rel, double* T_abs, double* 
         if (cov) memcpy(cov + 36 * (size_t)i, src + 32, 36 * sizeof(double));
     }
     if (stats) HIPCHK(hipMemcpy(stats, h->d_rig_stats, sizeof(int32_t) * TS_STATS_INTS * (size_t)n, hipMemcpyDeviceToHost));
+    return TSLAM_OK;
+}
+
+int tslam_ba_read_map(tslam_handle* h, int pair, int64_t* gid, uint32_t* desc) {
+    if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
+    if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
+    int rc = tslam_sync(h);
+    if (rc != TSLAM_OK) return rc;
+    const size_t WK = (size_t)h->prm.ba_window * h->g.K;
+    if (gid) HIPCHK(hipMemcpy(gid, h->ba.gid + pair * WK, 8 * WK, hipMemcpyDeviceToHost));
+    if (desc) HIPCHK(hipMemcpy(desc, h->ba.kf_desc + pair * WK * 8, 32 * WK, hipMemcpyDeviceToHost));
+    return TSLAM_OK;
+}
+
+int tslam_map_upload(tslam_handle* h, const double* xyz, const uint32_t* desc, int64_t n) {
+    if (!h || n < 0 || (n && (!xyz || !desc))) return fail(TSLAM_EINVAL, "bad argument");
+    if (n > (1 << 20) - 1) return fail(TSLAM_EINVAL, "at most 2^20 - 1 map points");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    if (n > h->map_cap) {
+        if (h->d_map_xyz) {   // grow: release the old buffers
+            for (void* p : {(void*)h->d_map_xyz, (void*)h->d_map_desc}) {
+                (void)hipFree(p);
+                h->allocs.erase(std::remove(h->allocs.begin(), h->allocs.end(), p), h->allocs.end());
+            }
+        }
+        int rc = dev_alloc(h, (void**)&h->d_map_xyz, sizeof(double) * 3 * n);
+        if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_map_desc, sizeof(uint32_t) * 8 * n);
+        if (rc != TSLAM_OK) return rc;
+        h->map_cap = n;
+    }
+    if (!h->d_rl_match) {
+        const size_t K = h->g.K;
+        int rc = dev_alloc(h, (void**)&h->d_rl_match, sizeof(int32_t) * K);
+        if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_corr, sizeof(double) * TS_CORR_DOUBLES * K);
+        if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_stats, sizeof(int32_t) * TS_STATS_INTS);
+        if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_pose, sizeof(double) * TS_POSE_DOUBLES);
+        if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_ransac, sizeof(uint32_t) * TS_RANSAC_WORDS * TS_MAX_SPLITS);
+        if (rc != TSLAM_OK) return rc;
+    }
+    if (n) {
+        HIPCHK(hipMemcpy(h->d_map_xyz, xyz, sizeof(double) * 3 * n, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(h->d_map_desc, desc, sizeof(uint32_t) * 8 * n, hipMemcpyHostToDevice));
+    }
+    h->map_n = n;
+    return TSLAM_OK;
+}
+
+int tslam_relocalize(tslam_handle* h, int pair, int64_t frame, double* cam_T_world, double* cov, int32_t* stats) {
+    if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
+    if (!h->d_rl_match) return fail(TSLAM_ESTATE, "no map uploaded (tslam_map_upload)");
+    if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_relocalize inside a batch");
+    if (frame < 0 || frame >= h->frames_done || frame < h->frames_done - h->R)
+        return fail(TSLAM_EINVAL, "frame is not resident in the ring");
+    HIPCHK(hipSetDevice(h->device));
+    const BatchCtx c = make_ctx(h);
+    hipStream_t s = h->last_stream;
+    if (h->map_n == 0) {
+        const int32_t st[8] = {1, 0, 0, 0, -1, (int32_t)frame, 0, 0};
+        HIPCHK(hipMemcpy(h->d_rl_stats, st, sizeof(st), hipMemcpyHostToDevice));
+    } else {
+        launch_reloc(c, pair, frame, h->d_map_xyz, h->d_map_desc, (int)h->map_n, h->d_rl_match, h->d_rl_corr,
+                     h->d_rl_stats, h->d_rl_pose, h->d_rl_ransac, s);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    double pose[TS_POSE_DOUBLES];
+    HIPCHK(hipMemcpy(pose, h->d_rl_pose, sizeof(pose), hipMemcpyDeviceToHost));
+    int32_t st[TS_STATS_INTS];
+    HIPCHK(hipMemcpy(st, h->d_rl_stats, sizeof(st), hipMemcpyDeviceToHost));
+    if (h->map_n == 0 || st[0] != 0)
+        for (int i = 0; i < 16; ++i) pose[i] = (i % 5) == 0 ? 1.0 : 0.0;
+    if (cam_T_world) memcpy(cam_T_world, pose, 16 * sizeof(double));
+    if (cov) memcpy(cov, pose + 32, 36 * sizeof(double));
+    if (stats) memcpy(stats, st, sizeof(st));
     return TSLAM_OK;
 }
 

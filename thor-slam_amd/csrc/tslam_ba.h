@@ -29,6 +29,8 @@ struct BaStore {
     double* d;
     int32_t* lm;
     double* X;
+    uint32_t* kf_desc;  // [P][W*K][8] descriptor of every keyframe keypoint (a landmark id's descriptor)
+    int64_t* gid;       // [P][W*K] global landmark id (creation frame * K + keypoint), kept on re-homing
     // scratch (sizes for W*K landmarks/observations)
     int32_t* remap;    // [K]
     int32_t* cnt;      // [WK] observations per landmark id (after the gate)
@@ -77,6 +79,8 @@ struct BaPair {
     double* d;
     int32_t* lm;
     double* X;
+    uint32_t* kf_desc;
+    int64_t* gid;
     int32_t *remap, *cnt, *li, *lm_id, *camobs, *obs_cam, *obs_k, *obs_id, *cam_off, *counts, *tiles;
     uint8_t* keep;
     double *obs_W, *obs_Ug, *obs_Vg, *lm_L, *lm_gp, *part, *C, *cam_U, *dc, *flops;
@@ -93,6 +97,8 @@ __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, in
     q.d = s.d + p * WK;
     q.lm = s.lm + p * WK;
     q.X = s.X + p * WK * 3;
+    q.kf_desc = s.kf_desc + p * WK * 8;
+    q.gid = s.gid + p * WK;
     q.remap = s.remap; q.cnt = s.cnt; q.li = s.li; q.lm_id = s.lm_id; q.keep = s.keep; q.camobs = s.camobs;
     q.obs_cam = s.obs_cam; q.obs_k = s.obs_k; q.obs_id = s.obs_id; q.cam_off = s.cam_off;
     q.counts = s.counts + 4 * p;

@@ -85,6 +85,9 @@ _SIGNATURES = {
     "tslam_pack_features": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
     "tslam_set_rig": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_read_rig_poses": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 4),
+    "tslam_ba_read_map": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_map_upload": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
+    "tslam_relocalize": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64] + [ctypes.c_void_p] * 3),
     "tslam_ba_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6),
     "tslam_ba_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
@@ -293,6 +296,30 @@ class Handle:
         _check(self.lib.tslam_ba_read(self.h, int(pair), *(a.ctypes.data for a in (frames, T, lm, X, uvd, cnt))))
         return {"frames": frames, "T_cw": T, "lm": lm.astype(np.int64), "X": X, "u": uvd[0], "v": uvd[1],
                 "d": uvd[2], "n_obs": int(cnt[0]), "n_lm": int(cnt[1]), "ok": bool(cnt[2])}
+
+    def ba_read_map(self, pair: int = 0) -> dict:
+        """Global landmark ids and keyframe-keypoint descriptors of the window (by landmark id)."""
+        WK = self.cfg.ba_window * self.K
+        gid = np.zeros(WK, dtype=np.int64)
+        desc = np.zeros((WK, 8), dtype=np.uint32)
+        _check(self.lib.tslam_ba_read_map(self.h, int(pair), gid.ctypes.data, desc.ctypes.data))
+        return {"gid": gid, "desc": desc}
+
+    def map_upload(self, xyz: np.ndarray, desc: np.ndarray) -> None:
+        """Upload a relocalisation map: world points [n][3] f64 and rBRIEF descriptors [n][8] u32."""
+        xyz = np.ascontiguousarray(xyz, dtype=np.float64).reshape(-1, 3)
+        desc = np.ascontiguousarray(desc, dtype=np.uint32).reshape(-1, 8)
+        if xyz.shape[0] != desc.shape[0]:
+            raise ValueError("xyz and desc must have the same number of points")
+        _check(self.lib.tslam_map_upload(self.h, xyz.ctypes.data, desc.ctypes.data, int(xyz.shape[0])))
+
+    def relocalize(self, frame: int, pair: int = 0) -> dict:
+        """cam_T_world of a resident frame's left camera in the uploaded map (synchronises)."""
+        T = np.zeros((4, 4))
+        cov = np.zeros((6, 6))
+        st = np.zeros(8, dtype=np.int32)
+        _check(self.lib.tslam_relocalize(self.h, int(pair), int(frame), T.ctypes.data, cov.ctypes.data, st.ctypes.data))
+        return {"T": T, "cov": cov, "stats": st}
 
     def ba_profile(self, max_launches: int = 0) -> dict:
         """Schur-kernel HIP-event time / launches / algorithmic flops since the last call; re-arms
