@@ -114,8 +114,9 @@ def test_engine_contract_defaults():
     assert eng.get_tracking_state() == TrackingState.NOT_INITIALIZED
     with pytest.raises(RuntimeError, match="Not initialized"):
         eng.process_frames(None)
-    with pytest.raises(NotImplementedError):
-        eng.save_map("x")
+    assert eng.save_map("x") is False           # implemented (§8f item 3): nothing mapped yet
+    with pytest.raises(RuntimeError, match="Not initialized"):
+        eng.relocalize()
     with eng as e:
         assert isinstance(e, SlamEngine)
     assert eng.get_tracking_state() == TrackingState.NOT_INITIALIZED

@@ -77,3 +77,50 @@ def test_relocalise_fails_cleanly_on_an_unrelated_map():
     got = h.relocalize(0)
     h.close()
     assert got["stats"][0] != 0 and np.array_equal(got["T"], np.eye(4))
+
+
+def test_engine_save_load_relocalize(tmp_path):
+    """Session 1 (local BA on) maps the room and saves it; session 2 loads the map, sees a later
+    frame, relocalises, and from then on publishes poses in session 1's world frame."""
+    from thor_slam_amd.camera import CameraRig, Extrinsics
+    from thor_slam_amd.params import HipSlamConfig
+    from thor_slam_amd.slam import TrackingState
+    from thor_slam_amd.slam.hip_engine import HipSlamEngine
+
+    from helpers import make_source
+    from test_gpu_ba import BA_ITEMS
+
+    def engine(cfg):
+        src = make_source(0)
+        rig = CameraRig([src], rig_extrinsics={src.name: Extrinsics.from_4x4_matrix(src.rig_T_source)})
+        rig.start()
+        eng = HipSlamEngine(num_cameras=2, config=cfg)
+        eng.initialize(rig.calibration)
+        return eng, rig
+
+    eng, rig = engine(HipSlamConfig(**dict(BA_ITEMS)))
+    assert eng.save_map(str(tmp_path / "empty.npz")) is False
+    poses1 = [eng.process_frames(rig.get_synchronized_frames()) for _ in range(12)]
+    path = str(tmp_path / "room.npz")
+    assert eng.save_map(path)
+    smap = eng.get_map()
+    eng.shutdown()
+    with np.load(path, allow_pickle=False) as z:
+        assert z["points"].shape[0] == len(smap.points) or z["points"].shape[0] >= len(smap.points)
+        assert z["desc"].dtype == np.uint32 and z["desc"].shape[1] == 8
+
+    eng2, rig2 = engine(HipSlamConfig())
+    assert eng2.relocalize() is False                # no map yet
+    assert eng2.load_map(path)
+    for _ in range(8):                               # session 2 starts at frame 8 of the same path
+        rig2.get_synchronized_frames()
+    p = eng2.process_frames(rig2.get_synchronized_frames())
+    assert eng2.relocalize()
+    assert eng2.get_tracking_state() == TrackingState.TRACKING
+    p = eng2._latest_pose
+    assert np.linalg.norm(p.position - poses1[8].position) < 0.02
+    for k in range(9, 12):
+        p = eng2.process_frames(rig2.get_synchronized_frames())
+        assert np.linalg.norm(p.position - poses1[k].position) < 0.02, k
+    assert eng2.load_map(str(tmp_path / "missing.npz")) is False
+    eng2.shutdown()

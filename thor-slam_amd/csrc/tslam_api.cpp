@@ -765,6 +765,8 @@ int tslam_relocalize(tslam_handle* h, int pair, int64_t frame, double* cam_T_wor
     HIPCHK(hipMemcpy(st, h->d_rl_stats, sizeof(st), hipMemcpyDeviceToHost));
     if (h->map_n == 0 || st[0] != 0)
         for (int i = 0; i < 16; ++i) pose[i] = (i % 5) == 0 ? 1.0 : 0.0;
+    pose[12] = pose[13] = pose[14] = 0.0;   // k_refine writes the 3x4 part only
+    pose[15] = 1.0;
     if (cam_T_world) memcpy(cam_T_world, pose, 16 * sizeof(double));
     if (cov) memcpy(cov, pose + 32, 36 * sizeof(double));
     if (stats) memcpy(stats, st, sizeof(st));

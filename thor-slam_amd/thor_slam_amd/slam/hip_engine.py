@@ -89,6 +89,9 @@ class HipSlamEngine(SlamEngine):
         self._kf_final: dict[int, np.ndarray] = {}   # last BA estimate (rect world_T_cam) per keyframe
         self._kf_stamp: dict[int, float] = {}
         self._ba_window: dict | None = None
+        self._map_points: dict[int, tuple] = {}   # global landmark id -> (xyz rect-0 frame, desc, observations)
+        self._map_offset = np.eye(4)              # map world <- session world, set by relocalize()
+        self._map_loaded = False
 
     # ------------------------------------------------------------------------------------------
     def initialize(self, calibration: RigCalibration, config: SlamConfig | None = None) -> None:
@@ -242,6 +245,7 @@ class HipSlamEngine(SlamEngine):
                 self._fe_at[g0 + k] = res["T_abs"][k, 0].copy()
         win = self._handle.ba_read(0)
         self._ba_window = win
+        self._accumulate_map(win)
         live = {}
         for s_, f in enumerate(win["frames"]):
             if f >= 0:
@@ -259,6 +263,15 @@ class HipSlamEngine(SlamEngine):
             out.append(live[kf] @ _invert(self._fe_at[kf]))
         return out
 
+    def _accumulate_map(self, win: dict) -> None:
+        """Merge the window's landmarks (latest BA positions) into the persistent map by global id."""
+        mp = self._handle.ba_read_map(0)
+        occ = win["frames"] >= 0
+        ids, counts = np.unique(win["lm"][occ], return_counts=True)
+        keep = ids >= 0
+        for i, n in zip(ids[keep], counts[keep]):
+            self._map_points[int(mp["gid"][i])] = (win["X"][i].copy(), mp["desc"][i].copy(), int(n))
+
     def _publish(self, res: dict, stamps: list[float]) -> None:
         latest = None
         state = self._state
@@ -268,6 +281,7 @@ class HipSlamEngine(SlamEngine):
             status, body, cov = self._body_pose(res, k)
             if corr is not None and status != POSE_LOST:
                 body = bt @ corr[k] @ res["T_abs"][k, 0] @ _invert(bt)
+            body = self._map_offset @ body
             if status == POSE_LOST:
                 state = TrackingState.LOST
                 latest = None
@@ -322,12 +336,74 @@ class HipSlamEngine(SlamEngine):
             smap.timestamp = pose.timestamp
         return smap
 
+    # -- map persistence / relocalisation (interface.py:228-256) -----------
+    def save_map(self, path: str) -> bool:
+        """Write the landmarks gathered by local BA (world = base_link frame, rBRIEF descriptors,
+        global ids, observation counts) and every keyframe pose to ``path`` (NumPy .npz, no
+        pickles).  False when there is nothing to save (local BA off or no landmark yet)."""
+        if not self._map_points or self._handle is None:
+            return False
+        bt = self._base_T_rect
+        gids = np.array(sorted(self._map_points), dtype=np.int64)
+        xyz = np.stack([self._map_points[g][0] for g in gids])
+        desc = np.stack([self._map_points[g][1] for g in gids]).astype(np.uint32)
+        obs = np.array([self._map_points[g][2] for g in gids], dtype=np.int64)
+        smap = self.get_map()
+        kf = np.stack([p.to_4x4_matrix() for p in smap.keyframe_poses]) if smap.keyframe_poses else np.zeros((0, 4, 4))
+        with open(path, "wb") as fh:
+            np.savez(fh, points=xyz @ bt[:3, :3].T + bt[:3, 3], desc=desc, gid=gids, observations=obs,
+                     keyframe_world_T_base=kf, keyframe_stamps=np.array([p.timestamp for p in smap.keyframe_poses]),
+                     base_T_rect=bt)
+        return True
+
+    def load_map(self, path: str) -> bool:
+        """Load a map written by ``save_map`` and upload it for ``relocalize``."""
+        if self._handle is None:
+            raise RuntimeError("Not initialized")
+        try:
+            with np.load(path, allow_pickle=False) as z:
+                pts, desc = np.asarray(z["points"], dtype=np.float64), np.asarray(z["desc"], dtype=np.uint32)
+        except (OSError, KeyError, ValueError) as exc:
+            logger.warning("load_map(%s) failed: %s", path, exc)
+            return False
+        inv_bt = _invert(self._base_T_rect)
+        self._handle.map_upload(pts @ inv_bt[:3, :3].T + inv_bt[:3, 3], desc)   # into the rect-left frame
+        self._map_loaded = True
+        return True
+
+    def relocalize(self) -> bool:
+        """Pose the latest processed frame in the loaded map (descriptor matching + P3P-RANSAC on
+        the device); on success the published poses continue in the map's world frame."""
+        if self._handle is None:
+            raise RuntimeError("Not initialized")
+        if not self._map_loaded or self._handle.frames_done == 0:
+            return False
+        self.flush()
+        res = self._handle.relocalize(self._handle.frames_done - 1)
+        if int(res["stats"][0]) != POSE_OK:
+            return False
+        bt = self._base_T_rect
+        map_pose = bt @ _invert(res["T"]) @ _invert(bt)                  # map world_T_base of that frame
+        with self._pose_lock:
+            cur = self._latest_pose
+        session = (_invert(self._map_offset) @ cur.to_4x4_matrix()) if cur is not None else np.eye(4)
+        self._map_offset = map_pose @ _invert(session)
+        if cur is not None:
+            body = map_pose
+            with self._pose_lock:
+                self._latest_pose = SlamPose(position=body[:3, 3].copy(), rotation=Rotation.from_matrix(body[:3, :3]).as_quat(),
+                                             timestamp=cur.timestamp, tracking_state=TrackingState.TRACKING,
+                                             confidence=cur.confidence, covariance=cur.covariance)
+                self._state = TrackingState.TRACKING
+        return True
+
     def reset(self) -> None:
         with self._pose_lock:
             self._latest_pose = None
         self._staged = []
         self._keyframe_poses = []
         self._fe_at, self._kf_final, self._kf_stamp, self._ba_window = {}, {}, {}, None
+        self._map_points, self._map_offset = {}, np.eye(4)
         if self._handle is not None:
             self._handle.reset()
         self._state = TrackingState.INITIALIZING
