@@ -184,6 +184,13 @@ int tslam_layout(tslam_handle* h, int64_t* out16, int32_t* level_info18);
 /* Copy the keypoints + descriptors + counts of the last batch into `dst` (device):
  * [n_frames][cams] blocks of (K*8 + K*32 + levels*4) bytes, then a pose trailer per
  * (frame, pair) of T_rel[16] + cov[36] f64 and stats[8] i32.  Returns the total in *bytes. */
+/* IMU fusion (the gyro samples of SynchronizedFrameSet.sensor_data,
+ * types.py:268-269, filled by rig.py:403-407): a rotation prior for each (frame, pair) of the NEXT
+ * batch, prior[n][P][10] = the predicted rectified-left relative rotation R (row-major 3x3, the
+ * rotation part of T_rel) and a weight W (px^2 / rad^2; 0 = none).  A7's Gauss-Newton then
+ * minimises sum |reprojection|^2 + W |log(R_prior R^T)|^2 (small-angle form); RANSAC is unchanged. */
+int tslam_set_motion_prior(tslam_handle* h, const double* prior, int n_frames);
+
 /* Rig pose (replaces the multi-camera fusion cuVSLAM does for the rig of
  * isaac_ros.py:364-411): base_T_rect[P][16] = the rectified-left frame of each pair in the rig's
  * base frame (RigCalibration.get_world_extrinsics, rig.py:35-70, composed with the

@@ -602,8 +602,11 @@ def solve6(hm: np.ndarray, g: np.ndarray):
     return x, lm
 
 
-def refine(rot, trn, corr, intr, thr2, iters):
-    """Gauss-Newton on the current inliers, re-selected every iteration.  Returns R, t, H, stats."""
+def refine(rot, trn, corr, intr, thr2, iters, prior=None):
+    """Gauss-Newton on the current inliers, re-selected every iteration.  Returns R, t, H, stats.
+
+    ``prior`` = (R_prior, W): IMU rotation prior, the term
+    W/2 |w - delta|^2 with delta = vee of the antisymmetric part of R_prior R^T (small angle)."""
     fx, fy, cx, cy = intr
     u = cx - corr["du"]
     v = cy - corr["dv"]
@@ -635,6 +638,14 @@ def refine(rot, trn, corr, intr, thr2, iters):
             for j in range(i, 6):
                 hm[i, j] = np.sum(jx[i] * jx[j]) + np.sum(jy[i] * jy[j])
                 hm[j, i] = hm[i, j]
+        if prior is not None and prior[1] > 0:
+            rp, w = prior
+            mq = np.array([[(rp[i, 0] * rot[j, 0] + rp[i, 1] * rot[j, 1]) + rp[i, 2] * rot[j, 2] for j in range(3)]
+                           for i in range(3)])
+            dl = [0.5 * (mq[2, 1] - mq[1, 2]), 0.5 * (mq[0, 2] - mq[2, 0]), 0.5 * (mq[1, 0] - mq[0, 1])]
+            for i in range(3):
+                hm[3 + i, 3 + i] += w
+                g[3 + i] += w * dl[i]
         sol = solve6(hm, g)
         if sol is None:
             return rot, trn, None, n_in, 0.0
@@ -762,7 +773,7 @@ def bearings(corr, intr):
     return bx / n, by / n, 1.0 / n
 
 
-def estimate_pose(corr: dict, intr, cfg, frame: int) -> dict:
+def estimate_pose(corr: dict, intr, cfg, frame: int, prior=None) -> dict:
     """P3P-RANSAC + Gauss-Newton: T (4x4, cam_{t-1} -> cam_t), covariance, counts, status."""
     n = corr["X"].size
     thr2 = float(cfg.ransac_thr_px) * float(cfg.ransac_thr_px)
@@ -783,7 +794,7 @@ def estimate_pose(corr: dict, intr, cfg, frame: int) -> dict:
         return out
     r0 = rot.reshape(-1, 3, 3)[best]
     t0 = trn.reshape(-1, 3)[best]
-    r1, t1, hm, n_in, sq = refine(r0, t0, corr, intr, thr2, cfg.refine_iters)
+    r1, t1, hm, n_in, sq = refine(r0, t0, corr, intr, thr2, cfg.refine_iters, prior)
     out["n_inliers"] = n_in
     if hm is None or n_in < cfg.min_inliers:
         return out
@@ -814,7 +825,7 @@ class OracleTracker:
         self.frame = 0
         self.world_T_cam = np.eye(4)
 
-    def step(self, left_raw: np.ndarray, right_raw: np.ndarray) -> dict:
+    def step(self, left_raw: np.ndarray, right_raw: np.ndarray, prior=None) -> dict:
         cfg, rp = self.cfg, self.rect
         left = remap(left_raw, rp["map_l"])
         right = remap(right_raw, rp["map_r"])
@@ -823,7 +834,7 @@ class OracleTracker:
         disp = stereo_subpixel(fl, fr, sm[0], fl["levels"], fr["levels"])
         cur = {"left": fl, "right": fr, "stereo": sm[0], "stereo_full": sm, "disp": disp,
                "rect_left": left, "rect_right": right}
-        return self._advance(cur)
+        return self._advance(cur, prior)
 
     def step_rgbd(self, bgr: np.ndarray, depth_mm: np.ndarray) -> dict:
         """One RGB-D frame: colour -> gray -> undistort -> features; depth -> disparity."""
@@ -835,7 +846,7 @@ class OracleTracker:
         cur = {"left": fl, "right": None, "stereo": stereo, "disp": disp, "rect_left": left}
         return self._advance(cur)
 
-    def _advance(self, cur: dict) -> dict:
+    def _advance(self, cur: dict, prior=None) -> dict:
         cfg, rp = self.cfg, self.rect
         intr = (rp["fx"], rp["fy"], rp["cx"], rp["cy"])
         res = {"frame": self.frame, "cur": cur}
@@ -847,7 +858,7 @@ class OracleTracker:
             cur["temporal"] = tm[0]
             cur["temporal_full"] = tm
             corr = build_correspondences(self.prev, cur, tm[0], (rp["fx"], rp["fy"], rp["cx"], rp["cy"], rp["fx"] * rp["baseline"]))
-            est = estimate_pose(corr, intr, cfg, self.frame)
+            est = estimate_pose(corr, intr, cfg, self.frame, prior)
             res.update(est)
             res["corr"] = corr
             if est["status"] == 0:

@@ -248,3 +248,29 @@ def test_rgbd_oracle_follows_ground_truth_and_record_layout():
     np.testing.assert_allclose(d[ok], r.fx / z, rtol=1e-12)
     gt = np.linalg.inv(src.camera_pose(0, 0)) @ src.camera_pose(2, 0)
     assert np.linalg.norm(res["world_T_cam"][:3, 3] - gt[:3, 3]) < 0.1 * np.linalg.norm(gt[:3, 3]) + 2e-3
+
+
+def test_refine_rotation_prior_pulls_towards_prior():
+    """IMU prior (§8f item 2): weight 0 leaves A7's refinement unchanged; a huge weight pins the
+    rotation to the prior while the translation still fits the points."""
+    from scipy.spatial.transform import Rotation
+
+    rng = np.random.default_rng(5)
+    n = 80
+    X = np.stack([rng.uniform(-1, 1, n), rng.uniform(-1, 1, n), rng.uniform(3, 6, n)], 1)
+    R = Rotation.from_rotvec([0.01, -0.02, 0.005]).as_matrix()
+    t = np.array([0.02, 0.0, -0.01])
+    Xc = X @ R.T + t
+    fx = fy = 400.0
+    cx, cy = 320.0, 200.0
+    u = fx * Xc[:, 0] / Xc[:, 2] + cx
+    v = fy * Xc[:, 1] / Xc[:, 2] + cy
+    corr = {"X": X[:, 0], "Y": X[:, 1], "Z": X[:, 2], "du": cx - u, "dv": cy - v, "u": u, "v": v}
+    intr = (fx, fy, cx, cy)
+    r0 = Rotation.from_rotvec([0.012, -0.018, 0.004]).as_matrix()
+    a = O.refine(r0, t + 0.001, corr, intr, 4.0, 8)
+    b = O.refine(r0, t + 0.001, corr, intr, 4.0, 8, prior=(np.eye(3), 0.0))
+    np.testing.assert_array_equal(a[0], b[0])
+    rp = Rotation.from_rotvec([0.011, -0.02, 0.005]).as_matrix()
+    c = O.refine(r0, t + 0.001, corr, intr, 1e6, 8, prior=(rp, 1e12))
+    assert np.abs(Rotation.from_matrix(c[0] @ rp.T).as_rotvec()).max() < 1e-6

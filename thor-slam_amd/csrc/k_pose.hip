@@ -511,6 +511,21 @@ __global__ __launch_bounds__(POSE_THREADS) void k_refine(BatchCtx c, int S) {
                         ++k;
                     }
                 for (int r0 = 0; r0 < 6; ++r0) gv[r0] = -tot[21 + r0];
+                if (c.prior) {   // IMU rotation prior (weight W, px^2 / rad^2): W/2 |w - delta|^2
+                    const double* pr = c.prior + (size_t)fp * TS_PRIOR_DOUBLES;
+                    const double W = pr[9];
+                    if (W > 0.0) {
+                        double Mq[9];
+                        for (int i = 0; i < 3; ++i)
+                            for (int j = 0; j < 3; ++j)
+                                Mq[3 * i + j] = (pr[3 * i] * s_R[3 * j] + pr[3 * i + 1] * s_R[3 * j + 1]) + pr[3 * i + 2] * s_R[3 * j + 2];
+                        const double dl[3] = {0.5 * (Mq[7] - Mq[5]), 0.5 * (Mq[2] - Mq[6]), 0.5 * (Mq[3] - Mq[1])};
+                        for (int i = 0; i < 3; ++i) {
+                            Hm[(3 + i) * 6 + 3 + i] += W;
+                            gv[3 + i] += W * dl[i];
+                        }
+                    }
+                }
                 for (int q = 0; q < 36; ++q) L[q] = 0.0;
                 if (!solve6(Hm, gv, x, L)) {
                     s_flag = 1;

@@ -56,6 +56,9 @@ struct tslam_handle {
     double* d_rig_pose = nullptr;
     int32_t* d_rig_stats = nullptr;
     double* d_rig_state = nullptr;
+    // IMU rotation prior for the next batch (tslam_set_motion_prior)
+    double* d_prior = nullptr;
+    bool prior_armed = false;
     // relocalisation map (tslam_map_upload) and scratch
     double* d_map_xyz = nullptr;
     uint32_t* d_map_desc = nullptr;
@@ -267,6 +270,7 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.pose = (double*)h->buf[TSLAM_BUF_POSE].ptr;
     c.stats = (int32_t*)h->buf[TSLAM_BUF_STATS].ptr;
     c.state = h->d_state;
+    c.prior = h->prior_armed ? h->d_prior : nullptr;
     c.rig_E = h->d_rig_E;
     c.rig_Einv = h->d_rig_E ? h->d_rig_E + 16 * h->P : nullptr;
     c.rig_pose = h->d_rig_pose;
@@ -481,6 +485,7 @@ int tslam_end_batch(tslam_handle* h) {
     if (!h->in_batch) return fail(TSLAM_ESTATE, "no batch in progress");
     h->frames_done += h->cur_n;
     h->in_batch = false;
+    h->prior_armed = false;   // a prior applies to one batch
     return TSLAM_OK;
 }
 
@@ -644,6 +649,22 @@ int tslam_pack_features(tslam_handle* h, void* dst, int64_t* bytes, void* stream
     const BatchCtx c = make_ctx(h);
     launch_pack(c, (uint8_t*)dst, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
+    return TSLAM_OK;
+}
+
+int tslam_set_motion_prior(tslam_handle* h, const double* prior, int n_frames) {
+    if (!h || !prior) return fail(TSLAM_EINVAL, "bad argument");
+    if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_set_motion_prior inside a batch");
+    if (n_frames < 1 || n_frames > h->B) return fail(TSLAM_EINVAL, "n_frames must be in [1, max_batch]");
+    HIPCHK(hipSetDevice(h->device));
+    if (!h->d_prior) {
+        const int rc = dev_alloc(h, (void**)&h->d_prior, sizeof(double) * TS_PRIOR_DOUBLES * h->P * h->B);
+        if (rc != TSLAM_OK) return rc;
+    }
+    std::vector<double> buf((size_t)TS_PRIOR_DOUBLES * h->P * h->B, 0.0);   // frames past n: weight 0
+    memcpy(buf.data(), prior, sizeof(double) * TS_PRIOR_DOUBLES * h->P * n_frames);
+    HIPCHK(hipMemcpy(h->d_prior, buf.data(), sizeof(double) * buf.size(), hipMemcpyHostToDevice));
+    h->prior_armed = true;
     return TSLAM_OK;
 }
 

@@ -84,6 +84,7 @@ _SIGNATURES = {
     "tslam_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_pack_features": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
     "tslam_set_rig": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_set_motion_prior": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "tslam_read_rig_poses": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 4),
     "tslam_ba_read_map": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_map_upload": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
@@ -236,6 +237,15 @@ class Handle:
             "T_rel": t_rel.reshape(shape + (4, 4)), "T_abs": t_abs.reshape(shape + (4, 4)),
             "cov": cov.reshape(shape + (6, 6)), "stats": stats.reshape(shape + (8,)),
         }
+
+    def set_motion_prior(self, rot: np.ndarray, weight: np.ndarray) -> None:
+        """Rotation prior for the next batch: rot [n][P][3][3] (predicted T_rel rotations), weight [n][P]."""
+        rot = np.asarray(rot, dtype=np.float64)
+        n = rot.shape[0]
+        buf = np.zeros((n, self.n_pairs, 10))
+        buf[..., :9] = rot.reshape(n, self.n_pairs, 9)
+        buf[..., 9] = np.asarray(weight, dtype=np.float64).reshape(n, self.n_pairs)
+        _check(self.lib.tslam_set_motion_prior(self.h, np.ascontiguousarray(buf).ctypes.data, int(n)))
 
     def set_rig(self, base_T_rect: list) -> None:
         """Enable the rig pose: base_T_rect-left (4x4) of every pair, in pair order."""

@@ -45,6 +45,9 @@ class HipSlamConfig(SlamConfig):
     ba_iters: int = 5               # Gauss-Newton steps per window solve
     ba_lambda: float = 1.0          # Levenberg damping (px^2 units)
     ba_outlier_px: float = 3.0      # observations farther than this at the start are dropped
+    # IMU fusion: gyro-predicted rotation prior in the pose Gauss-Newton
+    imu_fusion: bool = False
+    imu_rot_sigma: float = 2e-3     # rad, std of the per-frame gyro rotation prediction (1 px = 1 unit)
     # input kind: RGB-D (BASELINE configs[4]) = per source a colour camera (cam_idx 0, BGR) and a
     # depth image aligned to it (cam_idx 1, u16 mm); depth replaces stereo matching
     rgbd: bool = False

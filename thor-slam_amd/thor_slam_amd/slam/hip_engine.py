@@ -81,6 +81,9 @@ class HipSlamEngine(SlamEngine):
         self._pose_lock = threading.Lock()
         self._frame_count = 0
         self._staged: list[tuple[np.ndarray, float]] = []
+        self._staged_gyro: list[np.ndarray | None] = []
+        self._prev_stamp: float | None = None      # timestamp of the last submitted frame (IMU dt)
+        self._base_R_imu = np.eye(3)
         self._torch = None
         self._dev_images = None
         self._host_images = None
@@ -129,6 +132,8 @@ class HipSlamEngine(SlamEngine):
             self._base_T_rects = [self._cameras[l].extrinsics.to_4x4_matrix() @ r.left_optical_T_rect()
                                   for (l, _), r in zip(self._pairs, self._rects)]
             self._base_T_rect = self._base_T_rects[0]
+            imu = getattr(calibration, "imu_extrinsics", None)   # world(base)_T_imu, RDF-converted by the caller
+            self._base_R_imu = imu.to_4x4_matrix()[:3, :3] if imu is not None else np.eye(3)
             if len(self._pairs) > 1:   # the rig's body motion is solved on the device from all pairs
                 self._handle.set_rig(self._base_T_rects)
         except RuntimeError:
@@ -176,6 +181,7 @@ class HipSlamEngine(SlamEngine):
             with self._pose_lock:
                 return self._latest_pose
         self._staged.append((imgs, float(frame_set.timestamp)))
+        self._staged_gyro.append(self._gyro_of(frame_set))
         if len(self._staged) >= self._config.batch_size:
             self.flush()
         with self._pose_lock:
@@ -192,11 +198,42 @@ class HipSlamEngine(SlamEngine):
             host[k] = imgs
         stream = torch.cuda.current_stream(self._device)
         self._dev_images[:n].copy_(self._host_images[:n], non_blocking=True)
+        stamps = [ts for _, ts in self._staged]
+        if self._config.imu_fusion:
+            self._set_imu_prior(stamps, self._staged_gyro)
         self._handle.submit(self._dev_images.data_ptr(), n, stream.cuda_stream)
         res = self._read(n)
-        stamps = [ts for _, ts in self._staged]
-        self._staged = []
+        self._staged, self._staged_gyro = [], []
+        self._prev_stamp = stamps[-1]
         self._publish(res, stamps)
+
+    # -- IMU fusion -------------------------------------------------------
+    @staticmethod
+    def _gyro_of(frame_set: SynchronizedFrameSet) -> np.ndarray | None:
+        """Gyroscope sample [rad/s] (IMU axes) of a synchronised set, from ``sensor_data``
+        (IMUData or a dict with "gyroscope"; rig.py:403-407)."""
+        d = getattr(frame_set, "sensor_data", None)
+        if d is None:
+            return None
+        g = d.get("gyroscope") if isinstance(d, dict) else getattr(d, "gyroscope", None)
+        return None if g is None else np.asarray(g, dtype=np.float64).reshape(3)
+
+    def _set_imu_prior(self, stamps: list[float], gyros: list) -> None:
+        """Per staged frame and pair: the rectified-left rotation predicted by the gyro over the
+        frame interval, R = exp(-[w_rect dt]x), with weight (1 px / imu_rot_sigma)^2."""
+        P = len(self._pairs)
+        rot = np.tile(np.eye(3), (len(stamps), P, 1, 1))
+        wgt = np.zeros((len(stamps), P))
+        prev = self._prev_stamp
+        w0 = 1.0 / (self._config.imu_rot_sigma ** 2)
+        for k, (ts, gy) in enumerate(zip(stamps, gyros)):
+            if gy is not None and prev is not None and ts > prev:
+                w_base = self._base_R_imu @ gy
+                for p, bt in enumerate(self._base_T_rects):
+                    rot[k, p] = Rotation.from_rotvec(-(bt[:3, :3].T @ w_base) * (ts - prev)).as_matrix()
+                    wgt[k, p] = w0
+            prev = ts
+        self._handle.set_motion_prior(rot, wgt)
 
     def process_batch(self, images, timestamps: list[float] | None = None, stream=None) -> dict:
         """Throughput entry: ``images`` is a device uint8 tensor already in HBM: [n, 2P, H, W] gray
@@ -400,7 +437,7 @@ class HipSlamEngine(SlamEngine):
     def reset(self) -> None:
         with self._pose_lock:
             self._latest_pose = None
-        self._staged = []
+        self._staged, self._staged_gyro, self._prev_stamp = [], [], None
         self._keyframe_poses = []
         self._fe_at, self._kf_final, self._kf_stamp, self._ba_window = {}, {}, {}, None
         self._map_points, self._map_offset = {}, np.eye(4)

@@ -25,10 +25,14 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from .calib import RDF_TO_FLU_MATRIX, undistort_normalized
-from .camera.types import CameraFrame, CameraSource, Extrinsics, Intrinsics
+from scipy.spatial.transform import Rotation
+
+from .camera.types import CameraFrame, CameraSource, Extrinsics, IMUData, Intrinsics
 from .rgbd import pack_rgbd
 
 TEXTURE_SIZE = 1024
+# OAK IMU axes (DRB: x down, y right, z back) -> camera RDF, as in run_slam.py:262-270
+DRB_TO_RDF = np.array([[0, 1, 0, 0], [1, 0, 0, 0], [0, 0, -1, 0], [0, 0, 0, 1]], dtype=np.float64)
 TEXEL_M = 0.01
 
 
@@ -177,6 +181,8 @@ class SyntheticStereoSource(CameraSource):
         t0: float = 1000.0,
         jitter_s: float = 0.0,
         n_frames: int = 100,
+        imu: bool = False,
+        gyro_noise: float = 0.0,
     ) -> None:
         self._name = name
         self.scene = scene or RoomScene(seed=seed)
@@ -194,6 +200,8 @@ class SyntheticStereoSource(CameraSource):
             m = np.eye(4)
             m[0, 3] = sx * baseline
             self._extr.append(Extrinsics.from_4x4_matrix(m))
+        self.imu = imu
+        self.gyro_noise = gyro_noise
         self._index = 0
         self._running = False
         self._lock = threading.Lock()
@@ -216,14 +224,36 @@ class SyntheticStereoSource(CameraSource):
         return list(self._extr)
 
     def get_sensor_extrinsics(self) -> Extrinsics | None:
-        return None
+        """IMU -> source: the IMU sits at the source origin, axes in the OAK's DRB convention
+        (the chain of run_slam.py:252-283 turns it into RDF with DRB_TO_RDF)."""
+        return Extrinsics.from_4x4_matrix(np.eye(4)) if self.imu else None
+
+    def imu_sample(self, i: int) -> IMUData:
+        """Gyro = the source's rotation from frame i-1 to i over the frame interval (DRB axes) +
+        N(0, gyro_noise^2); accelerometer = gravity's reaction in the IMU frame."""
+        dt = 1.0 / self.fps
+        r0 = self.camera_pose(max(i - 1, 0), 0)[:3, :3]
+        r1 = self.camera_pose(i, 0)[:3, :3]
+        w_rdf = Rotation.from_matrix(r0.T @ r1).as_rotvec() / dt
+        d = DRB_TO_RDF[:3, :3]
+        w = d.T @ w_rdf
+        if self.gyro_noise:
+            w = w + np.random.default_rng((self.seed, i, 99)).normal(0.0, self.gyro_noise, 3)
+        acc = d.T @ (r1.T @ np.array([0.0, 0.0, 9.81]))
+        return IMUData(accelerometer=acc, gyroscope=w, timestamp=self.timestamp(i), sequence_num=i)
 
     def get_timestamped_sensor_data(self) -> tuple[dict | None, float | None]:
-        return None, None
+        if not self.imu:
+            return None, None
+        s = self.imu_sample(self._index)
+        return s, s.timestamp
+
+    def try_get_timestamped_sensor_data(self) -> tuple[dict | None, float | None]:
+        return self.get_timestamped_sensor_data()
 
     @property
     def has_sensor_data(self) -> bool:
-        return False
+        return self.imu
 
     def get_latest_frames(self) -> list[CameraFrame]:
         if not self._running:
