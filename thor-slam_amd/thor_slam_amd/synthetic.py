@@ -27,7 +27,7 @@ import numpy as np
 from .calib import RDF_TO_FLU_MATRIX, undistort_normalized
 from scipy.spatial.transform import Rotation
 
-from .camera.types import CameraFrame, CameraSource, Extrinsics, IMUData, Intrinsics
+from .camera.types import CameraFrame, CameraSource, Extrinsics, Intrinsics
 from .rgbd import pack_rgbd
 
 TEXTURE_SIZE = 1024
@@ -228,9 +228,11 @@ class SyntheticStereoSource(CameraSource):
         (the chain of run_slam.py:252-283 turns it into RDF with DRB_TO_RDF)."""
         return Extrinsics.from_4x4_matrix(np.eye(4)) if self.imu else None
 
-    def imu_sample(self, i: int) -> IMUData:
+    def imu_sample(self, i: int) -> dict:
         """Gyro = the source's rotation from frame i-1 to i over the frame interval (DRB axes) +
-        N(0, gyro_noise^2); accelerometer = gravity's reaction in the IMU frame."""
+        N(0, gyro_noise^2); accelerometer = gravity's reaction in the IMU frame.  A dict with the
+        IMUData fields, the form the reference's rig carries (luxonis.py:1155-1158 casts to dict and
+        indexes ["timestamp"]; its IMUData class has no constructor)."""
         dt = 1.0 / self.fps
         r0 = self.camera_pose(max(i - 1, 0), 0)[:3, :3]
         r1 = self.camera_pose(i, 0)[:3, :3]
@@ -240,13 +242,13 @@ class SyntheticStereoSource(CameraSource):
         if self.gyro_noise:
             w = w + np.random.default_rng((self.seed, i, 99)).normal(0.0, self.gyro_noise, 3)
         acc = d.T @ (r1.T @ np.array([0.0, 0.0, 9.81]))
-        return IMUData(accelerometer=acc, gyroscope=w, timestamp=self.timestamp(i), sequence_num=i)
+        return {"accelerometer": acc, "gyroscope": w, "timestamp": self.timestamp(i), "sequence_num": i}
 
     def get_timestamped_sensor_data(self) -> tuple[dict | None, float | None]:
         if not self.imu:
             return None, None
         s = self.imu_sample(self._index)
-        return s, s.timestamp
+        return s, s["timestamp"]
 
     def try_get_timestamped_sensor_data(self) -> tuple[dict | None, float | None]:
         return self.get_timestamped_sensor_data()
