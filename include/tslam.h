@@ -198,6 +198,16 @@ int tslam_set_motion_prior(tslam_handle* h, const double* prior, int n_frames);
  * pairs' correspondences (generalised PnP: per-pair RANSAC winners as candidates scored on every
  * pair, then a joint Gauss-Newton) and chains it. */
 int tslam_set_rig(tslam_handle* h, const double* base_T_rect);
+/* Rig fusion across ranks (one stereo source per GPU, the rig-level solve after the
+ * all-gather).  base_T_rect[world * n_pairs][16], rank-major.  tslam_rig_fuse reads the gathered
+ * tslam_pack_features blocks of one batch (frames first_frame .. +n_frames-1; [world][block bytes],
+ * device memory) and, per frame,
+ * combines every tracked pair's body motion by information weighting (each pair's 6x6 covariance
+ * rotated into the body frame), then chains it; read with tslam_read_rig_poses.  Enqueued on
+ * `stream` (after the collective), no synchronisation; in this mode tslam_read_rig_poses returns
+ * max_batch records (the first n_frames are the last fused batch). */
+int tslam_set_rig_ranks(tslam_handle* h, int world, const double* base_T_rect);
+int tslam_rig_fuse(tslam_handle* h, const void* gathered, int world, int64_t first_frame, int n_frames, void* stream);
 /* Body-frame results of the last batch (synchronises): per frame T_rel (body_{t-1} -> body_t
  * point map), T_abs (world_T_base, world = base at frame 0), 6x6 covariance, stats
  * {status, n_corr (all pairs), n_inliers, best candidate count, best candidate, frame, 0, 0}. */

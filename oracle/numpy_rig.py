@@ -141,3 +141,44 @@ class RigChain:
         if res["status"] == 0:
             self.world_T_base = self.world_T_base @ inv_rigid(res["T"])
         return self.world_T_base.copy()
+
+
+def fuse_information(items: list[tuple], E: list[np.ndarray]) -> dict:
+    """Rig fusion across ranks (the multi-GPU layout): ``items[q]`` =
+    (status, T_rel 4x4, cov 6x6) of pair q.  Each tracked pair's body motion M_q = (E_q T_q) E_q^-1
+    with information inv(R6 cov R6^T), R6 = blockdiag(R_e, R_e); combined in the tangent space of
+    the first tracked pair: xi = (sum L)^-1 sum L xi_q, xi_q = (t, rotvec) of M_ref^-1 M_q,
+    M = M_ref [exp(xi_w) | xi_rho]; covariance (sum L)^-1."""
+    from scipy.spatial.transform import Rotation
+
+    sum_l = np.zeros((6, 6))
+    sum_lx = np.zeros(6)
+    mref = None
+    used = 0
+    init = any(st == 2 for st, _, _ in items)
+    for (st, T, cov), e in zip(items, E):
+        if st != 0:
+            continue
+        M = mul4(mul4(e, T), inv_rigid(e))
+        r6 = np.zeros((6, 6))
+        r6[:3, :3] = r6[3:, 3:] = e[:3, :3]
+        cb = r6 @ cov @ r6.T
+        try:
+            np.linalg.cholesky(cb)
+        except np.linalg.LinAlgError:
+            continue
+        lam = np.linalg.inv(cb)
+        if mref is None:
+            mref = M
+        d = mul4(inv_rigid(mref), M)
+        xi = np.concatenate([d[:3, 3], Rotation.from_matrix(d[:3, :3]).as_rotvec()])
+        sum_l += lam
+        sum_lx += lam @ xi
+        used += 1
+    if not used:
+        return {"status": 2 if init else 1, "T": np.eye(4), "cov": np.zeros((6, 6)), "used": 0}
+    xi = np.linalg.solve(sum_l, sum_lx)
+    x = np.eye(4)
+    x[:3, :3] = Rotation.from_rotvec(xi[3:]).as_matrix()
+    x[:3, 3] = xi[:3]
+    return {"status": 0, "T": mul4(mref, x), "cov": np.linalg.inv(sum_l), "used": used}

@@ -111,3 +111,46 @@ def test_rig_pose_survives_a_blind_pair():
     assert (r["stats"][1:, 0] == 0).all()               # the rig is not
     gt = np.linalg.inv(sc["traj"][0]) @ sc["traj"][5]
     assert np.linalg.norm(r["T_abs"][5][:3, 3] - gt[:3, 3]) < 0.1 * np.linalg.norm(gt[:3, 3]) + 2e-3
+
+
+def test_rig_fusion_across_ranks_matches_numpy():
+    """Multi-GPU layout rehearsed on one GPU: one handle per pair ("rank"), their packed blocks
+    concatenated as the all-gather would, fused on the device (tslam_rig_fuse) vs numpy."""
+    import torch
+
+    from oracle.numpy_rig import RigChain, fuse_information
+    from thor_slam_amd._lib import Handle
+
+    sc = rig_scenario()
+    n = 6
+    stream = torch.cuda.current_stream().cuda_stream
+    handles, blocks, per = [], [], []
+    for q in range(2):
+        h = Handle([sc["rects"][q]], sc["cfg"], max_batch=n)
+        dev = torch.from_numpy(np.ascontiguousarray(sc["frames"][:, 2 * q:2 * q + 2])).cuda()
+        h.submit(dev.data_ptr(), n, stream)
+        per.append(h.read_poses(n))
+        blk = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
+        nb = h.pack_features(blk.data_ptr(), stream)
+        blocks.append(blk[:nb])
+        handles.append(h)
+    gathered = torch.cat(blocks).contiguous()
+    h0 = handles[0]
+    h0.set_rig_ranks(sc["E"])
+    h0.rig_fuse(gathered.data_ptr(), 2, 0, n, stream)
+    got = h0.read_rig_poses(n)
+    for h in handles:
+        h.close()
+    chain = RigChain()
+    for f in range(n):
+        items = [(int(per[q]["stats"][f, 0, 0]), per[q]["T_rel"][f, 0], per[q]["cov"][f, 0]) for q in range(2)]
+        w = fuse_information(items, sc["E"])
+        w_abs = chain.step(w)
+        assert got["stats"][f, 0] == w["status"], f
+        if w["status"] == 0:
+            assert got["stats"][f, 1] == w["used"] == 2
+            assert rel_frobenius(got["T_rel"][f], w["T"]) < 1e-9
+            assert rel_frobenius(got["cov"][f], w["cov"]) < 1e-6
+        assert rel_frobenius(got["T_abs"][f], w_abs) < 1e-9
+    gt = np.linalg.inv(sc["traj"][0]) @ sc["traj"][n - 1]
+    assert np.linalg.norm(got["T_abs"][n - 1][:3, 3] - gt[:3, 3]) < 0.1 * np.linalg.norm(gt[:3, 3]) + 2e-3

@@ -893,6 +893,10 @@ __global__ __launch_bounds__(POSE_THREADS) void k_rig_pose(BatchCtx c) {
 
 void launch_rig(const BatchCtx& c, hipStream_t s) {
     hipLaunchKernelGGL(k_rig_pose, dim3(c.n), dim3(POSE_THREADS), 0, s, c);
+    launch_rig_chain(c, s);
+}
+
+void launch_rig_chain(const BatchCtx& c, hipStream_t s) {
     BatchCtx r = c;   // chain the body motions with the pair chain kernel: one "pair", the rig
     r.pose = c.rig_pose;
     r.stats = c.rig_stats;

@@ -52,6 +52,7 @@ struct tslam_handle {
     uint8_t* d_gray = nullptr;   // RGB-D: converted colour images [B][P][H][W]
     // rig pose (tslam_set_rig): E = base_T_rect-left per pair, its inverse, body-frame results
     bool rig = false;
+    int rig_world = 0, rig_q = 0, rig_cap = 0;   // ranks mode: world size; E entries; allocated
     double* d_rig_E = nullptr;
     double* d_rig_pose = nullptr;
     int32_t* d_rig_stats = nullptr;
@@ -272,7 +273,7 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.state = h->d_state;
     c.prior = h->prior_armed ? h->d_prior : nullptr;
     c.rig_E = h->d_rig_E;
-    c.rig_Einv = h->d_rig_E ? h->d_rig_E + 16 * h->P : nullptr;
+    c.rig_Einv = h->d_rig_E ? h->d_rig_E + 16 * h->rig_q : nullptr;
     c.rig_pose = h->d_rig_pose;
     c.rig_stats = h->d_rig_stats;
     c.rig_state = h->d_rig_state;
@@ -668,16 +669,13 @@ int tslam_set_motion_prior(tslam_handle* h, const double* prior, int n_frames) {
     return TSLAM_OK;
 }
 
-int tslam_set_rig(tslam_handle* h, const double* base_T_rect) {
-    if (!h || !base_T_rect) return fail(TSLAM_EINVAL, "bad argument");
-    if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_set_rig inside a batch");
+static int set_rig_E(tslam_handle* h, int q_total, const double* base_T_rect) {
     HIPCHK(hipSetDevice(h->device));
-    const int P = h->P;
-    std::vector<double> e(32 * (size_t)P, 0.0);
-    for (int p = 0; p < P; ++p) {
-        const double* E = base_T_rect + 16 * p;
-        double* inv = e.data() + 16 * (P + p);
-        for (int i = 0; i < 16; ++i) e[16 * p + i] = E[i];
+    std::vector<double> e(32 * (size_t)q_total, 0.0);
+    for (int q = 0; q < q_total; ++q) {
+        const double* E = base_T_rect + 16 * q;
+        double* inv = e.data() + 16 * (q_total + q);
+        for (int i = 0; i < 16; ++i) e[16 * q + i] = E[i];
         if (E[12] != 0.0 || E[13] != 0.0 || E[14] != 0.0 || E[15] != 1.0) return fail(TSLAM_EINVAL, "base_T_rect must be rigid 4x4");
         for (int i = 0; i < 3; ++i) {   // [R^T | -R^T t]
             for (int j = 0; j < 3; ++j) inv[4 * i + j] = E[4 * j + i];
@@ -685,9 +683,18 @@ int tslam_set_rig(tslam_handle* h, const double* base_T_rect) {
         }
         inv[15] = 1.0;
     }
-    if (!h->d_rig_E) {
-        int rc = dev_alloc(h, (void**)&h->d_rig_E, sizeof(double) * 32 * P);
-        if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rig_pose, sizeof(double) * TS_POSE_DOUBLES * h->B);
+    if (q_total > h->rig_cap) {
+        if (h->d_rig_E) {
+            (void)hipFree(h->d_rig_E);
+            h->allocs.erase(std::remove(h->allocs.begin(), h->allocs.end(), (void*)h->d_rig_E), h->allocs.end());
+            h->d_rig_E = nullptr;
+        }
+        const int rc = dev_alloc(h, (void**)&h->d_rig_E, sizeof(double) * 32 * q_total);
+        if (rc != TSLAM_OK) return rc;
+        h->rig_cap = q_total;
+    }
+    if (!h->d_rig_pose) {
+        int rc = dev_alloc(h, (void**)&h->d_rig_pose, sizeof(double) * TS_POSE_DOUBLES * h->B);
         if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rig_stats, sizeof(int32_t) * TS_STATS_INTS * h->B);
         if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rig_state, sizeof(double) * 16);
         if (rc != TSLAM_OK) return rc;
@@ -695,16 +702,52 @@ int tslam_set_rig(tslam_handle* h, const double* base_T_rect) {
         HIPCHK(hipMemcpy(h->d_rig_state, eye, sizeof(eye), hipMemcpyHostToDevice));
     }
     HIPCHK(hipMemcpy(h->d_rig_E, e.data(), sizeof(double) * e.size(), hipMemcpyHostToDevice));
+    h->rig_q = q_total;
+    return TSLAM_OK;
+}
+
+int tslam_set_rig(tslam_handle* h, const double* base_T_rect) {
+    if (!h || !base_T_rect) return fail(TSLAM_EINVAL, "bad argument");
+    if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_set_rig inside a batch");
+    const int rc = set_rig_E(h, h->P, base_T_rect);
+    if (rc != TSLAM_OK) return rc;
     h->rig = true;
+    h->rig_world = 0;
+    return TSLAM_OK;
+}
+
+int tslam_set_rig_ranks(tslam_handle* h, int world, const double* base_T_rect) {
+    if (!h || !base_T_rect || world < 1 || world > 64) return fail(TSLAM_EINVAL, "bad argument");
+    if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_set_rig_ranks inside a batch");
+    const int rc = set_rig_E(h, world * h->P, base_T_rect);
+    if (rc != TSLAM_OK) return rc;
+    h->rig = false;
+    h->rig_world = world;
+    return TSLAM_OK;
+}
+
+int tslam_rig_fuse(tslam_handle* h, const void* gathered, int world, int64_t first_frame, int n_frames, void* stream) {
+    if (!h || !gathered) return fail(TSLAM_EINVAL, "bad argument");
+    if (h->rig_world != world) return fail(TSLAM_ESTATE, "tslam_set_rig_ranks with this world size first");
+    if (n_frames < 1 || n_frames > h->B) return fail(TSLAM_EINVAL, "n_frames must be in [1, max_batch]");
+    HIPCHK(hipSetDevice(h->device));
+    BatchCtx c = make_ctx(h);
+    c.n = n_frames;
+    c.g0 = first_frame;
+    const int64_t K = h->g.K, L = h->g.n_levels;
+    const int64_t rank_bytes = (int64_t)n_frames * h->C * (K * 40 + L * 4) +
+                               (int64_t)n_frames * h->P * (52 * 8 + TS_STATS_INTS * 4);
+    launch_rig_fuse(c, (const uint8_t*)gathered, rank_bytes, world, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
     return TSLAM_OK;
 }
 
 int tslam_read_rig_poses(tslam_handle* h, double* T_rel, double* T_abs, double* cov, int32_t* stats) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
-    if (!h->rig) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig)");
+    if (!h->d_rig_pose) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig / tslam_set_rig_ranks)");
     int rc = tslam_sync(h);
     if (rc != TSLAM_OK) return rc;
-    const int n = h->cur_n;
+    const int n = h->rig_world ? h->B : h->cur_n;   // ranks mode: the last fused batch (caller slices)
     std::vector<double> pose((size_t)n * TS_POSE_DOUBLES);
     HIPCHK(hipMemcpy(pose.data(), h->d_rig_pose, sizeof(double) * pose.size(), hipMemcpyDeviceToHost));
     for (int i = 0; i < n; ++i) {

@@ -139,6 +139,8 @@ void launch_pose(const BatchCtx& c, hipStream_t s);
 void launch_chain(const BatchCtx& c, hipStream_t s);
 void launch_pack(const BatchCtx& c, uint8_t* dst, hipStream_t s);
 void launch_rig(const BatchCtx& c, hipStream_t s);
+void launch_rig_chain(const BatchCtx& c, hipStream_t s);
+void launch_rig_fuse(const BatchCtx& c, const uint8_t* gathered, int64_t rank_bytes, int world, hipStream_t s);
 void launch_pose_solve(const BatchCtx& c, hipStream_t s);
 void launch_reloc(const BatchCtx& c, int pair, int64_t frame, const double* map_xyz, const uint32_t* map_desc, int M,
                   int32_t* match, double* corr, int32_t* stats, double* pose, double* ransac, hipStream_t s);

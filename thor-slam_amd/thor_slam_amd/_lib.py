@@ -86,6 +86,9 @@ _SIGNATURES = {
     "tslam_set_rig": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_set_motion_prior": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "tslam_read_rig_poses": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 4),
+    "tslam_set_rig_ranks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "tslam_rig_fuse": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+                                      ctypes.c_void_p]),
     "tslam_ba_read_map": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_map_upload": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     "tslam_relocalize": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64] + [ctypes.c_void_p] * 3),
@@ -254,14 +257,28 @@ class Handle:
             raise ValueError(f"need {self.n_pairs} 4x4 matrices")
         _check(self.lib.tslam_set_rig(self.h, e.ctypes.data))
 
+    def set_rig_ranks(self, base_T_rect: list) -> None:
+        """Rig fusion across ranks: base_T_rect-left of every pair of every rank (rank-major)."""
+        e = np.ascontiguousarray(np.stack([np.asarray(m, dtype=np.float64) for m in base_T_rect]))
+        if e.shape[1:] != (4, 4) or e.shape[0] % self.n_pairs:
+            raise ValueError("need world * n_pairs 4x4 matrices")
+        _check(self.lib.tslam_set_rig_ranks(self.h, int(e.shape[0] // self.n_pairs), e.ctypes.data))
+
+    def rig_fuse(self, gathered_dev_ptr: int, world: int, first_frame: int, n_frames: int, stream: int = 0) -> None:
+        """Fuse the gathered blocks of one batch into body motions (enqueued on ``stream``)."""
+        _check(self.lib.tslam_rig_fuse(self.h, ctypes.c_void_p(gathered_dev_ptr), int(world), int(first_frame),
+                                       int(n_frames), ctypes.c_void_p(stream)))
+        self._rig_fused_n = int(n_frames)
+
     def read_rig_poses(self, n_frames: int) -> dict:
         """Body-frame rig motion of the last batch (synchronises)."""
-        t_rel = np.zeros((n_frames, 4, 4))
-        t_abs = np.zeros((n_frames, 4, 4))
-        cov = np.zeros((n_frames, 6, 6))
-        stats = np.zeros((n_frames, 8), dtype=np.int32)
+        cap = self.batch if getattr(self, "_rig_fused_n", None) is not None else n_frames
+        t_rel = np.zeros((cap, 4, 4))
+        t_abs = np.zeros((cap, 4, 4))
+        cov = np.zeros((cap, 6, 6))
+        stats = np.zeros((cap, 8), dtype=np.int32)
         _check(self.lib.tslam_read_rig_poses(self.h, t_rel.ctypes.data, t_abs.ctypes.data, cov.ctypes.data, stats.ctypes.data))
-        return {"T_rel": t_rel, "T_abs": t_abs, "cov": cov, "stats": stats}
+        return {"T_rel": t_rel[:n_frames], "T_abs": t_abs[:n_frames], "cov": cov[:n_frames], "stats": stats[:n_frames]}
 
     # -- buffer access (tests) -------------------------------------------------------------
     def buffer_info(self, which: str) -> tuple[int, int, int]:
