@@ -278,10 +278,33 @@ def main() -> None:
     # two exchange buffers: batch s packs into buffer s % 2 and all-gathers it asynchronously over
     # RCCL while batch s + 1 computes (the buffer is reused only after its gather has completed)
     exchanges = [FeatureExchange(layout, "cuda" if on_device else "cpu", world) for _ in range(2)] if world > 1 else []
-    pending = [None, None]
+    pending = {"work": None, "buf": 0, "batch": -1}   # the in-flight all-gather (one at a time)
     staging = torch.empty((layout.rank_bytes,), dtype=torch.uint8, device="cuda") if world > 1 and not on_device else None
+    recv_dev = None
+    if world > 1:
+        # the rig-level solve after the gather: every rank fuses all ranks' body
+        # motions on its device; the rig extrinsics of every rank's pair are exchanged once
+        bt = torch.from_numpy(np.ascontiguousarray(cams[0].extrinsics.to_4x4_matrix() @ rect.left_optical_T_rect()))
+        if on_device:
+            every = torch.empty((world, 4, 4), dtype=torch.float64, device="cuda")
+            dist.all_gather_into_tensor(every, bt.cuda())
+            every = every.cpu()
+        else:
+            parts = [torch.empty((4, 4), dtype=torch.float64) for _ in range(world)]
+            dist.all_gather(parts, bt)
+            every = torch.stack(parts)
+            recv_dev = torch.empty((world * layout.rank_bytes,), dtype=torch.uint8, device="cuda")
+        h.set_rig_ranks(list(every.numpy()))
     names = list(KERNELS) + (["local_ba"] if c4 else [])
     n_ev = len(names) + 1
+
+    def finish_exchange() -> None:
+        """Make the stream wait for the in-flight gather (the host does not block) and run the
+        rig fusion of that batch on the device."""
+        if pending["work"] is not None:
+            pending["work"].wait()
+            h.rig_fuse(exchanges[pending["buf"]].recv.data_ptr(), world, pending["batch"] * B, B, sp)
+            pending["work"] = None
 
     def step(s: int, evs=None) -> None:
         # one batch = every kernel of the hot path in order on `stream`; in the timed steps HIP
@@ -301,20 +324,19 @@ def main() -> None:
             k = s % 2
             ex = exchanges[k]
             if on_device:
-                if pending[k] is not None:
-                    pending[k].wait()
+                # batch s-1's gather ran while batch s computed: fuse it, then ship batch s
+                finish_exchange()
                 h.pack_features(ex.send.data_ptr(), sp)
-                pending[k] = ex.all_gather(async_op=True)
-            else:
+                pending.update(work=ex.all_gather(async_op=True), buf=k, batch=s)
+            else:   # gloo rehearsal: host gather, then the same device fusion
                 h.pack_features(staging.data_ptr(), sp)
                 ex.send.copy_(staging.cpu())
                 ex.all_gather()
+                recv_dev.copy_(ex.recv)
+                h.rig_fuse(recv_dev.data_ptr(), world, s * B, B, sp)
 
     def drain() -> None:
-        for k in range(2):
-            if pending[k] is not None:
-                pending[k].wait()
-                pending[k] = None
+        finish_exchange()
 
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_ev)] for _ in range(args.steps)]
     for s in range(args.warmup):
@@ -341,6 +363,9 @@ def main() -> None:
         elapsed = float(tt.item())
     res = h.read_poses(B)
     ok_frac = float(np.mean(res["stats"][:, 0, 0] == 0))
+    rig_ok = None
+    if world > 1:
+        rig_ok = float(np.mean(h.read_rig_poses(B)["stats"][:, 0] == 0))
 
     # ---- per-kernel durations of the timed launches (HIP events on the launch stream) ----------
     per_kernel_us = {k: 0.0 for k in names}
@@ -437,12 +462,14 @@ def main() -> None:
             "frames_per_step": B,
             "n_features": cfg.n_features,
             "parallelism": f"one {'RGB-D camera' if c5 else 'stereo source'} per GPU x{world}"
-                           + (" + RCCL all-gather of keypoints/descriptors" if world > 1 else ""),
+                           + (" + RCCL all-gather of keypoints/descriptors/poses + on-device rig fusion"
+                              if world > 1 else ""),
         },
         "roofline": roofline,
         "latency_b1_ms": lat_ms,
         "per_kernel_us_per_batch": per_kernel_us,
         "tracking_ok_fraction_last_batch": ok_frac,
+        "rig_fusion_ok_fraction_last_batch": rig_ok,
         "render_s": t_render,
     }
     if front_roofline is not None:
