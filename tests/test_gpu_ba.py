@@ -143,3 +143,27 @@ def test_engine_publishes_ba_poses_and_map():
     fe_err = np.linalg.norm((bt @ sc["oracle"][n - 1]["world_T_cam"] @ inv(bt))[:3, 3] - gt[:3, 3])
     assert np.linalg.norm(poses[-1].position - gt[:3, 3]) < fe_err
     eng.shutdown()
+
+
+def test_ba_on_its_own_stream_matches():
+    """The BA stage on a second stream, overlapping the next batches' front end (the library
+    orders it with events and a pose snapshot): same windows as the oracle."""
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    n, batch = 12, 3
+    sc, want = _scenario_and_oracle(n)
+    h = Handle([sc["rect"]], sc["cfg"], max_batch=batch)
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    main, side = torch.cuda.current_stream(), torch.cuda.Stream()
+    try:
+        for b0 in range(0, n, batch):
+            h.begin_batch(dev[b0:].data_ptr(), batch)
+            for st in ("rectify", "detect", "describe", "match", "pose"):
+                h.run_stage(st, main.cuda_stream)
+            h.run_stage("ba", side.cuda_stream)
+            h.end_batch()
+        _compare(h.ba_read(0), want[n - 1], "two streams, final window")
+    finally:
+        h.close()

@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256) void k_ba_insert(BatchCtx c, BaArgs a) {
     const int f = (int)(g - c.g0);                  // frame of the current batch
     const int rslot = ring_slot(c, g);
     if (threadIdx.x == 0) {
-        const double* Tfe = c.pose + (size_t)(f * c.P + p) * TS_POSE_DOUBLES + 16;   // world_T_cam
+        const double* Tfe = a.fe + (size_t)(f * c.P + p) * 16;   // world_T_cam (front-end snapshot)
         double Twc[16];
         if (a.prev < 0) {
             for (int e = 0; e < 16; ++e) Twc[e] = Tfe[e];
@@ -744,6 +744,18 @@ __global__ __launch_bounds__(256) void k_ba_backsub(BatchCtx c, BaArgs a) {
 // ---------------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------------
+// The batch's front-end poses (T_abs) copied out of the per-batch pose buffer on the front-end
+// stream, so the BA of this batch may run on another stream while the next batch reuses it.
+__global__ __launch_bounds__(256) void k_ba_snapshot(BatchCtx c, double* dst) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= c.n * c.P * 16) return;
+    dst[i] = c.pose[(size_t)(i / 16) * TS_POSE_DOUBLES + 16 + i % 16];
+}
+
+void launch_ba_snapshot(const BatchCtx& c, double* dst, hipStream_t s) {
+    hipLaunchKernelGGL(k_ba_snapshot, dim3((c.n * c.P * 16 + 255) / 256), dim3(256), 0, s, c, dst);
+}
+
 void launch_ba_keyframe(const BatchCtx& c, const BaArgs& a, bool evict, hipStream_t s) {
     const int K = c.g.K;
     if (evict) {

@@ -90,6 +90,12 @@ struct tslam_handle {
     int64_t ba_nkf = 0;
     int64_t ba_last = -1;    // newest frame inserted
     BaTiming ba_timing{};    // k_ba_schur events while profiling is on
+    // BA on its own stream (overlapping the next batch): events and the batch parity
+    int64_t batch_idx = 0;
+    bool batch_started = false;
+    hipStream_t ba_stream = nullptr;
+    hipEvent_t ev_fe = nullptr, ev_ba[2] = {nullptr, nullptr};
+    bool ba_pending[2] = {false, false};
     std::vector<hipEvent_t> ba_events;
 };
 
@@ -169,7 +175,7 @@ static int alloc_ba(tslam_handle* h) {
         {(void**)&b.counts, 4 * 4 * P},      {(void**)&b.tiles, 4 * 2 * TS_BA_TILES},      {(void**)&b.obs_W, 8 * WK * 18},    {(void**)&b.obs_Ug, 8 * WK * 27},
         {(void**)&b.lm_L, 8 * WK * 6},       {(void**)&b.lm_gp, 8 * WK * 3},     {(void**)&b.C, 8 * 64 * 64},
         {(void**)&b.part, 8 * (size_t)TS_BA_SPLIT * 64 * 64}, {(void**)&b.cam_U, 8 * W * 27}, {(void**)&b.dc, 8 * W * 6},
-        {(void**)&b.flops, 8},
+        {(void**)&b.flops, 8},               {(void**)&b.fe_pose, 8 * 2 * (size_t)h->B * P * 16},
     };
     for (const A& a : list) {
         const int rc = dev_alloc(h, a.p, a.bytes);
@@ -205,11 +211,12 @@ static BatchCtx make_ctx(tslam_handle* h);
 // A8: every keyframe of the current batch (g % ba_kf_interval == 0) enters each pair's window,
 // evicting the oldest when the window is full, and the window is solved.  Host bookkeeping of
 // the slots only; nothing synchronises.
-static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s) {
+static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const double* fe) {
     const int W = h->prm.ba_window, iv = h->prm.ba_kf_interval;
     for (int64_t g = c.g0; g < c.g0 + c.n; ++g) {
         if (g % iv != 0 || g <= h->ba_last) continue;
         BaArgs a = ba_args(h);
+        a.fe = fe;
         a.frame = g;
         a.slot = (int)(h->ba_nkf % W);
         int ord[TS_BA_MAXW];
@@ -346,7 +353,9 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     // the ring keeps frame t-1 of a batch's first frame; with BA it also keeps the frames a
     // keyframe's temporal match chain walks back over
     h->R = 2 * p.max_batch;
-    if (p.ba_window) h->R = std::max(h->R, p.ba_kf_interval + 1);
+    // with BA the ring also keeps the frames a keyframe's match chain walks back over, even while
+    // the next batch runs (BA may run on its own stream): R = 2B + interval + 1
+    if (p.ba_window) h->R = 2 * p.max_batch + p.ba_kf_interval + 1;
     build_geometry(h);
     for (int i = 0; i < h->P; ++i) {
         h->calib[i].fx = pairs[i].fx;
@@ -444,6 +453,8 @@ int tslam_destroy(tslam_handle* h) {
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();
     for (hipEvent_t e : h->ba_events) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {h->ev_fe, h->ev_ba[0], h->ev_ba[1]})
+        if (e) (void)hipEventDestroy(e);
     free_all(h);
     delete h;
     return TSLAM_OK;
@@ -462,6 +473,7 @@ int tslam_reset(tslam_handle* h) {
     for (int i = 0; i < TS_BA_MAXW; ++i) h->ba_frame[i] = -1;
     h->ba_nkf = 0;
     h->ba_last = -1;
+    h->ba_pending[0] = h->ba_pending[1] = false;
     h->in_batch = false;
     h->cur_n = 0;
     return TSLAM_OK;
@@ -478,6 +490,7 @@ int tslam_begin_batch(tslam_handle* h, const uint8_t* images, int n_frames) {
     h->cur_n = n_frames;
     h->cur_g0 = h->frames_done;
     h->in_batch = true;
+    h->batch_started = false;
     return TSLAM_OK;
 }
 
@@ -487,6 +500,7 @@ int tslam_end_batch(tslam_handle* h) {
     h->frames_done += h->cur_n;
     h->in_batch = false;
     h->prior_armed = false;   // a prior applies to one batch
+    h->batch_idx += 1;
     return TSLAM_OK;
 }
 
@@ -495,7 +509,15 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
     if (!h->in_batch) return fail(TSLAM_ESTATE, "tslam_begin_batch first");
     HIPCHK(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
-    h->last_stream = s;
+    if (stage != TSLAM_STAGE_BA) {
+        if (!h->batch_started) {   // the first front-end work of a batch: the BA of the batch two
+            const int par = (int)(h->batch_idx & 1);   // back (same ring slots) must have finished
+            if (h->ba_pending[par]) HIPCHK(hipStreamWaitEvent(s, h->ev_ba[par], 0));
+            h->ba_pending[par] = false;
+            h->batch_started = true;
+        }
+        h->last_stream = s;
+    }
     const BatchCtx c = make_ctx(h);
     if (h->prm.rgbd && (stage == TSLAM_STAGE_RECTIFY || stage == TSLAM_STAGE_ALL || stage == TSLAM_KERNEL_RECTIFY_PYRAMID))
         launch_rgbd_gray(c, h->d_gray, s);   // the colour images become the gray input of rectify
@@ -519,16 +541,41 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
             launch_pose(c, s);
             launch_chain(c, s);
             if (h->rig) launch_rig(c, s);
-            if (h->prm.ba_window) run_ba(h, c, s);
+            if (h->prm.ba_window) {
+                double* snap = h->ba.fe_pose + (size_t)(h->batch_idx & 1) * h->B * h->P * 16;
+                launch_ba_snapshot(c, snap, s);
+                run_ba(h, c, s, snap);
+            }
             break;
         case TSLAM_KERNEL_RIG:
             if (!h->rig) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig)");
             launch_rig(c, s);
             break;
-        case TSLAM_STAGE_BA:
+        case TSLAM_STAGE_BA: {
+            // may run on its own stream: it depends on this batch's front end (event) and only
+            // reads ring buffers plus a snapshot of the batch's poses, so the next batch can start
             if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
-            run_ba(h, c, s);
+            const int par = (int)(h->batch_idx & 1);
+            double* snap = h->ba.fe_pose + (size_t)par * h->B * h->P * 16;
+            hipStream_t fs = h->last_stream;
+            launch_ba_snapshot(c, snap, fs);
+            const bool other = s != fs;
+            if (other) {
+                if (!h->ev_fe) {
+                    HIPCHK(hipEventCreateWithFlags(&h->ev_fe, hipEventDisableTiming));
+                    HIPCHK(hipEventCreateWithFlags(&h->ev_ba[0], hipEventDisableTiming));
+                    HIPCHK(hipEventCreateWithFlags(&h->ev_ba[1], hipEventDisableTiming));
+                }
+                HIPCHK(hipEventRecord(h->ev_fe, fs));
+                HIPCHK(hipStreamWaitEvent(s, h->ev_fe, 0));
+            }
+            run_ba(h, c, s, snap);
+            if (other) {
+                HIPCHK(hipEventRecord(h->ev_ba[par], s));
+                h->ba_pending[par] = true;
+            }
             break;
+        }
         case TSLAM_KERNEL_RECTIFY_PYRAMID: launch_rectify_pyramid(c, s); break;
         case TSLAM_KERNEL_DETECT: launch_detect(c, s); break;
         case TSLAM_KERNEL_SELECT: launch_select(c, s); break;

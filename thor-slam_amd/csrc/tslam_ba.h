@@ -54,6 +54,7 @@ struct BaStore {
     double* cam_U;     // [W][27]
     double* dc;        // [W][6]
     double* flops;     // [1] algorithmic Schur-product flops accumulated (profiling)
+    double* fe_pose;   // [2][B][P][16] front-end world_T_cam of the batch (snapshot per batch parity)
 };
 
 struct BaArgs {
@@ -68,6 +69,7 @@ struct BaArgs {
     int order[TS_BA_MAXW];      // evict: remaining slots; gather/solve: occupied slots, oldest first
     int iters, nsplit;
     double lam, outlier_px;
+    const double* fe;           // insert: this batch's front-end pose snapshot [B][P][16]
 };
 
 // Per-pair view (the scratch pointers are shared).
@@ -108,6 +110,7 @@ __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, in
     return q;
 }
 
+void launch_ba_snapshot(const BatchCtx& c, double* dst, hipStream_t s);
 void launch_ba_keyframe(const BatchCtx& c, const BaArgs& a, bool evict, hipStream_t s);
 // timing: when non-null, an event pair is recorded around every k_ba_schur launch (profiling)
 struct BaTiming {
