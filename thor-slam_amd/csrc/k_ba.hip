@@ -369,41 +369,9 @@ __device__ __forceinline__ void ba_obs_jac(const double* T, const double* X, dou
     }
 }
 
-// One thread per observation: W_o = J_c^T J_p and J_p^T J_p | J_p^T r (per observation, read back
-// per landmark), J_c^T J_c | J_c^T r (structure-of-arrays, summed per camera).
-__global__ __launch_bounds__(256) void k_ba_jac(BatchCtx c, BaArgs a) {
-    __shared__ double s_T[TS_BA_MAXW][12];
-    const int K = c.g.K, WK = a.W * K;
-    BaPair q = ba_pair(c, a, a.pair);
-    for (int i = threadIdx.x; i < a.n_order * 12; i += blockDim.x) s_T[i / 12][i % 12] = q.T[(size_t)a.order[i / 12] * 16 + i % 12];
-    __syncthreads();
-    const int o = blockIdx.x * blockDim.x + threadIdx.x;
-    if (o >= q.counts[0]) return;
-    const PairCalib cal = c.calib[a.pair];
-    const int ci = q.obs_cam[o], id = q.obs_id[o];
-    const size_t so = (size_t)a.order[ci] * K + q.obs_k[o];
-    const double X[3] = {q.X[(size_t)id * 3], q.X[(size_t)id * 3 + 1], q.X[(size_t)id * 3 + 2]};
-    double Jc[3][6], Jp[3][3], res[3];
-    ba_obs_jac(s_T[ci], X, q.u[so], q.v[so], q.d[so], cal, Jc, Jp, res);
-    for (int i = 0; i < 6; ++i)
-        for (int j = 0; j < 3; ++j) q.obs_W[(size_t)o * 18 + 3 * i + j] = (Jc[0][i] * Jp[0][j] + Jc[1][i] * Jp[1][j]) + Jc[2][i] * Jp[2][j];
-    int e = 0;
-    for (int i = 0; i < 6; ++i)
-        for (int j = i; j < 6; ++j) q.obs_Ug[(size_t)(e++) * WK + o] = (Jc[0][i] * Jc[0][j] + Jc[1][i] * Jc[1][j]) + Jc[2][i] * Jc[2][j];
-    for (int i = 0; i < 6; ++i) q.obs_Ug[(size_t)(21 + i) * WK + o] = (Jc[0][i] * res[0] + Jc[1][i] * res[1]) + Jc[2][i] * res[2];
-    e = 0;
-    for (int i = 0; i < 3; ++i)
-        for (int j = i; j < 3; ++j) q.obs_Vg[(size_t)o * 9 + (e++)] = (Jp[0][i] * Jp[0][j] + Jp[1][i] * Jp[1][j]) + Jp[2][i] * Jp[2][j];
-    for (int i = 0; i < 3; ++i) q.obs_Vg[(size_t)o * 9 + 6 + i] = (Jp[0][i] * res[0] + Jp[1][i] * res[1]) + Jp[2][i] * res[2];
-}
-
 // One wave per (window camera, element): U_c = sum J_c^T J_c, g_c = sum J_c^T r over the camera's
 // observations (lanes stride them, 4 accumulators, DPP wave sum: a fixed order).
-__global__ __launch_bounds__(64) void k_ba_camred(BatchCtx c, BaArgs a) {
-    const int WK = a.W * c.g.K;
-    BaPair q = ba_pair(c, a, a.pair);
-    const int ci = blockIdx.x / 27, e = blockIdx.x % 27;
-    const int lane = threadIdx.x;
+__device__ void ba_camred_wave(const BaPair& q, int WK, int ci, int e, int lane) {
     const int o0 = q.cam_off[ci], o1 = q.cam_off[ci + 1];
     const double* src = q.obs_Ug + (size_t)e * WK;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
@@ -423,48 +391,77 @@ typedef double d4v __attribute__((ext_vector_type(4)));
 #define BA_CHUNK 32          // landmarks per LDS tile (96 Schur columns)
 #define BA_QPITCH 80         // doubles per tile column: 160 dwords = 32 mod 64 banks, so the four
                              // columns one MFMA operand read touches fall in disjoint bank halves
+#define BA_SCHUR_THREADS (BA_CHUNK * TS_BA_MAXW)   // 320: one thread per (landmark, window camera)
 
-// The landmark side of the Schur complement, fused: per chunk of BA_CHUNK landmarks,
-//   1. one thread per landmark: V = sum J_p^T J_p + lam I (camera order), g_p, L = chol(V),
-//      y = L^-1 g_p (L and g_p also go to HBM for the back substitution);
-//   2. the chunk's Schur columns into an LDS tile Q[3 * BA_CHUNK][64]: column 3l + j holds
-//      (W_o L^-T)[:, j] in the 6 rows of the observing camera (0 when unobserved) and y_j in row 60;
-//   3. C += Q^T Q on the FP64 matrix cores (v_mfma_f64_16x16x4f64): wave w owns rows 16w..16w+15.
-// Blocks stride the chunks; each block writes its 64 x 64 partial (summed by k_ba_reduce).
-__global__ __launch_bounds__(256) void k_ba_schur(BatchCtx c, BaArgs a) {
+// The landmark side of one Gauss-Newton step, fused; per chunk of BA_CHUNK landmarks:
+//   1. one thread per (landmark, camera) with an observation: J_c, J_p, r (ba_obs_jac) ->
+//      W_o = J_c^T J_p and J_p^T J_p | J_p^T r into LDS; W_o (for the back substitution) and
+//      J_c^T J_c | J_c^T r (summed per camera by k_ba_reduce) to HBM;
+//   2. one thread per landmark: V = lam I + sum_c J_p^T J_p (camera order), g_p, L = chol(V),
+//      y = L^-1 g_p (L, g_p to HBM for the back substitution);
+//   3. the chunk's Schur columns into an LDS tile Q[3 * BA_CHUNK][64]: column 3l + j holds
+//      (W_o L^-T)[:, j] in the 6 rows of the observing camera (0 when unobserved), y_j in row 60;
+//   4. C += Q^T Q on the FP64 matrix cores (v_mfma_f64_16x16x4f64), waves 0-3 own 16 rows each.
+// Blocks stride the chunks; each block that had a chunk writes its 64 x 64 partial.
+__global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArgs a) {
     __shared__ double s_Q[3 * BA_CHUNK * BA_QPITCH];
+    __shared__ double s_W[BA_CHUNK][TS_BA_MAXW][18];
+    __shared__ double s_Vg[BA_CHUNK][TS_BA_MAXW][9];
+    __shared__ int s_has[BA_CHUNK][TS_BA_MAXW];
     __shared__ double s_L[BA_CHUNK][6];
-    __shared__ int s_co[BA_CHUNK][TS_BA_MAXW];
-    const int WK = a.W * c.g.K, n = a.n_order;
+    __shared__ double s_T[TS_BA_MAXW][12];
+    const int K = c.g.K, WK = a.W * K, n = a.n_order;
     BaPair q = ba_pair(c, a, a.pair);
     const int L = q.counts[1];
+    const PairCalib cal = c.calib[a.pair];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int kk = lane >> 4, rc = lane & 15;
+    for (int i = threadIdx.x; i < n * 12; i += blockDim.x) s_T[i / 12][i % 12] = q.T[(size_t)a.order[i / 12] * 16 + i % 12];
     d4v acc[4];
     for (int t = 0; t < 4; ++t) acc[t] = (d4v){0.0, 0.0, 0.0, 0.0};
     for (int l0 = blockIdx.x * BA_CHUNK; l0 < L; l0 += gridDim.x * BA_CHUNK) {
         const int nl = min(BA_CHUNK, L - l0);
-        // 1. per-landmark factor (loads issued unconditionally from clamped indices, then masked:
-        //    the kernel is latency bound, so every load of a thread is in flight at once)
-        if (threadIdx.x < BA_CHUNK) {
-            const int li = threadIdx.x, r = min(l0 + li, L - 1);
-            const bool live = li < nl;
-            int co[TS_BA_MAXW];
-#pragma unroll
-            for (int ci = 0; ci < TS_BA_MAXW; ++ci) co[ci] = q.camobs[(size_t)min(ci, n - 1) * WK + r];
-            double vo[TS_BA_MAXW][9];
-#pragma unroll
-            for (int ci = 0; ci < TS_BA_MAXW; ++ci)
-#pragma unroll
-                for (int e = 0; e < 9; ++e) vo[ci][e] = q.obs_Vg[(size_t)max(co[ci], 0) * 9 + e];
-            double vg[9] = {a.lam, 0.0, 0.0, a.lam, 0.0, a.lam, 0.0, 0.0, 0.0};   // V00 V01 V02 V11 V12 V22 g
-#pragma unroll
-            for (int ci = 0; ci < TS_BA_MAXW; ++ci) {
-                const bool use = ci < n && co[ci] >= 0;
-                s_co[li][ci] = ci < n ? co[ci] : -1;
-#pragma unroll
-                for (int e = 0; e < 9; ++e) vg[e] += use ? vo[ci][e] : 0.0;
+        __syncthreads();
+        // 1. Jacobians of every (landmark, camera) observation of the chunk
+        {
+            const int li = threadIdx.x / TS_BA_MAXW, ci = threadIdx.x - li * TS_BA_MAXW;
+            const int r = l0 + li;
+            const int o = (li < nl && ci < n) ? q.camobs[(size_t)ci * WK + r] : -1;
+            s_has[li][ci] = o >= 0;
+            if (o >= 0) {
+                const int id = q.lm_id[r];
+                const size_t so = (size_t)a.order[ci] * K + q.obs_k[o];
+                const double X[3] = {q.X[(size_t)id * 3], q.X[(size_t)id * 3 + 1], q.X[(size_t)id * 3 + 2]};
+                double Jc[3][6], Jp[3][3], res[3];
+                ba_obs_jac(s_T[ci], X, q.u[so], q.v[so], q.d[so], cal, Jc, Jp, res);
+                double* W = s_W[li][ci];
+                for (int i = 0; i < 6; ++i)
+                    for (int j = 0; j < 3; ++j) {
+                        const double w = (Jc[0][i] * Jp[0][j] + Jc[1][i] * Jp[1][j]) + Jc[2][i] * Jp[2][j];
+                        W[3 * i + j] = w;
+                        q.obs_W[(size_t)o * 18 + 3 * i + j] = w;
+                    }
+                int e = 0;
+                for (int i = 0; i < 6; ++i)
+                    for (int j = i; j < 6; ++j) q.obs_Ug[(size_t)(e++) * WK + o] = (Jc[0][i] * Jc[0][j] + Jc[1][i] * Jc[1][j]) + Jc[2][i] * Jc[2][j];
+                for (int i = 0; i < 6; ++i) q.obs_Ug[(size_t)(21 + i) * WK + o] = (Jc[0][i] * res[0] + Jc[1][i] * res[1]) + Jc[2][i] * res[2];
+                double* vg = s_Vg[li][ci];
+                e = 0;
+                for (int i = 0; i < 3; ++i)
+                    for (int j = i; j < 3; ++j) vg[e++] = (Jp[0][i] * Jp[0][j] + Jp[1][i] * Jp[1][j]) + Jp[2][i] * Jp[2][j];
+                for (int i = 0; i < 3; ++i) vg[6 + i] = (Jp[0][i] * res[0] + Jp[1][i] * res[1]) + Jp[2][i] * res[2];
             }
+        }
+        __syncthreads();
+        // 2. per-landmark factor
+        if (threadIdx.x < BA_CHUNK) {
+            const int li = threadIdx.x, r = l0 + li;
+            const bool live = li < nl;
+            double vg[9] = {a.lam, 0.0, 0.0, a.lam, 0.0, a.lam, 0.0, 0.0, 0.0};   // V00 V01 V02 V11 V12 V22 g
+            for (int ci = 0; ci < n; ++ci)
+                if (s_has[li][ci])
+#pragma unroll
+                    for (int e = 0; e < 9; ++e) vg[e] += s_Vg[li][ci][e];
             const double l00 = sqrt(vg[0] > 1e-300 ? vg[0] : 1e-300);
             const double l10 = vg[1] / l00, l20 = vg[2] / l00;
             const double d11 = vg[3] - l10 * l10;
@@ -485,56 +482,43 @@ __global__ __launch_bounds__(256) void k_ba_schur(BatchCtx c, BaArgs a) {
             }
         }
         __syncthreads();
-        // 2. Schur columns: thread = (row, wave); items = landmarks wave, wave + 4, ...:
-        //    z = L^-1 W_o[row % 6, :]^T for the observation o of the row's camera (0 if none)
-        {
-            const int row = threadIdx.x & 63, ci = min(row / 6, TS_BA_MAXW - 1), rr = row - 6 * (row / 6);
-            constexpr int NU = BA_CHUNK / 4;
-            int o[NU];
-            double w[NU][3];
-#pragma unroll
-            for (int u = 0; u < NU; ++u) o[u] = s_co[wave + 4 * u][ci];
-#pragma unroll
-            for (int u = 0; u < NU; ++u) {
-                const double* W = q.obs_W + (size_t)max(o[u], 0) * 18 + 3 * rr;
-                w[u][0] = W[0];
-                w[u][1] = W[1];
-                w[u][2] = W[2];
-            }
-            const bool row_ok = row < 6 * n && row != 60;
-#pragma unroll
-            for (int u = 0; u < NU; ++u) {
-                const int li = wave + 4 * u;
+        // 3. Schur columns: item = (landmark, row != 60), all from LDS
+        for (int it = threadIdx.x; it < BA_CHUNK * 64; it += blockDim.x) {
+            const int li = it >> 6, row = it & 63;
+            if (row == 60) continue;
+            const int ci = row / 6, rr = row - 6 * ci;
+            double z0 = 0.0, z1 = 0.0, z2 = 0.0;
+            if (li < nl && ci < n && s_has[li][ci]) {
+                const double* W = s_W[li][ci] + 3 * rr;
                 const double* Lm = s_L[li];
-                const bool use = row_ok && li < nl && o[u] >= 0;
-                const double z0 = w[u][0] * Lm[0];
-                const double z1 = (w[u][1] - Lm[1] * z0) * Lm[2];
-                const double z2 = ((w[u][2] - Lm[3] * z0) - Lm[4] * z1) * Lm[5];
-                if (row != 60) {
-                    s_Q[(3 * li) * BA_QPITCH + row] = use ? z0 : 0.0;
-                    s_Q[(3 * li + 1) * BA_QPITCH + row] = use ? z1 : 0.0;
-                    s_Q[(3 * li + 2) * BA_QPITCH + row] = use ? z2 : 0.0;
-                }
+                z0 = W[0] * Lm[0];
+                z1 = (W[1] - Lm[1] * z0) * Lm[2];
+                z2 = ((W[2] - Lm[3] * z0) - Lm[4] * z1) * Lm[5];
+            }
+            s_Q[(3 * li) * BA_QPITCH + row] = z0;
+            s_Q[(3 * li + 1) * BA_QPITCH + row] = z1;
+            s_Q[(3 * li + 2) * BA_QPITCH + row] = z2;
+        }
+        __syncthreads();
+        // 4. C += Q^T Q over the chunk's columns (zero columns past nl contribute nothing)
+        if (wave < 4) {
+            const int ksteps = (3 * nl + 3) >> 2;
+            for (int st = 0; st < ksteps; ++st) {
+                const double* col = s_Q + (4 * st + kk) * BA_QPITCH;
+                const double b0 = col[rc], b1 = col[16 + rc], b2 = col[32 + rc], b3 = col[48 + rc];
+                const double av = wave == 0 ? b0 : wave == 1 ? b1 : wave == 2 ? b2 : b3;
+                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b0, acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b1, acc[1], 0, 0, 0);
+                acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b2, acc[2], 0, 0, 0);
+                acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b3, acc[3], 0, 0, 0);
             }
         }
-        __syncthreads();
-        // 3. C += Q^T Q over the chunk's columns (zero columns past nl contribute nothing)
-        const int ksteps = (3 * nl + 3) >> 2;
-        for (int st = 0; st < ksteps; ++st) {
-            const double* col = s_Q + (4 * st + kk) * BA_QPITCH;
-            const double b0 = col[rc], b1 = col[16 + rc], b2 = col[32 + rc], b3 = col[48 + rc];
-            const double av = wave == 0 ? b0 : wave == 1 ? b1 : wave == 2 ? b2 : b3;
-            acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b0, acc[0], 0, 0, 0);
-            acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b1, acc[1], 0, 0, 0);
-            acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b2, acc[2], 0, 0, 0);
-            acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b3, acc[3], 0, 0, 0);
-        }
-        __syncthreads();
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {   // algorithmic flops of the dense Schur product
         const double rows = 6.0 * n + 1.0;
         q.flops[0] += 2.0 * rows * rows * 3.0 * L;
     }
+    if (blockIdx.x * BA_CHUNK >= L || wave >= 4) return;   // no chunk: no partial
     double* out = q.part + (size_t)blockIdx.x * 64 * 64;
     const int a0 = 16 * wave;
     // C/D layout of v_mfma_f64_16x16x4f64: col = lane & 15, row = (lane >> 4) + 4 * reg
@@ -544,14 +528,27 @@ __global__ __launch_bounds__(256) void k_ba_schur(BatchCtx c, BaArgs a) {
         for (int rg = 0; rg < 4; ++rg) out[(size_t)(a0 + kk + 4 * rg) * 64 + 16 * t + rc] = acc[t][rg];
 }
 
-// Fixed-order sum of the split-K partials (one thread per element of C).
+// Fixed-order sum of the partials of the blocks that had a chunk: block = 64 elements of C,
+// 4 waves each summing every 4th partial, then the 4 wave sums in order.  Blocks 64.. reduce the
+// camera blocks U_c, g_c.
 __global__ __launch_bounds__(256) void k_ba_reduce(BatchCtx c, BaArgs a) {
+    __shared__ double s_p[4][64];
     BaPair q = ba_pair(c, a, a.pair);
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x >= 64) {   // the camera side: one wave per (camera, element)
+        const int item = (blockIdx.x - 64) * 4 + (int)(threadIdx.x >> 6);
+        if (item < a.n_order * 27) ba_camred_wave(q, a.W * c.g.K, item / 27, item % 27, threadIdx.x & 63);
+        return;
+    }
+    const int L = q.counts[1];
+    const int np = min(a.nsplit, (L + BA_CHUNK - 1) / BA_CHUNK);
+    const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+    const int e = blockIdx.x * 64 + lane;
     double s = 0.0;
-#pragma unroll 16
-    for (int b = 0; b < a.nsplit; ++b) s += q.part[(size_t)b * 4096 + e];
-    q.C[e] = s;
+#pragma unroll 8
+    for (int b = grp; b < np; b += 4) s += q.part[(size_t)b * 4096 + e];
+    s_p[grp][lane] = s;
+    __syncthreads();
+    if (grp == 0) q.C[e] = ((s_p[0][lane] + s_p[1][lane]) + s_p[2][lane]) + s_p[3][lane];
 }
 
 // Reduced camera system (camera 0 = gauge): S = blockdiag(U + lam) - C, b = -g_c + C[:, 60].
@@ -780,13 +777,11 @@ void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming
     hipLaunchKernelGGL(k_ba_tilescatter, dim3(ntiles), dim3(256), 0, s, c, a);
     hipLaunchKernelGGL(k_ba_camobs, dim3(nb), dim3(256), 0, s, c, a);
     for (int it = 0; it < a.iters; ++it) {
-        hipLaunchKernelGGL(k_ba_jac, dim3(nb), dim3(256), 0, s, c, a);
-        hipLaunchKernelGGL(k_ba_camred, dim3(a.n_order * 27), dim3(64), 0, s, c, a);
         const bool rec = timing && timing->used < timing->cap;
         if (rec) (void)hipEventRecord(timing->ev[2 * timing->used], s);
-        hipLaunchKernelGGL(k_ba_schur, dim3(a.nsplit), dim3(256), 0, s, c, a);
+        hipLaunchKernelGGL(k_ba_schur, dim3(a.nsplit), dim3(BA_SCHUR_THREADS), 0, s, c, a);
         if (rec) (void)hipEventRecord(timing->ev[2 * timing->used++ + 1], s);
-        hipLaunchKernelGGL(k_ba_reduce, dim3(16), dim3(256), 0, s, c, a);
+        hipLaunchKernelGGL(k_ba_reduce, dim3(64 + (a.n_order * 27 + 3) / 4), dim3(256), 0, s, c, a);
         hipLaunchKernelGGL(k_ba_solve, dim3(1), dim3(1024), 0, s, c, a);
         hipLaunchKernelGGL(k_ba_backsub, dim3(16 * nb), dim3(256), 0, s, c, a);
     }

@@ -15,7 +15,7 @@
 #include "tslam_common.h"
 
 #define TS_BA_MAXD 54   // 6 * (TS_BA_MAXW - 1): the reduced camera system without the gauge
-#define TS_BA_SPLIT 64  // split-K blocks of the Schur GEMM
+#define TS_BA_SPLIT 256 // blocks of the Schur product (32-landmark chunks dealt over them; 8192 landmarks in one round)
 #define TS_BA_TILES 128 // scan tiles of a solve's compaction (landmark + observation tiles)
 
 static_assert(6 * TS_BA_MAXW + 1 <= 64, "the BA camera system (6 rows per keyframe + rhs) is 64 wide");
