@@ -565,19 +565,32 @@ __global__ __launch_bounds__(1024) void k_ba_solve(BatchCtx c, BaArgs a) {
         if (threadIdx.x == 0) q.counts[2] = 0;
         return;
     }
+    // stage C and the camera blocks in LDS first (every load in flight at once), then build S
+    __shared__ double s_C[64 * 64];
+    __shared__ double s_U[TS_BA_MAXW * 27];
+    {
+        double v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = q.C[threadIdx.x + 1024 * k];
+        const double u = (int)threadIdx.x < n * 27 ? q.cam_U[threadIdx.x] : 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s_C[threadIdx.x + 1024 * k] = v[k];
+        if ((int)threadIdx.x < n * 27) s_U[threadIdx.x] = u;
+    }
+    __syncthreads();
     for (int i = threadIdx.x; i < m * mp; i += blockDim.x) {
         const int rr = i / mp, cc = i - rr * mp;
         const int R = rr + 6;
         double v;
         if (cc == m) {
-            v = -q.cam_U[(size_t)(R / 6) * 27 + 21 + R % 6] + q.C[R * 64 + 60];
+            v = -s_U[(R / 6) * 27 + 21 + R % 6] + s_C[R * 64 + 60];
         } else {
             const int Cc = cc + 6;
-            v = -q.C[R * 64 + Cc];
+            v = -s_C[R * 64 + Cc];
             if (R / 6 == Cc / 6) {
                 const int i0 = R % 6, j0 = Cc % 6;
                 const int lo = min(i0, j0), hi = max(i0, j0);
-                v += q.cam_U[(size_t)(R / 6) * 27 + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)] + (i0 == j0 ? a.lam : 0.0);
+                v += s_U[(R / 6) * 27 + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)] + (i0 == j0 ? a.lam : 0.0);
             }
         }
         s_S[i] = v;
@@ -589,8 +602,11 @@ __global__ __launch_bounds__(1024) void k_ba_solve(BatchCtx c, BaArgs a) {
     //    block's columns and the rhs, S[i][k] -= (S[i][j] / d_j) S[k][j] (wave-synchronous);
     //  trailing (all threads): S[i][k] -= sum_j (S[i][j] / d_j) S[k][j] for c0+6 <= k <= i.
     // Column j below the pivot is left as L'[i][j] * d_j.
+#ifndef BA_TT
+#define BA_TT 1   // 2x2 and 4x4 register tiles measured slower (the update is latency-bound)
+#endif
 #ifndef BA_XP_NOELIM
-    __shared__ double s_rd[6];
+    __shared__ double s_P[TS_BA_MAXD * 6];
     for (int c0 = 0; c0 < m; c0 += 6) {
         if (threadIdx.x < 64) {
             // panel in registers: lane = row i (>= c0) holds its 6 block entries and its rhs; the
@@ -601,6 +617,7 @@ __global__ __launch_bounds__(1024) void k_ba_solve(BatchCtx c, BaArgs a) {
 #pragma unroll
             for (int e = 0; e < 6; ++e) pv[e] = row ? s_S[i * mp + c0 + e] : 0.0;
             bool good = true;
+            double rdv[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
                 const double dj = readlane_f64(pv[j], j);
@@ -618,27 +635,47 @@ __global__ __launch_bounds__(1024) void k_ba_solve(BatchCtx c, BaArgs a) {
                     if (below && k <= (int)threadIdx.x) pv[k] -= sij * skj;
                 }
                 if (below) rh -= sij * rhj;
-                if (threadIdx.x == 0) s_rd[j] = rj;
+                rdv[j] = rj;
             }
             if (!good && threadIdx.x == 0) s_ok = 0;
             if (row) {
 #pragma unroll
-                for (int e = 0; e < 6; ++e) s_S[i * mp + c0 + e] = pv[e];
+                for (int e = 0; e < 6; ++e) {
+                    s_S[i * mp + c0 + e] = pv[e];
+                    s_P[i * 6 + e] = pv[e] * rdv[e];   // L'[i][c0+e] for the trailing update
+                }
                 s_S[i * mp + m] = rh;
             }
         }
         __syncthreads();
         if (!s_ok) break;
-        const int c1 = c0 + 6, nt = m - c1;
-        for (int t = threadIdx.x; t < nt * nt; t += blockDim.x) {
-            const int i = c1 + t / nt, k = c1 + t % nt;
-            if (k > i) continue;
-            const double* si = s_S + i * mp + c0;
-            const double* sk = s_S + k * mp + c0;
-            double acc = 0.0;
+        // trailing update in BA_TT x BA_TT register tiles (lower triangle): a tile loads its scaled
+        // and plain panel rows once
+        const int c1 = c0 + 6, nt = m - c1, T = (nt + BA_TT - 1) / BA_TT;
+        for (int t = threadIdx.x; t < T * T; t += blockDim.x) {
+            const int ti = t / T, tk = t - ti * T;
+            if (tk > ti) continue;
+            const int i0 = c1 + BA_TT * ti, k0 = c1 + BA_TT * tk;
+            double pi[BA_TT][6], pk[BA_TT][6];
 #pragma unroll
-            for (int e = 0; e < 6; ++e) acc += (si[e] * s_rd[e]) * sk[e];
-            s_S[i * mp + k] -= acc;
+            for (int r = 0; r < BA_TT; ++r)
+#pragma unroll
+                for (int e = 0; e < 6; ++e) {
+                    pi[r][e] = i0 + r < m ? s_P[(i0 + r) * 6 + e] : 0.0;
+                    pk[r][e] = k0 + r < m ? s_S[(k0 + r) * mp + c0 + e] : 0.0;
+                }
+#pragma unroll
+            for (int r = 0; r < BA_TT; ++r)
+#pragma unroll
+                for (int q2 = 0; q2 < BA_TT; ++q2) {
+                    const int ii = i0 + r, k = k0 + q2;
+                    if (ii < m && k <= ii) {
+                        double acc = 0.0;
+#pragma unroll
+                        for (int e = 0; e < 6; ++e) acc += pi[r][e] * pk[q2][e];
+                        s_S[ii * mp + k] -= acc;
+                    }
+                }
         }
         __syncthreads();
     }
