@@ -300,6 +300,8 @@ def main() -> None:
     # C4: local BA runs on its own stream, overlapping the next batch's front end (the library
     # orders it after this batch's pose stage and the batch after next after it)
     ba_stream = torch.cuda.Stream() if c4 else None
+    ba_done = [torch.cuda.Event(), torch.cuda.Event()] if c4 else None
+    ba_issued = [False, False]
 
     def finish_exchange() -> None:
         """Make the stream wait for the in-flight gather (the host does not block) and run the
@@ -313,6 +315,10 @@ def main() -> None:
         # one batch = every kernel of the hot path in order on `stream`; in the timed steps HIP
         # events bracket each kernel (the per-kernel durations below are from these launches)
         h.begin_batch(seq[s * B].data_ptr(), B)
+        if c4 and ba_issued[s % 2]:
+            # the BA of batch s-2 shares this batch's ring slots: wait for it here (the library
+            # would), so the per-kernel events below time the kernels, not the wait
+            stream.wait_event(ba_done[s % 2])
         if evs is not None:
             evs[0].record(stream)
         for i, k in enumerate(names):
@@ -321,6 +327,8 @@ def main() -> None:
                 if evs is not None:
                     evs[-2].record(ba_stream)   # BA timed on its own stream: [start, end)
                 h.run_stage("ba", ba_stream.cuda_stream)
+                ba_done[s % 2].record(ba_stream)
+                ba_issued[s % 2] = True
                 if evs is not None:
                     evs[-1].record(ba_stream)
                 continue
