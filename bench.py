@@ -211,6 +211,8 @@ def main() -> None:
     ap.add_argument("--latency-frames", type=int, default=20, help="B=1 submissions timed for latency_b1_ms")
     ap.add_argument("--out", type=str, default="", help="also write the JSON line to this file")
     ap.add_argument("--dist-backend", type=str, default="nccl", help="nccl (RCCL) or gloo (rehearsal, host copy)")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="1: front and back kernels on two streams (batch s+1's front overlaps batch s's back)")
     ap.add_argument("--pmc", type=str, default=str(ROOT / "profiles" / "pmc_latest.json"),
                     help="PMC summary (tools/pmc_summary.py) used for roofline.traffic when its batch matches")
     args = ap.parse_args()
@@ -296,45 +298,61 @@ def main() -> None:
             recv_dev = torch.empty((world * layout.rank_bytes,), dtype=torch.uint8, device="cuda")
         h.set_rig_ranks(list(every.numpy()))
     names = list(KERNELS) + (["local_ba"] if c4 else [])
-    n_ev = len(names) + 1
-    # C4: local BA runs on its own stream, overlapping the next batch's front end (the library
-    # orders it after this batch's pose stage and the batch after next after it)
+    BACK = {"match", "match_refine", "pose", "chain"}
+    # two streams: the front kernels (rectify .. describe) of batch s + 1 overlap the back kernels
+    # (match .. chain) of batch s; the library orders batch s's back after its front and batch s's
+    # front after the back of batch s - 2 (ring slots); the exchange and fusion follow the back.
+    bstream = torch.cuda.Stream() if args.pipeline else stream
+    bsp = bstream.cuda_stream
+    back_done = [torch.cuda.Event(), torch.cuda.Event()]
+    back_issued = [False, False]
+    # C4: local BA runs on a third stream, overlapping the next batches
     ba_stream = torch.cuda.Stream() if c4 else None
     ba_done = [torch.cuda.Event(), torch.cuda.Event()] if c4 else None
     ba_issued = [False, False]
 
     def finish_exchange() -> None:
-        """Make the stream wait for the in-flight gather (the host does not block) and run the
+        """Make the back stream wait for the in-flight gather (the host does not block) and run the
         rig fusion of that batch on the device."""
         if pending["work"] is not None:
-            pending["work"].wait()
-            h.rig_fuse(exchanges[pending["buf"]].recv.data_ptr(), world, pending["batch"] * B, B, sp)
+            with torch.cuda.stream(bstream):
+                pending["work"].wait()
+            h.rig_fuse(exchanges[pending["buf"]].recv.data_ptr(), world, pending["batch"] * B, B, bsp)
             pending["work"] = None
 
     def step(s: int, evs=None) -> None:
-        # one batch = every kernel of the hot path in order on `stream`; in the timed steps HIP
-        # events bracket each kernel (the per-kernel durations below are from these launches)
+        # one batch = every kernel of the hot path; in the timed steps each kernel is bracketed by
+        # a pair of HIP events on the stream it runs on (the per-kernel durations below)
         h.begin_batch(seq[s * B].data_ptr(), B)
+        # the waits the library would insert, made here so the events time kernels, not waits
         if c4 and ba_issued[s % 2]:
-            # the BA of batch s-2 shares this batch's ring slots: wait for it here (the library
-            # would), so the per-kernel events below time the kernels, not the wait
             stream.wait_event(ba_done[s % 2])
-        if evs is not None:
-            evs[0].record(stream)
+        if bstream is not stream and back_issued[s % 2]:
+            stream.wait_event(back_done[s % 2])
+        first_back = True
         for i, k in enumerate(names):
             if k == "local_ba":
-                ba_stream.wait_stream(stream)
+                ba_stream.wait_stream(bstream)
                 if evs is not None:
-                    evs[-2].record(ba_stream)   # BA timed on its own stream: [start, end)
+                    evs[i][0].record(ba_stream)
                 h.run_stage("ba", ba_stream.cuda_stream)
                 ba_done[s % 2].record(ba_stream)
                 ba_issued[s % 2] = True
                 if evs is not None:
-                    evs[-1].record(ba_stream)
+                    evs[i][1].record(ba_stream)
                 continue
-            h.run_kernel(k, sp)
+            st = bstream if k in BACK else stream
+            if k in BACK and first_back and bstream is not stream:
+                bstream.wait_stream(stream)
+                first_back = False
             if evs is not None:
-                evs[i + 1].record(stream)
+                evs[i][0].record(st)
+            h.run_kernel(k, st.cuda_stream)
+            if evs is not None:
+                evs[i][1].record(st)
+        if bstream is not stream:
+            back_done[s % 2].record(bstream)
+            back_issued[s % 2] = True
         h.end_batch()
         if exchanges:  # the exchange step: every rank's keypoints/descriptors/poses to all ranks
             k = s % 2
@@ -342,19 +360,23 @@ def main() -> None:
             if on_device:
                 # batch s-1's gather ran while batch s computed: fuse it, then ship batch s
                 finish_exchange()
-                h.pack_features(ex.send.data_ptr(), sp)
-                pending.update(work=ex.all_gather(async_op=True), buf=k, batch=s)
+                h.pack_features(ex.send.data_ptr(), bsp)
+                with torch.cuda.stream(bstream):
+                    pending.update(work=ex.all_gather(async_op=True), buf=k, batch=s)
             else:   # gloo rehearsal: host gather, then the same device fusion
-                h.pack_features(staging.data_ptr(), sp)
+                h.pack_features(staging.data_ptr(), bsp)
+                bstream.synchronize()
                 ex.send.copy_(staging.cpu())
                 ex.all_gather()
-                recv_dev.copy_(ex.recv)
-                h.rig_fuse(recv_dev.data_ptr(), world, s * B, B, sp)
+                with torch.cuda.stream(bstream):
+                    recv_dev.copy_(ex.recv)
+                h.rig_fuse(recv_dev.data_ptr(), world, s * B, B, bsp)
 
     def drain() -> None:
         finish_exchange()
 
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_ev + 2)] for _ in range(args.steps)]
+    events = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in names]
+              for _ in range(args.steps)]
     for s in range(args.warmup):
         step(s)
     drain()
@@ -387,8 +409,7 @@ def main() -> None:
     per_kernel_us = {k: 0.0 for k in names}
     for evs in events:
         for i, k in enumerate(names):
-            a, b = (evs[-2], evs[-1]) if k == "local_ba" else (evs[i], evs[i + 1])
-            per_kernel_us[k] += a.elapsed_time(b) * 1e3 / args.steps  # us
+            per_kernel_us[k] += evs[i][0].elapsed_time(evs[i][1]) * 1e3 / args.steps  # us
     unit_bytes = (frame_bytes(rect.width, rect.height, cfg.n_features, n_img=1, channels=5, matchings=1) if c5 else
                   frame_bytes(rect.width, rect.height, cfg.n_features))
     dom_bytes = unit_bytes * B          # §8d per-frame bytes x the frames one launch processes

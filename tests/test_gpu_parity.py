@@ -188,3 +188,38 @@ def test_c4_size_bit_exact():
         if i:
             assert rec["stats"][4] == o["best_hyp"] and rec["stats"][2] == o["n_inliers"]
             assert rel_frobenius(rec["T_abs"], o["world_T_cam"]) < 1e-9
+
+
+def test_two_stream_pipeline_bit_exact():
+    """Front stages (rectify .. describe) on one stream, back stages (match .. pose) on another,
+    so batch s + 1's front overlaps batch s's back (the library orders them with events; the ring
+    keeps 2B + 1 frames): results identical to the oracle."""
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    n, batch = 8, 2
+    sc = scenario(seed=0, n=n)
+    cfg = sc["cfg"]
+    h = Handle([sc["rect"]], cfg, max_batch=batch)
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    fs, bs = torch.cuda.current_stream(), torch.cuda.Stream()
+    for b0 in range(0, n, batch):   # no host synchronisation between batches: they overlap
+        h.begin_batch(dev[b0:].data_ptr(), batch)
+        for st in ("rectify", "detect", "describe"):
+            h.run_stage(st, fs.cuda_stream)
+        for st in ("match", "pose"):
+            h.run_stage(st, bs.cuda_stream)
+        h.end_batch()
+    res = h.read_poses(batch)
+    K = cfg.n_features
+    for g in range(n - 2 * batch, n):   # the frames still in the ring (2B + 1)
+        o = sc["oracle"][g]
+        _check_image_features(o["cur"]["left"], h.keypoints(g, 0), cfg, f"frame {g} left")
+        np.testing.assert_array_equal(h.frame_block("temporal", h.ring_slot(g), np.int32)[:K], o["cur"]["temporal"])
+        np.testing.assert_array_equal(h.frame_block("stereo", h.ring_slot(g), np.int32)[:K], o["cur"]["stereo"])
+    for f in range(batch):
+        o = sc["oracle"][n - batch + f]
+        assert res["stats"][f, 0, 4] == o["best_hyp"] and res["stats"][f, 0, 2] == o["n_inliers"]
+        assert rel_frobenius(res["T_abs"][f, 0], o["world_T_cam"]) < 1e-9
+    h.close()

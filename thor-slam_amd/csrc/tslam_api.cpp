@@ -96,6 +96,12 @@ struct tslam_handle {
     hipStream_t ba_stream = nullptr;
     hipEvent_t ev_fe = nullptr, ev_ba[2] = {nullptr, nullptr};
     bool ba_pending[2] = {false, false};
+    // front (rectify .. describe) and back (match .. chain) stages on two streams: batch s's back
+    // waits for its front; batch s's front waits for the back of batch s - 2 (shared ring slots)
+    hipStream_t front_stream = nullptr, back_stream = nullptr;
+    bool front_started = false, back_started = false;
+    hipEvent_t ev_front = nullptr, ev_back[2] = {nullptr, nullptr};
+    bool back_pending[2] = {false, false};
     std::vector<hipEvent_t> ba_events;
 };
 
@@ -352,7 +358,9 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     h->B = p.max_batch;
     // the ring keeps frame t-1 of a batch's first frame; with BA it also keeps the frames a
     // keyframe's temporal match chain walks back over
-    h->R = 2 * p.max_batch;
+    // the ring keeps frame t-1 of a batch's first frame while the front stages of the next batch
+    // run (front / back on two streams): R = 2B + 1
+    h->R = 2 * p.max_batch + 1;
     // with BA the ring also keeps the frames a keyframe's match chain walks back over, even while
     // the next batch runs (BA may run on its own stream): R = 2B + interval + 1
     if (p.ba_window) h->R = 2 * p.max_batch + p.ba_kf_interval + 1;
@@ -453,7 +461,7 @@ int tslam_destroy(tslam_handle* h) {
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();
     for (hipEvent_t e : h->ba_events) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {h->ev_fe, h->ev_ba[0], h->ev_ba[1]})
+    for (hipEvent_t e : {h->ev_fe, h->ev_ba[0], h->ev_ba[1], h->ev_front, h->ev_back[0], h->ev_back[1]})
         if (e) (void)hipEventDestroy(e);
     free_all(h);
     delete h;
@@ -474,6 +482,7 @@ int tslam_reset(tslam_handle* h) {
     h->ba_nkf = 0;
     h->ba_last = -1;
     h->ba_pending[0] = h->ba_pending[1] = false;
+    h->back_pending[0] = h->back_pending[1] = false;
     h->in_batch = false;
     h->cur_n = 0;
     return TSLAM_OK;
@@ -491,6 +500,8 @@ int tslam_begin_batch(tslam_handle* h, const uint8_t* images, int n_frames) {
     h->cur_g0 = h->frames_done;
     h->in_batch = true;
     h->batch_started = false;
+    h->front_started = h->back_started = false;
+    h->front_stream = h->back_stream = nullptr;
     return TSLAM_OK;
 }
 
@@ -500,6 +511,11 @@ int tslam_end_batch(tslam_handle* h) {
     h->frames_done += h->cur_n;
     h->in_batch = false;
     h->prior_armed = false;   // a prior applies to one batch
+    if (h->back_started && h->front_started && h->back_stream != h->front_stream) {
+        const int par = (int)(h->batch_idx & 1);
+        HIPCHK(hipEventRecord(h->ev_back[par], h->back_stream));
+        h->back_pending[par] = true;
+    }
     h->batch_idx += 1;
     return TSLAM_OK;
 }
@@ -509,15 +525,43 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
     if (!h->in_batch) return fail(TSLAM_ESTATE, "tslam_begin_batch first");
     HIPCHK(hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
-    if (stage != TSLAM_STAGE_BA) {
-        if (!h->batch_started) {   // the first front-end work of a batch: the BA of the batch two
-            const int par = (int)(h->batch_idx & 1);   // back (same ring slots) must have finished
-            if (h->ba_pending[par]) HIPCHK(hipStreamWaitEvent(s, h->ev_ba[par], 0));
-            h->ba_pending[par] = false;
-            h->batch_started = true;
-        }
-        h->last_stream = s;
+    const bool front = stage == TSLAM_STAGE_ALL || stage == TSLAM_STAGE_RECTIFY || stage == TSLAM_STAGE_DETECT ||
+                       stage == TSLAM_STAGE_DESCRIBE || (stage >= TSLAM_KERNEL_RECTIFY_PYRAMID && stage <= TSLAM_KERNEL_DESCRIBE);
+    const bool back = stage == TSLAM_STAGE_ALL || stage == TSLAM_STAGE_MATCH || stage == TSLAM_STAGE_POSE ||
+                      (stage >= TSLAM_KERNEL_MATCH && stage <= TSLAM_KERNEL_RIG);
+    if (!h->ev_front) {
+        HIPCHK(hipEventCreateWithFlags(&h->ev_front, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&h->ev_back[0], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&h->ev_back[1], hipEventDisableTiming));
     }
+    const int par = (int)(h->batch_idx & 1);
+    if (stage != TSLAM_STAGE_BA && !h->batch_started) {
+        // the first work of a batch: the BA of the batch two back (same ring slots) must be done
+        if (h->ba_pending[par]) HIPCHK(hipStreamWaitEvent(s, h->ev_ba[par], 0));
+        h->ba_pending[par] = false;
+        h->batch_started = true;
+    }
+    if (front && !h->front_started) {
+        // ... and so must the back stages of the batch two back (they read the frames whose ring
+        // slots this batch's front stages overwrite)
+        if (h->back_pending[par]) HIPCHK(hipStreamWaitEvent(s, h->ev_back[par], 0));
+        h->back_pending[par] = false;
+        h->front_started = true;
+        h->front_stream = s;
+    }
+    if (back && !h->back_started) {
+        if (h->front_started && h->front_stream != s) {   // this batch's features come from the front stream
+            HIPCHK(hipEventRecord(h->ev_front, h->front_stream));
+            HIPCHK(hipStreamWaitEvent(s, h->ev_front, 0));
+        }
+        h->back_started = true;
+        h->back_stream = s;
+    }
+    if (front && h->front_started && s != h->front_stream && !back)
+        return fail(TSLAM_ESTATE, "all front stages of a batch must use one stream");
+    if (back && h->back_started && s != h->back_stream && !front)
+        return fail(TSLAM_ESTATE, "all back stages of a batch must use one stream");
+    if (stage != TSLAM_STAGE_BA) h->last_stream = s;
     const BatchCtx c = make_ctx(h);
     if (h->prm.rgbd && (stage == TSLAM_STAGE_RECTIFY || stage == TSLAM_STAGE_ALL || stage == TSLAM_KERNEL_RECTIFY_PYRAMID))
         launch_rgbd_gray(c, h->d_gray, s);   // the colour images become the gray input of rectify
