@@ -45,6 +45,8 @@ METRIC = "synced stereo frames/sec (detect+match+pose) @640×400, 1/2/4/8 GPU"
 METRIC_C4 = "synced stereo frames/sec (detect+match+pose+10-keyframe local BA) @1280×800, 1 GPU"
 METRIC_C5 = "RGB-D frames/sec (BGR+depth, detect+match+pose) @1280×720, one camera per GPU, 1/2/4 GPU"
 HBM_PEAK_GBS = 8000.0
+# VALU issue: 256 CUs x 4 SIMD-32, a wave64 instruction every 2 cycles per SIMD at 2.4 GHz
+VALU_PEAK_WINST = 256 * 4 * 2.4e9 / 2
 FP64_MFMA_PEAK_TFS = 78.6   # MI355X FP64 matrix peak (AMD spec; the microarch guide lists no FP64 row)
 # bench kernel label -> device symbol (rocprofv3 / PMC summaries); "pose" is k_corr+k_ransac+k_refine
 KERNEL_SYMBOL = {"rectify_pyramid": "k_rectify_pyramid", "detect": "k_detect", "select": "k_select",
@@ -428,12 +430,20 @@ def main() -> None:
         mfma["frac"] = mfma["achieved"] / mfma["peak"]
 
     traffic = None
+    valu = None
     pmc_path = Path(args.pmc)
     if pmc_path.exists():
         pmc = json.loads(pmc_path.read_text())
         kern = pmc.get("kernels", {}).get(KERNEL_SYMBOL.get(dom, ""), None)
-        if kern is not None and pmc.get("batch_frames") == B:
+        if kern is not None and pmc.get("batch_frames") == B and pmc.get("config", "c2") == args.config:
             traffic = kern["hbm_bytes_per_launch"]
+            if kern.get("valu_insts_per_launch"):
+                # the path is integer-VALU bound: wave64 VALU instructions per launch
+                # (PMC SQ_INSTS_VALU) / the same event-timed duration, against the issue peak
+                rate = kern["valu_insts_per_launch"] / (per_kernel_us[dom] * 1e-6)
+                valu = {"bound": "valu", "achieved": rate / 1e12, "peak": VALU_PEAK_WINST / 1e12,
+                        "unit": "T wave-instructions/s", "frac": rate / VALU_PEAK_WINST,
+                        "insts_per_launch": kern["valu_insts_per_launch"]}
 
     # ---- B = 1 latency: one frame submitted and its pose read back -------------
     lat_ms = None
@@ -465,6 +475,7 @@ def main() -> None:
         "avg_launch_us": per_kernel_us[dom],
         "kernel_own_bytes_per_launch": None if c5 else kernel_bytes(dom, B, h, cfg, rect.is_identity),
         "end_to_end_hbm_frac": unit_bytes * (frames_total / elapsed / world) / (HBM_PEAK_GBS * 1e9),
+        "valu": valu,
     }
     if mfma is not None and mfma["time_per_step_us"] > per_kernel_us[dom]:
         roofline, front_roofline = mfma, roofline   # the Schur product is the step's dominant kernel

@@ -5,7 +5,12 @@ FETCH_SIZE reports half the bytes of a wide coalesced read on gfx950, so
 traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  The doubling is exact only for 16-B/lane streams;
 byte-granular gathers are uncalibrated, so both the raw and the corrected numbers are kept.
 
-usage: python tools/pmc_summary.py FETCH_DIR WRITE_DIR OUT_JSON [--batch B]
+An optional third pass (``--sq DIR``: SQ_INSTS_VALU, SQ_WAVES) adds the VALU wave-instructions
+per launch, the numerator of the VALU-issue roofline in bench.py (peak: 256 CUs x 4 SIMD-32 x
+2.4 GHz / 2 cycles per wave64 instruction = 1.2288e12 wave-instructions/s, MI355X_MICROARCH.md
+"Execution model").
+
+usage: python tools/pmc_summary.py FETCH_DIR WRITE_DIR OUT_JSON [--batch B] [--sq SQ_DIR]
 """
 
 import collections
@@ -15,18 +20,25 @@ import sys
 from pathlib import Path
 
 
-def load(d):
-    rows = list(csv.DictReader(open(Path(d) / "run_counter_collection.csv")))
+def load(d, counter=None):
+    files = sorted(Path(d).rglob("*counter_collection.csv"))
+    if not files:
+        raise SystemExit(f"no *counter_collection.csv under {d}")
+    rows = [r for fp in files for r in csv.DictReader(open(fp))]
     agg = collections.defaultdict(list)
     for r in rows:
-        agg[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
+        if counter is None or r["Counter_Name"] == counter:
+            agg[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
 def main():
     fetch, write, out = sys.argv[1], sys.argv[2], sys.argv[3]
     batch = int(sys.argv[sys.argv.index("--batch") + 1]) if "--batch" in sys.argv else None
+    sq = sys.argv[sys.argv.index("--sq") + 1] if "--sq" in sys.argv else None
     f, w = load(fetch), load(write)
+    valu = load(sq, "SQ_INSTS_VALU") if sq else {}
+    waves = load(sq, "SQ_WAVES") if sq else {}
     res = {}
     for k in sorted(set(f) | set(w)):
         if not k.startswith("k_"):
@@ -34,6 +46,9 @@ def main():
         fk, wk = f.get(k, 0.0), w.get(k, 0.0)
         res[k] = {"FETCH_SIZE_KiB": fk, "WRITE_SIZE_KiB": wk, "hbm_bytes_per_launch": (2 * fk + wk) * 1024.0,
                   "hbm_bytes_per_launch_uncorrected": (fk + wk) * 1024.0}
+        if k in valu:
+            res[k]["valu_insts_per_launch"] = valu[k]
+            res[k]["waves_per_launch"] = waves.get(k)
     Path(out).write_text(json.dumps({"batch_frames": batch, "kernels": res}, indent=1))
     print(json.dumps(res, indent=1))
 
