@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 3
+#define TSLAM_ABI_VERSION 4
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -241,6 +241,34 @@ int tslam_map_upload(tslam_handle* h, const double* xyz, const uint32_t* desc, i
 int tslam_relocalize(tslam_handle* h, int pair, int64_t frame, double* cam_T_world, double* cov, int32_t* stats);
 
 int tslam_pack_features(tslam_handle* h, void* dst, int64_t* bytes, void* stream);
+
+/* Loop closure + keyframe pose graph (the reference only forwards
+ * SlamConfig.enable_loop_closure, thor_slam/slam/interface.py:155-156, to cuVSLAM).  Spec and CPU
+ * restatement: oracle/numpy_loop.py.  All of these synchronise the handle's stream.
+ *
+ * tslam_loop_init: a keyframe database of `max_keyframes` entries (ring: entry = count mod
+ *   max_keyframes) with `signature` (<= 256) descriptors per keyframe for place recognition;
+ *   tslam_reset empties it.
+ * tslam_loop_add_keyframe: store resident `frame` of `pair`: its valid left keypoints with a stereo
+ *   disparity d > 0, in keypoint order, as camera-frame landmarks (z = fx*B/d, x = (u-cx) z/fx,
+ *   y = (v-cy) z/fy; u, v level-0) + rBRIEF-256; returns the entry and its landmark count.
+ * tslam_loop_read_keyframe: copy entry `slot` out (xyz[n][3], desc[n][8]; NULL skips).
+ * tslam_loop_query: votes[j] for entries j < n_candidates: the query entry's first `signature`
+ *   descriptors matched by brute-force Hamming against entry j's (A6 max_hamming + ratio rule).
+ * tslam_loop_verify: cam_q_T_cam_c of resident `frame` against entry `slot`'s landmarks by the
+ *   relocalisation matcher and A7's P3P-RANSAC + Gauss-Newton; stats as tslam_read_poses.
+ * tslam_pose_graph: `iters` Gauss-Newton iterations on nodes world_T_node[n_nodes][16] (in/out,
+ *   node 0 fixed; n_nodes <= 1024) with edges[n_edges][2] = (a, b), meas[n_edges][16] = measured
+ *   T_a^-1 T_b, info[n_edges][36]; residual Log(meas^-1 T_a^-1 T_b) in (rho, phi) order, dense
+ *   normal equations factored by blocked Cholesky (FP64 MFMA trailing updates); *cost = sum of
+ *   e^T info e at the returned poses (cost may be NULL). */
+int tslam_loop_init(tslam_handle* h, int max_keyframes, int signature);
+int tslam_loop_add_keyframe(tslam_handle* h, int pair, int64_t frame, int* slot, int* n_landmarks);
+int tslam_loop_read_keyframe(tslam_handle* h, int slot, double* xyz, uint32_t* desc, int* n);
+int tslam_loop_query(tslam_handle* h, int slot, int n_candidates, int32_t* votes);
+int tslam_loop_verify(tslam_handle* h, int pair, int64_t frame, int slot, double* T_qc, double* cov, int32_t* stats);
+int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_edges, const int32_t* edges,
+                     const double* meas, const double* info, int iters, double* cost);
 
 #ifdef __cplusplus
 }

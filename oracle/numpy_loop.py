@@ -1,0 +1,236 @@
+"""SURVEY.md §8f items 1 + 3 — keyframe pose graph and loop closure, CPU restatement.
+
+TEST INFRASTRUCTURE (see ``oracle/__init__.py``): the checker for ``k_loop.hip`` and
+``k_posegraph.hip``, never imported by the product.  The reference exposes loop closure only as a
+flag (``SlamConfig.enable_loop_closure``, ``thor_slam/slam/interface.py:155-156``) forwarded to
+the closed cuVSLAM node, so this file is the spec and parity against the reference is unpinned
+like rows A2-A8.
+
+Keyframe database (one entry per keyframe, pair 0's rectified left camera):
+
+* landmarks = the valid keypoints of the left image that have a stereo disparity d > 0 (finite),
+  in keypoint order; camera-frame position z = fx*B / d, x = (u - cx) z / fx, y = (v - cy) z / fy
+  with (u, v) the level-0 keypoint position (the A8 insertion formula);
+* signature = the first ``S`` landmarks (keypoints are ordered by level, then by descending FAST
+  score, so these are the strongest level-0 corners with depth).
+
+Place recognition (``vote``): each signature descriptor of the query keyframe is matched against
+a candidate's signature by brute-force Hamming: best = lexicographic min of (distance, index),
+second = min distance over the others; a vote iff best <= max_hamming and (single entry or
+100 * best < ratio_pct * second).  The candidate's score is its vote count.
+
+Geometric verification (``verify``): the query frame's keypoints against the candidate's
+landmarks with the relocalisation matcher and A7's P3P-RANSAC + Gauss-Newton
+(``numpy_map.relocalize``), giving cam_q_T_cam_c.
+
+Pose graph (``optimize``): nodes T_i = world_T_cam_i, edges (i, j, Z_ij, Omega_ij) with
+Z_ij the measured T_i^-1 T_j.  se(3) vectors are xi = (rho, phi) (translation first);
+Exp(xi) = [Exp_SO3(phi), V(phi) rho].  Residual e_ij = Log(Z_ij^-1 T_i^-1 T_j); right
+perturbations T <- T Exp(delta) give
+
+    J_j = Jr^-1(e),    J_i = -Jr^-1(e) Ad(T_j^-1 T_i),    Jr^-1(e) ~ I + ad(e) / 2,
+
+Ad(R, t) = [[R, t^ R], [0, R]], ad(rho, phi) = [[phi^, rho^], [0, phi^]].  Each Gauss-Newton
+iteration assembles H = sum J^T Omega J and g = sum J^T Omega e over the free nodes (node 0 is
+the gauge and stays fixed), solves H delta = -g by Cholesky and applies T_i <- T_i Exp(delta_i).
+The cost is sum e^T Omega e at the returned poses.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from .numpy_map import hamming, relocalize
+from .numpy_slam import level0_coords
+
+# --------------------------------------------------------------------------------------------
+# keyframe database
+# --------------------------------------------------------------------------------------------
+
+
+def keyframe_landmarks(left: dict, disp: np.ndarray, intr) -> dict:
+    """Compacted stereo landmarks of one keyframe: xyz [n][3] (camera frame), desc [n][8] u32,
+    kp [n] (keypoint index)."""
+    fx, fy, cx, cy, fxb = intr
+    kp = left["kp"]
+    K = left["desc"].shape[0]
+    d = np.asarray(disp[:K], dtype=np.float64)
+    ok = np.asarray(left["valid"][:K], dtype=bool) & np.isfinite(d)
+    ok &= np.where(np.isfinite(d), d, 0.0) > 0.0
+    ks = np.nonzero(ok)[0]
+    u, v = level0_coords(kp["x"][ks], kp["y"][ks], kp["level"][ks])
+    z = fxb / d[ks]
+    xyz = np.stack([(u - cx) * z / fx, (v - cy) * z / fy, z], axis=1) if ks.size else np.zeros((0, 3))
+    return {"xyz": xyz, "desc": np.asarray(left["desc"][ks], dtype=np.uint32), "kp": ks}
+
+
+def vote(q_desc: np.ndarray, c_desc: np.ndarray, S: int, max_hamming: int, ratio_pct: int) -> int:
+    """Votes of the query signature (first S of q_desc) against a candidate signature."""
+    q = np.asarray(q_desc[:S], dtype=np.uint32)
+    c = np.asarray(c_desc[:S], dtype=np.uint32)
+    if q.shape[0] == 0 or c.shape[0] == 0:
+        return 0
+    d = hamming(q, c)
+    best = np.argmin(d, axis=1)
+    bd = d[np.arange(q.shape[0]), best]
+    if c.shape[0] > 1:
+        d2 = d.copy()
+        d2[np.arange(q.shape[0]), best] = 1 << 30
+        sd = d2.min(axis=1)
+        ok = (bd <= max_hamming) & (100 * bd < ratio_pct * sd)
+    else:
+        ok = bd <= max_hamming
+    return int(ok.sum())
+
+
+def verify(feat_q: dict, cand: dict, intr4, cfg, frame: int) -> dict:
+    """cam_q_T_cam_c of keyframe q against candidate c's landmarks (relocalisation matcher)."""
+    return relocalize(feat_q, cand["xyz"], cand["desc"], intr4, cfg, frame)
+
+
+# --------------------------------------------------------------------------------------------
+# SE(3) helpers (the formulas k_posegraph.hip follows)
+# --------------------------------------------------------------------------------------------
+
+
+def hat(w: np.ndarray) -> np.ndarray:
+    return np.array([[0.0, -w[2], w[1]], [w[2], 0.0, -w[0]], [-w[1], w[0], 0.0]])
+
+
+def _abc(th2: float):
+    """A = sin t / t, B = (1 - cos t) / t^2 = 2 sin^2(t/2) / t^2, C = (t - sin t) / t^3
+    (four Taylor terms below t^2 = 1e-3, where C's direct form cancels)."""
+    if th2 < 1e-3:
+        t4, t6 = th2 * th2, th2 * th2 * th2
+        return (1.0 - th2 / 6.0 + t4 / 120.0 - t6 / 5040.0, 0.5 - th2 / 24.0 + t4 / 720.0 - t6 / 40320.0,
+                1.0 / 6.0 - th2 / 120.0 + t4 / 5040.0 - t6 / 362880.0)
+    th = np.sqrt(th2)
+    s, h = np.sin(th), np.sin(0.5 * th)
+    return s / th, 2.0 * h * h / th2, (th - s) / (th2 * th)
+
+
+def se3_exp(xi: np.ndarray) -> np.ndarray:
+    rho, phi = xi[:3], xi[3:]
+    th2 = float(phi @ phi)
+    A, B, C = _abc(th2)
+    W = hat(phi)
+    W2 = W @ W
+    T = np.eye(4)
+    T[:3, :3] = np.eye(3) + A * W + B * W2
+    T[:3, 3] = (np.eye(3) + B * W + C * W2) @ rho
+    return T
+
+
+def so3_log(R: np.ndarray) -> np.ndarray:
+    """phi with |phi| < pi: theta = atan2(|v| / 2, (tr R - 1) / 2), v = vee(R - R^T) = 2 sin(theta) axis."""
+    v = np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
+    s = 0.5 * np.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2])
+    c = (R[0, 0] + R[1, 1] + R[2, 2] - 1.0) * 0.5
+    th = np.arctan2(s, c)
+    if th < 1e-5:
+        return v * (0.5 * (1.0 + th * th / 6.0))
+    return v * (th / (2.0 * s))
+
+
+def se3_log(T: np.ndarray) -> np.ndarray:
+    phi = so3_log(T[:3, :3])
+    th2 = float(phi @ phi)
+    W = hat(phi)
+    if th2 < 1e-3:   # k = (1 - A / 2B) / t^2
+        k = 1.0 / 12.0 + th2 / 720.0 + th2 * th2 / 30240.0 + th2 * th2 * th2 / 1209600.0
+    else:
+        A, B, _ = _abc(th2)
+        k = (1.0 - A / (2.0 * B)) / th2
+    Vinv = np.eye(3) - 0.5 * W + k * (W @ W)
+    return np.concatenate([Vinv @ T[:3, 3], phi])
+
+
+def inv_se3(T: np.ndarray) -> np.ndarray:
+    out = np.eye(4)
+    out[:3, :3] = T[:3, :3].T
+    out[:3, 3] = -(T[:3, :3].T @ T[:3, 3])
+    return out
+
+
+def adjoint(T: np.ndarray) -> np.ndarray:
+    R, t = T[:3, :3], T[:3, 3]
+    out = np.zeros((6, 6))
+    out[:3, :3] = R
+    out[:3, 3:] = hat(t) @ R
+    out[3:, 3:] = R
+    return out
+
+
+def jr_inv(e: np.ndarray) -> np.ndarray:
+    ad = np.zeros((6, 6))
+    ad[:3, :3] = hat(e[3:])
+    ad[:3, 3:] = hat(e[:3])
+    ad[3:, 3:] = hat(e[3:])
+    return np.eye(6) + 0.5 * ad
+
+
+def edge_terms(Ti: np.ndarray, Tj: np.ndarray, Z: np.ndarray):
+    """(e, J_i, J_j) of one edge."""
+    Tij = inv_se3(Ti) @ Tj
+    e = se3_log(inv_se3(Z) @ Tij)
+    Jr = jr_inv(e)
+    return e, -Jr @ adjoint(inv_se3(Tij)), Jr
+
+
+def graph_cost(T: np.ndarray, edges: np.ndarray, Z: np.ndarray, info: np.ndarray) -> float:
+    cost = 0.0
+    for k, (i, j) in enumerate(edges):
+        e, _, _ = edge_terms(T[i], T[j], Z[k])
+        cost += float(e @ info[k] @ e)
+    return cost
+
+
+def optimize(T0: np.ndarray, edges: np.ndarray, Z: np.ndarray, info: np.ndarray, iters: int) -> dict:
+    """Gauss-Newton on the pose graph (node 0 fixed); returns poses, cost, per-iteration |delta|."""
+    T = np.array(T0, dtype=np.float64, copy=True)
+    N = T.shape[0]
+    n = 6 * (N - 1)
+    steps = []
+    for _ in range(iters):
+        if n == 0:
+            break
+        H = np.zeros((n, n))
+        g = np.zeros(n)
+        for k, (i, j) in enumerate(edges):
+            e, Ji, Jj = edge_terms(T[i], T[j], Z[k])
+            W = info[k]
+            for (a, Ja) in ((i, Ji), (j, Jj)):
+                if a == 0:
+                    continue
+                ra = 6 * (a - 1)
+                g[ra:ra + 6] += Ja.T @ W @ e
+                for (b, Jb) in ((i, Ji), (j, Jj)):
+                    if b == 0:
+                        continue
+                    rb = 6 * (b - 1)
+                    H[ra:ra + 6, rb:rb + 6] += Ja.T @ W @ Jb
+        L = np.linalg.cholesky(H)
+        y = np.linalg.solve(L, -g)
+        delta = np.linalg.solve(L.T, y)
+        for a in range(1, N):
+            T[a] = T[a] @ se3_exp(delta[6 * (a - 1):6 * a])
+        steps.append(float(np.abs(delta).max()))
+    return {"T": T, "cost": graph_cost(T, edges, Z, info), "steps": steps}
+
+
+# --------------------------------------------------------------------------------------------
+# the engine's loop-closure policy, restated (HipSlamEngine loop closure follows it)
+# --------------------------------------------------------------------------------------------
+
+
+def loop_information(sigma_t: float, sigma_r: float) -> np.ndarray:
+    return np.diag([1.0 / sigma_t ** 2] * 3 + [1.0 / sigma_r ** 2] * 3)
+
+
+def best_candidate(votes: np.ndarray, n_allowed: int, min_votes: int) -> int:
+    """Highest vote among slots [0, n_allowed), ties to the oldest; -1 below min_votes."""
+    if n_allowed <= 0:
+        return -1
+    v = np.asarray(votes[:n_allowed])
+    j = int(np.argmax(v))
+    return j if v[j] >= min_votes else -1

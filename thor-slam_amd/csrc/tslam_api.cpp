@@ -70,6 +70,19 @@ struct tslam_handle {
     double* d_rl_pose = nullptr;
     double* d_rl_ransac = nullptr;
     int64_t* d_wedges = nullptr;
+    // loop closure (tslam_loop_*): keyframe database, one entry per keyframe, slot = count mod cap
+    int lp_cap = 0, lp_S = 0;
+    int64_t lp_count = 0;
+    double* d_lp_xyz = nullptr;      // [cap][K][3] camera-frame landmarks (compacted)
+    uint32_t* d_lp_desc = nullptr;   // [cap][K][8]
+    int32_t* d_lp_n = nullptr;       // [cap]
+    int32_t* d_lp_votes = nullptr;   // [cap]
+    std::vector<int32_t> lp_n;       // host mirror of d_lp_n
+    // pose graph (tslam_pose_graph) scratch, grown on demand
+    int pg_nodes = 0, pg_edges = 0, pg_np = 0;
+    double *d_pg_T = nullptr, *d_pg_Z = nullptr, *d_pg_info = nullptr, *d_pg_terms = nullptr;
+    double *d_pg_H = nullptr, *d_pg_g = nullptr, *d_pg_delta = nullptr;
+    int32_t *d_pg_edges = nullptr, *d_pg_adj_off = nullptr, *d_pg_adj = nullptr;
     Buffer buf[TSLAM_BUF_COUNT];
     uint32_t* d_cand = nullptr;
     uint32_t* d_ccount = nullptr;
@@ -112,6 +125,16 @@ static int dev_alloc(tslam_handle* h, void** p, size_t bytes) {
     h->allocs.push_back(*p);
     HIPCHK(hipMemset(*p, 0, bytes));
     return TSLAM_OK;
+}
+
+// release *p (if any) and allocate `bytes` fresh (zeroed)
+static int dev_realloc(tslam_handle* h, void** p, size_t bytes) {
+    if (*p) {
+        (void)hipFree(*p);
+        h->allocs.erase(std::remove(h->allocs.begin(), h->allocs.end(), *p), h->allocs.end());
+        *p = nullptr;
+    }
+    return dev_alloc(h, p, bytes);
 }
 
 static void free_all(tslam_handle* h) {
@@ -481,6 +504,8 @@ int tslam_reset(tslam_handle* h) {
     for (int i = 0; i < TS_BA_MAXW; ++i) h->ba_frame[i] = -1;
     h->ba_nkf = 0;
     h->ba_last = -1;
+    h->lp_count = 0;   // the keyframe database belongs to the session
+    std::fill(h->lp_n.begin(), h->lp_n.end(), 0);
     h->ba_pending[0] = h->ba_pending[1] = false;
     h->back_pending[0] = h->back_pending[1] = false;
     h->in_batch = false;
@@ -862,6 +887,45 @@ int tslam_ba_read_map(tslam_handle* h, int pair, int64_t* gid, uint32_t* desc) {
     return TSLAM_OK;
 }
 
+static int ensure_reloc_scratch(tslam_handle* h) {
+    if (h->d_rl_match) return TSLAM_OK;
+    const size_t K = h->g.K;
+    int rc = dev_alloc(h, (void**)&h->d_rl_match, sizeof(int32_t) * K);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_corr, sizeof(double) * TS_CORR_DOUBLES * K);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_stats, sizeof(int32_t) * TS_STATS_INTS);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_pose, sizeof(double) * TS_POSE_DOUBLES);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_ransac, sizeof(uint32_t) * TS_RANSAC_WORDS * TS_MAX_SPLITS);
+    return rc;
+}
+
+// reloc-path solve of `frame` (pair) against M landmarks; result copied to the host
+static int reloc_solve(tslam_handle* h, int pair, int64_t frame, const double* map_xyz, const uint32_t* map_desc,
+                       int64_t M, double* T_out, double* cov, int32_t* stats) {
+    const BatchCtx c = make_ctx(h);
+    hipStream_t s = h->last_stream;
+    if (M == 0) {
+        const int32_t st[8] = {1, 0, 0, 0, -1, (int32_t)frame, 0, 0};
+        HIPCHK(hipMemcpy(h->d_rl_stats, st, sizeof(st), hipMemcpyHostToDevice));
+    } else {
+        launch_reloc(c, pair, frame, map_xyz, map_desc, (int)M, h->d_rl_match, h->d_rl_corr, h->d_rl_stats,
+                     h->d_rl_pose, h->d_rl_ransac, s);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    double pose[TS_POSE_DOUBLES];
+    HIPCHK(hipMemcpy(pose, h->d_rl_pose, sizeof(pose), hipMemcpyDeviceToHost));
+    int32_t st[TS_STATS_INTS];
+    HIPCHK(hipMemcpy(st, h->d_rl_stats, sizeof(st), hipMemcpyDeviceToHost));
+    if (M == 0 || st[0] != 0)
+        for (int i = 0; i < 16; ++i) pose[i] = (i % 5) == 0 ? 1.0 : 0.0;
+    pose[12] = pose[13] = pose[14] = 0.0;   // k_refine writes the 3x4 part only
+    pose[15] = 1.0;
+    if (T_out) memcpy(T_out, pose, 16 * sizeof(double));
+    if (cov) memcpy(cov, pose + 32, 36 * sizeof(double));
+    if (stats) memcpy(stats, st, sizeof(st));
+    return TSLAM_OK;
+}
+
 int tslam_map_upload(tslam_handle* h, const double* xyz, const uint32_t* desc, int64_t n) {
     if (!h || n < 0 || (n && (!xyz || !desc))) return fail(TSLAM_EINVAL, "bad argument");
     if (n > (1 << 20) - 1) return fail(TSLAM_EINVAL, "at most 2^20 - 1 map points");
@@ -879,13 +943,8 @@ int tslam_map_upload(tslam_handle* h, const double* xyz, const uint32_t* desc, i
         if (rc != TSLAM_OK) return rc;
         h->map_cap = n;
     }
-    if (!h->d_rl_match) {
-        const size_t K = h->g.K;
-        int rc = dev_alloc(h, (void**)&h->d_rl_match, sizeof(int32_t) * K);
-        if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_corr, sizeof(double) * TS_CORR_DOUBLES * K);
-        if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_stats, sizeof(int32_t) * TS_STATS_INTS);
-        if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_pose, sizeof(double) * TS_POSE_DOUBLES);
-        if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_ransac, sizeof(uint32_t) * TS_RANSAC_WORDS * TS_MAX_SPLITS);
+    {
+        int rc = ensure_reloc_scratch(h);
         if (rc != TSLAM_OK) return rc;
     }
     if (n) {
@@ -903,28 +962,171 @@ int tslam_relocalize(tslam_handle* h, int pair, int64_t frame, double* cam_T_wor
     if (frame < 0 || frame >= h->frames_done || frame < h->frames_done - h->R)
         return fail(TSLAM_EINVAL, "frame is not resident in the ring");
     HIPCHK(hipSetDevice(h->device));
+    return reloc_solve(h, pair, frame, h->d_map_xyz, h->d_map_desc, h->map_n, cam_T_world, cov, stats);
+}
+
+// -- loop closure: keyframe database, place recognition, verification, pose graph ---------------
+int tslam_loop_init(tslam_handle* h, int max_keyframes, int signature) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (max_keyframes < 1 || max_keyframes > (1 << 16)) return fail(TSLAM_EINVAL, "max_keyframes must be in [1, 65536]");
+    if (signature < 1 || signature > 256) return fail(TSLAM_EINVAL, "signature must be in [1, 256]");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    const size_t K = h->g.K, cap = max_keyframes;
+    int rc = dev_realloc(h, (void**)&h->d_lp_xyz, sizeof(double) * 3 * K * cap);
+    if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_lp_desc, sizeof(uint32_t) * 8 * K * cap);
+    if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_lp_n, sizeof(int32_t) * cap);
+    if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_lp_votes, sizeof(int32_t) * cap);
+    if (rc == TSLAM_OK) rc = ensure_reloc_scratch(h);
+    if (rc != TSLAM_OK) return rc;
+    h->lp_cap = max_keyframes;
+    h->lp_S = signature;
+    h->lp_count = 0;
+    h->lp_n.assign(cap, 0);
+    return TSLAM_OK;
+}
+
+int tslam_loop_add_keyframe(tslam_handle* h, int pair, int64_t frame, int* slot, int* n_landmarks) {
+    if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
+    if (!h->lp_cap) return fail(TSLAM_ESTATE, "loop database not initialised (tslam_loop_init)");
+    if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_loop_add_keyframe inside a batch");
+    if (frame < 0 || frame >= h->frames_done || frame < h->frames_done - h->R)
+        return fail(TSLAM_EINVAL, "frame is not resident in the ring");
+    HIPCHK(hipSetDevice(h->device));
+    const int sl = (int)(h->lp_count % h->lp_cap);
+    const size_t K = h->g.K;
     const BatchCtx c = make_ctx(h);
     hipStream_t s = h->last_stream;
-    if (h->map_n == 0) {
-        const int32_t st[8] = {1, 0, 0, 0, -1, (int32_t)frame, 0, 0};
-        HIPCHK(hipMemcpy(h->d_rl_stats, st, sizeof(st), hipMemcpyHostToDevice));
-    } else {
-        launch_reloc(c, pair, frame, h->d_map_xyz, h->d_map_desc, (int)h->map_n, h->d_rl_match, h->d_rl_corr,
-                     h->d_rl_stats, h->d_rl_pose, h->d_rl_ransac, s);
-        HIPCHK(hipGetLastError());
-    }
+    launch_loop_store(c, pair, frame, h->d_lp_xyz + (size_t)sl * K * 3, h->d_lp_desc + (size_t)sl * K * 8, h->d_lp_n + sl, s);
+    HIPCHK(hipGetLastError());
+    int32_t n = 0;
+    HIPCHK(hipMemcpyAsync(&n, h->d_lp_n + sl, sizeof(n), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    double pose[TS_POSE_DOUBLES];
-    HIPCHK(hipMemcpy(pose, h->d_rl_pose, sizeof(pose), hipMemcpyDeviceToHost));
-    int32_t st[TS_STATS_INTS];
-    HIPCHK(hipMemcpy(st, h->d_rl_stats, sizeof(st), hipMemcpyDeviceToHost));
-    if (h->map_n == 0 || st[0] != 0)
-        for (int i = 0; i < 16; ++i) pose[i] = (i % 5) == 0 ? 1.0 : 0.0;
-    pose[12] = pose[13] = pose[14] = 0.0;   // k_refine writes the 3x4 part only
-    pose[15] = 1.0;
-    if (cam_T_world) memcpy(cam_T_world, pose, 16 * sizeof(double));
-    if (cov) memcpy(cov, pose + 32, 36 * sizeof(double));
-    if (stats) memcpy(stats, st, sizeof(st));
+    h->lp_n[sl] = n;
+    ++h->lp_count;
+    if (slot) *slot = sl;
+    if (n_landmarks) *n_landmarks = n;
+    return TSLAM_OK;
+}
+
+int tslam_loop_read_keyframe(tslam_handle* h, int slot, double* xyz, uint32_t* desc, int* n) {
+    if (!h || !h->lp_cap) return fail(TSLAM_ESTATE, "loop database not initialised (tslam_loop_init)");
+    if (slot < 0 || slot >= h->lp_cap) return fail(TSLAM_EINVAL, "slot out of range");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipStreamSynchronize(h->last_stream));
+    const size_t K = h->g.K, m = h->lp_n[slot];
+    if (xyz && m) HIPCHK(hipMemcpy(xyz, h->d_lp_xyz + (size_t)slot * K * 3, sizeof(double) * 3 * m, hipMemcpyDeviceToHost));
+    if (desc && m) HIPCHK(hipMemcpy(desc, h->d_lp_desc + (size_t)slot * K * 8, sizeof(uint32_t) * 8 * m, hipMemcpyDeviceToHost));
+    if (n) *n = (int)m;
+    return TSLAM_OK;
+}
+
+int tslam_loop_query(tslam_handle* h, int slot, int n_candidates, int32_t* votes) {
+    if (!h || !h->lp_cap) return fail(TSLAM_ESTATE, "loop database not initialised (tslam_loop_init)");
+    if (slot < 0 || slot >= h->lp_cap) return fail(TSLAM_EINVAL, "slot out of range");
+    if (n_candidates < 0 || n_candidates > h->lp_cap) return fail(TSLAM_EINVAL, "n_candidates out of range");
+    if (n_candidates == 0) return TSLAM_OK;
+    HIPCHK(hipSetDevice(h->device));
+    hipStream_t s = h->last_stream;
+    launch_loop_vote(h->d_lp_desc, h->d_lp_n, h->g.K, h->lp_S, slot, n_candidates, h->prm.max_hamming, h->prm.ratio_pct,
+                     h->d_lp_votes, s);
+    HIPCHK(hipGetLastError());
+    if (votes) HIPCHK(hipMemcpyAsync(votes, h->d_lp_votes, sizeof(int32_t) * n_candidates, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return TSLAM_OK;
+}
+
+int tslam_loop_verify(tslam_handle* h, int pair, int64_t frame, int slot, double* T_qc, double* cov, int32_t* stats) {
+    if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
+    if (!h->lp_cap) return fail(TSLAM_ESTATE, "loop database not initialised (tslam_loop_init)");
+    if (slot < 0 || slot >= h->lp_cap) return fail(TSLAM_EINVAL, "slot out of range");
+    if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_loop_verify inside a batch");
+    if (frame < 0 || frame >= h->frames_done || frame < h->frames_done - h->R)
+        return fail(TSLAM_EINVAL, "frame is not resident in the ring");
+    HIPCHK(hipSetDevice(h->device));
+    const size_t K = h->g.K;
+    return reloc_solve(h, pair, frame, h->d_lp_xyz + (size_t)slot * K * 3, h->d_lp_desc + (size_t)slot * K * 8,
+                       h->lp_n[slot], T_qc, cov, stats);
+}
+
+int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_edges, const int32_t* edges,
+                     const double* meas, const double* info, int iters, double* cost) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (n_nodes < 1 || n_nodes > 1024) return fail(TSLAM_EINVAL, "n_nodes must be in [1, 1024]");
+    if (n_edges < 0 || (n_edges && (!edges || !meas || !info)) || !world_T_node || iters < 0)
+        return fail(TSLAM_EINVAL, "bad argument");
+    // incident-edge lists (CSR, by edge index) of every node; every free node needs an edge
+    std::vector<int32_t> off(n_nodes + 1, 0), adj(2 * (size_t)n_edges);
+    for (int k = 0; k < n_edges; ++k) {
+        const int a = edges[2 * k], b = edges[2 * k + 1];
+        if (a < 0 || a >= n_nodes || b < 0 || b >= n_nodes || a == b) return fail(TSLAM_EINVAL, "bad edge");
+        ++off[a + 1];
+        ++off[b + 1];
+    }
+    for (int i = 0; i < n_nodes; ++i) off[i + 1] += off[i];
+    {
+        std::vector<int32_t> fill(off.begin(), off.end() - 1);
+        for (int k = 0; k < n_edges; ++k) {
+            adj[fill[edges[2 * k]]++] = (k << 1);
+            adj[fill[edges[2 * k + 1]]++] = (k << 1) | 1;
+        }
+    }
+    for (int i = 1; i < n_nodes; ++i)
+        if (off[i + 1] == off[i]) return fail(TSLAM_EINVAL, "a free node has no edge");
+    HIPCHK(hipSetDevice(h->device));
+    const int n = 6 * (n_nodes - 1), np = (n + 31) / 32 * 32;
+    int rc = TSLAM_OK;
+    if (n_nodes > h->pg_nodes) {
+        rc = dev_realloc(h, (void**)&h->d_pg_T, sizeof(double) * 16 * n_nodes);
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_adj_off, sizeof(int32_t) * (n_nodes + 1));
+        if (rc != TSLAM_OK) return rc;
+        h->pg_nodes = n_nodes;
+    }
+    if (n_edges > h->pg_edges) {
+        rc = dev_realloc(h, (void**)&h->d_pg_Z, sizeof(double) * 16 * n_edges);
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_info, sizeof(double) * 36 * n_edges);
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_terms, sizeof(double) * 128 * n_edges);
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_edges, sizeof(int32_t) * 2 * n_edges);
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_adj, sizeof(int32_t) * 2 * n_edges);
+        if (rc != TSLAM_OK) return rc;
+        h->pg_edges = n_edges;
+    }
+    if (np > h->pg_np) {
+        rc = dev_realloc(h, (void**)&h->d_pg_H, sizeof(double) * (size_t)np * np);
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_g, sizeof(double) * np);
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_delta, sizeof(double) * np);
+        if (rc != TSLAM_OK) return rc;
+        h->pg_np = np;
+    }
+    hipStream_t s = h->last_stream;
+    HIPCHK(hipMemcpyAsync(h->d_pg_T, world_T_node, sizeof(double) * 16 * n_nodes, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(h->d_pg_adj_off, off.data(), sizeof(int32_t) * (n_nodes + 1), hipMemcpyHostToDevice, s));
+    if (n_edges) {
+        HIPCHK(hipMemcpyAsync(h->d_pg_Z, meas, sizeof(double) * 16 * n_edges, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(h->d_pg_info, info, sizeof(double) * 36 * n_edges, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(h->d_pg_edges, edges, sizeof(int32_t) * 2 * n_edges, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(h->d_pg_adj, adj.data(), sizeof(int32_t) * 2 * n_edges, hipMemcpyHostToDevice, s));
+    }
+    if (n > 0)
+        for (int it = 0; it < iters; ++it)
+            launch_pose_graph_iteration(h->d_pg_T, h->d_pg_edges, h->d_pg_Z, h->d_pg_info, n_nodes, n_edges, h->d_pg_adj_off,
+                                        h->d_pg_adj, h->d_pg_terms, h->d_pg_H, h->d_pg_g, h->d_pg_delta, s);
+    std::vector<double> terms;
+    if (cost && n_edges) {
+        launch_pose_graph_cost(h->d_pg_T, h->d_pg_edges, h->d_pg_Z, h->d_pg_info, n_edges, h->d_pg_terms, s);
+        terms.resize((size_t)128 * n_edges);
+        HIPCHK(hipMemcpyAsync(terms.data(), h->d_pg_terms, sizeof(double) * terms.size(), hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(world_T_node, h->d_pg_T, sizeof(double) * 16 * n_nodes, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (cost) {
+        double cs = 0.0;
+        for (int k = 0; k < n_edges; ++k) cs += terms[(size_t)128 * k + 120];
+        *cost = cs;
+    }
+    for (int i = 0; i < 16 * n_nodes; ++i)
+        if (!std::isfinite(world_T_node[i])) return fail(TSLAM_ESTATE, "pose graph: normal matrix not positive definite");
     return TSLAM_OK;
 }
 

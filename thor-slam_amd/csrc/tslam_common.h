@@ -144,6 +144,15 @@ void launch_rig_fuse(const BatchCtx& c, const uint8_t* gathered, int64_t rank_by
 void launch_pose_solve(const BatchCtx& c, hipStream_t s);
 void launch_reloc(const BatchCtx& c, int pair, int64_t frame, const double* map_xyz, const uint32_t* map_desc, int M,
                   int32_t* match, double* corr, int32_t* stats, double* pose, double* ransac, hipStream_t s);
+void launch_loop_store(const BatchCtx& c, int pair, int64_t frame, double* xyz, uint32_t* desc, int32_t* n_out,
+                       hipStream_t s);
+void launch_loop_vote(const uint32_t* db_desc, const int32_t* db_n, int K, int S, int q_slot, int n_cand,
+                      int max_hamming, int ratio_pct, int32_t* votes, hipStream_t s);
+void launch_pose_graph_iteration(double* T, const int32_t* edges, const double* Z, const double* info, int N, int E,
+                                 const int32_t* adj_off, const int32_t* adj, double* terms, double* H, double* g,
+                                 double* delta, hipStream_t s);
+void launch_pose_graph_cost(const double* T, const int32_t* edges, const double* Z, const double* info, int E,
+                            double* terms, hipStream_t s);
 void launch_rgbd_gray(const BatchCtx& c, uint8_t* gray, hipStream_t s);
 void launch_rgbd_depth(const BatchCtx& c, hipStream_t s);
 

@@ -95,6 +95,15 @@ _SIGNATURES = {
     "tslam_ba_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6),
     "tslam_ba_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
+    "tslam_loop_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "tslam_loop_add_keyframe": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
+                                               ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "tslam_loop_read_keyframe": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.POINTER(ctypes.c_int)]),
+    "tslam_loop_query": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    "tslam_loop_verify": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int] + [ctypes.c_void_p] * 3),
+    "tslam_pose_graph": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
 }
 
 
@@ -347,6 +356,50 @@ class Handle:
         st = np.zeros(8, dtype=np.int32)
         _check(self.lib.tslam_relocalize(self.h, int(pair), int(frame), T.ctypes.data, cov.ctypes.data, st.ctypes.data))
         return {"T": T, "cov": cov, "stats": st}
+
+    # -- loop closure + pose graph --------------------------------
+    def loop_init(self, max_keyframes: int = 1024, signature: int = 256) -> None:
+        _check(self.lib.tslam_loop_init(self.h, int(max_keyframes), int(signature)))
+
+    def loop_add_keyframe(self, frame: int, pair: int = 0) -> tuple[int, int]:
+        """Store a resident frame's stereo landmarks in the keyframe database -> (entry, landmarks)."""
+        slot, n = ctypes.c_int(), ctypes.c_int()
+        _check(self.lib.tslam_loop_add_keyframe(self.h, int(pair), int(frame), ctypes.byref(slot), ctypes.byref(n)))
+        return int(slot.value), int(n.value)
+
+    def loop_read_keyframe(self, slot: int) -> dict:
+        n = ctypes.c_int()
+        _check(self.lib.tslam_loop_read_keyframe(self.h, int(slot), None, None, ctypes.byref(n)))
+        xyz = np.zeros((max(n.value, 1), 3))
+        desc = np.zeros((max(n.value, 1), 8), dtype=np.uint32)
+        _check(self.lib.tslam_loop_read_keyframe(self.h, int(slot), xyz.ctypes.data, desc.ctypes.data, ctypes.byref(n)))
+        return {"xyz": xyz[:n.value], "desc": desc[:n.value]}
+
+    def loop_query(self, slot: int, n_candidates: int) -> np.ndarray:
+        """Place-recognition votes of entry ``slot`` against entries [0, n_candidates)."""
+        votes = np.zeros(max(int(n_candidates), 1), dtype=np.int32)
+        _check(self.lib.tslam_loop_query(self.h, int(slot), int(n_candidates), votes.ctypes.data))
+        return votes[:int(n_candidates)]
+
+    def loop_verify(self, frame: int, slot: int, pair: int = 0) -> dict:
+        """cam_q_T_cam_c of a resident frame against a database entry (synchronises)."""
+        T = np.zeros((4, 4))
+        cov = np.zeros((6, 6))
+        st = np.zeros(8, dtype=np.int32)
+        _check(self.lib.tslam_loop_verify(self.h, int(pair), int(frame), int(slot), T.ctypes.data, cov.ctypes.data,
+                                          st.ctypes.data))
+        return {"T": T, "cov": cov, "stats": st}
+
+    def pose_graph(self, T: np.ndarray, edges: np.ndarray, meas: np.ndarray, info: np.ndarray, iters: int) -> dict:
+        """Gauss-Newton on a keyframe pose graph (node 0 fixed) on the device -> poses, cost."""
+        T = np.ascontiguousarray(np.array(T, dtype=np.float64).reshape(-1, 4, 4))
+        edges = np.ascontiguousarray(np.asarray(edges, dtype=np.int32).reshape(-1, 2))
+        meas = np.ascontiguousarray(np.asarray(meas, dtype=np.float64).reshape(-1, 4, 4))
+        info = np.ascontiguousarray(np.asarray(info, dtype=np.float64).reshape(-1, 6, 6))
+        cost = ctypes.c_double()
+        _check(self.lib.tslam_pose_graph(self.h, int(T.shape[0]), T.ctypes.data, int(edges.shape[0]), edges.ctypes.data,
+                                         meas.ctypes.data, info.ctypes.data, int(iters), ctypes.byref(cost)))
+        return {"T": T, "cost": cost.value}
 
     def ba_profile(self, max_launches: int = 0) -> dict:
         """Schur-kernel HIP-event time / launches / algorithmic flops since the last call; re-arms

@@ -48,6 +48,17 @@ class HipSlamConfig(SlamConfig):
     # IMU fusion: gyro-predicted rotation prior in the pose Gauss-Newton
     imu_fusion: bool = False
     imu_rot_sigma: float = 2e-3     # rad, std of the per-frame gyro rotation prediction (1 px = 1 unit)
+    # loop closure + keyframe pose graph; on when the reference's
+    # SlamConfig.enable_loop_closure is (interface.py:155-156; single stereo pair / RGB-D camera)
+    loop_kf_interval: int = 5       # frame g is a loop-closure keyframe iff g % loop_kf_interval == 0
+    loop_max_keyframes: int = 1024  # keyframe database entries (= pose-graph nodes)
+    loop_signature: int = 256       # place-recognition descriptors per keyframe
+    loop_min_gap: int = 20          # candidates are at least this many keyframes older
+    loop_min_votes: int = 40        # signature votes a candidate needs
+    loop_min_inliers: int = 40      # verified RANSAC inliers a loop edge needs
+    pg_iters: int = 8               # Gauss-Newton iterations per pose-graph solve
+    pg_sigma_t: float = 0.01        # m, std of an edge's translation
+    pg_sigma_r: float = 0.005       # rad, std of an edge's rotation
     # input kind: RGB-D (BASELINE configs[4]) = per source a colour camera (cam_idx 0, BGR) and a
     # depth image aligned to it (cam_idx 1, u16 mm); depth replaces stereo matching
     rgbd: bool = False
@@ -71,6 +82,8 @@ class HipSlamConfig(SlamConfig):
             raise ValueError("ba_window must be 0 (off) or in [2, 10]")
         if self.ba_kf_interval < 1 or self.ba_iters < 1:
             raise ValueError("ba_kf_interval and ba_iters must be >= 1")
+        if not (1 <= self.loop_max_keyframes <= 1024 and 1 <= self.loop_signature <= 256 and self.loop_kf_interval >= 1):
+            raise ValueError("loop_max_keyframes must be in [1, 1024], loop_signature in [1, 256], loop_kf_interval >= 1")
         if not 0 <= self.max_hamming <= 253:
             raise ValueError("max_hamming must be in [0, 253] (the mutual check keeps distances as bytes)")
 

@@ -64,6 +64,28 @@ def _invert(t: np.ndarray) -> np.ndarray:
     return out
 
 
+class _LoopGraph:
+    """Host side of loop closure: keyframe nodes (rect-left world_T_cam), edges, and the
+    correction applied to poses after the last solve (corrected = corr @ raw)."""
+
+    def __init__(self) -> None:
+        self.frames: list[int] = []
+        self.stamps: list[float] = []
+        self.raw: list[np.ndarray] = []     # pose at insertion, before loop correction
+        self.T: list[np.ndarray] = []       # current (optimised) node poses
+        self.edges: list[tuple[int, int]] = []
+        self.meas: list[np.ndarray] = []
+        self.info: list[np.ndarray] = []
+        self.loops: list[tuple[int, int, int]] = []
+        self.corr = np.eye(4)
+        self.cost = 0.0
+        self.full = False
+
+    @staticmethod
+    def information(cfg) -> np.ndarray:
+        return np.diag([1.0 / cfg.pg_sigma_t ** 2] * 3 + [1.0 / cfg.pg_sigma_r ** 2] * 3)
+
+
 class HipSlamEngine(SlamEngine):
     """Stereo visual odometry front end (detect -> match -> pose) running on one MI355X."""
 
@@ -95,6 +117,7 @@ class HipSlamEngine(SlamEngine):
         self._map_points: dict[int, tuple] = {}   # global landmark id -> (xyz rect-0 frame, desc, observations)
         self._map_offset = np.eye(4)              # map world <- session world, set by relocalize()
         self._map_loaded = False
+        self._loop: _LoopGraph | None = None     # set up by initialize() when loop closure is on
 
     # ------------------------------------------------------------------------------------------
     def initialize(self, calibration: RigCalibration, config: SlamConfig | None = None) -> None:
@@ -136,6 +159,13 @@ class HipSlamEngine(SlamEngine):
             self._base_R_imu = imu.to_4x4_matrix()[:3, :3] if imu is not None else np.eye(3)
             if len(self._pairs) > 1:   # the rig's body motion is solved on the device from all pairs
                 self._handle.set_rig(self._base_T_rects)
+            self._loop = None
+            if cfg.enable_loop_closure:
+                if len(self._pairs) == 1:
+                    self._handle.loop_init(cfg.loop_max_keyframes, cfg.loop_signature)
+                    self._loop = _LoopGraph()
+                else:
+                    logger.warning("loop closure runs on single-pair rigs only; disabled for %d pairs", len(self._pairs))
         except RuntimeError:
             raise
         except Exception as exc:  # per interface.py:187-188
@@ -318,6 +348,12 @@ class HipSlamEngine(SlamEngine):
             status, body, cov = self._body_pose(res, k)
             if corr is not None and status != POSE_LOST:
                 body = bt @ corr[k] @ res["T_abs"][k, 0] @ _invert(bt)
+            if self._loop is not None and status != POSE_LOST:
+                g = self._handle.frames_done - len(stamps) + k
+                raw = _invert(bt) @ body @ bt                      # rect-left world_T_cam before loop correction
+                if status == POSE_OK and g % self._config.loop_kf_interval == 0:
+                    self._loop_keyframe(g, raw, ts)
+                body = bt @ self._loop.corr @ raw @ _invert(bt)
             body = self._map_offset @ body
             if status == POSE_LOST:
                 state = TrackingState.LOST
@@ -342,6 +378,68 @@ class HipSlamEngine(SlamEngine):
             self._state = state
         self._last_result = res
 
+    # -- loop closure + keyframe pose graph ---------------------------
+    def _loop_keyframe(self, g: int, raw: np.ndarray, ts: float) -> None:
+        """Keyframe g: store it in the device database, add its odometry edge, look for a loop
+        among the keyframes at least ``loop_min_gap`` older (signature votes, then RANSAC
+        verification) and, on a verified loop, re-solve the pose graph on the device."""
+        cfg, lp, h = self._config, self._loop, self._handle
+        idx = len(lp.frames)
+        if idx >= cfg.loop_max_keyframes:
+            if not lp.full:
+                logger.warning("loop closure: keyframe database full (%d); no further keyframes", idx)
+                lp.full = True
+            return
+        slot, _ = h.loop_add_keyframe(g)
+        assert slot == idx
+        info = lp.information(cfg)
+        if idx == 0:
+            T = lp.corr @ raw
+        else:
+            Z = _invert(lp.raw[-1]) @ raw
+            T = lp.T[-1] @ Z
+            lp.edges.append((idx - 1, idx))
+            lp.meas.append(Z)
+            lp.info.append(info)
+        lp.frames.append(g)
+        lp.stamps.append(ts)
+        lp.raw.append(raw.copy())
+        lp.T.append(T)
+        n_allowed = idx - cfg.loop_min_gap + 1
+        if n_allowed <= 0:
+            return
+        votes = h.loop_query(slot, n_allowed)
+        j = int(np.argmax(votes))
+        if votes[j] < cfg.loop_min_votes:
+            return
+        ver = h.loop_verify(g, j)
+        if int(ver["stats"][0]) != POSE_OK or int(ver["stats"][2]) < cfg.loop_min_inliers:
+            return
+        lp.edges.append((j, idx))
+        lp.meas.append(_invert(ver["T"]))     # T_c^-1 T_q = inv(cam_q_T_cam_c)
+        lp.info.append(info)
+        lp.loops.append((lp.frames[j], g, int(ver["stats"][2])))
+        sol = h.pose_graph(np.stack(lp.T), np.array(lp.edges), np.stack(lp.meas), np.stack(lp.info), cfg.pg_iters)
+        lp.T = list(sol["T"])
+        lp.cost = sol["cost"]
+        lp.corr = lp.T[-1] @ _invert(raw)
+        logger.info("loop closure: keyframe %d -> %d (%d inliers), pose graph cost %.3g", lp.frames[j], g,
+                    int(ver["stats"][2]), sol["cost"])
+
+    @property
+    def loop_closures(self) -> list[tuple[int, int, int]]:
+        """Verified loops so far: (older keyframe frame, newer keyframe frame, inliers)."""
+        return list(self._loop.loops) if self._loop is not None else []
+
+    @property
+    def pose_graph(self) -> dict | None:
+        """The keyframe pose graph: frames, world_T_cam (rect-left) per node, edges (a, b)."""
+        if self._loop is None:
+            return None
+        lp = self._loop
+        return {"frames": list(lp.frames), "T": np.array(lp.T).reshape(-1, 4, 4), "edges": list(lp.edges),
+                "meas": [m.copy() for m in lp.meas], "cost": lp.cost}
+
     # ------------------------------------------------------------------------------------------
     def get_tracking_state(self) -> TrackingState:
         return self._state
@@ -350,7 +448,15 @@ class HipSlamEngine(SlamEngine):
         """Without BA: the (re)initialisation poses.  With BA: every keyframe so far at its latest
         BA estimate (world_T_base) and the landmarks of pair 0's window (world frame, with their
         observation counts)."""
-        if self._config.ba_window <= 0 or self._ba_window is None:
+        if self._loop is not None and self._loop.frames and (self._config.ba_window <= 0 or self._ba_window is None):
+            bt = self._base_T_rect
+            kfs = []
+            for T, ts in zip(self._loop.T, self._loop.stamps):
+                body = self._map_offset @ bt @ T @ _invert(bt)
+                kfs.append(SlamPose(position=body[:3, 3].copy(), rotation=Rotation.from_matrix(body[:3, :3]).as_quat(),
+                                    timestamp=ts, tracking_state=TrackingState.TRACKING, confidence=1.0))
+            smap = SlamMap(keyframe_poses=kfs)
+        elif self._config.ba_window <= 0 or self._ba_window is None:
             smap = SlamMap(keyframe_poses=list(self._keyframe_poses))
         else:
             bt = self._base_T_rect
@@ -441,6 +547,8 @@ class HipSlamEngine(SlamEngine):
         self._keyframe_poses = []
         self._fe_at, self._kf_final, self._kf_stamp, self._ba_window = {}, {}, {}, None
         self._map_points, self._map_offset = {}, np.eye(4)
+        if self._loop is not None:
+            self._loop = _LoopGraph()
         if self._handle is not None:
             self._handle.reset()
         self._state = TrackingState.INITIALIZING
