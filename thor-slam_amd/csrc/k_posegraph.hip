@@ -11,7 +11,8 @@
 //                  multiple of 32 with identity): fixed-order sums over the node's incident edges
 //                  (CSR built on the host, sorted by edge) — deterministic, no atomics;
 //   k_pg_potrf     right-looking blocked Cholesky, panel k: every block factors the 32x32 diagonal
-//                  tile in LDS (block 0 writes it), blocks 1.. solve their tile row of the panel;
+//                  tile in registers (block 0 writes it), blocks 1.. solve their tile row of the
+//                  panel; tiles outside the matrix profile (zero, no fill-in) are skipped;
 //   k_pg_syrk      trailing update A_IJ -= L_Ik L_Jk^T, one 32x32 tile per block, four waves of
 //                  v_mfma_f64_16x16x4f64 (the dense J^T J work on the FP64 matrix cores);
 //   k_pg_trsv      one block: blocked forward / backward substitution (wave 0 solves the 32x32
@@ -21,7 +22,7 @@
 
 #define PG_TILE 32
 #define PG_TERMS 128   // doubles per edge: H_aa 36, H_ab 36, H_bb 36, g_a 6, g_b 6, cost 1
-#define PG_TRSV_THREADS 256
+#define PG_TRSV_THREADS 1024
 #define PG_MAX_N 6144  // padded unknowns held in LDS by k_pg_trsv (1024 nodes)
 
 typedef double pg_d4 __attribute__((ext_vector_type(4)));
@@ -249,55 +250,81 @@ __global__ __launch_bounds__(256) void k_pg_assemble(const double* terms, const 
 }
 
 // ---------------------------------------------------------------------------------------------
-// blocked Cholesky
+// blocked Cholesky over the profile: ftile[I] = first tile column holding a nonzero of tile row
+// I (host-computed from the graph; Cholesky fill-in stays inside the profile), so tiles (I, J)
+// with J < ftile[I] are zero throughout and are skipped everywhere.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_pg_potrf(double* H, int np, int k) {
-    __shared__ double s_L[PG_TILE][PG_TILE + 1];
-    __shared__ double s_A[PG_TILE][PG_TILE + 1];
-    const int t = threadIdx.x;
-    const size_t d0 = (size_t)k * PG_TILE;
-    for (int i = t; i < PG_TILE * PG_TILE; i += 64) s_L[i / PG_TILE][i % PG_TILE] = H[(d0 + i / PG_TILE) * np + d0 + i % PG_TILE];
-    __syncthreads();
+
+// lane `l` (compile-time) of a wave-wide double, through v_readlane (no LDS round trip)
+__device__ __forceinline__ double pg_lane(double v, int l) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l), hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// The 32x32 diagonal tile at (d0, d0) factored in registers: lane t (mod 32) holds row t; column j
+// of step j is broadcast by v_readlane.  Returns row t of L (lower part valid).
+__device__ __forceinline__ void pg_factor_tile(const double* H, int np, size_t d0, int t, double* r) {
+#pragma unroll
+    for (int c = 0; c < PG_TILE; ++c) r[c] = H[(d0 + t) * np + d0 + c];
+#pragma unroll
     for (int j = 0; j < PG_TILE; ++j) {
-        if (t == 0) s_L[j][j] = sqrt(s_L[j][j]);   // a non-positive pivot gives NaN (checked on the host)
-        __syncthreads();
-        if (t > j && t < PG_TILE) s_L[t][j] /= s_L[j][j];
-        __syncthreads();
-        for (int i = t; i < PG_TILE * PG_TILE; i += 64) {
-            const int r = i / PG_TILE, c = i % PG_TILE;
-            if (c > j && r >= c) s_L[r][c] -= s_L[r][j] * s_L[c][j];
+        const double ljj = sqrt(pg_lane(r[j], j));   // a non-positive pivot gives NaN (host check)
+        r[j] = t == j ? ljj : (t > j ? r[j] / ljj : r[j]);
+#pragma unroll
+        for (int c = j + 1; c < PG_TILE; ++c) {
+            const double lcj = pg_lane(r[j], c);
+            if (t >= c) r[c] -= r[j] * lcj;
         }
-        __syncthreads();
     }
+}
+
+// panel k: block 0 writes L_kk; block b >= 1 solves tile row I = k + b (X L_kk^T = A_Ik), unless
+// that tile row is outside the profile of column k.
+__global__ __launch_bounds__(64) void k_pg_potrf(double* H, int np, int k, const int32_t* ftile) {
+    __shared__ double s_L[PG_TILE][PG_TILE + 1];
+    const int I = k + blockIdx.x;
+    if (blockIdx.x > 0 && ftile[I] > k) return;
+    const int t = threadIdx.x & (PG_TILE - 1);
+    const size_t d0 = (size_t)k * PG_TILE;
+    double r[PG_TILE];
+    pg_factor_tile(H, np, d0, t, r);
     if (blockIdx.x == 0) {
-        for (int i = t; i < PG_TILE * PG_TILE; i += 64) {
-            const int r = i / PG_TILE, c = i % PG_TILE;
-            if (c <= r) H[(d0 + r) * np + d0 + c] = s_L[r][c];
-        }
+        if (threadIdx.x < PG_TILE)
+#pragma unroll
+            for (int c = 0; c < PG_TILE; ++c)
+                if (c <= t) H[(d0 + t) * np + d0 + c] = r[c];
         return;
     }
-    // tile row I = k + blockIdx.x of the panel: X L_kk^T = A_Ik
-    const size_t r0 = d0 + (size_t)blockIdx.x * PG_TILE;
-    for (int i = t; i < PG_TILE * PG_TILE; i += 64) s_A[i / PG_TILE][i % PG_TILE] = H[(r0 + i / PG_TILE) * np + d0 + i % PG_TILE];
+    if (threadIdx.x < PG_TILE)
+#pragma unroll
+        for (int c = 0; c < PG_TILE; ++c) s_L[t][c] = r[c];
     __syncthreads();
-    if (t < PG_TILE) {
-        for (int c = 0; c < PG_TILE; ++c) {
-            double x = s_A[t][c];
-            for (int m = 0; m < c; ++m) x -= s_A[t][m] * s_L[c][m];
-            s_A[t][c] = x / s_L[c][c];
-        }
+    if (threadIdx.x >= PG_TILE) return;
+    // row t of the tile in registers; L_kk read as LDS broadcasts (no dependent LDS round trips)
+    const size_t r0 = (size_t)I * PG_TILE + t;
+    double a[PG_TILE];
+#pragma unroll
+    for (int c = 0; c < PG_TILE; ++c) a[c] = H[r0 * np + d0 + c];
+#pragma unroll
+    for (int c = 0; c < PG_TILE; ++c) {
+        double x = a[c];
+#pragma unroll
+        for (int m = 0; m < c; ++m) x -= a[m] * s_L[c][m];
+        a[c] = x / s_L[c][c];
     }
-    __syncthreads();
-    for (int i = t; i < PG_TILE * PG_TILE; i += 64) H[(r0 + i / PG_TILE) * np + d0 + i % PG_TILE] = s_A[i / PG_TILE][i % PG_TILE];
+#pragma unroll
+    for (int c = 0; c < PG_TILE; ++c) H[r0 * np + d0 + c] = a[c];
 }
 
 // trailing tiles (I, J), k < J <= I < nt, dealt as a lower triangle: block b -> (ti, tj)
-__global__ __launch_bounds__(256) void k_pg_syrk(double* H, int np, int k) {
+__global__ __launch_bounds__(256) void k_pg_syrk(double* H, int np, int k, const int32_t* ftile) {
     int ti = (int)((sqrt(8.0 * blockIdx.x + 1.0) - 1.0) * 0.5);
     while ((ti + 1) * (ti + 2) / 2 <= (int)blockIdx.x) ++ti;
     while (ti * (ti + 1) / 2 > (int)blockIdx.x) --ti;
     const int tj = blockIdx.x - ti * (ti + 1) / 2;
     const int I = k + 1 + ti, J = k + 1 + tj;
+    if (ftile[I] > k || ftile[J] > k) return;   // L_Ik or L_Jk is zero
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int qi = wave >> 1, qj = wave & 1;
     const int rc = lane & 15, kk = lane >> 4;
@@ -314,47 +341,65 @@ __global__ __launch_bounds__(256) void k_pg_syrk(double* H, int np, int k) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_pg_trsv: delta = -(L L^T)^-1 g in one block (np <= PG_MAX_N)
+// k_pg_trsv: delta = -(L L^T)^-1 g in one block (np <= PG_MAX_N).  Wave 0 solves each diagonal
+// tile from registers (lane shuffles); the off-diagonal updates skip tiles outside the profile:
+// forward rows two per wave-instruction (32 lanes read a contiguous 256-B row segment, then a
+// 32-lane sum), backward one column element per thread (consecutive threads, consecutive bytes).
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(PG_TRSV_THREADS) void k_pg_trsv(const double* H, int np, const double* g, double* delta) {
+__global__ __launch_bounds__(PG_TRSV_THREADS) void k_pg_trsv(const double* H, int np, const double* g, double* delta,
+                                                             const int32_t* ftile) {
     __shared__ double s_r[PG_MAX_N];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int nt = np / PG_TILE;
+    const int tl = lane & (PG_TILE - 1), half = lane >> 5;
     for (int i = t; i < np; i += PG_TRSV_THREADS) s_r[i] = -g[i];
     __syncthreads();
     for (int k = 0; k < nt; ++k) {   // forward: L y = -g
         const int d0 = k * PG_TILE;
         if (wave == 0) {
-            double y = lane < PG_TILE ? s_r[d0 + lane] : 0.0;
+            double l[PG_TILE];
+#pragma unroll
+            for (int c = 0; c < PG_TILE; ++c) l[c] = H[(size_t)(d0 + tl) * np + d0 + c];
+            double y = s_r[d0 + tl];
+#pragma unroll
             for (int c = 0; c < PG_TILE; ++c) {
-                if (lane == c) y /= H[(size_t)(d0 + c) * np + d0 + c];
-                const double yc = __shfl(y, c, 64);
-                if (lane > c && lane < PG_TILE) y -= H[(size_t)(d0 + lane) * np + d0 + c] * yc;
+                if (tl == c) y /= l[c];
+                const double yc = pg_lane(y, c);
+                if (tl > c) y -= l[c] * yc;
             }
-            if (lane < PG_TILE) s_r[d0 + lane] = y;
+            if (lane < PG_TILE) s_r[d0 + tl] = y;
         }
         __syncthreads();
-        for (int r = d0 + PG_TILE + t; r < np; r += PG_TRSV_THREADS) {
-            const double* row = H + (size_t)r * np + d0;
-            double acc = s_r[r];
-            for (int c = 0; c < PG_TILE; ++c) acc -= row[c] * s_r[d0 + c];
-            s_r[r] = acc;
+        const double yk = s_r[d0 + tl];
+        for (int I = k + 1; I < nt; ++I) {
+            if (ftile[I] > k) continue;   // uniform
+            for (int rr = 2 * wave + half; rr < PG_TILE; rr += 2 * (PG_TRSV_THREADS / 64)) {
+                const int m = I * PG_TILE + rr;
+                double v = H[(size_t)m * np + d0 + tl] * yk;
+#pragma unroll
+                for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
+                if (tl == 0) s_r[m] -= v;
+            }
         }
         __syncthreads();
     }
     for (int k = nt - 1; k >= 0; --k) {   // backward: L^T x = y
         const int d0 = k * PG_TILE;
         if (wave == 0) {
-            double x = lane < PG_TILE ? s_r[d0 + lane] : 0.0;
+            double lc[PG_TILE];   // column tl of the diagonal tile: lc[c] = L[d0 + c][d0 + tl]
+#pragma unroll
+            for (int c = 0; c < PG_TILE; ++c) lc[c] = H[(size_t)(d0 + c) * np + d0 + tl];
+            double x = s_r[d0 + tl];
+#pragma unroll
             for (int c = PG_TILE - 1; c >= 0; --c) {
-                if (lane == c) x /= H[(size_t)(d0 + c) * np + d0 + c];
-                const double xc = __shfl(x, c, 64);
-                if (lane < c) x -= H[(size_t)(d0 + c) * np + d0 + lane] * xc;
+                if (tl == c) x /= lc[c];
+                const double xc = pg_lane(x, c);
+                if (tl < c) x -= lc[c] * xc;
             }
-            if (lane < PG_TILE) s_r[d0 + lane] = x;
+            if (lane < PG_TILE) s_r[d0 + tl] = x;
         }
         __syncthreads();
-        for (int m = t; m < d0; m += PG_TRSV_THREADS) {
+        for (int m = ftile[k] * PG_TILE + t; m < d0; m += PG_TRSV_THREADS) {
             double acc = s_r[m];
             for (int c = 0; c < PG_TILE; ++c) acc -= H[(size_t)(d0 + c) * np + m] * s_r[d0 + c];
             s_r[m] = acc;
@@ -375,17 +420,17 @@ __global__ __launch_bounds__(64) void k_pg_update(double* T, const double* delta
 }
 
 void launch_pose_graph_iteration(double* T, const int32_t* edges, const double* Z, const double* info, int N, int E,
-                                 const int32_t* adj_off, const int32_t* adj, double* terms, double* H, double* g,
-                                 double* delta, hipStream_t s) {
+                                 const int32_t* adj_off, const int32_t* adj, const int32_t* ftile, double* terms,
+                                 double* H, double* g, double* delta, hipStream_t s) {
     const int n = 6 * (N - 1), np = (n + PG_TILE - 1) / PG_TILE * PG_TILE, nt = np / PG_TILE;
     hipLaunchKernelGGL(k_pg_edges, dim3((E + 63) / 64), dim3(64), 0, s, T, edges, Z, info, E, terms);
     hipLaunchKernelGGL(k_pg_assemble, dim3((np + 255) / 256, np), dim3(256), 0, s, terms, edges, adj_off, adj, n, np, H, g);
     for (int k = 0; k < nt; ++k) {
-        hipLaunchKernelGGL(k_pg_potrf, dim3(nt - k), dim3(64), 0, s, H, np, k);
+        hipLaunchKernelGGL(k_pg_potrf, dim3(nt - k), dim3(64), 0, s, H, np, k, ftile);
         const int m = nt - k - 1;
-        if (m > 0) hipLaunchKernelGGL(k_pg_syrk, dim3(m * (m + 1) / 2), dim3(256), 0, s, H, np, k);
+        if (m > 0) hipLaunchKernelGGL(k_pg_syrk, dim3(m * (m + 1) / 2), dim3(256), 0, s, H, np, k, ftile);
     }
-    hipLaunchKernelGGL(k_pg_trsv, dim3(1), dim3(PG_TRSV_THREADS), 0, s, H, np, g, delta);
+    hipLaunchKernelGGL(k_pg_trsv, dim3(1), dim3(PG_TRSV_THREADS), 0, s, H, np, g, delta, ftile);
     hipLaunchKernelGGL(k_pg_update, dim3((N + 62) / 64), dim3(64), 0, s, T, delta, N);
 }
 

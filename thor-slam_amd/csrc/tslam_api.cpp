@@ -82,7 +82,7 @@ struct tslam_handle {
     int pg_nodes = 0, pg_edges = 0, pg_np = 0;
     double *d_pg_T = nullptr, *d_pg_Z = nullptr, *d_pg_info = nullptr, *d_pg_terms = nullptr;
     double *d_pg_H = nullptr, *d_pg_g = nullptr, *d_pg_delta = nullptr;
-    int32_t *d_pg_edges = nullptr, *d_pg_adj_off = nullptr, *d_pg_adj = nullptr;
+    int32_t *d_pg_edges = nullptr, *d_pg_adj_off = nullptr, *d_pg_adj = nullptr, *d_pg_ftile = nullptr;
     Buffer buf[TSLAM_BUF_COUNT];
     uint32_t* d_cand = nullptr;
     uint32_t* d_ccount = nullptr;
@@ -1074,7 +1074,20 @@ int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_e
     for (int i = 1; i < n_nodes; ++i)
         if (off[i + 1] == off[i]) return fail(TSLAM_EINVAL, "a free node has no edge");
     HIPCHK(hipSetDevice(h->device));
-    const int n = 6 * (n_nodes - 1), np = (n + 31) / 32 * 32;
+    const int n = 6 * (n_nodes - 1), np = (n + 31) / 32 * 32, nt = np / 32;
+    // profile of the normal matrix: row block of node p (>= 1) starts at its lowest free
+    // neighbour (or itself); ftile[I] = first nonzero tile column of tile row I
+    std::vector<int32_t> ftile(std::max(nt, 1));
+    for (int I = 0; I < nt; ++I) ftile[I] = I;
+    for (int p = 1; p < n_nodes; ++p) {
+        int lo = p;
+        for (int i = off[p]; i < off[p + 1]; ++i) {
+            const int k = adj[i] >> 1, other = edges[2 * k + ((adj[i] & 1) ? 0 : 1)];
+            if (other >= 1) lo = std::min(lo, other);
+        }
+        const int col = 6 * (lo - 1) / 32;
+        for (int r = 6 * (p - 1); r < 6 * p; ++r) ftile[r / 32] = std::min(ftile[r / 32], col);
+    }
     int rc = TSLAM_OK;
     if (n_nodes > h->pg_nodes) {
         rc = dev_realloc(h, (void**)&h->d_pg_T, sizeof(double) * 16 * n_nodes);
@@ -1093,6 +1106,7 @@ int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_e
     }
     if (np > h->pg_np) {
         rc = dev_realloc(h, (void**)&h->d_pg_H, sizeof(double) * (size_t)np * np);
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_ftile, sizeof(int32_t) * (np / 32));
         if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_g, sizeof(double) * np);
         if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_delta, sizeof(double) * np);
         if (rc != TSLAM_OK) return rc;
@@ -1101,6 +1115,7 @@ int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_e
     hipStream_t s = h->last_stream;
     HIPCHK(hipMemcpyAsync(h->d_pg_T, world_T_node, sizeof(double) * 16 * n_nodes, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(h->d_pg_adj_off, off.data(), sizeof(int32_t) * (n_nodes + 1), hipMemcpyHostToDevice, s));
+    if (nt) HIPCHK(hipMemcpyAsync(h->d_pg_ftile, ftile.data(), sizeof(int32_t) * nt, hipMemcpyHostToDevice, s));
     if (n_edges) {
         HIPCHK(hipMemcpyAsync(h->d_pg_Z, meas, sizeof(double) * 16 * n_edges, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(h->d_pg_info, info, sizeof(double) * 36 * n_edges, hipMemcpyHostToDevice, s));
@@ -1110,7 +1125,7 @@ int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_e
     if (n > 0)
         for (int it = 0; it < iters; ++it)
             launch_pose_graph_iteration(h->d_pg_T, h->d_pg_edges, h->d_pg_Z, h->d_pg_info, n_nodes, n_edges, h->d_pg_adj_off,
-                                        h->d_pg_adj, h->d_pg_terms, h->d_pg_H, h->d_pg_g, h->d_pg_delta, s);
+                                        h->d_pg_adj, h->d_pg_ftile, h->d_pg_terms, h->d_pg_H, h->d_pg_g, h->d_pg_delta, s);
     std::vector<double> terms;
     if (cost && n_edges) {
         launch_pose_graph_cost(h->d_pg_T, h->d_pg_edges, h->d_pg_Z, h->d_pg_info, n_edges, h->d_pg_terms, s);

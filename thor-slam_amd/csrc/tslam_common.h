@@ -149,8 +149,8 @@ void launch_loop_store(const BatchCtx& c, int pair, int64_t frame, double* xyz, 
 void launch_loop_vote(const uint32_t* db_desc, const int32_t* db_n, int K, int S, int q_slot, int n_cand,
                       int max_hamming, int ratio_pct, int32_t* votes, hipStream_t s);
 void launch_pose_graph_iteration(double* T, const int32_t* edges, const double* Z, const double* info, int N, int E,
-                                 const int32_t* adj_off, const int32_t* adj, double* terms, double* H, double* g,
-                                 double* delta, hipStream_t s);
+                                 const int32_t* adj_off, const int32_t* adj, const int32_t* ftile, double* terms,
+                                 double* H, double* g, double* delta, hipStream_t s);
 void launch_pose_graph_cost(const double* T, const int32_t* edges, const double* Z, const double* info, int E,
                             double* terms, hipStream_t s);
 void launch_rgbd_gray(const BatchCtx& c, uint8_t* gray, hipStream_t s);
