@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 4
+#define TSLAM_ABI_VERSION 5
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -269,6 +269,25 @@ int tslam_loop_query(tslam_handle* h, int slot, int n_candidates, int32_t* votes
 int tslam_loop_verify(tslam_handle* h, int pair, int64_t frame, int slot, double* T_qc, double* cov, int32_t* stats);
 int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_edges, const int32_t* edges,
                      const double* meas, const double* info, int iters, double* cost);
+
+/* RGB-D dense mapping (the reference runs nvblox on the RGB + u16 depth
+ * topics, scripts/run_pipeline.py:218-256, voxel 0.05 m / truncation 4 voxels / 10 m,
+ * launch/thor_nvblox.launch.py:26-36).  Spec and CPU restatement: oracle/numpy_tsdf.py.
+ *
+ * tslam_tsdf_init: a dense volume of dims[3] = (nx, ny, nz) voxels of voxel_size metres with its
+ *   corner at origin[3] (tracking world frame = rectified left camera of frame 0); tsdf f32 (m)
+ *   and weight f32, zeroed (also by tslam_reset).
+ * tslam_tsdf_integrate: integrate n_frames depth images (device u16 mm [H][W] of pair `pair`'s
+ *   camera, frames stride_bytes apart; for RGB-D records [BGR | depth] pass record + 3*H*W and the
+ *   record stride) with camera poses world_T_cam[n][16] (host; a NaN pose skips its frame) or, when world_T_cam is NULL, the
+ *   device-resident tracked poses of frames first_frame.. of the last batch (untracked frames are
+ *   skipped).  Enqueued on `stream` (NULL: the handle's last stream).
+ * tslam_tsdf_read: copy the volume out (synchronises); tsdf / weight may be NULL. */
+int tslam_tsdf_init(tslam_handle* h, const double* origin, const int32_t* dims, double voxel_size, double trunc_vox,
+                    double max_dist, double max_weight);
+int tslam_tsdf_integrate(tslam_handle* h, int pair, const void* depth, int64_t stride_bytes, int n_frames,
+                         int64_t first_frame, const double* world_T_cam, void* stream);
+int tslam_tsdf_read(tslam_handle* h, float* tsdf, float* weight);
 
 #ifdef __cplusplus
 }

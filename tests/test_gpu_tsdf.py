@@ -1,0 +1,123 @@
+"""RGB-D dense mapping: ``k_tsdf.hip`` vs ``oracle/numpy_tsdf.py`` on
+identical depth frames and poses — TSDF and weight volumes bit-exact (same IEEE f64 operations,
+f32 storage after every frame), for host poses and for the device-resident tracked poses, with and
+without an undistortion table; a batch equals one call per frame; the integrated surface sits at
+the rendered depth."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from helpers import DISTORTION
+from oracle import numpy_tsdf as TS
+from thor_slam_amd.calib import extract_cameras, rgbd_pairs, rgbd_undistort
+from thor_slam_amd.camera.rig import CameraRig
+from thor_slam_amd.params import HipSlamConfig
+from thor_slam_amd.synthetic import SyntheticRGBDSource
+
+pytestmark = pytest.mark.gpu
+
+ORIGIN = (-2.0, -1.5, 0.5)     # rect world (frame-0 camera, RDF): 4 m x 3 m x 5 m ahead of it
+DIMS = (80, 60, 100)
+VOX, TRUNC_VOX, MAX_D, MAX_W = 0.05, 4.0, 10.0, 100.0
+
+
+def _inv(T):
+    """cam_T_world with k_tsdf_poses' expression order."""
+    out = np.eye(4)
+    for r in range(3):
+        for k in range(3):
+            out[r, k] = T[k, r]
+        out[r, 3] = -((T[0, r] * T[0, 3] + T[1, r] * T[1, 3]) + T[2, r] * T[2, 3])
+    return out
+
+
+def _setup(distorted: bool, n: int, width=320, height=240):
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    src = SyntheticRGBDSource(width=width, height=height, distortion=DISTORTION if distorted else None)
+    cams = extract_cameras(CameraRig([src]).calibration, 2)
+    (ci, _), = rgbd_pairs(cams)
+    rect = rgbd_undistort(cams[ci])
+    cfg = HipSlamConfig(rgbd=True, n_features=1000, n_levels=3)
+    rec = src.render_rgbd_sequence(n)[:, None, :]
+    h = Handle([rect], cfg, max_batch=n)
+    dev = torch.from_numpy(np.ascontiguousarray(rec)).cuda()
+    h.submit(dev.data_ptr(), n, torch.cuda.current_stream().cuda_stream)
+    res = h.read_poses(n)
+    depth = [rec[f, 0, 3 * width * height:].view(np.uint16).reshape(height, width) for f in range(n)]
+    return src, rect, h, dev, res, depth
+
+
+def _oracle(rect, depth, world_T_cam, use):
+    t = np.zeros(DIMS[::-1], dtype=np.float32)
+    w = np.zeros(DIMS[::-1], dtype=np.float32)
+    intr = (rect.fx, rect.fy, rect.cx, rect.cy)
+    for d, T, u in zip(depth, world_T_cam, use):
+        if u:
+            TS.integrate(t, w, d, _inv(T), intr, ORIGIN, VOX, TRUNC_VOX * VOX, MAX_D, MAX_W,
+                         None if rect.is_identity else rect.map_left)
+    return t, w
+
+
+@pytest.mark.parametrize("distorted", [False, True])
+def test_tsdf_host_poses_bit_exact(distorted):
+    n = 4
+    src, rect, h, dev, res, depth = _setup(distorted, n)
+    W, H = rect.width, rect.height
+    poses = res["T_abs"][:, 0]
+    h.tsdf_init(ORIGIN, DIMS, VOX, TRUNC_VOX, MAX_D, MAX_W)
+    h.tsdf_integrate(dev.data_ptr() + 3 * W * H, 5 * W * H, n, world_T_cam=poses)
+    t, w = h.tsdf_read()
+    want_t, want_w = _oracle(rect, depth, poses, [True] * n)
+    assert (want_w > 0).sum() > 10000
+    np.testing.assert_array_equal(w, want_w)
+    np.testing.assert_array_equal(t, want_t)
+    h.close()
+
+
+def test_tsdf_device_poses_and_batch_equivalence():
+    n = 4
+    src, rect, h, dev, res, depth = _setup(False, n)
+    W, H = rect.width, rect.height
+    h.tsdf_init(ORIGIN, DIMS, VOX, TRUNC_VOX, MAX_D, MAX_W)
+    h.tsdf_integrate(dev.data_ptr() + 3 * W * H, 5 * W * H, n, first_frame=0)   # device-resident poses
+    t_dev, w_dev = h.tsdf_read()
+    st = res["stats"][:, 0, 0]
+    want_t, want_w = _oracle(rect, depth, res["T_abs"][:, 0], [s == 0 or (s == 2 and f == 0) for f, s in enumerate(st)])
+    np.testing.assert_array_equal(w_dev, want_w)
+    np.testing.assert_array_equal(t_dev, want_t)
+    # one frame per call == the whole batch in one launch; a NaN pose skips its frame
+    h.reset()
+    h.tsdf_init(ORIGIN, DIMS, VOX, TRUNC_VOX, MAX_D, MAX_W)
+    for f in range(n):
+        h.tsdf_integrate(dev[f:].data_ptr() + 3 * W * H, 5 * W * H, 1, world_T_cam=res["T_abs"][f:f + 1, 0])
+    nan = np.full((1, 4, 4), np.nan)
+    h.tsdf_integrate(dev.data_ptr() + 3 * W * H, 5 * W * H, 1, world_T_cam=nan)
+    t1, w1 = h.tsdf_read()
+    np.testing.assert_array_equal(w1, want_w)
+    np.testing.assert_array_equal(t1, want_t)
+    h.close()
+
+
+def test_tsdf_surface_at_rendered_depth():
+    src, rect, h, dev, res, depth = _setup(False, 1)
+    W, H = rect.width, rect.height
+    h.tsdf_init(ORIGIN, DIMS, VOX, TRUNC_VOX, MAX_D, MAX_W)
+    h.tsdf_integrate(dev.data_ptr() + 3 * W * H, 5 * W * H, 1, world_T_cam=np.eye(4)[None])
+    t, w = h.tsdf_read()
+    h.close()
+    # the voxel column on the optical axis (x = y = 0): the zero crossing is at the centre depth
+    i = int((0.0 - ORIGIN[0]) / VOX)
+    j = int((0.0 - ORIGIN[1]) / VOX)
+    col_t, col_w = t[:, j, i], w[:, j, i]
+    ks = np.nonzero((col_w[:-1] > 0) & (col_w[1:] > 0) & (col_t[:-1] > 0) & (col_t[1:] <= 0))[0]
+    assert ks.size == 1
+    k = ks[0]
+    z0, z1 = ORIGIN[2] + VOX * (k + 0.5), ORIGIN[2] + VOX * (k + 1.5)
+    zc = z0 + (z1 - z0) * col_t[k] / (col_t[k] - col_t[k + 1])
+    d = depth[0][int(rect.cy + 0.5), int(rect.cx + 0.5)] * 0.001
+    assert abs(zc - d) < 0.03, (zc, d)

@@ -83,6 +83,11 @@ struct tslam_handle {
     double *d_pg_T = nullptr, *d_pg_Z = nullptr, *d_pg_info = nullptr, *d_pg_terms = nullptr;
     double *d_pg_H = nullptr, *d_pg_g = nullptr, *d_pg_delta = nullptr;
     int32_t *d_pg_edges = nullptr, *d_pg_adj_off = nullptr, *d_pg_adj = nullptr, *d_pg_ftile = nullptr;
+    // RGB-D dense mapping (tslam_tsdf_*): dense TSDF volume + per-launch pose scratch
+    bool tsdf_on = false;
+    TsdfArgs tsdf{};
+    double* d_tsdf_poses = nullptr;   // [TSDF_MAX_FRAMES][TSDF_POSE]
+    double* d_tsdf_wTc = nullptr;     // [TSDF_MAX_FRAMES][16] host poses staged
     Buffer buf[TSLAM_BUF_COUNT];
     uint32_t* d_cand = nullptr;
     uint32_t* d_ccount = nullptr;
@@ -504,6 +509,11 @@ int tslam_reset(tslam_handle* h) {
     for (int i = 0; i < TS_BA_MAXW; ++i) h->ba_frame[i] = -1;
     h->ba_nkf = 0;
     h->ba_last = -1;
+    if (h->tsdf_on) {   // so does the dense map
+        const size_t nv = (size_t)h->tsdf.nx * h->tsdf.ny * h->tsdf.nz;
+        HIPCHK(hipMemset(h->tsdf.tsdf, 0, sizeof(float) * nv));
+        HIPCHK(hipMemset(h->tsdf.weight, 0, sizeof(float) * nv));
+    }
     h->lp_count = 0;   // the keyframe database belongs to the session
     std::fill(h->lp_n.begin(), h->lp_n.end(), 0);
     h->ba_pending[0] = h->ba_pending[1] = false;
@@ -1047,6 +1057,88 @@ int tslam_loop_verify(tslam_handle* h, int pair, int64_t frame, int slot, double
     const size_t K = h->g.K;
     return reloc_solve(h, pair, frame, h->d_lp_xyz + (size_t)slot * K * 3, h->d_lp_desc + (size_t)slot * K * 8,
                        h->lp_n[slot], T_qc, cov, stats);
+}
+
+// -- RGB-D dense mapping: TSDF integration -------------------------------------------------------
+int tslam_tsdf_init(tslam_handle* h, const double* origin, const int32_t* dims, double voxel_size, double trunc_vox,
+                    double max_dist, double max_weight) {
+    if (!h || !origin || !dims) return fail(TSLAM_EINVAL, "bad argument");
+    if (dims[0] < 1 || dims[1] < 1 || dims[2] < 1 || (int64_t)dims[0] * dims[1] * dims[2] > ((int64_t)1 << 31))
+        return fail(TSLAM_EINVAL, "dims must be >= 1 with at most 2^31 voxels");
+    if (!(voxel_size > 0.0) || !(trunc_vox > 0.0) || !(max_dist > 0.0) || !(max_weight >= 1.0))
+        return fail(TSLAM_EINVAL, "voxel_size, trunc_vox, max_dist must be > 0 and max_weight >= 1");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    const size_t nv = (size_t)dims[0] * dims[1] * dims[2];
+    TsdfArgs& a = h->tsdf;
+    int rc = dev_realloc(h, (void**)&a.tsdf, sizeof(float) * nv);
+    if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&a.weight, sizeof(float) * nv);
+    if (rc == TSLAM_OK && !h->d_tsdf_poses) rc = dev_alloc(h, (void**)&h->d_tsdf_poses, sizeof(double) * TSDF_MAX_FRAMES * TSDF_POSE);
+    if (rc == TSLAM_OK && !h->d_tsdf_wTc) rc = dev_alloc(h, (void**)&h->d_tsdf_wTc, sizeof(double) * TSDF_MAX_FRAMES * 16);
+    if (rc != TSLAM_OK) return rc;
+    a.nx = dims[0];
+    a.ny = dims[1];
+    a.nz = dims[2];
+    a.ox = origin[0];
+    a.oy = origin[1];
+    a.oz = origin[2];
+    a.s = voxel_size;
+    a.trunc = trunc_vox * voxel_size;
+    a.max_dist = max_dist;
+    a.max_weight = max_weight;
+    h->tsdf_on = true;
+    return TSLAM_OK;
+}
+
+int tslam_tsdf_integrate(tslam_handle* h, int pair, const void* depth, int64_t stride_bytes, int n_frames,
+                         int64_t first_frame, const double* world_T_cam, void* stream) {
+    if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
+    if (!h->tsdf_on) return fail(TSLAM_ESTATE, "no TSDF volume (tslam_tsdf_init)");
+    if (!depth || n_frames < 0 || (n_frames > 1 && stride_bytes < 2LL * h->W * h->H)) return fail(TSLAM_EINVAL, "bad depth / stride");
+    if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_tsdf_integrate inside a batch");
+    int f0 = 0;
+    if (!world_T_cam) {   // device poses: frames of the last batch
+        f0 = (int)(first_frame - h->cur_g0);
+        if (first_frame < h->cur_g0 || f0 + n_frames > h->cur_n)
+            return fail(TSLAM_EINVAL, "device poses: frames must belong to the last batch");
+    }
+    HIPCHK(hipSetDevice(h->device));
+    hipStream_t s = stream ? (hipStream_t)stream : h->last_stream;
+    const BatchCtx c = make_ctx(h);
+    const int cam = c.cpp * pair;
+    TsdfArgs a = h->tsdf;
+    a.W = h->W;
+    a.H = h->H;
+    a.fx = h->calib[pair].fx;
+    a.fy = h->calib[pair].fy;
+    a.cx = h->calib[pair].cx;
+    a.cy = h->calib[pair].cy;
+    a.map = ((h->map_mask >> cam) & 1u) ? h->d_maps + (size_t)cam * h->W * h->H * 2 : nullptr;
+    a.stride = stride_bytes;
+    for (int b0 = 0; b0 < n_frames; b0 += TSDF_MAX_FRAMES) {
+        a.n = std::min(TSDF_MAX_FRAMES, n_frames - b0);
+        a.depth = static_cast<const uint8_t*>(depth) + (size_t)b0 * stride_bytes;
+        const double* wtc = nullptr;
+        if (world_T_cam) {
+            HIPCHK(hipMemcpyAsync(h->d_tsdf_wTc, world_T_cam + (size_t)16 * b0, sizeof(double) * 16 * a.n,
+                                  hipMemcpyHostToDevice, s));
+            wtc = h->d_tsdf_wTc;
+        }
+        launch_tsdf(c, pair, f0 + b0, wtc, a, h->d_tsdf_poses, s);
+        HIPCHK(hipGetLastError());
+        if (world_T_cam) HIPCHK(hipStreamSynchronize(s));   // the staged host poses are reused
+    }
+    return TSLAM_OK;
+}
+
+int tslam_tsdf_read(tslam_handle* h, float* tsdf, float* weight) {
+    if (!h || !h->tsdf_on) return fail(TSLAM_ESTATE, "no TSDF volume (tslam_tsdf_init)");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    const size_t nv = (size_t)h->tsdf.nx * h->tsdf.ny * h->tsdf.nz;
+    if (tsdf) HIPCHK(hipMemcpy(tsdf, h->tsdf.tsdf, sizeof(float) * nv, hipMemcpyDeviceToHost));
+    if (weight) HIPCHK(hipMemcpy(weight, h->tsdf.weight, sizeof(float) * nv, hipMemcpyDeviceToHost));
+    return TSLAM_OK;
 }
 
 int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_edges, const int32_t* edges,

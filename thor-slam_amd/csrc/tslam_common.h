@@ -153,6 +153,25 @@ void launch_pose_graph_iteration(double* T, const int32_t* edges, const double* 
                                  double* H, double* g, double* delta, hipStream_t s);
 void launch_pose_graph_cost(const double* T, const int32_t* edges, const double* Z, const double* info, int E,
                             double* terms, hipStream_t s);
+// TSDF volume + one integration launch (k_tsdf.hip)
+#define TSDF_MAX_FRAMES 256
+#define TSDF_POSE 13   // cam_T_world R (9), t (3), use flag
+struct TsdfArgs {
+    float* tsdf;
+    float* weight;
+    int nx, ny, nz;
+    double ox, oy, oz, s;
+    double trunc, max_dist, max_weight;
+    const uint8_t* depth;      // frame 0's depth (u16 mm), frames `stride` bytes apart
+    int64_t stride;
+    int n;                     // frames
+    int W, H;
+    double fx, fy, cx, cy;
+    const int32_t* map;        // [H][W][2] undistortion table (fixed point, 5 bits) or null
+    const double* poses;       // [n][TSDF_POSE]
+};
+void launch_tsdf(const BatchCtx& c, int pair, int f0, const double* host_wTc_dev, const TsdfArgs& a, double* poses,
+                 hipStream_t s);
 void launch_rgbd_gray(const BatchCtx& c, uint8_t* gray, hipStream_t s);
 void launch_rgbd_depth(const BatchCtx& c, hipStream_t s);
 

@@ -102,6 +102,11 @@ _SIGNATURES = {
                                                 ctypes.POINTER(ctypes.c_int)]),
     "tslam_loop_query": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     "tslam_loop_verify": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int] + [ctypes.c_void_p] * 3),
+    "tslam_tsdf_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_double, ctypes.c_double]),
+    "tslam_tsdf_integrate": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                            ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_tsdf_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_pose_graph": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
 }
@@ -400,6 +405,34 @@ class Handle:
         _check(self.lib.tslam_pose_graph(self.h, int(T.shape[0]), T.ctypes.data, int(edges.shape[0]), edges.ctypes.data,
                                          meas.ctypes.data, info.ctypes.data, int(iters), ctypes.byref(cost)))
         return {"T": T, "cost": cost.value}
+
+    # -- RGB-D dense mapping ------------------------------------------
+    def tsdf_init(self, origin, dims, voxel_size: float = 0.05, trunc_vox: float = 4.0, max_dist: float = 10.0,
+                  max_weight: float = 100.0) -> None:
+        o = np.ascontiguousarray(origin, dtype=np.float64).reshape(3)
+        d = np.ascontiguousarray(dims, dtype=np.int32).reshape(3)
+        self._tsdf_dims = tuple(int(x) for x in d)
+        _check(self.lib.tslam_tsdf_init(self.h, o.ctypes.data, d.ctypes.data, float(voxel_size), float(trunc_vox),
+                                        float(max_dist), float(max_weight)))
+
+    def tsdf_integrate(self, depth_dev_ptr: int, stride_bytes: int, n_frames: int, first_frame: int = 0,
+                       world_T_cam: np.ndarray | None = None, pair: int = 0, stream: int = 0) -> None:
+        """Integrate n depth frames (device u16 mm, ``stride_bytes`` apart) with host poses
+        world_T_cam [n][4][4], or the last batch's tracked device poses when None."""
+        poses = None
+        if world_T_cam is not None:
+            poses = np.ascontiguousarray(np.asarray(world_T_cam, dtype=np.float64).reshape(-1, 4, 4))
+        _check(self.lib.tslam_tsdf_integrate(self.h, int(pair), ctypes.c_void_p(depth_dev_ptr), int(stride_bytes),
+                                             int(n_frames), int(first_frame),
+                                             None if poses is None else poses.ctypes.data, ctypes.c_void_p(stream)))
+
+    def tsdf_read(self) -> tuple[np.ndarray, np.ndarray]:
+        """(tsdf, weight) as f32 [nz][ny][nx] (synchronises)."""
+        nx, ny, nz = self._tsdf_dims
+        t = np.zeros((nz, ny, nx), dtype=np.float32)
+        w = np.zeros((nz, ny, nx), dtype=np.float32)
+        _check(self.lib.tslam_tsdf_read(self.h, t.ctypes.data, w.ctypes.data))
+        return t, w
 
     def ba_profile(self, max_launches: int = 0) -> dict:
         """Schur-kernel HIP-event time / launches / algorithmic flops since the last call; re-arms
