@@ -199,6 +199,27 @@ def cpu_baseline(frames: np.ndarray, rect, cfg, budget_s: float, procs: int) -> 
                       f"{len(chunks)} process(es) x {budget_s:.0f} s"}
 
 
+# the synthetic room (8 x 8 x 3 m, FLU) in the tracking world (rect-left camera of frame 0, RDF):
+# x in [-6.9, 1.1], y in [-1.5, 1.5], z in [-4, 4] m; the volume adds 0.3-0.5 m around it
+TSDF_ORIGIN = (-7.2, -1.8, -4.4)
+TSDF_DIMS = (176, 72, 176)
+
+
+def tsdf_report(h, us: float, B: int, width: int, height: int) -> dict:
+    """k_tsdf_integrate of one batch: voxel (tsdf, weight) read-modify-write once per launch
+    (8 + 8 B per observed voxel) + the batch's depth images read once; the voxel-frame updates
+    (the per-voxel projection work) beside it."""
+    t, w = h.tsdf_read()
+    nv = int(np.prod(TSDF_DIMS))
+    observed = int((w > 0).sum())
+    alg = nv * 16 + B * width * height * 2
+    return {"kernel": "k_tsdf_integrate", "volume_voxels": nv, "voxel_size_m": 0.05, "truncation_voxels": 4,
+            "frames_per_launch": B, "avg_launch_us": us, "observed_voxels": observed,
+            "voxel_frame_updates_per_s": nv * B / (us * 1e-6),
+            "roofline": {"bound": "hbm", "achieved": alg / (us * 1e-6) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": alg}}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -215,6 +236,9 @@ def main() -> None:
     ap.add_argument("--dist-backend", type=str, default="nccl", help="nccl (RCCL) or gloo (rehearsal, host copy)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="1: front and back kernels on two streams (batch s+1's front overlaps batch s's back)")
+    ap.add_argument("--tsdf", type=int, default=0,
+                    help="c5: also integrate every batch's depth into a TSDF volume with the device poses "
+                         "(nvblox-shaped dense map, SURVEY.md §8f item 4); reported under dense_map")
     ap.add_argument("--pmc", type=str, default=str(ROOT / "profiles" / "pmc_latest.json"),
                     help="PMC summary (tools/pmc_summary.py) used for roofline.traffic when its batch matches")
     args = ap.parse_args()
@@ -299,7 +323,9 @@ def main() -> None:
             every = torch.stack(parts)
             recv_dev = torch.empty((world * layout.rank_bytes,), dtype=torch.uint8, device="cuda")
         h.set_rig_ranks(list(every.numpy()))
-    names = list(KERNELS) + (["local_ba"] if c4 else [])
+    names = list(KERNELS) + (["local_ba"] if c4 else []) + (["tsdf"] if c5 and args.tsdf else [])
+    if c5 and args.tsdf:
+        h.tsdf_init(TSDF_ORIGIN, TSDF_DIMS, 0.05, 4.0, 10.0, 100.0)
     BACK = {"match", "match_refine", "pose", "chain"}
     # two streams: the front kernels (rectify .. describe) of batch s + 1 overlap the back kernels
     # (match .. chain) of batch s; the library orders batch s's back after its front and batch s's
@@ -333,6 +359,8 @@ def main() -> None:
             stream.wait_event(back_done[s % 2])
         first_back = True
         for i, k in enumerate(names):
+            if k == "tsdf":
+                continue
             if k == "local_ba":
                 ba_stream.wait_stream(bstream)
                 if evs is not None:
@@ -356,6 +384,14 @@ def main() -> None:
             back_done[s % 2].record(bstream)
             back_issued[s % 2] = True
         h.end_batch()
+        if "tsdf" in names:   # the batch's depth into the volume, with its device-resident poses
+            i = names.index("tsdf")
+            if evs is not None:
+                evs[i][0].record(bstream)
+            h.tsdf_integrate(seq[s * B].data_ptr() + 3 * width * height, 5 * width * height, B,
+                             first_frame=s * B, stream=bsp)
+            if evs is not None:
+                evs[i][1].record(bstream)
         if exchanges:  # the exchange step: every rank's keypoints/descriptors/poses to all ranks
             k = s % 2
             ex = exchanges[k]
@@ -416,7 +452,7 @@ def main() -> None:
                   frame_bytes(rect.width, rect.height, cfg.n_features))
     dom_bytes = unit_bytes * B          # §8d per-frame bytes x the frames one launch processes
     schur = h.ba_profile(0) if c4 else None
-    front = {k: v for k, v in per_kernel_us.items() if k != "local_ba"}
+    front = {k: v for k, v in per_kernel_us.items() if k not in ("local_ba", "tsdf")}
     dom = max(front, key=front.get)
     achieved = dom_bytes / (per_kernel_us[dom] * 1e-6) / 1e9
     mfma = None
@@ -523,6 +559,8 @@ def main() -> None:
     }
     if front_roofline is not None:
         out["front_end_roofline"] = front_roofline
+    if "tsdf" in names:
+        out["dense_map"] = tsdf_report(h, per_kernel_us["tsdf"], B, width, height)
     if rank == 0 and args.cpu_budget > 0:
         if c5:
             out["cpu_baseline"] = cpu_baseline_rgbd(np.stack([b for b, _ in rgbd_frames]), np.stack([d for _, d in rgbd_frames]),

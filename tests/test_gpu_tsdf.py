@@ -121,3 +121,71 @@ def test_tsdf_surface_at_rendered_depth():
     zc = z0 + (z1 - z0) * col_t[k] / (col_t[k] - col_t[k + 1])
     d = depth[0][int(rect.cy + 0.5), int(rect.cx + 0.5)] * 0.001
     assert abs(zc - d) < 0.03, (zc, d)
+
+
+def test_tsdf_brick_cull_wide_volume():
+    """A volume all around the camera (behind it, beside it, beyond the integration distance) and
+    rotated poses: the per-brick frustum cull must never drop an update the per-voxel test makes
+    (odd dims exercise partial bricks at every border)."""
+    n = 4
+    src, rect, h, dev, res, depth = _setup(True, n)
+    W, H = rect.width, rect.height
+    origin, dims = (-3.1, -1.9, -2.3), (123, 77, 141)
+    rng = np.random.default_rng(7)
+    poses = []
+    for f in range(n):
+        a = rng.normal(size=3) * 0.4
+        K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+        th = np.linalg.norm(a)
+        R = np.eye(3) + np.sin(th) / th * K + (1 - np.cos(th)) / th ** 2 * K @ K
+        T = np.eye(4)
+        T[:3, :3], T[:3, 3] = R, rng.normal(size=3) * 0.3
+        poses.append(T)
+    poses = np.stack(poses)
+    h.tsdf_init(origin, dims, VOX, TRUNC_VOX, 3.0, MAX_W)
+    h.tsdf_integrate(dev.data_ptr() + 3 * W * H, 5 * W * H, n, world_T_cam=poses)
+    t, w = h.tsdf_read()
+    h.close()
+    want_t = np.zeros(dims[::-1], dtype=np.float32)
+    want_w = np.zeros(dims[::-1], dtype=np.float32)
+    for d, T in zip(depth, poses):
+        TS.integrate(want_t, want_w, d, _inv(T), (rect.fx, rect.fy, rect.cx, rect.cy), origin, VOX, TRUNC_VOX * VOX,
+                     3.0, MAX_W, rect.map_left)
+    assert 10000 < (want_w > 0).sum() < 0.5 * want_w.size
+    np.testing.assert_array_equal(w, want_w)
+    np.testing.assert_array_equal(t, want_t)
+
+
+def test_engine_dense_map():
+    """HipSlamEngine(rgbd, dense_map): each batch's depth integrated with its device-resident tracked
+    poses, bit-exact with the oracle on the poses the device tracked; world_T_volume = base_T_rect."""
+    from thor_slam_amd.camera import Extrinsics
+    from thor_slam_amd.slam.hip_engine import HipSlamEngine
+
+    n = 6
+    src = SyntheticRGBDSource(width=320, height=240)
+    rig = CameraRig([src], rig_extrinsics={src.name: Extrinsics.from_4x4_matrix(src.rig_T_source)})
+    rig.start()
+    cfg = HipSlamConfig(rgbd=True, n_features=1000, n_levels=3, batch_size=n, dense_map=True,
+                        tsdf_origin=ORIGIN, tsdf_dims=DIMS, tsdf_integrator_max_integration_distance_m=MAX_D,
+                        tsdf_max_weight=MAX_W)
+    eng = HipSlamEngine(num_cameras=2, config=cfg)
+    eng.initialize(rig.calibration)
+    depth = []
+    for _ in range(n):
+        fs = rig.get_synchronized_frames()
+        depth.append(np.array(fs.frame_sets[src.name].frames[1].image))
+        eng.process_frames(fs)
+    dm = eng.get_dense_map()
+    res = eng.handle.read_poses(n)
+    rect = eng.rectifications[0]
+    st = res["stats"][:, 0, 0]
+    want_t, want_w = _oracle(rect, depth, res["T_abs"][:, 0], [s == 0 or (s == 2 and f == 0) for f, s in enumerate(st)])
+    assert (want_w > 0).sum() > 10000
+    np.testing.assert_array_equal(dm["weight"], want_w)
+    np.testing.assert_array_equal(dm["tsdf"], want_t)
+    bt = src.rig_T_source @ src.get_extrinsics()[0].to_4x4_matrix() @ rect.left_optical_T_rect()
+    np.testing.assert_allclose(dm["world_T_volume"], bt, atol=1e-12)
+    eng.reset()
+    assert not eng.get_dense_map()["weight"].any()
+    eng.shutdown()

@@ -62,6 +62,18 @@ class HipSlamConfig(SlamConfig):
     # input kind: RGB-D (BASELINE configs[4]) = per source a colour camera (cam_idx 0, BGR) and a
     # depth image aligned to it (cam_idx 1, u16 mm); depth replaces stereo matching
     rgbd: bool = False
+    # RGB-D dense mapping: the depth of pair 0 (the reference maps camera_0
+    # only, launch/thor_nvblox.launch.py:50-56) integrated into a dense TSDF volume on the device
+    # with the tracked poses; nvblox's parameters and defaults (thor_nvblox.launch.py:26-36)
+    dense_map: bool = False
+    voxel_size: float = 0.05
+    tsdf_integrator_max_integration_distance_m: float = 10.0
+    tsdf_integrator_truncation_distance_vox: float = 4.0
+    tsdf_max_weight: float = 100.0
+    # the volume, axis-aligned in the tracking world (rectified camera of the first frame, RDF:
+    # x right, y down, z forward): corner (m) and voxel counts (x, y, z); 10 x 4 x 11 m by default
+    tsdf_origin: tuple = (-5.0, -2.0, -1.0)
+    tsdf_dims: tuple = (200, 80, 220)
     # pipeline
     batch_size: int = 1             # frames per submission (1 = synchronous latency mode)
 
@@ -78,6 +90,14 @@ class HipSlamConfig(SlamConfig):
             raise ValueError("fast_threshold must be in [0, 254]")
         if self.batch_size < 1:
             raise ValueError("batch_size must be >= 1")
+        if self.dense_map:
+            if not self.rgbd:
+                raise ValueError("dense_map needs rgbd=True (depth input)")
+            if not (self.voxel_size > 0 and self.tsdf_integrator_max_integration_distance_m > 0
+                    and self.tsdf_integrator_truncation_distance_vox > 0 and self.tsdf_max_weight >= 1):
+                raise ValueError("voxel_size, integration distance, truncation must be > 0, max weight >= 1")
+            if len(self.tsdf_dims) != 3 or min(self.tsdf_dims) < 1 or len(self.tsdf_origin) != 3:
+                raise ValueError("tsdf_dims must be 3 positive voxel counts, tsdf_origin 3 coordinates")
         if not (self.ba_window == 0 or 2 <= self.ba_window <= 10):
             raise ValueError("ba_window must be 0 (off) or in [2, 10]")
         if self.ba_kf_interval < 1 or self.ba_iters < 1:

@@ -22,6 +22,9 @@ the window, ``W_ba(kf) inv(W_fe(kf)) W_fe(g)`` (the oldest window keyframe's whe
 already evicted it), and ``get_map`` returns the keyframes (BA estimates) and the window's
 landmarks.  With several pairs each keeps its own window (``handle.ba_read(p)``); the published
 pose stays the fused front end and ``get_map`` uses pair 0.
+With ``dense_map`` (RGB-D input) every batch's depth of pair 0 is integrated into a dense TSDF
+volume on the device with the batch's tracked poses (nvblox's role in the reference pipeline,
+``scripts/run_pipeline.py:218-256``); ``get_dense_map`` returns it.
 ``confidence`` follows isaac_ros.py:312.  With ``batch_size > 1`` frames are staged and the
 batch runs on the GPU when full (or on ``flush``); the returned pose is then the latest completed
 one, as the reference allows (its pose lags the published frame, isaac_ros.py:429-430).
@@ -159,6 +162,10 @@ class HipSlamEngine(SlamEngine):
             self._base_R_imu = imu.to_4x4_matrix()[:3, :3] if imu is not None else np.eye(3)
             if len(self._pairs) > 1:   # the rig's body motion is solved on the device from all pairs
                 self._handle.set_rig(self._base_T_rects)
+            if cfg.dense_map:
+                self._handle.tsdf_init(cfg.tsdf_origin, cfg.tsdf_dims, cfg.voxel_size,
+                                       cfg.tsdf_integrator_truncation_distance_vox,
+                                       cfg.tsdf_integrator_max_integration_distance_m, cfg.tsdf_max_weight)
             self._loop = None
             if cfg.enable_loop_closure:
                 if len(self._pairs) == 1:
@@ -232,6 +239,7 @@ class HipSlamEngine(SlamEngine):
         if self._config.imu_fusion:
             self._set_imu_prior(stamps, self._staged_gyro)
         self._handle.submit(self._dev_images.data_ptr(), n, stream.cuda_stream)
+        self._integrate_depth(self._dev_images.data_ptr(), n, stream.cuda_stream)
         res = self._read(n)
         self._staged, self._staged_gyro = [], []
         self._prev_stamp = stamps[-1]
@@ -273,9 +281,37 @@ class HipSlamEngine(SlamEngine):
         n = int(images.shape[0])
         s = stream if stream is not None else self._torch.cuda.current_stream(self._device)
         self._handle.submit(images.data_ptr(), n, s.cuda_stream)
+        self._integrate_depth(images.data_ptr(), n, s.cuda_stream)
         res = self._read(n)
         self._publish(res, timestamps or [float(i) for i in range(n)])
         return res
+
+    # -- RGB-D dense mapping ----------------------------------------------
+    def _integrate_depth(self, records_ptr: int, n: int, stream: int) -> None:
+        """The batch's depth images of pair 0 into the TSDF volume, with the batch's device-resident
+        tracked poses (untracked frames are skipped), on the batch's stream."""
+        if not self._config.dense_map:
+            return
+        r = self._rects[0]
+        hw = r.width * r.height
+        self._handle.tsdf_integrate(records_ptr + 3 * hw, 5 * hw * len(self._pairs), n,
+                                    first_frame=self._handle.frames_done - n, pair=0, stream=stream)
+
+    def get_dense_map(self) -> dict | None:
+        """The TSDF volume (nvblox-shaped): ``tsdf`` / ``weight`` f32 [nz][ny][nx] (metres of
+        truncated signed distance; weight 0 = never observed), the voxel grid (``origin``,
+        ``voxel_size``, voxel (i, j, k) centred at origin + voxel_size (i, j, k) + voxel_size / 2 in
+        the tracking world) and ``world_T_volume`` (4x4: that frame in the published world =
+        base_link at the first frame).  None unless ``dense_map`` is on.  Synchronises."""
+        cfg = self._config
+        if not cfg.dense_map or self._handle is None:
+            return None
+        self.flush()
+        tsdf, weight = self._handle.tsdf_read()
+        return {"tsdf": tsdf, "weight": weight, "origin": np.array(cfg.tsdf_origin, dtype=np.float64),
+                "voxel_size": float(cfg.voxel_size),
+                "truncation_m": cfg.tsdf_integrator_truncation_distance_vox * cfg.voxel_size,
+                "world_T_volume": self._map_offset @ self._base_T_rect}
 
     def _read(self, n: int) -> dict:
         res = self._handle.read_poses(n)
