@@ -3,9 +3,13 @@
 // and the integer-SAD sub-pixel refinements (A6b stereo disparity, A7a temporal position).
 // Bit-exact with oracle.match / oracle.stereo_subpixel / oracle.temporal_subpixel.
 //
-// k_match: one thread per query, 256 queries per block; the train descriptors of the same level
-// are staged in LDS in chunks of 512 (16 KiB) and read as LDS broadcasts, so each pair costs
-// 8 v_xor + 8 v_bcnt (popcount with accumulate) and a compare.  The train side's best query
+// k_match: one thread per query, 256 queries per block.  The train side of a pair is
+// wave-uniform, so its record and descriptor come through SCALAR loads (constant address space,
+// s_load_dwordx4/x8 into SGPRs, served by the scalar cache) and feed the VALU as SGPR operands:
+// each pair costs 8 v_xor + 8 v_bcnt (popcount with accumulate) and a compare, with no LDS read
+// (an LDS broadcast of a 32-byte descriptor still returns 2 KiB per wave at 128 B/clk, which made
+// the LDS, not the VALU, the bound).  Train records are staged in LDS in chunks of 512 only for
+// the mutual check's per-train minimum.  The train side's best query
 // (for the mutual check) comes from a per-wave distance tile read transposed (lane = train),
 // an LDS atomicMin per wave, and one global atomicMin per train descriptor per block: min is
 // order-independent, so the result is deterministic.
@@ -18,15 +22,16 @@
 #define TS_TILE_PITCH 68
 
 __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
-    __shared__ uint4 s_desc[TS_MATCH_CHUNK * 2];
-    __shared__ uint32_t s_xy[TS_MATCH_CHUNK];
     __shared__ uint32_t s_idx[TS_MATCH_CHUNK];
     __shared__ uint32_t s_tmin[TS_MATCH_CHUNK];
     __shared__ uint8_t s_tile[4][64][TS_TILE_PITCH];   // per wave: min(distance, 254)[train jj][query lane]
     __shared__ uint32_t s_qi[4][64];
-    const int z = blockIdx.y;                 // (f * P + p) * 2 + mode
-    const int mode = z & 1;
-    const int fp = z >> 1;
+    // blockIdx.y: the temporal blocks (the heavy ones: a window of rows, not a row band) of every
+    // frame first, then the stereo blocks, so the short stereo blocks fill the launch's tail
+    const int nfp = c.n * c.P;
+    const int z = blockIdx.y;
+    const int mode = z < nfp ? 1 : 0;
+    const int fp = z < nfp ? z : z - nfp;     // f * P + p
     const int p = fp % c.P;
     const int f = fp / c.P;
     const int64_t g = c.g0 + f;
@@ -85,54 +90,54 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
             a = min(a, __shfl_xor(a, o, 64));
             b = max(b, __shfl_xor(b, o, 64));
         }
-        wy0 = a;
-        wy1 = b;
+        wy0 = __builtin_amdgcn_readfirstlane(a);   // equal in every lane: make it provably uniform
+        wy1 = __builtin_amdgcn_readfirstlane(b);
     }
     const bool wave_active = wy1 >= 0;
     const int wt0 = wave_active ? (int)trs[max(0, wy0 - reach)] : 0;
     const int wt1 = wave_active ? (int)trs[min(Hl - 1, wy1 + reach) + 1] : 0;
 
-    int best_d = 1 << 20, best_j = 0x7FFFFFFF, second_d = 1 << 20;
+    // (distance << 16 | train index) keys: the lexicographic (distance, index) minimum is one
+    // v_min_u32, and the second-best distance is the minimum over every key but the best one,
+    // min(second, max(best, key)) (keys are distinct: train indices are) — the oracle's rule
+    uint32_t best_key = 0xFFFFFFFFu, second_key = 0xFFFFFFFFu;
+    // the geometric gate as one box, branch-free: stereo 1 <= x_q - x_t <= max_disp and
+    // |y_q - y_t| <= row_tol; temporal |x_q - x_t| <= window and |y_q - y_t| <= window
+    const int gx_lo = mode == 0 ? 1 : -win, gx_hi = mode == 0 ? dmax : win, gy_tol = mode == 0 ? row_tol : win;
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    typedef const __attribute__((address_space(4))) v4u cv4u;       // uniform address -> s_load
+    cv4u* ctys = (cv4u*)(uintptr_t)tys;
+    cv4u* ctdesc = (cv4u*)(uintptr_t)tdesc;
     for (int j0 = t0; j0 < t1; j0 += TS_MATCH_CHUNK) {
         const int jn = min(TS_MATCH_CHUNK, t1 - j0);
         __syncthreads();
-        // contiguous y-sorted train records and descriptors (no index indirection)
         for (int i = threadIdx.x; i < jn; i += blockDim.x) {
-            const uint4 rec = tys[j0 + i];
-            s_desc[2 * i] = tdesc[2 * (j0 + i)];
-            s_desc[2 * i + 1] = tdesc[2 * (j0 + i) + 1];
-            s_xy[i] = rec.x;
-            s_idx[i] = rec.z;
+            s_idx[i] = tys[j0 + i].z;
             s_tmin[i] = 0xFFFFFFFFu;
         }
         __syncthreads();
         const int ja = max(wt0, j0) - j0, jb = min(wt1, j0 + jn) - j0;
         for (int jt = ja; jt < jb; jt += 64) {
             const int jcount = min(64, jb - jt);
-            // phase 1: this lane's query against up to 64 train descriptors (LDS broadcasts).
-            // Straight-line and unrolled by 8 so the LDS loads of 8 descriptors are in flight together.
+            // phase 1: this lane's query against up to 64 train descriptors, each a wave-uniform
+            // record + descriptor in SGPRs; unrolled by 8 so 8 descriptors' scalar loads are in
+            // flight together
             for (int jj0 = 0; jj0 < 64; jj0 += 8) {
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const int jj = jj0 + u;
-                    const int j = min(jt + jj, jb - 1);
-                    const uint32_t txy = s_xy[j];
-                    const uint4 a = s_desc[2 * j], b = s_desc[2 * j + 1];
-                    const int tx = txy & 0xFFFF, ty = txy >> 16;
+                    const int j = j0 + min(jt + jj, jb - 1);
+                    const v4u rec = ctys[j];
+                    const v4u a = ctdesc[2 * j], b = ctdesc[2 * j + 1];
+                    const int tx = rec.x & 0xFFFF, ty = rec.x >> 16;
                     const int dxy = qx - tx;
-                    const bool geo = mode == 0 ? (abs(qy - ty) <= row_tol && dxy >= 1 && dxy <= dmax)
-                                               : (abs(dxy) <= win && abs(qy - ty) <= win);
-                    const bool elig = geo && active && jj < jcount;
-                    const int dd = __popc(q[0] ^ a.x) + __popc(q[1] ^ a.y) + __popc(q[2] ^ a.z) + __popc(q[3] ^ a.w) +
-                                   __popc(q[4] ^ b.x) + __popc(q[5] ^ b.y) + __popc(q[6] ^ b.z) + __popc(q[7] ^ b.w);
-                    const int tj = (int)s_idx[j];
-                    // lexicographic (distance, train index) minimum; scan order is irrelevant
-                    const bool better = elig && (dd < best_d || (dd == best_d && tj < best_j));
-                    const bool sec = elig && !better && dd < second_d;
-                    second_d = better ? best_d : (sec ? dd : second_d);
-                    best_d = better ? dd : best_d;
-                    best_j = better ? tj : best_j;
-                    s_tile[wave][jj][lane] = (uint8_t)(elig ? min(dd, 254) : 255);
+                    const bool elig = dxy >= gx_lo && dxy <= gx_hi && abs(qy - ty) <= gy_tol && active && jj < jcount;
+                    const uint32_t dd = __popc(q[0] ^ a.x) + __popc(q[1] ^ a.y) + __popc(q[2] ^ a.z) + __popc(q[3] ^ a.w) +
+                                        __popc(q[4] ^ b.x) + __popc(q[5] ^ b.y) + __popc(q[6] ^ b.z) + __popc(q[7] ^ b.w);
+                    const uint32_t key = elig ? ((dd << 16) | rec.z) : 0xFFFFFFFFu;
+                    second_key = min(second_key, max(best_key, key));
+                    best_key = min(best_key, key);
+                    s_tile[wave][jj][lane] = (uint8_t)(elig ? min(dd, 254u) : 255u);
                 }
                 if (jj0 + 8 >= jcount) break;
             }
@@ -164,8 +169,8 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
             if (s_tmin[i] != 0xFFFFFFFFu) atomicMin(&c.tbest[mbase + s_idx[i]], s_tmin[i]);
     }
     if (active) {
-        c.qbest[mbase + qi] = best_d < (1 << 20) ? (((uint32_t)best_d << 16) | (uint32_t)best_j) : 0xFFFFFFFFu;
-        c.qsecond[mbase + qi] = second_d >= (1 << 20) ? 256u : (uint32_t)second_d;
+        c.qbest[mbase + qi] = best_key;
+        c.qsecond[mbase + qi] = second_key == 0xFFFFFFFFu ? 256u : (second_key >> 16);
     }
 }
 
