@@ -3,27 +3,23 @@
 // and the integer-SAD sub-pixel refinements (A6b stereo disparity, A7a temporal position).
 // Bit-exact with oracle.match / oracle.stereo_subpixel / oracle.temporal_subpixel.
 //
-// k_match: one thread per query, 256 queries per block.  The train side of a pair is
-// wave-uniform, so its record and descriptor come through SCALAR loads (constant address space,
-// s_load_dwordx4/x8 into SGPRs, served by the scalar cache) and feed the VALU as SGPR operands:
-// each pair costs 8 v_xor + 8 v_bcnt (popcount with accumulate) and a compare, with no LDS read
-// (an LDS broadcast of a 32-byte descriptor still returns 2 KiB per wave at 128 B/clk, which made
-// the LDS, not the VALU, the bound).  Train records are staged in LDS in chunks of 512 only for
-// the mutual check's per-train minimum.  The train side's best query
-// (for the mutual check) comes from a per-wave distance tile read transposed (lane = train),
-// an LDS atomicMin per wave, and one global atomicMin per train descriptor per block: min is
+// k_match: one thread per query, 256 queries per block, 4 independent waves (no block barrier).
+// The train side of a pair is wave-uniform, so its record and descriptor come through SCALAR
+// loads (constant address space, s_load_dwordx4/x8 into SGPRs, served by the scalar cache) and
+// feed the VALU as SGPR operands: each pair costs 8 v_xor + 8 v_bcnt and a few compares, with no
+// LDS read (an LDS broadcast of a 32-byte descriptor still returns 2 KiB per wave at 128 B/clk).
+// The train side's best query (for the mutual check) comes from a per-wave distance tile read
+// transposed (lane = train) and one global atomicMin per train descriptor per wave tile: min is
 // order-independent, so the result is deterministic.
 #include "tslam_common.h"
 
 // Distances enter the mutual check as bytes: the train side's best query only matters when its
 // distance is <= the query's best <= max_hamming <= 253 (validated), so min(d, 254) keeps every
 // decision exact; 255 marks "not eligible".  Rows padded to 68 B for conflict-free transposed
-// reads.  Total LDS 40 KiB -> 4 blocks per CU.
+// reads.  LDS 18 KiB per block.
 #define TS_TILE_PITCH 68
 
 __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
-    __shared__ uint32_t s_idx[TS_MATCH_CHUNK];
-    __shared__ uint32_t s_tmin[TS_MATCH_CHUNK];
     __shared__ uint8_t s_tile[4][64][TS_TILE_PITCH];   // per wave: min(distance, 254)[train jj][query lane]
     __shared__ uint32_t s_qi[4][64];
     // blockIdx.y: the temporal blocks (the heavy ones: a window of rows, not a row band) of every
@@ -76,12 +72,7 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     s_qi[wave][lane] = (uint32_t)qi;
     const int row_tol = c.mp.row_tol, dmax = c.mp.max_disp >> l, win = c.mp.window >> l;
     const int reach = mode == 0 ? row_tol : win;
-    // rows any query of the block / of this wave can match (queries are y-sorted)
-    const int qlast = min(qn, q0 + 256) - 1;
-    const int by0 = qys[q0].x >> 16;
-    const int by1 = qys[qlast].x >> 16;
-    const int t0 = trs[max(0, by0 - reach)];
-    const int t1 = trs[min(Hl - 1, by1 + reach) + 1];
+    // rows any query of this wave can match (queries are y-sorted)
     int wy0, wy1;
     {
         int a = active ? qy : (1 << 20), b = active ? qy : -1;
@@ -108,65 +99,56 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     typedef const __attribute__((address_space(4))) v4u cv4u;       // uniform address -> s_load
     cv4u* ctys = (cv4u*)(uintptr_t)tys;
     cv4u* ctdesc = (cv4u*)(uintptr_t)tdesc;
-    for (int j0 = t0; j0 < t1; j0 += TS_MATCH_CHUNK) {
-        const int jn = min(TS_MATCH_CHUNK, t1 - j0);
-        __syncthreads();
-        for (int i = threadIdx.x; i < jn; i += blockDim.x) {
-            s_idx[i] = tys[j0 + i].z;
-            s_tmin[i] = 0xFFFFFFFFu;
-        }
-        __syncthreads();
-        const int ja = max(wt0, j0) - j0, jb = min(wt1, j0 + jn) - j0;
-        for (int jt = ja; jt < jb; jt += 64) {
-            const int jcount = min(64, jb - jt);
-            // phase 1: this lane's query against up to 64 train descriptors, each a wave-uniform
-            // record + descriptor in SGPRs; unrolled by 8 so 8 descriptors' scalar loads are in
-            // flight together
-            for (int jj0 = 0; jj0 < 64; jj0 += 8) {
+    // The 4 waves are independent (no block barrier): each walks its own train range in tiles of
+    // 64 and publishes each train descriptor's best query with one global atomicMin per tile
+    // (min is order-independent, so the result is deterministic).
+    for (int jt = wt0; jt < wt1; jt += 64) {
+        const int jcount = min(64, wt1 - jt);
+        const uint32_t my_train = lane < jcount ? tys[jt + lane].z : 0u;   // phase 2's train (lane)
+        // phase 1: this lane's query against up to 64 train descriptors, each a wave-uniform
+        // record + descriptor in SGPRs; unrolled by 8 so 8 descriptors' scalar loads are in
+        // flight together
+        for (int jj0 = 0; jj0 < 64; jj0 += 8) {
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int jj = jj0 + u;
-                    const int j = j0 + min(jt + jj, jb - 1);
-                    const v4u rec = ctys[j];
-                    const v4u a = ctdesc[2 * j], b = ctdesc[2 * j + 1];
-                    const int tx = rec.x & 0xFFFF, ty = rec.x >> 16;
-                    const int dxy = qx - tx;
-                    const bool elig = dxy >= gx_lo && dxy <= gx_hi && abs(qy - ty) <= gy_tol && active && jj < jcount;
-                    const uint32_t dd = __popc(q[0] ^ a.x) + __popc(q[1] ^ a.y) + __popc(q[2] ^ a.z) + __popc(q[3] ^ a.w) +
-                                        __popc(q[4] ^ b.x) + __popc(q[5] ^ b.y) + __popc(q[6] ^ b.z) + __popc(q[7] ^ b.w);
-                    const uint32_t key = elig ? ((dd << 16) | rec.z) : 0xFFFFFFFFu;
-                    second_key = min(second_key, max(best_key, key));
-                    best_key = min(best_key, key);
-                    s_tile[wave][jj][lane] = (uint8_t)(elig ? min(dd, 254u) : 255u);
-                }
-                if (jj0 + 8 >= jcount) break;
+            for (int u = 0; u < 8; ++u) {
+                const int jj = jj0 + u;
+                const int j = jt + min(jj, jcount - 1);
+                const v4u rec = ctys[j];
+                const v4u a = ctdesc[2 * j], b = ctdesc[2 * j + 1];
+                const int tx = rec.x & 0xFFFF, ty = rec.x >> 16;
+                const int dxy = qx - tx;
+                const bool elig = dxy >= gx_lo && dxy <= gx_hi && abs(qy - ty) <= gy_tol && active && jj < jcount;
+                const uint32_t dd = __popc(q[0] ^ a.x) + __popc(q[1] ^ a.y) + __popc(q[2] ^ a.z) + __popc(q[3] ^ a.w) +
+                                    __popc(q[4] ^ b.x) + __popc(q[5] ^ b.y) + __popc(q[6] ^ b.z) + __popc(q[7] ^ b.w);
+                const uint32_t key = elig ? ((dd << 16) | rec.z) : 0xFFFFFFFFu;
+                second_key = min(second_key, max(best_key, key));
+                best_key = min(best_key, key);
+                s_tile[wave][jj][lane] = (uint8_t)(elig ? min(dd, 254u) : 255u);
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_wave_barrier();
-            // phase 2: transposed read, lane = train descriptor: (distance, query) minimum over
-            // the wave's 64 queries, 4 queries per dword read (row pitch 68 B = 17 dwords, an
-            // odd stride, so the 64 lanes hit 64 different banks), no cross-lane reduction
-            if (lane < jcount) {
-                uint32_t best = 0xFFFFFFFFu;
-                const uint32_t* row = reinterpret_cast<const uint32_t*>(&s_tile[wave][lane][0]);
+            if (jj0 + 8 >= jcount) break;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        // phase 2: transposed read, lane = train descriptor: (distance, query) minimum over
+        // the wave's 64 queries, 4 queries per dword read (row pitch 68 B = 17 dwords, an
+        // odd stride, so the 64 lanes hit 64 different banks), no cross-lane reduction
+        if (lane < jcount) {
+            uint32_t best = 0xFFFFFFFFu;
+            const uint32_t* row = reinterpret_cast<const uint32_t*>(&s_tile[wave][lane][0]);
 #pragma unroll 4
-                for (int r4 = 0; r4 < 16; ++r4) {
-                    const uint32_t d4 = row[r4];
+            for (int r4 = 0; r4 < 16; ++r4) {
+                const uint32_t d4 = row[r4];
 #pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-                        const uint32_t d = (d4 >> (8 * b)) & 0xFFu;
-                        const uint32_t key = (d << 16) | s_qi[wave][4 * r4 + b];
-                        best = (d != 0xFFu && key < best) ? key : best;
-                    }
+                for (int b = 0; b < 4; ++b) {
+                    const uint32_t d = (d4 >> (8 * b)) & 0xFFu;
+                    const uint32_t key = (d << 16) | s_qi[wave][4 * r4 + b];
+                    best = (d != 0xFFu && key < best) ? key : best;
                 }
-                if (best != 0xFFFFFFFFu) atomicMin(&s_tmin[jt + lane], best);
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_wave_barrier();
+            if (best != 0xFFFFFFFFu) atomicMin(&c.tbest[mbase + my_train], best);
         }
-        __syncthreads();
-        for (int i = threadIdx.x; i < jn; i += blockDim.x)
-            if (s_tmin[i] != 0xFFFFFFFFu) atomicMin(&c.tbest[mbase + s_idx[i]], s_tmin[i]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
     }
     if (active) {
         c.qbest[mbase + qi] = best_key;
