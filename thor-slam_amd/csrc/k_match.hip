@@ -19,6 +19,14 @@
 // reads.  LDS 18 KiB per block.
 #define TS_TILE_PITCH 68
 
+// popcount(x) + acc as one v_bcnt_u32_b32 (the compiler would re-associate a chain of
+// __popc(x) + acc into bcnt + v_add3 trees)
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
+
 __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     __shared__ uint8_t s_tile[4][64][TS_TILE_PITCH];   // per wave: min(distance, 254)[train jj][query lane]
     __shared__ uint32_t s_qi[4][64];
@@ -86,7 +94,7 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     }
     const bool wave_active = wy1 >= 0;
     const int wt0 = wave_active ? (int)trs[max(0, wy0 - reach)] : 0;
-    const int wt1 = wave_active ? (int)trs[min(Hl - 1, wy1 + reach) + 1] : 0;
+    int wt1 = wave_active ? (int)trs[min(Hl - 1, wy1 + reach) + 1] : 0;
 
     // (distance << 16 | train index) keys: the lexicographic (distance, index) minimum is one
     // v_min_u32, and the second-best distance is the minimum over every key but the best one,
@@ -95,6 +103,9 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     // the geometric gate as one box, branch-free: stereo 1 <= x_q - x_t <= max_disp and
     // |y_q - y_t| <= row_tol; temporal |x_q - x_t| <= window and |y_q - y_t| <= window
     const int gx_lo = mode == 0 ? 1 : -win, gx_hi = mode == 0 ? dmax : win, gy_tol = mode == 0 ? row_tol : win;
+    const uint32_t gx_span = (uint32_t)(gx_hi - gx_lo), gy_span = (uint32_t)(2 * gy_tol);
+    if (!active) qx = -(1 << 24);   // an inactive lane fails the x range test
+    if (gx_hi < gx_lo) wt1 = wt0;   // empty disparity range at this level: nothing is eligible
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     typedef const __attribute__((address_space(4))) v4u cv4u;       // uniform address -> s_load
     cv4u* ctys = (cv4u*)(uintptr_t)tys;
@@ -115,11 +126,19 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
                 const int j = jt + min(jj, jcount - 1);
                 const v4u rec = ctys[j];
                 const v4u a = ctdesc[2 * j], b = ctdesc[2 * j + 1];
+                // gate as two unsigned range tests (one v_sub + one v_cmp each; the train's
+                // offsets are scalar): gx_lo <= qx - tx <= gx_hi, -gy_tol <= qy - ty <= gy_tol
                 const int tx = rec.x & 0xFFFF, ty = rec.x >> 16;
-                const int dxy = qx - tx;
-                const bool elig = dxy >= gx_lo && dxy <= gx_hi && abs(qy - ty) <= gy_tol && active && jj < jcount;
-                const uint32_t dd = __popc(q[0] ^ a.x) + __popc(q[1] ^ a.y) + __popc(q[2] ^ a.z) + __popc(q[3] ^ a.w) +
-                                    __popc(q[4] ^ b.x) + __popc(q[5] ^ b.y) + __popc(q[6] ^ b.z) + __popc(q[7] ^ b.w);
+                const bool elig = (uint32_t)(qx - (tx + gx_lo)) <= gx_span && (uint32_t)(qy - (ty - gy_tol)) <= gy_span &&
+                                  jj < jcount;
+                uint32_t dd = __popc(q[0] ^ a.x);   // v_bcnt accumulate chain (8 v_xor + 8 v_bcnt)
+                dd = bcnt_acc(q[1] ^ a.y, dd);
+                dd = bcnt_acc(q[2] ^ a.z, dd);
+                dd = bcnt_acc(q[3] ^ a.w, dd);
+                dd = bcnt_acc(q[4] ^ b.x, dd);
+                dd = bcnt_acc(q[5] ^ b.y, dd);
+                dd = bcnt_acc(q[6] ^ b.z, dd);
+                dd = bcnt_acc(q[7] ^ b.w, dd);
                 const uint32_t key = elig ? ((dd << 16) | rec.z) : 0xFFFFFFFFu;
                 second_key = min(second_key, max(best_key, key));
                 best_key = min(best_key, key);
