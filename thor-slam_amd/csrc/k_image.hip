@@ -562,10 +562,12 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
 
 // ---------------------------------------------------------------------------------------------
 // A4 top-K: exact K_l smallest keys of an image level, sorted ascending.
-// Radix select on (score bin, y, x) histograms, then a bitonic sort of the survivors in LDS.
-// grid (n_levels, n*C), block 256.
+// Radix select on (score bin, y, x) histograms, then counting sorts (bitonic fallback) in LDS.
+// grid (n*C, n_levels), block 1024: blockIdx.y = level, so every level-0 block (the ~10k-
+// candidate sweeps) is dispatched in the first round and the short upper-level blocks follow;
+// LDS (42 KiB) and wave slots allow 2 such blocks per CU = 512 at once.
 // ---------------------------------------------------------------------------------------------
-#define SEL_THREADS 256
+#define SEL_THREADS 1024
 #define SEL_MAX 8192
 
 // smallest bin b with sum(h[0..b]) >= need; returns b and the count strictly before it.
@@ -656,8 +658,8 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
     __shared__ uint32_t s_pref[SEL_THREADS + 1];
     __shared__ int s_bin;
     __shared__ uint32_t s_before, s_nsel, s_flag;
-    const int l = blockIdx.x;
-    const int img = blockIdx.y;
+    const int l = blockIdx.y;
+    const int img = blockIdx.x;
     const int cam = img % c.C;
     const int f = img / c.C;
     const int Kl = c.g.Kq[l];
@@ -670,10 +672,8 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
     // band counts -> exclusive prefix (flat candidate index i lives in band b with
     // s_pref[b] <= i < s_pref[b+1]); every pass below is then one flat, independent-load sweep
     // over the level's candidates (a per-band loop serialised ~25 dependent global round trips)
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-        s_h[i] = gh[i];
-        s_part[i] = i < nb ? cnt[i] : 0u;
-    }
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_h[i] = gh[i];
+    for (int i = threadIdx.x; i < SEL_THREADS; i += blockDim.x) s_part[i] = i < nb ? cnt[i] : 0u;
     __syncthreads();
     for (int o = 1; o < SEL_THREADS; o <<= 1) {
         const uint32_t v = threadIdx.x >= (unsigned)o ? s_part[threadIdx.x - o] : 0u;
@@ -765,8 +765,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
     if (counting) {
         for (int i = threadIdx.x; i < nsel; i += SEL_THREADS) atomicAdd(&s_h[s_keys[i] >> 22], 1u);
         __syncthreads();
-        const uint32_t cnt_b = s_h[threadIdx.x];   // one score bucket per thread
-        if (cnt_b > TS_SEL_BUCKET_MAX) s_flag = 1;
+        if (threadIdx.x < 256 && s_h[threadIdx.x] > TS_SEL_BUCKET_MAX) s_flag = 1;   // one score bucket per thread
         block_exclusive_scan(s_h, 256, s_part);      // s_h[b] = bucket offset
     }
     __syncthreads();
@@ -877,6 +876,6 @@ void launch_detect(const BatchCtx& c, hipStream_t s) {
 }
 
 void launch_select(const BatchCtx& c, hipStream_t s) {
-    dim3 grid(c.g.n_levels, c.n * c.C);
+    dim3 grid(c.n * c.C, c.g.n_levels);
     hipLaunchKernelGGL(k_select, grid, dim3(SEL_THREADS), 0, s, c);
 }
