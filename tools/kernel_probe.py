@@ -25,6 +25,7 @@ def main() -> None:
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=400)
     ap.add_argument("--features", type=int, default=2000)
+    ap.add_argument("--splits", type=int, default=0, help="RANSAC splits per frame (0: the library's choice)")
     args = ap.parse_args()
     import torch
 
@@ -46,7 +47,7 @@ def main() -> None:
         uniq = src.render_stereo_sequence(16)
     frames = uniq[triangle_indices(2 * B, len(uniq))]
     dev = torch.from_numpy(frames).cuda()
-    h = Handle([rect], HipSlamConfig(n_features=args.features), max_batch=B)
+    h = Handle([rect], HipSlamConfig(n_features=args.features), max_batch=B, ransac_splits=args.splits)
     stream = torch.cuda.current_stream()
     s = stream.cuda_stream
     h.submit(dev[:B].data_ptr(), B, s)
