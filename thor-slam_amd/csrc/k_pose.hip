@@ -284,20 +284,70 @@ __global__ __launch_bounds__(POSE_THREADS) void k_corr(BatchCtx c) {
     if (tid == 0) write_stats(sout, n < max(6, c.pp.min_inliers) ? 1 : 3, n, 0, 0, -1, g);  // 3 = "to be solved"
 }
 
-// ---- k_ransac: one split of the hypotheses of one (frame, pair) -----------------------------
-// grid (n*P*S): block (fp, split) solves P3P for hypotheses [h0, h1) (one per thread), then
-// scores its 4*(h1-h0) poses: correspondences stay in registers (TS_RS_CPT per thread), poses
-// are LDS broadcasts, inlier counts are wave ballots (integer sums: order-independent); writes
-// its best (count+1)<<12 | (4095 - pose index) key and that pose.
+// ---- k_p3p: one thread per (frame, pair, hypothesis) -------------------------------------
+// Draws the hypothesis' 3 correspondences (splitmix64 of (seed, frame, h)), solves P3P and writes
+// its 4 candidate poses [R 9 | t 3] to c.hyp (first element NaN = no solution).
+__global__ __launch_bounds__(POSE_THREADS) void k_p3p(BatchCtx c) {
+    const int H = c.pp.n_hyp;
+    const int gid = blockIdx.x * POSE_THREADS + threadIdx.x;
+    if (gid >= c.n * c.P * H) return;
+    const int fp = gid / H, h = gid - fp * H;
+    const int p = fp % c.P;
+    const int f = fp / c.P;
+    const int64_t g = c.g0 + f;
+    const int32_t* sout = c.stats + (size_t)fp * TS_STATS_INTS;
+    if (sout[0] != 3) return;
+    const int n = sout[1];
+    const double* corr = c.corr + ((size_t)f * c.P + p) * c.g.K * TS_CORR_DOUBLES;
+    const uint64_t base_rng = splitmix64(c.pp.seed ^ ((uint64_t)g * 0x9E3779B97F4A7C15ull));
+    uint32_t r[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) r[k] = (uint32_t)(splitmix64(base_rng ^ ((uint64_t)h * 4ull + (uint64_t)k)) >> 32);
+    const uint32_t un = (uint32_t)n;
+    int i0 = (int)(r[0] % un);
+    int i1 = (int)(r[1] % (un - 1));
+    i1 += (i1 >= i0);
+    int i2 = (int)(r[2] % (un - 2));
+    const int lo = min(i0, i1), hi = max(i0, i1);
+    i2 += (i2 >= lo);
+    i2 += (i2 >= hi);
+    const int idx[3] = {i0, i1, i2};
+    V3 pw[3], fb[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double* cr = corr + (size_t)idx[k] * TS_CORR_DOUBLES;
+        pw[k] = {cr[0], cr[1], cr[2]};
+        fb[k] = {cr[5], cr[6], cr[7]};
+    }
+    Pose sol[4];
+    const int mask = p3p_solve(pw, fb, sol);
+    double* out = c.hyp + ((size_t)fp * 4 * H + 4 * h) * 12;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+        double* dst = out + s2 * 12;
+        if ((mask >> s2) & 1) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) dst[k] = sol[s2].r[k];
+            dst[9] = sol[s2].t[0]; dst[10] = sol[s2].t[1]; dst[11] = sol[s2].t[2];
+        } else {
+            dst[0] = __builtin_nan("");
+        }
+    }
+}
+
+// ---- k_ransac: score one split of the poses of one (frame, pair) ---------------------------
+// grid (n*P*S): block (fp, split) scores the 4*(h1-h0) candidate poses of hypotheses [h0, h1):
+// correspondences stay in registers (TS_RS_CPT per thread); a pose is wave-uniform, so it comes
+// through scalar loads (SGPR operands of the f64 VALU ops — an LDS broadcast of its 96 bytes
+// returned 6 KiB per wave and bound the loop); inlier counts are wave ballots (integer sums:
+// order-independent).  Writes its best (count+1)<<12 | (4095 - pose index) key and that pose.
 __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
-    extern __shared__ __attribute__((aligned(16))) double s_pose[];   // [4*Hs][12]
     __shared__ int s_cnt[4 * TS_MAX_HYP_SPLIT];
     __shared__ uint32_t s_wbest[4];
     const int fp = blockIdx.x / S;
     const int split = blockIdx.x % S;
     const int p = fp % c.P;
     const int f = fp / c.P;
-    const int64_t g = c.g0 + f;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int32_t* sout = c.stats + (size_t)fp * TS_STATS_INTS;
     uint32_t* kout = reinterpret_cast<uint32_t*>(c.ransac) + ((size_t)fp * S + split) * TS_RANSAC_WORDS;
@@ -313,44 +363,9 @@ __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
     const PairCalib cal = c.calib[p];
     const double fx = cal.fx, fy = cal.fy;
     const double* corr = c.corr + ((size_t)f * c.P + p) * c.g.K * TS_CORR_DOUBLES;
-    const uint64_t base_rng = splitmix64(c.pp.seed ^ ((uint64_t)g * 0x9E3779B97F4A7C15ull));
-    for (int t = tid; t < nh; t += POSE_THREADS) {
-        const int h = h0 + t;
-        uint32_t r[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) r[k] = (uint32_t)(splitmix64(base_rng ^ ((uint64_t)h * 4ull + (uint64_t)k)) >> 32);
-        const uint32_t un = (uint32_t)n;
-        int i0 = (int)(r[0] % un);
-        int i1 = (int)(r[1] % (un - 1));
-        i1 += (i1 >= i0);
-        int i2 = (int)(r[2] % (un - 2));
-        const int lo = min(i0, i1), hi = max(i0, i1);
-        i2 += (i2 >= lo);
-        i2 += (i2 >= hi);
-        const int idx[3] = {i0, i1, i2};
-        V3 pw[3], fb[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const double* cr = corr + (size_t)idx[k] * TS_CORR_DOUBLES;
-            pw[k] = {cr[0], cr[1], cr[2]};
-            fb[k] = {cr[5], cr[6], cr[7]};
-        }
-        Pose sol[4];
-        const int mask = p3p_solve(pw, fb, sol);
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {
-            double* dst = s_pose + (size_t)(4 * t + s2) * 12;
-            if ((mask >> s2) & 1) {
-#pragma unroll
-                for (int k = 0; k < 9; ++k) dst[k] = sol[s2].r[k];
-                dst[9] = sol[s2].t[0]; dst[10] = sol[s2].t[1]; dst[11] = sol[s2].t[2];
-            } else {
-                dst[0] = __builtin_nan("");
-            }
-        }
-    }
-    // scoring: every thread holds TS_RS_CPT correspondences in registers and walks the poses
-    // (LDS broadcasts); per pose and wave the inliers are ballot popcounts, added into s_cnt
+    const double* hyp = c.hyp + ((size_t)fp * 4 * H + 4 * h0) * 12;   // this split's poses
+    typedef const __attribute__((address_space(4))) double cdouble;   // uniform address -> s_load
+    cdouble* chyp = (cdouble*)(uintptr_t)hyp;
     const int npose = 4 * nh;
     for (int i = tid; i < npose; i += POSE_THREADS) s_cnt[i] = 0;
     __syncthreads();
@@ -367,12 +382,12 @@ __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
             for (int q = 0; q < 5; ++q) cx5[k][q] = cr[q];
         }
         for (int pi = 0; pi < npose; ++pi) {
-            const double* ps = s_pose + (size_t)pi * 12;
-            if (__builtin_isnan(ps[0])) continue;   // uniform
+            cdouble* ps = chyp + (size_t)pi * 12;
             double R[9], t[3];
 #pragma unroll
             for (int k = 0; k < 9; ++k) R[k] = ps[k];
             t[0] = ps[9]; t[1] = ps[10]; t[2] = ps[11];
+            if (__builtin_isnan(R[0])) continue;   // uniform
             int cnt = 0;
 #pragma unroll
             for (int k = 0; k < TS_RS_CPT; ++k) {
@@ -385,7 +400,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
     __syncthreads();
     uint32_t my_best = 0;
     for (int pi = tid; pi < npose; pi += POSE_THREADS) {
-        const bool valid = !__builtin_isnan(s_pose[(size_t)pi * 12]);
+        const bool valid = !__builtin_isnan(hyp[(size_t)pi * 12]);
         const int gidx = 4 * h0 + pi;
         const uint32_t key = valid ? ((uint32_t)(s_cnt[pi] + 1) << 12) | (uint32_t)(4095 - gidx) : (uint32_t)(4095 - gidx);
         my_best = key > my_best ? key : my_best;
@@ -403,7 +418,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
     if (tid == 0) kout[0] = best;
     if (tid < 12 && best != 0u) {
         const int gidx = 4095 - (int)(best & 4095u);
-        const double v = s_pose[(size_t)(gidx - 4 * h0) * 12 + tid];
+        const double v = hyp[(size_t)(gidx - 4 * h0) * 12 + tid];
         reinterpret_cast<double*>(kout + 2)[tid] = v;
     }
 }
@@ -907,29 +922,27 @@ void launch_rig_chain(const BatchCtx& c, hipStream_t s) {
 
 int ransac_splits(const BatchCtx& c) {
     if (c.pp.splits > 0) return min(min(c.pp.splits, c.pp.n_hyp), TS_MAX_SPLITS);
-    // enough blocks to fill the chip (>= 1024: 16 waves per CU), at least 8 hypotheses per
-    // split (measured at B = 256: S = 2 / 4 / 8 / 16 -> 354 / 307 / 331 / 396 us for the pose stage)
+    // scoring blocks (>= 4096: 64 waves per CU over the launch), at least 8 hypotheses per split
+    // (measured at B = 256: S = 4 / 8 / 16 -> 325 / 295 / 283 us for the pose stage)
     const int frames = c.n * c.P;
-    int S = (1024 + frames - 1) / frames;
+    int S = (4096 + frames - 1) / frames;
     S = max(1, min(S, max(1, c.pp.n_hyp / 8)));
     return min(S, TS_MAX_SPLITS);
 }
 
 void launch_pose(const BatchCtx& c, hipStream_t s) {
     const int S = ransac_splits(c);
-    const int hs = (c.pp.n_hyp + S - 1) / S;
-    const size_t lds = (size_t)4 * hs * 12 * sizeof(double);
     hipLaunchKernelGGL(k_corr, dim3(c.n * c.P), dim3(POSE_THREADS), 0, s, c);
-    hipLaunchKernelGGL(k_ransac, dim3(c.n * c.P * S), dim3(POSE_THREADS), lds, s, c, S);
+    hipLaunchKernelGGL(k_p3p, dim3((c.n * c.P * c.pp.n_hyp + POSE_THREADS - 1) / POSE_THREADS), dim3(POSE_THREADS), 0, s, c);
+    hipLaunchKernelGGL(k_ransac, dim3(c.n * c.P * S), dim3(POSE_THREADS), 0, s, c, S);
     hipLaunchKernelGGL(k_refine, dim3(c.n * c.P), dim3(POSE_THREADS), 0, s, c, S);
 }
 
 // RANSAC + refinement only, on correspondences another kernel wrote (relocalisation).
 void launch_pose_solve(const BatchCtx& c, hipStream_t s) {
     const int S = ransac_splits(c);
-    const int hs = (c.pp.n_hyp + S - 1) / S;
-    const size_t lds = (size_t)4 * hs * 12 * sizeof(double);
-    hipLaunchKernelGGL(k_ransac, dim3(c.n * c.P * S), dim3(POSE_THREADS), lds, s, c, S);
+    hipLaunchKernelGGL(k_p3p, dim3((c.n * c.P * c.pp.n_hyp + POSE_THREADS - 1) / POSE_THREADS), dim3(POSE_THREADS), 0, s, c);
+    hipLaunchKernelGGL(k_ransac, dim3(c.n * c.P * S), dim3(POSE_THREADS), 0, s, c, S);
     hipLaunchKernelGGL(k_refine, dim3(c.n * c.P), dim3(POSE_THREADS), 0, s, c, S);
 }
 

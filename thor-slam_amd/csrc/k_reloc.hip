@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256) void k_reloc_corr(BatchCtx c, int cam, int slo
 }
 
 void launch_reloc(const BatchCtx& c, int pair, int64_t frame, const double* map_xyz, const uint32_t* map_desc, int M,
-                  int32_t* match, double* corr, int32_t* stats, double* pose, double* ransac, hipStream_t s) {
+                  int32_t* match, double* corr, int32_t* stats, double* pose, double* ransac, double* hyp, hipStream_t s) {
     const int slot = ring_slot(c, frame), cam = c.cpp * pair;
     hipLaunchKernelGGL(k_reloc_match, dim3((c.g.K + 255) / 256), dim3(256), 0, s, c, cam, slot, map_desc, M, match);
     hipLaunchKernelGGL(k_reloc_corr, dim3(1), dim3(256), 0, s, c, cam, slot, pair, map_xyz, match, corr, stats, frame);
@@ -133,5 +133,6 @@ void launch_reloc(const BatchCtx& c, int pair, int64_t frame, const double* map_
     r.stats = stats;
     r.pose = pose;
     r.ransac = ransac;
+    r.hyp = hyp;
     launch_pose_solve(r, s);
 }

@@ -69,6 +69,7 @@ struct tslam_handle {
     int32_t* d_rl_stats = nullptr;
     double* d_rl_pose = nullptr;
     double* d_rl_ransac = nullptr;
+    double* d_rl_hyp = nullptr;
     int64_t* d_wedges = nullptr;
     // loop closure (tslam_loop_*): keyframe database, one entry per keyframe, slot = count mod cap
     int lp_cap = 0, lp_S = 0;
@@ -94,6 +95,7 @@ struct tslam_handle {
     uint32_t* d_hist = nullptr;
     double* d_state = nullptr;
     double* d_ransac = nullptr;
+    double* d_hyp = nullptr;
     int64_t frames_done = 0;
     // current batch
     const uint8_t* cur_images = nullptr;
@@ -319,6 +321,7 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.rig_stats = h->d_rig_stats;
     c.rig_state = h->d_rig_state;
     c.ransac = h->d_ransac;
+    c.hyp = h->d_hyp;
     c.brief_table = h->d_brief;
     c.wedges = h->d_wedges;
     for (int p = 0; p < h->P; ++p) c.calib[p] = h->calib[p];
@@ -438,6 +441,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_hist, sizeof(uint32_t) * (size_t)B * C * L * 256);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_state, sizeof(double) * 16 * (size_t)P);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_ransac, sizeof(uint32_t) * TS_RANSAC_WORDS * TS_MAX_SPLITS * (size_t)B * P);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_hyp, sizeof(double) * 12 * 4 * (size_t)p.ransac_hypotheses * B * P);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_brief, sizeof(TSLAM_BRIEF_TABLE));
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_wedges, sizeof(TSLAM_WEDGES));
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_maps, sizeof(int32_t) * (size_t)C * W * H * 2);
@@ -905,6 +909,7 @@ static int ensure_reloc_scratch(tslam_handle* h) {
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_stats, sizeof(int32_t) * TS_STATS_INTS);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_pose, sizeof(double) * TS_POSE_DOUBLES);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_ransac, sizeof(uint32_t) * TS_RANSAC_WORDS * TS_MAX_SPLITS);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_hyp, sizeof(double) * 12 * 4 * (size_t)h->prm.ransac_hypotheses);
     return rc;
 }
 
@@ -918,7 +923,7 @@ static int reloc_solve(tslam_handle* h, int pair, int64_t frame, const double* m
         HIPCHK(hipMemcpy(h->d_rl_stats, st, sizeof(st), hipMemcpyHostToDevice));
     } else {
         launch_reloc(c, pair, frame, map_xyz, map_desc, (int)M, h->d_rl_match, h->d_rl_corr, h->d_rl_stats,
-                     h->d_rl_pose, h->d_rl_ransac, s);
+                     h->d_rl_pose, h->d_rl_ransac, h->d_rl_hyp, s);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipStreamSynchronize(s));

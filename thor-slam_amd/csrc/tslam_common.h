@@ -109,6 +109,7 @@ struct BatchCtx {
     double* corr;
     double* pose;
     double* ransac;        // [B][P][TS_MAX_SPLITS][13] split winners (key word + pose)
+    double* hyp;           // [B][P][4 * n_hyp][12] P3P candidate poses (k_p3p -> k_ransac)
     int32_t* stats;
     double* state;
     const double* prior;   // [B][P][10] IMU rotation prior of the batch (tslam_set_motion_prior) or null
@@ -143,7 +144,7 @@ void launch_rig_chain(const BatchCtx& c, hipStream_t s);
 void launch_rig_fuse(const BatchCtx& c, const uint8_t* gathered, int64_t rank_bytes, int world, hipStream_t s);
 void launch_pose_solve(const BatchCtx& c, hipStream_t s);
 void launch_reloc(const BatchCtx& c, int pair, int64_t frame, const double* map_xyz, const uint32_t* map_desc, int M,
-                  int32_t* match, double* corr, int32_t* stats, double* pose, double* ransac, hipStream_t s);
+                  int32_t* match, double* corr, int32_t* stats, double* pose, double* ransac, double* hyp, hipStream_t s);
 void launch_loop_store(const BatchCtx& c, int pair, int64_t frame, double* xyz, uint32_t* desc, int32_t* n_out,
                        hipStream_t s);
 void launch_loop_vote(const uint32_t* db_desc, const int32_t* db_n, int K, int S, int q_slot, int n_cand,
