@@ -305,8 +305,7 @@ __device__ __forceinline__ void glds16(const uint4* src, uint4* wave_dst) {
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 // Horizontal 1-4-6-4-1 of the 4 pixels x0..x0+3 of one tile row as two u16 pairs:
-// ev = (h[x0], h[x0+2]), od = (h[x0+1], h[x0+3]).  Byte windows D_k = row[x0-2+k .. x0+1+k];
-// (D_k & 0x00FF00FF) are the taps of the even pair, (D_k >> 8) & 0x00FF00FF of the odd pair.
+// ev = (h[x0], h[x0+2]), od = (h[x0+1], h[x0+3]).  Byte windows D_k = row[x0-2+k .. x0+1+k].
 // Column clamp (x-2 < 0, x+2 > W-1) only for the first and last quad of a row.
 __device__ __forceinline__ void hsum4(const uint8_t* row, int x0, int W, u16x2* ev, u16x2* od) {
     uint32_t D[5];
@@ -327,11 +326,13 @@ __device__ __forceinline__ void hsum4(const uint8_t* row, int x0, int W, u16x2* 
             D[k] = w;
         }
     }
-    const u16x2 four = {4, 4}, six = {6, 6};
-    auto lo = [](uint32_t v) { return __builtin_bit_cast(u16x2, v & 0x00FF00FFu); };
-    auto hi = [](uint32_t v) { return __builtin_bit_cast(u16x2, (v >> 8) & 0x00FF00FFu); };
-    *ev = lo(D[0]) + four * lo(D[1]) + six * lo(D[2]) + four * lo(D[3]) + lo(D[4]);
-    *od = hi(D[0]) + four * hi(D[1]) + six * hi(D[2]) + four * hi(D[3]) + hi(D[4]);
+    // pixel x0 + j: taps row[x0-2+j .. x0+1+j] = bytes of D_j against weights (1, 4, 6, 4), plus
+    // row[x0+2+j] = byte 3 of D_{j+1}: one v_dot4_u32_u8 with that byte as the accumulator
+    uint32_t hj[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) hj[j] = __builtin_amdgcn_udot4(D[j], 0x04060401u, D[j + 1] >> 24, false);
+    *ev = __builtin_bit_cast(u16x2, hj[0] | (hj[2] << 16));   // sums <= 16 * 255: u16 lanes
+    *od = __builtin_bit_cast(u16x2, hj[1] | (hj[3] << 16));
 }
 
 __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
@@ -428,8 +429,11 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
         // divergence; items (row, quad) dealt over the block
         uint32_t* score32 = (uint32_t*)score;
         const int W4 = W >> 2;
-        for (int it = threadIdx.x; it < (TS_BAND_ROWS + 2) * W4; it += TS_DET_THREADS) {
-            const int r = it / W4, x4 = it - r * W4;
+        // (row, quad) of item it = threadIdx.x + k * TS_DET_THREADS, stepped without a division
+        const int dr = TS_DET_THREADS / W4, dq = TS_DET_THREADS - dr * W4;
+        int r = (int)threadIdx.x / W4, x4 = (int)threadIdx.x - r * W4;
+        for (int it = threadIdx.x; it < (TS_BAND_ROWS + 2) * W4;
+             it += TS_DET_THREADS, r += dr, x4 += dq, (x4 >= W4 ? (x4 -= W4, ++r) : 0)) {
             const int y = y0 - 1 + r;
             uint32_t sc4 = 0;
             if (y >= 3 && y < H - 3) {
@@ -469,13 +473,15 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
         const uint32_t* sc32 = (const uint32_t*)score;
         constexpr uint32_t k64 = 0x64646464u;
         const h16x2 half = {(_Float16)0.5, (_Float16)0.5};
-        for (int i0 = wave * 64; i0 < (yhi - ylo) * W4; i0 += TS_DET_THREADS) {
+        const int dr = TS_DET_THREADS / W4, dq = TS_DET_THREADS - dr * W4;
+        int yy = (wave * 64 + lane) / W4, q = wave * 64 + lane - yy * W4;   // stepped without a division
+        for (int i0 = wave * 64; i0 < (yhi - ylo) * W4;
+             i0 += TS_DET_THREADS, yy += dr, q += dq, (q >= W4 ? (q -= W4, ++yy) : 0)) {
             const int it = i0 + lane;
             uint32_t kbits = 0;   // bit j: pixel x0 + j survives
             int y = 0, x0 = 0;
             uint32_t P = 0;
             if (it < (yhi - ylo) * W4) {
-                const int yy = it / W4, q = it - yy * W4;
                 y = ylo + yy;
                 x0 = 4 * q;
                 const int r = y - y0 + 1;
