@@ -285,15 +285,15 @@ __device__ __forceinline__ uint32_t fast4(const uint8_t* rc, int W, int x0, int 
 }
 
 // ---------------------------------------------------------------------------------------------
-// A3 smoothing + A4 FAST/NMS candidates for one 16-row band of one level.
-// grid (total_bands, n*C), block 512 (8 waves).  LDS: image rows [y0-4, y0+20) (row-clamped),
-// scores of rows [y0-1, y0+17).  ~36 KiB per block -> 4 blocks = 32 waves per CU (the kernel is
-// latency-bound, so occupancy is what hides the LDS and memory latencies).  Work inside each
-// phase is dealt to the 8 waves in equal (row, 64-lane chunk) items.
+// A3 smoothing + A4 FAST/NMS candidates for one band of BR = g.band_rows rows of one level.
+// grid (total_bands, n*C), block 512 (8 waves).  LDS: image rows [y0-4, y0+BR+4) (row-clamped),
+// scores of rows [y0-1, y0+BR+1): (2 BR + 10) W bytes.  BR = 32 at W <= 640 (47 KiB, 3 blocks per
+// CU = the VGPR limit at 70 registers; 1.25x halo rows instead of 1.5x at BR = 16: 778 -> 725 us
+// per 256-frame batch), 16 at wider images (54 KiB at W = 1280).  Work inside each phase is dealt
+// to the 8 waves in equal (row, 64-lane chunk) items.
 // ---------------------------------------------------------------------------------------------
 #define TS_DET_THREADS 512
 #define TS_SMOOTH_GROUPS 2                                // smoothing items = (quad, row group)
-#define TS_SMOOTH_ROWS (TS_BAND_ROWS / TS_SMOOTH_GROUPS)
 #define TS_DET_WAVES (TS_DET_THREADS / 64)
 
 // 16-byte async global -> LDS copy; `wave_dst` is the wave-uniform LDS base, lane k lands at +16k
@@ -346,19 +346,20 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
     while (l + 1 < c.g.n_levels && (int)blockIdx.x >= c.g.band_start[l + 1]) ++l;
     const int band = blockIdx.x - c.g.band_start[l];
     const int W = c.g.W[l], H = c.g.H[l];
-    const int y0 = band * TS_BAND_ROWS;
+    const int BR = c.g.band_rows;
+    const int y0 = band * BR;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const size_t img_off = ((size_t)ring_slot(c, c.g0 + f) * c.C + cam) * c.g.pyr_bytes + c.g.pyr_off[l];
     const uint8_t* src = c.pyr + img_off;
     uint8_t* smo = c.smo + ((size_t)f * c.C + cam) * c.g.pyr_bytes + c.g.pyr_off[l];
-    const int NR = TS_BAND_ROWS + 2 * TS_DET_HALO;
+    const int NR = BR + 2 * TS_DET_HALO;
     uint8_t* tile = lds;
     uint8_t* score = lds + NR * W;
     const int thr = c.fast_threshold;
     // dword rows (W % 4 == 0: every config in BASELINE.json) take the packed paths; byte rows
     // the scalar ones
     const bool wide = ((W & 3) == 0) && ((img_off & 3) == 0);
-    const int rows_here = min(TS_BAND_ROWS, H - y0);
+    const int rows_here = min(BR, H - y0);
 
     for (int i = threadIdx.x; i < 256; i += TS_DET_THREADS) s_hist[i] = 0;
     if (threadIdx.x == 0) s_count = 0;
@@ -389,7 +390,8 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
         const u16x2 four = {4, 4}, six = {6, 6}, rnd = {128, 128};
         for (int it = threadIdx.x; it < TS_SMOOTH_GROUPS * W4; it += TS_DET_THREADS) {
             const int half = it / W4, q = it - half * W4, x0 = 4 * q;
-            const int o0 = TS_SMOOTH_ROWS * half, o1 = min(o0 + TS_SMOOTH_ROWS, rows_here);   // output rows (band-relative)
+            const int SR = BR / TS_SMOOTH_GROUPS;
+            const int o0 = SR * half, o1 = min(o0 + SR, rows_here);   // output rows (band-relative)
             if (o0 >= o1) continue;
             u16x2 e[5], d[5];
 #pragma unroll
@@ -432,7 +434,7 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
         // (row, quad) of item it = threadIdx.x + k * TS_DET_THREADS, stepped without a division
         const int dr = TS_DET_THREADS / W4, dq = TS_DET_THREADS - dr * W4;
         int r = (int)threadIdx.x / W4, x4 = (int)threadIdx.x - r * W4;
-        for (int it = threadIdx.x; it < (TS_BAND_ROWS + 2) * W4;
+        for (int it = threadIdx.x; it < (BR + 2) * W4;
              it += TS_DET_THREADS, r += dr, x4 += dq, (x4 >= W4 ? (x4 -= W4, ++r) : 0)) {
             const int y = y0 - 1 + r;
             uint32_t sc4 = 0;
@@ -448,7 +450,7 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
             score32[r * W4 + x4] = sc4;
         }
     } else {
-        for (int i = threadIdx.x; i < (TS_BAND_ROWS + 2) * W; i += TS_DET_THREADS) {
+        for (int i = threadIdx.x; i < (BR + 2) * W; i += TS_DET_THREADS) {
             const int r = i / W, x = i - r * W;
             const int y = y0 - 1 + r;
             int sc = 0;
@@ -464,7 +466,7 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
     // 3x3 NMS (ties -> earlier raster position) inside the margin; emit keys.
     const int M = c.margin;
     uint32_t* cand = c.cand + ((size_t)f * c.C + cam) * c.g.cand_total + c.g.cand_off[l] + (size_t)band * c.g.cand_cap[l];
-    const int ylo = max(y0, M), yhi = min(y0 + TS_BAND_ROWS, H - M);
+    const int ylo = max(y0, M), yhi = min(y0 + BR, H - M);
     if (wide) {
         // 4 pixels per lane: keep = p > max(4 earlier neighbours) && p >= max(4 later ones), on
         // the two f16 pixel pairs (1024 + score, exact), no divergence; survivors are appended
@@ -875,7 +877,7 @@ void launch_rectify_pyramid(const BatchCtx& c, hipStream_t s) {
 }
 
 void launch_detect(const BatchCtx& c, hipStream_t s) {
-    const size_t lds = (size_t)(TS_BAND_ROWS + 2 * TS_DET_HALO + TS_BAND_ROWS + 2) * c.g.W[0];
+    const size_t lds = (size_t)(c.g.band_rows + 2 * TS_DET_HALO + c.g.band_rows + 2) * c.g.W[0];
     dim3 grid(c.g.total_bands, c.n * c.C);
     (void)hipMemsetAsync(c.hist, 0, sizeof(uint32_t) * 256 * c.g.n_levels * c.C * (size_t)c.n, s);
     hipLaunchKernelGGL(k_detect, grid, dim3(TS_DET_THREADS), lds, s, c);

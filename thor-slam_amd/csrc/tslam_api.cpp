@@ -171,13 +171,14 @@ static void build_geometry(tslam_handle* h) {
     g.Kq[0] = p.n_features - sumq;
     g.pyr_bytes = (off + 15) & ~15;
     int ko = 0, bs = 0, co = 0, qs = 0;
+    g.band_rows = (2 * TS_BAND_ROWS_MAX + 10) * g.W[0] <= 48 * 1024 ? TS_BAND_ROWS_MAX : 16;
     for (int l = 0; l < p.n_levels; ++l) {
         g.koff[l] = ko;
         ko += g.Kq[l];
-        g.nbands[l] = (g.H[l] + TS_BAND_ROWS - 1) / TS_BAND_ROWS;
+        g.nbands[l] = (g.H[l] + g.band_rows - 1) / g.band_rows;
         g.band_start[l] = bs;
         bs += g.nbands[l];
-        g.cand_cap[l] = (TS_BAND_ROWS / 2) * (g.W[l] / 2 + 1);
+        g.cand_cap[l] = (g.band_rows / 2) * (g.W[l] / 2 + 1);
         g.cand_off[l] = co;
         co += g.nbands[l] * g.cand_cap[l];
         g.qtiles[l] = (g.Kq[l] + 255) / 256;

@@ -26,7 +26,9 @@
 #include <stdint.h>
 
 #define TS_MAX_LEVELS 6
-#define TS_BAND_ROWS 16
+// detect band height: 32 rows while the band's LDS (2 * rows + 10 rows of W bytes) stays <= 48 KiB
+// (3 blocks per CU; fewer halo rows and barriers per pixel), else 16 (LevelGeom::band_rows)
+#define TS_BAND_ROWS_MAX 32
 #define TS_DET_HALO 4
 #define TS_RECT_BAND 32
 #define TS_MATCH_CHUNK 512
@@ -48,6 +50,7 @@ struct LevelGeom {
     int pyr_bytes;
     int K;
     int Kq[TS_MAX_LEVELS], koff[TS_MAX_LEVELS];
+    int band_rows;                 // detect band height (16 or TS_BAND_ROWS_MAX, by level-0 width)
     int nbands[TS_MAX_LEVELS], band_start[TS_MAX_LEVELS];
     int total_bands;
     int cand_cap[TS_MAX_LEVELS];   // keys per band at level l
