@@ -295,25 +295,30 @@ __global__ __launch_bounds__(256) void k_refine_stereo(BatchCtx c) {
     }
 }
 
-// Temporal refinement (A7a): validity + position by 5x5 SAD search + 2-D parabola.  Two queries
-// per wave (half-waves, 25 lanes each).  The query's 11x11 patch at t-1 and the 15x15 search
-// window at t are staged in LDS (a few coalesced loads per query instead of 88 gathers per lane),
-// rows padded to 16 bytes and read back as ds_read_b128.  grid xcd_grid(n*P, ceil(K/8)), block 256.
+// Temporal refinement (A7a): validity + position by 5x5 SAD search + 2-D parabola.  Eight queries
+// per wave, 8 lanes each (lane = query slot * 8 + sub), so the dependent chain of loads (record ->
+// match validity -> previous keypoint -> image rows) is paid once per 8 queries, not per 2.  The
+// query's 11x11 patch at t-1 and its 15x15 search window at t are staged in LDS (sub-lane s loads
+// rows s, s+8, .. of the 26), rows padded to 16 bytes and read back as ds_read_b128; sub-lane s
+// scores offsets s, s+8, s+16, s+24 of the 25; the first minimum is an xor-shuffle over the 8
+// lanes.  grid xcd_grid(n*P, ceil(K/32)), block 256.
 #define TS_RT_AROWS 11
 #define TS_RT_BROWS 15
+#define TS_RT_QPB 32   // queries per block
 __global__ __launch_bounds__(256) void k_refine_temporal(BatchCtx c) {
-    __shared__ uint4 s_a[8][TS_RT_AROWS];   // [query slot][row]: 11 bytes used (+ zero pad)
-    __shared__ uint4 s_b[8][TS_RT_BROWS];   // 15 bytes used
+    __shared__ uint4 s_a[TS_RT_QPB][TS_RT_AROWS];   // [query slot][row]: 11 bytes used (+ zero pad)
+    __shared__ uint4 s_b[TS_RT_QPB][TS_RT_BROWS];   // 15 bytes used
+    __shared__ int s_cost[TS_RT_QPB][25];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int K = c.g.K;
     int z, local;
-    if (!xcd_image_block(blockIdx.x, c.n * c.P, (K + 7) / 8, &z, &local)) return;
+    if (!xcd_image_block(blockIdx.x, c.n * c.P, (K + TS_RT_QPB - 1) / TS_RT_QPB, &z, &local)) return;
     const int p = z % c.P, f = z / c.P;
     const int64_t g = c.g0 + f;
     const int slot = ring_slot(c, g);
-    const int half = lane >> 5, hl = lane & 31;
-    const int qslot = wave * 2 + half;
-    const int pos = local * 8 + qslot;
+    const int sub = lane & 7;
+    const int qslot = wave * 8 + (lane >> 3);
+    const int pos = local * TS_RT_QPB + qslot;
     const bool live = pos < K;
     const size_t mbase = (((size_t)f * c.P + p) * 2 + 1) * K;
     const int qcam = c.cpp * p;
@@ -330,14 +335,14 @@ __global__ __launch_bounds__(256) void k_refine_temporal(BatchCtx c) {
     int32_t* out_idx = c.temporal + ((size_t)slot * c.P + p) * K;
     double* out_uv = c.tuv + (((size_t)f * c.P + p) * K + qi) * 2;
     const double nanv = __builtin_nan("");
-    if (live && hl == 0) out_idx[qi] = j;
-    if (live && hl == 0 && j < 0) {
+    if (live && sub == 0) out_idx[qi] = j;
+    if (live && sub == 0 && j < 0) {
         out_uv[0] = nanv;
         out_uv[1] = nanv;
     }
-    int qx = 0, qy = 0, W = 0;
+    int qx = 0, qy = 0;
     if (j >= 0) {
-        W = c.g.W[l];
+        const int W = c.g.W[l];
         qx = qxy & 0xFFFF;
         qy = qxy >> 16;
         const int pslot = ring_slot(c, g - 1);
@@ -345,62 +350,58 @@ __global__ __launch_bounds__(256) void k_refine_temporal(BatchCtx c) {
         const int px = pxy & 0xFFFF, py = pxy >> 16;
         const uint8_t* A = c.pyr + ((size_t)pslot * c.C + qcam) * c.g.pyr_bytes + c.g.pyr_off[l];
         const uint8_t* B = c.pyr + ((size_t)slot * c.C + qcam) * c.g.pyr_bytes + c.g.pyr_off[l];
-        // stage: lanes 0..10 the patch rows (3 dwords via row11), lanes 11..25 the window rows
-        // (15 bytes from 5 aligned dwords + alignbyte)
-        uint4 v = {0u, 0u, 0u, 0u};
-        if (hl < TS_RT_AROWS) {
-            uint32_t w3[3];
-            row11(A, W, py - TS_SAD_HALF + hl, px - TS_SAD_HALF, w3);
-            v = {w3[0], w3[1], w3[2], 0u};
-            s_a[qslot][hl] = v;
-        } else if (hl < TS_RT_AROWS + TS_RT_BROWS) {
-            const int r = hl - TS_RT_AROWS;
-            const uint8_t* a = B + (size_t)(qy - TS_SAD_HALF - TS_SAD_RANGE + r) * W + (qx - TS_SAD_HALF - TS_SAD_RANGE);
-            const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 3u);
-            const uint32_t* q = reinterpret_cast<const uint32_t*>(a - sh);
-            const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
-            v = {__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
-                 __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh) & 0x00FFFFFFu};
-            s_b[qslot][r] = v;
+        // stage: rows 0..10 the patch (3 dwords via row11), rows 11..25 the window (15 bytes from
+        // 5 aligned dwords + alignbyte); row r by sub-lane r % 8
+        for (int hl = sub; hl < TS_RT_AROWS + TS_RT_BROWS; hl += 8) {
+            if (hl < TS_RT_AROWS) {
+                uint32_t w3[3];
+                row11(A, W, py - TS_SAD_HALF + hl, px - TS_SAD_HALF, w3);
+                s_a[qslot][hl] = uint4{w3[0], w3[1], w3[2], 0u};
+            } else {
+                const int r = hl - TS_RT_AROWS;
+                const uint8_t* a = B + (size_t)(qy - TS_SAD_HALF - TS_SAD_RANGE + r) * W + (qx - TS_SAD_HALF - TS_SAD_RANGE);
+                const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 3u);
+                const uint32_t* q = reinterpret_cast<const uint32_t*>(a - sh);
+                const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
+                s_b[qslot][r] = uint4{__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                                      __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh) & 0x00FFFFFFu};
+            }
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // staged rows before the reads (own wave)
-    const int BIG = 0x7FFFFFFF;
-    int cost = BIG;
-    if (j >= 0 && hl < 25) {
-        const int kx = hl % 5, ky = hl / 5;
-        uint32_t s = 0;
+    uint32_t key = 0xFFFFFFFFu;   // first minimum of (cost << 5 | offset) over this lane's offsets
+    if (j >= 0) {
+        for (int o = sub; o < 25; o += 8) {
+            const int kx = o % 5, ky = o / 5;
+            uint32_t s = 0;
 #pragma unroll
-        for (int dy = 0; dy < TS_RT_AROWS; ++dy) {
-            const uint4 ra = s_a[qslot][dy];
-            const uint4 rb = s_b[qslot][dy + ky];
-            // window bytes kx .. kx+10 of the 15-byte row
-            const uint32_t b0 = __builtin_amdgcn_alignbyte(rb.y, rb.x, kx & 3);
-            const uint32_t b1 = __builtin_amdgcn_alignbyte(rb.z, rb.y, kx & 3);
-            const uint32_t b2 = __builtin_amdgcn_alignbyte(rb.w, rb.z, kx & 3);
-            const uint32_t b3 = rb.w >> (8 * (kx & 3));
-            const bool hi = kx >= 4;   // kx == 4: shift by a whole dword
-            const uint32_t w0 = hi ? b1 : b0, w1 = hi ? b2 : b1, w2 = (hi ? b3 : b2) & 0x00FFFFFFu;
-            s = __builtin_amdgcn_sad_u8(ra.x, w0, s);
-            s = __builtin_amdgcn_sad_u8(ra.y, w1, s);
-            s = __builtin_amdgcn_sad_u8(ra.z, w2, s);
+            for (int dy = 0; dy < TS_RT_AROWS; ++dy) {
+                const uint4 ra = s_a[qslot][dy];
+                const uint4 rb = s_b[qslot][dy + ky];
+                // window bytes kx .. kx+10 of the 15-byte row
+                const uint32_t b0 = __builtin_amdgcn_alignbyte(rb.y, rb.x, kx & 3);
+                const uint32_t b1 = __builtin_amdgcn_alignbyte(rb.z, rb.y, kx & 3);
+                const uint32_t b2 = __builtin_amdgcn_alignbyte(rb.w, rb.z, kx & 3);
+                const uint32_t b3 = rb.w >> (8 * (kx & 3));
+                const bool hi = kx >= 4;   // kx == 4: shift by a whole dword
+                const uint32_t w0 = hi ? b1 : b0, w1 = hi ? b2 : b1, w2 = (hi ? b3 : b2) & 0x00FFFFFFu;
+                s = __builtin_amdgcn_sad_u8(ra.x, w0, s);
+                s = __builtin_amdgcn_sad_u8(ra.y, w1, s);
+                s = __builtin_amdgcn_sad_u8(ra.z, w2, s);
+            }
+            s_cost[qslot][o] = (int)s;
+            key = min(key, (s << 5) | (uint32_t)o);
         }
-        cost = (int)s;
     }
-    // first minimum of (cost << 5 | offset) inside each half-wave: DPP row minima + readlanes
-    uint32_t key = (j >= 0 && hl < 25) ? (((uint32_t)cost << 5) | (uint32_t)hl) : 0xFFFFFFFFu;
-    key = min(key, (uint32_t)__builtin_amdgcn_mov_dpp((int)key, 0xB1, 0xF, 0xF, false));
-    key = min(key, (uint32_t)__builtin_amdgcn_mov_dpp((int)key, 0x4E, 0xF, 0xF, false));
-    key = min(key, (uint32_t)__builtin_amdgcn_mov_dpp((int)key, 0x141, 0xF, 0xF, false));
-    key = min(key, (uint32_t)__builtin_amdgcn_mov_dpp((int)key, 0x140, 0xF, 0xF, false));
-    const uint32_t k0 = min((uint32_t)__builtin_amdgcn_readlane((int)key, 0), (uint32_t)__builtin_amdgcn_readlane((int)key, 16));
-    const uint32_t k1 = min((uint32_t)__builtin_amdgcn_readlane((int)key, 32), (uint32_t)__builtin_amdgcn_readlane((int)key, 48));
-    const int a = (int)((half ? k1 : k0) & 31u);
-    const int hb = half * 32;
-    const int c0 = __shfl(cost, hb + a, 64);
-    const int cl = __shfl(cost, hb + max(a - 1, 0), 64), cr = __shfl(cost, hb + min(a + 1, 31), 64);
-    const int cu = __shfl(cost, hb + max(a - 5, 0), 64), cd = __shfl(cost, hb + min(a + 5, 31), 64);
-    if (j >= 0 && hl == 0) {
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) key = min(key, (uint32_t)__shfl_xor((int)key, m, 64));
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // costs of the 8 lanes before the reads
+    if (j >= 0 && sub == 0) {
+        const int a = (int)(key & 31u);
+        const int* cq = s_cost[qslot];
+        const int c0 = cq[a];
+        const int cl = cq[max(a - 1, 0)], cr = cq[min(a + 1, 24)];
+        const int cu = cq[max(a - 5, 0)], cd = cq[min(a + 5, 24)];
         const int ky = a / 5, kx = a % 5;
         double u = nanv, v = nanv;
         if (kx > 0 && kx < 4 && ky > 0 && ky < 4) {
@@ -428,5 +429,5 @@ void launch_match_refine(const BatchCtx& c, hipStream_t s) {
         launch_rgbd_depth(c, s);
     else
         hipLaunchKernelGGL(k_refine_stereo, dim3(xcd_grid(c.n * c.P, (K + 4 * TS_RS_Q - 1) / (4 * TS_RS_Q))), dim3(256), 0, s, c);
-    hipLaunchKernelGGL(k_refine_temporal, dim3(xcd_grid(c.n * c.P, (K + 7) / 8)), dim3(256), 0, s, c);
+    hipLaunchKernelGGL(k_refine_temporal, dim3(xcd_grid(c.n * c.P, (K + TS_RT_QPB - 1) / TS_RT_QPB)), dim3(256), 0, s, c);
 }
