@@ -236,6 +236,8 @@ def main() -> None:
     ap.add_argument("--dist-backend", type=str, default="nccl", help="nccl (RCCL) or gloo (rehearsal, host copy)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="1: front and back kernels on two streams (batch s+1's front overlaps batch s's back)")
+    ap.add_argument("--front-priority", type=int, default=1,
+                    help="1: run the front kernels on a high-priority stream (pipelined mode)")
     ap.add_argument("--tsdf", type=int, default=0,
                     help="c5: also integrate every batch's depth into a TSDF volume with the device poses "
                          "(nvblox-shaped dense map, SURVEY.md §8f item 4); reported under dense_map")
@@ -299,7 +301,10 @@ def main() -> None:
     idx = torch.from_numpy(triangle_indices(total, args.unique)).cuda()
     seq = torch.from_numpy(uniq).cuda().index_select(0, idx).contiguous()  # [total, 2, H, W] (c5: [total, 1, 5HW]) in HBM
     h = Handle([rect], cfg, max_batch=B, device=dev_index)
-    stream = torch.cuda.current_stream()
+    # the front stream (rectify .. describe) is the critical path of the pipelined step: with
+    # --front-priority 1 it is a high-priority stream, so the back kernels fill the gaps around it
+    stream = (torch.cuda.Stream(priority=-1) if args.front_priority and args.pipeline else torch.cuda.current_stream())
+    torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
     layout = BlockLayout(n_frames=B, n_cams=1 if c5 else 2, K=cfg.n_features, L=cfg.n_levels)
     on_device = args.dist_backend == "nccl"
