@@ -431,11 +431,17 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
         // divergence; items (row, quad) dealt over the block
         uint32_t* score32 = (uint32_t*)score;
         const int W4 = W >> 2;
+        // only where the NMS reads: rows y in [M-1, H-M], columns [M-1, W-M] (keypoints lie in
+        // [M, W-M) x [M, H-M)); the margin is ~20 % of a 640x400 pyramid's pixels.  Score words
+        // outside are never read for a pixel inside the margin.
+        const int Mg = c.margin;
+        const int ra = max(0, Mg - y0), rb = min(BR + 2, H - Mg + 2 - y0);
+        const int qa = (Mg - 1) >> 2, nq = ((W - Mg) >> 2) + 1 - qa;
         // (row, quad) of item it = threadIdx.x + k * TS_DET_THREADS, stepped without a division
-        const int dr = TS_DET_THREADS / W4, dq = TS_DET_THREADS - dr * W4;
-        int r = (int)threadIdx.x / W4, x4 = (int)threadIdx.x - r * W4;
-        for (int it = threadIdx.x; it < (BR + 2) * W4;
-             it += TS_DET_THREADS, r += dr, x4 += dq, (x4 >= W4 ? (x4 -= W4, ++r) : 0)) {
+        const int dr = TS_DET_THREADS / nq, dq = TS_DET_THREADS - dr * nq;
+        int r = ra + (int)threadIdx.x / nq, x4 = qa + (int)threadIdx.x % nq;
+        for (int it = threadIdx.x; it < max(rb - ra, 0) * nq;
+             it += TS_DET_THREADS, r += dr, x4 += dq, (x4 >= qa + nq ? (x4 -= nq, ++r) : 0)) {
             const int y = y0 - 1 + r;
             uint32_t sc4 = 0;
             if (y >= 3 && y < H - 3) {
