@@ -21,11 +21,6 @@
 
 #define TS_DT_G 4   // keypoints per orientation / table-load group
 
-__device__ __forceinline__ int dt_count(int W, int H, int* nx) {
-    *nx = (W + TS_DT_W - 1) / TS_DT_W;
-    return *nx * ((H + TS_DT_H - 1) / TS_DT_H);
-}
-
 // 16-byte async global -> LDS copy; `wave_dst` is the wave-uniform LDS base, lane k lands at +16k
 __device__ __forceinline__ void glds16d(const void* src, void* wave_dst) {
     __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
@@ -63,20 +58,14 @@ __global__ __launch_bounds__(256) void k_describe(BatchCtx c) {
     __shared__ uint16_t s_list[TS_DT_W * TS_DT_H / 4];   // NMS keeps at most one per 2x2
     __shared__ uint32_t s_n;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // block -> (image, level, tile); all tiles of one image on one XCD
-    int tiles = 0;
-    for (int l = 0; l < c.g.n_levels; ++l) {
-        int nx;
-        tiles += dt_count(c.g.W[l], c.g.H[l], &nx);
-    }
+    // block -> (image, level, tile); all tiles of one image on one XCD (tile geometry from the
+    // host: no scalar divisions per block beyond the tile's row)
     int img, local;
-    if (!xcd_image_block(blockIdx.x, c.n * c.C, tiles, &img, &local)) return;
-    int l = 0, nx = 1;
-    for (;; ++l) {
-        const int t = dt_count(c.g.W[l], c.g.H[l], &nx);
-        if (local < t || l + 1 == c.g.n_levels) break;
-        local -= t;
-    }
+    if (!xcd_image_block(blockIdx.x, c.n * c.C, c.g.dt_total, &img, &local)) return;
+    int l = 0;
+    while (l + 1 < c.g.n_levels && local >= c.g.dt_start[l + 1]) ++l;
+    local -= c.g.dt_start[l];
+    const int nx = c.g.dt_nx[l];
     const int ty = local / nx, tx = local - ty * nx;
     const int W = c.g.W[l], H = c.g.H[l];
     const int x0 = tx * TS_DT_W, y0 = ty * TS_DT_H;
@@ -215,8 +204,5 @@ __global__ __launch_bounds__(256) void k_describe(BatchCtx c) {
 }
 
 void launch_describe(const BatchCtx& c, hipStream_t s) {
-    int tiles = 0;
-    for (int l = 0; l < c.g.n_levels; ++l)
-        tiles += ((c.g.W[l] + TS_DT_W - 1) / TS_DT_W) * ((c.g.H[l] + TS_DT_H - 1) / TS_DT_H);
-    hipLaunchKernelGGL(k_describe, dim3(xcd_grid(c.n * c.C, tiles)), dim3(256), 0, s, c);
+    hipLaunchKernelGGL(k_describe, dim3(xcd_grid(c.n * c.C, c.g.dt_total)), dim3(256), 0, s, c);
 }

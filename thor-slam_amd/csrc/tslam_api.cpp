@@ -172,6 +172,7 @@ static void build_geometry(tslam_handle* h) {
     g.pyr_bytes = (off + 15) & ~15;
     int ko = 0, bs = 0, co = 0, qs = 0;
     g.band_rows = (2 * TS_BAND_ROWS_MAX + 10) * g.W[0] <= 48 * 1024 ? TS_BAND_ROWS_MAX : 16;
+    g.dt_total = 0;
     for (int l = 0; l < p.n_levels; ++l) {
         g.koff[l] = ko;
         ko += g.Kq[l];
@@ -181,6 +182,9 @@ static void build_geometry(tslam_handle* h) {
         g.cand_cap[l] = (g.band_rows / 2) * (g.W[l] / 2 + 1);
         g.cand_off[l] = co;
         co += g.nbands[l] * g.cand_cap[l];
+        g.dt_nx[l] = (g.W[l] + TS_DT_W - 1) / TS_DT_W;
+        g.dt_start[l] = g.dt_total;
+        g.dt_total += g.dt_nx[l] * ((g.H[l] + TS_DT_H - 1) / TS_DT_H);
         g.qtiles[l] = (g.Kq[l] + 255) / 256;
         g.qtile_start[l] = qs;
         qs += g.qtiles[l];

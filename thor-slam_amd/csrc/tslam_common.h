@@ -60,6 +60,8 @@ struct LevelGeom {
     int total_qtiles;
     int rs_off[TS_MAX_LEVELS];     // u16 offset of level l's row-start table (H_l + 1 entries)
     int rs_total;                  // u16 per image
+    int dt_nx[TS_MAX_LEVELS], dt_start[TS_MAX_LEVELS];   // describe tiles: per row of level l, first tile
+    int dt_total;                  // describe tiles per image
 };
 
 struct PairCalib {
