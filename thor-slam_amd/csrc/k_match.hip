@@ -193,21 +193,6 @@ __device__ __forceinline__ void row11(const uint8_t* img, int W, int y, int x0, 
     w[2] = __builtin_amdgcn_alignbyte(d3, d2, sh) & 0x00FFFFFFu;
 }
 
-// 11x11 integer SAD between patch a (centre ax, ay) and patch b (centre bx, by), pitch W:
-// 33 v_sad_u8 (4 |a-b| + accumulate per instruction).
-__device__ __forceinline__ int sad11(const uint8_t* a, int ax, int ay, const uint8_t* b, int bx, int by, int W) {
-    uint32_t s = 0;
-    for (int dy = -TS_SAD_HALF; dy <= TS_SAD_HALF; ++dy) {
-        uint32_t ra[3], rb[3];
-        row11(a, W, ay + dy, ax - TS_SAD_HALF, ra);
-        row11(b, W, by + dy, bx - TS_SAD_HALF, rb);
-        s = __builtin_amdgcn_sad_u8(ra[0], rb[0], s);
-        s = __builtin_amdgcn_sad_u8(ra[1], rb[1], s);
-        s = __builtin_amdgcn_sad_u8(ra[2], rb[2], s);
-    }
-    return (int)s;
-}
-
 // Validity of the match of query keypoint qi (max distance, ratio, mutual); returns the train
 // index or -1.
 __device__ __forceinline__ int match_valid(const BatchCtx& c, size_t mbase, int qi) {
@@ -219,22 +204,29 @@ __device__ __forceinline__ int match_valid(const BatchCtx& c, size_t mbase, int 
     return (bd <= c.mp.max_hamming && bd * 100 < c.mp.ratio_pct * sd && (int)(tb & 0xFFFF) == qi) ? j : -1;
 }
 
-// Stereo refinement (A6b): validity + disparity by 5-offset SAD + parabola.  One wave serves
-// 12 queries, 5 lanes each (lane = query slot * 5 + offset), so the index chain and the loads of
-// a query are issued once per 12 queries; the SAD rows are direct dword loads (the 5 lanes of a
-// query share the left patch lines).  grid xcd_grid(n*P, ceil(K/48)), block 256.
-#define TS_RS_Q 12
+// Stereo refinement (A6b): validity + disparity by 5-offset SAD + parabola.  Eight queries per
+// wave, 8 lanes each (lane = query slot * 8 + sub), as the temporal refinement: the query's 11x11
+// left patch and the 15x11 right window (offsets -2..+2 around the matched x) are staged in LDS,
+// 22 rows dealt over the 8 lanes, so a query costs ~27 row loads instead of 5 x 88 scattered
+// dword gathers (the texture-address path, not the VALU, bound the per-lane version); sub-lanes
+// 0..4 score the 5 offsets from LDS; the first minimum is an xor-shuffle over the 8 lanes.
+// grid xcd_grid(n*P, ceil(K/32)), block 256.
+#define TS_RS_QPB 32   // queries per block
 __global__ __launch_bounds__(256) void k_refine_stereo(BatchCtx c) {
+    __shared__ uint4 s_a[TS_RS_QPB][11];   // left patch rows: 11 bytes used
+    __shared__ uint4 s_b[TS_RS_QPB][11];   // right window rows: 15 bytes used
+    __shared__ int s_cost[TS_RS_QPB][5];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int K = c.g.K;
     int z, local;
-    if (!xcd_image_block(blockIdx.x, c.n * c.P, (K + 4 * TS_RS_Q - 1) / (4 * TS_RS_Q), &z, &local)) return;
+    if (!xcd_image_block(blockIdx.x, c.n * c.P, (K + TS_RS_QPB - 1) / TS_RS_QPB, &z, &local)) return;
     const int p = z % c.P, f = z / c.P;
     const int64_t g = c.g0 + f;
     const int slot = ring_slot(c, g);
-    const int qs = lane / 5, k = lane - 5 * qs;
-    const int pos = (local * 4 + wave) * TS_RS_Q + qs;
-    const bool live = lane < 5 * TS_RS_Q && pos < K;
+    const int sub = lane & 7;
+    const int qslot = wave * 8 + (lane >> 3);
+    const int pos = local * TS_RS_QPB + qslot;
+    const bool live = pos < K;
     const size_t mbase = (((size_t)f * c.P + p) * 2 + 0) * K;
     const int qcam = c.cpp * p;
     const size_t qkb = ((size_t)slot * c.C + qcam) * K;
@@ -248,44 +240,64 @@ __global__ __launch_bounds__(256) void k_refine_stereo(BatchCtx c) {
         if (rec.w) j = match_valid(c, mbase, qi);
     }
     const double nanv = __builtin_nan("");
-    if (live && k == 0 && j < 0) {
+    if (live && sub == 0 && j < 0) {
         c.stereo[((size_t)slot * c.P + p) * K + qi] = -1;
         c.disp[((size_t)slot * c.P + p) * K + qi] = nanv;
     }
-    const int BIG = 0x7FFFFFFF;
-    int cost = BIG, qx = 0, xr = 0;
+    int qx = 0, xr = 0;
     if (j >= 0) {
         const int W = c.g.W[l];
         qx = qxy & 0xFFFF;
         const int qy = qxy >> 16;
         xr = c.kps[(((size_t)slot * c.C + qcam + 1) * K + j) * 2] & 0xFFFF;
-        const uint8_t* L = c.pyr + ((size_t)slot * c.C + qcam) * c.g.pyr_bytes + c.g.pyr_off[l];
-        const uint8_t* R = c.pyr + ((size_t)slot * c.C + qcam + 1) * c.g.pyr_bytes + c.g.pyr_off[l];
-        cost = sad11(L, qx, qy, R, xr + k - TS_SAD_RANGE, qy, W);
+        const uint8_t* Lp = c.pyr + ((size_t)slot * c.C + qcam) * c.g.pyr_bytes + c.g.pyr_off[l];
+        const uint8_t* Rp = c.pyr + ((size_t)slot * c.C + qcam + 1) * c.g.pyr_bytes + c.g.pyr_off[l];
+        for (int hl = sub; hl < 22; hl += 8) {
+            if (hl < 11) {
+                uint32_t w3[3];
+                row11(Lp, W, qy - TS_SAD_HALF + hl, qx - TS_SAD_HALF, w3);
+                s_a[qslot][hl] = uint4{w3[0], w3[1], w3[2], 0u};
+            } else {
+                const int r = hl - 11;
+                const uint8_t* a = Rp + (size_t)(qy - TS_SAD_HALF + r) * W + (xr - TS_SAD_HALF - TS_SAD_RANGE);
+                const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 3u);
+                const uint32_t* q = reinterpret_cast<const uint32_t*>(a - sh);
+                const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
+                s_b[qslot][r] = uint4{__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                                      __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh) & 0x00FFFFFFu};
+            }
+        }
     }
-    // first minimum over the 5 offsets of each query: (cost << 5 | k) over the lane group
-    const int base = 5 * qs;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // staged rows before the reads (own wave)
     uint32_t key = 0xFFFFFFFFu;
-    int cs[5];
+    if (j >= 0 && sub < 5) {
+        const int kx = sub;   // window bytes kx .. kx+10: right patch centred at xr + kx - 2
+        uint32_t s = 0;
 #pragma unroll
-    for (int u = 0; u < 5; ++u) {
-        cs[u] = __shfl(cost, min(base + u, 63), 64);
-        const uint32_t ku = cs[u] == BIG ? 0xFFFFFFFFu : (((uint32_t)cs[u] << 5) | (uint32_t)u);
-        key = ku < key ? ku : key;
+        for (int dy = 0; dy < 11; ++dy) {
+            const uint4 ra = s_a[qslot][dy];
+            const uint4 rb = s_b[qslot][dy];
+            const uint32_t b0 = __builtin_amdgcn_alignbyte(rb.y, rb.x, kx & 3);
+            const uint32_t b1 = __builtin_amdgcn_alignbyte(rb.z, rb.y, kx & 3);
+            const uint32_t b2 = __builtin_amdgcn_alignbyte(rb.w, rb.z, kx & 3);
+            const uint32_t b3 = rb.w >> (8 * (kx & 3));
+            const bool hi = kx >= 4;
+            const uint32_t w0 = hi ? b1 : b0, w1 = hi ? b2 : b1, w2 = (hi ? b3 : b2) & 0x00FFFFFFu;
+            s = __builtin_amdgcn_sad_u8(ra.x, w0, s);
+            s = __builtin_amdgcn_sad_u8(ra.y, w1, s);
+            s = __builtin_amdgcn_sad_u8(ra.z, w2, s);
+        }
+        s_cost[qslot][sub] = (int)s;
+        key = (s << 5) | (uint32_t)sub;
     }
-    if (j >= 0 && k == 0) {
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) key = min(key, (uint32_t)__shfl_xor((int)key, m, 64));
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // costs of the 5 lanes before the reads
+    if (j >= 0 && sub == 0) {
         const int ks = (int)(key & 31u);
         double d0 = nanv;
         if (ks > 0 && ks < 4) {
-            int c0 = cs[0], cm = cs[0], cp = cs[0];
-#pragma unroll
-            for (int u = 1; u < 4; ++u)
-                if (u == ks) {
-                    cm = cs[u - 1];
-                    c0 = cs[u];
-                    cp = cs[u + 1];
-                }
-            const double delta = parabola(cm, c0, cp);
+            const double delta = parabola(s_cost[qslot][ks - 1], s_cost[qslot][ks], s_cost[qslot][ks + 1]);
             const double sc = (double)(1 << l);
             const double v = ((double)qx - ((double)(xr + (ks - TS_SAD_RANGE)) + delta)) * sc;
             if (v > 0.0) d0 = v;
@@ -428,6 +440,6 @@ void launch_match_refine(const BatchCtx& c, hipStream_t s) {
     if (c.rgbd)
         launch_rgbd_depth(c, s);
     else
-        hipLaunchKernelGGL(k_refine_stereo, dim3(xcd_grid(c.n * c.P, (K + 4 * TS_RS_Q - 1) / (4 * TS_RS_Q))), dim3(256), 0, s, c);
+        hipLaunchKernelGGL(k_refine_stereo, dim3(xcd_grid(c.n * c.P, (K + TS_RS_QPB - 1) / TS_RS_QPB)), dim3(256), 0, s, c);
     hipLaunchKernelGGL(k_refine_temporal, dim3(xcd_grid(c.n * c.P, (K + TS_RT_QPB - 1) / TS_RT_QPB)), dim3(256), 0, s, c);
 }
