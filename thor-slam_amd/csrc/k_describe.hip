@@ -19,7 +19,7 @@
 // shared with the host (tslam_api.cpp builds the BRIEF offset table for TS_DT_P)
 #include "tslam_describe.h"
 
-#define TS_DT_G 4   // keypoints per orientation / table-load group
+#define TS_DT_G 1   // keypoints per orientation / table-load group (1 / 2 / 4 / 8: 461 / 467 / 480 / 567 us)
 
 // 16-byte async global -> LDS copy; `wave_dst` is the wave-uniform LDS base, lane k lands at +16k
 __device__ __forceinline__ void glds16d(const void* src, void* wave_dst) {
