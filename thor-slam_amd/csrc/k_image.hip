@@ -289,7 +289,8 @@ __device__ __forceinline__ uint32_t fast4(const uint8_t* rc, int W, int x0, int 
 // grid (total_bands, n*C), block 512 (8 waves).  LDS: image rows [y0-4, y0+BR+4) (row-clamped),
 // scores of rows [y0-1, y0+BR+1): (2 BR + 10) W bytes.  BR = 32 at W <= 640 (47 KiB, 3 blocks per
 // CU = the VGPR limit at 70 registers; 1.25x halo rows instead of 1.5x at BR = 16: 778 -> 725 us
-// per 256-frame batch), 16 at wider images (54 KiB at W = 1280).  Work inside each phase is dealt
+// per 256-frame batch), 24 at W = 1280 (74 KiB, 2 blocks per CU as at 16: 611 -> 575 us per
+// 50-frame C4 batch).  Work inside each phase is dealt
 // to the 8 waves in equal (row, 64-lane chunk) items.
 // ---------------------------------------------------------------------------------------------
 #define TS_DET_THREADS 512

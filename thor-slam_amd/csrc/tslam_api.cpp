@@ -171,7 +171,11 @@ static void build_geometry(tslam_handle* h) {
     g.Kq[0] = p.n_features - sumq;
     g.pyr_bytes = (off + 15) & ~15;
     int ko = 0, bs = 0, co = 0, qs = 0;
-    g.band_rows = (2 * TS_BAND_ROWS_MAX + 10) * g.W[0] <= 48 * 1024 ? TS_BAND_ROWS_MAX : 16;
+    // detect band height: the tallest of 32 / 24 / 16 rows whose band (2 * rows + 10 rows of W
+    // bytes of LDS) keeps 3 (W <= 640) or 2 (W <= 1280) blocks per CU; measured 778 -> 690 us
+    // at 640x400 (32 rows) and 611 -> 575 us at 1280x800 (24 rows) against 16
+    g.band_rows = (2 * TS_BAND_ROWS_MAX + 10) * g.W[0] <= 48 * 1024 ? TS_BAND_ROWS_MAX
+                : (2 * 24 + 10) * g.W[0] <= 78 * 1024 ? 24 : 16;
     g.dt_total = 0;
     for (int l = 0; l < p.n_levels; ++l) {
         g.koff[l] = ko;

@@ -27,7 +27,7 @@
 
 #define TS_MAX_LEVELS 6
 // detect band height: 32 rows while the band's LDS (2 * rows + 10 rows of W bytes) stays <= 48 KiB
-// (3 blocks per CU; fewer halo rows and barriers per pixel), else 16 (LevelGeom::band_rows)
+// (3 blocks per CU; fewer halo rows and barriers per pixel), else 24 or 16 (LevelGeom::band_rows)
 #define TS_BAND_ROWS_MAX 32
 #define TS_DET_HALO 4
 #define TS_RECT_BAND 32
