@@ -20,7 +20,8 @@
  *                          describe / match / pose); tslam_detect ... tslam_pose are aliases
  *   tslam_ba_read       <- the map/keyframe side of cuVSLAM (SlamEngine.get_map, interface.py:207) —
  *                          here: the A8 sliding keyframe window (poses, landmarks) of a pair
- *   tslam_pack_features keypoint+descriptor block for the multi-GPU all-gather
+ *   tslam_set_shard ... one camera stream per GPU: the blocks a sharded rig
+ *                          exchanges over RCCL (stream blocks, raw images, pose records)
  *
  * Conventions: every function returns 0 on success or a negative TSLAM_E* code;
  * tslam_last_error() returns a thread-local message for the last failure.  A handle is not
@@ -37,7 +38,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 5
+#define TSLAM_ABI_VERSION 6
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -135,7 +136,8 @@ enum tslam_stage {
     TSLAM_KERNEL_MATCH_REFINE = 15,
     TSLAM_KERNEL_POSE = 16,
     TSLAM_KERNEL_CHAIN = 17,
-    TSLAM_KERNEL_RIG = 18           /* rig pose + its chain (after tslam_set_rig) */
+    TSLAM_KERNEL_RIG = 18           /* rig pose + its chain (after tslam_set_rig; sharded: the range's rig pose only,
+                                       KERNEL_CHAIN then chains the pairs and the rig) */
 };
 
 const char* tslam_last_error(void);
@@ -164,8 +166,10 @@ int tslam_sync(tslam_handle* h);
 /* Results of the last submitted batch (blocks until it is done).  Per frame f and pair p
  * (index f * n_pairs + p): T_rel[16] (cam_{t-1} -> cam_t), T_abs[16] (first left camera frame ->
  * current left camera frame, row-major), cov[36] (rho, omega), stats[8] = {status, n_corr,
- * n_inliers, best_count, best_hyp, global_frame, 0, 0}.  Any pointer may be NULL. */
-int tslam_read_poses(tslam_handle* h, double* T_rel, double* T_abs, double* cov, int32_t* stats);
+ * n_inliers, best_count, best_hyp, global_frame, 0, 0}.  Any pointer may be NULL.  The outputs
+ * hold `max_frames` frames (TSLAM_EINVAL when the batch has more); TSLAM_ESTATE when no batch has
+ * run since tslam_create / tslam_reset. */
+int tslam_read_poses(tslam_handle* h, int max_frames, double* T_rel, double* T_abs, double* cov, int32_t* stats);
 
 int tslam_reset(tslam_handle* h);
 int64_t tslam_frames_done(tslam_handle* h);
@@ -181,9 +185,6 @@ int tslam_ring_slot(tslam_handle* h, int64_t global_frame);
  * level_info[0..17] with {W_l, H_l, K_l} for l < 6. */
 int tslam_layout(tslam_handle* h, int64_t* out16, int32_t* level_info18);
 
-/* Copy the keypoints + descriptors + counts of the last batch into `dst` (device):
- * [n_frames][cams] blocks of (K*8 + K*32 + levels*4) bytes, then a pose trailer per
- * (frame, pair) of T_rel[16] + cov[36] f64 and stats[8] i32.  Returns the total in *bytes. */
 /* IMU fusion (the gyro samples of SynchronizedFrameSet.sensor_data,
  * types.py:268-269, filled by rig.py:403-407): a rotation prior for each (frame, pair) of the NEXT
  * batch, prior[n][P][10] = the predicted rectified-left relative rotation R (row-major 3x3, the
@@ -198,20 +199,46 @@ int tslam_set_motion_prior(tslam_handle* h, const double* prior, int n_frames);
  * pairs' correspondences (generalised PnP: per-pair RANSAC winners as candidates scored on every
  * pair, then a joint Gauss-Newton) and chains it. */
 int tslam_set_rig(tslam_handle* h, const double* base_T_rect);
-/* Rig fusion across ranks (one stereo source per GPU, the rig-level solve after the
- * all-gather).  base_T_rect[world * n_pairs][16], rank-major.  tslam_rig_fuse reads the gathered
- * tslam_pack_features blocks of one batch (frames first_frame .. +n_frames-1; [world][block bytes],
- * device memory) and, per frame,
- * combines every tracked pair's body motion by information weighting (each pair's 6x6 covariance
- * rotated into the body frame), then chains it; read with tslam_read_rig_poses.  Enqueued on
- * `stream` (after the collective), no synchronisation; in this mode tslam_read_rig_poses returns
- * max_batch records (the first n_frames are the last fused batch). */
-int tslam_set_rig_ranks(tslam_handle* h, int world, const double* base_T_rect);
-int tslam_rig_fuse(tslam_handle* h, const void* gathered, int world, int64_t first_frame, int n_frames, void* stream);
 /* Body-frame results of the last batch (synchronises): per frame T_rel (body_{t-1} -> body_t
  * point map), T_abs (world_T_base, world = base at frame 0), 6x6 covariance, stats
- * {status, n_corr (all pairs), n_inliers, best candidate count, best candidate, frame, 0, 0}. */
-int tslam_read_rig_poses(tslam_handle* h, double* T_rel, double* T_abs, double* cov, int32_t* stats);
+ * {status, n_corr (all pairs), n_inliers, best candidate count, best candidate, frame, 0, 0}.
+ * Capacity and state errors as tslam_read_poses. */
+int tslam_read_rig_poses(tslam_handle* h, int max_frames, double* T_rel, double* T_abs, double* cov, int32_t* stats);
+
+/* Sharded rig: one camera stream per GPU (replaces cuVSLAM's multicam mode,
+ * launch/thor_visual_slam.launch.py:49,81, whose rig is RigCalibration.get_world_extrinsics,
+ * rig.py:35-70).  Every rank creates the same handle for the whole rig (all pairs, tslam_set_rig
+ * for a multi-pair rig), then tslam_set_shard(h, cam_lo, cam_hi, rank, world):
+ *   - its front stages (RECTIFY, DETECT, DESCRIBE) process cameras [cam_lo, cam_hi) of every frame
+ *     of a batch; tslam_begin_batch then takes images [n][cam_hi - cam_lo][H][W];
+ *   - its back stages (MATCH, POSE) process frames [rank*n/world, (rank+1)*n/world) of the batch
+ *     for every pair (plus the rig pose), after the other cameras of frames lo-1 .. hi-1 were
+ *     brought in: tslam_unpack_streams (the exchanged stream blocks) + tslam_import_raw (their raw
+ *     images, rectified into the ring);
+ *   - CHAIN chains the whole batch after tslam_unpack_poses of every rank's records.
+ * Per batch (s = the caller's stream order; collectives are the caller's, e.g. RCCL all-to-all /
+ * all-gather through torch.distributed):
+ *   begin_batch -> RECTIFY, DETECT, DESCRIBE -> pack_streams(frames lo_q-1.. for every rank q)
+ *   -> all-to-all (raw images + stream blocks) -> import_raw + unpack_streams -> MATCH, POSE
+ *   -> pack_poses -> all-gather -> unpack_poses -> KERNEL_CHAIN -> end_batch.
+ * Every rank then holds the same per-pair and rig poses as an unsharded handle fed all cameras.
+ * Requires n % world == 0 per batch, stereo (not RGB-D), ba_window == 0. */
+int tslam_set_shard(tslam_handle* h, int cam_lo, int cam_hi, int rank, int world);
+/* Bytes of one stream block (per frame and camera) and of one pose record (per frame). */
+int tslam_exchange_sizes(tslam_handle* h, int64_t* stream_block, int64_t* pose_record);
+/* Stream blocks of frames first_frame .. +n_frames-1 (global indices, ring-resident; frames < 0
+ * pack as zeros / are skipped on unpack) x cameras [cam_lo, cam_hi), frame-major, device memory. */
+int tslam_pack_streams(tslam_handle* h, int64_t first_frame, int n_frames, int cam_lo, int cam_hi, void* dst, void* stream);
+int tslam_unpack_streams(tslam_handle* h, int64_t first_frame, int n_frames, int cam_lo, int cam_hi, const void* src,
+                         void* stream);
+/* Rectify + pyramid raw images [n_frames][cam_hi - cam_lo][H][W] (device) of global frames
+ * first_frame.. into the ring (frames < 0 skipped). */
+int tslam_import_raw(tslam_handle* h, const uint8_t* images, int64_t first_frame, int n_frames, int cam_lo, int cam_hi,
+                     void* stream);
+/* Pose records (per frame: pose f64[P][68], rig pose f64[68], stats i32[P][8], rig stats i32[8])
+ * of this rank's frame range of the current batch -> dst; all n frames <- src (frame order). */
+int tslam_pack_poses(tslam_handle* h, void* dst, void* stream);
+int tslam_unpack_poses(tslam_handle* h, const void* src, void* stream);
 
 /* A8 window of stereo pair `pair` after the last enqueued solve (synchronises the device),
  * indexed by slot (slot = keyframe number mod ba_window): frames[W] (global frame, -1 = empty),
@@ -239,8 +266,6 @@ int tslam_ba_read_map(tslam_handle* h, int pair, int64_t* gid, uint32_t* desc);
  * tslam_read_poses (status 0 = relocalised); cam_T_world = identity when it fails. */
 int tslam_map_upload(tslam_handle* h, const double* xyz, const uint32_t* desc, int64_t n);
 int tslam_relocalize(tslam_handle* h, int pair, int64_t frame, double* cam_T_world, double* cov, int32_t* stats);
-
-int tslam_pack_features(tslam_handle* h, void* dst, int64_t* bytes, void* stream);
 
 /* Loop closure + keyframe pose graph (the reference only forwards
  * SlamConfig.enable_loop_closure, thor_slam/slam/interface.py:155-156, to cuVSLAM).  Spec and CPU

@@ -41,6 +41,37 @@ def scenario(seed: int = 0, n: int = 4, width: int = 640, height: int = 400, dis
     return {"cfg": cfg, "src": src, "rect": rect, "frames": frames, "oracle": results, "cams": cams}
 
 
+C3_SOURCES = ("192.168.2.21", "192.168.2.22", "192.168.2.23", "192.168.2.25")   # run_slam.py:45-50 CAMERA_MAP
+
+
+@functools.lru_cache(maxsize=4)
+def rig_scene(names: tuple = ("192.168.2.21", "192.168.2.25"), n: int = 6, traj_len: int = 40, width: int = 640,
+              height: int = 400):
+    """A multi-source rig on the brackets.urdf joints (tests/golden/brackets_joints.json) in one
+    shared room: product rectification, base_T_rect-left per pair, and frames [n][C][H][W] in the
+    global camera order of isaac_ros.py:138-157 (sorted source names x cam_idx)."""
+    import json
+    from pathlib import Path
+
+    from thor_slam_amd.camera import Extrinsics
+    from thor_slam_amd.synthetic import RoomScene, circle_trajectory
+
+    mats = json.loads((Path(__file__).parent / "golden" / "brackets_joints.json").read_text())
+    scene = RoomScene(seed=0)
+    traj = circle_trajectory(traj_len)
+    srcs = [SyntheticStereoSource(name=nm, scene=scene, trajectory=traj, rig_T_source=np.array(mats[nm]), seed=k,
+                                  width=width, height=height) for k, nm in enumerate(names)]
+    rig = CameraRig(srcs, rig_extrinsics={nm: Extrinsics.from_4x4_matrix(np.array(mats[nm])) for nm in names})
+    cams = extract_cameras(rig.calibration, 2 * len(names))
+    pairs = stereo_pairs(cams)
+    rects = [stereo_rectify(cams[l], cams[r]) for l, r in pairs]
+    E = [cams[l].extrinsics.to_4x4_matrix() @ r.left_optical_T_rect() for (l, _), r in zip(pairs, rects)]
+    by_name = {s.name: s for s in srcs}
+    frames = np.stack([np.stack([by_name[cams[l].source_name].render_image(i, c) for l, _ in pairs for c in (0, 1)])
+                       for i in range(n)])
+    return {"frames": frames, "rects": rects, "E": E, "traj": traj, "cams": cams, "pairs": pairs, "sources": srcs}
+
+
 def rel_frobenius(a: np.ndarray, b: np.ndarray) -> float:
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
 

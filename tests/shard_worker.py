@@ -1,0 +1,41 @@
+"""One rank of tests/test_gpu_shard.py::test_dist_shard_gloo_two_processes (launched by
+torch.distributed.run): the 2-pair bracket rig sharded over WORLD_SIZE processes with
+DistShardedRig on the gloo backend; writes its per-batch poses to <out>/rank<r>.json."""
+
+from __future__ import annotations
+
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from helpers import rig_scene
+from thor_slam_amd.params import HipSlamConfig
+from thor_slam_amd.shard import DistShardedRig
+
+
+def main() -> None:
+    out, batch, nb = Path(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    torch.cuda.set_device(0)
+    sc = rig_scene(("192.168.2.21", "192.168.2.25"), batch * nb)
+    rig = DistShardedRig(sc["rects"], HipSlamConfig(), batch, base_T_rect=sc["E"])
+    S = rig.plan.streams_per_rank
+    mine = torch.from_numpy(np.ascontiguousarray(sc["frames"][:, rank * S:(rank + 1) * S])).cuda()
+    res = []
+    for b in range(nb):
+        rig.step(mine[b * batch:(b + 1) * batch])
+        r = rig.read()
+        res.append({part: {k: np.asarray(v).tolist() for k, v in r[part].items() if k != "cov"} for part in r})
+    rig.close()
+    (out / f"rank{rank}.json").write_text(json.dumps(res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

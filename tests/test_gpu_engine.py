@@ -143,38 +143,35 @@ def test_engine_two_source_rig_solves_body_motion():
     eng.shutdown()
 
 
-def test_pack_features_matches_host_block():
-    """tslam_pack_features (device gather) == dist.pack_block of the handle's own outputs."""
+def test_stream_blocks_roundtrip():
+    """tslam_pack_streams (ring -> exchange blocks) then tslam_unpack_streams into a second
+    handle: every ring buffer the back end reads (keypoints, level counts, y-sorted records and
+    descriptors, row index) is byte-identical; frames before the sequence start pack as zeros."""
     import torch
 
     from thor_slam_amd._lib import Handle
-    from thor_slam_amd.dist import BlockLayout, pack_block, unpack_rank_block
 
     sc = scenario(seed=0, n=3)
     cfg, rect = sc["cfg"], sc["rect"]
     n = 3
     h = Handle([rect], cfg, max_batch=n)
+    h2 = Handle([rect], cfg, max_batch=n)
     dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
     s = torch.cuda.current_stream().cuda_stream
     h.submit(dev.data_ptr(), n, s)
-    res = h.read_poses(n)
-    layout = BlockLayout(n_frames=n, n_cams=2, K=cfg.n_features, L=cfg.n_levels)
-    out = torch.zeros(layout.rank_bytes, dtype=torch.uint8, device="cuda")
-    assert h.pack_features(out.data_ptr(), s) == layout.rank_bytes
+    block, _ = h.exchange_sizes()
+    out = torch.full((n + 1, 2, block), 7, dtype=torch.uint8, device="cuda")
+    h.pack_streams(-1, n + 1, 0, 2, out.data_ptr(), s)
+    h2.unpack_streams(-1, n + 1, 0, 2, out.data_ptr(), s)
     torch.cuda.synchronize()
-    got = out.cpu().numpy()
-    kps = np.zeros((n, 2, layout.K, 2), np.uint32)
-    desc = np.zeros((n, 2, layout.K, 8), np.uint32)
-    counts = np.zeros((n, 2, layout.L), np.int32)
-    for f in range(n):
-        for cam in range(2):
-            k = h.keypoints(f, cam)
-            kps[f, cam, :, 0] = k["x"] | (k["y"] << 16)
-            kps[f, cam, :, 1] = k["level"] | (k["angle"] << 8) | (k["score"] << 16)
-            desc[f, cam] = k["desc"]
-            counts[f, cam] = k["counts"]
-    want = pack_block(layout, kps, desc, counts, res["T_rel"], res["cov"], res["stats"])
-    np.testing.assert_array_equal(got, want)
-    dec = unpack_rank_block(layout, got)
-    np.testing.assert_array_equal(dec["stats"], res["stats"])
+    K, L = cfg.n_features, cfg.n_levels
+    assert not out[0, :, :K * 8 + 4 * L].any()                 # frame -1: zeros
+    for which in ("keypoints", "kcount", "ysorted", "desc_ys", "rowstart"):
+        for g in range(n):
+            np.testing.assert_array_equal(h2.frame_block(which, h2.ring_slot(g), np.uint8),
+                                          h.frame_block(which, h.ring_slot(g), np.uint8), err_msg=which)
+    kp = out[1, 0, :K * 8].cpu().numpy().view(np.uint32).reshape(K, 2)
+    want = h.keypoints(0, 0)
+    np.testing.assert_array_equal(kp[:, 0] & 0xFFFF, want["x"])
     h.close()
+    h2.close()

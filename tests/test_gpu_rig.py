@@ -9,39 +9,23 @@ motions and chained world_T_base within 1e-9 relative Frobenius.
 from __future__ import annotations
 
 import functools
-import json
-from pathlib import Path
 
 import numpy as np
 import pytest
 
-from helpers import rel_frobenius
+from helpers import C3_SOURCES, rel_frobenius, rig_scene
 from oracle import numpy_slam as O
 from oracle.numpy_rig import RigChain, rig_pose
-from thor_slam_amd.calib import extract_cameras, stereo_pairs, stereo_rectify
-from thor_slam_amd.camera import CameraRig, Extrinsics
 from thor_slam_amd.params import HipSlamConfig
-from thor_slam_amd.synthetic import RoomScene, SyntheticStereoSource, circle_trajectory
 
 pytestmark = pytest.mark.gpu
-NAMES = ["192.168.2.21", "192.168.2.25"]
+NAMES = ("192.168.2.21", "192.168.2.25")
 
 
 @functools.lru_cache(maxsize=2)
-def rig_scenario(n: int = 6):
-    mats = json.loads((Path(__file__).parent / "golden" / "brackets_joints.json").read_text())
-    scene = RoomScene(seed=0)
-    traj = circle_trajectory(40)
-    srcs = [SyntheticStereoSource(name=nm, scene=scene, trajectory=traj, rig_T_source=np.array(mats[nm]), seed=k)
-            for k, nm in enumerate(NAMES)]
-    rig = CameraRig(srcs, rig_extrinsics={nm: Extrinsics.from_4x4_matrix(np.array(mats[nm])) for nm in NAMES})
-    cams = extract_cameras(rig.calibration, 4)
-    pairs = stereo_pairs(cams)
-    rects = [stereo_rectify(cams[l], cams[r]) for l, r in pairs]
-    E = [cams[l].extrinsics.to_4x4_matrix() @ r.left_optical_T_rect() for (l, _), r in zip(pairs, rects)]
-    by_name = {s.name: s for s in srcs}
-    frames = np.stack([np.stack([by_name[cams[l].source_name].render_image(i, c) for l, _ in pairs for c in (0, 1)])
-                       for i in range(n)])   # [n][4][H][W]
+def rig_scenario(n: int = 6, names: tuple = NAMES):
+    sc = dict(rig_scene(tuple(names), n))
+    frames, rects, E = sc["frames"], sc["rects"], sc["E"]
     cfg = HipSlamConfig()
     trks = [O.OracleTracker(cfg, dict(fx=r.fx, fy=r.fy, cx=r.cx, cy=r.cy, baseline=r.baseline, map_l=r.map_left,
                                       map_r=r.map_right)) for r in rects]
@@ -57,7 +41,7 @@ def rig_scenario(n: int = 6):
         res = rig_pose(items, E, cfg)
         res["T_abs"] = chain.step(res)
         want.append(res)
-    return {"frames": frames, "rects": rects, "E": E, "cfg": cfg, "want": want, "traj": traj}
+    return {"frames": frames, "rects": rects, "E": E, "cfg": cfg, "want": want, "traj": sc["traj"]}
 
 
 @pytest.mark.parametrize("batch", [6, 2])
@@ -113,44 +97,32 @@ def test_rig_pose_survives_a_blind_pair():
     assert np.linalg.norm(r["T_abs"][5][:3, 3] - gt[:3, 3]) < 0.1 * np.linalg.norm(gt[:3, 3]) + 2e-3
 
 
-def test_rig_fusion_across_ranks_matches_numpy():
-    """Multi-GPU layout rehearsed on one GPU: one handle per pair ("rank"), their packed blocks
-    concatenated as the all-gather would, fused on the device (tslam_rig_fuse) vs numpy."""
+def check_rig_against_oracle(sc, got):
+    for i, (g, w) in enumerate(zip(got, sc["want"])):
+        assert g["stats"][0] == w["status"], i
+        if i == 0:
+            continue
+        assert g["stats"][4] == w["best"] and abs(int(g["stats"][2]) - w["n_inliers"]) <= 2, (i, g["stats"], w)
+        assert rel_frobenius(g["T_rel"], w["T"]) < 1e-9, i
+        assert rel_frobenius(g["T_abs"], w["T_abs"]) < 1e-9, i
+        assert rel_frobenius(g["cov"], w["cov"]) < 1e-6, i
+
+
+def test_c3_eight_stream_rig_matches_oracle():
+    """BASELINE.json configs[2] (C3): the four OAK sources of run_slam.py:45-50 on the
+    brackets.urdf joints, 8 streams / 4 stereo pairs, one handle on one GPU, 5 frames against the
+    oracle's per-pair trackers + rig pose (oracle/numpy_rig.py)."""
     import torch
 
-    from oracle.numpy_rig import RigChain, fuse_information
     from thor_slam_amd._lib import Handle
 
-    sc = rig_scenario()
-    n = 6
-    stream = torch.cuda.current_stream().cuda_stream
-    handles, blocks, per = [], [], []
-    for q in range(2):
-        h = Handle([sc["rects"][q]], sc["cfg"], max_batch=n)
-        dev = torch.from_numpy(np.ascontiguousarray(sc["frames"][:, 2 * q:2 * q + 2])).cuda()
-        h.submit(dev.data_ptr(), n, stream)
-        per.append(h.read_poses(n))
-        blk = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
-        nb = h.pack_features(blk.data_ptr(), stream)
-        blocks.append(blk[:nb])
-        handles.append(h)
-    gathered = torch.cat(blocks).contiguous()
-    h0 = handles[0]
-    h0.set_rig_ranks(sc["E"])
-    h0.rig_fuse(gathered.data_ptr(), 2, 0, n, stream)
-    got = h0.read_rig_poses(n)
-    for h in handles:
-        h.close()
-    chain = RigChain()
-    for f in range(n):
-        items = [(int(per[q]["stats"][f, 0, 0]), per[q]["T_rel"][f, 0], per[q]["cov"][f, 0]) for q in range(2)]
-        w = fuse_information(items, sc["E"])
-        w_abs = chain.step(w)
-        assert got["stats"][f, 0] == w["status"], f
-        if w["status"] == 0:
-            assert got["stats"][f, 1] == w["used"] == 2
-            assert rel_frobenius(got["T_rel"][f], w["T"]) < 1e-9
-            assert rel_frobenius(got["cov"][f], w["cov"]) < 1e-6
-        assert rel_frobenius(got["T_abs"][f], w_abs) < 1e-9
-    gt = np.linalg.inv(sc["traj"][0]) @ sc["traj"][n - 1]
-    assert np.linalg.norm(got["T_abs"][n - 1][:3, 3] - gt[:3, 3]) < 0.1 * np.linalg.norm(gt[:3, 3]) + 2e-3
+    sc = rig_scenario(5, C3_SOURCES)
+    assert sc["frames"].shape[1] == 8
+    h = Handle(sc["rects"], sc["cfg"], max_batch=5)
+    h.set_rig(sc["E"])
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    h.submit(dev.data_ptr(), 5, torch.cuda.current_stream().cuda_stream)
+    r = h.read_rig_poses(5)
+    h.close()
+    check_rig_against_oracle(sc, [{k: r[k][f] for k in r} for f in range(5)])
+    assert (r["stats"][1:, 0] == 0).all()

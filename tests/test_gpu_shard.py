@@ -1,0 +1,115 @@
+"""Sharded rig: one camera stream per GPU, RCCL all-to-all of raw images + stream
+blocks, per-pair A6/A7 + rig pose on each rank's frame range, all-gather of pose records.
+
+Every rank must end each batch with exactly (bit for bit) the per-pair and rig poses of one
+unsharded handle fed all cameras (which tests/test_gpu_rig.py checks against the oracle), and
+the ring slots a rank imported must hold the other ranks' keypoints byte for byte.  The ranks
+run in one process on one GPU (LocalShardedRig: the collectives become device copies; the
+handles, kernels and buffers are the ones the multi-process path uses);
+test_dist_shard_gloo_two_processes runs the real torch.distributed path with 2 processes.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from helpers import C3_SOURCES, rig_scene
+from thor_slam_amd.params import HipSlamConfig
+
+pytestmark = pytest.mark.gpu
+TWO = ("192.168.2.21", "192.168.2.25")
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def unsharded(sc, cfg, batch, n_batches):
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    h = Handle(sc["rects"], cfg, max_batch=batch)
+    h.set_rig(sc["E"])
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    out = []
+    for b in range(n_batches):
+        h.submit(dev[b * batch].data_ptr(), batch, torch.cuda.current_stream().cuda_stream)
+        out.append({"pairs": h.read_poses(batch), "rig": h.read_rig_poses(batch)})
+    kps = h.keypoints(n_batches * batch - 1, 0)
+    h.close()
+    return out, kps
+
+
+def assert_identical(got, want):
+    for part in ("pairs", "rig"):
+        for k in ("T_rel", "T_abs", "cov", "stats"):
+            np.testing.assert_array_equal(got[part][k], want[part][k], err_msg=f"{part}.{k}")
+
+
+@pytest.mark.parametrize("world,exchange", [(2, "alltoall"), (4, "alltoall"), (4, "allgather")])
+def test_sharded_two_pair_rig_identical(world, exchange):
+    """4 cameras over 2 ranks (a pair per rank) or 4 ranks (one stream per rank), 3 batches."""
+    import torch
+
+    from thor_slam_amd.shard import LocalShardedRig
+
+    batch, nb = 4, 3
+    sc = rig_scene(TWO, batch * nb)
+    cfg = HipSlamConfig()
+    want, kps = unsharded(sc, cfg, batch, nb)
+    rig = LocalShardedRig(sc["rects"], cfg, world=world, batch=batch, base_T_rect=sc["E"], exchange=exchange)
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    for b in range(nb):
+        rig.step(dev[b * batch:(b + 1) * batch])
+        for r in range(world):
+            assert_identical(rig.read(r), want[b])
+    assert (want[-1]["rig"]["stats"][:, 0] == 0).all()
+    # the last rank solves the batch's last frame: camera 0's keypoints there came over the exchange
+    got = rig.ranks[world - 1].h.keypoints(nb * batch - 1, 0)
+    for k in ("x", "y", "level", "score", "counts"):
+        np.testing.assert_array_equal(got[k], kps[k])
+    rig.close()
+
+
+def test_sharded_c3_one_stream_per_rank_identical():
+    """C3 (BASELINE.json configs[2]): the four OAK sources of run_slam.py:45-50, 8 streams, one
+    stream per rank on 8 ranks, 2 batches of 8 frames, identical to the unsharded rig."""
+    import torch
+
+    from thor_slam_amd.shard import LocalShardedRig
+
+    batch, nb = 8, 2
+    sc = rig_scene(C3_SOURCES, batch * nb)
+    cfg = HipSlamConfig()
+    want, _ = unsharded(sc, cfg, batch, nb)
+    rig = LocalShardedRig(sc["rects"], cfg, world=8, batch=batch, base_T_rect=sc["E"])
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    for b in range(nb):
+        rig.step(dev[b * batch:(b + 1) * batch])
+        for r in (0, 3, 7):
+            assert_identical(rig.read(r), want[b])
+    assert (want[-1]["rig"]["stats"][:, 0] == 0).all()
+    rig.close()
+
+
+def test_dist_shard_gloo_two_processes(tmp_path):
+    """The torch.distributed path (DistShardedRig) with 2 processes on this GPU, gloo (host-staged
+    collectives), 2 pairs, one pair per rank, 2 batches: both ranks == the unsharded handle."""
+    batch, nb = 4, 2
+    sc = rig_scene(TWO, batch * nb)
+    want, _ = unsharded(sc, HipSlamConfig(), batch, nb)
+    env = dict(os.environ, PYTHONPATH=f"{ROOT}:{ROOT / 'thor-slam_amd'}:{ROOT / 'tests'}")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1",
+           "--master-port=29517", str(ROOT / "tests" / "shard_worker.py"), str(tmp_path), str(batch), str(nb)]
+    subprocess.run(cmd, check=True, env=env, timeout=240)
+    for r in range(2):
+        got = json.loads((tmp_path / f"rank{r}.json").read_text())
+        for b in range(nb):
+            for part in ("pairs", "rig"):
+                for k in ("T_rel", "T_abs", "stats"):
+                    np.testing.assert_array_equal(np.array(got[b][part][k]), want[b][part][k], err_msg=f"{r} {b} {part}.{k}")

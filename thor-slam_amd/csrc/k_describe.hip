@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void k_describe(BatchCtx c) {
     // block -> (image, level, tile); all tiles of one image on one XCD (tile geometry from the
     // host: no scalar divisions per block beyond the tile's row)
     int img, local;
-    if (!xcd_image_block(blockIdx.x, c.n * c.C, c.g.dt_total, &img, &local)) return;
+    if (!xcd_image_block(blockIdx.x, c.n * c.ncam, c.g.dt_total, &img, &local)) return;
     int l = 0;
     while (l + 1 < c.g.n_levels && local >= c.g.dt_start[l + 1]) ++l;
     local -= c.g.dt_start[l];
@@ -69,7 +69,8 @@ __global__ __launch_bounds__(256) void k_describe(BatchCtx c) {
     const int ty = local / nx, tx = local - ty * nx;
     const int W = c.g.W[l], H = c.g.H[l];
     const int x0 = tx * TS_DT_W, y0 = ty * TS_DT_H;
-    const int cam = img % c.C, f = img / c.C;
+    int cam, f;
+    view_image(c, img, &f, &cam);
     const int slot = ring_slot(c, c.g0 + f);
     const size_t ib = (size_t)slot * c.C + cam;
     const uint8_t* raw = c.pyr + ib * c.g.pyr_bytes + c.g.pyr_off[l];
@@ -204,5 +205,5 @@ __global__ __launch_bounds__(256) void k_describe(BatchCtx c) {
 }
 
 void launch_describe(const BatchCtx& c, hipStream_t s) {
-    hipLaunchKernelGGL(k_describe, dim3(xcd_grid(c.n * c.C, c.g.dt_total)), dim3(256), 0, s, c);
+    hipLaunchKernelGGL(k_describe, dim3(xcd_grid(c.n * c.ncam, c.g.dt_total)), dim3(256), 0, s, c);
 }

@@ -37,9 +37,9 @@ __device__ __forceinline__ uint32_t box4(uint32_t r0a, uint32_t r0b, uint32_t r1
 
 __global__ __launch_bounds__(256) void k_rectify_pyramid(BatchCtx c) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int img = blockIdx.y;             // f * C + cam
-    const int cam = img % c.C;
-    const int f = img / c.C;
+    const int img = blockIdx.y;             // f * ncam + view camera
+    int f, cam;
+    view_image(c, img, &f, &cam);
     const int W = c.W, H = c.H;
     const int y0 = blockIdx.x * TS_RECT_BAND;
     const int rows0 = min(TS_RECT_BAND, H - y0);
@@ -341,8 +341,8 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
     __shared__ uint32_t s_hist[256];
     __shared__ uint32_t s_count;
     const int img = blockIdx.y;
-    const int cam = img % c.C;
-    const int f = img / c.C;
+    int f, cam;
+    view_image(c, img, &f, &cam);
     int l = 0;
     while (l + 1 < c.g.n_levels && (int)blockIdx.x >= c.g.band_start[l + 1]) ++l;
     const int band = blockIdx.x - c.g.band_start[l];
@@ -675,8 +675,8 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
     __shared__ uint32_t s_before, s_nsel, s_flag;
     const int l = blockIdx.y;
     const int img = blockIdx.x;
-    const int cam = img % c.C;
-    const int f = img / c.C;
+    int f, cam;
+    view_image(c, img, &f, &cam);
     const int Kl = c.g.Kq[l];
     const uint32_t* cand = c.cand + ((size_t)f * c.C + cam) * c.g.cand_total + c.g.cand_off[l];
     const uint32_t* cnt = c.ccount + ((size_t)f * c.C + cam) * c.g.total_bands + c.g.band_start[l];
@@ -879,18 +879,22 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
 void launch_rectify_pyramid(const BatchCtx& c, hipStream_t s) {
     size_t lds = 0;
     for (int l = 0; l < c.g.n_levels; ++l) lds += (size_t)(TS_RECT_BAND >> l) * c.g.W[l];
-    dim3 grid((c.H + TS_RECT_BAND - 1) / TS_RECT_BAND, c.n * c.C);
+    dim3 grid((c.H + TS_RECT_BAND - 1) / TS_RECT_BAND, c.n * c.ncam);
     hipLaunchKernelGGL(k_rectify_pyramid, grid, dim3(256), lds, s, c);
 }
 
 void launch_detect(const BatchCtx& c, hipStream_t s) {
     const size_t lds = (size_t)(c.g.band_rows + 2 * TS_DET_HALO + c.g.band_rows + 2) * c.g.W[0];
-    dim3 grid(c.g.total_bands, c.n * c.C);
-    (void)hipMemsetAsync(c.hist, 0, sizeof(uint32_t) * 256 * c.g.n_levels * c.C * (size_t)c.n, s);
+    dim3 grid(c.g.total_bands, c.n * c.ncam);
+    const size_t per_cam = sizeof(uint32_t) * 256 * c.g.n_levels;   // hist [B][C][L][256]: the view's cameras
+    if (c.ncam == c.C)
+        (void)hipMemsetAsync(c.hist, 0, per_cam * c.C * (size_t)c.n, s);
+    else
+        (void)hipMemset2DAsync(reinterpret_cast<uint8_t*>(c.hist) + per_cam * c.cam0, per_cam * c.C, 0, per_cam * c.ncam, c.n, s);
     hipLaunchKernelGGL(k_detect, grid, dim3(TS_DET_THREADS), lds, s, c);
 }
 
 void launch_select(const BatchCtx& c, hipStream_t s) {
-    dim3 grid(c.n * c.C, c.g.n_levels);
+    dim3 grid(c.n * c.ncam, c.g.n_levels);
     hipLaunchKernelGGL(k_select, grid, dim3(SEL_THREADS), 0, s, c);
 }

@@ -32,7 +32,8 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     __shared__ uint32_t s_qi[4][64];
     // blockIdx.y: the temporal blocks (the heavy ones: a window of rows, not a row band) of every
     // frame first, then the stereo blocks, so the short stereo blocks fill the launch's tail
-    const int nfp = c.n * c.P;
+    // (stereo-only launches, match_modes == 1: blockIdx.y = f * P + p, all stereo)
+    const int nfp = c.match_modes == 1 ? 0 : c.n * c.P;
     const int z = blockIdx.y;
     const int mode = z < nfp ? 1 : 0;
     const int fp = z < nfp ? z : z - nfp;     // f * P + p
@@ -431,8 +432,19 @@ __global__ __launch_bounds__(256) void k_refine_temporal(BatchCtx c) {
 void launch_match(const BatchCtx& c, hipStream_t s) {
     (void)hipMemsetAsync(c.tbest, 0xFF, sizeof(uint32_t) * (size_t)c.n * c.P * 2 * c.g.K, s);
     (void)hipMemsetAsync(c.qbest, 0xFF, sizeof(uint32_t) * (size_t)c.n * c.P * 2 * c.g.K, s);
-    dim3 grid(c.g.total_qtiles, c.n * c.P * 2);
+    dim3 grid(c.g.total_qtiles, c.n * c.P * (c.match_modes == 1 ? 1 : 2));
     hipLaunchKernelGGL(k_match, grid, dim3(256), 0, s, c);
+}
+
+// Stereo matching + refinement only (the sharded rig's pre-pass for the frame before a rank's
+// range, whose disparities the range's first frame triangulates from).
+void launch_match_stereo(const BatchCtx& c, hipStream_t s) {
+    BatchCtx st = c;
+    st.match_modes = 1;
+    (void)hipMemsetAsync(st.tbest, 0xFF, sizeof(uint32_t) * (size_t)st.n * st.P * 2 * st.g.K, s);
+    (void)hipMemsetAsync(st.qbest, 0xFF, sizeof(uint32_t) * (size_t)st.n * st.P * 2 * st.g.K, s);
+    hipLaunchKernelGGL(k_match, dim3(st.g.total_qtiles, st.n * st.P), dim3(256), 0, s, st);
+    hipLaunchKernelGGL(k_refine_stereo, dim3(xcd_grid(st.n * st.P, (st.g.K + TS_RS_QPB - 1) / TS_RS_QPB)), dim3(256), 0, s, st);
 }
 
 void launch_match_refine(const BatchCtx& c, hipStream_t s) {

@@ -906,8 +906,12 @@ __global__ __launch_bounds__(POSE_THREADS) void k_rig_pose(BatchCtx c) {
     }
 }
 
-void launch_rig(const BatchCtx& c, hipStream_t s) {
+void launch_rig_pose(const BatchCtx& c, hipStream_t s) {
     hipLaunchKernelGGL(k_rig_pose, dim3(c.n), dim3(POSE_THREADS), 0, s, c);
+}
+
+void launch_rig(const BatchCtx& c, hipStream_t s) {
+    launch_rig_pose(c, s);
     launch_rig_chain(c, s);
 }
 

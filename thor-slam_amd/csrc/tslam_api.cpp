@@ -52,7 +52,7 @@ struct tslam_handle {
     uint8_t* d_gray = nullptr;   // RGB-D: converted colour images [B][P][H][W]
     // rig pose (tslam_set_rig): E = base_T_rect-left per pair, its inverse, body-frame results
     bool rig = false;
-    int rig_world = 0, rig_q = 0, rig_cap = 0;   // ranks mode: world size; E entries; allocated
+    int rig_q = 0, rig_cap = 0;   // E entries set; allocated
     double* d_rig_E = nullptr;
     double* d_rig_pose = nullptr;
     int32_t* d_rig_stats = nullptr;
@@ -123,6 +123,9 @@ struct tslam_handle {
     hipEvent_t ev_front = nullptr, ev_back[2] = {nullptr, nullptr};
     bool back_pending[2] = {false, false};
     std::vector<hipEvent_t> ba_events;
+    // sharded rig (tslam_set_shard): front-end cameras [sh_cam_lo, sh_cam_hi) and back-end frames
+    // [rank * n / world, (rank + 1) * n / world) of every batch
+    int sh_cam_lo = 0, sh_cam_hi = 0, sh_rank = 0, sh_world = 1;
 };
 
 static int dev_alloc(tslam_handle* h, void** p, size_t bytes) {
@@ -347,7 +350,92 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.pp.seed = h->prm.ransac_seed;
     c.fast_threshold = h->prm.fast_threshold;
     c.margin = h->prm.edge_margin;
+    c.cam0 = h->sh_cam_lo;
+    c.ncam = h->sh_cam_hi - h->sh_cam_lo;
+    c.match_modes = 3;
     return c;
+}
+
+// The back-end context of batch frames [lo, hi): frame lo is the context's frame 0 and every
+// batch-indexed buffer is offset to batch frame lo, so results land where a whole-batch run puts
+// them (ring-indexed buffers need no offset: they are addressed by global frame).
+static BatchCtx range_ctx(const BatchCtx& c, int lo, int hi) {
+    BatchCtx r = c;
+    const size_t P = c.P, K = c.g.K, f = lo;
+    r.g0 = c.g0 + lo;
+    r.n = hi - lo;
+    r.qbest += f * P * 2 * K;
+    r.qsecond += f * P * 2 * K;
+    r.tbest += f * P * 2 * K;
+    r.tuv += f * P * K * 2;
+    r.corr += f * P * K * TS_CORR_DOUBLES;
+    r.pose += f * P * TS_POSE_DOUBLES;
+    r.stats += f * P * TS_STATS_INTS;
+    r.ransac += f * P * TS_MAX_SPLITS * TS_RANSAC_WORDS / 2;
+    r.hyp += f * P * 4 * (size_t)c.pp.n_hyp * 12;
+    if (r.prior) r.prior += f * P * TS_PRIOR_DOUBLES;
+    if (r.rig_pose) r.rig_pose += f * TS_POSE_DOUBLES;
+    if (r.rig_stats) r.rig_stats += f * TS_STATS_INTS;
+    return r;
+}
+
+static void shard_range(const tslam_handle* h, int n, int* lo, int* hi) {
+    *lo = h->sh_rank * n / h->sh_world;
+    *hi = (h->sh_rank + 1) * n / h->sh_world;
+}
+
+// Stages of a sharded handle (tslam_set_shard, world > 1).  Front stages run on the handle's
+// cameras for every frame of the batch; back stages on the rank's frame range [lo, hi) of the
+// batch, after the exchange has filled the other cameras' ring slots for frames lo-1 .. hi-1:
+// MATCH first re-derives the stereo disparities of frame lo-1 (the range's first frame
+// triangulates from them; the rank that owns lo-1 computes the same values), POSE adds the rig
+// pose of the range (no chaining), and CHAIN chains the whole batch once every rank's pose
+// records are back (tslam_unpack_poses), identically on every rank.
+static int run_sharded_stage(tslam_handle* h, const BatchCtx& c, int stage, hipStream_t s) {
+    int lo, hi;
+    shard_range(h, c.n, &lo, &hi);
+    const BatchCtx cb = range_ctx(c, lo, hi);
+    const bool pre = c.g0 + lo - 1 >= 0;   // frame lo - 1 exists
+    BatchCtx cp = c;                        // the pre-pass: frame lo - 1, batch scratch at frame 0
+    cp.g0 = c.g0 + lo - 1;
+    cp.n = 1;
+    switch (stage) {
+        case TSLAM_STAGE_RECTIFY: launch_rectify_pyramid(c, s); break;
+        case TSLAM_STAGE_DETECT: launch_detect(c, s); launch_select(c, s); break;
+        case TSLAM_STAGE_DESCRIBE: launch_describe(c, s); break;
+        case TSLAM_KERNEL_RECTIFY_PYRAMID: launch_rectify_pyramid(c, s); break;
+        case TSLAM_KERNEL_DETECT: launch_detect(c, s); break;
+        case TSLAM_KERNEL_SELECT: launch_select(c, s); break;
+        case TSLAM_KERNEL_DESCRIBE: launch_describe(c, s); break;
+        case TSLAM_STAGE_MATCH:
+            if (pre) launch_match_stereo(cp, s);
+            launch_match(cb, s);
+            launch_match_refine(cb, s);
+            break;
+        case TSLAM_KERNEL_MATCH:
+            if (pre) launch_match_stereo(cp, s);
+            launch_match(cb, s);
+            break;
+        case TSLAM_KERNEL_MATCH_REFINE: launch_match_refine(cb, s); break;
+        case TSLAM_STAGE_POSE:
+            launch_pose(cb, s);
+            if (h->rig) launch_rig_pose(cb, s);
+            break;
+        case TSLAM_KERNEL_POSE: launch_pose(cb, s); break;
+        case TSLAM_KERNEL_RIG:
+            if (!h->rig) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig)");
+            launch_rig_pose(cb, s);
+            break;
+        case TSLAM_KERNEL_CHAIN:
+            launch_chain(c, s);
+            if (h->rig) launch_rig_chain(c, s);
+            break;
+        default:
+            return fail(TSLAM_ESTATE, "a sharded handle runs its stages one by one around the exchange "
+                                      "(RECTIFY..DESCRIBE, pack/exchange/unpack, MATCH, POSE, exchange, CHAIN)");
+    }
+    HIPCHK(hipGetLastError());
+    return TSLAM_OK;
 }
 
 extern "C" {
@@ -396,6 +484,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     h->P = p.n_pairs;
     h->C = (p.rgbd ? 1 : 2) * p.n_pairs;
     h->B = p.max_batch;
+    h->sh_cam_hi = h->C;
     // the ring keeps frame t-1 of a batch's first frame; with BA it also keeps the frames a
     // keyframe's temporal match chain walks back over
     // the ring keeps frame t-1 of a batch's first frame while the front stages of the next batch
@@ -611,6 +700,7 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
         return fail(TSLAM_ESTATE, "all back stages of a batch must use one stream");
     if (stage != TSLAM_STAGE_BA) h->last_stream = s;
     const BatchCtx c = make_ctx(h);
+    if (h->sh_world > 1) return run_sharded_stage(h, c, stage, s);
     if (h->prm.rgbd && (stage == TSLAM_STAGE_RECTIFY || stage == TSLAM_STAGE_ALL || stage == TSLAM_KERNEL_RECTIFY_PYRAMID))
         launch_rgbd_gray(c, h->d_gray, s);   // the colour images become the gray input of rectify
     switch (stage) {
@@ -705,21 +795,28 @@ int tslam_sync(tslam_handle* h) {
     return TSLAM_OK;
 }
 
-int tslam_read_poses(tslam_handle* h, double* T_rel, double* T_abs, double* cov, int32_t* stats) {
-    if (!h) return fail(TSLAM_EINVAL, "null handle");
-    int rc = tslam_sync(h);
-    if (rc != TSLAM_OK) return rc;
-    const int n = h->cur_n * h->P;
+static int copy_pose_records(const double* dev_pose, const int32_t* dev_stats, int n, double* T_rel, double* T_abs,
+                             double* cov, int32_t* stats) {
     std::vector<double> pose((size_t)n * TS_POSE_DOUBLES);
-    HIPCHK(hipMemcpy(pose.data(), h->buf[TSLAM_BUF_POSE].ptr, sizeof(double) * pose.size(), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(pose.data(), dev_pose, sizeof(double) * pose.size(), hipMemcpyDeviceToHost));
     for (int i = 0; i < n; ++i) {
         const double* src = pose.data() + (size_t)i * TS_POSE_DOUBLES;
         if (T_rel) memcpy(T_rel + 16 * (size_t)i, src, 16 * sizeof(double));
         if (T_abs) memcpy(T_abs + 16 * (size_t)i, src + 16, 16 * sizeof(double));
         if (cov) memcpy(cov + 36 * (size_t)i, src + 32, 36 * sizeof(double));
     }
-    if (stats) HIPCHK(hipMemcpy(stats, h->buf[TSLAM_BUF_STATS].ptr, sizeof(int32_t) * TS_STATS_INTS * (size_t)n, hipMemcpyDeviceToHost));
+    if (stats) HIPCHK(hipMemcpy(stats, dev_stats, sizeof(int32_t) * TS_STATS_INTS * (size_t)n, hipMemcpyDeviceToHost));
     return TSLAM_OK;
+}
+
+int tslam_read_poses(tslam_handle* h, int max_frames, double* T_rel, double* T_abs, double* cov, int32_t* stats) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (h->cur_n == 0) return fail(TSLAM_ESTATE, "no batch has run since tslam_create / tslam_reset");
+    if (max_frames < h->cur_n) return fail(TSLAM_EINVAL, "output capacity (max_frames) is smaller than the last batch");
+    int rc = tslam_sync(h);
+    if (rc != TSLAM_OK) return rc;
+    return copy_pose_records((const double*)h->buf[TSLAM_BUF_POSE].ptr, (const int32_t*)h->buf[TSLAM_BUF_STATS].ptr,
+                             h->cur_n * h->P, T_rel, T_abs, cov, stats);
 }
 
 int tslam_buffer_info(tslam_handle* h, int which, void** device_ptr, int64_t* bytes_total, int64_t* bytes_per_frame) {
@@ -775,20 +872,6 @@ int tslam_layout(tslam_handle* h, int64_t* out16, int32_t* level_info18) {
             level_info18[3 * l + 2] = h->g.Kq[l];
         }
     }
-    return TSLAM_OK;
-}
-
-int tslam_pack_features(tslam_handle* h, void* dst, int64_t* bytes, void* stream) {
-    if (!h || !dst) return fail(TSLAM_EINVAL, "bad argument");
-    const int64_t K = h->g.K, L = h->g.n_levels;
-    const int64_t per_cam = K * 8 + K * 32 + L * 4;
-    const int64_t feat = (int64_t)h->cur_n * h->C * per_cam;
-    const int64_t pose_bytes = (16 + 36) * 8 + TS_STATS_INTS * 4;
-    if (bytes) *bytes = feat + (int64_t)h->cur_n * h->P * pose_bytes;
-    HIPCHK(hipSetDevice(h->device));
-    const BatchCtx c = make_ctx(h);
-    launch_pack(c, (uint8_t*)dst, (hipStream_t)stream);
-    HIPCHK(hipGetLastError());
     return TSLAM_OK;
 }
 
@@ -851,51 +934,105 @@ int tslam_set_rig(tslam_handle* h, const double* base_T_rect) {
     const int rc = set_rig_E(h, h->P, base_T_rect);
     if (rc != TSLAM_OK) return rc;
     h->rig = true;
-    h->rig_world = 0;
     return TSLAM_OK;
 }
 
-int tslam_set_rig_ranks(tslam_handle* h, int world, const double* base_T_rect) {
-    if (!h || !base_T_rect || world < 1 || world > 64) return fail(TSLAM_EINVAL, "bad argument");
-    if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_set_rig_ranks inside a batch");
-    const int rc = set_rig_E(h, world * h->P, base_T_rect);
+int tslam_read_rig_poses(tslam_handle* h, int max_frames, double* T_rel, double* T_abs, double* cov, int32_t* stats) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (!h->rig) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig)");
+    if (h->cur_n == 0) return fail(TSLAM_ESTATE, "no batch has run since tslam_create / tslam_reset");
+    if (max_frames < h->cur_n) return fail(TSLAM_EINVAL, "output capacity (max_frames) is smaller than the last batch");
+    int rc = tslam_sync(h);
     if (rc != TSLAM_OK) return rc;
-    h->rig = false;
-    h->rig_world = world;
+    return copy_pose_records(h->d_rig_pose, h->d_rig_stats, h->cur_n, T_rel, T_abs, cov, stats);
+}
+
+// -- sharded rig ------------------------------------------------------------------
+int tslam_set_shard(tslam_handle* h, int cam_lo, int cam_hi, int rank, int world) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_set_shard inside a batch");
+    if (cam_lo < 0 || cam_hi > h->C || cam_lo >= cam_hi) return fail(TSLAM_EINVAL, "camera range outside [0, cameras)");
+    if (world < 1 || rank < 0 || rank >= world || world > h->B) return fail(TSLAM_EINVAL, "need 0 <= rank < world <= max_batch");
+    if (world > 1 && (h->prm.rgbd || h->prm.ba_window)) return fail(TSLAM_EINVAL, "sharding covers stereo rigs without local BA");
+    h->sh_cam_lo = cam_lo;
+    h->sh_cam_hi = cam_hi;
+    h->sh_rank = rank;
+    h->sh_world = world;
     return TSLAM_OK;
 }
 
-int tslam_rig_fuse(tslam_handle* h, const void* gathered, int world, int64_t first_frame, int n_frames, void* stream) {
-    if (!h || !gathered) return fail(TSLAM_EINVAL, "bad argument");
-    if (h->rig_world != world) return fail(TSLAM_ESTATE, "tslam_set_rig_ranks with this world size first");
-    if (n_frames < 1 || n_frames > h->B) return fail(TSLAM_EINVAL, "n_frames must be in [1, max_batch]");
+int tslam_exchange_sizes(tslam_handle* h, int64_t* stream_block, int64_t* pose_record) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (stream_block) *stream_block = stream_block_bytes(h->g);
+    if (pose_record) *pose_record = pose_record_bytes(h->P);
+    return TSLAM_OK;
+}
+
+static int check_frames_cams(tslam_handle* h, int64_t first_frame, int n_frames, int cam_lo, int cam_hi) {
+    if (n_frames < 1 || n_frames > h->R) return fail(TSLAM_EINVAL, "n_frames must be in [1, ring]");
+    if (cam_lo < 0 || cam_hi > h->C || cam_lo >= cam_hi) return fail(TSLAM_EINVAL, "camera range outside [0, cameras)");
+    if (first_frame + n_frames < 0) return fail(TSLAM_EINVAL, "frame range before the sequence start");
+    return TSLAM_OK;
+}
+
+int tslam_pack_streams(tslam_handle* h, int64_t first_frame, int n_frames, int cam_lo, int cam_hi, void* dst, void* stream) {
+    if (!h || !dst) return fail(TSLAM_EINVAL, "bad argument");
+    int rc = check_frames_cams(h, first_frame, n_frames, cam_lo, cam_hi);
+    if (rc != TSLAM_OK) return rc;
     HIPCHK(hipSetDevice(h->device));
-    BatchCtx c = make_ctx(h);
-    c.n = n_frames;
-    c.g0 = first_frame;
-    const int64_t K = h->g.K, L = h->g.n_levels;
-    const int64_t rank_bytes = (int64_t)n_frames * h->C * (K * 40 + L * 4) +
-                               (int64_t)n_frames * h->P * (52 * 8 + TS_STATS_INTS * 4);
-    launch_rig_fuse(c, (const uint8_t*)gathered, rank_bytes, world, (hipStream_t)stream);
+    launch_stream_blocks(make_ctx(h), true, first_frame, n_frames, cam_lo, cam_hi - cam_lo, (uint8_t*)dst, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
     return TSLAM_OK;
 }
 
-int tslam_read_rig_poses(tslam_handle* h, double* T_rel, double* T_abs, double* cov, int32_t* stats) {
-    if (!h) return fail(TSLAM_EINVAL, "null handle");
-    if (!h->d_rig_pose) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig / tslam_set_rig_ranks)");
-    int rc = tslam_sync(h);
+int tslam_unpack_streams(tslam_handle* h, int64_t first_frame, int n_frames, int cam_lo, int cam_hi, const void* src,
+                         void* stream) {
+    if (!h || !src) return fail(TSLAM_EINVAL, "bad argument");
+    int rc = check_frames_cams(h, first_frame, n_frames, cam_lo, cam_hi);
     if (rc != TSLAM_OK) return rc;
-    const int n = h->rig_world ? h->B : h->cur_n;   // ranks mode: the last fused batch (caller slices)
-    std::vector<double> pose((size_t)n * TS_POSE_DOUBLES);
-    HIPCHK(hipMemcpy(pose.data(), h->d_rig_pose, sizeof(double) * pose.size(), hipMemcpyDeviceToHost));
-    for (int i = 0; i < n; ++i) {
-        const double* src = pose.data() + (size_t)i * TS_POSE_DOUBLES;
-        if (T_rel) memcpy(T_rel + 16 * (size_t)i, src, 16 * sizeof(double));
-        if (T_abs) memcpy(T_abs + 16 * (size_t)i, src + 16, 16 * sizeof(double));
-        if (cov) memcpy(cov + 36 * (size_t)i, src + 32, 36 * sizeof(double));
-    }
-    if (stats) HIPCHK(hipMemcpy(stats, h->d_rig_stats, sizeof(int32_t) * TS_STATS_INTS * (size_t)n, hipMemcpyDeviceToHost));
+    HIPCHK(hipSetDevice(h->device));
+    launch_stream_blocks(make_ctx(h), false, first_frame, n_frames, cam_lo, cam_hi - cam_lo, (uint8_t*)src, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return TSLAM_OK;
+}
+
+int tslam_import_raw(tslam_handle* h, const uint8_t* images, int64_t first_frame, int n_frames, int cam_lo, int cam_hi,
+                     void* stream) {
+    if (!h || !images) return fail(TSLAM_EINVAL, "bad argument");
+    int rc = check_frames_cams(h, first_frame, n_frames, cam_lo, cam_hi);
+    if (rc != TSLAM_OK) return rc;
+    if (h->prm.rgbd) return fail(TSLAM_EINVAL, "tslam_import_raw takes gray stereo images");
+    HIPCHK(hipSetDevice(h->device));
+    BatchCtx c = make_ctx(h);
+    const int ncam = cam_hi - cam_lo;
+    const int64_t skip = first_frame < 0 ? -first_frame : 0;   // frames before the sequence start
+    c.images = images + (size_t)skip * ncam * h->W * h->H;
+    c.g0 = first_frame + skip;
+    c.n = (int)(n_frames - skip);
+    c.cam0 = cam_lo;
+    c.ncam = ncam;
+    launch_rectify_pyramid(c, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return TSLAM_OK;
+}
+
+int tslam_pack_poses(tslam_handle* h, void* dst, void* stream) {
+    if (!h || !dst) return fail(TSLAM_EINVAL, "bad argument");
+    if (!h->in_batch) return fail(TSLAM_ESTATE, "tslam_pack_poses inside a batch (after its POSE stage)");
+    HIPCHK(hipSetDevice(h->device));
+    int lo, hi;
+    shard_range(h, h->cur_n, &lo, &hi);
+    launch_pose_records(make_ctx(h), true, lo, hi - lo, (uint8_t*)dst, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return TSLAM_OK;
+}
+
+int tslam_unpack_poses(tslam_handle* h, const void* src, void* stream) {
+    if (!h || !src) return fail(TSLAM_EINVAL, "bad argument");
+    if (!h->in_batch) return fail(TSLAM_ESTATE, "tslam_unpack_poses inside a batch (before its CHAIN stage)");
+    HIPCHK(hipSetDevice(h->device));
+    launch_pose_records(make_ctx(h), false, 0, h->cur_n, (uint8_t*)src, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
     return TSLAM_OK;
 }
 

@@ -85,6 +85,10 @@ struct BatchCtx {
     int cpp;               // cameras per pair: 2 (stereo), 1 (RGB-D: colour camera + aligned depth)
     int rgbd;
     int n;                 // frames in this batch
+    // camera view of the front-end kernels (rectify .. describe): cameras cam0 .. cam0+ncam-1 of
+    // every frame, images [n][ncam][H][W] (the whole rig: 0, C; a sharded rig: the rank's streams)
+    int cam0, ncam;
+    int match_modes;       // k_match: 3 = temporal + stereo, 1 = stereo only (sharded pre-pass)
     int64_t g0;            // global index of the batch's first frame
     int W, H;              // level-0 size
     // inputs
@@ -133,6 +137,11 @@ struct BatchCtx {
 };
 
 static inline __host__ __device__ int ring_slot(const BatchCtx& c, int64_t g) { return (int)(g % c.R); }
+// front-end image index (f * ncam + view camera) -> frame, rig camera
+__device__ __forceinline__ void view_image(const BatchCtx& c, int img, int* f, int* cam) {
+    *f = img / c.ncam;
+    *cam = c.cam0 + (img - *f * c.ncam);
+}
 
 // host launchers (one per stage kernel set)
 void launch_rectify_pyramid(const BatchCtx& c, hipStream_t s);
@@ -141,12 +150,18 @@ void launch_select(const BatchCtx& c, hipStream_t s);
 void launch_describe(const BatchCtx& c, hipStream_t s);
 void launch_match(const BatchCtx& c, hipStream_t s);
 void launch_match_refine(const BatchCtx& c, hipStream_t s);
+void launch_match_stereo(const BatchCtx& c, hipStream_t s);
 void launch_pose(const BatchCtx& c, hipStream_t s);
 void launch_chain(const BatchCtx& c, hipStream_t s);
-void launch_pack(const BatchCtx& c, uint8_t* dst, hipStream_t s);
 void launch_rig(const BatchCtx& c, hipStream_t s);
+void launch_rig_pose(const BatchCtx& c, hipStream_t s);
 void launch_rig_chain(const BatchCtx& c, hipStream_t s);
-void launch_rig_fuse(const BatchCtx& c, const uint8_t* gathered, int64_t rank_bytes, int world, hipStream_t s);
+// sharded rig exchange (k_exchange.hip): stream blocks (per frame x camera) and pose records (per frame)
+int64_t stream_block_bytes(const LevelGeom& g);
+int64_t pose_record_bytes(int P);
+void launch_stream_blocks(const BatchCtx& c, bool pack, int64_t first, int n_frames, int cam_lo, int ncam, uint8_t* blk,
+                          hipStream_t s);
+void launch_pose_records(const BatchCtx& c, bool pack, int f0, int n, uint8_t* rec, hipStream_t s);
 void launch_pose_solve(const BatchCtx& c, hipStream_t s);
 void launch_reloc(const BatchCtx& c, int pair, int64_t frame, const double* map_xyz, const uint32_t* map_desc, int M,
                   int32_t* match, double* corr, int32_t* stats, double* pose, double* ransac, double* hyp, hipStream_t s);

@@ -30,6 +30,7 @@ KERNELS = {
     "rectify_pyramid": 10, "detect": 11, "select": 12, "describe": 13,
     "match": 14, "match_refine": 15, "pose": 16, "chain": 17,
 }
+RIG_KERNEL = 18   # rig pose (+ chain; sharded: the range's rig pose only)
 POSE_OK, POSE_LOST, POSE_INIT = 0, 1, 2
 
 
@@ -73,7 +74,7 @@ _SIGNATURES = {
     "tslam_match": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_pose": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_sync": (ctypes.c_int, [ctypes.c_void_p]),
-    "tslam_read_poses": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_read_poses": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 4),
     "tslam_reset": (ctypes.c_int, [ctypes.c_void_p]),
     "tslam_frames_done": (ctypes.c_int64, [ctypes.c_void_p]),
     "tslam_buffer_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
@@ -82,13 +83,19 @@ _SIGNATURES = {
     "tslam_copy_in": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64]),
     "tslam_ring_slot": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "tslam_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
-    "tslam_pack_features": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
     "tslam_set_rig": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_set_motion_prior": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
-    "tslam_read_rig_poses": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 4),
-    "tslam_set_rig_ranks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
-    "tslam_rig_fuse": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
-                                      ctypes.c_void_p]),
+    "tslam_read_rig_poses": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 4),
+    "tslam_set_shard": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "tslam_exchange_sizes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+    "tslam_pack_streams": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_unpack_streams": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_import_raw": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_void_p]),
+    "tslam_pack_poses": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_unpack_poses": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_ba_read_map": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_map_upload": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     "tslam_relocalize": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64] + [ctypes.c_void_p] * 3),
@@ -236,6 +243,9 @@ class Handle:
     def run_kernel(self, name: str, stream: int = 0) -> None:
         _check(self.lib.tslam_run_stage(self.h, KERNELS[name], ctypes.c_void_p(stream)))
 
+    def run_rig(self, stream: int = 0) -> None:
+        _check(self.lib.tslam_run_stage(self.h, RIG_KERNEL, ctypes.c_void_p(stream)))
+
     def end_batch(self) -> None:
         _check(self.lib.tslam_end_batch(self.h))
 
@@ -248,7 +258,8 @@ class Handle:
         t_abs = np.zeros((n, 4, 4))
         cov = np.zeros((n, 6, 6))
         stats = np.zeros((n, 8), dtype=np.int32)
-        _check(self.lib.tslam_read_poses(self.h, t_rel.ctypes.data, t_abs.ctypes.data, cov.ctypes.data, stats.ctypes.data))
+        _check(self.lib.tslam_read_poses(self.h, int(n_frames), t_rel.ctypes.data, t_abs.ctypes.data, cov.ctypes.data,
+                                         stats.ctypes.data))
         shape = (n_frames, self.n_pairs)
         return {
             "T_rel": t_rel.reshape(shape + (4, 4)), "T_abs": t_abs.reshape(shape + (4, 4)),
@@ -271,28 +282,43 @@ class Handle:
             raise ValueError(f"need {self.n_pairs} 4x4 matrices")
         _check(self.lib.tslam_set_rig(self.h, e.ctypes.data))
 
-    def set_rig_ranks(self, base_T_rect: list) -> None:
-        """Rig fusion across ranks: base_T_rect-left of every pair of every rank (rank-major)."""
-        e = np.ascontiguousarray(np.stack([np.asarray(m, dtype=np.float64) for m in base_T_rect]))
-        if e.shape[1:] != (4, 4) or e.shape[0] % self.n_pairs:
-            raise ValueError("need world * n_pairs 4x4 matrices")
-        _check(self.lib.tslam_set_rig_ranks(self.h, int(e.shape[0] // self.n_pairs), e.ctypes.data))
-
-    def rig_fuse(self, gathered_dev_ptr: int, world: int, first_frame: int, n_frames: int, stream: int = 0) -> None:
-        """Fuse the gathered blocks of one batch into body motions (enqueued on ``stream``)."""
-        _check(self.lib.tslam_rig_fuse(self.h, ctypes.c_void_p(gathered_dev_ptr), int(world), int(first_frame),
-                                       int(n_frames), ctypes.c_void_p(stream)))
-        self._rig_fused_n = int(n_frames)
-
     def read_rig_poses(self, n_frames: int) -> dict:
         """Body-frame rig motion of the last batch (synchronises)."""
-        cap = self.batch if getattr(self, "_rig_fused_n", None) is not None else n_frames
-        t_rel = np.zeros((cap, 4, 4))
-        t_abs = np.zeros((cap, 4, 4))
-        cov = np.zeros((cap, 6, 6))
-        stats = np.zeros((cap, 8), dtype=np.int32)
-        _check(self.lib.tslam_read_rig_poses(self.h, t_rel.ctypes.data, t_abs.ctypes.data, cov.ctypes.data, stats.ctypes.data))
-        return {"T_rel": t_rel[:n_frames], "T_abs": t_abs[:n_frames], "cov": cov[:n_frames], "stats": stats[:n_frames]}
+        t_rel = np.zeros((n_frames, 4, 4))
+        t_abs = np.zeros((n_frames, 4, 4))
+        cov = np.zeros((n_frames, 6, 6))
+        stats = np.zeros((n_frames, 8), dtype=np.int32)
+        _check(self.lib.tslam_read_rig_poses(self.h, int(n_frames), t_rel.ctypes.data, t_abs.ctypes.data, cov.ctypes.data,
+                                             stats.ctypes.data))
+        return {"T_rel": t_rel, "T_abs": t_abs, "cov": cov, "stats": stats}
+
+    # -- sharded rig (SURVEY.md §8e; thor_slam_amd/shard.py drives these) --------------------
+    def set_shard(self, cam_lo: int, cam_hi: int, rank: int, world: int) -> None:
+        _check(self.lib.tslam_set_shard(self.h, int(cam_lo), int(cam_hi), int(rank), int(world)))
+
+    def exchange_sizes(self) -> tuple[int, int]:
+        """(bytes of one stream block, bytes of one pose record)."""
+        sb, pr = ctypes.c_int64(), ctypes.c_int64()
+        _check(self.lib.tslam_exchange_sizes(self.h, ctypes.byref(sb), ctypes.byref(pr)))
+        return int(sb.value), int(pr.value)
+
+    def pack_streams(self, first_frame: int, n_frames: int, cam_lo: int, cam_hi: int, dst_ptr: int, stream: int = 0) -> None:
+        _check(self.lib.tslam_pack_streams(self.h, int(first_frame), int(n_frames), int(cam_lo), int(cam_hi),
+                                           ctypes.c_void_p(dst_ptr), ctypes.c_void_p(stream)))
+
+    def unpack_streams(self, first_frame: int, n_frames: int, cam_lo: int, cam_hi: int, src_ptr: int, stream: int = 0) -> None:
+        _check(self.lib.tslam_unpack_streams(self.h, int(first_frame), int(n_frames), int(cam_lo), int(cam_hi),
+                                             ctypes.c_void_p(src_ptr), ctypes.c_void_p(stream)))
+
+    def import_raw(self, images_ptr: int, first_frame: int, n_frames: int, cam_lo: int, cam_hi: int, stream: int = 0) -> None:
+        _check(self.lib.tslam_import_raw(self.h, ctypes.c_void_p(images_ptr), int(first_frame), int(n_frames), int(cam_lo),
+                                         int(cam_hi), ctypes.c_void_p(stream)))
+
+    def pack_poses(self, dst_ptr: int, stream: int = 0) -> None:
+        _check(self.lib.tslam_pack_poses(self.h, ctypes.c_void_p(dst_ptr), ctypes.c_void_p(stream)))
+
+    def unpack_poses(self, src_ptr: int, stream: int = 0) -> None:
+        _check(self.lib.tslam_unpack_poses(self.h, ctypes.c_void_p(src_ptr), ctypes.c_void_p(stream)))
 
     # -- buffer access (tests) -------------------------------------------------------------
     def buffer_info(self, which: str) -> tuple[int, int, int]:
@@ -318,11 +344,6 @@ class Handle:
         """All bytes of one frame slot of a buffer (ring slot or batch slot, per the layout)."""
         _, _, per = self.buffer_info(which)
         return self.copy_out(which, slot * per, per, dtype)
-
-    def pack_features(self, dst_dev_ptr: int, stream: int = 0) -> int:
-        nb = ctypes.c_int64()
-        _check(self.lib.tslam_pack_features(self.h, ctypes.c_void_p(dst_dev_ptr), ctypes.byref(nb), ctypes.c_void_p(stream)))
-        return int(nb.value)
 
     def ba_read(self, pair: int = 0) -> dict:
         """A8 keyframe window of one pair (synchronises): slot-indexed frames, cam_T_world,

@@ -305,6 +305,21 @@ class SyntheticStereoSource(CameraSource):
         return self.trajectory[i % len(self.trajectory)]
 
 
+def synthetic_rig(joints: dict, names: list[str] | tuple[str, ...], width: int = 640, height: int = 400,
+                  traj_len: int = 40, scene_seed: int = 0):
+    """Stereo sources mounted on a rig's joints (``joints[name]`` = rig_T_source 4x4, e.g. the
+    brackets.urdf joints of ``scripts/run_slam.py:45-50``'s CAMERA_MAP) in one shared room along
+    one body trajectory -> (sources, CameraRig with those rig extrinsics)."""
+    from .camera.rig import CameraRig
+
+    scene = RoomScene(seed=scene_seed)
+    traj = circle_trajectory(traj_len)
+    srcs = [SyntheticStereoSource(name=nm, scene=scene, trajectory=traj, rig_T_source=np.array(joints[nm]), seed=k,
+                                  width=width, height=height) for k, nm in enumerate(names)]
+    rig = CameraRig(srcs, rig_extrinsics={nm: Extrinsics.from_4x4_matrix(np.array(joints[nm])) for nm in names})
+    return srcs, rig
+
+
 class SyntheticRGBDSource(SyntheticStereoSource):
     """An RGB-D source (BASELINE configs[4]): frames are [colour BGR u8, depth u16 mm] from one
     camera, the depth aligned to the colour image (same K and D, as Luxonis ``depth_align_to_rgb``,
