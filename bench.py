@@ -1,27 +1,38 @@
 """Throughput bench: synced stereo frames/sec (detect + match + pose) @ 640x400 on MI355X.
 
 python bench.py --gpus N --steps K --warmup W   (N > 1 under torch.distributed.run, one rank/GPU)
+python bench.py --config c3 [--gpus N]          (BASELINE.json configs[2]: 4-OAK bracket rig, 8 streams)
 python bench.py --config c4                     (BASELINE.json configs[3]: 1280x800, K=4000, + local BA)
 python bench.py --config c5 [--gpus 4]          (BASELINE.json configs[4]: RGB-D 1280x720, one camera per GPU)
 
-* workload (BASELINE.json configs[1], C2): one stereo pair 640x400 per GPU, K=2000 ORB-style
-  keypoints per image, synthetic room sequence (seed = rank); a *step* = one batch of
-  ``--batch`` synchronised stereo frames pushed through the whole hot path
-  (rectify -> pyramid -> FAST/NMS/top-K -> orientation + rBRIEF -> stereo + temporal Hamming
-  match -> sub-pixel refinement -> P3P-RANSAC -> Gauss-Newton -> pose chaining).
+* N = 1, config c2 (BASELINE.json configs[1]): one stereo pair 640x400, K=2000 ORB-style
+  keypoints per image, synthetic room sequence; a *step* = one batch of ``--batch`` synchronised
+  stereo frames pushed through the whole hot path (rectify -> pyramid -> FAST/NMS/top-K ->
+  orientation + rBRIEF -> stereo + temporal Hamming match -> sub-pixel refinement -> P3P-RANSAC
+  -> Gauss-Newton -> pose chaining).
+* N > 1 (c2): one camera STREAM per GPU (BASELINE.json north_star): N streams =
+  N/2 stereo sources of the bracket rig (scripts/run_slam.py:45-50, brackets.urdf joints), the
+  sharded rig of thor_slam_amd/shard.py (front end per stream, RCCL all-to-all of raw images +
+  stream blocks, per-pair back end + rig pose on each rank's frame range, all-gather of pose
+  records).  value = synced stereo (pair) frames/s of the whole rig; weak scaling (one stream
+  per GPU).
+* c3: the 4-source bracket rig (8 streams, 4 pairs) sharded over --gpus N (N = 1: one handle);
+  value = rig frames/s (one frame = all 8 images); strong scaling.
 * inputs are rendered on the host before timing and are resident in HBM (a triangle-wave
   replay of ``--unique`` rendered frames, so consecutive frames stay consecutive in time).
-* N > 1: weak scaling, one stereo source per rank; each step also all-gathers the packed
-  keypoint + descriptor block of every rank over RCCL (the exchange step of SURVEY.md §8e).
 * timing: barrier + synchronize on both sides of exactly K steps; MAX over ranks.
-* roofline: per-kernel HIP-event timing of one batch run kernel by kernel on the same stream,
+* roofline: per-kernel HIP-event timing of the timed steps on the stream each kernel runs on,
   for the dominant kernel: algorithmic bytes / average duration vs 8 TB/s.
-* cpu_baseline (rank 0, N=1 context): the NumPy oracle on a bounded sample of the same frames.
+* cpu_baseline (rank 0, N = 1): the NumPy oracle on a bounded sample of the same frames, over
+  the host cores this process may use, plus the one-process figure.
+* boundary (c2, N = 1): HipSlamEngine.process_frames on host SynchronizedFrameSets from the
+  CameraRig (the drop-in boundary, scripts/run_slam.py:314-328) at batch 1 and 64.
 * --config c4: the same step plus the A8 stage (every 5th frame a keyframe of a 10-keyframe
   window, 5 Gauss-Newton iterations per keyframe); the roofline is then that of the dominant
   kernel of the step, the FP64-MFMA Schur product when it dominates (HIP events around its launches).
-* --config c5: RGB-D frames (BGR u8 + aligned u16 mm depth, 1280x720) of one camera per GPU; the
-  colour image is converted on the device and depth replaces the stereo matching.
+* --config c5: RGB-D frames (BGR u8 + aligned u16 mm depth, 1280x720) of one camera per GPU
+  (independent replicas for N > 1: RGB-D cameras have no cross-camera matching); the colour
+  image is converted on the device and depth replaces the stereo matching.
 """
 
 from __future__ import annotations
@@ -29,6 +40,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 from concurrent.futures import ProcessPoolExecutor
@@ -42,6 +54,7 @@ for _p in (ROOT, ROOT / "thor-slam_amd"):
         sys.path.insert(0, str(_p))
 
 METRIC = "synced stereo frames/sec (detect+match+pose) @640×400, 1/2/4/8 GPU"
+METRIC_C3 = "synced rig frames/sec (4 stereo pairs = 8 streams, detect+match+pose+rig pose) @640×400, 1/2/4/8 GPU"
 METRIC_C4 = "synced stereo frames/sec (detect+match+pose+10-keyframe local BA) @1280×800, 1 GPU"
 METRIC_C5 = "RGB-D frames/sec (BGR+depth, detect+match+pose) @1280×720, one camera per GPU, 1/2/4 GPU"
 HBM_PEAK_GBS = 8000.0
@@ -51,9 +64,13 @@ FP64_MFMA_PEAK_TFS = 78.6   # MI355X FP64 matrix peak (AMD spec; the microarch g
 # bench kernel label -> device symbol (rocprofv3 / PMC summaries); "pose" is k_corr+k_ransac+k_refine
 KERNEL_SYMBOL = {"rectify_pyramid": "k_rectify_pyramid", "detect": "k_detect", "select": "k_select",
                  "describe": "k_describe", "match": "k_match", "match_refine": "k_refine_temporal",
-                 "pose": "k_ransac", "chain": "k_chain"}
+                 "pose": "k_ransac", "chain": "k_chain", "rig": "k_rig_pose"}
+# the bracket rig of scripts/run_slam.py:45-50 (CAMERA_MAP), global camera order = sorted names
+RIG_SOURCES = ("192.168.2.21", "192.168.2.22", "192.168.2.23", "192.168.2.25")
+JOINTS = ROOT / "tests" / "golden" / "brackets_joints.json"   # brackets.urdf joints (tests/test_boundary.py pins them)
 
 
+# ---- rendering ------------------------------------------------------------------------------
 def _render_chunk(args):
     seed, idx, width, height = args
     from thor_slam_amd.synthetic import SyntheticStereoSource
@@ -78,27 +95,63 @@ def render_frames(seed: int, n: int, workers: int, width: int = 640, height: int
     return out
 
 
+def rig_setup(names, width: int = 640, height: int = 400):
+    """Bracket rig of `names`: sources, flat camera list, stereo pairs, rectifications, base_T_rect-left."""
+    from thor_slam_amd.calib import extract_cameras, stereo_pairs, stereo_rectify
+    from thor_slam_amd.synthetic import synthetic_rig
+
+    joints = json.loads(JOINTS.read_text())
+    srcs, rig = synthetic_rig(joints, names, width, height)
+    cams = extract_cameras(rig.calibration, 2 * len(names))
+    pairs = stereo_pairs(cams)
+    rects = [stereo_rectify(cams[l], cams[r]) for l, r in pairs]
+    E = [cams[l].extrinsics.to_4x4_matrix() @ r.left_optical_T_rect() for (l, _), r in zip(pairs, rects)]
+    return srcs, cams, pairs, rects, E
+
+
+def _render_rig_chunk(args):
+    names, items, width, height = args   # items: (frame, global camera)
+    srcs, cams, _, _, _ = rig_setup(names, width, height)
+    by = {s.name: s for s in srcs}
+    return [by[cams[c].source_name].render_image(i, cams[c].cam_idx) for i, c in items]
+
+
+def render_rig_frames(names, n: int, cam_lo: int, cam_hi: int, workers: int, width: int = 640,
+                      height: int = 400) -> np.ndarray:
+    """[n][cam_hi - cam_lo][H][W] u8 of the rig's global cameras cam_lo .. cam_hi-1."""
+    items = [(i, c) for i in range(n) for c in range(cam_lo, cam_hi)]
+    chunks = [items[k::workers] for k in range(workers) if items[k::workers]]
+    out = np.empty((n, cam_hi - cam_lo, height, width), dtype=np.uint8)
+    with ProcessPoolExecutor(max_workers=max(1, len(chunks))) as ex:
+        for ch, imgs in zip(chunks, ex.map(_render_rig_chunk, [(tuple(names), ch, width, height) for ch in chunks])):
+            for (i, c), img in zip(ch, imgs):
+                out[i, c - cam_lo] = img
+    return out
+
+
 def triangle_indices(total: int, unique: int) -> np.ndarray:
     period = 2 * (unique - 1)
     k = np.arange(total) % period
     return np.where(k < unique, k, period - k)
 
 
+# ---- algorithmic bytes (SURVEY.md §8d) --------------------------------------------------------
 def frame_bytes(W: int, H: int, K: int, n_img: int = 2, n_pairs: int = 1, channels: int = 1, matchings: int = 2) -> int:
-    """SURVEY.md §8d compulsory bytes per stereo frame: read the images, write keypoints (12 B) and
+    """SURVEY.md §8d compulsory bytes per synced frame: read the images, write keypoints (12 B) and
     descriptors (32 B), write the match records (8 B per keypoint, for the stereo and the temporal
-    matching of each pair).  C2: 2 * (256,000 + 88,000) + 2 * 16,000 = 720,000 B.  RGB-D (C5): one
-    image of 5 bytes per pixel (BGR + u16 depth), temporal matching only."""
+    matching of each pair).  C2: 2 * (256,000 + 88,000) + 2 * 16,000 = 720,000 B; the C3 rig frame
+    is 4x that.  RGB-D (C5): one image of 5 bytes per pixel (BGR + u16 depth), temporal matching only."""
     return n_img * (W * H * channels + K * (12 + 32)) + matchings * n_pairs * K * 8
 
 
-def kernel_bytes(name: str, B: int, h, cfg, maps_identity: bool) -> float:
-    """Algorithmic (compulsory) HBM bytes of one launch of a kernel over B stereo frames."""
+def kernel_bytes(name: str, B: int, h, cfg, maps_identity: bool, n_img_per_frame: int = 2) -> float:
+    """Algorithmic (compulsory) HBM bytes of one launch of a kernel over B frames."""
     W, H, K = h.width, h.height, cfg.n_features
-    imgs = 2 * B
+    imgs = n_img_per_frame * B
+    pairs = imgs // 2
     pyr = sum(w * hh for w, hh in h.level_wh)
     if name == "rectify_pyramid":
-        maps = 0 if maps_identity else 2 * W * H * 8
+        maps = 0 if maps_identity else n_img_per_frame * W * H * 8
         return imgs * (W * H + pyr) + maps
     if name == "detect":
         return imgs * (pyr + pyr)          # read the levels, write the smoothed levels
@@ -107,14 +160,35 @@ def kernel_bytes(name: str, B: int, h, cfg, maps_identity: bool) -> float:
     if name == "describe":
         return imgs * K * (8 + 32)         # read keypoints, write descriptors
     if name == "match":
-        return B * 2 * (2 * K * 32 + K * 8)  # two matchings: read query+train descriptors, write best/second
+        return pairs * 2 * (2 * K * 32 + K * 8)  # two matchings: read query+train descriptors, write best/second
     if name == "match_refine":
-        return B * 2 * K * (8 + 16)
+        return pairs * 2 * K * (8 + 16)
     if name == "pose":
-        return B * K * (4 + 16 + 8 * 8)
+        return pairs * K * (4 + 16 + 8 * 8)
     if name == "chain":
-        return B * 68 * 8
+        return pairs * 68 * 8
     return 0.0
+
+
+# ---- CPU baseline (the oracle on the host cores) -------------------------------------------------
+def usable_cpus() -> int:
+    """CPUs this process may use: the affinity mask, capped at the pool's per-GPU share (16)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("TSLAM_CPU_SHARE", "16"))))
+
+
+def cpu_model() -> str:
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
 
 
 def _oracle_worker(args):
@@ -126,6 +200,21 @@ def _oracle_worker(args):
     from thor_slam_amd.params import HipSlamConfig
 
     cfg = HipSlamConfig(**cfg_d)
+    if isinstance(rect_d, list):   # a rig: one tracker per pair + the rig pose
+        from oracle.numpy_rig import rig_pose
+
+        rects, E = rect_d
+        trks = [O.OracleTracker(cfg, r) for r in rects]
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < budget_s:
+            i = n % len(frames)
+            outs = [trk.step(frames[i, 2 * q], frames[i, 2 * q + 1]) for q, trk in enumerate(trks)]
+            if n:
+                rig_pose([{"status": o["status"], "T": o["T"], "corr": o.get("corr"),
+                           "intr": (r["fx"], r["fy"], r["cx"], r["cy"])} for o, r in zip(outs, rects)], E, cfg)
+            n += 1
+        return n, time.perf_counter() - t0
     trk = O.OracleTracker(cfg, rect_d)
     bat = None
     if cfg.ba_window > 0:
@@ -161,42 +250,40 @@ def _oracle_worker_rgbd(args):
     return n, time.perf_counter() - t0
 
 
-def cpu_baseline_rgbd(bgr: np.ndarray, depth: np.ndarray, rect, cfg, budget_s: float, procs: int) -> dict:
-    import dataclasses
-
-    rect_d = dict(fx=rect.fx, fy=rect.fy, cx=rect.cx, cy=rect.cy, baseline=rect.baseline,
-                  map_l=rect.map_left, map_r=rect.map_right)
-    cfg_d = dataclasses.asdict(cfg)
-    parts = [(b, d) for b, d in zip(np.array_split(bgr, procs), np.array_split(depth, procs)) if len(b)]
-    with ProcessPoolExecutor(max_workers=len(parts)) as ex:
-        results = list(ex.map(_oracle_worker, [(pt, rect_d, cfg_d, budget_s) for pt in parts]))
-    n = sum(r[0] for r in results)
-    wall = max(r[1] for r in results)
-    return {"value": n / wall, "unit": "frames/s", "cores": len(parts), "kind": "port",
-            "sample": f"{n} synthetic {bgr.shape[2]}x{bgr.shape[1]} RGB-D frames (seed 0, {len(bgr)} distinct, replayed "
-                      f"per process), NumPy oracle step_rgbd, {len(parts)} process(es) x {budget_s:.0f} s"}
+def _rect_dict(r) -> dict:
+    return dict(fx=r.fx, fy=r.fy, cx=r.cx, cy=r.cy, baseline=r.baseline, map_l=r.map_left, map_r=r.map_right)
 
 
-def cpu_baseline(frames: np.ndarray, rect, cfg, budget_s: float, procs: int) -> dict:
-    """The NumPy oracle on the host cores: `procs` processes, each tracking a contiguous chunk of the
-    same frames (relative-pose work is independent per frame pair)."""
-    import dataclasses
-
-    rect_d = dict(fx=rect.fx, fy=rect.fy, cx=rect.cx, cy=rect.cy, baseline=rect.baseline,
-                  map_l=rect.map_left, map_r=rect.map_right)
-    cfg_d = dataclasses.asdict(cfg)
-    chunks = [c for c in np.array_split(frames, procs) if len(c)]
-    if len(chunks) == 1:
-        results = [_oracle_worker((chunks[0], rect_d, cfg_d, budget_s))]
+def _run_oracle(parts: list, rect_d, cfg_d: dict, budget_s: float) -> tuple[int, float]:
+    if len(parts) == 1:
+        results = [_oracle_worker((parts[0], rect_d, cfg_d, budget_s))]
     else:
-        with ProcessPoolExecutor(max_workers=len(chunks)) as ex:
-            results = list(ex.map(_oracle_worker, [(c, rect_d, cfg_d, budget_s) for c in chunks]))
-    n = sum(r[0] for r in results)
-    wall = max(r[1] for r in results)
-    return {"value": n / wall, "unit": "frames/s", "cores": len(chunks), "kind": "port",
-            "sample": f"{n} synthetic {frames.shape[3]}x{frames.shape[2]} stereo frames (seed 0, {len(frames)} distinct, "
-                      f"replayed per process), NumPy oracle{' + local BA' if cfg.ba_window else ''}, "
-                      f"{len(chunks)} process(es) x {budget_s:.0f} s"}
+        with ProcessPoolExecutor(max_workers=len(parts)) as ex:
+            results = list(ex.map(_oracle_worker, [(pt, rect_d, cfg_d, budget_s) for pt in parts]))
+    return sum(r[0] for r in results), max(r[1] for r in results)
+
+
+def cpu_baseline(frames, rect_d, cfg, budget_s: float, procs: int, what: str) -> dict:
+    """The NumPy oracle on the host: `procs` processes, each tracking a contiguous chunk of the same
+    frames (relative-pose work is independent per frame pair), and one process alone.
+    `frames` is an array [n][...] or a (bgr, depth) pair for RGB-D."""
+    import dataclasses
+
+    cfg_d = dataclasses.asdict(cfg)
+
+    def split(k):
+        if isinstance(frames, tuple):
+            return [tuple(z) for z in zip(*(np.array_split(a, k) for a in frames)) if len(z[0])]
+        return [c for c in np.array_split(frames, k) if len(c)]
+
+    parts = split(procs)
+    n, wall = _run_oracle(parts, rect_d, cfg_d, budget_s)
+    n1, wall1 = _run_oracle(split(1), rect_d, cfg_d, max(3.0, budget_s / 2))
+    return {"value": n / wall, "unit": "frames/s", "cores": len(parts), "kind": "port",
+            "sample": f"{n} {what} ({len(parts)} process(es) x {budget_s:.0f} s, each replaying a contiguous chunk), "
+                      f"NumPy oracle{' + local BA' if cfg.ba_window else ''}",
+            "single_core": {"value": n1 / wall1, "cores": 1, "sample": f"{n1} frames, 1 process x {wall1:.0f} s"},
+            "usable_cpus": usable_cpus(), "host_cpus_visible": os.cpu_count(), "cpu_model": cpu_model()}
 
 
 # the synthetic room (8 x 8 x 3 m, FLU) in the tracking world (rect-left camera of frame 0, RDF):
@@ -220,65 +307,137 @@ def tsdf_report(h, us: float, B: int, width: int, height: int) -> dict:
                          "frac": alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": alg}}
 
 
-def main() -> None:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=["c2", "c4", "c5"], default="c2",
-                    help="BASELINE.json configs[1] (c2), configs[3] (c4) or configs[4] (c5)")
-    ap.add_argument("--batch", type=int, default=0, help="frames per step (0 = 256 for c2, 50 for c4, 128 for c5)")
-    ap.add_argument("--unique", type=int, default=0, help="distinct rendered frames, triangle-wave replay (0 = 48 / 24)")
-    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU baseline (0 = skip)")
-    ap.add_argument("--cpu-procs", type=int, default=8, help="oracle processes for the CPU baseline")
-    ap.add_argument("--latency-frames", type=int, default=20, help="B=1 submissions timed for latency_b1_ms")
-    ap.add_argument("--out", type=str, default="", help="also write the JSON line to this file")
-    ap.add_argument("--dist-backend", type=str, default="nccl", help="nccl (RCCL) or gloo (rehearsal, host copy)")
-    ap.add_argument("--pipeline", type=int, default=1,
-                    help="1: front and back kernels on two streams (batch s+1's front overlaps batch s's back)")
-    ap.add_argument("--front-priority", type=int, default=1,
-                    help="1: run the front kernels on a high-priority stream (pipelined mode)")
-    ap.add_argument("--tsdf", type=int, default=0,
-                    help="c5: also integrate every batch's depth into a TSDF volume with the device poses "
-                         "(nvblox-shaped dense map, SURVEY.md §8f item 4); reported under dense_map")
-    ap.add_argument("--pmc", type=str, default=str(ROOT / "profiles" / "pmc_latest.json"),
-                    help="PMC summary (tools/pmc_summary.py) used for roofline.traffic when its batch matches")
-    args = ap.parse_args()
+def pmc_traffic(args, dom: str, per_kernel_us: dict, B: int) -> tuple:
+    """roofline.traffic (and the VALU-issue roofline) of the dominant kernel from the committed PMC
+    summary (tools/pmc_summary.py) when its batch and config match this run."""
+    pmc_path = Path(args.pmc)
+    if not pmc_path.exists():
+        return None, None, None
+    pmc = json.loads(pmc_path.read_text())
+    kern = pmc.get("kernels", {}).get(KERNEL_SYMBOL.get(dom, ""), None)
+    if kern is None or pmc.get("batch_frames") != B or pmc.get("config", "c2") != args.config:
+        return None, None, None
+    valu = None
+    if kern.get("valu_insts_per_launch"):
+        # the path is integer-VALU bound (DESIGN.md §5): wave64 VALU instructions per launch
+        # (PMC SQ_INSTS_VALU) / the same event-timed duration, against the issue peak
+        rate = kern["valu_insts_per_launch"] / (per_kernel_us[dom] * 1e-6)
+        valu = {"bound": "valu", "achieved": rate / 1e12, "peak": VALU_PEAK_WINST / 1e12,
+                "unit": "T wave-instructions/s", "frac": rate / VALU_PEAK_WINST,
+                "insts_per_launch": kern["valu_insts_per_launch"]}
+    return kern["hbm_bytes_per_launch"], valu, kern.get("traffic_note")
 
+
+# ---- the drop-in boundary (SlamEngine.process_frames on host frame sets) ----------------------
+class _ReplaySource:
+    """A CameraSource replaying pre-rendered [left, right] frames (triangle wave) at 30 fps
+    timestamps: the CameraRig input of the boundary leg without per-frame rendering."""
+
+    def __init__(self, name, frames, intr, extr):
+        self._name, self.frames, self.intr, self.extr = name, frames, intr, extr
+        self.i = 0
+
+    @property
+    def name(self):
+        return self._name
+
+    def start(self):
+        pass
+
+    def stop(self):
+        pass
+
+    def get_latest_frames(self):
+        from thor_slam_amd.camera.types import CameraFrame
+
+        k = triangle_indices(self.i + 1, len(self.frames))[-1]
+        ts = 1000.0 + self.i / 30.0
+        self.i += 1
+        return [CameraFrame(image=self.frames[k, c], timestamp=ts, sequence_num=self.i, camera_name=f"{self._name}_{c}")
+                for c in (0, 1)]
+
+    def try_get_latest_frames(self):
+        return self.get_latest_frames()
+
+    def get_intrinsics(self):
+        return self.intr
+
+    def get_extrinsics(self):
+        return self.extr
+
+    def get_sensor_extrinsics(self):
+        return None
+
+    def get_timestamped_sensor_data(self):
+        return None, None
+
+    def try_get_timestamped_sensor_data(self):
+        return None, None
+
+    @property
+    def has_sensor_data(self):
+        return False
+
+
+def boundary_bench(uniq: np.ndarray, src, n_frames: int, batch_sizes=(1, 64)) -> dict:
+    """HipSlamEngine.process_frames timed over `n_frames` SynchronizedFrameSets produced by the
+    CameraRig from host numpy frames (the reference's loop, scripts/run_slam.py:314-328), per
+    engine batch size; frame sets are built before timing (the camera is not what is measured)."""
+    from thor_slam_amd.camera.rig import CameraRig
+    from thor_slam_amd.params import HipSlamConfig
+    from thor_slam_amd.slam.hip_engine import HipSlamEngine
+
+    rep = _ReplaySource(src.name, uniq, src.get_intrinsics(), src.get_extrinsics())
+    rig = CameraRig([rep])
+    rig.start()
+    sets = []
+    while len(sets) < n_frames:
+        s = rig.get_synchronized_frames()
+        if s is not None:
+            sets.append(s)
+    out = {"frames": n_frames, "image_bytes_per_frame": int(uniq[0].nbytes)}
+    for b in batch_sizes:
+        eng = HipSlamEngine(num_cameras=2, config=HipSlamConfig(batch_size=b, enable_loop_closure=False))
+        eng.initialize(rig.calibration)
+        for s in sets[:2 * b + 8]:   # warm-up
+            eng.process_frames(s)
+        eng.flush()
+        eng.reset()
+        t0 = time.perf_counter()
+        for s in sets:
+            eng.process_frames(s)
+        eng.flush()
+        dt = time.perf_counter() - t0
+        st = eng.get_tracking_state()
+        eng.shutdown()
+        out[f"fps_b{b}"] = n_frames / dt
+        out[f"ingress_GBps_b{b}"] = n_frames * uniq[0].nbytes / dt / 1e9
+        out[f"state_b{b}"] = st.name
+    return out
+
+
+# ---- single handle (N = 1, and c5 replicas) ---------------------------------------------------
+def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     import torch
     import torch.distributed as dist
 
     from thor_slam_amd._lib import KERNELS, Handle
     from thor_slam_amd.calib import extract_cameras, stereo_pairs, stereo_rectify
-    from thor_slam_amd.dist import BlockLayout, FeatureExchange
     from thor_slam_amd.camera.rig import CameraRig
     from thor_slam_amd.params import HipSlamConfig
     from thor_slam_amd.rgbd import pack_rgbd
     from thor_slam_amd.synthetic import SyntheticStereoSource
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    dev_index = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(dev_index)
-    if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
-        else:
-            dist.init_process_group(args.dist_backend)
-
-    c4, c5 = args.config == "c4", args.config == "c5"
-    if c4 and world > 1:
-        raise SystemExit("--config c4 is a single-GPU configuration")
+    c3, c4, c5 = args.config == "c3", args.config == "c4", args.config == "c5"
     width, height = (1280, 800) if c4 else (1280, 720) if c5 else (640, 400)
     cfg = (HipSlamConfig(n_features=4000, ba_window=10, ba_kf_interval=5, ba_iters=5) if c4 else
            HipSlamConfig(rgbd=True) if c5 else HipSlamConfig())
     B = args.batch or (50 if c4 else 128 if c5 else 256)
     args.unique = args.unique or (24 if (c4 or c5) else 48)
-    workers = max(1, min(16, (os.cpu_count() or 2) // max(1, world), args.unique))
+    workers = max(1, min(16, usable_cpus(), args.unique * (8 if c3 else 1)))
     t_r = time.perf_counter()
+    E = None
+    src = None
     if c5:
         from thor_slam_amd.calib import rgbd_pairs, rgbd_undistort
         from thor_slam_amd.synthetic import SyntheticRGBDSource
@@ -286,55 +445,42 @@ def main() -> None:
         src = SyntheticRGBDSource(seed=rank, n_frames=args.unique, width=width, height=height)
         cams = extract_cameras(CameraRig([src]).calibration, 2)
         (ci, _), = rgbd_pairs(cams)
-        rect = rgbd_undistort(cams[ci])
+        rects = [rgbd_undistort(cams[ci])]
         rgbd_frames = [src.render_rgbd(i) for i in range(args.unique)]
         uniq = np.stack([pack_rgbd(b, d) for b, d in rgbd_frames])[:, None, :]   # [n][1][5HW]
+    elif c3:
+        _, cams, pairs, rects, E = rig_setup(RIG_SOURCES, width, height)
+        uniq = render_rig_frames(RIG_SOURCES, args.unique, 0, 2 * len(rects), workers, width, height)
     else:
         src = SyntheticStereoSource(seed=rank, n_frames=args.unique, width=width, height=height)
         cams = extract_cameras(CameraRig([src]).calibration, 2)
         (li, ri), = stereo_pairs(cams)
-        rect = stereo_rectify(cams[li], cams[ri])
+        rects = [stereo_rectify(cams[li], cams[ri])]
         uniq = render_frames(rank, args.unique, workers, width, height)
     t_render = time.perf_counter() - t_r
+    P = len(rects)
+    rect = rects[0]
+    n_img = uniq.shape[1] if not c5 else 1
 
     total = (args.warmup + args.steps) * B
     idx = torch.from_numpy(triangle_indices(total, args.unique)).cuda()
-    seq = torch.from_numpy(uniq).cuda().index_select(0, idx).contiguous()  # [total, 2, H, W] (c5: [total, 1, 5HW]) in HBM
-    h = Handle([rect], cfg, max_batch=B, device=dev_index)
+    seq = torch.from_numpy(uniq).cuda().index_select(0, idx).contiguous()  # [total, C, H, W] (c5: [total, 1, 5HW]) in HBM
+    h = Handle(rects, cfg, max_batch=B, device=dev_index)
+    if P > 1:
+        h.set_rig(E)
     # the front stream (rectify .. describe) is the critical path of the pipelined step: with
     # --front-priority 1 it is a high-priority stream, so the back kernels fill the gaps around it
     stream = (torch.cuda.Stream(priority=-1) if args.front_priority and args.pipeline else torch.cuda.current_stream())
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
-    layout = BlockLayout(n_frames=B, n_cams=1 if c5 else 2, K=cfg.n_features, L=cfg.n_levels)
-    on_device = args.dist_backend == "nccl"
-    # two exchange buffers: batch s packs into buffer s % 2 and all-gathers it asynchronously over
-    # RCCL while batch s + 1 computes (the buffer is reused only after its gather has completed)
-    exchanges = [FeatureExchange(layout, "cuda" if on_device else "cpu", world) for _ in range(2)] if world > 1 else []
-    pending = {"work": None, "buf": 0, "batch": -1}   # the in-flight all-gather (one at a time)
-    staging = torch.empty((layout.rank_bytes,), dtype=torch.uint8, device="cuda") if world > 1 and not on_device else None
-    recv_dev = None
-    if world > 1:
-        # the rig-level solve after the gather: every rank fuses all ranks' body
-        # motions on its device; the rig extrinsics of every rank's pair are exchanged once
-        bt = torch.from_numpy(np.ascontiguousarray(cams[0].extrinsics.to_4x4_matrix() @ rect.left_optical_T_rect()))
-        if on_device:
-            every = torch.empty((world, 4, 4), dtype=torch.float64, device="cuda")
-            dist.all_gather_into_tensor(every, bt.cuda())
-            every = every.cpu()
-        else:
-            parts = [torch.empty((4, 4), dtype=torch.float64) for _ in range(world)]
-            dist.all_gather(parts, bt)
-            every = torch.stack(parts)
-            recv_dev = torch.empty((world * layout.rank_bytes,), dtype=torch.uint8, device="cuda")
-        h.set_rig_ranks(list(every.numpy()))
-    names = list(KERNELS) + (["local_ba"] if c4 else []) + (["tsdf"] if c5 and args.tsdf else [])
+    kern = list(KERNELS) + (["rig"] if P > 1 else [])
+    names = kern + (["local_ba"] if c4 else []) + (["tsdf"] if c5 and args.tsdf else [])
     if c5 and args.tsdf:
         h.tsdf_init(TSDF_ORIGIN, TSDF_DIMS, 0.05, 4.0, 10.0, 100.0)
-    BACK = {"match", "match_refine", "pose", "chain"}
+    BACK = {"match", "match_refine", "pose", "chain", "rig"}
     # two streams: the front kernels (rectify .. describe) of batch s + 1 overlap the back kernels
     # (match .. chain) of batch s; the library orders batch s's back after its front and batch s's
-    # front after the back of batch s - 2 (ring slots); the exchange and fusion follow the back.
+    # front after the back of batch s - 2 (ring slots)
     bstream = torch.cuda.Stream() if args.pipeline else stream
     bsp = bstream.cuda_stream
     back_done = [torch.cuda.Event(), torch.cuda.Event()]
@@ -344,14 +490,11 @@ def main() -> None:
     ba_done = [torch.cuda.Event(), torch.cuda.Event()] if c4 else None
     ba_issued = [False, False]
 
-    def finish_exchange() -> None:
-        """Make the back stream wait for the in-flight gather (the host does not block) and run the
-        rig fusion of that batch on the device."""
-        if pending["work"] is not None:
-            with torch.cuda.stream(bstream):
-                pending["work"].wait()
-            h.rig_fuse(exchanges[pending["buf"]].recv.data_ptr(), world, pending["batch"] * B, B, bsp)
-            pending["work"] = None
+    def run(k: str, st) -> None:
+        if k == "rig":
+            h.run_rig(st.cuda_stream)
+        else:
+            h.run_kernel(k, st.cuda_stream)
 
     def step(s: int, evs=None) -> None:
         # one batch = every kernel of the hot path; in the timed steps each kernel is bracketed by
@@ -382,7 +525,7 @@ def main() -> None:
                 first_back = False
             if evs is not None:
                 evs[i][0].record(st)
-            h.run_kernel(k, st.cuda_stream)
+            run(k, st)
             if evs is not None:
                 evs[i][1].record(st)
         if bstream is not stream:
@@ -397,32 +540,11 @@ def main() -> None:
                              first_frame=s * B, stream=bsp)
             if evs is not None:
                 evs[i][1].record(bstream)
-        if exchanges:  # the exchange step: every rank's keypoints/descriptors/poses to all ranks
-            k = s % 2
-            ex = exchanges[k]
-            if on_device:
-                # batch s-1's gather ran while batch s computed: fuse it, then ship batch s
-                finish_exchange()
-                h.pack_features(ex.send.data_ptr(), bsp)
-                with torch.cuda.stream(bstream):
-                    pending.update(work=ex.all_gather(async_op=True), buf=k, batch=s)
-            else:   # gloo rehearsal: host gather, then the same device fusion
-                h.pack_features(staging.data_ptr(), bsp)
-                bstream.synchronize()
-                ex.send.copy_(staging.cpu())
-                ex.all_gather()
-                with torch.cuda.stream(bstream):
-                    recv_dev.copy_(ex.recv)
-                h.rig_fuse(recv_dev.data_ptr(), world, s * B, B, bsp)
-
-    def drain() -> None:
-        finish_exchange()
 
     events = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in names]
               for _ in range(args.steps)]
     for s in range(args.warmup):
         step(s)
-    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -432,7 +554,6 @@ def main() -> None:
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(args.warmup + k, events[k])
-    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -443,30 +564,28 @@ def main() -> None:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     res = h.read_poses(B)
-    ok_frac = float(np.mean(res["stats"][:, 0, 0] == 0))
-    rig_ok = None
-    if world > 1:
-        rig_ok = float(np.mean(h.read_rig_poses(B)["stats"][:, 0] == 0))
+    ok_frac = float(np.mean(res["stats"][:, :, 0] == 0))
+    rig_ok = float(np.mean(h.read_rig_poses(B)["stats"][:, 0] == 0)) if P > 1 else None
 
     # ---- the same kernels run alone (after the timed region, one stream, 3 batches): under the
     # two-stream pipeline a kernel shares the GPU with the other stream's kernels, so its timed
     # duration above includes that sharing; these isolated durations are the kernel's own speed
-    iso_us = {k: 0.0 for k in KERNELS}
+    iso_us = {k: 0.0 for k in kern}
     n_iso = 3
     torch.cuda.synchronize()
     for r in range(n_iso):
         s_iso = r % (args.warmup + args.steps)   # replayed input: only the durations are used
         h.begin_batch(seq[s_iso * B].data_ptr(), B)
-        pairs = []
-        for k in KERNELS:
+        prs = []
+        for k in kern:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            h.run_kernel(k, sp)
+            run(k, stream)
             e1.record(stream)
-            pairs.append((k, e0, e1))
+            prs.append((k, e0, e1))
         h.end_batch()
         torch.cuda.synchronize()
-        for k, e0, e1 in pairs:
+        for k, e0, e1 in prs:
             iso_us[k] += e0.elapsed_time(e1) * 1e3 / n_iso
 
     # ---- per-kernel durations of the timed launches (HIP events on the launch stream) ----------
@@ -475,7 +594,7 @@ def main() -> None:
         for i, k in enumerate(names):
             per_kernel_us[k] += evs[i][0].elapsed_time(evs[i][1]) * 1e3 / args.steps  # us
     unit_bytes = (frame_bytes(rect.width, rect.height, cfg.n_features, n_img=1, channels=5, matchings=1) if c5 else
-                  frame_bytes(rect.width, rect.height, cfg.n_features))
+                  frame_bytes(rect.width, rect.height, cfg.n_features, n_img=2 * P, n_pairs=P))
     dom_bytes = unit_bytes * B          # §8d per-frame bytes x the frames one launch processes
     schur = h.ba_profile(0) if c4 else None
     front = {k: v for k, v in per_kernel_us.items() if k not in ("local_ba", "tsdf")}
@@ -490,27 +609,14 @@ def main() -> None:
                 "algorithmic_flops_per_launch": flops, "avg_launch_us": avg_us, "launches_timed": schur["launches"],
                 "time_per_step_us": schur["ms"] * 1e3 / args.steps}
         mfma["frac"] = mfma["achieved"] / mfma["peak"]
-
-    traffic = None
-    valu = None
-    pmc_path = Path(args.pmc)
-    if pmc_path.exists():
-        pmc = json.loads(pmc_path.read_text())
-        kern = pmc.get("kernels", {}).get(KERNEL_SYMBOL.get(dom, ""), None)
-        if kern is not None and pmc.get("batch_frames") == B and pmc.get("config", "c2") == args.config:
-            traffic = kern["hbm_bytes_per_launch"]
-            if kern.get("valu_insts_per_launch"):
-                # the path is integer-VALU bound: wave64 VALU instructions per launch
-                # (PMC SQ_INSTS_VALU) / the same event-timed duration, against the issue peak
-                rate = kern["valu_insts_per_launch"] / (per_kernel_us[dom] * 1e-6)
-                valu = {"bound": "valu", "achieved": rate / 1e12, "peak": VALU_PEAK_WINST / 1e12,
-                        "unit": "T wave-instructions/s", "frac": rate / VALU_PEAK_WINST,
-                        "insts_per_launch": kern["valu_insts_per_launch"]}
+    traffic, valu, traffic_note = pmc_traffic(args, dom, per_kernel_us, B)
 
     # ---- B = 1 latency: one frame submitted and its pose read back -------------
     lat_ms = None
     if rank == 0 and args.latency_frames > 0:
-        h1 = Handle([rect], cfg, max_batch=1, device=dev_index)
+        h1 = Handle(rects, cfg, max_batch=1, device=dev_index)
+        if P > 1:
+            h1.set_rig(E)
         lat = []
         for i in range(args.latency_frames + 3):
             torch.cuda.synchronize()
@@ -531,11 +637,12 @@ def main() -> None:
         "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS,
         "traffic": traffic,
+        "traffic_note": traffic_note,
         "algorithmic_bytes_per_launch": dom_bytes,
         "algorithmic_bytes_per_frame": unit_bytes,
         "frames_per_launch": B,
         "avg_launch_us": per_kernel_us[dom],
-        "kernel_own_bytes_per_launch": None if c5 else kernel_bytes(dom, B, h, cfg, rect.is_identity),
+        "kernel_own_bytes_per_launch": None if c5 else kernel_bytes(dom, B, h, cfg, rect.is_identity, n_img),
         "end_to_end_hbm_frac": unit_bytes * (frames_total / elapsed / world) / (HBM_PEAK_GBS * 1e9),
         "valu": valu,
     }
@@ -558,51 +665,234 @@ def main() -> None:
         workload = ("C4: 1x stereo pair 1280x800, 4000 FAST/rBRIEF keypoints per image, 4 levels, stereo+temporal "
                     "brute-force Hamming, P3P-RANSAC(128)+GN pose, 10-keyframe local BA (keyframe every 5 frames, "
                     "5 Gauss-Newton iterations, Schur complement on FP64 MFMA)")
+    elif c3:
+        workload = ("C3: 4x OAK stereo rig (8 streams, brackets.urdf joints, sources of run_slam.py:45-50) 640x400, "
+                    "2000 FAST/rBRIEF keypoints per image, per-pair stereo+temporal brute-force Hamming + "
+                    "P3P-RANSAC(128)+GN, rig pose by generalised PnP over all pairs, on one GPU")
     else:
         workload = ("C2: 1x stereo pair 640x400 per GPU, 2000 FAST/rBRIEF keypoints per image, 4 levels, "
                     "stereo+temporal brute-force Hamming, P3P-RANSAC(128)+GN pose")
+    value = frames_total / elapsed
     out = {
-        "metric": METRIC_C4 if c4 else METRIC_C5 if c5 else METRIC,
-        "value": frames_total / elapsed,
+        "metric": METRIC_C4 if c4 else METRIC_C5 if c5 else METRIC_C3 if c3 else METRIC,
+        "value": value,
         "unit": "frames/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if c3 else "weak",
         "vs_baseline": None,
-        "dtype": "u8" + ("+f64" if c4 else ""),
+        "dtype": "u8" + ("+f64" if (c4 or c3) else ""),
         "data": f"synthetic: seeded room renderer, {args.unique} distinct {width}x{height} "
-                f"{'RGB-D' if c5 else 'stereo'} frames per rank replayed as a triangle wave, resident in HBM before timing",
+                f"{'RGB-D' if c5 else 'rig' if c3 else 'stereo'} frames per rank replayed as a triangle wave, "
+                f"resident in HBM before timing",
         "config": {
             "workload": workload,
             "frames_per_step": B,
             "n_features": cfg.n_features,
-            "parallelism": f"one {'RGB-D camera' if c5 else 'stereo source'} per GPU x{world}"
-                           + (" + RCCL all-gather of keypoints/descriptors/poses + on-device rig fusion"
-                              if world > 1 else ""),
+            "parallelism": (f"one {'RGB-D camera' if c5 else 'stereo source'} per GPU x{world}"
+                            + (" (independent replicas)" if world > 1 else "")) if not c3 else "the whole rig on 1 GPU",
         },
         "roofline": roofline,
         "latency_b1_ms": lat_ms,
         "per_kernel_us_per_batch": per_kernel_us,
         "per_kernel_us_isolated": iso_us,
         "tracking_ok_fraction_last_batch": ok_frac,
-        "rig_fusion_ok_fraction_last_batch": rig_ok,
+        "rig_ok_fraction_last_batch": rig_ok,
         "render_s": t_render,
     }
+    if c3:
+        out["stereo_pair_frames_per_s"] = value * P
     if front_roofline is not None:
         out["front_end_roofline"] = front_roofline
     if "tsdf" in names:
         out["dense_map"] = tsdf_report(h, per_kernel_us["tsdf"], B, width, height)
-    if rank == 0 and args.cpu_budget > 0:
-        if c5:
-            out["cpu_baseline"] = cpu_baseline_rgbd(np.stack([b for b, _ in rgbd_frames]), np.stack([d for _, d in rgbd_frames]),
-                                                    rect, cfg, args.cpu_budget, args.cpu_procs)
-        else:
-            out["cpu_baseline"] = cpu_baseline(uniq, rect, cfg, args.cpu_budget, args.cpu_procs)
-        out["cpu_baseline"]["host_cpus_visible"] = os.cpu_count()
     h.close()
+    if rank == 0 and world == 1 and args.boundary_frames > 0 and args.config == "c2":
+        out["boundary"] = boundary_bench(uniq, src, args.boundary_frames)
+    if rank == 0 and world == 1 and args.cpu_budget > 0:
+        procs = args.cpu_procs or usable_cpus()
+        if c5:
+            bgr = np.stack([b for b, _ in rgbd_frames])
+            dep = np.stack([d for _, d in rgbd_frames])
+            out["cpu_baseline"] = cpu_baseline((bgr, dep), _rect_dict(rect), cfg, args.cpu_budget, procs,
+                                               f"synthetic {width}x{height} RGB-D frames ({len(bgr)} distinct)")
+        elif c3:
+            out["cpu_baseline"] = cpu_baseline(uniq, [[_rect_dict(r) for r in rects], E], cfg, args.cpu_budget, procs,
+                                               f"synthetic {width}x{height} 8-stream rig frames ({len(uniq)} distinct)")
+            out["cpu_baseline"]["unit"] = "rig frames/s"
+        else:
+            out["cpu_baseline"] = cpu_baseline(uniq, _rect_dict(rect), cfg, args.cpu_budget, procs,
+                                               f"synthetic {width}x{height} stereo frames ({len(uniq)} distinct)")
+    return out
+
+
+# ---- sharded rig (N > 1): one camera stream per GPU -------------------------------------------
+def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
+    import torch
+    import torch.distributed as dist
+
+    from thor_slam_amd.params import HipSlamConfig
+    from thor_slam_amd.shard import DistShardedRig, ShardPlan, StageTimer
+
+    c3 = args.config == "c3"
+    if not c3 and world % 2:
+        raise SystemExit("c2 over several GPUs shards stereo pairs' streams: --gpus must be even")
+    names = RIG_SOURCES if c3 else RIG_SOURCES[:world // 2]
+    width, height = 640, 400
+    cfg = HipSlamConfig()
+    B = args.batch or 256
+    args.unique = args.unique or 48
+    _, cams, pairs, rects, E = rig_setup(names, width, height)
+    P, C = len(rects), 2 * len(rects)
+    plan = ShardPlan(C, world, B)
+    c0, c1 = plan.cams(rank)
+    workers = max(1, min(16, max(2, usable_cpus() // max(1, world)), args.unique * (c1 - c0)))
+    t_r = time.perf_counter()
+    uniq = render_rig_frames(names, args.unique, c0, c1, workers, width, height)   # this rank's streams only
+    t_render = time.perf_counter() - t_r
+    total = (args.warmup + args.steps) * B
+    idx = torch.from_numpy(triangle_indices(total, args.unique)).cuda()
+    seq = torch.from_numpy(uniq).cuda().index_select(0, idx).contiguous()   # [total, S, H, W] in HBM
+    rig = DistShardedRig(rects, cfg, B, base_T_rect=E if P > 1 else None, device=dev_index, exchange=args.exchange,
+                         front_priority=bool(args.front_priority))
+    for s in range(args.warmup):
+        rig.step(seq[s * B:(s + 1) * B])
+    rig.drain()
+    dist.barrier()
+    torch.cuda.synchronize()
+    timer = StageTimer()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        s = args.warmup + k
+        rig.step(seq[s * B:(s + 1) * B], timer)
+    rig.drain()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    elapsed = float(tt.item())
+    res = rig.read()
+    ok = float(np.mean(res["pairs"]["stats"][:, :, 0] == 0))
+    rig_ok = float(np.mean(res["rig"]["stats"][:, 0] == 0)) if P > 1 else None
+    per_kernel_us = timer.mean_us()
+    # the dominant kernel's algorithmic bytes: the §8d rig-frame bytes x the share of the rig one
+    # launch covers (front kernels: S of C streams for B frames; back kernels: all streams for B/N frames)
+    S = plan.streams_per_rank
+    unit_bytes = frame_bytes(width, height, cfg.n_features, n_img=2 * P, n_pairs=P)   # per rig frame
+    front = ("rectify_pyramid", "detect", "select", "describe")
+    dom = max(per_kernel_us, key=per_kernel_us.get)
+    share = (S / C) * B if dom in front else B / world
+    dom_bytes = unit_bytes * share
+    achieved = dom_bytes / (per_kernel_us[dom] * 1e-6) / 1e9
+    sb, pr = rig.rk.block, rig.rk.record
+    alltoall = args.exchange == "alltoall"
+    xbytes = {  # what one rank sends per step
+        "raw_images": ((world - 1) * plan.recv_frames if alltoall else (B + 1)) * S * width * height,
+        "stream_blocks": ((world - 1) * plan.recv_frames if alltoall else (B + 1)) * S * sb,
+        "pose_records": plan.frames_per_rank * pr,
+        "stream_block_bytes": sb,
+        "pose_record_bytes": pr,
+    }
+    rig.close()
+    frames_total = args.steps * B        # rig frames
+    value = frames_total / elapsed * (1 if c3 else P)
+    out = {
+        "metric": METRIC_C3 if c3 else METRIC,
+        "value": value,
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong" if c3 else "weak",
+        "vs_baseline": None,
+        "dtype": "u8+f64",
+        "data": f"synthetic: seeded room renderer, {args.unique} distinct 640x400 frames of each rank's camera "
+                f"streams (bracket rig, one shared room) replayed as a triangle wave, resident in HBM before timing",
+        "config": {
+            "workload": ("C3: 4x OAK stereo rig (8 streams, brackets.urdf joints, sources of run_slam.py:45-50)"
+                         if c3 else f"C2 streams over {world} GPUs: {P} stereo source(s) of the bracket rig "
+                                    f"({C} streams), one camera stream per GPU")
+                        + ", 640x400, 2000 FAST/rBRIEF keypoints per image, per-pair stereo+temporal Hamming + "
+                          "P3P-RANSAC(128)+GN" + (", rig pose by generalised PnP over all pairs" if P > 1 else ""),
+            "frames_per_step": B,
+            "streams": C,
+            "stereo_pairs": P,
+            "n_features": cfg.n_features,
+            "parallelism": (f"{S} camera stream(s) per GPU x{world}: front end per stream, RCCL "
+                            f"{'all-to-all' if alltoall else 'all-gather'} of raw images + keypoint/descriptor "
+                            f"stream blocks, per-pair back end + rig pose on each GPU's {plan.frames_per_rank}-frame "
+                            f"range, RCCL all-gather of pose records"),
+        },
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "algorithmic_bytes_per_launch": dom_bytes, "algorithmic_bytes_per_rig_frame": unit_bytes,
+                     "avg_launch_us": per_kernel_us[dom], "rank": rank},
+        "per_kernel_us_per_batch": per_kernel_us,
+        "exchange_bytes_per_step": xbytes,
+        "tracking_ok_fraction_last_batch": ok,
+        "rig_ok_fraction_last_batch": rig_ok,
+        "render_s": t_render,
+    }
+    if c3:
+        out["stereo_pair_frames_per_s"] = value * P
+    else:
+        out["rig_frames_per_s"] = frames_total / elapsed
+    return out
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
+                    help="BASELINE.json configs[1] (c2), configs[2] (c3), configs[3] (c4) or configs[4] (c5)")
+    ap.add_argument("--batch", type=int, default=0, help="frames per step (0 = 256 for c2/c3, 50 for c4, 128 for c5)")
+    ap.add_argument("--unique", type=int, default=0, help="distinct rendered frames, triangle-wave replay (0 = 48 / 24)")
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-procs", type=int, default=0, help="oracle processes for the CPU baseline (0 = usable CPUs)")
+    ap.add_argument("--latency-frames", type=int, default=20, help="B=1 submissions timed for latency_b1_ms")
+    ap.add_argument("--boundary-frames", type=int, default=1024,
+                    help="c2: frames timed through HipSlamEngine.process_frames (0 = skip)")
+    ap.add_argument("--out", type=str, default="", help="also write the JSON line to this file")
+    ap.add_argument("--dist-backend", type=str, default="nccl", help="nccl (RCCL) or gloo (rehearsal, host copy)")
+    ap.add_argument("--exchange", choices=["alltoall", "allgather"], default="alltoall",
+                    help="sharded rig: all-to-all of the frames each rank solves, or all-gather of everything")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="1: front and back kernels on two streams (batch s+1's front overlaps batch s's back)")
+    ap.add_argument("--front-priority", type=int, default=1,
+                    help="1: run the front kernels on a high-priority stream (pipelined mode)")
+    ap.add_argument("--tsdf", type=int, default=0,
+                    help="c5: also integrate every batch's depth into a TSDF volume with the device poses "
+                         "(nvblox-shaped dense map, SURVEY.md §8f item 4); reported under dense_map")
+    ap.add_argument("--pmc", type=str, default=str(ROOT / "profiles" / "pmc_latest.json"),
+                    help="PMC summary (tools/pmc_summary.py) used for roofline.traffic when its batch matches")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.config == "c4" and world > 1:
+        raise SystemExit("--config c4 is a single-GPU configuration")
+    dev_index = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(args.dist_backend)
+    sharded = world > 1 and args.config in ("c2", "c3")
+    out = run_sharded(args, world, rank, dev_index) if sharded else run_single(args, world, rank, dev_index)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
