@@ -163,6 +163,30 @@ int tslam_pose(tslam_handle* h, void* stream);
 
 int tslam_sync(tslam_handle* h);
 
+/* Asynchronous host boundary (what IsaacRosAdapter.process_frames + _odom_cb do over DDS,
+ * isaac_ros.py:327-430 and :308-325; the pose may lag the frame, :429-430).
+ *
+ * tslam_submit_host: copy `n_frames` host frames ([n][2*n_pairs][H][W] gray, or RGB-D records
+ *   [n][n_pairs][5*H*W]) into the handle's pinned staging buffer of the batch's parity (waiting
+ *   only for that buffer's previous DMA), enqueue the DMA and the whole hot path on the handle's
+ *   own streams (front stages on a high-priority stream overlapping the previous batch's back
+ *   stages) and the batch's results into a pinned slot; returns without waiting for the device.
+ *   timestamps[n] (seconds, the frames' SynchronizedFrameSet.timestamp) may be NULL.  At most two
+ *   batches' results are held: an unread batch s-2 is dropped when batch s is submitted.
+ * tslam_poll_batch: results of the oldest unread submitted batch: returns 1 and fills the outputs
+ *   (per frame and pair as tslam_read_poses, the rig's T_abs/cov/stats when tslam_set_rig, the
+ *   timestamps, its first global frame and frame count) when it has completed (or, with `block`,
+ *   after waiting for it); 0 when no batch is ready / pending.  Pointers may be NULL.
+ * tslam_poll_pose: non-blocking; the last frame of the newest completed batch not returned before:
+ *   T[16] = its T_abs (the rig's world_T_base after tslam_set_rig, else the first pair's left-camera
+ *   pose), cov[36], ts, state (TSLAM_POSE_*), conf = clamp(1 / (1 + tr(cov[:3,:3])), 0, 1)
+ *   (isaac_ros.py:312; 1 when not tracked).  Returns 1 when a newer pose was written, else 0. */
+int tslam_submit_host(tslam_handle* h, const uint8_t* host_images, const double* timestamps, int n_frames);
+int tslam_poll_batch(tslam_handle* h, int block, int max_frames, double* T_rel, double* T_abs, double* cov, int32_t* stats,
+                     double* rig_T_abs, double* rig_cov, int32_t* rig_stats, double* ts, int64_t* first_frame,
+                     int* n_frames);
+int tslam_poll_pose(tslam_handle* h, double* T, double* cov, double* ts, int32_t* state, float* conf);
+
 /* Results of the last submitted batch (blocks until it is done).  Per frame f and pair p
  * (index f * n_pairs + p): T_rel[16] (cam_{t-1} -> cam_t), T_abs[16] (first left camera frame ->
  * current left camera frame, row-major), cov[36] (rho, omega), stats[8] = {status, n_corr,

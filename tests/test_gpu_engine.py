@@ -117,7 +117,9 @@ def test_engine_two_source_rig_solves_body_motion():
     eng.initialize(rig.calibration)
     n = 6
     for _ in range(n):
-        pose = eng.process_frames(rig.get_synchronized_frames())
+        eng.process_frames(rig.get_synchronized_frames())
+    eng.flush()   # batches may still be in flight (asynchronous submission): publish them all
+    pose = eng._latest_pose
     assert eng.get_tracking_state() == TrackingState.TRACKING
     # oracle: track each pair on the CPU and fuse with the same host rule
     cams = extract_cameras(rig.calibration, 4)
@@ -175,3 +177,79 @@ def test_stream_blocks_roundtrip():
     np.testing.assert_array_equal(kp[:, 0] & 0xFFFF, want["x"])
     h.close()
     h2.close()
+
+
+def test_submit_host_async_matches_device_submit():
+    """tslam_submit_host (pinned double-buffered staging, own streams, results in pinned slots)
+    gives the same poses as tslam_submit on device frames; tslam_poll_batch returns batches in
+    order with their timestamps; tslam_poll_pose returns the newest completed frame once, with
+    the isaac_ros.py:312 confidence."""
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    sc = scenario(seed=0, n=6)
+    cfg, rect = sc["cfg"], sc["rect"]
+    frames = np.ascontiguousarray(sc["frames"])
+    ref = Handle([rect], cfg, max_batch=2)
+    dev = torch.from_numpy(frames).cuda()
+    want = []
+    for b in range(3):
+        ref.submit(dev[2 * b].data_ptr(), 2, torch.cuda.current_stream().cuda_stream)
+        want.append(ref.read_poses(2))
+    ref.close()
+    h = Handle([rect], cfg, max_batch=2)
+    got = []
+    for b in range(3):
+        if b == 2:   # two batches in flight at most: collect the oldest first
+            got.append(h.poll_batch(block=True))
+        h.submit_host(frames[2 * b:2 * b + 2], [10.0 + 2 * b, 10.0 + 2 * b + 1])
+    while len(got) < 3:
+        got.append(h.poll_batch(block=True))
+    assert h.poll_batch(block=True) is None
+    for b, (g, w) in enumerate(zip(got, want)):
+        assert g["first_frame"] == 2 * b and g["n"] == 2
+        np.testing.assert_array_equal(g["timestamps"], [10.0 + 2 * b, 11.0 + 2 * b])
+        np.testing.assert_array_equal(g["T_abs"], w["T_abs"])
+        np.testing.assert_array_equal(g["stats"], w["stats"])
+    p = h.poll_pose()
+    assert p is not None and p["timestamp"] == 15.0 and p["state"] == 0
+    np.testing.assert_array_equal(p["T"], want[2]["T_abs"][1, 0])
+    cov = want[2]["cov"][1, 0]
+    assert abs(p["confidence"] - min(1.0, max(0.0, 1.0 / (1.0 + np.trace(cov[:3, :3]))))) < 1e-6
+    assert h.poll_pose() is None   # nothing newer
+    h.close()
+
+
+def test_engine_async_equals_sync():
+    """HipSlamEngine with batches in flight (loop closure off) publishes the same poses as the
+    synchronous mode (loop closure on, which waits for every batch)."""
+    from thor_slam_amd.camera.rig import CameraRig
+    from thor_slam_amd.params import HipSlamConfig
+    from thor_slam_amd.slam.hip_engine import HipSlamEngine
+
+    from helpers import make_source
+
+    poses = {}
+    for mode, loop in (("async", False), ("sync", True)):
+        src = make_source(seed=1, n_frames=40)
+        rig = CameraRig([src])
+        rig.start()
+        eng = HipSlamEngine(num_cameras=2, config=HipSlamConfig(batch_size=3, enable_loop_closure=loop))
+        eng.initialize(rig.calibration)
+        out = []
+        for _ in range(10):
+            p = eng.process_frames(rig.get_synchronized_frames())
+            out.append(None if p is None else (p.timestamp, p.to_4x4_matrix()))
+        eng.flush()
+        last = eng.process_frames(rig.get_synchronized_frames())
+        eng.flush()
+        poses[mode] = (out, eng._latest_pose.to_4x4_matrix(), eng._latest_pose.timestamp)
+        eng.shutdown()
+    a, s = poses["async"], poses["sync"]
+    np.testing.assert_allclose(a[1], s[1], rtol=0, atol=1e-12)
+    assert a[2] == s[2]
+    # async publishes lag by at most one batch, never run ahead of the sync mode
+    for (pa, ps) in zip(a[0], s[0]):
+        if pa is not None and ps is not None:
+            assert pa[0] <= ps[0]

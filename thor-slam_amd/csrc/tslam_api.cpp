@@ -126,6 +126,27 @@ struct tslam_handle {
     // sharded rig (tslam_set_shard): front-end cameras [sh_cam_lo, sh_cam_hi) and back-end frames
     // [rank * n / world, (rank + 1) * n / world) of every batch
     int sh_cam_lo = 0, sh_cam_hi = 0, sh_rank = 0, sh_world = 1;
+    // asynchronous host boundary (tslam_submit_host / tslam_poll_*): the handle's own front/back
+    // streams, pinned staging + device input per batch parity, pinned result slots per parity
+    hipStream_t as_front = nullptr, as_back = nullptr;
+    uint8_t* as_stage[2] = {nullptr, nullptr};   // pinned host
+    uint8_t* as_input[2] = {nullptr, nullptr};   // device
+    hipEvent_t as_staged[2] = {nullptr, nullptr};   // DMA out of as_stage[k] done
+    bool as_staged_armed[2] = {false, false};
+    struct ResultSlot {
+        double* pose = nullptr;       // pinned [B][P][68]
+        int32_t* stats = nullptr;     // pinned [B][P][8]
+        double* rig_pose = nullptr;   // pinned [B][68]
+        int32_t* rig_stats = nullptr; // pinned [B][8]
+        std::vector<double> ts;
+        hipEvent_t ev = nullptr;
+        int64_t batch = -1, g0 = 0;
+        int n = 0;
+        bool pending = false;         // completed or in flight, not yet returned by tslam_poll_batch
+    } as_res[2];
+    int64_t as_batches = 0;           // batches submitted through tslam_submit_host
+    int64_t as_last_pose_batch = -1;  // newest batch tslam_poll_pose returned
+    std::vector<void*> host_allocs;
 };
 
 static int dev_alloc(tslam_handle* h, void** p, size_t bytes) {
@@ -150,6 +171,8 @@ static int dev_realloc(tslam_handle* h, void** p, size_t bytes) {
 static void free_all(tslam_handle* h) {
     for (void* p : h->allocs) (void)hipFree(p);
     h->allocs.clear();
+    for (void* p : h->host_allocs) (void)hipHostFree(p);
+    h->host_allocs.clear();
 }
 
 static void build_geometry(tslam_handle* h) {
@@ -591,8 +614,11 @@ int tslam_destroy(tslam_handle* h) {
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();
     for (hipEvent_t e : h->ba_events) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {h->ev_fe, h->ev_ba[0], h->ev_ba[1], h->ev_front, h->ev_back[0], h->ev_back[1]})
+    for (hipEvent_t e : {h->ev_fe, h->ev_ba[0], h->ev_ba[1], h->ev_front, h->ev_back[0], h->ev_back[1],
+                         h->as_staged[0], h->as_staged[1], h->as_res[0].ev, h->as_res[1].ev})
         if (e) (void)hipEventDestroy(e);
+    for (hipStream_t st : {h->as_front, h->as_back})
+        if (st) (void)hipStreamDestroy(st);
     free_all(h);
     delete h;
     return TSLAM_OK;
@@ -622,7 +648,157 @@ int tslam_reset(tslam_handle* h) {
     h->back_pending[0] = h->back_pending[1] = false;
     h->in_batch = false;
     h->cur_n = 0;
+    for (auto& r : h->as_res) r.pending = false;   // results of batches before the reset are dropped
+    h->as_last_pose_batch = h->as_batches - 1;
     return TSLAM_OK;
+}
+
+// -- asynchronous host boundary -------------------------------------------------------------------
+static int64_t host_frame_bytes(const tslam_handle* h) {
+    return h->prm.rgbd ? (int64_t)h->P * 5 * h->W * h->H : (int64_t)h->C * h->W * h->H;
+}
+
+static int ensure_async(tslam_handle* h) {
+    if (h->as_front) return TSLAM_OK;
+    int lo = 0, hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIPCHK(hipStreamCreateWithPriority(&h->as_front, hipStreamNonBlocking, hi));   // front = critical path
+    HIPCHK(hipStreamCreateWithFlags(&h->as_back, hipStreamNonBlocking));
+    const size_t in_bytes = (size_t)h->B * host_frame_bytes(h);
+    const size_t B = h->B, P = h->P;
+    for (int k = 0; k < 2; ++k) {
+        void* p = nullptr;
+        HIPCHK(hipHostMalloc(&p, in_bytes, hipHostMallocDefault));
+        h->host_allocs.push_back(p);
+        h->as_stage[k] = (uint8_t*)p;
+        int rc = dev_alloc(h, (void**)&h->as_input[k], in_bytes);
+        if (rc != TSLAM_OK) return rc;
+        HIPCHK(hipEventCreateWithFlags(&h->as_staged[k], hipEventDisableTiming));
+        auto& r = h->as_res[k];
+        const size_t bytes[4] = {8 * B * P * TS_POSE_DOUBLES, 4 * B * P * TS_STATS_INTS, 8 * B * TS_POSE_DOUBLES,
+                                 4 * B * TS_STATS_INTS};
+        void** dst[4] = {(void**)&r.pose, (void**)&r.stats, (void**)&r.rig_pose, (void**)&r.rig_stats};
+        for (int i = 0; i < 4; ++i) {
+            HIPCHK(hipHostMalloc(dst[i], bytes[i], hipHostMallocDefault));
+            h->host_allocs.push_back(*dst[i]);
+        }
+        r.ts.assign(B, 0.0);
+        HIPCHK(hipEventCreateWithFlags(&r.ev, hipEventDisableTiming));
+    }
+    return TSLAM_OK;
+}
+
+int tslam_submit_host(tslam_handle* h, const uint8_t* host_images, const double* timestamps, int n_frames) {
+    if (!h || !host_images) return fail(TSLAM_EINVAL, "bad argument");
+    if (n_frames < 1 || n_frames > h->B) return fail(TSLAM_EINVAL, "n_frames must be in [1, max_batch]");
+    if (h->sh_world > 1) return fail(TSLAM_ESTATE, "a sharded handle is driven stage by stage");
+    HIPCHK(hipSetDevice(h->device));
+    int rc = ensure_async(h);
+    if (rc != TSLAM_OK) return rc;
+    const int k = (int)(h->as_batches & 1);
+    const size_t bytes = (size_t)n_frames * host_frame_bytes(h);
+    // the staging buffer of this parity is free once the DMA of batch s-2 out of it finished
+    if (h->as_staged_armed[k]) HIPCHK(hipEventSynchronize(h->as_staged[k]));
+    memcpy(h->as_stage[k], host_images, bytes);
+    // the device input of this parity: batch s-2's rectify read it earlier on the same stream
+    HIPCHK(hipMemcpyAsync(h->as_input[k], h->as_stage[k], bytes, hipMemcpyHostToDevice, h->as_front));
+    HIPCHK(hipEventRecord(h->as_staged[k], h->as_front));
+    h->as_staged_armed[k] = true;
+    if ((rc = tslam_begin_batch(h, h->as_input[k], n_frames)) != TSLAM_OK) return rc;
+    const int stages[5] = {TSLAM_STAGE_RECTIFY, TSLAM_STAGE_DETECT, TSLAM_STAGE_DESCRIBE, TSLAM_STAGE_MATCH, TSLAM_STAGE_POSE};
+    for (int i = 0; i < 5 && rc == TSLAM_OK; ++i) rc = tslam_run_stage(h, stages[i], i < 3 ? h->as_front : h->as_back);
+    if (rc == TSLAM_OK && h->prm.ba_window) rc = tslam_run_stage(h, TSLAM_STAGE_BA, h->as_back);
+    const int64_t g0 = h->cur_g0;
+    const int rc2 = tslam_end_batch(h);
+    if (rc != TSLAM_OK || rc2 != TSLAM_OK) return rc != TSLAM_OK ? rc : rc2;
+    // results of this batch into the pinned slot of its parity (an unread batch s-2 there is dropped)
+    auto& r = h->as_res[k];
+    const size_t n = n_frames, P = h->P;
+    HIPCHK(hipMemcpyAsync(r.pose, h->buf[TSLAM_BUF_POSE].ptr, 8 * n * P * TS_POSE_DOUBLES, hipMemcpyDeviceToHost, h->as_back));
+    HIPCHK(hipMemcpyAsync(r.stats, h->buf[TSLAM_BUF_STATS].ptr, 4 * n * P * TS_STATS_INTS, hipMemcpyDeviceToHost, h->as_back));
+    if (h->rig) {
+        HIPCHK(hipMemcpyAsync(r.rig_pose, h->d_rig_pose, 8 * n * TS_POSE_DOUBLES, hipMemcpyDeviceToHost, h->as_back));
+        HIPCHK(hipMemcpyAsync(r.rig_stats, h->d_rig_stats, 4 * n * TS_STATS_INTS, hipMemcpyDeviceToHost, h->as_back));
+    }
+    HIPCHK(hipEventRecord(r.ev, h->as_back));
+    for (int i = 0; i < n_frames; ++i) r.ts[i] = timestamps ? timestamps[i] : (double)(g0 + i);
+    r.batch = h->as_batches;
+    r.g0 = g0;
+    r.n = n_frames;
+    r.pending = true;
+    h->as_batches += 1;
+    return TSLAM_OK;
+}
+
+static void unpack_records(const double* pose, int n, double* T_rel, double* T_abs, double* cov) {
+    for (int i = 0; i < n; ++i) {
+        const double* src = pose + (size_t)i * TS_POSE_DOUBLES;
+        if (T_rel) memcpy(T_rel + 16 * (size_t)i, src, 16 * sizeof(double));
+        if (T_abs) memcpy(T_abs + 16 * (size_t)i, src + 16, 16 * sizeof(double));
+        if (cov) memcpy(cov + 36 * (size_t)i, src + 32, 36 * sizeof(double));
+    }
+}
+
+int tslam_poll_batch(tslam_handle* h, int block, int max_frames, double* T_rel, double* T_abs, double* cov, int32_t* stats,
+                     double* rig_T_abs, double* rig_cov, int32_t* rig_stats, double* ts, int64_t* first_frame,
+                     int* n_frames) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    HIPCHK(hipSetDevice(h->device));
+    // the oldest unread batch
+    int k = -1;
+    for (int i = 0; i < 2; ++i)
+        if (h->as_res[i].pending && (k < 0 || h->as_res[i].batch < h->as_res[k].batch)) k = i;
+    if (k < 0) return 0;
+    auto& r = h->as_res[k];
+    if (block) {
+        HIPCHK(hipEventSynchronize(r.ev));
+    } else {
+        const hipError_t q = hipEventQuery(r.ev);
+        if (q == hipErrorNotReady) return 0;
+        if (q != hipSuccess) return fail(TSLAM_EHIP, std::string("hipEventQuery: ") + hipGetErrorString(q));
+    }
+    if (max_frames < r.n) return fail(TSLAM_EINVAL, "output capacity (max_frames) is smaller than the batch");
+    const int np = r.n * h->P;
+    unpack_records(r.pose, np, T_rel, T_abs, cov);
+    if (stats) memcpy(stats, r.stats, sizeof(int32_t) * TS_STATS_INTS * np);
+    if (h->rig) {
+        unpack_records(r.rig_pose, r.n, nullptr, rig_T_abs, rig_cov);
+        if (rig_stats) memcpy(rig_stats, r.rig_stats, sizeof(int32_t) * TS_STATS_INTS * r.n);
+    }
+    if (ts) memcpy(ts, r.ts.data(), sizeof(double) * r.n);
+    if (first_frame) *first_frame = r.g0;
+    if (n_frames) *n_frames = r.n;
+    r.pending = false;
+    return 1;
+}
+
+int tslam_poll_pose(tslam_handle* h, double* T, double* cov, double* ts, int32_t* state, float* conf) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    HIPCHK(hipSetDevice(h->device));
+    int k = -1;   // the newest completed batch
+    for (int i = 0; i < 2; ++i) {
+        const auto& r = h->as_res[i];
+        if (r.batch < 0 || r.batch <= h->as_last_pose_batch || (k >= 0 && r.batch < h->as_res[k].batch)) continue;
+        const hipError_t q = hipEventQuery(r.ev);
+        if (q == hipErrorNotReady) continue;
+        if (q != hipSuccess) return fail(TSLAM_EHIP, std::string("hipEventQuery: ") + hipGetErrorString(q));
+        k = i;
+    }
+    if (k < 0) return 0;
+    const auto& r = h->as_res[k];
+    const int f = r.n - 1;
+    const double* rec = h->rig ? r.rig_pose + (size_t)f * TS_POSE_DOUBLES : r.pose + (size_t)f * h->P * TS_POSE_DOUBLES;
+    const int32_t* st = h->rig ? r.rig_stats + (size_t)f * TS_STATS_INTS : r.stats + (size_t)f * h->P * TS_STATS_INTS;
+    if (T) memcpy(T, rec + 16, 16 * sizeof(double));
+    if (cov) memcpy(cov, rec + 32, 36 * sizeof(double));
+    if (ts) *ts = r.ts[f];
+    if (state) *state = st[0];
+    if (conf) {   // isaac_ros.py:312: clamp(1 / (1 + trace(cov[:3, :3])), 0, 1); 1 when not tracked
+        const double tr = rec[32] + rec[32 + 7] + rec[32 + 14];
+        *conf = st[0] == TSLAM_POSE_OK ? (float)std::min(1.0, std::max(0.0, 1.0 / (1.0 + tr))) : 1.0f;
+    }
+    h->as_last_pose_batch = r.batch;
+    return 1;
 }
 
 int64_t tslam_frames_done(tslam_handle* h) { return h ? h->frames_done : -1; }

@@ -86,6 +86,10 @@ _SIGNATURES = {
     "tslam_set_rig": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_set_motion_prior": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "tslam_read_rig_poses": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 4),
+    "tslam_submit_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "tslam_poll_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 8
+                         + [ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int)]),
+    "tslam_poll_pose": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 5),
     "tslam_set_shard": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "tslam_exchange_sizes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "tslam_pack_streams": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -291,6 +295,48 @@ class Handle:
         _check(self.lib.tslam_read_rig_poses(self.h, int(n_frames), t_rel.ctypes.data, t_abs.ctypes.data, cov.ctypes.data,
                                              stats.ctypes.data))
         return {"T_rel": t_rel, "T_abs": t_abs, "cov": cov, "stats": stats}
+
+    # -- asynchronous host boundary ------------------------------------------------------------
+    def submit_host(self, images: np.ndarray, timestamps=None) -> None:
+        """Host frames [n][...] (contiguous u8: [n][2P][H][W] gray or [n][P][5HW] RGB-D) -> the
+        device, asynchronously (tslam_submit_host)."""
+        images = np.ascontiguousarray(images, dtype=np.uint8)
+        n = int(images.shape[0])
+        ts = None if timestamps is None else np.ascontiguousarray(timestamps, dtype=np.float64)
+        _check(self.lib.tslam_submit_host(self.h, images.ctypes.data, None if ts is None else ts.ctypes.data, n))
+
+    def poll_batch(self, block: bool = False) -> dict | None:
+        """Results of the oldest unread submitted batch, or None when none is ready."""
+        B, P = self.max_batch, self.n_pairs
+        t_rel, t_abs = np.zeros((B, P, 4, 4)), np.zeros((B, P, 4, 4))
+        cov, stats = np.zeros((B, P, 6, 6)), np.zeros((B, P, 8), dtype=np.int32)
+        r_abs, r_cov, r_st = np.zeros((B, 4, 4)), np.zeros((B, 6, 6)), np.zeros((B, 8), dtype=np.int32)
+        ts = np.zeros(B)
+        g0, n = ctypes.c_int64(), ctypes.c_int()
+        rc = self.lib.tslam_poll_batch(self.h, int(block), B, *(a.ctypes.data for a in (t_rel, t_abs, cov, stats, r_abs,
+                                                                                       r_cov, r_st, ts)),
+                                       ctypes.byref(g0), ctypes.byref(n))
+        if rc < 0:
+            _check(rc)
+        if rc == 0:
+            return None
+        k = n.value
+        out = {"T_rel": t_rel[:k], "T_abs": t_abs[:k], "cov": cov[:k], "stats": stats[:k], "timestamps": ts[:k],
+               "first_frame": int(g0.value), "n": k}
+        out["rig"] = {"T_abs": r_abs[:k], "cov": r_cov[:k], "stats": r_st[:k]}
+        return out
+
+    def poll_pose(self) -> dict | None:
+        """Newest completed pose not returned before (non-blocking), or None."""
+        T, cov = np.zeros((4, 4)), np.zeros((6, 6))
+        ts, st, conf = ctypes.c_double(), ctypes.c_int32(), ctypes.c_float()
+        rc = self.lib.tslam_poll_pose(self.h, T.ctypes.data, cov.ctypes.data, ctypes.addressof(ts), ctypes.addressof(st),
+                                      ctypes.addressof(conf))
+        if rc < 0:
+            _check(rc)
+        if rc == 0:
+            return None
+        return {"T": T, "cov": cov, "timestamp": ts.value, "state": st.value, "confidence": conf.value}
 
     # -- sharded rig (SURVEY.md §8e; thor_slam_amd/shard.py drives these) --------------------
     def set_shard(self, cam_lo: int, cam_hi: int, rank: int, world: int) -> None:

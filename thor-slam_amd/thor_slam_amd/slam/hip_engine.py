@@ -26,8 +26,13 @@ With ``dense_map`` (RGB-D input) every batch's depth of pair 0 is integrated int
 volume on the device with the batch's tracked poses (nvblox's role in the reference pipeline,
 ``scripts/run_pipeline.py:218-256``); ``get_dense_map`` returns it.
 ``confidence`` follows isaac_ros.py:312.  With ``batch_size > 1`` frames are staged and the
-batch runs on the GPU when full (or on ``flush``); the returned pose is then the latest completed
-one, as the reference allows (its pose lags the published frame, isaac_ros.py:429-430).
+batch runs on the GPU when full (or on ``flush``).  Submission is asynchronous
+(``tslam_submit_host``: pinned double-buffered staging, the batch's H2D copy and kernels on the
+handle's own streams, results copied back into pinned slots) and completed batches are
+published by non-blocking polls, so the host prepares batch s+1 while the device runs batch s;
+the returned pose is the latest completed one, as the reference allows (its pose lags the
+published frame, isaac_ros.py:429-430).  Local BA, loop closure and the dense map read device
+state per batch, so with those on every batch is waited for before the next one is staged.
 """
 
 from __future__ import annotations
@@ -58,6 +63,18 @@ def bgr_to_gray(img: np.ndarray) -> np.ndarray:
     g = img[..., 1].astype(np.int32)
     r = img[..., 2].astype(np.int32)
     return ((r * 4899 + g * 9617 + b * 1868 + 8192) >> 14).astype(np.uint8)
+
+
+def adjoint(t: np.ndarray) -> np.ndarray:
+    """SE(3) adjoint of a rigid 4x4 in the solver's (rho, omega) twist order: a left perturbation
+    exp(xi) of a pose P becomes exp(Ad_T xi) of T P T^-1, so cov' = Ad cov Ad^T with
+    Ad = [[R, [t]x R], [0, R]]."""
+    r, tv = t[:3, :3], t[:3, 3]
+    tx = np.array([[0.0, -tv[2], tv[1]], [tv[2], 0.0, -tv[0]], [-tv[1], tv[0], 0.0]])
+    ad = np.zeros((6, 6))
+    ad[:3, :3] = ad[3:, 3:] = r
+    ad[:3, 3:] = tx @ r
+    return ad
 
 
 def _invert(t: np.ndarray) -> np.ndarray:
@@ -121,6 +138,7 @@ class HipSlamEngine(SlamEngine):
         self._map_offset = np.eye(4)              # map world <- session world, set by relocalize()
         self._map_loaded = False
         self._loop: _LoopGraph | None = None     # set up by initialize() when loop closure is on
+        self._in_flight = 0                       # batches submitted, not yet published
 
     # ------------------------------------------------------------------------------------------
     def initialize(self, calibration: RigCalibration, config: SlamConfig | None = None) -> None:
@@ -220,30 +238,65 @@ class HipSlamEngine(SlamEngine):
         self._staged.append((imgs, float(frame_set.timestamp)))
         self._staged_gyro.append(self._gyro_of(frame_set))
         if len(self._staged) >= self._config.batch_size:
-            self.flush()
+            self._submit_staged()
+        self._drain(block=False)
         with self._pose_lock:
             return self._latest_pose
 
-    def flush(self) -> None:
-        """Run the staged frames through the GPU pipeline and publish their poses."""
-        if not self._staged or self._handle is None:
-            return
-        torch = self._torch
+    @property
+    def _async(self) -> bool:
+        """Batches may stay in flight across calls (nothing reads per-batch device state)."""
+        cfg = self._config
+        return cfg.ba_window <= 0 and self._loop is None and not cfg.dense_map
+
+    def _submit_staged(self) -> None:
         n = len(self._staged)
-        host = self._host_images.numpy()
-        for k, (imgs, _) in enumerate(self._staged):
-            host[k] = imgs
-        stream = torch.cuda.current_stream(self._device)
-        self._dev_images[:n].copy_(self._host_images[:n], non_blocking=True)
+        if n == 0:
+            return
         stamps = [ts for _, ts in self._staged]
         if self._config.imu_fusion:
             self._set_imu_prior(stamps, self._staged_gyro)
-        self._handle.submit(self._dev_images.data_ptr(), n, stream.cuda_stream)
-        self._integrate_depth(self._dev_images.data_ptr(), n, stream.cuda_stream)
-        res = self._read(n)
+        if self._config.dense_map:   # the TSDF reads the batch's depth records on the device
+            torch = self._torch
+            host = self._host_images.numpy()
+            for k, (imgs, _) in enumerate(self._staged):
+                host[k] = imgs
+            stream = torch.cuda.current_stream(self._device)
+            self._dev_images[:n].copy_(self._host_images[:n], non_blocking=True)
+            self._handle.submit(self._dev_images.data_ptr(), n, stream.cuda_stream)
+            self._integrate_depth(self._dev_images.data_ptr(), n, stream.cuda_stream)
+            self._staged, self._staged_gyro = [], []
+            self._prev_stamp = stamps[-1]
+            self._publish(self._read(n), stamps, self._handle.frames_done - n)
+            return
+        imgs = self._staged[0][0][None] if n == 1 else np.stack([im for im, _ in self._staged])
+        if self._in_flight >= 2:   # the handle keeps two batches' results: publish the older first
+            self._drain(block=True, limit=1)
+        self._handle.submit_host(imgs, stamps)
+        self._in_flight += 1
         self._staged, self._staged_gyro = [], []
         self._prev_stamp = stamps[-1]
-        self._publish(res, stamps)
+        if not self._async:
+            self._drain(block=True)
+
+    def _drain(self, block: bool, limit: int | None = None) -> None:
+        """Publish completed batches in order (all in flight with ``block``; at most ``limit``)."""
+        done = 0
+        while self._in_flight > 0 and (limit is None or done < limit):
+            res = self._handle.poll_batch(block=block)
+            if res is None:
+                return
+            self._in_flight -= 1
+            done += 1
+            self._publish(res, list(res["timestamps"]), res["first_frame"])
+
+    def flush(self) -> None:
+        """Run the staged frames through the GPU pipeline and publish the poses of every batch
+        submitted so far (waits for the device)."""
+        if self._handle is None:
+            return
+        self._submit_staged()
+        self._drain(block=True)
 
     # -- IMU fusion (SURVEY.md §8f item 2) -------------------------------------------------------
     @staticmethod
@@ -280,10 +333,11 @@ class HipSlamEngine(SlamEngine):
             raise RuntimeError("Not initialized")
         n = int(images.shape[0])
         s = stream if stream is not None else self._torch.cuda.current_stream(self._device)
+        self.flush()
         self._handle.submit(images.data_ptr(), n, s.cuda_stream)
         self._integrate_depth(images.data_ptr(), n, s.cuda_stream)
         res = self._read(n)
-        self._publish(res, timestamps or [float(i) for i in range(n)])
+        self._publish(res, timestamps or [float(i) for i in range(n)], self._handle.frames_done - n)
         return res
 
     # -- RGB-D dense mapping ----------------------------------------------
@@ -322,13 +376,12 @@ class HipSlamEngine(SlamEngine):
     def _body_pose(self, res: dict, k: int) -> tuple[int, np.ndarray, np.ndarray]:
         """(status, world_T_base, 6x6 body covariance) of frame k of a batch result."""
         bt = self._base_T_rect
-        rot6 = np.zeros((6, 6))
-        rot6[:3, :3] = rot6[3:, 3:] = bt[:3, :3]
         stats = res["stats"][k, :, 0]
         if len(self._pairs) == 1:
             status = int(stats[0])
             body = bt @ res["T_abs"][k, 0] @ _invert(bt)
-            cov = rot6 @ res["cov"][k, 0] @ rot6.T if status == POSE_OK else np.zeros((6, 6))
+            ad = adjoint(bt)   # camera-frame twist -> base-frame twist (rotation and lever arm)
+            cov = ad @ res["cov"][k, 0] @ ad.T if status == POSE_OK else np.zeros((6, 6))
             return status, body, cov
         # multi-pair rig: the device's generalised PnP over all pairs (k_rig_pose), already in the
         # base frame and chained (world = base_link at the first frame)
@@ -337,12 +390,11 @@ class HipSlamEngine(SlamEngine):
         cov = rig["cov"][k] if status == POSE_OK else np.zeros((6, 6))
         return status, rig["T_abs"][k].copy(), cov
 
-    def _ba_corrections(self, res: dict, n: int):
+    def _ba_corrections(self, res: dict, n: int, g0: int):
         """Per frame of the batch: the rect-frame correction W_ba(kf) inv(W_fe(kf)) (or None)."""
         cfg = self._config
         if cfg.ba_window <= 0:
             return None
-        g0 = self._handle.frames_done - n
         for k in range(n):
             if (g0 + k) % cfg.ba_kf_interval == 0:
                 self._fe_at[g0 + k] = res["T_abs"][k, 0].copy()
@@ -375,17 +427,17 @@ class HipSlamEngine(SlamEngine):
         for i, n in zip(ids[keep], counts[keep]):
             self._map_points[int(mp["gid"][i])] = (win["X"][i].copy(), mp["desc"][i].copy(), int(n))
 
-    def _publish(self, res: dict, stamps: list[float]) -> None:
+    def _publish(self, res: dict, stamps: list[float], g0: int) -> None:
         latest = None
         state = self._state
-        corr = self._ba_corrections(res, len(stamps))
+        corr = self._ba_corrections(res, len(stamps), g0)
         bt = self._base_T_rect
         for k, ts in enumerate(stamps):
             status, body, cov = self._body_pose(res, k)
             if corr is not None and status != POSE_LOST:
                 body = bt @ corr[k] @ res["T_abs"][k, 0] @ _invert(bt)
             if self._loop is not None and status != POSE_LOST:
-                g = self._handle.frames_done - len(stamps) + k
+                g = g0 + k
                 raw = _invert(bt) @ body @ bt                      # rect-left world_T_cam before loop correction
                 if status == POSE_OK and g % self._config.loop_kf_interval == 0:
                     self._loop_keyframe(g, raw, ts)
@@ -406,7 +458,7 @@ class HipSlamEngine(SlamEngine):
             )
             if status == POSE_INIT:
                 self._keyframe_poses.append(latest)
-            g = self._handle.frames_done - len(stamps) + k
+            g = g0 + k
             if self._config.ba_window > 0 and g % self._config.ba_kf_interval == 0:
                 self._kf_stamp[g] = ts
         with self._pose_lock:
@@ -577,6 +629,7 @@ class HipSlamEngine(SlamEngine):
         return True
 
     def reset(self) -> None:
+        self._in_flight = 0
         with self._pose_lock:
             self._latest_pose = None
         self._staged, self._staged_gyro, self._prev_stamp = [], [], None
