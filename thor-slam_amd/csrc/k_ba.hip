@@ -605,7 +605,6 @@ __global__ __launch_bounds__(1024) void k_ba_solve(BatchCtx c, BaArgs a) {
 #ifndef BA_TT
 #define BA_TT 1   // 2x2 and 4x4 register tiles measured slower (the update is latency-bound)
 #endif
-#ifndef BA_XP_NOELIM
     __shared__ double s_P[TS_BA_MAXD * 6];
     for (int c0 = 0; c0 < m; c0 += 6) {
         if (threadIdx.x < 64) {
@@ -679,14 +678,9 @@ __global__ __launch_bounds__(1024) void k_ba_solve(BatchCtx c, BaArgs a) {
         }
         __syncthreads();
     }
-#endif
     __syncthreads();
     const bool ok = s_ok;
-#ifdef BA_XP_NOSUB
-    if (false) {
-#else
     if (ok && threadIdx.x < 64) {
-#endif
         // D L'^T x = b'':  x_k = b''_k / d_k - sum_{i > k} L'[i][k] x_i   (lane k, i descending)
         const int k = threadIdx.x;
         const double rk = k < m ? 1.0 / s_S[k * mp + k] : 1.0;
