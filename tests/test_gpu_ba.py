@@ -167,3 +167,33 @@ def test_ba_on_its_own_stream_matches():
         _compare(h.ba_read(0), want[n - 1], "two streams, final window")
     finally:
         h.close()
+
+
+C4_ITEMS = (("n_features", 4000), ("ba_window", 10), ("ba_kf_interval", 5), ("ba_iters", 5), ("ba_lambda", 1.0),
+            ("ba_outlier_px", 3.0))
+
+
+@pytest.mark.slow
+def test_ba_window_parity_c4():
+    """BASELINE.json configs[3] (C4) as bench.py --config c4 runs it: 1280x800, K=4000, a
+    10-keyframe window with a keyframe every 5 frames and 5 Gauss-Newton iterations, batches of
+    50 frames; 56 frames = 12 keyframes, so the full 10-slot window is solved and then evicts
+    twice.  Compared with the oracle after every batch (frames 49 and 55)."""
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    n, batch = 56, 50
+    sc = scenario(seed=0, n=n, width=1280, height=800, cfg_items=C4_ITEMS)
+    want = _oracle_windows(sc)
+    h = Handle([sc["rect"]], sc["cfg"], max_batch=batch)
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    try:
+        for b0 in range(0, n, batch):
+            nb = min(batch, n - b0)
+            h.submit(dev[b0:].data_ptr(), nb, torch.cuda.current_stream().cuda_stream)
+            _compare(h.ba_read(0), want[b0 + nb - 1], f"after frame {b0 + nb - 1}")
+    finally:
+        h.close()
+    assert (want[-1]["frames"] >= 0).all() and want[-1]["frames"].min() == 10   # keyframes 0 and 5 evicted
+    assert want[-1]["solve"]["n_lm"] > 1000
