@@ -294,7 +294,6 @@ __device__ __forceinline__ uint32_t fast4(const uint8_t* rc, int W, int x0, int 
 // to the 8 waves in equal (row, 64-lane chunk) items.
 // ---------------------------------------------------------------------------------------------
 #define TS_DET_THREADS 512
-#define TS_SMOOTH_GROUPS 2                                // smoothing items = (quad, row group)
 #define TS_DET_WAVES (TS_DET_THREADS / 64)
 
 // 16-byte async global -> LDS copy; `wave_dst` is the wave-uniform LDS base, lane k lands at +16k
@@ -347,7 +346,7 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
     while (l + 1 < c.g.n_levels && (int)blockIdx.x >= c.g.band_start[l + 1]) ++l;
     const int band = blockIdx.x - c.g.band_start[l];
     const int W = c.g.W[l], H = c.g.H[l];
-    const int BR = c.g.band_rows;
+    const int BR = c.g.band_rows[l];
     const int y0 = band * BR;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const size_t img_off = ((size_t)ring_slot(c, c.g0 + f) * c.C + cam) * c.g.pyr_bytes + c.g.pyr_off[l];
@@ -389,9 +388,10 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
         // through 5 registers; u16 pairs cannot overflow (16 * 16 * 255 + 128 < 2^16)
         const int W4 = W >> 2;
         const u16x2 four = {4, 4}, six = {6, 6}, rnd = {128, 128};
-        for (int it = threadIdx.x; it < TS_SMOOTH_GROUPS * W4; it += TS_DET_THREADS) {
+        const int groups = c.g.smooth_groups[l];
+        const int SR = (BR + groups - 1) / groups;
+        for (int it = threadIdx.x; it < groups * W4; it += TS_DET_THREADS) {
             const int half = it / W4, q = it - half * W4, x0 = 4 * q;
-            const int SR = BR / TS_SMOOTH_GROUPS;
             const int o0 = SR * half, o1 = min(o0 + SR, rows_here);   // output rows (band-relative)
             if (o0 >= o1) continue;
             u16x2 e[5], d[5];
@@ -884,7 +884,7 @@ void launch_rectify_pyramid(const BatchCtx& c, hipStream_t s) {
 }
 
 void launch_detect(const BatchCtx& c, hipStream_t s) {
-    const size_t lds = (size_t)(c.g.band_rows + 2 * TS_DET_HALO + c.g.band_rows + 2) * c.g.W[0];
+    const size_t lds = (size_t)c.g.det_lds;
     dim3 grid(c.g.total_bands, c.n * c.ncam);
     const size_t per_cam = sizeof(uint32_t) * 256 * c.g.n_levels;   // hist [B][C][L][256]: the view's cameras
     if (c.ncam == c.C)

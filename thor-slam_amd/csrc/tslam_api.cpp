@@ -197,19 +197,31 @@ static void build_geometry(tslam_handle* h) {
     g.Kq[0] = p.n_features - sumq;
     g.pyr_bytes = (off + 15) & ~15;
     int ko = 0, bs = 0, co = 0, qs = 0;
-    // detect band height: the tallest of 32 / 24 / 16 rows whose band (2 * rows + 10 rows of W
-    // bytes of LDS) keeps 3 (W <= 640) or 2 (W <= 1280) blocks per CU; measured 778 -> 690 us
-    // at 640x400 (32 rows) and 611 -> 575 us at 1280x800 (24 rows) against 16
-    g.band_rows = (2 * TS_BAND_ROWS_MAX + 10) * g.W[0] <= 48 * 1024 ? TS_BAND_ROWS_MAX
-                : (2 * 24 + 10) * g.W[0] <= 78 * 1024 ? 24 : 16;
+    // detect band height at level 0: the tallest of 32 / 24 / 16 rows whose band (2 * rows + 10
+    // rows of W bytes of LDS) keeps 3 (W <= 640) or 2 (W <= 1280) blocks per CU; measured 778 ->
+    // 690 us at 640x400 (32 rows) and 611 -> 575 us at 1280x800 (24 rows) against 16.  Coarser
+    // levels take taller bands in the same LDS budget (fewer blocks and halo rows, similar pixels
+    // per block), equalised over the level's rows: 640x400 -> 32 / 68 / 100 / 50 rows, 26 -> 18
+    // blocks per image, 662 -> 625 us per 256-frame batch
+    const int br0 = (2 * TS_BAND_ROWS_MAX + 10) * g.W[0] <= 48 * 1024 ? TS_BAND_ROWS_MAX
+                  : (2 * 24 + 10) * g.W[0] <= 78 * 1024 ? 24 : 16;
+    const int det_budget = (2 * br0 + 10) * g.W[0];
+    g.det_lds = 0;
+    for (int l = 0; l < p.n_levels; ++l) {
+        const int maxr = l == 0 ? br0 : std::max(br0, std::min(128, (det_budget / g.W[l] - 10) / 2));
+        const int nb = (g.H[l] + maxr - 1) / maxr;
+        g.band_rows[l] = l == 0 ? br0 : ((g.H[l] + nb - 1) / nb + 1) & ~1;
+        g.smooth_groups[l] = std::max(2, g.band_rows[l] / 16);
+        g.det_lds = std::max(g.det_lds, (2 * g.band_rows[l] + 10) * g.W[l]);
+    }
     g.dt_total = 0;
     for (int l = 0; l < p.n_levels; ++l) {
         g.koff[l] = ko;
         ko += g.Kq[l];
-        g.nbands[l] = (g.H[l] + g.band_rows - 1) / g.band_rows;
+        g.nbands[l] = (g.H[l] + g.band_rows[l] - 1) / g.band_rows[l];
         g.band_start[l] = bs;
         bs += g.nbands[l];
-        g.cand_cap[l] = (g.band_rows / 2) * (g.W[l] / 2 + 1);
+        g.cand_cap[l] = ((g.band_rows[l] + 1) / 2) * (g.W[l] / 2 + 1);
         g.cand_off[l] = co;
         co += g.nbands[l] * g.cand_cap[l];
         g.dt_nx[l] = (g.W[l] + TS_DT_W - 1) / TS_DT_W;

@@ -50,7 +50,9 @@ struct LevelGeom {
     int pyr_bytes;
     int K;
     int Kq[TS_MAX_LEVELS], koff[TS_MAX_LEVELS];
-    int band_rows;                 // detect band height (16 or TS_BAND_ROWS_MAX, by level-0 width)
+    int band_rows[TS_MAX_LEVELS];  // detect band height per level (LevelGeom rule in build_geometry)
+    int smooth_groups[TS_MAX_LEVELS];   // detect smoothing: row groups per band (items = groups x quads)
+    int det_lds;                   // detect dynamic LDS bytes: max over levels of (2 rows + 10) x W
     int nbands[TS_MAX_LEVELS], band_start[TS_MAX_LEVELS];
     int total_bands;
     int cand_cap[TS_MAX_LEVELS];   // keys per band at level l
