@@ -116,7 +116,9 @@ enum tslam_buffer {
     TSLAM_BUF_YSORTED = 15,  /* u32 [ring][cams][K][4]           per level, by (y, rank): {x | y<<16, lvl | score<<16, kp index, valid} */
     TSLAM_BUF_ROWSTART = 16, /* u16 [ring][cams][sum(H_l+1)]     per level: first y-sorted position of row y */
     TSLAM_BUF_DESC_YS = 17,  /* u32 [ring][cams][K][8]           descriptors in the y-sorted order */
-    TSLAM_BUF_COUNT = 18
+    TSLAM_BUF_DET_THR = 18,  /* u32 [1][cams][levels]            speculative FAST threshold te in use (0 = t + 1) */
+    TSLAM_BUF_DET_FAIL = 19, /* u32 [batch][cams][levels]        1 = the last batch's image-level took the fallback */
+    TSLAM_BUF_COUNT = 20
 };
 
 enum tslam_stage {

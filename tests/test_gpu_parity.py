@@ -223,3 +223,42 @@ def test_two_stream_pipeline_bit_exact():
         assert res["stats"][f, 0, 4] == o["best_hyp"] and res["stats"][f, 0, 2] == o["n_inliers"]
         assert rel_frobenius(res["T_abs"][f, 0], o["world_T_cam"]) < 1e-9
     h.close()
+
+
+def test_speculative_fast_threshold_exact_across_batches():
+    """A4 speculative threshold: from the second batch on, detect scores exactly only
+    the pixels that may reach a margin below the previous batch's K-th score per level.  Batches
+    of 1 over 6 frames run it for frames 1..5: keypoints and descriptors stay bit-exact."""
+    sc, per = hip_run(seed=0, batch=1, n=6)
+    for i, (ora, got) in enumerate(zip(sc["oracle"], per)):
+        for cam, side in enumerate(("left", "right")):
+            _check_image_features(ora["cur"][side], got["kp"][cam], sc["cfg"], f"frame {i} {side}")
+
+
+def test_speculative_fast_threshold_fallback_is_exact():
+    """A low-contrast batch after a textured one: the learnt threshold leaves fewer than K
+    candidates, select flags the images, and the flag-gated fallback (detect + select at t + 1)
+    restores the exact keypoints."""
+    import torch
+
+    from oracle import numpy_slam as O
+    from thor_slam_amd._lib import Handle
+
+    sc = scenario(seed=0, n=4)
+    cfg, rect = sc["cfg"], sc["rect"]
+    frames = np.ascontiguousarray(sc["frames"]).copy()
+    frames[2:] = (frames[2:].astype(np.int32) // 3 + 85).astype(np.uint8)   # contrast / 3
+    h = Handle([rect], cfg, max_batch=2)
+    dev = torch.from_numpy(frames).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    h.submit(dev[0].data_ptr(), 2, s)
+    h.submit(dev[2].data_ptr(), 2, s)
+    trk = O.OracleTracker(cfg, dict(fx=rect.fx, fy=rect.fy, cx=rect.cx, cy=rect.cy, baseline=rect.baseline,
+                                    map_l=rect.map_left, map_r=rect.map_right))
+    ora = [trk.step(frames[i, 0], frames[i, 1]) for i in range(4)]
+    for i in range(2, 4):
+        for cam, side in enumerate(("left", "right")):
+            _check_image_features(ora[i]["cur"][side], h.keypoints(i, cam), cfg, f"frame {i} {side}")
+    # the low-contrast frames really have fewer strong corners than the learnt threshold admits
+    assert min(ora[2]["cur"]["left"]["kp"]["score"][ora[2]["cur"]["left"]["valid"]]) < 40
+    h.close()

@@ -212,6 +212,11 @@ __device__ __forceinline__ h16x2 hmax3(h16x2 a, h16x2 b, h16x2 c) {
     return __builtin_elementwise_maximum(a, __builtin_elementwise_maximum(b, c));
 }
 
+// Exact FAST-9 scores of the 4 pixels x0..x0+3 of tile row `rc` (pitch W), thresholded (score >
+// thr, else 0), as 4 bytes.  Straight-line packed f16: the pixels travel as (x0, x0+2) / (x0+1,
+// x0+3) pairs; a byte b becomes the f16 1024 + b (0x64 as its high byte, one v_perm per pair), so
+// every difference, min and max below is exact.  The 16 circle windows come from 3 dword LDS reads
+// per circle row + v_alignbyte; each 9-arc minimum is min3(min3 of 3, 3, 3) (v_pk_minimum3_f16).
 __device__ __forceinline__ uint32_t fast4(const uint8_t* rc, int W, int x0, int thr) {
     // circle index k -> (dx, dy): 0 (0,-3) 1 (1,-3) 2 (2,-2) 3 (3,-1) 4 (3,0) 5 (3,1) 6 (2,2)
     // 7 (1,3) 8 (0,3) 9 (-1,3) 10 (-2,2) 11 (-3,1) 12 (-3,0) 13 (-3,-1) 14 (-2,-2) 15 (-1,-3)
@@ -284,6 +289,59 @@ __device__ __forceinline__ uint32_t fast4(const uint8_t* rc, int W, int x0, int 
     return out;
 }
 
+
+// Phase A of FAST at the speculative threshold te: every 9-arc of the circle holds one of circle
+// indices {0, 8} and one of {4, 12}, so score >= te needs max(p0, p8) and max(p4, p12) >= c + te
+// (bright) or min(p0, p8) and min(p4, p12) <= c - te (dark).  4 pixels x0..x0+3 of tile row `rc`
+// (pitch W) from 5 dword LDS reads, on f16 pairs 1024 + byte (exact): bit j = pixel x0 + j may
+// reach te (~20 VALU per quad against ~270 for the exact scores).
+__device__ __forceinline__ uint32_t fast4_maybe(const uint8_t* rc, int W, int x0, h16x2 te2) {
+    const uint32_t* p = (const uint32_t*)(rc + x0);
+    const int Wd = W >> 2;
+    const uint32_t up = p[-3 * Wd], dn = p[3 * Wd];
+    const uint32_t a = p[-1], b = p[0], cc = p[1];
+    const uint32_t w4 = __builtin_amdgcn_alignbyte(cc, b, 3), w12 = __builtin_amdgcn_alignbyte(b, a, 1);
+    constexpr uint32_t k64 = 0x64646464u;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {   // h = 0: pixels x0, x0+2; h = 1: pixels x0+1, x0+3
+        const uint32_t sel = h ? 0x00070005u : 0x00060004u;
+        auto toh = [sel](uint32_t v) { return __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(v, k64, sel)); };
+        const h16x2 p0 = toh(up), p8 = toh(dn), p4 = toh(w4), p12 = toh(w12), c = toh(b);
+        const h16x2 bmin = __builtin_elementwise_minimum(__builtin_elementwise_maximum(p0, p8),
+                                                         __builtin_elementwise_maximum(p4, p12));
+        const h16x2 dmax = __builtin_elementwise_maximum(__builtin_elementwise_minimum(p0, p8),
+                                                         __builtin_elementwise_minimum(p4, p12));
+        const h16x2 v = __builtin_elementwise_maximum(bmin - (c + te2), (c - te2) - dmax);   // >= 0: candidate
+        const uint32_t vb = ~__builtin_bit_cast(uint32_t, v);
+        bits |= ((vb >> 15) & 1u) << h;
+        bits |= ((vb >> 31) & 1u) << (h + 2);
+    }
+    return bits;
+}
+
+// Phase B: exact scores (>= te, else 0) of the `cnt` (<= 64) candidate quads at q (entries
+// r << 16 | quad: score row r, columns 4 quad .. 4 quad + 3), one quad per lane with the dense
+// aligned-dword fast4, written as the quad's score word.  Wave-local (no block barrier).
+#define TS_DET_Q 128   // per-wave candidate queue (quads): flushed at 64, + <= 64 per append
+#ifndef TS_DET_U
+#define TS_DET_U 4     // phase-A items per lane per iteration
+#endif
+__device__ __forceinline__ void fast_flush(const uint32_t* q, int cnt, const uint8_t* tile, uint32_t* score32, int W,
+                                           int te) {
+    const int lane = threadIdx.x & 63;
+    if (lane >= cnt) return;
+    const uint32_t e = q[lane];
+    const int r = (int)(e >> 16), x4 = (int)(e & 0xFFFFu), x0 = 4 * x4;
+    uint32_t sc4 = fast4(tile + (r + TS_DET_HALO - 1) * W, W, x0, te - 1);
+    if (x0 < 3) sc4 &= 0xFFFFFFFFu << (8 * (3 - x0));                  // x >= 3
+    if (x0 + 4 > W - 3) {                                              // x < W-3
+        const int keep = max(W - 3 - x0, 0);
+        sc4 &= keep >= 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u);
+    }
+    score32[r * (W >> 2) + x4] = sc4;
+}
+
 // ---------------------------------------------------------------------------------------------
 // A3 smoothing + A4 FAST/NMS candidates for one band of BR = g.band_rows rows of one level.
 // grid (total_bands, n*C), block 512 (8 waves).  LDS: image rows [y0-4, y0+BR+4) (row-clamped),
@@ -339,11 +397,17 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ uint32_t s_hist[256];
     __shared__ uint32_t s_count;
+    __shared__ uint32_t s_q[TS_DET_WAVES][TS_DET_Q];
     const int img = blockIdx.y;
     int f, cam;
     view_image(c, img, &f, &cam);
     int l = 0;
     while (l + 1 < c.g.n_levels && (int)blockIdx.x >= c.g.band_start[l + 1]) ++l;
+    const size_t fcl = ((size_t)f * c.C + cam) * c.g.n_levels + l;
+    if (c.det_mode == 1 && !c.det_fail[fcl]) return;   // fallback launch: only the flagged images
+    // speculative threshold: scores below te cannot reach the level's top K (select checks it)
+    const int te = c.det_mode == 1 ? c.fast_threshold + 1
+                                   : max(c.fast_threshold + 1, (int)c.det_thr[(size_t)cam * c.g.n_levels + l]);
     const int band = blockIdx.x - c.g.band_start[l];
     const int W = c.g.W[l], H = c.g.H[l];
     const int BR = c.g.band_rows[l];
@@ -426,10 +490,12 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
         }
     }
 
-    // FAST scores (thresholded) for rows y0-1 .. y0+16
+    // FAST scores (>= te, else 0) for rows y0-1 .. y0+BR
     if (wide) {
-        // 4 pixels per lane (fast4): 21 dword LDS reads and ~250 packed-f16 ops per quad, no
-        // divergence; items (row, quad) dealt over the block
+        // phase A over (row, quad) items: the four compass points of 4 pixels per lane; quads
+        // with a candidate pixel (~30 % at a learnt te against ~90 % at t) go to the wave's LDS
+        // queue (ballot + mbcnt) and get the exact scores, one quad per lane, in rounds of 64
+        // (phase B, the dense fast4); the others keep a zero score word
         uint32_t* score32 = (uint32_t*)score;
         const int W4 = W >> 2;
         // only where the NMS reads: rows y in [M-1, H-M], columns [M-1, W-M] (keypoints lie in
@@ -438,24 +504,61 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
         const int Mg = c.margin;
         const int ra = max(0, Mg - y0), rb = min(BR + 2, H - Mg + 2 - y0);
         const int qa = (Mg - 1) >> 2, nq = ((W - Mg) >> 2) + 1 - qa;
-        // (row, quad) of item it = threadIdx.x + k * TS_DET_THREADS, stepped without a division
+        const _Float16 tef = (_Float16)te;
+        const h16x2 te2 = {tef, tef};
+        uint32_t* q = s_q[wave];
+        int qn = 0;   // wave-uniform
+        const int nitems = max(rb - ra, 0) * nq;
+        // (row, quad) of item it = wave * 64 + lane + k * TS_DET_THREADS, stepped without a division;
+        // TS_DET_U items per lane per iteration, so their 5 LDS reads each are in flight together
+        // (one item per iteration left phase A waiting on LDS latency)
         const int dr = TS_DET_THREADS / nq, dq = TS_DET_THREADS - dr * nq;
-        int r = ra + (int)threadIdx.x / nq, x4 = qa + (int)threadIdx.x % nq;
-        for (int it = threadIdx.x; it < max(rb - ra, 0) * nq;
-             it += TS_DET_THREADS, r += dr, x4 += dq, (x4 >= qa + nq ? (x4 -= nq, ++r) : 0)) {
-            const int y = y0 - 1 + r;
-            uint32_t sc4 = 0;
-            if (y >= 3 && y < H - 3) {
-                const int x0 = 4 * x4;
-                sc4 = fast4(tile + (r + TS_DET_HALO - 1) * W, W, x0, thr);
-                if (x0 < 3) sc4 &= 0xFFFFFFFFu << (8 * (3 - x0));                    // x >= 3
-                if (x0 + 4 > W - 3) {                                                // x < W-3
-                    const int keep = max(W - 3 - x0, 0);                             // pixels kept
-                    sc4 &= keep >= 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u);
+        int r = ra + (wave * 64 + lane) / nq, x4 = qa + (wave * 64 + lane) % nq;
+        for (int i0 = wave * 64; i0 < nitems; i0 += TS_DET_U * TS_DET_THREADS) {
+            int ru[TS_DET_U], xu[TS_DET_U];
+            bool cand[TS_DET_U];
+#pragma unroll
+            for (int u = 0; u < TS_DET_U; ++u) {
+                ru[u] = r;
+                xu[u] = x4;
+                r += dr;
+                x4 += dq;
+                if (x4 >= qa + nq) {
+                    x4 -= nq;
+                    ++r;
                 }
             }
-            score32[r * W4 + x4] = sc4;
+#pragma unroll
+            for (int u = 0; u < TS_DET_U; ++u) {
+                const bool active = i0 + u * TS_DET_THREADS + lane < nitems;
+                const int y = y0 - 1 + ru[u], x0 = 4 * xu[u];
+                cand[u] = false;
+                if (active) {
+                    if (y >= 3 && y < H - 3) {
+                        uint32_t c4 = fast4_maybe(tile + (ru[u] + TS_DET_HALO - 1) * W, W, x0, te2);
+                        if (x0 < 3) c4 &= 0xFu << (3 - x0);                              // x >= 3
+                        if (x0 + 4 > W - 3) c4 &= (1u << max(W - 3 - x0, 0)) - 1u;        // x < W-3
+                        cand[u] = c4 != 0;
+                    }
+                    if (!cand[u]) score32[ru[u] * W4 + xu[u]] = 0;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < TS_DET_U; ++u) {
+                const uint64_t bm = __ballot(cand[u]);
+                if (cand[u])
+                    q[qn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u))] =
+                        ((uint32_t)ru[u] << 16) | (uint32_t)xu[u];
+                qn += (int)__popcll(bm);
+                // a wave's LDS operations complete in issue order, and the queue is wave-private:
+                // no fence between its entries' stores and the flush's loads
+                if (qn >= 64) {
+                    fast_flush(q + qn - 64, 64, tile, score32, W, te);
+                    qn -= 64;
+                }
+            }
         }
+        if (qn > 0) fast_flush(q, qn, tile, score32, W, te);
     } else {
         for (int i = threadIdx.x; i < (BR + 2) * W; i += TS_DET_THREADS) {
             const int r = i / W, x = i - r * W;
@@ -463,7 +566,7 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
             int sc = 0;
             if (y >= 3 && y < H - 3 && x >= 3 && x < W - 3) {
                 sc = fast9_score(tile, W, r + TS_DET_HALO - 1, x, thr);
-                if (sc <= thr) sc = 0;
+                if (sc < te) sc = 0;
             }
             score[i] = (uint8_t)sc;
         }
@@ -677,6 +780,8 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
     const int img = blockIdx.x;
     int f, cam;
     view_image(c, img, &f, &cam);
+    const size_t fcl = ((size_t)f * c.C + cam) * c.g.n_levels + l;
+    if (c.det_mode == 1 && !c.det_fail[fcl]) return;   // fallback launch: only the flagged images
     const int Kl = c.g.Kq[l];
     const uint32_t* cand = c.cand + ((size_t)f * c.C + cam) * c.g.cand_total + c.g.cand_off[l];
     const uint32_t* cnt = c.ccount + ((size_t)f * c.C + cam) * c.g.total_bands + c.g.band_start[l];
@@ -812,7 +917,24 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
         kp[2 * i] = xy;
         kp[2 * i + 1] = meta;
     }
-    if (threadIdx.x == 0) c.kcount[((size_t)slot * c.C + cam) * c.g.n_levels + l] = nsel;
+    if (threadIdx.x == 0) {
+        c.kcount[((size_t)slot * c.C + cam) * c.g.n_levels + l] = nsel;
+        // speculative threshold: the candidates are the NMS survivors with score >= te; the top K
+        // is exact iff at least K of them exist (a pixel below te can neither be selected nor
+        // suppress one at or above it) or te = t + 1.  Otherwise flag the image for the
+        // fallback pass.  Next batch's te for this (camera, level): a margin below the K-th score
+        // (the minimum over the batch's frames), t + 1 when the level had fewer than K.
+        const int tfull = c.fast_threshold + 1;
+        const int te = c.det_mode == 1 ? tfull : max(tfull, (int)c.det_thr[(size_t)cam * c.g.n_levels + l]);
+        const bool short_k = (int)total < Kl;
+        if (c.det_mode == 0) c.det_fail[fcl] = (short_k && te > tfull) ? 1u : 0u;
+        int next = tfull;
+        if (!short_k && nsel > 0) {
+            const int sk = 255 - (int)(s_keys[nsel - 1] >> 22);   // the K-th score (keys sorted ascending)
+            next = max(tfull, sk - 4);
+        }
+        atomicMin(&c.det_thr_acc[(size_t)cam * c.g.n_levels + l], (uint32_t)next);
+    }
 
     // y-sorted order of this level (by y, then rank) + row-start table, for band-limited matching
     uint4* ys = c.ys + ((size_t)slot * c.C + cam) * c.g.K + c.g.koff[l];
@@ -894,7 +1016,34 @@ void launch_detect(const BatchCtx& c, hipStream_t s) {
     hipLaunchKernelGGL(k_detect, grid, dim3(TS_DET_THREADS), lds, s, c);
 }
 
+// hist of the flagged images back to zero before their fallback detect (it accumulates)
+__global__ void k_det_fallback_prep(BatchCtx c) {
+    const int img = blockIdx.x, l = blockIdx.y;
+    int f, cam;
+    view_image(c, img, &f, &cam);
+    const size_t fcl = ((size_t)f * c.C + cam) * c.g.n_levels + l;
+    if (!c.det_fail[fcl]) return;
+    c.hist[fcl * 256 + threadIdx.x] = 0u;
+}
+
+// next batch's te <- this batch's running minimum; the minimum restarts (view cameras)
+__global__ void k_det_thr_commit(BatchCtx c) {
+    const int i = threadIdx.x;
+    if (i >= c.ncam * c.g.n_levels) return;
+    const size_t k = (size_t)c.cam0 * c.g.n_levels + i;
+    const_cast<uint32_t*>(c.det_thr)[k] = c.det_thr_acc[k];
+    c.det_thr_acc[k] = 0xFFFFFFFFu;
+}
+
 void launch_select(const BatchCtx& c, hipStream_t s) {
     dim3 grid(c.n * c.ncam, c.g.n_levels);
     hipLaunchKernelGGL(k_select, grid, dim3(SEL_THREADS), 0, s, c);
+    // fallback for images whose speculative threshold left fewer than K candidates: detect and
+    // select again at t + 1, gated on the device flags (near-empty launches when none is set)
+    BatchCtx fb = c;
+    fb.det_mode = 1;
+    hipLaunchKernelGGL(k_det_fallback_prep, grid, dim3(256), 0, s, fb);
+    hipLaunchKernelGGL(k_detect, dim3(c.g.total_bands, c.n * c.ncam), dim3(TS_DET_THREADS), (size_t)c.g.det_lds, s, fb);
+    hipLaunchKernelGGL(k_select, grid, dim3(SEL_THREADS), 0, s, fb);
+    hipLaunchKernelGGL(k_det_thr_commit, dim3(1), dim3(256), 0, s, c);
 }

@@ -92,6 +92,7 @@ struct tslam_handle {
     Buffer buf[TSLAM_BUF_COUNT];
     uint32_t* d_cand = nullptr;
     uint32_t* d_ccount = nullptr;
+    uint32_t* d_det_thr_acc = nullptr;   // [C][L] running minimum of the next te
     uint32_t* d_hist = nullptr;
     double* d_state = nullptr;
     double* d_ransac = nullptr;
@@ -369,6 +370,10 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.rig_state = h->d_rig_state;
     c.ransac = h->d_ransac;
     c.hyp = h->d_hyp;
+    c.det_thr = (const uint32_t*)h->buf[TSLAM_BUF_DET_THR].ptr;
+    c.det_thr_acc = h->d_det_thr_acc;
+    c.det_fail = (uint32_t*)h->buf[TSLAM_BUF_DET_FAIL].ptr;
+    c.det_mode = 0;
     c.brief_table = h->d_brief;
     c.wedges = h->d_wedges;
     for (int p = 0; p < h->P; ++p) c.calib[p] = h->calib[p];
@@ -561,6 +566,8 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
         {TSLAM_BUF_YSORTED, R, C * K * 16},
         {TSLAM_BUF_DESC_YS, R, C * K * 8 * 4},
         {TSLAM_BUF_ROWSTART, R, C * (int64_t)h->g.rs_total * 2},
+        {TSLAM_BUF_DET_THR, 1, C * L * 4},
+        {TSLAM_BUF_DET_FAIL, B, C * L * 4},
     };
     int rc = TSLAM_OK;
     for (const Spec& s : specs) {
@@ -572,6 +579,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_cand, sizeof(uint32_t) * (size_t)B * C * h->g.cand_total);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_ccount, sizeof(uint32_t) * (size_t)B * C * h->g.total_bands);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_hist, sizeof(uint32_t) * (size_t)B * C * L * 256);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_det_thr_acc, sizeof(uint32_t) * (size_t)C * L);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_state, sizeof(double) * 16 * (size_t)P);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_ransac, sizeof(uint32_t) * TS_RANSAC_WORDS * TS_MAX_SPLITS * (size_t)B * P);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_hyp, sizeof(double) * 12 * 4 * (size_t)p.ransac_hypotheses * B * P);
@@ -646,6 +654,9 @@ int tslam_reset(tslam_handle* h) {
     HIPCHK(hipMemcpy(h->d_state, eye.data(), sizeof(double) * eye.size(), hipMemcpyHostToDevice));
     if (h->d_rig_state) HIPCHK(hipMemcpy(h->d_rig_state, eye.data(), sizeof(double) * 16, hipMemcpyHostToDevice));
     h->frames_done = 0;
+    // the speculative FAST threshold starts exact (t + 1) and learns from the first batch
+    HIPCHK(hipMemset(h->buf[TSLAM_BUF_DET_THR].ptr, 0, sizeof(uint32_t) * (size_t)h->C * h->g.n_levels));
+    HIPCHK(hipMemset(h->d_det_thr_acc, 0xFF, sizeof(uint32_t) * (size_t)h->C * h->g.n_levels));
     for (int i = 0; i < TS_BA_MAXW; ++i) h->ba_frame[i] = -1;
     h->ba_nkf = 0;
     h->ba_last = -1;

@@ -130,6 +130,13 @@ struct BatchCtx {
     double* rig_pose;      // [B][68]  body T_rel, T_abs, cov
     int32_t* rig_stats;    // [B][8]
     double* rig_state;     // [16]
+    // A4 speculative FAST threshold (DESIGN.md §5 "detect"): te[cam][l] in use, its running
+    // minimum for the next batch, per (frame, cam, level) fallback flags, launch mode
+    // (0: te = max(t + 1, det_thr), flags set by select; 1: te = t + 1 for flagged images only)
+    const uint32_t* det_thr;      // [C][L]
+    uint32_t* det_thr_acc;        // [C][L]
+    uint32_t* det_fail;           // [B][C][L]
+    int det_mode;
     const uint32_t* brief_table;  // [30][256] LDS patch byte offsets of the two points (lo | hi << 16)
     const int64_t* wedges;        // [31][2]
     PairCalib calib[8];

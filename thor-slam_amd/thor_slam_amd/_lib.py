@@ -22,7 +22,7 @@ LIB_PATH = Path(__file__).resolve().parent / LIB_NAME
 BUF = {
     "pyramid": 0, "smooth": 1, "keypoints": 2, "kcount": 3, "desc": 4, "stereo": 5, "disp": 6,
     "temporal": 7, "temporal_uv": 8, "corr": 9, "pose": 10, "stats": 11, "qbest": 12,
-    "qsecond": 13, "tbest": 14, "ysorted": 15, "rowstart": 16, "desc_ys": 17,
+    "qsecond": 13, "tbest": 14, "ysorted": 15, "rowstart": 16, "desc_ys": 17, "det_thr": 18, "det_fail": 19,
 }
 STAGE = {"rectify": 0, "detect": 1, "describe": 2, "match": 3, "pose": 4, "all": 5, "ba": 6}
 # single kernels, in pipeline order (bench.py times each with HIP events)

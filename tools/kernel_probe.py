@@ -53,6 +53,9 @@ def main() -> None:
     h.submit(dev[:B].data_ptr(), B, s)
     h.submit(dev[B:].data_ptr(), B, s)
     torch.cuda.synchronize()
+    import numpy as np
+
+    print("te per camera x level:", h.frame_block("det_thr", 0, np.uint32).reshape(2, -1).tolist())
     h.begin_batch(dev[:B].data_ptr(), B)
     for name in args.kernels.split(","):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
