@@ -393,7 +393,10 @@ __device__ __forceinline__ void hsum4(const uint8_t* row, int x0, int W, u16x2* 
     *od = __builtin_bit_cast(u16x2, hj[1] | (hj[3] << 16));
 }
 
-__global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
+// MODE 0: speculative threshold (k_detect); MODE 1: exact fallback at t + 1 for the flagged
+// images (k_detect_fallback, its own symbol so profiles keep the two launches apart)
+template <int MODE>
+__device__ __forceinline__ void detect_body(const BatchCtx& c) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ uint32_t s_hist[256];
     __shared__ uint32_t s_count;
@@ -404,9 +407,9 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
     int l = 0;
     while (l + 1 < c.g.n_levels && (int)blockIdx.x >= c.g.band_start[l + 1]) ++l;
     const size_t fcl = ((size_t)f * c.C + cam) * c.g.n_levels + l;
-    if (c.det_mode == 1 && !c.det_fail[fcl]) return;   // fallback launch: only the flagged images
+    if (MODE == 1 && !c.det_fail[fcl]) return;   // fallback launch: only the flagged images
     // speculative threshold: scores below te cannot reach the level's top K (select checks it)
-    const int te = c.det_mode == 1 ? c.fast_threshold + 1
+    const int te = MODE == 1 ? c.fast_threshold + 1
                                    : max(c.fast_threshold + 1, (int)c.det_thr[(size_t)cam * c.g.n_levels + l]);
     const int band = blockIdx.x - c.g.band_start[l];
     const int W = c.g.W[l], H = c.g.H[l];
@@ -678,6 +681,9 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) {
         if (s_hist[i]) atomicAdd(&gh[i], s_hist[i]);
 }
 
+__global__ __launch_bounds__(TS_DET_THREADS) void k_detect(BatchCtx c) { detect_body<0>(c); }
+__global__ __launch_bounds__(TS_DET_THREADS) void k_detect_fallback(BatchCtx c) { detect_body<1>(c); }
+
 // ---------------------------------------------------------------------------------------------
 // A4 top-K: exact K_l smallest keys of an image level, sorted ascending.
 // Radix select on (score bin, y, x) histograms, then counting sorts (bitonic fallback) in LDS.
@@ -769,7 +775,8 @@ __device__ void bitonic_sort(uint32_t* a, int n) {
     }
 }
 
-__global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
+template <int MODE>
+__device__ __forceinline__ void select_body(const BatchCtx& c) {
     __shared__ uint32_t s_keys[SEL_MAX];
     __shared__ uint32_t s_h[2048];
     __shared__ uint32_t s_part[SEL_THREADS];
@@ -781,7 +788,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
     int f, cam;
     view_image(c, img, &f, &cam);
     const size_t fcl = ((size_t)f * c.C + cam) * c.g.n_levels + l;
-    if (c.det_mode == 1 && !c.det_fail[fcl]) return;   // fallback launch: only the flagged images
+    if (MODE == 1 && !c.det_fail[fcl]) return;   // fallback launch: only the flagged images
     const int Kl = c.g.Kq[l];
     const uint32_t* cand = c.cand + ((size_t)f * c.C + cam) * c.g.cand_total + c.g.cand_off[l];
     const uint32_t* cnt = c.ccount + ((size_t)f * c.C + cam) * c.g.total_bands + c.g.band_start[l];
@@ -925,9 +932,9 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
         // fallback pass.  Next batch's te for this (camera, level): a margin below the K-th score
         // (the minimum over the batch's frames), t + 1 when the level had fewer than K.
         const int tfull = c.fast_threshold + 1;
-        const int te = c.det_mode == 1 ? tfull : max(tfull, (int)c.det_thr[(size_t)cam * c.g.n_levels + l]);
+        const int te = MODE == 1 ? tfull : max(tfull, (int)c.det_thr[(size_t)cam * c.g.n_levels + l]);
         const bool short_k = (int)total < Kl;
-        if (c.det_mode == 0) c.det_fail[fcl] = (short_k && te > tfull) ? 1u : 0u;
+        if (MODE == 0) c.det_fail[fcl] = (short_k && te > tfull) ? 1u : 0u;
         int next = tfull;
         if (!short_k && nsel > 0) {
             const int sk = 255 - (int)(s_keys[nsel - 1] >> 22);   // the K-th score (keys sorted ascending)
@@ -995,6 +1002,9 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) {
     }
 }
 
+__global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) { select_body<0>(c); }
+__global__ __launch_bounds__(SEL_THREADS) void k_select_fallback(BatchCtx c) { select_body<1>(c); }
+
 // ---------------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------------
@@ -1040,10 +1050,8 @@ void launch_select(const BatchCtx& c, hipStream_t s) {
     hipLaunchKernelGGL(k_select, grid, dim3(SEL_THREADS), 0, s, c);
     // fallback for images whose speculative threshold left fewer than K candidates: detect and
     // select again at t + 1, gated on the device flags (near-empty launches when none is set)
-    BatchCtx fb = c;
-    fb.det_mode = 1;
-    hipLaunchKernelGGL(k_det_fallback_prep, grid, dim3(256), 0, s, fb);
-    hipLaunchKernelGGL(k_detect, dim3(c.g.total_bands, c.n * c.ncam), dim3(TS_DET_THREADS), (size_t)c.g.det_lds, s, fb);
-    hipLaunchKernelGGL(k_select, grid, dim3(SEL_THREADS), 0, s, fb);
+    hipLaunchKernelGGL(k_det_fallback_prep, grid, dim3(256), 0, s, c);
+    hipLaunchKernelGGL(k_detect_fallback, dim3(c.g.total_bands, c.n * c.ncam), dim3(TS_DET_THREADS), (size_t)c.g.det_lds, s, c);
+    hipLaunchKernelGGL(k_select_fallback, grid, dim3(SEL_THREADS), 0, s, c);
     hipLaunchKernelGGL(k_det_thr_commit, dim3(1), dim3(256), 0, s, c);
 }

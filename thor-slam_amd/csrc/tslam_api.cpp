@@ -373,7 +373,6 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.det_thr = (const uint32_t*)h->buf[TSLAM_BUF_DET_THR].ptr;
     c.det_thr_acc = h->d_det_thr_acc;
     c.det_fail = (uint32_t*)h->buf[TSLAM_BUF_DET_FAIL].ptr;
-    c.det_mode = 0;
     c.brief_table = h->d_brief;
     c.wedges = h->d_wedges;
     for (int p = 0; p < h->P; ++p) c.calib[p] = h->calib[p];

@@ -136,7 +136,7 @@ struct BatchCtx {
     const uint32_t* det_thr;      // [C][L]
     uint32_t* det_thr_acc;        // [C][L]
     uint32_t* det_fail;           // [B][C][L]
-    int det_mode;
+
     const uint32_t* brief_table;  // [30][256] LDS patch byte offsets of the two points (lo | hi << 16)
     const int64_t* wedges;        // [31][2]
     PairCalib calib[8];

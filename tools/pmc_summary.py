@@ -36,7 +36,7 @@ def load(d, counter=None):
 
 
 # kernels whose HBM reads are 16-byte-per-lane coalesced streams (the FETCH_SIZE halving applies)
-WIDE_READS = {"k_rectify_pyramid", "k_detect", "k_describe", "k_stream_blocks", "k_tsdf_integrate"}
+WIDE_READS = {"k_rectify_pyramid", "k_detect", "k_detect_fallback", "k_describe", "k_stream_blocks", "k_tsdf_integrate"}
 
 
 def main():
