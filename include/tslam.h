@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 6
+#define TSLAM_ABI_VERSION 7
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -96,6 +96,20 @@ typedef struct {
     int32_t rgbd_pad;             /* reserved, 0                                              */
 } tslam_params;
 
+/* One raw camera as IsaacRosAdapter publishes it (camera_info K/D + the rig extrinsics,
+ * isaac_ros.py:364-411; CameraConfig of thor_slam/slam/interface.py).  Input of tslam_create_rig. */
+typedef struct {
+    int32_t width, height;        /* image size                                               */
+    double K[9];                  /* camera matrix, row-major (camera_info.k)                  */
+    double D[14];                 /* distortion coefficients (camera_info.d), n_coeffs valid;  */
+    int32_t n_coeffs;             /*   >= 8 rational_polynomial[:8], 5 plumb_bob, 4 equidistant, else plumb_bob
+                                       zero-padded (isaac_ros.py:370-383)                       */
+    int32_t cam_idx;              /* index within its source: 0 = left / colour, 1 = right / depth */
+    double world_T_cam[16];       /* RigCalibration.get_world_extrinsics (rig.py:35-70), row-major,
+                                     optical (RDF) camera frame in the rig's base frame          */
+    const char* source;           /* source name (NULL = "")                                   */
+} tslam_camera_desc;
+
 /* Buffers exposed for parity tests (tslam_buffer_info / tslam_copy_out / tslam_copy_in). */
 enum tslam_buffer {
     TSLAM_BUF_PYRAMID = 0,   /* u8  [ring][cams][pyr_bytes]      rectified levels             */
@@ -147,6 +161,24 @@ int tslam_abi_version(void);
 
 int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int device, tslam_handle** out);
 int tslam_destroy(tslam_handle* h);
+
+/* Create a handle from raw calibration, doing on the host what HipSlamEngine.initialize does
+ * through thor_slam_amd/calib.py (C++ restatement in tslam_calib.cpp, byte-identical tables):
+ * cameras in extract_cameras order (sources sorted by name, isaac_ros.py:138-157), stereo pairs =
+ * a cam_idx 1 camera directly after cam_idx 0 of its source, Bouguet rectification of each pair
+ * (rgbd: undistortion of the colour camera), params->n_pairs = the pair count (0 = take it), and
+ * for more than one pair tslam_set_rig with each pair's base_T_rect.
+ * tslam_rig_pairs: the (left, right) indices into `cams` of the pairs (pairs[2*max_pairs] may be
+ *   NULL); returns the pair count.
+ * tslam_rectify_pair / tslam_rgbd_undistort: one pair's rectified intrinsics + baseline (the
+ *   desc's map pointers are set to the given buffers), the [H][W][2] int32 1/32-px tables
+ *   (NULL = skip), base_T_rect[16] = world_T_cam(left) * left_optical_T_rect (NULL = skip) and
+ *   rect_rot[18] = the two 3x3 rectifying rotations (NULL = skip). */
+int tslam_create_rig(const tslam_camera_desc* cams, int n_cams, const tslam_params* params, int device, tslam_handle** out);
+int tslam_rig_pairs(const tslam_camera_desc* cams, int n_cams, int32_t* pairs, int max_pairs);
+int tslam_rectify_pair(const tslam_camera_desc* left, const tslam_camera_desc* right, tslam_stereo_desc* desc,
+                       int32_t* map_left, int32_t* map_right, double* base_T_rect, double* rect_rot);
+int tslam_rgbd_undistort(const tslam_camera_desc* color, tslam_stereo_desc* desc, int32_t* map, double* base_T_rect);
 
 /* Run the whole hot path on `n_frames` (<= max_batch) frames.  `images` is device memory laid out
  * [n_frames][2*n_pairs][H][W] u8 (left, right per pair).  Frames get consecutive global indices. */

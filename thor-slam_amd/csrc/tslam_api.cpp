@@ -25,6 +25,11 @@ int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
+}  // namespace
+
+int tslam_internal_fail(int code, const char* msg) { return fail(code, msg); }
+
+namespace {
 
 #define HIPCHK(expr)                                                                           \
     do {                                                                                       \
@@ -156,6 +161,9 @@ static int dev_alloc(tslam_handle* h, void** p, size_t bytes) {
     if (e != hipSuccess) return fail(TSLAM_ENOMEM, std::string("hipMalloc failed: ") + hipGetErrorString(e));
     h->allocs.push_back(*p);
     HIPCHK(hipMemset(*p, 0, bytes));
+    // hipMemset is ordered on the null stream only: the handle's non-blocking streams (and the
+    // caller's) could otherwise write the buffer before the zeroing lands on it
+    HIPCHK(hipDeviceSynchronize());
     return TSLAM_OK;
 }
 
@@ -362,7 +370,7 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.pose = (double*)h->buf[TSLAM_BUF_POSE].ptr;
     c.stats = (int32_t*)h->buf[TSLAM_BUF_STATS].ptr;
     c.state = h->d_state;
-    c.prior = h->prior_armed ? h->d_prior : nullptr;
+    c.prior = h->prior_armed ? h->d_prior + (size_t)(h->batch_idx & 1) * TS_PRIOR_DOUBLES * h->P * h->B : nullptr;
     c.rig_E = h->d_rig_E;
     c.rig_Einv = h->d_rig_E ? h->d_rig_E + 16 * h->rig_q : nullptr;
     c.rig_pose = h->d_rig_pose;
@@ -672,6 +680,8 @@ int tslam_reset(tslam_handle* h) {
     h->cur_n = 0;
     for (auto& r : h->as_res) r.pending = false;   // results of batches before the reset are dropped
     h->as_last_pose_batch = h->as_batches - 1;
+    // hipMemset runs on the null stream, which the handle's non-blocking streams do not wait for
+    HIPCHK(hipDeviceSynchronize());
     return TSLAM_OK;
 }
 
@@ -1078,13 +1088,21 @@ int tslam_set_motion_prior(tslam_handle* h, const double* prior, int n_frames) {
     if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_set_motion_prior inside a batch");
     if (n_frames < 1 || n_frames > h->B) return fail(TSLAM_EINVAL, "n_frames must be in [1, max_batch]");
     HIPCHK(hipSetDevice(h->device));
-    if (!h->d_prior) {
-        const int rc = dev_alloc(h, (void**)&h->d_prior, sizeof(double) * TS_PRIOR_DOUBLES * h->P * h->B);
+    const size_t slot = (size_t)TS_PRIOR_DOUBLES * h->P * h->B;
+    if (!h->d_prior) {   // one slot per batch parity: batch s-1 may still be reading its prior
+        const int rc = dev_alloc(h, (void**)&h->d_prior, sizeof(double) * 2 * slot);
         if (rc != TSLAM_OK) return rc;
     }
-    std::vector<double> buf((size_t)TS_PRIOR_DOUBLES * h->P * h->B, 0.0);   // frames past n: weight 0
+    // the slot's previous reader is batch s-2's pose stage
+    const int par = (int)(h->batch_idx & 1);
+    if (h->back_pending[par]) {
+        HIPCHK(hipEventSynchronize(h->ev_back[par]));
+    } else {
+        HIPCHK(hipDeviceSynchronize());
+    }
+    std::vector<double> buf(slot, 0.0);   // frames past n: weight 0
     memcpy(buf.data(), prior, sizeof(double) * TS_PRIOR_DOUBLES * h->P * n_frames);
-    HIPCHK(hipMemcpy(h->d_prior, buf.data(), sizeof(double) * buf.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->d_prior + par * slot, buf.data(), sizeof(double) * buf.size(), hipMemcpyHostToDevice));
     h->prior_armed = true;
     return TSLAM_OK;
 }

@@ -1,7 +1,8 @@
 // tslam_common.h — device-side layout shared by the gfx950 kernels and the C-ABI host code.
 //
 // HBM layout (one handle = one device, P stereo pairs, C = 2P cameras, K keypoints/image,
-// batch B frames, ring R = 2B frames so frame t-1 of a batch's first frame is still resident):
+// batch B frames, ring R = 2B + 1 frames (+ the keyframe interval with BA) so frame t-1 of a
+// batch's first frame is still resident while the next batch's front stages run):
 //
 //   pyramid  u8  [R][C][pyr_bytes]   rectified level 0 + 2x2 box levels, each level dense (pitch W_l)
 //   smooth   u8  [B][C][pyr_bytes]   5x5 binomial of every level (BRIEF sampling image)

@@ -57,6 +57,30 @@ class Params(ctypes.Structure):
     ]
 
 
+class CameraDesc(ctypes.Structure):
+    """tslam_camera_desc: one raw camera (camera_info K/D + world extrinsics, isaac_ros.py:364-411)."""
+    _fields_ = [
+        ("width", ctypes.c_int32), ("height", ctypes.c_int32), ("K", ctypes.c_double * 9), ("D", ctypes.c_double * 14),
+        ("n_coeffs", ctypes.c_int32), ("cam_idx", ctypes.c_int32), ("world_T_cam", ctypes.c_double * 16),
+        ("source", ctypes.c_char_p),
+    ]
+
+
+def camera_desc(cam) -> CameraDesc:
+    """A ``CameraConfig`` (intrinsics + world extrinsics) as a ``tslam_camera_desc``."""
+    d = CameraDesc()
+    intr = cam.intrinsics
+    d.width, d.height = int(intr.width), int(intr.height)
+    d.K[:] = [float(v) for v in np.asarray(intr.matrix, dtype=np.float64).reshape(9)]
+    coeffs = np.asarray(intr.coeffs, dtype=np.float64).flatten()[:14]
+    d.D[:len(coeffs)] = [float(v) for v in coeffs]
+    d.n_coeffs = len(coeffs)
+    d.cam_idx = int(cam.cam_idx)
+    d.world_T_cam[:] = [float(v) for v in cam.extrinsics.to_4x4_matrix().reshape(16)]
+    d.source = str(cam.source_name).encode()
+    return d
+
+
 _lib: ctypes.CDLL | None = None
 
 # name -> (restype, argtypes); every symbol include/tslam.h declares
@@ -65,6 +89,13 @@ _SIGNATURES = {
     "tslam_abi_version": (ctypes.c_int, []),
     "tslam_create": (ctypes.c_int, [ctypes.POINTER(StereoDesc), ctypes.POINTER(Params), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "tslam_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "tslam_create_rig": (ctypes.c_int, [ctypes.POINTER(CameraDesc), ctypes.c_int, ctypes.POINTER(Params), ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_void_p)]),
+    "tslam_rig_pairs": (ctypes.c_int, [ctypes.POINTER(CameraDesc), ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
+    "tslam_rectify_pair": (ctypes.c_int, [ctypes.POINTER(CameraDesc), ctypes.POINTER(CameraDesc), ctypes.POINTER(StereoDesc),
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_rgbd_undistort": (ctypes.c_int, [ctypes.POINTER(CameraDesc), ctypes.POINTER(StereoDesc), ctypes.c_void_p,
+                                             ctypes.c_void_p]),
     "tslam_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "tslam_begin_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "tslam_run_stage": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
@@ -177,6 +208,30 @@ def make_params(cfg: HipSlamConfig, max_batch: int, n_pairs: int, ransac_splits:
     )
 
 
+def native_rectify_pair(left, right=None, rgbd: bool = False) -> dict:
+    """``tslam_rectify_pair`` (``tslam_rgbd_undistort`` with ``rgbd``) on two ``CameraConfig``:
+    the library's C++ restatement of ``calib.stereo_rectify`` / ``calib.rgbd_undistort``."""
+    lib = load_library()
+    dl = camera_desc(left)
+    h, w = int(dl.height), int(dl.width)
+    desc = StereoDesc()
+    ml = np.zeros((h, w, 2), np.int32)
+    mr = np.zeros((h, w, 2), np.int32)
+    base = np.zeros((4, 4))
+    rot = np.zeros((2, 3, 3))
+    if rgbd:
+        _check(lib.tslam_rgbd_undistort(ctypes.byref(dl), ctypes.byref(desc), ml.ctypes.data, base.ctypes.data))
+        mr[...] = ml
+        rot[:] = np.eye(3)
+    else:
+        dr = camera_desc(right)
+        _check(lib.tslam_rectify_pair(ctypes.byref(dl), ctypes.byref(dr), ctypes.byref(desc), ml.ctypes.data,
+                                      mr.ctypes.data, base.ctypes.data, rot.ctypes.data))
+    return {"width": desc.width, "height": desc.height, "fx": desc.fx, "fy": desc.fy, "cx": desc.cx, "cy": desc.cy,
+            "baseline": desc.baseline, "map_left": ml, "map_right": mr, "base_T_rect": base,
+            "rect_left": rot[0], "rect_right": rot[1]}
+
+
 class Handle:
     """Owns one ``tslam_handle`` (one device, ``n_pairs`` stereo pairs, batches <= ``max_batch``)."""
 
@@ -204,6 +259,32 @@ class Handle:
         _check(self.lib.tslam_create(descs, ctypes.byref(params), int(device), ctypes.byref(h)))
         self.h = h
         self._maps = []
+        self._read_layout()
+
+    @classmethod
+    def from_cameras(cls, cams: list, cfg: HipSlamConfig, max_batch: int = 1, device: int = 0,
+                     ransac_splits: int = 0) -> "Handle":
+        """``tslam_create_rig``: the handle from raw per-camera calibration (``CameraConfig`` list),
+        rectified and paired by the library's C++ host code; multi-pair rigs get ``tslam_set_rig``."""
+        self = cls.__new__(cls)
+        self.lib = load_library()
+        cfg.validate()
+        self.cfg = cfg
+        descs = (CameraDesc * len(cams))(*[camera_desc(c) for c in cams])
+        n_pairs = self.lib.tslam_rig_pairs(descs, len(cams), None, 0)
+        _check(min(n_pairs, 0))
+        self.n_pairs = n_pairs
+        self.cams_per_pair = 1 if cfg.rgbd else 2
+        self.n_cams = self.cams_per_pair * n_pairs
+        self.max_batch = int(max_batch)
+        params = make_params(cfg, max_batch, 0, ransac_splits)
+        h = ctypes.c_void_p()
+        _check(self.lib.tslam_create_rig(descs, len(cams), ctypes.byref(params), int(device), ctypes.byref(h)))
+        self.h = h
+        self._read_layout()
+        return self
+
+    def _read_layout(self) -> None:
         lay = (ctypes.c_int64 * 16)()
         lev = (ctypes.c_int32 * 18)()
         _check(self.lib.tslam_layout(self.h, lay, lev))
