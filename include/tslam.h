@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 7
+#define TSLAM_ABI_VERSION 8
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -243,11 +243,16 @@ int tslam_ring_slot(tslam_handle* h, int64_t global_frame);
  * level_info[0..17] with {W_l, H_l, K_l} for l < 6. */
 int tslam_layout(tslam_handle* h, int64_t* out16, int32_t* level_info18);
 
-/* IMU fusion (the gyro samples of SynchronizedFrameSet.sensor_data,
- * types.py:268-269, filled by rig.py:403-407): a rotation prior for each (frame, pair) of the NEXT
- * batch, prior[n][P][10] = the predicted rectified-left relative rotation R (row-major 3x3, the
- * rotation part of T_rel) and a weight W (px^2 / rad^2; 0 = none).  A7's Gauss-Newton then
- * minimises sum |reprojection|^2 + W |log(R_prior R^T)|^2 (small-angle form); RANSAC is unchanged. */
+/* IMU fusion (the gyro + accelerometer samples of
+ * SynchronizedFrameSet.sensor_data, types.py:268-269, filled by rig.py:403-407, noise densities of
+ * launch/thor_visual_slam.launch.py:82-93): a motion prior for each (frame, pair) of the NEXT
+ * batch, prior[n][P][16] = {R[9], W_r, t[3], W_t, 0, 0}: the predicted rectified-left relative
+ * pose T_rel = [R | t] (R row-major) with weights W_r (px^2 / rad^2) and W_t (px^2 / m^2), 0 = none.
+ * A7's Gauss-Newton then minimises sum |reprojection|^2 + W_r |log(R_prior R^T)|^2 (small-angle
+ * form) + W_t |t - t_prior|^2; RANSAC is unchanged.  A frame that is not tracked (LOST) but has
+ * W_t > 0 is chained with the prediction (its T_rel record becomes [R | t]; status stays LOST),
+ * so the trajectory continues through visual dropouts.  thor_slam_amd/imu.py computes the
+ * priors from the samples (gyro integration, velocity / gravity / accelerometer-bias filter). */
 int tslam_set_motion_prior(tslam_handle* h, const double* prior, int n_frames);
 
 /* Rig pose (replaces the multi-camera fusion cuVSLAM does for the rig of

@@ -605,8 +605,9 @@ def solve6(hm: np.ndarray, g: np.ndarray):
 def refine(rot, trn, corr, intr, thr2, iters, prior=None):
     """Gauss-Newton on the current inliers, re-selected every iteration.  Returns R, t, H, stats.
 
-    ``prior`` = (R_prior, W): IMU rotation prior, the term
-    W/2 |w - delta|^2 with delta = vee of the antisymmetric part of R_prior R^T (small angle)."""
+    ``prior`` = (R_prior, W) or (R_prior, W, t_prior, W_t): IMU prior, the
+    term W/2 |w - delta|^2 with delta = vee of the antisymmetric part of R_prior R^T (small angle),
+    and W_t/2 |t + rho - t_prior|^2 (accelerometer translation prediction)."""
     fx, fy, cx, cy = intr
     u = cx - corr["du"]
     v = cy - corr["dv"]
@@ -639,13 +640,18 @@ def refine(rot, trn, corr, intr, thr2, iters, prior=None):
                 hm[i, j] = np.sum(jx[i] * jx[j]) + np.sum(jy[i] * jy[j])
                 hm[j, i] = hm[i, j]
         if prior is not None and prior[1] > 0:
-            rp, w = prior
+            rp, w = prior[0], prior[1]
             mq = np.array([[(rp[i, 0] * rot[j, 0] + rp[i, 1] * rot[j, 1]) + rp[i, 2] * rot[j, 2] for j in range(3)]
                            for i in range(3)])
             dl = [0.5 * (mq[2, 1] - mq[1, 2]), 0.5 * (mq[0, 2] - mq[2, 0]), 0.5 * (mq[1, 0] - mq[0, 1])]
             for i in range(3):
                 hm[3 + i, 3 + i] += w
                 g[3 + i] += w * dl[i]
+        if prior is not None and len(prior) > 2 and prior[3] > 0:
+            tp, wt = prior[2], prior[3]
+            for i in range(3):
+                hm[i, i] += wt
+                g[i] += wt * (tp[i] - trn[i])
         sol = solve6(hm, g)
         if sol is None:
             return rot, trn, None, n_in, 0.0
@@ -861,8 +867,14 @@ class OracleTracker:
             est = estimate_pose(corr, intr, cfg, self.frame, prior)
             res.update(est)
             res["corr"] = corr
-            if est["status"] == 0:
-                t = est["T"]
+            if est["status"] != 0 and prior is not None and len(prior) > 2 and prior[3] > 0:
+                # untracked frame with an accelerometer prediction: it moves by the IMU's T_rel
+                t = np.eye(4)
+                t[:3, :3], t[:3, 3] = prior[0], prior[2]
+                res["T"] = t
+                est = dict(est, status=-1)
+            if est["status"] <= 0:
+                t = res["T"]
                 inv = np.eye(4)
                 inv[:3, :3] = t[:3, :3].T
                 inv[:3, 3] = -(t[:3, :3].T @ t[:3, 3])

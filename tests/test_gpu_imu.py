@@ -93,3 +93,101 @@ def test_engine_with_imu_source():
     r_imu = np.linalg.norm(Rotation.from_matrix(p_imu.to_4x4_matrix()[:3, :3].T @ gt[:3, :3]).as_rotvec())
     r_vis = np.linalg.norm(Rotation.from_matrix(p_vis.to_4x4_matrix()[:3, :3].T @ gt[:3, :3]).as_rotvec())
     assert r_imu < r_vis + 2e-3 and e_imu < e_vis + 5e-3
+
+
+def _imu_rig(n_frames=40, blackout=None, accel_noise=0.0, gyro_noise=0.0):
+    from thor_slam_amd.camera import CameraRig, Extrinsics
+    from thor_slam_amd.camera.types import IMUExtrinsics
+    from thor_slam_amd.synthetic import DRB_TO_RDF, SyntheticStereoSource
+
+    src = SyntheticStereoSource(seed=0, imu=True, gyro_noise=gyro_noise, accel_noise=accel_noise, blackout=blackout,
+                                n_frames=n_frames)
+    rig_T = src.rig_T_source
+    rig = CameraRig([src], rig_extrinsics={src.name: Extrinsics.from_4x4_matrix(rig_T)}, imu_source=src.name,
+                    imu_extrinsics=IMUExtrinsics(src.name, Extrinsics.from_4x4_matrix(rig_T @ DRB_TO_RDF)))
+    return src, rig
+
+
+def _run_engine(rig, n, cfg):
+    from thor_slam_amd.slam.hip_engine import HipSlamEngine
+
+    rig.start()
+    eng = HipSlamEngine(num_cameras=2, config=cfg)
+    eng.initialize(rig.calibration)
+    got = []
+    orig = eng._publish
+
+    def record(res, stamps, g0):
+        got.append({k: np.array(res[k][:len(stamps)]) for k in ("T_abs", "T_rel", "stats")})
+        orig(res, stamps, g0)
+
+    eng._publish = record
+    for _ in range(n):
+        eng.process_frames(rig.get_synchronized_frames())
+    eng.flush()
+    rects = eng._rects
+    eng.shutdown()
+    cat = {k: np.concatenate([g[k] for g in got]) for k in got[0]}
+    return cat, rects
+
+
+def test_accelerometer_prior_and_dropout_match_oracle():
+    """The engine's gyro + accelerometer leg (host filter -> tslam_set_motion_prior -> k_refine's
+    translation prior and k_chain's IMU chaining) against oracle/numpy_imu.run_sequence on the same
+    frames and samples, across a 3-frame visual dropout: statuses and RANSAC winners identical,
+    T_abs within 1e-9."""
+    from oracle import numpy_imu as OI
+    from thor_slam_amd.params import HipSlamConfig
+
+    n, batch = 20, 4
+    src, rig = _imu_rig(blackout=(9, 12), accel_noise=0.01, gyro_noise=1e-4)
+    cfg = HipSlamConfig(imu_fusion=True, imu_accel=True, batch_size=batch)
+    res, rects = _run_engine(rig, n, cfg)
+    rect = rects[0]
+    cal = rig.calibration
+    from thor_slam_amd.calib import extract_cameras
+
+    cams = extract_cameras(cal, 2)
+    bt = cams[0].extrinsics.to_4x4_matrix() @ rect.left_optical_T_rect()
+    ri = bt[:3, :3].T @ cal.imu_extrinsics.to_4x4_matrix()[:3, :3]
+    samples = []
+    for i in range(n):
+        s = src.imu_sample(i)
+        dt = None if i == 0 else src.timestamp(i) - src.timestamp(i - 1)
+        samples.append((dt, s["gyroscope"], s["accelerometer"]))
+    trk = O.OracleTracker(cfg, dict(fx=rect.fx, fy=rect.fy, cx=rect.cx, cy=rect.cy, baseline=rect.baseline,
+                                    map_l=rect.map_left, map_r=rect.map_right))
+    frames = np.stack([np.stack([src.render_image(i, 0), src.render_image(i, 1)]) for i in range(n)])
+    filt = OI.ImuFilter(ri, cfg.accelerometer_noise_density, cfg.accelerometer_random_walk, cfg.imu_rot_sigma,
+                        cfg.imu_trans_floor)
+    want = OI.run_sequence(trk, frames, samples, batch, filt)
+    status = [int(w["status"]) for w in want]
+    assert status[9:13] == [1, 1, 1, 1] and status[13:] == [0] * (n - 13)   # the dropout, then tracking
+    for g in range(n):
+        st = res["stats"][g, 0]
+        assert st[0] == want[g]["status"], g
+        if want[g]["status"] == 0:
+            assert st[4] == want[g]["best_hyp"] and st[2] == want[g]["n_inliers"], g
+        assert rel_frobenius(res["T_abs"][g, 0], want[g]["world_T_cam"]) < 1e-9, g
+
+
+def test_accelerometer_bridges_a_visual_dropout():
+    """Through a 6-frame dropout the gyro-only prior cannot move the camera; the accelerometer
+    leg carries it, so the end-of-sequence position error drops well below the gyro-only one."""
+    from thor_slam_amd.params import HipSlamConfig
+
+    n = 30
+    errs = {}
+    for accel in (False, True):
+        src, rig = _imu_rig(blackout=(10, 16), accel_noise=0.01, gyro_noise=1e-4)
+        cfg = HipSlamConfig(imu_fusion=True, imu_accel=accel, batch_size=1)
+        res, rects = _run_engine(rig, n, cfg)
+        rect = rects[0]
+        cams_T = [src.camera_pose(i, 0) for i in (0, n - 1)]
+        # ground truth in the rectified-left frame of frame 0 (rectification is the identity here)
+        gt = np.linalg.inv(cams_T[0]) @ cams_T[1]
+        assert rect.is_identity and int(res["stats"][n - 1, 0, 0]) == 0
+        errs[accel] = np.linalg.norm(res["T_abs"][n - 1, 0][:3, 3] - gt[:3, 3])
+    travelled = 0.5 * 7 / 30.0   # 0.5 m/s through the 7 untracked frames
+    assert errs[False] > 0.5 * travelled
+    assert errs[True] < 0.25 * errs[False], errs

@@ -540,6 +540,14 @@ __global__ __launch_bounds__(POSE_THREADS) void k_refine(BatchCtx c, int S) {
                             gv[3 + i] += W * dl[i];
                         }
                     }
+                    // accelerometer translation prior (weight W_t, px^2 / m^2): W_t/2 |t + rho - t_prior|^2
+                    const double Wt = pr[13];
+                    if (Wt > 0.0) {
+                        for (int i = 0; i < 3; ++i) {
+                            Hm[i * 6 + i] += Wt;
+                            gv[i] += Wt * (pr[10 + i] - s_t[i]);
+                        }
+                    }
                 }
                 for (int q = 0; q < 36; ++q) L[q] = 0.0;
                 if (!solve6(Hm, gv, x, L)) {
@@ -635,13 +643,33 @@ __global__ __launch_bounds__(256) void k_chain(BatchCtx c) {
             }
             for (int fl = tid; fl < nf; fl += blockDim.x) s_status[fl] = c.stats[(size_t)((f0 + fl) * c.P + p) * TS_STATS_INTS];
             __syncthreads();
+            // an untracked frame with an accelerometer prediction (W_t > 0) moves by the IMU's
+            // T_rel = [R_prior | t_prior]; its pose record's T_rel becomes that prediction
+            if (c.prior) {
+                for (int i = tid; i < nf * 16; i += blockDim.x) {
+                    const int fl = i / 16, e = i % 16, r = e / 4, q = e % 4;
+                    const size_t fp = (size_t)(f0 + fl) * c.P + p;
+                    const double* pr = c.prior + fp * TS_PRIOR_DOUBLES;
+                    if (s_status[fl] == 0 || !(pr[13] > 0.0)) continue;
+                    double v;
+                    if (r == 3) v = q == 3 ? 1.0 : 0.0;
+                    else if (q < 3) v = pr[3 * q + r];
+                    else v = -((pr[r] * pr[10] + pr[3 + r] * pr[11]) + pr[6 + r] * pr[12]);
+                    s_inv[fl][e] = v;
+                    c.pose[fp * TS_POSE_DOUBLES + e] = r == 3 ? (q == 3 ? 1.0 : 0.0) : (q < 3 ? pr[3 * r + q] : pr[10 + r]);
+                }
+                __syncthreads();
+                for (int fl = tid; fl < nf; fl += blockDim.x)
+                    if (s_status[fl] != 0 && c.prior[(size_t)((f0 + fl) * c.P + p) * TS_PRIOR_DOUBLES + 13] > 0.0) s_status[fl] = -1;
+                __syncthreads();
+            }
             if (tid < 64) {
                 const int j = lane & 3;
                 for (int fl = 0; fl < nf; ++fl) {
                     // row i of T lives in this lane's quad: quad_perm broadcasts of lanes 0..3
                     const double t0 = dpp_f64c<0x00>(T), t1 = dpp_f64c<0x55>(T);
                     const double t2 = dpp_f64c<0xAA>(T), t3 = dpp_f64c<0xFF>(T);
-                    if (s_status[fl] == 0) {
+                    if (s_status[fl] <= 0) {   // tracked (0) or IMU-propagated (-1)
                         const double* inv = s_inv[fl];
                         T = ((t0 * inv[j] + t1 * inv[4 + j]) + t2 * inv[8 + j]) + t3 * inv[12 + j];
                     }

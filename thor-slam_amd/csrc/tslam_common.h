@@ -41,7 +41,7 @@
 #define TS_MAX_HYP 1024
 #define TS_MAX_SPLITS 32   // RANSAC blocks per frame
 #define TS_RANSAC_WORDS 26 // per split: key + pad + 12 doubles
-#define TS_PRIOR_DOUBLES 10 // per (frame, pair): prior rotation (row-major 3x3) + weight
+#define TS_PRIOR_DOUBLES 16 // per (frame, pair): IMU prior R (row-major 3x3), W_r, t[3], W_t, 0, 0
 #define TS_BA_MAXW 10      // keyframes per BA window (6 camera rows each in the 64-wide system)
 
 struct LevelGeom {
@@ -124,7 +124,7 @@ struct BatchCtx {
     double* hyp;           // [B][P][4 * n_hyp][12] P3P candidate poses (k_p3p -> k_ransac)
     int32_t* stats;
     double* state;
-    const double* prior;   // [B][P][10] IMU rotation prior of the batch (tslam_set_motion_prior) or null
+    const double* prior;   // [B][P][16] IMU prior of the batch (tslam_set_motion_prior) or null
     // rig: base_T_rect-left of each pair and its inverse, body-frame results
     const double* rig_E;   // [P][16]
     const double* rig_Einv;

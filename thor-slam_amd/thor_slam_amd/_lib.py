@@ -351,13 +351,18 @@ class Handle:
             "cov": cov.reshape(shape + (6, 6)), "stats": stats.reshape(shape + (8,)),
         }
 
-    def set_motion_prior(self, rot: np.ndarray, weight: np.ndarray) -> None:
-        """Rotation prior for the next batch: rot [n][P][3][3] (predicted T_rel rotations), weight [n][P]."""
+    def set_motion_prior(self, rot: np.ndarray, weight: np.ndarray, trans: np.ndarray | None = None,
+                         trans_weight: np.ndarray | None = None) -> None:
+        """Motion prior for the next batch: rot [n][P][3][3] (predicted T_rel rotations), weight
+        [n][P]; optionally trans [n][P][3] (predicted T_rel translations) and trans_weight [n][P]."""
         rot = np.asarray(rot, dtype=np.float64)
         n = rot.shape[0]
-        buf = np.zeros((n, self.n_pairs, 10))
+        buf = np.zeros((n, self.n_pairs, 16))
         buf[..., :9] = rot.reshape(n, self.n_pairs, 9)
         buf[..., 9] = np.asarray(weight, dtype=np.float64).reshape(n, self.n_pairs)
+        if trans is not None:
+            buf[..., 10:13] = np.asarray(trans, dtype=np.float64).reshape(n, self.n_pairs, 3)
+            buf[..., 13] = np.asarray(trans_weight, dtype=np.float64).reshape(n, self.n_pairs)
         _check(self.lib.tslam_set_motion_prior(self.h, np.ascontiguousarray(buf).ctypes.data, int(n)))
 
     def set_rig(self, base_T_rect: list) -> None:

@@ -48,6 +48,13 @@ class HipSlamConfig(SlamConfig):
     # IMU fusion: gyro-predicted rotation prior in the pose Gauss-Newton
     imu_fusion: bool = False
     imu_rot_sigma: float = 2e-3     # rad, std of the per-frame gyro rotation prediction (1 px = 1 unit)
+    # ... plus the accelerometer leg (thor_slam_amd/imu.py): velocity / gravity / bias state, a
+    # translation prior, and IMU chaining through visual dropouts; noise model of
+    # launch/thor_visual_slam.launch.py:82-93
+    imu_accel: bool = False
+    accelerometer_noise_density: float = 2.553e-3   # m/s^2/sqrt(Hz)
+    accelerometer_random_walk: float = 1.0493e-4    # m/s^3/sqrt(Hz)
+    imu_trans_floor: float = 1e-3   # m, added in quadrature to the predicted translation's std
     # loop closure + keyframe pose graph; on when the reference's
     # SlamConfig.enable_loop_closure is (interface.py:155-156; single stereo pair / RGB-D camera)
     loop_kf_interval: int = 5       # frame g is a loop-closure keyframe iff g % loop_kf_interval == 0
@@ -90,6 +97,8 @@ class HipSlamConfig(SlamConfig):
             raise ValueError("fast_threshold must be in [0, 254]")
         if self.batch_size < 1:
             raise ValueError("batch_size must be >= 1")
+        if self.imu_accel and not self.imu_fusion:
+            raise ValueError("imu_accel needs imu_fusion=True")
         if self.dense_map:
             if not self.rgbd:
                 raise ValueError("dense_map needs rgbd=True (depth input)")

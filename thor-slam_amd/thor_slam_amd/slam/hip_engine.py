@@ -48,6 +48,7 @@ from ..calib import (StereoRectification, confidence_from_covariance, extract_ca
                      stereo_pairs, stereo_rectify)
 from ..camera.rig import RigCalibration
 from ..camera.types import SynchronizedFrameSet
+from ..imu import ImuPropagator
 from ..params import HipSlamConfig
 from ..rgbd import pack_rgbd
 from .interface import CameraConfig, MapPoint, SlamConfig, SlamEngine, SlamMap, SlamPose, TrackingState
@@ -123,7 +124,9 @@ class HipSlamEngine(SlamEngine):
         self._pose_lock = threading.Lock()
         self._frame_count = 0
         self._staged: list[tuple[np.ndarray, float]] = []
-        self._staged_gyro: list[np.ndarray | None] = []
+        self._staged_imu: list[tuple | None] = []    # (gyro, accel) per staged frame
+        self._imu: ImuPropagator | None = None       # accelerometer leg (imu_accel)
+        self._imu_batches: list[list] = []            # IMU samples of submitted, unpublished batches
         self._prev_stamp: float | None = None      # timestamp of the last submitted frame (IMU dt)
         self._base_R_imu = np.eye(3)
         self._torch = None
@@ -178,6 +181,10 @@ class HipSlamEngine(SlamEngine):
             self._base_T_rect = self._base_T_rects[0]
             imu = getattr(calibration, "imu_extrinsics", None)   # world(base)_T_imu, RDF-converted by the caller
             self._base_R_imu = imu.to_4x4_matrix()[:3, :3] if imu is not None else np.eye(3)
+            self._imu = None
+            if cfg.imu_fusion and cfg.imu_accel:
+                self._imu = ImuPropagator(self._base_T_rect[:3, :3].T @ self._base_R_imu, cfg.accelerometer_noise_density,
+                                          cfg.accelerometer_random_walk, cfg.imu_rot_sigma, cfg.imu_trans_floor)
             if len(self._pairs) > 1:   # the rig's body motion is solved on the device from all pairs
                 self._handle.set_rig(self._base_T_rects)
             if cfg.dense_map:
@@ -236,7 +243,7 @@ class HipSlamEngine(SlamEngine):
             with self._pose_lock:
                 return self._latest_pose
         self._staged.append((imgs, float(frame_set.timestamp)))
-        self._staged_gyro.append(self._gyro_of(frame_set))
+        self._staged_imu.append(self._imu_of(frame_set))
         if len(self._staged) >= self._config.batch_size:
             self._submit_staged()
         self._drain(block=False)
@@ -247,7 +254,7 @@ class HipSlamEngine(SlamEngine):
     def _async(self) -> bool:
         """Batches may stay in flight across calls (nothing reads per-batch device state)."""
         cfg = self._config
-        return cfg.ba_window <= 0 and self._loop is None and not cfg.dense_map
+        return cfg.ba_window <= 0 and self._loop is None and not cfg.dense_map and self._imu is None
 
     def _submit_staged(self) -> None:
         n = len(self._staged)
@@ -255,7 +262,7 @@ class HipSlamEngine(SlamEngine):
             return
         stamps = [ts for _, ts in self._staged]
         if self._config.imu_fusion:
-            self._set_imu_prior(stamps, self._staged_gyro)
+            self._set_imu_prior(stamps, self._staged_imu)
         if self._config.dense_map:   # the TSDF reads the batch's depth records on the device
             torch = self._torch
             host = self._host_images.numpy()
@@ -265,7 +272,7 @@ class HipSlamEngine(SlamEngine):
             self._dev_images[:n].copy_(self._host_images[:n], non_blocking=True)
             self._handle.submit(self._dev_images.data_ptr(), n, stream.cuda_stream)
             self._integrate_depth(self._dev_images.data_ptr(), n, stream.cuda_stream)
-            self._staged, self._staged_gyro = [], []
+            self._staged, self._staged_imu = [], []
             self._prev_stamp = stamps[-1]
             self._publish(self._read(n), stamps, self._handle.frames_done - n)
             return
@@ -274,7 +281,7 @@ class HipSlamEngine(SlamEngine):
             self._drain(block=True, limit=1)
         self._handle.submit_host(imgs, stamps)
         self._in_flight += 1
-        self._staged, self._staged_gyro = [], []
+        self._staged, self._staged_imu = [], []
         self._prev_stamp = stamps[-1]
         if not self._async:
             self._drain(block=True)
@@ -300,24 +307,32 @@ class HipSlamEngine(SlamEngine):
 
     # -- IMU fusion -------------------------------------------------------
     @staticmethod
-    def _gyro_of(frame_set: SynchronizedFrameSet) -> np.ndarray | None:
-        """Gyroscope sample [rad/s] (IMU axes) of a synchronised set, from ``sensor_data``
-        (IMUData or a dict with "gyroscope"; rig.py:403-407)."""
+    def _imu_of(frame_set: SynchronizedFrameSet) -> tuple | None:
+        """(gyroscope [rad/s], accelerometer [m/s^2] or None) in IMU axes of a synchronised set,
+        from ``sensor_data`` (IMUData or a dict with "gyroscope" / "accelerometer"; rig.py:403-407)."""
         d = getattr(frame_set, "sensor_data", None)
         if d is None:
             return None
-        g = d.get("gyroscope") if isinstance(d, dict) else getattr(d, "gyroscope", None)
-        return None if g is None else np.asarray(g, dtype=np.float64).reshape(3)
+        get = d.get if isinstance(d, dict) else (lambda k: getattr(d, k, None))
+        g, a = get("gyroscope"), get("accelerometer")
+        if g is None:
+            return None
+        return (np.asarray(g, dtype=np.float64).reshape(3), None if a is None else np.asarray(a, dtype=np.float64).reshape(3))
 
-    def _set_imu_prior(self, stamps: list[float], gyros: list) -> None:
+    def _set_imu_prior(self, stamps: list[float], imus: list) -> None:
         """Per staged frame and pair: the rectified-left rotation predicted by the gyro over the
-        frame interval, R = exp(-[w_rect dt]x), with weight (1 px / imu_rot_sigma)^2."""
+        frame interval, R = exp(-[w_rect dt]x), with weight (1 px / imu_rot_sigma)^2; with the
+        accelerometer leg, the whole predicted T_rel and its weights (thor_slam_amd/imu.py)."""
+        if self._imu is not None:
+            self._set_inertial_prior(stamps, imus)
+            return
         P = len(self._pairs)
         rot = np.tile(np.eye(3), (len(stamps), P, 1, 1))
         wgt = np.zeros((len(stamps), P))
         prev = self._prev_stamp
         w0 = 1.0 / (self._config.imu_rot_sigma ** 2)
-        for k, (ts, gy) in enumerate(zip(stamps, gyros)):
+        for k, (ts, imu) in enumerate(zip(stamps, imus)):
+            gy = None if imu is None else imu[0]
             if gy is not None and prev is not None and ts > prev:
                 w_base = self._base_R_imu @ gy
                 for p, bt in enumerate(self._base_T_rects):
@@ -325,6 +340,40 @@ class HipSlamEngine(SlamEngine):
                     wgt[k, p] = w0
             prev = ts
         self._handle.set_motion_prior(rot, wgt)
+
+    def _set_inertial_prior(self, stamps: list[float], imus: list) -> None:
+        """Gyro + accelerometer: per frame the predicted T_rel of pair 0's rectified-left camera
+        (moved into every other pair's camera through the rig, inv(E_p) E_0 T inv(E_0) E_p) with its
+        rotation and translation weights.  The samples are kept for the filter's update."""
+        imu, prev = self._imu, self._prev_stamp
+        samples = []
+        for ts, s in zip(stamps, imus):
+            ok = s is not None and s[1] is not None
+            if ok and not imu.ready:
+                imu.begin(s[1])            # this frame anchors the filter: no prior for it
+                samples.append((None, None, None))
+            elif ok and prev is not None and ts > prev:
+                samples.append((ts - prev, s[0], s[1]))
+            else:
+                samples.append((None, None, None))
+            prev = ts
+        steps = imu.batch_priors(samples)
+        P, n = len(self._pairs), len(stamps)
+        rot = np.tile(np.eye(3), (n, P, 1, 1))
+        trn = np.zeros((n, P, 3))
+        wr, wt = np.zeros((n, P)), np.zeros((n, P))
+        e0 = self._base_T_rects[0]
+        for k, st in enumerate(steps):
+            if st is None:
+                continue
+            t0 = np.eye(4)
+            t0[:3, :3], t0[:3, 3] = st.R_rel, st.t_rel
+            for p, ep in enumerate(self._base_T_rects):
+                tp = t0 if p == 0 else _invert(ep) @ e0 @ t0 @ _invert(e0) @ ep
+                rot[k, p], trn[k, p] = tp[:3, :3], tp[:3, 3]
+                wr[k, p], wt[k, p] = st.w_rot, st.w_trans
+        self._handle.set_motion_prior(rot, wr, trn, wt)
+        self._imu_batches.append(samples)
 
     def process_batch(self, images, timestamps: list[float] | None = None, stream=None) -> dict:
         """Throughput entry: ``images`` is a device uint8 tensor already in HBM: [n, 2P, H, W] gray
@@ -428,6 +477,8 @@ class HipSlamEngine(SlamEngine):
             self._map_points[int(mp["gid"][i])] = (win["X"][i].copy(), mp["desc"][i].copy(), int(n))
 
     def _publish(self, res: dict, stamps: list[float], g0: int) -> None:
+        if self._imu is not None and self._imu_batches:   # the filter absorbs pair 0's motions
+            self._imu.absorb(self._imu_batches.pop(0), res["stats"][:, 0, 0], res["T_rel"][:, 0], res["cov"][:, 0])
         latest = None
         state = self._state
         corr = self._ba_corrections(res, len(stamps), g0)
@@ -632,7 +683,10 @@ class HipSlamEngine(SlamEngine):
         self._in_flight = 0
         with self._pose_lock:
             self._latest_pose = None
-        self._staged, self._staged_gyro, self._prev_stamp = [], [], None
+        self._staged, self._staged_imu, self._prev_stamp = [], [], None
+        self._imu_batches = []
+        if self._imu is not None:
+            self._imu.reset()
         self._keyframe_poses = []
         self._fe_at, self._kf_final, self._kf_stamp, self._ba_window = {}, {}, {}, None
         self._map_points, self._map_offset = {}, np.eye(4)

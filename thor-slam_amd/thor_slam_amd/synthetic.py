@@ -183,6 +183,8 @@ class SyntheticStereoSource(CameraSource):
         n_frames: int = 100,
         imu: bool = False,
         gyro_noise: float = 0.0,
+        accel_noise: float = 0.0,
+        blackout: tuple[int, int] | None = None,
     ) -> None:
         self._name = name
         self.scene = scene or RoomScene(seed=seed)
@@ -202,6 +204,8 @@ class SyntheticStereoSource(CameraSource):
             self._extr.append(Extrinsics.from_4x4_matrix(m))
         self.imu = imu
         self.gyro_noise = gyro_noise
+        self.accel_noise = accel_noise
+        self.blackout = blackout   # frames [a, b) render as a uniform grey (a visual dropout)
         self._index = 0
         self._running = False
         self._lock = threading.Lock()
@@ -228,11 +232,19 @@ class SyntheticStereoSource(CameraSource):
         (the chain of run_slam.py:252-283 turns it into RDF with DRB_TO_RDF)."""
         return Extrinsics.from_4x4_matrix(np.eye(4)) if self.imu else None
 
+    def imu_position(self, i: int) -> np.ndarray:
+        """World position of the IMU (the source origin) at frame i."""
+        return (self.trajectory[i % len(self.trajectory)] @ self.rig_T_source)[:3, 3]
+
     def imu_sample(self, i: int) -> dict:
-        """Gyro = the source's rotation from frame i-1 to i over the frame interval (DRB axes) +
-        N(0, gyro_noise^2); accelerometer = gravity's reaction in the IMU frame.  A dict with the
-        IMUData fields, the form the reference's rig carries (luxonis.py:1155-1158 casts to dict and
-        indexes ["timestamp"]; its IMUData class has no constructor)."""
+        """The sample of the interval (i-1, i]: gyro = the source's rotation from frame i-1 to i over
+        the frame interval (DRB axes) + N(0, gyro_noise^2); accelerometer = the specific force
+        R^T (a - g) in the IMU axes of frame i-1, with the world acceleration a the second
+        difference of the IMU positions around frame i-1 (so p_i = p_{i-1} + v dt + a dt^2 / 2
+        holds for the central-difference velocity v) and g = (0, 0, -9.81) (the renderer's world is
+        z-up) + N(0, accel_noise^2).  A dict with the IMUData fields, the form the reference's rig
+        carries (luxonis.py:1155-1158 casts to dict and indexes ["timestamp"]; its IMUData class has
+        no constructor)."""
         dt = 1.0 / self.fps
         r0 = self.camera_pose(max(i - 1, 0), 0)[:3, :3]
         r1 = self.camera_pose(i, 0)[:3, :3]
@@ -241,7 +253,14 @@ class SyntheticStereoSource(CameraSource):
         w = d.T @ w_rdf
         if self.gyro_noise:
             w = w + np.random.default_rng((self.seed, i, 99)).normal(0.0, self.gyro_noise, 3)
-        acc = d.T @ (r1.T @ np.array([0.0, 0.0, 9.81]))
+        if i == 0:
+            a_w = np.zeros(3)   # the sequence starts at rest (the filter's gravity alignment)
+        else:
+            k = max(i - 1, 1)
+            a_w = (self.imu_position(k + 1) - 2.0 * self.imu_position(k) + self.imu_position(k - 1)) / dt ** 2
+        acc = d.T @ (r0.T @ (a_w + np.array([0.0, 0.0, 9.81])))
+        if self.accel_noise:
+            acc = acc + np.random.default_rng((self.seed, i, 98)).normal(0.0, self.accel_noise, 3)
         return {"accelerometer": acc, "gyroscope": w, "timestamp": self.timestamp(i), "sequence_num": i}
 
     def get_timestamped_sensor_data(self) -> tuple[dict | None, float | None]:
@@ -283,6 +302,8 @@ class SyntheticStereoSource(CameraSource):
         return body @ self.rig_T_source @ self._extr[cam].to_4x4_matrix()
 
     def render_image(self, i: int, cam: int) -> np.ndarray:
+        if self.blackout is not None and self.blackout[0] <= i < self.blackout[1]:
+            return np.full((self.height, self.width), 128, dtype=np.uint8)
         rng = np.random.default_rng((self.seed, i, cam))
         return self.scene.render(self.camera_pose(i, cam), self._intr[cam], rng)
 
