@@ -316,6 +316,12 @@ int tslam_ba_read(tslam_handle* h, int pair, int64_t* frames, double* cam_T_worl
  * (2 (6n+1)^2 3L per launch, n keyframes, L landmarks), then re-arms timing for up to
  * `max_launches` further launches (0 = off). */
 int tslam_ba_profile(tslam_handle* h, int max_launches, double* schur_ms, int64_t* schur_launches, double* schur_flops);
+/* Measurement: `reps` back-to-back k_ba_schur launches on pair `pair`'s last solved window (the
+ * kernel only rewrites its own outputs), between two HIP events on `stream`: the average launch
+ * duration and the algorithmic flops per launch (for the FP64 MFMA roofline, without per-launch
+ * events inside the timed steps). */
+int tslam_ba_replay_schur(tslam_handle* h, int pair, int reps, void* stream, double* us_per_launch,
+                          double* flops_per_launch);
 
 /* Map side of A8 for persistence (synchronises): per landmark id of pair `pair`'s window the
  * global landmark id (creation frame * K + keypoint; -1 / stale where no landmark lives) and the

@@ -410,6 +410,7 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
     __shared__ int s_has[BA_CHUNK][TS_BA_MAXW];
     __shared__ double s_L[BA_CHUNK][6];
     __shared__ double s_T[TS_BA_MAXW][12];
+    __shared__ double s_bs[BA_CHUNK][TS_BA_MAXW][3];
     const int K = c.g.K, WK = a.W * K, n = a.n_order;
     BaPair q = ba_pair(c, a, a.pair);
     const int L = q.counts[1];
@@ -419,9 +420,50 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
     for (int i = threadIdx.x; i < n * 12; i += blockDim.x) s_T[i / 12][i % 12] = q.T[(size_t)a.order[i / 12] * 16 + i % 12];
     d4v acc[4];
     for (int t = 0; t < 4; ++t) acc[t] = (d4v){0.0, 0.0, 0.0, 0.0};
+    const bool bsub = a.fused_backsub && q.counts[2];   // the previous solve succeeded
     for (int l0 = blockIdx.x * BA_CHUNK; l0 < L; l0 += gridDim.x * BA_CHUNK) {
         const int nl = min(BA_CHUNK, L - l0);
         __syncthreads();
+        // 0. the previous iteration's landmark update for the chunk (what k_ba_backsub does,
+        //    fused: this block factored these landmarks then): dp = V^-1 (-g_p - sum_c W_o^T dc_c)
+        if (bsub) {
+            const int li = threadIdx.x / TS_BA_MAXW, ci = threadIdx.x - li * TS_BA_MAXW;
+            const int r = l0 + li;
+            const int o = (li < nl && ci >= 1 && ci < n) ? q.camobs[(size_t)ci * WK + r] : -1;   // dc of camera 0 is zero
+            double t[3] = {0.0, 0.0, 0.0};
+            if (o >= 0) {
+                const double* W = q.obs_W + (size_t)o * 18;
+                const double* dc = q.dc + 6 * ci;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    double acc = 0.0;
+#pragma unroll
+                    for (int e = 0; e < 6; ++e) acc += W[3 * e + j] * dc[e];
+                    t[j] = acc;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 3; ++j) s_bs[li][ci][j] = t[j];
+            __syncthreads();
+            if (threadIdx.x < nl) {
+                const int rr = l0 + threadIdx.x;
+                double rhs[3];
+                for (int j = 0; j < 3; ++j) {
+                    double sum = 0.0;
+                    for (int cj = 1; cj < n; ++cj) sum += s_bs[threadIdx.x][cj][j];
+                    rhs[j] = -q.lm_gp[(size_t)j * WK + rr] - sum;
+                }
+                const double L0 = q.lm_L[rr], L1 = q.lm_L[(size_t)WK + rr], L2 = q.lm_L[(size_t)2 * WK + rr];
+                const double L3 = q.lm_L[(size_t)3 * WK + rr], L4 = q.lm_L[(size_t)4 * WK + rr], L5 = q.lm_L[(size_t)5 * WK + rr];
+                const double y0 = rhs[0] / L0, y1 = (rhs[1] - L1 * y0) / L2, y2 = ((rhs[2] - L3 * y0) - L4 * y1) / L5;
+                const double x2 = y2 / L5, x1 = (y1 - L4 * x2) / L2, x0 = ((y0 - L1 * x1) - L3 * x2) / L0;
+                const int id = q.lm_id[rr];
+                q.X[(size_t)id * 3] += x0;
+                q.X[(size_t)id * 3 + 1] += x1;
+                q.X[(size_t)id * 3 + 2] += x2;
+            }
+            __syncthreads();
+        }
         // 1. Jacobians of every (landmark, camera) observation of the chunk
         {
             const int li = threadIdx.x / TS_BA_MAXW, ci = threadIdx.x - li * TS_BA_MAXW;
@@ -552,169 +594,150 @@ __global__ __launch_bounds__(256) void k_ba_reduce(BatchCtx c, BaArgs a) {
 }
 
 // Reduced camera system (camera 0 = gauge): S = blockdiag(U + lam) - C, b = -g_c + C[:, 60].
-// LDL^T elimination with the right-hand side as an extra column (one barrier per pivot), then
-// the back substitution on one wave (lane = row); camera updates R <- cayley(w) R, t <- ... + rho.
-__global__ __launch_bounds__(1024) void k_ba_solve(BatchCtx c, BaArgs a) {
-    __shared__ double s_S[TS_BA_MAXD * (TS_BA_MAXD + 1)];
-    __shared__ double s_x[TS_BA_MAXD];
-    __shared__ int s_ok;
+// LDL^T of [S | b] (the right-hand side as column M: forward substitution fused) on 8 waves,
+// every one of them holding all rows: lane i = row i (rows past m = 6 (n - 1) are identity rows,
+// so one fully unrolled code serves every window size) and wave w the columns k = 8 t + w.
+// Step j: the owner wave of column j (j % 8) divides it by the pivot d_j (v_readlane of lane j)
+// and posts the multipliers l_ij in LDS; after one barrier every wave subtracts l_ij * S[j][k]
+// from its columns, the pivot row's entries coming from lane j of the same wave by v_readlane.
+// Lane k's row freezes at step k, so by symmetry its entries right of the diagonal are then
+// column k of L D: they go to LDS, and wave 0 runs the back substitution D L^T x = y (x_i by
+// readlane, lanes k < i subtract (S[k][i] / d_k) x_i).  Camera updates R <- cayley(w) R,
+// t <- ... + rho follow.
+#define BA_SOLVE_WAVES 8   // 4 / 8 / 16 waves: 21.8 / 19.4 / 20.1 us per solve alone (exp microbenchmark)
+#define BA_SOLVE_COLS ((TS_BA_MAXD + BA_SOLVE_WAVES) / BA_SOLVE_WAVES)   // columns per wave (+ the rhs)
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, BaArgs a) {
+    constexpr int M = TS_BA_MAXD;
+    constexpr int NT = BA_SOLVE_COLS;
+    constexpr int WV = BA_SOLVE_WAVES;
+    static_assert(TS_BA_MAXW * 27 <= 64 * WV, "one camera-block load per thread");
+    __shared__ double s_C[64 * 64];   // C, then the frozen rows (S[k][i], i > k) for the back substitution
+    __shared__ double s_U[TS_BA_MAXW * 27];
+    __shared__ double s_l[2][64];
+    __shared__ double s_d[64];
+    __shared__ double s_x[64];
+    __shared__ int s_ok[2];   // per step parity: the pivot was positive
     BaPair q = ba_pair(c, a, a.pair);
     const int n = a.n_order;
-    const int m = 6 * (n - 1), mp = m + 1;
+    const int m = 6 * (n - 1);
     if (q.counts[1] == 0 || n < 2) {
         if (threadIdx.x == 0) q.counts[2] = 0;
         return;
     }
-    // stage C and the camera blocks in LDS first (every load in flight at once), then build S
-    __shared__ double s_C[64 * 64];
-    __shared__ double s_U[TS_BA_MAXW * 27];
-    {
-        double v[4];
+    {   // stage C and the camera blocks (every load in flight at once)
+        constexpr int NL = 4096 / (64 * WV);
+        double v[NL];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = q.C[threadIdx.x + 1024 * k];
-        const double u = (int)threadIdx.x < n * 27 ? q.cam_U[threadIdx.x] : 0.0;
+        for (int k = 0; k < NL; ++k) v[k] = q.C[threadIdx.x + 64 * WV * k];
+        const double u0 = (int)threadIdx.x < n * 27 ? q.cam_U[threadIdx.x] : 0.0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) s_C[threadIdx.x + 1024 * k] = v[k];
-        if ((int)threadIdx.x < n * 27) s_U[threadIdx.x] = u;
+        for (int k = 0; k < NL; ++k) s_C[threadIdx.x + 64 * WV * k] = v[k];
+        if ((int)threadIdx.x < n * 27) s_U[threadIdx.x] = u0;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < m * mp; i += blockDim.x) {
-        const int rr = i / mp, cc = i - rr * mp;
-        const int R = rr + 6;
-        double v;
-        if (cc == m) {
-            v = -s_U[(R / 6) * 27 + 21 + R % 6] + s_C[R * 64 + 60];
-        } else {
-            const int Cc = cc + 6;
+    const int i = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const bool live = i < m;
+    const int R = i + 6, ci = R / 6, i0 = R % 6;
+    double r[NT];   // row i, columns WV t + w
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int k = WV * t + w;
+        double v = (k == i) ? 1.0 : 0.0;   // identity rows / columns past m
+        if (k == M) {
+            v = live ? -s_U[ci * 27 + 21 + i0] + s_C[R * 64 + 60] : 0.0;
+        } else if (live && k < m) {
+            const int Cc = k + 6;
             v = -s_C[R * 64 + Cc];
-            if (R / 6 == Cc / 6) {
-                const int i0 = R % 6, j0 = Cc % 6;
+            if (ci == Cc / 6) {
+                const int j0 = Cc % 6;
                 const int lo = min(i0, j0), hi = max(i0, j0);
-                v += s_U[(R / 6) * 27 + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)] + (i0 == j0 ? a.lam : 0.0);
+                v += s_U[ci * 27 + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)] + (i0 == j0 ? a.lam : 0.0);
             }
         }
-        s_S[i] = v;
+        r[t] = v;
     }
-    if (threadIdx.x == 0) s_ok = 1;
-    __syncthreads();
-    // S = L' D L'^T by 6-column blocks (one camera each).  For block J (columns c0..c0+5):
-    //  panel (wave 0, lane = row i >= c0): the unblocked steps j = c0..c0+5 restricted to the
-    //    block's columns and the rhs, S[i][k] -= (S[i][j] / d_j) S[k][j] (wave-synchronous);
-    //  trailing (all threads): S[i][k] -= sum_j (S[i][j] / d_j) S[k][j] for c0+6 <= k <= i.
-    // Column j below the pivot is left as L'[i][j] * d_j.
-#ifndef BA_TT
-#define BA_TT 1   // 2x2 and 4x4 register tiles measured slower (the update is latency-bound)
-#endif
-    __shared__ double s_P[TS_BA_MAXD * 6];
-    for (int c0 = 0; c0 < m; c0 += 6) {
-        if (threadIdx.x < 64) {
-            // panel in registers: lane = row i (>= c0) holds its 6 block entries and its rhs; the
-            // pivot row's entries come by readlane (lane j - c0), so the 6 steps need no LDS trip
-            const int i = c0 + (int)threadIdx.x;
-            const bool row = i < m;
-            double pv[6], rh = row ? s_S[i * mp + m] : 0.0;
-#pragma unroll
-            for (int e = 0; e < 6; ++e) pv[e] = row ? s_S[i * mp + c0 + e] : 0.0;
-            bool good = true;
-            double rdv[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                const double dj = readlane_f64(pv[j], j);
-                if (!(dj > 0.0)) {   // uniform across the wave
-                    good = false;
-                    break;
-                }
-                const double rj = 1.0 / dj;
-                const double sij = pv[j] * rj;
-                const double rhj = readlane_f64(rh, j);
-                const bool below = (int)threadIdx.x > j && row;
-#pragma unroll
-                for (int k = j + 1; k < 6; ++k) {
-                    const double skj = readlane_f64(pv[j], k);   // S[c0 + k][c0 + j]
-                    if (below && k <= (int)threadIdx.x) pv[k] -= sij * skj;
-                }
-                if (below) rh -= sij * rhj;
-                rdv[j] = rj;
-            }
-            if (!good && threadIdx.x == 0) s_ok = 0;
-            if (row) {
-#pragma unroll
-                for (int e = 0; e < 6; ++e) {
-                    s_S[i * mp + c0 + e] = pv[e];
-                    s_P[i * 6 + e] = pv[e] * rdv[e];   // L'[i][c0+e] for the trailing update
-                }
-                s_S[i * mp + m] = rh;
-            }
+    // multipliers of step j: the owner of column j (wave j % WV) divides it by the pivot d_j (lane
+    // j) and posts them in LDS (buffer j & 1, with the pivot's sign check).  Look-ahead: during
+    // step j the owner of column j + 1 updates that column first and posts step j + 1's
+    // multipliers before its other columns, so one barrier per step separates them.
+    auto post = [&](int j, double col) {
+        const double d = readlane_f64(col, j);
+        s_l[j & 1][i] = (i > j && d > 0.0) ? col / d : 0.0;
+        if (i == 0) {
+            s_d[j] = d;
+            s_ok[j & 1] = d > 0.0;   // the buffer of step j - 2: every wave has read it
         }
-        __syncthreads();
-        if (!s_ok) break;
-        // trailing update in BA_TT x BA_TT register tiles (lower triangle): a tile loads its scaled
-        // and plain panel rows once
-        const int c1 = c0 + 6, nt = m - c1, T = (nt + BA_TT - 1) / BA_TT;
-        for (int t = threadIdx.x; t < T * T; t += blockDim.x) {
-            const int ti = t / T, tk = t - ti * T;
-            if (tk > ti) continue;
-            const int i0 = c1 + BA_TT * ti, k0 = c1 + BA_TT * tk;
-            double pi[BA_TT][6], pk[BA_TT][6];
+    };
+    if (w == 0) post(0, r[0]);
+    __syncthreads();
+    bool good = true;
 #pragma unroll
-            for (int r = 0; r < BA_TT; ++r)
+    for (int j = 0; j < M; ++j) {
+        if (!s_ok[j & 1]) {   // block-uniform
+            good = false;
+            break;
+        }
+        const double l = s_l[j & 1][i];
+        const int j1 = j + 1, t1 = j1 / WV;
+        const bool ahead = j1 < M && w == (j1 % WV);   // this wave owns the next pivot column
+        if (ahead) {
+            r[t1] -= l * readlane_f64(r[t1], j);
+            post(j1, r[t1]);
+        }
 #pragma unroll
-                for (int e = 0; e < 6; ++e) {
-                    pi[r][e] = i0 + r < m ? s_P[(i0 + r) * 6 + e] : 0.0;
-                    pk[r][e] = k0 + r < m ? s_S[(k0 + r) * mp + c0 + e] : 0.0;
-                }
-#pragma unroll
-            for (int r = 0; r < BA_TT; ++r)
-#pragma unroll
-                for (int q2 = 0; q2 < BA_TT; ++q2) {
-                    const int ii = i0 + r, k = k0 + q2;
-                    if (ii < m && k <= ii) {
-                        double acc = 0.0;
-#pragma unroll
-                        for (int e = 0; e < 6; ++e) acc += pi[r][e] * pk[q2][e];
-                        s_S[ii * mp + k] -= acc;
-                    }
-                }
+        for (int t = 0; t < NT; ++t) {
+            if (WV * t + WV - 1 <= j) continue;   // every column of t is at or left of j (compile time)
+            if (ahead && t == t1) continue;
+            const double p = readlane_f64(r[t], j);
+            if (WV * t + w > j) r[t] -= l * p;
         }
         __syncthreads();
     }
+    // frozen rows -> LDS (row k, column i = 4 t + w > k), then wave 0 solves D L^T x = y
     __syncthreads();
-    const bool ok = s_ok;
-    if (ok && threadIdx.x < 64) {
-        // D L'^T x = b'':  x_k = b''_k / d_k - sum_{i > k} L'[i][k] x_i   (lane k, i descending)
-        const int k = threadIdx.x;
-        const double rk = k < m ? 1.0 / s_S[k * mp + k] : 1.0;
-        double r = k < m ? s_S[k * mp + m] * rk : 0.0;
-        for (int i = m - 1; i >= 0; --i) {
-            const double lik = k < i ? s_S[i * mp + k] * rk : 0.0;   // independent of the chain
-            r -= lik * readlane_f64(r, i);
+    if (good) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int k = WV * t + w;
+            if (k <= M) s_C[i * 64 + k] = r[t];
         }
-        if (k < m) s_x[k] = r;
     }
     __syncthreads();
+    if (good && w == 0) {
+        const double rd = 1.0 / s_d[i < M ? i : 0];
+        double x = i < M ? s_C[i * 64 + M] * rd : 0.0;
+#pragma unroll
+        for (int i2 = M - 1; i2 > 0; --i2) {
+            const double xi = readlane_f64(x, i2);
+            if (i < i2) x -= (s_C[i * 64 + i2] * rd) * xi;
+        }
+        s_x[i] = x;
+    }
+    __syncthreads();
+    const bool ok = good;
     if (threadIdx.x == 0) q.counts[2] = ok;
-    for (int i = threadIdx.x; i < 6 * n; i += blockDim.x) q.dc[i] = (i < 6 || !ok) ? 0.0 : s_x[i - 6];
+    for (int e = threadIdx.x; e < 6 * n; e += blockDim.x) q.dc[e] = (e < 6 || !ok) ? 0.0 : s_x[e - 6];
     if (ok && (int)threadIdx.x >= 1 && (int)threadIdx.x < n) {
-        const int ci = threadIdx.x;
-        const double* x = s_x + 6 * (ci - 1);
+        const int cj = threadIdx.x;
+        const double* x = s_x + 6 * (cj - 1);
         const double w0 = x[3], w1 = x[4], w2 = x[5];
         const double A[9] = {0.0, -w2, w1, w2, 0.0, -w0, -w1, w0, 0.0};
         double A2[9];
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) A2[3 * i + j] = (A[3 * i] * A[j] + A[3 * i + 1] * A[3 + j]) + A[3 * i + 2] * A[6 + j];
+        for (int ii = 0; ii < 3; ++ii)
+            for (int jj = 0; jj < 3; ++jj) A2[3 * ii + jj] = (A[3 * ii] * A[jj] + A[3 * ii + 1] * A[3 + jj]) + A[3 * ii + 2] * A[6 + jj];
         const double n2 = (w0 * w0 + w1 * w1) + w2 * w2;
         const double sc = 4.0 / (4.0 + n2);
         double RU[9];
         for (int e = 0; e < 9; ++e) RU[e] = ((e % 4) == 0 ? 1.0 : 0.0) + sc * (A[e] + 0.5 * A2[e]);
-        double* T = q.T + (size_t)a.order[ci] * 16;
+        double* T = q.T + (size_t)a.order[cj] * 16;
         double Rn[9], tn[3];
-        for (int i = 0; i < 3; ++i) {
-            for (int j = 0; j < 3; ++j) Rn[3 * i + j] = (RU[3 * i] * T[j] + RU[3 * i + 1] * T[4 + j]) + RU[3 * i + 2] * T[8 + j];
-            tn[i] = ((RU[3 * i] * T[3] + RU[3 * i + 1] * T[7]) + RU[3 * i + 2] * T[11]) + x[i];
+        for (int ii = 0; ii < 3; ++ii) {
+            for (int jj = 0; jj < 3; ++jj) Rn[3 * ii + jj] = (RU[3 * ii] * T[jj] + RU[3 * ii + 1] * T[4 + jj]) + RU[3 * ii + 2] * T[8 + jj];
+            tn[ii] = ((RU[3 * ii] * T[3] + RU[3 * ii + 1] * T[7]) + RU[3 * ii + 2] * T[11]) + x[ii];
         }
-        for (int i = 0; i < 3; ++i) {
-            for (int j = 0; j < 3; ++j) T[4 * i + j] = Rn[3 * i + j];
-            T[4 * i + 3] = tn[i];
+        for (int ii = 0; ii < 3; ++ii) {
+            for (int jj = 0; jj < 3; ++jj) T[4 * ii + jj] = Rn[3 * ii + jj];
+            T[4 * ii + 3] = tn[ii];
         }
     }
 }
@@ -795,6 +818,12 @@ void launch_ba_keyframe(const BatchCtx& c, const BaArgs& a, bool evict, hipStrea
     hipLaunchKernelGGL(k_ba_insert, dim3((K + 255) / 256), dim3(256), 0, s, c, a);
 }
 
+void launch_ba_schur(const BatchCtx& c, const BaArgs& a, hipStream_t s) {
+    BaArgs ai = a;
+    ai.fused_backsub = 0;   // a replay must not move the landmarks
+    hipLaunchKernelGGL(k_ba_schur, dim3(a.nsplit), dim3(BA_SCHUR_THREADS), 0, s, c, ai);
+}
+
 void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing) {
     // grids sized for the window's maximum (counts live on the device; threads past them exit)
     const int WK = a.W * c.g.K;
@@ -807,13 +836,15 @@ void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming
     hipLaunchKernelGGL(k_ba_tilescan, dim3(1), dim3(64), 0, s, c, a);
     hipLaunchKernelGGL(k_ba_tilescatter, dim3(ntiles), dim3(256), 0, s, c, a);
     hipLaunchKernelGGL(k_ba_camobs, dim3(nb), dim3(256), 0, s, c, a);
+    BaArgs ai = a;
     for (int it = 0; it < a.iters; ++it) {
         const bool rec = timing && timing->used < timing->cap;
+        ai.fused_backsub = it > 0;   // iteration it - 1's landmark update happens inside this Schur pass
         if (rec) (void)hipEventRecord(timing->ev[2 * timing->used], s);
-        hipLaunchKernelGGL(k_ba_schur, dim3(a.nsplit), dim3(BA_SCHUR_THREADS), 0, s, c, a);
+        hipLaunchKernelGGL(k_ba_schur, dim3(a.nsplit), dim3(BA_SCHUR_THREADS), 0, s, c, ai);
         if (rec) (void)hipEventRecord(timing->ev[2 * timing->used++ + 1], s);
         hipLaunchKernelGGL(k_ba_reduce, dim3(64 + (a.n_order * 27 + 3) / 4), dim3(256), 0, s, c, a);
-        hipLaunchKernelGGL(k_ba_solve, dim3(1), dim3(1024), 0, s, c, a);
-        hipLaunchKernelGGL(k_ba_backsub, dim3(16 * nb), dim3(256), 0, s, c, a);
+        hipLaunchKernelGGL(k_ba_solve, dim3(1), dim3(64 * BA_SOLVE_WAVES), 0, s, c, a);
     }
+    hipLaunchKernelGGL(k_ba_backsub, dim3(16 * nb), dim3(256), 0, s, c, a);   // the last iteration's
 }

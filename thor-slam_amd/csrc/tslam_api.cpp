@@ -116,6 +116,7 @@ struct tslam_handle {
     int64_t ba_nkf = 0;
     int64_t ba_last = -1;    // newest frame inserted
     BaTiming ba_timing{};    // k_ba_schur events while profiling is on
+    std::vector<BaArgs> ba_solved;   // per pair: the arguments of its last window solve (replays)
     // BA on its own stream (overlapping the next batch): events and the batch parity
     int64_t batch_idx = 0;
     bool batch_started = false;
@@ -327,6 +328,8 @@ static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const doub
         for (int p = 0; p < h->P; ++p) {
             a.pair = p;
             launch_ba_solve(c, a, s, h->ba_timing.ev ? &h->ba_timing : nullptr);
+            h->ba_solved.resize(h->P);
+            h->ba_solved[p] = a;
         }
     }
 }
@@ -667,6 +670,7 @@ int tslam_reset(tslam_handle* h) {
     for (int i = 0; i < TS_BA_MAXW; ++i) h->ba_frame[i] = -1;
     h->ba_nkf = 0;
     h->ba_last = -1;
+    h->ba_solved.clear();
     if (h->tsdf_on) {   // so does the dense map
         const size_t nv = (size_t)h->tsdf.nx * h->tsdf.ny * h->tsdf.nz;
         HIPCHK(hipMemset(h->tsdf.tsdf, 0, sizeof(float) * nv));
@@ -1623,6 +1627,35 @@ int tslam_ba_read(tslam_handle* h, int pair, int64_t* frames, double* cam_T_worl
         HIPCHK(hipMemcpy(obs_uvd + 2 * WK, b.d + pair * WK, 8 * WK, hipMemcpyDeviceToHost));
     }
     if (counts) HIPCHK(hipMemcpy(counts, b.counts + 4 * pair, 4 * 4, hipMemcpyDeviceToHost));
+    return TSLAM_OK;
+}
+
+int tslam_ba_replay_schur(tslam_handle* h, int pair, int reps, void* stream, double* us_per_launch,
+                          double* flops_per_launch) {
+    if (!h || pair < 0 || pair >= h->P || reps < 1) return fail(TSLAM_EINVAL, "bad argument");
+    if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
+    if ((int)h->ba_solved.size() <= pair) return fail(TSLAM_ESTATE, "no window solved yet");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    const double zero = 0.0;
+    HIPCHK(hipMemcpy(h->ba.flops, &zero, sizeof(double), hipMemcpyHostToDevice));
+    hipStream_t s = (hipStream_t)stream;
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    const BatchCtx c = make_ctx(h);
+    HIPCHK(hipEventRecord(e0, s));
+    for (int r = 0; r < reps; ++r) launch_ba_schur(c, h->ba_solved[pair], s);
+    HIPCHK(hipEventRecord(e1, s));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.0f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    double fl = 0.0;
+    HIPCHK(hipMemcpy(&fl, h->ba.flops, sizeof(double), hipMemcpyDeviceToHost));
+    if (us_per_launch) *us_per_launch = 1e3 * ms / reps;
+    if (flops_per_launch) *flops_per_launch = fl / reps;
     return TSLAM_OK;
 }
 

@@ -68,6 +68,7 @@ struct BaArgs {
     int n_order;                // keyframes in `order`
     int order[TS_BA_MAXW];      // evict: remaining slots; gather/solve: occupied slots, oldest first
     int iters, nsplit;
+    int fused_backsub;          // schur: first apply the previous iteration's landmark back substitution
     double lam, outlier_px;
     const double* fe;           // insert: this batch's front-end pose snapshot [B][P][16]
 };
@@ -118,3 +119,5 @@ struct BaTiming {
     int cap, used;
 };
 void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing);
+// one k_ba_schur launch on the window state `a` (measurement replays)
+void launch_ba_schur(const BatchCtx& c, const BaArgs& a, hipStream_t s);

@@ -135,6 +135,8 @@ _SIGNATURES = {
     "tslam_map_upload": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     "tslam_relocalize": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64] + [ctypes.c_void_p] * 3),
     "tslam_ba_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6),
+    "tslam_ba_replay_schur": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "tslam_ba_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
     "tslam_loop_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
@@ -586,6 +588,13 @@ class Handle:
         w = np.zeros((nz, ny, nx), dtype=np.float32)
         _check(self.lib.tslam_tsdf_read(self.h, t.ctypes.data, w.ctypes.data))
         return t, w
+
+    def ba_replay_schur(self, pair: int = 0, reps: int = 50, stream: int = 0) -> dict:
+        """Average k_ba_schur duration (HIP events around ``reps`` replays) and flops per launch."""
+        us, fl = ctypes.c_double(), ctypes.c_double()
+        _check(self.lib.tslam_ba_replay_schur(self.h, int(pair), int(reps), ctypes.c_void_p(stream), ctypes.byref(us),
+                                              ctypes.byref(fl)))
+        return {"us": us.value, "flops": fl.value, "reps": int(reps)}
 
     def ba_profile(self, max_launches: int = 0) -> dict:
         """Schur-kernel HIP-event time / launches / algorithmic flops since the last call; re-arms
