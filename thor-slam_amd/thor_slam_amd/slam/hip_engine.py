@@ -193,11 +193,11 @@ class HipSlamEngine(SlamEngine):
                                        cfg.tsdf_integrator_max_integration_distance_m, cfg.tsdf_max_weight)
             self._loop = None
             if cfg.enable_loop_closure:
-                if len(self._pairs) == 1:
-                    self._handle.loop_init(cfg.loop_max_keyframes, cfg.loop_signature)
-                    self._loop = _LoopGraph()
-                else:
-                    logger.warning("loop closure runs on single-pair rigs only; disabled for %d pairs", len(self._pairs))
+                # place recognition and loop verification on pair 0's camera; on a multi-pair rig
+                # the keyframe nodes are pair 0's rectified-left poses taken from the rig's body
+                # poses (k_rig_pose), and the pose-graph correction moves the body poses
+                self._handle.loop_init(cfg.loop_max_keyframes, cfg.loop_signature)
+                self._loop = _LoopGraph()
         except RuntimeError:
             raise
         except Exception as exc:  # per interface.py:187-188
