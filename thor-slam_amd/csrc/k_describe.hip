@@ -35,7 +35,7 @@ __device__ __forceinline__ void stage_tile(const uint8_t* level, int W, int H, i
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (wide16) {
         const int per_row = TS_DT_P / 16, n = nrows * per_row;
-        for (int i0 = wave * 64; i0 < n; i0 += 256) {
+        for (int i0 = wave * 64; i0 < n; i0 += TS_DT_THREADS) {
             const int i = i0 + lane;
             if (i < n) {
                 const int r = i / per_row, q = i - r * per_row;
@@ -44,7 +44,7 @@ __device__ __forceinline__ void stage_tile(const uint8_t* level, int W, int H, i
             }
         }
     } else {
-        for (int i = threadIdx.x; i < nrows * TS_DT_P; i += 256) {
+        for (int i = threadIdx.x; i < nrows * TS_DT_P; i += TS_DT_THREADS) {
             const int r = i / TS_DT_P, q = i - r * TS_DT_P;
             const int y = r0 + r, x = c0 + q;
             if (y >= 0 && y < H && x >= 0 && x < W) lds[i] = level[(size_t)y * W + x];
@@ -52,7 +52,7 @@ __device__ __forceinline__ void stage_tile(const uint8_t* level, int W, int H, i
     }
 }
 
-__global__ __launch_bounds__(256) void k_describe(BatchCtx c) {
+__global__ __launch_bounds__(TS_DT_THREADS) void k_describe(BatchCtx c) {
     __shared__ __attribute__((aligned(16))) uint8_t s_raw[TS_DT_RAW_ROWS * TS_DT_P];
     __shared__ __attribute__((aligned(16))) uint8_t s_smo[TS_DT_SMO_ROWS * TS_DT_P];
     __shared__ uint16_t s_list[TS_DT_W * TS_DT_H / 4];   // NMS keeps at most one per 2x2
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void k_describe(BatchCtx c) {
     // padding slots of the level get zero descriptors (first tile of the level does it)
     if (local == 0) {
         const int Kl = c.g.Kq[l];
-        for (int i = kn * 8 + threadIdx.x; i < Kl * 8; i += 256) {
+        for (int i = kn * 8 + threadIdx.x; i < Kl * 8; i += TS_DT_THREADS) {
             desc[(size_t)(c.g.koff[l] + i / 8) * 8 + (i & 7)] = 0u;
             desc_ys[(size_t)(c.g.koff[l] + i / 8) * 8 + (i & 7)] = 0u;
         }
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void k_describe(BatchCtx c) {
 
     // keypoints of the tile: the records of its rows filtered by x, compacted into an LDS list
     // so the 4 waves get equal shares (order is irrelevant: every keypoint is independent)
-    for (int p = pa + threadIdx.x; p < pb; p += 256) {
+    for (int p = pa + threadIdx.x; p < pb; p += TS_DT_THREADS) {
         const int x = ys[p].x & 0xFFFF;
         if (x >= x0 && x < x0 + TS_DT_W) s_list[atomicAdd(&s_n, 1u)] = (uint16_t)p;
     }
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) void k_describe(BatchCtx c) {
     const int n = (int)s_n;
     // groups of TS_DT_G keypoints per wave: all orientations, then all table rows (one exposed
     // latency per group), then the descriptors
-    for (int g0 = wave * TS_DT_G; g0 < n; g0 += 4 * TS_DT_G) {
+    for (int g0 = wave * TS_DT_G; g0 < n; g0 += (TS_DT_THREADS / 64) * TS_DT_G) {
         int bin[TS_DT_G], pos[TS_DT_G];
         uint4 rec[TS_DT_G];
 #pragma unroll
@@ -205,5 +205,5 @@ __global__ __launch_bounds__(256) void k_describe(BatchCtx c) {
 }
 
 void launch_describe(const BatchCtx& c, hipStream_t s) {
-    hipLaunchKernelGGL(k_describe, dim3(xcd_grid(c.n * c.ncam, c.g.dt_total)), dim3(256), 0, s, c);
+    hipLaunchKernelGGL(k_describe, dim3(xcd_grid(c.n * c.ncam, c.g.dt_total)), dim3(TS_DT_THREADS), 0, s, c);
 }

@@ -2,7 +2,15 @@
 #pragma once
 
 #define TS_DT_W 128                         // tile columns
-#define TS_DT_H 32                          // tile rows
+// 128 x 64 tiles on 8 waves: the row halos are staged for 64 rows instead of 32 and the LDS
+// (44 KB) still holds 3 blocks = 6 waves per SIMD (461 -> 446 us per 256-frame batch alone;
+// 128 x 32 on 8 waves 517, 128 x 64 on 4 waves 501)
+#ifndef TS_DT_H
+#define TS_DT_H 64                          // tile rows
+#endif
+#ifndef TS_DT_THREADS
+#define TS_DT_THREADS 512                   // threads per describe block
+#endif
 #define TS_DT_HX 32                         // column halo: >= 18 and keeps 16-byte alignment
 // LDS pitch (and staged width) of both images: 208 = 13 x 16 B.  The 16 extra columns move the
 // rows against the 64 LDS banks: the rotated BRIEF reads of a wave conflict ~2.5-way instead of
