@@ -179,6 +179,40 @@ __device__ __forceinline__ bool is_inlier(const double* R, const double* t, cons
     return zc > 0.0 && e2 < lim;
 }
 
+// The same decision from an f32 evaluation with a rigorous error bound: +1 inlier, 0 outlier,
+// -1 undecided (the exact f64 test decides).  With u = 2^-24, each of xc, yc, zc (three f32
+// FMAs over inputs rounded to f32) is within 5u a (a = the sum of the term magnitudes), ex and ey
+// within 8u (f a_x + |du| a_z), and D = thr2 zc^2 - (ex^2 + ey^2) within
+// 16u [|ex| (fx a_x + |du| a_z) + |ey| (fy a_y + |dv| a_z) + thr2 |zc| a_z + ex^2 + ey^2 + thr2 zc^2]
+// to first order; the test uses twice that, which also covers the second-order terms, the f32
+// evaluation of the bound and the f64 reference's own rounding (~2^-53 of the same sum).  So
+// D > E and zc > E_z mean the f64 test says inlier, D < -E or zc < -E_z outlier.
+struct PoseF32 {
+    float R[9], t[3], aR[9], at[3];
+};
+__device__ __forceinline__ int inlier_f32(const PoseF32& P, const float* c, float fx, float fy, float thr2) {
+    const float X = c[0], Y = c[1], Z = c[2], du = c[3], dv = c[4];
+    const float aX = fabsf(X), aY = fabsf(Y), aZ = fabsf(Z);
+    const float xc = fmaf(P.R[0], X, fmaf(P.R[1], Y, fmaf(P.R[2], Z, P.t[0])));
+    const float yc = fmaf(P.R[3], X, fmaf(P.R[4], Y, fmaf(P.R[5], Z, P.t[1])));
+    const float zc = fmaf(P.R[6], X, fmaf(P.R[7], Y, fmaf(P.R[8], Z, P.t[2])));
+    const float ax = fmaf(P.aR[0], aX, fmaf(P.aR[1], aY, fmaf(P.aR[2], aZ, P.at[0])));
+    const float ay = fmaf(P.aR[3], aX, fmaf(P.aR[4], aY, fmaf(P.aR[5], aZ, P.at[1])));
+    const float az = fmaf(P.aR[6], aX, fmaf(P.aR[7], aY, fmaf(P.aR[8], aZ, P.at[2])));
+    const float ex = fmaf(fx, xc, du * zc);
+    const float ey = fmaf(fy, yc, dv * zc);
+    const float e2 = fmaf(ex, ex, ey * ey);
+    const float lim = thr2 * (zc * zc);
+    const float D = lim - e2;
+    const float adu = fabsf(du), adv = fabsf(dv);
+    const float bsum = fmaf(fabsf(ex), fmaf(fx, ax, adu * az), fmaf(fabsf(ey), fmaf(fy, ay, adv * az), fmaf(thr2 * fabsf(zc), az, e2 + lim)));
+    const float E = bsum * (32.0f / 16777216.0f);
+    const float Ez = az * (32.0f / 16777216.0f);
+    if (zc < -Ez || D < -E) return 0;
+    if (zc > Ez && D > E) return 1;
+    return -1;
+}
+
 // Cholesky solve of H x = g (oracle.solve6); returns false when H is not positive definite.
 __device__ bool solve6(const double* Hm, const double* g, double* x, double* L) {
     for (int j = 0; j < 6; ++j) {
@@ -370,8 +404,9 @@ __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
     for (int i = tid; i < npose; i += POSE_THREADS) s_cnt[i] = 0;
     __syncthreads();
     const double thr2 = c.pp.thr2;
+    const float fxf = (float)fx, fyf = (float)fy, thr2f = (float)thr2;
     for (int c0 = 0; c0 < n; c0 += POSE_THREADS * TS_RS_CPT) {
-        double cx5[TS_RS_CPT][5];
+        float cf[TS_RS_CPT][5];
         bool have[TS_RS_CPT];
 #pragma unroll
         for (int k = 0; k < TS_RS_CPT; ++k) {
@@ -379,20 +414,35 @@ __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
             have[k] = ci < n;
             const double* cr = corr + (size_t)(have[k] ? ci : 0) * TS_CORR_DOUBLES;
 #pragma unroll
-            for (int q = 0; q < 5; ++q) cx5[k][q] = cr[q];
+            for (int q = 0; q < 5; ++q) cf[k][q] = (float)cr[q];
         }
         for (int pi = 0; pi < npose; ++pi) {
             cdouble* ps = chyp + (size_t)pi * 12;
-            double R[9], t[3];
+            if (__builtin_isnan(ps[0])) continue;   // uniform
+            PoseF32 P;
 #pragma unroll
-            for (int k = 0; k < 9; ++k) R[k] = ps[k];
-            t[0] = ps[9]; t[1] = ps[10]; t[2] = ps[11];
-            if (__builtin_isnan(R[0])) continue;   // uniform
+            for (int k = 0; k < 9; ++k) {
+                P.R[k] = (float)ps[k];
+                P.aR[k] = fabsf(P.R[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                P.t[k] = (float)ps[9 + k];
+                P.at[k] = fabsf(P.t[k]);
+            }
             int cnt = 0;
 #pragma unroll
             for (int k = 0; k < TS_RS_CPT; ++k) {
-                const bool in = have[k] && is_inlier(R, t, cx5[k], fx, fy, thr2);
-                cnt += __popcll(__ballot(in));
+                int v = have[k] ? inlier_f32(P, cf[k], fxf, fyf, thr2f) : 0;
+                if (v < 0) {   // near the threshold: the exact f64 test (rare, divergent)
+                    double R[9], t[3];
+                    const double* cr = corr + (size_t)(c0 + k * POSE_THREADS + tid) * TS_CORR_DOUBLES;
+#pragma unroll
+                    for (int q = 0; q < 9; ++q) R[q] = ps[q];
+                    t[0] = ps[9]; t[1] = ps[10]; t[2] = ps[11];
+                    v = is_inlier(R, t, cr, fx, fy, thr2) ? 1 : 0;
+                }
+                cnt += __popcll(__ballot(v != 0));
             }
             if (lane == 0 && cnt) atomicAdd(&s_cnt[pi], cnt);
         }
@@ -503,10 +553,9 @@ __global__ __launch_bounds__(POSE_THREADS) void k_refine(BatchCtx c, int S) {
             acc[27] += rx * rx + ry * ry;
             acc[28] += 1.0;
         }
-#pragma unroll
-        for (int k = 0; k < N_ACC; ++k) {
-            const double w = wave_sum_f64(acc[k]);
-            if (lane == 0) s_red[wave][k] = w;
+        {
+            const double w = wave_multi_sum(acc);   // the sum of acc[lane >> 1]
+            if ((lane & 1) == 0 && (lane >> 1) < N_ACC) s_red[wave][lane >> 1] = w;
         }
         __syncthreads();
         if (tid == 0) {
@@ -840,10 +889,9 @@ __global__ __launch_bounds__(POSE_THREADS) void k_rig_pose(BatchCtx c) {
                 acc[28] += 1.0;
             }
         }
-#pragma unroll
-        for (int k = 0; k < N_ACC; ++k) {
-            const double w = wave_sum_f64(acc[k]);
-            if (lane == 0) s_red[wave][k] = w;
+        {
+            const double w = wave_multi_sum(acc);   // the sum of acc[lane >> 1]
+            if ((lane & 1) == 0 && (lane >> 1) < N_ACC) s_red[wave][lane >> 1] = w;
         }
         __syncthreads();
         if (tid == 0) {

@@ -284,6 +284,32 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
     return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
 }
 
+// Wave sums of N <= 32 f64 values at once (a transposing butterfly): at the exchange with lane
+// distance d = 32, 16, .., 2 every lane keeps half of its values (the upper half when lane & d)
+// and adds its partner's copy of that half, so value k ends in lanes 2k and 2k + 1 after a last
+// exchange at distance 1.  31 shuffles for 32 values instead of 32 separate reductions; a fixed
+// order, so deterministic.  Returns the sum of value lane >> 1 (lanes past 2N hold zeros).
+template <int N>
+__device__ __forceinline__ double wave_multi_sum(const double (&in)[N]) {
+    static_assert(N <= 32, "at most 32 values");
+    double v[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) v[k] = k < N ? in[k] : 0.0;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int h = 16; h >= 1; h >>= 1) {   // values per lane after this exchange
+        const int d = 2 * h;              // lane distance 32, 16, 8, 4, 2
+        const bool upper = (lane & d) != 0;
+#pragma unroll
+        for (int j = 0; j < h; ++j) {
+            const double keep = upper ? v[h + j] : v[j];
+            const double send = upper ? v[j] : v[h + j];
+            v[j] = keep + __shfl_xor(send, d, 64);
+        }
+    }
+    return v[0] + __shfl_xor(v[0], 1, 64);
+}
+
 // XCD-aware 1-D block mapping: blocks are dealt round-robin over the 8 XCDs, so block b runs on the
 // XCD labelled b % 8.  Give all `bpi` blocks of one image the same label, so that image's pyramid
 // lines are fetched into one L2 only.  Speed only: correctness never depends on placement.
