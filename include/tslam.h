@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 8
+#define TSLAM_ABI_VERSION 9
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -302,6 +302,24 @@ int tslam_import_raw(tslam_handle* h, const uint8_t* images, int64_t first_frame
  * of this rank's frame range of the current batch -> dst; all n frames <- src (frame order). */
 int tslam_pack_poses(tslam_handle* h, void* dst, void* stream);
 int tslam_unpack_poses(tslam_handle* h, const void* src, void* stream);
+
+/* Multi-GPU without a host framework (tslam_comm_init): the sharded rig above,
+ * driven by the library over RCCL (librccl, ncclSend / ncclRecv / ncclAllGather on xGMI).
+ * tslam_comm_unique_id: a fresh ncclUniqueId (128 bytes); rank 0 makes it and hands it to the
+ *   other ranks over the host's own channel.
+ * tslam_comm_init: this handle (the whole rig: tslam_create_rig, or tslam_create + tslam_set_rig)
+ *   joins the `world`-rank communicator as `rank` (one rank per GPU, the handle's device) and owns
+ *   cameras [rank*C/world, (rank+1)*C/world) and batch frames [rank*B/world, (rank+1)*B/world)
+ *   (C and max_batch divisible by world; stereo rigs without local BA).
+ * tslam_submit_sharded: one batch of max_batch frames of this rank's cameras ([B][C/world][H][W]
+ *   u8 in HBM) on `stream`: front end of its cameras; raw images + stream blocks of the frames
+ *   every other rank solves sent point to point; back end (+ rig pose) of its frame range; pose
+ *   records all-gathered; the chain.  Every rank then reads the whole rig's poses with
+ *   tslam_read_poses / tslam_read_rig_poses, identical to one handle fed all cameras.  The
+ *   collectives are on `stream` after the kernels (nothing synchronises the host). */
+int tslam_comm_unique_id(void* id128);
+int tslam_comm_init(tslam_handle* h, const void* id128, int rank, int world);
+int tslam_submit_sharded(tslam_handle* h, const uint8_t* images, void* stream);
 
 /* A8 window of stereo pair `pair` after the last enqueued solve (synchronises the device),
  * indexed by slot (slot = keyframe number mod ba_window): frames[W] (global frame, -1 = empty),

@@ -113,3 +113,29 @@ def test_dist_shard_gloo_two_processes(tmp_path):
             for part in ("pairs", "rig"):
                 for k in ("T_rel", "T_abs", "stats"):
                     np.testing.assert_array_equal(np.array(got[b][part][k]), want[b][part][k], err_msg=f"{r} {b} {part}.{k}")
+
+
+def test_rccl_driven_shard_world_one_identical():
+    """The library's own RCCL driver (tslam_comm_init + tslam_submit_sharded) on a
+    1-rank communicator: the sharded stage runner over the whole range, the pose-record pack /
+    ncclAllGather / unpack and the chain must reproduce the unsharded handle bit for bit (more
+    ranks need more GPUs than the test box has: RCCL refuses two ranks on one device)."""
+    import torch
+
+    from thor_slam_amd._lib import Handle, comm_unique_id
+
+    sc = rig_scene(names=TWO, n=12)
+    cfg = HipSlamConfig()
+    batch, nb = 4, 3
+    want, _ = unsharded(sc, cfg, batch, nb)
+    h = Handle(sc["rects"], cfg, max_batch=batch)
+    h.set_rig(sc["E"])
+    h.comm_init(comm_unique_id(), 0, 1)
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    for b in range(nb):
+        h.submit_sharded(dev[b * batch].data_ptr(), s)
+        got = {"pairs": h.read_poses(batch), "rig": h.read_rig_poses(batch)}
+        assert_identical(got, want[b])
+    assert (want[-1]["rig"]["stats"][:, 0] == 0).all()
+    h.close()

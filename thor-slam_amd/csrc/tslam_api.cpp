@@ -4,6 +4,7 @@
 // caller's stream.  The launch functions never allocate, copy synchronously or synchronise, so
 // a batch can be captured into a hipGraph by the caller.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -133,6 +134,12 @@ struct tslam_handle {
     // sharded rig (tslam_set_shard): front-end cameras [sh_cam_lo, sh_cam_hi) and back-end frames
     // [rank * n / world, (rank + 1) * n / world) of every batch
     int sh_cam_lo = 0, sh_cam_hi = 0, sh_rank = 0, sh_world = 1;
+    // RCCL-driven sharding (tslam_comm_init / tslam_submit_sharded): the communicator and the
+    // exchange buffers of this rank (device), the previous batch's last frame of its cameras
+    bool sh_comm = false;
+    ncclComm_t comm = nullptr;
+    uint8_t *x_raw_send = nullptr, *x_raw_recv = nullptr, *x_feat_send = nullptr, *x_feat_recv = nullptr;
+    uint8_t *x_pose_send = nullptr, *x_pose_recv = nullptr, *x_prev_raw = nullptr;
     // asynchronous host boundary (tslam_submit_host / tslam_poll_*): the handle's own front/back
     // streams, pinned staging + device input per batch parity, pinned result slots per parity
     hipStream_t as_front = nullptr, as_back = nullptr;
@@ -179,6 +186,10 @@ static int dev_realloc(tslam_handle* h, void** p, size_t bytes) {
 }
 
 static void free_all(tslam_handle* h) {
+    if (h->comm) {
+        (void)ncclCommDestroy(h->comm);
+        h->comm = nullptr;
+    }
     for (void* p : h->allocs) (void)hipFree(p);
     h->allocs.clear();
     for (void* p : h->host_allocs) (void)hipHostFree(p);
@@ -727,7 +738,7 @@ static int ensure_async(tslam_handle* h) {
 int tslam_submit_host(tslam_handle* h, const uint8_t* host_images, const double* timestamps, int n_frames) {
     if (!h || !host_images) return fail(TSLAM_EINVAL, "bad argument");
     if (n_frames < 1 || n_frames > h->B) return fail(TSLAM_EINVAL, "n_frames must be in [1, max_batch]");
-    if (h->sh_world > 1) return fail(TSLAM_ESTATE, "a sharded handle is driven stage by stage");
+    if (h->sh_world > 1 || h->sh_comm) return fail(TSLAM_ESTATE, "a sharded handle is driven stage by stage");
     HIPCHK(hipSetDevice(h->device));
     int rc = ensure_async(h);
     if (rc != TSLAM_OK) return rc;
@@ -912,7 +923,7 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
         return fail(TSLAM_ESTATE, "all back stages of a batch must use one stream");
     if (stage != TSLAM_STAGE_BA) h->last_stream = s;
     const BatchCtx c = make_ctx(h);
-    if (h->sh_world > 1) return run_sharded_stage(h, c, stage, s);
+    if (h->sh_world > 1 || h->sh_comm) return run_sharded_stage(h, c, stage, s);
     if (h->prm.rgbd && (stage == TSLAM_STAGE_RECTIFY || stage == TSLAM_STAGE_ALL || stage == TSLAM_KERNEL_RECTIFY_PYRAMID))
         launch_rgbd_gray(c, h->d_gray, s);   // the colour images become the gray input of rectify
     switch (stage) {
@@ -1179,6 +1190,123 @@ int tslam_set_shard(tslam_handle* h, int cam_lo, int cam_hi, int rank, int world
     h->sh_rank = rank;
     h->sh_world = world;
     return TSLAM_OK;
+}
+
+int tslam_comm_unique_id(void* id128) {
+    if (!id128) return fail(TSLAM_EINVAL, "null id");
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+    ncclUniqueId id;
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(TSLAM_EHIP, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    memcpy(id128, &id, sizeof(id));
+    return TSLAM_OK;
+}
+
+int tslam_comm_init(tslam_handle* h, const void* id128, int rank, int world) {
+    if (!h || !id128) return fail(TSLAM_EINVAL, "bad argument");
+    if (h->comm) return fail(TSLAM_ESTATE, "communicator already set");
+    if (world < 1 || rank < 0 || rank >= world) return fail(TSLAM_EINVAL, "need 0 <= rank < world");
+    if (h->C % world || h->B % world) return fail(TSLAM_EINVAL, "cameras and max_batch must divide by world");
+    const int S = h->C / world;
+    int rc = tslam_set_shard(h, rank * S, (rank + 1) * S, rank, world);
+    if (rc != TSLAM_OK) return rc;
+    if (h->prm.rgbd || h->prm.ba_window) return fail(TSLAM_EINVAL, "sharding covers stereo rigs without local BA");
+    HIPCHK(hipSetDevice(h->device));
+    ncclUniqueId id;
+    memcpy(&id, id128, sizeof(id));
+    const ncclResult_t r = ncclCommInitRank(&h->comm, world, id, rank);
+    if (r != ncclSuccess) {
+        h->comm = nullptr;
+        return fail(TSLAM_EHIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    const size_t nr = (size_t)h->B / world + 1, img = (size_t)h->W * h->H;
+    const size_t blk = (size_t)stream_block_bytes(h->g), rec = (size_t)pose_record_bytes(h->P);
+    const size_t fpr = (size_t)h->B / world;
+    struct A {
+        uint8_t** p;
+        size_t bytes;
+    } list[] = {{&h->x_raw_send, world * nr * S * img}, {&h->x_raw_recv, world * nr * S * img},
+                {&h->x_feat_send, world * nr * S * blk}, {&h->x_feat_recv, world * nr * S * blk},
+                {&h->x_pose_send, fpr * rec},           {&h->x_pose_recv, world * fpr * rec},
+                {&h->x_prev_raw, S * img}};
+    for (const A& a : list) {
+        rc = dev_alloc(h, (void**)a.p, a.bytes);
+        if (rc != TSLAM_OK) return rc;
+    }
+    h->sh_comm = true;
+    return TSLAM_OK;
+}
+
+#define NCCLCHK(expr)                                                                        \
+    do {                                                                                     \
+        ncclResult_t r__ = (expr);                                                           \
+        if (r__ != ncclSuccess) return fail(TSLAM_EHIP, std::string(#expr) + ": " + ncclGetErrorString(r__)); \
+    } while (0)
+
+// One batch of a rank of an RCCL-sharded rig, on `stream`: the same phases as the Python driver
+// (thor_slam_amd/shard.py RankShard): raw images + stream blocks of the rank's cameras to every
+// other rank for the frames that rank solves (its range and the frame before), the back end of
+// the rank's own range, the pose records all-gathered, the chain.
+int tslam_submit_sharded(tslam_handle* h, const uint8_t* images, void* stream) {
+    if (!h || !images) return fail(TSLAM_EINVAL, "bad argument");
+    if (!h->sh_comm) return fail(TSLAM_ESTATE, "tslam_comm_init first");
+    HIPCHK(hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    const int N = h->sh_world, me = h->sh_rank, B = h->B, S = h->sh_cam_hi - h->sh_cam_lo;
+    const size_t fpr = (size_t)B / N, nr = fpr + 1, img = (size_t)h->W * h->H;
+    const size_t blk = (size_t)stream_block_bytes(h->g), rec = (size_t)pose_record_bytes(h->P);
+    const size_t raw_q = nr * S * img, feat_q = nr * S * blk;   // bytes per destination
+    const int64_t g0 = h->frames_done;
+    int rc = tslam_begin_batch(h, images, B);
+    if (rc != TSLAM_OK) return rc;
+    // raw images for every destination: its frames lo-1 .. hi-1 of this rank's cameras
+    for (int q = 0; q < N; ++q) {
+        if (q == me) continue;
+        const int lo = (int)(q * fpr);
+        uint8_t* out = h->x_raw_send + q * raw_q;
+        const uint8_t* first = lo == 0 ? h->x_prev_raw : images + (size_t)(lo - 1) * S * img;
+        HIPCHK(hipMemcpyAsync(out, first, S * img, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(out + S * img, images + (size_t)lo * S * img, fpr * S * img, hipMemcpyDeviceToDevice, s));
+    }
+    HIPCHK(hipMemcpyAsync(h->x_prev_raw, images + (size_t)(B - 1) * S * img, S * img, hipMemcpyDeviceToDevice, s));
+    // front end of this rank's cameras, then their stream blocks per destination
+    const int front[3] = {TSLAM_STAGE_RECTIFY, TSLAM_STAGE_DETECT, TSLAM_STAGE_DESCRIBE};
+    for (int st : front)
+        if ((rc = tslam_run_stage(h, st, s)) != TSLAM_OK) return rc;
+    for (int q = 0; q < N; ++q) {
+        if (q == me) continue;
+        rc = tslam_pack_streams(h, g0 + (int64_t)q * fpr - 1, (int)nr, h->sh_cam_lo, h->sh_cam_hi,
+                                h->x_feat_send + q * feat_q, s);
+        if (rc != TSLAM_OK) return rc;
+    }
+    // exchange 1: point-to-point all-to-all of raw images and stream blocks
+    if (N > 1) {
+        NCCLCHK(ncclGroupStart());
+        for (int q = 0; q < N; ++q) {
+            if (q == me) continue;
+            NCCLCHK(ncclSend(h->x_raw_send + q * raw_q, raw_q, ncclUint8, q, h->comm, s));
+            NCCLCHK(ncclRecv(h->x_raw_recv + q * raw_q, raw_q, ncclUint8, q, h->comm, s));
+            NCCLCHK(ncclSend(h->x_feat_send + q * feat_q, feat_q, ncclUint8, q, h->comm, s));
+            NCCLCHK(ncclRecv(h->x_feat_recv + q * feat_q, feat_q, ncclUint8, q, h->comm, s));
+        }
+        NCCLCHK(ncclGroupEnd());
+    }
+    // the other ranks' cameras of frames lo-1 .. hi-1 of this rank's range into the ring
+    const int64_t first = g0 + (int64_t)me * fpr - 1;
+    for (int q = 0; q < N; ++q) {
+        if (q == me) continue;
+        const int c0 = q * S, c1 = (q + 1) * S;
+        if ((rc = tslam_import_raw(h, h->x_raw_recv + q * raw_q, first, (int)nr, c0, c1, s)) != TSLAM_OK) return rc;
+        if ((rc = tslam_unpack_streams(h, first, (int)nr, c0, c1, h->x_feat_recv + q * feat_q, s)) != TSLAM_OK) return rc;
+    }
+    // back end of this rank's frames, exchange 2 (pose records), the chain on every rank
+    if ((rc = tslam_run_stage(h, TSLAM_STAGE_MATCH, s)) != TSLAM_OK) return rc;
+    if ((rc = tslam_run_stage(h, TSLAM_STAGE_POSE, s)) != TSLAM_OK) return rc;
+    if ((rc = tslam_pack_poses(h, h->x_pose_send, s)) != TSLAM_OK) return rc;
+    NCCLCHK(ncclAllGather(h->x_pose_send, h->x_pose_recv, fpr * rec, ncclUint8, h->comm, s));
+    if ((rc = tslam_unpack_poses(h, h->x_pose_recv, s)) != TSLAM_OK) return rc;
+    if ((rc = tslam_run_stage(h, TSLAM_KERNEL_CHAIN, s)) != TSLAM_OK) return rc;
+    return tslam_end_batch(h);
 }
 
 int tslam_exchange_sizes(tslam_handle* h, int64_t* stream_block, int64_t* pose_record) {

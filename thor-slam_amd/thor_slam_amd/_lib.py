@@ -89,6 +89,9 @@ _SIGNATURES = {
     "tslam_abi_version": (ctypes.c_int, []),
     "tslam_create": (ctypes.c_int, [ctypes.POINTER(StereoDesc), ctypes.POINTER(Params), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "tslam_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "tslam_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "tslam_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "tslam_submit_sharded": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_create_rig": (ctypes.c_int, [ctypes.POINTER(CameraDesc), ctypes.c_int, ctypes.POINTER(Params), ctypes.c_int,
                                          ctypes.POINTER(ctypes.c_void_p)]),
     "tslam_rig_pairs": (ctypes.c_int, [ctypes.POINTER(CameraDesc), ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
@@ -232,6 +235,13 @@ def native_rectify_pair(left, right=None, rgbd: bool = False) -> dict:
     return {"width": desc.width, "height": desc.height, "fx": desc.fx, "fy": desc.fy, "cx": desc.cx, "cy": desc.cy,
             "baseline": desc.baseline, "map_left": ml, "map_right": mr, "base_T_rect": base,
             "rect_left": rot[0], "rect_right": rot[1]}
+
+
+def comm_unique_id() -> bytes:
+    """``tslam_comm_unique_id``: a fresh RCCL unique id (128 bytes) for ``Handle.comm_init``."""
+    buf = (ctypes.c_uint8 * 128)()
+    _check(load_library().tslam_comm_unique_id(buf))
+    return bytes(buf)
 
 
 class Handle:
@@ -427,6 +437,15 @@ class Handle:
         return {"T": T, "cov": cov, "timestamp": ts.value, "state": st.value, "confidence": conf.value}
 
     # -- sharded rig (thor_slam_amd/shard.py drives these) --------------------
+    def comm_init(self, unique_id: bytes, rank: int, world: int) -> None:
+        """``tslam_comm_init``: join an RCCL communicator and own this rank's shard of the rig."""
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
+        _check(self.lib.tslam_comm_init(self.h, buf, int(rank), int(world)))
+
+    def submit_sharded(self, images_dev_ptr: int, stream: int = 0) -> None:
+        """``tslam_submit_sharded``: one batch of this rank's cameras, exchanges over RCCL."""
+        _check(self.lib.tslam_submit_sharded(self.h, ctypes.c_void_p(images_dev_ptr), ctypes.c_void_p(stream)))
+
     def set_shard(self, cam_lo: int, cam_hi: int, rank: int, world: int) -> None:
         _check(self.lib.tslam_set_shard(self.h, int(cam_lo), int(cam_hi), int(rank), int(world)))
 
