@@ -262,3 +262,39 @@ def test_speculative_fast_threshold_fallback_is_exact():
     # the low-contrast frames really have fewer strong corners than the learnt threshold admits
     assert min(ora[2]["cur"]["left"]["kp"]["score"][ora[2]["cur"]["left"]["valid"]]) < 40
     h.close()
+
+
+@pytest.mark.slow
+def test_c1_sequence_100_frames():
+    """Config C1 (BASELINE.json configs[0]): the 100-frame 640x400 sequence end to end, in ragged
+    batches of 32 (32, 32, 32, 4), against the oracle run frame by frame.  Every frame's keypoint
+    counts, match and correspondence counts, RANSAC winner and inlier count are identical, and the
+    chained absolute pose stays within 1e-9 relative Frobenius of the oracle's over the whole
+    sequence (association or chaining drift would show up here, not in the 4-frame tests)."""
+    n = 100
+    sc, per = hip_run(seed=5, batch=32, n=n)
+    n_tracked = 0
+    for i, rec in enumerate(per):
+        o = sc["oracle"][i]
+        for cam, side in enumerate(("left", "right")):
+            np.testing.assert_array_equal(rec["kp"][cam]["counts"], np.array(o["cur"][side]["counts"]),
+                                          err_msg=f"frame {i} {side} counts")
+        valid = o["cur"]["left"]["valid"]
+        for k in ("x", "y", "angle"):
+            np.testing.assert_array_equal(rec["kp"][0][k][valid], o["cur"]["left"]["kp"][k][valid],
+                                          err_msg=f"frame {i} left {k}")
+        np.testing.assert_array_equal(rec["kp"][0]["desc"][valid], o["cur"]["left"]["desc"][valid],
+                                      err_msg=f"frame {i} left descriptors")
+        st = rec["stats"]
+        if i == 0:
+            assert st[0] == 2
+            continue
+        assert st[0] == o["status"], f"frame {i}: status {st[0]} vs {o['status']}"
+        assert st[1] == o["n_corr"], f"frame {i}: n_corr {st[1]} vs {o['n_corr']}"
+        if o["status"] == 0:
+            n_tracked += 1
+            assert st[4] == o["best_hyp"] and st[3] == o["best_count"], f"frame {i}: RANSAC winner differs"
+            assert st[2] == o["n_inliers"], f"frame {i}: inliers {st[2]} vs {o['n_inliers']}"
+            assert rel_frobenius(rec["T_rel"], o["T"]) < 1e-9, f"frame {i}: T_rel"
+        assert rel_frobenius(rec["T_abs"], o["world_T_cam"]) < 1e-9, f"frame {i}: T_abs"
+    assert n_tracked >= 90, f"only {n_tracked} of {n - 1} frames tracked"
