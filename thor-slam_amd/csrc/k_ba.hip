@@ -5,22 +5,21 @@
 // complement on the cameras, Gauss-Newton with Levenberg damping, gauge = oldest keyframe).
 //
 // Per window solve: k_ba_gate gates the observations at the current estimate and counts them per
-// landmark; a tiled scan (k_ba_tilecount / tilescan / tilescatter) keeps landmarks seen >= 2 times,
-// ranks them (compact index) and builds the observation list; k_ba_camobs the camera x landmark
-// table of observation indices.
+// landmark; a tiled scan (k_ba_tilecount, k_ba_tilescatter) keeps landmarks seen >= 2 times,
+// ranks them (compact index) and builds the observation list; k_ba_camobs scatters the camera x
+// landmark table and k_ba_slots turns it into the dense (landmark, camera) slot table that every
+// iteration reads with one level of indexing (and resets the scratch for the next solve).
 // Then per Gauss-Newton iteration:
-//   k_ba_jac     one thread per observation: J_c, J_p, r -> W_o = J_c^T J_p, J_c^T J_c | J_c^T r,
-//                J_p^T J_p | J_p^T r;
-//   k_ba_camred  one wave per (camera, element): U_c = sum J_c^T J_c, g_c = sum J_c^T r;
-//   k_ba_schur   per chunk of 32 landmarks: V_i = sum J_p^T J_p + lam I, g_p,i, L_i = chol(V_i),
-//                y_i = L_i^-1 g_p,i; the chunk's Schur columns Q_i = [W_o L_i^-T] (rows of the
-//                observing camera) with y_i in row 60 in an LDS tile; C += Q^T Q on the FP64
-//                matrix cores (v_mfma_f64_16x16x4f64).  C[0:60,0:60] = sum_i W V^-1 W^T and
-//                C[0:60, 60] = sum_i W V^-1 g_p; blocks stride the chunks (split-K partials);
-//   k_ba_reduce  fixed-order sum of the split partials;
+//   k_ba_schur   per chunk of 32 landmarks: the previous iteration's landmark update (fused back
+//                substitution), then J_c, J_p, r per observation -> W_o, J_c^T J_c | J_c^T r;
+//                V_i = sum J_p^T J_p + lam I, g_p,i, L_i = chol(V_i), y_i = L_i^-1 g_p,i; the
+//                chunk's Schur columns Q_i = [W_o L_i^-T] (rows of the observing camera) with y_i
+//                in row 60 in an LDS tile; C += Q^T Q on the FP64 matrix cores
+//                (v_mfma_f64_16x16x4f64), blocks striding the chunks (split-K partials);
+//   k_ba_reduce  fixed-order sum of the split partials, and the camera blocks U_c, g_c;
 //   k_ba_solve   one block: S = blockdiag(U + lam) - C, b = -g_c + C[:,60] without camera 0,
-//                LDL^T elimination + back substitution, camera updates (Cayley);
-//   k_ba_backsub 16 lanes per landmark: dp = V^-1 (-g_p - sum W_o^T dc), X += dp.
+//                blocked LDL^T + back substitution, camera updates (Cayley);
+// and after the last one k_ba_backsub: dp = V^-1 (-g_p - sum W_o^T dc), X = Xc + dp.
 // Every reduction has a fixed order, so a solve is deterministic run to run.  Floating-point
 // results differ from the oracle's (LU solves, numpy summation order) at the 1e-14 level.
 #include "tslam_ba.h"
@@ -123,6 +122,7 @@ __global__ __launch_bounds__(256) void k_ba_insert(BatchCtx c, BaArgs a) {
     const PairCalib cal = c.calib[p];
     const double* disp = c.disp + ((size_t)rslot * c.P + p) * K;
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x) {
+        q.remap[k] = 0x7F7F7F7F;   // for the next eviction (k_ba_evict_* have run)
         double u = __builtin_nan(""), v = __builtin_nan("");
         const bool valid = kp_obs(c, rslot, c.cpp * p, k, &u, &v);
         const double dd = disp[k];
@@ -221,8 +221,8 @@ __global__ __launch_bounds__(256) void k_ba_gate(BatchCtx c, BaArgs a) {
 //   landmark tiles over the ids (flag: >= 2 gated observations) -> compact index li = rank of the
 //   id, lm_id = its inverse;  observation tiles per window camera over its keypoints (flag: gated
 //   and its landmark kept) -> the observation list in (camera, keypoint) order.
-// k_ba_tilecount counts every tile, k_ba_tilescan scans the counts (one block), k_ba_tilescatter
-// writes, k_ba_camobs fills the camera x landmark table.
+// k_ba_tilecount counts every tile, k_ba_tilescatter scans the counts and writes, k_ba_camobs
+// fills the camera x landmark table.
 #define BA_TILE (256 * BA_SCAN_ITEMS)
 
 struct BaTiles {
@@ -279,40 +279,38 @@ __global__ __launch_bounds__(256) void k_ba_tilecount(BatchCtx c, BaArgs a) {
     if (threadIdx.x == 0) q.tiles[blockIdx.x] = tot;
 }
 
-__global__ __launch_bounds__(64) void k_ba_tilescan(BatchCtx c, BaArgs a) {
-    BaPair q = ba_pair(c, a, a.pair);
-    const BaTiles t = ba_tiles(c, a);
-    if (threadIdx.x != 0) return;
-    int run = 0;
-    for (int b = 0; b < t.n_lm_tiles; ++b) {
-        const int v = q.tiles[b];
-        q.tiles[TS_BA_TILES + b] = run;
-        run += v;
-    }
-    q.counts[1] = run;
-    run = 0;
-    for (int ci = 0; ci < a.n_order; ++ci) {
-        q.cam_off[ci] = run;
-        for (int tt = 0; tt < t.per_cam; ++tt) {
-            const int b = t.n_lm_tiles + ci * t.per_cam + tt;
-            const int v = q.tiles[b];
-            q.tiles[TS_BA_TILES + b] = run;
-            run += v;
-        }
-    }
-    q.cam_off[a.n_order] = run;
-    q.counts[0] = run;
-}
-
+// Scatter after the tile counts; each block takes its tile's offset from the counts of the tiles
+// before it (landmark tiles and observation tiles are scanned separately), and block 0 also
+// publishes the totals and the per-camera observation ranges (no separate scan launch).
 __global__ __launch_bounds__(256) void k_ba_tilescatter(BatchCtx c, BaArgs a) {
     __shared__ int s_tmp[32];
+    __shared__ int s_cnt[TS_BA_TILES];
     BaPair q = ba_pair(c, a, a.pair);
+    const BaTiles t = ba_tiles(c, a);
+    const int ntiles = t.n_lm_tiles + a.n_order * t.per_cam;
+    for (int j = threadIdx.x; j < ntiles; j += blockDim.x) s_cnt[j] = q.tiles[j];
     int fl[BA_SCAN_ITEMS], ids[BA_SCAN_ITEMS], ci, k0, cnt = 0;
     ba_tile_flags(c, a, q, blockIdx.x, fl, ids, &ci, &k0);
 #pragma unroll
     for (int it = 0; it < BA_SCAN_ITEMS; ++it) cnt += fl[it];
     int tot;
-    int pos = q.tiles[TS_BA_TILES + blockIdx.x] + block_scan_excl(cnt, s_tmp, &tot);
+    const int within = block_scan_excl(cnt, s_tmp, &tot);   // its barriers order the s_cnt stores
+    const int first = (int)blockIdx.x < t.n_lm_tiles ? 0 : t.n_lm_tiles;
+    int base = 0;
+    for (int j = first; j < (int)blockIdx.x; ++j) base += s_cnt[j];   // LDS broadcast reads
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        int run = 0;
+        for (int b = 0; b < t.n_lm_tiles; ++b) run += s_cnt[b];
+        q.counts[1] = run;
+        run = 0;
+        for (int cc = 0; cc < a.n_order; ++cc) {
+            q.cam_off[cc] = run;
+            for (int tt = 0; tt < t.per_cam; ++tt) run += s_cnt[t.n_lm_tiles + cc * t.per_cam + tt];
+        }
+        q.cam_off[a.n_order] = run;
+        q.counts[0] = run;
+    }
+    int pos = base + within;
     if (ci < 0) {
         const int NID = a.W * c.g.K;
 #pragma unroll
@@ -337,6 +335,39 @@ __global__ __launch_bounds__(256) void k_ba_camobs(BatchCtx c, BaArgs a) {
     const int o = blockIdx.x * blockDim.x + threadIdx.x;
     if (o >= q.counts[0]) return;
     q.camobs[(size_t)q.obs_cam[o] * a.W * c.g.K + q.li[q.obs_id[o]]] = o;
+}
+
+// The solve's dense slot table: slot s = r * TS_BA_MAXW + ci of compact landmark r and window
+// camera ci gets its observation index (or -1) and (u, v, d); Xc[r] = X[lm_id[r]].  Resets the
+// camobs entries it reads and the gate counts, so neither needs a memset before the next solve.
+__global__ __launch_bounds__(256) void k_ba_slots(BatchCtx c, BaArgs a) {
+    BaPair q = ba_pair(c, a, a.pair);
+    const int K = c.g.K, WK = a.W * K;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < WK) q.cnt[t] = 0;   // read by the tile kernels only, which have run
+    const int L = q.counts[1];
+    const int r = t / TS_BA_MAXW, ci = t - r * TS_BA_MAXW;
+    if (r >= L) return;
+    int o = -1;
+    if (ci < a.n_order) {
+        int32_t* e = q.camobs + (size_t)ci * WK + r;
+        o = *e;
+        if (o >= 0) *e = -1;
+    }
+    q.lo_o[t] = o;
+    if (o >= 0) {
+        const size_t so = (size_t)a.order[ci] * K + q.obs_k[o];
+        double* uvd = q.lo_uvd + (size_t)t * 4;
+        uvd[0] = q.u[so];
+        uvd[1] = q.v[so];
+        uvd[2] = q.d[so];
+        uvd[3] = 0.0;
+    }
+    if (ci == 0) {
+        const int id = q.lm_id[r];
+#pragma unroll
+        for (int e = 0; e < 3; ++e) q.Xc[(size_t)r * 3 + e] = q.X[(size_t)id * 3 + e];
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -388,6 +419,12 @@ __device__ void ba_camred_wave(const BaPair& q, int WK, int ci, int e, int lane)
 }
 
 typedef double d4v __attribute__((ext_vector_type(4)));
+
+// Workgroup barrier ordering LDS only: waits for this wave's LDS operations, not for its HBM
+// stores (a __syncthreads() would wait for those too), so stores drain behind the barrier.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 #define BA_CHUNK 32          // landmarks per LDS tile (96 Schur columns)
 #define BA_QPITCH 80         // doubles per tile column: 160 dwords = 32 mod 64 banks, so the four
                              // columns one MFMA operand read touches fall in disjoint bank halves
@@ -405,12 +442,12 @@ typedef double d4v __attribute__((ext_vector_type(4)));
 // Blocks stride the chunks; each block that had a chunk writes its 64 x 64 partial.
 __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArgs a) {
     __shared__ double s_Q[3 * BA_CHUNK * BA_QPITCH];
-    __shared__ double s_W[BA_CHUNK][TS_BA_MAXW][18];
     __shared__ double s_Vg[BA_CHUNK][TS_BA_MAXW][9];
     __shared__ int s_has[BA_CHUNK][TS_BA_MAXW];
     __shared__ double s_L[BA_CHUNK][6];
     __shared__ double s_T[TS_BA_MAXW][12];
     __shared__ double s_bs[BA_CHUNK][TS_BA_MAXW][3];
+    __shared__ double s_X[BA_CHUNK][3];
     const int K = c.g.K, WK = a.W * K, n = a.n_order;
     BaPair q = ba_pair(c, a, a.pair);
     const int L = q.counts[1];
@@ -423,78 +460,109 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
     const bool bsub = a.fused_backsub && q.counts[2];   // the previous solve succeeded
     for (int l0 = blockIdx.x * BA_CHUNK; l0 < L; l0 += gridDim.x * BA_CHUNK) {
         const int nl = min(BA_CHUNK, L - l0);
-        __syncthreads();
-        // 0. the previous iteration's landmark update for the chunk (what k_ba_backsub does,
-        //    fused: this block factored these landmarks then): dp = V^-1 (-g_p - sum_c W_o^T dc_c)
+        lds_barrier();
+        // every global read of the chunk is one level of indexing (the k_ba_slots table), issued
+        // up front: slot (li, ci) = thread / TS_BA_MAXW, thread % TS_BA_MAXW; landmark li = thread
+        const int li = threadIdx.x / TS_BA_MAXW, ci = threadIdx.x - li * TS_BA_MAXW;
+        const int r = l0 + li;
+        const size_t sl = (size_t)r * TS_BA_MAXW + ci;
+        const bool in = li < nl && ci < n;
+        const int o = in ? q.lo_o[sl] : -1;
+        double uvd[3] = {0.0, 0.0, 0.0};
+        if (in) {
+            const double* pu = q.lo_uvd + sl * 4;
+            uvd[0] = pu[0]; uvd[1] = pu[1]; uvd[2] = pu[2];
+        }
+        const bool lmt = (int)threadIdx.x < nl;   // landmark thread of landmark l0 + threadIdx.x
+        const int rl = l0 + threadIdx.x;
+        double Xl[3] = {0.0, 0.0, 0.0};
+        if (lmt) {
+            Xl[0] = q.Xc[(size_t)rl * 3]; Xl[1] = q.Xc[(size_t)rl * 3 + 1]; Xl[2] = q.Xc[(size_t)rl * 3 + 2];
+        }
+        // 0. the previous iteration's landmark update for the chunk (this block factored these
+        //    landmarks then): dp = V^-1 (-g_p - sum_c W_o^T dc_c), Xc += dp
         if (bsub) {
-            const int li = threadIdx.x / TS_BA_MAXW, ci = threadIdx.x - li * TS_BA_MAXW;
-            const int r = l0 + li;
-            const int o = (li < nl && ci >= 1 && ci < n) ? q.camobs[(size_t)ci * WK + r] : -1;   // dc of camera 0 is zero
             double t[3] = {0.0, 0.0, 0.0};
-            if (o >= 0) {
-                const double* W = q.obs_W + (size_t)o * 18;
-                const double* dc = q.dc + 6 * ci;
+            if (in && ci >= 1) {   // dc of camera 0 is zero
+                double Wv[18], dcv[6];
+                const double* W = q.lo_W + sl * 18;
 #pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    double acc = 0.0;
+                for (int e = 0; e < 18; ++e) Wv[e] = W[e];
 #pragma unroll
-                    for (int e = 0; e < 6; ++e) acc += W[3 * e + j] * dc[e];
-                    t[j] = acc;
+                for (int e = 0; e < 6; ++e) dcv[e] = q.dc[6 * ci + e];
+                if (o >= 0) {
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) {
+                        double acc = 0.0;
+#pragma unroll
+                        for (int e = 0; e < 6; ++e) acc += Wv[3 * e + j] * dcv[e];
+                        t[j] = acc;
+                    }
                 }
             }
+            double gp[3] = {0.0, 0.0, 0.0}, Lf[6] = {1.0, 0.0, 1.0, 0.0, 0.0, 1.0};
+            if (lmt) {
 #pragma unroll
-            for (int j = 0; j < 3; ++j) s_bs[li][ci][j] = t[j];
-            __syncthreads();
-            if (threadIdx.x < nl) {
-                const int rr = l0 + threadIdx.x;
+                for (int j = 0; j < 3; ++j) gp[j] = q.lm_gp[(size_t)j * WK + rl];
+#pragma unroll
+                for (int j = 0; j < 6; ++j) Lf[j] = q.lm_L[(size_t)j * WK + rl];
+            }
+            if (li < BA_CHUNK) {
+#pragma unroll
+                for (int j = 0; j < 3; ++j) s_bs[li][ci][j] = t[j];
+            }
+            lds_barrier();
+            if (lmt) {
                 double rhs[3];
                 for (int j = 0; j < 3; ++j) {
                     double sum = 0.0;
                     for (int cj = 1; cj < n; ++cj) sum += s_bs[threadIdx.x][cj][j];
-                    rhs[j] = -q.lm_gp[(size_t)j * WK + rr] - sum;
+                    rhs[j] = -gp[j] - sum;
                 }
-                const double L0 = q.lm_L[rr], L1 = q.lm_L[(size_t)WK + rr], L2 = q.lm_L[(size_t)2 * WK + rr];
-                const double L3 = q.lm_L[(size_t)3 * WK + rr], L4 = q.lm_L[(size_t)4 * WK + rr], L5 = q.lm_L[(size_t)5 * WK + rr];
+                const double L0 = Lf[0], L1 = Lf[1], L2 = Lf[2], L3 = Lf[3], L4 = Lf[4], L5 = Lf[5];
                 const double y0 = rhs[0] / L0, y1 = (rhs[1] - L1 * y0) / L2, y2 = ((rhs[2] - L3 * y0) - L4 * y1) / L5;
                 const double x2 = y2 / L5, x1 = (y1 - L4 * x2) / L2, x0 = ((y0 - L1 * x1) - L3 * x2) / L0;
-                const int id = q.lm_id[rr];
-                q.X[(size_t)id * 3] += x0;
-                q.X[(size_t)id * 3 + 1] += x1;
-                q.X[(size_t)id * 3 + 2] += x2;
-            }
-            __syncthreads();
-        }
-        // 1. Jacobians of every (landmark, camera) observation of the chunk
-        {
-            const int li = threadIdx.x / TS_BA_MAXW, ci = threadIdx.x - li * TS_BA_MAXW;
-            const int r = l0 + li;
-            const int o = (li < nl && ci < n) ? q.camobs[(size_t)ci * WK + r] : -1;
-            s_has[li][ci] = o >= 0;
-            if (o >= 0) {
-                const int id = q.lm_id[r];
-                const size_t so = (size_t)a.order[ci] * K + q.obs_k[o];
-                const double X[3] = {q.X[(size_t)id * 3], q.X[(size_t)id * 3 + 1], q.X[(size_t)id * 3 + 2]};
-                double Jc[3][6], Jp[3][3], res[3];
-                ba_obs_jac(s_T[ci], X, q.u[so], q.v[so], q.d[so], cal, Jc, Jp, res);
-                double* W = s_W[li][ci];
-                for (int i = 0; i < 6; ++i)
-                    for (int j = 0; j < 3; ++j) {
-                        const double w = (Jc[0][i] * Jp[0][j] + Jc[1][i] * Jp[1][j]) + Jc[2][i] * Jp[2][j];
-                        W[3 * i + j] = w;
-                        q.obs_W[(size_t)o * 18 + 3 * i + j] = w;
-                    }
-                int e = 0;
-                for (int i = 0; i < 6; ++i)
-                    for (int j = i; j < 6; ++j) q.obs_Ug[(size_t)(e++) * WK + o] = (Jc[0][i] * Jc[0][j] + Jc[1][i] * Jc[1][j]) + Jc[2][i] * Jc[2][j];
-                for (int i = 0; i < 6; ++i) q.obs_Ug[(size_t)(21 + i) * WK + o] = (Jc[0][i] * res[0] + Jc[1][i] * res[1]) + Jc[2][i] * res[2];
-                double* vg = s_Vg[li][ci];
-                e = 0;
-                for (int i = 0; i < 3; ++i)
-                    for (int j = i; j < 3; ++j) vg[e++] = (Jp[0][i] * Jp[0][j] + Jp[1][i] * Jp[1][j]) + Jp[2][i] * Jp[2][j];
-                for (int i = 0; i < 3; ++i) vg[6 + i] = (Jp[0][i] * res[0] + Jp[1][i] * res[1]) + Jp[2][i] * res[2];
+                Xl[0] += x0;
+                Xl[1] += x1;
+                Xl[2] += x2;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) q.Xc[(size_t)rl * 3 + j] = Xl[j];
             }
         }
-        __syncthreads();
+        if (lmt) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) s_X[threadIdx.x][j] = Xl[j];
+        }
+        lds_barrier();
+        // 1. Jacobians of every (landmark, camera) observation of the chunk; W_o stays in this
+        //    thread's registers for step 3 (and goes to HBM for the next pass's landmark update)
+        double Wr[18];
+#pragma unroll
+        for (int e = 0; e < 18; ++e) Wr[e] = 0.0;
+        s_has[li][ci] = o >= 0;
+        if (o >= 0) {
+            double Jc[3][6], Jp[3][3], res[3];
+            ba_obs_jac(s_T[ci], s_X[li], uvd[0], uvd[1], uvd[2], cal, Jc, Jp, res);
+            double* Wg = q.lo_W + sl * 18;
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const double w = (Jc[0][i] * Jp[0][j] + Jc[1][i] * Jp[1][j]) + Jc[2][i] * Jp[2][j];
+                    Wr[3 * i + j] = w;
+                    Wg[3 * i + j] = w;
+                }
+            int e = 0;
+            for (int i = 0; i < 6; ++i)
+                for (int j = i; j < 6; ++j) q.obs_Ug[(size_t)(e++) * WK + o] = (Jc[0][i] * Jc[0][j] + Jc[1][i] * Jc[1][j]) + Jc[2][i] * Jc[2][j];
+            for (int i = 0; i < 6; ++i) q.obs_Ug[(size_t)(21 + i) * WK + o] = (Jc[0][i] * res[0] + Jc[1][i] * res[1]) + Jc[2][i] * res[2];
+            double* vg = s_Vg[li][ci];
+            e = 0;
+            for (int i = 0; i < 3; ++i)
+                for (int j = i; j < 3; ++j) vg[e++] = (Jp[0][i] * Jp[0][j] + Jp[1][i] * Jp[1][j]) + Jp[2][i] * Jp[2][j];
+            for (int i = 0; i < 3; ++i) vg[6 + i] = (Jp[0][i] * res[0] + Jp[1][i] * res[1]) + Jp[2][i] * res[2];
+        }
+        lds_barrier();   // LDS only: the HBM stores above drain behind it
         // 2. per-landmark factor
         if (threadIdx.x < BA_CHUNK) {
             const int li = threadIdx.x, r = l0 + li;
@@ -514,34 +582,40 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
             const double y0 = vg[6] / l00, y1 = (vg[7] - l10 * y0) / l11, y2 = ((vg[8] - l20 * y0) - l21 * y1) / l22;
             s_L[li][0] = 1.0 / l00; s_L[li][1] = l10; s_L[li][2] = 1.0 / l11; s_L[li][3] = l20; s_L[li][4] = l21;
             s_L[li][5] = 1.0 / l22;
-            s_Q[(3 * li) * BA_QPITCH + 60] = live ? y0 : 0.0;
-            s_Q[(3 * li + 1) * BA_QPITCH + 60] = live ? y1 : 0.0;
-            s_Q[(3 * li + 2) * BA_QPITCH + 60] = live ? y2 : 0.0;
+            const double yv[3] = {y0, y1, y2};
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {   // rows 60 (y) .. 63 of the landmark's three columns
+                double* colq = s_Q + (3 * li + j) * BA_QPITCH;
+                colq[60] = live ? yv[j] : 0.0;
+                colq[61] = 0.0;
+                colq[62] = 0.0;
+                colq[63] = 0.0;
+            }
             if (live) {
                 q.lm_L[r] = l00; q.lm_L[(size_t)WK + r] = l10; q.lm_L[(size_t)2 * WK + r] = l11;
                 q.lm_L[(size_t)3 * WK + r] = l20; q.lm_L[(size_t)4 * WK + r] = l21; q.lm_L[(size_t)5 * WK + r] = l22;
                 q.lm_gp[r] = vg[6]; q.lm_gp[(size_t)WK + r] = vg[7]; q.lm_gp[(size_t)2 * WK + r] = vg[8];
             }
         }
-        __syncthreads();
-        // 3. Schur columns: item = (landmark, row != 60), all from LDS
-        for (int it = threadIdx.x; it < BA_CHUNK * 64; it += blockDim.x) {
-            const int li = it >> 6, row = it & 63;
-            if (row == 60) continue;
-            const int ci = row / 6, rr = row - 6 * ci;
-            double z0 = 0.0, z1 = 0.0, z2 = 0.0;
-            if (li < nl && ci < n && s_has[li][ci]) {
-                const double* W = s_W[li][ci] + 3 * rr;
-                const double* Lm = s_L[li];
-                z0 = W[0] * Lm[0];
-                z1 = (W[1] - Lm[1] * z0) * Lm[2];
-                z2 = ((W[2] - Lm[3] * z0) - Lm[4] * z1) * Lm[5];
+        lds_barrier();
+        // 3. Schur columns: thread (landmark, camera) writes the camera's 6 rows of the landmark's
+        //    3 columns, (W_o L^-T) or zeros
+        {
+            const double* Lm = s_L[li];
+            const double i0 = Lm[0], m1 = Lm[1], i2 = Lm[2], m3 = Lm[3], m4 = Lm[4], i5 = Lm[5];
+#pragma unroll
+            for (int rr = 0; rr < 6; ++rr) {
+                const double* W = Wr + 3 * rr;
+                const double z0 = W[0] * i0;
+                const double z1 = (W[1] - m1 * z0) * i2;
+                const double z2 = ((W[2] - m3 * z0) - m4 * z1) * i5;
+                const int row = 6 * ci + rr;
+                s_Q[(3 * li) * BA_QPITCH + row] = o >= 0 ? z0 : 0.0;
+                s_Q[(3 * li + 1) * BA_QPITCH + row] = o >= 0 ? z1 : 0.0;
+                s_Q[(3 * li + 2) * BA_QPITCH + row] = o >= 0 ? z2 : 0.0;
             }
-            s_Q[(3 * li) * BA_QPITCH + row] = z0;
-            s_Q[(3 * li + 1) * BA_QPITCH + row] = z1;
-            s_Q[(3 * li + 2) * BA_QPITCH + row] = z2;
         }
-        __syncthreads();
+        lds_barrier();
         // 4. C += Q^T Q over the chunk's columns (zero columns past nl contribute nothing)
         if (wave < 4) {
             const int ksteps = (3 * nl + 3) >> 2;
@@ -594,127 +668,170 @@ __global__ __launch_bounds__(256) void k_ba_reduce(BatchCtx c, BaArgs a) {
 }
 
 // Reduced camera system (camera 0 = gauge): S = blockdiag(U + lam) - C, b = -g_c + C[:, 60].
-// LDL^T of [S | b] (the right-hand side as column M: forward substitution fused) on 8 waves,
-// every one of them holding all rows: lane i = row i (rows past m = 6 (n - 1) are identity rows,
-// so one fully unrolled code serves every window size) and wave w the columns k = 8 t + w.
-// Step j: the owner wave of column j (j % 8) divides it by the pivot d_j (v_readlane of lane j)
-// and posts the multipliers l_ij in LDS; after one barrier every wave subtracts l_ij * S[j][k]
-// from its columns, the pivot row's entries coming from lane j of the same wave by v_readlane.
-// Lane k's row freezes at step k, so by symmetry its entries right of the diagonal are then
-// column k of L D: they go to LDS, and wave 0 runs the back substitution D L^T x = y (x_i by
-// readlane, lanes k < i subtract (S[k][i] / d_k) x_i).  Camera updates R <- cayley(w) R,
-// t <- ... + rho follow.
-#define BA_SOLVE_WAVES 8   // 4 / 8 / 16 waves: 21.8 / 19.4 / 20.1 us per solve alone (exp microbenchmark)
-#define BA_SOLVE_COLS ((TS_BA_MAXD + BA_SOLVE_WAVES) / BA_SOLVE_WAVES)   // columns per wave (+ the rhs)
+// Blocked right-looking LDL^T over the 6-wide camera blocks (m = 6 (n - 1) <= 54), one block of
+// 8 waves, the lower triangle of S in LDS:
+//   * wave 0 factors the panels: lane i = row i holds the 6 columns of block b and the right-hand
+//     side; column step jj takes the pivot d_jj from lane jj (v_readlane), the multipliers
+//     l_ij = S_ij / d_jj, and updates the block's later columns and the right-hand side in
+//     registers (forward substitution fused); the panel (l_ij and l_ij d_jj) goes to LDS;
+//   * look-ahead: during step b wave 0 applies panel b to block column b + 1 and factors panel
+//     b + 1 at once, while waves 1-7 apply panel b to the trailing columns >= 6 (b + 2) (lane =
+//     row, wave = every 7th column); one barrier per block step (9 at a full window instead of
+//     the 54 of a column-by-column elimination), panels double-buffered;
+//   * wave 0 then solves D L^T x = y (x_i by readlane, l_ki from the upper triangle, where the
+//     panel wave left them).
+// Camera updates R <- cayley(w) R, t <- ... + rho follow.
+#define BA_SOLVE_WAVES 8
+#define BA_SP 65   // LDS row pitch of S (doubles)
 __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, BaArgs a) {
-    constexpr int M = TS_BA_MAXD;
-    constexpr int NT = BA_SOLVE_COLS;
-    constexpr int WV = BA_SOLVE_WAVES;
-    static_assert(TS_BA_MAXW * 27 <= 64 * WV, "one camera-block load per thread");
-    __shared__ double s_C[64 * 64];   // C, then the frozen rows (S[k][i], i > k) for the back substitution
+    static_assert(TS_BA_MAXW * 27 <= 64 * BA_SOLVE_WAVES, "one camera-block load per thread");
+    __shared__ double s_S[64 * BA_SP];             // lower: S; upper (row j, column i > j): l_ij
     __shared__ double s_U[TS_BA_MAXW * 27];
-    __shared__ double s_l[2][64];
+    __shared__ __attribute__((aligned(16))) double s_pl[2][64][6];   // panel multipliers l_ij
+    __shared__ __attribute__((aligned(16))) double s_pq[2][64][6];   // l_ij d_j
     __shared__ double s_d[64];
     __shared__ double s_x[64];
-    __shared__ int s_ok[2];   // per step parity: the pivot was positive
+    __shared__ int s_ok;
     BaPair q = ba_pair(c, a, a.pair);
     const int n = a.n_order;
-    const int m = 6 * (n - 1);
+    const int m = 6 * (n - 1), nb = n - 1;
     if (q.counts[1] == 0 || n < 2) {
         if (threadIdx.x == 0) q.counts[2] = 0;
         return;
     }
-    {   // stage C and the camera blocks (every load in flight at once)
-        constexpr int NL = 4096 / (64 * WV);
-        double v[NL];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // stage C (every thread's 8 loads in flight at once) and the camera blocks
+    constexpr int NL = 4096 / (64 * BA_SOLVE_WAVES);
+    double cv[NL];
 #pragma unroll
-        for (int k = 0; k < NL; ++k) v[k] = q.C[threadIdx.x + 64 * WV * k];
-        const double u0 = (int)threadIdx.x < n * 27 ? q.cam_U[threadIdx.x] : 0.0;
+    for (int k = 0; k < NL; ++k) cv[k] = q.C[threadIdx.x + 64 * BA_SOLVE_WAVES * k];
+    if ((int)threadIdx.x < n * 27) s_U[threadIdx.x] = q.cam_U[threadIdx.x];
+    __syncthreads();
+    // S_ik = -C[i+6][k+6] (+ U + lam inside a camera block), lower triangle; row i's right-hand
+    // side -g_c + C[i+6][60] into s_x[i] (read back by wave 0)
 #pragma unroll
-        for (int k = 0; k < NL; ++k) s_C[threadIdx.x + 64 * WV * k] = v[k];
-        if ((int)threadIdx.x < n * 27) s_U[threadIdx.x] = u0;
+    for (int k8 = 0; k8 < NL; ++k8) {
+        const int e = threadIdx.x + 64 * BA_SOLVE_WAVES * k8;
+        const int R = e >> 6, Cc = e & 63;
+        const int i = R - 6, k = Cc - 6;
+        if (i < 0 || i >= m) continue;
+        if (Cc == 60) {
+            s_x[i] = -s_U[(R / 6) * 27 + 21 + R % 6] + cv[k8];
+            continue;
+        }
+        if (k < 0 || k > i) continue;
+        double v = -cv[k8];
+        if (R / 6 == Cc / 6) {
+            const int ci = R / 6, i0 = R % 6, j0 = Cc % 6;
+            const int lo = min(i0, j0), hi = max(i0, j0);
+            v += s_U[ci * 27 + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)] + (i0 == j0 ? a.lam : 0.0);
+        }
+        s_S[i * BA_SP + k] = v;
     }
     __syncthreads();
-    const int i = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const bool live = i < m;
-    const int R = i + 6, ci = R / 6, i0 = R % 6;
-    double r[NT];   // row i, columns WV t + w
+    const bool live = lane < m;
+    double rhs = (w == 0 && live) ? s_x[lane] : 0.0;   // wave 0: right-hand side of row `lane`
+    bool good = true;   // wave 0: every pivot positive
+    double cl[6];       // wave 0: this lane's multipliers of the current panel
+    // wave 0: factor panel b from its 6 columns col[] (rows >= 6b current), into buffer b & 1
+    auto factor = [&](int b, double* col) {
+        const int b6 = 6 * b;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const int k = WV * t + w;
-        double v = (k == i) ? 1.0 : 0.0;   // identity rows / columns past m
-        if (k == M) {
-            v = live ? -s_U[ci * 27 + 21 + i0] + s_C[R * 64 + 60] : 0.0;
-        } else if (live && k < m) {
-            const int Cc = k + 6;
-            v = -s_C[R * 64 + Cc];
-            if (ci == Cc / 6) {
-                const int j0 = Cc % 6;
-                const int lo = min(i0, j0), hi = max(i0, j0);
-                v += s_U[ci * 27 + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)] + (i0 == j0 ? a.lam : 0.0);
-            }
-        }
-        r[t] = v;
-    }
-    // multipliers of step j: the owner of column j (wave j % WV) divides it by the pivot d_j (lane
-    // j) and posts them in LDS (buffer j & 1, with the pivot's sign check).  Look-ahead: during
-    // step j the owner of column j + 1 updates that column first and posts step j + 1's
-    // multipliers before its other columns, so one barrier per step separates them.
-    auto post = [&](int j, double col) {
-        const double d = readlane_f64(col, j);
-        s_l[j & 1][i] = (i > j && d > 0.0) ? col / d : 0.0;
-        if (i == 0) {
-            s_d[j] = d;
-            s_ok[j & 1] = d > 0.0;   // the buffer of step j - 2: every wave has read it
+        for (int j = 0; j < 6; ++j) {
+            const int jj = b6 + j;
+            const double d = readlane_f64(col[j], jj);
+            good = good && d > 0.0;
+            double inv = __builtin_amdgcn_rcp(d);   // + one Newton step: ~1 ulp, off the division chain
+            inv = inv * (2.0 - d * inv);
+            const double pre = col[j];
+            const double l = lane > jj ? pre * inv : 0.0;
+#pragma unroll
+            for (int k = j + 1; k < 6; ++k) col[k] -= l * readlane_f64(pre, b6 + k);
+            rhs -= l * readlane_f64(rhs, jj);
+            cl[j] = l;
+            s_pl[b & 1][lane][j] = l;
+            s_pq[b & 1][lane][j] = lane > jj ? pre : 0.0;
+            if (lane > jj && live) s_S[jj * BA_SP + lane] = l;   // upper triangle: for D L^T x = y
+            if (lane == jj) s_d[jj] = d;
         }
     };
-    if (w == 0) post(0, r[0]);
+    if (w == 0) {
+        double col[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) col[k] = live ? s_S[lane * BA_SP + k] : 0.0;
+        factor(0, col);
+    }
     __syncthreads();
-    bool good = true;
+    for (int b = 0; b < nb; ++b) {
+        const int pb = b & 1;
+        if (w == 0) {
+            if (b + 1 < nb) {
+                // block column b + 1, rows >= 6 (b + 1): apply panel b, then factor it
+                const int c0 = 6 * (b + 1);
+                double col[6];
 #pragma unroll
-    for (int j = 0; j < M; ++j) {
-        if (!s_ok[j & 1]) {   // block-uniform
-            good = false;
-            break;
-        }
-        const double l = s_l[j & 1][i];
-        const int j1 = j + 1, t1 = j1 / WV;
-        const bool ahead = j1 < M && w == (j1 % WV);   // this wave owns the next pivot column
-        if (ahead) {
-            r[t1] -= l * readlane_f64(r[t1], j);
-            post(j1, r[t1]);
-        }
+                for (int k = 0; k < 6; ++k) {
+                    const double* qk = s_pq[pb][c0 + k];
+                    double s = (lane >= c0 + k && live) ? s_S[lane * BA_SP + c0 + k] : 0.0;
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            if (WV * t + WV - 1 <= j) continue;   // every column of t is at or left of j (compile time)
-            if (ahead && t == t1) continue;
-            const double p = readlane_f64(r[t], j);
-            if (WV * t + w > j) r[t] -= l * p;
+                    for (int j = 0; j < 6; ++j) s -= cl[j] * qk[j];
+                    col[k] = s;
+                }
+                factor(b + 1, col);
+            }
+        } else {
+            // trailing columns k >= 6 (b + 2) with panel b: lane = row i, waves 1-7 deal the columns
+            const int c0 = 6 * (b + 2);
+            const int i = lane;
+            if (i >= c0 && i < m) {
+                double li[6];
+#pragma unroll
+                for (int j = 0; j < 6; ++j) li[j] = s_pl[pb][i][j];
+                // two columns per iteration, so their LDS reads are in flight together
+                int k = c0 + (w - 1);
+                for (; k + (BA_SOLVE_WAVES - 1) <= i; k += 2 * (BA_SOLVE_WAVES - 1)) {
+                    const int k2 = k + (BA_SOLVE_WAVES - 1);
+                    const double* qa = s_pq[pb][k];
+                    const double* qb = s_pq[pb][k2];
+                    double sa = s_S[i * BA_SP + k], sb = s_S[i * BA_SP + k2];
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) {
+                        sa -= li[j] * qa[j];
+                        sb -= li[j] * qb[j];
+                    }
+                    s_S[i * BA_SP + k] = sa;
+                    s_S[i * BA_SP + k2] = sb;
+                }
+                if (k <= i) {
+                    const double* qk = s_pq[pb][k];
+                    double sa = s_S[i * BA_SP + k];
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) sa -= li[j] * qk[j];
+                    s_S[i * BA_SP + k] = sa;
+                }
+            }
         }
         __syncthreads();
     }
-    // frozen rows -> LDS (row k, column i = 4 t + w > k), then wave 0 solves D L^T x = y
-    __syncthreads();
-    if (good) {
+    if (w == 0) {
+        // D L^T x = y: x_i = y_i / d_i - sum_{k > i} l_ki x_k (the row's l_ki preloaded, so the
+        // chain is readlane -> FMA only)
+        double lr[TS_BA_MAXD];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int k = WV * t + w;
-            if (k <= M) s_C[i * 64 + k] = r[t];
-        }
-    }
-    __syncthreads();
-    if (good && w == 0) {
-        const double rd = 1.0 / s_d[i < M ? i : 0];
-        double x = i < M ? s_C[i * 64 + M] * rd : 0.0;
+        for (int k = 0; k < TS_BA_MAXD; ++k) lr[k] = (lane < k && k < m) ? s_S[lane * BA_SP + k] : 0.0;
+        double x = live ? rhs / s_d[lane] : 0.0;
 #pragma unroll
-        for (int i2 = M - 1; i2 > 0; --i2) {
+        for (int i2 = TS_BA_MAXD - 1; i2 > 0; --i2) {
+            if (i2 >= m) continue;   // uniform
             const double xi = readlane_f64(x, i2);
-            if (i < i2) x -= (s_C[i * 64 + i2] * rd) * xi;
+            x -= lr[i2] * xi;
         }
-        s_x[i] = x;
+        s_x[lane] = x;
+        if (lane == 0) s_ok = good;
     }
     __syncthreads();
-    const bool ok = good;
+    const bool good_all = s_ok != 0;
+    const bool ok = good_all;
     if (threadIdx.x == 0) q.counts[2] = ok;
     for (int e = threadIdx.x; e < 6 * n; e += blockDim.x) q.dc[e] = (e < 6 || !ok) ? 0.0 : s_x[e - 6];
     if (ok && (int)threadIdx.x >= 1 && (int)threadIdx.x < n) {
@@ -742,20 +859,24 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, Ba
     }
 }
 
-// 16 lanes per landmark (lane = window camera): W_o^T dc_o of each observation, summed over the
-// 16 lanes by a fixed xor-butterfly; the first lane then solves dp = V^-1 (-g_p - sum) with the
-// stored Cholesky factor and moves the landmark, X += dp.
+// The last iteration's landmark update and the write-back of the window's landmarks: 16 lanes
+// per landmark (lane = window camera): W_o^T dc_o of each observation (slot table), summed over
+// the 16 lanes by a fixed xor-butterfly; the first lane then solves dp = V^-1 (-g_p - sum) with
+// the stored Cholesky factor and stores X[lm_id[r]] = Xc[r] + dp (Xc[r] alone when the last
+// solve failed).
 __global__ __launch_bounds__(256) void k_ba_backsub(BatchCtx c, BaArgs a) {
     const int WK = a.W * c.g.K;
     BaPair q = ba_pair(c, a, a.pair);
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     const int r = gid >> 4, ci = gid & 15;
     const int L = q.counts[1];
-    if (!q.counts[2] || (r & ~15) >= L) return;   // whole 16-landmark groups exit together
+    if ((r & ~15) >= L) return;   // whole 16-landmark groups exit together
     const bool live = r < L;
+    const bool upd = q.counts[2] != 0;
     const int rc = min(r, L - 1);
-    const int o = ci >= 1 && ci < a.n_order ? q.camobs[(size_t)ci * WK + rc] : -1;   // dc of camera 0 is zero
-    const double* W = q.obs_W + (size_t)max(o, 0) * 18;
+    const size_t sl = (size_t)rc * TS_BA_MAXW + min(ci, TS_BA_MAXW - 1);
+    const int o = upd && ci >= 1 && ci < a.n_order ? q.lo_o[sl] : -1;   // dc of camera 0 is zero
+    const double* W = q.lo_W + sl * 18;
     double wv[18];
 #pragma unroll
     for (int e = 0; e < 18; ++e) wv[e] = W[e];
@@ -773,23 +894,26 @@ __global__ __launch_bounds__(256) void k_ba_backsub(BatchCtx c, BaArgs a) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) t[j] += __shfl_xor(t[j], sh, 64);
     if (ci != 0 || !live) return;
-    double rhs[3];
-    for (int i = 0; i < 3; ++i) rhs[i] = -q.lm_gp[(size_t)i * WK + r] - t[i];
-    double Lm[3][3] = {{q.lm_L[r], 0.0, 0.0}, {q.lm_L[(size_t)WK + r], q.lm_L[(size_t)2 * WK + r], 0.0},
-                       {q.lm_L[(size_t)3 * WK + r], q.lm_L[(size_t)4 * WK + r], q.lm_L[(size_t)5 * WK + r]}};
-    double y[3], x[3];
-    for (int i = 0; i < 3; ++i) {
-        double v = rhs[i];
-        for (int k = 0; k < i; ++k) v -= Lm[i][k] * y[k];
-        y[i] = v / Lm[i][i];
-    }
-    for (int i = 2; i >= 0; --i) {
-        double v = y[i];
-        for (int k = i + 1; k < 3; ++k) v -= Lm[k][i] * x[k];
-        x[i] = v / Lm[i][i];
+    double x[3] = {0.0, 0.0, 0.0};
+    if (upd) {
+        double rhs[3];
+        for (int i = 0; i < 3; ++i) rhs[i] = -q.lm_gp[(size_t)i * WK + r] - t[i];
+        double Lm[3][3] = {{q.lm_L[r], 0.0, 0.0}, {q.lm_L[(size_t)WK + r], q.lm_L[(size_t)2 * WK + r], 0.0},
+                           {q.lm_L[(size_t)3 * WK + r], q.lm_L[(size_t)4 * WK + r], q.lm_L[(size_t)5 * WK + r]}};
+        double y[3];
+        for (int i = 0; i < 3; ++i) {
+            double v = rhs[i];
+            for (int k = 0; k < i; ++k) v -= Lm[i][k] * y[k];
+            y[i] = v / Lm[i][i];
+        }
+        for (int i = 2; i >= 0; --i) {
+            double v = y[i];
+            for (int k = i + 1; k < 3; ++k) v -= Lm[k][i] * x[k];
+            x[i] = v / Lm[i][i];
+        }
     }
     const int id = q.lm_id[r];
-    for (int i = 0; i < 3; ++i) q.X[(size_t)id * 3 + i] += x[i];
+    for (int i = 0; i < 3; ++i) q.X[(size_t)id * 3 + i] = upd ? q.Xc[(size_t)r * 3 + i] + x[i] : q.Xc[(size_t)r * 3 + i];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -811,7 +935,6 @@ void launch_ba_keyframe(const BatchCtx& c, const BaArgs& a, bool evict, hipStrea
     const int K = c.g.K;
     if (evict) {
         const int nb = (a.n_order * K + 255) / 256;
-        (void)hipMemsetAsync(a.st.remap, 0x7F, sizeof(int32_t) * K, s);
         hipLaunchKernelGGL(k_ba_evict_min, dim3(nb), dim3(256), 0, s, c, a);
         hipLaunchKernelGGL(k_ba_evict_move, dim3(nb), dim3(256), 0, s, c, a);
     }
@@ -828,14 +951,12 @@ void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming
     // grids sized for the window's maximum (counts live on the device; threads past them exit)
     const int WK = a.W * c.g.K;
     const int nb = (WK + 255) / 256;
-    (void)hipMemsetAsync(a.st.cnt, 0, sizeof(int32_t) * WK, s);
-    (void)hipMemsetAsync(a.st.camobs, 0xFF, sizeof(int32_t) * (size_t)a.n_order * WK, s);
     hipLaunchKernelGGL(k_ba_gate, dim3((a.n_order * c.g.K + 255) / 256), dim3(256), 0, s, c, a);
     const int ntiles = (WK + BA_TILE - 1) / BA_TILE + a.n_order * ((c.g.K + BA_TILE - 1) / BA_TILE);
     hipLaunchKernelGGL(k_ba_tilecount, dim3(ntiles), dim3(256), 0, s, c, a);
-    hipLaunchKernelGGL(k_ba_tilescan, dim3(1), dim3(64), 0, s, c, a);
     hipLaunchKernelGGL(k_ba_tilescatter, dim3(ntiles), dim3(256), 0, s, c, a);
     hipLaunchKernelGGL(k_ba_camobs, dim3(nb), dim3(256), 0, s, c, a);
+    hipLaunchKernelGGL(k_ba_slots, dim3((WK * TS_BA_MAXW + 255) / 256), dim3(256), 0, s, c, a);
     BaArgs ai = a;
     for (int it = 0; it < a.iters; ++it) {
         const bool rec = timing && timing->used < timing->cap;

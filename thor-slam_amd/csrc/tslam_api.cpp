@@ -276,7 +276,9 @@ static int alloc_ba(tslam_handle* h) {
         {(void**)&b.li, 4 * WK},             {(void**)&b.lm_id, 4 * WK},         {(void**)&b.keep, WK},
         {(void**)&b.camobs, 4 * W * WK},     {(void**)&b.obs_Vg, 8 * WK * 9},    {(void**)&b.obs_cam, 4 * WK},
         {(void**)&b.obs_k, 4 * WK},          {(void**)&b.obs_id, 4 * WK},        {(void**)&b.cam_off, 4 * (W + 1)},
-        {(void**)&b.counts, 4 * 4 * P},      {(void**)&b.tiles, 4 * 2 * TS_BA_TILES},      {(void**)&b.obs_W, 8 * WK * 18},    {(void**)&b.obs_Ug, 8 * WK * 27},
+        {(void**)&b.counts, 4 * 4 * P},      {(void**)&b.tiles, 4 * 2 * TS_BA_TILES},      {(void**)&b.obs_Ug, 8 * WK * 27},
+        {(void**)&b.lo_o, 4 * WK * TS_BA_MAXW}, {(void**)&b.lo_uvd, 32 * WK * TS_BA_MAXW}, {(void**)&b.lo_W, 8 * 18 * WK * TS_BA_MAXW},
+        {(void**)&b.Xc, 8 * WK * 3},
         {(void**)&b.lm_L, 8 * WK * 6},       {(void**)&b.lm_gp, 8 * WK * 3},     {(void**)&b.C, 8 * 64 * 64},
         {(void**)&b.part, 8 * (size_t)TS_BA_SPLIT * 64 * 64}, {(void**)&b.cam_U, 8 * W * 27}, {(void**)&b.dc, 8 * W * 6},
         {(void**)&b.flops, 8},               {(void**)&b.fe_pose, 8 * 2 * (size_t)h->B * P * 16},
@@ -285,6 +287,12 @@ static int alloc_ba(tslam_handle* h) {
         const int rc = dev_alloc(h, a.p, a.bytes);
         if (rc != TSLAM_OK) return rc;
     }
+    // scratch kept in its between-solves state by the kernels themselves (no per-solve memsets):
+    // camobs all -1 (k_ba_slots resets the entries k_ba_camobs set), remap all 0x7F7F7F7F
+    // (k_ba_insert refills it after an eviction), cnt zero (dev_alloc; k_ba_slots re-zeroes it)
+    HIPCHK(hipMemset(b.camobs, 0xFF, 4 * W * WK));
+    HIPCHK(hipMemset(b.remap, 0x7F, 4 * K));
+    HIPCHK(hipDeviceSynchronize());
     return TSLAM_OK;
 }
 

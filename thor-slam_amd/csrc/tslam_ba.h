@@ -32,19 +32,26 @@ struct BaStore {
     uint32_t* kf_desc;  // [P][W*K][8] descriptor of every keyframe keypoint (a landmark id's descriptor)
     int64_t* gid;       // [P][W*K] global landmark id (creation frame * K + keypoint), kept on re-homing
     // scratch (sizes for W*K landmarks/observations)
-    int32_t* remap;    // [K]
-    int32_t* cnt;      // [WK] observations per landmark id (after the gate)
+    int32_t* remap;    // [K] (0x7F7F7F7F between evictions: k_ba_insert refills it)
+    int32_t* cnt;      // [WK] observations per landmark id (after the gate; zero between solves)
     int32_t* li;       // [WK] compact index per id or -1
     int32_t* lm_id;    // [WK] id per compact index
     uint8_t* keep;     // [W*K] gate result per (window camera, keypoint)
     int32_t* camobs;   // [W][WK] observation index of (window camera, compact landmark) or -1
+                       // (all -1 between solves: k_ba_slots resets what k_ba_camobs set)
     int32_t* obs_cam;  // [WK] window position of the observing keyframe (0 = oldest)
     int32_t* obs_k;    // [WK]
     int32_t* obs_id;   // [WK]
     int32_t* cam_off;  // [W+1]
     int32_t* counts;   // [P][4] n_obs, L, solve ok, pad
     int32_t* tiles;    // [2][TS_BA_TILES] tile counts, tile offsets
-    double* obs_W;     // [WK][18]  W_o = J_c^T J_p (6x3, row-major), gathered per landmark
+    // per (compact landmark r, window camera ci) slot s = r * TS_BA_MAXW + ci (k_ba_slots): the
+    // observation index or -1, its (u, v, d), and W_o of the last linearisation — every per-
+    // iteration read of the Schur pass is one level of indexing
+    int32_t* lo_o;     // [WK * MAXW]
+    double* lo_uvd;    // [WK * MAXW][4]  u, v, d, 0
+    double* lo_W;      // [WK * MAXW][18] W_o = J_c^T J_p (6x3, row-major)
+    double* Xc;        // [WK][3] position of compact landmark r during the solve (X[lm_id[r]] after it)
     double* obs_Ug;    // [27][WK]  J_c^T J_c (upper 21) | J_c^T r (6), structure-of-arrays
     double* obs_Vg;    // [WK][9]   J_p^T J_p (upper 6) | J_p^T r (3), gathered per landmark
     double* lm_L;      // [6][WK]   (structure-of-arrays)   Cholesky factor of V_i (L00 L10 L11 L20 L21 L22)
@@ -84,9 +91,9 @@ struct BaPair {
     double* X;
     uint32_t* kf_desc;
     int64_t* gid;
-    int32_t *remap, *cnt, *li, *lm_id, *camobs, *obs_cam, *obs_k, *obs_id, *cam_off, *counts, *tiles;
+    int32_t *remap, *cnt, *li, *lm_id, *camobs, *obs_cam, *obs_k, *obs_id, *cam_off, *counts, *tiles, *lo_o;
     uint8_t* keep;
-    double *obs_W, *obs_Ug, *obs_Vg, *lm_L, *lm_gp, *part, *C, *cam_U, *dc, *flops;
+    double *lo_uvd, *lo_W, *Xc, *obs_Ug, *obs_Vg, *lm_L, *lm_gp, *part, *C, *cam_U, *dc, *flops;
 };
 
 __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, int p) {
@@ -106,7 +113,7 @@ __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, in
     q.obs_cam = s.obs_cam; q.obs_k = s.obs_k; q.obs_id = s.obs_id; q.cam_off = s.cam_off;
     q.counts = s.counts + 4 * p;
     q.tiles = s.tiles;
-    q.obs_W = s.obs_W; q.obs_Ug = s.obs_Ug; q.obs_Vg = s.obs_Vg; q.lm_L = s.lm_L; q.lm_gp = s.lm_gp; q.part = s.part; q.C = s.C;
+    q.lo_o = s.lo_o; q.lo_uvd = s.lo_uvd; q.lo_W = s.lo_W; q.Xc = s.Xc; q.obs_Ug = s.obs_Ug; q.obs_Vg = s.obs_Vg; q.lm_L = s.lm_L; q.lm_gp = s.lm_gp; q.part = s.part; q.C = s.C;
     q.cam_U = s.cam_U; q.dc = s.dc; q.flops = s.flops;
     return q;
 }
