@@ -325,7 +325,9 @@ __device__ __forceinline__ uint32_t fast4_maybe(const uint8_t* rc, int W, int x0
 // aligned-dword fast4, written as the quad's score word.  Wave-local (no block barrier).
 #define TS_DET_Q 128   // per-wave candidate queue (quads): flushed at 64, + <= 64 per append
 #ifndef TS_DET_U
-#define TS_DET_U 4     // phase-A items per lane per iteration
+#define TS_DET_U 2     // phase-A items per lane per iteration: 2 / 3 / 4 -> 71 / 79 / 80+5 spilled VGPRs;
+                       // 467 / 466 / 478 us alone, 931 / 957 / 978 us beside the back end, C2 bench
+                       // 145.0k / 143.1k / 141.6k frames/s (round 2)
 #endif
 __device__ __forceinline__ void fast_flush(const uint32_t* q, int cnt, const uint8_t* tile, uint32_t* score32, int W,
                                            int te) {
@@ -682,7 +684,7 @@ __device__ __forceinline__ void detect_body(const BatchCtx& c) {
         if (s_hist[i]) atomicAdd(&gh[i], s_hist[i]);
 }
 
-// 6 waves per SIMD (VGPRs <= 80, 6 spilled dwords): three 512-thread blocks per CU, as the LDS
+// 6 waves per SIMD (VGPRs <= 80; 71 without spills at TS_DET_U = 2): three 512-thread blocks per CU, as the LDS
 // allows, instead of two at 84 VGPRs (567 -> 528 us per 256-frame batch alone)
 __global__ __launch_bounds__(TS_DET_THREADS) __attribute__((amdgpu_waves_per_eu(6))) void k_detect(BatchCtx c) {
     detect_body<0>(c);
