@@ -1,6 +1,8 @@
-"""One rank of tests/test_gpu_shard.py::test_dist_shard_gloo_two_processes (launched by
-torch.distributed.run): the 2-pair bracket rig sharded over WORLD_SIZE processes with
-DistShardedRig on the gloo backend; writes its per-batch poses to <out>/rank<r>.json."""
+"""One rank of tests/test_gpu_shard.py's DistShardedRig tests (launched by torch.distributed.run):
+the 2-pair bracket rig sharded over WORLD_SIZE processes with DistShardedRig on the gloo backend
+(host-staged) or the nccl (RCCL) backend; writes its per-batch poses to <out>/rank<r>.json.
+
+usage: shard_worker.py OUT BATCH NB [gloo|nccl]"""
 
 from __future__ import annotations
 
@@ -19,9 +21,13 @@ from thor_slam_amd.shard import DistShardedRig
 
 def main() -> None:
     out, batch, nb = Path(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
-    dist.init_process_group("gloo")
-    rank, world = dist.get_rank(), dist.get_world_size()
+    backend = sys.argv[4] if len(sys.argv) > 4 else "gloo"
     torch.cuda.set_device(0)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
     sc = rig_scene(("192.168.2.21", "192.168.2.25"), batch * nb)
     rig = DistShardedRig(sc["rects"], HipSlamConfig(), batch, base_T_rect=sc["E"])
     S = rig.plan.streams_per_rank

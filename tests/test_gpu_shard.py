@@ -115,6 +115,25 @@ def test_dist_shard_gloo_two_processes(tmp_path):
                     np.testing.assert_array_equal(np.array(got[b][part][k]), want[b][part][k], err_msg=f"{r} {b} {part}.{k}")
 
 
+def test_dist_shard_rccl_world_one(tmp_path):
+    """DistShardedRig on the nccl (RCCL) backend, the bench's multi-GPU path, with one process:
+    the all-to-all of images and stream blocks, the pose all-gather on its own communicator and
+    the stream / event ordering between them must reproduce the unsharded handle bit for bit
+    (more ranks need more GPUs than the test box has: RCCL refuses two ranks on one device)."""
+    batch, nb = 4, 3
+    sc = rig_scene(TWO, batch * nb)
+    want, _ = unsharded(sc, HipSlamConfig(), batch, nb)
+    env = dict(os.environ, PYTHONPATH=f"{ROOT}:{ROOT / 'thor-slam_amd'}:{ROOT / 'tests'}")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr=127.0.0.1",
+           "--master-port=29519", str(ROOT / "tests" / "shard_worker.py"), str(tmp_path), str(batch), str(nb), "nccl"]
+    subprocess.run(cmd, check=True, env=env, timeout=240)
+    got = json.loads((tmp_path / "rank0.json").read_text())
+    for b in range(nb):
+        for part in ("pairs", "rig"):
+            for k in ("T_rel", "T_abs", "stats"):
+                np.testing.assert_array_equal(np.array(got[b][part][k]), want[b][part][k], err_msg=f"{b} {part}.{k}")
+
+
 def test_rccl_driven_shard_world_one_identical():
     """The library's own RCCL driver (tslam_comm_init + tslam_submit_sharded) on a
     1-rank communicator: the sharded stage runner over the whole range, the pose-record pack /

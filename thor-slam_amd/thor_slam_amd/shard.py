@@ -311,6 +311,13 @@ class DistShardedRig:
         self.rk = RankShard(rects, cfg, self.plan, self.rank, base_T_rect, device, exchange)
         self.exchange = exchange
         self.on_device = dist.get_backend() == "nccl"
+        # The pose all-gather runs on a communicator of its own: one process group's collectives
+        # execute in issue order on one internal stream, so a gather waiting for batch s's back
+        # end would otherwise hold up batch s+1's image and stream-block exchanges behind it (the
+        # exchanges then could not overlap the back end).  Every rank issues both groups'
+        # collectives in the same order; RCCL kernels are a few blocks each, so the two can run
+        # side by side.
+        self.pose_group = dist.new_group(ranks=list(range(self.world)), backend="nccl") if self.on_device else None
         self.front_stream = torch.cuda.Stream(device=device, priority=-1 if front_priority else 0)
         self.back_stream = torch.cuda.Stream(device=device)
         self.x_stream = torch.cuda.Stream(device=device)
@@ -322,7 +329,9 @@ class DistShardedRig:
         torch, dist = self.torch, self.dist
         if self.on_device:
             with torch.cuda.stream(stream):
-                if kind == "pose" or self.exchange == "allgather":
+                if kind == "pose":
+                    w = dist.all_gather_into_tensor(recv, send, group=self.pose_group, async_op=True)
+                elif self.exchange == "allgather":
                     w = dist.all_gather_into_tensor(recv, send, async_op=True)
                 else:
                     w = dist.all_to_all_single(recv, send, async_op=True)
