@@ -490,6 +490,12 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     ba_done = [torch.cuda.Event(), torch.cuda.Event()] if c4 else None
     ba_issued = [False, False]
 
+    # kernels bracketed by HIP events inside the timed steps: every event pair is a marker on the
+    # GPU timeline, so by default only the dominant kernel's (detect; the roofline's live launch
+    # time) — the other kernels' durations come from the isolated runs after the timed region
+    timed_all = args.kernel_events == "all"
+    timed_set = set(args.kernel_events.split(",")) if not timed_all else set(names)
+
     def run(k: str, st) -> None:
         if k == "rig":
             h.run_rig(st.cuda_stream)
@@ -523,10 +529,11 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
             if k in BACK and first_back and bstream is not stream:
                 bstream.wait_stream(stream)
                 first_back = False
-            if evs is not None:
+            timed = evs is not None and (timed_all or k in timed_set)
+            if timed:
                 evs[i][0].record(st)
             run(k, st)
-            if evs is not None:
+            if timed:
                 evs[i][1].record(st)
         if bstream is not stream:
             back_done[s % 2].record(bstream)
@@ -587,10 +594,11 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
             iso_us[k] += e0.elapsed_time(e1) * 1e3 / n_iso
 
     # ---- per-kernel durations of the timed launches (HIP events on the launch stream) ----------
-    per_kernel_us = {k: 0.0 for k in names}
+    per_kernel_us = {}
     for evs in events:
         for i, k in enumerate(names):
-            per_kernel_us[k] += evs[i][0].elapsed_time(evs[i][1]) * 1e3 / args.steps  # us
+            if timed_all or k in timed_set:
+                per_kernel_us[k] = per_kernel_us.get(k, 0.0) + evs[i][0].elapsed_time(evs[i][1]) * 1e3 / args.steps  # us
     unit_bytes = (frame_bytes(rect.width, rect.height, cfg.n_features, n_img=1, channels=5, matchings=1) if c5 else
                   frame_bytes(rect.width, rect.height, cfg.n_features, n_img=2 * P, n_pairs=P))
     dom_bytes = unit_bytes * B          # §8d per-frame bytes x the frames one launch processes
@@ -643,6 +651,7 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
         "algorithmic_bytes_per_frame": unit_bytes,
         "frames_per_launch": B,
         "avg_launch_us": per_kernel_us[dom],
+        "largest_isolated_kernel": max(iso_us, key=iso_us.get),
         "kernel_own_bytes_per_launch": None if c5 else kernel_bytes(dom, B, h, cfg, rect.is_identity, n_img),
         "end_to_end_hbm_frac": unit_bytes * (frames_total / elapsed / world) / (HBM_PEAK_GBS * 1e9),
         "valu": valu,
@@ -871,6 +880,9 @@ def main() -> None:
     ap.add_argument("--tsdf", type=int, default=0,
                     help="c5: also integrate every batch's depth into a TSDF volume with the device poses "
                          "(nvblox-shaped dense map, SURVEY.md §8f item 4); reported under dense_map")
+    ap.add_argument("--kernel-events", type=str, default="detect,local_ba,tsdf",
+                    help="kernels timed with HIP events inside the timed steps: 'all' or a comma list "
+                         "(default: the roofline kernel detect, C4 BA stage, C5 TSDF)")
     ap.add_argument("--pmc", type=str, default=str(ROOT / "profiles" / "pmc_latest.json"),
                     help="PMC summary (tools/pmc_summary.py) used for roofline.traffic when its batch matches")
     args = ap.parse_args()

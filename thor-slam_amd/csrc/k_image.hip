@@ -799,14 +799,17 @@ __device__ __forceinline__ void select_body(const BatchCtx& c) {
     const int Kl = c.g.Kq[l];
     const uint32_t* cand = c.cand + ((size_t)f * c.C + cam) * c.g.cand_total + c.g.cand_off[l];
     const uint32_t* cnt = c.ccount + ((size_t)f * c.C + cam) * c.g.total_bands + c.g.band_start[l];
-    const uint32_t* gh = c.hist + (((size_t)f * c.C + cam) * c.g.n_levels + l) * 256;
+    uint32_t* gh = c.hist + (((size_t)f * c.C + cam) * c.g.n_levels + l) * 256;
     const int nb = c.g.nbands[l];
     const int cap = c.g.cand_cap[l];
 
     // band counts -> exclusive prefix (flat candidate index i lives in band b with
     // s_pref[b] <= i < s_pref[b+1]); every pass below is then one flat, independent-load sweep
     // over the level's candidates (a per-band loop serialised ~25 dependent global round trips)
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_h[i] = gh[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        s_h[i] = gh[i];
+        gh[i] = 0u;   // back to zero for the next detect of this image-level (fallback or next batch)
+    }
     for (int i = threadIdx.x; i < SEL_THREADS; i += blockDim.x) s_part[i] = i < nb ? cnt[i] : 0u;
     __syncthreads();
     for (int o = 1; o < SEL_THREADS; o <<= 1) {
@@ -1028,22 +1031,9 @@ void launch_rectify_pyramid(const BatchCtx& c, hipStream_t s) {
 void launch_detect(const BatchCtx& c, hipStream_t s) {
     const size_t lds = (size_t)c.g.det_lds;
     dim3 grid(c.g.total_bands, c.n * c.ncam);
-    const size_t per_cam = sizeof(uint32_t) * 256 * c.g.n_levels;   // hist [B][C][L][256]: the view's cameras
-    if (c.ncam == c.C)
-        (void)hipMemsetAsync(c.hist, 0, per_cam * c.C * (size_t)c.n, s);
-    else
-        (void)hipMemset2DAsync(reinterpret_cast<uint8_t*>(c.hist) + per_cam * c.cam0, per_cam * c.C, 0, per_cam * c.ncam, c.n, s);
+    // hist [B][C][L][256] is zero here: zeroed at allocation, and every select (speculative or
+    // fallback) zeroes its image-level's histogram once it has read it
     hipLaunchKernelGGL(k_detect, grid, dim3(TS_DET_THREADS), lds, s, c);
-}
-
-// hist of the flagged images back to zero before their fallback detect (it accumulates)
-__global__ void k_det_fallback_prep(BatchCtx c) {
-    const int img = blockIdx.x, l = blockIdx.y;
-    int f, cam;
-    view_image(c, img, &f, &cam);
-    const size_t fcl = ((size_t)f * c.C + cam) * c.g.n_levels + l;
-    if (!c.det_fail[fcl]) return;
-    c.hist[fcl * 256 + threadIdx.x] = 0u;
 }
 
 // next batch's te <- this batch's running minimum; the minimum restarts (view cameras)
@@ -1060,7 +1050,6 @@ void launch_select(const BatchCtx& c, hipStream_t s) {
     hipLaunchKernelGGL(k_select, grid, dim3(SEL_THREADS), 0, s, c);
     // fallback for images whose speculative threshold left fewer than K candidates: detect and
     // select again at t + 1, gated on the device flags (near-empty launches when none is set)
-    hipLaunchKernelGGL(k_det_fallback_prep, grid, dim3(256), 0, s, c);
     hipLaunchKernelGGL(k_detect_fallback, dim3(c.g.total_bands, c.n * c.ncam), dim3(TS_DET_THREADS), (size_t)c.g.det_lds, s, c);
     hipLaunchKernelGGL(k_select_fallback, grid, dim3(SEL_THREADS), 0, s, c);
     hipLaunchKernelGGL(k_det_thr_commit, dim3(1), dim3(256), 0, s, c);
