@@ -217,7 +217,10 @@ __device__ __forceinline__ h16x2 hmax3(h16x2 a, h16x2 b, h16x2 c) {
 // x0+3) pairs; a byte b becomes the f16 1024 + b (0x64 as its high byte, one v_perm per pair), so
 // every difference, min and max below is exact.  The 16 circle windows come from 3 dword LDS reads
 // per circle row + v_alignbyte; each 9-arc minimum is min3(min3 of 3, 3, 3) (v_pk_minimum3_f16).
-__device__ __forceinline__ uint32_t fast4(const uint8_t* rc, int W, int x0, int thr) {
+// SIDE: 1 = bright arcs only (max over arcs of min(I_p) - I_c), 2 = dark only, 3 = both (the
+// score).  A pixel whose other side cannot reach thr + 1 (phase A's test) has its score on one side.
+template <int SIDE>
+__device__ __forceinline__ uint32_t fast4s(const uint8_t* rc, int W, int x0, int thr) {
     // circle index k -> (dx, dy): 0 (0,-3) 1 (1,-3) 2 (2,-2) 3 (3,-1) 4 (3,0) 5 (3,1) 6 (2,2)
     // 7 (1,3) 8 (0,3) 9 (-1,3) 10 (-2,2) 11 (-3,1) 12 (-3,0) 13 (-3,-1) 14 (-2,-2) 15 (-1,-3)
     uint32_t win[16], cen;
@@ -258,29 +261,36 @@ __device__ __forceinline__ uint32_t fast4(const uint8_t* rc, int W, int x0, int 
         h16x2 p[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) p[k] = toh(win[k]);
-        h16x2 a3[16], b3[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            a3[k] = hmin3(p[k], p[(k + 1) & 15], p[(k + 2) & 15]);
-            b3[k] = hmax3(p[k], p[(k + 1) & 15], p[(k + 2) & 15]);
-        }
-        h16x2 a9[16], b9[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            a9[k] = hmin3(a3[k], a3[(k + 3) & 15], a3[(k + 6) & 15]);
-            b9[k] = hmax3(b3[k], b3[(k + 3) & 15], b3[(k + 6) & 15]);
-        }
-        h16x2 br = hmax3(a9[0], a9[1], a9[2]), dk = hmin3(b9[0], b9[1], b9[2]);
-#pragma unroll
-        for (int k = 3; k < 15; k += 2) {
-            br = hmax3(br, a9[k], a9[k + 1]);
-            dk = hmin3(dk, b9[k], b9[k + 1]);
-        }
-        br = __builtin_elementwise_maximum(br, a9[15]);
-        dk = __builtin_elementwise_minimum(dk, b9[15]);
         const h16x2 cc = toh(cen);
         const h16x2 zero = {(_Float16)0, (_Float16)0};
-        const h16x2 sc = hmax3(br - cc, cc - dk, zero) + (h16x2){(_Float16)1024, (_Float16)1024};
+        h16x2 sb = zero, sd = zero;
+        if (SIDE & 1) {
+            h16x2 a3[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) a3[k] = hmin3(p[k], p[(k + 1) & 15], p[(k + 2) & 15]);
+            h16x2 a9[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) a9[k] = hmin3(a3[k], a3[(k + 3) & 15], a3[(k + 6) & 15]);
+            h16x2 br = hmax3(a9[0], a9[1], a9[2]);
+#pragma unroll
+            for (int k = 3; k < 15; k += 2) br = hmax3(br, a9[k], a9[k + 1]);
+            br = __builtin_elementwise_maximum(br, a9[15]);
+            sb = br - cc;
+        }
+        if (SIDE & 2) {
+            h16x2 b3[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) b3[k] = hmax3(p[k], p[(k + 1) & 15], p[(k + 2) & 15]);
+            h16x2 b9[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) b9[k] = hmax3(b3[k], b3[(k + 3) & 15], b3[(k + 6) & 15]);
+            h16x2 dk = hmin3(b9[0], b9[1], b9[2]);
+#pragma unroll
+            for (int k = 3; k < 15; k += 2) dk = hmin3(dk, b9[k], b9[k + 1]);
+            dk = __builtin_elementwise_minimum(dk, b9[15]);
+            sd = cc - dk;
+        }
+        const h16x2 sc = hmax3(sb, sd, zero) + (h16x2){(_Float16)1024, (_Float16)1024};
         const uint32_t bits = __builtin_bit_cast(uint32_t, sc) & 0x03FF03FFu;   // (score, score) as u16
         const uint32_t s0 = bits & 0xFFFFu, s1 = bits >> 16;
         out |= (s0 > (uint32_t)thr ? s0 : 0u) << (8 * h);
@@ -294,7 +304,8 @@ __device__ __forceinline__ uint32_t fast4(const uint8_t* rc, int W, int x0, int 
 // indices {0, 8} and one of {4, 12}, so score >= te needs max(p0, p8) and max(p4, p12) >= c + te
 // (bright) or min(p0, p8) and min(p4, p12) <= c - te (dark).  4 pixels x0..x0+3 of tile row `rc`
 // (pitch W) from 5 dword LDS reads, on f16 pairs 1024 + byte (exact): bit j = pixel x0 + j may
-// reach te (~20 VALU per quad against ~270 for the exact scores).
+// reach te on the bright side, bit 4 + j on the dark side (~25 VALU per quad against ~270 for the
+// exact scores of both sides).
 __device__ __forceinline__ uint32_t fast4_maybe(const uint8_t* rc, int W, int x0, h16x2 te2) {
     const uint32_t* p = (const uint32_t*)(rc + x0);
     const int Wd = W >> 2;
@@ -312,36 +323,50 @@ __device__ __forceinline__ uint32_t fast4_maybe(const uint8_t* rc, int W, int x0
                                                          __builtin_elementwise_maximum(p4, p12));
         const h16x2 dmax = __builtin_elementwise_maximum(__builtin_elementwise_minimum(p0, p8),
                                                          __builtin_elementwise_minimum(p4, p12));
-        const h16x2 v = __builtin_elementwise_maximum(bmin - (c + te2), (c - te2) - dmax);   // >= 0: candidate
-        const uint32_t vb = ~__builtin_bit_cast(uint32_t, v);
+        const uint32_t vb = ~__builtin_bit_cast(uint32_t, bmin - (c + te2));   // sign clear: bright candidate
+        const uint32_t vd = ~__builtin_bit_cast(uint32_t, (c - te2) - dmax);   // dark candidate
         bits |= ((vb >> 15) & 1u) << h;
         bits |= ((vb >> 31) & 1u) << (h + 2);
+        bits |= ((vd >> 15) & 1u) << (h + 4);
+        bits |= ((vd >> 31) & 1u) << (h + 6);
     }
-    return bits;
+    return bits;   // bit j: pixel x0 + j may reach te bright; bit 4 + j: dark
 }
 
 // Phase B: exact scores (>= te, else 0) of the `cnt` (<= 64) candidate quads at q (entries
-// r << 16 | quad: score row r, columns 4 quad .. 4 quad + 3), one quad per lane with the dense
-// aligned-dword fast4, written as the quad's score word.  Wave-local (no block barrier).
-#define TS_DET_Q 128   // per-wave candidate queue (quads): flushed at 64, + <= 64 per append
+// r << 9 | quad: score row r, columns 4 quad .. 4 quad + 3), one quad per lane with the dense
+// aligned-dword fast4s of one side, combined by a byte-wise max into the quad's score word (zeroed
+// by phase A; a quad with candidates on both sides is in both queues).  92 % of the candidate quads
+// have candidates on one side only, so splitting the queue by side skips half the arc work.
+// Wave-local (no block barrier).
+#define TS_DET_Q 128   // per-wave, per-side candidate queue (quads): flushed at 64, + <= 64 per append
 #ifndef TS_DET_U
 #define TS_DET_U 2     // phase-A items per lane per iteration: 2 / 3 / 4 -> 71 / 79 / 80+5 spilled VGPRs;
                        // 467 / 466 / 478 us alone, 931 / 957 / 978 us beside the back end, C2 bench
                        // 145.0k / 143.1k / 141.6k frames/s (round 2)
 #endif
-__device__ __forceinline__ void fast_flush(const uint32_t* q, int cnt, const uint8_t* tile, uint32_t* score32, int W,
+__device__ __forceinline__ uint32_t bytes_max(uint32_t a, uint32_t b) {
+    typedef unsigned short u16v2 __attribute__((ext_vector_type(2)));
+    const u16v2 ae = __builtin_bit_cast(u16v2, a & 0x00FF00FFu), ao = __builtin_bit_cast(u16v2, (a >> 8) & 0x00FF00FFu);
+    const u16v2 be = __builtin_bit_cast(u16v2, b & 0x00FF00FFu), bo = __builtin_bit_cast(u16v2, (b >> 8) & 0x00FF00FFu);
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(ae, be)) |
+           (__builtin_bit_cast(uint32_t, __builtin_elementwise_max(ao, bo)) << 8);
+}
+template <int SIDE>
+__device__ __forceinline__ void fast_flush(const uint16_t* q, int cnt, const uint8_t* tile, uint32_t* score32, int W,
                                            int te) {
     const int lane = threadIdx.x & 63;
     if (lane >= cnt) return;
     const uint32_t e = q[lane];
-    const int r = (int)(e >> 16), x4 = (int)(e & 0xFFFFu), x0 = 4 * x4;
-    uint32_t sc4 = fast4(tile + (r + TS_DET_HALO - 1) * W, W, x0, te - 1);
+    const int r = (int)(e >> 9), x4 = (int)(e & 511u), x0 = 4 * x4;
+    uint32_t sc4 = fast4s<SIDE>(tile + (r + TS_DET_HALO - 1) * W, W, x0, te - 1);
     if (x0 < 3) sc4 &= 0xFFFFFFFFu << (8 * (3 - x0));                  // x >= 3
     if (x0 + 4 > W - 3) {                                              // x < W-3
         const int keep = max(W - 3 - x0, 0);
         sc4 &= keep >= 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u);
     }
-    score32[r * (W >> 2) + x4] = sc4;
+    uint32_t* w = score32 + r * (W >> 2) + x4;
+    *w = bytes_max(*w, sc4);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -402,7 +427,7 @@ __device__ __forceinline__ void detect_body(const BatchCtx& c) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ uint32_t s_hist[256];
     __shared__ uint32_t s_count;
-    __shared__ uint32_t s_q[TS_DET_WAVES][TS_DET_Q];
+    __shared__ uint16_t s_q[TS_DET_WAVES][2][TS_DET_Q];   // per wave: bright, dark candidate quads
     const int img = blockIdx.y;
     int f, cam;
     view_image(c, img, &f, &cam);
@@ -512,8 +537,9 @@ __device__ __forceinline__ void detect_body(const BatchCtx& c) {
         const int qa = (Mg - 1) >> 2, nq = ((W - Mg) >> 2) + 1 - qa;
         const _Float16 tef = (_Float16)te;
         const h16x2 te2 = {tef, tef};
-        uint32_t* q = s_q[wave];
-        int qn = 0;   // wave-uniform
+        uint16_t* qb = s_q[wave][0];
+        uint16_t* qd = s_q[wave][1];
+        int nqb = 0, nqd = 0;   // wave-uniform
         const int nitems = max(rb - ra, 0) * nq;
         // (row, quad) of item it = wave * 64 + lane + k * TS_DET_THREADS, stepped without a division;
         // TS_DET_U items per lane per iteration, so their 5 LDS reads each are in flight together
@@ -522,7 +548,7 @@ __device__ __forceinline__ void detect_body(const BatchCtx& c) {
         int r = ra + (wave * 64 + lane) / nq, x4 = qa + (wave * 64 + lane) % nq;
         for (int i0 = wave * 64; i0 < nitems; i0 += TS_DET_U * TS_DET_THREADS) {
             int ru[TS_DET_U], xu[TS_DET_U];
-            bool cand[TS_DET_U];
+            bool cb[TS_DET_U], cd[TS_DET_U];
 #pragma unroll
             for (int u = 0; u < TS_DET_U; ++u) {
                 ru[u] = r;
@@ -538,33 +564,40 @@ __device__ __forceinline__ void detect_body(const BatchCtx& c) {
             for (int u = 0; u < TS_DET_U; ++u) {
                 const bool active = i0 + u * TS_DET_THREADS + lane < nitems;
                 const int y = y0 - 1 + ru[u], x0 = 4 * xu[u];
-                cand[u] = false;
+                cb[u] = cd[u] = false;
                 if (active) {
                     if (y >= 3 && y < H - 3) {
                         uint32_t c4 = fast4_maybe(tile + (ru[u] + TS_DET_HALO - 1) * W, W, x0, te2);
-                        if (x0 < 3) c4 &= 0xFu << (3 - x0);                              // x >= 3
-                        if (x0 + 4 > W - 3) c4 &= (1u << max(W - 3 - x0, 0)) - 1u;        // x < W-3
-                        cand[u] = c4 != 0;
+                        if (x0 < 3) c4 &= 0x11u * ((0xFu << (3 - x0)) & 0xFu);          // x >= 3 (both nibbles)
+                        if (x0 + 4 > W - 3) c4 &= 0x11u * ((1u << max(W - 3 - x0, 0)) - 1u);   // x < W-3
+                        cb[u] = (c4 & 0xFu) != 0;
+                        cd[u] = (c4 >> 4) != 0;
                     }
-                    if (!cand[u]) score32[ru[u] * W4 + xu[u]] = 0;
+                    score32[ru[u] * W4 + xu[u]] = 0;   // the flushes max their scores into it
                 }
             }
 #pragma unroll
             for (int u = 0; u < TS_DET_U; ++u) {
-                const uint64_t bm = __ballot(cand[u]);
-                if (cand[u])
-                    q[qn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u))] =
-                        ((uint32_t)ru[u] << 16) | (uint32_t)xu[u];
-                qn += (int)__popcll(bm);
-                // a wave's LDS operations complete in issue order, and the queue is wave-private:
+                const uint32_t ent = ((uint32_t)ru[u] << 9) | (uint32_t)xu[u];
+                const uint64_t bb = __ballot(cb[u]), bd = __ballot(cd[u]);
+                if (cb[u]) qb[nqb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u))] = (uint16_t)ent;
+                if (cd[u]) qd[nqd + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bd >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bd, 0u))] = (uint16_t)ent;
+                nqb += (int)__popcll(bb);
+                nqd += (int)__popcll(bd);
+                // a wave's LDS operations complete in issue order, and the queues are wave-private:
                 // no fence between its entries' stores and the flush's loads
-                if (qn >= 64) {
-                    fast_flush(q + qn - 64, 64, tile, score32, W, te);
-                    qn -= 64;
+                if (nqb >= 64) {
+                    fast_flush<1>(qb + nqb - 64, 64, tile, score32, W, te);
+                    nqb -= 64;
+                }
+                if (nqd >= 64) {
+                    fast_flush<2>(qd + nqd - 64, 64, tile, score32, W, te);
+                    nqd -= 64;
                 }
             }
         }
-        if (qn > 0) fast_flush(q, qn, tile, score32, W, te);
+        if (nqb > 0) fast_flush<1>(qb, nqb, tile, score32, W, te);
+        if (nqd > 0) fast_flush<2>(qd, nqd, tile, score32, W, te);
     } else {
         for (int i = threadIdx.x; i < (BR + 2) * W; i += TS_DET_THREADS) {
             const int r = i / W, x = i - r * W;

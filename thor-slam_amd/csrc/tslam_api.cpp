@@ -229,7 +229,9 @@ static void build_geometry(tslam_handle* h) {
     const int det_budget = (2 * br0 + 10) * g.W[0];
     g.det_lds = 0;
     for (int l = 0; l < p.n_levels; ++l) {
-        const int maxr = l == 0 ? br0 : std::max(br0, std::min(128, (det_budget / g.W[l] - 10) / 2));
+        // <= 124 rows: detect's phase-B queue entries hold the score row (< 128) in 7 bits and the
+        // quad (< 512, so W <= 2044) in 9
+        const int maxr = l == 0 ? br0 : std::max(br0, std::min(124, (det_budget / g.W[l] - 10) / 2));
         const int nb = (g.H[l] + maxr - 1) / maxr;
         g.band_rows[l] = l == 0 ? br0 : ((g.H[l] + nb - 1) / nb + 1) & ~1;
         g.smooth_groups[l] = std::max(2, g.band_rows[l] / 16);
