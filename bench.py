@@ -60,6 +60,9 @@ METRIC_C5 = "RGB-D frames/sec (BGR+depth, detect+match+pose) @1280×720, one cam
 HBM_PEAK_GBS = 8000.0
 # VALU issue: 256 CUs x 4 SIMD-32, a wave64 instruction every 2 cycles per SIMD at 2.4 GHz
 VALU_PEAK_WINST = 256 * 4 * 2.4e9 / 2
+# C2 frames per step: 1024 amortises each launch's ramp and drain (measured on one MI355X, round 2:
+# 147.3k / 153.3k / 154.0k / 155.3k frames/s at B = 256 / 512 / 768 / 1024)
+C2_BATCH = 1024
 FP64_MFMA_PEAK_TFS = 78.6   # MI355X FP64 matrix peak (AMD spec; the microarch guide lists no FP64 row)
 # bench kernel label -> device symbol (rocprofv3 / PMC summaries); "pose" is k_corr+k_ransac+k_refine
 KERNEL_SYMBOL = {"rectify_pyramid": "k_rectify_pyramid", "detect": "k_detect", "select": "k_select",
@@ -432,7 +435,7 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     width, height = (1280, 800) if c4 else (1280, 720) if c5 else (640, 400)
     cfg = (HipSlamConfig(n_features=4000, ba_window=10, ba_kf_interval=5, ba_iters=5) if c4 else
            HipSlamConfig(rgbd=True) if c5 else HipSlamConfig())
-    B = args.batch or (50 if c4 else 128 if c5 else 256)
+    B = args.batch or (50 if c4 else 128 if c5 else 256 if c3 else C2_BATCH)
     args.unique = args.unique or (24 if (c4 or c5) else 48)
     workers = max(1, min(16, usable_cpus(), args.unique * (8 if c3 else 1)))
     t_r = time.perf_counter()
@@ -753,7 +756,7 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
     names = RIG_SOURCES if c3 else RIG_SOURCES[:world // 2]
     width, height = 640, 400
     cfg = HipSlamConfig()
-    B = args.batch or 256
+    B = args.batch or (256 if c3 else C2_BATCH)
     args.unique = args.unique or 48
     _, cams, pairs, rects, E = rig_setup(names, width, height)
     P, C = len(rects), 2 * len(rects)
@@ -862,7 +865,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="BASELINE.json configs[1] (c2), configs[2] (c3), configs[3] (c4) or configs[4] (c5)")
-    ap.add_argument("--batch", type=int, default=0, help="frames per step (0 = 256 for c2/c3, 50 for c4, 128 for c5)")
+    ap.add_argument("--batch", type=int, default=0, help="frames per step (0 = C2_BATCH for c2, 256 for c3, 50 for c4, 128 for c5)")
     ap.add_argument("--unique", type=int, default=0, help="distinct rendered frames, triangle-wave replay (0 = 48 / 24)")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU baseline (0 = skip)")
     ap.add_argument("--cpu-procs", type=int, default=0, help="oracle processes for the CPU baseline (0 = usable CPUs)")

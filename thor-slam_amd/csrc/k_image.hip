@@ -369,6 +369,72 @@ __device__ __forceinline__ void fast_flush(const uint16_t* q, int cnt, const uin
     *w = bytes_max(*w, sc4);
 }
 
+// 3x3 NMS of the `cnt` (<= 64) queued nonzero score quads at q (entries r << 9 | quad: score row
+// r = y - y0 + 1, pixels 4 quad .. 4 quad + 3), one quad per lane; survivors inside the margin
+// M <= x < W - M are appended to `cand` (one LDS atomic per wave) and counted in `hist`.
+// Wave-local (no block barrier).
+__device__ __forceinline__ void nms_flush(const uint16_t* q, int cnt, const uint32_t* sc32, int W4, int W, int M, int y0,
+                                          uint32_t* cand, uint32_t* count, uint32_t* hist) {
+    const int lane = threadIdx.x & 63;
+    constexpr uint32_t k64 = 0x64646464u;
+    const h16x2 half = {(_Float16)0.5, (_Float16)0.5};
+    uint32_t kbits = 0;   // bit j: pixel x0 + j survives
+    uint32_t P = 0;
+    int y = 0, x0 = 0;
+    if (lane < cnt) {
+        const uint32_t e = q[lane];
+        const int r = (int)(e >> 9), qq = (int)(e & 511u);
+        y = y0 - 1 + r;
+        x0 = 4 * qq;
+        const uint32_t* pm = sc32 + r * W4 + qq;
+        const uint32_t* pu = pm - W4;
+        const uint32_t* pd = pm + W4;
+        P = pm[0];
+        const uint32_t ua = pu[-1], ub = pu[0], uc = pu[1];
+        const uint32_t ma = pm[-1], mc = pm[1];
+        const uint32_t da = pd[-1], db = pd[0], dc = pd[1];
+        const uint32_t ul = __builtin_amdgcn_alignbyte(ub, ua, 3), ur = __builtin_amdgcn_alignbyte(uc, ub, 1);
+        const uint32_t ml = __builtin_amdgcn_alignbyte(P, ma, 3), mr = __builtin_amdgcn_alignbyte(mc, P, 1);
+        const uint32_t dl = __builtin_amdgcn_alignbyte(db, da, 3), dr = __builtin_amdgcn_alignbyte(dc, db, 1);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t sel = h ? 0x00070005u : 0x00060004u;
+            auto toh = [sel](uint32_t v) { return __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(v, k64, sel)); };
+            const h16x2 pp = toh(P);
+            const h16x2 before = hmax3(hmax3(toh(ul), toh(ub), toh(ur)), toh(ml), toh(ml));
+            const h16x2 after = hmax3(hmax3(toh(dl), toh(db), toh(dr)), toh(mr), toh(mr));
+            const h16x2 k = __builtin_elementwise_minimum((pp - before) - half, pp - after);
+            const uint32_t nb = ~__builtin_bit_cast(uint32_t, k);
+            kbits |= ((nb >> 15) & 1u) << h;
+            kbits |= ((nb >> 31) & 1u) << (h + 2);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (x0 + j < M || x0 + j >= W - M) kbits &= ~(1u << j);
+    }
+    uint64_t bm[4];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        bm[j] = __ballot((kbits >> j) & 1u);
+        tot += (uint32_t)__popcll(bm[j]);
+    }
+    if (tot == 0) return;   // wave-uniform
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(count, tot);
+    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if ((kbits >> j) & 1u) {
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm[j], 0u));
+            const uint32_t pv = (P >> (8 * j)) & 0xFFu;
+            cand[base + rank] = ((255u - pv) << 22) | ((uint32_t)y << 11) | (uint32_t)(x0 + j);
+            atomicAdd(&hist[255 - pv], 1u);
+        }
+        base += (uint32_t)__popcll(bm[j]);
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // A3 smoothing + A4 FAST/NMS candidates for one band of BR = g.band_rows rows of one level.
 // grid (total_bands, n*C), block 512 (8 waves).  LDS: image rows [y0-4, y0+BR+4) (row-clamped),
@@ -461,11 +527,17 @@ __device__ __forceinline__ void detect_body(const BatchCtx& c) {
         // LDS-DMA: each wave-instruction lands 1 KiB of the lane-linear tile, no VGPRs
         const int W16 = W >> 4, n16 = NR * W16;
         const uint4* s16 = (const uint4*)src;
+        // (row, chunk) of i = i0 + lane stepped without a division per chunk
+        const int dr = TS_DET_THREADS / W16, dx = TS_DET_THREADS - dr * W16;
+        int r = (wave * 64 + lane) / W16, x = wave * 64 + lane - r * W16;
         for (int i0 = wave * 64; i0 < n16; i0 += TS_DET_THREADS) {
-            const int i = i0 + lane;
-            if (i < n16) {
-                const int r = i / W16, x = i - r * W16;
+            if (i0 + lane < n16)
                 glds16(s16 + (size_t)min(max(y0 - TS_DET_HALO + r, 0), H - 1) * W16 + x, (uint4*)tile + i0);
+            r += dr;
+            x += dx;
+            if (x >= W16) {
+                x -= W16;
+                ++r;
             }
         }
     } else {
@@ -617,77 +689,35 @@ __device__ __forceinline__ void detect_body(const BatchCtx& c) {
     uint32_t* cand = c.cand + ((size_t)f * c.C + cam) * c.g.cand_total + c.g.cand_off[l] + (size_t)band * c.g.cand_cap[l];
     const int ylo = max(y0, M), yhi = min(y0 + BR, H - M);
     if (wide) {
-        // 4 pixels per lane: keep = p > max(4 earlier neighbours) && p >= max(4 later ones), on
-        // the two f16 pixel pairs (1024 + score, exact), no divergence; survivors are appended
-        // with one LDS atomic per wave and pixel slot
+        // Only quads with a nonzero score word can hold a survivor (~10 % of them at a learnt te),
+        // but a wave of 64 quads almost always has one, so a dense pass ran the whole test for
+        // every quad.  A scan over the score words (one LDS read + a ballot per quad) queues the
+        // nonzero quads in the wave's (now idle) phase-B queue; each 64 queued quads get the test:
+        // 4 pixels per lane, keep = p > max(4 earlier neighbours) && p >= max(4 later ones), on the
+        // two f16 pixel pairs (1024 + score, exact); survivors are appended with one LDS atomic
+        // per wave and pixel slot.  The candidate order in `cand` never mattered (select sorts by
+        // key, and the LDS atomics already made it arrival order).
         const int W4 = W >> 2;
         const uint32_t* sc32 = (const uint32_t*)score;
-        constexpr uint32_t k64 = 0x64646464u;
-        const h16x2 half = {(_Float16)0.5, (_Float16)0.5};
+        uint16_t* nq = s_q[wave][0];   // 2 * TS_DET_Q contiguous entries: phase B is done (barrier)
+        int nn = 0;                    // wave-uniform
         const int dr = TS_DET_THREADS / W4, dq = TS_DET_THREADS - dr * W4;
         int yy = (wave * 64 + lane) / W4, q = wave * 64 + lane - yy * W4;   // stepped without a division
         for (int i0 = wave * 64; i0 < (yhi - ylo) * W4;
              i0 += TS_DET_THREADS, yy += dr, q += dq, (q >= W4 ? (q -= W4, ++yy) : 0)) {
-            const int it = i0 + lane;
-            uint32_t kbits = 0;   // bit j: pixel x0 + j survives
-            int y = 0, x0 = 0;
-            uint32_t P = 0;
-            if (it < (yhi - ylo) * W4) {
-                y = ylo + yy;
-                x0 = 4 * q;
-                const int r = y - y0 + 1;
-                const uint32_t* pm = sc32 + r * W4 + q;
-                P = pm[0];
-                if (P && x0 + 4 > M && x0 < W - M) {
-                    const uint32_t* pu = pm - W4;
-                    const uint32_t* pd = pm + W4;
-                    const uint32_t ua = pu[-1], ub = pu[0], uc = pu[1];
-                    const uint32_t ma = pm[-1], mc = pm[1];
-                    const uint32_t da = pd[-1], db = pd[0], dc = pd[1];
-                    const uint32_t ul = __builtin_amdgcn_alignbyte(ub, ua, 3), ur = __builtin_amdgcn_alignbyte(uc, ub, 1);
-                    const uint32_t ml = __builtin_amdgcn_alignbyte(P, ma, 3), mr = __builtin_amdgcn_alignbyte(mc, P, 1);
-                    const uint32_t dl = __builtin_amdgcn_alignbyte(db, da, 3), dr = __builtin_amdgcn_alignbyte(dc, db, 1);
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const uint32_t sel = h ? 0x00070005u : 0x00060004u;
-                        auto toh = [sel](uint32_t v) { return __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(v, k64, sel)); };
-                        const h16x2 pp = toh(P);
-                        const h16x2 before = hmax3(hmax3(toh(ul), toh(ub), toh(ur)), toh(ml), toh(ml));
-                        const h16x2 after = hmax3(hmax3(toh(dl), toh(db), toh(dr)), toh(mr), toh(mr));
-                        const h16x2 k = __builtin_elementwise_minimum((pp - before) - half, pp - after);
-                        const uint32_t nb = ~__builtin_bit_cast(uint32_t, k);
-                        kbits |= ((nb >> 15) & 1u) << h;
-                        kbits |= ((nb >> 31) & 1u) << (h + 2);
-                    }
-                    // margin: M <= x < W - M
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        if (x0 + j < M || x0 + j >= W - M) kbits &= ~(1u << j);
-                }
-            }
-            // append: one LDS atomic per wave for its 4 pixel slots
-            uint64_t bm[4];
-            uint32_t tot = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                bm[j] = __ballot((kbits >> j) & 1u);
-                tot += (uint32_t)__popcll(bm[j]);
-            }
-            if (tot == 0) continue;   // wave-uniform
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(&s_count, tot);
-            base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if ((kbits >> j) & 1u) {
-                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm[j], 0u));
-                    const uint32_t pv = (P >> (8 * j)) & 0xFFu;
-                    cand[base + rank] = ((255u - pv) << 22) | ((uint32_t)y << 11) | (uint32_t)(x0 + j);
-                    atomicAdd(&s_hist[255 - pv], 1u);
-                }
-                base += (uint32_t)__popcll(bm[j]);
+            bool nz = false;
+            const int r = ylo + yy - y0 + 1;
+            if (i0 + lane < (yhi - ylo) * W4) nz = sc32[r * W4 + q] != 0u && 4 * q + 4 > M && 4 * q < W - M;
+            const uint64_t bm = __ballot(nz);
+            if (nz) nq[nn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u))] =
+                        (uint16_t)(((uint32_t)r << 9) | (uint32_t)q);
+            nn += (int)__popcll(bm);
+            if (nn >= 64) {
+                nms_flush(nq + nn - 64, 64, sc32, W4, W, M, y0, cand, &s_count, s_hist);
+                nn -= 64;
             }
         }
+        if (nn > 0) nms_flush(nq, nn, sc32, W4, W, M, y0, cand, &s_count, s_hist);
     } else {
         const int xspan = W - 2 * M, nchx = (xspan + 63) >> 6;
         for (int it = wave; it < (yhi - ylo) * nchx; it += TS_DET_WAVES) {
