@@ -333,6 +333,32 @@ __device__ __forceinline__ uint32_t fast4_maybe(const uint8_t* rc, int W, int x0
     return bits;   // bit j: pixel x0 + j may reach te bright; bit 4 + j: dark
 }
 
+// fast4_maybe reduced to the quad's two queue decisions: bit 0 = some pixel may reach te on the
+// bright side, bit 1 = on the dark side (a sign bit clear in either f16 pair), without the per-pixel
+// bits (~20 VALU fewer per item).  Valid where no pixel of the quad needs the x / y border masks.
+__device__ __forceinline__ uint32_t fast4_any(const uint8_t* rc, int W, int x0, h16x2 te2) {
+    const uint32_t* p = (const uint32_t*)(rc + x0);
+    const int Wd = W >> 2;
+    const uint32_t up = p[-3 * Wd], dn = p[3 * Wd];
+    const uint32_t a = p[-1], b = p[0], cc = p[1];
+    const uint32_t w4 = __builtin_amdgcn_alignbyte(cc, b, 3), w12 = __builtin_amdgcn_alignbyte(b, a, 1);
+    constexpr uint32_t k64 = 0x64646464u;
+    uint32_t ab = 0xFFFFFFFFu, ad = 0xFFFFFFFFu;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t sel = h ? 0x00070005u : 0x00060004u;
+        auto toh = [sel](uint32_t v) { return __builtin_bit_cast(h16x2, __builtin_amdgcn_perm(v, k64, sel)); };
+        const h16x2 p0 = toh(up), p8 = toh(dn), p4 = toh(w4), p12 = toh(w12), c = toh(b);
+        const h16x2 bmin = __builtin_elementwise_minimum(__builtin_elementwise_maximum(p0, p8),
+                                                         __builtin_elementwise_maximum(p4, p12));
+        const h16x2 dmax = __builtin_elementwise_maximum(__builtin_elementwise_minimum(p0, p8),
+                                                         __builtin_elementwise_minimum(p4, p12));
+        ab &= __builtin_bit_cast(uint32_t, bmin - (c + te2));   // sign clear: bright candidate
+        ad &= __builtin_bit_cast(uint32_t, (c - te2) - dmax);   // dark candidate
+    }
+    return ((~ab & 0x80008000u) != 0u ? 1u : 0u) | ((~ad & 0x80008000u) != 0u ? 2u : 0u);
+}
+
 // Phase B: exact scores (>= te, else 0) of the `cnt` (<= 64) candidate quads at q (entries
 // r << 9 | quad: score row r, columns 4 quad .. 4 quad + 3), one quad per lane with the dense
 // aligned-dword fast4s of one side, combined by a byte-wise max into the quad's score word (zeroed
@@ -354,16 +380,18 @@ __device__ __forceinline__ uint32_t bytes_max(uint32_t a, uint32_t b) {
 }
 template <int SIDE>
 __device__ __forceinline__ void fast_flush(const uint16_t* q, int cnt, const uint8_t* tile, uint32_t* score32, int W,
-                                           int te) {
+                                           int te, bool border) {
     const int lane = threadIdx.x & 63;
     if (lane >= cnt) return;
     const uint32_t e = q[lane];
     const int r = (int)(e >> 9), x4 = (int)(e & 511u), x0 = 4 * x4;
     uint32_t sc4 = fast4s<SIDE>(tile + (r + TS_DET_HALO - 1) * W, W, x0, te - 1);
-    if (x0 < 3) sc4 &= 0xFFFFFFFFu << (8 * (3 - x0));                  // x >= 3
-    if (x0 + 4 > W - 3) {                                              // x < W-3
-        const int keep = max(W - 3 - x0, 0);
-        sc4 &= keep >= 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u);
+    if (border) {   // margin < 7 only: a quad may hold pixels outside [3, W-3)
+        if (x0 < 3) sc4 &= 0xFFFFFFFFu << (8 * (3 - x0));                  // x >= 3
+        if (x0 + 4 > W - 3) {                                              // x < W-3
+            const int keep = max(W - 3 - x0, 0);
+            sc4 &= keep >= 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u);
+        }
     }
     uint32_t* w = score32 + r * (W >> 2) + x4;
     *w = bytes_max(*w, sc4);
@@ -607,6 +635,9 @@ __device__ __forceinline__ void detect_body(const BatchCtx& c) {
         const int Mg = c.margin;
         const int ra = max(0, Mg - y0), rb = min(BR + 2, H - Mg + 2 - y0);
         const int qa = (Mg - 1) >> 2, nq = ((W - Mg) >> 2) + 1 - qa;
+        // with Mg >= 7 every scored pixel lies in rows [Mg-1, H-Mg] and columns [4 qa, W-Mg+3]
+        // inside [3, H-3) x [3, W-3): the FAST border tests are needed only below that
+        const bool border = Mg < 7;
         const _Float16 tef = (_Float16)te;
         const h16x2 te2 = {tef, tef};
         uint16_t* qb = s_q[wave][0];
@@ -638,7 +669,11 @@ __device__ __forceinline__ void detect_body(const BatchCtx& c) {
                 const int y = y0 - 1 + ru[u], x0 = 4 * xu[u];
                 cb[u] = cd[u] = false;
                 if (active) {
-                    if (y >= 3 && y < H - 3) {
+                    if (!border) {
+                        const uint32_t m = fast4_any(tile + (ru[u] + TS_DET_HALO - 1) * W, W, x0, te2);
+                        cb[u] = (m & 1u) != 0u;
+                        cd[u] = (m & 2u) != 0u;
+                    } else if (y >= 3 && y < H - 3) {
                         uint32_t c4 = fast4_maybe(tile + (ru[u] + TS_DET_HALO - 1) * W, W, x0, te2);
                         if (x0 < 3) c4 &= 0x11u * ((0xFu << (3 - x0)) & 0xFu);          // x >= 3 (both nibbles)
                         if (x0 + 4 > W - 3) c4 &= 0x11u * ((1u << max(W - 3 - x0, 0)) - 1u);   // x < W-3
@@ -659,17 +694,17 @@ __device__ __forceinline__ void detect_body(const BatchCtx& c) {
                 // a wave's LDS operations complete in issue order, and the queues are wave-private:
                 // no fence between its entries' stores and the flush's loads
                 if (nqb >= 64) {
-                    fast_flush<1>(qb + nqb - 64, 64, tile, score32, W, te);
+                    fast_flush<1>(qb + nqb - 64, 64, tile, score32, W, te, border);
                     nqb -= 64;
                 }
                 if (nqd >= 64) {
-                    fast_flush<2>(qd + nqd - 64, 64, tile, score32, W, te);
+                    fast_flush<2>(qd + nqd - 64, 64, tile, score32, W, te, border);
                     nqd -= 64;
                 }
             }
         }
-        if (nqb > 0) fast_flush<1>(qb, nqb, tile, score32, W, te);
-        if (nqd > 0) fast_flush<2>(qd, nqd, tile, score32, W, te);
+        if (nqb > 0) fast_flush<1>(qb, nqb, tile, score32, W, te, border);
+        if (nqd > 0) fast_flush<2>(qd, nqd, tile, score32, W, te, border);
     } else {
         for (int i = threadIdx.x; i < (BR + 2) * W; i += TS_DET_THREADS) {
             const int r = i / W, x = i - r * W;
