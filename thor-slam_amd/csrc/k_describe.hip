@@ -27,33 +27,38 @@ __device__ __forceinline__ void glds16d(const void* src, void* wave_dst) {
                                      (__attribute__((address_space(3))) void*)wave_dst, 16, 0, 0);
 }
 
-// Copy rows [r0, r0 + nrows) x columns [c0, c0 + TS_DT_P) of a level (pitch W, H rows) into an
-// LDS image of pitch TS_DT_P.  Rows outside the level and words outside [0, W) are skipped (the
-// keypoint margin guarantees no keypoint reads them).
-__device__ __forceinline__ void stage_tile(const uint8_t* level, int W, int H, int r0, int c0, int nrows,
+// Copy rows [r0, r0 + nrows) x the first NLD of the NCH 16-byte chunks of columns [cs, cs + 16 NCH)
+// of a level (pitch W, H rows) into an LDS image of pitch 16 NCH (lane-linear: the LDS-DMA lands a
+// wave's 64 chunks contiguously; chunks NLD.. of a row are LDS pitch padding).  Rows outside the
+// level and chunks outside [0, W) are skipped (the keypoint margin guarantees no keypoint reads
+// them).
+template <int NCH, int NLD = NCH>
+__device__ __forceinline__ void stage_tile(const uint8_t* level, int W, int H, int r0, int cs, int nrows,
                                            uint8_t* lds, bool wide16) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (wide16) {
-        const int per_row = TS_DT_P / 16, n = nrows * per_row;
+        const int n = nrows * NCH;
         for (int i0 = wave * 64; i0 < n; i0 += TS_DT_THREADS) {
             const int i = i0 + lane;
             if (i < n) {
-                const int r = i / per_row, q = i - r * per_row;
-                const int y = r0 + r, x = c0 + 16 * q;
-                if (y >= 0 && y < H && x >= 0 && x + 16 <= W) glds16d(level + (size_t)y * W + x, lds + 16 * i0);
+                const int r = i / NCH, q = i - r * NCH;
+                const int y = r0 + r, x = cs + 16 * q;
+                if (q < NLD && y >= 0 && y < H && x >= 0 && x + 16 <= W) glds16d(level + (size_t)y * W + x, lds + 16 * i0);
             }
         }
     } else {
-        for (int i = threadIdx.x; i < nrows * TS_DT_P; i += TS_DT_THREADS) {
-            const int r = i / TS_DT_P, q = i - r * TS_DT_P;
-            const int y = r0 + r, x = c0 + q;
+        for (int i = threadIdx.x; i < nrows * 16 * NCH; i += TS_DT_THREADS) {
+            const int r = i / (16 * NCH), q = i - r * (16 * NCH);
+            const int y = r0 + r, x = cs + q;
             if (y >= 0 && y < H && x >= 0 && x < W) lds[i] = level[(size_t)y * W + x];
         }
     }
 }
 
 __global__ __launch_bounds__(TS_DT_THREADS) void k_describe(BatchCtx c) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_raw[TS_DT_RAW_ROWS * TS_DT_P];
+    // raw tile: the orientation discs' columns [x0 - 16, x0 + 144) only (10 chunks), + 1 row of
+    // slack for the masked bytes the last disc row's dword window reads past the row end
+    __shared__ __attribute__((aligned(16))) uint8_t s_raw[(TS_DT_RAW_ROWS + 1) * TS_DT_RAW_P];
     __shared__ __attribute__((aligned(16))) uint8_t s_smo[TS_DT_SMO_ROWS * TS_DT_P];
     __shared__ uint16_t s_list[TS_DT_W * TS_DT_H / 4];   // NMS keeps at most one per 2x2
     __shared__ uint32_t s_n;
@@ -96,9 +101,11 @@ __global__ __launch_bounds__(TS_DT_THREADS) void k_describe(BatchCtx c) {
     __syncthreads();
 
     const bool wide16 = ((W & 15) == 0) && ((c.g.pyr_off[l] & 15) == 0) && ((c.g.pyr_bytes & 15) == 0);
-    const int c0 = x0 - TS_DT_HX;
-    stage_tile(raw, W, H, y0 - 15, c0, TS_DT_RAW_ROWS, s_raw, wide16);
-    stage_tile(smo, W, H, y0 - 18, c0, TS_DT_SMO_ROWS, s_smo, wide16);
+    const int c0 = x0 - TS_DT_HX;        // smoothed tile's column origin (pitch TS_DT_P)
+    const int cr = x0 - 16;              // raw tile's column origin (pitch TS_DT_RAW_P)
+    stage_tile<TS_DT_RAW_P / 16>(raw, W, H, y0 - 15, cr, TS_DT_RAW_ROWS, s_raw, wide16);
+    // smoothed tile: BRIEF reads columns [x0 - 18, x0 + 146): chunks 0..11; chunk 12 is the pad
+    stage_tile<TS_DT_P / 16, (TS_DT_W + 2 * TS_DT_HX) / 16>(smo, W, H, y0 - 18, c0, TS_DT_SMO_ROWS, s_smo, wide16);
 
     // per-lane disc weights (pixel dx = 4w - 15 + j, dy = r - 15 of slot s = lane + 64 i)
     uint32_t wx[5], mk[5];
@@ -119,7 +126,7 @@ __global__ __launch_bounds__(TS_DT_THREADS) void k_describe(BatchCtx c) {
         wx[i] = a;
         mk[i] = m;
         dyl[i] = r - 15;
-        rofs[i] = min(r, 30) * TS_DT_P + 4 * w;   // LDS byte offset of the word (before the kp origin)
+        rofs[i] = min(r, 30) * TS_DT_RAW_P + 4 * w;   // LDS byte offset of the word (before the kp origin)
     }
     // wedge directions as doubles: |u| < 2^25 and |m| < 2^23, so every product and difference
     // below is an exact integer in f64 (< 2^53) and the sign tests equal the int64 ones
@@ -150,7 +157,7 @@ __global__ __launch_bounds__(TS_DT_THREADS) void k_describe(BatchCtx c) {
             if (pos[g] < 0) continue;
             const int x = rec[g].x & 0xFFFF, y = rec[g].x >> 16;
             // orientation: disc origin (x - 15, y - 15) in the raw tile
-            const int ob = (y - y0) * TS_DT_P + (x - 15 - c0);
+            const int ob = (y - y0) * TS_DT_RAW_P + (x - 15 - cr);
             const uint32_t sh = (uint32_t)ob & 3u;
             const uint8_t* obase = s_raw + (ob & ~3);
             int sx = 0, s1 = 0, sy = 0;

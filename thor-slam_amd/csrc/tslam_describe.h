@@ -20,4 +20,5 @@
 #endif
 #define TS_DT_P (TS_DT_W + 2 * TS_DT_HX + TS_DT_PAD)
 #define TS_DT_RAW_ROWS (TS_DT_H + 30)       // raw level: orientation disc radius 15
+#define TS_DT_RAW_P 160                     // raw tile pitch: columns [x0 - 16, x0 + 144), 10 x 16 B
 #define TS_DT_SMO_ROWS (TS_DT_H + 36)       // smoothed level: rotated BRIEF radius 18
