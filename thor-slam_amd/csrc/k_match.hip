@@ -3,7 +3,11 @@
 // and the integer-SAD sub-pixel refinements (A6b stereo disparity, A7a temporal position).
 // Bit-exact with oracle.match / oracle.stereo_subpixel / oracle.temporal_subpixel.
 //
-// k_match: one thread per query, 256 queries per block, 4 independent waves (no block barrier).
+// k_match: one thread per query, 256 queries per block, 4 waves.  Temporal blocks re-deal their
+// 256 y-sorted queries by x (one rank sort in LDS, the only block barrier), so each wave holds an
+// x-quartile: its queries' gate box then admits about half of the train columns, and each 64-train
+// tile is compacted by a ballot of the box test before any Hamming work (stereo blocks keep the
+// y order: their row band is what limits them).
 // The train side of a pair is wave-uniform, so its record and descriptor come through SCALAR
 // loads (constant address space, s_load_dwordx4/x8 into SGPRs, served by the scalar cache) and
 // feed the VALU as SGPR operands: each pair costs 8 v_xor + 8 v_bcnt and a few compares, with no
@@ -30,6 +34,8 @@ __device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
 __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     __shared__ uint8_t s_tile[4][64][TS_TILE_PITCH];   // per wave: min(distance, 254)[train jj][query lane]
     __shared__ uint32_t s_qi[4][64];
+    __shared__ uint32_t s_tr[4][64];    // per wave: the compacted tile's train keypoint indices
+    __shared__ uint32_t s_key[256];     // temporal: (x, slot) sort keys, then the dealt positions
     // blockIdx.y: the temporal blocks (the heavy ones: a window of rows, not a row band) of every
     // frame first, then the stereo blocks, so the short stereo blocks fill the launch's tail
     // (stereo-only launches, match_modes == 1: blockIdx.y = f * P + p, all stereo)
@@ -66,7 +72,26 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     const int Hl = c.g.H[l];
 
     // queries in y-sorted order: this block holds positions q0 .. q0+255 of the level
-    const int qpos = q0 + threadIdx.x;
+    int qpos = q0 + threadIdx.x;
+    if (mode == 1) {
+        // deal the block's queries by x: thread t takes the query of x-rank t (inactive slots,
+        // keyed past every x, stay last); keys are distinct, so the ranks are a permutation
+        const uint32_t key = qpos < qn ? (uint32_t)(qys[qpos].x & 0xFFFF) << 8 | threadIdx.x
+                                       : 0x1000000u | threadIdx.x;
+        s_key[threadIdx.x] = key;
+        __syncthreads();
+        int rank = 0;
+        const uint4* k4 = reinterpret_cast<const uint4*>(s_key);
+#pragma unroll 8
+        for (int i = 0; i < 64; ++i) {
+            const uint4 v = k4[i];
+            rank += (v.x < key) + (v.y < key) + (v.z < key) + (v.w < key);
+        }
+        __syncthreads();
+        s_key[rank] = (uint32_t)qpos;
+        __syncthreads();
+        qpos = (int)s_key[threadIdx.x];
+    }
     const bool active = qpos < qn;
     uint32_t q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int qx = 0, qy = 0, qi = 0;
@@ -81,17 +106,22 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     s_qi[wave][lane] = (uint32_t)qi;
     const int row_tol = c.mp.row_tol, dmax = c.mp.max_disp >> l, win = c.mp.window >> l;
     const int reach = mode == 0 ? row_tol : win;
-    // rows any query of this wave can match (queries are y-sorted)
-    int wy0, wy1;
+    // the box of this wave's queries: rows any of them can match (the train range) and columns
+    int wy0, wy1, wx0, wx1;
     {
         int a = active ? qy : (1 << 20), b = active ? qy : -1;
+        int ax = active ? qx : (1 << 20), bx = active ? qx : -1;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
             a = min(a, __shfl_xor(a, o, 64));
             b = max(b, __shfl_xor(b, o, 64));
+            ax = min(ax, __shfl_xor(ax, o, 64));
+            bx = max(bx, __shfl_xor(bx, o, 64));
         }
         wy0 = __builtin_amdgcn_readfirstlane(a);   // equal in every lane: make it provably uniform
         wy1 = __builtin_amdgcn_readfirstlane(b);
+        wx0 = __builtin_amdgcn_readfirstlane(ax);
+        wx1 = __builtin_amdgcn_readfirstlane(bx);
     }
     const bool wave_active = wy1 >= 0;
     const int wt0 = wave_active ? (int)trs[max(0, wy0 - reach)] : 0;
@@ -105,6 +135,8 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     // |y_q - y_t| <= row_tol; temporal |x_q - x_t| <= window and |y_q - y_t| <= window
     const int gx_lo = mode == 0 ? 1 : -win, gx_hi = mode == 0 ? dmax : win, gy_tol = mode == 0 ? row_tol : win;
     const uint32_t gx_span = (uint32_t)(gx_hi - gx_lo), gy_span = (uint32_t)(2 * gy_tol);
+    // a train column some query of the wave can reach: qx - tx in [gx_lo, gx_hi] for a wave qx
+    const uint32_t bx0 = (uint32_t)(wx0 - gx_hi), bx_span = (uint32_t)(wx1 - gx_lo - (wx0 - gx_hi));
     if (!active) qx = -(1 << 24);   // an inactive lane fails the x range test
     if (gx_hi < gx_lo) wt1 = wt0;   // empty disparity range at this level: nothing is eligible
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -115,16 +147,28 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     // 64 and publishes each train descriptor's best query with one global atomicMin per tile
     // (min is order-independent, so the result is deterministic).
     for (int jt = wt0; jt < wt1; jt += 64) {
-        const int jcount = min(64, wt1 - jt);
-        const uint32_t my_train = lane < jcount ? tys[jt + lane].z : 0u;   // phase 2's train (lane)
-        // phase 1: this lane's query against up to 64 train descriptors, each a wave-uniform
-        // record + descriptor in SGPRs; unrolled by 8 so 8 descriptors' scalar loads are in
-        // flight together
-        for (int jj0 = 0; jj0 < 64; jj0 += 8) {
+        // compaction: the tile's trains inside the wave's column box, in index order
+        bool inbox = false;
+        uint32_t tz = 0;
+        if (jt + lane < wt1) {
+            const uint4 r = tys[jt + lane];
+            inbox = (uint32_t)((int)(r.x & 0xFFFF) - (int)bx0) <= bx_span;
+            tz = r.z;
+        }
+        uint64_t tm = __ballot(inbox);
+        if (tm == 0) continue;
+        const int jcount = __popcll(tm);
+        if (inbox) s_tr[wave][__builtin_amdgcn_mbcnt_hi((uint32_t)(tm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)tm, 0u))] = tz;
+        const int jlast = jt + 63 - __builtin_clzll(tm);
+        // phase 1: this lane's query against the compacted trains, each a wave-uniform record +
+        // descriptor in SGPRs (index from the mask's lowest set bit); unrolled by 8 so 8
+        // descriptors' scalar loads are in flight together
+        for (int jj0 = 0; jj0 < jcount; jj0 += 8) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int jj = jj0 + u;
-                const int j = jt + min(jj, jcount - 1);
+                const int j = tm ? jt + __builtin_ctzll(tm) : jlast;
+                tm &= tm - 1;
                 const v4u rec = ctys[j];
                 const v4u a = ctdesc[2 * j], b = ctdesc[2 * j + 1];
                 // gate as two unsigned range tests (one v_sub + one v_cmp each; the train's
@@ -145,14 +189,14 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
                 best_key = min(best_key, key);
                 s_tile[wave][jj][lane] = (uint8_t)(elig ? min(dd, 254u) : 255u);
             }
-            if (jj0 + 8 >= jcount) break;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
-        // phase 2: transposed read, lane = train descriptor: (distance, query) minimum over
+        // phase 2: transposed read, lane = compacted train: (distance, query) minimum over
         // the wave's 64 queries, 4 queries per dword read (row pitch 68 B = 17 dwords, an
         // odd stride, so the 64 lanes hit 64 different banks), no cross-lane reduction
         if (lane < jcount) {
+            const uint32_t my_train = s_tr[wave][lane];
             uint32_t best = 0xFFFFFFFFu;
             const uint32_t* row = reinterpret_cast<const uint32_t*>(&s_tile[wave][lane][0]);
 #pragma unroll 4
