@@ -31,9 +31,9 @@ __device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
     return r;
 }
 
-__global__ __launch_bounds__(256) void k_match(BatchCtx c) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_match(BatchCtx c) {
     __shared__ uint8_t s_tile[4][64][TS_TILE_PITCH];   // per wave: min(distance, 254)[train jj][query lane]
-    __shared__ uint32_t s_qi[4][64];
+    __shared__ __attribute__((aligned(16))) uint32_t s_qi[4][64];
     __shared__ uint32_t s_tr[4][64];    // per wave: the compacted tile's train keypoint indices
     __shared__ uint32_t s_key[256];     // temporal: (x, slot) sort keys, then the dealt positions
     // blockIdx.y: the temporal blocks (the heavy ones: a window of rows, not a row band) of every
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
         __syncthreads();
         int rank = 0;
         const uint4* k4 = reinterpret_cast<const uint4*>(s_key);
-#pragma unroll 8
+#pragma unroll 4
         for (int i = 0; i < 64; ++i) {
             const uint4 v = k4[i];
             rank += (v.x < key) + (v.y < key) + (v.z < key) + (v.w < key);
@@ -197,26 +197,29 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
         // odd stride, so the 64 lanes hit 64 different banks), no cross-lane reduction
         if (lane < jcount) {
             const uint32_t my_train = s_tr[wave][lane];
+            // an ineligible pair's key (255 << 16 | query) exceeds every eligible one (distance
+            // <= 254), so a plain minimum is exact and "no eligible query" is best >= 255 << 16
             uint32_t best = 0xFFFFFFFFu;
             const uint32_t* row = reinterpret_cast<const uint32_t*>(&s_tile[wave][lane][0]);
-#pragma unroll 4
+            const uint4* qi4 = reinterpret_cast<const uint4*>(&s_qi[wave][0]);
+#pragma unroll 2
             for (int r4 = 0; r4 < 16; ++r4) {
                 const uint32_t d4 = row[r4];
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const uint32_t d = (d4 >> (8 * b)) & 0xFFu;
-                    const uint32_t key = (d << 16) | s_qi[wave][4 * r4 + b];
-                    best = (d != 0xFFu && key < best) ? key : best;
-                }
+                const uint4 qq = qi4[r4];
+                best = min(best, __builtin_amdgcn_ubfe(d4, 0, 8) << 16 | qq.x);
+                best = min(best, __builtin_amdgcn_ubfe(d4, 8, 8) << 16 | qq.y);
+                best = min(best, __builtin_amdgcn_ubfe(d4, 16, 8) << 16 | qq.z);
+                best = min(best, (d4 >> 24) << 16 | qq.w);
             }
-            if (best != 0xFFFFFFFFu) atomicMin(&c.tbest[mbase + my_train], best);
+            if (best < (255u << 16)) atomicMin(&c.tbest[mbase + my_train], best);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
     }
     if (active) {
-        c.qbest[mbase + qi] = best_key;
-        c.qsecond[mbase + qi] = second_key == 0xFFFFFFFFu ? 256u : (second_key >> 16);
+        const int qk = (int)s_qi[wave][lane];   // re-read: one VGPR less through the train loop
+        c.qbest[mbase + qk] = best_key;
+        c.qsecond[mbase + qk] = second_key == 0xFFFFFFFFu ? 256u : (second_key >> 16);
     }
 }
 
