@@ -55,6 +55,35 @@ __device__ __forceinline__ void stage_tile(const uint8_t* level, int W, int H, i
     }
 }
 
+// Per-lane orientation disc constants of slot s = lane + 64 i (i < 5): byte weights dx + 15 and
+// the 0/1 mask of the 4 pixels of dword w = s % 9 in disc row r = s / 9 (pixel dx = 4w - 15 + j,
+// dy = r - 15, inside the radius-15 disc), dy, and the word's LDS offset in the raw tile.  Built
+// at compile time: one 16-byte load per slot instead of the per-block disc arithmetic.
+struct DiscSlot {
+    uint32_t wx, mk;
+    int32_t dy, rofs;
+};
+struct DiscTable {
+    DiscSlot e[320];
+};
+constexpr DiscTable make_disc_table() {
+    DiscTable t{};
+    for (int s = 0; s < 320; ++s) {
+        const int r = s / 9, w = s - 9 * r;
+        uint32_t a = 0, m = 0;
+        for (int j = 0; j < 4; ++j) {
+            const int dx = 4 * w - 15 + j, dy = r - 15;
+            if (r < 31 && dx <= 15 && dx * dx + dy * dy <= 225) {
+                a |= (uint32_t)(dx + 15) << (8 * j);
+                m |= 1u << (8 * j);
+            }
+        }
+        t.e[s] = DiscSlot{a, m, r - 15, (r < 30 ? r : 30) * TS_DT_RAW_P + 4 * w};
+    }
+    return t;
+}
+__constant__ DiscTable c_disc = make_disc_table();
+
 __global__ __launch_bounds__(TS_DT_THREADS) void k_describe(BatchCtx c) {
     // raw tile: the orientation discs' columns [x0 - 16, x0 + 144) only (10 chunks), + 1 row of
     // slack for the masked bytes the last disc row's dword window reads past the row end
@@ -107,26 +136,16 @@ __global__ __launch_bounds__(TS_DT_THREADS) void k_describe(BatchCtx c) {
     // smoothed tile: BRIEF reads columns [x0 - 18, x0 + 146): chunks 0..11; chunk 12 is the pad
     stage_tile<TS_DT_P / 16, (TS_DT_W + 2 * TS_DT_HX) / 16>(smo, W, H, y0 - 18, c0, TS_DT_SMO_ROWS, s_smo, wide16);
 
-    // per-lane disc weights (pixel dx = 4w - 15 + j, dy = r - 15 of slot s = lane + 64 i)
+    // per-lane disc constants (slot s = lane + 64 i; see DiscTable)
     uint32_t wx[5], mk[5];
     int dyl[5], rofs[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
-        const int s = lane + 64 * i;
-        const int r = s / 9, w = s - 9 * r;
-        uint32_t a = 0, m = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int dx = 4 * w - 15 + j, dy = r - 15;
-            if (r < 31 && dx <= 15 && dx * dx + dy * dy <= 225) {
-                a |= (uint32_t)(dx + 15) << (8 * j);
-                m |= 1u << (8 * j);
-            }
-        }
-        wx[i] = a;
-        mk[i] = m;
-        dyl[i] = r - 15;
-        rofs[i] = min(r, 30) * TS_DT_RAW_P + 4 * w;   // LDS byte offset of the word (before the kp origin)
+        const uint4 d = reinterpret_cast<const uint4*>(&c_disc)[lane + 64 * i];
+        wx[i] = d.x;
+        mk[i] = d.y;
+        dyl[i] = (int)d.z;
+        rofs[i] = (int)d.w;
     }
     // wedge directions as doubles: |u| < 2^25 and |m| < 2^23, so every product and difference
     // below is an exact integer in f64 (< 2^53) and the sign tests equal the int64 ones
