@@ -189,8 +189,8 @@ __global__ __launch_bounds__(TS_DT_THREADS) void k_describe(BatchCtx c) {
                 s1 += mm;
                 sy += dyl[i] * mm;
             }
-            const int m10 = __builtin_amdgcn_readfirstlane(wave_sum_dpp(sx - 15 * s1));
-            const int m01 = __builtin_amdgcn_readfirstlane(wave_sum_dpp(sy));
+            const int m10 = wave_sum_dpp(sx - 15 * s1);
+            const int m01 = wave_sum_dpp(sy);
             const double d01 = (double)m01, d10 = (double)m10;
             const bool hit = lane < 30 && (wa0 * d01 - wa1 * d10) >= 0.0 && (wb0 * d01 - wb1 * d10) < 0.0;
             const uint64_t hm = __ballot(hit);

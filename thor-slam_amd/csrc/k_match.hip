@@ -31,6 +31,12 @@ __device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
     return r;
 }
 
+__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_match(BatchCtx c) {
     __shared__ uint8_t s_tile[4][64][TS_TILE_PITCH];   // per wave: min(distance, 254)[train jj][query lane]
     __shared__ __attribute__((aligned(16))) uint32_t s_qi[4][64];
@@ -185,7 +191,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                 dd = bcnt_acc(q[6] ^ b.z, dd);
                 dd = bcnt_acc(q[7] ^ b.w, dd);
                 const uint32_t key = elig ? ((dd << 16) | rec.z) : 0xFFFFFFFFu;
-                second_key = min(second_key, max(best_key, key));
+                second_key = med3_u32(best_key, second_key, key);   // = min(second, max(best, key)): best <= second
                 best_key = min(best_key, key);
                 s_tile[wave][jj][lane] = (uint8_t)(elig ? min(dd, 254u) : 255u);
             }

@@ -240,12 +240,17 @@ __device__ __forceinline__ uint32_t wave_min_dpp(uint32_t v) {
 
 // Wave-uniform sum via the same DPP row reduction (result in an SGPR).
 __device__ __forceinline__ int wave_sum_dpp(int v) {
-    v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
-    v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);
-    v += __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false);
-    v += __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false);
-    return (__builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16)) +
-           (__builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48));
+    // old = 0 (the identity) lets each step fuse into one v_add_u32_dpp; after the 4 row steps
+    // every lane holds its row's sum, row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) fold
+    // the rows into lane 63 — 6 VALU + 1 readlane instead of 4 DPP moves, 4 adds and 4 readlanes
+    // (exact: integer sums, every lane of the wave active)
+    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
+    return __builtin_amdgcn_readlane(v, 63);
 }
 
 // f64 DPP move (both halves) for the row reductions below.
