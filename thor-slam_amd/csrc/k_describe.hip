@@ -55,13 +55,15 @@ __device__ __forceinline__ void stage_tile(const uint8_t* level, int W, int H, i
     }
 }
 
-// Per-lane orientation disc constants of slot s = lane + 64 i (i < 5): byte weights dx + 15 and
-// the 0/1 mask of the 4 pixels of dword w = s % 9 in disc row r = s / 9 (pixel dx = 4w - 15 + j,
-// dy = r - 15, inside the radius-15 disc), dy, and the word's LDS offset in the raw tile.  Built
-// at compile time: one 16-byte load per slot instead of the per-block disc arithmetic.
+// Per-lane orientation disc constants of slot s = lane + 64 i (i < 5): byte weights dx + 15,
+// dy + 15 and the 0/1 mask of the 4 pixels of dword w = s % 9 in disc row r = s / 9 (pixel
+// dx = 4w - 15 + j, dy = r - 15, inside the radius-15 disc), and the word's LDS offset in the raw
+// tile.  Built at compile time: one 16-byte load per slot instead of the per-block disc
+// arithmetic.  The offset weights keep all three moment sums on v_dot4_u32_u8 (no 32-bit
+// multiplies): m10 = sum (dx + 15) I - 15 sum I, m01 = sum (dy + 15) I - 15 sum I.
 struct DiscSlot {
-    uint32_t wx, mk;
-    int32_t dy, rofs;
+    uint32_t wx, mk, wy;
+    int32_t rofs;
 };
 struct DiscTable {
     DiscSlot e[320];
@@ -70,15 +72,16 @@ constexpr DiscTable make_disc_table() {
     DiscTable t{};
     for (int s = 0; s < 320; ++s) {
         const int r = s / 9, w = s - 9 * r;
-        uint32_t a = 0, m = 0;
+        uint32_t a = 0, m = 0, b = 0;
         for (int j = 0; j < 4; ++j) {
             const int dx = 4 * w - 15 + j, dy = r - 15;
             if (r < 31 && dx <= 15 && dx * dx + dy * dy <= 225) {
                 a |= (uint32_t)(dx + 15) << (8 * j);
                 m |= 1u << (8 * j);
+                b |= (uint32_t)(dy + 15) << (8 * j);
             }
         }
-        t.e[s] = DiscSlot{a, m, r - 15, (r < 30 ? r : 30) * TS_DT_RAW_P + 4 * w};
+        t.e[s] = DiscSlot{a, m, b, (r < 30 ? r : 30) * TS_DT_RAW_P + 4 * w};
     }
     return t;
 }
@@ -137,14 +140,14 @@ __global__ __launch_bounds__(TS_DT_THREADS) void k_describe(BatchCtx c) {
     stage_tile<TS_DT_P / 16, (TS_DT_W + 2 * TS_DT_HX) / 16>(smo, W, H, y0 - 18, c0, TS_DT_SMO_ROWS, s_smo, wide16);
 
     // per-lane disc constants (slot s = lane + 64 i; see DiscTable)
-    uint32_t wx[5], mk[5];
-    int dyl[5], rofs[5];
+    uint32_t wx[5], mk[5], wy[5];
+    int rofs[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
         const uint4 d = reinterpret_cast<const uint4*>(&c_disc)[lane + 64 * i];
         wx[i] = d.x;
         mk[i] = d.y;
-        dyl[i] = (int)d.z;
+        wy[i] = d.z;
         rofs[i] = (int)d.w;
     }
     // wedge directions as doubles: |u| < 2^25 and |m| < 2^23, so every product and difference
@@ -179,18 +182,19 @@ __global__ __launch_bounds__(TS_DT_THREADS) void k_describe(BatchCtx c) {
             const int ob = (y - y0) * TS_DT_RAW_P + (x - 15 - cr);
             const uint32_t sh = (uint32_t)ob & 3u;
             const uint8_t* obase = s_raw + (ob & ~3);
-            int sx = 0, s1 = 0, sy = 0;
+            uint32_t sx = 0, s1 = 0, sy = 0;
 #pragma unroll
             for (int i = 0; i < 5; ++i) {
                 const uint32_t* wp = reinterpret_cast<const uint32_t*>(obase + rofs[i]);
                 const uint32_t v = __builtin_amdgcn_alignbyte(wp[1], wp[0], sh);
-                const int mm = (int)__builtin_amdgcn_udot4(mk[i], v, 0u, false);
-                sx = (int)__builtin_amdgcn_udot4(wx[i], v, (uint32_t)sx, false);
-                s1 += mm;
-                sy += dyl[i] * mm;
+                s1 = __builtin_amdgcn_udot4(mk[i], v, s1, false);
+                sx = __builtin_amdgcn_udot4(wx[i], v, sx, false);
+                sy = __builtin_amdgcn_udot4(wy[i], v, sy, false);
             }
-            const int m10 = wave_sum_dpp(sx - 15 * s1);
-            const int m01 = wave_sum_dpp(sy);
+            // per-lane sums < 2^17: 15 * s1 as one full-rate 24-bit multiply
+            const int s15 = (int)__umul24(s1, 15u);
+            const int m10 = wave_sum_dpp((int)sx - s15);
+            const int m01 = wave_sum_dpp((int)sy - s15);
             const double d01 = (double)m01, d10 = (double)m10;
             const bool hit = lane < 30 && (wa0 * d01 - wa1 * d10) >= 0.0 && (wb0 * d01 - wb1 * d10) < 0.0;
             const uint64_t hm = __ballot(hit);
@@ -217,11 +221,11 @@ __global__ __launch_bounds__(TS_DT_THREADS) void k_describe(BatchCtx c) {
                 words[2 * j + 1] = (uint32_t)(bm >> 32);
             }
             const int kidx = (int)rec[g].z;
-            if (lane < 8) {
-                uint32_t w = words[0];
+            // word j (wave-uniform) into lane j: 8 v_writelane
+            uint32_t w = 0;
 #pragma unroll
-                for (int j = 1; j < 8; ++j)
-                    if (lane == j) w = words[j];
+            for (int j = 0; j < 8; ++j) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(w) : "s"(words[j]), "i"(j));
+            if (lane < 8) {
                 desc[(size_t)kidx * 8 + lane] = w;
                 desc_ys[(size_t)(c.g.koff[l] + pos[g]) * 8 + lane] = w;
             }
