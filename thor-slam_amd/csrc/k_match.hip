@@ -435,28 +435,37 @@ __global__ __launch_bounds__(256) void k_refine_temporal(BatchCtx c) {
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // staged rows before the reads (own wave)
+    // sub-lane kx < 5 scores the 5 offsets (kx, ky = 0..4) of its column shift: each window row is
+    // realigned once (its 11 bytes from kx on) and serves every ky it meets (patch row dy = r - ky);
+    // the sums are integers, so the costs equal a per-offset loop's
     uint32_t key = 0xFFFFFFFFu;   // first minimum of (cost << 5 | offset) over this lane's offsets
-    if (j >= 0) {
-        for (int o = sub; o < 25; o += 8) {
-            const int kx = o % 5, ky = o / 5;
-            uint32_t s = 0;
+    if (j >= 0 && sub < 5) {
+        const int kx = sub, kh = kx >> 2;
+        const uint32_t sh = (uint32_t)(kx & 3);
+        const uint32_t* wb = reinterpret_cast<const uint32_t*>(&s_b[qslot][0]);
+        uint32_t s[5] = {0u, 0u, 0u, 0u, 0u};
 #pragma unroll
-            for (int dy = 0; dy < TS_RT_AROWS; ++dy) {
+        for (int r = 0; r < TS_RT_BROWS; ++r) {
+            // kx == 4: start one word later with no byte shift (the 4th word is then unused)
+            const uint32_t d0 = wb[4 * r + kh], d1 = wb[4 * r + kh + 1], d2 = wb[4 * r + kh + 2], d3 = wb[4 * r + 3 - kh];
+            const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+            const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+            const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh) & 0x00FFFFFFu;
+#pragma unroll
+            for (int ky = 0; ky < 5; ++ky) {
+                const int dy = r - ky;
+                if (dy < 0 || dy >= TS_RT_AROWS) continue;   // compile-time
                 const uint4 ra = s_a[qslot][dy];
-                const uint4 rb = s_b[qslot][dy + ky];
-                // window bytes kx .. kx+10 of the 15-byte row
-                const uint32_t b0 = __builtin_amdgcn_alignbyte(rb.y, rb.x, kx & 3);
-                const uint32_t b1 = __builtin_amdgcn_alignbyte(rb.z, rb.y, kx & 3);
-                const uint32_t b2 = __builtin_amdgcn_alignbyte(rb.w, rb.z, kx & 3);
-                const uint32_t b3 = rb.w >> (8 * (kx & 3));
-                const bool hi = kx >= 4;   // kx == 4: shift by a whole dword
-                const uint32_t w0 = hi ? b1 : b0, w1 = hi ? b2 : b1, w2 = (hi ? b3 : b2) & 0x00FFFFFFu;
-                s = __builtin_amdgcn_sad_u8(ra.x, w0, s);
-                s = __builtin_amdgcn_sad_u8(ra.y, w1, s);
-                s = __builtin_amdgcn_sad_u8(ra.z, w2, s);
+                s[ky] = __builtin_amdgcn_sad_u8(ra.x, w0, s[ky]);
+                s[ky] = __builtin_amdgcn_sad_u8(ra.y, w1, s[ky]);
+                s[ky] = __builtin_amdgcn_sad_u8(ra.z, w2, s[ky]);
             }
-            s_cost[qslot][o] = (int)s;
-            key = min(key, (s << 5) | (uint32_t)o);
+        }
+#pragma unroll
+        for (int ky = 0; ky < 5; ++ky) {
+            const int o = ky * 5 + kx;
+            s_cost[qslot][o] = (int)s[ky];
+            key = min(key, (s[ky] << 5) | (uint32_t)o);
         }
     }
 #pragma unroll
