@@ -326,17 +326,18 @@ __global__ __launch_bounds__(256) void k_refine_stereo(BatchCtx c) {
     uint32_t key = 0xFFFFFFFFu;
     if (j >= 0 && sub < 5) {
         const int kx = sub;   // window bytes kx .. kx+10: right patch centred at xr + kx - 2
+        // kx == 4: start one word later with no byte shift (the 4th word is then unused)
+        const int kh = kx >> 2;
+        const uint32_t sh = (uint32_t)(kx & 3);
+        const uint32_t* wb = reinterpret_cast<const uint32_t*>(&s_b[qslot][0]);
         uint32_t s = 0;
 #pragma unroll
         for (int dy = 0; dy < 11; ++dy) {
             const uint4 ra = s_a[qslot][dy];
-            const uint4 rb = s_b[qslot][dy];
-            const uint32_t b0 = __builtin_amdgcn_alignbyte(rb.y, rb.x, kx & 3);
-            const uint32_t b1 = __builtin_amdgcn_alignbyte(rb.z, rb.y, kx & 3);
-            const uint32_t b2 = __builtin_amdgcn_alignbyte(rb.w, rb.z, kx & 3);
-            const uint32_t b3 = rb.w >> (8 * (kx & 3));
-            const bool hi = kx >= 4;
-            const uint32_t w0 = hi ? b1 : b0, w1 = hi ? b2 : b1, w2 = (hi ? b3 : b2) & 0x00FFFFFFu;
+            const uint32_t d0 = wb[4 * dy + kh], d1 = wb[4 * dy + kh + 1], d2 = wb[4 * dy + kh + 2], d3 = wb[4 * dy + 3 - kh];
+            const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+            const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+            const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh) & 0x00FFFFFFu;
             s = __builtin_amdgcn_sad_u8(ra.x, w0, s);
             s = __builtin_amdgcn_sad_u8(ra.y, w1, s);
             s = __builtin_amdgcn_sad_u8(ra.z, w2, s);
