@@ -919,20 +919,24 @@ __device__ __forceinline__ void select_body(const BatchCtx& c) {
     if (threadIdx.x <= (unsigned)nb) s_pref[threadIdx.x] = threadIdx.x == 0 ? 0u : s_part[threadIdx.x - 1];
     __syncthreads();
     const int ncand = (int)s_pref[nb];
-    auto fetch = [&](int i) -> uint32_t {
-        int lo = 0, hi = nb;
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if ((int)s_pref[mid] <= i) lo = mid; else hi = mid;
-        }
-        return cand[(size_t)lo * cap + (i - (int)s_pref[lo])];
-    };
-    // sweep(fn): fn(key) for every candidate, 4 independent loads in flight per thread
+    // sweep(fn): fn(key) for every candidate, 4 independent loads in flight per thread.  A
+    // thread's indices only grow along a sweep, so its band (the b with s_pref[b] <= i <
+    // s_pref[b+1]; s_pref[nb] = ncand ends the walk) advances from the previous one instead of a
+    // binary search per candidate; band * cap < 2^21 (W, H <= 2047, tslam_create), so the address
+    // is a full-rate 24-bit multiply
     auto sweep = [&](auto&& fn) {
+        int lo = 0;
         for (int i0 = threadIdx.x; i0 < ncand; i0 += 4 * SEL_THREADS) {
             uint32_t k[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) k[u] = i0 + u * SEL_THREADS < ncand ? fetch(i0 + u * SEL_THREADS) : 0u;
+            for (int u = 0; u < 4; ++u) {
+                const int i = i0 + u * SEL_THREADS;
+                k[u] = 0u;
+                if (i < ncand) {
+                    while ((int)s_pref[lo + 1] <= i) ++lo;
+                    k[u] = cand[__umul24((uint32_t)lo, (uint32_t)cap) + (uint32_t)(i - (int)s_pref[lo])];
+                }
+            }
 #pragma unroll
             for (int u = 0; u < 4; ++u)
                 if (i0 + u * SEL_THREADS < ncand) fn(k[u]);
