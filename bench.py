@@ -174,13 +174,24 @@ def kernel_bytes(name: str, B: int, h, cfg, maps_identity: bool, n_img_per_frame
 
 
 # ---- CPU baseline (the oracle on the host cores) -------------------------------------------------
-def usable_cpus() -> int:
-    """CPUs this process may use: the affinity mask, capped at the pool's per-GPU share (16)."""
+def affinity_cpus() -> int:
+    """CPUs in this process's affinity mask."""
     try:
-        n = len(os.sched_getaffinity(0))
+        return len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(n, int(os.environ.get("TSLAM_CPU_SHARE", "16"))))
+        return os.cpu_count() or 1
+
+
+def cpu_share() -> int:
+    """The host CPUs one GPU's job gets on the GPU pool (16; TSLAM_CPU_SHARE): the box exposes the
+    whole node's cores (256 on the MI355X nodes) to every job, and its rules size worker pools to
+    this share."""
+    return max(1, int(os.environ.get("TSLAM_CPU_SHARE", "16")))
+
+
+def usable_cpus() -> int:
+    """CPUs this process may use: the affinity mask, capped at the per-GPU share."""
+    return max(1, min(affinity_cpus(), cpu_share()))
 
 
 def cpu_model() -> str:
@@ -282,11 +293,19 @@ def cpu_baseline(frames, rect_d, cfg, budget_s: float, procs: int, what: str) ->
     parts = split(procs)
     n, wall = _run_oracle(parts, rect_d, cfg_d, budget_s)
     n1, wall1 = _run_oracle(split(1), rect_d, cfg_d, max(3.0, budget_s / 2))
-    return {"value": n / wall, "unit": "frames/s", "cores": len(parts), "kind": "port",
+    node = os.cpu_count() or 1
+    rate = n / wall
+    return {"value": rate, "unit": "frames/s", "cores": len(parts), "kind": "port",
             "sample": f"{n} {what} ({len(parts)} process(es) x {budget_s:.0f} s, each replaying a contiguous chunk), "
                       f"NumPy oracle{' + local BA' if cfg.ba_window else ''}",
             "single_core": {"value": n1 / wall1, "cores": 1, "sample": f"{n1} frames, 1 process x {wall1:.0f} s"},
-            "usable_cpus": usable_cpus(), "host_cpus_visible": os.cpu_count(), "cpu_model": cpu_model()}
+            # the cores used are the per-GPU share of the node (pool rule: worker pools sized to
+            # it); the whole node's figure is the linear extrapolation of the measured per-process
+            # rate (frames are independent), stated as such
+            "per_gpu_share": {"cores": len(parts), "value": rate},
+            "node": {"cores": node, "affinity_cpus": affinity_cpus(), "value_extrapolated": rate / len(parts) * node,
+                     "method": "measured per-process rate x node cores (not run: the pool caps a job at its share)"},
+            "cpu_model": cpu_model()}
 
 
 # the synthetic room (8 x 8 x 3 m, FLU) in the tracking world (rect-left camera of frame 0, RDF):
@@ -858,6 +877,41 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
     return out
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def launch_command(n: int, argv: list[str], port: int, script: str | os.PathLike | None = None) -> list[str]:
+    """The torch.distributed.run command of an N-rank bench (one process per GPU, rendezvous on
+    127.0.0.1; each rank reads RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* from its env)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", str(script or ROOT / "bench.py"), *argv]
+
+
+def self_launch(n: int, argv: list[str], timeout_s: float, script: str | os.PathLike | None = None) -> int:
+    """Run the N ranks as a child process group and return its exit code (124 when it runs past
+    ``timeout_s``: the whole group is killed, so a rank stuck in RCCL init cannot hang the bench).
+    Rank 0's JSON line reaches stdout through the inherited descriptors."""
+    import signal
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                            "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC for RCCL on this host driver
+    cmd = launch_command(n, argv, free_port(), script)
+    proc = subprocess.Popen(cmd, env=env, start_new_session=True)
+    try:
+        return proc.wait(timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        print(f"bench: {n}-rank run exceeded {timeout_s:.0f} s; killing it", file=sys.stderr, flush=True)
+        os.killpg(proc.pid, signal.SIGKILL)
+        proc.wait()
+        return 124
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -888,7 +942,14 @@ def main() -> None:
                          "(default: the roofline kernel detect, C4 BA stage, C5 TSDF)")
     ap.add_argument("--pmc", type=str, default=str(ROOT / "profiles" / "pmc_latest.json"),
                     help="PMC summary (tools/pmc_summary.py) used for roofline.traffic when its batch matches")
+    ap.add_argument("--launch-timeout", type=float, default=1500.0,
+                    help="--gpus N > 1 without WORLD_SIZE: seconds before the self-launched ranks are killed")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # N ranks requested from a plain `python bench.py --gpus N`: launch them (before this
+        # process touches the GPU) and report rank 0's line
+        sys.exit(self_launch(args.gpus, sys.argv[1:], args.launch_timeout))
 
     import torch
     import torch.distributed as dist
@@ -898,15 +959,23 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if world > 1 and args.dist_backend == "nccl" and world > torch.cuda.device_count():
+        raise SystemExit(f"--gpus {world} over RCCL needs one GPU per rank ({torch.cuda.device_count()} visible); "
+                         "use --dist-backend gloo to rehearse several ranks on one GPU")
     if args.config == "c4" and world > 1:
         raise SystemExit("--config c4 is a single-GPU configuration")
     dev_index = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev_index)
     if world > 1:
+        import datetime
+
+        # a collective (or the communicator's eager init) that does not complete in this time
+        # aborts the rank with an error instead of hanging the job
+        tmo = datetime.timedelta(seconds=300)
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index), timeout=tmo)
         else:
-            dist.init_process_group(args.dist_backend)
+            dist.init_process_group(args.dist_backend, timeout=tmo)
     sharded = world > 1 and args.config in ("c2", "c3")
     out = run_sharded(args, world, rank, dev_index) if sharded else run_single(args, world, rank, dev_index)
     if world > 1:

@@ -21,7 +21,10 @@
  *   tslam_ba_read       <- the map/keyframe side of cuVSLAM (SlamEngine.get_map, interface.py:207) —
  *                          here: the A8 sliding keyframe window (poses, landmarks) of a pair
  *   tslam_set_shard ... one camera stream per GPU: the blocks a sharded rig
- *                          exchanges over RCCL (stream blocks, raw images, pose records)
+ *                          exchanges over RCCL (stream blocks, raw images, pair blocks, pose records)
+ *   tslam_comm_init,    <- cuVSLAM's multicam mode (launch/thor_visual_slam.launch.py:49,81) for a
+ *   tslam_group_create     rig spread over GPUs: the library's own driver of the sharded rig, one
+ *                          process per GPU (RCCL) or one process for all of them (RCCL clique)
  *
  * Conventions: every function returns 0 on success or a negative TSLAM_E* code;
  * tslam_last_error() returns a thread-local message for the last failure.  A handle is not
@@ -38,7 +41,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 9
+#define TSLAM_ABI_VERSION 10
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -285,8 +288,22 @@ int tslam_read_rig_poses(tslam_handle* h, int max_frames, double* T_rel, double*
  *   -> all-to-all (raw images + stream blocks) -> import_raw + unpack_streams -> MATCH, POSE
  *   -> pack_poses -> all-gather -> unpack_poses -> KERNEL_CHAIN -> end_batch.
  * Every rank then holds the same per-pair and rig poses as an unsharded handle fed all cameras.
- * Requires n % world == 0 per batch, stereo (not RGB-D), ba_window == 0. */
+ * Requires n % world == 0 per batch (tslam_begin_batch rejects other n) and ba_window == 0.
+ *
+ * RGB-D rigs (params.rgbd; each "pair" is one colour camera + its aligned depth, so a camera's
+ * back end needs no other camera) shard by camera only, and no image moves: begin_batch takes the
+ * rank's records [n][cam_hi - cam_lo][5*H*W]; RECTIFY .. DESCRIBE, MATCH and POSE track the rank's
+ * cameras over the whole batch; tslam_pack_pairs (its cameras, each peer's frame range) ->
+ * all-to-all -> tslam_unpack_pairs (the peers' cameras, its own range); KERNEL_RIG solves the rig
+ * pose of its range; then pack_poses -> all-gather -> unpack_poses -> KERNEL_CHAIN as above. */
 int tslam_set_shard(tslam_handle* h, int cam_lo, int cam_hi, int rank, int world);
+/* Bytes of one pair block (RGB-D sharding; per batch frame and camera: pose f64[68], stats i32[8],
+ * correspondences f64[K][8]). */
+int tslam_pair_block_bytes(tslam_handle* h, int64_t* bytes);
+/* Pair blocks of batch frames f0 .. f0+n_frames-1 x pairs [pair_lo, pair_hi) (frame-major) to / from
+ * device memory, inside a batch (pack after POSE, unpack before KERNEL_RIG). */
+int tslam_pack_pairs(tslam_handle* h, int f0, int n_frames, int pair_lo, int pair_hi, void* dst, void* stream);
+int tslam_unpack_pairs(tslam_handle* h, int f0, int n_frames, int pair_lo, int pair_hi, const void* src, void* stream);
 /* Bytes of one stream block (per frame and camera) and of one pose record (per frame). */
 int tslam_exchange_sizes(tslam_handle* h, int64_t* stream_block, int64_t* pose_record);
 /* Stream blocks of frames first_frame .. +n_frames-1 (global indices, ring-resident; frames < 0
@@ -310,16 +327,36 @@ int tslam_unpack_poses(tslam_handle* h, const void* src, void* stream);
  * tslam_comm_init: this handle (the whole rig: tslam_create_rig, or tslam_create + tslam_set_rig)
  *   joins the `world`-rank communicator as `rank` (one rank per GPU, the handle's device) and owns
  *   cameras [rank*C/world, (rank+1)*C/world) and batch frames [rank*B/world, (rank+1)*B/world)
- *   (C and max_batch divisible by world; stereo rigs without local BA).
+ *   (C and max_batch divisible by world; stereo or RGB-D rigs without local BA).
  * tslam_submit_sharded: one batch of max_batch frames of this rank's cameras ([B][C/world][H][W]
- *   u8 in HBM) on `stream`: front end of its cameras; raw images + stream blocks of the frames
- *   every other rank solves sent point to point; back end (+ rig pose) of its frame range; pose
- *   records all-gathered; the chain.  Every rank then reads the whole rig's poses with
- *   tslam_read_poses / tslam_read_rig_poses, identical to one handle fed all cameras.  The
- *   collectives are on `stream` after the kernels (nothing synchronises the host). */
+ *   u8 in HBM; RGB-D records [B][C/world][5*H*W]) once `stream` has them: front end of its
+ *   cameras; raw images + stream blocks of the frames every other rank solves sent point to point
+ *   (RGB-D: its cameras' pair blocks); back end (+ rig pose) of its frame range; pose records
+ *   all-gathered; the chain.  The library runs the phases on streams of its own — front (high
+ *   priority), exchange, back — with double-buffered exchange buffers, so batch s's image exchange
+ *   overlaps its front end and batch s+1's front end overlaps batch s's back end; `stream` then
+ *   waits for the batch.  Every rank then reads the whole rig's poses with tslam_read_poses /
+ *   tslam_read_rig_poses, identical to one handle fed all cameras.  Nothing synchronises the host. */
 int tslam_comm_unique_id(void* id128);
 int tslam_comm_init(tslam_handle* h, const void* id128, int rank, int world);
 int tslam_submit_sharded(tslam_handle* h, const uint8_t* images, void* stream);
+
+/* One process driving the whole sharded rig (the SlamEngine boundary on several GPUs): handles[r]
+ * (the same rig on every handle, one per rank, created on the rank's device) become ranks
+ * 0 .. n-1 of one driver, as after tslam_comm_init.
+ *   TSLAM_TRANSPORT_RCCL: an RCCL clique over the handles' devices (ncclCommInitAll; one device per
+ *     handle), all ranks' sends / receives issued inside one ncclGroupStart / ncclGroupEnd;
+ *   TSLAM_TRANSPORT_COPY: device-to-device copies (hipMemcpyAsync) instead of RCCL, same buffers and
+ *     ordering; several ranks may share a device (tests world > 1 on one GPU).
+ * tslam_group_submit: one batch; images[r] = rank r's cameras as for tslam_submit_sharded, streams[r]
+ *   (NULL array or entries = each device's null stream) orders the input and then waits for the batch.
+ * tslam_group_destroy before destroying the handles (they return to unsharded). */
+#define TSLAM_TRANSPORT_RCCL 0
+#define TSLAM_TRANSPORT_COPY 1
+typedef struct tslam_group tslam_group;
+int tslam_group_create(tslam_handle* const* handles, int n, int transport, tslam_group** out);
+int tslam_group_submit(tslam_group* g, const uint8_t* const* images, void* const* streams);
+int tslam_group_destroy(tslam_group* g);
 
 /* A8 window of stereo pair `pair` after the last enqueued solve (synchronises the device),
  * indexed by slot (slot = keyframe number mod ba_window): frames[W] (global frame, -1 = empty),

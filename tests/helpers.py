@@ -150,3 +150,29 @@ def scripted_sources():
         ScriptedSource("192.168.2.21", 1 / 30, 100.011, 0.004, seed=2),
         ScriptedSource("192.168.2.23", 1 / 15, 100.020, 0.002, seed=3),
     ]
+
+
+@functools.lru_cache(maxsize=2)
+def rgbd_rig_scene(names: tuple = ("192.168.2.21", "192.168.2.22", "192.168.2.23", "192.168.2.25"), n: int = 5,
+                   traj_len: int = 40, width: int = 1280, height: int = 720):
+    """The 4-camera RGB-D rig of BASELINE.json configs[4] on the brackets.urdf joints: product
+    undistortion, base_T_cam per camera and records [n][P][5*H*W] in the global camera order
+    (sorted source names; per source the colour camera, its depth aligned)."""
+    import json
+    from pathlib import Path
+
+    from thor_slam_amd.calib import rgbd_pairs, rgbd_undistort
+    from thor_slam_amd.rgbd import pack_rgbd
+    from thor_slam_amd.synthetic import synthetic_rgbd_rig
+
+    mats = json.loads((Path(__file__).parent / "golden" / "brackets_joints.json").read_text())
+    srcs, rig = synthetic_rgbd_rig(mats, names, width, height, traj_len)
+    cams = extract_cameras(rig.calibration, 2 * len(names))
+    pairs = rgbd_pairs(cams)
+    rects = [rgbd_undistort(cams[c]) for c, _ in pairs]
+    E = [cams[c].extrinsics.to_4x4_matrix() @ r.left_optical_T_rect() for (c, _), r in zip(pairs, rects)]
+    by_name = {s.name: s for s in srcs}
+    raw = [[by_name[cams[c].source_name].render_rgbd(i) for c, _ in pairs] for i in range(n)]
+    records = np.stack([np.stack([pack_rgbd(b, d) for b, d in fr]) for fr in raw])
+    return {"raw": raw, "records": records, "rects": rects, "E": E, "traj": srcs[0].trajectory,
+            "cams": cams, "pairs": pairs, "sources": srcs}

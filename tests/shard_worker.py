@@ -2,7 +2,10 @@
 the 2-pair bracket rig sharded over WORLD_SIZE processes with DistShardedRig on the gloo backend
 (host-staged) or the nccl (RCCL) backend; writes its per-batch poses to <out>/rank<r>.json.
 
-usage: shard_worker.py OUT BATCH NB [gloo|nccl]"""
+With a fifth argument ``rgbd`` the rig is the 4-camera RGB-D rig (one camera per rank at world 4,
+pair-block exchange) at 640x400.
+
+usage: shard_worker.py OUT BATCH NB [gloo|nccl] [rgbd]"""
 
 from __future__ import annotations
 
@@ -14,7 +17,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from helpers import rig_scene
+from helpers import rgbd_rig_scene, rig_scene
 from thor_slam_amd.params import HipSlamConfig
 from thor_slam_amd.shard import DistShardedRig
 
@@ -28,10 +31,16 @@ def main() -> None:
     else:
         dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
-    sc = rig_scene(("192.168.2.21", "192.168.2.25"), batch * nb)
-    rig = DistShardedRig(sc["rects"], HipSlamConfig(), batch, base_T_rect=sc["E"])
+    rgbd = len(sys.argv) > 5 and sys.argv[5] == "rgbd"
+    if rgbd:
+        sc = rgbd_rig_scene(n=batch * nb, width=640, height=400)
+        frames = sc["records"]
+    else:
+        sc = rig_scene(("192.168.2.21", "192.168.2.25"), batch * nb)
+        frames = sc["frames"]
+    rig = DistShardedRig(sc["rects"], HipSlamConfig(rgbd=rgbd), batch, base_T_rect=sc["E"])
     S = rig.plan.streams_per_rank
-    mine = torch.from_numpy(np.ascontiguousarray(sc["frames"][:, rank * S:(rank + 1) * S])).cuda()
+    mine = torch.from_numpy(np.ascontiguousarray(frames[:, rank * S:(rank + 1) * S])).cuda()
     res = []
     for b in range(nb):
         rig.step(mine[b * batch:(b + 1) * batch])

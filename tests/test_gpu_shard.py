@@ -158,3 +158,78 @@ def test_rccl_driven_shard_world_one_identical():
         assert_identical(got, want[b])
     assert (want[-1]["rig"]["stats"][:, 0] == 0).all()
     h.close()
+
+
+def _group_run(sc, cfg, world, batch, nb, transport):
+    import torch
+
+    from thor_slam_amd._lib import Handle, HandleGroup
+
+    hs = [Handle(sc["rects"], cfg, max_batch=batch) for _ in range(world)]
+    for h in hs:
+        h.set_rig(sc["E"])
+    grp = HandleGroup(hs, transport)
+    S = sc["frames"].shape[1] // world
+    parts = [torch.from_numpy(np.ascontiguousarray(sc["frames"][:, r * S:(r + 1) * S])).cuda() for r in range(world)]
+    out = []
+    for b in range(nb):
+        grp.submit([p[b * batch].data_ptr() for p in parts])
+        out.append([{"pairs": h.read_poses(batch), "rig": h.read_rig_poses(batch)} for h in hs])
+    grp.close()
+    for h in hs:
+        h.close()
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_library_driver_copy_transport_identical(world):
+    """The library's own sharded driver (tslam_group_*: the code behind tslam_submit_sharded) with
+    world ranks on this GPU and device copies for the collectives: raw-image staging per peer,
+    stream-block packing, imports, double-buffered exchange buffers, pose records and the chain ==
+    the unsharded handle, bit for bit, over 3 batches."""
+    batch, nb = 4, 3
+    sc = rig_scene(TWO, batch * nb)
+    cfg = HipSlamConfig()
+    want, _ = unsharded(sc, cfg, batch, nb)
+    got = _group_run(sc, cfg, world, batch, nb, "copy")
+    for b in range(nb):
+        for r in range(world):
+            assert_identical(got[b][r], want[b])
+
+
+def test_library_driver_c3_eight_ranks_identical():
+    """C3 through the library driver: 8 streams, one per rank, 8 ranks (copy transport)."""
+    batch, nb = 8, 2
+    sc = rig_scene(C3_SOURCES, batch * nb)
+    cfg = HipSlamConfig()
+    want, _ = unsharded(sc, cfg, batch, nb)
+    got = _group_run(sc, cfg, 8, batch, nb, "copy")
+    for b in range(nb):
+        for r in (0, 5, 7):
+            assert_identical(got[b][r], want[b])
+
+
+def test_library_driver_rccl_clique_one_device():
+    """tslam_group_create(RCCL): ncclCommInitAll clique (one device here), grouped sends /
+    receives and the all-gather on the pose communicator == the unsharded handle."""
+    batch, nb = 4, 3
+    sc = rig_scene(TWO, batch * nb)
+    cfg = HipSlamConfig()
+    want, _ = unsharded(sc, cfg, batch, nb)
+    got = _group_run(sc, cfg, 1, batch, nb, "rccl")
+    for b in range(nb):
+        assert_identical(got[b][0], want[b])
+
+
+def test_sharded_batch_must_divide_by_world():
+    """tslam_begin_batch refuses a batch that does not split into equal frame ranges."""
+    from thor_slam_amd._lib import Handle
+
+    sc = rig_scene(TWO, 4)
+    h = Handle(sc["rects"], HipSlamConfig(), max_batch=4)
+    h.set_shard(0, 2, 0, 2)
+    with pytest.raises(RuntimeError, match="divisible by world"):
+        h.begin_batch(1 << 20, 3)
+    h.begin_batch(1 << 20, 2)   # accepted (nothing launched)
+    h.end_batch()
+    h.close()

@@ -1,6 +1,6 @@
 // k_describe.hip — row A5 of SURVEY.md §8a: intensity-centroid orientation + rotated BRIEF-256.
 //
-// Tile-staged: a block owns a 128 x 32 tile of one level.  It copies the tile plus halo of the
+// Tile-staged: a block owns a 128 x 64 tile of one level.  It copies the tile plus halo of the
 // raw level (orientation) and of the smoothed level (BRIEF) into LDS with 16-byte LDS-DMA loads,
 // then serves every keypoint inside the tile from LDS, one wave per keypoint.  A wave-per-
 // keypoint design that fetched each 37x37 patch from L2 issued ~10 cache-line requests per

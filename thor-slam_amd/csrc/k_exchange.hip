@@ -108,3 +108,43 @@ void launch_pose_records(const BatchCtx& c, bool pack, int f0, int n, uint8_t* r
     if (pack) hipLaunchKernelGGL(k_pose_records<true>, dim3(n), dim3(256), 0, s, c, f0, rec);
     else hipLaunchKernelGGL(k_pose_records<false>, dim3(n), dim3(256), 0, s, c, f0, rec);
 }
+
+// pair block, per (batch frame, pair) of a camera-sharded RGB-D rig (each rank tracks its own
+// cameras over the whole batch; the rig pose of a frame range needs every camera's
+// correspondences): pose f64[68] | stats i32[8] | corr f64[K][8] (rows past stats[1] are not
+// copied).  The rig pose reads nothing else of a pair (k_rig_pose).
+static inline __host__ __device__ int64_t pair_block_size(int K) {
+    return (int64_t)TS_POSE_DOUBLES * 8 + TS_STATS_INTS * 4 + (int64_t)K * TS_CORR_DOUBLES * 8;
+}
+int64_t pair_block_bytes(const LevelGeom& g) { return pair_block_size(g.K); }
+
+// item = k * np + s: batch frame f0 + k, pair p0 + s
+template <bool PACK>
+__global__ __launch_bounds__(256) void k_pair_blocks(BatchCtx c, int f0, int p0, int np, uint8_t* blk) {
+    const int item = blockIdx.x;
+    const int f = f0 + item / np, p = p0 + item % np;
+    const int64_t K = c.g.K;
+    uint8_t* b = blk + (int64_t)item * pair_block_size((int)K);
+    const size_t fp = (size_t)f * c.P + p;
+    uint8_t* pose = reinterpret_cast<uint8_t*>(c.pose + fp * TS_POSE_DOUBLES);
+    uint8_t* stats = reinterpret_cast<uint8_t*>(c.stats + fp * TS_STATS_INTS);
+    uint8_t* corr = reinterpret_cast<uint8_t*>(c.corr + fp * K * TS_CORR_DOUBLES);
+    const int64_t so = (int64_t)TS_POSE_DOUBLES * 8, co = so + TS_STATS_INTS * 4;
+    if (PACK) {
+        copy_piece(b, pose, so);
+        copy_piece(b + so, stats, TS_STATS_INTS * 4);
+        const int n = min(max(c.stats[fp * TS_STATS_INTS + 1], 0), (int)K);
+        copy_piece(b + co, corr, (int64_t)n * TS_CORR_DOUBLES * 8);
+    } else {
+        copy_piece(pose, b, so);
+        copy_piece(stats, b + so, TS_STATS_INTS * 4);
+        const int n = min(max(reinterpret_cast<const int32_t*>(b + so)[1], 0), (int)K);
+        copy_piece(corr, b + co, (int64_t)n * TS_CORR_DOUBLES * 8);
+    }
+}
+
+void launch_pair_blocks(const BatchCtx& c, bool pack, int f0, int n_frames, int p0, int np, uint8_t* blk, hipStream_t s) {
+    const dim3 grid(n_frames * np);
+    if (pack) hipLaunchKernelGGL(k_pair_blocks<true>, grid, dim3(256), 0, s, c, f0, p0, np, blk);
+    else hipLaunchKernelGGL(k_pair_blocks<false>, grid, dim3(256), 0, s, c, f0, p0, np, blk);
+}

@@ -921,8 +921,8 @@ __device__ __forceinline__ void select_body(const BatchCtx& c) {
     const int ncand = (int)s_pref[nb];
     // sweep(fn): fn(key) for every candidate, 4 independent loads in flight per thread.  A
     // thread's indices only grow along a sweep, so its band (the b with s_pref[b] <= i <
-    // s_pref[b+1]; s_pref[nb] = ncand ends the walk) advances from the previous one instead of a
-    // binary search per candidate; band * cap < 2^21 (W, H <= 2047, tslam_create), so the address
+    // s_pref[b+1]; s_pref[nb] = ncand ends the walk) is found by walking forward from the
+    // previous candidate's band (no per-candidate search); band * cap < 2^21 (W, H <= 2047, tslam_create), so the address
     // is a full-rate 24-bit multiply
     auto sweep = [&](auto&& fn) {
         int lo = 0;

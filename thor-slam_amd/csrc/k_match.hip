@@ -45,12 +45,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     // blockIdx.y: the temporal blocks (the heavy ones: a window of rows, not a row band) of every
     // frame first, then the stereo blocks, so the short stereo blocks fill the launch's tail
     // (stereo-only launches, match_modes == 1: blockIdx.y = f * P + p, all stereo)
-    const int nfp = c.match_modes == 1 ? 0 : c.n * c.P;
+    const int nfp = c.match_modes == 1 ? 0 : c.n * c.npair;
     const int z = blockIdx.y;
     const int mode = z < nfp ? 1 : 0;
-    const int fp = z < nfp ? z : z - nfp;     // f * P + p
-    const int p = fp % c.P;
-    const int f = fp / c.P;
+    const int fl = z < nfp ? z : z - nfp;     // f * npair + (p - pair0)
+    const int p = c.pair0 + fl % c.npair;
+    const int f = fl / c.npair;
     const int64_t g = c.g0 + f;
     if (mode == 1 && g == 0) return;          // no previous frame
     if (mode == 0 && c.rgbd) return;          // RGB-D: depth replaces stereo matching
@@ -273,8 +273,8 @@ __global__ __launch_bounds__(256) void k_refine_stereo(BatchCtx c) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int K = c.g.K;
     int z, local;
-    if (!xcd_image_block(blockIdx.x, c.n * c.P, (K + TS_RS_QPB - 1) / TS_RS_QPB, &z, &local)) return;
-    const int p = z % c.P, f = z / c.P;
+    if (!xcd_image_block(blockIdx.x, c.n * c.npair, (K + TS_RS_QPB - 1) / TS_RS_QPB, &z, &local)) return;
+    const int p = c.pair0 + z % c.npair, f = z / c.npair;
     const int64_t g = c.g0 + f;
     const int slot = ring_slot(c, g);
     const int sub = lane & 7;
@@ -379,8 +379,8 @@ __global__ __launch_bounds__(256) void k_refine_temporal(BatchCtx c) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int K = c.g.K;
     int z, local;
-    if (!xcd_image_block(blockIdx.x, c.n * c.P, (K + TS_RT_QPB - 1) / TS_RT_QPB, &z, &local)) return;
-    const int p = z % c.P, f = z / c.P;
+    if (!xcd_image_block(blockIdx.x, c.n * c.npair, (K + TS_RT_QPB - 1) / TS_RT_QPB, &z, &local)) return;
+    const int p = c.pair0 + z % c.npair, f = z / c.npair;
     const int64_t g = c.g0 + f;
     const int slot = ring_slot(c, g);
     const int sub = lane & 7;
@@ -495,7 +495,7 @@ __global__ __launch_bounds__(256) void k_refine_temporal(BatchCtx c) {
 void launch_match(const BatchCtx& c, hipStream_t s) {
     (void)hipMemsetAsync(c.tbest, 0xFF, sizeof(uint32_t) * (size_t)c.n * c.P * 2 * c.g.K, s);
     (void)hipMemsetAsync(c.qbest, 0xFF, sizeof(uint32_t) * (size_t)c.n * c.P * 2 * c.g.K, s);
-    dim3 grid(c.g.total_qtiles, c.n * c.P * (c.match_modes == 1 ? 1 : 2));
+    dim3 grid(c.g.total_qtiles, c.n * c.npair * (c.match_modes == 1 ? 1 : 2));
     hipLaunchKernelGGL(k_match, grid, dim3(256), 0, s, c);
 }
 
@@ -506,8 +506,8 @@ void launch_match_stereo(const BatchCtx& c, hipStream_t s) {
     st.match_modes = 1;
     (void)hipMemsetAsync(st.tbest, 0xFF, sizeof(uint32_t) * (size_t)st.n * st.P * 2 * st.g.K, s);
     (void)hipMemsetAsync(st.qbest, 0xFF, sizeof(uint32_t) * (size_t)st.n * st.P * 2 * st.g.K, s);
-    hipLaunchKernelGGL(k_match, dim3(st.g.total_qtiles, st.n * st.P), dim3(256), 0, s, st);
-    hipLaunchKernelGGL(k_refine_stereo, dim3(xcd_grid(st.n * st.P, (st.g.K + TS_RS_QPB - 1) / TS_RS_QPB)), dim3(256), 0, s, st);
+    hipLaunchKernelGGL(k_match, dim3(st.g.total_qtiles, st.n * st.npair), dim3(256), 0, s, st);
+    hipLaunchKernelGGL(k_refine_stereo, dim3(xcd_grid(st.n * st.npair, (st.g.K + TS_RS_QPB - 1) / TS_RS_QPB)), dim3(256), 0, s, st);
 }
 
 void launch_match_refine(const BatchCtx& c, hipStream_t s) {
@@ -515,6 +515,6 @@ void launch_match_refine(const BatchCtx& c, hipStream_t s) {
     if (c.rgbd)
         launch_rgbd_depth(c, s);
     else
-        hipLaunchKernelGGL(k_refine_stereo, dim3(xcd_grid(c.n * c.P, (K + TS_RS_QPB - 1) / TS_RS_QPB)), dim3(256), 0, s, c);
-    hipLaunchKernelGGL(k_refine_temporal, dim3(xcd_grid(c.n * c.P, (K + TS_RT_QPB - 1) / TS_RT_QPB)), dim3(256), 0, s, c);
+        hipLaunchKernelGGL(k_refine_stereo, dim3(xcd_grid(c.n * c.npair, (K + TS_RS_QPB - 1) / TS_RS_QPB)), dim3(256), 0, s, c);
+    hipLaunchKernelGGL(k_refine_temporal, dim3(xcd_grid(c.n * c.npair, (K + TS_RT_QPB - 1) / TS_RT_QPB)), dim3(256), 0, s, c);
 }

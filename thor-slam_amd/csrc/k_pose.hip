@@ -252,9 +252,9 @@ __device__ __forceinline__ void write_stats(int32_t* so, int status, int n, int 
 // ---- k_corr: correspondences of one (frame, pair), ordered by the current keypoint index ------
 __global__ __launch_bounds__(POSE_THREADS) void k_corr(BatchCtx c) {
     __shared__ int s_scan[POSE_THREADS];
-    const int fp = blockIdx.x;
-    const int p = fp % c.P;
-    const int f = fp / c.P;
+    const int p = c.pair0 + (int)blockIdx.x % c.npair;   // (frame, pair) of the pair view
+    const int f = (int)blockIdx.x / c.npair;
+    const int fp = f * c.P + p;
     const int64_t g = c.g0 + f;
     const int tid = threadIdx.x;
     const int K = c.g.K;
@@ -324,10 +324,11 @@ __global__ __launch_bounds__(POSE_THREADS) void k_corr(BatchCtx c) {
 __global__ __launch_bounds__(POSE_THREADS) void k_p3p(BatchCtx c) {
     const int H = c.pp.n_hyp;
     const int gid = blockIdx.x * POSE_THREADS + threadIdx.x;
-    if (gid >= c.n * c.P * H) return;
-    const int fp = gid / H, h = gid - fp * H;
-    const int p = fp % c.P;
-    const int f = fp / c.P;
+    if (gid >= c.n * c.npair * H) return;
+    const int fl = gid / H, h = gid - fl * H;
+    const int p = c.pair0 + fl % c.npair;
+    const int f = fl / c.npair;
+    const int fp = f * c.P + p;
     const int64_t g = c.g0 + f;
     const int32_t* sout = c.stats + (size_t)fp * TS_STATS_INTS;
     if (sout[0] != 3) return;
@@ -378,10 +379,11 @@ __global__ __launch_bounds__(POSE_THREADS) void k_p3p(BatchCtx c) {
 __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
     __shared__ int s_cnt[4 * TS_MAX_HYP_SPLIT];
     __shared__ uint32_t s_wbest[4];
-    const int fp = blockIdx.x / S;
+    const int fl = blockIdx.x / S;
     const int split = blockIdx.x % S;
-    const int p = fp % c.P;
-    const int f = fp / c.P;
+    const int p = c.pair0 + fl % c.npair;
+    const int f = fl / c.npair;
+    const int fp = f * c.P + p;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int32_t* sout = c.stats + (size_t)fp * TS_STATS_INTS;
     uint32_t* kout = reinterpret_cast<uint32_t*>(c.ransac) + ((size_t)fp * S + split) * TS_RANSAC_WORDS;
@@ -479,9 +481,9 @@ __global__ __launch_bounds__(POSE_THREADS) void k_refine(BatchCtx c, int S) {
     __shared__ double s_red[4][N_ACC];
     __shared__ double s_R[9], s_t[3], s_H[36], s_misc[4];
     __shared__ int s_flag, s_best;
-    const int fp = blockIdx.x;
-    const int p = fp % c.P;
-    const int f = fp / c.P;
+    const int p = c.pair0 + (int)blockIdx.x % c.npair;
+    const int f = (int)blockIdx.x / c.npair;
+    const int fp = f * c.P + p;
     const int64_t g = c.g0 + f;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     int32_t* sout = c.stats + (size_t)fp * TS_STATS_INTS;
@@ -991,12 +993,51 @@ void launch_rig(const BatchCtx& c, hipStream_t s) {
     launch_rig_chain(c, s);
 }
 
+// The rig chain's IMU prediction per frame: the first pair with a translation prior (W_t > 0),
+// moved to the body frame, M = (E_p [R | t]) E_p^-1, in the prior record layout; weights kept.
+__global__ __launch_bounds__(256) void k_rig_prior(BatchCtx c) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= c.n) return;
+    double* out = c.rig_prior + (size_t)f * TS_PRIOR_DOUBLES;
+    int p = 0;
+    while (p < c.P && !(c.prior[((size_t)f * c.P + p) * TS_PRIOR_DOUBLES + 13] > 0.0)) ++p;
+    if (p == c.P) {
+        for (int i = 0; i < TS_PRIOR_DOUBLES; ++i) out[i] = 0.0;
+        return;
+    }
+    const double* pr = c.prior + ((size_t)f * c.P + p) * TS_PRIOR_DOUBLES;
+    double T[16], A[16], M[16];
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) T[4 * i + j] = pr[3 * i + j];
+        T[4 * i + 3] = pr[10 + i];
+        T[12 + i] = 0.0;
+    }
+    T[15] = 1.0;
+    mul4_fixed(c.rig_E + 16 * p, T, A);
+    mul4_fixed(A, c.rig_Einv + 16 * p, M);
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) out[3 * i + j] = M[4 * i + j];
+        out[10 + i] = M[4 * i + 3];
+    }
+    out[9] = pr[9];
+    out[13] = pr[13];
+    out[14] = out[15] = 0.0;
+}
+
 void launch_rig_chain(const BatchCtx& c, hipStream_t s) {
+    if (c.prior && c.rig_prior)
+        hipLaunchKernelGGL(k_rig_prior, dim3((c.n + 255) / 256), dim3(256), 0, s, c);
     BatchCtx r = c;   // chain the body motions with the pair chain kernel: one "pair", the rig
     r.pose = c.rig_pose;
     r.stats = c.rig_stats;
     r.state = c.rig_state;
     r.P = 1;
+    r.pair0 = 0;
+    r.npair = 1;
+    // the IMU priors are per (frame, pair) in each pair's rectified-left frame: the rig chain
+    // takes its body-frame prediction from c.rig_prior ([B][16], built by k_rig_prior), never the
+    // pair records
+    r.prior = c.prior ? c.rig_prior : nullptr;
     hipLaunchKernelGGL(k_chain, dim3(1), dim3(256), 0, s, r);
 }
 
@@ -1004,7 +1045,7 @@ int ransac_splits(const BatchCtx& c) {
     if (c.pp.splits > 0) return min(min(c.pp.splits, c.pp.n_hyp), TS_MAX_SPLITS);
     // scoring blocks (>= 4096: 64 waves per CU over the launch), at least 8 hypotheses per split
     // (measured at B = 256: S = 4 / 8 / 16 -> 325 / 295 / 283 us for the pose stage)
-    const int frames = c.n * c.P;
+    const int frames = c.n * c.npair;
     int S = (4096 + frames - 1) / frames;
     S = max(1, min(S, max(1, c.pp.n_hyp / 8)));
     return min(S, TS_MAX_SPLITS);
@@ -1012,18 +1053,18 @@ int ransac_splits(const BatchCtx& c) {
 
 void launch_pose(const BatchCtx& c, hipStream_t s) {
     const int S = ransac_splits(c);
-    hipLaunchKernelGGL(k_corr, dim3(c.n * c.P), dim3(POSE_THREADS), 0, s, c);
-    hipLaunchKernelGGL(k_p3p, dim3((c.n * c.P * c.pp.n_hyp + POSE_THREADS - 1) / POSE_THREADS), dim3(POSE_THREADS), 0, s, c);
-    hipLaunchKernelGGL(k_ransac, dim3(c.n * c.P * S), dim3(POSE_THREADS), 0, s, c, S);
-    hipLaunchKernelGGL(k_refine, dim3(c.n * c.P), dim3(POSE_THREADS), 0, s, c, S);
+    hipLaunchKernelGGL(k_corr, dim3(c.n * c.npair), dim3(POSE_THREADS), 0, s, c);
+    hipLaunchKernelGGL(k_p3p, dim3((c.n * c.npair * c.pp.n_hyp + POSE_THREADS - 1) / POSE_THREADS), dim3(POSE_THREADS), 0, s, c);
+    hipLaunchKernelGGL(k_ransac, dim3(c.n * c.npair * S), dim3(POSE_THREADS), 0, s, c, S);
+    hipLaunchKernelGGL(k_refine, dim3(c.n * c.npair), dim3(POSE_THREADS), 0, s, c, S);
 }
 
 // RANSAC + refinement only, on correspondences another kernel wrote (relocalisation).
 void launch_pose_solve(const BatchCtx& c, hipStream_t s) {
     const int S = ransac_splits(c);
-    hipLaunchKernelGGL(k_p3p, dim3((c.n * c.P * c.pp.n_hyp + POSE_THREADS - 1) / POSE_THREADS), dim3(POSE_THREADS), 0, s, c);
-    hipLaunchKernelGGL(k_ransac, dim3(c.n * c.P * S), dim3(POSE_THREADS), 0, s, c, S);
-    hipLaunchKernelGGL(k_refine, dim3(c.n * c.P), dim3(POSE_THREADS), 0, s, c, S);
+    hipLaunchKernelGGL(k_p3p, dim3((c.n * c.npair * c.pp.n_hyp + POSE_THREADS - 1) / POSE_THREADS), dim3(POSE_THREADS), 0, s, c);
+    hipLaunchKernelGGL(k_ransac, dim3(c.n * c.npair * S), dim3(POSE_THREADS), 0, s, c, S);
+    hipLaunchKernelGGL(k_refine, dim3(c.n * c.npair), dim3(POSE_THREADS), 0, s, c, S);
 }
 
 void launch_chain(const BatchCtx& c, hipStream_t s) {

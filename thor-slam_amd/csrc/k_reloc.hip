@@ -127,6 +127,8 @@ void launch_reloc(const BatchCtx& c, int pair, int64_t frame, const double* map_
     BatchCtx r = c;   // A7's RANSAC + refinement on the relocalisation scratch: one frame, one "pair"
     r.n = 1;
     r.P = 1;
+    r.pair0 = 0;
+    r.npair = 1;
     r.g0 = frame;
     r.calib[0] = c.calib[pair];
     r.corr = corr;

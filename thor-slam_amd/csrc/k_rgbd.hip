@@ -12,7 +12,7 @@
 
 // BGR -> gray, 4 pixels per thread (3 dword loads, 1 dword store) when W*H is a multiple of 4.
 __global__ __launch_bounds__(256) void k_rgbd_gray(BatchCtx c, uint8_t* gray) {
-    const int img = blockIdx.y;   // f * P + p
+    const int img = blockIdx.y;   // view image f * ncam + (camera - cam0): input and output [n][ncam]
     const size_t npx = (size_t)c.W * c.H;
     const uint8_t* src = c.rgbd_in + (size_t)img * npx * 5;
     uint8_t* dst = gray + (size_t)img * npx;
@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void k_rgbd_gray(BatchCtx c, uint8_t* gray) {
 // the keypoint is padding or the depth is 0.  stereo = the keypoint itself (or -1).
 __global__ __launch_bounds__(256) void k_rgbd_depth(BatchCtx c) {
     const int K = c.g.K;
-    const int fp = blockIdx.y, p = fp % c.P, f = fp / c.P;
+    const int fl = blockIdx.y, p = c.pair0 + fl % c.npair, f = fl / c.npair;   // camera p = pair p
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= K) return;
     const int slot = ring_slot(c, c.g0 + f);
@@ -65,7 +65,8 @@ __global__ __launch_bounds__(256) void k_rgbd_depth(BatchCtx c) {
             iy = min(max((m[1] + 16) >> 5, 0), c.H - 1);
         }
         const size_t npx = (size_t)c.W * c.H;
-        const uint16_t* depth = reinterpret_cast<const uint16_t*>(c.rgbd_in + ((size_t)f * c.P + p) * npx * 5 + npx * 3);
+        // the input records are the front-end view's, [n][ncam] from camera cam0
+        const uint16_t* depth = reinterpret_cast<const uint16_t*>(c.rgbd_in + ((size_t)f * c.ncam + (p - c.cam0)) * npx * 5 + npx * 3);
         const uint32_t mm = depth[(size_t)iy * c.W + ix];
         if (mm) disp = c.calib[p].fx / ((double)mm * 0.001);
     }
@@ -76,9 +77,9 @@ __global__ __launch_bounds__(256) void k_rgbd_depth(BatchCtx c) {
 
 void launch_rgbd_gray(const BatchCtx& c, uint8_t* gray, hipStream_t s) {
     const size_t groups = ((size_t)c.W * c.H + 3) / 4;
-    hipLaunchKernelGGL(k_rgbd_gray, dim3((unsigned)((groups + 255) / 256), c.n * c.P), dim3(256), 0, s, c, gray);
+    hipLaunchKernelGGL(k_rgbd_gray, dim3((unsigned)((groups + 255) / 256), c.n * c.ncam), dim3(256), 0, s, c, gray);
 }
 
 void launch_rgbd_depth(const BatchCtx& c, hipStream_t s) {
-    hipLaunchKernelGGL(k_rgbd_depth, dim3((c.g.K + 255) / 256, c.n * c.P), dim3(256), 0, s, c);
+    hipLaunchKernelGGL(k_rgbd_depth, dim3((c.g.K + 255) / 256, c.n * c.npair), dim3(256), 0, s, c);
 }

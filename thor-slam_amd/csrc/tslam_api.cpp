@@ -4,7 +4,6 @@
 // caller's stream.  The launch functions never allocate, copy synchronously or synchronise, so
 // a batch can be captured into a hipGraph by the caller.
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -17,6 +16,7 @@
 #include "tslam_ba.h"
 #include "tslam_common.h"
 #include "tslam_describe.h"
+#include "tslam_internal.h"
 #include "tslam_tables.h"
 
 namespace {
@@ -63,8 +63,12 @@ struct tslam_handle {
     double* d_rig_pose = nullptr;
     int32_t* d_rig_stats = nullptr;
     double* d_rig_state = nullptr;
-    // IMU rotation prior for the next batch (tslam_set_motion_prior)
+    // IMU rotation prior for the next batch (tslam_set_motion_prior); the rig's body-frame
+    // version of it (k_rig_prior), per batch parity
     double* d_prior = nullptr;
+    double* d_rig_prior = nullptr;
+    hipEvent_t ev_prior[2] = {nullptr, nullptr};   // the last reader of each prior slot is done
+    bool prior_read_armed[2] = {false, false};
     bool prior_armed = false;
     // relocalisation map (tslam_map_upload) and scratch
     double* d_map_xyz = nullptr;
@@ -134,12 +138,12 @@ struct tslam_handle {
     // sharded rig (tslam_set_shard): front-end cameras [sh_cam_lo, sh_cam_hi) and back-end frames
     // [rank * n / world, (rank + 1) * n / world) of every batch
     int sh_cam_lo = 0, sh_cam_hi = 0, sh_rank = 0, sh_world = 1;
-    // RCCL-driven sharding (tslam_comm_init / tslam_submit_sharded): the communicator and the
-    // exchange buffers of this rank (device), the previous batch's last frame of its cameras
+    // library-driven sharding (tslam_comm_init / tslam_group_create, tslam_shard.cpp): the driver
+    // that owns this rank's communicators, streams and exchange buffers (owned here after
+    // tslam_comm_init; a group owns it otherwise)
     bool sh_comm = false;
-    ncclComm_t comm = nullptr;
-    uint8_t *x_raw_send = nullptr, *x_raw_recv = nullptr, *x_feat_send = nullptr, *x_feat_recv = nullptr;
-    uint8_t *x_pose_send = nullptr, *x_pose_recv = nullptr, *x_prev_raw = nullptr;
+    tslam_shard_driver* drv = nullptr;
+    bool drv_owned = false;
     // asynchronous host boundary (tslam_submit_host / tslam_poll_*): the handle's own front/back
     // streams, pinned staging + device input per batch parity, pinned result slots per parity
     hipStream_t as_front = nullptr, as_back = nullptr;
@@ -186,10 +190,8 @@ static int dev_realloc(tslam_handle* h, void** p, size_t bytes) {
 }
 
 static void free_all(tslam_handle* h) {
-    if (h->comm) {
-        (void)ncclCommDestroy(h->comm);
-        h->comm = nullptr;
-    }
+    if (h->drv && h->drv_owned) tslam_internal_driver_destroy(h->drv);
+    h->drv = nullptr;
     for (void* p : h->allocs) (void)hipFree(p);
     h->allocs.clear();
     for (void* p : h->host_allocs) (void)hipHostFree(p);
@@ -400,6 +402,8 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.rig_pose = h->d_rig_pose;
     c.rig_stats = h->d_rig_stats;
     c.rig_state = h->d_rig_state;
+    c.rig_prior = (h->prior_armed && h->d_rig_prior) ? h->d_rig_prior + (size_t)(h->batch_idx & 1) * TS_PRIOR_DOUBLES * h->B
+                                                     : nullptr;
     c.ransac = h->d_ransac;
     c.hyp = h->d_hyp;
     c.det_thr = (const uint32_t*)h->buf[TSLAM_BUF_DET_THR].ptr;
@@ -423,6 +427,8 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.margin = h->prm.edge_margin;
     c.cam0 = h->sh_cam_lo;
     c.ncam = h->sh_cam_hi - h->sh_cam_lo;
+    c.pair0 = 0;
+    c.npair = h->P;
     c.match_modes = 3;
     return c;
 }
@@ -445,6 +451,7 @@ static BatchCtx range_ctx(const BatchCtx& c, int lo, int hi) {
     r.ransac += f * P * TS_MAX_SPLITS * TS_RANSAC_WORDS / 2;
     r.hyp += f * P * 4 * (size_t)c.pp.n_hyp * 12;
     if (r.prior) r.prior += f * P * TS_PRIOR_DOUBLES;
+    if (r.rig_prior) r.rig_prior += f * TS_PRIOR_DOUBLES;
     if (r.rig_pose) r.rig_pose += f * TS_POSE_DOUBLES;
     if (r.rig_stats) r.rig_stats += f * TS_STATS_INTS;
     return r;
@@ -462,7 +469,51 @@ static void shard_range(const tslam_handle* h, int n, int* lo, int* hi) {
 // triangulates from them; the rank that owns lo-1 computes the same values), POSE adds the rig
 // pose of the range (no chaining), and CHAIN chains the whole batch once every rank's pose
 // records are back (tslam_unpack_poses), identically on every rank.
+//
+// A camera-sharded RGB-D rig (each camera is a "pair": its back end needs no other camera) instead
+// tracks its own cameras over the whole batch: MATCH and POSE run on the pair view of its cameras
+// for every frame; the rig pose of its frame range (KERNEL_RIG) follows tslam_unpack_pairs of the
+// other ranks' pair blocks (pose, stats, correspondences); then pose records and CHAIN as above.
+static int run_sharded_rgbd_stage(tslam_handle* h, const BatchCtx& c, int stage, hipStream_t s) {
+    int lo, hi;
+    shard_range(h, c.n, &lo, &hi);
+    BatchCtx own = c;   // pair view: this rank's cameras (cameras per pair = 1)
+    own.pair0 = h->sh_cam_lo;
+    own.npair = h->sh_cam_hi - h->sh_cam_lo;
+    switch (stage) {
+        case TSLAM_STAGE_RECTIFY:
+        case TSLAM_KERNEL_RECTIFY_PYRAMID:
+            launch_rgbd_gray(c, h->d_gray, s);
+            launch_rectify_pyramid(c, s);
+            break;
+        case TSLAM_STAGE_DETECT: launch_detect(c, s); launch_select(c, s); break;
+        case TSLAM_STAGE_DESCRIBE: launch_describe(c, s); break;
+        case TSLAM_KERNEL_DETECT: launch_detect(c, s); break;
+        case TSLAM_KERNEL_SELECT: launch_select(c, s); break;
+        case TSLAM_KERNEL_DESCRIBE: launch_describe(c, s); break;
+        case TSLAM_STAGE_MATCH: launch_match(own, s); launch_match_refine(own, s); break;
+        case TSLAM_KERNEL_MATCH: launch_match(own, s); break;
+        case TSLAM_KERNEL_MATCH_REFINE: launch_match_refine(own, s); break;
+        case TSLAM_STAGE_POSE:
+        case TSLAM_KERNEL_POSE: launch_pose(own, s); break;
+        case TSLAM_KERNEL_RIG:
+            if (!h->rig) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig)");
+            launch_rig_pose(range_ctx(c, lo, hi), s);
+            break;
+        case TSLAM_KERNEL_CHAIN:
+            launch_chain(c, s);
+            if (h->rig) launch_rig_chain(c, s);
+            break;
+        default:
+            return fail(TSLAM_ESTATE, "a camera-sharded RGB-D handle runs its stages one by one: RECTIFY..DESCRIBE, "
+                                      "MATCH, POSE, pack/exchange/unpack pairs, KERNEL_RIG, pose records, CHAIN");
+    }
+    HIPCHK(hipGetLastError());
+    return TSLAM_OK;
+}
+
 static int run_sharded_stage(tslam_handle* h, const BatchCtx& c, int stage, hipStream_t s) {
+    if (h->prm.rgbd) return run_sharded_rgbd_stage(h, c, stage, s);
     int lo, hi;
     shard_range(h, c.n, &lo, &hi);
     const BatchCtx cb = range_ctx(c, lo, hi);
@@ -665,7 +716,8 @@ int tslam_destroy(tslam_handle* h) {
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();
     for (hipEvent_t e : h->ba_events) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {h->ev_fe, h->ev_ba[0], h->ev_ba[1], h->ev_front, h->ev_back[0], h->ev_back[1],
+    for (hipEvent_t e : {h->ev_fe, h->ev_ba[0], h->ev_ba[1], h->ev_front, h->ev_back[0], h->ev_back[1], h->ev_prior[0],
+                         h->ev_prior[1],
                          h->as_staged[0], h->as_staged[1], h->as_res[0].ev, h->as_res[1].ev})
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t st : {h->as_front, h->as_back})
@@ -865,6 +917,10 @@ int tslam_begin_batch(tslam_handle* h, const uint8_t* images, int n_frames) {
     if (!images) return fail(TSLAM_EINVAL, "null images");
     if (n_frames < 1 || n_frames > h->B) return fail(TSLAM_EINVAL, "n_frames must be in [1, max_batch]");
     if (h->in_batch) return fail(TSLAM_ESTATE, "previous batch not ended");
+    // a sharded batch splits into `world` equal frame ranges: the pose-record all-gather has a
+    // fixed size per rank, so an uneven or empty range would chain the wrong records
+    if ((h->sh_world > 1 || h->sh_comm) && n_frames % h->sh_world != 0)
+        return fail(TSLAM_EINVAL, "a sharded batch needs n_frames divisible by world");
     h->cur_images = images;
     h->cur_n = n_frames;
     h->cur_g0 = h->frames_done;
@@ -880,6 +936,12 @@ int tslam_end_batch(tslam_handle* h) {
     if (!h->in_batch) return fail(TSLAM_ESTATE, "no batch in progress");
     h->frames_done += h->cur_n;
     h->in_batch = false;
+    if (h->prior_armed) {   // the prior slot of this parity is free once this batch's last stage ran
+        const int par = (int)(h->batch_idx & 1);
+        if (!h->ev_prior[par]) HIPCHK(hipEventCreateWithFlags(&h->ev_prior[par], hipEventDisableTiming));
+        HIPCHK(hipEventRecord(h->ev_prior[par], h->last_stream));
+        h->prior_read_armed[par] = true;
+    }
     h->prior_armed = false;   // a prior applies to one batch
     if (h->back_started && h->front_started && h->back_stream != h->front_stream) {
         const int par = (int)(h->batch_idx & 1);
@@ -1118,12 +1180,16 @@ int tslam_set_motion_prior(tslam_handle* h, const double* prior, int n_frames) {
         const int rc = dev_alloc(h, (void**)&h->d_prior, sizeof(double) * 2 * slot);
         if (rc != TSLAM_OK) return rc;
     }
-    // the slot's previous reader is batch s-2's pose stage
+    if (h->rig && !h->d_rig_prior) {
+        const int rc = dev_alloc(h, (void**)&h->d_rig_prior, sizeof(double) * 2 * TS_PRIOR_DOUBLES * h->B);
+        if (rc != TSLAM_OK) return rc;
+    }
+    // the slot's previous reader is batch s-2 (pose + chain stages): wait for the event its last
+    // stage recorded, not for the whole device
     const int par = (int)(h->batch_idx & 1);
-    if (h->back_pending[par]) {
-        HIPCHK(hipEventSynchronize(h->ev_back[par]));
-    } else {
-        HIPCHK(hipDeviceSynchronize());
+    if (h->prior_read_armed[par]) {
+        HIPCHK(hipEventSynchronize(h->ev_prior[par]));
+        h->prior_read_armed[par] = false;
     }
     std::vector<double> buf(slot, 0.0);   // frames past n: weight 0
     memcpy(buf.data(), prior, sizeof(double) * TS_PRIOR_DOUBLES * h->P * n_frames);
@@ -1194,129 +1260,12 @@ int tslam_set_shard(tslam_handle* h, int cam_lo, int cam_hi, int rank, int world
     if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_set_shard inside a batch");
     if (cam_lo < 0 || cam_hi > h->C || cam_lo >= cam_hi) return fail(TSLAM_EINVAL, "camera range outside [0, cameras)");
     if (world < 1 || rank < 0 || rank >= world || world > h->B) return fail(TSLAM_EINVAL, "need 0 <= rank < world <= max_batch");
-    if (world > 1 && (h->prm.rgbd || h->prm.ba_window)) return fail(TSLAM_EINVAL, "sharding covers stereo rigs without local BA");
+    if (world > 1 && h->prm.ba_window) return fail(TSLAM_EINVAL, "sharding covers rigs without local BA");
     h->sh_cam_lo = cam_lo;
     h->sh_cam_hi = cam_hi;
     h->sh_rank = rank;
     h->sh_world = world;
     return TSLAM_OK;
-}
-
-int tslam_comm_unique_id(void* id128) {
-    if (!id128) return fail(TSLAM_EINVAL, "null id");
-    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
-    ncclUniqueId id;
-    const ncclResult_t r = ncclGetUniqueId(&id);
-    if (r != ncclSuccess) return fail(TSLAM_EHIP, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
-    memcpy(id128, &id, sizeof(id));
-    return TSLAM_OK;
-}
-
-int tslam_comm_init(tslam_handle* h, const void* id128, int rank, int world) {
-    if (!h || !id128) return fail(TSLAM_EINVAL, "bad argument");
-    if (h->comm) return fail(TSLAM_ESTATE, "communicator already set");
-    if (world < 1 || rank < 0 || rank >= world) return fail(TSLAM_EINVAL, "need 0 <= rank < world");
-    if (h->C % world || h->B % world) return fail(TSLAM_EINVAL, "cameras and max_batch must divide by world");
-    const int S = h->C / world;
-    int rc = tslam_set_shard(h, rank * S, (rank + 1) * S, rank, world);
-    if (rc != TSLAM_OK) return rc;
-    if (h->prm.rgbd || h->prm.ba_window) return fail(TSLAM_EINVAL, "sharding covers stereo rigs without local BA");
-    HIPCHK(hipSetDevice(h->device));
-    ncclUniqueId id;
-    memcpy(&id, id128, sizeof(id));
-    const ncclResult_t r = ncclCommInitRank(&h->comm, world, id, rank);
-    if (r != ncclSuccess) {
-        h->comm = nullptr;
-        return fail(TSLAM_EHIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-    }
-    const size_t nr = (size_t)h->B / world + 1, img = (size_t)h->W * h->H;
-    const size_t blk = (size_t)stream_block_bytes(h->g), rec = (size_t)pose_record_bytes(h->P);
-    const size_t fpr = (size_t)h->B / world;
-    struct A {
-        uint8_t** p;
-        size_t bytes;
-    } list[] = {{&h->x_raw_send, world * nr * S * img}, {&h->x_raw_recv, world * nr * S * img},
-                {&h->x_feat_send, world * nr * S * blk}, {&h->x_feat_recv, world * nr * S * blk},
-                {&h->x_pose_send, fpr * rec},           {&h->x_pose_recv, world * fpr * rec},
-                {&h->x_prev_raw, S * img}};
-    for (const A& a : list) {
-        rc = dev_alloc(h, (void**)a.p, a.bytes);
-        if (rc != TSLAM_OK) return rc;
-    }
-    h->sh_comm = true;
-    return TSLAM_OK;
-}
-
-#define NCCLCHK(expr)                                                                        \
-    do {                                                                                     \
-        ncclResult_t r__ = (expr);                                                           \
-        if (r__ != ncclSuccess) return fail(TSLAM_EHIP, std::string(#expr) + ": " + ncclGetErrorString(r__)); \
-    } while (0)
-
-// One batch of a rank of an RCCL-sharded rig, on `stream`: the same phases as the Python driver
-// (thor_slam_amd/shard.py RankShard): raw images + stream blocks of the rank's cameras to every
-// other rank for the frames that rank solves (its range and the frame before), the back end of
-// the rank's own range, the pose records all-gathered, the chain.
-int tslam_submit_sharded(tslam_handle* h, const uint8_t* images, void* stream) {
-    if (!h || !images) return fail(TSLAM_EINVAL, "bad argument");
-    if (!h->sh_comm) return fail(TSLAM_ESTATE, "tslam_comm_init first");
-    HIPCHK(hipSetDevice(h->device));
-    hipStream_t s = (hipStream_t)stream;
-    const int N = h->sh_world, me = h->sh_rank, B = h->B, S = h->sh_cam_hi - h->sh_cam_lo;
-    const size_t fpr = (size_t)B / N, nr = fpr + 1, img = (size_t)h->W * h->H;
-    const size_t blk = (size_t)stream_block_bytes(h->g), rec = (size_t)pose_record_bytes(h->P);
-    const size_t raw_q = nr * S * img, feat_q = nr * S * blk;   // bytes per destination
-    const int64_t g0 = h->frames_done;
-    int rc = tslam_begin_batch(h, images, B);
-    if (rc != TSLAM_OK) return rc;
-    // raw images for every destination: its frames lo-1 .. hi-1 of this rank's cameras
-    for (int q = 0; q < N; ++q) {
-        if (q == me) continue;
-        const int lo = (int)(q * fpr);
-        uint8_t* out = h->x_raw_send + q * raw_q;
-        const uint8_t* first = lo == 0 ? h->x_prev_raw : images + (size_t)(lo - 1) * S * img;
-        HIPCHK(hipMemcpyAsync(out, first, S * img, hipMemcpyDeviceToDevice, s));
-        HIPCHK(hipMemcpyAsync(out + S * img, images + (size_t)lo * S * img, fpr * S * img, hipMemcpyDeviceToDevice, s));
-    }
-    HIPCHK(hipMemcpyAsync(h->x_prev_raw, images + (size_t)(B - 1) * S * img, S * img, hipMemcpyDeviceToDevice, s));
-    // front end of this rank's cameras, then their stream blocks per destination
-    const int front[3] = {TSLAM_STAGE_RECTIFY, TSLAM_STAGE_DETECT, TSLAM_STAGE_DESCRIBE};
-    for (int st : front)
-        if ((rc = tslam_run_stage(h, st, s)) != TSLAM_OK) return rc;
-    for (int q = 0; q < N; ++q) {
-        if (q == me) continue;
-        rc = tslam_pack_streams(h, g0 + (int64_t)q * fpr - 1, (int)nr, h->sh_cam_lo, h->sh_cam_hi,
-                                h->x_feat_send + q * feat_q, s);
-        if (rc != TSLAM_OK) return rc;
-    }
-    // exchange 1: point-to-point all-to-all of raw images and stream blocks
-    if (N > 1) {
-        NCCLCHK(ncclGroupStart());
-        for (int q = 0; q < N; ++q) {
-            if (q == me) continue;
-            NCCLCHK(ncclSend(h->x_raw_send + q * raw_q, raw_q, ncclUint8, q, h->comm, s));
-            NCCLCHK(ncclRecv(h->x_raw_recv + q * raw_q, raw_q, ncclUint8, q, h->comm, s));
-            NCCLCHK(ncclSend(h->x_feat_send + q * feat_q, feat_q, ncclUint8, q, h->comm, s));
-            NCCLCHK(ncclRecv(h->x_feat_recv + q * feat_q, feat_q, ncclUint8, q, h->comm, s));
-        }
-        NCCLCHK(ncclGroupEnd());
-    }
-    // the other ranks' cameras of frames lo-1 .. hi-1 of this rank's range into the ring
-    const int64_t first = g0 + (int64_t)me * fpr - 1;
-    for (int q = 0; q < N; ++q) {
-        if (q == me) continue;
-        const int c0 = q * S, c1 = (q + 1) * S;
-        if ((rc = tslam_import_raw(h, h->x_raw_recv + q * raw_q, first, (int)nr, c0, c1, s)) != TSLAM_OK) return rc;
-        if ((rc = tslam_unpack_streams(h, first, (int)nr, c0, c1, h->x_feat_recv + q * feat_q, s)) != TSLAM_OK) return rc;
-    }
-    // back end of this rank's frames, exchange 2 (pose records), the chain on every rank
-    if ((rc = tslam_run_stage(h, TSLAM_STAGE_MATCH, s)) != TSLAM_OK) return rc;
-    if ((rc = tslam_run_stage(h, TSLAM_STAGE_POSE, s)) != TSLAM_OK) return rc;
-    if ((rc = tslam_pack_poses(h, h->x_pose_send, s)) != TSLAM_OK) return rc;
-    NCCLCHK(ncclAllGather(h->x_pose_send, h->x_pose_recv, fpr * rec, ncclUint8, h->comm, s));
-    if ((rc = tslam_unpack_poses(h, h->x_pose_recv, s)) != TSLAM_OK) return rc;
-    if ((rc = tslam_run_stage(h, TSLAM_KERNEL_CHAIN, s)) != TSLAM_OK) return rc;
-    return tslam_end_batch(h);
 }
 
 int tslam_exchange_sizes(tslam_handle* h, int64_t* stream_block, int64_t* pose_record) {
@@ -1373,6 +1322,64 @@ int tslam_import_raw(tslam_handle* h, const uint8_t* images, int64_t first_frame
     HIPCHK(hipGetLastError());
     return TSLAM_OK;
 }
+
+int tslam_pair_block_bytes(tslam_handle* h, int64_t* bytes) {
+    if (!h || !bytes) return fail(TSLAM_EINVAL, "bad argument");
+    *bytes = pair_block_bytes(h->g);
+    return TSLAM_OK;
+}
+
+static int pair_blocks(tslam_handle* h, bool pack, int f0, int n_frames, int pair_lo, int pair_hi, uint8_t* buf, void* stream) {
+    if (!h || !buf) return fail(TSLAM_EINVAL, "bad argument");
+    if (!h->in_batch) return fail(TSLAM_ESTATE, "pair blocks are packed / unpacked inside a batch");
+    if (f0 < 0 || n_frames < 1 || f0 + n_frames > h->cur_n) return fail(TSLAM_EINVAL, "frame range outside the batch");
+    if (pair_lo < 0 || pair_hi > h->P || pair_lo >= pair_hi) return fail(TSLAM_EINVAL, "pair range outside [0, pairs)");
+    HIPCHK(hipSetDevice(h->device));
+    launch_pair_blocks(make_ctx(h), pack, f0, n_frames, pair_lo, pair_hi - pair_lo, buf, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return TSLAM_OK;
+}
+
+int tslam_pack_pairs(tslam_handle* h, int f0, int n_frames, int pair_lo, int pair_hi, void* dst, void* stream) {
+    return pair_blocks(h, true, f0, n_frames, pair_lo, pair_hi, (uint8_t*)dst, stream);
+}
+
+int tslam_unpack_pairs(tslam_handle* h, int f0, int n_frames, int pair_lo, int pair_hi, const void* src, void* stream) {
+    return pair_blocks(h, false, f0, n_frames, pair_lo, pair_hi, (uint8_t*)src, stream);
+}
+
+int tslam_internal_info(tslam_handle* h, tslam_handle_info* o) {
+    if (!h || !o) return fail(TSLAM_EINVAL, "bad argument");
+    o->device = h->device;
+    o->W = h->W;
+    o->H = h->H;
+    o->P = h->P;
+    o->C = h->C;
+    o->B = h->B;
+    o->rgbd = h->prm.rgbd;
+    o->rig = h->rig ? 1 : 0;
+    o->ba = h->prm.ba_window;
+    o->frames_done = h->frames_done;
+    o->stream_block = stream_block_bytes(h->g);
+    o->pose_record = pose_record_bytes(h->P);
+    o->pair_block = pair_block_bytes(h->g);
+    o->cam_lo = h->sh_cam_lo;
+    o->cam_hi = h->sh_cam_hi;
+    o->rank = h->sh_rank;
+    o->world = h->sh_world;
+    return TSLAM_OK;
+}
+
+int tslam_internal_attach_driver(tslam_handle* h, tslam_shard_driver* d, bool owned) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (h->drv && h->drv_owned && h->drv != d) tslam_internal_driver_destroy(h->drv);
+    h->drv = d;
+    h->drv_owned = d && owned;
+    h->sh_comm = d != nullptr;
+    return TSLAM_OK;
+}
+
+tslam_shard_driver* tslam_internal_driver(tslam_handle* h) { return h ? h->drv : nullptr; }
 
 int tslam_pack_poses(tslam_handle* h, void* dst, void* stream) {
     if (!h || !dst) return fail(TSLAM_EINVAL, "bad argument");

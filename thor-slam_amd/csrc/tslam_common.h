@@ -91,6 +91,10 @@ struct BatchCtx {
     // camera view of the front-end kernels (rectify .. describe): cameras cam0 .. cam0+ncam-1 of
     // every frame, images [n][ncam][H][W] (the whole rig: 0, C; a sharded rig: the rank's streams)
     int cam0, ncam;
+    // pair view of the back-end kernels (match .. pose): pairs pair0 .. pair0+npair-1 of every
+    // frame (the whole rig: 0, P; a camera-sharded RGB-D rig: the rank's cameras); batch buffers
+    // keep their [n][P] layout
+    int pair0, npair;
     int match_modes;       // k_match: 3 = temporal + stereo, 1 = stereo only (sharded pre-pass)
     int64_t g0;            // global index of the batch's first frame
     int W, H;              // level-0 size
@@ -131,6 +135,7 @@ struct BatchCtx {
     double* rig_pose;      // [B][68]  body T_rel, T_abs, cov
     int32_t* rig_stats;    // [B][8]
     double* rig_state;     // [16]
+    double* rig_prior;     // [B][16] body-frame IMU prior (k_rig_prior, from the pairs' priors) or null
     // A4 speculative FAST threshold (DESIGN.md §5 "detect"): te[cam][l] in use, its running
     // minimum for the next batch, per (frame, cam, level) fallback flags, launch mode
     // (0: te = max(t + 1, det_thr), flags set by select; 1: te = t + 1 for flagged images only)
@@ -172,6 +177,9 @@ int64_t pose_record_bytes(int P);
 void launch_stream_blocks(const BatchCtx& c, bool pack, int64_t first, int n_frames, int cam_lo, int ncam, uint8_t* blk,
                           hipStream_t s);
 void launch_pose_records(const BatchCtx& c, bool pack, int f0, int n, uint8_t* rec, hipStream_t s);
+// camera-sharded RGB-D rig: pair blocks (per batch frame x pair: pose, stats, correspondences)
+int64_t pair_block_bytes(const LevelGeom& g);
+void launch_pair_blocks(const BatchCtx& c, bool pack, int f0, int n_frames, int p0, int np, uint8_t* blk, hipStream_t s);
 void launch_pose_solve(const BatchCtx& c, hipStream_t s);
 void launch_reloc(const BatchCtx& c, int pair, int64_t frame, const double* map_xyz, const uint32_t* map_desc, int M,
                   int32_t* match, double* corr, int32_t* stats, double* pose, double* ransac, double* hyp, hipStream_t s);

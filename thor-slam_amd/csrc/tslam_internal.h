@@ -1,0 +1,32 @@
+// tslam_internal.h — what the library's host files share beyond the public C-ABI (include/tslam.h):
+// the error setter, a read-only view of a handle's geometry, and the attachment of a sharded-rig
+// driver (tslam_shard.cpp) to the handles it drives.
+#pragma once
+
+#include <stdint.h>
+
+#include "../../include/tslam.h"
+
+struct tslam_shard_driver;   // tslam_shard.cpp
+
+#define TSLAM_INTERNAL __attribute__((visibility("hidden")))
+
+// sets tslam_last_error() and returns `code`
+int tslam_internal_fail(int code, const char* msg);
+
+// not exported from libtslam_hip.so (only include/tslam.h is its ABI)
+extern "C" {
+struct tslam_handle_info {
+    int device, W, H, P, C, B, rgbd, rig, ba;
+    int64_t frames_done;
+    int64_t stream_block, pose_record, pair_block;   // exchange unit sizes (bytes)
+    int cam_lo, cam_hi, rank, world;                 // tslam_set_shard
+};
+TSLAM_INTERNAL int tslam_internal_info(tslam_handle* h, tslam_handle_info* out);
+
+// `owned`: the handle destroys the driver with itself (tslam_comm_init); a group's driver is owned
+// by the group (tslam_group_destroy detaches it first).  NULL detaches.
+TSLAM_INTERNAL int tslam_internal_attach_driver(tslam_handle* h, tslam_shard_driver* d, bool owned);
+TSLAM_INTERNAL tslam_shard_driver* tslam_internal_driver(tslam_handle* h);
+TSLAM_INTERNAL void tslam_internal_driver_destroy(tslam_shard_driver* d);
+}  // extern "C"

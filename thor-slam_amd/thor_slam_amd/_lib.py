@@ -31,6 +31,7 @@ KERNELS = {
     "match": 14, "match_refine": 15, "pose": 16, "chain": 17,
 }
 RIG_KERNEL = 18   # rig pose (+ chain; sharded: the range's rig pose only)
+TRANSPORT = {"rccl": 0, "copy": 1}   # tslam_group_create
 POSE_OK, POSE_LOST, POSE_INIT = 0, 1, 2
 
 
@@ -132,6 +133,14 @@ _SIGNATURES = {
                                             ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_import_raw": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_void_p]),
+    "tslam_pair_block_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]),
+    "tslam_pack_pairs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_unpack_pairs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_group_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "tslam_group_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_group_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "tslam_pack_poses": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_unpack_poses": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_ba_read_map": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
@@ -467,6 +476,20 @@ class Handle:
         _check(self.lib.tslam_import_raw(self.h, ctypes.c_void_p(images_ptr), int(first_frame), int(n_frames), int(cam_lo),
                                          int(cam_hi), ctypes.c_void_p(stream)))
 
+    def pair_block_bytes(self) -> int:
+        """Bytes of one RGB-D pair block (pose, stats, correspondences of one frame and camera)."""
+        n = ctypes.c_int64()
+        _check(self.lib.tslam_pair_block_bytes(self.h, ctypes.byref(n)))
+        return int(n.value)
+
+    def pack_pairs(self, f0: int, n_frames: int, pair_lo: int, pair_hi: int, dst_ptr: int, stream: int = 0) -> None:
+        _check(self.lib.tslam_pack_pairs(self.h, int(f0), int(n_frames), int(pair_lo), int(pair_hi),
+                                         ctypes.c_void_p(dst_ptr), ctypes.c_void_p(stream)))
+
+    def unpack_pairs(self, f0: int, n_frames: int, pair_lo: int, pair_hi: int, src_ptr: int, stream: int = 0) -> None:
+        _check(self.lib.tslam_unpack_pairs(self.h, int(f0), int(n_frames), int(pair_lo), int(pair_hi),
+                                           ctypes.c_void_p(src_ptr), ctypes.c_void_p(stream)))
+
     def pack_poses(self, dst_ptr: int, stream: int = 0) -> None:
         _check(self.lib.tslam_pack_poses(self.h, ctypes.c_void_p(dst_ptr), ctypes.c_void_p(stream)))
 
@@ -635,3 +658,34 @@ class Handle:
             "level": (kp[:, 1] & 0xFF).astype(np.int64), "angle": ((kp[:, 1] >> 8) & 0xFF).astype(np.int64),
             "score": (kp[:, 1] >> 16).astype(np.int64), "counts": cnt.astype(np.int64), "desc": desc,
         }
+
+
+class HandleGroup:
+    """``tslam_group_create``: the handles (one per rank, the same rig) driven as one sharded rig
+    by the library from this process — an RCCL clique over their devices (``transport="rccl"``,
+    one device per handle) or device copies (``"copy"``, ranks may share a device)."""
+
+    def __init__(self, handles: list, transport: str = "rccl"):
+        self.lib = load_library()
+        self.handles = list(handles)
+        arr = (ctypes.c_void_p * len(handles))(*[h.h.value for h in handles])
+        g = ctypes.c_void_p()
+        _check(self.lib.tslam_group_create(arr, len(handles), TRANSPORT[transport], ctypes.byref(g)))
+        self.g = g
+
+    def submit(self, image_ptrs: list[int], streams: list[int] | None = None) -> None:
+        """One batch: rank r's cameras at device pointer image_ptrs[r] (layout of tslam_submit_sharded)."""
+        imgs = (ctypes.c_void_p * len(image_ptrs))(*[int(p) for p in image_ptrs])
+        sts = None if streams is None else (ctypes.c_void_p * len(streams))(*[int(s) for s in streams])
+        _check(self.lib.tslam_group_submit(self.g, imgs, sts))
+
+    def close(self) -> None:
+        if getattr(self, "g", None):
+            self.lib.tslam_group_destroy(self.g)
+            self.g = None
+
+    def __del__(self):  # noqa: D105
+        try:
+            self.close()
+        except Exception:
+            pass

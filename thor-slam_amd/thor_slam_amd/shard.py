@@ -24,6 +24,13 @@ Every rank ends the batch with exactly the poses an unsharded handle fed all cam
 blocks (``exchange="allgather"``) is the literal reading of ``north_star`` and is kept as an
 option: it sends every frame to every rank, ``world`` times the bytes of the all-to-all.
 
+An RGB-D rig (each "pair" is one colour camera with its aligned depth, ``HipSlamConfig.rgbd``)
+shards by camera only and moves no image: every rank tracks its own cameras over the whole batch
+(front end, temporal match + depth lookup, P3P-RANSAC + Gauss-Newton), then **exchange 1** is an
+all-to-all of *pair blocks* (per frame and camera: pose record, stats and the 3D-2D
+correspondences, ``tslam_pack_pairs``) so that each rank solves the rig pose of its frame range
+over all cameras; exchange 2 and the chain are as above.
+
 Three drivers share :class:`RankShard` (one rank's handle, buffers and phases):
 :class:`LocalShardedRig` (all ranks in one process on one device: tests and rehearsal),
 :class:`DistShardedRig` (one rank of a ``torch.distributed`` job, backend ``nccl`` = RCCL, or
@@ -132,6 +139,7 @@ class RankShard:
         if base_T_rect is not None and len(rects) > 1:
             self.h.set_rig(base_T_rect)
         self.rig = base_T_rect is not None and len(rects) > 1
+        self.rgbd = bool(cfg.rgbd)
         self.cam_lo, self.cam_hi = plan.cams(rank)
         self.h.set_shard(self.cam_lo, self.cam_hi, rank, plan.world)
         self.block, self.record = self.h.exchange_sizes()
@@ -140,6 +148,17 @@ class RankShard:
         self.img_bytes = W * H
         dev = torch.device("cuda", device)
         self.dev = dev
+        self.batches = 0
+        if self.rgbd:
+            # pair blocks: to each peer q, this rank's cameras over q's frame range
+            self.pblock = self.h.pair_block_bytes()
+            fpr = plan.frames_per_rank
+            self.frames_sent = fpr
+            self.feat_send = [torch.empty((N, fpr, S, self.pblock), dtype=torch.uint8, device=dev) for _ in range(2)]
+            self.feat_recv = [torch.empty((N, fpr, S, self.pblock), dtype=torch.uint8, device=dev) for _ in range(2)]
+            self.raw_send = self.raw_recv = None
+            self._pose_buffers(torch, dev)
+            return
         # per destination q: [nr][S][H*W] raw images and [nr][S][block] stream blocks (the
         # all-gather variant sends all B+1 frames to everyone); two sets by batch parity
         fr = nr if exchange == "alltoall" else plan.batch + 1
@@ -149,11 +168,13 @@ class RankShard:
         self.raw_recv = [torch.empty((N, fr, S, W * H), dtype=torch.uint8, device=dev) for _ in range(2)]
         self.feat_send = [torch.empty((nd, fr, S, self.block), dtype=torch.uint8, device=dev) for _ in range(2)]
         self.feat_recv = [torch.empty((N, fr, S, self.block), dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.pose_send = [torch.empty((plan.frames_per_rank, self.record), dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.pose_recv = [torch.empty((N, plan.frames_per_rank, self.record), dtype=torch.uint8, device=dev)
-                          for _ in range(2)]
+        self._pose_buffers(torch, dev)
         self.prev_raw = torch.zeros((S, W * H), dtype=torch.uint8, device=dev)   # last frame of the previous batch
-        self.batches = 0
+
+    def _pose_buffers(self, torch, dev) -> None:
+        N, fpr = self.plan.world, self.plan.frames_per_rank
+        self.pose_send = [torch.empty((fpr, self.record), dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.pose_recv = [torch.empty((N, fpr, self.record), dtype=torch.uint8, device=dev) for _ in range(2)]
 
     @property
     def g0(self) -> int:
@@ -217,9 +238,29 @@ class RankShard:
     def back(self, stream: int, timer=None) -> None:
         for k in ("match", "match_refine", "pose"):
             _timed(timer, k, lambda: self.h.run_kernel(k, stream))
+        if self.rgbd:   # the rig pose waits for the other cameras' pair blocks
+            return
         if self.rig:
             _timed(timer, "rig", lambda: self.h.run_rig(stream))
         self.h.pack_poses(self.pose_send[self.batches % 2].data_ptr(), stream)
+
+    # -- RGB-D: pair blocks (this rank's cameras tracked over the whole batch) ------------------
+    def pack_pairs(self, stream: int) -> None:
+        k, fpr = self.batches % 2, self.plan.frames_per_rank
+        for q in range(self.plan.world):
+            if q != self.rank:
+                self.h.pack_pairs(q * fpr, fpr, self.cam_lo, self.cam_hi, self.feat_send[k][q].data_ptr(), stream)
+
+    def rig_range(self, stream: int, timer=None) -> None:
+        """The other ranks' pair blocks of this rank's frame range in, its rig pose, its pose records out."""
+        k, fpr = self.batches % 2, self.plan.frames_per_rank
+        for q in range(self.plan.world):
+            if q != self.rank:
+                c0, c1 = self.plan.cams(q)
+                self.h.unpack_pairs(self.rank * fpr, fpr, c0, c1, self.feat_recv[k][q].data_ptr(), stream)
+        if self.rig:
+            _timed(timer, "rig", lambda: self.h.run_rig(stream))
+        self.h.pack_poses(self.pose_send[k].data_ptr(), stream)
 
     def finish(self, stream: int, timer=None) -> None:
         self.h.unpack_poses(self.pose_recv[self.batches % 2].data_ptr(), stream)
@@ -248,18 +289,23 @@ class LocalShardedRig:
         import torch
 
         self.torch = torch
-        n_cams = 2 * len(rects)
+        n_cams = (1 if cfg.rgbd else 2) * len(rects)
         self.plan = ShardPlan(n_cams, world, batch)
         self.ranks = [RankShard(rects, cfg, self.plan, r, base_T_rect, device, exchange) for r in range(world)]
         self.exchange = exchange
+        self.rgbd = bool(cfg.rgbd)
 
     def step(self, images, stream=None) -> None:
-        """images: device u8 [B][C][H][W] (all cameras); rank r gets its cameras' slice."""
+        """images: device u8 [B][C][H][W] (all cameras; RGB-D records [B][C][5HW]); rank r gets its
+        cameras' slice."""
         torch = self.torch
         st = stream or torch.cuda.current_stream()
         sp = st.cuda_stream
         S = self.plan.streams_per_rank
         parts = [images[:, r * S:(r + 1) * S].contiguous() for r in range(self.plan.world)]
+        if self.rgbd:
+            self._step_rgbd(parts, st)
+            return
         for r, rk in enumerate(self.ranks):
             rk.begin(parts[r])
             rk.stage_raw(st)
@@ -275,6 +321,29 @@ class LocalShardedRig:
         for rk in self.ranks:
             rk.import_remote(sp)
             rk.back(sp)
+        with torch.cuda.stream(st):
+            for rk in self.ranks:
+                k = rk.batches % 2
+                for q, src in enumerate(self.ranks):
+                    rk.pose_recv[k][q].copy_(src.pose_send[k])
+        for rk in self.ranks:
+            rk.finish(sp)
+
+    def _step_rgbd(self, parts, st) -> None:
+        torch, sp = self.torch, st.cuda_stream
+        for r, rk in enumerate(self.ranks):
+            rk.begin(parts[r])
+            rk.front(sp)
+            rk.back(sp)
+            rk.pack_pairs(sp)
+        with torch.cuda.stream(st):   # the all-to-all of pair blocks
+            for r, rk in enumerate(self.ranks):
+                k = rk.batches % 2
+                for q, src in enumerate(self.ranks):
+                    if q != r:
+                        rk.feat_recv[k][q].copy_(src.feat_send[k][r])
+        for rk in self.ranks:
+            rk.rig_range(sp)
         with torch.cuda.stream(st):
             for rk in self.ranks:
                 k = rk.batches % 2
@@ -307,7 +376,10 @@ class DistShardedRig:
 
         self.torch, self.dist = torch, dist
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
-        self.plan = ShardPlan(2 * len(rects), self.world, batch)
+        self.plan = ShardPlan((1 if cfg.rgbd else 2) * len(rects), self.world, batch)
+        self.rgbd = bool(cfg.rgbd)
+        if self.rgbd:
+            exchange = "alltoall"   # pair blocks go only to the rank that solves their frames
         self.rk = RankShard(rects, cfg, self.plan, self.rank, base_T_rect, device, exchange)
         self.exchange = exchange
         self.on_device = dist.get_backend() == "nccl"
@@ -355,7 +427,10 @@ class DistShardedRig:
             self.work[kind][k] = None
 
     def step(self, images, timer: StageTimer | None = None) -> None:
-        """images: device u8 [B][S][H][W] of this rank's cameras (resident)."""
+        """images: device u8 [B][S][H][W] of this rank's cameras (RGB-D: [B][S][5HW]), resident."""
+        if self.rgbd:
+            self._step_rgbd(images, timer)
+            return
         rk, k = self.rk, self.rk.batches % 2
         fs, bs, xs = self.front_stream, self.back_stream, self.x_stream
         rk.begin(images)
@@ -384,6 +459,29 @@ class DistShardedRig:
         self.consumed[k].record(bs)
         self.consumed_armed[k] = True
         rk.back(bs.cuda_stream, timer)
+        self._collective("pose", rk.pose_recv[k].view(-1), rk.pose_send[k].view(-1), k, bs)
+        self._wait("pose", k, bs)
+        rk.finish(bs.cuda_stream, timer)
+
+    def _step_rgbd(self, images, timer) -> None:
+        """RGB-D: own cameras' front end (front stream) and back end (back stream) over the whole
+        batch, then on the back stream the pair-block all-to-all, the range's rig pose, the pose
+        all-gather and the chain (the next batch's front end overlaps them)."""
+        rk, k = self.rk, self.rk.batches % 2
+        fs, bs = self.front_stream, self.back_stream
+        rk.begin(images)
+        fs.wait_stream(self.torch.cuda.current_stream())   # the caller's input is ready
+        bs.wait_stream(self.torch.cuda.current_stream())   # (the depth lookup reads it too)
+        if timer is not None:
+            timer.stream = fs
+        rk.front(fs.cuda_stream, timer)
+        if timer is not None:
+            timer.stream = bs
+        rk.back(bs.cuda_stream, timer)
+        rk.pack_pairs(bs.cuda_stream)
+        self._collective("feat", rk.feat_recv[k], rk.feat_send[k], k, bs)
+        self._wait("feat", k, bs)
+        rk.rig_range(bs.cuda_stream, timer)
         self._collective("pose", rk.pose_recv[k].view(-1), rk.pose_send[k].view(-1), k, bs)
         self._wait("pose", k, bs)
         rk.finish(bs.cuda_stream, timer)

@@ -374,3 +374,18 @@ class SyntheticRGBDSource(SyntheticStereoSource):
             out[k] = pack_rgbd(*self.render_rgbd(start + k))
         return out
 
+
+
+def synthetic_rgbd_rig(joints: dict, names: list[str] | tuple[str, ...], width: int = 1280, height: int = 720,
+                       traj_len: int = 40, scene_seed: int = 0):
+    """RGB-D sources (colour + aligned depth at the source origin) on a rig's joints in one shared
+    room along one body trajectory (the 4-camera nvblox-shaped rig of BASELINE.json configs[4],
+    scripts/run_pipeline.py:218-256) -> (sources, CameraRig with those rig extrinsics)."""
+    from .camera.rig import CameraRig
+
+    scene = RoomScene(seed=scene_seed)
+    traj = circle_trajectory(traj_len)
+    srcs = [SyntheticRGBDSource(name=nm, scene=scene, trajectory=traj, rig_T_source=np.array(joints[nm]), seed=k,
+                                width=width, height=height) for k, nm in enumerate(names)]
+    rig = CameraRig(srcs, rig_extrinsics={nm: Extrinsics.from_4x4_matrix(np.array(joints[nm])) for nm in names})
+    return srcs, rig
