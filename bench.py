@@ -3,7 +3,7 @@
 python bench.py --gpus N --steps K --warmup W   (N > 1 under torch.distributed.run, one rank/GPU)
 python bench.py --config c3 [--gpus N]          (BASELINE.json configs[2]: 4-OAK bracket rig, 8 streams)
 python bench.py --config c4                     (BASELINE.json configs[3]: 1280x800, K=4000, + local BA)
-python bench.py --config c5 [--gpus 4]          (BASELINE.json configs[4]: RGB-D 1280x720, one camera per GPU)
+python bench.py --config c5 [--gpus 4]          (BASELINE.json configs[4]: 4-camera RGB-D rig 1280x720, one camera per GPU)
 
 * N = 1, config c2 (BASELINE.json configs[1]): one stereo pair 640x400, K=2000 ORB-style
   keypoints per image, synthetic room sequence; a *step* = one batch of ``--batch`` synchronised
@@ -30,9 +30,12 @@ python bench.py --config c5 [--gpus 4]          (BASELINE.json configs[4]: RGB-D
 * --config c4: the same step plus the A8 stage (every 5th frame a keyframe of a 10-keyframe
   window, 5 Gauss-Newton iterations per keyframe); the roofline is then that of the dominant
   kernel of the step, the FP64-MFMA Schur product when it dominates (HIP events around its launches).
-* --config c5: RGB-D frames (BGR u8 + aligned u16 mm depth, 1280x720) of one camera per GPU
-  (independent replicas for N > 1: RGB-D cameras have no cross-camera matching); the colour
-  image is converted on the device and depth replaces the stereo matching.
+* --config c5: the 4-camera RGB-D rig (BGR u8 + aligned u16 mm depth, 1280x720 per camera, the
+  cameras on the brackets.urdf joints): per camera the colour image is converted on the device,
+  depth replaces stereo matching, and every frame gets the rig pose over all 4 cameras.  N = 1:
+  one handle for the whole rig; N = 2 / 4: the cameras sharded over the GPUs (each rank tracks its
+  own cameras, RCCL all-to-all of pair blocks, rig pose per frame range, pose all-gather); value =
+  rig frames/s, strong scaling.
 """
 
 from __future__ import annotations
@@ -56,13 +59,15 @@ for _p in (ROOT, ROOT / "thor-slam_amd"):
 METRIC = "synced stereo frames/sec (detect+match+pose) @640×400, 1/2/4/8 GPU"
 METRIC_C3 = "synced rig frames/sec (4 stereo pairs = 8 streams, detect+match+pose+rig pose) @640×400, 1/2/4/8 GPU"
 METRIC_C4 = "synced stereo frames/sec (detect+match+pose+10-keyframe local BA) @1280×800, 1 GPU"
-METRIC_C5 = "RGB-D frames/sec (BGR+depth, detect+match+pose) @1280×720, one camera per GPU, 1/2/4 GPU"
+METRIC_C5 = "RGB-D rig frames/sec (4 cameras, BGR+depth, detect+match+pose+rig pose) @1280×720, 1/2/4 GPU"
 HBM_PEAK_GBS = 8000.0
 # VALU issue: 256 CUs x 4 SIMD-32, a wave64 instruction every 2 cycles per SIMD at 2.4 GHz
 VALU_PEAK_WINST = 256 * 4 * 2.4e9 / 2
 # C2 frames per step: 1024 amortises each launch's ramp and drain (measured on one MI355X, round 2:
 # 147.3k / 153.3k / 154.0k / 155.3k frames/s at B = 256 / 512 / 768 / 1024)
 C2_BATCH = 1024
+# C5 rig frames per step: 4 periods of the 24-frame triangle wave (the resident batch is replayed)
+C5_BATCH = 184
 FP64_MFMA_PEAK_TFS = 78.6   # MI355X FP64 matrix peak (AMD spec; the microarch guide lists no FP64 row)
 # bench kernel label -> device symbol (rocprofv3 / PMC summaries); "pose" is k_corr+k_ransac+k_refine
 KERNEL_SYMBOL = {"rectify_pyramid": "k_rectify_pyramid", "detect": "k_detect", "select": "k_select",
@@ -129,6 +134,43 @@ def render_rig_frames(names, n: int, cam_lo: int, cam_hi: int, workers: int, wid
         for ch, imgs in zip(chunks, ex.map(_render_rig_chunk, [(tuple(names), ch, width, height) for ch in chunks])):
             for (i, c), img in zip(ch, imgs):
                 out[i, c - cam_lo] = img
+    return out
+
+
+def rgbd_rig_setup(names, width: int = 1280, height: int = 720):
+    """RGB-D rig of `names` on the bracket joints: sources, flat camera list, (colour, depth)
+    pairs, undistortions, base_T_cam of each colour camera."""
+    from thor_slam_amd.calib import extract_cameras, rgbd_pairs, rgbd_undistort
+    from thor_slam_amd.synthetic import synthetic_rgbd_rig
+
+    joints = json.loads(JOINTS.read_text())
+    srcs, rig = synthetic_rgbd_rig(joints, names, width, height)
+    cams = extract_cameras(rig.calibration, 2 * len(names))
+    pairs = rgbd_pairs(cams)
+    rects = [rgbd_undistort(cams[c]) for c, _ in pairs]
+    E = [cams[c].extrinsics.to_4x4_matrix() @ r.left_optical_T_rect() for (c, _), r in zip(pairs, rects)]
+    return srcs, cams, pairs, rects, E
+
+
+def _render_rgbd_chunk(args):
+    names, items, width, height = args   # items: (frame, rig camera = pair index)
+    from thor_slam_amd.rgbd import pack_rgbd
+
+    srcs, cams, pairs, _, _ = rgbd_rig_setup(names, width, height)
+    by = {s.name: s for s in srcs}
+    return [pack_rgbd(*by[cams[pairs[q][0]].source_name].render_rgbd(i)) for i, q in items]
+
+
+def render_rgbd_rig_frames(names, n: int, cam_lo: int, cam_hi: int, workers: int, width: int = 1280,
+                           height: int = 720) -> np.ndarray:
+    """[n][cam_hi - cam_lo][5*H*W] u8 device records of the RGB-D rig's cameras cam_lo .. cam_hi-1."""
+    items = [(i, c) for i in range(n) for c in range(cam_lo, cam_hi)]
+    chunks = [items[k::workers] for k in range(workers) if items[k::workers]]
+    out = np.empty((n, cam_hi - cam_lo, 5 * width * height), dtype=np.uint8)
+    with ProcessPoolExecutor(max_workers=max(1, len(chunks))) as ex:
+        for ch, recs in zip(chunks, ex.map(_render_rgbd_chunk, [(tuple(names), ch, width, height) for ch in chunks])):
+            for (i, c), rec in zip(ch, recs):
+                out[i, c - cam_lo] = rec
     return out
 
 
@@ -249,17 +291,23 @@ def _oracle_worker(args):
 
 
 def _oracle_worker_rgbd(args):
-    frames, rect_d, cfg_d, budget_s = args   # frames: (n, H, W, 3) BGR and (n, H, W) depth
+    frames, rect_d, cfg_d, budget_s = args   # frames: (n, P, H, W, 3) BGR and (n, P, H, W) depth
     from oracle import numpy_slam as O
+    from oracle.numpy_rig import rig_pose
     from thor_slam_amd.params import HipSlamConfig
 
     bgr, depth = frames
-    trk = O.OracleTracker(HipSlamConfig(**cfg_d), rect_d)
+    cfg = HipSlamConfig(**cfg_d)
+    rects, E = rect_d
+    trks = [O.OracleTracker(cfg, r) for r in rects]
     n = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
         i = n % len(bgr)
-        trk.step_rgbd(bgr[i], depth[i])
+        outs = [trk.step_rgbd(bgr[i, q], depth[i, q]) for q, trk in enumerate(trks)]
+        if n and len(rects) > 1:
+            rig_pose([{"status": o["status"], "T": o["T"], "corr": o.get("corr"),
+                       "intr": (r["fx"], r["fy"], r["cx"], r["cy"])} for o, r in zip(outs, rects)], E, cfg)
         n += 1
     return n, time.perf_counter() - t0
 
@@ -447,29 +495,21 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     from thor_slam_amd.calib import extract_cameras, stereo_pairs, stereo_rectify
     from thor_slam_amd.camera.rig import CameraRig
     from thor_slam_amd.params import HipSlamConfig
-    from thor_slam_amd.rgbd import pack_rgbd
     from thor_slam_amd.synthetic import SyntheticStereoSource
 
     c3, c4, c5 = args.config == "c3", args.config == "c4", args.config == "c5"
     width, height = (1280, 800) if c4 else (1280, 720) if c5 else (640, 400)
     cfg = (HipSlamConfig(n_features=4000, ba_window=10, ba_kf_interval=5, ba_iters=5) if c4 else
            HipSlamConfig(rgbd=True) if c5 else HipSlamConfig())
-    B = args.batch or (50 if c4 else 128 if c5 else 256 if c3 else C2_BATCH)
+    B = args.batch or (50 if c4 else C5_BATCH if c5 else 256 if c3 else C2_BATCH)
     args.unique = args.unique or (24 if (c4 or c5) else 48)
     workers = max(1, min(16, usable_cpus(), args.unique * (8 if c3 else 1)))
     t_r = time.perf_counter()
     E = None
     src = None
-    if c5:
-        from thor_slam_amd.calib import rgbd_pairs, rgbd_undistort
-        from thor_slam_amd.synthetic import SyntheticRGBDSource
-
-        src = SyntheticRGBDSource(seed=rank, n_frames=args.unique, width=width, height=height)
-        cams = extract_cameras(CameraRig([src]).calibration, 2)
-        (ci, _), = rgbd_pairs(cams)
-        rects = [rgbd_undistort(cams[ci])]
-        rgbd_frames = [src.render_rgbd(i) for i in range(args.unique)]
-        uniq = np.stack([pack_rgbd(b, d) for b, d in rgbd_frames])[:, None, :]   # [n][1][5HW]
+    if c5:   # the 4-camera RGB-D rig, whole on this GPU: records [n][4][5HW]
+        _, cams, pairs, rects, E = rgbd_rig_setup(RIG_SOURCES, width, height)
+        uniq = render_rgbd_rig_frames(RIG_SOURCES, args.unique, 0, len(rects), workers, width, height)
     elif c3:
         _, cams, pairs, rects, E = rig_setup(RIG_SOURCES, width, height)
         uniq = render_rig_frames(RIG_SOURCES, args.unique, 0, 2 * len(rects), workers, width, height)
@@ -485,8 +525,17 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     n_img = uniq.shape[1] if not c5 else 1
 
     total = (args.warmup + args.steps) * B
+    if c5:
+        # one batch in HBM, replayed every step: the batch spans whole periods of the triangle
+        # wave, so consecutive batches continue it seamlessly (4.6 MB per record keeps the resident
+        # input at one batch instead of (warmup + steps) of them)
+        period = 2 * (args.unique - 1)
+        if B % period:
+            raise SystemExit(f"--config c5 needs --batch a multiple of {period} (2 x (unique - 1))")
+        total = B
     idx = torch.from_numpy(triangle_indices(total, args.unique)).cuda()
-    seq = torch.from_numpy(uniq).cuda().index_select(0, idx).contiguous()  # [total, C, H, W] (c5: [total, 1, 5HW]) in HBM
+    seq = torch.from_numpy(uniq).cuda().index_select(0, idx).contiguous()  # [total, C, H, W] (c5: [B, 4, 5HW]) in HBM
+    step_base = (lambda s: 0) if c5 else (lambda s: s * B)
     h = Handle(rects, cfg, max_batch=B, device=dev_index)
     if P > 1:
         h.set_rig(E)
@@ -527,7 +576,7 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     def step(s: int, evs=None) -> None:
         # one batch = every kernel of the hot path; in the timed steps each kernel is bracketed by
         # a pair of HIP events on the stream it runs on (the per-kernel durations below)
-        h.begin_batch(seq[s * B].data_ptr(), B)
+        h.begin_batch(seq[step_base(s)].data_ptr(), B)
         # the waits the library would insert, made here so the events time kernels, not waits
         if c4 and ba_issued[s % 2]:
             stream.wait_event(ba_done[s % 2])
@@ -565,7 +614,7 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
             i = names.index("tsdf")
             if evs is not None:
                 evs[i][0].record(bstream)
-            h.tsdf_integrate(seq[s * B].data_ptr() + 3 * width * height, 5 * width * height, B,
+            h.tsdf_integrate(seq[step_base(s)].data_ptr() + 3 * width * height, 5 * width * height * P, B,
                              first_frame=s * B, stream=bsp)
             if evs is not None:
                 evs[i][1].record(bstream)
@@ -602,7 +651,7 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     torch.cuda.synchronize()
     for r in range(n_iso):
         s_iso = r % (args.warmup + args.steps)   # replayed input: only the durations are used
-        h.begin_batch(seq[s_iso * B].data_ptr(), B)
+        h.begin_batch(seq[step_base(s_iso)].data_ptr(), B)
         prs = []
         for k in kern:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -621,7 +670,7 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
         for i, k in enumerate(names):
             if timed_all or k in timed_set:
                 per_kernel_us[k] = per_kernel_us.get(k, 0.0) + evs[i][0].elapsed_time(evs[i][1]) * 1e3 / args.steps  # us
-    unit_bytes = (frame_bytes(rect.width, rect.height, cfg.n_features, n_img=1, channels=5, matchings=1) if c5 else
+    unit_bytes = (frame_bytes(rect.width, rect.height, cfg.n_features, n_img=P, n_pairs=P, channels=5, matchings=1) if c5 else
                   frame_bytes(rect.width, rect.height, cfg.n_features, n_img=2 * P, n_pairs=P))
     dom_bytes = unit_bytes * B          # §8d per-frame bytes x the frames one launch processes
     # C4's MFMA kernel: back-to-back replays of k_ba_schur on the last solved window, between two
@@ -690,9 +739,10 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     else:
         front_roofline = None
     if c5:
-        workload = ("C5: one RGB-D camera per GPU, 1280x720 BGR u8 + aligned u16 mm depth, on-device gray conversion, "
-                    "2000 FAST/rBRIEF keypoints, 4 levels, temporal brute-force Hamming, depth-lookup 3D points, "
-                    "P3P-RANSAC(128)+GN pose")
+        workload = ("C5: 4-camera RGB-D rig (brackets.urdf joints, sources of run_slam.py:45-50), 1280x720 BGR u8 + "
+                    "aligned u16 mm depth per camera, on-device gray conversion, 2000 FAST/rBRIEF keypoints, 4 levels, "
+                    "temporal brute-force Hamming, depth-lookup 3D points, P3P-RANSAC(128)+GN per camera, rig pose "
+                    "by generalised PnP over all cameras, on one GPU")
     elif c4:
         workload = ("C4: 1x stereo pair 1280x800, 4000 FAST/rBRIEF keypoints per image, 4 levels, stereo+temporal "
                     "brute-force Hamming, P3P-RANSAC(128)+GN pose, 10-keyframe local BA (keyframe every 5 frames, "
@@ -714,9 +764,9 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong" if c3 else "weak",
+        "scaling": "strong" if (c3 or c5) else "weak",
         "vs_baseline": None,
-        "dtype": "u8" + ("+f64" if (c4 or c3) else ""),
+        "dtype": "u8+f64",
         "data": f"synthetic: seeded room renderer, {args.unique} distinct {width}x{height} "
                 f"{'RGB-D' if c5 else 'rig' if c3 else 'stereo'} frames per rank replayed as a triangle wave, "
                 f"resident in HBM before timing",
@@ -724,8 +774,8 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
             "workload": workload,
             "frames_per_step": B,
             "n_features": cfg.n_features,
-            "parallelism": (f"one {'RGB-D camera' if c5 else 'stereo source'} per GPU x{world}"
-                            + (" (independent replicas)" if world > 1 else "")) if not c3 else "the whole rig on 1 GPU",
+            "parallelism": (f"one stereo source per GPU x{world}" + (" (independent replicas)" if world > 1 else ""))
+                           if not (c3 or c5) else "the whole rig on 1 GPU",
         },
         "roofline": roofline,
         "latency_b1_ms": lat_ms,
@@ -737,6 +787,8 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     }
     if c3:
         out["stereo_pair_frames_per_s"] = value * P
+    if c5:
+        out["camera_frames_per_s"] = value * P
     if front_roofline is not None:
         out["front_end_roofline"] = front_roofline
     if "tsdf" in names:
@@ -747,10 +799,17 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     if rank == 0 and world == 1 and args.cpu_budget > 0:
         procs = args.cpu_procs or usable_cpus()
         if c5:
-            bgr = np.stack([b for b, _ in rgbd_frames])
-            dep = np.stack([d for _, d in rgbd_frames])
-            out["cpu_baseline"] = cpu_baseline((bgr, dep), _rect_dict(rect), cfg, args.cpu_budget, procs,
-                                               f"synthetic {width}x{height} RGB-D frames ({len(bgr)} distinct)")
+            from thor_slam_amd.rgbd import unpack_rgbd
+
+            bgr = np.empty((len(uniq), P, height, width, 3), np.uint8)
+            dep = np.empty((len(uniq), P, height, width), np.uint16)
+            for i in range(len(uniq)):
+                for q in range(P):
+                    bgr[i, q], dep[i, q] = unpack_rgbd(uniq[i, q], width, height)
+            out["cpu_baseline"] = cpu_baseline((bgr, dep), [[_rect_dict(r) for r in rects], E], cfg, args.cpu_budget,
+                                               procs, f"synthetic {width}x{height} 4-camera RGB-D rig frames "
+                                                      f"({len(bgr)} distinct)")
+            out["cpu_baseline"]["unit"] = "rig frames/s"
         elif c3:
             out["cpu_baseline"] = cpu_baseline(uniq, [[_rect_dict(r) for r in rects], E], cfg, args.cpu_budget, procs,
                                                f"synthetic {width}x{height} 8-stream rig frames ({len(uniq)} distinct)")
@@ -769,29 +828,43 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
     from thor_slam_amd.params import HipSlamConfig
     from thor_slam_amd.shard import DistShardedRig, ShardPlan, StageTimer
 
-    c3 = args.config == "c3"
-    if not c3 and world % 2:
+    c3, c5 = args.config == "c3", args.config == "c5"
+    if args.config == "c2" and world % 2:
         raise SystemExit("c2 over several GPUs shards stereo pairs' streams: --gpus must be even")
-    names = RIG_SOURCES if c3 else RIG_SOURCES[:world // 2]
-    width, height = 640, 400
-    cfg = HipSlamConfig()
-    B = args.batch or (256 if c3 else C2_BATCH)
-    args.unique = args.unique or 48
-    _, cams, pairs, rects, E = rig_setup(names, width, height)
-    P, C = len(rects), 2 * len(rects)
+    if c5 and 4 % world:
+        raise SystemExit("c5 shards the 4 RGB-D cameras: --gpus must be 1, 2 or 4")
+    names = RIG_SOURCES if (c3 or c5) else RIG_SOURCES[:world // 2]
+    width, height = (1280, 720) if c5 else (640, 400)
+    cfg = HipSlamConfig(rgbd=True) if c5 else HipSlamConfig()
+    B = args.batch or (C5_BATCH if c5 else 256 if c3 else C2_BATCH)
+    args.unique = args.unique or (24 if c5 else 48)
+    if c5:
+        _, cams, pairs, rects, E = rgbd_rig_setup(names, width, height)
+        C = len(rects)
+    else:
+        _, cams, pairs, rects, E = rig_setup(names, width, height)
+        C = 2 * len(rects)
+    P = len(rects)
     plan = ShardPlan(C, world, B)
     c0, c1 = plan.cams(rank)
     workers = max(1, min(16, max(2, usable_cpus() // max(1, world)), args.unique * (c1 - c0)))
     t_r = time.perf_counter()
-    uniq = render_rig_frames(names, args.unique, c0, c1, workers, width, height)   # this rank's streams only
+    if c5:   # this rank's cameras only; one batch resident, replayed (whole triangle-wave periods)
+        uniq = render_rgbd_rig_frames(names, args.unique, c0, c1, workers, width, height)
+        if B % (2 * (args.unique - 1)):
+            raise SystemExit(f"--config c5 needs --batch a multiple of {2 * (args.unique - 1)}")
+        total = B
+    else:
+        uniq = render_rig_frames(names, args.unique, c0, c1, workers, width, height)   # this rank's streams only
+        total = (args.warmup + args.steps) * B
     t_render = time.perf_counter() - t_r
-    total = (args.warmup + args.steps) * B
     idx = torch.from_numpy(triangle_indices(total, args.unique)).cuda()
     seq = torch.from_numpy(uniq).cuda().index_select(0, idx).contiguous()   # [total, S, H, W] in HBM
+    batch_of = (lambda s: seq) if c5 else (lambda s: seq[s * B:(s + 1) * B])
     rig = DistShardedRig(rects, cfg, B, base_T_rect=E if P > 1 else None, device=dev_index, exchange=args.exchange,
                          front_priority=bool(args.front_priority))
     for s in range(args.warmup):
-        rig.step(seq[s * B:(s + 1) * B])
+        rig.step(batch_of(s))
     rig.drain()
     dist.barrier()
     torch.cuda.synchronize()
@@ -799,7 +872,7 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
     t0 = time.perf_counter()
     for k in range(args.steps):
         s = args.warmup + k
-        rig.step(seq[s * B:(s + 1) * B], timer)
+        rig.step(batch_of(s), timer)
     rig.drain()
     dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -813,26 +886,35 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
     # the dominant kernel's algorithmic bytes: the §8d rig-frame bytes x the share of the rig one
     # launch covers (front kernels: S of C streams for B frames; back kernels: all streams for B/N frames)
     S = plan.streams_per_rank
-    unit_bytes = frame_bytes(width, height, cfg.n_features, n_img=2 * P, n_pairs=P)   # per rig frame
+    unit_bytes = (frame_bytes(width, height, cfg.n_features, n_img=P, n_pairs=P, channels=5, matchings=1) if c5 else
+                  frame_bytes(width, height, cfg.n_features, n_img=2 * P, n_pairs=P))   # per rig frame
     front = ("rectify_pyramid", "detect", "select", "describe")
     dom = max(per_kernel_us, key=per_kernel_us.get)
-    share = (S / C) * B if dom in front else B / world
+    # front kernels (and, RGB-D, the whole per-camera back end) cover S of C cameras for B frames;
+    # the other back kernels all cameras for B / N frames
+    share = (S / C) * B if (dom in front or (c5 and dom != "rig")) else B / world
     dom_bytes = unit_bytes * share
     achieved = dom_bytes / (per_kernel_us[dom] * 1e-6) / 1e9
     sb, pr = rig.rk.block, rig.rk.record
-    alltoall = args.exchange == "alltoall"
-    xbytes = {  # what one rank sends per step
-        "raw_images": ((world - 1) * plan.recv_frames if alltoall else (B + 1)) * S * width * height,
-        "stream_blocks": ((world - 1) * plan.recv_frames if alltoall else (B + 1)) * S * sb,
-        "pose_records": plan.frames_per_rank * pr,
-        "stream_block_bytes": sb,
-        "pose_record_bytes": pr,
-    }
+    alltoall = args.exchange == "alltoall" or c5
+    if c5:
+        pb = rig.rk.pblock
+        xbytes = {"pair_blocks": (world - 1) * plan.frames_per_rank * S * pb, "pose_records": plan.frames_per_rank * pr,
+                  "pair_block_bytes": pb, "pose_record_bytes": pr}
+    else:
+        xbytes = {  # what one rank sends per step
+            "raw_images": ((world - 1) * plan.recv_frames if alltoall else (B + 1)) * S * width * height,
+            "stream_blocks": ((world - 1) * plan.recv_frames if alltoall else (B + 1)) * S * sb,
+            "pose_records": plan.frames_per_rank * pr,
+            "stream_block_bytes": sb,
+            "pose_record_bytes": pr,
+        }
+    xbytes["total_sent"] = sum(v for k_, v in xbytes.items() if not k_.endswith("_bytes"))
     rig.close()
     frames_total = args.steps * B        # rig frames
-    value = frames_total / elapsed * (1 if c3 else P)
+    value = frames_total / elapsed * (1 if (c3 or c5) else P)
     out = {
-        "metric": METRIC_C3 if c3 else METRIC,
+        "metric": METRIC_C3 if c3 else METRIC_C5 if c5 else METRIC,
         "value": value,
         "unit": "frames/s",
         "n_gpus": world,
@@ -840,22 +922,28 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong" if c3 else "weak",
+        "scaling": "strong" if (c3 or c5) else "weak",
         "vs_baseline": None,
         "dtype": "u8+f64",
-        "data": f"synthetic: seeded room renderer, {args.unique} distinct 640x400 frames of each rank's camera "
+        "data": f"synthetic: seeded room renderer, {args.unique} distinct {width}x{height} frames of each rank's camera "
                 f"streams (bracket rig, one shared room) replayed as a triangle wave, resident in HBM before timing",
         "config": {
-            "workload": ("C3: 4x OAK stereo rig (8 streams, brackets.urdf joints, sources of run_slam.py:45-50)"
-                         if c3 else f"C2 streams over {world} GPUs: {P} stereo source(s) of the bracket rig "
-                                    f"({C} streams), one camera stream per GPU")
-                        + ", 640x400, 2000 FAST/rBRIEF keypoints per image, per-pair stereo+temporal Hamming + "
-                          "P3P-RANSAC(128)+GN" + (", rig pose by generalised PnP over all pairs" if P > 1 else ""),
+            "workload": ("C5: 4-camera RGB-D rig (brackets.urdf joints), 1280x720 BGR + aligned u16 depth per camera, "
+                         "2000 FAST/rBRIEF keypoints, temporal Hamming + depth-lookup 3D points + P3P-RANSAC(128)+GN "
+                         "per camera, rig pose by generalised PnP over all cameras" if c5 else
+                         ("C3: 4x OAK stereo rig (8 streams, brackets.urdf joints, sources of run_slam.py:45-50)"
+                          if c3 else f"C2 streams over {world} GPUs: {P} stereo source(s) of the bracket rig "
+                                     f"({C} streams), one camera stream per GPU")
+                         + ", 640x400, 2000 FAST/rBRIEF keypoints per image, per-pair stereo+temporal Hamming + "
+                           "P3P-RANSAC(128)+GN" + (", rig pose by generalised PnP over all pairs" if P > 1 else "")),
             "frames_per_step": B,
             "streams": C,
             "stereo_pairs": P,
             "n_features": cfg.n_features,
-            "parallelism": (f"{S} camera stream(s) per GPU x{world}: front end per stream, RCCL "
+            "parallelism": (f"{S} RGB-D camera(s) per GPU x{world}: each GPU tracks its cameras over the batch, "
+                            f"RCCL all-to-all of pair blocks (pose + correspondences), rig pose on each GPU's "
+                            f"{plan.frames_per_rank}-frame range, RCCL all-gather of pose records" if c5 else
+                            f"{S} camera stream(s) per GPU x{world}: front end per stream, RCCL "
                             f"{'all-to-all' if alltoall else 'all-gather'} of raw images + keypoint/descriptor "
                             f"stream blocks, per-pair back end + rig pose on each GPU's {plan.frames_per_rank}-frame "
                             f"range, RCCL all-gather of pose records"),
@@ -872,6 +960,8 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
     }
     if c3:
         out["stereo_pair_frames_per_s"] = value * P
+    elif c5:
+        out["camera_frames_per_s"] = value * P
     else:
         out["rig_frames_per_s"] = frames_total / elapsed
     return out
@@ -976,7 +1066,7 @@ def main() -> None:
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index), timeout=tmo)
         else:
             dist.init_process_group(args.dist_backend, timeout=tmo)
-    sharded = world > 1 and args.config in ("c2", "c3")
+    sharded = world > 1 and args.config in ("c2", "c3", "c5")
     out = run_sharded(args, world, rank, dev_index) if sharded else run_single(args, world, rank, dev_index)
     if world > 1:
         dist.barrier()

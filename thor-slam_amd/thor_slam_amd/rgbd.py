@@ -14,3 +14,10 @@ def pack_rgbd(bgr: np.ndarray, depth: np.ndarray) -> np.ndarray:
     """One RGB-D record as the device reads it: BGR u8 bytes followed by the u16 depth bytes."""
     return np.concatenate([np.ascontiguousarray(bgr, dtype=np.uint8).reshape(-1),
                            np.ascontiguousarray(depth, dtype="<u2").view(np.uint8).reshape(-1)])
+
+
+def unpack_rgbd(record: np.ndarray, width: int, height: int) -> tuple[np.ndarray, np.ndarray]:
+    """Inverse of ``pack_rgbd``: (BGR u8 H x W x 3, depth u16 H x W) views of one record."""
+    rec = np.ascontiguousarray(record, dtype=np.uint8).reshape(-1)
+    n = width * height
+    return rec[:3 * n].reshape(height, width, 3), rec[3 * n:5 * n].view("<u2").reshape(height, width)
