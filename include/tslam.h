@@ -348,14 +348,15 @@ int tslam_submit_sharded(tslam_handle* h, const uint8_t* images, void* stream);
  *     handle), all ranks' sends / receives issued inside one ncclGroupStart / ncclGroupEnd;
  *   TSLAM_TRANSPORT_COPY: device-to-device copies (hipMemcpyAsync) instead of RCCL, same buffers and
  *     ordering; several ranks may share a device (tests world > 1 on one GPU).
- * tslam_group_submit: one batch; images[r] = rank r's cameras as for tslam_submit_sharded, streams[r]
- *   (NULL array or entries = each device's null stream) orders the input and then waits for the batch.
+ * tslam_group_submit: one batch of n_frames (a multiple of n, <= max_batch); images[r] = rank r's
+ *   cameras as for tslam_submit_sharded, streams[r] (NULL array or entries = each device's null
+ *   stream) orders the input and then waits for the batch.
  * tslam_group_destroy before destroying the handles (they return to unsharded). */
 #define TSLAM_TRANSPORT_RCCL 0
 #define TSLAM_TRANSPORT_COPY 1
 typedef struct tslam_group tslam_group;
 int tslam_group_create(tslam_handle* const* handles, int n, int transport, tslam_group** out);
-int tslam_group_submit(tslam_group* g, const uint8_t* const* images, void* const* streams);
+int tslam_group_submit(tslam_group* g, const uint8_t* const* images, int n_frames, void* const* streams);
 int tslam_group_destroy(tslam_group* g);
 
 /* A8 window of stereo pair `pair` after the last enqueued solve (synchronises the device),

@@ -233,3 +233,35 @@ def test_sharded_batch_must_divide_by_world():
     h.begin_batch(1 << 20, 2)   # accepted (nothing launched)
     h.end_batch()
     h.close()
+
+
+def test_library_driver_short_batches_identical():
+    """Batches of 4, 8 and 4 frames through a max_batch-8 group of 4 ranks (the per-batch frame
+    ranges, per-peer slots and the all-gather shrink with the batch) == the unsharded handle fed
+    the same batches."""
+    import torch
+
+    from thor_slam_amd._lib import Handle, HandleGroup
+
+    sizes = [4, 8, 4]
+    sc = rig_scene(TWO, sum(sizes))
+    cfg = HipSlamConfig()
+    h1 = Handle(sc["rects"], cfg, max_batch=8)
+    h1.set_rig(sc["E"])
+    hs = [Handle(sc["rects"], cfg, max_batch=8) for _ in range(4)]
+    for h in hs:
+        h.set_rig(sc["E"])
+    grp = HandleGroup(hs, "copy")
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    parts = [dev[:, r:r + 1].contiguous() for r in range(4)]
+    f0 = 0
+    for n in sizes:
+        h1.submit(dev[f0].data_ptr(), n, torch.cuda.current_stream().cuda_stream)
+        want = {"pairs": h1.read_poses(n), "rig": h1.read_rig_poses(n)}
+        grp.submit([p[f0].data_ptr() for p in parts], n)
+        for h in hs:
+            assert_identical({"pairs": h.read_poses(n), "rig": h.read_rig_poses(n)}, want)
+        f0 += n
+    grp.close()
+    for h in hs + [h1]:
+        h.close()

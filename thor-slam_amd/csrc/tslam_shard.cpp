@@ -77,8 +77,10 @@ enum Which { RAW = 0, FEAT = 1, POSE = 2 };
 struct tslam_shard_driver {
     int world = 1, transport = TSLAM_TRANSPORT_RCCL;
     bool rgbd = false, rig = false;
-    int S = 0, B = 0, fpr = 0, nr = 0;   // cameras per rank, batch, frames per rank, frames sent per peer
-    size_t img = 0, raw_q = 0, feat_q = 0, rec = 0;   // bytes: image, per peer (raw, features), pose record
+    int S = 0, B = 0;                    // cameras per rank, max_batch
+    int n = 0, fpr = 0, nr = 0;          // this batch: frames, frames per rank, frames sent per peer (stereo)
+    size_t img = 0, rec = 0, sblk = 0, pblk = 0;   // bytes: image, pose record, stream block, pair block
+    size_t raw_q = 0, feat_q = 0;        // this batch: bytes per peer (raw images, stream / pair blocks)
     int64_t batches = 0;
     std::vector<Rank> ranks;   // local ranks: all of a group, one after tslam_comm_init
 };
@@ -124,18 +126,26 @@ static int plan(tslam_shard_driver* d, tslam_handle* h, int world) {
     d->rig = in.rig != 0;
     d->S = in.C / world;
     d->B = in.B;
-    d->fpr = in.B / world;
-    d->nr = d->fpr + 1;
     d->img = (size_t)in.W * in.H;
     d->rec = (size_t)in.pose_record;
+    d->sblk = (size_t)in.stream_block;
+    d->pblk = (size_t)in.pair_block;
+    return TSLAM_OK;
+}
+
+// Per-batch geometry of n frames (n % world == 0, n <= max_batch): the buffers are sized for
+// max_batch, a shorter batch uses the front of each per-peer slot.
+static void geom(tslam_shard_driver* d, int n) {
+    d->n = n;
+    d->fpr = n / d->world;
+    d->nr = d->fpr + 1;
     if (d->rgbd) {
         d->raw_q = 0;
-        d->feat_q = (size_t)d->fpr * d->S * in.pair_block;   // my cameras' pair blocks of a peer's range
+        d->feat_q = (size_t)d->fpr * d->S * d->pblk;   // my cameras' pair blocks of a peer's range
     } else {
-        d->raw_q = (size_t)d->nr * d->S * d->img;              // frames lo-1 .. hi-1 of a peer's range
-        d->feat_q = (size_t)d->nr * d->S * in.stream_block;
+        d->raw_q = (size_t)d->nr * d->S * d->img;        // frames lo-1 .. hi-1 of a peer's range
+        d->feat_q = (size_t)d->nr * d->S * d->sblk;
     }
-    return TSLAM_OK;
 }
 
 static int setup_rank(tslam_shard_driver* d, Rank& r) {
@@ -151,6 +161,7 @@ static int setup_rank(tslam_shard_driver* d, Rank& r) {
     for (hipEvent_t* e : {&r.ev_in, &r.ev_front, &r.ev_x, &r.ev_push, &r.ev_done, &r.consumed[0], &r.consumed[1]})
         SHCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     const size_t N = d->world;
+    geom(d, d->B);   // allocation sizes: a full batch
     for (int k = 0; k < 2; ++k) {
         if (!d->rgbd) {
             RC(alloc(r, &r.raw_send[k], N * d->raw_q));
@@ -236,11 +247,14 @@ static int stage_raw(tslam_shard_driver* d, Rank& r, const uint8_t* images, int 
         SHCHK(hipMemcpyAsync(out, first, frame, hipMemcpyDeviceToDevice, r.xs));
         SHCHK(hipMemcpyAsync(out + frame, images + (size_t)lo * frame, (size_t)d->fpr * frame, hipMemcpyDeviceToDevice, r.xs));
     }
-    SHCHK(hipMemcpyAsync(r.prev_raw, images + (size_t)(d->B - 1) * frame, frame, hipMemcpyDeviceToDevice, r.xs));
+    SHCHK(hipMemcpyAsync(r.prev_raw, images + (size_t)(d->n - 1) * frame, frame, hipMemcpyDeviceToDevice, r.xs));
     return TSLAM_OK;
 }
 
-static int submit(tslam_shard_driver* d, const uint8_t* const* images, void* const* streams) {
+static int submit(tslam_shard_driver* d, const uint8_t* const* images, int n, void* const* streams) {
+    if (n < d->world || n > d->B || n % d->world)
+        return tslam_internal_fail(TSLAM_EINVAL, "a sharded batch needs world <= n_frames <= max_batch, n_frames % world == 0");
+    geom(d, n);
     const int k = (int)(d->batches & 1), N = d->world, S = d->S;
     const int front[3] = {TSLAM_STAGE_RECTIFY, TSLAM_STAGE_DETECT, TSLAM_STAGE_DESCRIBE};
     for (size_t i = 0; i < d->ranks.size(); ++i) {   // inputs, buffer reuse, raw images out
@@ -250,7 +264,7 @@ static int submit(tslam_shard_driver* d, const uint8_t* const* images, void* con
         for (hipStream_t s : {r.fs, r.xs, r.bs}) SHCHK(hipStreamWaitEvent(s, r.ev_in, 0));
         if (r.consumed_armed[k])
             for (hipStream_t s : {r.fs, r.xs}) SHCHK(hipStreamWaitEvent(s, r.consumed[k], 0));
-        RC(tslam_begin_batch(r.h, images[i], d->B));
+        RC(tslam_begin_batch(r.h, images[i], n));
         if (!d->rgbd) RC(stage_raw(d, r, images[i], k));
     }
     if (!d->rgbd) RC(exchange(d, RAW, k));
@@ -369,7 +383,7 @@ int tslam_submit_sharded(tslam_handle* h, const uint8_t* images, void* stream) {
     tslam_shard_driver* d = tslam_internal_driver(h);
     if (!d || d->ranks.size() != 1) return tslam_internal_fail(TSLAM_ESTATE, "tslam_comm_init first");
     void* streams[1] = {stream};
-    return submit(d, &images, streams);
+    return submit(d, &images, d->B, streams);
 }
 
 struct tslam_group {
@@ -432,11 +446,11 @@ int tslam_group_create(tslam_handle* const* handles, int n, int transport, tslam
     return TSLAM_OK;
 }
 
-int tslam_group_submit(tslam_group* g, const uint8_t* const* images, void* const* streams) {
+int tslam_group_submit(tslam_group* g, const uint8_t* const* images, int n_frames, void* const* streams) {
     if (!g || !g->d || !images) return tslam_internal_fail(TSLAM_EINVAL, "bad argument");
     for (size_t i = 0; i < g->d->ranks.size(); ++i)
         if (!images[i]) return tslam_internal_fail(TSLAM_EINVAL, "null images");
-    return submit(g->d, images, streams);
+    return submit(g->d, images, n_frames, streams);
 }
 
 int tslam_group_destroy(tslam_group* g) {

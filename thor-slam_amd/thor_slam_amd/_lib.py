@@ -139,7 +139,7 @@ _SIGNATURES = {
     "tslam_unpack_pairs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_group_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
-    "tslam_group_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_group_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "tslam_group_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "tslam_pack_poses": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_unpack_poses": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
@@ -673,11 +673,13 @@ class HandleGroup:
         _check(self.lib.tslam_group_create(arr, len(handles), TRANSPORT[transport], ctypes.byref(g)))
         self.g = g
 
-    def submit(self, image_ptrs: list[int], streams: list[int] | None = None) -> None:
-        """One batch: rank r's cameras at device pointer image_ptrs[r] (layout of tslam_submit_sharded)."""
+    def submit(self, image_ptrs: list[int], n_frames: int | None = None, streams: list[int] | None = None) -> None:
+        """One batch of ``n_frames`` (default max_batch; a multiple of the rank count): rank r's
+        cameras at device pointer image_ptrs[r] (layout of tslam_submit_sharded)."""
         imgs = (ctypes.c_void_p * len(image_ptrs))(*[int(p) for p in image_ptrs])
         sts = None if streams is None else (ctypes.c_void_p * len(streams))(*[int(s) for s in streams])
-        _check(self.lib.tslam_group_submit(self.g, imgs, sts))
+        n = self.handles[0].max_batch if n_frames is None else int(n_frames)
+        _check(self.lib.tslam_group_submit(self.g, imgs, n, sts))
 
     def close(self) -> None:
         if getattr(self, "g", None):

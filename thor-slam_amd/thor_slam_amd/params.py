@@ -83,6 +83,12 @@ class HipSlamConfig(SlamConfig):
     tsdf_dims: tuple = (200, 80, 220)
     # pipeline
     batch_size: int = 1             # frames per submission (1 = synchronous latency mode)
+    # one camera stream per GPU from one process (the rig cuVSLAM's multicam mode
+    # takes, launch/thor_visual_slam.launch.py:49,81): the rig's cameras sharded over these devices,
+    # rank r on devices[r] (empty = the engine's one device, unsharded).  shard_transport "rccl" =
+    # an RCCL clique over the devices (one per rank), "copy" = device copies (ranks may share a device)
+    devices: tuple = ()
+    shard_transport: str = "rccl"
 
     def validate(self) -> None:
         if not 1 <= self.n_levels <= MAX_LEVELS:
@@ -113,6 +119,13 @@ class HipSlamConfig(SlamConfig):
             raise ValueError("ba_kf_interval and ba_iters must be >= 1")
         if not (1 <= self.loop_max_keyframes <= 1024 and 1 <= self.loop_signature <= 256 and self.loop_kf_interval >= 1):
             raise ValueError("loop_max_keyframes must be in [1, 1024], loop_signature in [1, 256], loop_kf_interval >= 1")
+        if self.devices:
+            if self.batch_size % len(self.devices):
+                raise ValueError("batch_size must be a multiple of len(devices) (equal frame ranges per rank)")
+            if self.ba_window > 0 or self.dense_map:
+                raise ValueError("a sharded rig (devices) runs without local BA and the dense map")
+            if self.shard_transport not in ("rccl", "copy"):
+                raise ValueError("shard_transport must be 'rccl' or 'copy'")
         if not 0 <= self.max_hamming <= 253:
             raise ValueError("max_hamming must be in [0, 253] (the mutual check keeps distances as bytes)")
 

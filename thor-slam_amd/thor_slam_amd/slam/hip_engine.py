@@ -25,6 +25,12 @@ pose stays the fused front end and ``get_map`` uses pair 0.
 With ``dense_map`` (RGB-D input) every batch's depth of pair 0 is integrated into a dense TSDF
 volume on the device with the batch's tracked poses (nvblox's role in the reference pipeline,
 ``scripts/run_pipeline.py:218-256``); ``get_dense_map`` returns it.
+With ``HipSlamConfig(devices=[d0, d1, ...])`` the rig is sharded one camera stream per GPU from
+this one process (cuVSLAM's multicam mode, launch/thor_visual_slam.launch.py:49,81):
+one handle per device, driven by the library as one sharded rig (``tslam_group_*``: an RCCL clique
+over the devices, or device copies with ``shard_transport="copy"``); the published poses are
+bit-identical to the one-device engine's.  Frames are submitted in multiples of the device count
+(a trailing remainder waits for the next ``process_frames``); loop closure is not run sharded.
 ``confidence`` follows isaac_ros.py:312.  With ``batch_size > 1`` frames are staged and the
 batch runs on the GPU when full (or on ``flush``).  Submission is asynchronous
 (``tslam_submit_host``: pinned double-buffered staging, the batch's H2D copy and kernels on the
@@ -43,7 +49,7 @@ import threading
 import numpy as np
 from scipy.spatial.transform import Rotation
 
-from .._lib import POSE_INIT, POSE_LOST, POSE_OK, Handle
+from .._lib import POSE_INIT, POSE_LOST, POSE_OK, Handle, HandleGroup
 from ..calib import (StereoRectification, confidence_from_covariance, extract_cameras, rgbd_pairs, rgbd_undistort,
                      stereo_pairs, stereo_rectify)
 from ..camera.rig import RigCalibration
@@ -142,6 +148,7 @@ class HipSlamEngine(SlamEngine):
         self._map_loaded = False
         self._loop: _LoopGraph | None = None     # set up by initialize() when loop closure is on
         self._in_flight = 0                       # batches submitted, not yet published
+        self._shard: dict | None = None           # sharded rig (config.devices): handles, group, inputs
 
     # ------------------------------------------------------------------------------------------
     def initialize(self, calibration: RigCalibration, config: SlamConfig | None = None) -> None:
@@ -168,14 +175,17 @@ class HipSlamEngine(SlamEngine):
             if not torch.cuda.is_available():
                 raise RuntimeError("no ROCm device visible: the MI355X back end has no CPU fallback")
             self._torch = torch
-            self._handle = Handle(self._rects, cfg, max_batch=cfg.batch_size, device=self._device)
             rect0 = self._rects[0]
             if cfg.rgbd:   # one [BGR | u16 depth] record of 5*H*W bytes per camera
                 shape = (cfg.batch_size, len(self._pairs), 5 * rect0.height * rect0.width)
             else:
                 shape = (cfg.batch_size, 2 * len(self._pairs), rect0.height, rect0.width)
-            self._dev_images = torch.empty(shape, dtype=torch.uint8, device=f"cuda:{self._device}")
-            self._host_images = torch.empty(shape, dtype=torch.uint8).pin_memory()
+            if cfg.devices:
+                self._init_shard(shape)
+            else:
+                self._handle = Handle(self._rects, cfg, max_batch=cfg.batch_size, device=self._device)
+                self._dev_images = torch.empty(shape, dtype=torch.uint8, device=f"cuda:{self._device}")
+                self._host_images = torch.empty(shape, dtype=torch.uint8).pin_memory()
             self._base_T_rects = [self._cameras[l].extrinsics.to_4x4_matrix() @ r.left_optical_T_rect()
                                   for (l, _), r in zip(self._pairs, self._rects)]
             self._base_T_rect = self._base_T_rects[0]
@@ -185,14 +195,16 @@ class HipSlamEngine(SlamEngine):
             if cfg.imu_fusion and cfg.imu_accel:
                 self._imu = ImuPropagator(self._base_T_rect[:3, :3].T @ self._base_R_imu, cfg.accelerometer_noise_density,
                                           cfg.accelerometer_random_walk, cfg.imu_rot_sigma, cfg.imu_trans_floor)
-            if len(self._pairs) > 1:   # the rig's body motion is solved on the device from all pairs
+            if len(self._pairs) > 1 and self._shard is None:   # the rig's body motion, on the device from all pairs
                 self._handle.set_rig(self._base_T_rects)
             if cfg.dense_map:
                 self._handle.tsdf_init(cfg.tsdf_origin, cfg.tsdf_dims, cfg.voxel_size,
                                        cfg.tsdf_integrator_truncation_distance_vox,
                                        cfg.tsdf_integrator_max_integration_distance_m, cfg.tsdf_max_weight)
             self._loop = None
-            if cfg.enable_loop_closure:
+            if cfg.enable_loop_closure and self._shard is not None:
+                logger.warning("loop closure is not run on a sharded rig (devices=%s)", cfg.devices)
+            elif cfg.enable_loop_closure:
                 # place recognition and loop verification on pair 0's camera; on a multi-pair rig
                 # the keyframe nodes are pair 0's rectified-left poses taken from the rig's body
                 # poses (k_rig_pose), and the pose-graph correction moves the body poses
@@ -204,6 +216,55 @@ class HipSlamEngine(SlamEngine):
             raise RuntimeError(f"HipSlamEngine initialisation failed: {exc}") from exc
         self._state = TrackingState.INITIALIZING
         logger.info("Initialized HIP SLAM with %d cameras, %d stereo pair(s)", len(self._cameras), len(self._pairs))
+
+    def _init_shard(self, shape: tuple) -> None:
+        """One handle per device (the whole rig on each, rank r owning cameras [r*S, (r+1)*S)) and
+        the library's group driver over them; pinned staging + device input per rank."""
+        torch, cfg = self._torch, self._config
+        devs = [int(d) for d in cfg.devices]
+        world = len(devs)
+        n_cams = shape[1]
+        if n_cams % world:
+            raise RuntimeError(f"{n_cams} cameras do not split over {world} devices")
+        handles = []
+        for d in devs:
+            h = Handle(self._rects, cfg, max_batch=cfg.batch_size, device=d)
+            if len(self._rects) > 1:
+                h.set_rig([self._cameras[l].extrinsics.to_4x4_matrix() @ r.left_optical_T_rect()
+                           for (l, _), r in zip(self._pairs, self._rects)])
+            handles.append(h)
+        group = HandleGroup(handles, cfg.shard_transport)
+        S = n_cams // world
+        part = (cfg.batch_size, S) + tuple(shape[2:])
+        self._shard = {"handles": handles, "group": group, "world": world, "S": S, "devices": devs,
+                       "dev": [torch.empty(part, dtype=torch.uint8, device=f"cuda:{d}") for d in devs],
+                       "host": [torch.empty(part, dtype=torch.uint8).pin_memory() for _ in devs]}
+        self._handle = handles[0]   # every rank ends a batch with the whole rig's poses
+
+    def _submit_sharded(self) -> None:
+        """The staged frames in multiples of the device count through the group driver (rank r
+        gets its cameras' slice), then the batch's poses from rank 0; synchronous."""
+        sh, torch = self._shard, self._torch
+        n = len(self._staged) - len(self._staged) % sh["world"]
+        if n == 0:
+            return
+        batch, imus = self._staged[:n], self._staged_imu[:n]
+        stamps = [ts for _, ts in batch]
+        if self._config.imu_fusion:
+            self._set_imu_prior(stamps, imus)
+        S, ptrs, streams = sh["S"], [], []
+        for r, d in enumerate(sh["devices"]):
+            host = sh["host"][r].numpy()
+            for k, (imgs, _) in enumerate(batch):
+                host[k] = imgs[r * S:(r + 1) * S]
+            stream = torch.cuda.current_stream(d)
+            sh["dev"][r][:n].copy_(sh["host"][r][:n], non_blocking=True)
+            ptrs.append(sh["dev"][r].data_ptr())
+            streams.append(stream.cuda_stream)
+        sh["group"].submit(ptrs, n, streams)
+        self._staged, self._staged_imu = self._staged[n:], self._staged_imu[n:]
+        self._prev_stamp = stamps[-1]
+        self._publish(self._read(n), stamps, self._handle.frames_done - n)
 
     # ------------------------------------------------------------------------------------------
     def _frame_images(self, frame_set: SynchronizedFrameSet) -> np.ndarray | None:
@@ -259,6 +320,9 @@ class HipSlamEngine(SlamEngine):
     def _submit_staged(self) -> None:
         n = len(self._staged)
         if n == 0:
+            return
+        if self._shard is not None:
+            self._submit_sharded()
             return
         stamps = [ts for _, ts in self._staged]
         if self._config.imu_fusion:
@@ -339,7 +403,13 @@ class HipSlamEngine(SlamEngine):
                     rot[k, p] = Rotation.from_rotvec(-(bt[:3, :3].T @ w_base) * (ts - prev)).as_matrix()
                     wgt[k, p] = w0
             prev = ts
-        self._handle.set_motion_prior(rot, wgt)
+        self._set_motion_prior(rot, wgt)
+
+    def _set_motion_prior(self, *args) -> None:
+        """The batch's priors on the handle (every rank's handle on a sharded rig: each refines its
+        frame range and chains the whole batch)."""
+        for h in (self._shard["handles"] if self._shard is not None else [self._handle]):
+            h.set_motion_prior(*args)
 
     def _set_inertial_prior(self, stamps: list[float], imus: list) -> None:
         """Gyro + accelerometer: per frame the predicted T_rel of pair 0's rectified-left camera
@@ -372,7 +442,7 @@ class HipSlamEngine(SlamEngine):
                 tp = t0 if p == 0 else _invert(ep) @ e0 @ t0 @ _invert(e0) @ ep
                 rot[k, p], trn[k, p] = tp[:3, :3], tp[:3, 3]
                 wr[k, p], wt[k, p] = st.w_rot, st.w_trans
-        self._handle.set_motion_prior(rot, wr, trn, wt)
+        self._set_motion_prior(rot, wr, trn, wt)
         self._imu_batches.append(samples)
 
     def process_batch(self, images, timestamps: list[float] | None = None, stream=None) -> dict:
@@ -380,6 +450,8 @@ class HipSlamEngine(SlamEngine):
         stereo pairs, or [n, P, 5*H*W] RGB-D records (``rgbd.pack_rgbd``)."""
         if self._handle is None:
             raise RuntimeError("Not initialized")
+        if self._shard is not None:
+            raise RuntimeError("process_batch takes one device's images; a sharded rig (devices) uses process_frames")
         n = int(images.shape[0])
         s = stream if stream is not None else self._torch.cuda.current_stream(self._device)
         self.flush()
@@ -658,7 +730,7 @@ class HipSlamEngine(SlamEngine):
         the device); on success the published poses continue in the map's world frame."""
         if self._handle is None:
             raise RuntimeError("Not initialized")
-        if not self._map_loaded or self._handle.frames_done == 0:
+        if not self._map_loaded or self._handle.frames_done == 0 or self._shard is not None:
             return False
         self.flush()
         res = self._handle.relocalize(self._handle.frames_done - 1)
@@ -692,12 +764,21 @@ class HipSlamEngine(SlamEngine):
         self._map_points, self._map_offset = {}, np.eye(4)
         if self._loop is not None:
             self._loop = _LoopGraph()
-        if self._handle is not None:
-            self._handle.reset()
+        for h in (self._shard["handles"] if self._shard is not None else [self._handle] if self._handle else []):
+            h.reset()
         self._state = TrackingState.INITIALIZING
         self._frame_count = 0
 
     def shutdown(self) -> None:
+        if self._shard is not None:
+            if self._staged:
+                logger.warning("shutdown: %d staged frame(s) short of a multiple of %d devices were not tracked",
+                               len(self._staged), self._shard["world"])
+            self._shard["group"].close()
+            for h in self._shard["handles"]:
+                h.close()
+            self._shard = None
+            self._handle = None
         if self._handle is not None:
             self._handle.close()
             self._handle = None
