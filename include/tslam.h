@@ -211,7 +211,7 @@ int tslam_sync(tslam_handle* h);
  *   timestamps[n] (seconds, the frames' SynchronizedFrameSet.timestamp) may be NULL.  At most two
  *   batches' results are held: an unread batch s-2 is dropped when batch s is submitted.
  * tslam_poll_batch: results of the oldest unread submitted batch: returns 1 and fills the outputs
- *   (per frame and pair as tslam_read_poses, the rig's T_abs/cov/stats when tslam_set_rig, the
+ *   (per frame and pair as tslam_read_poses, the rig's T_rel/T_abs/cov/stats when tslam_set_rig, the
  *   timestamps, its first global frame and frame count) when it has completed (or, with `block`,
  *   after waiting for it); 0 when no batch is ready / pending.  Pointers may be NULL.
  * tslam_poll_pose: non-blocking; the last frame of the newest completed batch not returned before:
@@ -220,14 +220,15 @@ int tslam_sync(tslam_handle* h);
  *   (isaac_ros.py:312; 1 when not tracked).  Returns 1 when a newer pose was written, else 0. */
 int tslam_submit_host(tslam_handle* h, const uint8_t* host_images, const double* timestamps, int n_frames);
 int tslam_poll_batch(tslam_handle* h, int block, int max_frames, double* T_rel, double* T_abs, double* cov, int32_t* stats,
-                     double* rig_T_abs, double* rig_cov, int32_t* rig_stats, double* ts, int64_t* first_frame,
-                     int* n_frames);
+                     double* rig_T_rel, double* rig_T_abs, double* rig_cov, int32_t* rig_stats, double* ts,
+                     int64_t* first_frame, int* n_frames);
 int tslam_poll_pose(tslam_handle* h, double* T, double* cov, double* ts, int32_t* state, float* conf);
 
 /* Results of the last submitted batch (blocks until it is done).  Per frame f and pair p
  * (index f * n_pairs + p): T_rel[16] (cam_{t-1} -> cam_t), T_abs[16] (first left camera frame ->
  * current left camera frame, row-major), cov[36] (rho, omega), stats[8] = {status, n_corr,
- * n_inliers, best_count, best_hyp, global_frame, 0, 0}.  Any pointer may be NULL.  The outputs
+ * n_inliers, best_count, best_hyp, global_frame, sigma^2 (f64 in stats[6..7]: the reprojection
+ * variance that scales cov, 0 when not tracked)}.  Any pointer may be NULL.  The outputs
  * hold `max_frames` frames (TSLAM_EINVAL when the batch has more); TSLAM_ESTATE when no batch has
  * run since tslam_create / tslam_reset. */
 int tslam_read_poses(tslam_handle* h, int max_frames, double* T_rel, double* T_abs, double* cov, int32_t* stats);

@@ -809,6 +809,7 @@ def estimate_pose(corr: dict, intr, cfg, frame: int, prior=None) -> dict:
     sigma2 = sq / max(1, 2 * n_in - 6)
     out["T"] = t
     out["cov"] = np.linalg.inv(hm) * sigma2
+    out["sigma2"] = sigma2
     out["status"] = 0
     return out
 

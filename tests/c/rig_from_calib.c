@@ -118,7 +118,7 @@ static int cmd_run(const tslam_camera_desc* cams, int n, const char* params_path
         if ((rc = tslam_submit_host(h, frames + frame_bytes * f0, ts, nb))) return die("tslam_submit_host", rc);
         int64_t first = -1;
         int got = 0;
-        rc = tslam_poll_batch(h, 1, batch, NULL, T_abs, NULL, stats, np > 1 ? rig_T : NULL, NULL, NULL, ts, &first, &got);
+        rc = tslam_poll_batch(h, 1, batch, NULL, T_abs, NULL, stats, NULL, np > 1 ? rig_T : NULL, NULL, NULL, ts, &first, &got);
         if (rc != 1 || got != nb || first != f0) {
             fprintf(stderr, "poll_batch rc=%d got=%d first=%lld: %s\n", rc, got, (long long)first, tslam_last_error());
             return 1;

@@ -95,30 +95,42 @@ def test_engine_with_imu_source():
     assert r_imu < r_vis + 2e-3 and e_imu < e_vis + 5e-3
 
 
-def _imu_rig(n_frames=40, blackout=None, accel_noise=0.0, gyro_noise=0.0):
+def oracle_filter(cfg, rect_T_imu, accel=True):
+    from oracle import numpy_imu as OI
+
+    return OI.ImuFilter(rect_T_imu[:3, :3], cfg.accelerometer_noise_density, cfg.accelerometer_random_walk,
+                        cfg.gyroscope_noise_density, cfg.gyroscope_random_walk, cfg.imu_rot_floor, cfg.imu_trans_floor,
+                        ba0_sigma=cfg.imu_accel_bias_sigma, bg0_sigma=cfg.imu_gyro_bias_sigma, lever=rect_T_imu[:3, 3],
+                        accel=accel, vis_rot_floor=cfg.imu_vis_rot_floor)
+
+
+def _imu_rig(n_frames=40, blackout=None, accel_noise=0.0, gyro_noise=0.0, gyro_bias=None):
     from thor_slam_amd.camera import CameraRig, Extrinsics
     from thor_slam_amd.camera.types import IMUExtrinsics
     from thor_slam_amd.synthetic import DRB_TO_RDF, SyntheticStereoSource
 
     src = SyntheticStereoSource(seed=0, imu=True, gyro_noise=gyro_noise, accel_noise=accel_noise, blackout=blackout,
-                                n_frames=n_frames)
+                                n_frames=n_frames, gyro_bias=gyro_bias)
     rig_T = src.rig_T_source
     rig = CameraRig([src], rig_extrinsics={src.name: Extrinsics.from_4x4_matrix(rig_T)}, imu_source=src.name,
                     imu_extrinsics=IMUExtrinsics(src.name, Extrinsics.from_4x4_matrix(rig_T @ DRB_TO_RDF)))
     return src, rig
 
 
-def _run_engine(rig, n, cfg):
+def _run_engine(rig, n, cfg, num_cameras=2, keep=None):
     from thor_slam_amd.slam.hip_engine import HipSlamEngine
 
     rig.start()
-    eng = HipSlamEngine(num_cameras=2, config=cfg)
+    eng = HipSlamEngine(num_cameras=num_cameras, config=cfg)
     eng.initialize(rig.calibration)
     got = []
     orig = eng._publish
 
     def record(res, stamps, g0):
-        got.append({k: np.array(res[k][:len(stamps)]) for k in ("T_abs", "T_rel", "stats")})
+        rec = {k: np.array(res[k][:len(stamps)]) for k in ("T_abs", "T_rel", "stats")}
+        if "rig" in res:
+            rec.update({"rig_" + k: np.array(res["rig"][k][:len(stamps)]) for k in ("T_abs", "stats")})
+        got.append(rec)
         orig(res, stamps, g0)
 
     eng._publish = record
@@ -126,6 +138,9 @@ def _run_engine(rig, n, cfg):
         eng.process_frames(rig.get_synchronized_frames())
     eng.flush()
     rects = eng._rects
+    if keep is not None:
+        keep["imu"] = eng._imu
+        keep["pose"] = eng._latest_pose
     eng.shutdown()
     cat = {k: np.concatenate([g[k] for g in got]) for k in got[0]}
     return cat, rects
@@ -149,7 +164,7 @@ def test_accelerometer_prior_and_dropout_match_oracle():
 
     cams = extract_cameras(cal, 2)
     bt = cams[0].extrinsics.to_4x4_matrix() @ rect.left_optical_T_rect()
-    ri = bt[:3, :3].T @ cal.imu_extrinsics.to_4x4_matrix()[:3, :3]
+    rect_T_imu = np.linalg.inv(bt) @ cal.imu_extrinsics.to_4x4_matrix()
     samples = []
     for i in range(n):
         s = src.imu_sample(i)
@@ -158,8 +173,7 @@ def test_accelerometer_prior_and_dropout_match_oracle():
     trk = O.OracleTracker(cfg, dict(fx=rect.fx, fy=rect.fy, cx=rect.cx, cy=rect.cy, baseline=rect.baseline,
                                     map_l=rect.map_left, map_r=rect.map_right))
     frames = np.stack([np.stack([src.render_image(i, 0), src.render_image(i, 1)]) for i in range(n)])
-    filt = OI.ImuFilter(ri, cfg.accelerometer_noise_density, cfg.accelerometer_random_walk, cfg.imu_rot_sigma,
-                        cfg.imu_trans_floor)
+    filt = oracle_filter(cfg, rect_T_imu)
     want = OI.run_sequence(trk, frames, samples, batch, filt)
     status = [int(w["status"]) for w in want]
     assert status[9:13] == [1, 1, 1, 1] and status[13:] == [0] * (n - 13)   # the dropout, then tracking
@@ -191,3 +205,82 @@ def test_accelerometer_bridges_a_visual_dropout():
     travelled = 0.5 * 7 / 30.0   # 0.5 m/s through the 7 untracked frames
     assert errs[False] > 0.5 * travelled
     assert errs[True] < 0.25 * errs[False], errs
+
+
+def test_gyro_bias_estimated_and_drift_reduced():
+    """A constant gyroscope bias (30, -20, 25 mrad/s, an uncalibrated MEMS gyro): with the bias
+    state (learnt from the vision-only motions behind the prior-weighted solutions) the estimate
+    comes within 25 % of it and the trajectory through a 6-frame visual dropout ends closer to the
+    truth than with the bias pinned at zero (imu_gyro_bias_sigma ~ 0: no bias state, as round 2's
+    filter).  The residual estimate error is the vision's own correlated rotation error (~5 mrad/s
+    of yaw on this sequence), which no loosely coupled filter can tell from a bias."""
+    from thor_slam_amd.params import HipSlamConfig
+
+    bias = np.array([0.03, -0.02, 0.025])
+    n = 60
+    out = {}
+    for sigma in (0.01, 1e-9):
+        src, rig = _imu_rig(n_frames=n, blackout=(40, 46), accel_noise=0.01, gyro_noise=1e-4, gyro_bias=bias)
+        cfg = HipSlamConfig(batch_size=4, imu_gyro_bias_sigma=sigma, enable_loop_closure=False)
+        keep = {}
+        res, rects = _run_engine(rig, n, cfg, keep=keep)
+        gt = np.linalg.inv(src.camera_pose(0, 0)) @ src.camera_pose(n - 1, 0)
+        T = res["T_abs"][n - 1, 0]
+        out[sigma] = {"bg": keep["imu"].st.bg.copy(), "t": np.linalg.norm(T[:3, 3] - gt[:3, 3]),
+                      "r": Rotation.from_matrix(T[:3, :3].T @ gt[:3, :3]).magnitude(),
+                      "status": res["stats"][:, 0, 0]}
+    est = out[0.01]
+    assert (est["status"][40:46] == 1).all() and est["status"][-1] == 0
+    assert np.linalg.norm(est["bg"] - bias) < 0.25 * np.linalg.norm(bias), est["bg"]
+    assert np.linalg.norm(out[1e-9]["bg"]) < 1e-6
+    assert est["r"] < 0.5 * out[1e-9]["r"], (est["r"], out[1e-9]["r"])
+    assert est["t"] < out[1e-9]["t"], (est["t"], out[1e-9]["t"])
+
+
+def test_rig_imu_dropout_matches_oracle():
+    """A two-source rig with the IMU on source 0 and every camera blind for frames 9-11: the
+    engine (pair priors moved through the rig, k_rig_prior's body prediction in the rig chain,
+    the filter absorbing the rig's motion) against oracle/numpy_imu.run_rig_sequence: rig
+    statuses identical, rig world_T_base within 1e-9 through and after the dropout."""
+    import json
+    from pathlib import Path
+
+    from oracle import numpy_imu as OI
+    from thor_slam_amd.calib import extract_cameras, stereo_pairs, stereo_rectify
+    from thor_slam_amd.camera import CameraRig, Extrinsics
+    from thor_slam_amd.camera.types import IMUExtrinsics
+    from thor_slam_amd.params import HipSlamConfig
+    from thor_slam_amd.synthetic import DRB_TO_RDF, RoomScene, SyntheticStereoSource, circle_trajectory
+
+    n, batch = 16, 4
+    names = ("192.168.2.21", "192.168.2.25")
+    mats = json.loads((Path(__file__).parent / "golden" / "brackets_joints.json").read_text())
+    scene, traj = RoomScene(seed=0), circle_trajectory(40)
+    srcs = [SyntheticStereoSource(name=nm, scene=scene, trajectory=traj, rig_T_source=np.array(mats[nm]), seed=k,
+                                  imu=(k == 0), accel_noise=0.01, gyro_noise=1e-4, blackout=(9, 12))
+            for k, nm in enumerate(names)]
+    base_T_imu = np.array(mats[names[0]]) @ DRB_TO_RDF
+    rig = CameraRig(srcs, rig_extrinsics={nm: Extrinsics.from_4x4_matrix(np.array(mats[nm])) for nm in names},
+                    imu_source=names[0], imu_extrinsics=IMUExtrinsics(names[0], Extrinsics.from_4x4_matrix(base_T_imu)))
+    cfg = HipSlamConfig(batch_size=batch, enable_loop_closure=False)
+    res, rects = _run_engine(rig, n, cfg, num_cameras=4)
+    cams = extract_cameras(rig.calibration, 4)
+    pairs = stereo_pairs(cams)
+    E = [cams[l].extrinsics.to_4x4_matrix() @ r.left_optical_T_rect() for (l, _), r in zip(pairs, rects)]
+    by = {s.name: s for s in srcs}
+    frames = np.stack([np.stack([by[cams[l].source_name].render_image(i, c) for l, _ in pairs for c in (0, 1)])
+                       for i in range(n)])
+    samples = []
+    for i in range(n):
+        sm = srcs[0].imu_sample(i)
+        dt = None if i == 0 else srcs[0].timestamp(i) - srcs[0].timestamp(i - 1)
+        samples.append((dt, sm["gyroscope"], sm["accelerometer"]))
+    trks = [O.OracleTracker(cfg, dict(fx=r.fx, fy=r.fy, cx=r.cx, cy=r.cy, baseline=r.baseline, map_l=r.map_left,
+                                      map_r=r.map_right)) for r in rects]
+    filt = oracle_filter(cfg, np.linalg.inv(E[0]) @ base_T_imu)
+    want = OI.run_rig_sequence(trks, frames, samples, batch, filt, E, cfg)
+    status = [w["status"] for w in want]
+    assert status[9:12] == [1, 1, 1] and status[12:] == [0] * (n - 12)
+    for g in range(n):
+        assert res["rig_stats"][g, 0] == want[g]["status"], g
+        assert rel_frobenius(res["rig_T_abs"][g], want[g]["T_abs"]) < 1e-9, g

@@ -1,13 +1,13 @@
-"""The accelerometer leg's host side: the product filter
-(thor_slam_amd/imu.py) against its spec (oracle/numpy_imu.py), and the synthetic IMU against the
-trajectory it is sampled from.  CPU only."""
+"""IMU fusion's host side: the product filter (thor_slam_amd/imu.py) against
+its spec (oracle/numpy_imu.py) with and without the accelerometer leg, the gyroscope-bias estimate,
+and the synthetic IMU against the trajectory it is sampled from.  CPU only."""
 
 import numpy as np
 import pytest
 from scipy.spatial.transform import Rotation
 
 from oracle import numpy_imu as OI
-from thor_slam_amd.imu import ImuPropagator
+from thor_slam_amd.imu import ImuNoise, ImuPropagator
 from thor_slam_amd.synthetic import DRB_TO_RDF, SyntheticStereoSource
 
 
@@ -24,15 +24,27 @@ def _rect_R_imu(src):
     return DRB_TO_RDF[:3, :3]
 
 
-@pytest.mark.parametrize("batch", [1, 4])
-def test_filter_matches_oracle(batch):
+LEVER = np.array([0.0375, 0.0, 0.0])   # the IMU (source origin) seen from the left camera
+
+
+def _pair(accel: bool):
+    ri = DRB_TO_RDF[:3, :3]
+    noise = ImuNoise()
+    prod = ImuPropagator(ri, noise, lever=LEVER, accel=accel)
+    spec = OI.ImuFilter(ri, noise.acc_density, noise.acc_random_walk, noise.gyro_density, noise.gyro_random_walk,
+                        noise.rot_floor, noise.trans_floor, noise.v0_sigma, noise.ba0_sigma, noise.bg0_sigma,
+                        lever=LEVER, accel=accel, vis_rot_floor=noise.vis_rot_floor)
+    return prod, spec
+
+
+@pytest.mark.parametrize("batch,accel", [(1, True), (4, True), (4, False)])
+def test_filter_matches_oracle(batch, accel):
     """Priors and states agree over a sequence with tracked and lost frames, in the batch flow."""
-    src = SyntheticStereoSource(seed=0, imu=True, gyro_noise=1e-3, accel_noise=0.02, n_frames=40)
+    src = SyntheticStereoSource(seed=0, imu=True, gyro_noise=1e-3, accel_noise=0.02, n_frames=40,
+                                gyro_bias=[2e-3, -1e-3, 3e-3])
     n = 24
     smp = _samples(src, n)
-    ri = _rect_R_imu(src)
-    prod = ImuPropagator(ri, 2.553e-3, 1.0493e-4, 2e-3, 1e-3)
-    spec = OI.ImuFilter(ri, 2.553e-3, 1.0493e-4, 2e-3, 1e-3)
+    prod, spec = _pair(accel)
     rng = np.random.default_rng(1)
     for b0 in range(0, n, batch):
         idx = list(range(b0, min(n, b0 + batch)))
@@ -46,7 +58,7 @@ def test_filter_matches_oracle(batch):
             if g is not None:
                 np.testing.assert_allclose(g.R_rel, w[0], rtol=0, atol=1e-15)
                 np.testing.assert_allclose(g.t_rel, w[2], rtol=1e-12, atol=1e-15)
-                assert g.w_rot == w[1] and g.w_trans == pytest.approx(w[3], rel=1e-12)
+                assert g.w_rot == pytest.approx(w[1], rel=1e-12) and g.w_trans == pytest.approx(w[3], rel=1e-12)
         # results: the true relative motion (+ noise), some frames lost
         status = np.array([0 if (i % 7) else 1 for i in idx])
         t_rel, cov = [], []
@@ -63,7 +75,9 @@ def test_filter_matches_oracle(batch):
         np.testing.assert_allclose(prod.st.v, spec.v, rtol=1e-10, atol=1e-14)
         np.testing.assert_allclose(prod.st.ba, spec.ba, rtol=1e-10, atol=1e-14)
         np.testing.assert_allclose(prod.st.R, spec.R, rtol=0, atol=1e-14)
+        np.testing.assert_allclose(prod.st.bg, spec.bg, rtol=1e-10, atol=1e-14)
         assert prod.st.var_v == pytest.approx(spec.var_v, rel=1e-12)
+        assert prod.st.var_g == pytest.approx(spec.var_g, rel=1e-12)
 
 
 def test_synthetic_imu_integrates_to_the_trajectory():
@@ -71,7 +85,7 @@ def test_synthetic_imu_integrates_to_the_trajectory():
     rendered camera motion: the samples carry the trajectory's specific force and rotation."""
     src = SyntheticStereoSource(seed=0, imu=True, n_frames=60)
     ri = _rect_R_imu(src)
-    prod = ImuPropagator(ri, 2.553e-3, 1.0493e-4, 2e-3, 1e-3)
+    prod = ImuPropagator(ri, ImuNoise(), lever=LEVER)
     smp = _samples(src, 31)
     prod.begin(smp[0][2])
     # world = camera 0 at frame 0; the velocity at frame 0 such that the first interval's
@@ -81,15 +95,38 @@ def test_synthetic_imu_integrates_to_the_trajectory():
     dt = 1.0 / src.fps
     st = prod.st.copy()
     st.v = (pos[1] - pos[0]) / dt - 0.5 * (pos[2] - 2 * pos[1] + pos[0]) / dt
-    # the IMU sits 3.75 cm from the left camera: the camera's velocity differs from the IMU's by
-    # w x r (6.5 mm/s at 10 deg/s), which the camera-frame integration does not model
     p = np.zeros(3)
     for i in range(1, 31):
         s = prod.step(st, *smp[i])
         p = p + st.R @ (-(s.R_rel.T @ s.t_rel))
         st = prod.coast(st, s)
     truth = (np.linalg.inv(c0) @ src.camera_pose(30, 0))[:3, 3]
-    assert np.linalg.norm(p - truth) < 2e-3   # measured 0.6 mm
+    assert np.linalg.norm(p - truth) < 2e-3
     rot_true = (np.linalg.inv(c0) @ src.camera_pose(30, 0))[:3, :3]
     rot_err = Rotation.from_matrix(st.R.T @ rot_true).magnitude()
     assert rot_err < 1e-3
+
+
+def test_gyro_bias_estimate_converges():
+    """A constant gyroscope bias: the filter, fed the true visual motions (with the rotation
+    noise its covariance states), estimates it, and its rotation priors lose the bias."""
+    bias = np.array([4e-3, -2e-3, 3e-3])   # rad/s, DRB axes
+    src = SyntheticStereoSource(seed=0, imu=True, gyro_noise=1e-4, n_frames=120, gyro_bias=bias)
+    n = 90
+    smp = _samples(src, n)
+    prod, _ = _pair(False)
+    prod.begin()
+    rng = np.random.default_rng(3)
+    first_err = last_err = None
+    for i in range(1, n):
+        a, b = src.camera_pose(i - 1, 0), src.camera_pose(i, 0)
+        t = np.linalg.inv(b) @ a
+        s = prod.step(prod.st, *smp[i])
+        err = Rotation.from_matrix(s.R_rel @ t[:3, :3].T).magnitude()
+        first_err = err if first_err is None else first_err
+        last_err = err
+        noisy = Rotation.from_rotvec(rng.normal(0, 3e-5, 3)).as_matrix() @ t[:3, :3]
+        t[:3, :3] = noisy
+        prod.st = prod.correct(prod.st, s, t, np.diag([1e-6] * 3 + [(3e-5) ** 2] * 3))
+    assert np.linalg.norm(prod.st.bg - bias) < 0.1 * np.linalg.norm(bias), prod.st.bg
+    assert last_err < 0.2 * first_err, (first_err, last_err)

@@ -663,6 +663,9 @@ __global__ __launch_bounds__(POSE_THREADS) void k_refine(BatchCtx c, int S) {
                 if (solve6(s_H, e, col, L))
                     for (int q = 0; q < 6; ++q) pout[32 + q * 6 + k] = col[q] * sigma2;
             }
+            // stats[6..7]: sigma^2 (f64), so the host can take a motion prior back out of the
+            // covariance (the vision-only motion for the IMU filter's bias update)
+            *reinterpret_cast<double*>(sout + 6) = sigma2;
         }
     }
 }

@@ -849,8 +849,8 @@ static void unpack_records(const double* pose, int n, double* T_rel, double* T_a
 }
 
 int tslam_poll_batch(tslam_handle* h, int block, int max_frames, double* T_rel, double* T_abs, double* cov, int32_t* stats,
-                     double* rig_T_abs, double* rig_cov, int32_t* rig_stats, double* ts, int64_t* first_frame,
-                     int* n_frames) {
+                     double* rig_T_rel, double* rig_T_abs, double* rig_cov, int32_t* rig_stats, double* ts,
+                     int64_t* first_frame, int* n_frames) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
     HIPCHK(hipSetDevice(h->device));
     // the oldest unread batch
@@ -871,7 +871,7 @@ int tslam_poll_batch(tslam_handle* h, int block, int max_frames, double* T_rel, 
     unpack_records(r.pose, np, T_rel, T_abs, cov);
     if (stats) memcpy(stats, r.stats, sizeof(int32_t) * TS_STATS_INTS * np);
     if (h->rig) {
-        unpack_records(r.rig_pose, r.n, nullptr, rig_T_abs, rig_cov);
+        unpack_records(r.rig_pose, r.n, rig_T_rel, rig_T_abs, rig_cov);
         if (rig_stats) memcpy(rig_stats, r.rig_stats, sizeof(int32_t) * TS_STATS_INTS * r.n);
     }
     if (ts) memcpy(ts, r.ts.data(), sizeof(double) * r.n);

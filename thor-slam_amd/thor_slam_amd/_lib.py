@@ -122,7 +122,7 @@ _SIGNATURES = {
     "tslam_set_motion_prior": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "tslam_read_rig_poses": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 4),
     "tslam_submit_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
-    "tslam_poll_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 8
+    "tslam_poll_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 9
                          + [ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int)]),
     "tslam_poll_pose": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 5),
     "tslam_set_shard": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
@@ -417,11 +417,12 @@ class Handle:
         B, P = self.max_batch, self.n_pairs
         t_rel, t_abs = np.zeros((B, P, 4, 4)), np.zeros((B, P, 4, 4))
         cov, stats = np.zeros((B, P, 6, 6)), np.zeros((B, P, 8), dtype=np.int32)
-        r_abs, r_cov, r_st = np.zeros((B, 4, 4)), np.zeros((B, 6, 6)), np.zeros((B, 8), dtype=np.int32)
+        r_rel, r_abs = np.zeros((B, 4, 4)), np.zeros((B, 4, 4))
+        r_cov, r_st = np.zeros((B, 6, 6)), np.zeros((B, 8), dtype=np.int32)
         ts = np.zeros(B)
         g0, n = ctypes.c_int64(), ctypes.c_int()
-        rc = self.lib.tslam_poll_batch(self.h, int(block), B, *(a.ctypes.data for a in (t_rel, t_abs, cov, stats, r_abs,
-                                                                                       r_cov, r_st, ts)),
+        rc = self.lib.tslam_poll_batch(self.h, int(block), B, *(a.ctypes.data for a in (t_rel, t_abs, cov, stats, r_rel,
+                                                                                       r_abs, r_cov, r_st, ts)),
                                        ctypes.byref(g0), ctypes.byref(n))
         if rc < 0:
             _check(rc)
@@ -430,7 +431,7 @@ class Handle:
         k = n.value
         out = {"T_rel": t_rel[:k], "T_abs": t_abs[:k], "cov": cov[:k], "stats": stats[:k], "timestamps": ts[:k],
                "first_frame": int(g0.value), "n": k}
-        out["rig"] = {"T_abs": r_abs[:k], "cov": r_cov[:k], "stats": r_st[:k]}
+        out["rig"] = {"T_rel": r_rel[:k], "T_abs": r_abs[:k], "cov": r_cov[:k], "stats": r_st[:k]}
         return out
 
     def poll_pose(self) -> dict | None:

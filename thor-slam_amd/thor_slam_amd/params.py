@@ -45,16 +45,25 @@ class HipSlamConfig(SlamConfig):
     ba_iters: int = 5               # Gauss-Newton steps per window solve
     ba_lambda: float = 1.0          # Levenberg damping (px^2 units)
     ba_outlier_px: float = 3.0      # observations farther than this at the start are dropped
-    # IMU fusion: gyro-predicted rotation prior in the pose Gauss-Newton
-    imu_fusion: bool = False
-    imu_rot_sigma: float = 2e-3     # rad, std of the per-frame gyro rotation prediction (1 px = 1 unit)
-    # ... plus the accelerometer leg (thor_slam_amd/imu.py): velocity / gravity / bias state, a
-    # translation prior, and IMU chaining through visual dropouts; noise model of
-    # launch/thor_visual_slam.launch.py:82-93
-    imu_accel: bool = False
-    accelerometer_noise_density: float = 2.553e-3   # m/s^2/sqrt(Hz)
-    accelerometer_random_walk: float = 1.0493e-4    # m/s^3/sqrt(Hz)
+    # IMU fusion (thor_slam_amd/imu.py): the bias-corrected gyro rotation as a
+    # prior in the pose Gauss-Newton, with a gyroscope-bias state; None = on when the calibration
+    # carries the IMU extrinsics (the reference runs cuVSLAM with enable_imu_fusion:=true,
+    # Makefile:81; launch/thor_visual_slam.launch.py:69)
+    imu_fusion: bool | None = None
+    # ... plus the accelerometer leg: velocity / gravity / accelerometer-bias state with the IMU
+    # lever arm, a translation prior, and IMU chaining through visual dropouts (None = with
+    # imu_fusion)
+    imu_accel: bool | None = None
+    # noise model, launch/thor_visual_slam.launch.py:82-93 (calibrated on a 2.5 h rosbag, :97-104)
+    gyroscope_noise_density: float = 8.27e-5        # rad/s/sqrt(Hz)   (launch:82)
+    accelerometer_noise_density: float = 2.553e-3   # m/s^2/sqrt(Hz)   (launch:85)
+    gyroscope_random_walk: float = 1e-8             # rad/s^2/sqrt(Hz) (launch:88)
+    accelerometer_random_walk: float = 1.0493e-4    # m/s^3/sqrt(Hz)   (launch:91)
+    imu_rot_floor: float = 2e-4     # rad, added in quadrature to the predicted rotation's std (sync, calibration)
+    imu_vis_rot_floor: float = 1e-4  # rad, the vision's per-frame rotation error beyond its covariance
     imu_trans_floor: float = 1e-3   # m, added in quadrature to the predicted translation's std
+    imu_gyro_bias_sigma: float = 0.01   # rad/s, initial gyroscope-bias std
+    imu_accel_bias_sigma: float = 0.05  # m/s^2, initial accelerometer-bias std
     # loop closure + keyframe pose graph; on when the reference's
     # SlamConfig.enable_loop_closure is (interface.py:155-156; single stereo pair / RGB-D camera)
     loop_kf_interval: int = 5       # frame g is a loop-closure keyframe iff g % loop_kf_interval == 0
@@ -103,8 +112,8 @@ class HipSlamConfig(SlamConfig):
             raise ValueError("fast_threshold must be in [0, 254]")
         if self.batch_size < 1:
             raise ValueError("batch_size must be >= 1")
-        if self.imu_accel and not self.imu_fusion:
-            raise ValueError("imu_accel needs imu_fusion=True")
+        if self.imu_accel and self.imu_fusion is False:
+            raise ValueError("imu_accel needs IMU fusion (imu_fusion True or None)")
         if self.dense_map:
             if not self.rgbd:
                 raise ValueError("dense_map needs rgbd=True (depth input)")

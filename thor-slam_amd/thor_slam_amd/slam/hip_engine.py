@@ -54,7 +54,7 @@ from ..calib import (StereoRectification, confidence_from_covariance, extract_ca
                      stereo_pairs, stereo_rectify)
 from ..camera.rig import RigCalibration
 from ..camera.types import SynchronizedFrameSet
-from ..imu import ImuPropagator
+from ..imu import ImuNoise, ImuPropagator, vision_only
 from ..params import HipSlamConfig
 from ..rgbd import pack_rgbd
 from .interface import CameraConfig, MapPoint, SlamConfig, SlamEngine, SlamMap, SlamPose, TrackingState
@@ -131,7 +131,7 @@ class HipSlamEngine(SlamEngine):
         self._frame_count = 0
         self._staged: list[tuple[np.ndarray, float]] = []
         self._staged_imu: list[tuple | None] = []    # (gyro, accel) per staged frame
-        self._imu: ImuPropagator | None = None       # accelerometer leg (imu_accel)
+        self._imu: ImuPropagator | None = None       # IMU filter (gyro bias; accelerometer leg with imu_accel)
         self._imu_batches: list[list] = []            # IMU samples of submitted, unpublished batches
         self._prev_stamp: float | None = None      # timestamp of the last submitted frame (IMU dt)
         self._base_R_imu = np.eye(3)
@@ -190,11 +190,19 @@ class HipSlamEngine(SlamEngine):
                                   for (l, _), r in zip(self._pairs, self._rects)]
             self._base_T_rect = self._base_T_rects[0]
             imu = getattr(calibration, "imu_extrinsics", None)   # world(base)_T_imu, RDF-converted by the caller
-            self._base_R_imu = imu.to_4x4_matrix()[:3, :3] if imu is not None else np.eye(3)
+            base_T_imu = imu.to_4x4_matrix() if imu is not None else np.eye(4)
+            self._base_R_imu = base_T_imu[:3, :3]
             self._imu = None
-            if cfg.imu_fusion and cfg.imu_accel:
-                self._imu = ImuPropagator(self._base_T_rect[:3, :3].T @ self._base_R_imu, cfg.accelerometer_noise_density,
-                                          cfg.accelerometer_random_walk, cfg.imu_rot_sigma, cfg.imu_trans_floor)
+            # the reference fuses the IMU whenever it has one (enable_imu_fusion:=true, Makefile:81)
+            fusion = cfg.imu_fusion if cfg.imu_fusion is not None else imu is not None
+            if fusion:
+                accel = cfg.imu_accel if cfg.imu_accel is not None else True
+                noise = ImuNoise(cfg.gyroscope_noise_density, cfg.gyroscope_random_walk, cfg.accelerometer_noise_density,
+                                 cfg.accelerometer_random_walk, cfg.imu_rot_floor, cfg.imu_trans_floor,
+                                 ba0_sigma=cfg.imu_accel_bias_sigma, bg0_sigma=cfg.imu_gyro_bias_sigma,
+                                 vis_rot_floor=cfg.imu_vis_rot_floor)
+                rect_T_imu = _invert(self._base_T_rect) @ base_T_imu   # the IMU in pair 0's rectified-left camera
+                self._imu = ImuPropagator(rect_T_imu[:3, :3], noise, lever=rect_T_imu[:3, 3], accel=accel)
             if len(self._pairs) > 1 and self._shard is None:   # the rig's body motion, on the device from all pairs
                 self._handle.set_rig(self._base_T_rects)
             if cfg.dense_map:
@@ -250,7 +258,7 @@ class HipSlamEngine(SlamEngine):
             return
         batch, imus = self._staged[:n], self._staged_imu[:n]
         stamps = [ts for _, ts in batch]
-        if self._config.imu_fusion:
+        if self._imu is not None:
             self._set_imu_prior(stamps, imus)
         S, ptrs, streams = sh["S"], [], []
         for r, d in enumerate(sh["devices"]):
@@ -325,7 +333,7 @@ class HipSlamEngine(SlamEngine):
             self._submit_sharded()
             return
         stamps = [ts for _, ts in self._staged]
-        if self._config.imu_fusion:
+        if self._imu is not None:
             self._set_imu_prior(stamps, self._staged_imu)
         if self._config.dense_map:   # the TSDF reads the batch's depth records on the device
             torch = self._torch
@@ -384,41 +392,15 @@ class HipSlamEngine(SlamEngine):
         return (np.asarray(g, dtype=np.float64).reshape(3), None if a is None else np.asarray(a, dtype=np.float64).reshape(3))
 
     def _set_imu_prior(self, stamps: list[float], imus: list) -> None:
-        """Per staged frame and pair: the rectified-left rotation predicted by the gyro over the
-        frame interval, R = exp(-[w_rect dt]x), with weight (1 px / imu_rot_sigma)^2; with the
-        accelerometer leg, the whole predicted T_rel and its weights (thor_slam_amd/imu.py)."""
-        if self._imu is not None:
-            self._set_inertial_prior(stamps, imus)
-            return
-        P = len(self._pairs)
-        rot = np.tile(np.eye(3), (len(stamps), P, 1, 1))
-        wgt = np.zeros((len(stamps), P))
-        prev = self._prev_stamp
-        w0 = 1.0 / (self._config.imu_rot_sigma ** 2)
-        for k, (ts, imu) in enumerate(zip(stamps, imus)):
-            gy = None if imu is None else imu[0]
-            if gy is not None and prev is not None and ts > prev:
-                w_base = self._base_R_imu @ gy
-                for p, bt in enumerate(self._base_T_rects):
-                    rot[k, p] = Rotation.from_rotvec(-(bt[:3, :3].T @ w_base) * (ts - prev)).as_matrix()
-                    wgt[k, p] = w0
-            prev = ts
-        self._set_motion_prior(rot, wgt)
-
-    def _set_motion_prior(self, *args) -> None:
-        """The batch's priors on the handle (every rank's handle on a sharded rig: each refines its
-        frame range and chains the whole batch)."""
-        for h in (self._shard["handles"] if self._shard is not None else [self._handle]):
-            h.set_motion_prior(*args)
-
-    def _set_inertial_prior(self, stamps: list[float], imus: list) -> None:
-        """Gyro + accelerometer: per frame the predicted T_rel of pair 0's rectified-left camera
-        (moved into every other pair's camera through the rig, inv(E_p) E_0 T inv(E_0) E_p) with its
-        rotation and translation weights.  The samples are kept for the filter's update."""
+        """Per staged frame and pair: the motion predicted by the IMU filter (thor_slam_amd/imu.py)
+        for pair 0's rectified-left camera over the frame interval — the bias-corrected gyro
+        rotation with its weight and, with the accelerometer leg, the translation with its weight
+        — moved into every other pair's camera through the rig, inv(E_p) E_0 T inv(E_0) E_p.  The
+        samples are kept for the filter's update when the batch's results come back."""
         imu, prev = self._imu, self._prev_stamp
         samples = []
         for ts, s in zip(stamps, imus):
-            ok = s is not None and s[1] is not None
+            ok = s is not None and (s[1] is not None or not imu.accel)
             if ok and not imu.ready:
                 imu.begin(s[1])            # this frame anchors the filter: no prior for it
                 samples.append((None, None, None))
@@ -443,7 +425,13 @@ class HipSlamEngine(SlamEngine):
                 rot[k, p], trn[k, p] = tp[:3, :3], tp[:3, 3]
                 wr[k, p], wt[k, p] = st.w_rot, st.w_trans
         self._set_motion_prior(rot, wr, trn, wt)
-        self._imu_batches.append(samples)
+        self._imu_batches.append((samples, steps))
+
+    def _set_motion_prior(self, *args) -> None:
+        """The batch's priors on the handle (every rank's handle on a sharded rig: each refines its
+        frame range and chains the whole batch)."""
+        for h in (self._shard["handles"] if self._shard is not None else [self._handle]):
+            h.set_motion_prior(*args)
 
     def process_batch(self, images, timestamps: list[float] | None = None, stream=None) -> dict:
         """Throughput entry: ``images`` is a device uint8 tensor already in HBM: [n, 2P, H, W] gray
@@ -549,8 +537,23 @@ class HipSlamEngine(SlamEngine):
             self._map_points[int(mp["gid"][i])] = (win["X"][i].copy(), mp["desc"][i].copy(), int(n))
 
     def _publish(self, res: dict, stamps: list[float], g0: int) -> None:
-        if self._imu is not None and self._imu_batches:   # the filter absorbs pair 0's motions
-            self._imu.absorb(self._imu_batches.pop(0), res["stats"][:, 0, 0], res["T_rel"][:, 0], res["cov"][:, 0])
+        if self._imu is not None and self._imu_batches:   # the filter absorbs the tracked motions
+            samples, steps = self._imu_batches.pop(0)
+            if len(self._pairs) == 1:   # the vision-only motion behind each prior-weighted solution
+                st = res["stats"][:, 0]
+                sig = np.ascontiguousarray(st[:, 6:8]).view(np.float64)[:, 0]   # sigma^2 (tslam.h)
+                t_rel, cov = res["T_rel"][:, 0].copy(), res["cov"][:, 0].copy()
+                for k, step in enumerate(steps[:len(st)]):
+                    if step is not None and int(st[k, 0]) == POSE_OK:
+                        t_rel[k], cov[k] = vision_only(t_rel[k], cov[k], float(sig[k]), step)
+                self._imu.absorb(samples, st[:, 0], t_rel, cov)
+            else:   # the rig's body motion, moved into pair 0's camera (the filter's frame)
+                e0 = self._base_T_rects[0]
+                ie0, ad = _invert(e0), adjoint(_invert(e0))
+                rig = res["rig"]
+                t_rel = np.stack([ie0 @ m @ e0 for m in rig["T_rel"]])
+                cov = np.stack([ad @ c @ ad.T for c in rig["cov"]])
+                self._imu.absorb(samples, rig["stats"][:, 0], t_rel, cov)
         latest = None
         state = self._state
         corr = self._ba_corrections(res, len(stamps), g0)

@@ -185,6 +185,7 @@ class SyntheticStereoSource(CameraSource):
         gyro_noise: float = 0.0,
         accel_noise: float = 0.0,
         blackout: tuple[int, int] | None = None,
+        gyro_bias: np.ndarray | None = None,
     ) -> None:
         self._name = name
         self.scene = scene or RoomScene(seed=seed)
@@ -205,6 +206,7 @@ class SyntheticStereoSource(CameraSource):
         self.imu = imu
         self.gyro_noise = gyro_noise
         self.accel_noise = accel_noise
+        self.gyro_bias = np.zeros(3) if gyro_bias is None else np.asarray(gyro_bias, dtype=np.float64).reshape(3)
         self.blackout = blackout   # frames [a, b) render as a uniform grey (a visual dropout)
         self._index = 0
         self._running = False
@@ -238,7 +240,7 @@ class SyntheticStereoSource(CameraSource):
 
     def imu_sample(self, i: int) -> dict:
         """The sample of the interval (i-1, i]: gyro = the source's rotation from frame i-1 to i over
-        the frame interval (DRB axes) + N(0, gyro_noise^2); accelerometer = the specific force
+        the frame interval (DRB axes) + gyro_bias + N(0, gyro_noise^2); accelerometer = the specific force
         R^T (a - g) in the IMU axes of frame i-1, with the world acceleration a the second
         difference of the IMU positions around frame i-1 (so p_i = p_{i-1} + v dt + a dt^2 / 2
         holds for the central-difference velocity v) and g = (0, 0, -9.81) (the renderer's world is
@@ -250,7 +252,7 @@ class SyntheticStereoSource(CameraSource):
         r1 = self.camera_pose(i, 0)[:3, :3]
         w_rdf = Rotation.from_matrix(r0.T @ r1).as_rotvec() / dt
         d = DRB_TO_RDF[:3, :3]
-        w = d.T @ w_rdf
+        w = d.T @ w_rdf + self.gyro_bias
         if self.gyro_noise:
             w = w + np.random.default_rng((self.seed, i, 99)).normal(0.0, self.gyro_noise, 3)
         if i == 0:
