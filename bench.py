@@ -883,6 +883,8 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
     ok = float(np.mean(res["pairs"]["stats"][:, :, 0] == 0))
     rig_ok = float(np.mean(res["rig"]["stats"][:, 0] == 0)) if P > 1 else None
     per_kernel_us = timer.mean_us()
+    # exchange spans (HIP events across the streams): not kernels, reported on their own
+    exchange_us = {k: per_kernel_us.pop(k) for k in ("exchange_exposed", "pose_gather") if k in per_kernel_us}
     # the dominant kernel's algorithmic bytes: the §8d rig-frame bytes x the share of the rig one
     # launch covers (front kernels: S of C streams for B frames; back kernels: all streams for B/N frames)
     S = plan.streams_per_rank
@@ -954,6 +956,10 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
                      "avg_launch_us": per_kernel_us[dom], "rank": rank},
         "per_kernel_us_per_batch": per_kernel_us,
         "exchange_bytes_per_step": xbytes,
+        # exchange_exposed: front end packed -> both exchanges landed on the back stream (what the
+        # overlap does not hide); pose_gather: the pose-record all-gather on the back stream
+        "exchange_us": exchange_us,
+        "backend": args.dist_backend,
         "tracking_ok_fraction_last_batch": ok,
         "rig_ok_fraction_last_batch": rig_ok,
         "render_s": t_render,

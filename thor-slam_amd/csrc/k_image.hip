@@ -800,22 +800,32 @@ __global__ __launch_bounds__(TS_DET_THREADS) void k_detect_fallback(BatchCtx c) 
 #define SEL_MAX 8192
 
 // smallest bin b with sum(h[0..b]) >= need; returns b and the count strictly before it.
+// Inclusive scan of one value per thread over the block (SEL_THREADS = 16 waves): a 6-step
+// shuffle scan inside each wave, the 16 wave totals through LDS, two barriers in all (a
+// Hillis-Steele scan through LDS took 20).  s_w: 2 x 16 words, alternated by `phase` so that
+// back-to-back scans need no barrier between them.
+__device__ __forceinline__ uint32_t block_inclusive_scan(uint32_t v, uint32_t* s_w, int phase) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)v, o, 64);
+        if (lane >= o) v += t;
+    }
+    uint32_t* w = s_w + 16 * (phase & 1);
+    if (lane == 63) w[wave] = v;
+    __syncthreads();
+    uint32_t add = 0;
+    for (int k = 0; k < wave; ++k) add += w[k];
+    return v + add;
+}
+
 __device__ void block_find_crossing(const uint32_t* h, int nbins, uint32_t need, uint32_t* s_part,
                                     int* out_bin, uint32_t* out_before) {
     const int per = (nbins + SEL_THREADS - 1) / SEL_THREADS;
     const int b0 = threadIdx.x * per;
     uint32_t local = 0;
     for (int b = b0; b < min(b0 + per, nbins); ++b) local += h[b];
-    s_part[threadIdx.x] = local;
-    __syncthreads();
-    // inclusive Hillis-Steele scan over the 256 partial sums
-    for (int o = 1; o < SEL_THREADS; o <<= 1) {
-        const uint32_t v = threadIdx.x >= (unsigned)o ? s_part[threadIdx.x - o] : 0u;
-        __syncthreads();
-        s_part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    const uint32_t incl = s_part[threadIdx.x];
+    const uint32_t incl = block_inclusive_scan(local, s_part, 0);
     const uint32_t excl = incl - local;
     if (excl < need && incl >= need) {
         uint32_t cum = excl;
@@ -839,15 +849,7 @@ __device__ void block_exclusive_scan(uint32_t* a, int n, uint32_t* s_part) {
     const int b0 = threadIdx.x * per;
     uint32_t local = 0;
     for (int b = b0; b < min(b0 + per, n); ++b) local += a[b];
-    s_part[threadIdx.x] = local;
-    __syncthreads();
-    for (int o = 1; o < SEL_THREADS; o <<= 1) {
-        const uint32_t v = threadIdx.x >= (unsigned)o ? s_part[threadIdx.x - o] : 0u;
-        __syncthreads();
-        s_part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    uint32_t run = s_part[threadIdx.x] - local;
+    uint32_t run = block_inclusive_scan(local, s_part, 1) - local;
     for (int b = b0; b < min(b0 + per, n); ++b) {
         const uint32_t v = a[b];
         a[b] = run;
@@ -908,15 +910,12 @@ __device__ __forceinline__ void select_body(const BatchCtx& c) {
         s_h[i] = gh[i];
         gh[i] = 0u;   // back to zero for the next detect of this image-level (fallback or next batch)
     }
-    for (int i = threadIdx.x; i < SEL_THREADS; i += blockDim.x) s_part[i] = i < nb ? cnt[i] : 0u;
-    __syncthreads();
-    for (int o = 1; o < SEL_THREADS; o <<= 1) {
-        const uint32_t v = threadIdx.x >= (unsigned)o ? s_part[threadIdx.x - o] : 0u;
-        __syncthreads();
-        s_part[threadIdx.x] += v;
-        __syncthreads();
+    {
+        const uint32_t bc = (int)threadIdx.x < nb ? cnt[threadIdx.x] : 0u;
+        const uint32_t incl = block_inclusive_scan(bc, s_part, 1);
+        if (threadIdx.x == 0) s_pref[0] = 0u;
+        if ((int)threadIdx.x < nb) s_pref[threadIdx.x + 1] = incl;
     }
-    if (threadIdx.x <= (unsigned)nb) s_pref[threadIdx.x] = threadIdx.x == 0 ? 0u : s_part[threadIdx.x - 1];
     __syncthreads();
     const int ncand = (int)s_pref[nb];
     // sweep(fn): fn(key) for every candidate, 4 independent loads in flight per thread.  A

@@ -118,6 +118,17 @@ class StageTimer:
         e.record(self.stream)
         self.spans.setdefault(name, []).append((self._open, e))
 
+    def event(self, stream):
+        """A timing event recorded on ``stream`` now (for spans across streams)."""
+        import torch
+
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream)
+        return e
+
+    def span(self, name: str, e0, e1) -> None:
+        self.spans.setdefault(name, []).append((e0, e1))
+
     def mean_us(self) -> dict[str, float]:
         """Average microseconds per launch of each name (synchronise first)."""
         return {k: sum(a.elapsed_time(b) for a, b in v) * 1e3 / len(v) for k, v in self.spans.items()}
@@ -295,9 +306,11 @@ class LocalShardedRig:
         self.exchange = exchange
         self.rgbd = bool(cfg.rgbd)
 
-    def step(self, images, stream=None) -> None:
+    def step(self, images, stream=None, timer: StageTimer | None = None) -> None:
         """images: device u8 [B][C][H][W] (all cameras; RGB-D records [B][C][5HW]); rank r gets its
-        cameras' slice."""
+        cameras' slice.  With ``timer`` (its stream = ``stream``) every phase of every rank is
+        timed on the one stream: the kernels by name, ``stage_raw``, ``pack``, ``exchange`` (the
+        device copies standing in for the all-to-all), ``import``, ``pose_gather``."""
         torch = self.torch
         st = stream or torch.cuda.current_stream()
         sp = st.cuda_stream
@@ -308,26 +321,32 @@ class LocalShardedRig:
             return
         for r, rk in enumerate(self.ranks):
             rk.begin(parts[r])
-            rk.stage_raw(st)
-            rk.front(sp)
-            rk.pack_features(sp)
-        with torch.cuda.stream(st):   # the all-to-all / all-gather
-            for r, rk in enumerate(self.ranks):
-                k = rk.batches % 2
-                for q, src in enumerate(self.ranks):
-                    j = r if self.exchange == "alltoall" else 0
-                    rk.raw_recv[k][q].copy_(src.raw_send[k][j])
-                    rk.feat_recv[k][q].copy_(src.feat_send[k][j])
+            _timed(timer, "stage_raw", lambda: rk.stage_raw(st))
+            rk.front(sp, timer)
+            _timed(timer, "pack", lambda: rk.pack_features(sp))
+
+        def all_to_all():
+            with torch.cuda.stream(st):
+                for r, rk in enumerate(self.ranks):
+                    k = rk.batches % 2
+                    for q, src in enumerate(self.ranks):
+                        j = r if self.exchange == "alltoall" else 0
+                        rk.raw_recv[k][q].copy_(src.raw_send[k][j])
+                        rk.feat_recv[k][q].copy_(src.feat_send[k][j])
+        _timed(timer, "exchange", all_to_all)
         for rk in self.ranks:
-            rk.import_remote(sp)
-            rk.back(sp)
-        with torch.cuda.stream(st):
-            for rk in self.ranks:
-                k = rk.batches % 2
-                for q, src in enumerate(self.ranks):
-                    rk.pose_recv[k][q].copy_(src.pose_send[k])
+            rk.import_remote(sp, timer)
+            rk.back(sp, timer)
+
+        def all_gather():
+            with torch.cuda.stream(st):
+                for rk in self.ranks:
+                    k = rk.batches % 2
+                    for q, src in enumerate(self.ranks):
+                        rk.pose_recv[k][q].copy_(src.pose_send[k])
+        _timed(timer, "pose_gather", all_gather)
         for rk in self.ranks:
-            rk.finish(sp)
+            rk.finish(sp, timer)
 
     def _step_rgbd(self, parts, st) -> None:
         torch, sp = self.torch, st.cuda_stream
@@ -448,19 +467,25 @@ class DistShardedRig:
             timer.stream = fs
         rk.front(fs.cuda_stream, timer)
         rk.pack_features(fs.cuda_stream)
+        e_front = timer.event(fs) if timer is not None else None
         xs.wait_stream(fs)
         self._collective("feat", rk.feat_recv[k], rk.feat_send[k], k, xs)
         # back end of this rank's frame range, on the back stream, once both exchanges landed
         self._wait("raw", k, bs)
         self._wait("feat", k, bs)
         if timer is not None:
+            # the exchange left exposed: front end done -> both exchanges landed on the back stream
+            timer.span("exchange_exposed", e_front, timer.event(bs))
             timer.stream = bs
         rk.import_remote(bs.cuda_stream, timer)
         self.consumed[k].record(bs)
         self.consumed_armed[k] = True
         rk.back(bs.cuda_stream, timer)
+        e_p = timer.event(bs) if timer is not None else None
         self._collective("pose", rk.pose_recv[k].view(-1), rk.pose_send[k].view(-1), k, bs)
         self._wait("pose", k, bs)
+        if timer is not None:
+            timer.span("pose_gather", e_p, timer.event(bs))
         rk.finish(bs.cuda_stream, timer)
 
     def _step_rgbd(self, images, timer) -> None:
@@ -479,11 +504,17 @@ class DistShardedRig:
             timer.stream = bs
         rk.back(bs.cuda_stream, timer)
         rk.pack_pairs(bs.cuda_stream)
+        e_x = timer.event(bs) if timer is not None else None
         self._collective("feat", rk.feat_recv[k], rk.feat_send[k], k, bs)
         self._wait("feat", k, bs)
+        if timer is not None:
+            timer.span("exchange_exposed", e_x, timer.event(bs))
         rk.rig_range(bs.cuda_stream, timer)
+        e_p = timer.event(bs) if timer is not None else None
         self._collective("pose", rk.pose_recv[k].view(-1), rk.pose_send[k].view(-1), k, bs)
         self._wait("pose", k, bs)
+        if timer is not None:
+            timer.span("pose_gather", e_p, timer.event(bs))
         rk.finish(bs.cuda_stream, timer)
 
     def drain(self) -> None:
