@@ -544,7 +544,8 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     stream = (torch.cuda.Stream(priority=-1) if args.front_priority and args.pipeline else torch.cuda.current_stream())
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
-    kern = list(KERNELS) + (["rig"] if P > 1 else [])
+    # the rig pose runs before the chains (KERNEL_CHAIN chains the pairs and the rig in one launch)
+    kern = [k for k in KERNELS if k != "chain"] + (["rig"] if P > 1 else []) + ["chain"]
     names = kern + (["local_ba"] if c4 else []) + (["tsdf"] if c5 and args.tsdf else [])
     if c5 and args.tsdf:
         h.tsdf_init(TSDF_ORIGIN, TSDF_DIMS, 0.05, 4.0, 10.0, 100.0)

@@ -154,9 +154,9 @@ enum tslam_stage {
     TSLAM_KERNEL_MATCH = 14,        /* includes the scratch memsets */
     TSLAM_KERNEL_MATCH_REFINE = 15,
     TSLAM_KERNEL_POSE = 16,
-    TSLAM_KERNEL_CHAIN = 17,
-    TSLAM_KERNEL_RIG = 18           /* rig pose + its chain (after tslam_set_rig; sharded: the range's rig pose only,
-                                       KERNEL_CHAIN then chains the pairs and the rig) */
+    TSLAM_KERNEL_CHAIN = 17,        /* every pair's chain, and the rig's after tslam_set_rig (one block each) */
+    TSLAM_KERNEL_RIG = 18           /* rig pose (after tslam_set_rig; sharded: the range's); run it before
+                                       KERNEL_CHAIN */
 };
 
 const char* tslam_last_error(void);
@@ -316,6 +316,17 @@ int tslam_unpack_streams(tslam_handle* h, int64_t first_frame, int n_frames, int
  * first_frame.. into the ring (frames < 0 skipped). */
 int tslam_import_raw(tslam_handle* h, const uint8_t* images, int64_t first_frame, int n_frames, int cam_lo, int cam_hi,
                      void* stream);
+/* The all-to-all's peers, one launch each (stereo, world > 1, cameras [rank*S, (rank+1)*S); the
+ * layouts of an all-to-all of [world][B/world + 1][S][...] slots, slot q for / from rank q):
+ * tslam_stage_raw_peers: this rank's raw images of every peer q's frames lo_q-1 .. hi_q-1 (frame -1
+ *   = prev_raw [S][H][W], the previous batch's last frame) -> dst [world][nr][S][H][W];
+ * tslam_pack_streams_peers: their stream blocks -> dst [world][nr][S][stream_block];
+ * tslam_import_peers: every peer's raw images and stream blocks of this rank's frames lo-1 .. hi-1
+ *   (as received) -> rectified into the ring + unpacked (tslam_import_raw + tslam_unpack_streams
+ *   per peer in two launches). */
+int tslam_stage_raw_peers(tslam_handle* h, const uint8_t* prev_raw, void* dst, void* stream);
+int tslam_pack_streams_peers(tslam_handle* h, void* dst, void* stream);
+int tslam_import_peers(tslam_handle* h, const uint8_t* raw, const void* streams, void* stream);
 /* Pose records (per frame: pose f64[P][68], rig pose f64[68], stats i32[P][8], rig stats i32[8])
  * of this rank's frame range of the current batch -> dst; all n frames <- src (frame order). */
 int tslam_pack_poses(tslam_handle* h, void* dst, void* stream);

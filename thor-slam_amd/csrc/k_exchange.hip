@@ -70,6 +70,48 @@ __global__ __launch_bounds__(256) void k_stream_blocks(BatchCtx c, int64_t first
     }
 }
 
+// the per-item copy of k_stream_blocks (frame g, camera cam <-> block b)
+template <bool PACK>
+__device__ __forceinline__ void stream_block_item(const BatchCtx& c, int64_t g, int cam, uint8_t* b) {
+    const StreamBlock sb = stream_block(c.g);
+    if (g < 0) {
+        if (PACK)
+            for (int64_t i = threadIdx.x; i < sb.bytes / 16; i += blockDim.x) reinterpret_cast<uint4*>(b)[i] = uint4{0, 0, 0, 0};
+        return;
+    }
+    const size_t sc = (size_t)ring_slot(c, g) * c.C + cam;
+    const int64_t K = c.g.K;
+    uint8_t* ring[5] = {reinterpret_cast<uint8_t*>(c.kps + sc * K * 2), reinterpret_cast<uint8_t*>(c.kcount + sc * c.g.n_levels),
+                        reinterpret_cast<uint8_t*>(c.ys + sc * K), reinterpret_cast<uint8_t*>(c.desc_ys + sc * K * 8),
+                        reinterpret_cast<uint8_t*>(c.rowstart + sc * c.g.rs_total)};
+    const int64_t off[5] = {sb.kps, sb.kcount, sb.ys, sb.desc, sb.rowstart};
+    const int64_t len[5] = {K * 8, (int64_t)c.g.n_levels * 4, K * 16, K * 32, (int64_t)c.g.rs_total * 2};
+    for (int p = 0; p < 5; ++p) {
+        if (PACK) copy_piece(b + off[p], ring[p], len[p]);
+        else copy_piece(ring[p], b + off[p], len[p]);
+    }
+}
+
+// item over the world-1 peers' slots: (peer q != me, frame k, camera s) of [world][nr][S][block]
+template <bool PACK>
+__global__ __launch_bounds__(256) void k_stream_blocks_peers(BatchCtx c, int64_t g0, int fpr, int nr, int me, int S,
+                                                             uint8_t* blk) {
+    const int item = blockIdx.x, per = nr * S;
+    const int qq = item / per, q = qq < me ? qq : qq + 1;
+    const int r = item - qq * per, k = r / S, s = r - k * S;
+    uint8_t* b = blk + ((int64_t)q * per + r) * stream_block(c.g).bytes;
+    if (PACK) stream_block_item<true>(c, g0 + (int64_t)q * fpr - 1 + k, me * S + s, b);   // my cameras, q's frames
+    else stream_block_item<false>(c, g0 + (int64_t)me * fpr - 1 + k, q * S + s, b);       // q's cameras, my frames
+}
+
+void launch_stream_blocks_peers(const BatchCtx& c, bool pack, int64_t g0, int fpr, int nr, int world, int me, int S,
+                                uint8_t* blk, hipStream_t s) {
+    const dim3 grid((world - 1) * nr * S);
+    if (grid.x == 0) return;
+    if (pack) hipLaunchKernelGGL(k_stream_blocks_peers<true>, grid, dim3(256), 0, s, c, g0, fpr, nr, me, S, blk);
+    else hipLaunchKernelGGL(k_stream_blocks_peers<false>, grid, dim3(256), 0, s, c, g0, fpr, nr, me, S, blk);
+}
+
 void launch_stream_blocks(const BatchCtx& c, bool pack, int64_t first, int n_frames, int cam_lo, int ncam, uint8_t* blk,
                           hipStream_t s) {
     const dim3 grid(n_frames * ncam);
@@ -147,4 +189,26 @@ void launch_pair_blocks(const BatchCtx& c, bool pack, int f0, int n_frames, int 
     const dim3 grid(n_frames * np);
     if (pack) hipLaunchKernelGGL(k_pair_blocks<true>, grid, dim3(256), 0, s, c, f0, p0, np, blk);
     else hipLaunchKernelGGL(k_pair_blocks<false>, grid, dim3(256), 0, s, c, f0, p0, np, blk);
+}
+
+// Raw images of this rank's cameras for every peer (alltoall layout [world][nr][S][H*W]): slot q
+// = frames lo_q - 1 .. hi_q - 1 of the batch (frame -1 = `prev`, the previous batch's last frame);
+// one block per (peer, frame, camera) image, 16-byte copies.
+__global__ __launch_bounds__(256) void k_stage_raw_peers(const uint8_t* images, const uint8_t* prev, uint8_t* dst,
+                                                         int fpr, int nr, int me, int S, int64_t img_bytes) {
+    const int item = blockIdx.x, per = nr * S;
+    const int qq = item / per, q = qq < me ? qq : qq + 1;
+    const int r = item - qq * per, k = r / S, s = r - k * S;
+    const int f = q * fpr - 1 + k;   // batch frame
+    const uint8_t* src = f < 0 ? prev + (int64_t)s * img_bytes : images + ((int64_t)f * S + s) * img_bytes;
+    uint8_t* out = dst + ((int64_t)q * per + r) * img_bytes;
+    copy_piece(out, src, img_bytes);
+}
+
+void launch_stage_raw_peers(const uint8_t* images, const uint8_t* prev, uint8_t* dst, int fpr, int world, int me, int S,
+                            int64_t img_bytes, hipStream_t s) {
+    const int nr = fpr + 1;
+    if (world < 2) return;
+    hipLaunchKernelGGL(k_stage_raw_peers, dim3((world - 1) * nr * S), dim3(256), 0, s, images, prev, dst, fpr, nr, me, S,
+                       img_bytes);
 }

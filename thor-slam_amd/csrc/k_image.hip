@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256) void k_rectify_pyramid(BatchCtx c) {
     const int W = c.W, H = c.H;
     const int y0 = blockIdx.x * TS_RECT_BAND;
     const int rows0 = min(TS_RECT_BAND, H - y0);
-    const uint8_t* src = c.images + (size_t)img * W * H;
+    const uint8_t* src = c.images + view_src(c, img) * W * H;
     uint8_t* pyr = c.pyr + ((size_t)ring_slot(c, c.g0 + f) * c.C + cam) * c.g.pyr_bytes;
     const bool has_map = (c.map_mask >> cam) & 1u;
     const int32_t* map = c.maps + (size_t)cam * W * H * 2;
@@ -1125,7 +1125,8 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select_fallback(BatchCtx c) { s
 void launch_rectify_pyramid(const BatchCtx& c, hipStream_t s) {
     size_t lds = 0;
     for (int l = 0; l < c.g.n_levels; ++l) lds += (size_t)(TS_RECT_BAND >> l) * c.g.W[l];
-    dim3 grid((c.H + TS_RECT_BAND - 1) / TS_RECT_BAND, c.n * c.ncam);
+    const int imgs = c.peer_S ? (c.C / c.peer_S - 1) * c.n * c.peer_S : c.n * c.ncam;
+    dim3 grid((c.H + TS_RECT_BAND - 1) / TS_RECT_BAND, imgs);
     hipLaunchKernelGGL(k_rectify_pyramid, grid, dim3(256), lds, s, c);
 }
 

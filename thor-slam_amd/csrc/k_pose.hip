@@ -671,69 +671,84 @@ __global__ __launch_bounds__(POSE_THREADS) void k_refine(BatchCtx c, int S) {
 }
 
 // Pose chaining: T_abs(t) = T_abs(t-1) * inv(T_rel(t)) for every successful frame, in frame
-// order (the association is the oracle's, so results do not depend on the batch size).  The
-// block inverts all relative poses in parallel into LDS; then 16 lanes of wave 0 carry T, one
-// element each: per frame a lane gathers its row of T (4 quad DPP broadcasts) and computes its element
-// with the oracle's expression, so a frame costs one 4-term dot product of latency.
+// order (the association is the oracle's, so results do not depend on the batch size).  One block
+// per chain: blocks 0 .. P-1 the pairs, block P the rig's body motion (when chained in the same
+// launch) — the chains are independent, so a rig's pairs run side by side.  A block inverts its
+// relative poses in parallel into LDS; then 16 lanes of wave 0 carry T, one element each: per
+// frame a lane gathers its row of T (4 quad DPP broadcasts) and computes its element with the
+// oracle's expression.  The next frame's status and inverse are read from LDS while the current
+// one is computed and an untracked frame keeps T by a select, so a frame costs one dependent
+// broadcast + 4-term dot product (no LDS round trip or branch on the chain's critical path).
 #define TS_CHAIN_CHUNK 128
 __global__ __launch_bounds__(256) void k_chain(BatchCtx c) {
     __shared__ double s_inv[TS_CHAIN_CHUNK][16];
     __shared__ int s_status[TS_CHAIN_CHUNK];
     const int tid = threadIdx.x, lane = tid & 63;
-    for (int p = 0; p < c.P; ++p) {
-        double T = 0.0;
-        if (tid < 16) T = c.state[p * 16 + tid];
-        for (int f0 = 0; f0 < c.n; f0 += TS_CHAIN_CHUNK) {
-            const int nf = min(TS_CHAIN_CHUNK, c.n - f0);
-            __syncthreads();
+    const bool rig = (int)blockIdx.x >= c.P;   // the rig's chain (k_rig_pose's body motions)
+    const int P = rig ? 1 : c.P, p = rig ? 0 : (int)blockIdx.x;
+    double* pose = rig ? c.rig_pose : c.pose;
+    const int32_t* stats = rig ? c.rig_stats : c.stats;
+    double* state = rig ? c.rig_state : c.state + 16 * p;
+    const double* prior = rig ? (c.prior ? c.rig_prior : nullptr) : c.prior;
+    double T = 0.0;
+    if (tid < 16) T = state[tid];
+    for (int f0 = 0; f0 < c.n; f0 += TS_CHAIN_CHUNK) {
+        const int nf = min(TS_CHAIN_CHUNK, c.n - f0);
+        __syncthreads();
+        for (int i = tid; i < nf * 16; i += blockDim.x) {
+            const int fl = i / 16, e = i % 16, r = e / 4, q = e % 4;
+            const double* rel = pose + (size_t)((f0 + fl) * P + p) * TS_POSE_DOUBLES;
+            double v;
+            if (r == 3) v = q == 3 ? 1.0 : 0.0;
+            else if (q < 3) v = rel[4 * q + r];
+            else v = -((rel[r] * rel[3] + rel[4 + r] * rel[7]) + rel[8 + r] * rel[11]);
+            s_inv[fl][e] = v;
+        }
+        for (int fl = tid; fl < nf; fl += blockDim.x) s_status[fl] = stats[(size_t)((f0 + fl) * P + p) * TS_STATS_INTS];
+        __syncthreads();
+        // an untracked frame with an accelerometer prediction (W_t > 0) moves by the IMU's
+        // T_rel = [R_prior | t_prior]; its pose record's T_rel becomes that prediction
+        if (prior) {
             for (int i = tid; i < nf * 16; i += blockDim.x) {
                 const int fl = i / 16, e = i % 16, r = e / 4, q = e % 4;
-                const double* rel = c.pose + (size_t)((f0 + fl) * c.P + p) * TS_POSE_DOUBLES;
+                const size_t fp = (size_t)(f0 + fl) * P + p;
+                const double* pr = prior + fp * TS_PRIOR_DOUBLES;
+                if (s_status[fl] == 0 || !(pr[13] > 0.0)) continue;
                 double v;
                 if (r == 3) v = q == 3 ? 1.0 : 0.0;
-                else if (q < 3) v = rel[4 * q + r];
-                else v = -((rel[r] * rel[3] + rel[4 + r] * rel[7]) + rel[8 + r] * rel[11]);
+                else if (q < 3) v = pr[3 * q + r];
+                else v = -((pr[r] * pr[10] + pr[3 + r] * pr[11]) + pr[6 + r] * pr[12]);
                 s_inv[fl][e] = v;
+                pose[fp * TS_POSE_DOUBLES + e] = r == 3 ? (q == 3 ? 1.0 : 0.0) : (q < 3 ? pr[3 * r + q] : pr[10 + r]);
             }
-            for (int fl = tid; fl < nf; fl += blockDim.x) s_status[fl] = c.stats[(size_t)((f0 + fl) * c.P + p) * TS_STATS_INTS];
             __syncthreads();
-            // an untracked frame with an accelerometer prediction (W_t > 0) moves by the IMU's
-            // T_rel = [R_prior | t_prior]; its pose record's T_rel becomes that prediction
-            if (c.prior) {
-                for (int i = tid; i < nf * 16; i += blockDim.x) {
-                    const int fl = i / 16, e = i % 16, r = e / 4, q = e % 4;
-                    const size_t fp = (size_t)(f0 + fl) * c.P + p;
-                    const double* pr = c.prior + fp * TS_PRIOR_DOUBLES;
-                    if (s_status[fl] == 0 || !(pr[13] > 0.0)) continue;
-                    double v;
-                    if (r == 3) v = q == 3 ? 1.0 : 0.0;
-                    else if (q < 3) v = pr[3 * q + r];
-                    else v = -((pr[r] * pr[10] + pr[3 + r] * pr[11]) + pr[6 + r] * pr[12]);
-                    s_inv[fl][e] = v;
-                    c.pose[fp * TS_POSE_DOUBLES + e] = r == 3 ? (q == 3 ? 1.0 : 0.0) : (q < 3 ? pr[3 * r + q] : pr[10 + r]);
-                }
-                __syncthreads();
-                for (int fl = tid; fl < nf; fl += blockDim.x)
-                    if (s_status[fl] != 0 && c.prior[(size_t)((f0 + fl) * c.P + p) * TS_PRIOR_DOUBLES + 13] > 0.0) s_status[fl] = -1;
-                __syncthreads();
-            }
-            if (tid < 64) {
-                const int j = lane & 3;
-                for (int fl = 0; fl < nf; ++fl) {
-                    // row i of T lives in this lane's quad: quad_perm broadcasts of lanes 0..3
-                    const double t0 = dpp_f64c<0x00>(T), t1 = dpp_f64c<0x55>(T);
-                    const double t2 = dpp_f64c<0xAA>(T), t3 = dpp_f64c<0xFF>(T);
-                    if (s_status[fl] <= 0) {   // tracked (0) or IMU-propagated (-1)
-                        const double* inv = s_inv[fl];
-                        T = ((t0 * inv[j] + t1 * inv[4 + j]) + t2 * inv[8 + j]) + t3 * inv[12 + j];
-                    }
-                    if (lane < 16) c.pose[(size_t)((f0 + fl) * c.P + p) * TS_POSE_DOUBLES + 16 + lane] = T;
-                }
+            for (int fl = tid; fl < nf; fl += blockDim.x)
+                if (s_status[fl] != 0 && prior[(size_t)((f0 + fl) * P + p) * TS_PRIOR_DOUBLES + 13] > 0.0) s_status[fl] = -1;
+            __syncthreads();
+        }
+        if (tid < 64) {
+            const int j = lane & 3;
+            int st = s_status[0];
+            double i0 = s_inv[0][j], i1 = s_inv[0][4 + j], i2 = s_inv[0][8 + j], i3 = s_inv[0][12 + j];
+            for (int fl = 0; fl < nf; ++fl) {
+                const int fn = min(fl + 1, nf - 1);   // next frame's operands, off the critical path
+                const int st_n = s_status[fn];
+                const double n0 = s_inv[fn][j], n1 = s_inv[fn][4 + j], n2 = s_inv[fn][8 + j], n3 = s_inv[fn][12 + j];
+                // row i of T lives in this lane's quad: quad_perm broadcasts of lanes 0..3
+                const double t0 = dpp_f64c<0x00>(T), t1 = dpp_f64c<0x55>(T);
+                const double t2 = dpp_f64c<0xAA>(T), t3 = dpp_f64c<0xFF>(T);
+                const double nt = ((t0 * i0 + t1 * i1) + t2 * i2) + t3 * i3;
+                T = st <= 0 ? nt : T;   // tracked (0) or IMU-propagated (-1)
+                if (lane < 16) pose[(size_t)((f0 + fl) * P + p) * TS_POSE_DOUBLES + 16 + lane] = T;
+                st = st_n;
+                i0 = n0;
+                i1 = n1;
+                i2 = n2;
+                i3 = n3;
             }
         }
-        if (tid < 16) c.state[p * 16 + tid] = T;
-        __syncthreads();
     }
+    if (tid < 16) state[tid] = T;
 }
 
 // ---- rig pose: generalised PnP over every pair of the rig ---------------
@@ -991,10 +1006,6 @@ void launch_rig_pose(const BatchCtx& c, hipStream_t s) {
     hipLaunchKernelGGL(k_rig_pose, dim3(c.n), dim3(POSE_THREADS), 0, s, c);
 }
 
-void launch_rig(const BatchCtx& c, hipStream_t s) {
-    launch_rig_pose(c, s);
-    launch_rig_chain(c, s);
-}
 
 // The rig chain's IMU prediction per frame: the first pair with a translation prior (W_t > 0),
 // moved to the body frame, M = (E_p [R | t]) E_p^-1, in the prior record layout; weights kept.
@@ -1027,23 +1038,6 @@ __global__ __launch_bounds__(256) void k_rig_prior(BatchCtx c) {
     out[14] = out[15] = 0.0;
 }
 
-void launch_rig_chain(const BatchCtx& c, hipStream_t s) {
-    if (c.prior && c.rig_prior)
-        hipLaunchKernelGGL(k_rig_prior, dim3((c.n + 255) / 256), dim3(256), 0, s, c);
-    BatchCtx r = c;   // chain the body motions with the pair chain kernel: one "pair", the rig
-    r.pose = c.rig_pose;
-    r.stats = c.rig_stats;
-    r.state = c.rig_state;
-    r.P = 1;
-    r.pair0 = 0;
-    r.npair = 1;
-    // the IMU priors are per (frame, pair) in each pair's rectified-left frame: the rig chain
-    // takes its body-frame prediction from c.rig_prior ([B][16], built by k_rig_prior), never the
-    // pair records
-    r.prior = c.prior ? c.rig_prior : nullptr;
-    hipLaunchKernelGGL(k_chain, dim3(1), dim3(256), 0, s, r);
-}
-
 int ransac_splits(const BatchCtx& c) {
     if (c.pp.splits > 0) return min(min(c.pp.splits, c.pp.n_hyp), TS_MAX_SPLITS);
     // scoring blocks (>= 4096: 64 waves per CU over the launch), at least 8 hypotheses per split
@@ -1070,6 +1064,10 @@ void launch_pose_solve(const BatchCtx& c, hipStream_t s) {
     hipLaunchKernelGGL(k_refine, dim3(c.n * c.npair), dim3(POSE_THREADS), 0, s, c, S);
 }
 
-void launch_chain(const BatchCtx& c, hipStream_t s) {
-    hipLaunchKernelGGL(k_chain, dim3(1), dim3(256), 0, s, c);
+// Every pair's chain and, with `rig`, the rig's (after k_rig_prior moves the IMU prediction to
+// the body frame), one block each in one launch.
+void launch_chains(const BatchCtx& c, bool rig, hipStream_t s) {
+    if (rig && c.prior && c.rig_prior)
+        hipLaunchKernelGGL(k_rig_prior, dim3((c.n + 255) / 256), dim3(256), 0, s, c);
+    hipLaunchKernelGGL(k_chain, dim3(c.P + (rig ? 1 : 0)), dim3(256), 0, s, c);
 }

@@ -430,6 +430,7 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.pair0 = 0;
     c.npair = h->P;
     c.match_modes = 3;
+    c.peer_S = c.peer_me = c.peer_nbuf = c.peer_skip = 0;
     return c;
 }
 
@@ -500,10 +501,7 @@ static int run_sharded_rgbd_stage(tslam_handle* h, const BatchCtx& c, int stage,
             if (!h->rig) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig)");
             launch_rig_pose(range_ctx(c, lo, hi), s);
             break;
-        case TSLAM_KERNEL_CHAIN:
-            launch_chain(c, s);
-            if (h->rig) launch_rig_chain(c, s);
-            break;
+        case TSLAM_KERNEL_CHAIN: launch_chains(c, h->rig, s); break;
         default:
             return fail(TSLAM_ESTATE, "a camera-sharded RGB-D handle runs its stages one by one: RECTIFY..DESCRIBE, "
                                       "MATCH, POSE, pack/exchange/unpack pairs, KERNEL_RIG, pose records, CHAIN");
@@ -548,10 +546,7 @@ static int run_sharded_stage(tslam_handle* h, const BatchCtx& c, int stage, hipS
             if (!h->rig) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig)");
             launch_rig_pose(cb, s);
             break;
-        case TSLAM_KERNEL_CHAIN:
-            launch_chain(c, s);
-            if (h->rig) launch_rig_chain(c, s);
-            break;
+        case TSLAM_KERNEL_CHAIN: launch_chains(c, h->rig, s); break;
         default:
             return fail(TSLAM_ESTATE, "a sharded handle runs its stages one by one around the exchange "
                                       "(RECTIFY..DESCRIBE, pack/exchange/unpack, MATCH, POSE, exchange, CHAIN)");
@@ -1005,8 +1000,8 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
         case TSLAM_STAGE_MATCH: launch_match(c, s); launch_match_refine(c, s); break;
         case TSLAM_STAGE_POSE:
             launch_pose(c, s);
-            launch_chain(c, s);
-            if (h->rig) launch_rig(c, s);
+            if (h->rig) launch_rig_pose(c, s);
+            launch_chains(c, h->rig, s);
             break;
         case TSLAM_STAGE_ALL:
             launch_rectify_pyramid(c, s);
@@ -1016,8 +1011,8 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
             launch_match(c, s);
             launch_match_refine(c, s);
             launch_pose(c, s);
-            launch_chain(c, s);
-            if (h->rig) launch_rig(c, s);
+            if (h->rig) launch_rig_pose(c, s);
+            launch_chains(c, h->rig, s);
             if (h->prm.ba_window) {
                 double* snap = h->ba.fe_pose + (size_t)(h->batch_idx & 1) * h->B * h->P * 16;
                 launch_ba_snapshot(c, snap, s);
@@ -1026,7 +1021,7 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
             break;
         case TSLAM_KERNEL_RIG:
             if (!h->rig) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig)");
-            launch_rig(c, s);
+            launch_rig_pose(c, s);
             break;
         case TSLAM_STAGE_BA: {
             // may run on its own stream: it depends on this batch's front end (event) and only
@@ -1060,7 +1055,7 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
         case TSLAM_KERNEL_MATCH: launch_match(c, s); break;
         case TSLAM_KERNEL_MATCH_REFINE: launch_match_refine(c, s); break;
         case TSLAM_KERNEL_POSE: launch_pose(c, s); break;
-        case TSLAM_KERNEL_CHAIN: launch_chain(c, s); break;
+        case TSLAM_KERNEL_CHAIN: launch_chains(c, h->rig, s); break;
         default: return fail(TSLAM_EINVAL, "unknown stage");
     }
     HIPCHK(hipGetLastError());
@@ -1380,6 +1375,63 @@ int tslam_internal_attach_driver(tslam_handle* h, tslam_shard_driver* d, bool ow
 }
 
 tslam_shard_driver* tslam_internal_driver(tslam_handle* h) { return h ? h->drv : nullptr; }
+
+// -- the all-to-all's peers in one launch each (alltoall layout [world][nr][S]) -------------------
+static int check_peers(tslam_handle* h) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (!h->in_batch) return fail(TSLAM_ESTATE, "peer exchange blocks are packed / imported inside a batch");
+    if (h->sh_world < 2 || h->prm.rgbd) return fail(TSLAM_ESTATE, "a stereo handle sharded over world > 1");
+    if ((h->sh_cam_hi - h->sh_cam_lo) * h->sh_world != h->C || h->sh_cam_lo != h->sh_rank * (h->sh_cam_hi - h->sh_cam_lo))
+        return fail(TSLAM_EINVAL, "peer layout needs cameras [rank*S, (rank+1)*S)");
+    return TSLAM_OK;
+}
+
+int tslam_pack_streams_peers(tslam_handle* h, void* dst, void* stream) {
+    int rc = check_peers(h);
+    if (rc != TSLAM_OK) return rc;
+    if (!dst) return fail(TSLAM_EINVAL, "null buffer");
+    HIPCHK(hipSetDevice(h->device));
+    const int N = h->sh_world, S = h->sh_cam_hi - h->sh_cam_lo, fpr = h->cur_n / N;
+    launch_stream_blocks_peers(make_ctx(h), true, h->cur_g0, fpr, fpr + 1, N, h->sh_rank, S, (uint8_t*)dst,
+                               (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return TSLAM_OK;
+}
+
+int tslam_stage_raw_peers(tslam_handle* h, const uint8_t* prev_raw, void* dst, void* stream) {
+    int rc = check_peers(h);
+    if (rc != TSLAM_OK) return rc;
+    if (!prev_raw || !dst) return fail(TSLAM_EINVAL, "null buffer");
+    HIPCHK(hipSetDevice(h->device));
+    const int N = h->sh_world, S = h->sh_cam_hi - h->sh_cam_lo;
+    launch_stage_raw_peers(h->cur_images, prev_raw, (uint8_t*)dst, h->cur_n / N, N, h->sh_rank, S, (int64_t)h->W * h->H,
+                           (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return TSLAM_OK;
+}
+
+int tslam_import_peers(tslam_handle* h, const uint8_t* raw, const void* streams, void* stream) {
+    int rc = check_peers(h);
+    if (rc != TSLAM_OK) return rc;
+    if (!raw || !streams) return fail(TSLAM_EINVAL, "null buffer");
+    HIPCHK(hipSetDevice(h->device));
+    const int N = h->sh_world, S = h->sh_cam_hi - h->sh_cam_lo, fpr = h->cur_n / N, nr = fpr + 1;
+    const int64_t first = h->cur_g0 + (int64_t)h->sh_rank * fpr - 1;
+    const int skip = first < 0 ? 1 : 0;   // frame -1 (before the sequence start) is not imported
+    BatchCtx c = make_ctx(h);
+    c.images = raw;
+    c.g0 = first + skip;
+    c.n = nr - skip;
+    c.peer_S = S;
+    c.peer_me = h->sh_rank;
+    c.peer_nbuf = nr;
+    c.peer_skip = skip;
+    launch_rectify_pyramid(c, (hipStream_t)stream);
+    launch_stream_blocks_peers(make_ctx(h), false, h->cur_g0, fpr, nr, N, h->sh_rank, S, (uint8_t*)streams,
+                               (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return TSLAM_OK;
+}
 
 int tslam_pack_poses(tslam_handle* h, void* dst, void* stream) {
     if (!h || !dst) return fail(TSLAM_EINVAL, "bad argument");

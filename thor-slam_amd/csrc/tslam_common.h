@@ -96,6 +96,10 @@ struct BatchCtx {
     // keep their [n][P] layout
     int pair0, npair;
     int match_modes;       // k_match: 3 = temporal + stereo, 1 = stereo only (sharded pre-pass)
+    // peer layout of a sharded import (tslam_import_peers): images [world][nbuf][S][H][W] as the
+    // all-to-all delivers them; the launch covers the world-1 peers' slots (not peer_me's), frames
+    // peer_skip .. nbuf-1 of each (peer_S = 0: the plain [n][ncam] view above)
+    int peer_S, peer_me, peer_nbuf, peer_skip;
     int64_t g0;            // global index of the batch's first frame
     int W, H;              // level-0 size
     // inputs
@@ -152,10 +156,27 @@ struct BatchCtx {
 };
 
 static inline __host__ __device__ int ring_slot(const BatchCtx& c, int64_t g) { return (int)(g % c.R); }
-// front-end image index (f * ncam + view camera) -> frame, rig camera
+// front-end image index (f * ncam + view camera) -> frame, rig camera; in the peer layout the
+// index runs over (peer, frame, camera) of the world-1 peers
 __device__ __forceinline__ void view_image(const BatchCtx& c, int img, int* f, int* cam) {
+    if (c.peer_S) {
+        const int per = c.n * c.peer_S, qq = img / per, q = qq < c.peer_me ? qq : qq + 1;
+        const int r = img - qq * per;
+        *f = r / c.peer_S;
+        *cam = q * c.peer_S + (r - *f * c.peer_S);
+        return;
+    }
     *f = img / c.ncam;
     *cam = c.cam0 + (img - *f * c.ncam);
+}
+// the input image of view index img (its offset in c.images, in images)
+__device__ __forceinline__ size_t view_src(const BatchCtx& c, int img) {
+    if (c.peer_S) {
+        const int per = c.n * c.peer_S, qq = img / per, q = qq < c.peer_me ? qq : qq + 1;
+        const int r = img - qq * per, f = r / c.peer_S;
+        return ((size_t)q * c.peer_nbuf + c.peer_skip + f) * c.peer_S + (r - f * c.peer_S);
+    }
+    return (size_t)img;
 }
 
 // host launchers (one per stage kernel set)
@@ -167,15 +188,20 @@ void launch_match(const BatchCtx& c, hipStream_t s);
 void launch_match_refine(const BatchCtx& c, hipStream_t s);
 void launch_match_stereo(const BatchCtx& c, hipStream_t s);
 void launch_pose(const BatchCtx& c, hipStream_t s);
-void launch_chain(const BatchCtx& c, hipStream_t s);
-void launch_rig(const BatchCtx& c, hipStream_t s);
+void launch_chains(const BatchCtx& c, bool rig, hipStream_t s);   // every pair's chain (+ the rig's)
 void launch_rig_pose(const BatchCtx& c, hipStream_t s);
-void launch_rig_chain(const BatchCtx& c, hipStream_t s);
 // sharded rig exchange (k_exchange.hip): stream blocks (per frame x camera) and pose records (per frame)
 int64_t stream_block_bytes(const LevelGeom& g);
 int64_t pose_record_bytes(int P);
 void launch_stream_blocks(const BatchCtx& c, bool pack, int64_t first, int n_frames, int cam_lo, int ncam, uint8_t* blk,
                           hipStream_t s);
+// all peers at once (alltoall layout [world][nr][S][block]): pack this rank's cameras of every
+// peer q's frames g0 + q*fpr - 1 .. (slot q), or unpack every peer's cameras of frames
+// g0 + me*fpr - 1 .. (slot q <- cameras q*S ..); slot `me` untouched
+void launch_stream_blocks_peers(const BatchCtx& c, bool pack, int64_t g0, int fpr, int nr, int world, int me, int S,
+                                uint8_t* blk, hipStream_t s);
+void launch_stage_raw_peers(const uint8_t* images, const uint8_t* prev, uint8_t* dst, int fpr, int world, int me, int S,
+                            int64_t img_bytes, hipStream_t s);
 void launch_pose_records(const BatchCtx& c, bool pack, int f0, int n, uint8_t* rec, hipStream_t s);
 // camera-sharded RGB-D rig: pair blocks (per batch frame x pair: pose, stats, correspondences)
 int64_t pair_block_bytes(const LevelGeom& g);

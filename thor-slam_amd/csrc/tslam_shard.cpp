@@ -236,17 +236,11 @@ static int exchange(tslam_shard_driver* d, Which w, int k) {
 }
 
 // Raw images of this rank's cameras for every peer: its frames lo-1 .. hi-1 (frame -1 = the last
-// frame of the previous batch), on the exchange stream.
+// frame of the previous batch), one gather launch on the exchange stream; then this batch's last
+// frame becomes prev_raw.
 static int stage_raw(tslam_shard_driver* d, Rank& r, const uint8_t* images, int k) {
     const size_t frame = (size_t)d->S * d->img;
-    for (int q = 0; q < d->world; ++q) {
-        if (q == r.rank) continue;
-        const int lo = q * d->fpr;
-        uint8_t* out = r.raw_send[k] + (size_t)q * d->raw_q;
-        const uint8_t* first = lo == 0 ? r.prev_raw : images + (size_t)(lo - 1) * frame;
-        SHCHK(hipMemcpyAsync(out, first, frame, hipMemcpyDeviceToDevice, r.xs));
-        SHCHK(hipMemcpyAsync(out + frame, images + (size_t)lo * frame, (size_t)d->fpr * frame, hipMemcpyDeviceToDevice, r.xs));
-    }
+    if (d->world > 1) RC(tslam_stage_raw_peers(r.h, r.prev_raw, r.raw_send[k], r.xs));
     SHCHK(hipMemcpyAsync(r.prev_raw, images + (size_t)(d->n - 1) * frame, frame, hipMemcpyDeviceToDevice, r.xs));
     return TSLAM_OK;
 }
@@ -271,11 +265,7 @@ static int submit(tslam_shard_driver* d, const uint8_t* const* images, int n, vo
     for (Rank& r : d->ranks) {   // front end of the rank's cameras (+ its stream blocks per peer)
         for (int st : front) RC(tslam_run_stage(r.h, st, r.fs));
         if (d->rgbd) continue;
-        const int64_t g0 = tslam_frames_done(r.h);
-        for (int q = 0; q < N; ++q)
-            if (q != r.rank)
-                RC(tslam_pack_streams(r.h, g0 + (int64_t)q * d->fpr - 1, d->nr, r.rank * S, (r.rank + 1) * S,
-                                      r.feat_send[k] + (size_t)q * d->feat_q, r.fs));
+        if (N > 1) RC(tslam_pack_streams_peers(r.h, r.feat_send[k], r.fs));   // every peer's frames, one launch
         SHCHK(hipSetDevice(r.device));
         SHCHK(hipEventRecord(r.ev_front, r.fs));
         SHCHK(hipStreamWaitEvent(r.xs, r.ev_front, 0));
@@ -287,12 +277,7 @@ static int submit(tslam_shard_driver* d, const uint8_t* const* images, int n, vo
             SHCHK(hipSetDevice(r.device));
             SHCHK(hipEventRecord(r.ev_x, r.xs));
             SHCHK(hipStreamWaitEvent(r.bs, r.ev_x, 0));
-            const int64_t first = tslam_frames_done(r.h) + (int64_t)r.rank * d->fpr - 1;
-            for (int q = 0; q < N; ++q) {
-                if (q == r.rank) continue;
-                RC(tslam_import_raw(r.h, r.raw_recv[k] + (size_t)q * d->raw_q, first, d->nr, q * S, (q + 1) * S, r.bs));
-                RC(tslam_unpack_streams(r.h, first, d->nr, q * S, (q + 1) * S, r.feat_recv[k] + (size_t)q * d->feat_q, r.bs));
-            }
+            if (N > 1) RC(tslam_import_peers(r.h, r.raw_recv[k], r.feat_recv[k], r.bs));
             SHCHK(hipEventRecord(r.consumed[k], r.bs));
             r.consumed_armed[k] = true;
         }

@@ -133,6 +133,9 @@ _SIGNATURES = {
                                             ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_import_raw": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_void_p]),
+    "tslam_stage_raw_peers": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_pack_streams_peers": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_import_peers": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_pair_block_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]),
     "tslam_pack_pairs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_void_p, ctypes.c_void_p]),
@@ -476,6 +479,17 @@ class Handle:
     def import_raw(self, images_ptr: int, first_frame: int, n_frames: int, cam_lo: int, cam_hi: int, stream: int = 0) -> None:
         _check(self.lib.tslam_import_raw(self.h, ctypes.c_void_p(images_ptr), int(first_frame), int(n_frames), int(cam_lo),
                                          int(cam_hi), ctypes.c_void_p(stream)))
+
+    def stage_raw_peers(self, prev_raw_ptr: int, dst_ptr: int, stream: int = 0) -> None:
+        _check(self.lib.tslam_stage_raw_peers(self.h, ctypes.c_void_p(prev_raw_ptr), ctypes.c_void_p(dst_ptr),
+                                              ctypes.c_void_p(stream)))
+
+    def pack_streams_peers(self, dst_ptr: int, stream: int = 0) -> None:
+        _check(self.lib.tslam_pack_streams_peers(self.h, ctypes.c_void_p(dst_ptr), ctypes.c_void_p(stream)))
+
+    def import_peers(self, raw_ptr: int, streams_ptr: int, stream: int = 0) -> None:
+        _check(self.lib.tslam_import_peers(self.h, ctypes.c_void_p(raw_ptr), ctypes.c_void_p(streams_ptr),
+                                           ctypes.c_void_p(stream)))
 
     def pair_block_bytes(self) -> int:
         """Bytes of one RGB-D pair block (pose, stats, correspondences of one frame and camera)."""

@@ -207,6 +207,11 @@ class RankShard:
         torch = self.torch
         k = self.batches % 2
         imgs = self.images.reshape(self.plan.batch, self.plan.streams_per_rank, -1)
+        if self.exchange == "alltoall" and self.plan.world > 1:   # every peer's frames, one gather launch
+            self.h.stage_raw_peers(self.prev_raw.data_ptr(), self.raw_send[k].data_ptr(), stream.cuda_stream)
+            with torch.cuda.stream(stream):
+                self.prev_raw.copy_(imgs[-1])
+            return
         with torch.cuda.stream(stream):
             dests = range(self.plan.world) if self.exchange == "alltoall" else [0]
             for j, q in enumerate(dests):
@@ -222,6 +227,9 @@ class RankShard:
 
     def pack_features(self, stream: int) -> None:
         k = self.batches % 2
+        if self.exchange == "alltoall" and self.plan.world > 1:
+            self.h.pack_streams_peers(self.feat_send[k].data_ptr(), stream)
+            return
         dests = range(self.plan.world) if self.exchange == "alltoall" else [0]
         for j, q in enumerate(dests):
             self.h.pack_streams(self._first_sent(q), self.frames_sent, self.cam_lo, self.cam_hi,
@@ -234,6 +242,9 @@ class RankShard:
         """The other ranks' cameras of frames lo-1 .. hi-1 into the ring: raw -> rectify +
         pyramid, stream blocks -> keypoints / records / descriptors."""
         k = self.batches % 2
+        if self.exchange == "alltoall" and self.plan.world > 1:   # rectify + unpack every peer, two launches
+            self.h.import_peers(self.raw_recv[k].data_ptr(), self.feat_recv[k].data_ptr(), stream)
+            return
         lo, hi = self.plan.frames(self.rank)
         for q in range(self.plan.world):
             if q == self.rank:
