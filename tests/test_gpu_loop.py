@@ -6,7 +6,8 @@
 * the device pose graph (dense normal equations, blocked Cholesky with FP64-MFMA trailing
   updates) equals the oracle's Gauss-Newton within 1e-9 relative, from 1 node to 200 nodes;
 * HipSlamEngine closes the loop of a circular trajectory and the pose graph pulls the keyframes
-  towards the rendered ground truth."""
+  towards the rendered ground truth; on the two-source bracket rig place recognition runs over
+  every pair's keyframe entries, so a loop only pair 1 can see is still closed."""
 
 from __future__ import annotations
 
@@ -196,6 +197,22 @@ def _render_rig(idx):
     return [np.stack([s.render_image(i, c) for s in srcs for c in (0, 1)]) for i in idx]
 
 
+def _check_loop_edges(pg, bt, src):
+    """Every loop edge's measurement (T_a^-1 T_b of pair 0's rect-left camera, whichever pairs
+    recognised and verified the place) against the rendered ground truth."""
+    n = 0
+    for (a, b), Z in zip(pg["edges"], pg["meas"]):
+        if b == a + 1:
+            continue
+        fa, fb = pg["frames"][a], pg["frames"][b]
+        gt = np.linalg.inv(bt) @ np.linalg.inv(src.ground_truth_body(fa)) @ src.ground_truth_body(fb) @ bt
+        assert np.linalg.norm(Z[:3, 3] - gt[:3, 3]) < 0.03, (fa, fb, Z[:3, 3], gt[:3, 3])
+        ang = np.degrees(np.arccos(np.clip((np.trace(Z[:3, :3] @ gt[:3, :3].T) - 1) / 2, -1, 1)))
+        assert ang < 0.5, (fa, fb, ang)
+        n += 1
+    return n
+
+
 def test_engine_closes_the_loop_on_a_two_source_rig():
     """The bracket rig's two stereo sources on the loop trajectory: the rig pose (k_rig_pose) is
     tracked, place recognition and verification run on pair 0's camera, and the pose graph over
@@ -222,8 +239,12 @@ def test_engine_closes_the_loop_on_a_two_source_rig():
         eng.process_batch(dev[b0:b0 + 30], [srcs[0].timestamp(i) for i in range(b0, b0 + 30)])
     loops = eng.loop_closures
     assert loops, "no loop closed"
-    assert all(c <= 40 and q >= 225 for c, q, _ in loops), loops
     pg, lp, bt = eng.pose_graph, eng._loop, eng._base_T_rect
+    # rig-wide recognition: besides the same-pair loops after the full turn (frame >= 225), pair
+    # 1 sees pair 0's early view part-way round (and pair 0 pair 1's) -- every edge must agree
+    # with the ground truth
+    assert _check_loop_edges(pg, bt, srcs[0]) == len(loops)
+    assert any(c <= 40 and q >= 225 and p == r for (c, q, _), (p, r) in zip(loops, lp.pairs)), (loops, lp.pairs)
     gt0 = np.linalg.inv(srcs[0].ground_truth_body(0))
     err_raw, err_opt = [], []
     for g, raw, T in zip(pg["frames"], lp.raw, pg["T"]):
@@ -231,7 +252,54 @@ def test_engine_closes_the_loop_on_a_two_source_rig():
         err_raw.append(np.linalg.norm((bt @ raw @ np.linalg.inv(bt))[:3, 3] - gt[:3, 3]))
         err_opt.append(np.linalg.norm((bt @ T @ np.linalg.inv(bt))[:3, 3] - gt[:3, 3]))
     assert np.mean(err_opt[-5:]) <= np.mean(err_raw[-5:]) + 1e-4, (err_raw[-5:], err_opt[-5:])
-    assert max(err_opt) <= max(err_raw) + 1e-4, (max(err_raw), max(err_opt))
-    print("rig keyframe position error vs ground truth: raw max %.4f m, optimised max %.4f m, last-5 %.4f -> %.4f m"
-          % (max(err_raw), max(err_opt), np.mean(err_raw[-5:]), np.mean(err_opt[-5:])))
+    # the rig's raw drift is millimetres here, so the cross-pair loop edges (each within 3 cm /
+    # 0.5 deg of the truth) may spread a few millimetres over the graph
+    assert max(err_opt) < 0.03, (max(err_raw), max(err_opt))
+    print("rig loops %s (pairs %s); keyframe position error vs ground truth: raw max %.4f m, optimised max %.4f m, "
+          "last-5 %.4f -> %.4f m" % (loops, lp.pairs, max(err_raw), max(err_opt), np.mean(err_raw[-5:]),
+                                     np.mean(err_opt[-5:])))
+    eng.shutdown()
+
+
+def test_rig_loop_seen_only_by_pair_1():
+    """Rig-wide place recognition: pair 0 of the bracket rig is blind (flat images) for the whole
+    run, so only pair 1's keyframe entries can recognise the place; the loop is found, verified on
+    pair 1's camera, and its edge (moved into pair 0's frame through the rig extrinsics) agrees
+    with the ground-truth relative motion of pair 0's rectified-left camera."""
+    import torch
+
+    from thor_slam_amd.slam.hip_engine import HipSlamEngine
+
+    srcs, mats = _rig_loop_sources()
+    idx = list(range(LOOP_FRAMES))
+    chunks = [idx[i::16] for i in range(16)]
+    out = {}
+    with ProcessPoolExecutor(max_workers=16) as ex:
+        for c, frs in zip(chunks, ex.map(_render_rig, chunks)):
+            out.update(zip(c, frs))
+    frames = np.stack([out[i] for i in idx])
+    frames[:, 0:2] = 128                      # pair 0 blind
+    rig = CameraRig(srcs, rig_extrinsics={s.name: Extrinsics.from_4x4_matrix(np.array(mats[s.name])) for s in srcs})
+    cfg = HipSlamConfig(batch_size=30, enable_loop_closure=True)
+    eng = HipSlamEngine(num_cameras=4, config=cfg)
+    eng.initialize(rig.calibration, cfg)
+    dev = torch.from_numpy(frames).cuda()
+    for b0 in range(0, LOOP_FRAMES, 30):
+        eng.process_batch(dev[b0:b0 + 30], [srcs[0].timestamp(i) for i in range(b0, b0 + 30)])
+    loops = eng.loop_closures
+    assert loops, "no loop closed"
+    assert all(c <= 40 and q >= 225 for c, q, _ in loops), loops
+    lp, bt = eng._loop, eng._base_T_rect
+    assert lp.pairs and all(pq == (1, 1) for pq in lp.pairs), lp.pairs
+    pg = eng.pose_graph
+    _check_loop_edges(pg, bt, srcs[0])
+    gt0 = np.linalg.inv(srcs[0].ground_truth_body(0))
+    err_raw, err_opt = [], []
+    for g, raw, T in zip(pg["frames"], lp.raw, pg["T"]):
+        gt = gt0 @ srcs[0].ground_truth_body(g)
+        err_raw.append(np.linalg.norm((bt @ raw @ np.linalg.inv(bt))[:3, 3] - gt[:3, 3]))
+        err_opt.append(np.linalg.norm((bt @ T @ np.linalg.inv(bt))[:3, 3] - gt[:3, 3]))
+    assert np.mean(err_opt[-5:]) <= np.mean(err_raw[-5:]) + 1e-4, (err_raw[-5:], err_opt[-5:])
+    print("pair-1-only loop: %s; keyframe error raw max %.4f m, optimised max %.4f m"
+          % (loops, max(err_raw), max(err_opt)))
     eng.shutdown()

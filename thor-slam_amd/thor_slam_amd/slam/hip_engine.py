@@ -104,6 +104,7 @@ class _LoopGraph:
         self.meas: list[np.ndarray] = []
         self.info: list[np.ndarray] = []
         self.loops: list[tuple[int, int, int]] = []
+        self.pairs: list[tuple[int, int]] = []     # per loop: (pair of the older entry, verifying pair)
         self.corr = np.eye(4)
         self.cost = 0.0
         self.full = False
@@ -213,10 +214,14 @@ class HipSlamEngine(SlamEngine):
             if cfg.enable_loop_closure and self._shard is not None:
                 logger.warning("loop closure is not run on a sharded rig (devices=%s)", cfg.devices)
             elif cfg.enable_loop_closure:
-                # place recognition and loop verification on pair 0's camera; on a multi-pair rig
-                # the keyframe nodes are pair 0's rectified-left poses taken from the rig's body
-                # poses (k_rig_pose), and the pose-graph correction moves the body poses
-                self._handle.loop_init(cfg.loop_max_keyframes, cfg.loop_signature)
+                # place recognition over every pair's camera (P database entries per keyframe,
+                # keyframe-major) and verification on the pair that voted best; the keyframe nodes
+                # are pair 0's rectified-left poses (on a multi-pair rig taken from the rig's body
+                # poses, k_rig_pose), and the pose-graph correction moves the body poses
+                cap = cfg.loop_max_keyframes * len(self._pairs)
+                if cap > 1 << 16:
+                    raise ValueError(f"loop_max_keyframes * pairs = {cap} exceeds the 65536-entry database")
+                self._handle.loop_init(cap, cfg.loop_signature)
                 self._loop = _LoopGraph()
         except RuntimeError:
             raise
@@ -594,18 +599,22 @@ class HipSlamEngine(SlamEngine):
 
     # -- loop closure + keyframe pose graph ---------------------------
     def _loop_keyframe(self, g: int, raw: np.ndarray, ts: float) -> None:
-        """Keyframe g: store it in the device database, add its odometry edge, look for a loop
-        among the keyframes at least ``loop_min_gap`` older (signature votes, then RANSAC
-        verification) and, on a verified loop, re-solve the pose graph on the device."""
+        """Keyframe g: store every pair's view of it in the device database (entry idx * P + p),
+        add its odometry edge, look for a loop among the keyframes at least ``loop_min_gap`` older
+        (signature votes of each pair's entry against every older entry of every pair; the best
+        vote wins, lower pair first), verify it (RANSAC on the voting pair's camera against the
+        entry's landmarks) and, on a verified loop, re-solve the pose graph on the device.  A
+        pair-q view of a place pair p saw gives the node edge in pair 0's frame:
+        T_c^-1 T_q = M_p V^-1 M_q^-1 with V = cam_q_T_cam_p and M_p = rect0_T_rect_p."""
         cfg, lp, h = self._config, self._loop, self._handle
-        idx = len(lp.frames)
+        idx, P = len(lp.frames), len(self._pairs)
         if idx >= cfg.loop_max_keyframes:
             if not lp.full:
                 logger.warning("loop closure: keyframe database full (%d); no further keyframes", idx)
                 lp.full = True
             return
-        slot, _ = h.loop_add_keyframe(g)
-        assert slot == idx
+        slots = [h.loop_add_keyframe(g, pair=p)[0] for p in range(P)]
+        assert slots == list(range(idx * P, idx * P + P))
         info = lp.information(cfg)
         if idx == 0:
             T = lp.corr @ raw
@@ -622,17 +631,24 @@ class HipSlamEngine(SlamEngine):
         n_allowed = idx - cfg.loop_min_gap + 1
         if n_allowed <= 0:
             return
-        votes = h.loop_query(slot, n_allowed)
-        j = int(np.argmax(votes))
-        if votes[j] < cfg.loop_min_votes:
+        best, q, e = -1, 0, 0
+        for p, slot in enumerate(slots):
+            votes = h.loop_query(slot, n_allowed * P)
+            j = int(np.argmax(votes))
+            if votes[j] > best:
+                best, q, e = int(votes[j]), p, j
+        if best < cfg.loop_min_votes:
             return
-        ver = h.loop_verify(g, j)
+        ver = h.loop_verify(g, e, pair=q)
         if int(ver["stats"][0]) != POSE_OK or int(ver["stats"][2]) < cfg.loop_min_inliers:
             return
+        j, p = divmod(e, P)
+        m = [_invert(self._base_T_rects[0]) @ self._base_T_rects[k] for k in (p, q)]
         lp.edges.append((j, idx))
-        lp.meas.append(_invert(ver["T"]))     # T_c^-1 T_q = inv(cam_q_T_cam_c)
+        lp.meas.append(m[0] @ _invert(ver["T"]) @ _invert(m[1]))
         lp.info.append(info)
         lp.loops.append((lp.frames[j], g, int(ver["stats"][2])))
+        lp.pairs.append((p, q))
         sol = h.pose_graph(np.stack(lp.T), np.array(lp.edges), np.stack(lp.meas), np.stack(lp.info), cfg.pg_iters)
         lp.T = list(sol["T"])
         lp.cost = sol["cost"]
