@@ -187,27 +187,27 @@ __device__ __forceinline__ bool is_inlier(const double* R, const double* t, cons
 // to first order; the test uses twice that, which also covers the second-order terms, the f32
 // evaluation of the bound and the f64 reference's own rounding (~2^-53 of the same sum).  So
 // D > E and zc > E_z mean the f64 test says inlier, D < -E or zc < -E_z outlier.
-struct PoseF32 {
-    float R[9], t[3], aR[9], at[3];
-};
-__device__ __forceinline__ int inlier_f32(const PoseF32& P, const float* c, float fx, float fy, float thr2) {
-    const float X = c[0], Y = c[1], Z = c[2], du = c[3], dv = c[4];
-    const float aX = fabsf(X), aY = fabsf(Y), aZ = fabsf(Z);
-    const float xc = fmaf(P.R[0], X, fmaf(P.R[1], Y, fmaf(P.R[2], Z, P.t[0])));
-    const float yc = fmaf(P.R[3], X, fmaf(P.R[4], Y, fmaf(P.R[5], Z, P.t[1])));
-    const float zc = fmaf(P.R[6], X, fmaf(P.R[7], Y, fmaf(P.R[8], Z, P.t[2])));
-    const float ax = fmaf(P.aR[0], aX, fmaf(P.aR[1], aY, fmaf(P.aR[2], aZ, P.at[0])));
-    const float ay = fmaf(P.aR[3], aX, fmaf(P.aR[4], aY, fmaf(P.aR[5], aZ, P.at[1])));
-    const float az = fmaf(P.aR[6], aX, fmaf(P.aR[7], aY, fmaf(P.aR[8], aZ, P.at[2])));
+// The bound is taken with one magnitude for all three rows, a = rmax S + tmax >= a_x, a_y, a_z
+// (rmax = max |R_ij|, S = |X| + |Y| + |Z|, tmax = max |t_i|), which turns it into
+// a [|ex| (fx + |du|) + |ey| (fy + |dv|) + thr2 |zc|] + ex^2 + ey^2 + thr2 zc^2: per test 8
+// operations instead of 20, with fx + |du|, fy + |dv| and S per correspondence.
+// pf: the pose's f32 record (R 9, t 3, rmax, tmax; k_p3p); q: X Y Z du dv S fx+|du| fy+|dv|.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ int inlier_f32(const f32x16& pf, const float* q, float fx, float fy, float thr2) {
+    const float X = q[0], Y = q[1], Z = q[2], du = q[3], dv = q[4];
+    const float xc = fmaf(pf[0], X, fmaf(pf[1], Y, fmaf(pf[2], Z, pf[9])));
+    const float yc = fmaf(pf[3], X, fmaf(pf[4], Y, fmaf(pf[5], Z, pf[10])));
+    const float zc = fmaf(pf[6], X, fmaf(pf[7], Y, fmaf(pf[8], Z, pf[11])));
     const float ex = fmaf(fx, xc, du * zc);
     const float ey = fmaf(fy, yc, dv * zc);
     const float e2 = fmaf(ex, ex, ey * ey);
     const float lim = thr2 * (zc * zc);
     const float D = lim - e2;
-    const float adu = fabsf(du), adv = fabsf(dv);
-    const float bsum = fmaf(fabsf(ex), fmaf(fx, ax, adu * az), fmaf(fabsf(ey), fmaf(fy, ay, adv * az), fmaf(thr2 * fabsf(zc), az, e2 + lim)));
+    const float a = fmaf(pf[12], q[5], pf[13]);
+    const float inner = fmaf(fabsf(ex), q[6], fmaf(fabsf(ey), q[7], thr2 * fabsf(zc)));
+    const float bsum = fmaf(a, inner, e2 + lim);
     const float E = bsum * (32.0f / 16777216.0f);
-    const float Ez = az * (32.0f / 16777216.0f);
+    const float Ez = a * (32.0f / 16777216.0f);
     if (zc < -Ez || D < -E) return 0;
     if (zc > Ez && D > E) return 1;
     return -1;
@@ -320,7 +320,8 @@ __global__ __launch_bounds__(POSE_THREADS) void k_corr(BatchCtx c) {
 
 // ---- k_p3p: one thread per (frame, pair, hypothesis) -------------------------------------
 // Draws the hypothesis' 3 correspondences (splitmix64 of (seed, frame, h)), solves P3P and writes
-// its 4 candidate poses [R 9 | t 3] to c.hyp (first element NaN = no solution).
+// its 4 candidate poses to c.hyp ([R 9 | t 3] f64 + their f32 scoring copies, TS_HYP_DOUBLES;
+// first element NaN = no solution).
 __global__ __launch_bounds__(POSE_THREADS) void k_p3p(BatchCtx c) {
     const int H = c.pp.n_hyp;
     const int gid = blockIdx.x * POSE_THREADS + threadIdx.x;
@@ -356,16 +357,30 @@ __global__ __launch_bounds__(POSE_THREADS) void k_p3p(BatchCtx c) {
     }
     Pose sol[4];
     const int mask = p3p_solve(pw, fb, sol);
-    double* out = c.hyp + ((size_t)fp * 4 * H + 4 * h) * 12;
+    double* out = c.hyp + ((size_t)fp * 4 * H + 4 * h) * TS_HYP_DOUBLES;
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2) {
-        double* dst = out + s2 * 12;
+        double* dst = out + s2 * TS_HYP_DOUBLES;
         if ((mask >> s2) & 1) {
+            float* df = reinterpret_cast<float*>(dst + 12);
+            float rmax = 0.0f, tmax = 0.0f;
 #pragma unroll
-            for (int k = 0; k < 9; ++k) dst[k] = sol[s2].r[k];
-            dst[9] = sol[s2].t[0]; dst[10] = sol[s2].t[1]; dst[11] = sol[s2].t[2];
+            for (int k = 0; k < 9; ++k) {
+                dst[k] = sol[s2].r[k];
+                df[k] = (float)sol[s2].r[k];
+                rmax = fmaxf(rmax, fabsf(df[k]));
+            }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                dst[9 + k] = sol[s2].t[k];
+                df[9 + k] = (float)sol[s2].t[k];
+                tmax = fmaxf(tmax, fabsf(df[9 + k]));
+            }
+            df[12] = rmax;
+            df[13] = tmax;
         } else {
             dst[0] = __builtin_nan("");
+            reinterpret_cast<float*>(dst + 12)[0] = __builtin_nanf("");
         }
     }
 }
@@ -399,7 +414,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
     const PairCalib cal = c.calib[p];
     const double fx = cal.fx, fy = cal.fy;
     const double* corr = c.corr + ((size_t)f * c.P + p) * c.g.K * TS_CORR_DOUBLES;
-    const double* hyp = c.hyp + ((size_t)fp * 4 * H + 4 * h0) * 12;   // this split's poses
+    const double* hyp = c.hyp + ((size_t)fp * 4 * H + 4 * h0) * TS_HYP_DOUBLES;   // this split's poses
     typedef const __attribute__((address_space(4))) double cdouble;   // uniform address -> s_load
     cdouble* chyp = (cdouble*)(uintptr_t)hyp;
     const int npose = 4 * nh;
@@ -408,7 +423,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
     const double thr2 = c.pp.thr2;
     const float fxf = (float)fx, fyf = (float)fy, thr2f = (float)thr2;
     for (int c0 = 0; c0 < n; c0 += POSE_THREADS * TS_RS_CPT) {
-        float cf[TS_RS_CPT][5];
+        float cf[TS_RS_CPT][8];   // X Y Z du dv, |X| + |Y| + |Z|, fx + |du|, fy + |dv|
         bool have[TS_RS_CPT];
 #pragma unroll
         for (int k = 0; k < TS_RS_CPT; ++k) {
@@ -417,25 +432,22 @@ __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
             const double* cr = corr + (size_t)(have[k] ? ci : 0) * TS_CORR_DOUBLES;
 #pragma unroll
             for (int q = 0; q < 5; ++q) cf[k][q] = (float)cr[q];
+            cf[k][5] = fabsf(cf[k][0]) + fabsf(cf[k][1]) + fabsf(cf[k][2]);
+            cf[k][6] = fxf + fabsf(cf[k][3]);
+            cf[k][7] = fyf + fabsf(cf[k][4]);
         }
+        // correspondence slots no lane of this wave has are skipped (wave-uniform)
+        const int kmax = min(TS_RS_CPT, (n - c0 - wave * 64 + POSE_THREADS - 1) / POSE_THREADS);
         for (int pi = 0; pi < npose; ++pi) {
-            cdouble* ps = chyp + (size_t)pi * 12;
-            if (__builtin_isnan(ps[0])) continue;   // uniform
-            PoseF32 P;
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                P.R[k] = (float)ps[k];
-                P.aR[k] = fabsf(P.R[k]);
-            }
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                P.t[k] = (float)ps[9 + k];
-                P.at[k] = fabsf(P.t[k]);
-            }
+            cdouble* ps = chyp + (size_t)pi * TS_HYP_DOUBLES;
+            // the f32 record in one scalar load (SGPR operands of the test)
+            const f32x16 pf = *(const __attribute__((address_space(4))) f32x16*)(ps + 12);
+            if (__builtin_isnan(pf[0])) continue;   // uniform
             int cnt = 0;
 #pragma unroll
             for (int k = 0; k < TS_RS_CPT; ++k) {
-                int v = have[k] ? inlier_f32(P, cf[k], fxf, fyf, thr2f) : 0;
+                if (k >= kmax) break;   // uniform
+                int v = have[k] ? inlier_f32(pf, cf[k], fxf, fyf, thr2f) : 0;
                 if (v < 0) {   // near the threshold: the exact f64 test (rare, divergent)
                     double R[9], t[3];
                     const double* cr = corr + (size_t)(c0 + k * POSE_THREADS + tid) * TS_CORR_DOUBLES;
@@ -452,7 +464,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
     __syncthreads();
     uint32_t my_best = 0;
     for (int pi = tid; pi < npose; pi += POSE_THREADS) {
-        const bool valid = !__builtin_isnan(hyp[(size_t)pi * 12]);
+        const bool valid = !__builtin_isnan(hyp[(size_t)pi * TS_HYP_DOUBLES]);
         const int gidx = 4 * h0 + pi;
         const uint32_t key = valid ? ((uint32_t)(s_cnt[pi] + 1) << 12) | (uint32_t)(4095 - gidx) : (uint32_t)(4095 - gidx);
         my_best = key > my_best ? key : my_best;
@@ -470,7 +482,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
     if (tid == 0) kout[0] = best;
     if (tid < 12 && best != 0u) {
         const int gidx = 4095 - (int)(best & 4095u);
-        const double v = hyp[(size_t)(gidx - 4 * h0) * 12 + tid];
+        const double v = hyp[(size_t)(gidx - 4 * h0) * TS_HYP_DOUBLES + tid];
         reinterpret_cast<double*>(kout + 2)[tid] = v;
     }
 }

@@ -450,7 +450,7 @@ static BatchCtx range_ctx(const BatchCtx& c, int lo, int hi) {
     r.pose += f * P * TS_POSE_DOUBLES;
     r.stats += f * P * TS_STATS_INTS;
     r.ransac += f * P * TS_MAX_SPLITS * TS_RANSAC_WORDS / 2;
-    r.hyp += f * P * 4 * (size_t)c.pp.n_hyp * 12;
+    r.hyp += f * P * 4 * (size_t)c.pp.n_hyp * TS_HYP_DOUBLES;
     if (r.prior) r.prior += f * P * TS_PRIOR_DOUBLES;
     if (r.rig_prior) r.rig_prior += f * TS_PRIOR_DOUBLES;
     if (r.rig_pose) r.rig_pose += f * TS_POSE_DOUBLES;
@@ -659,7 +659,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_det_thr_acc, sizeof(uint32_t) * (size_t)C * L);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_state, sizeof(double) * 16 * (size_t)P);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_ransac, sizeof(uint32_t) * TS_RANSAC_WORDS * TS_MAX_SPLITS * (size_t)B * P);
-    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_hyp, sizeof(double) * 12 * 4 * (size_t)p.ransac_hypotheses * B * P);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_hyp, sizeof(double) * TS_HYP_DOUBLES * 4 * (size_t)p.ransac_hypotheses * B * P);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_brief, sizeof(TSLAM_BRIEF_TABLE));
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_wedges, sizeof(TSLAM_WEDGES));
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_maps, sizeof(int32_t) * (size_t)C * W * H * 2);
@@ -1472,7 +1472,7 @@ static int ensure_reloc_scratch(tslam_handle* h) {
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_stats, sizeof(int32_t) * TS_STATS_INTS);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_pose, sizeof(double) * TS_POSE_DOUBLES);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_ransac, sizeof(uint32_t) * TS_RANSAC_WORDS * TS_MAX_SPLITS);
-    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_hyp, sizeof(double) * 12 * 4 * (size_t)h->prm.ransac_hypotheses);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_hyp, sizeof(double) * TS_HYP_DOUBLES * 4 * (size_t)h->prm.ransac_hypotheses);
     return rc;
 }
 

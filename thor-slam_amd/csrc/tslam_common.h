@@ -39,6 +39,9 @@
 #define TS_STATS_INTS 8
 #define TS_CORR_DOUBLES 8
 #define TS_MAX_HYP 1024
+// one P3P candidate pose: [R 9 | t 3] f64, then f32 R 9, t 3, max |R_ij|, max |t_i| and 2 pad
+// (the scoring pass reads the f32 record through scalar loads as operands of its inlier test)
+#define TS_HYP_DOUBLES 20
 #define TS_MAX_SPLITS 32   // RANSAC blocks per frame
 #define TS_RANSAC_WORDS 26 // per split: key + pad + 12 doubles
 #define TS_PRIOR_DOUBLES 16 // per (frame, pair): IMU prior R (row-major 3x3), W_r, t[3], W_t, 0, 0
@@ -129,7 +132,7 @@ struct BatchCtx {
     double* corr;
     double* pose;
     double* ransac;        // [B][P][TS_MAX_SPLITS][13] split winners (key word + pose)
-    double* hyp;           // [B][P][4 * n_hyp][12] P3P candidate poses (k_p3p -> k_ransac)
+    double* hyp;           // [B][P][4 * n_hyp][TS_HYP_DOUBLES] P3P candidate poses (k_p3p -> k_ransac)
     int32_t* stats;
     double* state;
     const double* prior;   // [B][P][16] IMU prior of the batch (tslam_set_motion_prior) or null
