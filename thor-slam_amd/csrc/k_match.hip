@@ -3,33 +3,38 @@
 // and the integer-SAD sub-pixel refinements (A6b stereo disparity, A7a temporal position).
 // Bit-exact with oracle.match / oracle.stereo_subpixel / oracle.temporal_subpixel.
 //
-// k_match: one thread per query, 256 queries per block, 4 waves.  Temporal blocks re-deal their
-// 256 y-sorted queries by x (one rank sort in LDS, the only block barrier), so each wave holds an
-// x-quartile: its queries' gate box then admits about half of the train columns, and each 64-train
-// tile is compacted by a ballot of the box test before any Hamming work (stereo blocks keep the
-// y order: their row band is what limits them).
-// The train side of a pair is wave-uniform, so its record and descriptor come through SCALAR
-// loads (constant address space, s_load_dwordx4/x8 into SGPRs, served by the scalar cache) and
-// feed the VALU as SGPR operands: each pair costs 8 v_xor + 8 v_bcnt and a few compares, with no
-// LDS read (an LDS broadcast of a 32-byte descriptor still returns 2 KiB per wave at 128 B/clk).
-// The train side's best query (for the mutual check) comes from a per-wave distance tile read
-// transposed (lane = train) and one global atomicMin per train descriptor per wave tile: min is
-// order-independent, so the result is deterministic.
+// k_match: the Hamming distances come from the matrix cores.  A block holds 128 y-sorted queries
+// of one level, one 32-query MFMA row tile per wave (temporal blocks first re-deal their queries
+// by x, so each wave holds an x-quartile and its column box admits about half of the trains).
+// Each wave walks the train rows its queries can reach in chunks of 64 y-sorted positions,
+// compacts the trains inside its column box into an LDS ring (ballot + mbcnt), and scores every
+// full ring tile of 32 trains with four FP4 block-scaled MFMAs:
+//   Hamming(q, t) = |q| + sum_k (1 - 2 q_k) t_k
+// The query side is +-1 (e2m1 0b0010 / 0b1010), the train side the descriptor bits in place
+// (w & (0x11111111 << s): fp4 0.5 / 1 / 2, step 3 shifted to 2), undone by the E8M0 block scales
+// 2 / 1 / 0.5 / 0.5, and C starts at |q| of the row — every partial sum is a small integer, so
+// the f32 result is the exact distance (tools/mfma_hamming_probe.hip checks the encoding).
+// One tile costs 4 MFMAs + ~20 VALU of bit unpacking per lane where the VALU kernel spent 16
+// v_xor/v_bcnt per lane and pair; the remaining per-pair VALU is the geometric gate and the
+// best / second / mutual bookkeeping (9 ops).
+//
+// Keys.  A non-negative integer-valued f32 orders like its bits and leaves the low 15 mantissa
+// bits zero, so (distance, index) keys are bits(H) | index (index < 8192): the query side's best
+// is a v_min, its second a v_med3; an ineligible pair gets +inf bits (0x7F800000), above every
+// eligible key.  The train side's (distance, query) minimum for the mutual check uses the wave
+// slot (0..31) as the index: a wave's queries take their slots in keypoint-index order, so slot
+// order is query order.  Slot 2 * reg + h is MFMA row (reg & 3) + 8 (reg >> 2) + 4 h, i.e. the
+// row accumulator register reg of lane half h holds, so the slot's low bit is the lane half (ORed
+// in after the register minimum).  One global atomicMin per train and wave tile publishes it
+// in the (distance << 16 | query) format the refinement kernels read.
 #include "tslam_common.h"
 
-// Distances enter the mutual check as bytes: the train side's best query only matters when its
-// distance is <= the query's best <= max_hamming <= 253 (validated), so min(d, 254) keeps every
-// decision exact; 255 marks "not eligible".  Rows padded to 68 B for conflict-free transposed
-// reads.  LDS 18 KiB per block.
-#define TS_TILE_PITCH 68
+#define TS_MQ 128          // queries per k_match block (4 waves x one 32-row MFMA tile)
+#define TS_MRED_PITCH 33   // (best, second) rows of the final per-slot reduction, padded
 
-// popcount(x) + acc as one v_bcnt_u32_b32 (the compiler would re-associate a chain of
-// __popc(x) + acc into bcnt + v_add3 trees)
-__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
-    uint32_t r;
-    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
-    return r;
-}
+typedef int v8i_t __attribute__((ext_vector_type(8)));
+typedef float v16f_t __attribute__((ext_vector_type(16)));
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
     uint32_t r;
@@ -37,11 +42,27 @@ __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c)
     return r;
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_match(BatchCtx c) {
-    __shared__ uint8_t s_tile[4][64][TS_TILE_PITCH];   // per wave: min(distance, 254)[train jj][query lane]
-    __shared__ __attribute__((aligned(16))) uint32_t s_qi[4][64];
-    __shared__ uint32_t s_tr[4][64];    // per wave: the compacted tile's train keypoint indices
-    __shared__ uint32_t s_key[256];     // temporal: (x, slot) sort keys, then the dealt positions
+// the geometric gate of one (query row, train column) pair: both 16-bit halves of
+// (query gate word - train xy) within the spans (v_pk_sub_u16, v_pk_min_u16, v_cmp)
+__device__ __forceinline__ bool gate_ok(uint32_t qgate, uint32_t txy, uint32_t span) {
+    const u16x2_t d = __builtin_bit_cast(u16x2_t, qgate) - __builtin_bit_cast(u16x2_t, txy);
+    const u16x2_t m = __builtin_elementwise_min(d, __builtin_bit_cast(u16x2_t, span));
+    return __builtin_bit_cast(uint32_t, m) == __builtin_bit_cast(uint32_t, d);
+}
+
+__device__ __forceinline__ uint32_t key_dist(uint32_t key) {   // distance of a finite key
+    return (uint32_t)__uint_as_float(key & 0xFFFF8000u);
+}
+
+__global__ __launch_bounds__(256) void k_match(BatchCtx c) {
+    // per wave: the compacted-train ring during the walk, then the (best, second) reduction
+    __shared__ __attribute__((aligned(16))) uint2 s_red[4][32 * TS_MRED_PITCH];
+    __shared__ __attribute__((aligned(16))) uint32_t s_key[2][TS_MQ];  // temporal: (x, thread) sort keys, then the dealt positions
+    __shared__ __attribute__((aligned(16))) uint32_t s_wk[4][32];   // per wave: query-index sort keys
+    __shared__ uint32_t s_sq[4][32];      // per wave slot: query keypoint index (~0: empty slot)
+    __shared__ uint32_t s_sp[4][32];      // ... its y-sorted position
+    __shared__ uint32_t s_sg[4][32];      // ... gate word (qy + gy_tol) << 16 | (qx - gx_lo)
+    __shared__ float s_spc[4][32];        // ... |q| (popcount of the descriptor)
     // blockIdx.y: the temporal blocks (the heavy ones: a window of rows, not a row band) of every
     // frame first, then the stereo blocks, so the short stereo blocks fill the launch's tail
     // (stereo-only launches, match_modes == 1: blockIdx.y = f * P + p, all stereo)
@@ -64,9 +85,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     const int K = c.g.K;
     const int qn = c.kcount[((size_t)slot * c.C + qcam) * c.g.n_levels + l];
     const int tn = c.kcount[((size_t)tslot * c.C + tcam) * c.g.n_levels + l];
-    const int q0 = tile * 256;
+    const int q0 = tile * TS_MQ;
     if (q0 >= qn || tn == 0) return;          // block-uniform
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int ci = lane & 31, h = lane >> 5;  // MFMA column / row index, lane half (k half)
     const size_t qbase = ((size_t)slot * c.C + qcam) * K;
     const size_t tbase = ((size_t)tslot * c.C + tcam) * K;
     const size_t mbase = (((size_t)f * c.P + p) * 2 + mode) * K;
@@ -76,42 +98,69 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     const uint4* tdesc = reinterpret_cast<const uint4*>(c.desc_ys + (tbase + c.g.koff[l]) * 8);
     const uint16_t* trs = c.rowstart + ((size_t)tslot * c.C + tcam) * c.g.rs_total + c.g.rs_off[l];
     const int Hl = c.g.H[l];
+    const int row_tol = c.mp.row_tol, dmax = c.mp.max_disp >> l, win = c.mp.window >> l;
+    // the geometric gate as one box: stereo 1 <= x_q - x_t <= max_disp and |y_q - y_t| <= row_tol;
+    // temporal |x_q - x_t| <= window and |y_q - y_t| <= window
+    const int gx_lo = mode == 0 ? 1 : -win, gx_hi = mode == 0 ? dmax : win, gy_tol = mode == 0 ? row_tol : win;
+    const uint32_t span = (uint32_t)(2 * gy_tol) << 16 | (uint32_t)(gx_hi - gx_lo);
 
-    // queries in y-sorted order: this block holds positions q0 .. q0+255 of the level
-    int qpos = q0 + threadIdx.x;
+    // this wave's 32 queries: positions q0 + 32 wave + i (stereo: y order), or the block's x-ranks
+    // 32 wave .. 32 wave + 31 (temporal)
+    int qpos = q0 + 32 * wave + ci;
     if (mode == 1) {
-        // deal the block's queries by x: thread t takes the query of x-rank t (inactive slots,
-        // keyed past every x, stay last); keys are distinct, so the ranks are a permutation
-        const uint32_t key = qpos < qn ? (uint32_t)(qys[qpos].x & 0xFFFF) << 8 | threadIdx.x
-                                       : 0x1000000u | threadIdx.x;
-        s_key[threadIdx.x] = key;
+        if (threadIdx.x < TS_MQ) {
+            const int pos = q0 + (int)threadIdx.x;
+            s_key[0][threadIdx.x] = pos < qn ? (uint32_t)(qys[pos].x & 0xFFFF) << 8 | threadIdx.x : 0x1000000u | threadIdx.x;
+        }
         __syncthreads();
-        int rank = 0;
-        const uint4* k4 = reinterpret_cast<const uint4*>(s_key);
+        if (threadIdx.x < TS_MQ) {
+            const uint32_t key = s_key[0][threadIdx.x];
+            int rank = 0;
+            const uint4* k4 = reinterpret_cast<const uint4*>(s_key[0]);
 #pragma unroll 4
-        for (int i = 0; i < 64; ++i) {
+            for (int i = 0; i < TS_MQ / 4; ++i) {
+                const uint4 v = k4[i];
+                rank += (v.x < key) + (v.y < key) + (v.z < key) + (v.w < key);
+            }
+            s_key[1][rank] = (uint32_t)(q0 + (int)threadIdx.x);   // keys are distinct: a permutation
+        }
+        __syncthreads();
+        qpos = (int)s_key[1][32 * wave + ci];
+    }
+    const bool active = qpos < qn;
+    int qx = 0, qy = 0;
+    uint32_t qi = 0, pc = 0;
+    if (active) {
+        const uint4 rec = qys[qpos];
+        const uint4 d = qdesc[2 * qpos + h];
+        qi = rec.z;
+        qx = rec.x & 0xFFFF;
+        qy = rec.x >> 16;
+        pc = __popc(d.x) + __popc(d.y) + __popc(d.z) + __popc(d.w);
+    }
+    pc += (uint32_t)__shfl_xor((int)pc, 32, 64);
+    // slots in query-index order (the mutual check's tie-break): rank among the wave's 32
+    if (h == 0) s_wk[wave][ci] = active ? qi : 0x10000u | (uint32_t)ci;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    {
+        const uint32_t key = active ? qi : 0x10000u | (uint32_t)ci;
+        int rank = 0;
+        const uint4* k4 = reinterpret_cast<const uint4*>(s_wk[wave]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
             const uint4 v = k4[i];
             rank += (v.x < key) + (v.y < key) + (v.z < key) + (v.w < key);
         }
-        __syncthreads();
-        s_key[rank] = (uint32_t)qpos;
-        __syncthreads();
-        qpos = (int)s_key[threadIdx.x];
+        if (h == 0) {
+            s_sq[wave][rank] = active ? qi : 0xFFFFFFFFu;
+            s_sp[wave][rank] = (uint32_t)qpos;
+            // inactive: 0xFFFF halves fail every gate
+            s_sg[wave][rank] = active ? ((uint32_t)(qy + gy_tol) << 16 | ((uint32_t)(qx - gx_lo) & 0xFFFFu)) : 0xFFFFFFFFu;
+            s_spc[wave][rank] = (float)pc;
+        }
     }
-    const bool active = qpos < qn;
-    uint32_t q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    int qx = 0, qy = 0, qi = 0;
-    if (active) {
-        const uint4 rec = qys[qpos];
-        const uint4 a = qdesc[2 * qpos], b = qdesc[2 * qpos + 1];
-        q[0] = a.x; q[1] = a.y; q[2] = a.z; q[3] = a.w; q[4] = b.x; q[5] = b.y; q[6] = b.z; q[7] = b.w;
-        qi = (int)rec.z;
-        qx = rec.x & 0xFFFF;
-        qy = rec.x >> 16;
-    }
-    s_qi[wave][lane] = (uint32_t)qi;
-    const int row_tol = c.mp.row_tol, dmax = c.mp.max_disp >> l, win = c.mp.window >> l;
-    const int reach = mode == 0 ? row_tol : win;
     // the box of this wave's queries: rows any of them can match (the train range) and columns
     int wy0, wy1, wx0, wx1;
     {
@@ -129,103 +178,125 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
         wx0 = __builtin_amdgcn_readfirstlane(ax);
         wx1 = __builtin_amdgcn_readfirstlane(bx);
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const bool wave_active = wy1 >= 0;
+    const int reach = mode == 0 ? row_tol : win;
     const int wt0 = wave_active ? (int)trs[max(0, wy0 - reach)] : 0;
     int wt1 = wave_active ? (int)trs[min(Hl - 1, wy1 + reach) + 1] : 0;
-
-    // (distance << 16 | train index) keys: the lexicographic (distance, index) minimum is one
-    // v_min_u32, and the second-best distance is the minimum over every key but the best one,
-    // min(second, max(best, key)) (keys are distinct: train indices are) — the oracle's rule
-    uint32_t best_key = 0xFFFFFFFFu, second_key = 0xFFFFFFFFu;
-    // the geometric gate as one box, branch-free: stereo 1 <= x_q - x_t <= max_disp and
-    // |y_q - y_t| <= row_tol; temporal |x_q - x_t| <= window and |y_q - y_t| <= window
-    const int gx_lo = mode == 0 ? 1 : -win, gx_hi = mode == 0 ? dmax : win, gy_tol = mode == 0 ? row_tol : win;
-    const uint32_t gx_span = (uint32_t)(gx_hi - gx_lo), gy_span = (uint32_t)(2 * gy_tol);
+    if (gx_hi < gx_lo) wt1 = wt0;   // empty disparity range at this level: nothing is eligible
     // a train column some query of the wave can reach: qx - tx in [gx_lo, gx_hi] for a wave qx
     const uint32_t bx0 = (uint32_t)(wx0 - gx_hi), bx_span = (uint32_t)(wx1 - gx_lo - (wx0 - gx_hi));
-    if (!active) qx = -(1 << 24);   // an inactive lane fails the x range test
-    if (gx_hi < gx_lo) wt1 = wt0;   // empty disparity range at this level: nothing is eligible
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    typedef const __attribute__((address_space(4))) v4u cv4u;       // uniform address -> s_load
-    cv4u* ctys = (cv4u*)(uintptr_t)tys;
-    cv4u* ctdesc = (cv4u*)(uintptr_t)tdesc;
-    // The 4 waves are independent (no block barrier): each walks its own train range in tiles of
-    // 64 and publishes each train descriptor's best query with one global atomicMin per tile
-    // (min is order-independent, so the result is deterministic).
+
+    // A operand (rows = slots): lane (row ci, half h) holds, for MFMA step s, bit s of every nibble
+    // of descriptor words 4h .. 4h+3 of the query in slot(ci), as +-1
+    uint32_t qa[4][4];
+    {
+        const int srow = 2 * ((ci & 3) + 4 * (ci >> 3)) + ((ci >> 2) & 1);
+        uint4 d = {0u, 0u, 0u, 0u};
+        if (s_sq[wave][srow] != 0xFFFFFFFFu) d = qdesc[2 * (int)s_sp[wave][srow] + h];
+        const uint32_t w4[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) qa[s][j] = 0x22222222u | (((w4[j] >> s) & 0x11111111u) << 3);
+    }
+    // per accumulator register: the slot's |q| (the MFMA's C) and gate word
+    v16f_t cinit;
+    uint32_t qgate[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        cinit[r] = s_spc[wave][2 * r + h];
+        qgate[r] = s_sg[wave][2 * r + h];
+    }
+    uint32_t best[16], second[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) best[r] = second[r] = 0xFFFFFFFFu;
+
+    uint2* ring = s_red[wave];   // 128 entries {txy, tidx << 16 | position}
+    uint32_t head = 0, tail = 0;
+    // one 32-train tile from the ring (cnt <= 32 columns valid)
+    auto score_tile = [&](uint32_t cnt) {
+        const bool colv = (uint32_t)ci < cnt;
+        const uint2 e = colv ? ring[(head + ci) & 127] : uint2{0x80008000u, 0u};   // padding fails every gate
+        const uint32_t txy = e.x, tidx = e.y >> 16;
+        uint4 d = {0u, 0u, 0u, 0u};
+        if (colv) d = tdesc[2 * (int)(e.y & 0xFFFFu) + h];
+        const uint32_t w4[4] = {d.x, d.y, d.z, d.w};
+        v16f_t acc = cinit;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            v8i_t a, b;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                a[j] = (int)qa[s][j];
+                b[j] = (int)(s < 3 ? (w4[j] & (0x11111111u << s)) : ((w4[j] >> 1) & 0x44444444u));
+                a[j + 4] = 0;
+                b[j + 4] = 0;
+            }
+            acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 4, 4, 0, 127, 0, s == 0 ? 128 : s == 1 ? 127 : 126);
+        }
+        uint32_t tmin = 0xFFFFFFFFu;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t hb = gate_ok(qgate[r], txy, span) ? __float_as_uint(acc[r]) : 0x7F800000u;
+            const uint32_t key = hb | tidx;
+            second[r] = med3_u32(best[r], second[r], key);   // = min(second, max(best, key)): best <= second
+            best[r] = min(best[r], key);
+            tmin = min(tmin, hb | (uint32_t)(2 * r));
+        }
+        tmin |= (uint32_t)h;
+        tmin = min(tmin, (uint32_t)__shfl_xor((int)tmin, 32, 64));
+        if (h == 0 && colv && tmin < 0x7F800000u)
+            atomicMin(&c.tbest[mbase + tidx], key_dist(tmin & ~31u) << 16 | s_sq[wave][tmin & 31u]);
+        head += 32;
+    };
     for (int jt = wt0; jt < wt1; jt += 64) {
-        // compaction: the tile's trains inside the wave's column box, in index order
+        // compaction: the chunk's trains inside the wave's column box, in position order
         bool inbox = false;
-        uint32_t tz = 0;
+        uint2 e = {0u, 0u};
         if (jt + lane < wt1) {
             const uint4 r = tys[jt + lane];
             inbox = (uint32_t)((int)(r.x & 0xFFFF) - (int)bx0) <= bx_span;
-            tz = r.z;
+            e = uint2{r.x, r.z << 16 | (uint32_t)(jt + lane)};
         }
-        uint64_t tm = __ballot(inbox);
-        if (tm == 0) continue;
-        const int jcount = __popcll(tm);
-        if (inbox) s_tr[wave][__builtin_amdgcn_mbcnt_hi((uint32_t)(tm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)tm, 0u))] = tz;
-        const int jlast = jt + 63 - __builtin_clzll(tm);
-        // phase 1: this lane's query against the compacted trains, each a wave-uniform record +
-        // descriptor in SGPRs (index from the mask's lowest set bit); unrolled by 8 so 8
-        // descriptors' scalar loads are in flight together
-        for (int jj0 = 0; jj0 < jcount; jj0 += 8) {
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int jj = jj0 + u;
-                const int j = tm ? jt + __builtin_ctzll(tm) : jlast;
-                tm &= tm - 1;
-                const v4u rec = ctys[j];
-                const v4u a = ctdesc[2 * j], b = ctdesc[2 * j + 1];
-                // gate as two unsigned range tests (one v_sub + one v_cmp each; the train's
-                // offsets are scalar): gx_lo <= qx - tx <= gx_hi, -gy_tol <= qy - ty <= gy_tol
-                const int tx = rec.x & 0xFFFF, ty = rec.x >> 16;
-                const bool elig = (uint32_t)(qx - (tx + gx_lo)) <= gx_span && (uint32_t)(qy - (ty - gy_tol)) <= gy_span &&
-                                  jj < jcount;
-                uint32_t dd = __popc(q[0] ^ a.x);   // v_bcnt accumulate chain (8 v_xor + 8 v_bcnt)
-                dd = bcnt_acc(q[1] ^ a.y, dd);
-                dd = bcnt_acc(q[2] ^ a.z, dd);
-                dd = bcnt_acc(q[3] ^ a.w, dd);
-                dd = bcnt_acc(q[4] ^ b.x, dd);
-                dd = bcnt_acc(q[5] ^ b.y, dd);
-                dd = bcnt_acc(q[6] ^ b.z, dd);
-                dd = bcnt_acc(q[7] ^ b.w, dd);
-                const uint32_t key = elig ? ((dd << 16) | rec.z) : 0xFFFFFFFFu;
-                second_key = med3_u32(best_key, second_key, key);   // = min(second, max(best, key)): best <= second
-                best_key = min(best_key, key);
-                s_tile[wave][jj][lane] = (uint8_t)(elig ? min(dd, 254u) : 255u);
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint64_t m = __ballot(inbox);
+        if (inbox) ring[(tail + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))) & 127] = e;
+        tail += (uint32_t)__popcll(m);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        // phase 2: transposed read, lane = compacted train: (distance, query) minimum over
-        // the wave's 64 queries, 4 queries per dword read (row pitch 68 B = 17 dwords, an
-        // odd stride, so the 64 lanes hit 64 different banks), no cross-lane reduction
-        if (lane < jcount) {
-            const uint32_t my_train = s_tr[wave][lane];
-            // an ineligible pair's key (255 << 16 | query) exceeds every eligible one (distance
-            // <= 254), so a plain minimum is exact and "no eligible query" is best >= 255 << 16
-            uint32_t best = 0xFFFFFFFFu;
-            const uint32_t* row = reinterpret_cast<const uint32_t*>(&s_tile[wave][lane][0]);
-            const uint4* qi4 = reinterpret_cast<const uint4*>(&s_qi[wave][0]);
-#pragma unroll 2
-            for (int r4 = 0; r4 < 16; ++r4) {
-                const uint32_t d4 = row[r4];
-                const uint4 qq = qi4[r4];
-                best = min(best, __builtin_amdgcn_ubfe(d4, 0, 8) << 16 | qq.x);
-                best = min(best, __builtin_amdgcn_ubfe(d4, 8, 8) << 16 | qq.y);
-                best = min(best, __builtin_amdgcn_ubfe(d4, 16, 8) << 16 | qq.z);
-                best = min(best, (d4 >> 24) << 16 | qq.w);
-            }
-            if (best < (255u << 16)) atomicMin(&c.tbest[mbase + my_train], best);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        while (tail - head >= 32) score_tile(32);
     }
-    if (active) {
-        const int qk = (int)s_qi[wave][lane];   // re-read: one VGPR less through the train loop
-        c.qbest[mbase + qk] = best_key;
-        c.qsecond[mbase + qk] = second_key == 0xFFFFFFFFu ? 256u : (second_key >> 16);
+    if (tail != head) score_tile(tail - head);
+
+    // per slot: merge the 32 columns' (best, second) — best = min, second = min(s1, s2, max(b1, b2))
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint2* red = s_red[wave];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[(2 * r + h) * TS_MRED_PITCH + ci] = uint2{best[r], second[r]};
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t b = 0xFFFFFFFFu, s2 = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint2 v = red[ci * TS_MRED_PITCH + 16 * h + i];
+        s2 = min(min(s2, v.y), max(b, v.x));
+        b = min(b, v.x);
+    }
+    {
+        const uint32_t ob = (uint32_t)__shfl_xor((int)b, 32, 64), os = (uint32_t)__shfl_xor((int)s2, 32, 64);
+        s2 = min(min(s2, os), max(b, ob));
+        b = min(b, ob);
+    }
+    const uint32_t qk = s_sq[wave][ci];
+    if (h == 0 && qk != 0xFFFFFFFFu) {
+        c.qbest[mbase + qk] = b < 0x7F800000u ? key_dist(b) << 16 | (b & 0x7FFFu) : 0xFFFFFFFFu;
+        c.qsecond[mbase + qk] = s2 < 0x7F800000u ? key_dist(s2) : 256u;
     }
 }
 

@@ -252,7 +252,7 @@ static void build_geometry(tslam_handle* h) {
         g.dt_nx[l] = (g.W[l] + TS_DT_W - 1) / TS_DT_W;
         g.dt_start[l] = g.dt_total;
         g.dt_total += g.dt_nx[l] * ((g.H[l] + TS_DT_H - 1) / TS_DT_H);
-        g.qtiles[l] = (g.Kq[l] + 255) / 256;
+        g.qtiles[l] = (g.Kq[l] + 127) / 128;   // k_match: TS_MQ queries per block
         g.qtile_start[l] = qs;
         qs += g.qtiles[l];
     }
@@ -572,6 +572,10 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     if (p.fast_threshold < 0 || p.fast_threshold > 254) return fail(TSLAM_EINVAL, "fast_threshold must be in [0, 254]");
     if (p.max_batch < 1) return fail(TSLAM_EINVAL, "max_batch must be >= 1");
     if (p.max_hamming < 0 || p.max_hamming > 253) return fail(TSLAM_EINVAL, "max_hamming must be in [0, 253]");
+    // k_match packs the gate offsets into 16-bit halves (query xy + window < 2^15)
+    if (p.stereo_row_tol < 0 || p.stereo_row_tol > 2047 || p.max_disparity < 0 || p.max_disparity > 2047 ||
+        p.temporal_window < 0 || p.temporal_window > 2047)
+        return fail(TSLAM_EINVAL, "stereo_row_tol, max_disparity, temporal_window must be in [0, 2047]");
     if (!(p.ba_window == 0 || (p.ba_window >= 2 && p.ba_window <= TS_BA_MAXW)))
         return fail(TSLAM_EINVAL, "ba_window must be 0 (off) or in [2, 10]");
     if (p.ba_window && (p.ba_kf_interval < 1 || p.ba_iters < 1 || !(p.ba_lambda >= 0.0) || !(p.ba_outlier_px > 0.0)))

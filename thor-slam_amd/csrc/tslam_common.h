@@ -62,7 +62,7 @@ struct LevelGeom {
     int cand_cap[TS_MAX_LEVELS];   // keys per band at level l
     int cand_off[TS_MAX_LEVELS];   // u32 offset of level l's first band segment (per image)
     int cand_total;                // u32 per image
-    int qtiles[TS_MAX_LEVELS], qtile_start[TS_MAX_LEVELS];  // 256-query tiles per level
+    int qtiles[TS_MAX_LEVELS], qtile_start[TS_MAX_LEVELS];  // 128-query k_match tiles per level
     int total_qtiles;
     int rs_off[TS_MAX_LEVELS];     // u16 offset of level l's row-start table (H_l + 1 entries)
     int rs_total;                  // u16 per image
