@@ -31,6 +31,7 @@
 
 #define TS_MQ 128          // queries per k_match block (4 waves x one 32-row MFMA tile)
 #define TS_MRED_PITCH 33   // (best, second) rows of the final per-slot reduction, padded
+#define TS_MRING 1024      // compacted trains per walk round (the ring shares the reduction's LDS)
 
 typedef int v8i_t __attribute__((ext_vector_type(8)));
 typedef float v16f_t __attribute__((ext_vector_type(16)));
@@ -214,15 +215,16 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) best[r] = second[r] = 0xFFFFFFFFu;
 
-    uint2* ring = s_red[wave];   // 128 entries {txy, tidx << 16 | position}
-    uint32_t head = 0, tail = 0;
-    // one 32-train tile from the ring (cnt <= 32 columns valid)
-    auto score_tile = [&](uint32_t cnt) {
-        const bool colv = (uint32_t)ci < cnt;
-        const uint2 e = colv ? ring[(head + ci) & 127] : uint2{0x80008000u, 0u};   // padding fails every gate
-        const uint32_t txy = e.x, tidx = e.y >> 16;
-        uint4 d = {0u, 0u, 0u, 0u};
-        if (colv) d = tdesc[2 * (int)(e.y & 0xFFFFu) + h];
+    // The walk in rounds: compact the trains inside the wave's column box into the ring (chunks of
+    // 64 y-sorted positions, four chunks' record loads in flight at a time) until it holds
+    // TS_MRING - 256 or more (every round but a rare last one: all of them), then score the ring's
+    // 32-train tiles, two per loop trip, each tile's entries and descriptors loaded one tile ahead.
+    // Every load is unconditional (indices clamped into the ring; a padding column only gets the
+    // gate-failing xy) and the train-side minima go back into the ring entries (the flush's global
+    // atomics come after the round's last tile), so the loop body is straight-line code whose
+    // vmcnt waits cover exactly the tile being scored.
+    uint2* ring = s_red[wave];   // {txy, tidx << 16 | position}; after scoring {tmin, ...}
+    auto score = [&](const uint4& d, const uint2& e, uint32_t k, uint32_t n) {
         const uint32_t w4[4] = {d.x, d.y, d.z, d.w};
         v16f_t acc = cinit;
 #pragma unroll
@@ -237,6 +239,8 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
             }
             acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 4, 4, 0, 127, 0, s == 0 ? 128 : s == 1 ? 127 : 126);
         }
+        const uint32_t txy = k < n ? e.x : 0x80008000u;   // padding fails every gate
+        const uint32_t tidx = e.y >> 16;
         uint32_t tmin = 0xFFFFFFFFu;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -248,28 +252,56 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
         }
         tmin |= (uint32_t)h;
         tmin = min(tmin, (uint32_t)__shfl_xor((int)tmin, 32, 64));
-        if (h == 0 && colv && tmin < 0x7F800000u)
-            atomicMin(&c.tbest[mbase + tidx], key_dist(tmin & ~31u) << 16 | s_sq[wave][tmin & 31u]);
-        head += 32;
+        if (h == 0 && k < n) ring[k].x = tmin;
     };
-    for (int jt = wt0; jt < wt1; jt += 64) {
-        // compaction: the chunk's trains inside the wave's column box, in position order
-        bool inbox = false;
-        uint2 e = {0u, 0u};
-        if (jt + lane < wt1) {
-            const uint4 r = tys[jt + lane];
-            inbox = (uint32_t)((int)(r.x & 0xFFFF) - (int)bx0) <= bx_span;
-            e = uint2{r.x, r.z << 16 | (uint32_t)(jt + lane)};
+    for (int jt = wt0; jt < wt1;) {
+        uint32_t n = 0;
+        for (; jt < wt1 && n <= TS_MRING - 256; jt += 256) {
+            uint4 r4[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) r4[u] = tys[min(jt + 64 * u + lane, wt1 - 1)];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int j = jt + 64 * u + lane;
+                const bool inbox = j < wt1 && (uint32_t)((int)(r4[u].x & 0xFFFF) - (int)bx0) <= bx_span;
+                const uint64_t m = __ballot(inbox);
+                if (inbox)
+                    ring[n + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+                        uint2{r4[u].x, r4[u].z << 16 | (uint32_t)j};
+                n += (uint32_t)__popcll(m);
+            }
         }
-        const uint64_t m = __ballot(inbox);
-        if (inbox) ring[(tail + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))) & 127] = e;
-        tail += (uint32_t)__popcll(m);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        while (tail - head >= 32) score_tile(32);
+        if (n > 0) {
+            const uint32_t last = n - 1;
+            uint32_t k0 = (uint32_t)ci, k1 = 32u + (uint32_t)ci;
+            uint2 e0 = ring[min(k0, last)], e1 = ring[min(k1, last)];
+            uint4 d0 = tdesc[2 * (int)(e0.y & 0xFFFFu) + h], d1 = tdesc[2 * (int)(e1.y & 0xFFFFu) + h];
+            for (uint32_t t = 0; 32u * t < n; t += 2) {
+                score(d0, e0, k0, n);
+                k0 += 64u;
+                e0 = ring[min(k0, last)];
+                d0 = tdesc[2 * (int)(e0.y & 0xFFFFu) + h];
+                if (32u * (t + 1) < n) score(d1, e1, k1, n);
+                k1 += 64u;
+                e1 = ring[min(k1, last)];
+                d1 = tdesc[2 * (int)(e1.y & 0xFFFFu) + h];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // flush: each train's (distance, query) minimum over the wave's queries
+            for (uint32_t k = (uint32_t)lane; k < n; k += 64) {
+                const uint2 e = ring[k];
+                if (e.x < 0x7F800000u) atomicMin(&c.tbest[mbase + (e.y >> 16)], key_dist(e.x & ~31u) << 16 | s_sq[wave][e.x & 31u]);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the ring is refilled by the next round
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (tail != head) score_tile(tail - head);
 
     // per slot: merge the 32 columns' (best, second) — best = min, second = min(s1, s2, max(b1, b2))
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
