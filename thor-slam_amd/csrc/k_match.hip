@@ -32,6 +32,7 @@
 #define TS_MQ 128          // queries per k_match block (4 waves x one 32-row MFMA tile)
 #define TS_MRED_PITCH 33   // (best, second) rows of the final per-slot reduction, padded
 #define TS_MRING 1024      // compacted trains per walk round (the ring shares the reduction's LDS)
+#define TS_MCHUNKS 6       // 64-position chunks whose record loads are in flight together
 
 typedef int v8i_t __attribute__((ext_vector_type(8)));
 typedef float v16f_t __attribute__((ext_vector_type(16)));
@@ -60,8 +61,10 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     __shared__ __attribute__((aligned(16))) uint2 s_red[4][32 * TS_MRED_PITCH];
     __shared__ __attribute__((aligned(16))) uint32_t s_key[2][TS_MQ];  // temporal: (x, thread) sort keys, then the dealt positions
     __shared__ __attribute__((aligned(16))) uint32_t s_wk[4][32];   // per wave: query-index sort keys
+    __shared__ uint4 s_qrec[TS_MQ];       // the block's query records and descriptors (one load round)
+    __shared__ uint4 s_qdesc[2 * TS_MQ];
     __shared__ uint32_t s_sq[4][32];      // per wave slot: query keypoint index (~0: empty slot)
-    __shared__ uint32_t s_sp[4][32];      // ... its y-sorted position
+    __shared__ uint32_t s_si[4][32];      // ... its block-local index
     __shared__ uint32_t s_sg[4][32];      // ... gate word (qy + gy_tol) << 16 | (qx - gx_lo)
     __shared__ float s_spc[4][32];        // ... |q| (popcount of the descriptor)
     // blockIdx.y: the temporal blocks (the heavy ones: a window of rows, not a row band) of every
@@ -105,13 +108,36 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     const int gx_lo = mode == 0 ? 1 : -win, gx_hi = mode == 0 ? dmax : win, gy_tol = mode == 0 ? row_tol : win;
     const uint32_t span = (uint32_t)(2 * gy_tol) << 16 | (uint32_t)(gx_hi - gx_lo);
 
-    // this wave's 32 queries: positions q0 + 32 wave + i (stereo: y order), or the block's x-ranks
-    // 32 wave .. 32 wave + 31 (temporal)
-    int qpos = q0 + 32 * wave + ci;
+    // The block's 128 query records and descriptors land in LDS in one round of global loads, so
+    // every later setup step reads LDS; the records are y-sorted, so each wave's train rows (and
+    // the row-start loads for them) are known at once.
+    const int nq = min(TS_MQ, qn - q0);
+    {
+        const int t = threadIdx.x & (TS_MQ - 1), half = threadIdx.x >> 7;
+        const int pos = q0 + min(t, nq - 1);   // past nq: a clamped duplicate, never active
+        if (half == 0) s_qrec[t] = qys[pos];
+        s_qdesc[2 * t + half] = qdesc[2 * pos + half];
+    }
+    __syncthreads();
+    // this wave's 32 queries (block-local indices): 32 wave + i (stereo: y order), or the block's
+    // x-ranks 32 wave .. 32 wave + 31 (temporal); active ones come first in either order
+    const bool wave_active = 32 * wave < nq;
+    const int reach = mode == 0 ? row_tol : win;
+    int wt0 = 0, wt1 = 0;
+    {
+        // train rows: the wave's own (stereo) or the block's (temporal: an x-quartile spans them)
+        const int i0 = mode == 1 ? 0 : min(32 * wave, nq - 1), i1 = mode == 1 ? nq - 1 : min(32 * wave + 31, nq - 1);
+        const int wy0 = (int)(s_qrec[i0].x >> 16), wy1 = (int)(s_qrec[i1].x >> 16);
+        if (wave_active) {
+            wt0 = (int)trs[max(0, wy0 - reach)];
+            wt1 = (int)trs[min(Hl - 1, wy1 + reach) + 1];
+        }
+    }
+    int bi = 32 * wave + ci;
     if (mode == 1) {
         if (threadIdx.x < TS_MQ) {
-            const int pos = q0 + (int)threadIdx.x;
-            s_key[0][threadIdx.x] = pos < qn ? (uint32_t)(qys[pos].x & 0xFFFF) << 8 | threadIdx.x : 0x1000000u | threadIdx.x;
+            const int t = threadIdx.x;
+            s_key[0][t] = t < nq ? (s_qrec[t].x & 0xFFFF) << 8 | (uint32_t)t : 0x1000000u | (uint32_t)t;
         }
         __syncthreads();
         if (threadIdx.x < TS_MQ) {
@@ -123,17 +149,17 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
                 const uint4 v = k4[i];
                 rank += (v.x < key) + (v.y < key) + (v.z < key) + (v.w < key);
             }
-            s_key[1][rank] = (uint32_t)(q0 + (int)threadIdx.x);   // keys are distinct: a permutation
+            s_key[1][rank] = threadIdx.x;   // keys are distinct: a permutation
         }
         __syncthreads();
-        qpos = (int)s_key[1][32 * wave + ci];
+        bi = (int)s_key[1][32 * wave + ci];
     }
-    const bool active = qpos < qn;
+    const bool active = bi < nq;
     int qx = 0, qy = 0;
     uint32_t qi = 0, pc = 0;
     if (active) {
-        const uint4 rec = qys[qpos];
-        const uint4 d = qdesc[2 * qpos + h];
+        const uint4 rec = s_qrec[bi];
+        const uint4 d = s_qdesc[2 * bi + h];
         qi = rec.z;
         qx = rec.x & 0xFFFF;
         qy = rec.x >> 16;
@@ -156,36 +182,27 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
         }
         if (h == 0) {
             s_sq[wave][rank] = active ? qi : 0xFFFFFFFFu;
-            s_sp[wave][rank] = (uint32_t)qpos;
+            s_si[wave][rank] = (uint32_t)bi;
             // inactive: 0xFFFF halves fail every gate
             s_sg[wave][rank] = active ? ((uint32_t)(qy + gy_tol) << 16 | ((uint32_t)(qx - gx_lo) & 0xFFFFu)) : 0xFFFFFFFFu;
             s_spc[wave][rank] = (float)pc;
         }
     }
-    // the box of this wave's queries: rows any of them can match (the train range) and columns
-    int wy0, wy1, wx0, wx1;
+    // the columns of this wave's queries
+    int wx0, wx1;
     {
-        int a = active ? qy : (1 << 20), b = active ? qy : -1;
         int ax = active ? qx : (1 << 20), bx = active ? qx : -1;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
-            a = min(a, __shfl_xor(a, o, 64));
-            b = max(b, __shfl_xor(b, o, 64));
             ax = min(ax, __shfl_xor(ax, o, 64));
             bx = max(bx, __shfl_xor(bx, o, 64));
         }
-        wy0 = __builtin_amdgcn_readfirstlane(a);   // equal in every lane: make it provably uniform
-        wy1 = __builtin_amdgcn_readfirstlane(b);
-        wx0 = __builtin_amdgcn_readfirstlane(ax);
+        wx0 = __builtin_amdgcn_readfirstlane(ax);   // equal in every lane: make it provably uniform
         wx1 = __builtin_amdgcn_readfirstlane(bx);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const bool wave_active = wy1 >= 0;
-    const int reach = mode == 0 ? row_tol : win;
-    const int wt0 = wave_active ? (int)trs[max(0, wy0 - reach)] : 0;
-    int wt1 = wave_active ? (int)trs[min(Hl - 1, wy1 + reach) + 1] : 0;
     if (gx_hi < gx_lo) wt1 = wt0;   // empty disparity range at this level: nothing is eligible
     // a train column some query of the wave can reach: qx - tx in [gx_lo, gx_hi] for a wave qx
     const uint32_t bx0 = (uint32_t)(wx0 - gx_hi), bx_span = (uint32_t)(wx1 - gx_lo - (wx0 - gx_hi));
@@ -196,7 +213,7 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     {
         const int srow = 2 * ((ci & 3) + 4 * (ci >> 3)) + ((ci >> 2) & 1);
         uint4 d = {0u, 0u, 0u, 0u};
-        if (s_sq[wave][srow] != 0xFFFFFFFFu) d = qdesc[2 * (int)s_sp[wave][srow] + h];
+        if (s_sq[wave][srow] != 0xFFFFFFFFu) d = s_qdesc[2 * (int)s_si[wave][srow] + h];
         const uint32_t w4[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
         for (int s = 0; s < 4; ++s)
@@ -216,9 +233,10 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     for (int r = 0; r < 16; ++r) best[r] = second[r] = 0xFFFFFFFFu;
 
     // The walk in rounds: compact the trains inside the wave's column box into the ring (chunks of
-    // 64 y-sorted positions, four chunks' record loads in flight at a time) until it holds
-    // TS_MRING - 256 or more (every round but a rare last one: all of them), then score the ring's
-    // 32-train tiles, two per loop trip, each tile's entries and descriptors loaded one tile ahead.
+    // 64 y-sorted positions, TS_MCHUNKS chunks' record loads in flight at a time) until it holds
+    // TS_MRING - 64 TS_MCHUNKS or more (every round but a rare last one: all of them), then score
+    // the ring's 32-train tiles, each tile's entries and descriptors loaded one tile ahead (two
+    // tiles per loop trip measured slower: 173 VGPRs, 2 waves/SIMD).
     // Every load is unconditional (indices clamped into the ring; a padding column only gets the
     // gate-failing xy) and the train-side minima go back into the ring entries (the flush's global
     // atomics come after the round's last tile), so the loop body is straight-line code whose
@@ -256,12 +274,12 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     };
     for (int jt = wt0; jt < wt1;) {
         uint32_t n = 0;
-        for (; jt < wt1 && n <= TS_MRING - 256; jt += 256) {
-            uint4 r4[4];
+        for (; jt < wt1 && n <= TS_MRING - 64 * TS_MCHUNKS; jt += 64 * TS_MCHUNKS) {
+            uint4 r4[TS_MCHUNKS];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) r4[u] = tys[min(jt + 64 * u + lane, wt1 - 1)];
+            for (int u = 0; u < TS_MCHUNKS; ++u) r4[u] = tys[min(jt + 64 * u + lane, wt1 - 1)];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < TS_MCHUNKS; ++u) {
                 const int j = jt + 64 * u + lane;
                 const bool inbox = j < wt1 && (uint32_t)((int)(r4[u].x & 0xFFFF) - (int)bx0) <= bx_span;
                 const uint64_t m = __ballot(inbox);
@@ -276,18 +294,14 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (n > 0) {
             const uint32_t last = n - 1;
-            uint32_t k0 = (uint32_t)ci, k1 = 32u + (uint32_t)ci;
-            uint2 e0 = ring[min(k0, last)], e1 = ring[min(k1, last)];
-            uint4 d0 = tdesc[2 * (int)(e0.y & 0xFFFFu) + h], d1 = tdesc[2 * (int)(e1.y & 0xFFFFu) + h];
-            for (uint32_t t = 0; 32u * t < n; t += 2) {
-                score(d0, e0, k0, n);
-                k0 += 64u;
-                e0 = ring[min(k0, last)];
-                d0 = tdesc[2 * (int)(e0.y & 0xFFFFu) + h];
-                if (32u * (t + 1) < n) score(d1, e1, k1, n);
-                k1 += 64u;
-                e1 = ring[min(k1, last)];
-                d1 = tdesc[2 * (int)(e1.y & 0xFFFFu) + h];
+            uint2 e0 = ring[min((uint32_t)ci, last)];
+            uint4 d0 = tdesc[2 * (int)(e0.y & 0xFFFFu) + h];
+            for (uint32_t k = (uint32_t)ci; k - (uint32_t)ci < n; k += 32u) {
+                const uint2 e1 = ring[min(k + 32u, last)];
+                const uint4 d1 = tdesc[2 * (int)(e1.y & 0xFFFFu) + h];
+                score(d0, e0, k, n);
+                e0 = e1;
+                d0 = d1;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
