@@ -339,10 +339,12 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
         s2 = min(min(s2, os), max(b, ob));
         b = min(b, ob);
     }
+    // stored by the query's y-sorted position (the refinement kernels load them beside its record)
     const uint32_t qk = s_sq[wave][ci];
     if (h == 0 && qk != 0xFFFFFFFFu) {
-        c.qbest[mbase + qk] = b < 0x7F800000u ? key_dist(b) << 16 | (b & 0x7FFFu) : 0xFFFFFFFFu;
-        c.qsecond[mbase + qk] = s2 < 0x7F800000u ? key_dist(s2) : 256u;
+        const size_t qp = mbase + c.g.koff[l] + q0 + s_si[wave][ci];
+        c.qbest[qp] = b < 0x7F800000u ? key_dist(b) << 16 | (b & 0x7FFFu) : 0xFFFFFFFFu;
+        c.qsecond[qp] = s2 < 0x7F800000u ? key_dist(s2) : 256u;
     }
 }
 
@@ -364,15 +366,21 @@ __device__ __forceinline__ void row11(const uint8_t* img, int W, int y, int x0, 
     w[2] = __builtin_amdgcn_alignbyte(d3, d2, sh) & 0x00FFFFFFu;
 }
 
-// Validity of the match of query keypoint qi (max distance, ratio, mutual); returns the train
-// index or -1.
-__device__ __forceinline__ int match_valid(const BatchCtx& c, size_t mbase, int qi) {
-    const uint32_t qb = c.qbest[mbase + qi];
-    if (qb == 0xFFFFFFFFu) return -1;
-    const int bd = qb >> 16, j = qb & 0xFFFF;
-    const int sd = c.qsecond[mbase + qi];
+// The match of the query at y-sorted position `pos` (keypoint qi): k_match stores (qbest, qsecond)
+// by position, so they load beside the query's record, and the train side's best query and the
+// train's keypoint word {x | y << 16} (image base tkb) load together once the best train j is
+// known — two dependent rounds instead of three.  Returns j when the match passes max distance,
+// ratio and the mutual check (and `ok`), else -1.
+__device__ __forceinline__ int match_lookup(const BatchCtx& c, size_t mbase, int pos, int qi, bool ok, size_t tkb,
+                                            uint32_t* tkp) {
+    const uint32_t qb = c.qbest[mbase + pos];
+    const uint32_t sd = c.qsecond[mbase + pos];
+    const int j = qb == 0xFFFFFFFFu ? 0 : (int)(qb & 0xFFFF);
     const uint32_t tb = c.tbest[mbase + j];
-    return (bd <= c.mp.max_hamming && bd * 100 < c.mp.ratio_pct * sd && (int)(tb & 0xFFFF) == qi) ? j : -1;
+    *tkp = c.kps[(tkb + j) * 2];
+    const int bd = (int)(qb >> 16);
+    return (ok && qb != 0xFFFFFFFFu && bd <= c.mp.max_hamming && bd * 100 < c.mp.ratio_pct * (int)sd &&
+            (int)(tb & 0xFFFF) == qi) ? j : -1;
 }
 
 // Stereo refinement (A6b): validity + disparity by 5-offset SAD + parabola.  Eight queries per
@@ -402,13 +410,13 @@ __global__ __launch_bounds__(256) void k_refine_stereo(BatchCtx c) {
     const int qcam = c.cpp * p;
     const size_t qkb = ((size_t)slot * c.C + qcam) * K;
     int l = 0, qi = 0, j = -1;
-    uint32_t qxy = 0;
+    uint32_t qxy = 0, tkp = 0;
     if (live) {
         const uint4 rec = c.ys[qkb + pos];
         qi = (int)rec.z;
         l = (int)(rec.y & 0xFFu);
         qxy = rec.x;
-        if (rec.w) j = match_valid(c, mbase, qi);
+        j = match_lookup(c, mbase, pos, qi, rec.w != 0, ((size_t)slot * c.C + qcam + 1) * K, &tkp);
     }
     const double nanv = __builtin_nan("");
     if (live && sub == 0 && j < 0) {
@@ -420,7 +428,7 @@ __global__ __launch_bounds__(256) void k_refine_stereo(BatchCtx c) {
         const int W = c.g.W[l];
         qx = qxy & 0xFFFF;
         const int qy = qxy >> 16;
-        xr = c.kps[(((size_t)slot * c.C + qcam + 1) * K + j) * 2] & 0xFFFF;
+        xr = tkp & 0xFFFF;
         const uint8_t* Lp = c.pyr + ((size_t)slot * c.C + qcam) * c.g.pyr_bytes + c.g.pyr_off[l];
         const uint8_t* Rp = c.pyr + ((size_t)slot * c.C + qcam + 1) * c.g.pyr_bytes + c.g.pyr_off[l];
         for (int hl = sub; hl < 22; hl += 8) {
@@ -508,13 +516,14 @@ __global__ __launch_bounds__(256) void k_refine_temporal(BatchCtx c) {
     const int qcam = c.cpp * p;
     const size_t qkb = ((size_t)slot * c.C + qcam) * K;
     int l = 0, qi = 0, j = -1;
-    uint32_t qxy = 0;
+    uint32_t qxy = 0, pxy = 0;
+    const int pslot = g > 0 ? ring_slot(c, g - 1) : slot;   // frame 0: nothing matches
     if (live) {
         const uint4 rec = c.ys[qkb + pos];
         qi = (int)rec.z;
         l = (int)(rec.y & 0xFFu);
         qxy = rec.x;
-        if (rec.w && g > 0) j = match_valid(c, mbase, qi);
+        j = match_lookup(c, mbase, pos, qi, rec.w != 0 && g > 0, ((size_t)pslot * c.C + qcam) * K, &pxy);
     }
     int32_t* out_idx = c.temporal + ((size_t)slot * c.P + p) * K;
     double* out_uv = c.tuv + (((size_t)f * c.P + p) * K + qi) * 2;
@@ -529,8 +538,6 @@ __global__ __launch_bounds__(256) void k_refine_temporal(BatchCtx c) {
         const int W = c.g.W[l];
         qx = qxy & 0xFFFF;
         qy = qxy >> 16;
-        const int pslot = ring_slot(c, g - 1);
-        const uint32_t pxy = c.kps[(((size_t)pslot * c.C + qcam) * K + j) * 2];
         const int px = pxy & 0xFFFF, py = pxy >> 16;
         const uint8_t* A = c.pyr + ((size_t)pslot * c.C + qcam) * c.g.pyr_bytes + c.g.pyr_off[l];
         const uint8_t* B = c.pyr + ((size_t)slot * c.C + qcam) * c.g.pyr_bytes + c.g.pyr_off[l];
