@@ -154,15 +154,14 @@ class KeyframeWindow:
         xc = np.einsum("nij,nj->ni", R, X) + t
         return xc, self.fx * xc[:, 0] / xc[:, 2] + self.cx, self.fy * xc[:, 1] / xc[:, 2] + self.cy
 
-    def solve(self) -> dict:
+    def prepare(self, T: np.ndarray) -> dict | None:
+        """Observation set of a solve at cameras ``T`` (cam_T_world per occupied slot, oldest
+        first): the outlier / depth gate at the current estimate, then >= 2 observations per
+        landmark.  None when fewer than two keyframes are occupied."""
         p = self.p
-        slots = self.order()
-        n = len(slots)
-        if n < 2:
-            return {"n_obs": 0, "n_lm": 0}
+        if T.shape[0] < 2:
+            return None
         cam, lm, uo, vo, do = self.observations()
-        T = self.T_cw[slots]
-        # outlier / depth gate at the initial estimate, then >= 2 observations per landmark
         xc, pu, pv = self._project(T[cam, :3, :3], T[cam, :3, 3], self.X[lm])
         keep = (xc[:, 2] > 0) & ((pu - uo) ** 2 + (pv - vo) ** 2 <= p.outlier_px * p.outlier_px)
         cnt = np.bincount(lm[keep], minlength=self.X.shape[0])
@@ -170,72 +169,202 @@ class KeyframeWindow:
         cam, lm, uo, vo, do = cam[keep], lm[keep], uo[keep], vo[keep], do[keep]
         st = np.isfinite(do)                           # observations with a stereo row
         ur = np.where(st, uo - np.where(st, do, 0.0), 0.0)
-        base = self.fxb / self.fx
         ids, li = np.unique(lm, return_inverse=True)   # compact landmark index per observation
-        L = ids.size
-        X = self.X[ids].copy()
-        Rs, ts = T[:, :3, :3].copy(), T[:, :3, 3].copy()
+        return {"n": T.shape[0], "cam": cam, "lm": lm, "uo": uo, "vo": vo, "st": st, "ur": ur, "ids": ids, "li": li,
+                "X": self.X[ids].copy()}
+
+    def linearize(self, ob: dict, Rs: np.ndarray, ts: np.ndarray) -> dict:
+        """One Gauss-Newton linearisation at cameras (Rs, ts) and landmarks ob["X"]: the reduced
+        camera system WITHOUT the camera damping, S = blockdiag(U_c) - sum W_o V_i^-1 W_o'^T and
+        b = -g_c + sum W_o V_i^-1 g_p,i (6n x 6n, 6n), and what the back substitution needs."""
+        p = self.p
+        n, cam, li, uo, vo, st, ur, X = ob["n"], ob["cam"], ob["li"], ob["uo"], ob["vo"], ob["st"], ob["ur"], ob["X"]
+        L = ob["ids"].size
         fx, fy = self.fx, self.fy
+        base = self.fxb / self.fx
+        R = Rs[cam]
+        xc = np.einsum("nij,nj->ni", R, X[li]) + ts[cam]
+        iz = 1.0 / xc[:, 2]
+        r3 = np.where(st, fx * (xc[:, 0] - base) * iz + self.cx - ur, 0.0)
+        r = np.stack([fx * xc[:, 0] * iz + self.cx - uo, fy * xc[:, 1] * iz + self.cy - vo, r3], axis=1)
+        dpi = np.zeros((cam.size, 3, 3))
+        dpi[:, 0, 0] = fx * iz
+        dpi[:, 0, 2] = -fx * xc[:, 0] * iz * iz
+        dpi[:, 1, 1] = fy * iz
+        dpi[:, 1, 2] = -fy * xc[:, 1] * iz * iz
+        dpi[:, 2, 0] = np.where(st, fx * iz, 0.0)
+        dpi[:, 2, 2] = np.where(st, -fx * (xc[:, 0] - base) * iz * iz, 0.0)
+        skew = np.zeros((cam.size, 3, 3))
+        skew[:, 0, 1], skew[:, 0, 2] = -xc[:, 2], xc[:, 1]
+        skew[:, 1, 0], skew[:, 1, 2] = xc[:, 2], -xc[:, 0]
+        skew[:, 2, 0], skew[:, 2, 1] = -xc[:, 1], xc[:, 0]
+        Jc = np.concatenate([dpi, -np.einsum("nij,njk->nik", dpi, skew)], axis=2)   # n x 3 x 6
+        Jp = np.einsum("nij,njk->nik", dpi, R)                                        # n x 3 x 3
+        U = np.zeros((n, 6, 6))
+        gc = np.zeros((n, 6))
+        np.add.at(U, cam, np.einsum("nki,nkj->nij", Jc, Jc))
+        np.add.at(gc, cam, np.einsum("nki,nk->ni", Jc, r))
+        V = np.tile(np.eye(3) * p.lam, (L, 1, 1))
+        gp = np.zeros((L, 3))
+        np.add.at(V, li, np.einsum("nki,nkj->nij", Jp, Jp))
+        np.add.at(gp, li, np.einsum("nki,nk->ni", Jp, r))
+        Vinv = np.linalg.inv(V)
+        Wo = np.einsum("nki,nkj->nij", Jc, Jp)                                        # n x 6 x 3
+        S = np.zeros((6 * n, 6 * n))
+        for c in range(n):
+            S[6 * c:6 * c + 6, 6 * c:6 * c + 6] += U[c]
+        b = -gc.reshape(-1).copy()
+        WV = np.einsum("nij,njk->nik", Wo, Vinv[li])                                   # W_o V_i^-1
+        np.add.at(b.reshape(n, 6), cam, np.einsum("nij,nj->ni", WV, gp[li]))
+        order = np.argsort(li, kind="stable")
+        starts = np.searchsorted(li[order], np.arange(L + 1))
+        for i in range(L):
+            obs = order[starts[i]:starts[i + 1]]
+            for a in obs:
+                for bb in obs:
+                    ca, cb = cam[a], cam[bb]
+                    S[6 * ca:6 * ca + 6, 6 * cb:6 * cb + 6] -= WV[a] @ Wo[bb].T
+        return {"S": S, "b": b, "Wo": Wo, "gp": gp, "Vinv": Vinv}
+
+    @staticmethod
+    def landmark_update(ob: dict, lin: dict, dcc: np.ndarray) -> np.ndarray:
+        """dp_i = V_i^-1 (-g_p,i - sum_o W_o^T dc_o) for camera updates dcc (n x 6)."""
+        rhs = -lin["gp"].copy()
+        np.add.at(rhs, ob["li"], -np.einsum("nji,nj->ni", lin["Wo"], dcc[ob["cam"]]))
+        return np.einsum("lij,lj->li", lin["Vinv"], rhs)
+
+    def solve(self) -> dict:
+        p = self.p
+        slots = self.order()
+        n = len(slots)
+        T = self.T_cw[slots]
+        ob = self.prepare(T)
+        if ob is None:
+            return {"n_obs": 0, "n_lm": 0}
+        Rs, ts = T[:, :3, :3].copy(), T[:, :3, 3].copy()
         for _ in range(p.iters):
-            R = Rs[cam]
-            xc = np.einsum("nij,nj->ni", R, X[li]) + ts[cam]
-            iz = 1.0 / xc[:, 2]
-            r3 = np.where(st, fx * (xc[:, 0] - base) * iz + self.cx - ur, 0.0)
-            r = np.stack([fx * xc[:, 0] * iz + self.cx - uo, fy * xc[:, 1] * iz + self.cy - vo, r3], axis=1)
-            dpi = np.zeros((lm.size, 3, 3))
-            dpi[:, 0, 0] = fx * iz
-            dpi[:, 0, 2] = -fx * xc[:, 0] * iz * iz
-            dpi[:, 1, 1] = fy * iz
-            dpi[:, 1, 2] = -fy * xc[:, 1] * iz * iz
-            dpi[:, 2, 0] = np.where(st, fx * iz, 0.0)
-            dpi[:, 2, 2] = np.where(st, -fx * (xc[:, 0] - base) * iz * iz, 0.0)
-            skew = np.zeros((lm.size, 3, 3))
-            skew[:, 0, 1], skew[:, 0, 2] = -xc[:, 2], xc[:, 1]
-            skew[:, 1, 0], skew[:, 1, 2] = xc[:, 2], -xc[:, 0]
-            skew[:, 2, 0], skew[:, 2, 1] = -xc[:, 1], xc[:, 0]
-            Jc = np.concatenate([dpi, -np.einsum("nij,njk->nik", dpi, skew)], axis=2)   # n x 3 x 6
-            Jp = np.einsum("nij,njk->nik", dpi, R)                                        # n x 3 x 3
-            U = np.zeros((n, 6, 6))
-            gc = np.zeros((n, 6))
-            np.add.at(U, cam, np.einsum("nki,nkj->nij", Jc, Jc))
-            np.add.at(gc, cam, np.einsum("nki,nk->ni", Jc, r))
-            V = np.tile(np.eye(3) * p.lam, (L, 1, 1))
-            gp = np.zeros((L, 3))
-            np.add.at(V, li, np.einsum("nki,nkj->nij", Jp, Jp))
-            np.add.at(gp, li, np.einsum("nki,nk->ni", Jp, r))
-            Vinv = np.linalg.inv(V)
-            Wo = np.einsum("nki,nkj->nij", Jc, Jp)                                        # n x 6 x 3
-            S = np.zeros((6 * n, 6 * n))
-            for c in range(n):
-                S[6 * c:6 * c + 6, 6 * c:6 * c + 6] += U[c] + p.lam * np.eye(6)
-            b = -gc.reshape(-1).copy()
-            WV = np.einsum("nij,njk->nik", Wo, Vinv[li])                                   # W_o V_i^-1
-            np.add.at(b.reshape(n, 6), cam, np.einsum("nij,nj->ni", WV, gp[li]))
-            order = np.argsort(li, kind="stable")
-            starts = np.searchsorted(li[order], np.arange(L + 1))
-            for i in range(L):
-                obs = order[starts[i]:starts[i + 1]]
-                for a in obs:
-                    for bb in obs:
-                        ca, cb = cam[a], cam[bb]
-                        S[6 * ca:6 * ca + 6, 6 * cb:6 * cb + 6] -= WV[a] @ Wo[bb].T
+            lin = self.linearize(ob, Rs, ts)
+            S = lin["S"] + p.lam * np.eye(6 * n)
             dc = np.zeros(6 * n)
-            dc[6:] = np.linalg.solve(S[6:, 6:], b[6:])
+            dc[6:] = np.linalg.solve(S[6:, 6:], lin["b"][6:])
             dcc = dc.reshape(n, 6)
-            rhs = -gp.copy()
-            np.add.at(rhs, li, -np.einsum("nji,nj->ni", Wo, dcc[cam]))
-            dp = np.einsum("lij,lj->li", Vinv, rhs)
+            dp = self.landmark_update(ob, lin, dcc)
             for c in range(1, n):
                 ru = cayley(dcc[c, 3:])
                 Rs[c] = ru @ Rs[c]
                 ts[c] = ru @ ts[c] + dcc[c, :3]
-            X = X + dp
+            ob["X"] = ob["X"] + dp
         for c, s in enumerate(slots):
             self.T_cw[s, :3, :3], self.T_cw[s, :3, 3] = Rs[c], ts[c]
-        self.X[ids] = X
-        xc, pu, pv = self._project(Rs[cam], ts[cam], X[li])
-        rms = float(np.sqrt(np.mean((pu - uo) ** 2 + (pv - vo) ** 2))) if lm.size else 0.0
-        return {"n_obs": int(lm.size), "n_lm": int(L), "rms_px": rms}
+        return self._finish(ob, Rs, ts)
+
+    def _finish(self, ob: dict, Rs: np.ndarray, ts: np.ndarray) -> dict:
+        cam, li, uo, vo = ob["cam"], ob["li"], ob["uo"], ob["vo"]
+        self.X[ob["ids"]] = ob["X"]
+        xc, pu, pv = self._project(Rs[cam], ts[cam], ob["X"][li])
+        rms = float(np.sqrt(np.mean((pu - uo) ** 2 + (pv - vo) ** 2))) if cam.size else 0.0
+        return {"n_obs": int(cam.size), "n_lm": int(ob["ids"].size), "rms_px": rms}
+
+
+def _skew(t: np.ndarray) -> np.ndarray:
+    return np.array([[0.0, -t[2], t[1]], [t[2], 0.0, -t[0]], [-t[1], t[0], 0.0]])
+
+
+def adjoint_rl(T: np.ndarray) -> np.ndarray:
+    """Adjoint of rigid T = [R | t] for left perturbations in (rho, omega) order:
+    (I + (Ad d)^) T = T (I + d^), Ad = [[R, [t]x R], [0, R]]."""
+    R, t = T[:3, :3], T[:3, 3]
+    A = np.zeros((6, 6))
+    A[:3, :3] = R
+    A[:3, 3:] = _skew(t) @ R
+    A[3:, 3:] = R
+    return A
+
+
+class RigKeyframeWindow:
+    """The rig-level A8 window: ONE body pose per keyframe (body_T_world, slots shared by the
+    pairs) and each pair's observations and landmarks in its own ``KeyframeWindow`` whose cameras
+    are functions of the body poses, cam_T_world_p = E_p^-1 B (E_p = base_T_rect-left).
+
+    Solve (rig extension of ``KeyframeWindow.solve``; spec shared with k_ba.hip's rig kernels):
+    a left body update B <- (I + d^) B moves pair p's camera by Ad_p d, Ad_p = adjoint_rl(E_p^-1),
+    so each pair's reduced system (S_p, b_p) at its cameras E_p^-1 B — undamped, landmark damping
+    inside as in the one-pair solve — enters the body system as
+        S = sum_p Ad_p^T S_p Ad_p (6x6 blocks, pairs in order) + lam I,   b = sum_p Ad_p^T b_p;
+    body 0 (oldest keyframe) is the gauge; S' dB = b' by Cholesky; each pair's landmarks move by
+    its back substitution with dc_p = Ad_p dB; bodies R <- cayley(w) R, t <- cayley(w) t + rho, then
+    every pair's cameras are recomputed as E_p^-1 B."""
+
+    def __init__(self, K: int, intrs: list, E: list[np.ndarray], params: BAParams):
+        from .numpy_rig import inv_rigid, mul4
+
+        self._mul4 = mul4
+        self.pairs = [KeyframeWindow(K, intr, params) for intr in intrs]
+        self.E = [np.asarray(e, dtype=np.float64) for e in E]
+        self.Einv = [inv_rigid(e) for e in self.E]
+        self.Ad = [adjoint_rl(ei) for ei in self.Einv]
+        self.p = params
+        self.B = np.tile(np.eye(4), (params.window, 1, 1))   # body_T_world per slot
+
+    @property
+    def frame(self) -> np.ndarray:
+        return self.pairs[0].frame
+
+    def order(self) -> list[int]:
+        return self.pairs[0].order()
+
+    def cams(self, p: int, B: np.ndarray) -> np.ndarray:
+        return np.stack([self._mul4(self.Einv[p], b) for b in B])
+
+    def add_keyframe(self, g: int, B_new: np.ndarray, obs: list[tuple]) -> int:
+        """Keyframe g with body pose ``B_new`` (body_T_world); ``obs[p]`` = (u, v, disp, link) of
+        pair p as for ``KeyframeWindow.add_keyframe``."""
+        slot = -1
+        for p, (w, (u, v, disp, link)) in enumerate(zip(self.pairs, obs)):
+            slot = w.add_keyframe(g, self._mul4(self.Einv[p], B_new), u, v, disp, link)
+        self.B[slot] = B_new
+        return slot
+
+    def solve(self) -> dict:
+        p = self.p
+        slots = self.order()
+        n = len(slots)
+        if n < 2:
+            return {"n_obs": 0, "n_lm": 0}
+        B = self.B[slots].copy()
+        obs = [w.prepare(self.cams(q, B)) for q, w in enumerate(self.pairs)]
+        for _ in range(p.iters):
+            S = p.lam * np.eye(6 * n)
+            b = np.zeros(6 * n)
+            lins = []
+            for q, w in enumerate(self.pairs):
+                T = self.cams(q, B)
+                lin = w.linearize(obs[q], T[:, :3, :3].copy(), T[:, :3, 3].copy())
+                lins.append(lin)
+                A = np.kron(np.eye(n), self.Ad[q])
+                S = S + A.T @ lin["S"] @ A
+                b = b + A.T @ lin["b"]
+            dB = np.zeros(6 * n)
+            dB[6:] = np.linalg.solve(S[6:, 6:], b[6:])
+            dBB = dB.reshape(n, 6)
+            for q, w in enumerate(self.pairs):
+                dcc = dBB @ self.Ad[q].T                   # dc_p = Ad_p dB per camera
+                obs[q]["X"] = obs[q]["X"] + w.landmark_update(obs[q], lins[q], dcc)
+            for c in range(1, n):
+                ru = cayley(dBB[c, 3:])
+                B[c, :3, :3] = ru @ B[c, :3, :3]
+                B[c, :3, 3] = ru @ B[c, :3, 3] + dBB[c, :3]
+        self.B[slots] = B
+        out = {"n_obs": 0, "n_lm": 0, "pairs": []}
+        for q, w in enumerate(self.pairs):
+            T = self.cams(q, B)
+            for c, s in enumerate(slots):
+                w.T_cw[s] = T[c]
+            r = w._finish(obs[q], T[:, :3, :3], T[:, :3, 3])
+            out["pairs"].append(r)
+            out["n_obs"] += r["n_obs"]
+            out["n_lm"] += r["n_lm"]
+        return out
 
 
 def keyframe_observations(left: dict, K: int):
@@ -288,5 +417,43 @@ class BATracker:
         u, v = keyframe_observations(cur["left"], self.K)
         slot = w.add_keyframe(g, _inv_rigid(T_wc), u, v, np.asarray(cur["disp"], dtype=np.float64), link)
         self.Tfe[slot] = W_fe
+        self.last_solve = w.solve()
+        return self.last_solve
+
+
+class RigBATracker:
+    """Drives a ``RigKeyframeWindow`` from the pairs' ``OracleTracker.step`` results and the rig's
+    body front end (``world_T_body`` of ``RigChain``, world = base_link at frame 0), in frame
+    order.  Keyframe g's initial body pose is ``W_ba(prev) inv(W_fe(prev)) W_fe(g)`` in body terms
+    (the rig restatement of ``BATracker``)."""
+
+    def __init__(self, K: int, intrs: list, E: list[np.ndarray], params: BAParams):
+        self.win = RigKeyframeWindow(K, intrs, E, params)
+        self.K = K
+        self.p = params
+        self.Tfe = np.tile(np.eye(4), (params.window, 1, 1))   # world_T_body at insertion
+        self.temporal: list[list[np.ndarray]] = [[] for _ in intrs]
+        self.last_solve: dict | None = None
+
+    def step(self, g: int, results: list[dict], world_T_body: np.ndarray) -> dict | None:
+        for q, res in enumerate(results):
+            self.temporal[q].insert(0, np.asarray(res["cur"]["temporal"], dtype=np.int64))
+            del self.temporal[q][self.p.kf_interval:]
+        if g % self.p.kf_interval:
+            return None
+        w = self.win
+        first = w.pairs[0].n_kf == 0
+        if first:
+            T_wb = world_T_body.copy()
+        else:
+            prev = w.order()[-1]
+            T_wb = _inv_rigid(w.B[prev]) @ _inv_rigid(self.Tfe[prev]) @ world_T_body
+        obs = []
+        for q, res in enumerate(results):
+            u, v = keyframe_observations(res["cur"]["left"], self.K)
+            link = None if first else chain_links(self.temporal[q][: self.p.kf_interval])
+            obs.append((u, v, np.asarray(res["cur"]["disp"], dtype=np.float64), link))
+        slot = w.add_keyframe(g, _inv_rigid(T_wb), obs)
+        self.Tfe[slot] = world_T_body
         self.last_solve = w.solve()
         return self.last_solve
