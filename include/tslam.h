@@ -375,7 +375,12 @@ int tslam_group_destroy(tslam_group* g);
  * indexed by slot (slot = keyframe number mod ba_window): frames[W] (global frame, -1 = empty),
  * cam_T_world[W][16] (BA estimate), landmark[W][K] (id = home slot * K + keypoint, or -1),
  * points[W*K][3] (world position by id), obs_uvd[3][W][K] (u, v, disparity; NaN = none),
- * counts[4] (observations, landmarks, last solve ok, 0).  Any output pointer may be NULL. */
+ * counts[4] (observations, landmarks, last solve ok, 0).  Any output pointer may be NULL.
+ * Rig-level A8: on a handle with tslam_set_rig over several pairs the keyframes of all pairs are
+ * solved as ONE window of body poses (every pair's reduced camera system moved into the body frame
+ * by the adjoint of E_p^-1 and summed; the pairs' cameras are E_p^-1 B); pair = n_pairs then reads
+ * that body window: cam_T_world[W][16] = body_T_world (base_link), counts = the joint ones,
+ * landmark / points / obs_uvd filled with -1 / 0 / NaN (the landmarks live in the pairs' windows). */
 int tslam_ba_read(tslam_handle* h, int pair, int64_t* frames, double* cam_T_world, int32_t* landmark,
                   double* points, double* obs_uvd, int32_t* counts);
 

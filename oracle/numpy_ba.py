@@ -330,7 +330,7 @@ class RigKeyframeWindow:
         slots = self.order()
         n = len(slots)
         if n < 2:
-            return {"n_obs": 0, "n_lm": 0}
+            return {"n_obs": 0, "n_lm": 0, "pairs": [{"n_obs": 0, "n_lm": 0} for _ in self.pairs]}
         B = self.B[slots].copy()
         obs = [w.prepare(self.cams(q, B)) for q, w in enumerate(self.pairs)]
         for _ in range(p.iters):

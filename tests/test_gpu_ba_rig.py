@@ -1,0 +1,108 @@
+"""Rig-level A8: one window of body poses over the keyframes of every
+pair of the two-source bracket rig, HIP (k_ba.hip rig kernels) vs ``oracle/numpy_ba.py``
+(``RigKeyframeWindow`` / ``RigBATracker``), driven by the oracle's per-pair tracking and rig chain.
+
+Bar: keyframe slots, landmark ids and observations identical (integer / copied values); every
+pair's cameras and the body poses within 1e-9 relative Frobenius, landmark positions within 1e-9
+relative (the stated product tolerance is 1e-4); each pair's cameras stay at E_p^-1 B.
+"""
+
+from __future__ import annotations
+
+import functools
+
+import numpy as np
+import pytest
+
+from helpers import rel_frobenius, rig_scene
+from oracle import numpy_slam as O
+from oracle.numpy_ba import BAParams, RigBATracker
+from oracle.numpy_rig import RigChain, inv_rigid, rig_pose
+from thor_slam_amd.params import HipSlamConfig
+
+pytestmark = pytest.mark.gpu
+NAMES = ("192.168.2.21", "192.168.2.25")
+BA_ITEMS = dict(ba_window=4, ba_kf_interval=2, ba_iters=3, ba_lambda=1.0, ba_outlier_px=3.0)
+N = 10
+
+
+@functools.lru_cache(maxsize=1)
+def rig_ba_scenario():
+    sc = dict(rig_scene(NAMES, N))
+    frames, rects, E = sc["frames"], sc["rects"], sc["E"]
+    cfg = HipSlamConfig(**BA_ITEMS)
+    trks = [O.OracleTracker(cfg, dict(fx=r.fx, fy=r.fy, cx=r.cx, cy=r.cy, baseline=r.baseline, map_l=r.map_left,
+                                      map_r=r.map_right)) for r in rects]
+    bp = BAParams(window=cfg.ba_window, kf_interval=cfg.ba_kf_interval, iters=cfg.ba_iters, lam=cfg.ba_lambda,
+                  outlier_px=cfg.ba_outlier_px)
+    intrs = [(r.fx, r.fy, r.cx, r.cy, r.fx * r.baseline) for r in rects]
+    ba = RigBATracker(cfg.n_features, intrs, E, bp)
+    chain = RigChain()
+    snaps = []
+    for i in range(N):
+        outs = [trk.step(frames[i, 2 * q], frames[i, 2 * q + 1]) for q, trk in enumerate(trks)]
+        if i == 0:
+            T_abs = np.eye(4)
+        else:
+            items = [{"status": o["status"], "T": o["T"], "corr": o.get("corr"), "intr": (r.fx, r.fy, r.cx, r.cy)}
+                     for o, r in zip(outs, rects)]
+            T_abs = chain.step(rig_pose(items, E, cfg))
+        ba.step(i, outs, T_abs)
+        w = ba.win
+        snaps.append({"frames": w.frame.copy(), "B": w.B.copy(), "solve": ba.last_solve,
+                      "pairs": [{"T_cw": pw.T_cw.copy(), "lm": pw.lm.copy(), "X": pw.X.copy(), "u": pw.u.copy(),
+                                 "v": pw.v.copy(), "d": pw.d.copy()} for pw in w.pairs]})
+    return {"frames": frames, "rects": rects, "E": E, "cfg": cfg, "snaps": snaps, "traj": sc["traj"]}
+
+
+def _compare(h, want: dict, E, where: str):
+    P = len(E)
+    body = h.ba_read(P)
+    np.testing.assert_array_equal(body["frames"], want["frames"], err_msg=where)
+    occ = want["frames"] >= 0
+    for s in np.nonzero(occ)[0]:
+        assert rel_frobenius(body["T_cw"][s], want["B"][s]) < 1e-9, (where, "body", s)
+    for p in range(P):
+        got, wp = h.ba_read(p), want["pairs"][p]
+        np.testing.assert_array_equal(got["lm"][occ], wp["lm"][occ], err_msg=f"{where} pair {p}")
+        for key in ("u", "v", "d"):
+            np.testing.assert_array_equal(got[key][occ], wp[key][occ], err_msg=f"{where} pair {p} {key}")
+        for s in np.nonzero(occ)[0]:
+            assert rel_frobenius(got["T_cw"][s], wp["T_cw"][s]) < 1e-9, (where, p, s)
+            assert rel_frobenius(got["T_cw"][s], inv_rigid(E[p]) @ body["T_cw"][s]) < 1e-12, (where, p, s)
+        ids = np.unique(wp["lm"][occ])
+        ids = ids[ids >= 0]
+        assert ids.size > 0, (where, p)
+        err = np.linalg.norm(got["X"][ids] - wp["X"][ids], axis=1) / np.linalg.norm(wp["X"][ids], axis=1)
+        assert err.max() < 1e-9, (where, p, float(err.max()))
+    if want["solve"] is not None and want["solve"]["n_obs"]:
+        assert body["n_obs"] == want["solve"]["n_obs"] and body["n_lm"] == want["solve"]["n_lm"], where
+        assert body["ok"], where
+
+
+@pytest.mark.parametrize("batch", [N, 3])
+def test_rig_ba_matches_oracle(batch):
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    sc = rig_ba_scenario()
+    h = Handle(sc["rects"], sc["cfg"], max_batch=batch)
+    h.set_rig(sc["E"])
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    for b0 in range(0, N, batch):
+        nb = min(batch, N - b0)
+        h.submit(dev[b0:].data_ptr(), nb, torch.cuda.current_stream().cuda_stream)
+        h.read_poses(nb)
+        _compare(h, sc["snaps"][b0 + nb - 1], sc["E"], f"after frame {b0 + nb - 1}")
+    h.close()
+
+
+def test_rig_ba_every_pair_contributes():
+    """Both pairs' landmarks enter the joint solve, and the window holds the evicted-then-refilled
+    slots (5 keyframes through a 4-slot window)."""
+    sc = rig_ba_scenario()
+    last = sc["snaps"][-1]
+    assert (last["frames"] >= 0).sum() == 4 and 0 not in last["frames"]
+    per = last["solve"]["pairs"]
+    assert len(per) == 2 and all(r["n_obs"] > 0 and r["n_lm"] > 0 for r in per)

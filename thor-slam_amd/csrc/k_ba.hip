@@ -96,7 +96,11 @@ __global__ __launch_bounds__(256) void k_ba_insert(BatchCtx c, BaArgs a) {
     const int64_t g = a.frame;
     const int f = (int)(g - c.g0);                  // frame of the current batch
     const int rslot = ring_slot(c, g);
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && a.pose_given) {   // rig-level A8: E_p^-1 B set by k_ba_rig_insert
+        for (int e = 0; e < 16; ++e) s_T[e] = q.T[(size_t)a.slot * 16 + e];
+        if (blockIdx.x == 0)
+            for (int e = 0; e < 16; ++e) q.Tfe[(size_t)a.slot * 16 + e] = a.fe[(size_t)(f * c.P + p) * 16 + e];
+    } else if (threadIdx.x == 0) {
         const double* Tfe = a.fe + (size_t)(f * c.P + p) * 16;   // world_T_cam (front-end snapshot)
         double Twc[16];
         if (a.prev < 0) {
@@ -947,7 +951,8 @@ void launch_ba_schur(const BatchCtx& c, const BaArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_ba_schur, dim3(a.nsplit), dim3(BA_SCHUR_THREADS), 0, s, c, ai);
 }
 
-void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing) {
+// A solve's observation set of pair a.pair (gate, compaction, slot table).
+static void launch_ba_prepare(const BatchCtx& c, const BaArgs& a, hipStream_t s) {
     // grids sized for the window's maximum (counts live on the device; threads past them exit)
     const int WK = a.W * c.g.K;
     const int nb = (WK + 255) / 256;
@@ -957,15 +962,188 @@ void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming
     hipLaunchKernelGGL(k_ba_tilescatter, dim3(ntiles), dim3(256), 0, s, c, a);
     hipLaunchKernelGGL(k_ba_camobs, dim3(nb), dim3(256), 0, s, c, a);
     hipLaunchKernelGGL(k_ba_slots, dim3((WK * TS_BA_MAXW + 255) / 256), dim3(256), 0, s, c, a);
+}
+
+// One linearisation of pair a.pair: the Schur pass (+ iteration it - 1's landmark update when
+// `it` > 0) and the reduction to C, U_c, g_c.
+static void launch_ba_linearize(const BatchCtx& c, const BaArgs& a, int it, hipStream_t s, BaTiming* timing) {
     BaArgs ai = a;
+    const bool rec = timing && timing->used < timing->cap;
+    ai.fused_backsub = it > 0;   // iteration it - 1's landmark update happens inside this Schur pass
+    if (rec) (void)hipEventRecord(timing->ev[2 * timing->used], s);
+    hipLaunchKernelGGL(k_ba_schur, dim3(a.nsplit), dim3(BA_SCHUR_THREADS), 0, s, c, ai);
+    if (rec) (void)hipEventRecord(timing->ev[2 * timing->used++ + 1], s);
+    hipLaunchKernelGGL(k_ba_reduce, dim3(64 + (a.n_order * 27 + 3) / 4), dim3(256), 0, s, c, a);
+}
+
+static void launch_ba_backsub(const BatchCtx& c, const BaArgs& a, hipStream_t s) {
+    const int nb = (a.W * c.g.K + 255) / 256;
+    hipLaunchKernelGGL(k_ba_backsub, dim3(16 * nb), dim3(256), 0, s, c, a);   // the last iteration's
+}
+
+void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing) {
+    launch_ba_prepare(c, a, s);
     for (int it = 0; it < a.iters; ++it) {
-        const bool rec = timing && timing->used < timing->cap;
-        ai.fused_backsub = it > 0;   // iteration it - 1's landmark update happens inside this Schur pass
-        if (rec) (void)hipEventRecord(timing->ev[2 * timing->used], s);
-        hipLaunchKernelGGL(k_ba_schur, dim3(a.nsplit), dim3(BA_SCHUR_THREADS), 0, s, c, ai);
-        if (rec) (void)hipEventRecord(timing->ev[2 * timing->used++ + 1], s);
-        hipLaunchKernelGGL(k_ba_reduce, dim3(64 + (a.n_order * 27 + 3) / 4), dim3(256), 0, s, c, a);
+        launch_ba_linearize(c, a, it, s, timing);
         hipLaunchKernelGGL(k_ba_solve, dim3(1), dim3(64 * BA_SOLVE_WAVES), 0, s, c, a);
     }
-    hipLaunchKernelGGL(k_ba_backsub, dim3(16 * nb), dim3(256), 0, s, c, a);   // the last iteration's
+    launch_ba_backsub(c, a, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+// rig-level A8 (oracle RigKeyframeWindow): one body pose per keyframe, storage pair c.P
+// ---------------------------------------------------------------------------------------------
+// Adjoint of rigid T = [R | t] for left perturbations in (rho, omega) order:
+// (I + (Ad d)^) T = T (I + d^), Ad = [[R, [t]x R], [0, R]].
+__device__ __forceinline__ void adjoint_rl(const double* T, double A[6][6]) {
+    const double t0 = T[3], t1 = T[7], t2 = T[11];
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) A[i][j] = 0.0;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            A[i][j] = T[4 * i + j];
+            A[3 + i][3 + j] = T[4 * i + j];
+        }
+    // [t]x R: row 0 = -t2 R1 + t1 R2, row 1 = t2 R0 - t0 R2, row 2 = -t1 R0 + t0 R1
+    for (int j = 0; j < 3; ++j) {
+        const double r0 = T[j], r1 = T[4 + j], r2 = T[8 + j];
+        A[0][3 + j] = -t2 * r1 + t1 * r2;
+        A[1][3 + j] = t2 * r0 - t0 * r2;
+        A[2][3 + j] = -t1 * r0 + t0 * r1;
+    }
+}
+
+// The batch's rig front-end body poses (T_abs of the rig records: world_T_body).
+__global__ __launch_bounds__(256) void k_ba_snapshot_rig(BatchCtx c, double* dst) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= c.n * 16) return;
+    dst[i] = c.rig_pose[(size_t)(i / 16) * TS_POSE_DOUBLES + 16 + i % 16];
+}
+
+// Keyframe a.frame's body pose into slot a.slot of the body window: B = inv(W_ba(prev)
+// inv(W_fe(prev)) W_fe(g)) (body terms, RigBATracker), and every pair's camera E_p^-1 B.
+__global__ void k_ba_rig_insert(BatchCtx c, BaArgs a) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    BaPair qb = ba_pair(c, a, c.P);
+    const int f = (int)(a.frame - c.g0);
+    const double* fe = a.fe_body + (size_t)f * 16;   // world_T_body
+    double Twb[16], Tbw[16];
+    if (a.prev < 0) {
+        for (int e = 0; e < 16; ++e) Twb[e] = fe[e];
+    } else {
+        double Wba[16], ifp[16], tmp[16];
+        inv_rigid(qb.T + (size_t)a.prev * 16, Wba);
+        inv_rigid(qb.Tfe + (size_t)a.prev * 16, ifp);
+        mul4(Wba, ifp, tmp);
+        mul4(tmp, fe, Twb);
+    }
+    inv_rigid(Twb, Tbw);
+    for (int e = 0; e < 16; ++e) {
+        qb.T[(size_t)a.slot * 16 + e] = Tbw[e];
+        qb.Tfe[(size_t)a.slot * 16 + e] = fe[e];
+    }
+    for (int p = 0; p < c.P; ++p) mul4(c.rig_Einv + 16 * p, Tbw, a.st.T + ((size_t)p * a.W + a.slot) * 16);
+}
+
+// The body system of an iteration from every pair's reduced system (block r = row, thread = column):
+// S = sum_p Ad_p^T S_p Ad_p with S_p = blockdiag(U_c) - C_p (undamped), b = sum_p Ad_p^T b_p with
+// b_p = -g_c + C_p[:, 60], Ad_p = adjoint_rl(E_p^-1); written as the body pair's C = -S (column 60:
+// b) and U = 0, so k_ba_solve on the body pair solves (lam I + S) dB = b.
+__global__ __launch_bounds__(64) void k_ba_rig_combine(BatchCtx c, BaArgs a) {
+    const int n = a.n_order, r = blockIdx.x, col = threadIdx.x;
+    BaPair qb = ba_pair(c, a, c.P);
+    double v = 0.0;
+    if (r < 6 * n && (col < 6 * n || col == 60)) {
+        const int ci = r / 6, i = r - 6 * ci;
+        for (int p = 0; p < c.P; ++p) {
+            BaPair q = ba_pair(c, a, p);
+            double A[6][6];
+            adjoint_rl(c.rig_Einv + 16 * p, A);
+            const double* U = q.cam_U + (size_t)ci * 27;
+            if (col == 60) {   // (Ad^T b_p)[i]
+                double acc = 0.0;
+                for (int aa = 0; aa < 6; ++aa) acc += A[aa][i] * (-U[21 + aa] + q.C[(6 * ci + aa) * 64 + 60]);
+                v += acc;
+                continue;
+            }
+            const int cj = col / 6, j = col - 6 * cj;
+            double acc = 0.0;
+            for (int aa = 0; aa < 6; ++aa) {
+                double sb = 0.0;   // (S_p Ad)[aa][j]
+                for (int bb = 0; bb < 6; ++bb) {
+                    double sab = -q.C[(6 * ci + aa) * 64 + 6 * cj + bb];
+                    if (ci == cj) {
+                        const int lo = aa < bb ? aa : bb, hi = aa < bb ? bb : aa;
+                        sab += U[lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];
+                    }
+                    sb += sab * A[bb][j];
+                }
+                acc += A[aa][i] * sb;
+            }
+            v += acc;
+        }
+        if (col != 60) v = -v;
+    }
+    qb.C[r * 64 + col] = v;
+    if (r == 0) {
+        for (int e = col; e < a.W * 27; e += 64) qb.cam_U[e] = 0.0;
+        if (col == 0) {
+            int nobs = 0, L = 0;
+            for (int p = 0; p < c.P; ++p) {
+                nobs += a.st.counts[4 * p];
+                L += a.st.counts[4 * p + 1];
+            }
+            qb.counts[0] = nobs;
+            qb.counts[1] = L;
+        }
+    }
+}
+
+// After the body solve: every pair's cameras E_p^-1 B, its camera updates dc_p = Ad_p dB (for the
+// landmark back substitution) and the solve's status (block = pair, thread = window camera).
+__global__ __launch_bounds__(64) void k_ba_rig_expand(BatchCtx c, BaArgs a) {
+    const int p = blockIdx.x, cj = threadIdx.x;
+    BaPair q = ba_pair(c, a, p), qb = ba_pair(c, a, c.P);
+    if (cj < a.n_order) {
+        const int slot = a.order[cj];
+        mul4(c.rig_Einv + 16 * p, qb.T + (size_t)slot * 16, q.T + (size_t)slot * 16);
+        double A[6][6];
+        adjoint_rl(c.rig_Einv + 16 * p, A);
+        for (int i = 0; i < 6; ++i) {
+            double acc = 0.0;
+            for (int j = 0; j < 6; ++j) acc += A[i][j] * qb.dc[6 * cj + j];
+            q.dc[6 * cj + i] = acc;
+        }
+    }
+    if (cj == 0) q.counts[2] = qb.counts[2];
+}
+
+void launch_ba_snapshot_rig(const BatchCtx& c, double* dst, hipStream_t s) {
+    hipLaunchKernelGGL(k_ba_snapshot_rig, dim3((c.n * 16 + 255) / 256), dim3(256), 0, s, c, dst);
+}
+
+void launch_ba_rig_keyframe(const BatchCtx& c, const BaArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_ba_rig_insert, dim3(1), dim3(64), 0, s, c, a);
+}
+
+void launch_ba_rig_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing) {
+    BaArgs ap = a, ab = a;
+    ab.pair = c.P;
+    for (int p = 0; p < c.P; ++p) {
+        ap.pair = p;
+        launch_ba_prepare(c, ap, s);
+    }
+    for (int it = 0; it < a.iters; ++it) {
+        for (int p = 0; p < c.P; ++p) {
+            ap.pair = p;
+            launch_ba_linearize(c, ap, it, s, timing);
+        }
+        hipLaunchKernelGGL(k_ba_rig_combine, dim3(64), dim3(64), 0, s, c, ab);
+        hipLaunchKernelGGL(k_ba_solve, dim3(1), dim3(64 * BA_SOLVE_WAVES), 0, s, c, ab);
+        hipLaunchKernelGGL(k_ba_rig_expand, dim3(c.P), dim3(64), 0, s, c, ab);
+    }
+    for (int p = 0; p < c.P; ++p) {
+        ap.pair = p;
+        launch_ba_backsub(c, ap, s);
+    }
 }

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <limits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -267,8 +268,10 @@ static void build_geometry(tslam_handle* h) {
     g.rs_total = (ro + 7) & ~7;
 }
 
+// Storage pairs of A8: the P stereo pairs plus pair P, the body window of the rig-level solve
+// (tslam_ba.h); every storage pair has its own solve scratch (strides as in ba_pair).
 static int alloc_ba(tslam_handle* h) {
-    const size_t W = h->prm.ba_window, K = h->g.K, P = h->P, WK = W * K;
+    const size_t W = h->prm.ba_window, K = h->g.K, P = h->P + 1, WK = W * K, M = TS_BA_MAXW;
     BaStore& b = h->ba;
     struct A {
         void** p;
@@ -276,16 +279,18 @@ static int alloc_ba(tslam_handle* h) {
     } list[] = {
         {(void**)&b.T, 8 * P * W * 16},      {(void**)&b.Tfe, 8 * P * W * 16},   {(void**)&b.u, 8 * P * WK},
         {(void**)&b.v, 8 * P * WK},          {(void**)&b.d, 8 * P * WK},         {(void**)&b.lm, 4 * P * WK},
-        {(void**)&b.X, 8 * P * WK * 3},      {(void**)&b.kf_desc, 32 * P * WK},   {(void**)&b.gid, 8 * P * WK},      {(void**)&b.remap, 4 * K},          {(void**)&b.cnt, 4 * WK},
-        {(void**)&b.li, 4 * WK},             {(void**)&b.lm_id, 4 * WK},         {(void**)&b.keep, WK},
-        {(void**)&b.camobs, 4 * W * WK},     {(void**)&b.obs_Vg, 8 * WK * 9},    {(void**)&b.obs_cam, 4 * WK},
-        {(void**)&b.obs_k, 4 * WK},          {(void**)&b.obs_id, 4 * WK},        {(void**)&b.cam_off, 4 * (W + 1)},
-        {(void**)&b.counts, 4 * 4 * P},      {(void**)&b.tiles, 4 * 2 * TS_BA_TILES},      {(void**)&b.obs_Ug, 8 * WK * 27},
-        {(void**)&b.lo_o, 4 * WK * TS_BA_MAXW}, {(void**)&b.lo_uvd, 32 * WK * TS_BA_MAXW}, {(void**)&b.lo_W, 8 * 18 * WK * TS_BA_MAXW},
-        {(void**)&b.Xc, 8 * WK * 3},
-        {(void**)&b.lm_L, 8 * WK * 6},       {(void**)&b.lm_gp, 8 * WK * 3},     {(void**)&b.C, 8 * 64 * 64},
-        {(void**)&b.part, 8 * (size_t)TS_BA_SPLIT * 64 * 64}, {(void**)&b.cam_U, 8 * W * 27}, {(void**)&b.dc, 8 * W * 6},
-        {(void**)&b.flops, 8},               {(void**)&b.fe_pose, 8 * 2 * (size_t)h->B * P * 16},
+        {(void**)&b.X, 8 * P * WK * 3},      {(void**)&b.kf_desc, 32 * P * WK},  {(void**)&b.gid, 8 * P * WK},
+        {(void**)&b.remap, 4 * P * K},       {(void**)&b.cnt, 4 * P * WK},
+        {(void**)&b.li, 4 * P * WK},         {(void**)&b.lm_id, 4 * P * WK},     {(void**)&b.keep, P * WK},
+        {(void**)&b.camobs, 4 * P * W * WK}, {(void**)&b.obs_Vg, 8 * P * WK * 9}, {(void**)&b.obs_cam, 4 * P * WK},
+        {(void**)&b.obs_k, 4 * P * WK},      {(void**)&b.obs_id, 4 * P * WK},    {(void**)&b.cam_off, 4 * P * (W + 1)},
+        {(void**)&b.counts, 4 * 4 * P},      {(void**)&b.tiles, 4 * P * 2 * TS_BA_TILES}, {(void**)&b.obs_Ug, 8 * P * WK * 27},
+        {(void**)&b.lo_o, 4 * P * WK * M},   {(void**)&b.lo_uvd, 32 * P * WK * M}, {(void**)&b.lo_W, 8 * 18 * P * WK * M},
+        {(void**)&b.Xc, 8 * P * WK * 3},
+        {(void**)&b.lm_L, 8 * P * WK * 6},   {(void**)&b.lm_gp, 8 * P * WK * 3}, {(void**)&b.C, 8 * P * 64 * 64},
+        {(void**)&b.part, 8 * P * (size_t)TS_BA_SPLIT * 64 * 64}, {(void**)&b.cam_U, 8 * P * W * 27}, {(void**)&b.dc, 8 * P * W * 6},
+        {(void**)&b.flops, 8},               {(void**)&b.fe_pose, 8 * 2 * (size_t)h->B * h->P * 16},
+        {(void**)&b.fe_body, 8 * 2 * (size_t)h->B * 16},
     };
     for (const A& a : list) {
         const int rc = dev_alloc(h, a.p, a.bytes);
@@ -294,8 +299,8 @@ static int alloc_ba(tslam_handle* h) {
     // scratch kept in its between-solves state by the kernels themselves (no per-solve memsets):
     // camobs all -1 (k_ba_slots resets the entries k_ba_camobs set), remap all 0x7F7F7F7F
     // (k_ba_insert refills it after an eviction), cnt zero (dev_alloc; k_ba_slots re-zeroes it)
-    HIPCHK(hipMemset(b.camobs, 0xFF, 4 * W * WK));
-    HIPCHK(hipMemset(b.remap, 0x7F, 4 * K));
+    HIPCHK(hipMemset(b.camobs, 0xFF, 4 * P * W * WK));
+    HIPCHK(hipMemset(b.remap, 0x7F, 4 * P * K));
     HIPCHK(hipDeviceSynchronize());
     return TSLAM_OK;
 }
@@ -324,10 +329,14 @@ static int ba_order(const tslam_handle* h, int skip, int* out) {
 
 static BatchCtx make_ctx(tslam_handle* h);
 
+// Rig-level A8: a handle with tslam_set_rig over several pairs solves one body window.
+static bool ba_rig(const tslam_handle* h) { return h->rig && h->P > 1 && h->prm.ba_window; }
+
 // A8: every keyframe of the current batch (g % ba_kf_interval == 0) enters each pair's window,
-// evicting the oldest when the window is full, and the window is solved.  Host bookkeeping of
-// the slots only; nothing synchronises.
-static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const double* fe) {
+// evicting the oldest when the window is full, and the window is solved (per pair, or for a rig
+// one joint body solve: launch_ba_rig_solve).  Host bookkeeping of the slots only; nothing
+// synchronises.  `fe_body`: the rig front end's snapshot of the batch (rig-level A8).
+static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const double* fe, const double* fe_body) {
     const int W = h->prm.ba_window, iv = h->prm.ba_kf_interval;
     for (int64_t g = c.g0; g < c.g0 + c.n; ++g) {
         if (g % iv != 0 || g <= h->ba_last) continue;
@@ -340,6 +349,12 @@ static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const doub
         a.prev = nocc ? ord[nocc - 1] : -1;
         const bool evict = h->ba_frame[a.slot] >= 0;
         if (evict) a.n_order = ba_order(h, a.slot, a.order);
+        const bool rig = ba_rig(h);
+        if (rig) {   // the body pose first, every pair's camera E_p^-1 B
+            a.fe_body = fe_body;
+            a.pose_given = 1;
+            launch_ba_rig_keyframe(c, a, s);
+        }
         for (int p = 0; p < h->P; ++p) {
             a.pair = p;
             launch_ba_keyframe(c, a, evict, s);
@@ -348,10 +363,18 @@ static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const doub
         h->ba_nkf += 1;
         h->ba_last = g;
         a.n_order = ba_order(h, -1, a.order);
+        h->ba_solved.resize(h->P);
+        if (rig) {
+            launch_ba_rig_solve(c, a, s, h->ba_timing.ev ? &h->ba_timing : nullptr);
+            for (int p = 0; p < h->P; ++p) {
+                h->ba_solved[p] = a;
+                h->ba_solved[p].pair = p;
+            }
+            continue;
+        }
         for (int p = 0; p < h->P; ++p) {
             a.pair = p;
             launch_ba_solve(c, a, s, h->ba_timing.ev ? &h->ba_timing : nullptr);
-            h->ba_solved.resize(h->P);
             h->ba_solved[p] = a;
         }
     }
@@ -1019,8 +1042,10 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
             launch_chains(c, h->rig, s);
             if (h->prm.ba_window) {
                 double* snap = h->ba.fe_pose + (size_t)(h->batch_idx & 1) * h->B * h->P * 16;
+                double* snap_body = h->ba.fe_body + (size_t)(h->batch_idx & 1) * h->B * 16;
                 launch_ba_snapshot(c, snap, s);
-                run_ba(h, c, s, snap);
+                if (ba_rig(h)) launch_ba_snapshot_rig(c, snap_body, s);
+                run_ba(h, c, s, snap, snap_body);
             }
             break;
         case TSLAM_KERNEL_RIG:
@@ -1033,8 +1058,10 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
             if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
             const int par = (int)(h->batch_idx & 1);
             double* snap = h->ba.fe_pose + (size_t)par * h->B * h->P * 16;
+            double* snap_body = h->ba.fe_body + (size_t)par * h->B * 16;
             hipStream_t fs = h->last_stream;
             launch_ba_snapshot(c, snap, fs);
+            if (ba_rig(h)) launch_ba_snapshot_rig(c, snap_body, fs);
             const bool other = s != fs;
             if (other) {
                 if (!h->ev_fe) {
@@ -1045,7 +1072,7 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
                 HIPCHK(hipEventRecord(h->ev_fe, fs));
                 HIPCHK(hipStreamWaitEvent(s, h->ev_fe, 0));
             }
-            run_ba(h, c, s, snap);
+            run_ba(h, c, s, snap, snap_body);
             if (other) {
                 HIPCHK(hipEventRecord(h->ev_ba[par], s));
                 h->ba_pending[par] = true;
@@ -1811,7 +1838,7 @@ int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_e
 
 int tslam_ba_read(tslam_handle* h, int pair, int64_t* frames, double* cam_T_world, int32_t* landmark,
                   double* points, double* obs_uvd, int32_t* counts) {
-    if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
+    if (!h || pair < 0 || pair > h->P || (pair == h->P && !ba_rig(h))) return fail(TSLAM_EINVAL, "bad handle or pair");
     if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
     int rc = tslam_sync(h);
     if (rc != TSLAM_OK) return rc;
@@ -1819,6 +1846,14 @@ int tslam_ba_read(tslam_handle* h, int pair, int64_t* frames, double* cam_T_worl
     const BaStore& b = h->ba;
     if (frames)
         for (size_t s = 0; s < W; ++s) frames[s] = h->ba_frame[s];
+    if (pair == h->P) {   // the rig's body window: body_T_world per slot and the joint counts only
+        if (cam_T_world) HIPCHK(hipMemcpy(cam_T_world, b.T + pair * W * 16, 8 * W * 16, hipMemcpyDeviceToHost));
+        if (counts) HIPCHK(hipMemcpy(counts, b.counts + 4 * pair, 4 * 4, hipMemcpyDeviceToHost));
+        if (landmark) std::fill(landmark, landmark + WK, -1);
+        if (points) std::fill(points, points + WK * 3, 0.0);
+        if (obs_uvd) std::fill(obs_uvd, obs_uvd + 3 * WK, std::numeric_limits<double>::quiet_NaN());
+        return TSLAM_OK;
+    }
     if (cam_T_world) HIPCHK(hipMemcpy(cam_T_world, b.T + pair * W * 16, 8 * W * 16, hipMemcpyDeviceToHost));
     if (landmark) HIPCHK(hipMemcpy(landmark, b.lm + pair * WK, 4 * WK, hipMemcpyDeviceToHost));
     if (points) HIPCHK(hipMemcpy(points, b.X + pair * WK * 3, 8 * WK * 3, hipMemcpyDeviceToHost));

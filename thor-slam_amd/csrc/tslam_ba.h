@@ -6,10 +6,15 @@
 //   u v d f64 [P][W][K]     level-0 observation of every keypoint, disparity (NaN = none)
 //   lm   i32 [P][W][K]      landmark id (home slot * K + keypoint) or -1
 //   X    f64 [P][W*K][3]    landmark positions (world), indexed by id
-// Per solve (scratch, shared by the pairs: their solves are ordered on one stream):
-//   observation lists, the camera x landmark observation table, Jacobian blocks and the split-K
-//   partials of the 64 x 64 Schur product C.  The camera system is 64 wide: 6 rows per keyframe
-//   (<= 10 keyframes = 60 rows) and row 60 = the landmark right-hand side.
+// Per solve (scratch, one set per pair: the rig-level solve keeps every pair's linearisation alive
+// across an iteration): observation lists, the camera x landmark observation table, Jacobian
+// blocks and the split-K partials of the 64 x 64 Schur product C.  The camera system is 64 wide:
+// 6 rows per keyframe (<= 10 keyframes = 60 rows) and row 60 = the landmark
+// right-hand side.
+// Rig-level A8 (a handle with tslam_set_rig and P > 1; oracle RigKeyframeWindow): storage pair P
+// is the BODY window — T[P] = body_T_world per slot, Tfe[P] = the rig front end's world_T_body at
+// insertion, and its C / cam_U / dc / counts hold the combined body system of an iteration; every
+// pair's cameras are E_p^-1 T[P].
 #pragma once
 
 #include "tslam_common.h"
@@ -62,6 +67,7 @@ struct BaStore {
     double* dc;        // [W][6]
     double* flops;     // [1] algorithmic Schur-product flops accumulated (profiling)
     double* fe_pose;   // [2][B][P][16] front-end world_T_cam of the batch (snapshot per batch parity)
+    double* fe_body;   // [2][B][16] rig front end's world_T_body of the batch (rig-level A8)
 };
 
 struct BaArgs {
@@ -76,8 +82,10 @@ struct BaArgs {
     int order[TS_BA_MAXW];      // evict: remaining slots; gather/solve: occupied slots, oldest first
     int iters, nsplit;
     int fused_backsub;          // schur: first apply the previous iteration's landmark back substitution
+    int pose_given;             // insert: the slot's cam_T_world is already set (rig-level A8)
     double lam, outlier_px;
     const double* fe;           // insert: this batch's front-end pose snapshot [B][P][16]
+    const double* fe_body;      // rig insert: the rig front end's snapshot [B][16]
 };
 
 // Per-pair view (the scratch pointers are shared).
@@ -97,7 +105,7 @@ struct BaPair {
 };
 
 __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, int p) {
-    const size_t WK = (size_t)a.W * c.g.K;
+    const size_t W = (size_t)a.W, K = (size_t)c.g.K, WK = W * K, M = TS_BA_MAXW;
     const BaStore& s = a.st;
     BaPair q;
     q.T = s.T + (size_t)p * a.W * 16;
@@ -109,12 +117,18 @@ __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, in
     q.X = s.X + p * WK * 3;
     q.kf_desc = s.kf_desc + p * WK * 8;
     q.gid = s.gid + p * WK;
-    q.remap = s.remap; q.cnt = s.cnt; q.li = s.li; q.lm_id = s.lm_id; q.keep = s.keep; q.camobs = s.camobs;
-    q.obs_cam = s.obs_cam; q.obs_k = s.obs_k; q.obs_id = s.obs_id; q.cam_off = s.cam_off;
+    // per-pair scratch (strides: ba_scratch_sizes in tslam_api.cpp)
+    q.remap = s.remap + p * K; q.cnt = s.cnt + p * WK; q.li = s.li + p * WK; q.lm_id = s.lm_id + p * WK;
+    q.keep = s.keep + p * WK; q.camobs = s.camobs + p * W * WK;
+    q.obs_cam = s.obs_cam + p * WK; q.obs_k = s.obs_k + p * WK; q.obs_id = s.obs_id + p * WK;
+    q.cam_off = s.cam_off + p * (W + 1);
     q.counts = s.counts + 4 * p;
-    q.tiles = s.tiles;
-    q.lo_o = s.lo_o; q.lo_uvd = s.lo_uvd; q.lo_W = s.lo_W; q.Xc = s.Xc; q.obs_Ug = s.obs_Ug; q.obs_Vg = s.obs_Vg; q.lm_L = s.lm_L; q.lm_gp = s.lm_gp; q.part = s.part; q.C = s.C;
-    q.cam_U = s.cam_U; q.dc = s.dc; q.flops = s.flops;
+    q.tiles = s.tiles + p * 2 * TS_BA_TILES;
+    q.lo_o = s.lo_o + p * WK * M; q.lo_uvd = s.lo_uvd + p * WK * M * 4; q.lo_W = s.lo_W + p * WK * M * 18;
+    q.Xc = s.Xc + p * WK * 3; q.obs_Ug = s.obs_Ug + p * WK * 27; q.obs_Vg = s.obs_Vg + p * WK * 9;
+    q.lm_L = s.lm_L + p * WK * 6; q.lm_gp = s.lm_gp + p * WK * 3;
+    q.part = s.part + p * (size_t)TS_BA_SPLIT * 4096; q.C = s.C + p * 4096;
+    q.cam_U = s.cam_U + p * W * 27; q.dc = s.dc + p * W * 6; q.flops = s.flops;
     return q;
 }
 
@@ -126,5 +140,10 @@ struct BaTiming {
     int cap, used;
 };
 void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing);
+// rig-level A8: the body snapshot of the batch, a keyframe's body pose (and every pair's camera at
+// E_p^-1 B), and the joint solve over all pairs (storage pair c.P = the body window)
+void launch_ba_snapshot_rig(const BatchCtx& c, double* dst, hipStream_t s);
+void launch_ba_rig_keyframe(const BatchCtx& c, const BaArgs& a, hipStream_t s);
+void launch_ba_rig_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing);
 // one k_ba_schur launch on the window state `a` (measurement replays)
 void launch_ba_schur(const BatchCtx& c, const BaArgs& a, hipStream_t s);

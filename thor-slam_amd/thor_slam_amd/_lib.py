@@ -538,7 +538,9 @@ class Handle:
 
     def ba_read(self, pair: int = 0) -> dict:
         """A8 keyframe window of one pair (synchronises): slot-indexed frames, cam_T_world,
-        landmark ids, landmark positions (by id), observations and the last solve's counts."""
+        landmark ids, landmark positions (by id), observations and the last solve's counts.
+        On a rig (``set_rig``, several pairs) ``pair = n_pairs`` reads the body window of the
+        rig-level solve: ``T_cw`` is body_T_world per slot, counts are the joint ones."""
         W, K = self.cfg.ba_window, self.K
         frames = np.zeros(W, dtype=np.int64)
         T = np.zeros((W, 4, 4))
