@@ -106,3 +106,54 @@ def test_rig_ba_every_pair_contributes():
     assert (last["frames"] >= 0).sum() == 4 and 0 not in last["frames"]
     per = last["solve"]["pairs"]
     assert len(per) == 2 and all(r["n_obs"] > 0 and r["n_lm"] > 0 for r in per)
+
+
+def test_engine_publishes_the_rig_body_window():
+    """HipSlamEngine on the two-source rig with local BA: the window is the body window, get_map
+    returns the body keyframes (in-window ones = the device's BA estimates) and every pair's
+    landmarks, and a keyframe frame's published pose is its BA body pose."""
+    import json
+    from pathlib import Path
+
+    import torch
+
+    from thor_slam_amd.camera import CameraRig, Extrinsics
+    from thor_slam_amd.slam.hip_engine import HipSlamEngine
+
+    sc = rig_scene(NAMES, N)
+    mats = json.loads((Path(__file__).parent / "golden" / "brackets_joints.json").read_text())
+    srcs = sc["sources"]
+    rig = CameraRig(srcs, rig_extrinsics={s.name: Extrinsics.from_4x4_matrix(np.array(mats[s.name])) for s in srcs})
+    cfg = HipSlamConfig(batch_size=N, **BA_ITEMS)
+    eng = HipSlamEngine(num_cameras=4, config=cfg)
+    eng.initialize(rig.calibration, cfg)
+    assert len(eng._pairs) == 2
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    stamps = [srcs[0].timestamp(i) for i in range(N)]
+    eng.process_batch(dev[: N - 1], stamps[: N - 1])   # ends on keyframe 8
+    latest = eng._latest_pose.to_4x4_matrix()
+    body = eng._handle.ba_read(2)
+    s8 = int(np.nonzero(body["frames"] == 8)[0][0])
+    assert rel_frobenius(latest, np.linalg.inv(body["T_cw"][s8])) < 1e-9
+    eng.process_batch(dev[N - 1:], stamps[N - 1:])
+    smap = eng.get_map()
+    # frames 2, 4, 6, 8: keyframe 0 was inserted and evicted inside the first batch, before the
+    # engine read the window (as for one pair)
+    assert len(smap.keyframe_poses) == 4
+    body = eng._handle.ba_read(2)
+    by_stamp = {p.timestamp: p.to_4x4_matrix() for p in smap.keyframe_poses}
+    for s_, f in enumerate(body["frames"]):
+        if f >= 0:
+            assert rel_frobenius(by_stamp[stamps[f]], np.linalg.inv(body["T_cw"][s_])) < 1e-12
+    n_pts = 0
+    for p in range(2):
+        w = eng._handle.ba_read(p)
+        occ = w["frames"] >= 0
+        ids = np.unique(w["lm"][occ])
+        n_pts += int((ids >= 0).sum())
+    assert len(smap.points) == n_pts and n_pts > 0
+    # and the published trajectory follows the rendered body motion (world = base at frame 0)
+    gt = np.linalg.inv(sc["traj"][0]) @ sc["traj"][N - 1]
+    got = eng._latest_pose.to_4x4_matrix()
+    assert np.linalg.norm(got[:3, 3] - gt[:3, 3]) < 0.1 * np.linalg.norm(gt[:3, 3]) + 2e-3
+    eng.shutdown()

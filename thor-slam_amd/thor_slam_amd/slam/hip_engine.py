@@ -20,8 +20,10 @@ With local BA on (``ba_window > 0``, SURVEY.md §8a A8, one stereo pair) a frame
 front-end pose carried by the correction of the newest keyframe at or before it that is still in
 the window, ``W_ba(kf) inv(W_fe(kf)) W_fe(g)`` (the oldest window keyframe's when the batch has
 already evicted it), and ``get_map`` returns the keyframes (BA estimates) and the window's
-landmarks.  With several pairs each keeps its own window (``handle.ba_read(p)``); the published
-pose stays the fused front end and ``get_map`` uses pair 0.
+landmarks.  With several pairs the keyframes of all pairs form ONE window of body poses (the
+rig-level solve, ``handle.ba_read(n_pairs)``; each pair keeps its landmarks, ``ba_read(p)``): the
+published pose is the rig's front end carried by the body correction ``B_ba(kf) inv(B_fe(kf))``,
+and ``get_map`` returns the body keyframes and every pair's landmarks.
 With ``dense_map`` (RGB-D input) every batch's depth of pair 0 is integrated into a dense TSDF
 volume on the device with the batch's tracked poses (nvblox's role in the reference pipeline,
 ``scripts/run_pipeline.py:218-256``); ``get_dense_map`` returns it.
@@ -144,6 +146,7 @@ class HipSlamEngine(SlamEngine):
         self._kf_final: dict[int, np.ndarray] = {}   # last BA estimate (rect world_T_cam) per keyframe
         self._kf_stamp: dict[int, float] = {}
         self._ba_window: dict | None = None
+        self._ba_pairs: list[dict] = []
         self._map_points: dict[int, tuple] = {}   # global landmark id -> (xyz rect-0 frame, desc, observations)
         self._map_offset = np.eye(4)              # map world <- session world, set by relocalize()
         self._map_loaded = False
@@ -505,16 +508,21 @@ class HipSlamEngine(SlamEngine):
         return status, rig["T_abs"][k].copy(), cov
 
     def _ba_corrections(self, res: dict, n: int, g0: int):
-        """Per frame of the batch: the rect-frame correction W_ba(kf) inv(W_fe(kf)) (or None)."""
+        """Per frame of the batch: the correction W_ba(kf) inv(W_fe(kf)) (or None) — rect-left
+        world_T_cam terms for one pair, world_T_body (base) terms for a rig's body window."""
         cfg = self._config
         if cfg.ba_window <= 0:
             return None
+        P = len(self._pairs)
+        rig = P > 1
         for k in range(n):
             if (g0 + k) % cfg.ba_kf_interval == 0:
-                self._fe_at[g0 + k] = res["T_abs"][k, 0].copy()
-        win = self._handle.ba_read(0)
+                self._fe_at[g0 + k] = (res["rig"]["T_abs"][k] if rig else res["T_abs"][k, 0]).copy()
+        win = self._handle.ba_read(P if rig else 0)
         self._ba_window = win
-        self._accumulate_map(win)
+        self._ba_pairs = [self._handle.ba_read(q) for q in range(P)] if rig else [win]
+        for q, w in enumerate(self._ba_pairs):
+            self._accumulate_map(w, q)
         live = {}
         for s_, f in enumerate(win["frames"]):
             if f >= 0:
@@ -522,7 +530,7 @@ class HipSlamEngine(SlamEngine):
                 self._kf_final[int(f)] = live[int(f)]
         for f in [f for f in self._fe_at if f not in live and f < min(live, default=0)]:
             del self._fe_at[f]   # evicted: its final estimate is kept in _kf_final
-        if not live or len(self._pairs) != 1:
+        if not live:
             return None
         frames = sorted(live)
         out = []
@@ -532,14 +540,18 @@ class HipSlamEngine(SlamEngine):
             out.append(live[kf] @ _invert(self._fe_at[kf]))
         return out
 
-    def _accumulate_map(self, win: dict) -> None:
-        """Merge the window's landmarks (latest BA positions) into the persistent map by global id."""
-        mp = self._handle.ba_read_map(0)
+    def _accumulate_map(self, win: dict, pair: int = 0) -> None:
+        """Merge a window's landmarks (latest BA positions) into the persistent map by global id
+        (rect-left frame of pair 0; a rig's pairs keep theirs apart: key gid * n_pairs + pair)."""
+        mp = self._handle.ba_read_map(pair)
+        P = len(self._pairs)
+        to_rect0 = _invert(self._base_T_rect) if P > 1 else np.eye(4)   # a rig's BA world is the base frame
         occ = win["frames"] >= 0
         ids, counts = np.unique(win["lm"][occ], return_counts=True)
         keep = ids >= 0
         for i, n in zip(ids[keep], counts[keep]):
-            self._map_points[int(mp["gid"][i])] = (win["X"][i].copy(), mp["desc"][i].copy(), int(n))
+            x = to_rect0[:3, :3] @ win["X"][i] + to_rect0[:3, 3]
+            self._map_points[int(mp["gid"][i]) * P + pair] = (x, mp["desc"][i].copy(), int(n))
 
     def _publish(self, res: dict, stamps: list[float], g0: int) -> None:
         if self._imu is not None and self._imu_batches:   # the filter absorbs the tracked motions
@@ -565,8 +577,8 @@ class HipSlamEngine(SlamEngine):
         bt = self._base_T_rect
         for k, ts in enumerate(stamps):
             status, body, cov = self._body_pose(res, k)
-            if corr is not None and status != POSE_LOST:
-                body = bt @ corr[k] @ res["T_abs"][k, 0] @ _invert(bt)
+            if corr is not None and status != POSE_LOST:   # a rig's correction is in body terms
+                body = corr[k] @ body if len(self._pairs) > 1 else bt @ corr[k] @ res["T_abs"][k, 0] @ _invert(bt)
             if self._loop is not None and status != POSE_LOST:
                 g = g0 + k
                 raw = _invert(bt) @ body @ bt                      # rect-left world_T_cam before loop correction
@@ -689,21 +701,23 @@ class HipSlamEngine(SlamEngine):
         elif self._config.ba_window <= 0 or self._ba_window is None:
             smap = SlamMap(keyframe_poses=list(self._keyframe_poses))
         else:
-            bt = self._base_T_rect
+            rig = len(self._pairs) > 1   # body window: keyframes are already world_T_base, landmarks in base
+            bt = np.eye(4) if rig else self._base_T_rect
             kfs = []
             for f in sorted(self._kf_final):
                 body = bt @ self._kf_final[f] @ _invert(bt)
                 kfs.append(SlamPose(position=body[:3, 3].copy(), rotation=Rotation.from_matrix(body[:3, :3]).as_quat(),
                                     timestamp=self._kf_stamp.get(f, float(f)), tracking_state=TrackingState.TRACKING,
                                     confidence=1.0))
-            win = self._ba_window
-            occ = win["frames"] >= 0
-            ids, counts = np.unique(win["lm"][occ], return_counts=True)
-            keep = ids >= 0
-            ids, counts = ids[keep], counts[keep]
-            pts = win["X"][ids] @ bt[:3, :3].T + bt[:3, 3]
-            smap = SlamMap(points=[MapPoint(position=p.copy(), observations=int(c)) for p, c in zip(pts, counts)],
-                           keyframe_poses=kfs)
+            points = []
+            for win in self._ba_pairs:
+                occ = win["frames"] >= 0
+                ids, counts = np.unique(win["lm"][occ], return_counts=True)
+                keep = ids >= 0
+                ids, counts = ids[keep], counts[keep]
+                pts = win["X"][ids] @ bt[:3, :3].T + bt[:3, 3]
+                points += [MapPoint(position=p.copy(), observations=int(c)) for p, c in zip(pts, counts)]
+            smap = SlamMap(points=points, keyframe_poses=kfs)
         pose = self._latest_pose
         if pose is not None:
             smap.timestamp = pose.timestamp
@@ -779,7 +793,7 @@ class HipSlamEngine(SlamEngine):
         if self._imu is not None:
             self._imu.reset()
         self._keyframe_poses = []
-        self._fe_at, self._kf_final, self._kf_stamp, self._ba_window = {}, {}, {}, None
+        self._fe_at, self._kf_final, self._kf_stamp, self._ba_window, self._ba_pairs = {}, {}, {}, None, []
         self._map_points, self._map_offset = {}, np.eye(4)
         if self._loop is not None:
             self._loop = _LoopGraph()
