@@ -516,23 +516,21 @@ __device__ __forceinline__ void hsum4(const uint8_t* row, int x0, int W, u16x2* 
 
 // MODE 0: speculative threshold (k_detect); MODE 1: exact fallback at t + 1 for the flagged
 // images (k_detect_fallback, its own symbol so profiles keep the two launches apart)
+// (bx: the band over all levels, img: the view image; the fallback runs only flagged image-levels)
 template <int MODE>
-__device__ __forceinline__ void detect_body(const BatchCtx& c) {
+__device__ __forceinline__ void detect_body(const BatchCtx& c, int bx, int img) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ uint32_t s_hist[256];
     __shared__ uint32_t s_count;
     __shared__ uint16_t s_q[TS_DET_WAVES][2][TS_DET_Q];   // per wave: bright, dark candidate quads
-    const int img = blockIdx.y;
     int f, cam;
     view_image(c, img, &f, &cam);
     int l = 0;
-    while (l + 1 < c.g.n_levels && (int)blockIdx.x >= c.g.band_start[l + 1]) ++l;
-    const size_t fcl = ((size_t)f * c.C + cam) * c.g.n_levels + l;
-    if (MODE == 1 && !c.det_fail[fcl]) return;   // fallback launch: only the flagged images
+    while (l + 1 < c.g.n_levels && bx >= c.g.band_start[l + 1]) ++l;
     // speculative threshold: scores below te cannot reach the level's top K (select checks it)
     const int te = MODE == 1 ? c.fast_threshold + 1
                                    : max(c.fast_threshold + 1, (int)c.det_thr[(size_t)cam * c.g.n_levels + l]);
-    const int band = blockIdx.x - c.g.band_start[l];
+    const int band = bx - c.g.band_start[l];
     const int W = c.g.W[l], H = c.g.H[l];
     const int BR = c.g.band_rows[l];
     const int y0 = band * BR;
@@ -776,7 +774,7 @@ __device__ __forceinline__ void detect_body(const BatchCtx& c) {
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) c.ccount[((size_t)f * c.C + cam) * c.g.total_bands + blockIdx.x] = s_count;
+    if (threadIdx.x == 0) c.ccount[((size_t)f * c.C + cam) * c.g.total_bands + bx] = s_count;
     uint32_t* gh = c.hist + (((size_t)f * c.C + cam) * c.g.n_levels + l) * 256;
     for (int i = threadIdx.x; i < 256; i += TS_DET_THREADS)
         if (s_hist[i]) atomicAdd(&gh[i], s_hist[i]);
@@ -785,9 +783,46 @@ __device__ __forceinline__ void detect_body(const BatchCtx& c) {
 // 6 waves per SIMD (VGPRs <= 80; 71 without spills at TS_DET_U = 2): three 512-thread blocks per CU, as the LDS
 // allows, instead of two at 84 VGPRs (567 -> 528 us per 256-frame batch alone)
 __global__ __launch_bounds__(TS_DET_THREADS) __attribute__((amdgpu_waves_per_eu(6))) void k_detect(BatchCtx c) {
-    detect_body<0>(c);
+    detect_body<0>(c, blockIdx.x, blockIdx.y);
 }
-__global__ __launch_bounds__(TS_DET_THREADS) void k_detect_fallback(BatchCtx c) { detect_body<1>(c); }
+
+// The exact fallback at t + 1 for the image-levels whose speculative select came short (rare):
+// TS_FB_BLOCKS persistent blocks scan the (image, level) flags, one per thread and a block-wide OR,
+// and run every band of a flagged image-level (detect) or its top-K (select) in turn.  With no
+// flag set a launch is one flag load per thread; the per-band / per-level grids of the
+// speculative kernels had cost ~55 us of empty blocks per 1024-frame batch on the critical path.
+#define TS_FB_BLOCKS 32
+template <typename F>
+__device__ __forceinline__ void for_flagged_levels(const BatchCtx& c, int nthreads, F&& fn) {
+    __shared__ int s_items[1024];
+    __shared__ int s_n;
+    const int L = c.g.n_levels, total = c.n * c.ncam * L;
+    for (int i0 = blockIdx.x * nthreads; i0 < total; i0 += gridDim.x * nthreads) {
+        if (threadIdx.x == 0) s_n = 0;
+        __syncthreads();
+        const int i = i0 + (int)threadIdx.x;
+        if (i < total) {
+            int f, cam;
+            view_image(c, i / L, &f, &cam);
+            if (c.det_fail[((size_t)f * c.C + cam) * L + i % L]) s_items[atomicAdd(&s_n, 1)] = i;
+        }
+        __syncthreads();
+        const int n = s_n;
+        for (int k = 0; k < n; ++k) {
+            fn(s_items[k] / L, s_items[k] % L);
+            __syncthreads();   // LDS reuse by the next item
+        }
+    }
+}
+
+__global__ __launch_bounds__(TS_DET_THREADS) void k_detect_fallback(BatchCtx c) {
+    for_flagged_levels(c, TS_DET_THREADS, [&](int img, int l) {
+        for (int b = 0; b < c.g.nbands[l]; ++b) {
+            detect_body<1>(c, c.g.band_start[l] + b, img);
+            __syncthreads();
+        }
+    });
+}
 
 // ---------------------------------------------------------------------------------------------
 // A4 top-K: exact K_l smallest keys of an image level, sorted ascending.
@@ -883,19 +918,16 @@ __device__ void bitonic_sort(uint32_t* a, int n) {
 }
 
 template <int MODE>
-__device__ __forceinline__ void select_body(const BatchCtx& c) {
+__device__ __forceinline__ void select_body(const BatchCtx& c, int img, int l) {
     __shared__ uint32_t s_keys[SEL_MAX];
     __shared__ uint32_t s_h[2048];
     __shared__ uint32_t s_part[SEL_THREADS];
     __shared__ uint32_t s_pref[SEL_THREADS + 1];
     __shared__ int s_bin;
     __shared__ uint32_t s_before, s_nsel, s_flag;
-    const int l = blockIdx.y;
-    const int img = blockIdx.x;
     int f, cam;
     view_image(c, img, &f, &cam);
     const size_t fcl = ((size_t)f * c.C + cam) * c.g.n_levels + l;
-    if (MODE == 1 && !c.det_fail[fcl]) return;   // fallback launch: only the flagged images
     const int Kl = c.g.Kq[l];
     const uint32_t* cand = c.cand + ((size_t)f * c.C + cam) * c.g.cand_total + c.g.cand_off[l];
     const uint32_t* cnt = c.ccount + ((size_t)f * c.C + cam) * c.g.total_bands + c.g.band_start[l];
@@ -1116,8 +1148,10 @@ __device__ __forceinline__ void select_body(const BatchCtx& c) {
     }
 }
 
-__global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) { select_body<0>(c); }
-__global__ __launch_bounds__(SEL_THREADS) void k_select_fallback(BatchCtx c) { select_body<1>(c); }
+__global__ __launch_bounds__(SEL_THREADS) void k_select(BatchCtx c) { select_body<0>(c, blockIdx.x, blockIdx.y); }
+__global__ __launch_bounds__(SEL_THREADS) void k_select_fallback(BatchCtx c) {
+    for_flagged_levels(c, SEL_THREADS, [&](int img, int l) { select_body<1>(c, img, l); });
+}
 
 // ---------------------------------------------------------------------------------------------
 // host launchers
@@ -1152,7 +1186,7 @@ void launch_select(const BatchCtx& c, hipStream_t s) {
     hipLaunchKernelGGL(k_select, grid, dim3(SEL_THREADS), 0, s, c);
     // fallback for images whose speculative threshold left fewer than K candidates: detect and
     // select again at t + 1, gated on the device flags (near-empty launches when none is set)
-    hipLaunchKernelGGL(k_detect_fallback, dim3(c.g.total_bands, c.n * c.ncam), dim3(TS_DET_THREADS), (size_t)c.g.det_lds, s, c);
-    hipLaunchKernelGGL(k_select_fallback, grid, dim3(SEL_THREADS), 0, s, c);
+    hipLaunchKernelGGL(k_detect_fallback, dim3(TS_FB_BLOCKS), dim3(TS_DET_THREADS), (size_t)c.g.det_lds, s, c);
+    hipLaunchKernelGGL(k_select_fallback, dim3(TS_FB_BLOCKS), dim3(SEL_THREADS), 0, s, c);
     hipLaunchKernelGGL(k_det_thr_commit, dim3(1), dim3(256), 0, s, c);
 }
