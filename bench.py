@@ -377,6 +377,36 @@ def tsdf_report(h, us: float, B: int, width: int, height: int) -> dict:
                          "frac": alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": alg}}
 
 
+def dense_outputs_report(h, reps: int = 10) -> dict:
+    """The dense-map outputs of the integrated volume (k_dense.hip): marching-cubes extraction
+    (count + scan + one 8-byte count read back + emit) and the capped ESDF (sites, three window
+    passes, finish), wall-clock per call after a synchronise, averaged over `reps` calls."""
+    import ctypes
+
+    import torch
+
+    nv = int(np.prod(TSDF_DIMS))
+    n = ctypes.c_int64()
+    out = {}
+    for name, call in (("mesh_extract", lambda: h.lib.tslam_mesh_extract(h.h, 1e-4, ctypes.byref(n), None)),
+                       ("esdf", lambda: h.lib.tslam_esdf_compute(h.h, 2.0, 1.0, 1e-4, None))):
+        call()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            call()
+        torch.cuda.synchronize()
+        out[name + "_us"] = (time.perf_counter() - t0) / reps * 1e6
+    # ESDF: tsdf + weight read once and the f32 field written (12 B per voxel) — the rest is cache
+    alg = nv * 12
+    out.update({"triangles": int(n.value), "esdf_max_distance_m": 2.0, "esdf_window_voxels": 40,
+                "esdf_voxels_per_s": nv / (out["esdf_us"] * 1e-6),
+                "esdf_roofline": {"bound": "hbm", "achieved": alg / (out["esdf_us"] * 1e-6) / 1e9, "peak": HBM_PEAK_GBS,
+                                  "unit": "GB/s", "frac": alg / (out["esdf_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                                  "algorithmic_bytes_per_call": alg}})
+    return out
+
+
 def pmc_traffic(args, dom: str, per_kernel_us: dict, B: int) -> tuple:
     """roofline.traffic (and the VALU-issue roofline) of the dominant kernel from the committed PMC
     summary (tools/pmc_summary.py) when its batch and config match this run."""
@@ -794,6 +824,7 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
         out["front_end_roofline"] = front_roofline
     if "tsdf" in names:
         out["dense_map"] = tsdf_report(h, per_kernel_us["tsdf"], B, width, height)
+        out["dense_map"]["outputs"] = dense_outputs_report(h)
     h.close()
     if rank == 0 and world == 1 and args.boundary_frames > 0 and args.config == "c2":
         out["boundary"] = boundary_bench(uniq, src, args.boundary_frames)

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 10
+#define TSLAM_ABI_VERSION 11
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -449,12 +449,37 @@ int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_e
  *   record stride) with camera poses world_T_cam[n][16] (host; a NaN pose skips its frame) or, when world_T_cam is NULL, the
  *   device-resident tracked poses of frames first_frame.. of the last batch (untracked frames are
  *   skipped).  Enqueued on `stream` (NULL: the handle's last stream).
- * tslam_tsdf_read: copy the volume out (synchronises); tsdf / weight may be NULL. */
+ * tslam_tsdf_read: copy the volume out (synchronises); tsdf / weight may be NULL.
+ * tslam_tsdf_write: replace the volume (a saved dense map reloaded; synchronises). */
 int tslam_tsdf_init(tslam_handle* h, const double* origin, const int32_t* dims, double voxel_size, double trunc_vox,
                     double max_dist, double max_weight);
 int tslam_tsdf_integrate(tslam_handle* h, int pair, const void* depth, int64_t stride_bytes, int n_frames,
                          int64_t first_frame, const double* world_T_cam, void* stream);
 int tslam_tsdf_read(tslam_handle* h, float* tsdf, float* weight);
+int tslam_tsdf_write(tslam_handle* h, const float* tsdf, const float* weight);
+
+/* Dense-map outputs of the TSDF volume — what nvblox publishes after integration (its mesh and
+ * ESDF / distance-slice outputs; launch/thor_nvblox.launch.py:21-103 starts the node the reference
+ * feeds).  Spec: thor_slam_amd/dense.py; CPU restatement: oracle/numpy_dense.py.  Every value
+ * follows from the volume alone (f32 tsdf / weight [nz][ny][nx]).
+ *
+ * tslam_mesh_extract: marching cubes over the voxel centres (cubes whose 8 voxels have weight >=
+ *   min_weight; inside = tsdf < 0) into the handle's triangle buffer, on `stream` (NULL: the
+ *   handle's last stream); waits for the triangle count only (*n_tris).
+ * tslam_mesh_read: copy the first min(max_tris, count) triangles out, 9 f32 each (three xyz
+ *   vertices in metres, facing positive tsdf), in cube order (synchronises).
+ * tslam_esdf_compute: exact Euclidean signed distance (m) of every observed voxel (weight >=
+ *   min_weight) to the nearest site (observed, |tsdf| <= site_vox * voxel), negative inside (tsdf
+ *   < 0), +-max_dist beyond floor(max_dist / voxel) voxels (<= 2048), NaN unobserved; enqueued on
+ *   `stream` into the handle's ESDF volume.
+ * tslam_esdf_read: copy the ESDF volume out (synchronises).
+ * tslam_esdf_slice: 2-D unsigned distance map out[nz][nx] over the height band y0 <= j < y1 (a
+ *   column is a site / observed when any of its band's voxels is; synchronous). */
+int tslam_mesh_extract(tslam_handle* h, double min_weight, int64_t* n_tris, void* stream);
+int tslam_mesh_read(tslam_handle* h, float* tris, int64_t max_tris);
+int tslam_esdf_compute(tslam_handle* h, double max_dist, double site_vox, double min_weight, void* stream);
+int tslam_esdf_read(tslam_handle* h, float* esdf);
+int tslam_esdf_slice(tslam_handle* h, int y0, int y1, double max_dist, double site_vox, double min_weight, float* out);
 
 #ifdef __cplusplus
 }

@@ -186,6 +186,21 @@ def test_engine_dense_map():
     np.testing.assert_array_equal(dm["tsdf"], want_t)
     bt = src.rig_T_source @ src.get_extrinsics()[0].to_4x4_matrix() @ rect.left_optical_T_rect()
     np.testing.assert_allclose(dm["world_T_volume"], bt, atol=1e-12)
+    # the dense-map outputs nvblox publishes, from the same volume (oracle/numpy_dense.py)
+    from oracle import numpy_dense as DN
+
+    mesh = eng.get_mesh()
+    want_m = DN.extract_mesh(want_t, want_w, ORIGIN, VOX, cfg.mesh_integrator_min_weight)
+    assert want_m.shape[0] > 1000
+    np.testing.assert_array_equal(mesh["triangles"].view(np.uint32), want_m.view(np.uint32))
+    es = eng.get_esdf()
+    want_e = DN.esdf(want_t, want_w, VOX, cfg.esdf_integrator_max_distance_m)
+    np.testing.assert_array_equal(es["esdf"].view(np.uint32), want_e.view(np.uint32))
+    sl = eng.get_esdf_slice()
+    y0, y1 = sl["band"]
+    assert y1 - y0 == 20
+    want_s = DN.esdf_slice(want_t, want_w, VOX, cfg.esdf_integrator_max_distance_m, y0, y1)
+    np.testing.assert_array_equal(sl["distance"].view(np.uint32), want_s.view(np.uint32))
     eng.reset()
     assert not eng.get_dense_map()["weight"].any()
     eng.shutdown()

@@ -100,6 +100,24 @@ struct tslam_handle {
     TsdfArgs tsdf{};
     double* d_tsdf_poses = nullptr;   // [TSDF_MAX_FRAMES][TSDF_POSE]
     double* d_tsdf_wTc = nullptr;     // [TSDF_MAX_FRAMES][16] host poses staged
+    // dense-map outputs (tslam_mesh_* / tslam_esdf_*): scratch sized on first use
+    uint8_t* d_mesh_cfg = nullptr;    // [cubes] configuration bytes
+    uint32_t* d_mesh_bsum = nullptr;  // [blocks] triangle totals
+    uint64_t* d_mesh_boff = nullptr;  // [blocks] first triangle; [blocks] = mesh total
+    size_t mesh_cubes_cap = 0;
+    float* d_mesh_tris = nullptr;     // [tri cap][9]
+    int64_t mesh_tris_cap = 0, mesh_n = 0;
+    int32_t* d_edt[2] = {nullptr, nullptr};
+    size_t edt_cap = 0;
+    float* d_esdf = nullptr;          // [nz][ny][nx]
+    size_t esdf_cap = 0;
+    bool esdf_valid = false;
+    float* d_dist_tab = nullptr;      // [R^2 + 1]
+    int dist_tab_R = -1;
+    double dist_tab_s = 0.0;
+    uint8_t* d_slice_obs = nullptr;
+    float* d_slice = nullptr;
+    size_t slice_cap = 0;
     Buffer buf[TSLAM_BUF_COUNT];
     uint32_t* d_cand = nullptr;
     uint32_t* d_ccount = nullptr;
@@ -1686,6 +1704,8 @@ int tslam_tsdf_init(tslam_handle* h, const double* origin, const int32_t* dims, 
     a.max_dist = max_dist;
     a.max_weight = max_weight;
     h->tsdf_on = true;
+    h->esdf_valid = false;   // outputs of the previous volume are gone
+    h->mesh_n = 0;
     return TSLAM_OK;
 }
 
@@ -1737,6 +1757,179 @@ int tslam_tsdf_read(tslam_handle* h, float* tsdf, float* weight) {
     const size_t nv = (size_t)h->tsdf.nx * h->tsdf.ny * h->tsdf.nz;
     if (tsdf) HIPCHK(hipMemcpy(tsdf, h->tsdf.tsdf, sizeof(float) * nv, hipMemcpyDeviceToHost));
     if (weight) HIPCHK(hipMemcpy(weight, h->tsdf.weight, sizeof(float) * nv, hipMemcpyDeviceToHost));
+    return TSLAM_OK;
+}
+
+int tslam_tsdf_write(tslam_handle* h, const float* tsdf, const float* weight) {
+    if (!h || !h->tsdf_on) return fail(TSLAM_ESTATE, "no TSDF volume (tslam_tsdf_init)");
+    if (!tsdf || !weight) return fail(TSLAM_EINVAL, "null volume");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    const size_t nv = (size_t)h->tsdf.nx * h->tsdf.ny * h->tsdf.nz;
+    HIPCHK(hipMemcpy(h->tsdf.tsdf, tsdf, sizeof(float) * nv, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->tsdf.weight, weight, sizeof(float) * nv, hipMemcpyHostToDevice));
+    h->esdf_valid = false;
+    return TSLAM_OK;
+}
+
+// -- dense-map outputs: marching-cubes mesh, ESDF, 2-D ESDF slice (k_dense.hip) ------------------
+static DenseArgs dense_args(const tslam_handle* h, double min_weight) {
+    const TsdfArgs& t = h->tsdf;
+    DenseArgs a{};
+    a.tsdf = t.tsdf;
+    a.weight = t.weight;
+    a.nx = t.nx;
+    a.ny = t.ny;
+    a.nz = t.nz;
+    a.n_cubes = (t.nx > 1 && t.ny > 1 && t.nz > 1) ? (uint32_t)((int64_t)(t.nx - 1) * (t.ny - 1) * (t.nz - 1)) : 0u;
+    a.n_voxels = (int64_t)t.nx * t.ny * t.nz;
+    a.ox = t.ox;
+    a.oy = t.oy;
+    a.oz = t.oz;
+    a.s = t.s;
+    a.sf = (float)t.s;
+    a.min_weight = (float)min_weight;
+    return a;
+}
+
+static int grow(tslam_handle* h, void** p, size_t* cap, size_t need) {
+    if (*cap >= need && *p) return TSLAM_OK;
+    const int rc = dev_realloc(h, p, need);
+    *cap = rc == TSLAM_OK ? need : 0;
+    return rc;
+}
+
+int tslam_mesh_extract(tslam_handle* h, double min_weight, int64_t* n_tris, void* stream) {
+    if (!h || !h->tsdf_on) return fail(TSLAM_ESTATE, "no TSDF volume (tslam_tsdf_init)");
+    if (!(min_weight >= 0.0)) return fail(TSLAM_EINVAL, "min_weight must be >= 0");
+    HIPCHK(hipSetDevice(h->device));
+    hipStream_t s = stream ? (hipStream_t)stream : h->last_stream;
+    const DenseArgs a = dense_args(h, min_weight);
+    h->mesh_n = 0;
+    if (a.n_cubes == 0) {
+        if (n_tris) *n_tris = 0;
+        return TSLAM_OK;
+    }
+    const size_t nb = (a.n_cubes + 255) / 256;
+    size_t cap = h->mesh_cubes_cap;
+    if (cap < a.n_cubes) {   // the three scratch arrays follow the cube count
+        size_t c0 = 0, c1 = 0, c2 = 0;
+        int rc = grow(h, (void**)&h->d_mesh_cfg, &c0, a.n_cubes);
+        if (rc == TSLAM_OK) rc = grow(h, (void**)&h->d_mesh_bsum, &c1, sizeof(uint32_t) * nb);
+        if (rc == TSLAM_OK) rc = grow(h, (void**)&h->d_mesh_boff, &c2, sizeof(uint64_t) * (nb + 1));
+        if (rc != TSLAM_OK) return rc;
+        h->mesh_cubes_cap = a.n_cubes;
+    }
+    launch_mesh_count(a, h->d_mesh_cfg, h->d_mesh_bsum, h->d_mesh_boff, h->d_mesh_boff + nb, s);
+    HIPCHK(hipGetLastError());
+    uint64_t total = 0;   // the buffer is sized to the count: one small read back
+    HIPCHK(hipMemcpyAsync(&total, h->d_mesh_boff + nb, sizeof(total), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if ((int64_t)total > h->mesh_tris_cap) {
+        size_t c = 0;
+        const int64_t want = (int64_t)total + (int64_t)total / 4 + 1024;
+        const int rc = grow(h, (void**)&h->d_mesh_tris, &c, sizeof(float) * 9 * (size_t)want);
+        if (rc != TSLAM_OK) return rc;
+        h->mesh_tris_cap = want;
+    }
+    launch_mesh_emit(a, h->d_mesh_cfg, h->d_mesh_boff, h->d_mesh_tris, h->mesh_tris_cap, s);
+    HIPCHK(hipGetLastError());
+    h->mesh_n = (int64_t)total;
+    if (n_tris) *n_tris = (int64_t)total;
+    return TSLAM_OK;
+}
+
+int tslam_mesh_read(tslam_handle* h, float* tris, int64_t max_tris) {
+    if (!h || !h->tsdf_on) return fail(TSLAM_ESTATE, "no TSDF volume (tslam_tsdf_init)");
+    if (max_tris < 0 || (max_tris > 0 && !tris)) return fail(TSLAM_EINVAL, "bad buffer");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    const int64_t n = std::min(max_tris, h->mesh_n);
+    if (n > 0) HIPCHK(hipMemcpy(tris, h->d_mesh_tris, sizeof(float) * 9 * (size_t)n, hipMemcpyDeviceToHost));
+    return TSLAM_OK;
+}
+
+// f32 distance of every squared voxel distance 0..R^2 (sqrt in f32, times s in f32, IEEE on the host)
+static int dist_table(tslam_handle* h, int R, double s) {
+    if (h->dist_tab_R == R && h->dist_tab_s == s && h->d_dist_tab) return TSLAM_OK;
+    const size_t n = (size_t)R * R + 1;
+    std::vector<float> tab(n);
+    const float sf = (float)s;
+    for (size_t d = 0; d < n; ++d) tab[d] = std::sqrt((float)d) * sf;
+    const int rc = dev_realloc(h, (void**)&h->d_dist_tab, sizeof(float) * n);
+    if (rc != TSLAM_OK) return rc;
+    HIPCHK(hipMemcpy(h->d_dist_tab, tab.data(), sizeof(float) * n, hipMemcpyHostToDevice));
+    h->dist_tab_R = R;
+    h->dist_tab_s = s;
+    return TSLAM_OK;
+}
+
+static int esdf_setup(tslam_handle* h, double max_dist, double site_vox, double min_weight, size_t cells, DenseArgs* a,
+                      int* R) {
+    if (!h || !h->tsdf_on) return fail(TSLAM_ESTATE, "no TSDF volume (tslam_tsdf_init)");
+    if (!(max_dist > 0.0) || !(site_vox >= 0.0) || !(min_weight >= 0.0))
+        return fail(TSLAM_EINVAL, "max_dist must be > 0, site_vox and min_weight >= 0");
+    const double r = std::floor(max_dist / h->tsdf.s + 1e-9);
+    if (r < 0.0 || r > 2048.0) return fail(TSLAM_EINVAL, "max_dist / voxel_size must be at most 2048 voxels");
+    HIPCHK(hipSetDevice(h->device));
+    *R = (int)r;
+    *a = dense_args(h, min_weight);
+    a->site_dist = (float)(site_vox * h->tsdf.s);
+    a->max_dist = (float)max_dist;
+    a->cap = *R * *R + 1;
+    int rc = dist_table(h, *R, h->tsdf.s);
+    if (rc == TSLAM_OK && h->edt_cap < cells) {
+        size_t c0 = 0, c1 = 0;
+        rc = grow(h, (void**)&h->d_edt[0], &c0, sizeof(int32_t) * cells);
+        if (rc == TSLAM_OK) rc = grow(h, (void**)&h->d_edt[1], &c1, sizeof(int32_t) * cells);
+        h->edt_cap = rc == TSLAM_OK ? cells : 0;
+    }
+    return rc;
+}
+
+int tslam_esdf_compute(tslam_handle* h, double max_dist, double site_vox, double min_weight, void* stream) {
+    DenseArgs a;
+    int R = 0;
+    const size_t nv = h && h->tsdf_on ? (size_t)h->tsdf.nx * h->tsdf.ny * h->tsdf.nz : 0;
+    int rc = esdf_setup(h, max_dist, site_vox, min_weight, nv, &a, &R);
+    if (rc == TSLAM_OK) rc = grow(h, (void**)&h->d_esdf, &h->esdf_cap, sizeof(float) * nv);
+    if (rc != TSLAM_OK) return rc;
+    hipStream_t s = stream ? (hipStream_t)stream : h->last_stream;
+    launch_esdf(a, R, h->d_dist_tab, h->d_edt[0], h->d_edt[1], h->d_esdf, s);
+    HIPCHK(hipGetLastError());
+    h->esdf_valid = true;
+    return TSLAM_OK;
+}
+
+int tslam_esdf_read(tslam_handle* h, float* esdf) {
+    if (!h || !h->tsdf_on || !h->esdf_valid) return fail(TSLAM_ESTATE, "no ESDF (tslam_esdf_compute)");
+    if (!esdf) return fail(TSLAM_EINVAL, "null buffer");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    const size_t nv = (size_t)h->tsdf.nx * h->tsdf.ny * h->tsdf.nz;
+    HIPCHK(hipMemcpy(esdf, h->d_esdf, sizeof(float) * nv, hipMemcpyDeviceToHost));
+    return TSLAM_OK;
+}
+
+int tslam_esdf_slice(tslam_handle* h, int y0, int y1, double max_dist, double site_vox, double min_weight, float* out) {
+    if (!h || !h->tsdf_on) return fail(TSLAM_ESTATE, "no TSDF volume (tslam_tsdf_init)");
+    if (!out || y0 < 0 || y1 <= y0 || y1 > h->tsdf.ny) return fail(TSLAM_EINVAL, "need 0 <= y0 < y1 <= ny and a buffer");
+    DenseArgs a;
+    int R = 0;
+    const size_t nc = (size_t)h->tsdf.nx * h->tsdf.nz;
+    int rc = esdf_setup(h, max_dist, site_vox, min_weight, nc, &a, &R);
+    if (rc == TSLAM_OK && h->slice_cap < nc) {
+        size_t c0 = 0, c1 = 0;
+        rc = grow(h, (void**)&h->d_slice_obs, &c0, nc);
+        if (rc == TSLAM_OK) rc = grow(h, (void**)&h->d_slice, &c1, sizeof(float) * nc);
+        h->slice_cap = rc == TSLAM_OK ? nc : 0;
+    }
+    if (rc != TSLAM_OK) return rc;
+    hipStream_t s = h->last_stream;
+    launch_esdf_slice(a, y0, y1, R, h->d_dist_tab, h->d_edt[0], h->d_edt[1], h->d_slice_obs, h->d_slice, s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipMemcpy(out, h->d_slice, sizeof(float) * nc, hipMemcpyDeviceToHost));
     return TSLAM_OK;
 }
 

@@ -240,6 +240,27 @@ struct TsdfArgs {
 };
 void launch_tsdf(const BatchCtx& c, int pair, int f0, const double* host_wTc_dev, const TsdfArgs& a, double* poses,
                  hipStream_t s);
+// dense-map outputs of the TSDF volume (k_dense.hip): marching-cubes mesh, capped exact ESDF
+struct DenseArgs {
+    const float* tsdf;
+    const float* weight;
+    int nx, ny, nz;
+    uint32_t n_cubes;          // (nx - 1)(ny - 1)(nz - 1)
+    int64_t n_voxels;
+    double ox, oy, oz, s;      // volume corner and voxel size (voxel centres in f64, rounded to f32)
+    float sf;                  // (float)s
+    float min_weight;          // observed: weight >= min_weight
+    float site_dist;           // ESDF site: |tsdf| <= site_dist
+    float max_dist;            // ESDF value beyond R voxels
+    int32_t cap;               // R^2 + 1
+};
+void launch_mesh_count(const DenseArgs& a, uint8_t* cfg, uint32_t* block_sums, uint64_t* block_off, uint64_t* total,
+                       hipStream_t s);
+void launch_mesh_emit(const DenseArgs& a, const uint8_t* cfg, const uint64_t* block_off, float* tris, int64_t cap,
+                      hipStream_t s);
+void launch_esdf(const DenseArgs& a, int R, const float* tab, int32_t* g0, int32_t* g1, float* out, hipStream_t s);
+void launch_esdf_slice(const DenseArgs& a, int y0, int y1, int R, const float* tab, int32_t* g0, int32_t* g1,
+                       uint8_t* obs, float* out, hipStream_t s);
 void launch_rgbd_gray(const BatchCtx& c, uint8_t* gray, hipStream_t s);
 void launch_rgbd_depth(const BatchCtx& c, hipStream_t s);
 

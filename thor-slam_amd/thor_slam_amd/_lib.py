@@ -166,6 +166,13 @@ _SIGNATURES = {
     "tslam_tsdf_integrate": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
                                             ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_tsdf_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_tsdf_write": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_mesh_extract": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
+    "tslam_mesh_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
+    "tslam_esdf_compute": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_void_p]),
+    "tslam_esdf_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_esdf_slice": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                        ctypes.c_double, ctypes.c_void_p]),
     "tslam_pose_graph": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
 }
@@ -647,6 +654,42 @@ class Handle:
         w = np.zeros((nz, ny, nx), dtype=np.float32)
         _check(self.lib.tslam_tsdf_read(self.h, t.ctypes.data, w.ctypes.data))
         return t, w
+
+    def tsdf_write(self, tsdf: np.ndarray, weight: np.ndarray) -> None:
+        """Replace the volume (f32 [nz][ny][nx] each; synchronises)."""
+        nx, ny, nz = self._tsdf_dims
+        t = np.ascontiguousarray(tsdf, dtype=np.float32)
+        w = np.ascontiguousarray(weight, dtype=np.float32)
+        if t.shape != (nz, ny, nx) or w.shape != (nz, ny, nx):
+            raise ValueError(f"volume must be {(nz, ny, nx)}")
+        _check(self.lib.tslam_tsdf_write(self.h, t.ctypes.data, w.ctypes.data))
+
+    # -- dense-map outputs (nvblox's mesh / ESDF / distance slice; thor_slam_amd/dense.py) -------
+    def mesh(self, min_weight: float = 1e-4, stream: int = 0) -> np.ndarray:
+        """Marching-cubes triangle soup [n][3][3] f32 (metres), cube order (synchronises)."""
+        n = ctypes.c_int64()
+        _check(self.lib.tslam_mesh_extract(self.h, float(min_weight), ctypes.byref(n), ctypes.c_void_p(stream)))
+        out = np.zeros((n.value, 3, 3), dtype=np.float32)
+        _check(self.lib.tslam_mesh_read(self.h, out.ctypes.data, int(n.value)))
+        return out
+
+    def esdf(self, max_dist: float = 2.0, site_vox: float = 1.0, min_weight: float = 1e-4, stream: int = 0) -> np.ndarray:
+        """Signed distance field f32 [nz][ny][nx] (NaN = unobserved; synchronises)."""
+        nx, ny, nz = self._tsdf_dims
+        _check(self.lib.tslam_esdf_compute(self.h, float(max_dist), float(site_vox), float(min_weight),
+                                           ctypes.c_void_p(stream)))
+        out = np.zeros((nz, ny, nx), dtype=np.float32)
+        _check(self.lib.tslam_esdf_read(self.h, out.ctypes.data))
+        return out
+
+    def esdf_slice(self, y0: int, y1: int, max_dist: float = 2.0, site_vox: float = 1.0,
+                   min_weight: float = 1e-4) -> np.ndarray:
+        """2-D distance map f32 [nz][nx] over the height band y0 <= j < y1 (NaN = unobserved column)."""
+        nx, ny, nz = self._tsdf_dims
+        out = np.zeros((nz, nx), dtype=np.float32)
+        _check(self.lib.tslam_esdf_slice(self.h, int(y0), int(y1), float(max_dist), float(site_vox), float(min_weight),
+                                         out.ctypes.data))
+        return out
 
     def ba_replay_schur(self, pair: int = 0, reps: int = 50, stream: int = 0) -> dict:
         """Average k_ba_schur duration (HIP events around ``reps`` replays) and flops per launch."""

@@ -90,6 +90,15 @@ class HipSlamConfig(SlamConfig):
     # x right, y down, z forward): corner (m) and voxel counts (x, y, z); 10 x 4 x 11 m by default
     tsdf_origin: tuple = (-5.0, -2.0, -1.0)
     tsdf_dims: tuple = (200, 80, 220)
+    # dense-map outputs (get_mesh / get_esdf / get_esdf_slice; thor_slam_amd/dense.py): nvblox's
+    # mesh / ESDF integrator parameters (its defaults: min weight 1e-4, ESDF max distance 2 m, site
+    # distance 1 voxel) and the 2-D slice's height band (y down: metres in the tracking world)
+    mesh_integrator_min_weight: float = 1e-4
+    esdf_integrator_min_weight: float = 1e-4
+    esdf_integrator_max_distance_m: float = 2.0
+    esdf_integrator_max_site_distance_vox: float = 1.0
+    esdf_slice_min_height: float = -0.5
+    esdf_slice_max_height: float = 0.5
     # pipeline
     batch_size: int = 1             # frames per submission (1 = synchronous latency mode)
     # one camera stream per GPU from one process (the rig cuVSLAM's multicam mode

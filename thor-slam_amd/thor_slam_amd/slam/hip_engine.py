@@ -484,6 +484,46 @@ class HipSlamEngine(SlamEngine):
                 "truncation_m": cfg.tsdf_integrator_truncation_distance_vox * cfg.voxel_size,
                 "world_T_volume": self._map_offset @ self._base_T_rect}
 
+    def get_mesh(self) -> dict | None:
+        """The surface mesh of the TSDF volume (marching cubes on the device, k_dense.hip):
+        ``triangles`` f32 [n][3][3] (metres in the tracking world, facing free space) and
+        ``world_T_volume``.  None unless ``dense_map`` is on.  Synchronises."""
+        cfg = self._config
+        if not cfg.dense_map or self._handle is None:
+            return None
+        self.flush()
+        return {"triangles": self._handle.mesh(cfg.mesh_integrator_min_weight),
+                "world_T_volume": self._map_offset @ self._base_T_rect}
+
+    def get_esdf(self) -> dict | None:
+        """The Euclidean signed distance field of the volume (k_dense.hip): ``esdf`` f32
+        [nz][ny][nx] (metres, negative inside, +-esdf_integrator_max_distance_m beyond it, NaN
+        unobserved) on the TSDF grid.  None unless ``dense_map`` is on.  Synchronises."""
+        cfg = self._config
+        if not cfg.dense_map or self._handle is None:
+            return None
+        self.flush()
+        esdf = self._handle.esdf(cfg.esdf_integrator_max_distance_m, cfg.esdf_integrator_max_site_distance_vox,
+                                 cfg.esdf_integrator_min_weight)
+        return {"esdf": esdf, "origin": np.array(cfg.tsdf_origin, dtype=np.float64), "voxel_size": float(cfg.voxel_size),
+                "world_T_volume": self._map_offset @ self._base_T_rect}
+
+    def get_esdf_slice(self) -> dict | None:
+        """nvblox's 2-D distance map: unsigned distance f32 [nz][nx] to the nearest surface voxel of
+        the height band [esdf_slice_min_height, esdf_slice_max_height) (tracking-world y), NaN
+        where the band was never observed.  None unless ``dense_map`` is on.  Synchronises."""
+        cfg = self._config
+        if not cfg.dense_map or self._handle is None:
+            return None
+        self.flush()
+        s, y_org, ny = cfg.voxel_size, cfg.tsdf_origin[1], int(cfg.tsdf_dims[1])
+        y0 = int(np.clip(np.floor((cfg.esdf_slice_min_height - y_org) / s), 0, ny - 1))
+        y1 = int(np.clip(np.ceil((cfg.esdf_slice_max_height - y_org) / s), y0 + 1, ny))
+        dist = self._handle.esdf_slice(y0, y1, cfg.esdf_integrator_max_distance_m,
+                                       cfg.esdf_integrator_max_site_distance_vox, cfg.esdf_integrator_min_weight)
+        return {"distance": dist, "band": (y0, y1), "origin": np.array(cfg.tsdf_origin, dtype=np.float64),
+                "voxel_size": float(s), "world_T_volume": self._map_offset @ self._base_T_rect}
+
     def _read(self, n: int) -> dict:
         res = self._handle.read_poses(n)
         if len(self._pairs) > 1:
