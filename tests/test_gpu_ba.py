@@ -145,6 +145,30 @@ def test_engine_publishes_ba_poses_and_map():
     eng.shutdown()
 
 
+@pytest.mark.parametrize("mapping,cap", [(True, 50), (False, 100000)])
+def test_engine_map_size_and_mapping_switch(mapping, cap):
+    """SlamConfig.max_map_size bounds the persistent map, enable_mapping=False keeps none
+    (reference fields thor_slam/slam/interface.py:110-111); poses are unaffected."""
+    from thor_slam_amd.camera import CameraRig, Extrinsics
+    from thor_slam_amd.params import HipSlamConfig
+    from thor_slam_amd.slam.hip_engine import HipSlamEngine
+
+    from helpers import make_source
+
+    src = make_source(0)
+    rig = CameraRig([src], rig_extrinsics={src.name: Extrinsics.from_4x4_matrix(src.rig_T_source)})
+    rig.start()
+    eng = HipSlamEngine(num_cameras=2, config=HipSlamConfig(batch_size=1, enable_mapping=mapping, max_map_size=cap,
+                                                            **dict(BA_ITEMS)))
+    eng.initialize(rig.calibration)
+    for _ in range(8):
+        eng.process_frames(rig.get_synchronized_frames())
+    smap = eng.get_map()
+    assert len(smap.points) == (cap if mapping else 0)
+    assert len(smap.keyframe_poses) == 4
+    eng.shutdown()
+
+
 def test_ba_on_its_own_stream_matches():
     """The BA stage on a second stream, overlapping the next batches' front end (the library
     orders it with events and a pose snapshot): same windows as the oracle."""

@@ -582,7 +582,12 @@ class HipSlamEngine(SlamEngine):
 
     def _accumulate_map(self, win: dict, pair: int = 0) -> None:
         """Merge a window's landmarks (latest BA positions) into the persistent map by global id
-        (rect-left frame of pair 0; a rig's pairs keep theirs apart: key gid * n_pairs + pair)."""
+        (rect-left frame of pair 0; a rig's pairs keep theirs apart: key gid * n_pairs + pair).
+        ``SlamConfig.enable_mapping`` off keeps no map; ``max_map_size`` bounds it (the landmarks
+        updated longest ago go first; interface.py:110-111)."""
+        cfg = self._config
+        if not cfg.enable_mapping:
+            return
         mp = self._handle.ba_read_map(pair)
         P = len(self._pairs)
         to_rect0 = _invert(self._base_T_rect) if P > 1 else np.eye(4)   # a rig's BA world is the base frame
@@ -591,7 +596,11 @@ class HipSlamEngine(SlamEngine):
         keep = ids >= 0
         for i, n in zip(ids[keep], counts[keep]):
             x = to_rect0[:3, :3] @ win["X"][i] + to_rect0[:3, 3]
-            self._map_points[int(mp["gid"][i]) * P + pair] = (x, mp["desc"][i].copy(), int(n))
+            key = int(mp["gid"][i]) * P + pair
+            self._map_points.pop(key, None)   # re-inserted: most recently updated last
+            self._map_points[key] = (x, mp["desc"][i].copy(), int(n))
+        while len(self._map_points) > max(int(cfg.max_map_size), 0):
+            del self._map_points[next(iter(self._map_points))]
 
     def _publish(self, res: dict, stamps: list[float], g0: int) -> None:
         if self._imu is not None and self._imu_batches:   # the filter absorbs the tracked motions
@@ -757,6 +766,8 @@ class HipSlamEngine(SlamEngine):
                 ids, counts = ids[keep], counts[keep]
                 pts = win["X"][ids] @ bt[:3, :3].T + bt[:3, 3]
                 points += [MapPoint(position=p.copy(), observations=int(c)) for p, c in zip(pts, counts)]
+            # SlamConfig.enable_mapping / max_map_size (interface.py:110-111)
+            points = points[:max(int(self._config.max_map_size), 0)] if self._config.enable_mapping else []
             smap = SlamMap(points=points, keyframe_poses=kfs)
         pose = self._latest_pose
         if pose is not None:
