@@ -377,6 +377,28 @@ def tsdf_report(h, us: float, B: int, width: int, height: int) -> dict:
                          "frac": alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": alg}}
 
 
+def cu_masked_stream(dev_index: int, reserve: int, priority: int):
+    """A torch stream whose kernels may use every CU but the last `reserve` (hipExtStreamCreateWithCUMask)."""
+    import ctypes
+
+    import torch
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    n_cu = torch.cuda.get_device_properties(dev_index).multi_processor_count
+    words = (n_cu + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    for cu in range(n_cu - reserve):
+        mask[cu // 32] |= 1 << (cu % 32)
+    st = ctypes.c_void_p()
+    torch.cuda.set_device(dev_index)
+    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words), mask)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+    if priority:
+        pass   # CU-masked streams take the default priority
+    return torch.cuda.ExternalStream(st.value, device=torch.device("cuda", dev_index))
+
+
 def dense_outputs_report(h, reps: int = 10) -> dict:
     """The dense-map outputs of the integrated volume (k_dense.hip): marching-cubes extraction
     (count + scan + one 8-byte count read back + emit) and the capped ESDF (sites, three window
@@ -572,6 +594,9 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     # the front stream (rectify .. describe) is the critical path of the pipelined step: with
     # --front-priority 1 it is a high-priority stream, so the back kernels fill the gaps around it
     stream = (torch.cuda.Stream(priority=-1) if args.front_priority and args.pipeline else torch.cuda.current_stream())
+    masked = c4 and args.front_cu_reserve > 0 and args.pipeline
+    if masked:   # C4: the front / back kernels kept off the last CUs, which stay free for the BA chain
+        stream = cu_masked_stream(dev_index, args.front_cu_reserve, -1 if args.front_priority else 0)
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
     # the rig pose runs before the chains (KERNEL_CHAIN chains the pairs and the rig in one launch)
@@ -583,7 +608,7 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     # two streams: the front kernels (rectify .. describe) of batch s + 1 overlap the back kernels
     # (match .. chain) of batch s; the library orders batch s's back after its front and batch s's
     # front after the back of batch s - 2 (ring slots)
-    bstream = torch.cuda.Stream() if args.pipeline else stream
+    bstream = (cu_masked_stream(dev_index, args.front_cu_reserve, 0) if masked else torch.cuda.Stream()) if args.pipeline else stream
     bsp = bstream.cuda_stream
     back_done = [torch.cuda.Event(), torch.cuda.Event()]
     back_issued = [False, False]
@@ -1060,6 +1085,8 @@ def main() -> None:
                     help="sharded rig: all-to-all of the frames each rank solves, or all-gather of everything")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="1: front and back kernels on two streams (batch s+1's front overlaps batch s's back)")
+    ap.add_argument("--front-cu-reserve", type=int, default=0,
+                    help="C4: keep the front / back kernels off the last N CUs (left to the BA chain)")
     ap.add_argument("--front-priority", type=int, default=1,
                     help="1: run the front kernels on a high-priority stream (pipelined mode)")
     ap.add_argument("--tsdf", type=int, default=0,
