@@ -255,9 +255,73 @@ int tslam_layout(tslam_handle* h, int64_t* out16, int32_t* level_info18);
  * A7's Gauss-Newton then minimises sum |reprojection|^2 + W_r |log(R_prior R^T)|^2 (small-angle
  * form) + W_t |t - t_prior|^2; RANSAC is unchanged.  A frame that is not tracked (LOST) but has
  * W_t > 0 is chained with the prediction (its T_rel record becomes [R | t]; status stays LOST),
- * so the trajectory continues through visual dropouts.  thor_slam_amd/imu.py computes the
+ * so the trajectory continues through visual dropouts.  The tslam_imu_* filter below computes the
  * priors from the samples (gyro integration, velocity / gravity / accelerometer-bias filter). */
 int tslam_set_motion_prior(tslam_handle* h, const double* prior, int n_frames);
+
+/* The IMU filter behind those priors (host-side, native; the fusion cuVSLAM runs inside its
+ * library with enable_imu_fusion:=true, Makefile:81, on the IMUData of each
+ * SynchronizedFrameSet, types.py:268-269 / rig.py:403-407).  State: the rectified-left camera's
+ * orientation in the filter's world, the world velocity, gravity, the accelerometer and gyroscope
+ * biases (IMU axes) and their variances.  Noise (TSLAM_IMU_NOISE doubles): gyroscope noise
+ * density and random walk, accelerometer noise density and random walk
+ * (launch/thor_visual_slam.launch.py:82-90), rotation / translation prior floors, initial
+ * velocity / accelerometer-bias / gyroscope-bias sigmas, the vision's rotation floor.
+ *   tslam_imu_create: rect_R_imu (row-major), lever = the IMU's position in the camera frame (m),
+ *     accel = 0 for the gyro-only filter.  tslam_imu_begin: anchor at rest (accel: one sample in
+ *     IMU axes; NULL when gyro-only).
+ *   tslam_imu_predict / _coast / _correct: one frame interval's prediction from a state, the state
+ *     after an untracked interval, the state after a tracked one (T_rel row-major 4x4 mapping frame
+ *     k points to frame k + 1, cov the 6x6 (rho, omega) covariance).
+ *   tslam_imu_batch_priors: the next batch's predictions (dt[k] NaN = no sample -> valid[k] = 0),
+ *     the state coasted over the batch's earlier frames; tslam_imu_absorb: the batch's tracked
+ *     motions (status 0 = tracked) into the filter's state.
+ *   tslam_imu_vision_only: the vision-only motion and covariance behind a solution the device
+ *     weighted with a step's prior (one Gauss-Newton step on the vision alone; sigma2 from the pose
+ *     stats); T / cov copied through when no prior acted or the vision's normal matrix is not
+ *     positive definite.
+ * Spec: oracle/numpy_imu.py. */
+#define TSLAM_IMU_NOISE 10
+typedef struct tslam_imu tslam_imu;
+typedef struct tslam_imu_state {
+    double R[9];          /* world_R_cam */
+    double v[3];          /* world velocity, m/s */
+    double ba[3];         /* accelerometer bias, IMU axes */
+    double var_v, var_b;
+    double bg[3];         /* gyroscope bias, IMU axes */
+    double var_g;
+    double w_prev[3];     /* previous interval's camera-axes rate (valid when has_w_prev) */
+    int32_t has_w_prev, reserved;
+} tslam_imu_state;
+typedef struct tslam_imu_step {
+    double dt;
+    double gyro[3];
+    double w[3];          /* bias-corrected rate, camera axes */
+    double R_rel[9];
+    double t_rel[3];
+    double w_rot, w_trans;
+    double v1[3];         /* predicted velocity (valid when has_v1) */
+    double var_v1;
+    int32_t has_v1, reserved;
+} tslam_imu_step;
+int tslam_imu_create(const double* rect_R_imu, const double* noise, const double* lever, int accel, tslam_imu** out);
+void tslam_imu_destroy(tslam_imu* f);
+int tslam_imu_reset(tslam_imu* f);
+int tslam_imu_begin(tslam_imu* f, const double* accel);
+int tslam_imu_ready(const tslam_imu* f);
+int tslam_imu_get_state(const tslam_imu* f, tslam_imu_state* st);
+int tslam_imu_set_state(tslam_imu* f, const tslam_imu_state* st);
+int tslam_imu_predict(const tslam_imu* f, const tslam_imu_state* st, double dt, const double* gyro, const double* accel,
+                   tslam_imu_step* out);
+int tslam_imu_coast(const tslam_imu* f, const tslam_imu_state* st, const tslam_imu_step* s, tslam_imu_state* out);
+int tslam_imu_correct(const tslam_imu* f, const tslam_imu_state* st, const tslam_imu_step* s, const double* t_rel,
+                      const double* cov, tslam_imu_state* out);
+int tslam_imu_batch_priors(const tslam_imu* f, int n, const double* dt, const double* gyro, const double* accel,
+                           tslam_imu_step* out, int32_t* valid);
+int tslam_imu_absorb(tslam_imu* f, int n, const double* dt, const double* gyro, const double* accel,
+                     const int32_t* status, const double* t_rel, const double* cov);
+int tslam_imu_vision_only(const double* T, const double* cov, double sigma2, const tslam_imu_step* s, double* T_out,
+                          double* cov_out);
 
 /* Rig pose (replaces the multi-camera fusion cuVSLAM does for the rig of
  * isaac_ros.py:364-411): base_T_rect[P][16] = the rectified-left frame of each pair in the rig's

@@ -130,3 +130,38 @@ def test_gyro_bias_estimate_converges():
         prod.st = prod.correct(prod.st, s, t, np.diag([1e-6] * 3 + [(3e-5) ** 2] * 3))
     assert np.linalg.norm(prod.st.bg - bias) < 0.1 * np.linalg.norm(bias), prod.st.bg
     assert last_err < 0.2 * first_err, (first_err, last_err)
+
+
+def test_vision_only_matches_oracle():
+    """The native tslam_imu_vision_only against the spec's vision_only: a prior-weighted solution
+    moved back to the vision alone (pose and covariance), and the pass-through cases."""
+    from thor_slam_amd.imu import vision_only
+
+    prod, _ = _pair(True)
+    src = SyntheticStereoSource(seed=5, n_frames=4)
+    smp = _samples(src, 3)
+    prod.begin(smp[0][2])
+    s = prod.step(prod.st, *smp[1])
+    rng = np.random.default_rng(11)
+    for trial in range(20):
+        A = rng.standard_normal((6, 6))
+        cov = (A @ A.T + 6 * np.eye(6)) * 1e-10   # the vision well determined: H_v positive definite
+        T = np.eye(4)
+        T[:3, :3] = Rotation.from_rotvec(rng.normal(0, 0.01, 3)).as_matrix() @ s.R_rel
+        T[:3, 3] = s.t_rel + rng.normal(0, 1e-3, 3)
+        sigma2 = float(rng.uniform(0.5, 2.0))
+        got_T, got_C = vision_only(T, cov, sigma2, s)
+        want_T, want_C = OI.vision_only(T, cov, sigma2, (s.R_rel, s.w_rot, s.t_rel, s.w_trans))
+        np.testing.assert_allclose(got_T, want_T, rtol=0, atol=1e-12)
+        np.testing.assert_allclose(got_C, want_C, rtol=1e-9, atol=1e-22)
+        if trial == 0:
+            assert np.abs(got_T - T).max() > 0   # the prior acted: the vision-only pose differs
+    # pass-through: no sigma^2, no prior weight, and a vision normal matrix that is not positive definite
+    cov = np.eye(6) * 1e-6
+    for sig, st in ((0.0, s), (1.0, type(s)(s.dt, s.gyro, s.w, s.R_rel, s.t_rel, 0.0, 0.0, s.v1, s.var_v1))):
+        got_T, got_C = vision_only(T, cov, sig, st)
+        np.testing.assert_array_equal(got_T, T)
+        np.testing.assert_array_equal(got_C, cov)
+    big = type(s)(s.dt, s.gyro, s.w, s.R_rel, s.t_rel, 1e12, 1e12, s.v1, s.var_v1)
+    got_T, got_C = vision_only(T, cov, 1.0, big)
+    np.testing.assert_array_equal(got_T, T)

@@ -67,6 +67,24 @@ class CameraDesc(ctypes.Structure):
     ]
 
 
+class ImuState(ctypes.Structure):
+    """tslam_imu_state: the IMU filter's state (orientation, velocity, biases, variances)."""
+    _fields_ = [
+        ("R", ctypes.c_double * 9), ("v", ctypes.c_double * 3), ("ba", ctypes.c_double * 3), ("var_v", ctypes.c_double),
+        ("var_b", ctypes.c_double), ("bg", ctypes.c_double * 3), ("var_g", ctypes.c_double),
+        ("w_prev", ctypes.c_double * 3), ("has_w_prev", ctypes.c_int32), ("reserved", ctypes.c_int32),
+    ]
+
+
+class ImuStep(ctypes.Structure):
+    """tslam_imu_step: one frame interval's IMU prediction."""
+    _fields_ = [
+        ("dt", ctypes.c_double), ("gyro", ctypes.c_double * 3), ("w", ctypes.c_double * 3), ("R_rel", ctypes.c_double * 9),
+        ("t_rel", ctypes.c_double * 3), ("w_rot", ctypes.c_double), ("w_trans", ctypes.c_double),
+        ("v1", ctypes.c_double * 3), ("var_v1", ctypes.c_double), ("has_v1", ctypes.c_int32), ("reserved", ctypes.c_int32),
+    ]
+
+
 def camera_desc(cam) -> CameraDesc:
     """A ``CameraConfig`` (intrinsics + world extrinsics) as a ``tslam_camera_desc``."""
     d = CameraDesc()
@@ -85,7 +103,21 @@ def camera_desc(cam) -> CameraDesc:
 _lib: ctypes.CDLL | None = None
 
 # name -> (restype, argtypes); every symbol include/tslam.h declares
+_P = ctypes.c_void_p
 _SIGNATURES = {
+    "tslam_imu_create": (ctypes.c_int, [_P, _P, _P, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "tslam_imu_destroy": (None, [_P]),
+    "tslam_imu_reset": (ctypes.c_int, [_P]),
+    "tslam_imu_begin": (ctypes.c_int, [_P, _P]),
+    "tslam_imu_ready": (ctypes.c_int, [_P]),
+    "tslam_imu_get_state": (ctypes.c_int, [_P, _P]),
+    "tslam_imu_set_state": (ctypes.c_int, [_P, _P]),
+    "tslam_imu_predict": (ctypes.c_int, [_P, _P, ctypes.c_double, _P, _P, _P]),
+    "tslam_imu_coast": (ctypes.c_int, [_P, _P, _P, _P]),
+    "tslam_imu_correct": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
+    "tslam_imu_batch_priors": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P]),
+    "tslam_imu_absorb": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P, _P]),
+    "tslam_imu_vision_only": (ctypes.c_int, [_P, _P, ctypes.c_double, _P, _P, _P]),
     "tslam_last_error": (ctypes.c_char_p, []),
     "tslam_abi_version": (ctypes.c_int, []),
     "tslam_create": (ctypes.c_int, [ctypes.POINTER(StereoDesc), ctypes.POINTER(Params), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),

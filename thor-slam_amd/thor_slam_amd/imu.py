@@ -14,18 +14,23 @@ After every batch the state absorbs the tracked motions (velocity, accelerometer
 gyroscope-bias corrections weighted by the visual covariance).
 
 Frames: the rectified-left camera of pair 0; the filter's world is that camera where the filter
-started.  T_rel maps frame-k points to frame k+1 (X' = R_rel X + t_rel).  The spec, with the
-operation order the checker follows, is ``oracle/numpy_imu.py`` (not imported here).
+started.  T_rel maps frame-k points to frame k+1 (X' = R_rel X + t_rel).  The filter itself is
+native (``csrc/tslam_imu.cpp``, C-ABI ``tslam_imu_*`` in ``include/tslam.h``); this module binds
+it and keeps the state / step records as dataclasses.  The spec, with the operation order the
+checker follows, is ``oracle/numpy_imu.py`` (not imported here).
 """
 
 from __future__ import annotations
 
 from dataclasses import dataclass, field
 
-import numpy as np
-from scipy.spatial.transform import Rotation
+import ctypes
 
-GRAVITY = 9.81
+import numpy as np
+
+from . import _lib
+
+GRAVITY = 9.81   # m/s^2 (csrc/tslam_imu.cpp)
 
 
 @dataclass
@@ -73,138 +78,162 @@ class Step:
     var_v1: float
 
 
+def _c_state(st: InertialState) -> _lib.ImuState:
+    c = _lib.ImuState()
+    c.R[:] = [float(x) for x in np.asarray(st.R, dtype=np.float64).reshape(9)]
+    c.v[:] = [float(x) for x in np.asarray(st.v, dtype=np.float64)]
+    c.ba[:] = [float(x) for x in np.asarray(st.ba, dtype=np.float64)]
+    c.bg[:] = [float(x) for x in np.asarray(st.bg, dtype=np.float64)]
+    c.var_v, c.var_b, c.var_g = float(st.var_v), float(st.var_b), float(st.var_g)
+    if st.w_prev is not None:
+        c.w_prev[:] = [float(x) for x in np.asarray(st.w_prev, dtype=np.float64)]
+        c.has_w_prev = 1
+    return c
+
+
+def _py_state(c: _lib.ImuState) -> InertialState:
+    return InertialState(np.array(c.R[:]).reshape(3, 3), np.array(c.v[:]), np.array(c.ba[:]), c.var_v, c.var_b,
+                         np.array(c.bg[:]), c.var_g, np.array(c.w_prev[:]) if c.has_w_prev else None)
+
+
+def _c_step(s: Step) -> _lib.ImuStep:
+    c = _lib.ImuStep()
+    c.dt = float(s.dt)
+    c.gyro[:] = [float(x) for x in np.asarray(s.gyro, dtype=np.float64)]
+    c.w[:] = [float(x) for x in np.asarray(s.w, dtype=np.float64)]
+    c.R_rel[:] = [float(x) for x in np.asarray(s.R_rel, dtype=np.float64).reshape(9)]
+    c.t_rel[:] = [float(x) for x in np.asarray(s.t_rel, dtype=np.float64)]
+    c.w_rot, c.w_trans, c.var_v1 = float(s.w_rot), float(s.w_trans), float(s.var_v1)
+    if s.v1 is not None:
+        c.v1[:] = [float(x) for x in np.asarray(s.v1, dtype=np.float64)]
+        c.has_v1 = 1
+    return c
+
+
+def _py_step(c: _lib.ImuStep) -> Step:
+    return Step(c.dt, np.array(c.gyro[:]), np.array(c.w[:]), np.array(c.R_rel[:]).reshape(3, 3), np.array(c.t_rel[:]),
+                c.w_rot, c.w_trans, np.array(c.v1[:]) if c.has_v1 else None, c.var_v1)
+
+
+def _vec(x) -> ctypes.Array:
+    return (ctypes.c_double * 3)(*[float(v) for v in np.asarray(x, dtype=np.float64).reshape(3)])
+
+
 class ImuPropagator:
-    """IMU priors for the device and the inertial state behind them.  ``accel=False`` is the
-    gyro-only filter (rotation prior + gyroscope bias; no translation prior)."""
+    """IMU priors for the device and the inertial state behind them, on the native filter
+    (``tslam_imu_*``).  ``accel=False`` is the gyro-only filter (rotation prior + gyroscope bias;
+    no translation prior)."""
 
     def __init__(self, rect_R_imu: np.ndarray, noise: ImuNoise | None = None, lever: np.ndarray | None = None,
                  accel: bool = True):
         n = noise or ImuNoise()
-        self.Ri = np.asarray(rect_R_imu, dtype=np.float64)
-        self.na, self.rw = float(n.acc_density), float(n.acc_random_walk)
-        self.ng, self.rwg = float(n.gyro_density), float(n.gyro_random_walk)
-        self.rot_floor2, self.floor2 = float(n.rot_floor) ** 2, float(n.trans_floor) ** 2
-        self.vis_floor = float(n.vis_rot_floor)
-        self.v0_var, self.ba0_var, self.bg0_var = float(n.v0_sigma) ** 2, float(n.ba0_sigma) ** 2, float(n.bg0_sigma) ** 2
-        self.r = np.zeros(3) if lever is None else np.asarray(lever, dtype=np.float64).reshape(3)
+        self.lib = _lib.load_library()
+        ri = (ctypes.c_double * 9)(*[float(v) for v in np.asarray(rect_R_imu, dtype=np.float64).reshape(9)])
+        nz = (ctypes.c_double * 10)(n.gyro_density, n.gyro_random_walk, n.acc_density, n.acc_random_walk, n.rot_floor,
+                                    n.trans_floor, n.v0_sigma, n.ba0_sigma, n.bg0_sigma, n.vis_rot_floor)
+        lv = _vec(np.zeros(3) if lever is None else lever)
         self.accel = bool(accel)
-        self.g: np.ndarray | None = None
-        self.st = InertialState()
-        self._ready = False
+        self._f = ctypes.c_void_p()
+        _lib._check(self.lib.tslam_imu_create(ri, nz, lv, int(self.accel), ctypes.byref(self._f)))
+
+    def __del__(self):
+        f = getattr(self, "_f", None)
+        if f:
+            self.lib.tslam_imu_destroy(f)
+            self._f = None
 
     @property
     def ready(self) -> bool:
-        return self._ready
+        return bool(self.lib.tslam_imu_ready(self._f))
+
+    @property
+    def st(self) -> InertialState:
+        c = _lib.ImuState()
+        _lib._check(self.lib.tslam_imu_get_state(self._f, ctypes.byref(c)))
+        return _py_state(c)
+
+    @st.setter
+    def st(self, value: InertialState) -> None:
+        c = _c_state(value)
+        _lib._check(self.lib.tslam_imu_set_state(self._f, ctypes.byref(c)))
 
     def reset(self) -> None:
-        self.g = None
-        self.st = InertialState()
-        self._ready = False
+        _lib._check(self.lib.tslam_imu_reset(self._f))
 
     def begin(self, accel: np.ndarray | None = None) -> None:
         """Start at rest: the specific force is gravity's reaction (gyro-only: no sample needed)."""
-        self.g = np.zeros(3)
-        if self.accel:
-            f = self.Ri @ np.asarray(accel, dtype=np.float64)
-            self.g = -GRAVITY * f / np.linalg.norm(f)
-        self.st = InertialState(var_v=self.v0_var, var_b=self.ba0_var, var_g=self.bg0_var)
-        self._ready = True
+        _lib._check(self.lib.tslam_imu_begin(self._f, _vec(accel) if (self.accel and accel is not None) else None))
 
     def step(self, st: InertialState, dt: float, gyro: np.ndarray, accel: np.ndarray | None) -> Step:
-        gyro = np.asarray(gyro, dtype=np.float64)
-        w = self.Ri @ (gyro - st.bg)
-        r_rel = Rotation.from_rotvec(-w * dt).as_matrix()
-        w_rot = 1.0 / (self.ng ** 2 * dt + st.var_g * dt * dt + self.rot_floor2)
-        if not self.accel:
-            return Step(dt, gyro, w, r_rel, np.zeros(3), w_rot, 0.0, None, 0.0)
-        alpha = np.zeros(3) if st.w_prev is None else (w - st.w_prev) / dt
-        w_w, al_w, r_w = st.R @ w, st.R @ alpha, st.R @ self.r
-        a_w = (st.R @ (self.Ri @ (np.asarray(accel, dtype=np.float64) - st.ba)) + self.g
-               - np.cross(w_w, np.cross(w_w, r_w)) - np.cross(al_w, r_w))
-        centre = st.R.T @ (st.v * dt + 0.5 * a_w * dt * dt)   # new camera centre, old camera axes
-        var_t = st.var_v * dt ** 2 + self.na ** 2 * dt ** 3 / 3.0 + st.var_b * dt ** 4 / 4.0 + self.floor2
-        return Step(dt, gyro, w, r_rel, -(r_rel @ centre), w_rot, 1.0 / var_t, st.v + a_w * dt,
-                    st.var_v + self.na ** 2 * dt + st.var_b * dt * dt)
+        c, out = _c_state(st), _lib.ImuStep()
+        _lib._check(self.lib.tslam_imu_predict(self._f, ctypes.byref(c), float(dt), _vec(gyro),
+                                               _vec(accel) if accel is not None else None, ctypes.byref(out)))
+        return _py_step(out)
 
     def coast(self, st: InertialState, s: Step) -> InertialState:
         """No visual motion for the interval: the state follows the IMU."""
-        if not self.accel:
-            return InertialState(st.R @ s.R_rel.T, st.v, st.ba, st.var_v, st.var_b, st.bg,
-                                 st.var_g + self.rwg ** 2 * s.dt, s.w)
-        return InertialState(st.R @ s.R_rel.T, s.v1, st.ba, s.var_v1, st.var_b + self.rw ** 2 * s.dt, st.bg,
-                             st.var_g + self.rwg ** 2 * s.dt, s.w)
+        c, cs, out = _c_state(st), _c_step(s), _lib.ImuState()
+        _lib._check(self.lib.tslam_imu_coast(self._f, ctypes.byref(c), ctypes.byref(cs), ctypes.byref(out)))
+        return _py_state(out)
 
     def correct(self, st: InertialState, s: Step, t_rel: np.ndarray, cov: np.ndarray) -> InertialState:
         """A tracked interval: gyroscope bias (and, with the accelerometer leg, velocity and
         accelerometer bias) pulled towards the visual motion."""
-        dt = s.dt
-        rv = t_rel[:3, :3]
-        var_g1 = st.var_g + self.rwg ** 2 * dt
-        w_v = -Rotation.from_matrix(rv).as_rotvec() / dt
-        z = s.gyro - self.Ri.T @ w_v
-        var_z = np.trace(cov[3:, 3:]) / 3.0 / dt ** 2 + self.ng ** 2 / dt + (self.vis_floor / dt) ** 2
-        kg = var_g1 / (var_g1 + var_z)
-        bg, var_g = st.bg + kg * (z - st.bg), (1.0 - kg) * var_g1
-        if not self.accel:
-            return InertialState(st.R @ rv.T, st.v, st.ba, st.var_v, st.var_b, bg, var_g, s.w)
-        v_vis = (st.R @ (-(rv.T @ t_rel[:3, 3]))) / dt
-        var_vis = np.trace(cov[:3, :3]) / 3.0 / dt ** 2
-        innov = v_vis - s.v1
-        k = s.var_v1 / (s.var_v1 + var_vis)
-        var_b1 = st.var_b + self.rw ** 2 * dt
-        kb = var_b1 / (var_b1 + (var_vis + s.var_v1) / dt ** 2 + self.na ** 2 / dt)
-        e_imu = self.Ri.T @ (st.R.T @ (innov / dt))
-        return InertialState(st.R @ rv.T, s.v1 + k * innov, st.ba - kb * e_imu, (1.0 - k) * s.var_v1,
-                             (1.0 - kb) * var_b1, bg, var_g, s.w)
+        c, cs, out = _c_state(st), _c_step(s), _lib.ImuState()
+        t = np.ascontiguousarray(t_rel, dtype=np.float64).reshape(16)
+        cv = np.ascontiguousarray(cov, dtype=np.float64).reshape(36)
+        _lib._check(self.lib.tslam_imu_correct(self._f, ctypes.byref(c), ctypes.byref(cs), t.ctypes.data, cv.ctypes.data,
+                                               ctypes.byref(out)))
+        return _py_state(out)
+
+    def _arrays(self, samples: list):
+        n = len(samples)
+        dt = np.full(n, np.nan)
+        gy = np.zeros((n, 3))
+        ac = np.zeros((n, 3)) if self.accel else None
+        for k, (d, g, a) in enumerate(samples):
+            if d is None:
+                continue
+            dt[k] = float(d)
+            gy[k] = np.asarray(g, dtype=np.float64)
+            if ac is not None:
+                ac[k] = np.asarray(a, dtype=np.float64) if a is not None else np.nan
+        return n, dt, gy, ac
 
     def batch_priors(self, samples: list) -> list[Step | None]:
         """Per frame of the next batch (``samples`` = [(dt | None, gyro, accel)]): its prediction
-        from the current state coasted over the batch's earlier frames."""
-        st = self.st.copy()
-        out: list[Step | None] = []
-        for dt, gy, ac in samples:
-            if dt is None or not self.ready:
-                out.append(None)
-                continue
-            s = self.step(st, dt, gy, ac)
-            out.append(s)
-            st = self.coast(st, s)
-        return out
+        from the current state coasted over the batch's earlier frames (tslam_imu_batch_priors)."""
+        n, dt, gy, ac = self._arrays(samples)
+        out = (_lib.ImuStep * max(n, 1))()
+        valid = np.zeros(max(n, 1), dtype=np.int32)
+        _lib._check(self.lib.tslam_imu_batch_priors(self._f, n, dt.ctypes.data, gy.ctypes.data,
+                                                    None if ac is None else ac.ctypes.data, out, valid.ctypes.data))
+        return [_py_step(out[k]) if valid[k] else None for k in range(n)]
 
     def absorb(self, samples: list, status: np.ndarray, t_rel: np.ndarray, cov: np.ndarray) -> None:
-        """The batch's results in the filter's camera: status [n], T_rel [n][4][4], cov [n][6][6]."""
-        for k, (dt, gy, ac) in enumerate(samples):
-            if dt is None or not self.ready:
-                continue
-            s = self.step(self.st, dt, gy, ac)
-            self.st = self.correct(self.st, s, t_rel[k], cov[k]) if int(status[k]) == 0 else self.coast(self.st, s)
+        """The batch's results in the filter's camera: status [n], T_rel [n][4][4], cov [n][6][6]
+        (tslam_imu_absorb)."""
+        n, dt, gy, ac = self._arrays(samples)
+        st = np.ascontiguousarray(np.asarray(status)[:n], dtype=np.int32)
+        t = np.ascontiguousarray(np.asarray(t_rel, dtype=np.float64)[:n].reshape(n, 16))
+        cv = np.ascontiguousarray(np.asarray(cov, dtype=np.float64)[:n].reshape(n, 36))
+        _lib._check(self.lib.tslam_imu_absorb(self._f, n, dt.ctypes.data, gy.ctypes.data,
+                                              None if ac is None else ac.ctypes.data, st.ctypes.data, t.ctypes.data,
+                                              cv.ctypes.data))
 
 
 def vision_only(T: np.ndarray, cov: np.ndarray, sigma2: float, step: Step) -> tuple[np.ndarray, np.ndarray]:
     """The vision-only motion and covariance behind a solution the device weighted with ``step``'s
     prior: one Gauss-Newton step on the vision alone from the solution, with the vision's normal
-    matrix H_v = sigma^2 C^-1 - diag(W_t I, W_r I) in (rho, omega) and A7's left Cayley update.
-    The gyroscope-bias update needs it: a rotation the gyro prior already pulled cannot show the
-    bias.  (T, cov) unchanged when no prior acted or H_v is not positive definite."""
-    if not sigma2 > 0.0 or not (step.w_rot > 0.0 or step.w_trans > 0.0):
-        return T, cov
-    h = sigma2 * np.linalg.inv(cov)
-    hv = h.copy()
-    hv[:3, :3] -= step.w_trans * np.eye(3)
-    hv[3:, 3:] -= step.w_rot * np.eye(3)
-    hv = 0.5 * (hv + hv.T)
-    try:
-        np.linalg.cholesky(hv)
-    except np.linalg.LinAlgError:
-        return T, cov
-    R, t = T[:3, :3], T[:3, 3]
-    a = step.R_rel @ R.T
-    delta = 0.5 * np.array([a[2, 1] - a[1, 2], a[0, 2] - a[2, 0], a[1, 0] - a[0, 1]])
-    d = np.linalg.solve(hv, np.concatenate([step.w_trans * (t - step.t_rel), -step.w_rot * delta]))
-    w0, w1, w2 = d[3:]
-    A = np.array([[0.0, -w2, w1], [w2, 0.0, -w0], [-w1, w0, 0.0]])
-    ru = np.eye(3) + (4.0 / (4.0 + (w0 * w0 + w1 * w1) + w2 * w2)) * (A + 0.5 * (A @ A))
-    out = np.eye(4)
-    out[:3, :3] = ru @ R
-    out[:3, 3] = ru @ t + d[:3]
-    return out, sigma2 * np.linalg.inv(hv)
+    matrix H_v = sigma^2 C^-1 - diag(W_t I, W_r I) in (rho, omega) and A7's left Cayley update
+    (tslam_imu_vision_only).  The gyroscope-bias update needs it: a rotation the gyro prior already
+    pulled cannot show the bias.  (T, cov) unchanged when no prior acted or H_v is not positive
+    definite."""
+    lib = _lib.load_library()
+    t = np.ascontiguousarray(T, dtype=np.float64).reshape(16)
+    c = np.ascontiguousarray(cov, dtype=np.float64).reshape(36)
+    t_out, c_out = np.zeros(16), np.zeros(36)
+    cs = _c_step(step)
+    _lib._check(lib.tslam_imu_vision_only(t.ctypes.data, c.ctypes.data, float(sigma2), ctypes.byref(cs),
+                                          t_out.ctypes.data, c_out.ctypes.data))
+    return t_out.reshape(4, 4), c_out.reshape(6, 6)
