@@ -445,6 +445,7 @@ __device__ __forceinline__ void lds_barrier() {
 //   4. C += Q^T Q on the FP64 matrix cores (v_mfma_f64_16x16x4f64), waves 0-3 own 16 rows each.
 // Blocks stride the chunks; each block that had a chunk writes its 64 x 64 partial.
 __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArgs a) {
+#pragma clang fp contract(fast)   // single FMAs in the landmark chains (held to 1e-9, as k_ba_solve)
     __shared__ double s_Q[3 * BA_CHUNK * BA_QPITCH];
     __shared__ double s_Vg[BA_CHUNK][TS_BA_MAXW][9];
     __shared__ int s_has[BA_CHUNK][TS_BA_MAXW];
@@ -688,6 +689,9 @@ __global__ __launch_bounds__(256) void k_ba_reduce(BatchCtx c, BaArgs a) {
 #define BA_SOLVE_WAVES 8
 #define BA_SP 65   // LDS row pitch of S (doubles)
 __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, BaArgs a) {
+    // the elimination's a - l * b updates as single FMAs (the library builds with contraction off
+    // for the bit-exact pose kernels; this solve is only held to 1e-9 against the oracle's LU)
+#pragma clang fp contract(fast)
     static_assert(TS_BA_MAXW * 27 <= 64 * BA_SOLVE_WAVES, "one camera-block load per thread");
     __shared__ double s_S[64 * BA_SP];             // lower: S; upper (row j, column i > j): l_ij
     __shared__ double s_U[TS_BA_MAXW * 27];
