@@ -63,7 +63,7 @@ def test_random_signs_and_unobserved(handle, seed):
     rng = np.random.default_rng(seed)
     t = rng.uniform(-0.3, 0.3, (17, 23, 29)).astype(np.float32)
     w = rng.choice(np.array([0.0, 1.0, 3.0], dtype=np.float32), size=t.shape, p=[0.1, 0.6, 0.3])
-    m = _check_volume(handle, t, w, (0.25, -1.0, 2.0), 0.1, max_dists=(0.1, 0.35, 3.0))
+    m = _check_volume(handle, t, w, (0.25, -1.0, 2.0), 0.1, max_dists=(0.1, 0.35, 3.0, 8.0))   # R = 1, 3, 30 (LDS passes), 80 (direct)
     assert m.shape[0] > 10000
 
 

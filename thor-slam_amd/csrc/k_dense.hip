@@ -17,14 +17,15 @@
 //
 // ESDF, windowed exact distance transform (integer squared voxel distances; R = floor(max / s)):
 //   k_esdf_sites    site (observed, |tsdf| <= site) -> 0, else the cap R^2 + 1 (int32);
-//   k_edt_pass      along one axis: g'(x) = min_{|d| <= R} g(x + d) + d^2, capped — x, then y, then z
-//                   (exact for every distance <= R voxels; one thread per voxel, the x-neighbours of a
-//                   wave are its own row, y / z neighbours are coalesced rows);
+//   k_edt_pass_x_lds / k_edt_pass_yz_lds (R <= 64; k_edt_pass beyond): along one axis,
+//                   g'(x) = min_{|d| <= R} g(x + d) + d^2, capped — x, then y, then z (exact for every
+//                   distance <= R voxels); each block stages its line segments plus the R halo in
+//                   LDS once and the (2R + 1)-tap minimum runs on LDS reads;
 //   k_esdf_finish   sign (tsdf < 0 and not a site), s sqrt(d^2) from the host-built f32 table,
 //                   +-max beyond R, NaN where unobserved.
 //   The 2-D slice runs k_esdf_slice_sites (a column is a site / observed when any voxel of the
 //   height band is) and the x and z passes on the [nz][nx] plane.
-//   Roofline: L2 / VALU — (2R + 1) neighbour reads per voxel and pass, served from cache.
+//   Roofline: LDS / VALU — (2R + 1) LDS reads per voxel and pass; HBM reads the tile + halo once.
 #include "tslam_common.h"
 #include "tslam_mc_table.h"
 
@@ -201,6 +202,73 @@ __global__ __launch_bounds__(DENSE_THREADS) void k_edt_pass(const int32_t* g_in,
     g_out[v] = best < cap ? best : cap;
 }
 
+// The same pass staged through LDS, for R <= EDT_LDS_R (the usual 2 m / 5 cm = 40): every value a
+// block needs is read from HBM / L2 once into LDS and the (2R + 1)-tap minimum runs on LDS reads.
+//   x (stride 1): block = 256 consecutive voxels of one row, LDS = [x0 - R, x0 + 256 + R);
+//   y / z: block = 64 consecutive x columns x EDT_TA outputs along the axis, LDS = (EDT_TA + 2R)
+//   rows of 64 values; thread (column, quarter) computes EDT_TA / 4 outputs.
+#define EDT_LDS_R 64
+#define EDT_TA 64
+__global__ __launch_bounds__(DENSE_THREADS) void k_edt_pass_x_lds(const int32_t* g_in, int32_t* g_out, int nx,
+                                                                  int64_t rows, int R, int32_t cap) {
+    __shared__ int32_t s_g[DENSE_THREADS + 2 * EDT_LDS_R];
+    const int tiles = (nx + DENSE_THREADS - 1) / DENSE_THREADS;
+    const int64_t row = blockIdx.x / tiles;
+    const int x0 = (int)(blockIdx.x - row * tiles) * DENSE_THREADS;
+    const int32_t* in = g_in + row * nx;
+    for (int i = threadIdx.x; i < DENSE_THREADS + 2 * R; i += DENSE_THREADS) {
+        const int x = x0 - R + i;
+        s_g[i] = (x >= 0 && x < nx) ? in[x] : cap;   // outside the row: no site (cap never wins)
+    }
+    __syncthreads();
+    const int x = x0 + (int)threadIdx.x;
+    if (x >= nx) return;
+    const int32_t* c = s_g + threadIdx.x + R;
+    int32_t best = c[0];
+    for (int d = 1; d <= R; ++d) {
+        const int32_t dd = d * d;
+        best = min(best, min(c[-d], c[d]) + dd);
+    }
+    g_out[row * nx + x] = min(best, cap);
+}
+
+// y or z: `n` = extent along the axis, `stride` = its voxel stride, `nx` = the x extent (columns
+// of 64 are x-contiguous), `outer` = the count of independent planes (z for the y pass, 1 plane
+// of nx * ny columns for the z pass is handled by treating x as nx * ny).
+__global__ __launch_bounds__(DENSE_THREADS) void k_edt_pass_yz_lds(const int32_t* g_in, int32_t* g_out, int ncol,
+                                                                   int n, int64_t stride, int64_t plane, int R,
+                                                                   int32_t cap) {
+    extern __shared__ int32_t s_t[];   // [(EDT_TA + 2R)][64]
+    const int cgroups = (ncol + 63) / 64, agroups = (n + EDT_TA - 1) / EDT_TA;
+    int64_t b = blockIdx.x;
+    const int cg = (int)(b % cgroups);
+    b /= cgroups;
+    const int ag = (int)(b % agroups);
+    const int64_t p = b / agroups;                 // plane index
+    const int col0 = cg * 64, a0 = ag * EDT_TA;
+    const int lane = threadIdx.x & 63, quarter = threadIdx.x >> 6;
+    const int col = col0 + lane;
+    const int32_t* in = g_in + p * plane + col;
+    const int span = EDT_TA + 2 * R;
+    for (int r = quarter; r < span; r += 4) {
+        const int a = a0 - R + r;
+        s_t[r * 64 + lane] = (col < ncol && a >= 0 && a < n) ? in[(int64_t)a * stride] : cap;
+    }
+    __syncthreads();
+    if (col >= ncol) return;
+    for (int o = quarter; o < EDT_TA; o += 4) {
+        const int a = a0 + o;
+        if (a >= n) break;
+        const int32_t* c = s_t + (o + R) * 64 + lane;
+        int32_t best = c[0];
+        for (int d = 1; d <= R; ++d) {
+            const int32_t dd = d * d;
+            best = min(best, min(c[-d * 64], c[d * 64]) + dd);
+        }
+        g_out[p * plane + (int64_t)a * stride + col] = min(best, cap);
+    }
+}
+
 __global__ __launch_bounds__(DENSE_THREADS) void k_esdf_finish(DenseArgs a, const int32_t* g, const float* tab, float* out) {
     const int64_t v = (int64_t)blockIdx.x * DENSE_THREADS + threadIdx.x;
     if (v >= a.n_voxels) return;
@@ -235,13 +303,32 @@ void launch_mesh_emit(const DenseArgs& a, const uint8_t* cfg, const uint64_t* bl
     hipLaunchKernelGGL(k_mesh_emit, dim3(blocks_for(a.n_cubes)), dim3(DENSE_THREADS), 0, s, a, cfg, block_off, tris, cap);
 }
 
+// one windowed pass along an axis of a volume [outer][n][ncol]-shaped by strides: x (stride 1,
+// rows = every (y, z)), or y / z (columns = x, or x * y for z); LDS-staged for R <= EDT_LDS_R
+static void edt_pass(const int32_t* in, int32_t* out, int64_t total, int nx, int64_t rows, int axis_n, int64_t stride,
+                     int64_t plane, int ncol, int64_t planes, bool x_axis, int R, int32_t cap, hipStream_t s) {
+    if (R > EDT_LDS_R) {
+        hipLaunchKernelGGL(k_edt_pass, dim3(blocks_for(total)), dim3(DENSE_THREADS), 0, s, in, out, total, axis_n, stride,
+                           R, cap);
+    } else if (x_axis) {
+        const int64_t tiles = (nx + DENSE_THREADS - 1) / DENSE_THREADS;
+        hipLaunchKernelGGL(k_edt_pass_x_lds, dim3((unsigned)(rows * tiles)), dim3(DENSE_THREADS), 0, s, in, out, nx, rows,
+                           R, cap);
+    } else {
+        const int64_t nblk = (int64_t)((ncol + 63) / 64) * ((axis_n + EDT_TA - 1) / EDT_TA) * planes;
+        const size_t lds = sizeof(int32_t) * 64 * (EDT_TA + 2 * R);
+        hipLaunchKernelGGL(k_edt_pass_yz_lds, dim3((unsigned)nblk), dim3(DENSE_THREADS), lds, s, in, out, ncol, axis_n,
+                           stride, plane, R, cap);
+    }
+}
+
 void launch_esdf(const DenseArgs& a, int R, const float* tab, int32_t* g0, int32_t* g1, float* out, hipStream_t s) {
-    const int64_t nv = a.n_voxels;
+    const int64_t nv = a.n_voxels, sy = a.nx, sz = (int64_t)a.nx * a.ny;
     const unsigned nb = blocks_for(nv);
     hipLaunchKernelGGL(k_esdf_sites, dim3(nb), dim3(DENSE_THREADS), 0, s, a, g0);
-    hipLaunchKernelGGL(k_edt_pass, dim3(nb), dim3(DENSE_THREADS), 0, s, g0, g1, nv, a.nx, (int64_t)1, R, a.cap);
-    hipLaunchKernelGGL(k_edt_pass, dim3(nb), dim3(DENSE_THREADS), 0, s, g1, g0, nv, a.ny, (int64_t)a.nx, R, a.cap);
-    hipLaunchKernelGGL(k_edt_pass, dim3(nb), dim3(DENSE_THREADS), 0, s, g0, g1, nv, a.nz, (int64_t)a.nx * a.ny, R, a.cap);
+    edt_pass(g0, g1, nv, a.nx, (int64_t)a.ny * a.nz, a.nx, 1, 0, a.nx, 1, true, R, a.cap, s);              // x
+    edt_pass(g1, g0, nv, a.nx, 0, a.ny, sy, sz, a.nx, a.nz, false, R, a.cap, s);                          // y: planes z
+    edt_pass(g0, g1, nv, a.nx, 0, a.nz, sz, 0, (int)sz, 1, false, R, a.cap, s);                            // z: columns x*y
     hipLaunchKernelGGL(k_esdf_finish, dim3(nb), dim3(DENSE_THREADS), 0, s, a, g1, tab, out);
 }
 
@@ -250,7 +337,7 @@ void launch_esdf_slice(const DenseArgs& a, int y0, int y1, int R, const float* t
     const int64_t nc = (int64_t)a.nx * a.nz;
     const unsigned nb = blocks_for(nc);
     hipLaunchKernelGGL(k_esdf_slice_sites, dim3(nb), dim3(DENSE_THREADS), 0, s, a, y0, y1, g0, obs);
-    hipLaunchKernelGGL(k_edt_pass, dim3(nb), dim3(DENSE_THREADS), 0, s, g0, g1, nc, a.nx, (int64_t)1, R, a.cap);
-    hipLaunchKernelGGL(k_edt_pass, dim3(nb), dim3(DENSE_THREADS), 0, s, g1, g0, nc, a.nz, (int64_t)a.nx, R, a.cap);
+    edt_pass(g0, g1, nc, a.nx, a.nz, a.nx, 1, 0, a.nx, 1, true, R, a.cap, s);                              // x
+    edt_pass(g1, g0, nc, a.nx, 0, a.nz, a.nx, 0, a.nx, 1, false, R, a.cap, s);                             // z
     hipLaunchKernelGGL(k_esdf_slice_finish, dim3(nb), dim3(DENSE_THREADS), 0, s, a, g0, obs, tab, out);
 }
