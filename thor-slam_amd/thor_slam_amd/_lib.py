@@ -454,26 +454,32 @@ class Handle:
         ts = None if timestamps is None else np.ascontiguousarray(timestamps, dtype=np.float64)
         _check(self.lib.tslam_submit_host(self.h, images.ctypes.data, None if ts is None else ts.ctypes.data, n))
 
+    def _poll_buffers(self) -> tuple:
+        """Result arrays of tslam_poll_batch, allocated once with their pointers (a non-blocking poll
+        that finds nothing ready costs one C call, no allocation)."""
+        if getattr(self, "_pb", None) is None:
+            B, P = self.max_batch, self.n_pairs
+            arrs = (np.zeros((B, P, 4, 4)), np.zeros((B, P, 4, 4)), np.zeros((B, P, 6, 6)),
+                    np.zeros((B, P, 8), dtype=np.int32), np.zeros((B, 4, 4)), np.zeros((B, 4, 4)), np.zeros((B, 6, 6)),
+                    np.zeros((B, 8), dtype=np.int32), np.zeros(B))
+            g0, n = ctypes.c_int64(), ctypes.c_int()
+            self._pb = (arrs, tuple(ctypes.c_void_p(a.ctypes.data) for a in arrs), g0, n, ctypes.byref(g0),
+                        ctypes.byref(n))
+        return self._pb
+
     def poll_batch(self, block: bool = False) -> dict | None:
-        """Results of the oldest unread submitted batch, or None when none is ready."""
-        B, P = self.max_batch, self.n_pairs
-        t_rel, t_abs = np.zeros((B, P, 4, 4)), np.zeros((B, P, 4, 4))
-        cov, stats = np.zeros((B, P, 6, 6)), np.zeros((B, P, 8), dtype=np.int32)
-        r_rel, r_abs = np.zeros((B, 4, 4)), np.zeros((B, 4, 4))
-        r_cov, r_st = np.zeros((B, 6, 6)), np.zeros((B, 8), dtype=np.int32)
-        ts = np.zeros(B)
-        g0, n = ctypes.c_int64(), ctypes.c_int()
-        rc = self.lib.tslam_poll_batch(self.h, int(block), B, *(a.ctypes.data for a in (t_rel, t_abs, cov, stats, r_rel,
-                                                                                       r_abs, r_cov, r_st, ts)),
-                                       ctypes.byref(g0), ctypes.byref(n))
+        """Results of the oldest unread submitted batch (copies), or None when none is ready."""
+        arrs, ptrs, g0, n, g0_ref, n_ref = self._poll_buffers()
+        rc = self.lib.tslam_poll_batch(self.h, int(block), self.max_batch, *ptrs, g0_ref, n_ref)
         if rc < 0:
             _check(rc)
         if rc == 0:
             return None
         k = n.value
-        out = {"T_rel": t_rel[:k], "T_abs": t_abs[:k], "cov": cov[:k], "stats": stats[:k], "timestamps": ts[:k],
+        t_rel, t_abs, cov, stats, r_rel, r_abs, r_cov, r_st, ts = (a[:k].copy() for a in arrs)
+        out = {"T_rel": t_rel, "T_abs": t_abs, "cov": cov, "stats": stats, "timestamps": ts,
                "first_frame": int(g0.value), "n": k}
-        out["rig"] = {"T_rel": r_rel[:k], "T_abs": r_abs[:k], "cov": r_cov[:k], "stats": r_st[:k]}
+        out["rig"] = {"T_rel": r_rel, "T_abs": r_abs, "cov": r_cov, "stats": r_st}
         return out
 
     def poll_pose(self) -> dict | None:

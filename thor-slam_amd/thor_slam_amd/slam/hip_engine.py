@@ -135,7 +135,7 @@ class HipSlamEngine(SlamEngine):
         self._staged: list[tuple[np.ndarray, float]] = []
         self._staged_imu: list[tuple | None] = []    # (gyro, accel) per staged frame
         self._imu: ImuPropagator | None = None       # IMU filter (gyro bias; accelerometer leg with imu_accel)
-        self._imu_batches: list[list] = []            # IMU samples of submitted, unpublished batches
+        self._imu_batches: list = []                  # IMU samples of submitted, unpublished batches (None: no data)
         self._prev_stamp: float | None = None      # timestamp of the last submitted frame (IMU dt)
         self._base_R_imu = np.eye(3)
         self._torch = None
@@ -329,9 +329,12 @@ class HipSlamEngine(SlamEngine):
 
     @property
     def _async(self) -> bool:
-        """Batches may stay in flight across calls (nothing reads per-batch device state)."""
+        """Batches may stay in flight across calls (nothing reads per-batch device state; an IMU
+        filter that has seen no sample yet predicts nothing, so a rig whose calibration names an
+        IMU that sends no data keeps the asynchronous path)."""
         cfg = self._config
-        return cfg.ba_window <= 0 and self._loop is None and not cfg.dense_map and self._imu is None
+        return (cfg.ba_window <= 0 and self._loop is None and not cfg.dense_map
+                and (self._imu is None or not self._imu.ready))
 
     def _submit_staged(self) -> None:
         n = len(self._staged)
@@ -406,6 +409,9 @@ class HipSlamEngine(SlamEngine):
         — moved into every other pair's camera through the rig, inv(E_p) E_0 T inv(E_0) E_p.  The
         samples are kept for the filter's update when the batch's results come back."""
         imu, prev = self._imu, self._prev_stamp
+        if not imu.ready and all(s is None for s in imus):   # no IMU sample yet: nothing to predict,
+            self._imu_batches.append(None)                    # and the batch may stay in flight
+            return
         samples = []
         for ts, s in zip(stamps, imus):
             ok = s is not None and (s[1] is not None or not imu.accel)
@@ -603,8 +609,9 @@ class HipSlamEngine(SlamEngine):
             del self._map_points[next(iter(self._map_points))]
 
     def _publish(self, res: dict, stamps: list[float], g0: int) -> None:
-        if self._imu is not None and self._imu_batches:   # the filter absorbs the tracked motions
-            samples, steps = self._imu_batches.pop(0)
+        entry = self._imu_batches.pop(0) if self._imu is not None and self._imu_batches else None
+        if entry is not None:   # the filter absorbs the tracked motions
+            samples, steps = entry
             if len(self._pairs) == 1:   # the vision-only motion behind each prior-weighted solution
                 st = res["stats"][:, 0]
                 sig = np.ascontiguousarray(st[:, 6:8]).view(np.float64)[:, 0]   # sigma^2 (tslam.h)
