@@ -363,13 +363,13 @@ TSDF_DIMS = (176, 72, 176)
 
 
 def tsdf_report(h, us: float, B: int, width: int, height: int) -> dict:
-    """k_tsdf_integrate of one batch: voxel (tsdf, weight) read-modify-write once per launch
-    (8 + 8 B per observed voxel) + the batch's depth images read once; the voxel-frame updates
-    (the per-voxel projection work) beside it."""
+    """k_tsdf_integrate of one batch with the colour layer: voxel (tsdf, weight) and (R, G, B,
+    colour weight) read-modify-write once per launch (16 + 32 B per voxel) + the batch's depth and
+    BGR images read once; the voxel-frame updates (the per-voxel projection work) beside it."""
     t, w = h.tsdf_read()
     nv = int(np.prod(TSDF_DIMS))
     observed = int((w > 0).sum())
-    alg = nv * 16 + B * width * height * 2
+    alg = nv * 16 + nv * 32 + B * width * height * 5   # + the colour layer (RGB + weight f32) and BGR images
     return {"kernel": "k_tsdf_integrate", "volume_voxels": nv, "voxel_size_m": 0.05, "truncation_voxels": 4,
             "frames_per_launch": B, "avg_launch_us": us, "observed_voxels": observed,
             "voxel_frame_updates_per_s": nv * B / (us * 1e-6),
@@ -603,6 +603,7 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     kern = [k for k in KERNELS if k != "chain"] + (["rig"] if P > 1 else []) + ["chain"]
     names = kern + (["local_ba"] if c4 else []) + (["tsdf"] if c5 and args.tsdf else [])
     if c5 and args.tsdf:
+        h.tsdf_color(True)   # nvblox's colour layer with the TSDF (the engine's default)
         h.tsdf_init(TSDF_ORIGIN, TSDF_DIMS, 0.05, 4.0, 10.0, 100.0)
     BACK = {"match", "match_refine", "pose", "chain", "rig"}
     # two streams: the front kernels (rectify .. describe) of batch s + 1 overlap the back kernels
@@ -670,8 +671,9 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
             i = names.index("tsdf")
             if evs is not None:
                 evs[i][0].record(bstream)
-            h.tsdf_integrate(seq[step_base(s)].data_ptr() + 3 * width * height, 5 * width * height * P, B,
-                             first_frame=s * B, stream=bsp)
+            base = seq[step_base(s)].data_ptr()
+            h.tsdf_integrate_rgbd(base, base + 3 * width * height, 5 * width * height * P, B, first_frame=s * B,
+                                  stream=bsp)
             if evs is not None:
                 evs[i][1].record(bstream)
 

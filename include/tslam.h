@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 11
+#define TSLAM_ABI_VERSION 12
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -514,13 +514,24 @@ int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_e
  *   device-resident tracked poses of frames first_frame.. of the last batch (untracked frames are
  *   skipped).  Enqueued on `stream` (NULL: the handle's last stream).
  * tslam_tsdf_read: copy the volume out (synchronises); tsdf / weight may be NULL.
- * tslam_tsdf_write: replace the volume (a saved dense map reloaded; synchronises). */
+ * tslam_tsdf_write: replace the volume (a saved dense map reloaded; synchronises).
+ * Colour layer (nvblox's colour integration of the RGB image aligned with the depth):
+ * tslam_tsdf_color(h, 1) before tslam_tsdf_init adds a running colour (R, G, B f32 in [0, 255])
+ * and its weight per voxel; tslam_tsdf_integrate_rgbd integrates the BGR images `color` with the
+ * depth (both frames stride_bytes apart: an RGB-D record's colour and depth parts), the colour of
+ * the depth pixel into every updated voxel inside the truncation band;
+ * tslam_tsdf_read_color / _write_color copy it ([nz][ny][nx][3] and [nz][ny][nx]). */
 int tslam_tsdf_init(tslam_handle* h, const double* origin, const int32_t* dims, double voxel_size, double trunc_vox,
                     double max_dist, double max_weight);
 int tslam_tsdf_integrate(tslam_handle* h, int pair, const void* depth, int64_t stride_bytes, int n_frames,
                          int64_t first_frame, const double* world_T_cam, void* stream);
 int tslam_tsdf_read(tslam_handle* h, float* tsdf, float* weight);
 int tslam_tsdf_write(tslam_handle* h, const float* tsdf, const float* weight);
+int tslam_tsdf_color(tslam_handle* h, int enable);
+int tslam_tsdf_integrate_rgbd(tslam_handle* h, int pair, const void* color, const void* depth, int64_t stride_bytes,
+                              int n_frames, int64_t first_frame, const double* world_T_cam, void* stream);
+int tslam_tsdf_read_color(tslam_handle* h, float* rgb, float* weight);
+int tslam_tsdf_write_color(tslam_handle* h, const float* rgb, const float* weight);
 
 /* Dense-map outputs of the TSDF volume — what nvblox publishes after integration (its mesh and
  * ESDF / distance-slice outputs; launch/thor_nvblox.launch.py:21-103 starts the node the reference
@@ -532,6 +543,8 @@ int tslam_tsdf_write(tslam_handle* h, const float* tsdf, const float* weight);
  *   handle's last stream); waits for the triangle count only (*n_tris).
  * tslam_mesh_read: copy the first min(max_tris, count) triangles out, 9 f32 each (three xyz
  *   vertices in metres, facing positive tsdf), in cube order (synchronises).
+ * tslam_mesh_read_colors: with the colour layer, the vertices' colours (9 f32 per triangle: each
+ *   vertex takes the colour of its edge's voxel nearer to it).
  * tslam_esdf_compute: exact Euclidean signed distance (m) of every observed voxel (weight >=
  *   min_weight) to the nearest site (observed, |tsdf| <= site_vox * voxel), negative inside (tsdf
  *   < 0), +-max_dist beyond floor(max_dist / voxel) voxels (<= 2048), NaN unobserved; enqueued on
@@ -541,6 +554,7 @@ int tslam_tsdf_write(tslam_handle* h, const float* tsdf, const float* weight);
  *   column is a site / observed when any of its band's voxels is; synchronous). */
 int tslam_mesh_extract(tslam_handle* h, double min_weight, int64_t* n_tris, void* stream);
 int tslam_mesh_read(tslam_handle* h, float* tris, int64_t max_tris);
+int tslam_mesh_read_colors(tslam_handle* h, float* colors, int64_t max_tris);
 int tslam_esdf_compute(tslam_handle* h, double max_dist, double site_vox, double min_weight, void* stream);
 int tslam_esdf_read(tslam_handle* h, float* esdf);
 int tslam_esdf_slice(tslam_handle* h, int y0, int y1, double max_dist, double site_vox, double min_weight, float* out);

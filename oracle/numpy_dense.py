@@ -95,11 +95,15 @@ def _centres(origin, s, n, axis):
     return np.asarray(origin[axis] + s * (np.arange(n) + 0.5), dtype=np.float64).astype(np.float32)
 
 
-def extract_mesh(tsdf: np.ndarray, weight: np.ndarray, origin, s: float, min_weight: float) -> np.ndarray:
-    """Triangle soup [n][3 vertices][xyz] f32 in cube order ([k][j][i] of the base corner)."""
+def extract_mesh(tsdf: np.ndarray, weight: np.ndarray, origin, s: float, min_weight: float,
+                 color: np.ndarray | None = None):
+    """Triangle soup [n][3 vertices][xyz] f32 in cube order ([k][j][i] of the base corner); with a
+    colour layer ``color`` [nz][ny][nx][3] also (triangles, colours [n][3][3] f32): each vertex
+    takes the colour of its edge's voxel nearer to it (the base voxel when t < 1/2)."""
     nz, ny, nx = tsdf.shape
     if min(nx, ny, nz) < 2:
-        return np.zeros((0, 3, 3), dtype=np.float32)
+        empty = np.zeros((0, 3, 3), dtype=np.float32)
+        return empty if color is None else (empty, empty.copy())
     sl = [(slice(dz, nz - 1 + dz), slice(dy, ny - 1 + dy), slice(dx, nx - 1 + dx)) for dx, dy, dz in CORNER_OFFSETS]
     obs = np.ones((nz - 1, ny - 1, nx - 1), dtype=bool)
     cfg = np.zeros((nz - 1, ny - 1, nx - 1), dtype=np.int64)
@@ -110,10 +114,10 @@ def extract_mesh(tsdf: np.ndarray, weight: np.ndarray, origin, s: float, min_wei
     k, j, i = np.nonzero(cfg)   # row-major: cube order
     cx, cy, cz = _centres(origin, s, nx, 0), _centres(origin, s, ny, 1), _centres(origin, s, nz, 2)
     sf = np.float32(s)
-    out = []
+    out, cols = [], []
     for q in range(k.size):
         for tri in CONFIG_TRIANGLES[cfg[k[q], j[q], i[q]]]:
-            v = []
+            v, vc = [], []
             for e in tri:
                 a, m = divmod(e, 4)
                 o = [b for b in (0, 1, 2) if b != a]
@@ -126,8 +130,14 @@ def extract_mesh(tsdf: np.ndarray, weight: np.ndarray, origin, s: float, min_wei
                 p = [cx[bi], cy[bj], cz[bk]]
                 p[a] = p[a] + t * sf
                 v.append(p)
+                if color is not None:
+                    vc.append(color[bk, bj, bi] if t < np.float32(0.5) else color[ek, ej, ei])
             out.append(v)
-    return np.array(out, dtype=np.float32).reshape(-1, 3, 3)
+            cols.append(vc)
+    tris = np.array(out, dtype=np.float32).reshape(-1, 3, 3)
+    if color is None:
+        return tris
+    return tris, np.array(cols, dtype=np.float32).reshape(-1, 3, 3)
 
 
 def _window_pass(g: np.ndarray, axis: int, R: int, cap: int) -> np.ndarray:

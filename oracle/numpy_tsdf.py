@@ -26,6 +26,11 @@ table as the tracking image) with camera pose cam_T_world, per voxel, in f64:
     w' = w + 1;  tsdf' = (tsdf * w + obs) / w';  w' = min(w', max_weight)     (stored as f32)
 
 Frames are integrated in order; a batch of frames gives the same result as one call per frame.
+
+Colour layer (nvblox's colour integration on the RGB image aligned with the depth): with a BGR
+image, every voxel the frame updates whose surface distance is inside the truncation band
+(|sdf| <= trunc) also averages the colour of the same (undistorted) pixel, R, G, B in [0, 255]:
+cw' = cw + 1;  c' = (c * cw + obs) / cw' per channel;  cw' = min(cw', max_weight)  (stored as f32).
 """
 
 from __future__ import annotations
@@ -42,8 +47,10 @@ def voxel_centres(origin, dims, s) -> np.ndarray:
 
 
 def integrate(tsdf: np.ndarray, weight: np.ndarray, depth_mm: np.ndarray, cam_T_world: np.ndarray, intr,
-              origin, s: float, trunc: float, max_dist: float, max_weight: float, mp: np.ndarray | None = None):
-    """One frame into (tsdf, weight) [nz][ny][nx] f32, in place."""
+              origin, s: float, trunc: float, max_dist: float, max_weight: float, mp: np.ndarray | None = None,
+              bgr: np.ndarray | None = None, color: np.ndarray | None = None, color_w: np.ndarray | None = None):
+    """One frame into (tsdf, weight) [nz][ny][nx] f32, in place; with ``bgr`` [H][W][3] u8 also the
+    colour layer ``color`` [nz][ny][nx][3] (R, G, B) f32 and ``color_w`` f32."""
     fx, fy, cx, cy = intr
     h, w = depth_mm.shape
     c = voxel_centres(origin, tsdf.shape[::-1], s)
@@ -74,6 +81,14 @@ def integrate(tsdf: np.ndarray, weight: np.ndarray, depth_mm: np.ndarray, cam_T_
     new = (tsdf.astype(np.float64) * w0 + obs) / w1
     tsdf[ok] = new[ok].astype(np.float32)
     weight[ok] = np.minimum(w1, max_weight)[ok].astype(np.float32)
+    if bgr is not None:
+        band = ok & (sdf <= trunc)
+        obs_c = bgr[iy, ix][..., ::-1].astype(np.float64)              # R, G, B of the same pixel
+        cw0 = color_w.astype(np.float64)
+        cw1 = cw0 + 1.0
+        newc = (color.astype(np.float64) * cw0[..., None] + obs_c) / cw1[..., None]
+        color[band] = newc[band].astype(np.float32)
+        color_w[band] = np.minimum(cw1, max_weight)[band].astype(np.float32)
 
 
 def surface_points(tsdf: np.ndarray, weight: np.ndarray, origin, s: float) -> np.ndarray:

@@ -67,6 +67,30 @@ def test_random_signs_and_unobserved(handle, seed):
     assert m.shape[0] > 10000
 
 
+def test_mesh_vertex_colours():
+    """With the colour layer every vertex takes its edge's nearer voxel's colour (oracle bits)."""
+    from thor_slam_amd._lib import Handle
+
+    src = SyntheticStereoSource(seed=3, n_frames=2)
+    cams = extract_cameras(CameraRig([src]).calibration, 2)
+    (li, ri), = stereo_pairs(cams)
+    h = Handle([stereo_rectify(cams[li], cams[ri])], HipSlamConfig(), max_batch=2)
+    rng = np.random.default_rng(5)
+    t = rng.uniform(-0.3, 0.3, (13, 17, 19)).astype(np.float32)
+    w = rng.choice(np.array([0.0, 1.0, 2.0], dtype=np.float32), size=t.shape, p=[0.1, 0.6, 0.3])
+    col = rng.uniform(0, 255, t.shape + (3,)).astype(np.float32)
+    h.tsdf_color(True)
+    h.tsdf_init((0.0, 0.5, 1.0), (19, 17, 13), 0.1)
+    h.tsdf_write(t, w)
+    h.tsdf_write_color(col, np.ones_like(w))
+    tris, cols = h.mesh(colors=True)
+    want_t, want_c = D.extract_mesh(t, w, (0.0, 0.5, 1.0), 0.1, 1e-4, color=col)
+    assert tris.shape[0] > 1000
+    np.testing.assert_array_equal(_bits(tris), _bits(want_t))
+    np.testing.assert_array_equal(_bits(cols), _bits(want_c))
+    h.close()
+
+
 def test_edges(handle):
     t = np.full((6, 5, 4), 0.1, dtype=np.float32)
     w = np.zeros_like(t)

@@ -52,15 +52,18 @@ def _setup(distorted: bool, n: int, width=320, height=240):
     return src, rect, h, dev, res, depth
 
 
-def _oracle(rect, depth, world_T_cam, use):
+def _oracle(rect, depth, world_T_cam, use, bgr=None):
     t = np.zeros(DIMS[::-1], dtype=np.float32)
     w = np.zeros(DIMS[::-1], dtype=np.float32)
+    col = np.zeros(DIMS[::-1] + (3,), dtype=np.float32)
+    cw = np.zeros(DIMS[::-1], dtype=np.float32)
     intr = (rect.fx, rect.fy, rect.cx, rect.cy)
-    for d, T, u in zip(depth, world_T_cam, use):
+    for f, (d, T, u) in enumerate(zip(depth, world_T_cam, use)):
         if u:
             TS.integrate(t, w, d, _inv(T), intr, ORIGIN, VOX, TRUNC_VOX * VOX, MAX_D, MAX_W,
-                         None if rect.is_identity else rect.map_left)
-    return t, w
+                         None if rect.is_identity else rect.map_left,
+                         bgr=None if bgr is None else bgr[f], color=col, color_w=cw)
+    return (t, w) if bgr is None else (t, w, col, cw)
 
 
 @pytest.mark.parametrize("distorted", [False, True])
@@ -156,6 +159,31 @@ def test_tsdf_brick_cull_wide_volume():
     np.testing.assert_array_equal(t, want_t)
 
 
+@pytest.mark.parametrize("distorted", [False, True])
+def test_tsdf_color_layer_bit_exact(distorted):
+    """nvblox's colour layer: the record's BGR part integrated with its depth — colour and colour
+    weight bit-exact vs the oracle, the TSDF itself unchanged by it."""
+    n = 4
+    src, rect, h, dev, res, depth = _setup(distorted, n)
+    W, H = rect.width, rect.height
+    poses = res["T_abs"][:, 0]
+    h.tsdf_color(True)
+    h.tsdf_init(ORIGIN, DIMS, VOX, TRUNC_VOX, MAX_D, MAX_W)
+    h.tsdf_integrate_rgbd(dev.data_ptr(), dev.data_ptr() + 3 * W * H, 5 * W * H, n, world_T_cam=poses)
+    t, w = h.tsdf_read()
+    col, cw = h.tsdf_read_color()
+    rec = dev.cpu().numpy()
+    bgr = [rec[f, 0, :3 * W * H].reshape(H, W, 3) for f in range(n)]
+    want_t, want_w, want_c, want_cw = _oracle(rect, depth, poses, [True] * n, bgr=bgr)
+    np.testing.assert_array_equal(w, want_w)
+    np.testing.assert_array_equal(t, want_t)
+    assert (want_cw > 0).sum() > 1000 and (want_cw > 0).sum() < (want_w > 0).sum()   # the band only
+    np.testing.assert_array_equal(cw, want_cw)
+    np.testing.assert_array_equal(col, want_c)
+    assert col.max() > 10.0   # real colours, not zeros
+    h.close()
+
+
 def test_engine_dense_map():
     """HipSlamEngine(rgbd, dense_map): each batch's depth integrated with its device-resident tracked
     poses, bit-exact with the oracle on the poses the device tracked; world_T_volume = base_T_rect."""
@@ -171,16 +199,20 @@ def test_engine_dense_map():
                         tsdf_max_weight=MAX_W)
     eng = HipSlamEngine(num_cameras=2, config=cfg)
     eng.initialize(rig.calibration)
-    depth = []
+    depth, bgr = [], []
     for _ in range(n):
         fs = rig.get_synchronized_frames()
         depth.append(np.array(fs.frame_sets[src.name].frames[1].image))
+        bgr.append(np.array(fs.frame_sets[src.name].frames[0].image))
         eng.process_frames(fs)
     dm = eng.get_dense_map()
     res = eng.handle.read_poses(n)
     rect = eng.rectifications[0]
     st = res["stats"][:, 0, 0]
-    want_t, want_w = _oracle(rect, depth, res["T_abs"][:, 0], [s == 0 or (s == 2 and f == 0) for f, s in enumerate(st)])
+    want_t, want_w, want_c, want_cw = _oracle(rect, depth, res["T_abs"][:, 0],
+                                              [s == 0 or (s == 2 and f == 0) for f, s in enumerate(st)], bgr=bgr)
+    np.testing.assert_array_equal(dm["color_weight"], want_cw)
+    np.testing.assert_array_equal(dm["color"], want_c)
     assert (want_w > 0).sum() > 10000
     np.testing.assert_array_equal(dm["weight"], want_w)
     np.testing.assert_array_equal(dm["tsdf"], want_t)
@@ -190,9 +222,10 @@ def test_engine_dense_map():
     from oracle import numpy_dense as DN
 
     mesh = eng.get_mesh()
-    want_m = DN.extract_mesh(want_t, want_w, ORIGIN, VOX, cfg.mesh_integrator_min_weight)
+    want_m, want_mc = DN.extract_mesh(want_t, want_w, ORIGIN, VOX, cfg.mesh_integrator_min_weight, color=want_c)
     assert want_m.shape[0] > 1000
     np.testing.assert_array_equal(mesh["triangles"].view(np.uint32), want_m.view(np.uint32))
+    np.testing.assert_array_equal(mesh["colors"].view(np.uint32), want_mc.view(np.uint32))
     es = eng.get_esdf()
     want_e = DN.esdf(want_t, want_w, VOX, cfg.esdf_integrator_max_distance_m)
     np.testing.assert_array_equal(es["esdf"].view(np.uint32), want_e.view(np.uint32))

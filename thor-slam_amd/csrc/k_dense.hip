@@ -11,7 +11,8 @@
 //   k_mesh_emit   thread per cube again: block-local exclusive scan of the counts, the triangles'
 //                 vertices interpolated on the crossing edges (f32, edge values read from the
 //                 edge's lower voxel so both cubes of a shared edge produce the same vertex),
-//                 9 f32 per triangle in cube order.
+//                 9 f32 per triangle in cube order (+ 9 f32 of vertex colours with the colour
+//                 layer: each vertex takes its edge's nearer voxel's colour).
 //   Roofline: HBM — the 2 x 4 B of every voxel read once per pass (neighbour corners hit L2), plus
 //   1 B of configuration per cube and 36 B per triangle.
 //
@@ -115,7 +116,7 @@ __global__ __launch_bounds__(1024) void k_mesh_scan(const uint32_t* block_sums, 
 }
 
 __global__ __launch_bounds__(DENSE_THREADS) void k_mesh_emit(DenseArgs a, const uint8_t* cfg_in, const uint64_t* block_off,
-                                                             float* tris, int64_t cap) {
+                                                             float* tris, float* cols, int64_t cap) {
     __shared__ uint32_t s_w[DENSE_THREADS / 64];
     const uint32_t q = blockIdx.x * DENSE_THREADS + threadIdx.x;
     const uint32_t cfg = q < a.n_cubes ? cfg_in[q] : 0u;
@@ -158,6 +159,13 @@ __global__ __launch_bounds__(DENSE_THREADS) void k_mesh_emit(DenseArgs a, const 
             out[3 * vtx + 0] = p[0];
             out[3 * vtx + 1] = p[1];
             out[3 * vtx + 2] = p[2];
+            if (a.color) {   // the colour of the edge's voxel nearer to the vertex
+                const float* cv = a.color + 3 * (tt < 0.5f ? vb : vb + stride[ax]);
+                float* oc = cols + tri * 9 + 3 * vtx;
+                oc[0] = cv[0];
+                oc[1] = cv[1];
+                oc[2] = cv[2];
+            }
         }
     }
 }
@@ -298,9 +306,10 @@ void launch_mesh_count(const DenseArgs& a, uint8_t* cfg, uint32_t* block_sums, u
     hipLaunchKernelGGL(k_mesh_scan, dim3(1), dim3(1024), 0, s, block_sums, (int)nb, block_off, total);
 }
 
-void launch_mesh_emit(const DenseArgs& a, const uint8_t* cfg, const uint64_t* block_off, float* tris, int64_t cap,
-                      hipStream_t s) {
-    hipLaunchKernelGGL(k_mesh_emit, dim3(blocks_for(a.n_cubes)), dim3(DENSE_THREADS), 0, s, a, cfg, block_off, tris, cap);
+void launch_mesh_emit(const DenseArgs& a, const uint8_t* cfg, const uint64_t* block_off, float* tris, float* cols,
+                      int64_t cap, hipStream_t s) {
+    hipLaunchKernelGGL(k_mesh_emit, dim3(blocks_for(a.n_cubes)), dim3(DENSE_THREADS), 0, s, a, cfg, block_off, tris, cols,
+                       cap);
 }
 
 // one windowed pass along an axis of a volume [outer][n][ncol]-shaped by strides: x (stride 1,

@@ -13,7 +13,9 @@
 //   k_tsdf_integrate  per 16x4x4 brick: the frames whose view can reach the brick (bounding
 //                     sphere vs the frustum, one frame per thread, ballot), then per voxel for
 //                     each of those frames project the centre (f64), nearest depth pixel through
-//                     the undistortion table, truncated signed distance, weighted average.
+//                     the undistortion table, truncated signed distance, weighted average;
+//                     with the colour layer, the same pixel's colour averaged into the voxels
+//                     inside the truncation band (nvblox's colour integration).
 #include "tslam_common.h"
 
 // host poses: world_T_cam [n][16] -> cam_T_world; device poses: T_abs of batch frames (f0 + i)
@@ -96,6 +98,7 @@ __global__ __launch_bounds__(256) void k_tsdf_integrate(TsdfArgs a, int nbx, int
     const double X = a.ox + a.s * (i + 0.5), Y = a.oy + a.s * (j + 0.5), Z = a.oz + a.s * (k + 0.5);
     bool loaded = false;
     double ts = 0.0, w = 0.0;
+    double cr = 0.0, cg = 0.0, cb = 0.0, cw = 0.0;   // colour layer (loaded with the voxel)
     for (int wd = 0; wd < (a.n + 63) / 64; ++wd) {
         uint64_t m = s_mask[wd];   // wave-uniform: frames in order
         while (m) {
@@ -124,16 +127,36 @@ __global__ __launch_bounds__(256) void k_tsdf_integrate(TsdfArgs a, int nbx, int
             if (!loaded) {
                 ts = (double)a.tsdf[v];
                 w = (double)a.weight[v];
+                if (a.col) {
+                    cr = (double)a.col[3 * v];
+                    cg = (double)a.col[3 * v + 1];
+                    cb = (double)a.col[3 * v + 2];
+                    cw = (double)a.col_w[v];
+                }
                 loaded = true;
             }
             const double w1 = w + 1.0;
             ts = (double)(float)((ts * w + obs) / w1);   // stored as f32 after every frame (as the oracle)
             w = (double)(float)fmin(w1, a.max_weight);
+            if (a.col && sdf <= a.trunc) {   // colour inside the truncation band: the same pixel's BGR
+                const uint8_t* px = a.color + (size_t)f * a.stride + ((size_t)iy * a.W + ix) * 3;
+                const double c1 = cw + 1.0;
+                cr = (double)(float)((cr * cw + (double)px[2]) / c1);
+                cg = (double)(float)((cg * cw + (double)px[1]) / c1);
+                cb = (double)(float)((cb * cw + (double)px[0]) / c1);
+                cw = (double)(float)fmin(c1, a.max_weight);
+            }
         }
     }
     if (loaded) {
         a.tsdf[v] = (float)ts;
         a.weight[v] = (float)w;
+        if (a.col) {
+            a.col[3 * v] = (float)cr;
+            a.col[3 * v + 1] = (float)cg;
+            a.col[3 * v + 2] = (float)cb;
+            a.col_w[v] = (float)cw;
+        }
     }
 }
 

@@ -97,6 +97,7 @@ struct tslam_handle {
     int32_t *d_pg_edges = nullptr, *d_pg_adj_off = nullptr, *d_pg_adj = nullptr, *d_pg_ftile = nullptr;
     // RGB-D dense mapping (tslam_tsdf_*): dense TSDF volume + per-launch pose scratch
     bool tsdf_on = false;
+    bool tsdf_color = false;          // colour layer (tslam_tsdf_color)
     TsdfArgs tsdf{};
     double* d_tsdf_poses = nullptr;   // [TSDF_MAX_FRAMES][TSDF_POSE]
     double* d_tsdf_wTc = nullptr;     // [TSDF_MAX_FRAMES][16] host poses staged
@@ -106,6 +107,7 @@ struct tslam_handle {
     uint64_t* d_mesh_boff = nullptr;  // [blocks] first triangle; [blocks] = mesh total
     size_t mesh_cubes_cap = 0;
     float* d_mesh_tris = nullptr;     // [tri cap][9]
+    float* d_mesh_cols = nullptr;     // [tri cap][9] vertex colours (colour layer)
     int64_t mesh_tris_cap = 0, mesh_n = 0;
     int32_t* d_edt[2] = {nullptr, nullptr};
     size_t edt_cap = 0;
@@ -788,6 +790,10 @@ int tslam_reset(tslam_handle* h) {
         const size_t nv = (size_t)h->tsdf.nx * h->tsdf.ny * h->tsdf.nz;
         HIPCHK(hipMemset(h->tsdf.tsdf, 0, sizeof(float) * nv));
         HIPCHK(hipMemset(h->tsdf.weight, 0, sizeof(float) * nv));
+        if (h->tsdf.col) {
+            HIPCHK(hipMemset(h->tsdf.col, 0, sizeof(float) * 3 * nv));
+            HIPCHK(hipMemset(h->tsdf.col_w, 0, sizeof(float) * nv));
+        }
     }
     h->lp_count = 0;   // the keyframe database belongs to the session
     std::fill(h->lp_n.begin(), h->lp_n.end(), 0);
@@ -1690,6 +1696,10 @@ int tslam_tsdf_init(tslam_handle* h, const double* origin, const int32_t* dims, 
     TsdfArgs& a = h->tsdf;
     int rc = dev_realloc(h, (void**)&a.tsdf, sizeof(float) * nv);
     if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&a.weight, sizeof(float) * nv);
+    if (rc == TSLAM_OK && h->tsdf_color) {
+        rc = dev_realloc(h, (void**)&a.col, sizeof(float) * 3 * nv);
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&a.col_w, sizeof(float) * nv);
+    }
     if (rc == TSLAM_OK && !h->d_tsdf_poses) rc = dev_alloc(h, (void**)&h->d_tsdf_poses, sizeof(double) * TSDF_MAX_FRAMES * TSDF_POSE);
     if (rc == TSLAM_OK && !h->d_tsdf_wTc) rc = dev_alloc(h, (void**)&h->d_tsdf_wTc, sizeof(double) * TSDF_MAX_FRAMES * 16);
     if (rc != TSLAM_OK) return rc;
@@ -1709,8 +1719,30 @@ int tslam_tsdf_init(tslam_handle* h, const double* origin, const int32_t* dims, 
     return TSLAM_OK;
 }
 
+static int tsdf_integrate(tslam_handle* h, int pair, const void* color, const void* depth, int64_t stride_bytes,
+                          int n_frames, int64_t first_frame, const double* world_T_cam, void* stream);
+
 int tslam_tsdf_integrate(tslam_handle* h, int pair, const void* depth, int64_t stride_bytes, int n_frames,
                          int64_t first_frame, const double* world_T_cam, void* stream) {
+    return tsdf_integrate(h, pair, nullptr, depth, stride_bytes, n_frames, first_frame, world_T_cam, stream);
+}
+
+int tslam_tsdf_integrate_rgbd(tslam_handle* h, int pair, const void* color, const void* depth, int64_t stride_bytes,
+                              int n_frames, int64_t first_frame, const double* world_T_cam, void* stream) {
+    if (!color) return fail(TSLAM_EINVAL, "null colour images");
+    if (h && !h->tsdf_color) return fail(TSLAM_ESTATE, "no colour layer (tslam_tsdf_color before tslam_tsdf_init)");
+    return tsdf_integrate(h, pair, color, depth, stride_bytes, n_frames, first_frame, world_T_cam, stream);
+}
+
+int tslam_tsdf_color(tslam_handle* h, int enable) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (h->tsdf_on && (enable != 0) != h->tsdf_color) return fail(TSLAM_ESTATE, "tslam_tsdf_color before tslam_tsdf_init");
+    h->tsdf_color = enable != 0;
+    return TSLAM_OK;
+}
+
+static int tsdf_integrate(tslam_handle* h, int pair, const void* color, const void* depth, int64_t stride_bytes,
+                          int n_frames, int64_t first_frame, const double* world_T_cam, void* stream) {
     if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
     if (!h->tsdf_on) return fail(TSLAM_ESTATE, "no TSDF volume (tslam_tsdf_init)");
     if (!depth || n_frames < 0 || (n_frames > 1 && stride_bytes < 2LL * h->W * h->H)) return fail(TSLAM_EINVAL, "bad depth / stride");
@@ -1734,9 +1766,11 @@ int tslam_tsdf_integrate(tslam_handle* h, int pair, const void* depth, int64_t s
     a.cy = h->calib[pair].cy;
     a.map = ((h->map_mask >> cam) & 1u) ? h->d_maps + (size_t)cam * h->W * h->H * 2 : nullptr;
     a.stride = stride_bytes;
+    if (!color) a.col = a.col_w = nullptr;   // the colour layer keeps its state without colour input
     for (int b0 = 0; b0 < n_frames; b0 += TSDF_MAX_FRAMES) {
         a.n = std::min(TSDF_MAX_FRAMES, n_frames - b0);
         a.depth = static_cast<const uint8_t*>(depth) + (size_t)b0 * stride_bytes;
+        a.color = color ? static_cast<const uint8_t*>(color) + (size_t)b0 * stride_bytes : nullptr;
         const double* wtc = nullptr;
         if (world_T_cam) {
             HIPCHK(hipMemcpyAsync(h->d_tsdf_wTc, world_T_cam + (size_t)16 * b0, sizeof(double) * 16 * a.n,
@@ -1757,6 +1791,27 @@ int tslam_tsdf_read(tslam_handle* h, float* tsdf, float* weight) {
     const size_t nv = (size_t)h->tsdf.nx * h->tsdf.ny * h->tsdf.nz;
     if (tsdf) HIPCHK(hipMemcpy(tsdf, h->tsdf.tsdf, sizeof(float) * nv, hipMemcpyDeviceToHost));
     if (weight) HIPCHK(hipMemcpy(weight, h->tsdf.weight, sizeof(float) * nv, hipMemcpyDeviceToHost));
+    return TSLAM_OK;
+}
+
+int tslam_tsdf_read_color(tslam_handle* h, float* rgb, float* weight) {
+    if (!h || !h->tsdf_on || !h->tsdf_color) return fail(TSLAM_ESTATE, "no colour layer");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    const size_t nv = (size_t)h->tsdf.nx * h->tsdf.ny * h->tsdf.nz;
+    if (rgb) HIPCHK(hipMemcpy(rgb, h->tsdf.col, sizeof(float) * 3 * nv, hipMemcpyDeviceToHost));
+    if (weight) HIPCHK(hipMemcpy(weight, h->tsdf.col_w, sizeof(float) * nv, hipMemcpyDeviceToHost));
+    return TSLAM_OK;
+}
+
+int tslam_tsdf_write_color(tslam_handle* h, const float* rgb, const float* weight) {
+    if (!h || !h->tsdf_on || !h->tsdf_color) return fail(TSLAM_ESTATE, "no colour layer");
+    if (!rgb || !weight) return fail(TSLAM_EINVAL, "null colour volume");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    const size_t nv = (size_t)h->tsdf.nx * h->tsdf.ny * h->tsdf.nz;
+    HIPCHK(hipMemcpy(h->tsdf.col, rgb, sizeof(float) * 3 * nv, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->tsdf.col_w, weight, sizeof(float) * nv, hipMemcpyHostToDevice));
     return TSLAM_OK;
 }
 
@@ -1789,6 +1844,7 @@ static DenseArgs dense_args(const tslam_handle* h, double min_weight) {
     a.s = t.s;
     a.sf = (float)t.s;
     a.min_weight = (float)min_weight;
+    a.color = h->tsdf_color ? t.col : nullptr;
     return a;
 }
 
@@ -1825,17 +1881,28 @@ int tslam_mesh_extract(tslam_handle* h, double min_weight, int64_t* n_tris, void
     uint64_t total = 0;   // the buffer is sized to the count: one small read back
     HIPCHK(hipMemcpyAsync(&total, h->d_mesh_boff + nb, sizeof(total), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    if ((int64_t)total > h->mesh_tris_cap) {
-        size_t c = 0;
-        const int64_t want = (int64_t)total + (int64_t)total / 4 + 1024;
-        const int rc = grow(h, (void**)&h->d_mesh_tris, &c, sizeof(float) * 9 * (size_t)want);
+    if ((int64_t)total > h->mesh_tris_cap || (a.color && !h->d_mesh_cols)) {
+        size_t c = 0, c2 = 0;
+        const int64_t want = std::max((int64_t)total + (int64_t)total / 4 + 1024, h->mesh_tris_cap);
+        int rc = grow(h, (void**)&h->d_mesh_tris, &c, sizeof(float) * 9 * (size_t)want);
+        if (rc == TSLAM_OK && a.color) rc = grow(h, (void**)&h->d_mesh_cols, &c2, sizeof(float) * 9 * (size_t)want);
         if (rc != TSLAM_OK) return rc;
         h->mesh_tris_cap = want;
     }
-    launch_mesh_emit(a, h->d_mesh_cfg, h->d_mesh_boff, h->d_mesh_tris, h->mesh_tris_cap, s);
+    launch_mesh_emit(a, h->d_mesh_cfg, h->d_mesh_boff, h->d_mesh_tris, h->d_mesh_cols, h->mesh_tris_cap, s);
     HIPCHK(hipGetLastError());
     h->mesh_n = (int64_t)total;
     if (n_tris) *n_tris = (int64_t)total;
+    return TSLAM_OK;
+}
+
+int tslam_mesh_read_colors(tslam_handle* h, float* colors, int64_t max_tris) {
+    if (!h || !h->tsdf_on || !h->tsdf_color || !h->d_mesh_cols) return fail(TSLAM_ESTATE, "no colour layer mesh");
+    if (max_tris < 0 || (max_tris > 0 && !colors)) return fail(TSLAM_EINVAL, "bad buffer");
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    const int64_t n = std::min(max_tris, h->mesh_n);
+    if (n > 0) HIPCHK(hipMemcpy(colors, h->d_mesh_cols, sizeof(float) * 9 * (size_t)n, hipMemcpyDeviceToHost));
     return TSLAM_OK;
 }
 

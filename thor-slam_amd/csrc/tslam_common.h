@@ -237,6 +237,11 @@ struct TsdfArgs {
     double fx, fy, cx, cy;
     const int32_t* map;        // [H][W][2] undistortion table (fixed point, 5 bits) or null
     const double* poses;       // [n][TSDF_POSE]
+    // colour layer (null when off): frame 0's BGR image (frames `stride` bytes apart, as the
+    // depth), the running colour [nv][3] (R, G, B) f32 and its weight f32
+    const uint8_t* color;
+    float* col;
+    float* col_w;
 };
 void launch_tsdf(const BatchCtx& c, int pair, int f0, const double* host_wTc_dev, const TsdfArgs& a, double* poses,
                  hipStream_t s);
@@ -253,11 +258,12 @@ struct DenseArgs {
     float site_dist;           // ESDF site: |tsdf| <= site_dist
     float max_dist;            // ESDF value beyond R voxels
     int32_t cap;               // R^2 + 1
+    const float* color;        // mesh: the colour layer [nv][3] or null (no vertex colours)
 };
 void launch_mesh_count(const DenseArgs& a, uint8_t* cfg, uint32_t* block_sums, uint64_t* block_off, uint64_t* total,
                        hipStream_t s);
-void launch_mesh_emit(const DenseArgs& a, const uint8_t* cfg, const uint64_t* block_off, float* tris, int64_t cap,
-                      hipStream_t s);
+void launch_mesh_emit(const DenseArgs& a, const uint8_t* cfg, const uint64_t* block_off, float* tris, float* cols,
+                      int64_t cap, hipStream_t s);
 void launch_esdf(const DenseArgs& a, int R, const float* tab, int32_t* g0, int32_t* g1, float* out, hipStream_t s);
 void launch_esdf_slice(const DenseArgs& a, int y0, int y1, int R, const float* tab, int32_t* g0, int32_t* g1,
                        uint8_t* obs, float* out, hipStream_t s);

@@ -199,6 +199,13 @@ _SIGNATURES = {
                                             ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_tsdf_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_tsdf_write": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_tsdf_color": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "tslam_tsdf_integrate_rgbd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
+                                                 ctypes.c_void_p]),
+    "tslam_tsdf_read_color": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_tsdf_write_color": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_mesh_read_colors": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     "tslam_mesh_extract": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
     "tslam_mesh_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     "tslam_esdf_compute": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_void_p]),
@@ -674,6 +681,40 @@ class Handle:
         _check(self.lib.tslam_tsdf_init(self.h, o.ctypes.data, d.ctypes.data, float(voxel_size), float(trunc_vox),
                                         float(max_dist), float(max_weight)))
 
+    def tsdf_color(self, enable: bool = True) -> None:
+        """The colour layer (call before tsdf_init)."""
+        _check(self.lib.tslam_tsdf_color(self.h, int(bool(enable))))
+        self._tsdf_color = bool(enable)
+
+    def tsdf_integrate_rgbd(self, color_dev_ptr: int, depth_dev_ptr: int, stride_bytes: int, n_frames: int,
+                            first_frame: int = 0, world_T_cam: np.ndarray | None = None, pair: int = 0,
+                            stream: int = 0) -> None:
+        """Depth + BGR colour of n frames (device, both ``stride_bytes`` apart) into the volume and
+        its colour layer, with host poses or the last batch's tracked device poses."""
+        poses = None
+        if world_T_cam is not None:
+            poses = np.ascontiguousarray(np.asarray(world_T_cam, dtype=np.float64).reshape(-1, 4, 4))
+        _check(self.lib.tslam_tsdf_integrate_rgbd(self.h, int(pair), ctypes.c_void_p(color_dev_ptr),
+                                                  ctypes.c_void_p(depth_dev_ptr), int(stride_bytes), int(n_frames),
+                                                  int(first_frame), None if poses is None else poses.ctypes.data,
+                                                  ctypes.c_void_p(stream)))
+
+    def tsdf_read_color(self) -> tuple[np.ndarray, np.ndarray]:
+        """(colour [nz][ny][nx][3] R, G, B f32, weight [nz][ny][nx] f32) of the colour layer."""
+        nx, ny, nz = self._tsdf_dims
+        c = np.zeros((nz, ny, nx, 3), dtype=np.float32)
+        w = np.zeros((nz, ny, nx), dtype=np.float32)
+        _check(self.lib.tslam_tsdf_read_color(self.h, c.ctypes.data, w.ctypes.data))
+        return c, w
+
+    def tsdf_write_color(self, color: np.ndarray, weight: np.ndarray) -> None:
+        nx, ny, nz = self._tsdf_dims
+        c = np.ascontiguousarray(color, dtype=np.float32)
+        w = np.ascontiguousarray(weight, dtype=np.float32)
+        if c.shape != (nz, ny, nx, 3) or w.shape != (nz, ny, nx):
+            raise ValueError(f"colour layer must be {(nz, ny, nx, 3)} / {(nz, ny, nx)}")
+        _check(self.lib.tslam_tsdf_write_color(self.h, c.ctypes.data, w.ctypes.data))
+
     def tsdf_integrate(self, depth_dev_ptr: int, stride_bytes: int, n_frames: int, first_frame: int = 0,
                        world_T_cam: np.ndarray | None = None, pair: int = 0, stream: int = 0) -> None:
         """Integrate n depth frames (device u16 mm, ``stride_bytes`` apart) with host poses
@@ -703,13 +744,19 @@ class Handle:
         _check(self.lib.tslam_tsdf_write(self.h, t.ctypes.data, w.ctypes.data))
 
     # -- dense-map outputs (nvblox's mesh / ESDF / distance slice; thor_slam_amd/dense.py) -------
-    def mesh(self, min_weight: float = 1e-4, stream: int = 0) -> np.ndarray:
-        """Marching-cubes triangle soup [n][3][3] f32 (metres), cube order (synchronises)."""
+    def mesh(self, min_weight: float = 1e-4, stream: int = 0, colors: bool = False):
+        """Marching-cubes triangle soup [n][3][3] f32 (metres), cube order (synchronises); with
+        ``colors`` (colour layer) also the vertex colours [n][3][3] f32: (triangles, colours)."""
         n = ctypes.c_int64()
         _check(self.lib.tslam_mesh_extract(self.h, float(min_weight), ctypes.byref(n), ctypes.c_void_p(stream)))
         out = np.zeros((n.value, 3, 3), dtype=np.float32)
         _check(self.lib.tslam_mesh_read(self.h, out.ctypes.data, int(n.value)))
-        return out
+        if not colors:
+            return out
+        col = np.zeros((n.value, 3, 3), dtype=np.float32)
+        if n.value:
+            _check(self.lib.tslam_mesh_read_colors(self.h, col.ctypes.data, int(n.value)))
+        return out, col
 
     def esdf(self, max_dist: float = 2.0, site_vox: float = 1.0, min_weight: float = 1e-4, stream: int = 0) -> np.ndarray:
         """Signed distance field f32 [nz][ny][nx] (NaN = unobserved; synchronises)."""

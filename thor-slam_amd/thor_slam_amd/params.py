@@ -86,6 +86,8 @@ class HipSlamConfig(SlamConfig):
     tsdf_integrator_max_integration_distance_m: float = 10.0
     tsdf_integrator_truncation_distance_vox: float = 4.0
     tsdf_max_weight: float = 100.0
+    # nvblox's colour layer: the RGB image averaged into the voxels near the surface (mesh colours)
+    dense_color: bool = True
     # the volume, axis-aligned in the tracking world (rectified camera of the first frame, RDF:
     # x right, y down, z forward): corner (m) and voxel counts (x, y, z); 10 x 4 x 11 m by default
     tsdf_origin: tuple = (-5.0, -2.0, -1.0)

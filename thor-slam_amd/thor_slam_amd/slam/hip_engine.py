@@ -210,6 +210,8 @@ class HipSlamEngine(SlamEngine):
             if len(self._pairs) > 1 and self._shard is None:   # the rig's body motion, on the device from all pairs
                 self._handle.set_rig(self._base_T_rects)
             if cfg.dense_map:
+                if cfg.dense_color:
+                    self._handle.tsdf_color(True)
                 self._handle.tsdf_init(cfg.tsdf_origin, cfg.tsdf_dims, cfg.voxel_size,
                                        cfg.tsdf_integrator_truncation_distance_vox,
                                        cfg.tsdf_integrator_max_integration_distance_m, cfg.tsdf_max_weight)
@@ -471,8 +473,12 @@ class HipSlamEngine(SlamEngine):
             return
         r = self._rects[0]
         hw = r.width * r.height
-        self._handle.tsdf_integrate(records_ptr + 3 * hw, 5 * hw * len(self._pairs), n,
-                                    first_frame=self._handle.frames_done - n, pair=0, stream=stream)
+        if self._config.dense_color:   # the record's BGR part with its depth part
+            self._handle.tsdf_integrate_rgbd(records_ptr, records_ptr + 3 * hw, 5 * hw * len(self._pairs), n,
+                                             first_frame=self._handle.frames_done - n, pair=0, stream=stream)
+        else:
+            self._handle.tsdf_integrate(records_ptr + 3 * hw, 5 * hw * len(self._pairs), n,
+                                        first_frame=self._handle.frames_done - n, pair=0, stream=stream)
 
     def get_dense_map(self) -> dict | None:
         """The TSDF volume (nvblox-shaped): ``tsdf`` / ``weight`` f32 [nz][ny][nx] (metres of
@@ -485,19 +491,25 @@ class HipSlamEngine(SlamEngine):
             return None
         self.flush()
         tsdf, weight = self._handle.tsdf_read()
-        return {"tsdf": tsdf, "weight": weight, "origin": np.array(cfg.tsdf_origin, dtype=np.float64),
+        out = {}
+        if cfg.dense_color:
+            out["color"], out["color_weight"] = self._handle.tsdf_read_color()
+        return {**out, "tsdf": tsdf, "weight": weight, "origin": np.array(cfg.tsdf_origin, dtype=np.float64),
                 "voxel_size": float(cfg.voxel_size),
                 "truncation_m": cfg.tsdf_integrator_truncation_distance_vox * cfg.voxel_size,
                 "world_T_volume": self._map_offset @ self._base_T_rect}
 
     def get_mesh(self) -> dict | None:
         """The surface mesh of the TSDF volume (marching cubes on the device, k_dense.hip):
-        ``triangles`` f32 [n][3][3] (metres in the tracking world, facing free space) and
-        ``world_T_volume``.  None unless ``dense_map`` is on.  Synchronises."""
+        ``triangles`` f32 [n][3][3] (metres in the tracking world, facing free space), with the
+        colour layer ``colors`` f32 [n][3][3] (R, G, B per vertex), and ``world_T_volume``.  None unless ``dense_map`` is on.  Synchronises."""
         cfg = self._config
         if not cfg.dense_map or self._handle is None:
             return None
         self.flush()
+        if cfg.dense_color:
+            tris, cols = self._handle.mesh(cfg.mesh_integrator_min_weight, colors=True)
+            return {"triangles": tris, "colors": cols, "world_T_volume": self._map_offset @ self._base_T_rect}
         return {"triangles": self._handle.mesh(cfg.mesh_integrator_min_weight),
                 "world_T_volume": self._map_offset @ self._base_T_rect}
 
