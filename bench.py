@@ -735,6 +735,8 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     # HIP events (per-launch events inside the timed steps would add their own gaps to the BA chain)
     schur = h.ba_replay_schur(0, 50, sp) if c4 else None
     front = {k: v for k, v in per_kernel_us.items() if k not in ("local_ba", "tsdf")}
+    if not front:
+        raise SystemExit("--kernel-events must name at least one front-end kernel (the roofline's live launch time)")
     dom = max(front, key=front.get)
     achieved = dom_bytes / (per_kernel_us[dom] * 1e-6) / 1e9
     mfma = None
