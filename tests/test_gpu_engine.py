@@ -241,6 +241,8 @@ def test_engine_async_equals_sync():
         for _ in range(10):
             p = eng.process_frames(rig.get_synchronized_frames())
             out.append(None if p is None else (p.timestamp, p.to_4x4_matrix()))
+        if mode == "async":   # CameraRig names an identity IMU (rig.py:92-93) that sends no sample:
+            assert eng._imu is not None and eng._async   # the filter stays idle and batches stay in flight
         eng.flush()
         last = eng.process_frames(rig.get_synchronized_frames())
         eng.flush()
