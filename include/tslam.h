@@ -445,6 +445,13 @@ int tslam_group_destroy(tslam_group* g);
  * by the adjoint of E_p^-1 and summed; the pairs' cameras are E_p^-1 B); pair = n_pairs then reads
  * that body window: cam_T_world[W][16] = body_T_world (base_link), counts = the joint ones,
  * landmark / points / obs_uvd filled with -1 / 0 / NaN (the landmarks live in the pairs' windows). */
+/* IMU rotation factor of keyframe `frame` of `pair` for its local BA window (before the batch that
+ * contains the frame is submitted): M (row-major 3x3) = the gyro-integrated rotation from the
+ * previous keyframe's rectified-left camera to this one's (frame g - ba_kf_interval points to
+ * frame g), weight (1 / rad^2; 0 = none).  Every Gauss-Newton step of the window then adds the
+ * residual vee((M^T R_c R_{c-1}^T - ...) / 2) between window-consecutive keyframes (spec:
+ * oracle/numpy_ba.py imu_terms).  Pair windows only (a rig's body window ignores it). */
+int tslam_ba_imu_factor(tslam_handle* h, int pair, int64_t frame, const double* M, double weight);
 int tslam_ba_read(tslam_handle* h, int pair, int64_t* frames, double* cam_T_world, int32_t* landmark,
                   double* points, double* obs_uvd, int32_t* counts);
 

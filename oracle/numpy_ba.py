@@ -31,6 +31,13 @@ Spec (shared with ``thor-slam_amd/csrc/k_ba.hip``):
       ``b = -g_c + sum_i sum_{o in i} W_o V_i^-1 g_p,i`` with ``V_i = sum J_p^T J_p + lam I``;
     - ``S' dc = b'`` without camera 0 (Cholesky), ``dp_i = V_i^-1 (-g_p,i - sum_o W_o^T dc_o)``;
     - cameras ``R <- cayley(w) R, t <- cayley(w) t + rho``; points ``X += dp``.
+* IMU rotation factors (optional): keyframe g may carry the gyro-integrated rotation ``M`` from the
+  previous keyframe's camera to its own (frame g - kf_interval points to frame g) with a weight
+  ``w`` (1 / rad^2, 0 = none).  Between window-consecutive keyframes (c - 1, c) whose later one
+  carries a factor, with ``Q = R_c R_{c-1}^T`` and ``e = vee((A - A^T) / 2)``, ``A = M^T Q``: the
+  residual e has Jacobians ``Q^T`` on camera c's rotation and ``-I`` on camera c - 1's (left
+  updates), so ``S_cc += w I``, ``S_{c-1,c-1} += w I``, ``S_{c,c-1} += -w Q`` (rotation blocks),
+  ``b_c -= w Q e``, ``b_{c-1} += w e``; camera 0's rows drop with the gauge.
 """
 
 from __future__ import annotations
@@ -77,6 +84,8 @@ class KeyframeWindow:
         self.d = np.full((W, K), np.nan)
         self.lm = np.full((W, K), -1, dtype=np.int64)
         self.X = np.zeros((W * K, 3))
+        self.imu_M = np.tile(np.eye(3), (W, 1, 1))   # IMU rotation from the previous keyframe
+        self.imu_w = np.zeros(W)                     # its weight (0 = no factor)
         self.n_kf = 0
 
     # -- window bookkeeping --------------------------------------------------------------------
@@ -106,9 +115,10 @@ class KeyframeWindow:
         self.frame[slot] = -1
 
     def add_keyframe(self, g: int, T_cw: np.ndarray, u: np.ndarray, v: np.ndarray, disp: np.ndarray,
-                     link: np.ndarray | None) -> int:
+                     link: np.ndarray | None, imu: tuple | None = None) -> int:
         """Insert keyframe g (u, v level-0 observations, NaN = invalid; disp refined, NaN = none;
-        link into the previous keyframe or None for the first)."""
+        link into the previous keyframe or None for the first; imu = (M, w) the IMU rotation
+        factor from the previous keyframe, or None)."""
         K = self.K
         slot = self.n_kf % self.p.window
         prev = self.order()[-1] if self.n_kf else -1
@@ -116,6 +126,7 @@ class KeyframeWindow:
             self._evict(slot)
         self.frame[slot] = g
         self.T_cw[slot] = T_cw
+        self.imu_M[slot], self.imu_w[slot] = (np.eye(3), 0.0) if imu is None else (np.asarray(imu[0], float), float(imu[1]))
         self.u[slot], self.v[slot] = u, v
         self.d[slot] = np.where(np.isfinite(disp) & (disp > 0), disp, np.nan)
         valid = np.isfinite(u)
@@ -233,6 +244,23 @@ class KeyframeWindow:
         np.add.at(rhs, ob["li"], -np.einsum("nji,nj->ni", lin["Wo"], dcc[ob["cam"]]))
         return np.einsum("lij,lj->li", lin["Vinv"], rhs)
 
+    def imu_terms(self, slots: list[int], Rs: np.ndarray, S: np.ndarray, b: np.ndarray) -> None:
+        """The IMU rotation factors between window-consecutive keyframes, into S and b in place."""
+        for c in range(1, len(slots)):
+            w = self.imu_w[slots[c]]
+            if not w > 0.0:
+                continue
+            Q = Rs[c] @ Rs[c - 1].T
+            A = self.imu_M[slots[c]].T @ Q
+            e = 0.5 * np.array([A[2, 1] - A[1, 2], A[0, 2] - A[2, 0], A[1, 0] - A[0, 1]])
+            rc, rp = 6 * c + 3, 6 * (c - 1) + 3
+            S[rc:rc + 3, rc:rc + 3] += w * np.eye(3)
+            S[rp:rp + 3, rp:rp + 3] += w * np.eye(3)
+            S[rc:rc + 3, rp:rp + 3] -= w * Q
+            S[rp:rp + 3, rc:rc + 3] -= w * Q.T
+            b[rc:rc + 3] -= w * (Q @ e)
+            b[rp:rp + 3] += w * e
+
     def solve(self) -> dict:
         p = self.p
         slots = self.order()
@@ -244,6 +272,7 @@ class KeyframeWindow:
         Rs, ts = T[:, :3, :3].copy(), T[:, :3, 3].copy()
         for _ in range(p.iters):
             lin = self.linearize(ob, Rs, ts)
+            self.imu_terms(slots, Rs, lin["S"], lin["b"])
             S = lin["S"] + p.lam * np.eye(6 * n)
             dc = np.zeros(6 * n)
             dc[6:] = np.linalg.solve(S[6:, 6:], lin["b"][6:])
@@ -398,7 +427,8 @@ class BATracker:
         self.temporal: list[np.ndarray] = []   # newest first, the last kf_interval frames
         self.last_solve: dict | None = None
 
-    def step(self, res: dict) -> dict | None:
+    def step(self, res: dict, imu: tuple | None = None) -> dict | None:
+        """One frame's tracker result; ``imu`` = (M, w), the keyframe's IMU rotation factor."""
         g = int(res["frame"])
         cur = res["cur"]
         self.temporal.insert(0, np.asarray(cur["temporal"], dtype=np.int64))
@@ -415,7 +445,7 @@ class BATracker:
             T_wc = _inv_rigid(w.T_cw[prev]) @ _inv_rigid(self.Tfe[prev]) @ W_fe
             link = chain_links(self.temporal[: self.p.kf_interval])
         u, v = keyframe_observations(cur["left"], self.K)
-        slot = w.add_keyframe(g, _inv_rigid(T_wc), u, v, np.asarray(cur["disp"], dtype=np.float64), link)
+        slot = w.add_keyframe(g, _inv_rigid(T_wc), u, v, np.asarray(cur["disp"], dtype=np.float64), link, imu=imu)
         self.Tfe[slot] = W_fe
         self.last_solve = w.solve()
         return self.last_solve

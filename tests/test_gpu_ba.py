@@ -28,7 +28,20 @@ def _scenario_and_oracle(n: int):
     return sc, _oracle_windows(sc)
 
 
-def _oracle_windows(sc):
+def _imu_factors(sc, n: int, angle: float = 3e-3, weight: float = 1e5) -> dict:
+    """Per keyframe g > 0: the front end's rotation from keyframe g - interval to g, turned by
+    `angle` about z (so the factor pulls), and its weight."""
+    iv = sc["cfg"].ba_kf_interval
+    Rz = np.array([[np.cos(angle), -np.sin(angle), 0.0], [np.sin(angle), np.cos(angle), 0.0], [0.0, 0.0, 1.0]])
+    out = {}
+    for g in range(iv, n, iv):
+        Rc = np.linalg.inv(sc["oracle"][g]["world_T_cam"])[:3, :3]
+        Rp = np.linalg.inv(sc["oracle"][g - iv]["world_T_cam"])[:3, :3]
+        out[g] = (Rz @ Rc @ Rp.T, weight)
+    return out
+
+
+def _oracle_windows(sc, imu: dict | None = None):
     from oracle.numpy_ba import BAParams, BATracker
 
     cfg, rect = sc["cfg"], sc["rect"]
@@ -36,8 +49,8 @@ def _oracle_windows(sc):
                   outlier_px=cfg.ba_outlier_px)
     trk = BATracker(cfg.n_features, (rect.fx, rect.fy, rect.cx, rect.cy, rect.fx * rect.baseline), bp)
     snaps = []
-    for res in sc["oracle"]:
-        trk.step(res)
+    for g, res in enumerate(sc["oracle"]):
+        trk.step(res, imu=None if imu is None else imu.get(g))
         w = trk.win
         snaps.append({"frames": w.frame.copy(), "T_cw": w.T_cw.copy(), "lm": w.lm.copy(), "X": w.X.copy(),
                       "u": w.u.copy(), "v": w.v.copy(), "d": w.d.copy(), "solve": trk.last_solve})
@@ -81,6 +94,33 @@ def test_ba_window_parity(batch):
         h.close()
     assert (want[-1]["frames"] >= 0).all()
     assert want[-1]["solve"]["n_lm"] > 50
+
+
+def test_ba_imu_rotation_factors_parity():
+    """IMU rotation factors between window-consecutive keyframes (tslam_ba_imu_factor) against the
+    oracle's imu_terms: same windows to 1e-9, through evictions, in batches of 3 — and the factors
+    move the solution (it differs from the vision-only window)."""
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    n, batch = 12, 3
+    sc, plain = _scenario_and_oracle(n)
+    imu = _imu_factors(sc, n)
+    want = _oracle_windows(sc, imu)
+    h = Handle([sc["rect"]], sc["cfg"], max_batch=batch)
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    try:
+        for g, (M, w) in imu.items():
+            h.ba_imu_factor(g, M, w)
+        for b0 in range(0, n, batch):
+            h.submit(dev[b0:].data_ptr(), batch, torch.cuda.current_stream().cuda_stream)
+            _compare(h.ba_read(0), want[b0 + batch - 1], f"imu factors, after frame {b0 + batch - 1}")
+    finally:
+        h.close()
+    occ = want[-1]["frames"] >= 0
+    moved = max(rel_frobenius(want[-1]["T_cw"][s_], plain[-1]["T_cw"][s_]) for s_ in np.nonzero(occ)[0])
+    assert moved > 1e-6, moved
 
 
 def test_ba_stage_is_idempotent_per_batch():

@@ -122,6 +122,7 @@ __global__ __launch_bounds__(256) void k_ba_insert(BatchCtx c, BaArgs a) {
                 q.T[(size_t)a.slot * 16 + e] = Tcw[e];
             }
     }
+    if (blockIdx.x == 0 && threadIdx.x < 10) q.imu[(size_t)a.slot * 10 + threadIdx.x] = a.imu[threadIdx.x];
     __syncthreads();
     const PairCalib cal = c.calib[p];
     const double* disp = c.disp + ((size_t)rslot * c.P + p) * K;
@@ -735,6 +736,36 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, Ba
             v += s_U[ci * 27 + lo * 6 - lo * (lo - 1) / 2 + (hi - lo)] + (i0 == j0 ? a.lam : 0.0);
         }
         s_S[i * BA_SP + k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // IMU rotation factors between window-consecutive keyframes (oracle imu_terms): with
+        // Q = R_c R_{c-1}^T, e = vee((A - A^T) / 2), A = M^T Q — S_cc, S_{c-1,c-1} += w I,
+        // S_{c,c-1} -= w Q (rotation blocks, lower triangle), b_c -= w Q e, b_{c-1} += w e; camera 0
+        // (the gauge) has no rows
+        for (int cc = 1; cc < n; ++cc) {
+            const double* f = q.imu + (size_t)a.order[cc] * 10;
+            const double w = f[9];
+            if (!(w > 0.0)) continue;
+            const double* Tc = q.T + (size_t)a.order[cc] * 16;
+            const double* Tp = q.T + (size_t)a.order[cc - 1] * 16;
+            double Q[9], A[9];
+            for (int r = 0; r < 3; ++r)
+                for (int k = 0; k < 3; ++k) Q[3 * r + k] = Tc[4 * r] * Tp[4 * k] + Tc[4 * r + 1] * Tp[4 * k + 1] + Tc[4 * r + 2] * Tp[4 * k + 2];
+            for (int r = 0; r < 3; ++r)
+                for (int k = 0; k < 3; ++k) A[3 * r + k] = f[r] * Q[k] + f[3 + r] * Q[3 + k] + f[6 + r] * Q[6 + k];   // M^T Q
+            const double e[3] = {0.5 * (A[7] - A[5]), 0.5 * (A[2] - A[6]), 0.5 * (A[3] - A[1])};
+            const int rc = 6 * (cc - 1) + 3, rp = 6 * (cc - 2) + 3;
+            for (int r = 0; r < 3; ++r) {
+                s_S[(rc + r) * BA_SP + rc + r] += w;
+                s_x[rc + r] -= w * ((Q[3 * r] * e[0] + Q[3 * r + 1] * e[1]) + Q[3 * r + 2] * e[2]);
+                if (cc >= 2) {
+                    s_S[(rp + r) * BA_SP + rp + r] += w;
+                    s_x[rp + r] += w * e[r];
+                    for (int k = 0; k < 3; ++k) s_S[(rc + r) * BA_SP + rp + k] -= w * Q[3 * r + k];
+                }
+            }
+        }
     }
     __syncthreads();
     const bool live = lane < m;

@@ -6,7 +6,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <limits>
+#include <map>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -142,6 +144,7 @@ struct tslam_handle {
     int64_t ba_nkf = 0;
     int64_t ba_last = -1;    // newest frame inserted
     BaTiming ba_timing{};    // k_ba_schur events while profiling is on
+    std::map<std::pair<int, int64_t>, std::array<double, 10>> ba_imu;   // (pair, keyframe) -> IMU factor
     std::vector<BaArgs> ba_solved;   // per pair: the arguments of its last window solve (replays)
     // BA on its own stream (overlapping the next batch): events and the batch parity
     int64_t batch_idx = 0;
@@ -310,7 +313,7 @@ static int alloc_ba(tslam_handle* h) {
         {(void**)&b.lm_L, 8 * P * WK * 6},   {(void**)&b.lm_gp, 8 * P * WK * 3}, {(void**)&b.C, 8 * P * 64 * 64},
         {(void**)&b.part, 8 * P * (size_t)TS_BA_SPLIT * 64 * 64}, {(void**)&b.cam_U, 8 * P * W * 27}, {(void**)&b.dc, 8 * P * W * 6},
         {(void**)&b.flops, 8},               {(void**)&b.fe_pose, 8 * 2 * (size_t)h->B * h->P * 16},
-        {(void**)&b.fe_body, 8 * 2 * (size_t)h->B * 16},
+        {(void**)&b.fe_body, 8 * 2 * (size_t)h->B * 16}, {(void**)&b.imu, 8 * P * W * 10},
     };
     for (const A& a : list) {
         const int rc = dev_alloc(h, a.p, a.bytes);
@@ -377,8 +380,14 @@ static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const doub
         }
         for (int p = 0; p < h->P; ++p) {
             a.pair = p;
+            auto it = h->ba_imu.find({p, g});   // the keyframe's IMU rotation factor (if given)
+            for (int e = 0; e < 10; ++e) a.imu[e] = (!rig && it != h->ba_imu.end()) ? it->second[e] : 0.0;
+            if (it != h->ba_imu.end()) h->ba_imu.erase(it);
             launch_ba_keyframe(c, a, evict, s);
         }
+        for (int e = 0; e < 10; ++e) a.imu[e] = 0.0;
+        for (auto it = h->ba_imu.begin(); it != h->ba_imu.end();)   // factors of frames already past
+            it = it->first.second < g ? h->ba_imu.erase(it) : std::next(it);
         h->ba_frame[a.slot] = g;
         h->ba_nkf += 1;
         h->ba_last = g;
@@ -2093,6 +2102,17 @@ int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_e
     }
     for (int i = 0; i < 16 * n_nodes; ++i)
         if (!std::isfinite(world_T_node[i])) return fail(TSLAM_ESTATE, "pose graph: normal matrix not positive definite");
+    return TSLAM_OK;
+}
+
+int tslam_ba_imu_factor(tslam_handle* h, int pair, int64_t frame, const double* M, double weight) {
+    if (!h || !M || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad argument");
+    if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
+    if (!(weight >= 0.0) || frame < 0) return fail(TSLAM_EINVAL, "weight must be >= 0, frame >= 0");
+    std::array<double, 10> f{};
+    for (int e = 0; e < 9; ++e) f[e] = M[e];
+    f[9] = weight;
+    h->ba_imu[{pair, frame}] = f;
     return TSLAM_OK;
 }
 

@@ -68,6 +68,7 @@ struct BaStore {
     double* flops;     // [1] algorithmic Schur-product flops accumulated (profiling)
     double* fe_pose;   // [2][B][P][16] front-end world_T_cam of the batch (snapshot per batch parity)
     double* fe_body;   // [2][B][16] rig front end's world_T_body of the batch (rig-level A8)
+    double* imu;       // [P][W][10] IMU rotation factor per slot: M (row-major 9), weight (0 = none)
 };
 
 struct BaArgs {
@@ -86,6 +87,7 @@ struct BaArgs {
     double lam, outlier_px;
     const double* fe;           // insert: this batch's front-end pose snapshot [B][P][16]
     const double* fe_body;      // rig insert: the rig front end's snapshot [B][16]
+    double imu[10];             // insert: the keyframe's IMU rotation factor (M 9, weight; 0 = none)
 };
 
 // Per-pair view (the scratch pointers are shared).
@@ -102,6 +104,7 @@ struct BaPair {
     int32_t *remap, *cnt, *li, *lm_id, *camobs, *obs_cam, *obs_k, *obs_id, *cam_off, *counts, *tiles, *lo_o;
     uint8_t* keep;
     double *lo_uvd, *lo_W, *Xc, *obs_Ug, *obs_Vg, *lm_L, *lm_gp, *part, *C, *cam_U, *dc, *flops;
+    double* imu;
 };
 
 __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, int p) {
@@ -129,6 +132,7 @@ __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, in
     q.lm_L = s.lm_L + p * WK * 6; q.lm_gp = s.lm_gp + p * WK * 3;
     q.part = s.part + p * (size_t)TS_BA_SPLIT * 4096; q.C = s.C + p * 4096;
     q.cam_U = s.cam_U + p * W * 27; q.dc = s.dc + p * W * 6; q.flops = s.flops;
+    q.imu = s.imu + p * W * 10;
     return q;
 }
 

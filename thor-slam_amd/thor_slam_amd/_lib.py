@@ -199,6 +199,7 @@ _SIGNATURES = {
                                             ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_tsdf_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_tsdf_write": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_ba_imu_factor": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_double]),
     "tslam_tsdf_color": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "tslam_tsdf_integrate_rgbd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                                  ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
@@ -775,6 +776,12 @@ class Handle:
         _check(self.lib.tslam_esdf_slice(self.h, int(y0), int(y1), float(max_dist), float(site_vox), float(min_weight),
                                          out.ctypes.data))
         return out
+
+    def ba_imu_factor(self, frame: int, M: np.ndarray, weight: float, pair: int = 0) -> None:
+        """IMU rotation factor of keyframe ``frame`` (the rotation from the previous keyframe's
+        camera, 3x3, and its weight) for the local BA window."""
+        m = np.ascontiguousarray(M, dtype=np.float64).reshape(9)
+        _check(self.lib.tslam_ba_imu_factor(self.h, int(pair), int(frame), m.ctypes.data, float(weight)))
 
     def ba_replay_schur(self, pair: int = 0, reps: int = 50, stream: int = 0) -> dict:
         """Average k_ba_schur duration (HIP events around ``reps`` replays) and flops per launch."""
