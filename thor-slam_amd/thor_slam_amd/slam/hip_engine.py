@@ -136,6 +136,7 @@ class HipSlamEngine(SlamEngine):
         self._staged_imu: list[tuple | None] = []    # (gyro, accel) per staged frame
         self._imu: ImuPropagator | None = None       # IMU filter (gyro bias; accelerometer leg with imu_accel)
         self._imu_batches: list = []                  # IMU samples of submitted, unpublished batches (None: no data)
+        self._kf_imu: tuple | None = None             # gyro rotation since the last BA keyframe (R, var, first frame)
         self._prev_stamp: float | None = None      # timestamp of the last submitted frame (IMU dt)
         self._base_R_imu = np.eye(3)
         self._torch = None
@@ -426,6 +427,7 @@ class HipSlamEngine(SlamEngine):
                 samples.append((None, None, None))
             prev = ts
         steps = imu.batch_priors(samples)
+        self._ba_imu_factors(steps)
         P, n = len(self._pairs), len(stamps)
         rot = np.tile(np.eye(3), (n, P, 1, 1))
         trn = np.zeros((n, P, 3))
@@ -442,6 +444,29 @@ class HipSlamEngine(SlamEngine):
                 wr[k, p], wt[k, p] = st.w_rot, st.w_trans
         self._set_motion_prior(rot, wr, trn, wt)
         self._imu_batches.append((samples, steps))
+
+    def _ba_imu_factors(self, steps: list) -> None:
+        """The local BA's IMU rotation factors (one stereo pair): the per-frame gyro rotations of
+        the staged batch composed since the last keyframe; at each keyframe whose whole interval
+        had IMU steps, the rotation from the previous keyframe's camera and the inverse of the
+        summed rotation variances (1 / rad^2: the reprojection residuals have unit pixel weight)
+        go to tslam_ba_imu_factor before the batch is submitted."""
+        cfg = self._config
+        if cfg.ba_window <= 0 or len(self._pairs) != 1 or self._shard is not None:
+            return
+        g = self._handle.frames_done
+        for k, st in enumerate(steps):
+            gk = g + k
+            if st is None or self._kf_imu is None:
+                self._kf_imu = None if st is None else (st.R_rel.copy(), 1.0 / st.w_rot, gk)
+            else:
+                rot, var, start = self._kf_imu
+                self._kf_imu = (st.R_rel @ rot, var + 1.0 / st.w_rot, start)
+            if gk % cfg.ba_kf_interval == 0:
+                acc = self._kf_imu
+                if acc is not None and acc[2] == gk - cfg.ba_kf_interval + 1 and acc[1] > 0.0:
+                    self._handle.ba_imu_factor(gk, acc[0], 1.0 / acc[1])
+                self._kf_imu = (np.eye(3), 0.0, gk + 1)
 
     def _set_motion_prior(self, *args) -> None:
         """The batch's priors on the handle (every rank's handle on a sharded rig: each refines its
@@ -860,6 +885,7 @@ class HipSlamEngine(SlamEngine):
             self._latest_pose = None
         self._staged, self._staged_imu, self._prev_stamp = [], [], None
         self._imu_batches = []
+        self._kf_imu = None
         if self._imu is not None:
             self._imu.reset()
         self._keyframe_poses = []
