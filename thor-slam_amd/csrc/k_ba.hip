@@ -696,6 +696,7 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, Ba
     static_assert(TS_BA_MAXW * 27 <= 64 * BA_SOLVE_WAVES, "one camera-block load per thread");
     __shared__ double s_S[64 * BA_SP];             // lower: S; upper (row j, column i > j): l_ij
     __shared__ double s_U[TS_BA_MAXW * 27];
+    __shared__ double s_iw[TS_BA_MAXW];            // IMU rotation factor weight per window camera
     __shared__ __attribute__((aligned(16))) double s_pl[2][64][6];   // panel multipliers l_ij
     __shared__ __attribute__((aligned(16))) double s_pq[2][64][6];   // l_ij d_j
     __shared__ double s_d[64];
@@ -715,6 +716,7 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, Ba
 #pragma unroll
     for (int k = 0; k < NL; ++k) cv[k] = q.C[threadIdx.x + 64 * BA_SOLVE_WAVES * k];
     if ((int)threadIdx.x < n * 27) s_U[threadIdx.x] = q.cam_U[threadIdx.x];
+    if ((int)threadIdx.x < n) s_iw[threadIdx.x] = q.imu[(size_t)a.order[threadIdx.x] * 10 + 9];   // factor weights
     __syncthreads();
     // S_ik = -C[i+6][k+6] (+ U + lam inside a camera block), lower triangle; row i's right-hand
     // side -g_c + C[i+6][60] into s_x[i] (read back by wave 0)
@@ -738,15 +740,17 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, Ba
         s_S[i * BA_SP + k] = v;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    bool any_imu = false;
+    for (int cc = 1; cc < n; ++cc) any_imu = any_imu || s_iw[cc] > 0.0;   // (uniform: LDS broadcast)
+    if (any_imu && threadIdx.x == 0) {
         // IMU rotation factors between window-consecutive keyframes (oracle imu_terms): with
         // Q = R_c R_{c-1}^T, e = vee((A - A^T) / 2), A = M^T Q — S_cc, S_{c-1,c-1} += w I,
         // S_{c,c-1} -= w Q (rotation blocks, lower triangle), b_c -= w Q e, b_{c-1} += w e; camera 0
         // (the gauge) has no rows
         for (int cc = 1; cc < n; ++cc) {
-            const double* f = q.imu + (size_t)a.order[cc] * 10;
-            const double w = f[9];
+            const double w = s_iw[cc];
             if (!(w > 0.0)) continue;
+            const double* f = q.imu + (size_t)a.order[cc] * 10;
             const double* Tc = q.T + (size_t)a.order[cc] * 16;
             const double* Tp = q.T + (size_t)a.order[cc - 1] * 16;
             double Q[9], A[9];
@@ -767,7 +771,7 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, Ba
             }
         }
     }
-    __syncthreads();
+    if (any_imu) __syncthreads();
     const bool live = lane < m;
     double rhs = (w == 0 && live) ? s_x[lane] : 0.0;   // wave 0: right-hand side of row `lane`
     bool good = true;   // wave 0: every pivot positive
