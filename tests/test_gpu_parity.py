@@ -298,3 +298,50 @@ def test_c1_sequence_100_frames():
             assert rel_frobenius(rec["T_rel"], o["T"]) < 1e-9, f"frame {i}: T_rel"
         assert rel_frobenius(rec["T_abs"], o["world_T_cam"]) < 1e-9, f"frame {i}: T_abs"
     assert n_tracked >= 90, f"only {n_tracked} of {n - 1} frames tracked"
+
+
+@pytest.mark.parametrize("splits", [0, 1, 7])
+def test_ransac_bounded_scoring_with_outliers(splits):
+    """k_ransac drops a pose as soon as its count cannot reach the block's best key.  With 35 % of
+    the frame's refined positions moved 8-40 px (outliers to every pose), the RANSAC winner, its
+    count, the inliers and the refined pose still equal the oracle's exhaustive scoring."""
+    import torch
+
+    from oracle import numpy_slam as O
+    from thor_slam_amd._lib import Handle
+
+    sc = scenario(seed=0, n=3)
+    cfg, rect = sc["cfg"], sc["rect"]
+    K = cfg.n_features
+    h = Handle([rect], cfg, max_batch=1, ransac_splits=splits)
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    for g in range(2):
+        h.submit(dev[g:].data_ptr(), 1, s)
+    h.read_poses(1)
+    h.begin_batch(dev[2:].data_ptr(), 1)
+    for k in ("rectify_pyramid", "detect", "select", "describe", "match", "match_refine"):
+        h.run_kernel(k, s)
+    torch.cuda.synchronize()
+    corr = {k: np.array(v, copy=True) for k, v in sc["oracle"][2]["corr"].items()}
+    tuv = h.frame_block("temporal_uv", 0, np.float64)[: 2 * K].reshape(K, 2).copy()
+    np.testing.assert_array_equal(tuv[corr["j"], 0], corr["u"])
+    rng = np.random.default_rng(11)
+    m = rng.random(corr["j"].size) < 0.35
+    off = rng.uniform(8.0, 40.0, (int(m.sum()), 2)) * rng.choice([-1.0, 1.0], (int(m.sum()), 2))
+    corr["u"][m] += off[:, 0]
+    corr["v"][m] += off[:, 1]
+    corr["du"], corr["dv"] = rect.cx - corr["u"], rect.cy - corr["v"]
+    tuv[corr["j"], 0], tuv[corr["j"], 1] = corr["u"], corr["v"]
+    h.copy_in("temporal_uv", 0, tuv)
+    h.run_kernel("pose", s)
+    torch.cuda.synchronize()
+    st = h.frame_block("stats", 0, np.int32)[:5]
+    T = h.frame_block("pose", 0, np.float64)[:16].reshape(4, 4)
+    h.end_batch()
+    h.close()
+    o = O.estimate_pose(corr, (rect.fx, rect.fy, rect.cx, rect.cy), cfg, sc["oracle"][2]["frame"])
+    assert st[1] == corr["j"].size and 0.5 < o["best_count"] / st[1] < 0.75
+    assert (st[4], st[3]) == (o["best_hyp"], o["best_count"]), "RANSAC winner differs"
+    assert st[0] == o["status"] == 0 and st[2] == o["n_inliers"]
+    assert rel_frobenius(T, o["T"]) < 1e-9

@@ -241,8 +241,6 @@ __device__ bool solve6(const double* Hm, const double* g, double* x, double* L) 
 }
 
 #define POSE_THREADS 256
-#define TS_RS_CPT 4            // correspondences per thread per scoring pass
-#define TS_MAX_HYP_SPLIT 256   // hypotheses per RANSAC block (n_hyp <= 256)
 #define N_ACC 29   // 21 (upper H) + 6 (g) + 1 (sq) + 1 (count)
 
 __device__ __forceinline__ void write_stats(int32_t* so, int status, int n, int n_in, int best_cnt, int best_idx, int64_t g) {
@@ -386,14 +384,32 @@ __global__ __launch_bounds__(POSE_THREADS) void k_p3p(BatchCtx c) {
 }
 
 // ---- k_ransac: score one split of the poses of one (frame, pair) ---------------------------
-// grid (n*P*S): block (fp, split) scores the 4*(h1-h0) candidate poses of hypotheses [h0, h1):
-// correspondences stay in registers (TS_RS_CPT per thread); a pose is wave-uniform, so it comes
-// through scalar loads (SGPR operands of the f64 VALU ops — an LDS broadcast of its 96 bytes
-// returned 6 KiB per wave and bound the loop); inlier counts are wave ballots (integer sums:
-// order-independent).  Writes its best (count+1)<<12 | (4095 - pose index) key and that pose.
+// grid (n*P*S): block (fp, split) finds the best (count+1)<<12 | (4095 - pose index) key over the
+// 4*(h1-h0) candidate poses of hypotheses [h0, h1) and writes it with that pose.
+//
+// Bounded scoring: each wave takes its own poses (wave w: poses w, w+4, ...) and scans the frame's
+// correspondences 64 at a time (one per lane, inlier decisions by ballot), while the block keeps
+// the best key of the poses it has scored completely in LDS.  A pose whose count cannot reach that
+// key any more — count + unscanned < best count, or equal with a larger pose index — is dropped
+// mid-scan, and a pose that could not reach it with every correspondence an inlier is never
+// loaded.  The best key only grows and is always an exactly scored pose's, so every dropped pose
+// has a smaller key than the winner: the winner, its count and the pose are those of the
+// exhaustive scoring (the oracle's), only the work differs.  A wave first tests a pose on the
+// misses of the best pose it has scored itself (correct poses share their outliers), so a pose
+// that cannot win usually drops after that one chunk; with no outliers at all the first correct
+// root saturates the count and the remaining poses are not loaded.
+//
+// Correspondences are staged once per block in LDS as f32 (X Y Z du dv, |X|+|Y|+|Z|), the first
+// TS_RS_LDS_CAP of them (beyond that the f64 records are read from global memory); a pose is
+// wave-uniform, its f32 record in SGPR operands.
+#define TS_RS_LDS_CAP 2048
+#ifndef TS_RS_UNROLL
+#define TS_RS_UNROLL 4
+#endif
 __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
-    __shared__ int s_cnt[4 * TS_MAX_HYP_SPLIT];
-    __shared__ uint32_t s_wbest[4];
+    extern __shared__ float4 s_corr[];   // [cap] (X, Y, Z, du) then [cap] float2 (dv, S)
+    __shared__ uint32_t s_best;
+    __shared__ int s_wout[POSE_THREADS / 64][64];   // a wave's misses of the pose it is scanning
     const int fl = blockIdx.x / S;
     const int split = blockIdx.x % S;
     const int p = c.pair0 + fl % c.npair;
@@ -415,70 +431,140 @@ __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
     const double fx = cal.fx, fy = cal.fy;
     const double* corr = c.corr + ((size_t)f * c.P + p) * c.g.K * TS_CORR_DOUBLES;
     const double* hyp = c.hyp + ((size_t)fp * 4 * H + 4 * h0) * TS_HYP_DOUBLES;   // this split's poses
-    typedef const __attribute__((address_space(4))) double cdouble;   // uniform address -> s_load
-    cdouble* chyp = (cdouble*)(uintptr_t)hyp;
     const int npose = 4 * nh;
-    for (int i = tid; i < npose; i += POSE_THREADS) s_cnt[i] = 0;
+    const int cap = min(c.g.K, TS_RS_LDS_CAP);
+    const int nl = min(n, cap);
+    float2* s_cd = reinterpret_cast<float2*>(s_corr + cap);
+    for (int i = tid; i < nl; i += POSE_THREADS) {
+        const double* cr = corr + (size_t)i * TS_CORR_DOUBLES;
+        const float X = (float)cr[0], Y = (float)cr[1], Z = (float)cr[2];
+        s_corr[i] = make_float4(X, Y, Z, (float)cr[3]);
+        s_cd[i] = make_float2((float)cr[4], fabsf(X) + fabsf(Y) + fabsf(Z));
+    }
+    if (tid == 0) s_best = 0u;
     __syncthreads();
     const double thr2 = c.pp.thr2;
     const float fxf = (float)fx, fyf = (float)fy, thr2f = (float)thr2;
-    for (int c0 = 0; c0 < n; c0 += POSE_THREADS * TS_RS_CPT) {
-        float cf[TS_RS_CPT][8];   // X Y Z du dv, |X| + |Y| + |Z|, fx + |du|, fy + |dv|
-        bool have[TS_RS_CPT];
+    volatile uint32_t* vbest = &s_best;
+    // Per wave: the misses (first 64) of the best pose this wave has scored completely, one index
+    // per lane (-1: none).  The next pose is tested on those first: correct poses share their
+    // outliers, so a pose that cannot beat the block's best usually drops after one chunk.
+    int my_out = -1;
+    uint32_t my_key = 0u;
+    auto test = [&](const double* ps, const f32x16& pf, int i) -> int {
+        float q[8];
+        if (i < cap) {
+            const float4 a = s_corr[i];
+            const float2 b = s_cd[i];
+            q[0] = a.x; q[1] = a.y; q[2] = a.z; q[3] = a.w; q[4] = b.x; q[5] = b.y;
+        } else {
+            const double* cr = corr + (size_t)i * TS_CORR_DOUBLES;
 #pragma unroll
-        for (int k = 0; k < TS_RS_CPT; ++k) {
-            const int ci = c0 + k * POSE_THREADS + tid;
-            have[k] = ci < n;
-            const double* cr = corr + (size_t)(have[k] ? ci : 0) * TS_CORR_DOUBLES;
-#pragma unroll
-            for (int q = 0; q < 5; ++q) cf[k][q] = (float)cr[q];
-            cf[k][5] = fabsf(cf[k][0]) + fabsf(cf[k][1]) + fabsf(cf[k][2]);
-            cf[k][6] = fxf + fabsf(cf[k][3]);
-            cf[k][7] = fyf + fabsf(cf[k][4]);
+            for (int k = 0; k < 5; ++k) q[k] = (float)cr[k];
+            q[5] = fabsf(q[0]) + fabsf(q[1]) + fabsf(q[2]);
         }
-        // correspondence slots no lane of this wave has are skipped (wave-uniform)
-        const int kmax = min(TS_RS_CPT, (n - c0 - wave * 64 + POSE_THREADS - 1) / POSE_THREADS);
-        for (int pi = 0; pi < npose; ++pi) {
-            cdouble* ps = chyp + (size_t)pi * TS_HYP_DOUBLES;
-            // the f32 record in one scalar load (SGPR operands of the test)
-            const f32x16 pf = *(const __attribute__((address_space(4))) f32x16*)(ps + 12);
-            if (__builtin_isnan(pf[0])) continue;   // uniform
-            int cnt = 0;
+        q[6] = fxf + fabsf(q[3]);
+        q[7] = fyf + fabsf(q[4]);
+        int v = inlier_f32(pf, q, fxf, fyf, thr2f);
+        if (v < 0) {   // near the threshold: the exact f64 test (rare, divergent)
+            double R[9], t[3];
 #pragma unroll
-            for (int k = 0; k < TS_RS_CPT; ++k) {
-                if (k >= kmax) break;   // uniform
-                int v = have[k] ? inlier_f32(pf, cf[k], fxf, fyf, thr2f) : 0;
-                if (v < 0) {   // near the threshold: the exact f64 test (rare, divergent)
-                    double R[9], t[3];
-                    const double* cr = corr + (size_t)(c0 + k * POSE_THREADS + tid) * TS_CORR_DOUBLES;
+            for (int k = 0; k < 9; ++k) R[k] = ps[k];
+            t[0] = ps[9]; t[1] = ps[10]; t[2] = ps[11];
+            v = is_inlier(R, t, corr + (size_t)i * TS_CORR_DOUBLES, fx, fy, thr2) ? 1 : 0;
+        }
+        return v;
+    };
+    // Poses go in groups of RS_GROUP per wave step: lane (k = lane / 8, j = lane % 8) holds pose
+    // k's f32 record and tests it on entry j of the wave's outlier list, so the NaN checks and
+    // the outlier pre-tests of 8 poses cost one chunk; only poses that survive them are scanned,
+    // one at a time, with the record moved to SGPRs by readlane.
+    constexpr int RS_GROUP = 8;
+    bool done = false;
+    const int k = lane >> 3, j = lane & 7;
+    constexpr int GSTEP = (POSE_THREADS / 64) * RS_GROUP;
+    for (int g0 = wave; g0 < npose && !done; g0 += GSTEP) {
+        const uint32_t bnd0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)*vbest);
+        if ((((uint32_t)(n + 1) << 12) | (uint32_t)(4095 - (4 * h0 + g0))) < bnd0) break;   // no later pose can win
+        const int pk = g0 + (POSE_THREADS / 64) * k;
+        const double* psk = hyp + (size_t)(pk < npose ? pk : 0) * TS_HYP_DOUBLES;
+        f32x16 pl;   // this lane's pose record
+        {
+            const float4* r4 = reinterpret_cast<const float4*>(psk + 12);
 #pragma unroll
-                    for (int q = 0; q < 9; ++q) R[q] = ps[q];
-                    t[0] = ps[9]; t[1] = ps[10]; t[2] = ps[11];
-                    v = is_inlier(R, t, cr, fx, fy, thr2) ? 1 : 0;
-                }
-                cnt += __popcll(__ballot(v != 0));
+            for (int q = 0; q < 4; ++q) {
+                const float4 w = r4[q];
+                pl[4 * q] = w.x; pl[4 * q + 1] = w.y; pl[4 * q + 2] = w.z; pl[4 * q + 3] = w.w;
             }
-            if (lane == 0 && cnt) atomicAdd(&s_cnt[pi], cnt);
+        }
+        const bool valid = pk < npose && !__builtin_isnan(pl[0]);
+        if (pk < npose && !valid && j == 0) atomicMax(&s_best, (uint32_t)(4095 - (4 * h0 + pk)));   // key without a count
+        uint64_t pre = 0;   // lanes of the poses the outlier pre-test rules out
+        if (my_key != 0u) {   // uniform
+            const int idx = __shfl(my_out, j, 64);
+            const int v = (valid && idx >= 0) ? test(psk, pl, idx) : 1;
+            const uint64_t mm = __ballot(v == 0);
+            const int miss = __popcll((mm >> (8 * k)) & 0xFFull);
+            const uint32_t up = ((uint32_t)(n - miss + 1) << 12) | (uint32_t)(4095 - (4 * h0 + pk));
+            pre = __ballot(up < bnd0);
+        }
+        const uint64_t live = __ballot(valid && j == 0) & ~pre;   // bit 8k: pose k still to be scanned
+        for (int kk = 0; kk < RS_GROUP; ++kk) {
+            if (!((live >> (8 * kk)) & 1ull)) continue;   // uniform
+            const int pi = g0 + (POSE_THREADS / 64) * kk;
+            const uint32_t tag = (uint32_t)(4095 - (4 * h0 + pi));
+            // the block's best when this pose starts: it only grows, so a stale copy is still a
+            // bound (an LDS read per chunk would put a round trip in the scan's dependency chain)
+            const uint32_t bnd = (uint32_t)__builtin_amdgcn_readfirstlane((int)*vbest);
+            if ((((uint32_t)(n + 1) << 12) | tag) < bnd) {
+                done = true;
+                break;
+            }
+            const bool list_ok = (my_key >> 12) + 2u >= (bnd >> 12);
+            const double* ps = hyp + (size_t)pi * TS_HYP_DOUBLES;
+            f32x16 pf;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) pf[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pl[q]), 8 * kk));
+            int cnt = 0, nm = 0;
+            bool dropped = false;
+            for (int c0 = 0; c0 < n; c0 += 64 * TS_RS_UNROLL) {
+                // TS_RS_UNROLL independent chunks between two drop tests: a test per chunk puts the
+                // whole LDS -> VALU -> ballot -> branch chain of every chunk on the critical path
+    #pragma unroll
+                for (int u = 0; u < TS_RS_UNROLL; ++u) {
+                    const int cu = c0 + 64 * u;
+                    const int i = cu + lane;
+                    const int v = i < n ? test(ps, pf, i) : 1;
+                    const uint64_t mm = __ballot(v == 0);
+                    if (v == 0) {
+                        const int pos = nm + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+                        if (pos < 64) s_wout[wave][pos] = i;
+                    }
+                    nm += __popcll(mm);
+                    cnt += max(0, min(64, n - cu)) - __popcll(mm);
+                }
+                const int rest = max(0, n - (c0 + 64 * TS_RS_UNROLL));
+                // drop only once the wave's own outlier list is nearly as good as the block's
+                // best: a wave that kept dropping would keep a useless list (and pre-test nothing)
+                if (list_ok && (((uint32_t)(cnt + rest + 1) << 12) | tag) < bnd) {   // uniform
+                    dropped = true;
+                    break;
+                }
+            }
+            if (!dropped) {
+                const uint32_t key = ((uint32_t)(cnt + 1) << 12) | tag;
+                if (lane == 0) atomicMax(&s_best, key);
+                if (key > my_key) {
+                    my_key = key;
+                    __builtin_amdgcn_wave_barrier();
+                    my_out = lane < nm ? s_wout[wave][lane] : -1;
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
         }
     }
     __syncthreads();
-    uint32_t my_best = 0;
-    for (int pi = tid; pi < npose; pi += POSE_THREADS) {
-        const bool valid = !__builtin_isnan(hyp[(size_t)pi * TS_HYP_DOUBLES]);
-        const int gidx = 4 * h0 + pi;
-        const uint32_t key = valid ? ((uint32_t)(s_cnt[pi] + 1) << 12) | (uint32_t)(4095 - gidx) : (uint32_t)(4095 - gidx);
-        my_best = key > my_best ? key : my_best;
-    }
-    uint32_t wb = my_best;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t other = (uint32_t)__shfl_xor((int)wb, o, 64);
-        wb = other > wb ? other : wb;
-    }
-    if (lane == 0) s_wbest[wave] = wb;
-    __syncthreads();
-    uint32_t best = s_wbest[0];
-    for (int w = 1; w < 4; ++w) best = s_wbest[w] > best ? s_wbest[w] : best;
+    const uint32_t best = s_best;
     if (tid == 0) kout[0] = best;
     if (tid < 12 && best != 0u) {
         const int gidx = 4095 - (int)(best & 4095u);
@@ -658,27 +744,27 @@ __global__ __launch_bounds__(POSE_THREADS) void k_refine(BatchCtx c, int S) {
     cnt_local = wave_sum_i32(cnt_local);
     if (lane == 0) s_scan[wave] = cnt_local;
     __syncthreads();
+    const int n_in = ((s_scan[0] + s_scan[1]) + s_scan[2]) + s_scan[3];
+    const bool ok = !fail && n_in >= c.pp.min_inliers;
+    const double sigma2 = sq_last / (double)max(1, 2 * n_in - 6);
     if (tid == 0) {
-        const int n_in = ((s_scan[0] + s_scan[1]) + s_scan[2]) + s_scan[3];
-        const bool ok = !fail && n_in >= c.pp.min_inliers;
         write_stats(sout, ok ? 0 : 1, n, fail ? 0 : n_in, best_cnt, best_idx, g);
         if (ok) {
             for (int i = 0; i < 3; ++i) {
                 for (int j = 0; j < 3; ++j) pout[4 * i + j] = s_R[3 * i + j];
                 pout[4 * i + 3] = s_t[i];
             }
-            const double sigma2 = sq_last / (double)max(1, 2 * n_in - 6);
-            double L[36], e[6], col[6];
-            for (int q = 0; q < 36; ++q) L[q] = 0.0;
-            for (int k = 0; k < 6; ++k) {
-                for (int q = 0; q < 6; ++q) e[q] = q == k ? 1.0 : 0.0;
-                if (solve6(s_H, e, col, L))
-                    for (int q = 0; q < 6; ++q) pout[32 + q * 6 + k] = col[q] * sigma2;
-            }
             // stats[6..7]: sigma^2 (f64), so the host can take a motion prior back out of the
             // covariance (the vision-only motion for the IMU filter's bias update)
             *reinterpret_cast<double*>(sout + 6) = sigma2;
         }
+    }
+    if (ok && tid < 6) {   // covariance column k = tid: H^-1 e_k sigma^2, the six columns side by side
+        double L[36], e[6], col[6];
+        for (int q = 0; q < 36; ++q) L[q] = 0.0;
+        for (int q = 0; q < 6; ++q) e[q] = q == tid ? 1.0 : 0.0;
+        if (solve6(s_H, e, col, L))
+            for (int q = 0; q < 6; ++q) pout[32 + q * 6 + tid] = col[q] * sigma2;
     }
 }
 
@@ -996,21 +1082,20 @@ __global__ __launch_bounds__(POSE_THREADS) void k_rig_pose(BatchCtx c) {
     cnt_local = wave_sum_i32(cnt_local);
     if (lane == 0) s_cnt[wave][0] = cnt_local;
     __syncthreads();
+    const int n_in = ((s_cnt[0][0] + s_cnt[1][0]) + s_cnt[2][0]) + s_cnt[3][0];
+    const bool ok = !fail && n_in >= c.pp.min_inliers;
     if (tid == 0) {
-        const int n_in = ((s_cnt[0][0] + s_cnt[1][0]) + s_cnt[2][0]) + s_cnt[3][0];
-        const bool ok = !fail && n_in >= c.pp.min_inliers;
         write_stats(sout, ok ? 0 : 1, n_total, fail ? 0 : n_in, best_cnt, best_idx, g);
-        if (ok) {
+        if (ok)
             for (int e = 0; e < 12; ++e) pout[e] = s_M[0][e];
-            const double sigma2 = sq_last / (double)max(1, 2 * n_in - 6);
-            double L[36], e6[6], col[6];
-            for (int q = 0; q < 36; ++q) L[q] = 0.0;
-            for (int k = 0; k < 6; ++k) {
-                for (int q = 0; q < 6; ++q) e6[q] = q == k ? 1.0 : 0.0;
-                if (solve6(s_H, e6, col, L))
-                    for (int q = 0; q < 6; ++q) pout[32 + q * 6 + k] = col[q] * sigma2;
-            }
-        }
+    }
+    if (ok && tid < 6) {   // covariance column k = tid, the six columns side by side
+        const double sigma2 = sq_last / (double)max(1, 2 * n_in - 6);
+        double L[36], e6[6], col[6];
+        for (int q = 0; q < 36; ++q) L[q] = 0.0;
+        for (int q = 0; q < 6; ++q) e6[q] = q == tid ? 1.0 : 0.0;
+        if (solve6(s_H, e6, col, L))
+            for (int q = 0; q < 6; ++q) pout[32 + q * 6 + tid] = col[q] * sigma2;
     }
 }
 
@@ -1050,12 +1135,14 @@ __global__ __launch_bounds__(256) void k_rig_prior(BatchCtx c) {
     out[14] = out[15] = 0.0;
 }
 
+static size_t ransac_lds(const BatchCtx& c) { return (size_t)min(c.g.K, TS_RS_LDS_CAP) * (16 + 8); }
+
 int ransac_splits(const BatchCtx& c) {
     if (c.pp.splits > 0) return min(min(c.pp.splits, c.pp.n_hyp), TS_MAX_SPLITS);
-    // scoring blocks (>= 4096: 64 waves per CU over the launch), at least 8 hypotheses per split
-    // (measured at B = 256: S = 4 / 8 / 16 -> 325 / 295 / 283 us for the pose stage)
+    // scoring blocks (>= 1024: 4 per CU), at least 8 hypotheses per split; fewer splits let the
+    // bounded scoring drop more poses (one block's best key bounds all of its poses)
     const int frames = c.n * c.npair;
-    int S = (4096 + frames - 1) / frames;
+    int S = (1024 + frames - 1) / frames;
     S = max(1, min(S, max(1, c.pp.n_hyp / 8)));
     return min(S, TS_MAX_SPLITS);
 }
@@ -1064,7 +1151,7 @@ void launch_pose(const BatchCtx& c, hipStream_t s) {
     const int S = ransac_splits(c);
     hipLaunchKernelGGL(k_corr, dim3(c.n * c.npair), dim3(POSE_THREADS), 0, s, c);
     hipLaunchKernelGGL(k_p3p, dim3((c.n * c.npair * c.pp.n_hyp + POSE_THREADS - 1) / POSE_THREADS), dim3(POSE_THREADS), 0, s, c);
-    hipLaunchKernelGGL(k_ransac, dim3(c.n * c.npair * S), dim3(POSE_THREADS), 0, s, c, S);
+    hipLaunchKernelGGL(k_ransac, dim3(c.n * c.npair * S), dim3(POSE_THREADS), ransac_lds(c), s, c, S);
     hipLaunchKernelGGL(k_refine, dim3(c.n * c.npair), dim3(POSE_THREADS), 0, s, c, S);
 }
 
@@ -1072,7 +1159,7 @@ void launch_pose(const BatchCtx& c, hipStream_t s) {
 void launch_pose_solve(const BatchCtx& c, hipStream_t s) {
     const int S = ransac_splits(c);
     hipLaunchKernelGGL(k_p3p, dim3((c.n * c.npair * c.pp.n_hyp + POSE_THREADS - 1) / POSE_THREADS), dim3(POSE_THREADS), 0, s, c);
-    hipLaunchKernelGGL(k_ransac, dim3(c.n * c.npair * S), dim3(POSE_THREADS), 0, s, c, S);
+    hipLaunchKernelGGL(k_ransac, dim3(c.n * c.npair * S), dim3(POSE_THREADS), ransac_lds(c), s, c, S);
     hipLaunchKernelGGL(k_refine, dim3(c.n * c.npair), dim3(POSE_THREADS), 0, s, c, S);
 }
 

@@ -25,6 +25,8 @@ def main() -> None:
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=400)
     ap.add_argument("--features", type=int, default=2000)
+    ap.add_argument("--ransac-counters", action="store_true",
+                    help="print the per-block counters an instrumented k_ransac build leaves in qbest")
     ap.add_argument("--splits", type=int, default=0, help="RANSAC splits per frame (0: the library's choice)")
     args = ap.parse_args()
     import torch
@@ -64,6 +66,20 @@ def main() -> None:
         e1.record(stream)
         torch.cuda.synchronize()
         print(f"{name:16s} {1000 * e0.elapsed_time(e1):9.1f} us")
+    st = np.stack([h.frame_block("stats", i, np.int32)[:5] for i in range(0, B, max(1, B // 64))])
+    ok = st[:, 0] == 0
+    print("pose stats over %d sampled frames: tracked %d, correspondences n mean %.0f min %d max %d, "
+          "RANSAC best count / n mean %.3f min %.3f, refined inliers / n mean %.3f" % (
+              len(st), ok.sum(), st[:, 1].mean(), st[:, 1].min(), st[:, 1].max(),
+              (st[:, 3] / np.maximum(st[:, 1], 1)).mean(), (st[:, 3] / np.maximum(st[:, 1], 1)).min(),
+              (st[:, 2] / np.maximum(st[:, 1], 1)).mean()))
+    if args.ransac_counters:
+        names = ["break", "visited", "nan", "pre_drop", "superchunks", "scan_drop", "complete", "n"]
+        cnt = np.stack([h.frame_block("qbest", i, np.uint32)[:8] for i in range(B)]).astype(np.int64)
+        print("k_ransac counters per block: mean " + " ".join("%s %.1f" % (k, v) for k, v in zip(names, cnt.mean(0))))
+        print("  max " + " ".join("%s %d" % (k, v) for k, v in zip(names, cnt.max(0))))
+        top = np.argsort(-cnt[:, 4])[:5]
+        print("  slowest blocks (superchunks):", [(int(i), cnt[i].tolist()) for i in top])
     h.end_batch()
     # bandwidth reference: copy the pyramid slice of B frames (read + write)
     import ctypes
