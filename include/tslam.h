@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 12
+#define TSLAM_ABI_VERSION 13
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -96,7 +96,8 @@ typedef struct {
      * H*W] (images = [n][n_pairs][5*H*W] bytes; W*H even).  tslam_stereo_desc gives the colour
      * camera (baseline ignored, map_right unused); the stereo stage becomes a depth lookup. */
     int32_t rgbd;
-    int32_t rgbd_pad;             /* reserved, 0                                              */
+    int32_t ransac_mode;          /* RANSAC scoring: 0 auto (bounded from 256 frames per launch),
+                                     1 exhaustive, 2 bounded; never changes results             */
 } tslam_params;
 
 /* One raw camera as IsaacRosAdapter publishes it (camera_info K/D + the rig extrinsics,

@@ -22,14 +22,14 @@ N_FRAMES = 4
 
 @functools.lru_cache(maxsize=8)
 def hip_run(seed: int = 0, batch: int = N_FRAMES, distorted: bool = False, n: int = N_FRAMES, cfg_items: tuple = (),
-            splits: int = 0, width: int = 640, height: int = 400):
+            splits: int = 0, width: int = 640, height: int = 400, mode: str = "auto"):
     import torch
 
     from thor_slam_amd._lib import Handle
 
     sc = scenario(seed=seed, n=n, width=width, height=height, distorted=distorted, cfg_items=cfg_items)
     cfg = sc["cfg"]
-    h = Handle([sc["rect"]], cfg, max_batch=batch, ransac_splits=splits)
+    h = Handle([sc["rect"]], cfg, max_batch=batch, ransac_splits=splits, ransac_mode=mode)
     dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
     per = []
     K = cfg.n_features
@@ -153,8 +153,20 @@ def test_batch_size_invariance():
 
 @pytest.mark.parametrize("splits", [1, 3, 32])
 def test_ransac_split_invariance(splits):
+    """k_ransac_all (this size's automatic choice) at other split counts gives the same results."""
     _, a = hip_run()
     _, b = hip_run(splits=splits)
+    for i, (x, y) in enumerate(zip(a, b)):
+        np.testing.assert_array_equal(x["stats"], y["stats"], err_msg=f"frame {i}")
+        np.testing.assert_array_equal(x["T_abs"], y["T_abs"], err_msg=f"frame {i}")
+
+
+@pytest.mark.parametrize("splits", [0, 3])
+def test_ransac_bounded_equals_exhaustive(splits):
+    """The bounded kernel (k_ransac, forced) gives the same stats, winners and poses as the
+    exhaustive one on the pipeline's own correspondences."""
+    _, a = hip_run(mode="exhaustive")
+    _, b = hip_run(splits=splits, mode="bounded")
     for i, (x, y) in enumerate(zip(a, b)):
         np.testing.assert_array_equal(x["stats"], y["stats"], err_msg=f"frame {i}")
         np.testing.assert_array_equal(x["T_abs"], y["T_abs"], err_msg=f"frame {i}")
@@ -300,11 +312,12 @@ def test_c1_sequence_100_frames():
     assert n_tracked >= 90, f"only {n_tracked} of {n - 1} frames tracked"
 
 
-@pytest.mark.parametrize("splits", [0, 1, 7])
-def test_ransac_bounded_scoring_with_outliers(splits):
+@pytest.mark.parametrize("splits,mode", [(0, "bounded"), (1, "bounded"), (7, "bounded"), (0, "exhaustive"), (0, "auto")])
+def test_ransac_bounded_scoring_with_outliers(splits, mode):
     """k_ransac drops a pose as soon as its count cannot reach the block's best key.  With 35 % of
     the frame's refined positions moved 8-40 px (outliers to every pose), the RANSAC winner, its
-    count, the inliers and the refined pose still equal the oracle's exhaustive scoring."""
+    count, the inliers and the refined pose still equal the oracle's exhaustive scoring — with the
+    bounded kernel forced, the exhaustive one (k_ransac_all) forced, and the automatic choice."""
     import torch
 
     from oracle import numpy_slam as O
@@ -313,7 +326,7 @@ def test_ransac_bounded_scoring_with_outliers(splits):
     sc = scenario(seed=0, n=3)
     cfg, rect = sc["cfg"], sc["rect"]
     K = cfg.n_features
-    h = Handle([rect], cfg, max_batch=1, ransac_splits=splits)
+    h = Handle([rect], cfg, max_batch=1, ransac_splits=splits, ransac_mode=mode)
     dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
     s = torch.cuda.current_stream().cuda_stream
     for g in range(2):

@@ -241,6 +241,8 @@ __device__ bool solve6(const double* Hm, const double* g, double* x, double* L) 
 }
 
 #define POSE_THREADS 256
+#define TS_RS_CPT 4            // correspondences per thread per scoring pass (k_ransac_all)
+#define TS_MAX_HYP_SPLIT 256   // hypotheses per k_ransac_all block (n_hyp <= 256)
 #define N_ACC 29   // 21 (upper H) + 6 (g) + 1 (sq) + 1 (count)
 
 __device__ __forceinline__ void write_stats(int32_t* so, int status, int n, int n_in, int best_cnt, int best_idx, int64_t g) {
@@ -380,6 +382,111 @@ __global__ __launch_bounds__(POSE_THREADS) void k_p3p(BatchCtx c) {
             dst[0] = __builtin_nan("");
             reinterpret_cast<float*>(dst + 12)[0] = __builtin_nanf("");
         }
+    }
+}
+
+// ---- k_ransac_all: exhaustive scoring of one split (small launches) ------------------------
+// grid (n*P*S): block (fp, split) scores the 4*(h1-h0) candidate poses of hypotheses [h0, h1):
+// correspondences stay in registers (TS_RS_CPT per thread); a pose is wave-uniform, so it comes
+// through scalar loads (SGPR operands of the f64 VALU ops — an LDS broadcast of its 96 bytes
+// returned 6 KiB per wave and bound the loop); inlier counts are wave ballots (integer sums:
+// order-independent).  Writes its best (count+1)<<12 | (4095 - pose index) key and that pose.
+// Every pose is scored against every correspondence by the whole block: with few frames per
+// launch (B = 1 latency, C4's 50) the per-pose latency of k_ransac's one-wave scans would be the
+// launch's critical path, so those launches take this kernel (same keys, same winner).
+__global__ __launch_bounds__(POSE_THREADS) void k_ransac_all(BatchCtx c, int S) {
+    __shared__ int s_cnt[4 * TS_MAX_HYP_SPLIT];
+    __shared__ uint32_t s_wbest[4];
+    const int fl = blockIdx.x / S;
+    const int split = blockIdx.x % S;
+    const int p = c.pair0 + fl % c.npair;
+    const int f = fl / c.npair;
+    const int fp = f * c.P + p;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int32_t* sout = c.stats + (size_t)fp * TS_STATS_INTS;
+    uint32_t* kout = reinterpret_cast<uint32_t*>(c.ransac) + ((size_t)fp * S + split) * TS_RANSAC_WORDS;
+    if (sout[0] != 3) {
+        if (tid == 0) kout[0] = 0u;
+        return;
+    }
+    const int n = sout[1];
+    const int H = c.pp.n_hyp;
+    const int Hs = (H + S - 1) / S;
+    const int h0 = split * Hs, h1 = min(H, h0 + Hs);
+    const int nh = max(0, h1 - h0);
+    const PairCalib cal = c.calib[p];
+    const double fx = cal.fx, fy = cal.fy;
+    const double* corr = c.corr + ((size_t)f * c.P + p) * c.g.K * TS_CORR_DOUBLES;
+    const double* hyp = c.hyp + ((size_t)fp * 4 * H + 4 * h0) * TS_HYP_DOUBLES;   // this split's poses
+    typedef const __attribute__((address_space(4))) double cdouble;   // uniform address -> s_load
+    cdouble* chyp = (cdouble*)(uintptr_t)hyp;
+    const int npose = 4 * nh;
+    for (int i = tid; i < npose; i += POSE_THREADS) s_cnt[i] = 0;
+    __syncthreads();
+    const double thr2 = c.pp.thr2;
+    const float fxf = (float)fx, fyf = (float)fy, thr2f = (float)thr2;
+    for (int c0 = 0; c0 < n; c0 += POSE_THREADS * TS_RS_CPT) {
+        float cf[TS_RS_CPT][8];   // X Y Z du dv, |X| + |Y| + |Z|, fx + |du|, fy + |dv|
+        bool have[TS_RS_CPT];
+#pragma unroll
+        for (int k = 0; k < TS_RS_CPT; ++k) {
+            const int ci = c0 + k * POSE_THREADS + tid;
+            have[k] = ci < n;
+            const double* cr = corr + (size_t)(have[k] ? ci : 0) * TS_CORR_DOUBLES;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) cf[k][q] = (float)cr[q];
+            cf[k][5] = fabsf(cf[k][0]) + fabsf(cf[k][1]) + fabsf(cf[k][2]);
+            cf[k][6] = fxf + fabsf(cf[k][3]);
+            cf[k][7] = fyf + fabsf(cf[k][4]);
+        }
+        // correspondence slots no lane of this wave has are skipped (wave-uniform)
+        const int kmax = min(TS_RS_CPT, (n - c0 - wave * 64 + POSE_THREADS - 1) / POSE_THREADS);
+        for (int pi = 0; pi < npose; ++pi) {
+            cdouble* ps = chyp + (size_t)pi * TS_HYP_DOUBLES;
+            // the f32 record in one scalar load (SGPR operands of the test)
+            const f32x16 pf = *(const __attribute__((address_space(4))) f32x16*)(ps + 12);
+            if (__builtin_isnan(pf[0])) continue;   // uniform
+            int cnt = 0;
+#pragma unroll
+            for (int k = 0; k < TS_RS_CPT; ++k) {
+                if (k >= kmax) break;   // uniform
+                int v = have[k] ? inlier_f32(pf, cf[k], fxf, fyf, thr2f) : 0;
+                if (v < 0) {   // near the threshold: the exact f64 test (rare, divergent)
+                    double R[9], t[3];
+                    const double* cr = corr + (size_t)(c0 + k * POSE_THREADS + tid) * TS_CORR_DOUBLES;
+#pragma unroll
+                    for (int q = 0; q < 9; ++q) R[q] = ps[q];
+                    t[0] = ps[9]; t[1] = ps[10]; t[2] = ps[11];
+                    v = is_inlier(R, t, cr, fx, fy, thr2) ? 1 : 0;
+                }
+                cnt += __popcll(__ballot(v != 0));
+            }
+            if (lane == 0 && cnt) atomicAdd(&s_cnt[pi], cnt);
+        }
+    }
+    __syncthreads();
+    uint32_t my_best = 0;
+    for (int pi = tid; pi < npose; pi += POSE_THREADS) {
+        const bool valid = !__builtin_isnan(hyp[(size_t)pi * TS_HYP_DOUBLES]);
+        const int gidx = 4 * h0 + pi;
+        const uint32_t key = valid ? ((uint32_t)(s_cnt[pi] + 1) << 12) | (uint32_t)(4095 - gidx) : (uint32_t)(4095 - gidx);
+        my_best = key > my_best ? key : my_best;
+    }
+    uint32_t wb = my_best;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t other = (uint32_t)__shfl_xor((int)wb, o, 64);
+        wb = other > wb ? other : wb;
+    }
+    if (lane == 0) s_wbest[wave] = wb;
+    __syncthreads();
+    uint32_t best = s_wbest[0];
+    for (int w = 1; w < 4; ++w) best = s_wbest[w] > best ? s_wbest[w] : best;
+    if (tid == 0) kout[0] = best;
+    if (tid < 12 && best != 0u) {
+        const int gidx = 4095 - (int)(best & 4095u);
+        const double v = hyp[(size_t)(gidx - 4 * h0) * TS_HYP_DOUBLES + tid];
+        reinterpret_cast<double*>(kout + 2)[tid] = v;
     }
 }
 
@@ -1137,21 +1244,36 @@ __global__ __launch_bounds__(256) void k_rig_prior(BatchCtx c) {
 
 static size_t ransac_lds(const BatchCtx& c) { return (size_t)min(c.g.K, TS_RS_LDS_CAP) * (16 + 8); }
 
+// Bounded scoring (k_ransac) from 256 frames per launch; below that the exhaustive block-wide
+// kernel (k_ransac_all) has the shorter critical path (C4, B = 50: 82 against 117 us).
+static bool ransac_bounded(const BatchCtx& c) {
+    return c.pp.mode == 2 || (c.pp.mode == 0 && c.n * c.npair >= 256);
+}
+
 int ransac_splits(const BatchCtx& c) {
     if (c.pp.splits > 0) return min(min(c.pp.splits, c.pp.n_hyp), TS_MAX_SPLITS);
-    // scoring blocks (>= 1024: 4 per CU), at least 8 hypotheses per split; fewer splits let the
-    // bounded scoring drop more poses (one block's best key bounds all of its poses)
+    // bounded: >= 1024 blocks (4 per CU) - fewer splits let one block's best key bound more poses;
+    // exhaustive: >= 4096 blocks (measured at B = 256: S = 4 / 8 / 16 -> 325 / 295 / 283 us for the
+    // pose stage).  At least 8 hypotheses per split either way.
     const int frames = c.n * c.npair;
-    int S = (1024 + frames - 1) / frames;
+    const int target = ransac_bounded(c) ? 1024 : 4096;
+    int S = (target + frames - 1) / frames;
     S = max(1, min(S, max(1, c.pp.n_hyp / 8)));
     return min(S, TS_MAX_SPLITS);
+}
+
+static void launch_ransac(const BatchCtx& c, int S, hipStream_t s) {
+    if (ransac_bounded(c))
+        hipLaunchKernelGGL(k_ransac, dim3(c.n * c.npair * S), dim3(POSE_THREADS), ransac_lds(c), s, c, S);
+    else
+        hipLaunchKernelGGL(k_ransac_all, dim3(c.n * c.npair * S), dim3(POSE_THREADS), 0, s, c, S);
 }
 
 void launch_pose(const BatchCtx& c, hipStream_t s) {
     const int S = ransac_splits(c);
     hipLaunchKernelGGL(k_corr, dim3(c.n * c.npair), dim3(POSE_THREADS), 0, s, c);
     hipLaunchKernelGGL(k_p3p, dim3((c.n * c.npair * c.pp.n_hyp + POSE_THREADS - 1) / POSE_THREADS), dim3(POSE_THREADS), 0, s, c);
-    hipLaunchKernelGGL(k_ransac, dim3(c.n * c.npair * S), dim3(POSE_THREADS), ransac_lds(c), s, c, S);
+    launch_ransac(c, S, s);
     hipLaunchKernelGGL(k_refine, dim3(c.n * c.npair), dim3(POSE_THREADS), 0, s, c, S);
 }
 
@@ -1159,7 +1281,7 @@ void launch_pose(const BatchCtx& c, hipStream_t s) {
 void launch_pose_solve(const BatchCtx& c, hipStream_t s) {
     const int S = ransac_splits(c);
     hipLaunchKernelGGL(k_p3p, dim3((c.n * c.npair * c.pp.n_hyp + POSE_THREADS - 1) / POSE_THREADS), dim3(POSE_THREADS), 0, s, c);
-    hipLaunchKernelGGL(k_ransac, dim3(c.n * c.npair * S), dim3(POSE_THREADS), ransac_lds(c), s, c, S);
+    launch_ransac(c, S, s);
     hipLaunchKernelGGL(k_refine, dim3(c.n * c.npair), dim3(POSE_THREADS), 0, s, c, S);
 }
 

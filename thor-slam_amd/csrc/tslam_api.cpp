@@ -473,6 +473,7 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.pp.iters = h->prm.refine_iters;
     c.pp.min_inliers = h->prm.min_inliers;
     c.pp.splits = h->prm.ransac_splits;
+    c.pp.mode = h->prm.ransac_mode;
     c.pp.thr2 = h->prm.ransac_thr_px * h->prm.ransac_thr_px;
     c.pp.seed = h->prm.ransac_seed;
     c.fast_threshold = h->prm.fast_threshold;
@@ -634,6 +635,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
         return fail(TSLAM_EINVAL, "ba_kf_interval, ba_iters >= 1, ba_lambda >= 0, ba_outlier_px > 0");
     if (p.refine_iters < 1) return fail(TSLAM_EINVAL, "refine_iters must be >= 1");
     if (p.ransac_splits < 0 || p.ransac_splits > TS_MAX_SPLITS) return fail(TSLAM_EINVAL, "ransac_splits must be in [0, 32]");
+    if (p.ransac_mode < 0 || p.ransac_mode > 2) return fail(TSLAM_EINVAL, "ransac_mode must be 0, 1 or 2");
     const int W = pairs[0].width, H = pairs[0].height;
     if (W < 64 || H < 64 || W > 2047 || H > 2047) return fail(TSLAM_EINVAL, "image size must be within [64, 2047]");
     for (int i = 1; i < p.n_pairs; ++i)

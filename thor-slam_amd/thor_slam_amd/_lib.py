@@ -54,7 +54,7 @@ class Params(ctypes.Structure):
         ("max_batch", ctypes.c_int32), ("n_pairs", ctypes.c_int32), ("ransac_splits", ctypes.c_int32),
         ("ba_window", ctypes.c_int32), ("ba_kf_interval", ctypes.c_int32), ("ba_iters", ctypes.c_int32),
         ("ba_pad", ctypes.c_int32), ("ba_lambda", ctypes.c_double), ("ba_outlier_px", ctypes.c_double),
-        ("rgbd", ctypes.c_int32), ("rgbd_pad", ctypes.c_int32),
+        ("rgbd", ctypes.c_int32), ("ransac_mode", ctypes.c_int32),
     ]
 
 
@@ -262,13 +262,17 @@ def _check(rc: int) -> None:
         raise RuntimeError(f"tslam error {rc}: {msg.decode() if msg else ''}")
 
 
-def make_params(cfg: HipSlamConfig, max_batch: int, n_pairs: int, ransac_splits: int = 0) -> Params:
+RANSAC_MODE = {"auto": 0, "exhaustive": 1, "bounded": 2}   # tslam_params.ransac_mode
+
+
+def make_params(cfg: HipSlamConfig, max_batch: int, n_pairs: int, ransac_splits: int = 0,
+                ransac_mode: str = "auto") -> Params:
     return Params(
         cfg.n_features, cfg.n_levels, cfg.fast_threshold, cfg.edge_margin, cfg.max_hamming, cfg.ratio_pct,
         cfg.stereo_row_tol, cfg.max_disparity, cfg.temporal_window, cfg.ransac_hypotheses, cfg.refine_iters,
         cfg.min_inliers, float(cfg.ransac_thr_px), int(cfg.ransac_seed) & ((1 << 64) - 1), int(max_batch), int(n_pairs),
         int(ransac_splits), int(cfg.ba_window), int(cfg.ba_kf_interval), int(cfg.ba_iters), 0, float(cfg.ba_lambda),
-        float(cfg.ba_outlier_px), int(bool(cfg.rgbd)), 0,
+        float(cfg.ba_outlier_px), int(bool(cfg.rgbd)), RANSAC_MODE[ransac_mode],
     )
 
 
@@ -306,7 +310,8 @@ def comm_unique_id() -> bytes:
 class Handle:
     """Owns one ``tslam_handle`` (one device, ``n_pairs`` stereo pairs, batches <= ``max_batch``)."""
 
-    def __init__(self, rects: list, cfg: HipSlamConfig, max_batch: int = 1, device: int = 0, ransac_splits: int = 0):
+    def __init__(self, rects: list, cfg: HipSlamConfig, max_batch: int = 1, device: int = 0, ransac_splits: int = 0,
+                 ransac_mode: str = "auto"):
         self.lib = load_library()
         cfg.validate()
         self.cfg = cfg
@@ -325,7 +330,7 @@ class Handle:
                 None if ml is None else ml.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
                 None if mr is None else mr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
             )
-        params = make_params(cfg, max_batch, self.n_pairs, ransac_splits)
+        params = make_params(cfg, max_batch, self.n_pairs, ransac_splits, ransac_mode)
         h = ctypes.c_void_p()
         _check(self.lib.tslam_create(descs, ctypes.byref(params), int(device), ctypes.byref(h)))
         self.h = h
