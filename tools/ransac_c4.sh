@@ -8,7 +8,7 @@ for s in ${SPLITS:-2 4 8 16}; do
     python3 - "gpurun_out/$tag/s$s/stats/run_kernel_trace.csv" "$s" <<'PY'
 import csv, sys
 rows = [r for r in csv.DictReader(open(sys.argv[1]))]
-for k in ("k_ransac", "k_refine(", "k_p3p", "k_corr"):
+for k in ("k_ransac", "k_refine", "k_p3p", "k_corr"):
     print("splits", sys.argv[2], k, [round((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000, 1) for r in rows if r["Kernel_Name"].startswith(k)][-2:])
 PY
 done
