@@ -186,11 +186,15 @@ def test_other_seeds_and_config():
             assert rel_frobenius(rec["T_abs"], o["world_T_cam"]) < 1e-9
 
 
-def test_c4_size_bit_exact():
+@pytest.mark.parametrize("mode", ["auto", "bounded"])
+def test_c4_size_bit_exact(mode):
     """Config C4 geometry (1280x800, K=4000: the level-0 quota exceeds the counting-sort capacity,
-    so select takes its bitonic path) stays bit-exact, with a distorted lens."""
+    so select takes its bitonic path) stays bit-exact, with a distorted lens.  With the bounded
+    RANSAC forced, correspondences past its LDS capacity (2048) come from global memory."""
     items = (("n_features", 4000),)
-    sc, per = hip_run(seed=2, n=2, cfg_items=items, width=1280, height=800, distorted=True)
+    sc, per = hip_run(seed=2, n=2, cfg_items=items, width=1280, height=800, distorted=True, mode=mode)
+    if mode == "bounded":
+        assert per[1]["stats"][1] > 2048, "the frame should exceed the LDS staging capacity"
     for i, rec in enumerate(per):
         o = sc["oracle"][i]
         _check_image_features(o["cur"]["left"], rec["kp"][0], sc["cfg"], f"frame {i} left")
