@@ -251,7 +251,7 @@ __device__ __forceinline__ void write_stats(int32_t* so, int status, int n, int 
 
 // ---- k_corr: correspondences of one (frame, pair), ordered by the current keypoint index ------
 __global__ __launch_bounds__(POSE_THREADS) void k_corr(BatchCtx c) {
-    __shared__ int s_scan[POSE_THREADS];
+    __shared__ int s_scan[2 * (POSE_THREADS / 64)];
     const int p = c.pair0 + (int)blockIdx.x % c.npair;   // (frame, pair) of the pair view
     const int f = (int)blockIdx.x / c.npair;
     const int fp = f * c.P + p;
@@ -287,16 +287,20 @@ __global__ __launch_bounds__(POSE_THREADS) void k_corr(BatchCtx c) {
                 flag = __builtin_isfinite(d) && __builtin_isfinite(u) && __builtin_isfinite(v);
             }
         }
-        s_scan[tid] = flag;
+        // stream compaction in keypoint order: wave ballots + the 4 wave counts (double-buffered,
+        // one barrier per chunk of 256)
+        const uint64_t bm = __ballot(flag != 0);
+        const int lane = tid & 63, wave = tid >> 6;
+        int* wc = s_scan + ((base / POSE_THREADS) & 1) * 4;
+        if (lane == 0) wc[wave] = __popcll(bm);
         __syncthreads();
-        for (int o = 1; o < POSE_THREADS; o <<= 1) {
-            const int add = tid >= o ? s_scan[tid - o] : 0;
-            __syncthreads();
-            s_scan[tid] += add;
-            __syncthreads();
+        int before = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < POSE_THREADS / 64; ++w) {
+            before += w < wave ? wc[w] : 0;
+            tot += wc[w];
         }
-        const int pos = n + s_scan[tid] - flag;
-        const int tot = s_scan[POSE_THREADS - 1];
+        const int pos = n + before + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
         if (flag) {
             const uint32_t xy = kprev[2 * i], meta = kprev[2 * i + 1];
             const double sc = (double)(1 << (meta & 0xFF));
@@ -313,7 +317,6 @@ __global__ __launch_bounds__(POSE_THREADS) void k_corr(BatchCtx c) {
             cr[5] = bx / nn; cr[6] = by / nn; cr[7] = 1.0 / nn;
         }
         n += tot;
-        __syncthreads();
     }
     if (tid == 0) write_stats(sout, n < max(6, c.pp.min_inliers) ? 1 : 3, n, 0, 0, -1, g);  // 3 = "to be solved"
 }
