@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 13
+#define TSLAM_ABI_VERSION 14
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -98,6 +98,9 @@ typedef struct {
     int32_t rgbd;
     int32_t ransac_mode;          /* RANSAC scoring: 0 auto (bounded from 256 frames per launch),
                                      1 exhaustive, 2 bounded; never changes results             */
+    int32_t refine_block;         /* k_refine threads per frame: 0 auto (128 from 512 frames per
+                                     launch), 128 or 256; never changes results                  */
+    int32_t reserved0;            /* 0                                                        */
 } tslam_params;
 
 /* One raw camera as IsaacRosAdapter publishes it (camera_info K/D + the rig extrinsics,

@@ -123,6 +123,23 @@ def test_ba_imu_rotation_factors_parity():
     assert moved > 1e-6, moved
 
 
+def test_ba_imu_factor_rejects_non_finite():
+    """tslam_ba_imu_factor refuses an infinite / NaN weight or rotation entry (they would poison the
+    window's whole Schur system) and leaves the window unchanged."""
+    from thor_slam_amd._lib import Handle
+
+    sc, _ = _scenario_and_oracle(12)
+    h = Handle([sc["rect"]], sc["cfg"], max_batch=2)
+    try:
+        M = np.eye(3)
+        for Mx, w in ((M, np.inf), (M, np.nan), (M, -1.0), (np.full((3, 3), np.nan), 1.0), (M * np.inf, 1.0)):
+            with pytest.raises(RuntimeError, match="tslam error"):
+                h.ba_imu_factor(5, Mx, w)
+        h.ba_imu_factor(5, M, 1e3)   # finite: accepted
+    finally:
+        h.close()
+
+
 def test_ba_stage_is_idempotent_per_batch():
     """Running the BA stage again for the same batch inserts nothing twice."""
     import torch

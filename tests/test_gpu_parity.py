@@ -22,14 +22,14 @@ N_FRAMES = 4
 
 @functools.lru_cache(maxsize=8)
 def hip_run(seed: int = 0, batch: int = N_FRAMES, distorted: bool = False, n: int = N_FRAMES, cfg_items: tuple = (),
-            splits: int = 0, width: int = 640, height: int = 400, mode: str = "auto"):
+            splits: int = 0, width: int = 640, height: int = 400, mode: str = "auto", refine_block: int = 0):
     import torch
 
     from thor_slam_amd._lib import Handle
 
     sc = scenario(seed=seed, n=n, width=width, height=height, distorted=distorted, cfg_items=cfg_items)
     cfg = sc["cfg"]
-    h = Handle([sc["rect"]], cfg, max_batch=batch, ransac_splits=splits, ransac_mode=mode)
+    h = Handle([sc["rect"]], cfg, max_batch=batch, ransac_splits=splits, ransac_mode=mode, refine_block=refine_block)
     dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
     per = []
     K = cfg.n_features
@@ -362,3 +362,62 @@ def test_ransac_bounded_scoring_with_outliers(splits, mode):
     assert (st[4], st[3]) == (o["best_hyp"], o["best_count"]), "RANSAC winner differs"
     assert st[0] == o["status"] == 0 and st[2] == o["n_inliers"]
     assert rel_frobenius(T, o["T"]) < 1e-9
+
+
+def test_refine_block_128_parity():
+    """k_refine<128> (the automatic choice from 512 frames per launch) forced on a small batch:
+    the oracle's pose within 1e-9, and bit-identical to k_refine<256> — both follow the same
+    256-virtual-thread summation partition (k_pose.hip, RF_VIRT)."""
+    sc, a = hip_run(refine_block=128)
+    _, b = hip_run(refine_block=256)
+    for i, (x, y) in enumerate(zip(a, b)):
+        for k in ("stats", "T_rel", "T_abs", "cov"):
+            np.testing.assert_array_equal(x[k], y[k], err_msg=f"frame {i} {k}")
+        if i:
+            o = sc["oracle"][i]
+            assert x["stats"][4] == o["best_hyp"] and x["stats"][2] == o["n_inliers"]
+            assert rel_frobenius(x["T_rel"], o["T"]) < 1e-9
+            assert rel_frobenius(x["T_abs"], o["world_T_cam"]) < 1e-9
+
+
+def test_refine_512_frame_launch_invariance():
+    """One launch of 512 frames (auto: k_refine<128>, the bounded RANSAC) against the same launch with
+    k_refine<256> forced, and against launches of 64 frames: stats, poses and covariances
+    bit-identical on every frame; the first frames also equal the oracle."""
+    import torch
+
+    from oracle import numpy_slam as O
+    from thor_slam_amd._lib import Handle
+
+    n, unique = 512, 16
+    k = np.arange(n) % (2 * (unique - 1))
+    tri = np.where(k < unique, k, 2 * (unique - 1) - k)   # consecutive frames stay consecutive
+    sc = scenario(seed=0, n=4)
+    cfg, rect = sc["cfg"], sc["rect"]
+    distinct = sc["src"].render_stereo_sequence(unique)
+    frames = np.ascontiguousarray(distinct[tri])
+    dev = torch.from_numpy(frames).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    out = {}
+    for name, batch, rb in (("auto", n, 0), ("256", n, 256), ("b64", 64, 0)):
+        h = Handle([rect], cfg, max_batch=batch, refine_block=rb)
+        recs = {k: [] for k in ("stats", "T_rel", "T_abs", "cov")}
+        for b0 in range(0, n, batch):
+            h.submit(dev[b0:].data_ptr(), batch, s)
+            res = h.read_poses(batch)
+            for k in recs:
+                recs[k].append(np.array(res[k][:, 0], copy=True))
+        h.close()
+        out[name] = {k: np.concatenate(v) for k, v in recs.items()}
+    for other in ("256", "b64"):
+        for k in ("stats", "T_rel", "T_abs", "cov"):
+            np.testing.assert_array_equal(out["auto"][k], out[other][k], err_msg=f"{other}: {k}")
+    assert (out["auto"]["stats"][1:, 0] == 0).mean() > 0.95   # tracked
+    trk = O.OracleTracker(cfg, dict(fx=rect.fx, fy=rect.fy, cx=rect.cx, cy=rect.cy, baseline=rect.baseline,
+                                    map_l=rect.map_left, map_r=rect.map_right))
+    for i in range(4):
+        o = trk.step(frames[i, 0], frames[i, 1])
+        if i:
+            assert out["auto"]["stats"][i, 4] == o["best_hyp"] and out["auto"]["stats"][i, 2] == o["n_inliers"]
+            assert rel_frobenius(out["auto"]["T_rel"][i], o["T"]) < 1e-9
+

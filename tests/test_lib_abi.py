@@ -40,10 +40,10 @@ def test_struct_layouts_match_c(tmp_path):
 #include <stddef.h>
 #include "{HEADER}"
 int main(void) {{
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(tslam_params), offsetof(tslam_params, ransac_thr_px),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(tslam_params), offsetof(tslam_params, ransac_thr_px),
          offsetof(tslam_params, ransac_seed), offsetof(tslam_params, ransac_splits),
          offsetof(tslam_params, ba_window), offsetof(tslam_params, ba_lambda), offsetof(tslam_params, rgbd),
-         sizeof(tslam_stereo_desc), offsetof(tslam_stereo_desc, map_left));
+         offsetof(tslam_params, refine_block), sizeof(tslam_stereo_desc), offsetof(tslam_stereo_desc, map_left));
   return 0;
 }}""")
     exe = tmp_path / "probe"
@@ -51,7 +51,8 @@ int main(void) {{
     got = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
     P, S = _lib.Params, _lib.StereoDesc
     assert got == [ctypes.sizeof(P), P.ransac_thr_px.offset, P.ransac_seed.offset, P.ransac_splits.offset,
-                   P.ba_window.offset, P.ba_lambda.offset, P.rgbd.offset, ctypes.sizeof(S), S.map_left.offset]
+                   P.ba_window.offset, P.ba_lambda.offset, P.rgbd.offset, P.refine_block.offset, ctypes.sizeof(S),
+                   S.map_left.offset]
 
 
 def test_invalid_arguments_fail_cleanly():
@@ -61,10 +62,11 @@ def test_invalid_arguments_fail_cleanly():
     desc = _lib.StereoDesc(640, 400, 384.0, 384.0, 319.5, 199.5, 0.075, None, None)
     h = ctypes.c_void_p()
     bad = [
-        dict(n_pairs=0), dict(max_batch=0), dict(ransac_splits=99),
+        dict(n_pairs=0), dict(max_batch=0), dict(ransac_splits=99), dict(refine_block=64),
     ]
     for kw in bad:
-        prm = _lib.make_params(HipSlamConfig(), kw.get("max_batch", 4), kw.get("n_pairs", 1), kw.get("ransac_splits", 0))
+        prm = _lib.make_params(HipSlamConfig(), kw.get("max_batch", 4), kw.get("n_pairs", 1), kw.get("ransac_splits", 0),
+                               refine_block=kw.get("refine_block", 0))
         rc = lib.tslam_create(ctypes.byref(desc), ctypes.byref(prm), 0, ctypes.byref(h))
         assert rc == -1, kw
         assert lib.tslam_last_error()

@@ -1089,15 +1089,26 @@ __global__ void k_ba_rig_insert(BatchCtx c, BaArgs a) {
 // b_p = -g_c + C_p[:, 60], Ad_p = adjoint_rl(E_p^-1); written as the body pair's C = -S (column 60:
 // b) and U = 0, so k_ba_solve on the body pair solves (lam I + S) dB = b.
 __global__ __launch_bounds__(64) void k_ba_rig_combine(BatchCtx c, BaArgs a) {
+    // Ad_p is the same for every thread of the block: built once per pair into LDS (a per-thread
+    // array read at the runtime column j would live in scratch)
+    __shared__ double sA[6][6];
     const int n = a.n_order, r = blockIdx.x, col = threadIdx.x;
     BaPair qb = ba_pair(c, a, c.P);
     double v = 0.0;
-    if (r < 6 * n && (col < 6 * n || col == 60)) {
-        const int ci = r / 6, i = r - 6 * ci;
-        for (int p = 0; p < c.P; ++p) {
-            BaPair q = ba_pair(c, a, p);
+    const bool live = r < 6 * n && (col < 6 * n || col == 60);
+    const int ci = r / 6, i = r - 6 * ci;
+    for (int p = 0; p < c.P; ++p) {
+        __syncthreads();   // the previous pair's reads are done
+        if (col == 0) {
             double A[6][6];
             adjoint_rl(c.rig_Einv + 16 * p, A);
+            for (int aa = 0; aa < 6; ++aa)
+                for (int bb = 0; bb < 6; ++bb) sA[aa][bb] = A[aa][bb];
+        }
+        __syncthreads();
+        if (live) {
+            BaPair q = ba_pair(c, a, p);
+            const double(*A)[6] = sA;
             const double* U = q.cam_U + (size_t)ci * 27;
             if (col == 60) {   // (Ad^T b_p)[i]
                 double acc = 0.0;
@@ -1121,8 +1132,8 @@ __global__ __launch_bounds__(64) void k_ba_rig_combine(BatchCtx c, BaArgs a) {
             }
             v += acc;
         }
-        if (col != 60) v = -v;
     }
+    if (live && col != 60) v = -v;
     qb.C[r * 64 + col] = v;
     if (r == 0) {
         for (int e = col; e < a.W * 27; e += 64) qb.cam_U[e] = 0.0;

@@ -256,6 +256,11 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
                 b[j + 4] = 0;
             }
             acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 4, 4, 0, 127, 0, s == 0 ? 128 : s == 1 ? 127 : 126);
+            // b stays live past the MFMA, so the destination never lands on it: the compiler does
+            // not keep vdst of the block-scaled MFMA apart from its sources (no early-clobber), and
+            // a build that spilled put vdst over srcA and half of srcC — wrong stereo matches
+            // (DESIGN.md §5).  isa_guard.py checks every build's MFMA operands.
+            asm volatile("" ::"v"(b));
         }
         const uint32_t txy = k < n ? e.x : 0x80008000u;   // padding fails every gate
         const uint32_t tidx = e.y >> 16;

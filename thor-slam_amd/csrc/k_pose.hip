@@ -687,10 +687,18 @@ __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
 // k_refine's block is RF_THREADS = 128 (2 waves) for large launches: its 222 VGPRs allow 2 waves
 // per SIMD, so 4 such blocks fit a CU and 1024 frames run in one round instead of two (C2: 147
 // against 160 us; 64 threads: 185); small launches keep 256 threads per frame.
+// The normal-equation sums do not depend on the block size: they always follow the partition of
+// RF_VIRT = 256 virtual threads (virtual thread v sums correspondences v, v + 256, ...; virtual
+// wave w = v >> 6 is reduced by wave_multi_sum; the 4 wave sums are added in order).  A 128-thread
+// block runs the virtual threads in two passes (tid, then tid + 128), so the pose, covariance and
+// inlier decisions are bit-identical whatever the launch size (batch-size invariance, and the
+// sharded ranks' smaller launches against one device's).
+#define RF_VIRT 256
 template <int RF_THREADS>
 __global__ __launch_bounds__(RF_THREADS) void k_refine(BatchCtx c, int S) {
+    static_assert(RF_VIRT % RF_THREADS == 0, "virtual partition");
     __shared__ int s_scan[RF_THREADS / 64];
-    __shared__ double s_red[RF_THREADS / 64][N_ACC];
+    __shared__ double s_red[RF_VIRT / 64][N_ACC];
     __shared__ double s_R[9], s_t[3], s_H[36], s_misc[4];
     __shared__ int s_flag, s_best;
     const int p = c.pair0 + (int)blockIdx.x % c.npair;
@@ -738,10 +746,11 @@ __global__ __launch_bounds__(RF_THREADS) void k_refine(BatchCtx c, int S) {
 #pragma unroll
         for (int k = 0; k < 9; ++k) R[k] = s_R[k];
         t[0] = s_t[0]; t[1] = s_t[1]; t[2] = s_t[2];
+        for (int pass = 0; pass < RF_VIRT / RF_THREADS; ++pass) {
         double acc[N_ACC];
 #pragma unroll
         for (int k = 0; k < N_ACC; ++k) acc[k] = 0.0;
-        for (int ci = tid; ci < n; ci += RF_THREADS) {
+        for (int ci = tid + pass * RF_THREADS; ci < n; ci += RF_VIRT) {
             const double* cr = corr + (size_t)ci * TS_CORR_DOUBLES;
             if (!is_inlier(R, t, cr, fx, fy, thr2)) continue;
             const double X = cr[0], Y = cr[1], Z = cr[2];
@@ -769,14 +778,15 @@ __global__ __launch_bounds__(RF_THREADS) void k_refine(BatchCtx c, int S) {
         }
         {
             const double w = wave_multi_sum(acc);   // the sum of acc[lane >> 1]
-            if ((lane & 1) == 0 && (lane >> 1) < N_ACC) s_red[wave][lane >> 1] = w;
+            if ((lane & 1) == 0 && (lane >> 1) < N_ACC) s_red[wave + pass * (RF_THREADS / 64)][lane >> 1] = w;
+        }
         }
         __syncthreads();
         if (tid == 0) {
             double tot[N_ACC];
             for (int k = 0; k < N_ACC; ++k) {
                 tot[k] = s_red[0][k];
-                for (int w = 1; w < RF_THREADS / 64; ++w) tot[k] += s_red[w][k];
+                for (int w = 1; w < RF_VIRT / 64; ++w) tot[k] += s_red[w][k];
             }
             const int n_in = (int)tot[28];
             s_flag = 0;
@@ -1274,7 +1284,8 @@ int ransac_splits(const BatchCtx& c) {
 }
 
 static void launch_refine(const BatchCtx& c, int S, hipStream_t s) {
-    if (c.n * c.npair >= 512)
+    // the block size changes only the speed (RF_VIRT partition above), never the results
+    if (c.pp.refine_block == 128 || (c.pp.refine_block == 0 && c.n * c.npair >= 512))
         hipLaunchKernelGGL(k_refine<128>, dim3(c.n * c.npair), dim3(128), 0, s, c, S);
     else
         hipLaunchKernelGGL(k_refine<256>, dim3(c.n * c.npair), dim3(256), 0, s, c, S);

@@ -474,6 +474,7 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.pp.min_inliers = h->prm.min_inliers;
     c.pp.splits = h->prm.ransac_splits;
     c.pp.mode = h->prm.ransac_mode;
+    c.pp.refine_block = h->prm.refine_block;
     c.pp.thr2 = h->prm.ransac_thr_px * h->prm.ransac_thr_px;
     c.pp.seed = h->prm.ransac_seed;
     c.fast_threshold = h->prm.fast_threshold;
@@ -636,6 +637,8 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     if (p.refine_iters < 1) return fail(TSLAM_EINVAL, "refine_iters must be >= 1");
     if (p.ransac_splits < 0 || p.ransac_splits > TS_MAX_SPLITS) return fail(TSLAM_EINVAL, "ransac_splits must be in [0, 32]");
     if (p.ransac_mode < 0 || p.ransac_mode > 2) return fail(TSLAM_EINVAL, "ransac_mode must be 0, 1 or 2");
+    if (p.refine_block != 0 && p.refine_block != 128 && p.refine_block != 256)
+        return fail(TSLAM_EINVAL, "refine_block must be 0, 128 or 256");
     const int W = pairs[0].width, H = pairs[0].height;
     if (W < 64 || H < 64 || W > 2047 || H > 2047) return fail(TSLAM_EINVAL, "image size must be within [64, 2047]");
     for (int i = 1; i < p.n_pairs; ++i)
@@ -2110,7 +2113,11 @@ int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_e
 int tslam_ba_imu_factor(tslam_handle* h, int pair, int64_t frame, const double* M, double weight) {
     if (!h || !M || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad argument");
     if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
-    if (!(weight >= 0.0) || frame < 0) return fail(TSLAM_EINVAL, "weight must be >= 0, frame >= 0");
+    // non-finite inputs would poison the whole window's Schur system (k_ba_solve adds them to S, b)
+    if (!(weight >= 0.0) || !std::isfinite(weight) || frame < 0)
+        return fail(TSLAM_EINVAL, "weight must be finite and >= 0, frame >= 0");
+    for (int e = 0; e < 9; ++e)
+        if (!std::isfinite(M[e])) return fail(TSLAM_EINVAL, "rotation M must be finite");
     std::array<double, 10> f{};
     for (int e = 0; e < 9; ++e) f[e] = M[e];
     f[9] = weight;

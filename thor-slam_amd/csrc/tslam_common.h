@@ -81,6 +81,7 @@ struct MatchParams {
 struct PoseParams {
     int n_hyp, iters, min_inliers, splits;
     int mode;   // RANSAC scoring: 0 auto, 1 exhaustive (k_ransac_all), 2 bounded (k_ransac)
+    int refine_block;   // k_refine threads per frame: 0 auto, 128, 256
     double thr2;
     uint64_t seed;
 };

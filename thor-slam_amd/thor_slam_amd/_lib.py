@@ -55,6 +55,7 @@ class Params(ctypes.Structure):
         ("ba_window", ctypes.c_int32), ("ba_kf_interval", ctypes.c_int32), ("ba_iters", ctypes.c_int32),
         ("ba_pad", ctypes.c_int32), ("ba_lambda", ctypes.c_double), ("ba_outlier_px", ctypes.c_double),
         ("rgbd", ctypes.c_int32), ("ransac_mode", ctypes.c_int32),
+        ("refine_block", ctypes.c_int32), ("reserved0", ctypes.c_int32),
     ]
 
 
@@ -266,13 +267,13 @@ RANSAC_MODE = {"auto": 0, "exhaustive": 1, "bounded": 2}   # tslam_params.ransac
 
 
 def make_params(cfg: HipSlamConfig, max_batch: int, n_pairs: int, ransac_splits: int = 0,
-                ransac_mode: str = "auto") -> Params:
+                ransac_mode: str = "auto", refine_block: int = 0) -> Params:
     return Params(
         cfg.n_features, cfg.n_levels, cfg.fast_threshold, cfg.edge_margin, cfg.max_hamming, cfg.ratio_pct,
         cfg.stereo_row_tol, cfg.max_disparity, cfg.temporal_window, cfg.ransac_hypotheses, cfg.refine_iters,
         cfg.min_inliers, float(cfg.ransac_thr_px), int(cfg.ransac_seed) & ((1 << 64) - 1), int(max_batch), int(n_pairs),
         int(ransac_splits), int(cfg.ba_window), int(cfg.ba_kf_interval), int(cfg.ba_iters), 0, float(cfg.ba_lambda),
-        float(cfg.ba_outlier_px), int(bool(cfg.rgbd)), RANSAC_MODE[ransac_mode],
+        float(cfg.ba_outlier_px), int(bool(cfg.rgbd)), RANSAC_MODE[ransac_mode], int(refine_block), 0,
     )
 
 
@@ -311,7 +312,7 @@ class Handle:
     """Owns one ``tslam_handle`` (one device, ``n_pairs`` stereo pairs, batches <= ``max_batch``)."""
 
     def __init__(self, rects: list, cfg: HipSlamConfig, max_batch: int = 1, device: int = 0, ransac_splits: int = 0,
-                 ransac_mode: str = "auto"):
+                 ransac_mode: str = "auto", refine_block: int = 0):
         self.lib = load_library()
         cfg.validate()
         self.cfg = cfg
@@ -330,7 +331,7 @@ class Handle:
                 None if ml is None else ml.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
                 None if mr is None else mr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
             )
-        params = make_params(cfg, max_batch, self.n_pairs, ransac_splits, ransac_mode)
+        params = make_params(cfg, max_batch, self.n_pairs, ransac_splits, ransac_mode, refine_block)
         h = ctypes.c_void_p()
         _check(self.lib.tslam_create(descs, ctypes.byref(params), int(device), ctypes.byref(h)))
         self.h = h
