@@ -68,6 +68,8 @@ VALU_PEAK_WINST = 256 * 4 * 2.4e9 / 2
 C2_BATCH = 1024
 # C5 rig frames per step: 4 periods of the 24-frame triangle wave (the resident batch is replayed)
 C5_BATCH = 184
+# C3 rig frames per step (one GPU, and each step of the sharded rig)
+C3_BATCH = 256
 FP64_MFMA_PEAK_TFS = 78.6   # MI355X FP64 matrix peak (AMD spec; the microarch guide lists no FP64 row)
 # bench kernel label -> device symbol (rocprofv3 / PMC summaries); "pose" is k_corr+k_ransac+k_refine
 KERNEL_SYMBOL = {"rectify_pyramid": "k_rectify_pyramid", "detect": "k_detect", "select": "k_select",
@@ -553,7 +555,7 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     width, height = (1280, 800) if c4 else (1280, 720) if c5 else (640, 400)
     cfg = (HipSlamConfig(n_features=4000, ba_window=10, ba_kf_interval=5, ba_iters=5) if c4 else
            HipSlamConfig(rgbd=True) if c5 else HipSlamConfig())
-    B = args.batch or (50 if c4 else C5_BATCH if c5 else 256 if c3 else C2_BATCH)
+    B = args.batch or (50 if c4 else C5_BATCH if c5 else C3_BATCH if c3 else C2_BATCH)
     args.unique = args.unique or (24 if (c4 or c5) else 48)
     workers = max(1, min(16, usable_cpus(), args.unique * (8 if c3 else 1)))
     t_r = time.perf_counter()
@@ -883,6 +885,11 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
 
 # ---- sharded rig (N > 1): one camera stream per GPU -------------------------------------------
 def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
+    """The sharded rig through the library's own driver (tslam_shard.cpp, the code the SlamEngine and
+    the C-ABI ship): one process per rank over RCCL (tslam_comm_init + tslam_submit_sharded), or
+    with ``--transport copy`` all ranks in this one process on one GPU (tslam_group_create, device
+    copies: a rehearsal of the exchange on a one-GPU box).  ``--driver torch`` runs the
+    torch.distributed test double (thor_slam_amd/shard.py: DistShardedRig) instead."""
     import torch
     import torch.distributed as dist
 
@@ -890,6 +897,7 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
     from thor_slam_amd.shard import DistShardedRig, ShardPlan, StageTimer
 
     c3, c5 = args.config == "c3", args.config == "c5"
+    rehearse = args.transport == "copy"
     if args.config == "c2" and world % 2:
         raise SystemExit("c2 over several GPUs shards stereo pairs' streams: --gpus must be even")
     if c5 and 4 % world:
@@ -897,7 +905,7 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
     names = RIG_SOURCES if (c3 or c5) else RIG_SOURCES[:world // 2]
     width, height = (1280, 720) if c5 else (640, 400)
     cfg = HipSlamConfig(rgbd=True) if c5 else HipSlamConfig()
-    B = args.batch or (C5_BATCH if c5 else 256 if c3 else C2_BATCH)
+    B = args.batch or (C5_BATCH if c5 else C3_BATCH if c3 else C2_BATCH)
     args.unique = args.unique or (24 if c5 else 48)
     if c5:
         _, cams, pairs, rects, E = rgbd_rig_setup(names, width, height)
@@ -907,45 +915,93 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
         C = 2 * len(rects)
     P = len(rects)
     plan = ShardPlan(C, world, B)
-    c0, c1 = plan.cams(rank)
-    workers = max(1, min(16, max(2, usable_cpus() // max(1, world)), args.unique * (c1 - c0)))
+    local = list(range(world)) if rehearse else [rank]   # the ranks this process drives
+    c0, c1 = (0, C) if rehearse else plan.cams(rank)
+    workers = max(1, min(16, max(2, usable_cpus() // max(1, 1 if rehearse else world)), args.unique * (c1 - c0)))
     t_r = time.perf_counter()
-    if c5:   # this rank's cameras only; one batch resident, replayed (whole triangle-wave periods)
+    if c5:   # this process's cameras only; one batch resident, replayed (whole triangle-wave periods)
         uniq = render_rgbd_rig_frames(names, args.unique, c0, c1, workers, width, height)
         if B % (2 * (args.unique - 1)):
             raise SystemExit(f"--config c5 needs --batch a multiple of {2 * (args.unique - 1)}")
         total = B
     else:
-        uniq = render_rig_frames(names, args.unique, c0, c1, workers, width, height)   # this rank's streams only
+        uniq = render_rig_frames(names, args.unique, c0, c1, workers, width, height)   # this process's streams only
         total = (args.warmup + args.steps) * B
     t_render = time.perf_counter() - t_r
     idx = torch.from_numpy(triangle_indices(total, args.unique)).cuda()
-    seq = torch.from_numpy(uniq).cuda().index_select(0, idx).contiguous()   # [total, S, H, W] in HBM
-    batch_of = (lambda s: seq) if c5 else (lambda s: seq[s * B:(s + 1) * B])
-    rig = DistShardedRig(rects, cfg, B, base_T_rect=E if P > 1 else None, device=dev_index, exchange=args.exchange,
-                         front_priority=bool(args.front_priority))
+    S = plan.streams_per_rank
+    seqs = []   # per local rank: [total, S, H, W] (RGB-D: records) in HBM
+    full = torch.from_numpy(uniq).cuda()
+    for r in local:
+        lo = (plan.cams(r)[0] - c0)
+        seqs.append(full[:, lo:lo + S].index_select(0, idx).contiguous())
+    del full
+    batch_of = (lambda q, s: seqs[q]) if c5 else (lambda q, s: seqs[q][s * B:(s + 1) * B])
+    stream = torch.cuda.current_stream()
+    if args.driver == "torch":
+        if rehearse:
+            raise SystemExit("--transport copy rehearses the library driver (--driver library)")
+        rig = DistShardedRig(rects, cfg, B, base_T_rect=E if P > 1 else None, device=dev_index, exchange=args.exchange,
+                             front_priority=bool(args.front_priority))
+        step = lambda s, timer=None: rig.step(batch_of(0, s), timer)   # noqa: E731
+        drain = rig.drain
+    else:
+        from thor_slam_amd._lib import Handle, HandleGroup, comm_unique_id
+
+        hs = [Handle(rects, cfg, max_batch=B, device=dev_index) for _ in local]
+        for h in hs:
+            if P > 1:
+                h.set_rig(E)
+        if rehearse:
+            grp = HandleGroup(hs, "copy")
+            step = lambda s, timer=None: grp.submit([batch_of(q, s).data_ptr() for q in range(world)], B,  # noqa: E731
+                                                    [stream.cuda_stream] * world)
+        else:
+            uid = [comm_unique_id() if rank == 0 else None]
+            if world > 1:
+                dist.broadcast_object_list(uid, src=0)
+            hs[0].comm_init(uid[0], rank, world)
+            step = lambda s, timer=None: hs[0].submit_sharded(batch_of(0, s).data_ptr(), B, stream.cuda_stream)  # noqa: E731
+        drain = torch.cuda.synchronize
     for s in range(args.warmup):
-        rig.step(batch_of(s))
-    rig.drain()
-    dist.barrier()
+        step(s)
+    drain()
+    if world > 1 and not rehearse:
+        dist.barrier()
     torch.cuda.synchronize()
     timer = StageTimer()
+    if args.driver == "library":
+        hs[0].shard_options(profile=True)
     t0 = time.perf_counter()
     for k in range(args.steps):
         s = args.warmup + k
-        rig.step(batch_of(s), timer)
-    rig.drain()
-    dist.barrier()
+        step(s, timer)
+    drain()
+    if world > 1 and not rehearse:
+        dist.barrier()
     elapsed = time.perf_counter() - t0
-    tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    elapsed = float(tt.item())
-    res = rig.read()
+    if world > 1 and not rehearse:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    if args.driver == "library":
+        timings = [h.shard_timing()[0] for h in hs]
+        per_kernel_us = {k: max(t[k] for t in timings) for k in timings[0]}   # the slowest local rank
+        per_kernel_us = {k: v for k, v in per_kernel_us.items() if v > 0.0}
+        res = {"pairs": hs[0].read_poses(B)}
+        if P > 1:
+            res["rig"] = hs[0].read_rig_poses(B)
+        sb, pr = hs[0].exchange_sizes()
+        pb = hs[0].pair_block_bytes() if c5 else 0
+    else:
+        res = rig.read()
+        per_kernel_us = timer.mean_us()
+        sb, pr = rig.rk.block, rig.rk.record
+        pb = rig.rk.pblock if c5 else 0
     ok = float(np.mean(res["pairs"]["stats"][:, :, 0] == 0))
     rig_ok = float(np.mean(res["rig"]["stats"][:, 0] == 0)) if P > 1 else None
-    per_kernel_us = timer.mean_us()
     # exchange spans (HIP events across the streams): not kernels, reported on their own
-    exchange_us = {k: per_kernel_us.pop(k) for k in ("exchange_exposed", "pose_gather") if k in per_kernel_us}
+    exchange_us = {k: per_kernel_us.pop(k) for k in ("exchange_exposed", "exchange_wait", "pose_gather") if k in per_kernel_us}
     # the dominant kernel's algorithmic bytes: the §8d rig-frame bytes x the share of the rig one
     # launch covers (front kernels: S of C streams for B frames; back kernels: all streams for B/N frames)
     S = plan.streams_per_rank
@@ -958,10 +1014,8 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
     share = (S / C) * B if (dom in front or (c5 and dom != "rig")) else B / world
     dom_bytes = unit_bytes * share
     achieved = dom_bytes / (per_kernel_us[dom] * 1e-6) / 1e9
-    sb, pr = rig.rk.block, rig.rk.record
-    alltoall = args.exchange == "alltoall" or c5
+    alltoall = args.exchange == "alltoall" or c5 or args.driver == "library"
     if c5:
-        pb = rig.rk.pblock
         xbytes = {"pair_blocks": (world - 1) * plan.frames_per_rank * S * pb, "pose_records": plan.frames_per_rank * pr,
                   "pair_block_bytes": pb, "pose_record_bytes": pr}
     else:
@@ -973,14 +1027,20 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
             "pose_record_bytes": pr,
         }
     xbytes["total_sent"] = sum(v for k_, v in xbytes.items() if not k_.endswith("_bytes"))
-    rig.close()
+    if args.driver == "library":
+        if rehearse:
+            grp.close()
+        for h in hs:
+            h.close()
+    else:
+        rig.close()
     frames_total = args.steps * B        # rig frames
     value = frames_total / elapsed * (1 if (c3 or c5) else P)
     out = {
         "metric": METRIC_C3 if c3 else METRIC_C5 if c5 else METRIC,
         "value": value,
         "unit": "frames/s",
-        "n_gpus": world,
+        "n_gpus": 1 if rehearse else world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
@@ -1020,7 +1080,10 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
         # exchange_exposed: front end packed -> both exchanges landed on the back stream (what the
         # overlap does not hide); pose_gather: the pose-record all-gather on the back stream
         "exchange_us": exchange_us,
-        "backend": args.dist_backend,
+        "backend": (f"library driver, copy transport: {world} ranks on one GPU (rehearsal of the exchange, not a "
+                    f"scaling value)" if rehearse else "library driver (tslam_comm_init + tslam_submit_sharded), RCCL"
+                    if args.driver == "library" else f"torch.distributed {args.dist_backend} (DistShardedRig test double)"),
+        "ranks": world,
         "tracking_ok_fraction_last_batch": ok,
         "rig_ok_fraction_last_batch": rig_ok,
         "render_s": t_render,
@@ -1086,7 +1149,13 @@ def main() -> None:
     ap.add_argument("--out", type=str, default="", help="also write the JSON line to this file")
     ap.add_argument("--dist-backend", type=str, default="nccl", help="nccl (RCCL) or gloo (rehearsal, host copy)")
     ap.add_argument("--exchange", choices=["alltoall", "allgather"], default="alltoall",
-                    help="sharded rig: all-to-all of the frames each rank solves, or all-gather of everything")
+                    help="--driver torch: all-to-all of the frames each rank solves, or all-gather of everything")
+    ap.add_argument("--driver", choices=["library", "torch"], default="library",
+                    help="sharded rig: the library's own driver (shipped; RCCL from tslam_comm_init) or the "
+                         "torch.distributed test double (thor_slam_amd/shard.py)")
+    ap.add_argument("--transport", choices=["rccl", "copy"], default="rccl",
+                    help="copy: all --gpus ranks in this process on one GPU with device copies (tslam_group_create; "
+                         "a rehearsal of the library driver's exchange on a one-GPU box)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="1: front and back kernels on two streams (batch s+1's front overlaps batch s's back)")
     ap.add_argument("--front-cu-reserve", type=int, default=0,
@@ -1105,7 +1174,7 @@ def main() -> None:
                     help="--gpus N > 1 without WORLD_SIZE: seconds before the self-launched ranks are killed")
     args = ap.parse_args()
 
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and args.transport != "copy":
         # N ranks requested from a plain `python bench.py --gpus N`: launch them (before this
         # process touches the GPU) and report rank 0's line
         sys.exit(self_launch(args.gpus, sys.argv[1:], args.launch_timeout))
@@ -1113,19 +1182,21 @@ def main() -> None:
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rehearse = args.transport == "copy"
+    world = args.gpus if rehearse else int(os.environ.get("WORLD_SIZE", "1"))
+    rank = 0 if rehearse else int(os.environ.get("RANK", "0"))
+    local = 0 if rehearse else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    if world > 1 and args.dist_backend == "nccl" and world > torch.cuda.device_count():
+    if world > 1 and not rehearse and args.dist_backend == "nccl" and world > torch.cuda.device_count():
         raise SystemExit(f"--gpus {world} over RCCL needs one GPU per rank ({torch.cuda.device_count()} visible); "
-                         "use --dist-backend gloo to rehearse several ranks on one GPU")
+                         "use --transport copy to rehearse the library driver's ranks on one GPU "
+                         "(or --dist-backend gloo --driver torch for the torch.distributed test double)")
     if args.config == "c4" and world > 1:
         raise SystemExit("--config c4 is a single-GPU configuration")
     dev_index = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev_index)
-    if world > 1:
+    if world > 1 and not rehearse:
         import datetime
 
         # a collective (or the communicator's eager init) that does not complete in this time
@@ -1135,9 +1206,11 @@ def main() -> None:
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index), timeout=tmo)
         else:
             dist.init_process_group(args.dist_backend, timeout=tmo)
+    if world > 1 and not rehearse and args.driver == "library" and args.dist_backend != "nccl":
+        raise SystemExit("the library driver exchanges over RCCL: --dist-backend nccl (or --transport copy)")
     sharded = world > 1 and args.config in ("c2", "c3", "c5")
     out = run_sharded(args, world, rank, dev_index) if sharded else run_single(args, world, rank, dev_index)
-    if world > 1:
+    if world > 1 and not rehearse:
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0:

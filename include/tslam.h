@@ -406,20 +406,53 @@ int tslam_unpack_poses(tslam_handle* h, const void* src, void* stream);
  *   other ranks over the host's own channel.
  * tslam_comm_init: this handle (the whole rig: tslam_create_rig, or tslam_create + tslam_set_rig)
  *   joins the `world`-rank communicator as `rank` (one rank per GPU, the handle's device) and owns
- *   cameras [rank*C/world, (rank+1)*C/world) and batch frames [rank*B/world, (rank+1)*B/world)
- *   (C and max_batch divisible by world; stereo or RGB-D rigs without local BA).
- * tslam_submit_sharded: one batch of max_batch frames of this rank's cameras ([B][C/world][H][W]
- *   u8 in HBM; RGB-D records [B][C/world][5*H*W]) once `stream` has them: front end of its
- *   cameras; raw images + stream blocks of the frames every other rank solves sent point to point
- *   (RGB-D: its cameras' pair blocks); back end (+ rig pose) of its frame range; pose records
- *   all-gathered; the chain.  The library runs the phases on streams of its own — front (high
- *   priority), exchange, back — with double-buffered exchange buffers, so batch s's image exchange
- *   overlaps its front end and batch s+1's front end overlaps batch s's back end; `stream` then
- *   waits for the batch.  Every rank then reads the whole rig's poses with tslam_read_poses /
- *   tslam_read_rig_poses, identical to one handle fed all cameras.  Nothing synchronises the host. */
+ *   cameras [rank*C/world, (rank+1)*C/world) and, of an n-frame batch, frames
+ *   [rank*n/world, (rank+1)*n/world) (C divisible by world, world <= max_batch; a stereo rig may
+ *   run local BA: rank 0 solves it, see TSLAM_SHARD_GATHER; RGB-D rigs without local BA).
+ * tslam_submit_sharded: one batch of n_frames (1 .. max_batch; ranges may be uneven or empty) of
+ *   this rank's cameras ([n][C/world][H][W] u8 in HBM; RGB-D records [n][C/world][5*H*W]) once
+ *   `stream` has them: front end of its cameras; raw images (straight from the input) + stream
+ *   blocks of the frames every other rank solves sent point to point (RGB-D: its cameras' pair
+ *   blocks); back end (+ rig pose) of its frame range; pose records all-gathered; the chain.  The
+ *   library runs the phases on streams of its own — front (high priority), exchange, back — with
+ *   double-buffered exchange buffers, so batch s's image exchange overlaps its front end and batch
+ *   s+1's front end overlaps batch s's back end; `stream` then waits for the batch.  Every rank then
+ *   reads the whole rig's poses with tslam_read_poses / tslam_read_rig_poses, identical to one
+ *   handle fed all cameras.  Nothing synchronises the host. */
 int tslam_comm_unique_id(void* id128);
 int tslam_comm_init(tslam_handle* h, const void* id128, int rank, int world);
-int tslam_submit_sharded(tslam_handle* h, const uint8_t* images, void* stream);
+int tslam_submit_sharded(tslam_handle* h, const uint8_t* images, int n_frames, void* stream);
+
+/* Options of the driver behind a sharded handle (tslam_comm_init, or any handle of a group):
+ *   TSLAM_SHARD_GATHER   every rank sends rank 0 the temporal matches + refined disparities of its
+ *                        frame range and the keypoints + descriptors of its left cameras, so rank
+ *                        0's ring holds what local BA, loop closure (tslam_loop_*) and
+ *                        relocalisation (tslam_relocalize) read, as on one handle; rank 0 solves
+ *                        the local BA window (implied when ba_window > 0);
+ *   TSLAM_SHARD_RESULTS  every batch's poses go to the handle's pinned result slots, so
+ *                        tslam_poll_batch / tslam_poll_pose work on a sharded handle (the
+ *                        asynchronous boundary: submit, then poll);
+ *   TSLAM_SHARD_PROFILE  HIP events around every kernel and exchange of this rank's batches;
+ *                        tslam_shard_timing returns the average µs per batch of each segment
+ *                        (TSLAM_SEG_*) since its last call (synchronises) and the batch count;
+ *   TSLAM_SHARD_SERIAL   (profiling aid) every rank's work on one stream per device, shared by the
+ *                        ranks on it: with all ranks of a group on one GPU, each kernel and copy
+ *                        runs alone, so the profile gives isolated per-rank durations.
+ * Setting options waits for the work enqueued so far. */
+#define TSLAM_SHARD_GATHER 1
+#define TSLAM_SHARD_RESULTS 2
+#define TSLAM_SHARD_PROFILE 4
+#define TSLAM_SHARD_SERIAL 8
+enum tslam_segment {
+    TSLAM_SEG_RECTIFY = 0, TSLAM_SEG_DETECT, TSLAM_SEG_SELECT, TSLAM_SEG_DESCRIBE, TSLAM_SEG_PACK,
+    TSLAM_SEG_EXCHANGE_WAIT,   /* front end done -> the peers' images and stream blocks landed */
+    TSLAM_SEG_IMPORT, TSLAM_SEG_MATCH, TSLAM_SEG_MATCH_REFINE, TSLAM_SEG_POSE, TSLAM_SEG_RIG,
+    TSLAM_SEG_STATE,           /* state blocks packed (senders) / unpacked (rank 0) */
+    TSLAM_SEG_POSE_GATHER, TSLAM_SEG_CHAIN, TSLAM_SEG_BA,
+    TSLAM_SEG_COUNT
+};
+int tslam_shard_options(tslam_handle* h, int flags);
+int tslam_shard_timing(tslam_handle* h, double* out_us, int n_out);
 
 /* One process driving the whole sharded rig (the SlamEngine boundary on several GPUs): handles[r]
  * (the same rig on every handle, one per rank, created on the rank's device) become ranks
@@ -428,7 +461,7 @@ int tslam_submit_sharded(tslam_handle* h, const uint8_t* images, void* stream);
  *     handle), all ranks' sends / receives issued inside one ncclGroupStart / ncclGroupEnd;
  *   TSLAM_TRANSPORT_COPY: device-to-device copies (hipMemcpyAsync) instead of RCCL, same buffers and
  *     ordering; several ranks may share a device (tests world > 1 on one GPU).
- * tslam_group_submit: one batch of n_frames (a multiple of n, <= max_batch); images[r] = rank r's
+ * tslam_group_submit: one batch of n_frames (1 .. max_batch); images[r] = rank r's
  *   cameras as for tslam_submit_sharded, streams[r] (NULL array or entries = each device's null
  *   stream) orders the input and then waits for the batch.
  * tslam_group_destroy before destroying the handles (they return to unsharded). */

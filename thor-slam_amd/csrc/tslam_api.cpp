@@ -512,9 +512,36 @@ static BatchCtx range_ctx(const BatchCtx& c, int lo, int hi) {
     return r;
 }
 
-static void shard_range(const tslam_handle* h, int n, int* lo, int* hi) {
-    *lo = h->sh_rank * n / h->sh_world;
-    *hi = (h->sh_rank + 1) * n / h->sh_world;
+static void shard_range(const tslam_handle* h, int n, int* lo, int* hi) { peer_range(h->sh_rank, n, h->sh_world, lo, hi); }
+
+// A8 of the current batch.  It may run on its own stream: it depends on this batch's poses (event
+// on the stream of the last stage) and only reads ring buffers plus a snapshot of the batch's
+// poses, so the next batch can start.  A sharded rank runs it once its ring holds every pair's
+// keyframe data (rank 0 after the state gather, tslam_shard.cpp).
+static int ba_stage(tslam_handle* h, const BatchCtx& c, hipStream_t s) {
+    if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
+    const int par = (int)(h->batch_idx & 1);
+    double* snap = h->ba.fe_pose + (size_t)par * h->B * h->P * 16;
+    double* snap_body = h->ba.fe_body + (size_t)par * h->B * 16;
+    hipStream_t fs = h->last_stream;
+    launch_ba_snapshot(c, snap, fs);
+    if (ba_rig(h)) launch_ba_snapshot_rig(c, snap_body, fs);
+    const bool other = s != fs;
+    if (other) {
+        if (!h->ev_fe) {
+            HIPCHK(hipEventCreateWithFlags(&h->ev_fe, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&h->ev_ba[0], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&h->ev_ba[1], hipEventDisableTiming));
+        }
+        HIPCHK(hipEventRecord(h->ev_fe, fs));
+        HIPCHK(hipStreamWaitEvent(s, h->ev_fe, 0));
+    }
+    run_ba(h, c, s, snap, snap_body);
+    if (other) {
+        HIPCHK(hipEventRecord(h->ev_ba[par], s));
+        h->ba_pending[par] = true;
+    }
+    return TSLAM_OK;
 }
 
 // Stages of a sharded handle (tslam_set_shard, world > 1).  Front stages run on the handle's
@@ -553,7 +580,7 @@ static int run_sharded_rgbd_stage(tslam_handle* h, const BatchCtx& c, int stage,
         case TSLAM_KERNEL_POSE: launch_pose(own, s); break;
         case TSLAM_KERNEL_RIG:
             if (!h->rig) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig)");
-            launch_rig_pose(range_ctx(c, lo, hi), s);
+            if (hi > lo) launch_rig_pose(range_ctx(c, lo, hi), s);
             break;
         case TSLAM_KERNEL_CHAIN: launch_chains(c, h->rig, s); break;
         default:
@@ -569,7 +596,8 @@ static int run_sharded_stage(tslam_handle* h, const BatchCtx& c, int stage, hipS
     int lo, hi;
     shard_range(h, c.n, &lo, &hi);
     const BatchCtx cb = range_ctx(c, lo, hi);
-    const bool pre = c.g0 + lo - 1 >= 0;   // frame lo - 1 exists
+    const bool empty = hi <= lo;           // a short batch leaves this rank no frames
+    const bool pre = !empty && c.g0 + lo - 1 >= 0;   // frame lo - 1 exists
     BatchCtx cp = c;                        // the pre-pass: frame lo - 1, batch scratch at frame 0
     cp.g0 = c.g0 + lo - 1;
     cp.n = 1;
@@ -583,24 +611,31 @@ static int run_sharded_stage(tslam_handle* h, const BatchCtx& c, int stage, hipS
         case TSLAM_KERNEL_DESCRIBE: launch_describe(c, s); break;
         case TSLAM_STAGE_MATCH:
             if (pre) launch_match_stereo(cp, s);
-            launch_match(cb, s);
-            launch_match_refine(cb, s);
+            if (!empty) {
+                launch_match(cb, s);
+                launch_match_refine(cb, s);
+            }
             break;
         case TSLAM_KERNEL_MATCH:
             if (pre) launch_match_stereo(cp, s);
-            launch_match(cb, s);
+            if (!empty) launch_match(cb, s);
             break;
-        case TSLAM_KERNEL_MATCH_REFINE: launch_match_refine(cb, s); break;
+        case TSLAM_KERNEL_MATCH_REFINE:
+            if (!empty) launch_match_refine(cb, s);
+            break;
         case TSLAM_STAGE_POSE:
-            launch_pose(cb, s);
-            if (h->rig) launch_rig_pose(cb, s);
+            if (!empty) launch_pose(cb, s);
+            if (!empty && h->rig) launch_rig_pose(cb, s);
             break;
-        case TSLAM_KERNEL_POSE: launch_pose(cb, s); break;
+        case TSLAM_KERNEL_POSE:
+            if (!empty) launch_pose(cb, s);
+            break;
         case TSLAM_KERNEL_RIG:
             if (!h->rig) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig)");
-            launch_rig_pose(cb, s);
+            if (!empty) launch_rig_pose(cb, s);
             break;
         case TSLAM_KERNEL_CHAIN: launch_chains(c, h->rig, s); break;
+        case TSLAM_STAGE_BA: return ba_stage(h, c, s);   // rank 0 of a gathering driver
         default:
             return fail(TSLAM_ESTATE, "a sharded handle runs its stages one by one around the exchange "
                                       "(RECTIFY..DESCRIBE, pack/exchange/unpack, MATCH, POSE, exchange, CHAIN)");
@@ -827,22 +862,11 @@ static int64_t host_frame_bytes(const tslam_handle* h) {
     return h->prm.rgbd ? (int64_t)h->P * 5 * h->W * h->H : (int64_t)h->C * h->W * h->H;
 }
 
-static int ensure_async(tslam_handle* h) {
-    if (h->as_front) return TSLAM_OK;
-    int lo = 0, hi = 0;
-    HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HIPCHK(hipStreamCreateWithPriority(&h->as_front, hipStreamNonBlocking, hi));   // front = critical path
-    HIPCHK(hipStreamCreateWithFlags(&h->as_back, hipStreamNonBlocking));
-    const size_t in_bytes = (size_t)h->B * host_frame_bytes(h);
+// pinned result slots per batch parity (tslam_poll_batch / tslam_poll_pose read them)
+static int ensure_result_slots(tslam_handle* h) {
+    if (h->as_res[0].ev) return TSLAM_OK;
     const size_t B = h->B, P = h->P;
     for (int k = 0; k < 2; ++k) {
-        void* p = nullptr;
-        HIPCHK(hipHostMalloc(&p, in_bytes, hipHostMallocDefault));
-        h->host_allocs.push_back(p);
-        h->as_stage[k] = (uint8_t*)p;
-        int rc = dev_alloc(h, (void**)&h->as_input[k], in_bytes);
-        if (rc != TSLAM_OK) return rc;
-        HIPCHK(hipEventCreateWithFlags(&h->as_staged[k], hipEventDisableTiming));
         auto& r = h->as_res[k];
         const size_t bytes[4] = {8 * B * P * TS_POSE_DOUBLES, 4 * B * P * TS_STATS_INTS, 8 * B * TS_POSE_DOUBLES,
                                  4 * B * TS_STATS_INTS};
@@ -854,6 +878,51 @@ static int ensure_async(tslam_handle* h) {
         r.ts.assign(B, 0.0);
         HIPCHK(hipEventCreateWithFlags(&r.ev, hipEventDisableTiming));
     }
+    return TSLAM_OK;
+}
+
+static int ensure_async(tslam_handle* h) {
+    if (h->as_front) return TSLAM_OK;
+    int rc = ensure_result_slots(h);
+    if (rc != TSLAM_OK) return rc;
+    int lo = 0, hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIPCHK(hipStreamCreateWithPriority(&h->as_front, hipStreamNonBlocking, hi));   // front = critical path
+    HIPCHK(hipStreamCreateWithFlags(&h->as_back, hipStreamNonBlocking));
+    const size_t in_bytes = (size_t)h->B * host_frame_bytes(h);
+    for (int k = 0; k < 2; ++k) {
+        void* p = nullptr;
+        HIPCHK(hipHostMalloc(&p, in_bytes, hipHostMallocDefault));
+        h->host_allocs.push_back(p);
+        h->as_stage[k] = (uint8_t*)p;
+        rc = dev_alloc(h, (void**)&h->as_input[k], in_bytes);
+        if (rc != TSLAM_OK) return rc;
+        HIPCHK(hipEventCreateWithFlags(&h->as_staged[k], hipEventDisableTiming));
+    }
+    return TSLAM_OK;
+}
+
+// The current batch's results into the pinned slot of its parity on stream s (an unread batch s-2
+// there is dropped), for tslam_poll_batch / tslam_poll_pose.  Timestamps: `ts` or frame indices.
+static int stash_results(tslam_handle* h, const double* ts, hipStream_t s) {
+    int rc = ensure_result_slots(h);
+    if (rc != TSLAM_OK) return rc;
+    const int k = (int)(h->as_batches & 1);
+    auto& r = h->as_res[k];
+    const size_t n = h->cur_n, P = h->P;
+    HIPCHK(hipMemcpyAsync(r.pose, h->buf[TSLAM_BUF_POSE].ptr, 8 * n * P * TS_POSE_DOUBLES, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(r.stats, h->buf[TSLAM_BUF_STATS].ptr, 4 * n * P * TS_STATS_INTS, hipMemcpyDeviceToHost, s));
+    if (h->rig) {
+        HIPCHK(hipMemcpyAsync(r.rig_pose, h->d_rig_pose, 8 * n * TS_POSE_DOUBLES, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(r.rig_stats, h->d_rig_stats, 4 * n * TS_STATS_INTS, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipEventRecord(r.ev, s));
+    for (size_t i = 0; i < n; ++i) r.ts[i] = ts ? ts[i] : (double)(h->cur_g0 + (int64_t)i);
+    r.batch = h->as_batches;
+    r.g0 = h->cur_g0;
+    r.n = (int)n;
+    r.pending = true;
+    h->as_batches += 1;
     return TSLAM_OK;
 }
 
@@ -877,26 +946,10 @@ int tslam_submit_host(tslam_handle* h, const uint8_t* host_images, const double*
     const int stages[5] = {TSLAM_STAGE_RECTIFY, TSLAM_STAGE_DETECT, TSLAM_STAGE_DESCRIBE, TSLAM_STAGE_MATCH, TSLAM_STAGE_POSE};
     for (int i = 0; i < 5 && rc == TSLAM_OK; ++i) rc = tslam_run_stage(h, stages[i], i < 3 ? h->as_front : h->as_back);
     if (rc == TSLAM_OK && h->prm.ba_window) rc = tslam_run_stage(h, TSLAM_STAGE_BA, h->as_back);
-    const int64_t g0 = h->cur_g0;
+    // results of this batch into the pinned slot of its parity
+    if (rc == TSLAM_OK) rc = stash_results(h, timestamps, h->as_back);
     const int rc2 = tslam_end_batch(h);
-    if (rc != TSLAM_OK || rc2 != TSLAM_OK) return rc != TSLAM_OK ? rc : rc2;
-    // results of this batch into the pinned slot of its parity (an unread batch s-2 there is dropped)
-    auto& r = h->as_res[k];
-    const size_t n = n_frames, P = h->P;
-    HIPCHK(hipMemcpyAsync(r.pose, h->buf[TSLAM_BUF_POSE].ptr, 8 * n * P * TS_POSE_DOUBLES, hipMemcpyDeviceToHost, h->as_back));
-    HIPCHK(hipMemcpyAsync(r.stats, h->buf[TSLAM_BUF_STATS].ptr, 4 * n * P * TS_STATS_INTS, hipMemcpyDeviceToHost, h->as_back));
-    if (h->rig) {
-        HIPCHK(hipMemcpyAsync(r.rig_pose, h->d_rig_pose, 8 * n * TS_POSE_DOUBLES, hipMemcpyDeviceToHost, h->as_back));
-        HIPCHK(hipMemcpyAsync(r.rig_stats, h->d_rig_stats, 4 * n * TS_STATS_INTS, hipMemcpyDeviceToHost, h->as_back));
-    }
-    HIPCHK(hipEventRecord(r.ev, h->as_back));
-    for (int i = 0; i < n_frames; ++i) r.ts[i] = timestamps ? timestamps[i] : (double)(g0 + i);
-    r.batch = h->as_batches;
-    r.g0 = g0;
-    r.n = n_frames;
-    r.pending = true;
-    h->as_batches += 1;
-    return TSLAM_OK;
+    return rc != TSLAM_OK ? rc : rc2;
 }
 
 static void unpack_records(const double* pose, int n, double* T_rel, double* T_abs, double* cov) {
@@ -977,10 +1030,6 @@ int tslam_begin_batch(tslam_handle* h, const uint8_t* images, int n_frames) {
     if (!images) return fail(TSLAM_EINVAL, "null images");
     if (n_frames < 1 || n_frames > h->B) return fail(TSLAM_EINVAL, "n_frames must be in [1, max_batch]");
     if (h->in_batch) return fail(TSLAM_ESTATE, "previous batch not ended");
-    // a sharded batch splits into `world` equal frame ranges: the pose-record all-gather has a
-    // fixed size per rank, so an uneven or empty range would chain the wrong records
-    if ((h->sh_world > 1 || h->sh_comm) && n_frames % h->sh_world != 0)
-        return fail(TSLAM_EINVAL, "a sharded batch needs n_frames divisible by world");
     h->cur_images = images;
     h->cur_n = n_frames;
     h->cur_g0 = h->frames_done;
@@ -1091,30 +1140,8 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
             launch_rig_pose(c, s);
             break;
         case TSLAM_STAGE_BA: {
-            // may run on its own stream: it depends on this batch's front end (event) and only
-            // reads ring buffers plus a snapshot of the batch's poses, so the next batch can start
-            if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
-            const int par = (int)(h->batch_idx & 1);
-            double* snap = h->ba.fe_pose + (size_t)par * h->B * h->P * 16;
-            double* snap_body = h->ba.fe_body + (size_t)par * h->B * 16;
-            hipStream_t fs = h->last_stream;
-            launch_ba_snapshot(c, snap, fs);
-            if (ba_rig(h)) launch_ba_snapshot_rig(c, snap_body, fs);
-            const bool other = s != fs;
-            if (other) {
-                if (!h->ev_fe) {
-                    HIPCHK(hipEventCreateWithFlags(&h->ev_fe, hipEventDisableTiming));
-                    HIPCHK(hipEventCreateWithFlags(&h->ev_ba[0], hipEventDisableTiming));
-                    HIPCHK(hipEventCreateWithFlags(&h->ev_ba[1], hipEventDisableTiming));
-                }
-                HIPCHK(hipEventRecord(h->ev_fe, fs));
-                HIPCHK(hipStreamWaitEvent(s, h->ev_fe, 0));
-            }
-            run_ba(h, c, s, snap, snap_body);
-            if (other) {
-                HIPCHK(hipEventRecord(h->ev_ba[par], s));
-                h->ba_pending[par] = true;
-            }
+            const int rc = ba_stage(h, c, s);
+            if (rc != TSLAM_OK) return rc;
             break;
         }
         case TSLAM_KERNEL_RECTIFY_PYRAMID: launch_rectify_pyramid(c, s); break;
@@ -1324,7 +1351,8 @@ int tslam_set_shard(tslam_handle* h, int cam_lo, int cam_hi, int rank, int world
     if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_set_shard inside a batch");
     if (cam_lo < 0 || cam_hi > h->C || cam_lo >= cam_hi) return fail(TSLAM_EINVAL, "camera range outside [0, cameras)");
     if (world < 1 || rank < 0 || rank >= world || world > h->B) return fail(TSLAM_EINVAL, "need 0 <= rank < world <= max_batch");
-    if (world > 1 && h->prm.ba_window) return fail(TSLAM_EINVAL, "sharding covers rigs without local BA");
+    if (world > 1 && h->prm.ba_window && h->prm.rgbd)
+        return fail(TSLAM_EINVAL, "a camera-sharded RGB-D rig runs without local BA");
     h->sh_cam_lo = cam_lo;
     h->sh_cam_hi = cam_hi;
     h->sh_rank = rank;
@@ -1445,6 +1473,31 @@ int tslam_internal_attach_driver(tslam_handle* h, tslam_shard_driver* d, bool ow
 
 tslam_shard_driver* tslam_internal_driver(tslam_handle* h) { return h ? h->drv : nullptr; }
 
+int64_t tslam_internal_state_bytes(tslam_handle* h, int n, int rank, int cam_lo, int cam_hi) {
+    int lo, hi;
+    peer_range(rank, n, h->sh_world, &lo, &hi);
+    const int left0 = (cam_lo + 1) & ~1, nleft = cam_hi > left0 ? (cam_hi - left0 + 1) / 2 : 0;
+    return (int64_t)(hi - lo) * h->P * state_range_block_bytes(h->g) + (int64_t)n * nleft * state_camera_block_bytes(h->g);
+}
+
+int tslam_internal_state_blocks(tslam_handle* h, int pack, int rank, int cam_lo, int cam_hi, void* buf, void* stream) {
+    if (!h || !buf) return fail(TSLAM_EINVAL, "bad argument");
+    if (!h->in_batch) return fail(TSLAM_ESTATE, "state blocks are packed / unpacked inside a batch");
+    if (h->prm.rgbd) return fail(TSLAM_ESTATE, "state blocks describe a stereo rig");
+    HIPCHK(hipSetDevice(h->device));
+    launch_state_blocks(make_ctx(h), pack != 0, h->cur_n, h->sh_world, rank, cam_lo, cam_hi, (uint8_t*)buf,
+                        (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return TSLAM_OK;
+}
+
+int tslam_internal_stash(tslam_handle* h, void* stream) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (!h->in_batch) return fail(TSLAM_ESTATE, "results are stashed inside a batch (before tslam_end_batch)");
+    HIPCHK(hipSetDevice(h->device));
+    return stash_results(h, nullptr, (hipStream_t)stream);
+}
+
 // -- the all-to-all's peers in one launch each (alltoall layout [world][nr][S]) -------------------
 static int check_peers(tslam_handle* h) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
@@ -1460,8 +1513,8 @@ int tslam_pack_streams_peers(tslam_handle* h, void* dst, void* stream) {
     if (rc != TSLAM_OK) return rc;
     if (!dst) return fail(TSLAM_EINVAL, "null buffer");
     HIPCHK(hipSetDevice(h->device));
-    const int N = h->sh_world, S = h->sh_cam_hi - h->sh_cam_lo, fpr = h->cur_n / N;
-    launch_stream_blocks_peers(make_ctx(h), true, h->cur_g0, fpr, fpr + 1, N, h->sh_rank, S, (uint8_t*)dst,
+    const int N = h->sh_world, S = h->sh_cam_hi - h->sh_cam_lo;
+    launch_stream_blocks_peers(make_ctx(h), true, h->cur_g0, h->cur_n, N, peer_cap(h->B, N), h->sh_rank, S, (uint8_t*)dst,
                                (hipStream_t)stream);
     HIPCHK(hipGetLastError());
     return TSLAM_OK;
@@ -1473,8 +1526,8 @@ int tslam_stage_raw_peers(tslam_handle* h, const uint8_t* prev_raw, void* dst, v
     if (!prev_raw || !dst) return fail(TSLAM_EINVAL, "null buffer");
     HIPCHK(hipSetDevice(h->device));
     const int N = h->sh_world, S = h->sh_cam_hi - h->sh_cam_lo;
-    launch_stage_raw_peers(h->cur_images, prev_raw, (uint8_t*)dst, h->cur_n / N, N, h->sh_rank, S, (int64_t)h->W * h->H,
-                           (hipStream_t)stream);
+    launch_stage_raw_peers(h->cur_images, prev_raw, (uint8_t*)dst, h->cur_n, N, peer_cap(h->B, N), h->sh_rank, S,
+                           (int64_t)h->W * h->H, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
     return TSLAM_OK;
 }
@@ -1484,8 +1537,12 @@ int tslam_import_peers(tslam_handle* h, const uint8_t* raw, const void* streams,
     if (rc != TSLAM_OK) return rc;
     if (!raw || !streams) return fail(TSLAM_EINVAL, "null buffer");
     HIPCHK(hipSetDevice(h->device));
-    const int N = h->sh_world, S = h->sh_cam_hi - h->sh_cam_lo, fpr = h->cur_n / N, nr = fpr + 1;
-    const int64_t first = h->cur_g0 + (int64_t)h->sh_rank * fpr - 1;
+    const int N = h->sh_world, S = h->sh_cam_hi - h->sh_cam_lo, cap = peer_cap(h->B, N);
+    const int nr = peer_frames(h->sh_rank, h->cur_n, N);
+    if (nr == 0) return TSLAM_OK;   // an empty frame range: this rank's back end has nothing to do
+    int lo, hi;
+    shard_range(h, h->cur_n, &lo, &hi);
+    const int64_t first = h->cur_g0 + lo - 1;
     const int skip = first < 0 ? 1 : 0;   // frame -1 (before the sequence start) is not imported
     BatchCtx c = make_ctx(h);
     c.images = raw;
@@ -1493,10 +1550,10 @@ int tslam_import_peers(tslam_handle* h, const uint8_t* raw, const void* streams,
     c.n = nr - skip;
     c.peer_S = S;
     c.peer_me = h->sh_rank;
-    c.peer_nbuf = nr;
+    c.peer_nbuf = cap;
     c.peer_skip = skip;
-    launch_rectify_pyramid(c, (hipStream_t)stream);
-    launch_stream_blocks_peers(make_ctx(h), false, h->cur_g0, fpr, nr, N, h->sh_rank, S, (uint8_t*)streams,
+    if (c.n > 0) launch_rectify_pyramid(c, (hipStream_t)stream);
+    launch_stream_blocks_peers(make_ctx(h), false, h->cur_g0, h->cur_n, N, cap, h->sh_rank, S, (uint8_t*)streams,
                                (hipStream_t)stream);
     HIPCHK(hipGetLastError());
     return TSLAM_OK;
@@ -1517,7 +1574,9 @@ int tslam_unpack_poses(tslam_handle* h, const void* src, void* stream) {
     if (!h || !src) return fail(TSLAM_EINVAL, "bad argument");
     if (!h->in_batch) return fail(TSLAM_ESTATE, "tslam_unpack_poses inside a batch (before its CHAIN stage)");
     HIPCHK(hipSetDevice(h->device));
-    launch_pose_records(make_ctx(h), false, 0, h->cur_n, (uint8_t*)src, (hipStream_t)stream);
+    // rank q's records start at q * peer_records(n, world) (the all-gather pads every range to the
+    // longest); with equal ranges that is the contiguous batch order
+    launch_pose_records_gathered(make_ctx(h), h->sh_world, (const uint8_t*)src, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
     return TSLAM_OK;
 }

@@ -161,6 +161,23 @@ struct BatchCtx {
 };
 
 static inline __host__ __device__ int ring_slot(const BatchCtx& c, int64_t g) { return (int)(g % c.R); }
+
+// Sharded rig: rank q's back end owns batch frames [q n / world, (q + 1) n / world)
+// of an n-frame batch (any n in [1, max_batch]: ranges may differ by one frame or be empty) and
+// reads the other cameras of frames lo - 1 .. hi - 1 (none for an empty range).  Exchange slots
+// are sized for a full batch: peer_cap frames per peer.
+static inline __host__ __device__ void peer_range(int q, int n, int world, int* lo, int* hi) {
+    *lo = (int)((int64_t)q * n / world);
+    *hi = (int)((int64_t)(q + 1) * n / world);
+}
+static inline __host__ __device__ int peer_frames(int q, int n, int world) {
+    int lo, hi;
+    peer_range(q, n, world, &lo, &hi);
+    return hi > lo ? hi - lo + 1 : 0;
+}
+static inline __host__ __device__ int peer_cap(int max_batch, int world) { return (max_batch + world - 1) / world + 1; }
+// pose records per rank in the all-gather of an n-frame batch (ranges padded to the longest)
+static inline __host__ __device__ int peer_records(int n, int world) { return (n + world - 1) / world; }
 // front-end image index (f * ncam + view camera) -> frame, rig camera; in the peer layout the
 // index runs over (peer, frame, camera) of the world-1 peers
 __device__ __forceinline__ void view_image(const BatchCtx& c, int img, int* f, int* cam) {
@@ -200,14 +217,24 @@ int64_t stream_block_bytes(const LevelGeom& g);
 int64_t pose_record_bytes(int P);
 void launch_stream_blocks(const BatchCtx& c, bool pack, int64_t first, int n_frames, int cam_lo, int ncam, uint8_t* blk,
                           hipStream_t s);
-// all peers at once (alltoall layout [world][nr][S][block]): pack this rank's cameras of every
-// peer q's frames g0 + q*fpr - 1 .. (slot q), or unpack every peer's cameras of frames
-// g0 + me*fpr - 1 .. (slot q <- cameras q*S ..); slot `me` untouched
-void launch_stream_blocks_peers(const BatchCtx& c, bool pack, int64_t g0, int fpr, int nr, int world, int me, int S,
+// all peers at once (alltoall layout [world][cap][S][block], cap = peer_cap): pack this rank's
+// cameras of every peer q's frames lo_q - 1 .. hi_q - 1 (slot q), or unpack every peer's cameras
+// of frames lo_me - 1 .. hi_me - 1 (slot q <- cameras q*S ..); slot `me` untouched
+void launch_stream_blocks_peers(const BatchCtx& c, bool pack, int64_t g0, int n, int world, int cap, int me, int S,
                                 uint8_t* blk, hipStream_t s);
-void launch_stage_raw_peers(const uint8_t* images, const uint8_t* prev, uint8_t* dst, int fpr, int world, int me, int S,
-                            int64_t img_bytes, hipStream_t s);
+void launch_stage_raw_peers(const uint8_t* images, const uint8_t* prev, uint8_t* dst, int n, int world, int cap, int me,
+                            int S, int64_t img_bytes, hipStream_t s);
 void launch_pose_records(const BatchCtx& c, bool pack, int f0, int n, uint8_t* rec, hipStream_t s);
+// every frame of the batch from the all-gather's padded layout [world][peer_records][record]
+void launch_pose_records_gathered(const BatchCtx& c, int world, const uint8_t* rec, hipStream_t s);
+// state blocks a sharded rank sends to rank 0 so that rank 0's ring holds what local BA, loop
+// closure and relocalisation read (k_exchange.hip): per (frame of the sender's range, pair) the
+// temporal matches + refined disparities, per (batch frame, left camera of the sender's streams)
+// keypoints + level counts + descriptors; pack on the sender, unpack on rank 0 (per sender)
+int64_t state_range_block_bytes(const LevelGeom& g);
+int64_t state_camera_block_bytes(const LevelGeom& g);
+void launch_state_blocks(const BatchCtx& c, bool pack, int n, int world, int rank, int cam_lo, int cam_hi, uint8_t* blk,
+                         hipStream_t s);
 // camera-sharded RGB-D rig: pair blocks (per batch frame x pair: pose, stats, correspondences)
 int64_t pair_block_bytes(const LevelGeom& g);
 void launch_pair_blocks(const BatchCtx& c, bool pack, int f0, int n_frames, int p0, int np, uint8_t* blk, hipStream_t s);

@@ -29,4 +29,13 @@ TSLAM_INTERNAL int tslam_internal_info(tslam_handle* h, tslam_handle_info* out);
 TSLAM_INTERNAL int tslam_internal_attach_driver(tslam_handle* h, tslam_shard_driver* d, bool owned);
 TSLAM_INTERNAL tslam_shard_driver* tslam_internal_driver(tslam_handle* h);
 TSLAM_INTERNAL void tslam_internal_driver_destroy(tslam_shard_driver* d);
+
+// State gather of a sharded stereo rig (k_exchange.hip, state blocks): bytes of sender `rank`'s
+// payload for an n-frame batch; pack (on the sender, its own rank / cameras) or unpack (on rank 0,
+// the sender's rank and camera range) inside a batch, after the back end of the sender's range.
+TSLAM_INTERNAL int64_t tslam_internal_state_bytes(tslam_handle* h, int n, int rank, int cam_lo, int cam_hi);
+TSLAM_INTERNAL int tslam_internal_state_blocks(tslam_handle* h, int pack, int rank, int cam_lo, int cam_hi, void* buf,
+                                               void* stream);
+// the current batch's poses / stats into the handle's pinned result slots (tslam_poll_batch)
+TSLAM_INTERNAL int tslam_internal_stash(tslam_handle* h, void* stream);
 }  // extern "C"

@@ -10,13 +10,24 @@
 //   f : RECTIFY, DETECT, DESCRIBE, pack streams      │   b : MATCH, POSE (own cameras, whole batch),
 //   x : ── exchange 1 (raw images, stream blocks) ◄──┘       pack pair blocks per peer range
 //   b : import raw + unpack streams, MATCH, POSE(+rig)  b : ── exchange 1 (pair blocks)
-//                                                       b : unpack pairs, KERNEL_RIG (own range)
+//   b : [state blocks ── gather to rank 0 ── unpack]    b : unpack pairs, KERNEL_RIG (own range)
 //   b : pack pose records ── exchange 2 (all-gather) ── unpack, CHAIN  (both)
+//   b : [rank 0: local BA]; [results into pinned slots]
 //
 // f = front stream (high priority), x = exchange stream, b = back stream.  Batch s's raw exchange
 // overlaps its front end and batch s+1's front end overlaps batch s's back end; a parity's receive
 // buffers are reused once the imports of batch s-2 are done (event), its send buffers once the
 // collectives that read them are.  Nothing here synchronises the host.
+//
+// Any batch of 1 .. max_batch frames: rank q's back end owns frames [q n / N, (q + 1) n / N) (ranges
+// may differ by a frame or be empty), exchange slots are sized for a full batch (peer_cap frames),
+// the pose all-gather pads every range to peer_records(n, N) records.  Raw images go straight from
+// the caller's input (and the previous batch's last frame) to the peers: no staging copy.
+//
+// State gather (TSLAM_SHARD_GATHER, implied by local BA): every rank sends rank 0 the temporal
+// matches and disparities of its range and the keypoints + descriptors of its left cameras, so
+// rank 0's ring holds what the one-handle path's local BA, loop closure and relocalisation read;
+// rank 0 then runs the local BA itself (the other ranks keep no window).
 //
 // Transports: RCCL (ncclSend / ncclRecv / ncclAllGather over xGMI; two communicators per rank so
 // the pose all-gather of batch s, on the back stream, never shares a communicator with batch s+1's
@@ -27,10 +38,12 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
 
+#include "tslam_common.h"
 #include "tslam_internal.h"
 
 #define SHCHK(expr)                                                                                            \
@@ -52,38 +65,60 @@
     } while (0)
 
 namespace {
+struct Span {   // one timed segment of one batch (TSLAM_SHARD_PROFILE)
+    int seg;
+    hipEvent_t a, b;
+};
+
 struct Rank {
     tslam_handle* h = nullptr;
     int rank = 0, device = 0;
     ncclComm_t comm_x = nullptr, comm_p = nullptr;
     hipStream_t fs = nullptr, xs = nullptr, bs = nullptr;
+    hipStream_t serial = nullptr;   // TSLAM_SHARD_SERIAL: the device's one stream (owned by its first rank)
+    bool serial_owner = false;
     hipEvent_t ev_in = nullptr, ev_front = nullptr, ev_x = nullptr, ev_push = nullptr, ev_done = nullptr;
     hipEvent_t consumed[2] = {nullptr, nullptr};   // this parity's receive buffers were read
     bool consumed_armed[2] = {false, false};
     bool done_armed = false;
-    uint8_t* raw_send[2] = {nullptr, nullptr};
     uint8_t* raw_recv[2] = {nullptr, nullptr};
     uint8_t* feat_send[2] = {nullptr, nullptr};    // stream blocks (stereo) or pair blocks (RGB-D)
     uint8_t* feat_recv[2] = {nullptr, nullptr};
     uint8_t* pose_send[2] = {nullptr, nullptr};
     uint8_t* pose_recv[2] = {nullptr, nullptr};
+    uint8_t* state_buf[2] = {nullptr, nullptr};    // gather: the payload (sender) / all payloads (rank 0)
     uint8_t* prev_raw = nullptr;   // the previous batch's last frame of this rank's cameras
     std::vector<void*> allocs;
+    // profiling
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    std::vector<Span> spans;
+    double seg_us[TSLAM_SEG_COUNT] = {};
+    int64_t timed_batches = 0;
 };
 
-enum Which { RAW = 0, FEAT = 1, POSE = 2 };
+enum Which { RAW = 0, FEAT = 1, POSE = 2, STATE = 3 };
 }  // namespace
 
 struct tslam_shard_driver {
     int world = 1, transport = TSLAM_TRANSPORT_RCCL;
-    bool rgbd = false, rig = false;
-    int S = 0, B = 0;                    // cameras per rank, max_batch
-    int n = 0, fpr = 0, nr = 0;          // this batch: frames, frames per rank, frames sent per peer (stereo)
+    bool rgbd = false, rig = false, ba = false;
+    int flags = 0;                       // TSLAM_SHARD_* options
+    int S = 0, B = 0, cap = 0;           // cameras per rank, max_batch, frames per peer slot
+    int n = 0, maxr = 0;                 // this batch: frames, pose records per rank in the all-gather
     size_t img = 0, rec = 0, sblk = 0, pblk = 0;   // bytes: image, pose record, stream block, pair block
-    size_t raw_q = 0, feat_q = 0;        // this batch: bytes per peer (raw images, stream / pair blocks)
+    size_t state_cap = 0;                // bytes of one sender's state payload slot (full batch)
     int64_t batches = 0;
     std::vector<Rank> ranks;   // local ranks: all of a group, one after tslam_comm_init
+    bool gather() const { return world > 1 && !rgbd && (ba || (flags & TSLAM_SHARD_GATHER)); }
 };
+
+// The rank's streams: its own three, or with TSLAM_SHARD_SERIAL one stream per device shared by
+// every rank on it (each kernel and copy then runs alone: the per-rank profile of a one-GPU
+// rehearsal reports isolated durations)
+static hipStream_t FS(const tslam_shard_driver* d, const Rank& r) { return (d->flags & TSLAM_SHARD_SERIAL) ? r.serial : r.fs; }
+static hipStream_t XS(const tslam_shard_driver* d, const Rank& r) { return (d->flags & TSLAM_SHARD_SERIAL) ? r.serial : r.xs; }
+static hipStream_t BS(const tslam_shard_driver* d, const Rank& r) { return (d->flags & TSLAM_SHARD_SERIAL) ? r.serial : r.bs; }
 
 static void destroy_driver(tslam_shard_driver* d) {
     if (!d) return;
@@ -94,8 +129,10 @@ static void destroy_driver(tslam_shard_driver* d) {
         if (r.comm_x) (void)ncclCommDestroy(r.comm_x);
         for (hipEvent_t e : {r.ev_in, r.ev_front, r.ev_x, r.ev_push, r.ev_done, r.consumed[0], r.consumed[1]})
             if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : r.ev_pool) (void)hipEventDestroy(e);
         for (hipStream_t s : {r.fs, r.xs, r.bs})
             if (s) (void)hipStreamDestroy(s);
+        if (r.serial && r.serial_owner) (void)hipStreamDestroy(r.serial);
         for (void* p : r.allocs) (void)hipFree(p);
         r.allocs.clear();
     }
@@ -118,14 +155,16 @@ static int alloc(Rank& r, uint8_t** p, size_t bytes) {
 static int plan(tslam_shard_driver* d, tslam_handle* h, int world) {
     tslam_handle_info in{};
     RC(tslam_internal_info(h, &in));
-    if (in.ba) return tslam_internal_fail(TSLAM_EINVAL, "sharding covers rigs without local BA");
-    if (in.C % world || in.B % world)
-        return tslam_internal_fail(TSLAM_EINVAL, "cameras and max_batch must divide by world");
+    if (in.ba && in.rgbd) return tslam_internal_fail(TSLAM_EINVAL, "a camera-sharded RGB-D rig runs without local BA");
+    if (in.C % world) return tslam_internal_fail(TSLAM_EINVAL, "the cameras must divide by world");
+    if (world > in.B) return tslam_internal_fail(TSLAM_EINVAL, "world must be <= max_batch");
     d->world = world;
     d->rgbd = in.rgbd != 0;
     d->rig = in.rig != 0;
+    d->ba = in.ba != 0;
     d->S = in.C / world;
     d->B = in.B;
+    d->cap = peer_cap(in.B, world);
     d->img = (size_t)in.W * in.H;
     d->rec = (size_t)in.pose_record;
     d->sblk = (size_t)in.stream_block;
@@ -133,19 +172,18 @@ static int plan(tslam_shard_driver* d, tslam_handle* h, int world) {
     return TSLAM_OK;
 }
 
-// Per-batch geometry of n frames (n % world == 0, n <= max_batch): the buffers are sized for
-// max_batch, a shorter batch uses the front of each per-peer slot.
-static void geom(tslam_shard_driver* d, int n) {
-    d->n = n;
-    d->fpr = n / d->world;
-    d->nr = d->fpr + 1;
-    if (d->rgbd) {
-        d->raw_q = 0;
-        d->feat_q = (size_t)d->fpr * d->S * d->pblk;   // my cameras' pair blocks of a peer's range
-    } else {
-        d->raw_q = (size_t)d->nr * d->S * d->img;        // frames lo-1 .. hi-1 of a peer's range
-        d->feat_q = (size_t)d->nr * d->S * d->sblk;
-    }
+// bytes rank `q`'s slot carries for this batch: raw images / stream blocks of the frames q's back end
+// reads (lo_q - 1 .. hi_q - 1) of S cameras; pair blocks (RGB-D) of q's range; slot capacities
+static size_t raw_bytes(const tslam_shard_driver* d, int q) { return (size_t)peer_frames(q, d->n, d->world) * d->S * d->img; }
+static size_t feat_bytes(const tslam_shard_driver* d, int q) {
+    if (!d->rgbd) return (size_t)peer_frames(q, d->n, d->world) * d->S * d->sblk;
+    int lo, hi;
+    peer_range(q, d->n, d->world, &lo, &hi);
+    return (size_t)(hi - lo) * d->S * d->pblk;
+}
+static size_t raw_cap(const tslam_shard_driver* d) { return (size_t)d->cap * d->S * d->img; }
+static size_t feat_cap(const tslam_shard_driver* d) {
+    return d->rgbd ? (size_t)(d->cap - 1) * d->S * d->pblk : (size_t)d->cap * d->S * d->sblk;
 }
 
 static int setup_rank(tslam_shard_driver* d, Rank& r) {
@@ -160,46 +198,154 @@ static int setup_rank(tslam_shard_driver* d, Rank& r) {
     SHCHK(hipStreamCreateWithFlags(&r.bs, hipStreamNonBlocking));
     for (hipEvent_t* e : {&r.ev_in, &r.ev_front, &r.ev_x, &r.ev_push, &r.ev_done, &r.consumed[0], &r.consumed[1]})
         SHCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    const size_t N = d->world;
-    geom(d, d->B);   // allocation sizes: a full batch
+    const size_t N = d->world, maxr = (size_t)peer_records(d->B, d->world);
     for (int k = 0; k < 2; ++k) {
-        if (!d->rgbd) {
-            RC(alloc(r, &r.raw_send[k], N * d->raw_q));
-            RC(alloc(r, &r.raw_recv[k], N * d->raw_q));
-        }
-        RC(alloc(r, &r.feat_send[k], N * d->feat_q));
-        RC(alloc(r, &r.feat_recv[k], N * d->feat_q));
-        RC(alloc(r, &r.pose_send[k], (size_t)d->fpr * d->rec));
-        RC(alloc(r, &r.pose_recv[k], N * d->fpr * d->rec));
+        if (!d->rgbd) RC(alloc(r, &r.raw_recv[k], N * raw_cap(d)));
+        RC(alloc(r, &r.feat_send[k], N * feat_cap(d)));
+        RC(alloc(r, &r.feat_recv[k], N * feat_cap(d)));
+        RC(alloc(r, &r.pose_send[k], maxr * d->rec));
+        RC(alloc(r, &r.pose_recv[k], N * maxr * d->rec));
     }
     if (!d->rgbd) RC(alloc(r, &r.prev_raw, (size_t)d->S * d->img));
     SHCHK(hipDeviceSynchronize());   // the zeroing (null stream) lands before the rank's streams use them
     return TSLAM_OK;
 }
 
-// The stream an exchange runs on (sender and receiver side): stereo raw images and stream blocks
-// on the exchange stream, pair blocks and pose records on the back stream.
-static hipStream_t xstream(const tslam_shard_driver* d, const Rank& r, Which w) {
-    return (w == POSE || d->rgbd) ? r.bs : r.xs;
+// The state-gather buffers (allocated when the gather is first needed): a sender's payload slot
+// holds its largest payload (a full batch); rank 0 keeps one slot per rank.
+static int setup_gather(tslam_shard_driver* d) {
+    if (!d->gather() || d->state_cap) return TSLAM_OK;
+    size_t cap = 0;
+    for (int q = 0; q < d->world; ++q)
+        cap = std::max(cap, (size_t)tslam_internal_state_bytes(d->ranks[0].h, d->B, q, q * d->S, (q + 1) * d->S));
+    d->state_cap = (cap + 255) / 256 * 256;
+    for (Rank& r : d->ranks) {
+        SHCHK(hipSetDevice(r.device));
+        for (int k = 0; k < 2; ++k) RC(alloc(r, &r.state_buf[k], (r.rank == 0 ? d->world : 1) * d->state_cap));
+        SHCHK(hipDeviceSynchronize());
+    }
+    return TSLAM_OK;
 }
 
-static int exchange(tslam_shard_driver* d, Which w, int k) {
+// ---- profiling (TSLAM_SHARD_PROFILE) ------------------------------------------------------------
+static int span_begin(tslam_shard_driver* d, Rank& r, int seg, hipStream_t s) {
+    if (!(d->flags & TSLAM_SHARD_PROFILE)) return TSLAM_OK;
+    SHCHK(hipSetDevice(r.device));
+    while (r.ev_pool.size() < r.ev_used + 2) {
+        hipEvent_t e;
+        SHCHK(hipEventCreate(&e));
+        r.ev_pool.push_back(e);
+    }
+    Span sp{seg, r.ev_pool[r.ev_used], r.ev_pool[r.ev_used + 1]};
+    r.ev_used += 2;
+    SHCHK(hipEventRecord(sp.a, s));
+    r.spans.push_back(sp);
+    return TSLAM_OK;
+}
+static int span_end(tslam_shard_driver* d, Rank& r, hipStream_t s) {
+    if (!(d->flags & TSLAM_SHARD_PROFILE)) return TSLAM_OK;
+    SHCHK(hipEventRecord(r.spans.back().b, s));
+    return TSLAM_OK;
+}
+// the span between an event already recorded on one stream and now on another
+static int span_between(tslam_shard_driver* d, Rank& r, int seg, hipStream_t from, hipStream_t to) {
+    RC(span_begin(d, r, seg, from));
+    return span_end(d, r, to);
+}
+static int run_timed(tslam_shard_driver* d, Rank& r, int seg, int stage, hipStream_t s) {
+    RC(span_begin(d, r, seg, s));
+    RC(tslam_run_stage(r.h, stage, s));
+    return span_end(d, r, s);
+}
+
+// ---- exchanges ----------------------------------------------------------------------------------
+// The stream an exchange runs on (sender and receiver side): stereo raw images and stream blocks
+// on the exchange stream, pair blocks, state blocks and pose records on the back stream.
+static hipStream_t xstream(const tslam_shard_driver* d, const Rank& r, Which w) {
+    return (w == POSE || w == STATE || d->rgbd) ? BS(d, r) : XS(d, r);
+}
+
+// The pieces rank `src` sends rank `dst` for exchange w (at most two: a raw image slot of peer 0
+// starts with the previous batch's last frame), as (source pointer, destination offset, bytes).
+struct Piece {
+    const uint8_t* p;
+    size_t off, bytes;
+};
+static int pieces(const tslam_shard_driver* d, const Rank& src, int dst, Which w, int k, const uint8_t* images,
+                  Piece* out) {
+    if (w == RAW) {
+        const size_t frame = (size_t)d->S * d->img, total = raw_bytes(d, dst);
+        if (total == 0) return 0;
+        int lo, hi;
+        peer_range(dst, d->n, d->world, &lo, &hi);
+        if (lo > 0) {   // frames lo-1 .. hi-1 are contiguous in the input
+            out[0] = {images + (size_t)(lo - 1) * frame, 0, total};
+            return 1;
+        }
+        out[0] = {src.prev_raw, 0, frame};   // frame -1: the previous batch's last frame
+        out[1] = {images, frame, total - frame};
+        return 2;
+    }
+    if (w == FEAT) {
+        const size_t b = feat_bytes(d, dst);
+        if (b == 0) return 0;
+        out[0] = {src.feat_send[k] + (size_t)dst * feat_cap(d), 0, b};
+        return 1;
+    }
+    return 0;
+}
+
+static int exchange(tslam_shard_driver* d, Which w, int k, const uint8_t* const* images) {
     const int N = d->world;
+    if (w == STATE && !d->gather()) return TSLAM_OK;
+    auto recv_buf = [&](Rank& r, int src) -> uint8_t* {   // where src's data lands in r's buffers
+        if (w == RAW) return r.raw_recv[k] + (size_t)src * raw_cap(d);
+        if (w == FEAT) return r.feat_recv[k] + (size_t)src * feat_cap(d);
+        return r.state_buf[k] + (size_t)src * d->state_cap;
+    };
+    auto recv_bytes = [&](const Rank& r, int src) -> size_t {   // what r receives from src
+        if (w == RAW) return raw_bytes(d, r.rank);
+        if (w == FEAT) return feat_bytes(d, r.rank);
+        return (size_t)tslam_internal_state_bytes(r.h, d->n, src, src * d->S, (src + 1) * d->S);
+    };
     if (d->transport == TSLAM_TRANSPORT_RCCL) {
         NCCLCHK(ncclGroupStart());
-        for (Rank& r : d->ranks) {
+        for (size_t i = 0; i < d->ranks.size(); ++i) {
+            Rank& r = d->ranks[i];
             hipStream_t s = xstream(d, r, w);
             if (w == POSE) {
-                NCCLCHK(ncclAllGather(r.pose_send[k], r.pose_recv[k], (size_t)d->fpr * d->rec, ncclUint8, r.comm_p, s));
+                NCCLCHK(ncclAllGather(r.pose_send[k], r.pose_recv[k], (size_t)d->maxr * d->rec, ncclUint8, r.comm_p, s));
                 continue;
             }
-            uint8_t* snd = w == RAW ? r.raw_send[k] : r.feat_send[k];
-            uint8_t* rcv = w == RAW ? r.raw_recv[k] : r.feat_recv[k];
-            const size_t u = w == RAW ? d->raw_q : d->feat_q;
+            if (w == STATE) {   // every rank to rank 0
+                if (r.rank != 0) {
+                    const size_t b = recv_bytes(d->ranks[i], r.rank);
+                    if (b) NCCLCHK(ncclSend(r.state_buf[k], b, ncclUint8, 0, r.comm_p, s));
+                } else {
+                    for (int q = 1; q < N; ++q) {
+                        const size_t b = recv_bytes(r, q);
+                        if (b) NCCLCHK(ncclRecv(recv_buf(r, q), b, ncclUint8, q, r.comm_p, s));
+                    }
+                }
+                continue;
+            }
             for (int q = 0; q < N; ++q) {
                 if (q == r.rank) continue;
-                NCCLCHK(ncclSend(snd + q * u, u, ncclUint8, q, r.comm_x, s));
-                NCCLCHK(ncclRecv(rcv + q * u, u, ncclUint8, q, r.comm_x, s));
+                Piece pc[2];
+                const int np = pieces(d, r, q, w, k, images ? images[i] : nullptr, pc);
+                for (int j = 0; j < np; ++j) NCCLCHK(ncclSend(pc[j].p, pc[j].bytes, ncclUint8, q, r.comm_x, s));
+                // what q sends me, in the same pieces (q's view of my range)
+                const size_t b = recv_bytes(r, q);
+                if (b == 0) continue;
+                int lo, hi;
+                peer_range(r.rank, d->n, N, &lo, &hi);
+                if (w == RAW && lo == 0) {
+                    const size_t frame = (size_t)d->S * d->img;
+                    NCCLCHK(ncclRecv(recv_buf(r, q), frame, ncclUint8, q, r.comm_x, s));
+                    NCCLCHK(ncclRecv(recv_buf(r, q) + frame, b - frame, ncclUint8, q, r.comm_x, s));
+                } else {
+                    NCCLCHK(ncclRecv(recv_buf(r, q), b, ncclUint8, q, r.comm_x, s));
+                }
             }
         }
         NCCLCHK(ncclGroupEnd());
@@ -207,26 +353,35 @@ static int exchange(tslam_shard_driver* d, Which w, int k) {
     }
     // COPY: each sender pushes into its peers' receive buffers on its own exchange-side stream,
     // once the peer has consumed the previous use of that parity; the receivers wait for every push
-    for (Rank& src : d->ranks) {
+    for (size_t i = 0; i < d->ranks.size(); ++i) {
+        Rank& src = d->ranks[i];
         SHCHK(hipSetDevice(src.device));
         hipStream_t s = xstream(d, src, w);
         for (Rank& dst : d->ranks) {
             if (w == POSE) {
                 if (dst.done_armed && &dst != &src) SHCHK(hipStreamWaitEvent(s, dst.ev_done, 0));
-                SHCHK(hipMemcpyAsync(dst.pose_recv[k] + (size_t)src.rank * d->fpr * d->rec, src.pose_send[k],
-                                     (size_t)d->fpr * d->rec, hipMemcpyDeviceToDevice, s));
+                SHCHK(hipMemcpyAsync(dst.pose_recv[k] + (size_t)src.rank * d->maxr * d->rec, src.pose_send[k],
+                                     (size_t)d->maxr * d->rec, hipMemcpyDeviceToDevice, s));
                 continue;
             }
             if (&dst == &src) continue;
+            if (w == STATE) {
+                if (dst.rank != 0) continue;
+                if (dst.done_armed) SHCHK(hipStreamWaitEvent(s, dst.ev_done, 0));   // rank 0 unpacked batch s-2
+                const size_t b = recv_bytes(dst, src.rank);
+                if (b) SHCHK(hipMemcpyAsync(recv_buf(dst, src.rank), src.state_buf[k], b, hipMemcpyDeviceToDevice, s));
+                continue;
+            }
             if (dst.consumed_armed[k]) SHCHK(hipStreamWaitEvent(s, dst.consumed[k], 0));
-            const size_t u = w == RAW ? d->raw_q : d->feat_q;
-            const uint8_t* snd = (w == RAW ? src.raw_send[k] : src.feat_send[k]) + (size_t)dst.rank * u;
-            uint8_t* rcv = (w == RAW ? dst.raw_recv[k] : dst.feat_recv[k]) + (size_t)src.rank * u;
-            SHCHK(hipMemcpyAsync(rcv, snd, u, hipMemcpyDeviceToDevice, s));
+            Piece pc[2];
+            const int np = pieces(d, src, dst.rank, w, k, images ? images[i] : nullptr, pc);
+            for (int j = 0; j < np; ++j)
+                SHCHK(hipMemcpyAsync(recv_buf(dst, src.rank) + pc[j].off, pc[j].p, pc[j].bytes, hipMemcpyDeviceToDevice, s));
         }
         SHCHK(hipEventRecord(src.ev_push, s));
     }
     for (Rank& dst : d->ranks) {
+        if (w == STATE && dst.rank != 0) continue;
         SHCHK(hipSetDevice(dst.device));
         hipStream_t s = xstream(d, dst, w);
         for (Rank& src : d->ranks)
@@ -235,88 +390,159 @@ static int exchange(tslam_shard_driver* d, Which w, int k) {
     return TSLAM_OK;
 }
 
-// Raw images of this rank's cameras for every peer: its frames lo-1 .. hi-1 (frame -1 = the last
-// frame of the previous batch), one gather launch on the exchange stream; then this batch's last
-// frame becomes prev_raw.
-static int stage_raw(tslam_shard_driver* d, Rank& r, const uint8_t* images, int k) {
-    const size_t frame = (size_t)d->S * d->img;
-    if (d->world > 1) RC(tslam_stage_raw_peers(r.h, r.prev_raw, r.raw_send[k], r.xs));
-    SHCHK(hipMemcpyAsync(r.prev_raw, images + (size_t)(d->n - 1) * frame, frame, hipMemcpyDeviceToDevice, r.xs));
-    return TSLAM_OK;
-}
-
 static int submit(tslam_shard_driver* d, const uint8_t* const* images, int n, void* const* streams) {
-    if (n < d->world || n > d->B || n % d->world)
-        return tslam_internal_fail(TSLAM_EINVAL, "a sharded batch needs world <= n_frames <= max_batch, n_frames % world == 0");
-    geom(d, n);
+    if (n < 1 || n > d->B) return tslam_internal_fail(TSLAM_EINVAL, "a sharded batch needs 1 <= n_frames <= max_batch");
+    RC(setup_gather(d));
+    d->n = n;
+    d->maxr = peer_records(n, d->world);
     const int k = (int)(d->batches & 1), N = d->world, S = d->S;
-    const int front[3] = {TSLAM_STAGE_RECTIFY, TSLAM_STAGE_DETECT, TSLAM_STAGE_DESCRIBE};
-    for (size_t i = 0; i < d->ranks.size(); ++i) {   // inputs, buffer reuse, raw images out
+    const bool prof = (d->flags & TSLAM_SHARD_PROFILE) != 0;
+    for (size_t i = 0; i < d->ranks.size(); ++i) {   // inputs, buffer reuse
         Rank& r = d->ranks[i];
         SHCHK(hipSetDevice(r.device));
         SHCHK(hipEventRecord(r.ev_in, streams ? (hipStream_t)streams[i] : nullptr));
-        for (hipStream_t s : {r.fs, r.xs, r.bs}) SHCHK(hipStreamWaitEvent(s, r.ev_in, 0));
+        for (hipStream_t s : {FS(d, r), XS(d, r), BS(d, r)}) SHCHK(hipStreamWaitEvent(s, r.ev_in, 0));
         if (r.consumed_armed[k])
-            for (hipStream_t s : {r.fs, r.xs}) SHCHK(hipStreamWaitEvent(s, r.consumed[k], 0));
+            for (hipStream_t s : {FS(d, r), XS(d, r)}) SHCHK(hipStreamWaitEvent(s, r.consumed[k], 0));
         RC(tslam_begin_batch(r.h, images[i], n));
-        if (!d->rgbd) RC(stage_raw(d, r, images[i], k));
     }
-    if (!d->rgbd) RC(exchange(d, RAW, k));
-    for (Rank& r : d->ranks) {   // front end of the rank's cameras (+ its stream blocks per peer)
-        for (int st : front) RC(tslam_run_stage(r.h, st, r.fs));
+    if (!d->rgbd && N > 1) RC(exchange(d, RAW, k, images));   // straight from the inputs
+    for (size_t i = 0; i < d->ranks.size(); ++i) {   // this batch's last frame becomes prev_raw (after the sends)
+        Rank& r = d->ranks[i];
         if (d->rgbd) continue;
-        if (N > 1) RC(tslam_pack_streams_peers(r.h, r.feat_send[k], r.fs));   // every peer's frames, one launch
         SHCHK(hipSetDevice(r.device));
-        SHCHK(hipEventRecord(r.ev_front, r.fs));
-        SHCHK(hipStreamWaitEvent(r.xs, r.ev_front, 0));
+        const size_t frame = (size_t)S * d->img;
+        SHCHK(hipMemcpyAsync(r.prev_raw, images[i] + (size_t)(n - 1) * frame, frame, hipMemcpyDeviceToDevice, XS(d, r)));
     }
-    if (!d->rgbd) RC(exchange(d, FEAT, k));
+    for (Rank& r : d->ranks) {   // front end of the rank's cameras (+ its stream blocks per peer)
+        if (prof) {
+            RC(run_timed(d, r, TSLAM_SEG_RECTIFY, TSLAM_KERNEL_RECTIFY_PYRAMID, FS(d, r)));
+            RC(run_timed(d, r, TSLAM_SEG_DETECT, TSLAM_KERNEL_DETECT, FS(d, r)));
+            RC(run_timed(d, r, TSLAM_SEG_SELECT, TSLAM_KERNEL_SELECT, FS(d, r)));
+            RC(run_timed(d, r, TSLAM_SEG_DESCRIBE, TSLAM_KERNEL_DESCRIBE, FS(d, r)));
+        } else {
+            for (int st : {TSLAM_STAGE_RECTIFY, TSLAM_STAGE_DETECT, TSLAM_STAGE_DESCRIBE}) RC(tslam_run_stage(r.h, st, FS(d, r)));
+        }
+        if (d->rgbd) continue;
+        if (N > 1) {
+            RC(span_begin(d, r, TSLAM_SEG_PACK, FS(d, r)));
+            RC(tslam_pack_streams_peers(r.h, r.feat_send[k], FS(d, r)));   // every peer's frames, one launch
+            RC(span_end(d, r, FS(d, r)));
+        }
+        SHCHK(hipSetDevice(r.device));
+        SHCHK(hipEventRecord(r.ev_front, FS(d, r)));
+        SHCHK(hipStreamWaitEvent(XS(d, r), r.ev_front, 0));
+    }
+    if (!d->rgbd && N > 1) RC(exchange(d, FEAT, k, images));
     for (Rank& r : d->ranks) {   // back end
         if (!d->rgbd) {
             // the other cameras of frames lo-1 .. hi-1 of this rank's range into the ring
             SHCHK(hipSetDevice(r.device));
-            SHCHK(hipEventRecord(r.ev_x, r.xs));
-            SHCHK(hipStreamWaitEvent(r.bs, r.ev_x, 0));
-            if (N > 1) RC(tslam_import_peers(r.h, r.raw_recv[k], r.feat_recv[k], r.bs));
-            SHCHK(hipEventRecord(r.consumed[k], r.bs));
+            SHCHK(hipEventRecord(r.ev_x, XS(d, r)));
+            SHCHK(hipStreamWaitEvent(BS(d, r), r.ev_x, 0));
+            if (prof && N > 1) RC(span_between(d, r, TSLAM_SEG_EXCHANGE_WAIT, FS(d, r), BS(d, r)));   // front done -> data landed
+            if (N > 1) {
+                RC(span_begin(d, r, TSLAM_SEG_IMPORT, BS(d, r)));
+                RC(tslam_import_peers(r.h, r.raw_recv[k], r.feat_recv[k], BS(d, r)));
+                RC(span_end(d, r, BS(d, r)));
+            }
+            SHCHK(hipEventRecord(r.consumed[k], BS(d, r)));
             r.consumed_armed[k] = true;
         }
-        RC(tslam_run_stage(r.h, TSLAM_STAGE_MATCH, r.bs));
-        RC(tslam_run_stage(r.h, TSLAM_STAGE_POSE, r.bs));
+        if (prof) {
+            RC(run_timed(d, r, TSLAM_SEG_MATCH, TSLAM_KERNEL_MATCH, BS(d, r)));
+            RC(run_timed(d, r, TSLAM_SEG_MATCH_REFINE, TSLAM_KERNEL_MATCH_REFINE, BS(d, r)));
+            RC(run_timed(d, r, TSLAM_SEG_POSE, TSLAM_KERNEL_POSE, BS(d, r)));
+            if (d->rig && !d->rgbd) RC(run_timed(d, r, TSLAM_SEG_RIG, TSLAM_KERNEL_RIG, BS(d, r)));
+        } else {
+            RC(tslam_run_stage(r.h, TSLAM_STAGE_MATCH, BS(d, r)));
+            RC(tslam_run_stage(r.h, TSLAM_STAGE_POSE, BS(d, r)));
+        }
         if (d->rgbd)   // this rank's cameras over every peer's frame range
-            for (int q = 0; q < N; ++q)
-                if (q != r.rank)
-                    RC(tslam_pack_pairs(r.h, q * d->fpr, d->fpr, r.rank * S, (r.rank + 1) * S,
-                                        r.feat_send[k] + (size_t)q * d->feat_q, r.bs));
+            for (int q = 0; q < N; ++q) {
+                int lo, hi;
+                peer_range(q, n, N, &lo, &hi);
+                if (q != r.rank && hi > lo)
+                    RC(tslam_pack_pairs(r.h, lo, hi - lo, r.rank * S, (r.rank + 1) * S, r.feat_send[k] + (size_t)q * feat_cap(d),
+                                        BS(d, r)));
+            }
     }
     if (d->rgbd) {
-        RC(exchange(d, FEAT, k));
+        if (N > 1) RC(exchange(d, FEAT, k, images));
         for (Rank& r : d->ranks) {
+            int lo, hi;
+            peer_range(r.rank, n, N, &lo, &hi);
             for (int q = 0; q < N; ++q)
-                if (q != r.rank)
-                    RC(tslam_unpack_pairs(r.h, r.rank * d->fpr, d->fpr, q * S, (q + 1) * S,
-                                          r.feat_recv[k] + (size_t)q * d->feat_q, r.bs));
+                if (q != r.rank && hi > lo)
+                    RC(tslam_unpack_pairs(r.h, lo, hi - lo, q * S, (q + 1) * S, r.feat_recv[k] + (size_t)q * feat_cap(d), BS(d, r)));
             SHCHK(hipSetDevice(r.device));
-            SHCHK(hipEventRecord(r.consumed[k], r.bs));
+            SHCHK(hipEventRecord(r.consumed[k], BS(d, r)));
             r.consumed_armed[k] = true;
-            if (d->rig) RC(tslam_run_stage(r.h, TSLAM_KERNEL_RIG, r.bs));
+            if (d->rig) RC(run_timed(d, r, TSLAM_SEG_RIG, TSLAM_KERNEL_RIG, BS(d, r)));
         }
     }
-    for (Rank& r : d->ranks) RC(tslam_pack_poses(r.h, r.pose_send[k], r.bs));
-    RC(exchange(d, POSE, k));
+    if (d->gather()) {   // every rank's share of the pairs' state into rank 0's ring
+        for (Rank& r : d->ranks) {
+            if (r.rank == 0) continue;
+            RC(span_begin(d, r, TSLAM_SEG_STATE, BS(d, r)));
+            RC(tslam_internal_state_blocks(r.h, 1, r.rank, r.rank * S, (r.rank + 1) * S, r.state_buf[k], BS(d, r)));
+            RC(span_end(d, r, BS(d, r)));
+        }
+        RC(exchange(d, STATE, k, images));
+        for (Rank& r : d->ranks) {
+            if (r.rank != 0) continue;
+            RC(span_begin(d, r, TSLAM_SEG_STATE, BS(d, r)));
+            for (int q = 1; q < N; ++q)
+                RC(tslam_internal_state_blocks(r.h, 0, q, q * S, (q + 1) * S, r.state_buf[k] + (size_t)q * d->state_cap, BS(d, r)));
+            RC(span_end(d, r, BS(d, r)));
+        }
+    }
+    for (Rank& r : d->ranks) {
+        RC(tslam_pack_poses(r.h, r.pose_send[k], BS(d, r)));
+        RC(span_begin(d, r, TSLAM_SEG_POSE_GATHER, BS(d, r)));
+    }
+    RC(exchange(d, POSE, k, images));
     for (size_t i = 0; i < d->ranks.size(); ++i) {
         Rank& r = d->ranks[i];
-        RC(tslam_unpack_poses(r.h, r.pose_recv[k], r.bs));
-        RC(tslam_run_stage(r.h, TSLAM_KERNEL_CHAIN, r.bs));
+        RC(span_end(d, r, BS(d, r)));
+        RC(tslam_unpack_poses(r.h, r.pose_recv[k], BS(d, r)));
+        RC(run_timed(d, r, TSLAM_SEG_CHAIN, TSLAM_KERNEL_CHAIN, BS(d, r)));
+        // local BA on rank 0 once its ring holds every pair (the back stream keeps it ordered before
+        // the next batch's imports; tslam_run_stage orders it after the next-but-one front end)
+        if (d->ba && (r.rank == 0 || N == 1) && (d->gather() || N == 1))
+            RC(run_timed(d, r, TSLAM_SEG_BA, TSLAM_STAGE_BA, BS(d, r)));
+        if (d->flags & TSLAM_SHARD_RESULTS) RC(tslam_internal_stash(r.h, BS(d, r)));
         RC(tslam_end_batch(r.h));
         SHCHK(hipSetDevice(r.device));
-        SHCHK(hipEventRecord(r.ev_done, r.bs));
+        SHCHK(hipEventRecord(r.ev_done, BS(d, r)));
         r.done_armed = true;
         // the caller's stream orders after the batch (results in stream order)
         SHCHK(hipStreamWaitEvent(streams ? (hipStream_t)streams[i] : nullptr, r.ev_done, 0));
+        if (prof) r.timed_batches += 1;
     }
     d->batches += 1;
     return TSLAM_OK;
+}
+
+// Sum the finished spans into the per-segment totals (synchronises the rank's device).
+static int collect(Rank& r) {
+    if (r.spans.empty()) return TSLAM_OK;
+    SHCHK(hipSetDevice(r.device));
+    SHCHK(hipDeviceSynchronize());
+    for (const Span& sp : r.spans) {
+        float ms = 0.0f;
+        SHCHK(hipEventElapsedTime(&ms, sp.a, sp.b));
+        r.seg_us[sp.seg] += 1e3 * (double)ms;
+    }
+    r.spans.clear();
+    r.ev_used = 0;
+    return TSLAM_OK;
+}
+
+static Rank* rank_of(tslam_shard_driver* d, tslam_handle* h) {
+    for (Rank& r : d->ranks)
+        if (r.h == h) return &r;
+    return nullptr;
 }
 
 extern "C" {
@@ -351,7 +577,7 @@ int tslam_comm_init(tslam_handle* h, const void* id128, int rank, int world) {
         ncclUniqueId id;
         memcpy(&id, id128, sizeof(id));
         ncclResult_t nr = ncclCommInitRank(&r.comm_x, world, id, rank);
-        // the pose all-gather's own communicator (same ranks)
+        // the pose all-gather's (and the state gather's) own communicator (same ranks)
         if (nr == ncclSuccess) nr = ncclCommSplit(r.comm_x, 0, rank, &r.comm_p, nullptr);
         if (nr != ncclSuccess) rc = tslam_internal_fail(TSLAM_EHIP, (std::string("RCCL communicator: ") + ncclGetErrorString(nr)).c_str());
     }
@@ -363,12 +589,54 @@ int tslam_comm_init(tslam_handle* h, const void* id128, int rank, int world) {
     return rc;
 }
 
-int tslam_submit_sharded(tslam_handle* h, const uint8_t* images, void* stream) {
+int tslam_submit_sharded(tslam_handle* h, const uint8_t* images, int n_frames, void* stream) {
     if (!h || !images) return tslam_internal_fail(TSLAM_EINVAL, "bad argument");
     tslam_shard_driver* d = tslam_internal_driver(h);
     if (!d || d->ranks.size() != 1) return tslam_internal_fail(TSLAM_ESTATE, "tslam_comm_init first");
     void* streams[1] = {stream};
-    return submit(d, &images, d->B, streams);
+    return submit(d, &images, n_frames, streams);
+}
+
+int tslam_shard_options(tslam_handle* h, int flags) {
+    if (!h) return tslam_internal_fail(TSLAM_EINVAL, "null handle");
+    tslam_shard_driver* d = tslam_internal_driver(h);
+    if (!d) return tslam_internal_fail(TSLAM_ESTATE, "the handle is not driven (tslam_comm_init / tslam_group_create)");
+    if (flags & ~(TSLAM_SHARD_GATHER | TSLAM_SHARD_RESULTS | TSLAM_SHARD_PROFILE | TSLAM_SHARD_SERIAL))
+        return tslam_internal_fail(TSLAM_EINVAL, "unknown TSLAM_SHARD_* flag");
+    if ((flags & TSLAM_SHARD_GATHER) && d->rgbd)
+        return tslam_internal_fail(TSLAM_EINVAL, "the state gather describes a stereo rig");
+    // the streams may change (TSLAM_SHARD_SERIAL): everything enqueued so far finishes first
+    for (Rank& r : d->ranks) {
+        SHCHK(hipSetDevice(r.device));
+        SHCHK(hipDeviceSynchronize());
+    }
+    if (flags & TSLAM_SHARD_SERIAL)
+        for (size_t i = 0; i < d->ranks.size(); ++i) {
+            Rank& r = d->ranks[i];
+            if (r.serial) continue;
+            for (size_t j = 0; j < i && !r.serial; ++j)
+                if (d->ranks[j].device == r.device) r.serial = d->ranks[j].serial;
+            if (!r.serial) {
+                SHCHK(hipSetDevice(r.device));
+                SHCHK(hipStreamCreateWithFlags(&r.serial, hipStreamNonBlocking));
+                r.serial_owner = true;
+            }
+        }
+    d->flags = flags;
+    return TSLAM_OK;
+}
+
+int tslam_shard_timing(tslam_handle* h, double* out_us, int n_out) {
+    if (!h || !out_us || n_out < 1) return tslam_internal_fail(TSLAM_EINVAL, "bad argument");
+    tslam_shard_driver* d = tslam_internal_driver(h);
+    Rank* r = d ? rank_of(d, h) : nullptr;
+    if (!r) return tslam_internal_fail(TSLAM_ESTATE, "the handle is not driven (tslam_comm_init / tslam_group_create)");
+    RC(collect(*r));
+    const int64_t nb = r->timed_batches;
+    for (int i = 0; i < std::min(n_out, (int)TSLAM_SEG_COUNT); ++i) out_us[i] = nb ? r->seg_us[i] / (double)nb : 0.0;
+    for (double& v : r->seg_us) v = 0.0;
+    r->timed_batches = 0;
+    return (int)nb;
 }
 
 struct tslam_group {
@@ -387,7 +655,7 @@ int tslam_group_create(tslam_handle* const* handles, int n, int transport, tslam
         if (!handles[i]) return tslam_internal_fail(TSLAM_EINVAL, "null handle");
         RC(tslam_internal_info(handles[i], &in));
         if (in.C != in0.C || in.P != in0.P || in.B != in0.B || in.W != in0.W || in.H != in0.H || in.rgbd != in0.rgbd ||
-            in.rig != in0.rig)
+            in.rig != in0.rig || in.ba != in0.ba)
             return tslam_internal_fail(TSLAM_EINVAL, "a group's handles must describe the same rig and batch");
         if (tslam_internal_driver(handles[i])) return tslam_internal_fail(TSLAM_ESTATE, "handle already driven");
         devs[i] = in.device;

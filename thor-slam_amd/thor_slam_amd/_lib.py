@@ -32,6 +32,10 @@ KERNELS = {
 }
 RIG_KERNEL = 18   # rig pose (+ chain; sharded: the range's rig pose only)
 TRANSPORT = {"rccl": 0, "copy": 1}   # tslam_group_create
+SHARD_GATHER, SHARD_RESULTS, SHARD_PROFILE, SHARD_SERIAL = 1, 2, 4, 8   # tslam_shard_options
+# tslam_shard_timing segments (enum tslam_segment), in order
+SHARD_SEGMENTS = ("rectify_pyramid", "detect", "select", "describe", "pack", "exchange_wait", "import", "match",
+                  "match_refine", "pose", "rig", "state", "pose_gather", "chain", "local_ba")
 POSE_OK, POSE_LOST, POSE_INIT = 0, 1, 2
 
 
@@ -125,7 +129,9 @@ _SIGNATURES = {
     "tslam_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "tslam_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "tslam_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
-    "tslam_submit_sharded": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tslam_submit_sharded": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "tslam_shard_options": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "tslam_shard_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "tslam_create_rig": (ctypes.c_int, [ctypes.POINTER(CameraDesc), ctypes.c_int, ctypes.POINTER(Params), ctypes.c_int,
                                          ctypes.POINTER(ctypes.c_void_p)]),
     "tslam_rig_pairs": (ctypes.c_int, [ctypes.POINTER(CameraDesc), ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
@@ -514,9 +520,26 @@ class Handle:
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
         _check(self.lib.tslam_comm_init(self.h, buf, int(rank), int(world)))
 
-    def submit_sharded(self, images_dev_ptr: int, stream: int = 0) -> None:
-        """``tslam_submit_sharded``: one batch of this rank's cameras, exchanges over RCCL."""
-        _check(self.lib.tslam_submit_sharded(self.h, ctypes.c_void_p(images_dev_ptr), ctypes.c_void_p(stream)))
+    def submit_sharded(self, images_dev_ptr: int, n_frames: int | None = None, stream: int = 0) -> None:
+        """``tslam_submit_sharded``: one batch (default max_batch frames) of this rank's cameras,
+        exchanges over RCCL."""
+        n = self.max_batch if n_frames is None else int(n_frames)
+        _check(self.lib.tslam_submit_sharded(self.h, ctypes.c_void_p(images_dev_ptr), n, ctypes.c_void_p(stream)))
+
+    def shard_options(self, gather: bool = False, results: bool = False, profile: bool = False,
+                      serial: bool = False) -> None:
+        """``tslam_shard_options`` of the driver behind this (sharded) handle."""
+        flags = ((SHARD_GATHER if gather else 0) | (SHARD_RESULTS if results else 0) | (SHARD_PROFILE if profile else 0)
+                 | (SHARD_SERIAL if serial else 0))
+        _check(self.lib.tslam_shard_options(self.h, flags))
+
+    def shard_timing(self) -> tuple[dict, int]:
+        """``tslam_shard_timing``: average µs per batch of every segment of this rank (since the
+        last call; synchronises) and the number of batches."""
+        out = (ctypes.c_double * len(SHARD_SEGMENTS))()
+        nb = self.lib.tslam_shard_timing(self.h, out, len(SHARD_SEGMENTS))
+        _check(min(nb, 0))
+        return {k: float(v) for k, v in zip(SHARD_SEGMENTS, out)}, int(nb)
 
     def set_shard(self, cam_lo: int, cam_hi: int, rank: int, world: int) -> None:
         _check(self.lib.tslam_set_shard(self.h, int(cam_lo), int(cam_hi), int(rank), int(world)))

@@ -30,9 +30,11 @@ volume on the device with the batch's tracked poses (nvblox's role in the refere
 With ``HipSlamConfig(devices=[d0, d1, ...])`` the rig is sharded one camera stream per GPU from
 this one process (cuVSLAM's multicam mode, launch/thor_visual_slam.launch.py:49,81):
 one handle per device, driven by the library as one sharded rig (``tslam_group_*``: an RCCL clique
-over the devices, or device copies with ``shard_transport="copy"``); the published poses are
-bit-identical to the one-device engine's.  Frames are submitted in multiples of the device count
-(a trailing remainder waits for the next ``process_frames``); loop closure is not run sharded.
+over the devices, or device copies with ``shard_transport="copy"``).  It has the one-device engine's
+features: batches of any length (a short last batch at ``flush``), asynchronous submission (the
+driver's pinned result slots, polled like ``tslam_submit_host``'s), and — through the driver's
+state gather to rank 0 (``TSLAM_SHARD_GATHER``) — local BA (solved by rank 0), loop closure and
+relocalisation on rank 0's handle; the published poses are bit-identical to the one-device engine's.
 ``confidence`` follows isaac_ros.py:312.  With ``batch_size > 1`` frames are staged and the
 batch runs on the GPU when full (or on ``flush``).  Submission is asynchronous
 (``tslam_submit_host``: pinned double-buffered staging, the batch's H2D copy and kernels on the
@@ -217,9 +219,7 @@ class HipSlamEngine(SlamEngine):
                                        cfg.tsdf_integrator_truncation_distance_vox,
                                        cfg.tsdf_integrator_max_integration_distance_m, cfg.tsdf_max_weight)
             self._loop = None
-            if cfg.enable_loop_closure and self._shard is not None:
-                logger.warning("loop closure is not run on a sharded rig (devices=%s)", cfg.devices)
-            elif cfg.enable_loop_closure:
+            if cfg.enable_loop_closure:
                 # place recognition over every pair's camera (P database entries per keyframe,
                 # keyframe-major) and verification on the pair that voted best; the keyframe nodes
                 # are pair 0's rectified-left poses (on a multi-pair rig taken from the rig's body
@@ -238,8 +238,12 @@ class HipSlamEngine(SlamEngine):
 
     def _init_shard(self, shape: tuple) -> None:
         """One handle per device (the whole rig on each, rank r owning cameras [r*S, (r+1)*S)) and
-        the library's group driver over them; pinned staging + device input per rank."""
+        the library's group driver over them, with the state gather to rank 0 (local BA, loop
+        closure and relocalisation run on rank 0's handle) and pinned result slots (asynchronous
+        polling); pinned staging + device input per rank and batch parity."""
         torch, cfg = self._torch, self._config
+        if cfg.dense_map:
+            raise RuntimeError("the dense map runs on one device (devices=[] with dense_map)")
         devs = [int(d) for d in cfg.devices]
         world = len(devs)
         n_cams = shape[1]
@@ -253,37 +257,49 @@ class HipSlamEngine(SlamEngine):
                            for (l, _), r in zip(self._pairs, self._rects)])
             handles.append(h)
         group = HandleGroup(handles, cfg.shard_transport)
+        handles[0].shard_options(gather=True, results=True)
         S = n_cams // world
         part = (cfg.batch_size, S) + tuple(shape[2:])
-        self._shard = {"handles": handles, "group": group, "world": world, "S": S, "devices": devs,
-                       "dev": [torch.empty(part, dtype=torch.uint8, device=f"cuda:{d}") for d in devs],
-                       "host": [torch.empty(part, dtype=torch.uint8).pin_memory() for _ in devs]}
-        self._handle = handles[0]   # every rank ends a batch with the whole rig's poses
+        self._shard = {"handles": handles, "group": group, "world": world, "S": S, "devices": devs, "batches": 0,
+                       "dev": [[torch.empty(part, dtype=torch.uint8, device=f"cuda:{d}") for _ in range(2)] for d in devs],
+                       "host": [[torch.empty(part, dtype=torch.uint8).pin_memory() for _ in range(2)] for _ in devs],
+                       "h2d": [[None, None] for _ in devs]}
+        self._handle = handles[0]   # every rank ends a batch with the whole rig's poses; rank 0 has the rest
 
     def _submit_sharded(self) -> None:
-        """The staged frames in multiples of the device count through the group driver (rank r
-        gets its cameras' slice), then the batch's poses from rank 0; synchronous."""
+        """The staged frames (any count up to batch_size) through the group driver, rank r getting
+        its cameras' slice; the batch's results are polled from rank 0's pinned slots."""
         sh, torch = self._shard, self._torch
-        n = len(self._staged) - len(self._staged) % sh["world"]
-        if n == 0:
-            return
-        batch, imus = self._staged[:n], self._staged_imu[:n]
+        n = len(self._staged)
+        batch, imus = self._staged, self._staged_imu
         stamps = [ts for _, ts in batch]
         if self._imu is not None:
             self._set_imu_prior(stamps, imus)
+        k = sh["batches"] & 1
         S, ptrs, streams = sh["S"], [], []
         for r, d in enumerate(sh["devices"]):
-            host = sh["host"][r].numpy()
-            for k, (imgs, _) in enumerate(batch):
-                host[k] = imgs[r * S:(r + 1) * S]
+            if sh["h2d"][r][k] is not None:   # the pinned buffer of this parity: batch s-2's copy is done
+                sh["h2d"][r][k].synchronize()
+            host = sh["host"][r][k].numpy()
+            for i, (imgs, _) in enumerate(batch):
+                host[i] = imgs[r * S:(r + 1) * S]
             stream = torch.cuda.current_stream(d)
-            sh["dev"][r][:n].copy_(sh["host"][r][:n], non_blocking=True)
-            ptrs.append(sh["dev"][r].data_ptr())
+            # the device input of this parity: the driver made this stream wait for batch s-2
+            sh["dev"][r][k][:n].copy_(sh["host"][r][k][:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            sh["h2d"][r][k] = ev
+            ptrs.append(sh["dev"][r][k].data_ptr())
             streams.append(stream.cuda_stream)
+        if self._in_flight >= 2:   # rank 0 keeps two batches' results: publish the older first
+            self._drain(block=True, limit=1)
         sh["group"].submit(ptrs, n, streams)
-        self._staged, self._staged_imu = self._staged[n:], self._staged_imu[n:]
+        sh["batches"] += 1
+        self._in_flight += 1
+        self._staged, self._staged_imu = [], []
         self._prev_stamp = stamps[-1]
-        self._publish(self._read(n), stamps, self._handle.frames_done - n)
+        if not self._async:
+            self._drain(block=True)
 
     # ------------------------------------------------------------------------------------------
     def _frame_images(self, frame_set: SynchronizedFrameSet) -> np.ndarray | None:
@@ -452,7 +468,7 @@ class HipSlamEngine(SlamEngine):
         summed rotation variances (1 / rad^2: the reprojection residuals have unit pixel weight)
         go to tslam_ba_imu_factor before the batch is submitted."""
         cfg = self._config
-        if cfg.ba_window <= 0 or len(self._pairs) != 1 or self._shard is not None:
+        if cfg.ba_window <= 0 or len(self._pairs) != 1:
             return
         g = self._handle.frames_done
         for k, st in enumerate(steps):
@@ -858,7 +874,7 @@ class HipSlamEngine(SlamEngine):
         the device); on success the published poses continue in the map's world frame."""
         if self._handle is None:
             raise RuntimeError("Not initialized")
-        if not self._map_loaded or self._handle.frames_done == 0 or self._shard is not None:
+        if not self._map_loaded or self._handle.frames_done == 0:
             return False
         self.flush()
         res = self._handle.relocalize(self._handle.frames_done - 1)
@@ -899,10 +915,12 @@ class HipSlamEngine(SlamEngine):
         self._frame_count = 0
 
     def shutdown(self) -> None:
+        if self._handle is not None and (self._staged or self._in_flight):
+            try:   # the tail of the stream: staged frames run as a short last batch and are published
+                self.flush()
+            except RuntimeError as exc:
+                logger.warning("shutdown: the last %d staged frame(s) were not tracked: %s", len(self._staged), exc)
         if self._shard is not None:
-            if self._staged:
-                logger.warning("shutdown: %d staged frame(s) short of a multiple of %d devices were not tracked",
-                               len(self._staged), self._shard["world"])
             self._shard["group"].close()
             for h in self._shard["handles"]:
                 h.close()

@@ -1,13 +1,15 @@
-"""The sharded rig's phases in the one-process rehearsal (profiling aid, not the bench).
+"""The sharded rig's per-rank work in a one-GPU rehearsal of the library driver (profiling aid).
 
-    python tools/shard_probe.py [--world 8] [--batch 256] [--names 4]
+    python tools/shard_probe.py [--world 8] [--batch 256] [--names 4] [--steps 4] [--one-gpu]
 
-All ranks of a LocalShardedRig on this GPU, one stream: every phase of every rank timed with HIP
-events (kernels by name, raw staging, stream-block packing, the device copies standing in for the
-RCCL all-to-all and all-gather, the imports that rectify the remote raw images).  Prints per-step
-microseconds summed over the ranks and per rank, the bytes one rank sends per step, and the
-per-GPU compute of an N-GPU run (the sum of one rank's phases without the copies), which bounds
-the N-GPU step from below when the exchange is hidden.
+All `world` ranks of a tslam_group (copy transport) on this GPU with TSLAM_SHARD_SERIAL |
+TSLAM_SHARD_PROFILE: every kernel and copy of every rank runs alone on one stream and is timed
+with HIP events by the driver itself (tslam_shard_timing: rectify .. describe, stream-block pack,
+import of the peers' raw images + stream blocks, match .. rig pose, the pose all-gather, the
+chain).  Prints per rank the µs per step of each segment and its per-GPU compute (the segments
+without the device copies standing in for RCCL) — the N-GPU step when the exchange is hidden —
+the bytes one rank sends per step, and (--one-gpu) the one-GPU step of the same rig and batch
+through the pipelined single handle for the ratio.
 """
 
 from __future__ import annotations
@@ -15,11 +17,14 @@ from __future__ import annotations
 import argparse
 import json
 import sys
+import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 for p in (ROOT, ROOT / "thor-slam_amd"):
     sys.path.insert(0, str(p))
+
+EXCHANGE = ("exchange_wait", "pose_gather")   # device copies standing in for RCCL (and waits)
 
 
 def main() -> None:
@@ -28,38 +33,70 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--names", type=int, default=4, help="stereo sources of the bracket rig (2 streams each)")
     ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--one-gpu", action="store_true", help="also time the one-GPU pipelined step (bench run_single)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     import torch
 
     from bench import RIG_SOURCES, render_rig_frames, rig_setup, triangle_indices
+    from thor_slam_amd._lib import Handle, HandleGroup
     from thor_slam_amd.params import HipSlamConfig
-    from thor_slam_amd.shard import LocalShardedRig, StageTimer
 
     names = RIG_SOURCES[:args.names]
     _, cams, pairs, rects, E = rig_setup(names)
-    C, B = 2 * len(rects), args.batch
+    C, B, W = 2 * len(rects), args.batch, args.world
+    S = C // W
+    cfg = HipSlamConfig()
     uniq = render_rig_frames(names, 24, 0, C, 8)
     seq = torch.from_numpy(uniq[triangle_indices((args.steps + 1) * B, 24)]).cuda()
-    rig = LocalShardedRig(rects, HipSlamConfig(), world=args.world, batch=B, base_T_rect=E if len(rects) > 1 else None)
-    st = torch.cuda.current_stream()
-    rig.step(seq[:B], st)   # warm-up
-    timer = StageTimer()
-    timer.stream = st
-    for s in range(1, args.steps + 1):
-        rig.step(seq[s * B:(s + 1) * B], st, timer)
+    parts = [seq[:, r * S:(r + 1) * S].contiguous() for r in range(W)]
+    hs = [Handle(rects, cfg, max_batch=B) for _ in range(W)]
+    for h in hs:
+        if len(rects) > 1:
+            h.set_rig(E)
+    grp = HandleGroup(hs, "copy")
+    hs[0].shard_options(serial=True)
+    grp.submit([p[0].data_ptr() for p in parts], B)   # warm-up
     torch.cuda.synchronize()
-    tot = {k: sum(a.elapsed_time(b) for a, b in v) * 1e3 / args.steps for k, v in timer.spans.items()}
-    W = args.world
-    per_rank = {k: v / W for k, v in tot.items()}
-    rk = rig.ranks[0]
-    S, fr = rig.plan.streams_per_rank, rig.plan.recv_frames
-    sent = {"raw_images": (W - 1) * fr * S * rk.img_bytes, "stream_blocks": (W - 1) * fr * S * rk.block,
-            "pose_records": rig.plan.frames_per_rank * rk.record}
-    compute = sum(v for k, v in per_rank.items() if k not in ("exchange", "pose_gather"))
-    out = {"world": W, "batch": B, "streams": C, "stereo_pairs": len(rects), "us_per_step_all_ranks": tot,
-           "us_per_step_per_rank": per_rank, "per_gpu_compute_us": compute,
-           "bytes_sent_per_rank_per_step": sent, "bytes_sent_total": sum(sent.values())}
+    hs[0].shard_options(serial=True, profile=True)
+    for s in range(1, args.steps + 1):
+        grp.submit([p[s * B].data_ptr() for p in parts], B)
+    torch.cuda.synchronize()
+    per_rank = [h.shard_timing()[0] for h in hs]
+    compute = [sum(v for k, v in t.items() if k not in EXCHANGE) for t in per_rank]
+    sb, pr = hs[0].exchange_sizes()
+    fr = B // W + 1   # frames a rank reads of each peer's cameras
+    sent = {"raw_images": (W - 1) * fr * S * 640 * 400, "stream_blocks": (W - 1) * fr * S * sb,
+            "pose_records": (B // W) * pr}
+    grp.close()
+    for h in hs:
+        h.close()
+    out = {"world": W, "batch": B, "streams": C, "stereo_pairs": len(rects), "driver": "library (copy, serial)",
+           "us_per_step_per_rank": per_rank, "per_gpu_compute_us": max(compute),
+           "per_gpu_compute_us_by_rank": compute, "bytes_sent_per_rank_per_step": sent}
+    if args.one_gpu:
+        h = Handle(rects, cfg, max_batch=B)
+        if len(rects) > 1:
+            h.set_rig(E)
+        fs, bs = torch.cuda.Stream(priority=-1), torch.cuda.Stream()
+
+        def step(s):
+            h.begin_batch(seq[s * B].data_ptr(), B)
+            for st in ("rectify", "detect", "describe"):
+                h.run_stage(st, fs.cuda_stream)
+            for st in ("match", "pose"):
+                h.run_stage(st, bs.cuda_stream)
+            h.end_batch()
+
+        step(0)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s in range(1, args.steps + 1):
+            step(s)
+        torch.cuda.synchronize()
+        out["one_gpu_step_us"] = (time.perf_counter() - t0) / args.steps * 1e6
+        out["ratio_one_gpu_over_per_gpu"] = out["one_gpu_step_us"] / out["per_gpu_compute_us"]
+        h.close()
     line = json.dumps(out)
     print(line)
     if args.out:
