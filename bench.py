@@ -632,9 +632,11 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
         else:
             h.run_kernel(k, st.cuda_stream)
 
-    def step(s: int, evs=None) -> None:
+    def step(s: int, evs=None, outliers: int = 0) -> None:
         # one batch = every kernel of the hot path; in the timed steps each kernel is bracketed by
-        # a pair of HIP events on the stream it runs on (the per-kernel durations below)
+        # a pair of HIP events on the stream it runs on (the per-kernel durations below).
+        # `outliers` > 0: that percentage of the refined temporal positions is moved 8-40 px before
+        # the pose kernels (tslam_perturb_temporal, a benchmark hook) — RANSAC on hard data
         h.begin_batch(seq[step_base(s)].data_ptr(), B)
         # the waits the library would insert, made here so the events time kernels, not waits
         if c4 and ba_issued[s % 2]:
@@ -659,7 +661,9 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
             if k in BACK and first_back and bstream is not stream:
                 bstream.wait_stream(stream)
                 first_back = False
-            timed = evs is not None and (timed_all or k in timed_set)
+            timed = evs is not None and (timed_all or k in timed_set or (outliers and k == "pose"))
+            if outliers and k == "pose":
+                h.perturb_temporal(outliers, seed=s, stream=st.cuda_stream)
             if timed:
                 evs[i][0].record(st)
             run(k, st)
@@ -723,6 +727,55 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
         torch.cuda.synchronize()
         for k, e0, e1 in prs:
             iso_us[k] += e0.elapsed_time(e1) * 1e3 / n_iso
+
+    # ---- the pose stage on hard data: the same pipelined steps with
+    # --outliers % of every frame's refined temporal positions made outliers before the pose
+    # kernels, so the bounded RANSAC scoring cannot end at the first correct root
+    pose_outliers = None
+    if args.outliers > 0 and args.outlier_steps > 0 and not (c4 or c5):
+        ev_o = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in names]
+                for _ in range(args.outlier_steps)]
+        base_s = args.warmup + args.steps
+        step(base_s, outliers=args.outliers)   # warm-up (the learnt FAST threshold is unaffected)
+        torch.cuda.synchronize()
+        t_o = time.perf_counter()
+        for k in range(args.outlier_steps):
+            step(base_s + 1 + k, ev_o[k], outliers=args.outliers)
+        torch.cuda.synchronize()
+        el_o = time.perf_counter() - t_o
+        res_o = h.read_poses(B)
+        st_o = res_o["stats"][:, :, :]
+        ip = names.index("pose")
+        pose_pipe = sum(e[ip][0].elapsed_time(e[ip][1]) for e in ev_o) * 1e3 / args.outlier_steps
+        # the pose kernels alone on one stream, on a perturbed batch (3 batches)
+        iso_o = 0.0
+        for r in range(3):
+            h.begin_batch(seq[step_base(r)].data_ptr(), B)
+            for k in kern:
+                if k == "pose":
+                    h.perturb_temporal(args.outliers, seed=1000 + r, stream=sp)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    run(k, stream)
+                    e1.record(stream)
+                elif k not in ("rig", "chain"):
+                    run(k, stream)
+            h.end_batch()
+            torch.cuda.synchronize()
+            iso_o += e0.elapsed_time(e1) * 1e3 / 3
+        ok_o = st_o[:, :, 0] == 0
+        inl = np.where(ok_o, st_o[:, :, 2] / np.maximum(st_o[:, :, 1], 1), np.nan)
+        pose_outliers = {
+            "outlier_pct": args.outliers, "steps": args.outlier_steps,
+            "ms_per_step": el_o / args.outlier_steps * 1e3,
+            "frames_per_s": args.outlier_steps * B / el_o,
+            "pose_us_pipelined": pose_pipe, "pose_us_isolated": iso_o,
+            "clean_pose_us_isolated": iso_us["pose"],
+            "tracking_ok_fraction_last_batch": float(np.mean(ok_o)),
+            "inlier_fraction_mean": float(np.nanmean(inl)) if np.isfinite(inl).any() else None,
+            "method": "tslam_perturb_temporal (benchmark hook) between match_refine and pose: that share of every "
+                      "frame's refined temporal positions moved 8-40 px per axis; same pipelined steps and kernels",
+        }
 
     # ---- per-kernel durations of the timed launches (HIP events on the launch stream) ----------
     per_kernel_us = {}
@@ -841,6 +894,7 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
         },
         "roofline": roofline,
         "latency_b1_ms": lat_ms,
+        "pose_with_outliers": pose_outliers,
         "per_kernel_us_per_batch": per_kernel_us,
         "per_kernel_us_isolated": iso_us,
         "tracking_ok_fraction_last_batch": ok_frac,
@@ -1147,6 +1201,10 @@ def main() -> None:
     ap.add_argument("--boundary-frames", type=int, default=1024,
                     help="c2: frames timed through HipSlamEngine.process_frames (0 = skip)")
     ap.add_argument("--out", type=str, default="", help="also write the JSON line to this file")
+    ap.add_argument("--outliers", type=int, default=35,
+                    help="c2/c3: also time --outlier-steps pipelined steps with this %% of the refined temporal "
+                         "positions made outliers before the pose kernels (pose_with_outliers; 0 = skip)")
+    ap.add_argument("--outlier-steps", type=int, default=5)
     ap.add_argument("--dist-backend", type=str, default="nccl", help="nccl (RCCL) or gloo (rehearsal, host copy)")
     ap.add_argument("--exchange", choices=["alltoall", "allgather"], default="alltoall",
                     help="--driver torch: all-to-all of the frames each rank solves, or all-gather of everything")

@@ -163,6 +163,11 @@ enum tslam_stage {
                                        KERNEL_CHAIN */
 };
 
+/* Benchmark hook, never on the tracking path: inside a batch, after MATCH_REFINE, move `percent` %
+ * of the batch's refined temporal positions (per frame, pair, keypoint by a hash of `seed`) by
+ * 8..40 px per axis — outliers to every pose — so the pose stage can be timed on hard data. */
+int tslam_perturb_temporal(tslam_handle* h, int percent, uint64_t seed, void* stream);
+
 const char* tslam_last_error(void);
 int tslam_abi_version(void);
 
@@ -516,6 +521,13 @@ int tslam_ba_read_map(tslam_handle* h, int pair, int64_t* gid, uint32_t* desc);
  * tslam_read_poses (status 0 = relocalised); cam_T_world = identity when it fails. */
 int tslam_map_upload(tslam_handle* h, const double* xyz, const uint32_t* desc, int64_t n);
 int tslam_relocalize(tslam_handle* h, int pair, int64_t frame, double* cam_T_world, double* cov, int32_t* stats);
+/* Relocalisation of a whole rig (tslam_set_rig; map uploaded in the rig's base / world frame):
+ * every pair matches its left image of `frame` against the map, A7 solves each pair on the map
+ * points seen in its frame (E_p^-1 X), and the rig pose (candidates from every pair, scored on all
+ * pairs, joint Gauss-Newton) gives body_T_world[16] (+ cov[36] in the body frame, stats[8] as the
+ * rig's; pair_stats[P][8] per pair).  A map seen by any one pair relocalises the rig. */
+int tslam_relocalize_rig(tslam_handle* h, int64_t frame, double* body_T_world, double* cov, int32_t* stats,
+                         int32_t* pair_stats);
 
 /* Loop closure + keyframe pose graph (the reference only forwards
  * SlamConfig.enable_loop_closure, thor_slam/slam/interface.py:155-156, to cuVSLAM).  Spec and CPU

@@ -124,3 +124,61 @@ def test_engine_save_load_relocalize(tmp_path):
         assert np.linalg.norm(p.position - poses1[k].position) < 0.02, k
     assert eng2.load_map(str(tmp_path / "missing.npz")) is False
     eng2.shutdown()
+
+
+def test_rig_relocalisation_from_a_map_seen_by_pair_1():
+    """tslam_relocalize_rig on the two-source bracket rig: the map holds only pair 1's stereo
+    landmarks of frame 0 (base frame), so pair 0 cannot pose itself — the rig still relocalises from
+    pair 1's view through the rig pose.  Against oracle/numpy_map.relocalize_rig: every pair's
+    status, matches, RANSAC winner and inliers and the rig's winner / inliers identical, body_T_world
+    within 1e-9; and it equals the ground-truth body motion to 2 cm."""
+    import torch
+
+    from helpers import rig_scene
+    from oracle import numpy_slam as O
+    from oracle.numpy_map import relocalize_rig
+    from thor_slam_amd._lib import Handle
+    from thor_slam_amd.params import HipSlamConfig
+
+    names = ("192.168.2.21", "192.168.2.25")
+    n = 3
+    sc = rig_scene(names, n)
+    cfg = HipSlamConfig()
+    rects, E = sc["rects"], sc["E"]
+    trk = [O.OracleTracker(cfg, dict(fx=r.fx, fy=r.fy, cx=r.cx, cy=r.cy, baseline=r.baseline, map_l=r.map_left,
+                                     map_r=r.map_right)) for r in rects]
+    ora = [[trk[p].step(sc["frames"][f, 2 * p], sc["frames"][f, 2 * p + 1]) for p in range(len(rects))] for f in range(n)]
+    # the map: pair 1's left keypoints of frame 0 with a disparity, in the base frame of frame 0
+    r1, cur = rects[1], ora[0][1]["cur"]
+    left, disp = cur["left"], cur["disp"]
+    ok = left["valid"] & np.isfinite(disp) & (disp > 0)
+    u, v = O.level0_coords(left["kp"]["x"][ok], left["kp"]["y"][ok], left["kp"]["level"][ok])
+    z = r1.fx * r1.baseline / disp[ok]
+    cam = np.stack([(u - r1.cx) * z / r1.fx, (v - r1.cy) * z / r1.fy, z, np.ones_like(z)])
+    xyz = (np.asarray(E[1]) @ cam)[:3].T.copy()
+    desc = left["desc"][ok].astype(np.uint32)
+    assert xyz.shape[0] > 200
+    h = Handle(rects, cfg, max_batch=n)
+    h.set_rig(E)
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    h.submit(dev.data_ptr(), n, torch.cuda.current_stream().cuda_stream)
+    h.map_upload(xyz, desc)
+    g = n - 1
+    got = h.relocalize_rig(g)
+    h.close()
+    intrs = [(r.fx, r.fy, r.cx, r.cy) for r in rects]
+    want = relocalize_rig([ora[g][p]["cur"]["left"] for p in range(len(rects))], xyz, desc, intrs, E, cfg, g)
+    for p, wp in enumerate(want["pairs"]):
+        st = got["pair_stats"][p]
+        assert st[0] == wp["status"] and st[1] == wp["n_corr"], (p, st, wp["status"], wp["n_corr"])
+        if wp["status"] == 0:
+            assert st[2] == wp["n_inliers"] and st[4] == wp["best_hyp"]
+    assert got["pair_stats"][1][0] == 0 and got["pair_stats"][1][1] > 100   # pair 1 sees the map
+    assert got["pair_stats"][0][1] < got["pair_stats"][1][1] // 4             # pair 0 hardly does
+    st = got["stats"]
+    assert st[0] == want["status"] == 0
+    assert st[2] == want["n_inliers"] and st[4] == want["best"]
+    assert rel_frobenius(got["T"], want["T"]) < 1e-9
+    traj = sc["traj"]
+    gt = np.linalg.inv(np.linalg.inv(traj[0]) @ traj[g])   # body_T_world, world = body at frame 0
+    assert np.linalg.norm(got["T"][:3, 3] - gt[:3, 3]) < 0.02

@@ -1,0 +1,79 @@
+"""SURVEY.md §5 robustness: HipSlamEngine read from a second thread while the main thread runs
+``process_frames`` — the reference adapter's contract (its pose / map locks,
+thor_slam/slam/adapters/isaac_ros.py:82,314,429).  A reader thread polls get_tracking_state(),
+get_map() and save_map() the whole time; nothing may raise, the map's timestamp and the poses the
+main thread gets back never go backwards, and the tracking result equals a run without readers."""
+
+from __future__ import annotations
+
+import threading
+
+import numpy as np
+import pytest
+
+from thor_slam_amd.camera import CameraRig, Extrinsics
+from thor_slam_amd.params import HipSlamConfig
+from thor_slam_amd.synthetic import SyntheticStereoSource
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(cfg, n, reader: bool, tmp_path=None):
+    from thor_slam_amd.slam.hip_engine import HipSlamEngine
+
+    src = SyntheticStereoSource(seed=1, n_frames=n + 2)
+    rig = CameraRig([src], rig_extrinsics={src.name: Extrinsics.from_4x4_matrix(src.rig_T_source)})
+    rig.start()
+    eng = HipSlamEngine(num_cameras=2, config=cfg)
+    eng.initialize(rig.calibration)
+    stop, errors, reads, stamps = threading.Event(), [], [0], []
+
+    def read_loop():
+        k = 0
+        while not stop.is_set():
+            try:
+                eng.get_tracking_state()
+                m = eng.get_map()
+                if m.timestamp is not None:
+                    stamps.append(m.timestamp)
+                assert all(np.isfinite(p.position).all() for p in m.keyframe_poses)
+                if tmp_path is not None and k % 5 == 0:
+                    eng.save_map(str(tmp_path / f"map{k % 2}.npz"))
+                reads[0] += 1
+                k += 1
+            except Exception as exc:   # noqa: BLE001 - collected and reported by the main thread
+                errors.append(repr(exc))
+                return
+
+    th = threading.Thread(target=read_loop, daemon=True) if reader else None
+    if th:
+        th.start()
+    out = []
+    try:
+        for _ in range(n):
+            p = eng.process_frames(rig.get_synchronized_frames())
+            out.append(None if p is None else (p.timestamp, p.position.copy()))
+        eng.flush()
+    finally:
+        stop.set()
+        if th:
+            th.join(timeout=60)
+    final = eng.get_map()
+    eng.shutdown()
+    return out, errors, reads[0], stamps, final
+
+
+@pytest.mark.parametrize("cfg_items", [dict(batch_size=4), dict(batch_size=4, ba_window=10, enable_loop_closure=True)])
+def test_readers_on_another_thread(cfg_items, tmp_path):
+    cfg = HipSlamConfig(**cfg_items)
+    n = 40
+    got, errors, reads, stamps, final = _run(cfg, n, True, tmp_path)
+    assert not errors, errors
+    assert reads > 10
+    assert all(a <= b for a, b in zip(stamps, stamps[1:])), "map timestamps went backwards"
+    ts = [p[0] for p in got if p is not None]
+    assert all(a <= b for a, b in zip(ts, ts[1:])), "pose timestamps went backwards"
+    want, _, _, _, final_ref = _run(cfg, n, False)
+    assert [None if p is None else (p[0], p[1].tobytes()) for p in got] == \
+        [None if p is None else (p[0], p[1].tobytes()) for p in want]
+    assert len(final.keyframe_poses) == len(final_ref.keyframe_poses)

@@ -1006,7 +1006,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_rig_pose(BatchCtx c) {
     double* pout = c.rig_pose + (size_t)f * TS_POSE_DOUBLES;
     int32_t* sout = c.rig_stats + (size_t)f * TS_STATS_INTS;
     for (int i = tid; i < TS_POSE_DOUBLES; i += POSE_THREADS) pout[i] = (i < 16 && (i % 5) == 0) ? 1.0 : 0.0;
-    if (g == 0) {
+    if (g == 0 && !c.reloc) {
         if (tid == 0) write_stats(sout, 2, 0, 0, 0, -1, g);
         return;
     }
@@ -1304,6 +1304,30 @@ void launch_pose(const BatchCtx& c, hipStream_t s) {
     hipLaunchKernelGGL(k_p3p, dim3((c.n * c.npair * c.pp.n_hyp + POSE_THREADS - 1) / POSE_THREADS), dim3(POSE_THREADS), 0, s, c);
     launch_ransac(c, S, s);
     launch_refine(c, S, s);
+}
+
+// Benchmark hook (never on the product path): moves `percent` % of the batch's refined temporal
+// positions by 8..40 px per axis in a random direction — outliers to every pose, the regime of
+// tests/test_gpu_parity.py::test_ransac_bounded_scoring_with_outliers — decided per (frame, pair,
+// keypoint) by a counter hash of `seed`, so the pose stage can be timed where the bounded RANSAC
+// scoring (k_ransac) ends late.  Runs between MATCH_REFINE and POSE.
+__global__ __launch_bounds__(256) void k_perturb_uv(BatchCtx c, int percent, uint64_t seed) {
+    const int K = c.g.K;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)c.n * c.P * K) return;
+    const int k = (int)(i % K), fp = (int)(i / K), p = fp % c.P, f = fp / c.P;
+    double* uv = c.tuv + i * 2;
+    if (!(uv[0] == uv[0])) return;   // no refined position
+    const uint64_t h = splitmix64(seed ^ splitmix64(((uint64_t)(c.g0 + f) << 24) ^ ((uint64_t)p << 16) ^ (uint64_t)k));
+    if ((int)(h % 100u) >= percent) return;
+    const double du = 8.0 + (double)((h >> 8) % 33u), dv = 8.0 + (double)((h >> 16) % 33u);
+    uv[0] += ((h >> 40) & 1u) ? du : -du;
+    uv[1] += ((h >> 41) & 1u) ? dv : -dv;
+}
+
+void launch_perturb_uv(const BatchCtx& c, int percent, uint64_t seed, hipStream_t s) {
+    const int64_t n = (int64_t)c.n * c.P * c.g.K;
+    hipLaunchKernelGGL(k_perturb_uv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c, percent, seed);
 }
 
 // RANSAC + refinement only, on correspondences another kernel wrote (relocalisation).

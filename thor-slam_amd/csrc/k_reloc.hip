@@ -62,9 +62,11 @@ __global__ __launch_bounds__(256) void k_reloc_match(BatchCtx c, int cam, int sl
     match[q] = out;
 }
 
-// One block: the matches in keypoint order -> correspondence rows (A7 layout) + stats.
+// One block: the matches in keypoint order -> correspondence rows (A7 layout) + stats.  `xf`
+// (row-major 3x4, or null): the map point enters as xf * X (the rig's per-pair frame E_p^-1).
 __global__ __launch_bounds__(256) void k_reloc_corr(BatchCtx c, int cam, int slot, int pair, const double* map_xyz,
-                                                    const int32_t* match, double* corr, int32_t* stats, int64_t frame) {
+                                                    const double* xf, const int32_t* match, double* corr, int32_t* stats,
+                                                    int64_t frame) {
     __shared__ int s_tmp[32];
     const int K = c.g.K;
     const size_t ib = (size_t)slot * c.C + cam;
@@ -98,9 +100,14 @@ __global__ __launch_bounds__(256) void k_reloc_corr(BatchCtx c, int cam, int slo
             const double by = (v - cy) / fy;
             const double nn = sqrt((bx * bx + by * by) + 1.0);
             double* cr = corr + (size_t)(n + off + x - flag) * TS_CORR_DOUBLES;
-            cr[0] = map_xyz[(size_t)m * 3];
-            cr[1] = map_xyz[(size_t)m * 3 + 1];
-            cr[2] = map_xyz[(size_t)m * 3 + 2];
+            const double X = map_xyz[(size_t)m * 3], Y = map_xyz[(size_t)m * 3 + 1], Z = map_xyz[(size_t)m * 3 + 2];
+            if (xf) {
+                for (int e = 0; e < 3; ++e) cr[e] = ((xf[4 * e] * X + xf[4 * e + 1] * Y) + xf[4 * e + 2] * Z) + xf[4 * e + 3];
+            } else {
+                cr[0] = X;
+                cr[1] = Y;
+                cr[2] = Z;
+            }
             cr[3] = cx - u;
             cr[4] = cy - v;
             cr[5] = bx / nn;
@@ -123,7 +130,8 @@ void launch_reloc(const BatchCtx& c, int pair, int64_t frame, const double* map_
                   int32_t* match, double* corr, int32_t* stats, double* pose, double* ransac, double* hyp, hipStream_t s) {
     const int slot = ring_slot(c, frame), cam = c.cpp * pair;
     hipLaunchKernelGGL(k_reloc_match, dim3((c.g.K + 255) / 256), dim3(256), 0, s, c, cam, slot, map_desc, M, match);
-    hipLaunchKernelGGL(k_reloc_corr, dim3(1), dim3(256), 0, s, c, cam, slot, pair, map_xyz, match, corr, stats, frame);
+    hipLaunchKernelGGL(k_reloc_corr, dim3(1), dim3(256), 0, s, c, cam, slot, pair, map_xyz, (const double*)nullptr, match,
+                       corr, stats, frame);
     BatchCtx r = c;   // A7's RANSAC + refinement on the relocalisation scratch: one frame, one "pair"
     r.n = 1;
     r.P = 1;
@@ -137,4 +145,39 @@ void launch_reloc(const BatchCtx& c, int pair, int64_t frame, const double* map_
     r.ransac = ransac;
     r.hyp = hyp;
     launch_pose_solve(r, s);
+}
+
+// Relocalisation of a rig (tslam_relocalize_rig): every pair matches its left image of the frame
+// against the map (world = the rig's base frame) and sees the map points in its frame E_p^-1 X, so
+// that A7 per pair gives T_p = cam_p_T(E_p^-1 world) and k_rig_pose's model X_c = E_q^-1 M E_q X'
+// solves M = body_T_world from every pair's correspondences (candidates E_p T_p E_p^-1, scored on
+// all pairs, joint Gauss-Newton).  Scratch per pair: match [P][K], and a one-frame, P-pair batch
+// context (corr, stats, pose, ransac, hyp) + the rig record (rig_pose, rig_stats).
+void launch_reloc_rig(const BatchCtx& c, int64_t frame, const double* map_xyz, const uint32_t* map_desc, int M,
+                      int32_t* match, double* corr, int32_t* stats, double* pose, double* ransac, double* hyp,
+                      double* rig_pose, int32_t* rig_stats, hipStream_t s) {
+    const int slot = ring_slot(c, frame), K = c.g.K;
+    for (int p = 0; p < c.P; ++p) {
+        int32_t* mp = match + (size_t)p * K;
+        hipLaunchKernelGGL(k_reloc_match, dim3((K + 255) / 256), dim3(256), 0, s, c, c.cpp * p, slot, map_desc, M, mp);
+        hipLaunchKernelGGL(k_reloc_corr, dim3(1), dim3(256), 0, s, c, c.cpp * p, slot, p, map_xyz, c.rig_Einv + 16 * p, mp,
+                           corr + (size_t)p * K * TS_CORR_DOUBLES, stats + (size_t)p * TS_STATS_INTS, frame);
+    }
+    BatchCtx r = c;   // one frame, every pair
+    r.n = 1;
+    r.pair0 = 0;
+    r.npair = c.P;
+    r.g0 = frame;
+    r.corr = corr;
+    r.stats = stats;
+    r.pose = pose;
+    r.ransac = ransac;
+    r.hyp = hyp;
+    r.prior = nullptr;
+    r.rig_prior = nullptr;
+    r.rig_pose = rig_pose;
+    r.rig_stats = rig_stats;
+    r.reloc = 1;
+    launch_pose_solve(r, s);
+    launch_rig_pose(r, s);
 }

@@ -83,6 +83,8 @@ struct tslam_handle {
     double* d_rl_pose = nullptr;
     double* d_rl_ransac = nullptr;
     double* d_rl_hyp = nullptr;
+    double* d_rl_rig_pose = nullptr;    // tslam_relocalize_rig: the body record
+    int32_t* d_rl_rig_stats = nullptr;
     int64_t* d_wedges = nullptr;
     // loop closure (tslam_loop_*): keyframe database, one entry per keyframe, slot = count mod cap
     int lp_cap = 0, lp_S = 0;
@@ -484,6 +486,7 @@ static BatchCtx make_ctx(tslam_handle* h) {
     c.pair0 = 0;
     c.npair = h->P;
     c.match_modes = 3;
+    c.reloc = 0;
     c.peer_S = c.peer_me = c.peer_nbuf = c.peer_skip = 0;
     return c;
 }
@@ -1491,6 +1494,17 @@ int tslam_internal_state_blocks(tslam_handle* h, int pack, int rank, int cam_lo,
     return TSLAM_OK;
 }
 
+int tslam_perturb_temporal(tslam_handle* h, int percent, uint64_t seed, void* stream) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (!h->in_batch) return fail(TSLAM_ESTATE, "tslam_perturb_temporal inside a batch (after MATCH_REFINE)");
+    if (percent < 0 || percent > 100) return fail(TSLAM_EINVAL, "percent must be in [0, 100]");
+    if (h->sh_world > 1 || h->sh_comm) return fail(TSLAM_ESTATE, "tslam_perturb_temporal takes an unsharded handle");
+    HIPCHK(hipSetDevice(h->device));
+    if (percent > 0) launch_perturb_uv(make_ctx(h), percent, seed, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return TSLAM_OK;
+}
+
 int tslam_internal_stash(tslam_handle* h, void* stream) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
     if (!h->in_batch) return fail(TSLAM_ESTATE, "results are stashed inside a batch (before tslam_end_batch)");
@@ -1592,15 +1606,20 @@ int tslam_ba_read_map(tslam_handle* h, int pair, int64_t* gid, uint32_t* desc) {
     return TSLAM_OK;
 }
 
+// relocalisation scratch for every pair of the handle (one pair: tslam_relocalize uses pair slot 0;
+// the rig: tslam_relocalize_rig solves all pairs of one frame as a one-frame batch)
 static int ensure_reloc_scratch(tslam_handle* h) {
     if (h->d_rl_match) return TSLAM_OK;
-    const size_t K = h->g.K;
-    int rc = dev_alloc(h, (void**)&h->d_rl_match, sizeof(int32_t) * K);
-    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_corr, sizeof(double) * TS_CORR_DOUBLES * K);
-    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_stats, sizeof(int32_t) * TS_STATS_INTS);
-    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_pose, sizeof(double) * TS_POSE_DOUBLES);
-    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_ransac, sizeof(uint32_t) * TS_RANSAC_WORDS * TS_MAX_SPLITS);
-    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_hyp, sizeof(double) * TS_HYP_DOUBLES * 4 * (size_t)h->prm.ransac_hypotheses);
+    const size_t K = h->g.K, P = h->P;
+    int rc = dev_alloc(h, (void**)&h->d_rl_match, sizeof(int32_t) * K * P);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_corr, sizeof(double) * TS_CORR_DOUBLES * K * P);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_stats, sizeof(int32_t) * TS_STATS_INTS * P);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_pose, sizeof(double) * TS_POSE_DOUBLES * P);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_ransac, sizeof(uint32_t) * TS_RANSAC_WORDS * TS_MAX_SPLITS * P);
+    if (rc == TSLAM_OK)
+        rc = dev_alloc(h, (void**)&h->d_rl_hyp, sizeof(double) * TS_HYP_DOUBLES * 4 * (size_t)h->prm.ransac_hypotheses * P);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_rig_pose, sizeof(double) * TS_POSE_DOUBLES);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rl_rig_stats, sizeof(int32_t) * TS_STATS_INTS);
     return rc;
 }
 
@@ -1669,6 +1688,50 @@ int tslam_relocalize(tslam_handle* h, int pair, int64_t frame, double* cam_T_wor
         return fail(TSLAM_EINVAL, "frame is not resident in the ring");
     HIPCHK(hipSetDevice(h->device));
     return reloc_solve(h, pair, frame, h->d_map_xyz, h->d_map_desc, h->map_n, cam_T_world, cov, stats);
+}
+
+int tslam_relocalize_rig(tslam_handle* h, int64_t frame, double* body_T_world, double* cov, int32_t* stats,
+                         int32_t* pair_stats) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (!h->rig || h->rig_q != h->P) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig)");
+    if (h->prm.rgbd) return fail(TSLAM_ESTATE, "tslam_relocalize_rig takes a stereo rig");
+    if (!h->d_rl_match) return fail(TSLAM_ESTATE, "no map uploaded (tslam_map_upload)");
+    if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_relocalize_rig inside a batch");
+    if (frame < 0 || frame >= h->frames_done || frame < h->frames_done - h->R)
+        return fail(TSLAM_EINVAL, "frame is not resident in the ring");
+    HIPCHK(hipSetDevice(h->device));
+    const BatchCtx c = make_ctx(h);
+    hipStream_t s = h->last_stream;
+    const int P = h->P;
+    if (h->map_n == 0) {
+        std::vector<int32_t> st(TS_STATS_INTS * (size_t)(P + 1), 0);
+        for (int p = 0; p <= P; ++p) {
+            st[(size_t)p * TS_STATS_INTS] = 1;
+            st[(size_t)p * TS_STATS_INTS + 4] = -1;
+            st[(size_t)p * TS_STATS_INTS + 5] = (int32_t)frame;
+        }
+        HIPCHK(hipMemcpy(h->d_rl_stats, st.data(), sizeof(int32_t) * TS_STATS_INTS * P, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(h->d_rl_rig_stats, st.data() + (size_t)P * TS_STATS_INTS, sizeof(int32_t) * TS_STATS_INTS,
+                         hipMemcpyHostToDevice));
+    } else {
+        launch_reloc_rig(c, frame, h->d_map_xyz, h->d_map_desc, (int)h->map_n, h->d_rl_match, h->d_rl_corr, h->d_rl_stats,
+                         h->d_rl_pose, h->d_rl_ransac, h->d_rl_hyp, h->d_rl_rig_pose, h->d_rl_rig_stats, s);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    double pose[TS_POSE_DOUBLES];
+    int32_t st[TS_STATS_INTS];
+    HIPCHK(hipMemcpy(pose, h->d_rl_rig_pose, sizeof(pose), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(st, h->d_rl_rig_stats, sizeof(st), hipMemcpyDeviceToHost));
+    if (h->map_n == 0 || st[0] != 0)
+        for (int i = 0; i < 16; ++i) pose[i] = (i % 5) == 0 ? 1.0 : 0.0;
+    pose[12] = pose[13] = pose[14] = 0.0;   // k_rig_pose writes the 3x4 part
+    pose[15] = 1.0;
+    if (body_T_world) memcpy(body_T_world, pose, 16 * sizeof(double));
+    if (cov) memcpy(cov, pose + 32, 36 * sizeof(double));
+    if (stats) memcpy(stats, st, sizeof(st));
+    if (pair_stats) HIPCHK(hipMemcpy(pair_stats, h->d_rl_stats, sizeof(int32_t) * TS_STATS_INTS * P, hipMemcpyDeviceToHost));
+    return TSLAM_OK;
 }
 
 // -- loop closure: keyframe database, place recognition, verification, pose graph ---------------

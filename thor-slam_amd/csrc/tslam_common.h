@@ -101,6 +101,7 @@ struct BatchCtx {
     // keep their [n][P] layout
     int pair0, npair;
     int match_modes;       // k_match: 3 = temporal + stereo, 1 = stereo only (sharded pre-pass)
+    int reloc;             // k_rig_pose solves a relocalisation (frame 0 is not a first frame)
     // peer layout of a sharded import (tslam_import_peers): images [world][nbuf][S][H][W] as the
     // all-to-all delivers them; the launch covers the world-1 peers' slots (not peer_me's), frames
     // peer_skip .. nbuf-1 of each (peer_S = 0: the plain [n][ncam] view above)
@@ -162,22 +163,8 @@ struct BatchCtx {
 
 static inline __host__ __device__ int ring_slot(const BatchCtx& c, int64_t g) { return (int)(g % c.R); }
 
-// Sharded rig: rank q's back end owns batch frames [q n / world, (q + 1) n / world)
-// of an n-frame batch (any n in [1, max_batch]: ranges may differ by one frame or be empty) and
-// reads the other cameras of frames lo - 1 .. hi - 1 (none for an empty range).  Exchange slots
-// are sized for a full batch: peer_cap frames per peer.
-static inline __host__ __device__ void peer_range(int q, int n, int world, int* lo, int* hi) {
-    *lo = (int)((int64_t)q * n / world);
-    *hi = (int)((int64_t)(q + 1) * n / world);
-}
-static inline __host__ __device__ int peer_frames(int q, int n, int world) {
-    int lo, hi;
-    peer_range(q, n, world, &lo, &hi);
-    return hi > lo ? hi - lo + 1 : 0;
-}
-static inline __host__ __device__ int peer_cap(int max_batch, int world) { return (max_batch + world - 1) / world + 1; }
-// pose records per rank in the all-gather of an n-frame batch (ranges padded to the longest)
-static inline __host__ __device__ int peer_records(int n, int world) { return (n + world - 1) / world; }
+// sharded rig: frame ranges of the ranks (tslam_ranges.h)
+#include "tslam_ranges.h"
 // front-end image index (f * ncam + view camera) -> frame, rig camera; in the peer layout the
 // index runs over (peer, frame, camera) of the world-1 peers
 __device__ __forceinline__ void view_image(const BatchCtx& c, int img, int* f, int* cam) {
@@ -239,8 +226,12 @@ void launch_state_blocks(const BatchCtx& c, bool pack, int n, int world, int ran
 int64_t pair_block_bytes(const LevelGeom& g);
 void launch_pair_blocks(const BatchCtx& c, bool pack, int f0, int n_frames, int p0, int np, uint8_t* blk, hipStream_t s);
 void launch_pose_solve(const BatchCtx& c, hipStream_t s);
+void launch_perturb_uv(const BatchCtx& c, int percent, uint64_t seed, hipStream_t s);   // benchmark hook
 void launch_reloc(const BatchCtx& c, int pair, int64_t frame, const double* map_xyz, const uint32_t* map_desc, int M,
                   int32_t* match, double* corr, int32_t* stats, double* pose, double* ransac, double* hyp, hipStream_t s);
+void launch_reloc_rig(const BatchCtx& c, int64_t frame, const double* map_xyz, const uint32_t* map_desc, int M,
+                      int32_t* match, double* corr, int32_t* stats, double* pose, double* ransac, double* hyp,
+                      double* rig_pose, int32_t* rig_stats, hipStream_t s);
 void launch_loop_store(const BatchCtx& c, int pair, int64_t frame, double* xyz, uint32_t* desc, int32_t* n_out,
                        hipStream_t s);
 void launch_loop_vote(const uint32_t* db_desc, const int32_t* db_n, int K, int S, int q_slot, int n_cand,

@@ -131,6 +131,7 @@ _SIGNATURES = {
     "tslam_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "tslam_submit_sharded": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "tslam_shard_options": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "tslam_perturb_temporal": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p]),
     "tslam_shard_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "tslam_create_rig": (ctypes.c_int, [ctypes.POINTER(CameraDesc), ctypes.c_int, ctypes.POINTER(Params), ctypes.c_int,
                                          ctypes.POINTER(ctypes.c_void_p)]),
@@ -188,6 +189,8 @@ _SIGNATURES = {
     "tslam_ba_read_map": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_map_upload": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     "tslam_relocalize": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64] + [ctypes.c_void_p] * 3),
+    "tslam_relocalize_rig": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_void_p]),
     "tslam_ba_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6),
     "tslam_ba_replay_schur": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
@@ -410,6 +413,11 @@ class Handle:
 
     def run_kernel(self, name: str, stream: int = 0) -> None:
         _check(self.lib.tslam_run_stage(self.h, KERNELS[name], ctypes.c_void_p(stream)))
+
+    def perturb_temporal(self, percent: int, seed: int = 11, stream: int = 0) -> None:
+        """``tslam_perturb_temporal`` (benchmark hook): outliers into the batch's refined temporal
+        positions, between the match_refine and pose kernels."""
+        _check(self.lib.tslam_perturb_temporal(self.h, int(percent), int(seed) & ((1 << 64) - 1), ctypes.c_void_p(stream)))
 
     def run_rig(self, stream: int = 0) -> None:
         _check(self.lib.tslam_run_stage(self.h, RIG_KERNEL, ctypes.c_void_p(stream)))
@@ -657,6 +665,16 @@ class Handle:
         st = np.zeros(8, dtype=np.int32)
         _check(self.lib.tslam_relocalize(self.h, int(pair), int(frame), T.ctypes.data, cov.ctypes.data, st.ctypes.data))
         return {"T": T, "cov": cov, "stats": st}
+
+    def relocalize_rig(self, frame: int) -> dict:
+        """body_T_world of a resident frame of the rig (``set_rig``) in the uploaded map (base-frame
+        world points), from every pair's view (synchronises): T, cov, stats (the rig's), and
+        pair_stats [P][8]."""
+        T, cov = np.zeros((4, 4)), np.zeros((6, 6))
+        st, pst = np.zeros(8, dtype=np.int32), np.zeros((self.n_pairs, 8), dtype=np.int32)
+        _check(self.lib.tslam_relocalize_rig(self.h, int(frame), T.ctypes.data, cov.ctypes.data, st.ctypes.data,
+                                             pst.ctypes.data))
+        return {"T": T, "cov": cov, "stats": st, "pair_stats": pst}
 
     # -- loop closure + pose graph (SURVEY.md §8f items 1, 3) --------------------------------
     def loop_init(self, max_keyframes: int = 1024, signature: int = 256) -> None:

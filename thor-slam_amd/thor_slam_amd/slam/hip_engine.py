@@ -133,6 +133,10 @@ class HipSlamEngine(SlamEngine):
         self._base_T_rect: np.ndarray | None = None
         self._latest_pose: SlamPose | None = None
         self._pose_lock = threading.Lock()
+        # the map state _publish grows (BA keyframes, landmarks, loop graph) against readers on other
+        # threads (get_map / save_map while process_frames runs; the reference adapter's locks,
+        # isaac_ros.py:82,314,429)
+        self._map_lock = threading.RLock()
         self._frame_count = 0
         self._staged: list[tuple[np.ndarray, float]] = []
         self._staged_imu: list[tuple | None] = []    # (gyro, accel) per staged frame
@@ -662,6 +666,10 @@ class HipSlamEngine(SlamEngine):
             del self._map_points[next(iter(self._map_points))]
 
     def _publish(self, res: dict, stamps: list[float], g0: int) -> None:
+        with self._map_lock:
+            self._publish_locked(res, stamps, g0)
+
+    def _publish_locked(self, res: dict, stamps: list[float], g0: int) -> None:
         entry = self._imu_batches.pop(0) if self._imu is not None and self._imu_batches else None
         if entry is not None:   # the filter absorbs the tracked motions
             samples, steps = entry
@@ -797,8 +805,12 @@ class HipSlamEngine(SlamEngine):
 
     def get_map(self) -> SlamMap:
         """Without BA: the (re)initialisation poses.  With BA: every keyframe so far at its latest
-        BA estimate (world_T_base) and the landmarks of pair 0's window (world frame, with their
-        observation counts)."""
+        BA estimate (world_T_base) and the landmarks of every pair's window (world frame, with their
+        observation counts).  Safe to call from another thread while process_frames runs."""
+        with self._map_lock:
+            return self._get_map_locked()
+
+    def _get_map_locked(self) -> SlamMap:
         if self._loop is not None and self._loop.frames and (self._config.ba_window <= 0 or self._ba_window is None):
             bt = self._base_T_rect
             kfs = []
@@ -839,6 +851,10 @@ class HipSlamEngine(SlamEngine):
         """Write the landmarks gathered by local BA (world = base_link frame, rBRIEF descriptors,
         global ids, observation counts) and every keyframe pose to ``path`` (NumPy .npz, no
         pickles).  False when there is nothing to save (local BA off or no landmark yet)."""
+        with self._map_lock:
+            return self._save_map_locked(path)
+
+    def _save_map_locked(self, path: str) -> bool:
         if not self._map_points or self._handle is None:
             return False
         bt = self._base_T_rect
@@ -864,24 +880,34 @@ class HipSlamEngine(SlamEngine):
         except (OSError, KeyError, ValueError) as exc:
             logger.warning("load_map(%s) failed: %s", path, exc)
             return False
-        inv_bt = _invert(self._base_T_rect)
-        self._handle.map_upload(pts @ inv_bt[:3, :3].T + inv_bt[:3, 3], desc)   # into the rect-left frame
+        if len(self._pairs) > 1:   # a rig relocalises in the base frame from every pair (tslam_relocalize_rig)
+            self._handle.map_upload(pts, desc)
+        else:
+            inv_bt = _invert(self._base_T_rect)
+            self._handle.map_upload(pts @ inv_bt[:3, :3].T + inv_bt[:3, 3], desc)   # into the rect-left frame
         self._map_loaded = True
         return True
 
     def relocalize(self) -> bool:
         """Pose the latest processed frame in the loaded map (descriptor matching + P3P-RANSAC on
-        the device); on success the published poses continue in the map's world frame."""
+        the device; a rig: every pair's view, joined by the rig pose, so a map any one pair saw
+        relocalises it); on success the published poses continue in the map's world frame."""
         if self._handle is None:
             raise RuntimeError("Not initialized")
         if not self._map_loaded or self._handle.frames_done == 0:
             return False
         self.flush()
-        res = self._handle.relocalize(self._handle.frames_done - 1)
-        if int(res["stats"][0]) != POSE_OK:
-            return False
-        bt = self._base_T_rect
-        map_pose = bt @ _invert(res["T"]) @ _invert(bt)                  # map world_T_base of that frame
+        if len(self._pairs) > 1:   # every pair matches the map; the rig pose solves the body
+            res = self._handle.relocalize_rig(self._handle.frames_done - 1)
+            if int(res["stats"][0]) != POSE_OK:
+                return False
+            map_pose = _invert(res["T"])                                 # map world_T_base of that frame
+        else:
+            res = self._handle.relocalize(self._handle.frames_done - 1)
+            if int(res["stats"][0]) != POSE_OK:
+                return False
+            bt = self._base_T_rect
+            map_pose = bt @ _invert(res["T"]) @ _invert(bt)              # map world_T_base of that frame
         with self._pose_lock:
             cur = self._latest_pose
         session = (_invert(self._map_offset) @ cur.to_4x4_matrix()) if cur is not None else np.eye(4)
