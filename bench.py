@@ -589,7 +589,8 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
         total = B
     idx = torch.from_numpy(triangle_indices(total, args.unique)).cuda()
     seq = torch.from_numpy(uniq).cuda().index_select(0, idx).contiguous()  # [total, C, H, W] (c5: [B, 4, 5HW]) in HBM
-    step_base = (lambda s: 0) if c5 else (lambda s: s * B)
+    # the outlier steps after the timed region replay the resident batches
+    step_base = (lambda s: 0) if c5 else (lambda s: (s % (args.warmup + args.steps)) * B)
     h = Handle(rects, cfg, max_batch=B, device=dev_index)
     if P > 1:
         h.set_rig(E)
@@ -1008,6 +1009,7 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
                 h.set_rig(E)
         if rehearse:
             grp = HandleGroup(hs, "copy")
+            hs[0].shard_options(pipeline=True)
             step = lambda s, timer=None: grp.submit([batch_of(q, s).data_ptr() for q in range(world)], B,  # noqa: E731
                                                     [stream.cuda_stream] * world)
         else:
@@ -1015,6 +1017,7 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
             if world > 1:
                 dist.broadcast_object_list(uid, src=0)
             hs[0].comm_init(uid[0], rank, world)
+            hs[0].shard_options(pipeline=True)   # batch s+1's front end beside batch s's back end
             step = lambda s, timer=None: hs[0].submit_sharded(batch_of(0, s).data_ptr(), B, stream.cuda_stream)  # noqa: E731
         drain = torch.cuda.synchronize
     for s in range(args.warmup):
@@ -1025,7 +1028,7 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
     torch.cuda.synchronize()
     timer = StageTimer()
     if args.driver == "library":
-        hs[0].shard_options(profile=True)
+        hs[0].shard_options(profile=True, pipeline=True)
     t0 = time.perf_counter()
     for k in range(args.steps):
         s = args.warmup + k

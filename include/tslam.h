@@ -420,8 +420,9 @@ int tslam_unpack_poses(tslam_handle* h, const void* src, void* stream);
  *   blocks of the frames every other rank solves sent point to point (RGB-D: its cameras' pair
  *   blocks); back end (+ rig pose) of its frame range; pose records all-gathered; the chain.  The
  *   library runs the phases on streams of its own — front (high priority), exchange, back — with
- *   double-buffered exchange buffers, so batch s's image exchange overlaps its front end and batch
- *   s+1's front end overlaps batch s's back end; `stream` then waits for the batch.  Every rank then
+ *   double-buffered exchange buffers, so batch s's image exchange overlaps its front end; `stream`
+ *   then waits for the batch (with TSLAM_SHARD_PIPELINE only for its input: batch s+1's front end
+ *   then overlaps batch s's back end).  Every rank then
  *   reads the whole rig's poses with tslam_read_poses / tslam_read_rig_poses, identical to one
  *   handle fed all cameras.  Nothing synchronises the host. */
 int tslam_comm_unique_id(void* id128);
@@ -442,12 +443,23 @@ int tslam_submit_sharded(tslam_handle* h, const uint8_t* images, int n_frames, v
  *                        (TSLAM_SEG_*) since its last call (synchronises) and the batch count;
  *   TSLAM_SHARD_SERIAL   (profiling aid) every rank's work on one stream per device, shared by the
  *                        ranks on it: with all ranks of a group on one GPU, each kernel and copy
- *                        runs alone, so the profile gives isolated per-rank durations.
+ *                        runs alone, so the profile gives isolated per-rank durations;
+ *   TSLAM_SHARD_PIPELINE the caller's stream waits only until the batch has read its input and
+ *                        receive buffers (the caller may refill the input), not for the whole
+ *                        batch: the next batch's front end overlaps this one's back end.  Results
+ *                        are then read after a device synchronisation or through the result
+ *                        slots (TSLAM_SHARD_RESULTS + tslam_poll_*);
+ *   TSLAM_SHARD_SOLO     (profiling aid, groups only) rank 0 alone runs its work and every exchange
+ *                        is skipped (its receive buffers keep the last full batch's data): the
+ *                        per-GPU step of one rank of an N-GPU node with the exchange hidden, timed
+ *                        on one GPU.  Results are not meaningful; reset the handles afterwards.
  * Setting options waits for the work enqueued so far. */
 #define TSLAM_SHARD_GATHER 1
 #define TSLAM_SHARD_RESULTS 2
 #define TSLAM_SHARD_PROFILE 4
 #define TSLAM_SHARD_SERIAL 8
+#define TSLAM_SHARD_PIPELINE 16
+#define TSLAM_SHARD_SOLO 32
 enum tslam_segment {
     TSLAM_SEG_RECTIFY = 0, TSLAM_SEG_DETECT, TSLAM_SEG_SELECT, TSLAM_SEG_DESCRIBE, TSLAM_SEG_PACK,
     TSLAM_SEG_EXCHANGE_WAIT,   /* front end done -> the peers' images and stream blocks landed */

@@ -195,3 +195,86 @@ def test_results_slots_and_profile():
             assert hs[1].shard_timing()[1] == 0   # reset by the call
 
     _run(sc, HipSlamConfig(), sizes, 2, options={"results": True, "profile": True}, check=check)
+
+
+def test_pipelined_batches_identical():
+    """TSLAM_SHARD_PIPELINE: the caller's stream waits only for each batch's input, so batch s+1's
+    front end runs beside batch s's back end (batches submitted back to back, each polled from the
+    result slots one submission later): every batch's poses equal the unsharded handle's."""
+    import torch
+
+    from thor_slam_amd._lib import Handle, HandleGroup
+
+    sizes = [8, 8, 3, 8, 5]
+    sc = rig_scene(TWO, sum(sizes))
+    cfg = HipSlamConfig()
+    h1 = Handle(sc["rects"], cfg, max_batch=8)
+    h1.set_rig(sc["E"])
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    want, f0 = [], 0
+    for n in sizes:
+        h1.submit(dev[f0].data_ptr(), n, s)
+        want.append(_poses(h1, n))
+        f0 += n
+    h1.close()
+    world = 4
+    hs = [Handle(sc["rects"], cfg, max_batch=8) for _ in range(world)]
+    for h in hs:
+        h.set_rig(sc["E"])
+    grp = HandleGroup(hs, "copy")
+    hs[0].shard_options(results=True, pipeline=True)
+    S = sc["frames"].shape[1] // world
+    parts = [dev[:, r * S:(r + 1) * S].contiguous() for r in range(world)]
+
+    def check(b):
+        res = hs[0].poll_batch(block=True)
+        assert res is not None and res["n"] == sizes[b]
+        np.testing.assert_array_equal(res["T_abs"], want[b]["pairs"]["T_abs"], err_msg=f"batch {b}")
+        np.testing.assert_array_equal(res["stats"], want[b]["pairs"]["stats"], err_msg=f"batch {b}")
+        np.testing.assert_array_equal(res["rig"]["T_abs"], want[b]["rig"]["T_abs"], err_msg=f"batch {b}")
+
+    try:
+        f0 = 0
+        for b, n in enumerate(sizes):
+            grp.submit([p[f0].data_ptr() for p in parts], n)
+            f0 += n
+            if b:
+                check(b - 1)
+        check(len(sizes) - 1)
+        torch.cuda.synchronize()
+        _assert_identical(_poses(hs[2], sizes[-1]), want[-1], "last batch, rank 2")
+    finally:
+        grp.close()
+        for h in hs:
+            h.close()
+
+
+def test_solo_profiles_rank0_only():
+    """TSLAM_SHARD_SOLO (profiling aid): after a full batch, rank 0 alone runs its work with the
+    exchanges skipped; its profile counts the solo batches, the other ranks' none."""
+    import torch
+
+    from thor_slam_amd._lib import Handle, HandleGroup
+
+    sc = rig_scene(TWO, 16)
+    cfg = HipSlamConfig()
+    hs = [Handle(sc["rects"], cfg, max_batch=8) for _ in range(4)]
+    for h in hs:
+        h.set_rig(sc["E"])
+    grp = HandleGroup(hs, "copy")
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    parts = [dev[:, r:r + 1].contiguous() for r in range(4)]
+    try:
+        grp.submit([p[0].data_ptr() for p in parts], 8)
+        hs[0].shard_options(solo=True, pipeline=True, profile=True)
+        for _ in range(2):
+            grp.submit([p[8].data_ptr() for p in parts], 8)
+        torch.cuda.synchronize()
+        t0, nb0 = hs[0].shard_timing()
+        assert nb0 == 2 and t0["detect"] > 0.0 and t0["pose"] > 0.0 and t0["pose_gather"] >= 0.0
+        assert hs[1].shard_timing()[1] == 0
+    finally:
+        grp.close()
+        for h in hs:
+            h.close()

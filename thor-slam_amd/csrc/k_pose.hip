@@ -896,85 +896,154 @@ __global__ __launch_bounds__(RF_THREADS) void k_refine(BatchCtx c, int S) {
     }
 }
 
-// Pose chaining: T_abs(t) = T_abs(t-1) * inv(T_rel(t)) for every successful frame, in frame
-// order (the association is the oracle's, so results do not depend on the batch size).  One block
-// per chain: blocks 0 .. P-1 the pairs, block P the rig's body motion (when chained in the same
-// launch) — the chains are independent, so a rig's pairs run side by side.  A block inverts its
-// relative poses in parallel into LDS; then 16 lanes of wave 0 carry T, one element each: per
-// frame a lane gathers its row of T (4 quad DPP broadcasts) and computes its element with the
-// oracle's expression.  The next frame's status and inverse are read from LDS while the current
-// one is computed and an untracked frame keeps T by a select, so a frame costs one dependent
-// broadcast + 4-term dot product (no LDS round trip or branch on the chain's critical path).
-#define TS_CHAIN_CHUNK 128
+// Pose chaining: T_abs(g) = T_abs(g-1) * F(g), F(g) = inv(T_rel(g)) for a tracked frame (the IMU's
+// motion for an IMU-propagated one), the identity otherwise.  The association of the products is
+// fixed by the global frame index, so results do not depend on how frames are batched (nor on a
+// sharded rig's ranges): frames form global blocks of TS_CHAIN_BLK, and
+//   T_abs(g) = A(j) * Q(g),  Q(g) = Q(g-1) * F(g) inside block j (Q = I before its first frame),
+//   A(j) = A(j-1) * Q(last frame of block j-1).
+// The chain state is (A, Q) of the last chained frame (32 doubles); a batch whose first frame opens
+// a block first folds Q into A.  One block per chain (blocks 0 .. P-1 the pairs, block P the rig's
+// body motion), rounds of up to TS_CHAIN_SEGS global blocks: the round's factors are inverted in
+// parallel into LDS, the blocks' prefixes run side by side (16 lanes each, one element of Q per lane:
+// a row of Q by 4 quad-DPP broadcasts, its element of the product by a 4-term dot product, written
+// back over the factor in LDS), one 16-lane group chains the round's A's, and every element of
+// every A * Q is one parallel pass.  A launch of n frames costs about TS_CHAIN_BLK + n / TS_CHAIN_BLK
+// dependent steps instead of n (C2, 1,024 frames: 164 -> see DESIGN.md §5).
+#define TS_CHAIN_BLK 64
+#define TS_CHAIN_SEGS 4
+#define TS_CHAIN_ROUND (TS_CHAIN_BLK * TS_CHAIN_SEGS)
+
+// a * b of two row-major 4x4 matrices, element (i, j), the oracle's operation order
+__device__ __forceinline__ double mul4_elem(const double* a, const double* b, int i, int j) {
+    return ((a[4 * i] * b[j] + a[4 * i + 1] * b[4 + j]) + a[4 * i + 2] * b[8 + j]) + a[4 * i + 3] * b[12 + j];
+}
+
 __global__ __launch_bounds__(256) void k_chain(BatchCtx c) {
-    __shared__ double s_inv[TS_CHAIN_CHUNK][16];
-    __shared__ int s_status[TS_CHAIN_CHUNK];
-    const int tid = threadIdx.x, lane = tid & 63;
+    __shared__ double s_f[TS_CHAIN_ROUND][16];   // the round's factors, then its prefixes Q(f)
+    __shared__ int s_keep[TS_CHAIN_ROUND];        // 1: the frame does not move the chain
+    __shared__ double s_A[TS_CHAIN_SEGS + 1][16];  // A of each segment of the round (+ the next)
+    __shared__ double s_Qin[16];                    // the round's first segment's starting prefix
+    __shared__ double s_Ql[TS_CHAIN_SEGS][16];     // each segment's last prefix
+    const int tid = threadIdx.x;
     const bool rig = (int)blockIdx.x >= c.P;   // the rig's chain (k_rig_pose's body motions)
     const int P = rig ? 1 : c.P, p = rig ? 0 : (int)blockIdx.x;
     double* pose = rig ? c.rig_pose : c.pose;
     const int32_t* stats = rig ? c.rig_stats : c.stats;
-    double* state = rig ? c.rig_state : c.state + 16 * p;
+    double* state = rig ? c.rig_state : c.state + 32 * p;
     const double* prior = rig ? (c.prior ? c.rig_prior : nullptr) : c.prior;
-    double T = 0.0;
-    if (tid < 16) T = state[tid];
-    for (int f0 = 0; f0 < c.n; f0 += TS_CHAIN_CHUNK) {
-        const int nf = min(TS_CHAIN_CHUNK, c.n - f0);
+    const int off = (int)(c.g0 % TS_CHAIN_BLK);
+    if (tid < 16) {
+        const double A = state[tid], Q = state[16 + tid];
+        s_A[0][tid] = A;
+        s_Qin[tid] = Q;
+    }
+    __syncthreads();
+    if (off == 0 && tid < 16) {   // the batch opens a block: A = A * Q, Q = I
+        const int i = tid >> 2, j = tid & 3;
+        const double A = mul4_elem(s_A[0], s_Qin, i, j);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // every lane has read A, Q
+        s_A[0][tid] = A;
+        s_Qin[tid] = i == j ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    // segments of the batch: [0, len0), then whole global blocks, the last one possibly partial
+    const int len0 = min(c.n, TS_CHAIN_BLK - off);
+    const int nseg = 1 + (c.n - len0 + TS_CHAIN_BLK - 1) / TS_CHAIN_BLK;
+    for (int s0 = 0; s0 < nseg; s0 += TS_CHAIN_SEGS) {
+        const int ns = min(TS_CHAIN_SEGS, nseg - s0);
+        const int f0 = s0 == 0 ? 0 : len0 + (s0 - 1) * TS_CHAIN_BLK;   // the round's first frame
+        const int f1 = min(c.n, len0 + (s0 + ns - 1) * TS_CHAIN_BLK);  // one past its last
+        const int nf = f1 - f0;
+        // 1. factors F(f) = inv(T_rel(f)) into LDS; an untracked frame with an accelerometer
+        // prediction (W_t > 0) moves by the IMU's T_rel = [R_prior | t_prior] (its pose record's
+        // T_rel becomes that prediction); other untracked frames keep the chain
+        for (int fl = tid; fl < nf; fl += blockDim.x) {
+            const size_t fp = (size_t)(f0 + fl) * P + p;
+            const int st = stats[fp * TS_STATS_INTS];
+            const bool imu = st != 0 && prior && prior[fp * TS_PRIOR_DOUBLES + 13] > 0.0;
+            s_keep[fl] = (st == 0 || imu) ? 0 : 1;
+        }
         __syncthreads();
         for (int i = tid; i < nf * 16; i += blockDim.x) {
             const int fl = i / 16, e = i % 16, r = e / 4, q = e % 4;
-            const double* rel = pose + (size_t)((f0 + fl) * P + p) * TS_POSE_DOUBLES;
+            const size_t fp = (size_t)(f0 + fl) * P + p;
+            const double* rel = pose + fp * TS_POSE_DOUBLES;
+            const bool imu = stats[fp * TS_STATS_INTS] != 0 && !s_keep[fl];
             double v;
-            if (r == 3) v = q == 3 ? 1.0 : 0.0;
-            else if (q < 3) v = rel[4 * q + r];
-            else v = -((rel[r] * rel[3] + rel[4 + r] * rel[7]) + rel[8 + r] * rel[11]);
-            s_inv[fl][e] = v;
-        }
-        for (int fl = tid; fl < nf; fl += blockDim.x) s_status[fl] = stats[(size_t)((f0 + fl) * P + p) * TS_STATS_INTS];
-        __syncthreads();
-        // an untracked frame with an accelerometer prediction (W_t > 0) moves by the IMU's
-        // T_rel = [R_prior | t_prior]; its pose record's T_rel becomes that prediction
-        if (prior) {
-            for (int i = tid; i < nf * 16; i += blockDim.x) {
-                const int fl = i / 16, e = i % 16, r = e / 4, q = e % 4;
-                const size_t fp = (size_t)(f0 + fl) * P + p;
+            if (imu) {
                 const double* pr = prior + fp * TS_PRIOR_DOUBLES;
-                if (s_status[fl] == 0 || !(pr[13] > 0.0)) continue;
-                double v;
                 if (r == 3) v = q == 3 ? 1.0 : 0.0;
                 else if (q < 3) v = pr[3 * q + r];
                 else v = -((pr[r] * pr[10] + pr[3 + r] * pr[11]) + pr[6 + r] * pr[12]);
-                s_inv[fl][e] = v;
                 pose[fp * TS_POSE_DOUBLES + e] = r == 3 ? (q == 3 ? 1.0 : 0.0) : (q < 3 ? pr[3 * r + q] : pr[10 + r]);
+            } else {
+                if (r == 3) v = q == 3 ? 1.0 : 0.0;
+                else if (q < 3) v = rel[4 * q + r];
+                else v = -((rel[r] * rel[3] + rel[4 + r] * rel[7]) + rel[8 + r] * rel[11]);
             }
-            __syncthreads();
-            for (int fl = tid; fl < nf; fl += blockDim.x)
-                if (s_status[fl] != 0 && prior[(size_t)((f0 + fl) * P + p) * TS_PRIOR_DOUBLES + 13] > 0.0) s_status[fl] = -1;
-            __syncthreads();
+            s_f[fl][e] = v;
         }
-        if (tid < 64) {
-            const int j = lane & 3;
-            int st = s_status[0];
-            double i0 = s_inv[0][j], i1 = s_inv[0][4 + j], i2 = s_inv[0][8 + j], i3 = s_inv[0][12 + j];
-            for (int fl = 0; fl < nf; ++fl) {
-                const int fn = min(fl + 1, nf - 1);   // next frame's operands, off the critical path
-                const int st_n = s_status[fn];
-                const double n0 = s_inv[fn][j], n1 = s_inv[fn][4 + j], n2 = s_inv[fn][8 + j], n3 = s_inv[fn][12 + j];
-                // row i of T lives in this lane's quad: quad_perm broadcasts of lanes 0..3
-                const double t0 = dpp_f64c<0x00>(T), t1 = dpp_f64c<0x55>(T);
-                const double t2 = dpp_f64c<0xAA>(T), t3 = dpp_f64c<0xFF>(T);
-                const double nt = ((t0 * i0 + t1 * i1) + t2 * i2) + t3 * i3;
-                T = st <= 0 ? nt : T;   // tracked (0) or IMU-propagated (-1)
-                if (lane < 16) pose[(size_t)((f0 + fl) * P + p) * TS_POSE_DOUBLES + 16 + lane] = T;
-                st = st_n;
+        __syncthreads();
+        // 2. the prefixes: segment s0 + q by lanes 16q .. 16q + 15 of wave 0
+        if (tid < 16 * ns) {
+            const int q = tid >> 4, e = tid & 15, i = e >> 2, j = e & 3;
+            const int sg = s0 + q;
+            const int a = (sg == 0 ? 0 : len0 + (sg - 1) * TS_CHAIN_BLK) - f0;
+            const int b = min(c.n, sg == 0 ? len0 : len0 + sg * TS_CHAIN_BLK) - f0;
+            double Q = sg == 0 ? s_Qin[e] : (i == j ? 1.0 : 0.0);
+            double i0 = s_f[a][j], i1 = s_f[a][4 + j], i2 = s_f[a][8 + j], i3 = s_f[a][12 + j];
+            int keep = s_keep[a];
+            for (int fl = a; fl < b; ++fl) {
+                const int fn = min(fl + 1, b - 1);   // the next frame's operands, off the critical path
+                const double n0 = s_f[fn][j], n1 = s_f[fn][4 + j], n2 = s_f[fn][8 + j], n3 = s_f[fn][12 + j];
+                const int keep_n = s_keep[fn];
+                // row i of Q lives in this lane's quad: quad_perm broadcasts
+                const double t0 = dpp_f64c<0x00>(Q), t1 = dpp_f64c<0x55>(Q);
+                const double t2 = dpp_f64c<0xAA>(Q), t3 = dpp_f64c<0xFF>(Q);
+                const double nq = ((t0 * i0 + t1 * i1) + t2 * i2) + t3 * i3;
+                Q = keep ? Q : nq;
+                s_f[fl][e] = Q;   // every lane of the group read this frame's column above
+                keep = keep_n;
                 i0 = n0;
                 i1 = n1;
                 i2 = n2;
                 i3 = n3;
             }
+            s_Ql[q][e] = Q;
         }
+        __syncthreads();
+        // 3. the round's A's, in order: A(s + 1) = A(s) * Q_last(s)
+        if (tid < 16) {
+            const int i = tid >> 2, j = tid & 3;
+            for (int q = 0; q < ns; ++q) {
+                const double An = mul4_elem(s_A[q], s_Ql[q], i, j);
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                s_A[q + 1][tid] = An;
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            }
+        }
+        __syncthreads();
+        // 4. T_abs(f) = A(segment of f) * Q(f)
+        for (int i = tid; i < nf * 16; i += blockDim.x) {
+            const int fl = i / 16, e = i % 16;
+            const int f = f0 + fl;
+            const int q = (f < len0 ? 0 : 1 + (f - len0) / TS_CHAIN_BLK) - s0;
+            pose[((size_t)f * P + p) * TS_POSE_DOUBLES + 16 + e] = mul4_elem(s_A[q], s_f[fl], e >> 2, e & 3);
+        }
+        __syncthreads();
+        // the new state: (A, Q) of the round's last segment; the next round starts from A(ns)
+        if (tid < 16) {
+            const double Al = s_A[ns - 1][tid], Ql = s_Ql[ns - 1][tid], An = s_A[ns][tid];
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            if (s0 + ns == nseg) {
+                state[tid] = Al;
+                state[16 + tid] = Ql;
+            }
+            s_A[0][tid] = An;
+        }
+        __syncthreads();
     }
-    if (tid < 16) state[tid] = T;
 }
 
 // ---- rig pose: generalised PnP over every pair of the rig ---------------
@@ -992,11 +1061,16 @@ __device__ __forceinline__ void mul4_fixed(const double* A, const double* B, dou
 }
 
 #define TS_RIG_MAXP 8
-__global__ __launch_bounds__(POSE_THREADS) void k_rig_pose(BatchCtx c) {
+// 512 threads (8 waves) per frame: the kernel is a per-frame latency chain (scoring, then 8
+// Gauss-Newton sweeps over every pair's correspondences with a block reduction and a 6x6 solve
+// each); 198 VGPRs fit 2 waves per SIMD, and each thread's share of the sweeps halves
+#define RIG_THREADS 512
+#define RIG_WAVES (RIG_THREADS / 64)
+__global__ __launch_bounds__(RIG_THREADS) void k_rig_pose(BatchCtx c) {
     __shared__ double s_M[TS_RIG_MAXP][16];                  // candidates (body motions)
     __shared__ double s_T[TS_RIG_MAXP][TS_RIG_MAXP][12];     // [candidate][pair] R | t
-    __shared__ int s_cnt[4][TS_RIG_MAXP];
-    __shared__ double s_red[4][N_ACC];
+    __shared__ int s_cnt[RIG_WAVES][TS_RIG_MAXP];
+    __shared__ double s_red[RIG_WAVES][N_ACC];
     __shared__ double s_H[36], s_misc[2];
     __shared__ int s_nc, s_flag, s_best;
     const int f = blockIdx.x;
@@ -1005,7 +1079,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_rig_pose(BatchCtx c) {
     const int P = c.P, K = c.g.K;
     double* pout = c.rig_pose + (size_t)f * TS_POSE_DOUBLES;
     int32_t* sout = c.rig_stats + (size_t)f * TS_STATS_INTS;
-    for (int i = tid; i < TS_POSE_DOUBLES; i += POSE_THREADS) pout[i] = (i < 16 && (i % 5) == 0) ? 1.0 : 0.0;
+    for (int i = tid; i < TS_POSE_DOUBLES; i += RIG_THREADS) pout[i] = (i < 16 && (i % 5) == 0) ? 1.0 : 0.0;
     if (g == 0 && !c.reloc) {
         if (tid == 0) write_stats(sout, 2, 0, 0, 0, -1, g);
         return;
@@ -1032,7 +1106,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_rig_pose(BatchCtx c) {
         return;
     }
     // per (candidate, pair): T_q = (E_q^-1 M) E_q
-    for (int i = tid; i < nc * P; i += POSE_THREADS) {
+    for (int i = tid; i < nc * P; i += RIG_THREADS) {
         const int m = i / P, q = i % P;
         double A[16], T[16];
         mul4_fixed(c.rig_Einv + 16 * q, s_M[m], A);
@@ -1051,7 +1125,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_rig_pose(BatchCtx c) {
         const int nq = c.stats[(size_t)(f * P + q) * TS_STATS_INTS + 1];
         const double* corr = c.corr + ((size_t)f * P + q) * K * TS_CORR_DOUBLES;
         const double fx = c.calib[q].fx, fy = c.calib[q].fy;
-        for (int ci = tid; ci < nq; ci += POSE_THREADS) {
+        for (int ci = tid; ci < nq; ci += RIG_THREADS) {
             const double* cr = corr + (size_t)ci * TS_CORR_DOUBLES;
             for (int m = 0; m < nc; ++m) cnt[m] += is_inlier(s_T[m][q], s_T[m][q] + 9, cr, fx, fy, thr2) ? 1 : 0;
         }
@@ -1064,7 +1138,8 @@ __global__ __launch_bounds__(POSE_THREADS) void k_rig_pose(BatchCtx c) {
     if (tid == 0) {
         int best = 0, bc = -1;
         for (int m = 0; m < nc; ++m) {
-            const int t = ((s_cnt[0][m] + s_cnt[1][m]) + s_cnt[2][m]) + s_cnt[3][m];
+            int t = 0;
+            for (int w = 0; w < RIG_WAVES; ++w) t += s_cnt[w][m];
             if (t > bc) {
                 bc = t;
                 best = m;
@@ -1081,7 +1156,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_rig_pose(BatchCtx c) {
     bool fail = false;
     double sq_last = 0.0;
     for (int it = 0; it < c.pp.iters; ++it) {
-        for (int q = tid; q < P; q += POSE_THREADS) {
+        for (int q = tid; q < P; q += RIG_THREADS) {
             double A[16], T[16];
             mul4_fixed(c.rig_Einv + 16 * q, s_M[0], A);
             mul4_fixed(A, c.rig_E + 16 * q, T);
@@ -1102,7 +1177,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_rig_pose(BatchCtx c) {
             const double* R = s_T[0][q];
             const double* t = R + 9;
             const double* E = c.rig_E + 16 * q;
-            for (int ci = tid; ci < nq; ci += POSE_THREADS) {
+            for (int ci = tid; ci < nq; ci += RIG_THREADS) {
                 const double* cr = corr + (size_t)ci * TS_CORR_DOUBLES;
                 if (!is_inlier(R, t, cr, fx, fy, thr2)) continue;
                 const double X = cr[0], Y = cr[1], Z = cr[2];
@@ -1142,7 +1217,10 @@ __global__ __launch_bounds__(POSE_THREADS) void k_rig_pose(BatchCtx c) {
         __syncthreads();
         if (tid == 0) {
             double tot[N_ACC];
-            for (int k = 0; k < N_ACC; ++k) tot[k] = ((s_red[0][k] + s_red[1][k]) + s_red[2][k]) + s_red[3][k];
+            for (int k = 0; k < N_ACC; ++k) {
+                tot[k] = s_red[0][k];
+                for (int w = 1; w < RIG_WAVES; ++w) tot[k] += s_red[w][k];
+            }
             s_flag = 0;
             double Hm[36], gv[6], x[6], L[36];
             int k = 0;
@@ -1188,7 +1266,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_rig_pose(BatchCtx c) {
         sq_last = s_misc[0];
     }
     // final inliers of all pairs under M
-    for (int q = tid; q < P; q += POSE_THREADS) {
+    for (int q = tid; q < P; q += RIG_THREADS) {
         double A[16], T[16];
         mul4_fixed(c.rig_Einv + 16 * q, s_M[0], A);
         mul4_fixed(A, c.rig_E + 16 * q, T);
@@ -1203,14 +1281,15 @@ __global__ __launch_bounds__(POSE_THREADS) void k_rig_pose(BatchCtx c) {
         for (int q = 0; q < P; ++q) {
             const int nq = c.stats[(size_t)(f * P + q) * TS_STATS_INTS + 1];
             const double* corr = c.corr + ((size_t)f * P + q) * K * TS_CORR_DOUBLES;
-            for (int ci = tid; ci < nq; ci += POSE_THREADS)
+            for (int ci = tid; ci < nq; ci += RIG_THREADS)
                 cnt_local += is_inlier(s_T[0][q], s_T[0][q] + 9, corr + (size_t)ci * TS_CORR_DOUBLES, c.calib[q].fx,
                                        c.calib[q].fy, thr2) ? 1 : 0;
         }
     cnt_local = wave_sum_i32(cnt_local);
     if (lane == 0) s_cnt[wave][0] = cnt_local;
     __syncthreads();
-    const int n_in = ((s_cnt[0][0] + s_cnt[1][0]) + s_cnt[2][0]) + s_cnt[3][0];
+    int n_in = 0;
+    for (int w = 0; w < RIG_WAVES; ++w) n_in += s_cnt[w][0];
     const bool ok = !fail && n_in >= c.pp.min_inliers;
     if (tid == 0) {
         write_stats(sout, ok ? 0 : 1, n_total, fail ? 0 : n_in, best_cnt, best_idx, g);
@@ -1228,7 +1307,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_rig_pose(BatchCtx c) {
 }
 
 void launch_rig_pose(const BatchCtx& c, hipStream_t s) {
-    hipLaunchKernelGGL(k_rig_pose, dim3(c.n), dim3(POSE_THREADS), 0, s, c);
+    hipLaunchKernelGGL(k_rig_pose, dim3(c.n), dim3(RIG_THREADS), 0, s, c);
 }
 
 

@@ -66,9 +66,12 @@ __global__ __launch_bounds__(256) void k_reloc_match(BatchCtx c, int cam, int sl
 // (row-major 3x4, or null): the map point enters as xf * X (the rig's per-pair frame E_p^-1).
 __global__ __launch_bounds__(256) void k_reloc_corr(BatchCtx c, int cam, int slot, int pair, const double* map_xyz,
                                                     const double* xf, const int32_t* match, double* corr, int32_t* stats,
-                                                    int64_t frame) {
+                                                    double* pose, int64_t frame) {
     __shared__ int s_tmp[32];
     const int K = c.g.K;
+    // the pose record starts as k_corr leaves it (identity T_rel, zeros): k_refine writes the 3x4
+    // part only, and k_rig_pose reads the whole 4x4
+    for (int i = threadIdx.x; i < TS_POSE_DOUBLES; i += blockDim.x) pose[i] = (i < 16 && (i % 5) == 0) ? 1.0 : 0.0;
     const size_t ib = (size_t)slot * c.C + cam;
     const PairCalib cal = c.calib[pair];
     const double fx = cal.fx, fy = cal.fy, cx = cal.cx, cy = cal.cy;
@@ -131,7 +134,7 @@ void launch_reloc(const BatchCtx& c, int pair, int64_t frame, const double* map_
     const int slot = ring_slot(c, frame), cam = c.cpp * pair;
     hipLaunchKernelGGL(k_reloc_match, dim3((c.g.K + 255) / 256), dim3(256), 0, s, c, cam, slot, map_desc, M, match);
     hipLaunchKernelGGL(k_reloc_corr, dim3(1), dim3(256), 0, s, c, cam, slot, pair, map_xyz, (const double*)nullptr, match,
-                       corr, stats, frame);
+                       corr, stats, pose, frame);
     BatchCtx r = c;   // A7's RANSAC + refinement on the relocalisation scratch: one frame, one "pair"
     r.n = 1;
     r.P = 1;
@@ -161,7 +164,8 @@ void launch_reloc_rig(const BatchCtx& c, int64_t frame, const double* map_xyz, c
         int32_t* mp = match + (size_t)p * K;
         hipLaunchKernelGGL(k_reloc_match, dim3((K + 255) / 256), dim3(256), 0, s, c, c.cpp * p, slot, map_desc, M, mp);
         hipLaunchKernelGGL(k_reloc_corr, dim3(1), dim3(256), 0, s, c, c.cpp * p, slot, p, map_xyz, c.rig_Einv + 16 * p, mp,
-                           corr + (size_t)p * K * TS_CORR_DOUBLES, stats + (size_t)p * TS_STATS_INTS, frame);
+                           corr + (size_t)p * K * TS_CORR_DOUBLES, stats + (size_t)p * TS_STATS_INTS,
+                           pose + (size_t)p * TS_POSE_DOUBLES, frame);
     }
     BatchCtx r = c;   // one frame, every pair
     r.n = 1;

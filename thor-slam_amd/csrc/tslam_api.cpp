@@ -756,7 +756,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_ccount, sizeof(uint32_t) * (size_t)B * C * h->g.total_bands);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_hist, sizeof(uint32_t) * (size_t)B * C * L * 256);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_det_thr_acc, sizeof(uint32_t) * (size_t)C * L);
-    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_state, sizeof(double) * 16 * (size_t)P);
+    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_state, sizeof(double) * 32 * (size_t)P);   // chain (A, Q) per pair
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_ransac, sizeof(uint32_t) * TS_RANSAC_WORDS * TS_MAX_SPLITS * (size_t)B * P);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_hyp, sizeof(double) * TS_HYP_DOUBLES * 4 * (size_t)p.ransac_hypotheses * B * P);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_brief, sizeof(TSLAM_BRIEF_TABLE));
@@ -825,11 +825,11 @@ int tslam_reset(tslam_handle* h) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
-    std::vector<double> eye(16 * (size_t)h->P, 0.0);
-    for (int p = 0; p < h->P; ++p)
-        for (int k = 0; k < 4; ++k) eye[(size_t)p * 16 + 5 * k] = 1.0;
+    std::vector<double> eye(32 * (size_t)h->P, 0.0);   // every chain's (A, Q) = (I, I)
+    for (int q = 0; q < 2 * h->P; ++q)
+        for (int k = 0; k < 4; ++k) eye[(size_t)q * 16 + 5 * k] = 1.0;
     HIPCHK(hipMemcpy(h->d_state, eye.data(), sizeof(double) * eye.size(), hipMemcpyHostToDevice));
-    if (h->d_rig_state) HIPCHK(hipMemcpy(h->d_rig_state, eye.data(), sizeof(double) * 16, hipMemcpyHostToDevice));
+    if (h->d_rig_state) HIPCHK(hipMemcpy(h->d_rig_state, eye.data(), sizeof(double) * 32, hipMemcpyHostToDevice));
     h->frames_done = 0;
     // the speculative FAST threshold starts exact (t + 1) and learns from the first batch
     HIPCHK(hipMemset(h->buf[TSLAM_BUF_DET_THR].ptr, 0, sizeof(uint32_t) * (size_t)h->C * h->g.n_levels));
@@ -1319,9 +1319,9 @@ static int set_rig_E(tslam_handle* h, int q_total, const double* base_T_rect) {
     if (!h->d_rig_pose) {
         int rc = dev_alloc(h, (void**)&h->d_rig_pose, sizeof(double) * TS_POSE_DOUBLES * h->B);
         if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rig_stats, sizeof(int32_t) * TS_STATS_INTS * h->B);
-        if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rig_state, sizeof(double) * 16);
+        if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_rig_state, sizeof(double) * 32);   // chain (A, Q)
         if (rc != TSLAM_OK) return rc;
-        const double eye[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+        const double eye[32] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
         HIPCHK(hipMemcpy(h->d_rig_state, eye, sizeof(eye), hipMemcpyHostToDevice));
     }
     HIPCHK(hipMemcpy(h->d_rig_E, e.data(), sizeof(double) * e.size(), hipMemcpyHostToDevice));

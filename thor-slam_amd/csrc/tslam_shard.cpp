@@ -397,8 +397,14 @@ static int submit(tslam_shard_driver* d, const uint8_t* const* images, int n, vo
     d->maxr = peer_records(n, d->world);
     const int k = (int)(d->batches & 1), N = d->world, S = d->S;
     const bool prof = (d->flags & TSLAM_SHARD_PROFILE) != 0;
+    // TSLAM_SHARD_SOLO: rank 0's work only, no exchange (the receive buffers keep what the last
+    // full batch left): rank 0's step on a GPU of its own with the exchange hidden
+    const bool solo = (d->flags & TSLAM_SHARD_SOLO) != 0;
+    const bool xchg = N > 1 && !solo;
+    auto idle = [&](const Rank& r) { return solo && r.rank != 0; };
     for (size_t i = 0; i < d->ranks.size(); ++i) {   // inputs, buffer reuse
         Rank& r = d->ranks[i];
+        if (idle(r)) continue;
         SHCHK(hipSetDevice(r.device));
         SHCHK(hipEventRecord(r.ev_in, streams ? (hipStream_t)streams[i] : nullptr));
         for (hipStream_t s : {FS(d, r), XS(d, r), BS(d, r)}) SHCHK(hipStreamWaitEvent(s, r.ev_in, 0));
@@ -406,15 +412,16 @@ static int submit(tslam_shard_driver* d, const uint8_t* const* images, int n, vo
             for (hipStream_t s : {FS(d, r), XS(d, r)}) SHCHK(hipStreamWaitEvent(s, r.consumed[k], 0));
         RC(tslam_begin_batch(r.h, images[i], n));
     }
-    if (!d->rgbd && N > 1) RC(exchange(d, RAW, k, images));   // straight from the inputs
+    if (!d->rgbd && xchg) RC(exchange(d, RAW, k, images));   // straight from the inputs
     for (size_t i = 0; i < d->ranks.size(); ++i) {   // this batch's last frame becomes prev_raw (after the sends)
         Rank& r = d->ranks[i];
-        if (d->rgbd) continue;
+        if (d->rgbd || idle(r)) continue;
         SHCHK(hipSetDevice(r.device));
         const size_t frame = (size_t)S * d->img;
         SHCHK(hipMemcpyAsync(r.prev_raw, images[i] + (size_t)(n - 1) * frame, frame, hipMemcpyDeviceToDevice, XS(d, r)));
     }
     for (Rank& r : d->ranks) {   // front end of the rank's cameras (+ its stream blocks per peer)
+        if (idle(r)) continue;
         if (prof) {
             RC(run_timed(d, r, TSLAM_SEG_RECTIFY, TSLAM_KERNEL_RECTIFY_PYRAMID, FS(d, r)));
             RC(run_timed(d, r, TSLAM_SEG_DETECT, TSLAM_KERNEL_DETECT, FS(d, r)));
@@ -433,8 +440,9 @@ static int submit(tslam_shard_driver* d, const uint8_t* const* images, int n, vo
         SHCHK(hipEventRecord(r.ev_front, FS(d, r)));
         SHCHK(hipStreamWaitEvent(XS(d, r), r.ev_front, 0));
     }
-    if (!d->rgbd && N > 1) RC(exchange(d, FEAT, k, images));
+    if (!d->rgbd && xchg) RC(exchange(d, FEAT, k, images));
     for (Rank& r : d->ranks) {   // back end
+        if (idle(r)) continue;
         if (!d->rgbd) {
             // the other cameras of frames lo-1 .. hi-1 of this rank's range into the ring
             SHCHK(hipSetDevice(r.device));
@@ -468,8 +476,9 @@ static int submit(tslam_shard_driver* d, const uint8_t* const* images, int n, vo
             }
     }
     if (d->rgbd) {
-        if (N > 1) RC(exchange(d, FEAT, k, images));
+        if (xchg) RC(exchange(d, FEAT, k, images));
         for (Rank& r : d->ranks) {
+            if (idle(r)) continue;
             int lo, hi;
             peer_range(r.rank, n, N, &lo, &hi);
             for (int q = 0; q < N; ++q)
@@ -483,12 +492,12 @@ static int submit(tslam_shard_driver* d, const uint8_t* const* images, int n, vo
     }
     if (d->gather()) {   // every rank's share of the pairs' state into rank 0's ring
         for (Rank& r : d->ranks) {
-            if (r.rank == 0) continue;
+            if (r.rank == 0 || idle(r)) continue;
             RC(span_begin(d, r, TSLAM_SEG_STATE, BS(d, r)));
             RC(tslam_internal_state_blocks(r.h, 1, r.rank, r.rank * S, (r.rank + 1) * S, r.state_buf[k], BS(d, r)));
             RC(span_end(d, r, BS(d, r)));
         }
-        RC(exchange(d, STATE, k, images));
+        if (!solo) RC(exchange(d, STATE, k, images));
         for (Rank& r : d->ranks) {
             if (r.rank != 0) continue;
             RC(span_begin(d, r, TSLAM_SEG_STATE, BS(d, r)));
@@ -498,12 +507,14 @@ static int submit(tslam_shard_driver* d, const uint8_t* const* images, int n, vo
         }
     }
     for (Rank& r : d->ranks) {
+        if (idle(r)) continue;
         RC(tslam_pack_poses(r.h, r.pose_send[k], BS(d, r)));
         RC(span_begin(d, r, TSLAM_SEG_POSE_GATHER, BS(d, r)));
     }
-    RC(exchange(d, POSE, k, images));
+    if (!solo) RC(exchange(d, POSE, k, images));
     for (size_t i = 0; i < d->ranks.size(); ++i) {
         Rank& r = d->ranks[i];
+        if (idle(r)) continue;
         RC(span_end(d, r, BS(d, r)));
         RC(tslam_unpack_poses(r.h, r.pose_recv[k], BS(d, r)));
         RC(run_timed(d, r, TSLAM_SEG_CHAIN, TSLAM_KERNEL_CHAIN, BS(d, r)));
@@ -516,8 +527,11 @@ static int submit(tslam_shard_driver* d, const uint8_t* const* images, int n, vo
         SHCHK(hipSetDevice(r.device));
         SHCHK(hipEventRecord(r.ev_done, BS(d, r)));
         r.done_armed = true;
-        // the caller's stream orders after the batch (results in stream order)
-        SHCHK(hipStreamWaitEvent(streams ? (hipStream_t)streams[i] : nullptr, r.ev_done, 0));
+        // the caller's stream orders after the batch (results in stream order), or with
+        // TSLAM_SHARD_PIPELINE after the batch's last read of its input and receive buffers, so
+        // that the next batch's front end overlaps this batch's back end
+        SHCHK(hipStreamWaitEvent(streams ? (hipStream_t)streams[i] : nullptr,
+                                 (d->flags & TSLAM_SHARD_PIPELINE) ? r.consumed[k] : r.ev_done, 0));
         if (prof) r.timed_batches += 1;
     }
     d->batches += 1;
@@ -601,8 +615,11 @@ int tslam_shard_options(tslam_handle* h, int flags) {
     if (!h) return tslam_internal_fail(TSLAM_EINVAL, "null handle");
     tslam_shard_driver* d = tslam_internal_driver(h);
     if (!d) return tslam_internal_fail(TSLAM_ESTATE, "the handle is not driven (tslam_comm_init / tslam_group_create)");
-    if (flags & ~(TSLAM_SHARD_GATHER | TSLAM_SHARD_RESULTS | TSLAM_SHARD_PROFILE | TSLAM_SHARD_SERIAL))
+    if (flags & ~(TSLAM_SHARD_GATHER | TSLAM_SHARD_RESULTS | TSLAM_SHARD_PROFILE | TSLAM_SHARD_SERIAL |
+                  TSLAM_SHARD_PIPELINE | TSLAM_SHARD_SOLO))
         return tslam_internal_fail(TSLAM_EINVAL, "unknown TSLAM_SHARD_* flag");
+    if ((flags & TSLAM_SHARD_SOLO) && (int)d->ranks.size() != d->world)
+        return tslam_internal_fail(TSLAM_EINVAL, "TSLAM_SHARD_SOLO needs every rank in this process (tslam_group_create)");
     if ((flags & TSLAM_SHARD_GATHER) && d->rgbd)
         return tslam_internal_fail(TSLAM_EINVAL, "the state gather describes a stereo rig");
     // the streams may change (TSLAM_SHARD_SERIAL): everything enqueued so far finishes first

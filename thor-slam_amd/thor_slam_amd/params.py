@@ -140,10 +140,8 @@ class HipSlamConfig(SlamConfig):
         if not (1 <= self.loop_max_keyframes <= 1024 and 1 <= self.loop_signature <= 256 and self.loop_kf_interval >= 1):
             raise ValueError("loop_max_keyframes must be in [1, 1024], loop_signature in [1, 256], loop_kf_interval >= 1")
         if self.devices:
-            if self.batch_size % len(self.devices):
-                raise ValueError("batch_size must be a multiple of len(devices) (equal frame ranges per rank)")
-            if self.ba_window > 0 or self.dense_map:
-                raise ValueError("a sharded rig (devices) runs without local BA and the dense map")
+            if self.dense_map:   # the TSDF integrates on one device; local BA runs on rank 0 (state gather)
+                raise ValueError("a sharded rig (devices) runs without the dense map")
             if self.shard_transport not in ("rccl", "copy"):
                 raise ValueError("shard_transport must be 'rccl' or 'copy'")
         if not 0 <= self.max_hamming <= 253:

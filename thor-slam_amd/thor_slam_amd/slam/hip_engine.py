@@ -47,6 +47,7 @@ state per batch, so with those on every batch is waited for before the next one 
 
 from __future__ import annotations
 
+import collections
 import logging
 import threading
 
@@ -261,10 +262,11 @@ class HipSlamEngine(SlamEngine):
                            for (l, _), r in zip(self._pairs, self._rects)])
             handles.append(h)
         group = HandleGroup(handles, cfg.shard_transport)
-        handles[0].shard_options(gather=True, results=True)
+        handles[0].shard_options(gather=True, results=True, pipeline=True)   # results through the slots
         S = n_cams // world
         part = (cfg.batch_size, S) + tuple(shape[2:])
         self._shard = {"handles": handles, "group": group, "world": world, "S": S, "devices": devs, "batches": 0,
+                       "stamps": collections.deque(),
                        "dev": [[torch.empty(part, dtype=torch.uint8, device=f"cuda:{d}") for _ in range(2)] for d in devs],
                        "host": [[torch.empty(part, dtype=torch.uint8).pin_memory() for _ in range(2)] for _ in devs],
                        "h2d": [[None, None] for _ in devs]}
@@ -298,6 +300,7 @@ class HipSlamEngine(SlamEngine):
         if self._in_flight >= 2:   # rank 0 keeps two batches' results: publish the older first
             self._drain(block=True, limit=1)
         sh["group"].submit(ptrs, n, streams)
+        sh["stamps"].append(stamps)   # the driver's result slots carry frame indices, not timestamps
         sh["batches"] += 1
         self._in_flight += 1
         self._staged, self._staged_imu = [], []
@@ -401,7 +404,8 @@ class HipSlamEngine(SlamEngine):
                 return
             self._in_flight -= 1
             done += 1
-            self._publish(res, list(res["timestamps"]), res["first_frame"])
+            stamps = self._shard["stamps"].popleft() if self._shard is not None else list(res["timestamps"])
+            self._publish(res, stamps, res["first_frame"])
 
     def flush(self) -> None:
         """Run the staged frames through the GPU pipeline and publish the poses of every batch
@@ -935,6 +939,8 @@ class HipSlamEngine(SlamEngine):
         self._map_points, self._map_offset = {}, np.eye(4)
         if self._loop is not None:
             self._loop = _LoopGraph()
+        if self._shard is not None:
+            self._shard["stamps"].clear()
         for h in (self._shard["handles"] if self._shard is not None else [self._handle] if self._handle else []):
             h.reset()
         self._state = TrackingState.INITIALIZING

@@ -7,7 +7,9 @@ TSLAM_SHARD_PROFILE: every kernel and copy of every rank runs alone on one strea
 with HIP events by the driver itself (tslam_shard_timing: rectify .. describe, stream-block pack,
 import of the peers' raw images + stream blocks, match .. rig pose, the pose all-gather, the
 chain).  Prints per rank the µs per step of each segment and its per-GPU compute (the segments
-without the device copies standing in for RCCL) — the N-GPU step when the exchange is hidden —
+without the device copies standing in for RCCL, run one after another), then rank 0's pipelined
+step alone on the GPU (TSLAM_SHARD_SOLO | TSLAM_SHARD_PIPELINE: front end of batch s+1 beside the
+back end of batch s, exchanges skipped) — the N-GPU step when the exchange is hidden —
 the bytes one rank sends per step, and (--one-gpu) the one-GPU step of the same rig and batch
 through the pipelined single handle for the ratio.
 """
@@ -64,6 +66,18 @@ def main() -> None:
     torch.cuda.synchronize()
     per_rank = [h.shard_timing()[0] for h in hs]
     compute = [sum(v for k, v in t.items() if k not in EXCHANGE) for t in per_rank]
+    # rank 0 alone on the GPU, pipelined (TSLAM_SHARD_SOLO | TSLAM_SHARD_PIPELINE): its front end
+    # of batch s + 1 beside its back end of batch s on the driver's own streams, no exchange — the
+    # per-GPU step of an N-GPU node whose exchange is hidden
+    hs[0].shard_options(solo=True, pipeline=True)
+    stream = torch.cuda.current_stream().cuda_stream
+    grp.submit([p[0].data_ptr() for p in parts], B, [stream] * W)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(1, args.steps + 1):
+        grp.submit([p[s * B].data_ptr() for p in parts], B, [stream] * W)
+    torch.cuda.synchronize()
+    solo_us = (time.perf_counter() - t0) / args.steps * 1e6
     sb, pr = hs[0].exchange_sizes()
     fr = B // W + 1   # frames a rank reads of each peer's cameras
     sent = {"raw_images": (W - 1) * fr * S * 640 * 400, "stream_blocks": (W - 1) * fr * S * sb,
@@ -73,7 +87,8 @@ def main() -> None:
         h.close()
     out = {"world": W, "batch": B, "streams": C, "stereo_pairs": len(rects), "driver": "library (copy, serial)",
            "us_per_step_per_rank": per_rank, "per_gpu_compute_us": max(compute),
-           "per_gpu_compute_us_by_rank": compute, "bytes_sent_per_rank_per_step": sent}
+           "per_gpu_compute_us_by_rank": compute, "bytes_sent_per_rank_per_step": sent,
+           "rank0_pipelined_step_us": solo_us}
     if args.one_gpu:
         h = Handle(rects, cfg, max_batch=B)
         if len(rects) > 1:
@@ -96,6 +111,7 @@ def main() -> None:
         torch.cuda.synchronize()
         out["one_gpu_step_us"] = (time.perf_counter() - t0) / args.steps * 1e6
         out["ratio_one_gpu_over_per_gpu"] = out["one_gpu_step_us"] / out["per_gpu_compute_us"]
+        out["ratio_one_gpu_over_rank0_pipelined"] = out["one_gpu_step_us"] / solo_us
         h.close()
     line = json.dumps(out)
     print(line)
