@@ -68,8 +68,11 @@ VALU_PEAK_WINST = 256 * 4 * 2.4e9 / 2
 C2_BATCH = 1024
 # C5 rig frames per step: 4 periods of the 24-frame triangle wave (the resident batch is replayed)
 C5_BATCH = 184
-# C3 rig frames per step (one GPU, and each step of the sharded rig)
-C3_BATCH = 256
+# C3 rig frames per step (one GPU, and each step of the sharded rig): 1024, as C2 — at 8 ranks a
+# rank's back end then solves 128 frames, not 32 (the per-frame latency chains of the pose and rig
+# kernels stop dominating; tools/shard_probe.py: 1-GPU step / per-GPU step 6.1-6.7 at 1024 against
+# 4.2-4.5 at 256, profiles/r4e_probe_c3_w8_b*.json)
+C3_BATCH = 1024
 FP64_MFMA_PEAK_TFS = 78.6   # MI355X FP64 matrix peak (AMD spec; the microarch guide lists no FP64 row)
 # bench kernel label -> device symbol (rocprofv3 / PMC summaries); "pose" is k_corr+k_ransac+k_refine
 KERNEL_SYMBOL = {"rectify_pyramid": "k_rectify_pyramid", "detect": "k_detect", "select": "k_select",
@@ -379,8 +382,9 @@ def tsdf_report(h, us: float, B: int, width: int, height: int) -> dict:
                          "frac": alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": alg}}
 
 
-def cu_masked_stream(dev_index: int, reserve: int, priority: int):
-    """A torch stream whose kernels may use every CU but the last `reserve` (hipExtStreamCreateWithCUMask)."""
+def cu_masked_stream(dev_index: int, reserve: int, priority: int, cus: list | None = None):
+    """A torch stream whose kernels may use every CU but the last `reserve`, or only the CUs `cus`
+    (hipExtStreamCreateWithCUMask)."""
     import ctypes
 
     import torch
@@ -389,7 +393,7 @@ def cu_masked_stream(dev_index: int, reserve: int, priority: int):
     n_cu = torch.cuda.get_device_properties(dev_index).multi_processor_count
     words = (n_cu + 31) // 32
     mask = (ctypes.c_uint32 * words)()
-    for cu in range(n_cu - reserve):
+    for cu in (range(n_cu - reserve) if cus is None else cus):
         mask[cu // 32] |= 1 << (cu % 32)
     st = ctypes.c_void_p()
     torch.cuda.set_device(dev_index)
@@ -613,6 +617,9 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     # (match .. chain) of batch s; the library orders batch s's back after its front and batch s's
     # front after the back of batch s - 2 (ring slots)
     bstream = (cu_masked_stream(dev_index, args.front_cu_reserve, 0) if masked else torch.cuda.Stream()) if args.pipeline else stream
+    if args.back_cu and args.pipeline and not masked:   # experiment: the back kernels on N CUs spread over the chip
+        n_cu = torch.cuda.get_device_properties(dev_index).multi_processor_count
+        bstream = cu_masked_stream(dev_index, 0, 0, [i * n_cu // args.back_cu for i in range(args.back_cu)])
     bsp = bstream.cuda_stream
     back_done = [torch.cuda.Event(), torch.cuda.Event()]
     back_issued = [False, False]
@@ -1221,6 +1228,8 @@ def main() -> None:
                     help="1: front and back kernels on two streams (batch s+1's front overlaps batch s's back)")
     ap.add_argument("--front-cu-reserve", type=int, default=0,
                     help="C4: keep the front / back kernels off the last N CUs (left to the BA chain)")
+    ap.add_argument("--back-cu", type=int, default=0,
+                    help="experiment (c2/c3): the back kernels on a stream restricted to N CUs spread over the chip")
     ap.add_argument("--front-priority", type=int, default=1,
                     help="1: run the front kernels on a high-priority stream (pipelined mode)")
     ap.add_argument("--tsdf", type=int, default=0,

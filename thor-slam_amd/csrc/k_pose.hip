@@ -1084,6 +1084,19 @@ __global__ __launch_bounds__(RIG_THREADS) void k_rig_pose(BatchCtx c) {
         if (tid == 0) write_stats(sout, 2, 0, 0, 0, -1, g);
         return;
     }
+#ifdef TS_RIG_STAMPS   // experiment builds: phase durations of block 0 (s_memrealtime, 100 MHz)
+    uint64_t ts_prev = wall_clock64(), ts_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define RSTAMP(i)                                    \
+    do {                                             \
+        const uint64_t n_ = wall_clock64();          \
+        ts_acc[i] += n_ - ts_prev;                   \
+        ts_prev = n_;                                \
+    } while (0)
+#else
+#define RSTAMP(i) \
+    do {          \
+    } while (0)
+#endif
     if (tid == 0) {
         int nc = 0;
         for (int p = 0; p < P; ++p) {
@@ -1098,6 +1111,7 @@ __global__ __launch_bounds__(RIG_THREADS) void k_rig_pose(BatchCtx c) {
         s_nc = nc;
     }
     __syncthreads();
+    RSTAMP(0);
     const int nc = s_nc;
     int n_total = 0;
     for (int q = 0; q < P; ++q) n_total += c.stats[(size_t)(f * P + q) * TS_STATS_INTS + 1];
@@ -1117,6 +1131,7 @@ __global__ __launch_bounds__(RIG_THREADS) void k_rig_pose(BatchCtx c) {
         }
     }
     __syncthreads();
+    RSTAMP(1);
     // scoring: every candidate on every pair's correspondences (integer counts, order-free)
     int cnt[TS_RIG_MAXP];
     for (int m = 0; m < TS_RIG_MAXP; ++m) cnt[m] = 0;
@@ -1135,6 +1150,7 @@ __global__ __launch_bounds__(RIG_THREADS) void k_rig_pose(BatchCtx c) {
         if (lane == 0) s_cnt[wave][m] = w;
     }
     __syncthreads();
+    RSTAMP(2);
     if (tid == 0) {
         int best = 0, bc = -1;
         for (int m = 0; m < nc; ++m) {
@@ -1153,6 +1169,7 @@ __global__ __launch_bounds__(RIG_THREADS) void k_rig_pose(BatchCtx c) {
     // Gauss-Newton on the body motion (s_M[0] holds the current estimate)
     if (tid < 16) s_M[0][tid] = s_M[best_idx][tid];
     __syncthreads();
+    RSTAMP(3);
     bool fail = false;
     double sq_last = 0.0;
     for (int it = 0; it < c.pp.iters; ++it) {
@@ -1166,6 +1183,7 @@ __global__ __launch_bounds__(RIG_THREADS) void k_rig_pose(BatchCtx c) {
             }
         }
         __syncthreads();
+        RSTAMP(4);
         double acc[N_ACC];
 #pragma unroll
         for (int k = 0; k < N_ACC; ++k) acc[k] = 0.0;
@@ -1215,6 +1233,7 @@ __global__ __launch_bounds__(RIG_THREADS) void k_rig_pose(BatchCtx c) {
             if ((lane & 1) == 0 && (lane >> 1) < N_ACC) s_red[wave][lane >> 1] = w;
         }
         __syncthreads();
+        RSTAMP(5);
         if (tid == 0) {
             double tot[N_ACC];
             for (int k = 0; k < N_ACC; ++k) {
@@ -1259,6 +1278,7 @@ __global__ __launch_bounds__(RIG_THREADS) void k_rig_pose(BatchCtx c) {
             }
         }
         __syncthreads();
+        RSTAMP(6);
         if (s_flag) {
             fail = true;
             break;
@@ -1304,6 +1324,14 @@ __global__ __launch_bounds__(RIG_THREADS) void k_rig_pose(BatchCtx c) {
         if (solve6(s_H, e6, col, L))
             for (int q = 0; q < 6; ++q) pout[32 + q * 6 + tid] = col[q] * sigma2;
     }
+#ifdef TS_RIG_STAMPS
+    __syncthreads();
+    RSTAMP(7);
+    if (tid == 0 && (f == 0 || f == (int)gridDim.x - 1))
+        printf("rig_stamps f=%d cand %lu candT %lu score %lu best %lu gnT %lu gnAcc %lu gnSolve %lu final %lu (x10ns)\n", f,
+               ts_acc[0], ts_acc[1], ts_acc[2], ts_acc[3], ts_acc[4], ts_acc[5], ts_acc[6], ts_acc[7]);
+#endif
+#undef RSTAMP
 }
 
 void launch_rig_pose(const BatchCtx& c, hipStream_t s) {
