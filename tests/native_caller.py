@@ -15,7 +15,8 @@ EXE = ROOT / "tests" / "c" / "build" / "rig_from_calib"
 
 def build() -> Path:
     """Compile the caller with gcc against include/tslam.h and the in-tree libtslam_hip.so."""
-    if not EXE.exists() or EXE.stat().st_mtime < SRC.stat().st_mtime:
+    deps = (SRC, ROOT / "include" / "tslam.h")   # the caller bakes in the header's struct layouts
+    if not EXE.exists() or EXE.stat().st_mtime < max(d.stat().st_mtime for d in deps):
         EXE.parent.mkdir(parents=True, exist_ok=True)
         subprocess.run(["gcc", "-O2", "-Wall", "-Werror", "-std=c11", f"-I{ROOT / 'include'}", str(SRC), "-o", str(EXE),
                         f"-L{LIB_DIR}", "-ltslam_hip", f"-Wl,-rpath,{LIB_DIR}"], check=True)
