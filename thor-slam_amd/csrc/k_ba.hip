@@ -430,6 +430,27 @@ typedef double d4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
+#ifdef TS_BA_STAMPS   // experiment builds: phase durations (s_memrealtime, 100 MHz) printed by one thread
+#define BST_DECL uint64_t bst_prev = wall_clock64(), bst[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define BST(i)                              \
+    do {                                    \
+        const uint64_t n_ = wall_clock64(); \
+        bst[i] += n_ - bst_prev;            \
+        bst_prev = n_;                      \
+    } while (0)
+#define BST_PRINT(tag, cond) \
+    if (cond) printf(tag " %lu %lu %lu %lu %lu %lu %lu %lu (x10ns)\n", bst[0], bst[1], bst[2], bst[3], bst[4], bst[5], bst[6], bst[7])
+#else
+#define BST_DECL \
+    do {         \
+    } while (0)
+#define BST(i) \
+    do {       \
+    } while (0)
+#define BST_PRINT(tag, cond) \
+    do {                     \
+    } while (0)
+#endif
 #define BA_CHUNK 32          // landmarks per LDS tile (96 Schur columns)
 #define BA_QPITCH 80         // doubles per tile column: 160 dwords = 32 mod 64 banks, so the four
                              // columns one MFMA operand read touches fall in disjoint bank halves
@@ -460,6 +481,7 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
     const PairCalib cal = c.calib[a.pair];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int kk = lane >> 4, rc = lane & 15;
+    BST_DECL;
     for (int i = threadIdx.x; i < n * 12; i += blockDim.x) s_T[i / 12][i % 12] = q.T[(size_t)a.order[i / 12] * 16 + i % 12];
     d4v acc[4];
     for (int t = 0; t < 4; ++t) acc[t] = (d4v){0.0, 0.0, 0.0, 0.0};
@@ -467,6 +489,7 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
     for (int l0 = blockIdx.x * BA_CHUNK; l0 < L; l0 += gridDim.x * BA_CHUNK) {
         const int nl = min(BA_CHUNK, L - l0);
         lds_barrier();
+        BST(0);
         // every global read of the chunk is one level of indexing (the k_ba_slots table), issued
         // up front: slot (li, ci) = thread / TS_BA_MAXW, thread % TS_BA_MAXW; landmark li = thread
         const int li = threadIdx.x / TS_BA_MAXW, ci = threadIdx.x - li * TS_BA_MAXW;
@@ -540,6 +563,7 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
             for (int j = 0; j < 3; ++j) s_X[threadIdx.x][j] = Xl[j];
         }
         lds_barrier();
+        BST(1);
         // 1. Jacobians of every (landmark, camera) observation of the chunk; W_o stays in this
         //    thread's registers for step 3 (and goes to HBM for the next pass's landmark update)
         double Wr[18];
@@ -569,6 +593,7 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
             for (int i = 0; i < 3; ++i) vg[6 + i] = (Jp[0][i] * res[0] + Jp[1][i] * res[1]) + Jp[2][i] * res[2];
         }
         lds_barrier();   // LDS only: the HBM stores above drain behind it
+        BST(2);
         // 2. per-landmark factor
         if (threadIdx.x < BA_CHUNK) {
             const int li = threadIdx.x, r = l0 + li;
@@ -604,6 +629,7 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
             }
         }
         lds_barrier();
+        BST(3);
         // 3. Schur columns: thread (landmark, camera) writes the camera's 6 rows of the landmark's
         //    3 columns, (W_o L^-T) or zeros
         {
@@ -622,6 +648,7 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
             }
         }
         lds_barrier();
+        BST(4);
         // 4. C += Q^T Q over the chunk's columns (zero columns past nl contribute nothing)
         if (wave < 4) {
             const int ksteps = (3 * nl + 3) >> 2;
@@ -635,11 +662,13 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
                 acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b3, acc[3], 0, 0, 0);
             }
         }
+        BST(5);
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {   // algorithmic flops of the dense Schur product
         const double rows = 6.0 * n + 1.0;
         q.flops[0] += 2.0 * rows * rows * 3.0 * L;
     }
+    BST_PRINT("schur b0: stage+T, lm update, jacobians, factor, columns, mfma, -, -", blockIdx.x == 0 && threadIdx.x == 0);
     if (blockIdx.x * BA_CHUNK >= L || wave >= 4) return;   // no chunk: no partial
     double* out = q.part + (size_t)blockIdx.x * 64 * 64;
     const int a0 = 16 * wave;
@@ -689,7 +718,7 @@ __global__ __launch_bounds__(256) void k_ba_reduce(BatchCtx c, BaArgs a) {
 // Camera updates R <- cayley(w) R, t <- ... + rho follow.
 #define BA_SOLVE_WAVES 8
 #define BA_SP 65   // LDS row pitch of S (doubles)
-__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, BaArgs a) {
+__device__ __forceinline__ void ba_solve_block(const BatchCtx& c, const BaArgs& a) {
     // the elimination's a - l * b updates as single FMAs (the library builds with contraction off
     // for the bit-exact pose kernels; this solve is only held to 1e-9 against the oracle's LU)
 #pragma clang fp contract(fast)
@@ -710,6 +739,7 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, Ba
         return;
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    BST_DECL;
     // stage C (every thread's 8 loads in flight at once) and the camera blocks
     constexpr int NL = 4096 / (64 * BA_SOLVE_WAVES);
     double cv[NL];
@@ -718,6 +748,7 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, Ba
     if ((int)threadIdx.x < n * 27) s_U[threadIdx.x] = q.cam_U[threadIdx.x];
     if ((int)threadIdx.x < n) s_iw[threadIdx.x] = q.imu[(size_t)a.order[threadIdx.x] * 10 + 9];   // factor weights
     __syncthreads();
+    BST(0);
     // S_ik = -C[i+6][k+6] (+ U + lam inside a camera block), lower triangle; row i's right-hand
     // side -g_c + C[i+6][60] into s_x[i] (read back by wave 0)
 #pragma unroll
@@ -740,6 +771,7 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, Ba
         s_S[i * BA_SP + k] = v;
     }
     __syncthreads();
+    BST(1);
     bool any_imu = false;
     for (int cc = 1; cc < n; ++cc) any_imu = any_imu || s_iw[cc] > 0.0;   // (uniform: LDS broadcast)
     if (any_imu && threadIdx.x == 0) {
@@ -805,6 +837,7 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, Ba
         factor(0, col);
     }
     __syncthreads();
+    BST(2);
     for (int b = 0; b < nb; ++b) {
         const int pb = b & 1;
         if (w == 0) {
@@ -856,6 +889,7 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, Ba
         }
         __syncthreads();
     }
+    BST(3);
     if (w == 0) {
         // D L^T x = y: x_i = y_i / d_i - sum_{k > i} l_ki x_k (the row's l_ki preloaded, so the
         // chain is readlane -> FMA only)
@@ -873,6 +907,7 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, Ba
         if (lane == 0) s_ok = good;
     }
     __syncthreads();
+    BST(4);
     const bool good_all = s_ok != 0;
     const bool ok = good_all;
     if (threadIdx.x == 0) q.counts[2] = ok;
@@ -900,7 +935,12 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, Ba
             T[4 * ii + 3] = tn[ii];
         }
     }
+    BST(5);
+    BST_PRINT("solve: stage C, build S, panel 0, block steps, backsub, update, -, -", threadIdx.x == 1);
 }
+
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, BaArgs a) { ba_solve_block(c, a); }
+
 
 // The last iteration's landmark update and the write-back of the window's landmarks: 16 lanes
 // per landmark (lane = window camera): W_o^T dc_o of each observation (slot table), summed over
