@@ -838,7 +838,13 @@ __device__ __forceinline__ void ba_solve_block(const BatchCtx& c, const BaArgs& 
     }
     __syncthreads();
     BST(2);
+#ifdef TS_BA_STAMPS
+    uint64_t ls_work = 0, ls_wait = 0;   // per thread: the block steps' own work and barrier waits
+#endif
     for (int b = 0; b < nb; ++b) {
+#ifdef TS_BA_STAMPS
+        const uint64_t ls_t0 = wall_clock64();
+#endif
         const int pb = b & 1;
         if (w == 0) {
             if (b + 1 < nb) {
@@ -887,7 +893,14 @@ __device__ __forceinline__ void ba_solve_block(const BatchCtx& c, const BaArgs& 
                 }
             }
         }
+#ifdef TS_BA_STAMPS
+        const uint64_t ls_t1 = wall_clock64();
+        ls_work += ls_t1 - ls_t0;
+#endif
         __syncthreads();
+#ifdef TS_BA_STAMPS
+        ls_wait += wall_clock64() - ls_t1;
+#endif
     }
     BST(3);
     if (w == 0) {
@@ -937,6 +950,10 @@ __device__ __forceinline__ void ba_solve_block(const BatchCtx& c, const BaArgs& 
     }
     BST(5);
     BST_PRINT("solve: stage C, build S, panel 0, block steps, backsub, update, -, -", threadIdx.x == 1);
+#ifdef TS_BA_STAMPS
+    if (threadIdx.x == 0 || threadIdx.x == 64 || threadIdx.x == 448)
+        printf("solve steps thread %d: work %lu wait %lu (x10ns)\n", (int)threadIdx.x, ls_work, ls_wait);
+#endif
 }
 
 __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, BaArgs a) { ba_solve_block(c, a); }
