@@ -405,24 +405,6 @@ __device__ __forceinline__ void ba_obs_jac(const double* T, const double* X, dou
     }
 }
 
-// One wave per (window camera, element): U_c = sum J_c^T J_c, g_c = sum J_c^T r over the camera's
-// observations (lanes stride them, 4 accumulators, DPP wave sum: a fixed order).
-__device__ void ba_camred_wave(const BaPair& q, int WK, int ci, int e, int lane) {
-    const int o0 = q.cam_off[ci], o1 = q.cam_off[ci + 1];
-    const double* src = q.obs_Ug + (size_t)e * WK;
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    int o = o0 + lane;
-    for (; o + 192 < o1; o += 256) {
-        s0 += src[o];
-        s1 += src[o + 64];
-        s2 += src[o + 128];
-        s3 += src[o + 192];
-    }
-    for (; o < o1; o += 64) s0 += src[o];
-    const double s = wave_sum_f64((s0 + s1) + (s2 + s3));
-    if (lane == 0) q.cam_U[(size_t)ci * 27 + e] = s;
-}
-
 typedef double d4v __attribute__((ext_vector_type(4)));
 
 // Workgroup barrier ordering LDS only: waits for this wave's LDS operations, not for its HBM
@@ -459,19 +441,27 @@ __device__ __forceinline__ void lds_barrier() {
 // The landmark side of one Gauss-Newton step, fused; per chunk of BA_CHUNK landmarks:
 //   1. one thread per (landmark, camera) with an observation: J_c, J_p, r (ba_obs_jac) ->
 //      W_o = J_c^T J_p and J_p^T J_p | J_p^T r into LDS; W_o (for the back substitution) and
-//      J_c^T J_c | J_c^T r (summed per camera by k_ba_reduce) to HBM;
+//      J_c^T J_c | J_c^T r into LDS;
 //   2. one thread per landmark: V = lam I + sum_c J_p^T J_p (camera order), g_p, L = chol(V),
-//      y = L^-1 g_p (L, g_p to HBM for the back substitution);
+//      y = L^-1 g_p (L, g_p to HBM for the back substitution); beside them one thread per (camera,
+//      element) sums the chunk's J_c^T J_c | J_c^T r over its landmarks (landmark order) into the
+//      block's camera partial;
 //   3. the chunk's Schur columns into an LDS tile Q[3 * BA_CHUNK][64]: column 3l + j holds
 //      (W_o L^-T)[:, j] in the 6 rows of the observing camera (0 when unobserved), y_j in row 60;
 //   4. C += Q^T Q on the FP64 matrix cores (v_mfma_f64_16x16x4f64), waves 0-3 own 16 rows each.
-// Blocks stride the chunks; each block that had a chunk writes its 64 x 64 partial.
+// Blocks stride the chunks; each block that had a chunk writes its 64 x 64 partial and its camera
+// partial (TS_BA_PART doubles per block: C, then [camera][27]), which k_ba_reduce sums in a fixed
+// order.  The camera sums stay in the block instead of 27 scattered 8-byte stores per observation.
 __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArgs a) {
 #pragma clang fp contract(fast)   // single FMAs in the landmark chains (held to 1e-9, as k_ba_solve)
-    __shared__ double s_Q[3 * BA_CHUNK * BA_QPITCH];
+    // the Schur tile Q (phases 3-4) and the observations' camera blocks (phases 1-2) share LDS
+    constexpr int QN = 3 * BA_CHUNK * BA_QPITCH, CN = BA_CHUNK * TS_BA_MAXW * 27;
+    __shared__ double s_buf[QN > CN ? QN : CN];
+    double* const s_Q = s_buf;
+    double(*const s_cu)[TS_BA_MAXW][27] = reinterpret_cast<double(*)[TS_BA_MAXW][27]>(s_buf);
     __shared__ double s_Vg[BA_CHUNK][TS_BA_MAXW][9];
     __shared__ int s_has[BA_CHUNK][TS_BA_MAXW];
-    __shared__ double s_L[BA_CHUNK][6];
+    __shared__ double s_L[BA_CHUNK][9];   // inverse-diagonal Cholesky factor | y
     __shared__ double s_T[TS_BA_MAXW][12];
     __shared__ double s_bs[BA_CHUNK][TS_BA_MAXW][3];
     __shared__ double s_X[BA_CHUNK][3];
@@ -486,6 +476,8 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
     d4v acc[4];
     for (int t = 0; t < 4; ++t) acc[t] = (d4v){0.0, 0.0, 0.0, 0.0};
     const bool bsub = a.fused_backsub && q.counts[2];   // the previous solve succeeded
+    const int cu_item = (int)threadIdx.x - BA_CHUNK;     // (camera, element) of the camera sums
+    double cam_acc = 0.0;
     for (int l0 = blockIdx.x * BA_CHUNK; l0 < L; l0 += gridDim.x * BA_CHUNK) {
         const int nl = min(BA_CHUNK, L - l0);
         lds_barrier();
@@ -582,15 +574,19 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
                     Wr[3 * i + j] = w;
                     Wg[3 * i + j] = w;
                 }
+            double* cu = s_cu[li][ci];
             int e = 0;
             for (int i = 0; i < 6; ++i)
-                for (int j = i; j < 6; ++j) q.obs_Ug[(size_t)(e++) * WK + o] = (Jc[0][i] * Jc[0][j] + Jc[1][i] * Jc[1][j]) + Jc[2][i] * Jc[2][j];
-            for (int i = 0; i < 6; ++i) q.obs_Ug[(size_t)(21 + i) * WK + o] = (Jc[0][i] * res[0] + Jc[1][i] * res[1]) + Jc[2][i] * res[2];
+                for (int j = i; j < 6; ++j) cu[e++] = (Jc[0][i] * Jc[0][j] + Jc[1][i] * Jc[1][j]) + Jc[2][i] * Jc[2][j];
+            for (int i = 0; i < 6; ++i) cu[21 + i] = (Jc[0][i] * res[0] + Jc[1][i] * res[1]) + Jc[2][i] * res[2];
             double* vg = s_Vg[li][ci];
             e = 0;
             for (int i = 0; i < 3; ++i)
                 for (int j = i; j < 3; ++j) vg[e++] = (Jp[0][i] * Jp[0][j] + Jp[1][i] * Jp[1][j]) + Jp[2][i] * Jp[2][j];
             for (int i = 0; i < 3; ++i) vg[6 + i] = (Jp[0][i] * res[0] + Jp[1][i] * res[1]) + Jp[2][i] * res[2];
+        } else if (li < BA_CHUNK) {
+#pragma unroll
+            for (int e = 0; e < 27; ++e) s_cu[li][ci][e] = 0.0;
         }
         lds_barrier();   // LDS only: the HBM stores above drain behind it
         BST(2);
@@ -613,20 +609,19 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
             const double y0 = vg[6] / l00, y1 = (vg[7] - l10 * y0) / l11, y2 = ((vg[8] - l20 * y0) - l21 * y1) / l22;
             s_L[li][0] = 1.0 / l00; s_L[li][1] = l10; s_L[li][2] = 1.0 / l11; s_L[li][3] = l20; s_L[li][4] = l21;
             s_L[li][5] = 1.0 / l22;
-            const double yv[3] = {y0, y1, y2};
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {   // rows 60 (y) .. 63 of the landmark's three columns
-                double* colq = s_Q + (3 * li + j) * BA_QPITCH;
-                colq[60] = live ? yv[j] : 0.0;
-                colq[61] = 0.0;
-                colq[62] = 0.0;
-                colq[63] = 0.0;
-            }
+            s_L[li][6] = live ? y0 : 0.0;   // row 60 of the landmark's three columns (phase 3)
+            s_L[li][7] = live ? y1 : 0.0;
+            s_L[li][8] = live ? y2 : 0.0;
             if (live) {
                 q.lm_L[r] = l00; q.lm_L[(size_t)WK + r] = l10; q.lm_L[(size_t)2 * WK + r] = l11;
                 q.lm_L[(size_t)3 * WK + r] = l20; q.lm_L[(size_t)4 * WK + r] = l21; q.lm_L[(size_t)5 * WK + r] = l22;
                 q.lm_gp[r] = vg[6]; q.lm_gp[(size_t)WK + r] = vg[7]; q.lm_gp[(size_t)2 * WK + r] = vg[8];
             }
+        } else if (cu_item < n * 27) {   // the chunk's camera sums, landmark order
+            const int cc = cu_item / 27, e = cu_item - 27 * cc;
+            double sum = 0.0;
+            for (int l = 0; l < nl; ++l) sum += s_cu[l][cc][e];
+            cam_acc += sum;
         }
         lds_barrier();
         BST(3);
@@ -646,15 +641,32 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
                 s_Q[(3 * li + 1) * BA_QPITCH + row] = o >= 0 ? z1 : 0.0;
                 s_Q[(3 * li + 2) * BA_QPITCH + row] = o >= 0 ? z2 : 0.0;
             }
+            if (ci == 0) {
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {   // rows 60 (y) .. 63 of the landmark's three columns
+                    double* colq = s_Q + (3 * li + j) * BA_QPITCH;
+                    colq[60] = Lm[6 + j];
+                    colq[61] = 0.0;
+                    colq[62] = 0.0;
+                    colq[63] = 0.0;
+                }
+            }
         }
         lds_barrier();
         BST(4);
         // 4. C += Q^T Q over the chunk's columns (zero columns past nl contribute nothing)
         if (wave < 4) {
             const int ksteps = (3 * nl + 3) >> 2;
+            // the next k-step's operands load while this one's four MFMAs run
+            const double* col = s_Q + kk * BA_QPITCH + rc;
+            double n0 = col[0], n1 = col[16], n2 = col[32], n3 = col[48];
             for (int st = 0; st < ksteps; ++st) {
-                const double* col = s_Q + (4 * st + kk) * BA_QPITCH;
-                const double b0 = col[rc], b1 = col[16 + rc], b2 = col[32 + rc], b3 = col[48 + rc];
+                const double b0 = n0, b1 = n1, b2 = n2, b3 = n3;
+                const double* nx = col + 4 * min(st + 1, ksteps - 1) * BA_QPITCH;
+                n0 = nx[0];
+                n1 = nx[16];
+                n2 = nx[32];
+                n3 = nx[48];
                 const double av = wave == 0 ? b0 : wave == 1 ? b1 : wave == 2 ? b2 : b3;
                 acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b0, acc[0], 0, 0, 0);
                 acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b1, acc[1], 0, 0, 0);
@@ -669,8 +681,10 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
         q.flops[0] += 2.0 * rows * rows * 3.0 * L;
     }
     BST_PRINT("schur b0: stage+T, lm update, jacobians, factor, columns, mfma, -, -", blockIdx.x == 0 && threadIdx.x == 0);
-    if (blockIdx.x * BA_CHUNK >= L || wave >= 4) return;   // no chunk: no partial
-    double* out = q.part + (size_t)blockIdx.x * 64 * 64;
+    if (blockIdx.x * BA_CHUNK >= L) return;   // no chunk: no partial
+    if (cu_item >= 0 && cu_item < n * 27) q.part[(size_t)blockIdx.x * TS_BA_PART + 4096 + cu_item] = cam_acc;
+    if (wave >= 4) return;
+    double* out = q.part + (size_t)blockIdx.x * TS_BA_PART;
     const int a0 = 16 * wave;
     // C/D layout of v_mfma_f64_16x16x4f64: col = lane & 15, row = (lane >> 4) + 4 * reg
 #pragma unroll
@@ -679,27 +693,28 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
         for (int rg = 0; rg < 4; ++rg) out[(size_t)(a0 + kk + 4 * rg) * 64 + 16 * t + rc] = acc[t][rg];
 }
 
-// Fixed-order sum of the partials of the blocks that had a chunk: block = 64 elements of C,
-// 4 waves each summing every 4th partial, then the 4 wave sums in order.  Blocks 64.. reduce the
-// camera blocks U_c, g_c.
+// Fixed-order sum of the partials of the blocks that had a chunk: block = 64 elements of a
+// partial, 4 waves each summing every 4th partial, then the 4 wave sums in order.  Elements 0..4095
+// are C, 4096.. the camera blocks U_c, g_c ([camera][27]).
 __global__ __launch_bounds__(256) void k_ba_reduce(BatchCtx c, BaArgs a) {
     __shared__ double s_p[4][64];
     BaPair q = ba_pair(c, a, a.pair);
-    if (blockIdx.x >= 64) {   // the camera side: one wave per (camera, element)
-        const int item = (blockIdx.x - 64) * 4 + (int)(threadIdx.x >> 6);
-        if (item < a.n_order * 27) ba_camred_wave(q, a.W * c.g.K, item / 27, item % 27, threadIdx.x & 63);
-        return;
-    }
     const int L = q.counts[1];
     const int np = min(a.nsplit, (L + BA_CHUNK - 1) / BA_CHUNK);
     const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
     const int e = blockIdx.x * 64 + lane;
+    const bool live = e < 4096 + a.n_order * 27;
     double s = 0.0;
+    if (live) {
 #pragma unroll 8
-    for (int b = grp; b < np; b += 4) s += q.part[(size_t)b * 4096 + e];
+        for (int b = grp; b < np; b += 4) s += q.part[(size_t)b * TS_BA_PART + e];
+    }
     s_p[grp][lane] = s;
     __syncthreads();
-    if (grp == 0) q.C[e] = ((s_p[0][lane] + s_p[1][lane]) + s_p[2][lane]) + s_p[3][lane];
+    if (grp != 0 || !live) return;
+    const double v = ((s_p[0][lane] + s_p[1][lane]) + s_p[2][lane]) + s_p[3][lane];
+    if (e < 4096) q.C[e] = v;
+    else q.cam_U[e - 4096] = v;
 }
 
 // Reduced camera system (camera 0 = gauge): S = blockdiag(U + lam) - C, b = -g_c + C[:, 60].
@@ -1069,7 +1084,7 @@ static void launch_ba_linearize(const BatchCtx& c, const BaArgs& a, int it, hipS
     if (rec) (void)hipEventRecord(timing->ev[2 * timing->used], s);
     hipLaunchKernelGGL(k_ba_schur, dim3(a.nsplit), dim3(BA_SCHUR_THREADS), 0, s, c, ai);
     if (rec) (void)hipEventRecord(timing->ev[2 * timing->used++ + 1], s);
-    hipLaunchKernelGGL(k_ba_reduce, dim3(64 + (a.n_order * 27 + 3) / 4), dim3(256), 0, s, c, a);
+    hipLaunchKernelGGL(k_ba_reduce, dim3(64 + (a.n_order * 27 + 63) / 64), dim3(256), 0, s, c, a);
 }
 
 static void launch_ba_backsub(const BatchCtx& c, const BaArgs& a, hipStream_t s) {

@@ -22,8 +22,10 @@
 #define TS_BA_MAXD 54   // 6 * (TS_BA_MAXW - 1): the reduced camera system without the gauge
 #define TS_BA_SPLIT 256 // blocks of the Schur product (32-landmark chunks dealt over them; 8192 landmarks in one round)
 #define TS_BA_TILES 128 // scan tiles of a solve's compaction (landmark + observation tiles)
+#define TS_BA_PART (4096 + 288) // doubles per Schur block partial: C [64][64], then the camera blocks [MAXW][27]
 
 static_assert(6 * TS_BA_MAXW + 1 <= 64, "the BA camera system (6 rows per keyframe + rhs) is 64 wide");
+static_assert(TS_BA_MAXW * 27 <= 288, "a Schur partial holds every window camera's 27 sums");
 
 struct BaStore {
     // persistent, pair 0 (pair stride: W*16 doubles for T/Tfe, W*K for u/v/d/lm, W*K*3 for X)
@@ -57,11 +59,10 @@ struct BaStore {
     double* lo_uvd;    // [WK * MAXW][4]  u, v, d, 0
     double* lo_W;      // [WK * MAXW][18] W_o = J_c^T J_p (6x3, row-major)
     double* Xc;        // [WK][3] position of compact landmark r during the solve (X[lm_id[r]] after it)
-    double* obs_Ug;    // [27][WK]  J_c^T J_c (upper 21) | J_c^T r (6), structure-of-arrays
     double* obs_Vg;    // [WK][9]   J_p^T J_p (upper 6) | J_p^T r (3), gathered per landmark
     double* lm_L;      // [6][WK]   (structure-of-arrays)   Cholesky factor of V_i (L00 L10 L11 L20 L21 L22)
     double* lm_gp;     // [3][WK]
-    double* part;      // [TS_BA_SPLIT][64][64]
+    double* part;      // [TS_BA_SPLIT][TS_BA_PART] per Schur block: C partial, then [camera][27] partial
     double* C;         // [64][64]
     double* cam_U;     // [W][27]
     double* dc;        // [W][6]
@@ -103,7 +104,7 @@ struct BaPair {
     int64_t* gid;
     int32_t *remap, *cnt, *li, *lm_id, *camobs, *obs_cam, *obs_k, *obs_id, *cam_off, *counts, *tiles, *lo_o;
     uint8_t* keep;
-    double *lo_uvd, *lo_W, *Xc, *obs_Ug, *obs_Vg, *lm_L, *lm_gp, *part, *C, *cam_U, *dc, *flops;
+    double *lo_uvd, *lo_W, *Xc, *obs_Vg, *lm_L, *lm_gp, *part, *C, *cam_U, *dc, *flops;
     double* imu;
 };
 
@@ -128,9 +129,9 @@ __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, in
     q.counts = s.counts + 4 * p;
     q.tiles = s.tiles + p * 2 * TS_BA_TILES;
     q.lo_o = s.lo_o + p * WK * M; q.lo_uvd = s.lo_uvd + p * WK * M * 4; q.lo_W = s.lo_W + p * WK * M * 18;
-    q.Xc = s.Xc + p * WK * 3; q.obs_Ug = s.obs_Ug + p * WK * 27; q.obs_Vg = s.obs_Vg + p * WK * 9;
+    q.Xc = s.Xc + p * WK * 3; q.obs_Vg = s.obs_Vg + p * WK * 9;
     q.lm_L = s.lm_L + p * WK * 6; q.lm_gp = s.lm_gp + p * WK * 3;
-    q.part = s.part + p * (size_t)TS_BA_SPLIT * 4096; q.C = s.C + p * 4096;
+    q.part = s.part + p * (size_t)TS_BA_SPLIT * TS_BA_PART; q.C = s.C + p * 4096;
     q.cam_U = s.cam_U + p * W * 27; q.dc = s.dc + p * W * 6; q.flops = s.flops;
     q.imu = s.imu + p * W * 10;
     return q;
