@@ -541,8 +541,9 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
                     rhs[j] = -gp[j] - sum;
                 }
                 const double L0 = Lf[0], L1 = Lf[1], L2 = Lf[2], L3 = Lf[3], L4 = Lf[4], L5 = Lf[5];
-                const double y0 = rhs[0] / L0, y1 = (rhs[1] - L1 * y0) / L2, y2 = ((rhs[2] - L3 * y0) - L4 * y1) / L5;
-                const double x2 = y2 / L5, x1 = (y1 - L4 * x2) / L2, x0 = ((y0 - L1 * x1) - L3 * x2) / L0;
+                // L0, L2, L5 are the inverse diagonal (lm_L)
+                const double y0 = rhs[0] * L0, y1 = (rhs[1] - L1 * y0) * L2, y2 = ((rhs[2] - L3 * y0) - L4 * y1) * L5;
+                const double x2 = y2 * L5, x1 = (y1 - L4 * x2) * L2, x0 = ((y0 - L1 * x1) - L3 * x2) * L0;
                 Xl[0] += x0;
                 Xl[1] += x1;
                 Xl[2] += x2;
@@ -599,22 +600,23 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
                 if (s_has[li][ci])
 #pragma unroll
                     for (int e = 0; e < 9; ++e) vg[e] += s_Vg[li][ci][e];
-            const double l00 = sqrt(vg[0] > 1e-300 ? vg[0] : 1e-300);
-            const double l10 = vg[1] / l00, l20 = vg[2] / l00;
+            // one reciprocal per pivot, multiplications after it (the chain had 9 divisions)
+            const double i00 = 1.0 / sqrt(vg[0] > 1e-300 ? vg[0] : 1e-300);
+            const double l10 = vg[1] * i00, l20 = vg[2] * i00;
             const double d11 = vg[3] - l10 * l10;
-            const double l11 = sqrt(d11 > 1e-300 ? d11 : 1e-300);
-            const double l21 = (vg[4] - l20 * l10) / l11;
+            const double i11 = 1.0 / sqrt(d11 > 1e-300 ? d11 : 1e-300);
+            const double l21 = (vg[4] - l20 * l10) * i11;
             const double d22 = (vg[5] - l20 * l20) - l21 * l21;
-            const double l22 = sqrt(d22 > 1e-300 ? d22 : 1e-300);
-            const double y0 = vg[6] / l00, y1 = (vg[7] - l10 * y0) / l11, y2 = ((vg[8] - l20 * y0) - l21 * y1) / l22;
-            s_L[li][0] = 1.0 / l00; s_L[li][1] = l10; s_L[li][2] = 1.0 / l11; s_L[li][3] = l20; s_L[li][4] = l21;
-            s_L[li][5] = 1.0 / l22;
+            const double i22 = 1.0 / sqrt(d22 > 1e-300 ? d22 : 1e-300);
+            const double y0 = vg[6] * i00, y1 = (vg[7] - l10 * y0) * i11, y2 = ((vg[8] - l20 * y0) - l21 * y1) * i22;
+            s_L[li][0] = i00; s_L[li][1] = l10; s_L[li][2] = i11; s_L[li][3] = l20; s_L[li][4] = l21;
+            s_L[li][5] = i22;
             s_L[li][6] = live ? y0 : 0.0;   // row 60 of the landmark's three columns (phase 3)
             s_L[li][7] = live ? y1 : 0.0;
             s_L[li][8] = live ? y2 : 0.0;
             if (live) {
-                q.lm_L[r] = l00; q.lm_L[(size_t)WK + r] = l10; q.lm_L[(size_t)2 * WK + r] = l11;
-                q.lm_L[(size_t)3 * WK + r] = l20; q.lm_L[(size_t)4 * WK + r] = l21; q.lm_L[(size_t)5 * WK + r] = l22;
+                q.lm_L[r] = i00; q.lm_L[(size_t)WK + r] = l10; q.lm_L[(size_t)2 * WK + r] = i11;
+                q.lm_L[(size_t)3 * WK + r] = l20; q.lm_L[(size_t)4 * WK + r] = l21; q.lm_L[(size_t)5 * WK + r] = i22;
                 q.lm_gp[r] = vg[6]; q.lm_gp[(size_t)WK + r] = vg[7]; q.lm_gp[(size_t)2 * WK + r] = vg[8];
             }
         } else if (cu_item < n * 27) {   // the chunk's camera sums, landmark order
@@ -1019,12 +1021,12 @@ __global__ __launch_bounds__(256) void k_ba_backsub(BatchCtx c, BaArgs a) {
         for (int i = 0; i < 3; ++i) {
             double v = rhs[i];
             for (int k = 0; k < i; ++k) v -= Lm[i][k] * y[k];
-            y[i] = v / Lm[i][i];
+            y[i] = v * Lm[i][i];   // the diagonal is stored inverted
         }
         for (int i = 2; i >= 0; --i) {
             double v = y[i];
             for (int k = i + 1; k < 3; ++k) v -= Lm[k][i] * x[k];
-            x[i] = v / Lm[i][i];
+            x[i] = v * Lm[i][i];
         }
     }
     const int id = q.lm_id[r];

@@ -60,7 +60,7 @@ struct BaStore {
     double* lo_W;      // [WK * MAXW][18] W_o = J_c^T J_p (6x3, row-major)
     double* Xc;        // [WK][3] position of compact landmark r during the solve (X[lm_id[r]] after it)
     double* obs_Vg;    // [WK][9]   J_p^T J_p (upper 6) | J_p^T r (3), gathered per landmark
-    double* lm_L;      // [6][WK]   (structure-of-arrays)   Cholesky factor of V_i (L00 L10 L11 L20 L21 L22)
+    double* lm_L;      // [6][WK]   (structure-of-arrays)   Cholesky factor of V_i (1/L00 L10 1/L11 L20 L21 1/L22: diagonal inverted)
     double* lm_gp;     // [3][WK]
     double* part;      // [TS_BA_SPLIT][TS_BA_PART] per Schur block: C partial, then [camera][27] partial
     double* C;         // [64][64]
