@@ -735,6 +735,10 @@ __global__ __launch_bounds__(256) void k_ba_reduce(BatchCtx c, BaArgs a) {
 // Camera updates R <- cayley(w) R, t <- ... + rho follow.
 #define BA_SOLVE_WAVES 8
 #define BA_SP 65   // LDS row pitch of S (doubles)
+// `handoff`: C and the camera blocks were published by other workgroups of this launch with
+// write-through stores (k_ba_reduce_solve), so they are read with agent-scope loads that bypass
+// this CU's caches.
+template <bool handoff>
 __device__ __forceinline__ void ba_solve_block(const BatchCtx& c, const BaArgs& a) {
     // the elimination's a - l * b updates as single FMAs (the library builds with contraction off
     // for the bit-exact pose kernels; this solve is only held to 1e-9 against the oracle's LU)
@@ -761,8 +765,13 @@ __device__ __forceinline__ void ba_solve_block(const BatchCtx& c, const BaArgs& 
     constexpr int NL = 4096 / (64 * BA_SOLVE_WAVES);
     double cv[NL];
 #pragma unroll
-    for (int k = 0; k < NL; ++k) cv[k] = q.C[threadIdx.x + 64 * BA_SOLVE_WAVES * k];
-    if ((int)threadIdx.x < n * 27) s_U[threadIdx.x] = q.cam_U[threadIdx.x];
+    for (int k = 0; k < NL; ++k) {
+        const double* src = q.C + threadIdx.x + 64 * BA_SOLVE_WAVES * k;
+        cv[k] = handoff ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *src;
+    }
+    if ((int)threadIdx.x < n * 27)
+        s_U[threadIdx.x] = handoff ? __hip_atomic_load(q.cam_U + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : q.cam_U[threadIdx.x];
     if ((int)threadIdx.x < n) s_iw[threadIdx.x] = q.imu[(size_t)a.order[threadIdx.x] * 10 + 9];   // factor weights
     __syncthreads();
     BST(0);
@@ -973,7 +982,45 @@ __device__ __forceinline__ void ba_solve_block(const BatchCtx& c, const BaArgs& 
 #endif
 }
 
-__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, BaArgs a) { ba_solve_block(c, a); }
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, BaArgs a) { ba_solve_block<false>(c, a); }
+
+// k_ba_reduce and k_ba_solve in one launch (a stereo pair's own solve): the reduction's blocks
+// (k_ba_reduce's fixed order, waves 0-3) publish their sums with write-through (agent-scope)
+// stores, drain them (vmcnt(0)) and count themselves in; the block that arrives last runs the
+// solve, reading the sums with agent-scope loads.  No agent-scope release fence: on this GPU it
+// writes back the whole L2 of the XCD (the iteration's Schur partials and Jacobian blocks), which
+// cost more than the launch it saves (measured: 0.300 against 0.260 ms per keyframe).
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_solve(BatchCtx c, BaArgs a) {
+    __shared__ double s_p[4][64];
+    __shared__ int s_last;
+    BaPair q = ba_pair(c, a, a.pair);
+    const int L = q.counts[1];
+    const int np = min(a.nsplit, (L + BA_CHUNK - 1) / BA_CHUNK);
+    const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+    const int e = blockIdx.x * 64 + lane;
+    const bool live = e < 4096 + a.n_order * 27;
+    if (grp < 4) {
+        double sum = 0.0;
+        if (live) {
+#pragma unroll 8
+            for (int b = grp; b < np; b += 4) sum += q.part[(size_t)b * TS_BA_PART + e];
+        }
+        s_p[grp][lane] = sum;
+    }
+    __syncthreads();
+    if (grp == 0 && live) {
+        const double v = ((s_p[0][lane] + s_p[1][lane]) + s_p[2][lane]) + s_p[3][lane];
+        __hip_atomic_store(e < 4096 ? q.C + e : q.cam_U + (e - 4096), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the write-through stores have landed
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(q.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    if (threadIdx.x == 0) __hip_atomic_store(q.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+    ba_solve_block<true>(c, a);
+}
 
 
 // The last iteration's landmark update and the write-back of the window's landmarks: 16 lanes
@@ -1079,13 +1126,15 @@ static void launch_ba_prepare(const BatchCtx& c, const BaArgs& a, hipStream_t s)
 
 // One linearisation of pair a.pair: the Schur pass (+ iteration it - 1's landmark update when
 // `it` > 0) and the reduction to C, U_c, g_c.
-static void launch_ba_linearize(const BatchCtx& c, const BaArgs& a, int it, hipStream_t s, BaTiming* timing) {
+static void launch_ba_linearize(const BatchCtx& c, const BaArgs& a, int it, hipStream_t s, BaTiming* timing,
+                                bool reduce = true) {
     BaArgs ai = a;
     const bool rec = timing && timing->used < timing->cap;
     ai.fused_backsub = it > 0;   // iteration it - 1's landmark update happens inside this Schur pass
     if (rec) (void)hipEventRecord(timing->ev[2 * timing->used], s);
     hipLaunchKernelGGL(k_ba_schur, dim3(a.nsplit), dim3(BA_SCHUR_THREADS), 0, s, c, ai);
     if (rec) (void)hipEventRecord(timing->ev[2 * timing->used++ + 1], s);
+    if (!reduce) return;   // k_ba_reduce_solve follows
     hipLaunchKernelGGL(k_ba_reduce, dim3(64 + (a.n_order * 27 + 63) / 64), dim3(256), 0, s, c, a);
 }
 
@@ -1097,8 +1146,8 @@ static void launch_ba_backsub(const BatchCtx& c, const BaArgs& a, hipStream_t s)
 void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing) {
     launch_ba_prepare(c, a, s);
     for (int it = 0; it < a.iters; ++it) {
-        launch_ba_linearize(c, a, it, s, timing);
-        hipLaunchKernelGGL(k_ba_solve, dim3(1), dim3(64 * BA_SOLVE_WAVES), 0, s, c, a);
+        launch_ba_linearize(c, a, it, s, timing, false);
+        hipLaunchKernelGGL(k_ba_reduce_solve, dim3(64 + (a.n_order * 27 + 63) / 64), dim3(64 * BA_SOLVE_WAVES), 0, s, c, a);
     }
     launch_ba_backsub(c, a, s);
 }

@@ -309,7 +309,7 @@ static int alloc_ba(tslam_handle* h) {
         {(void**)&b.li, 4 * P * WK},         {(void**)&b.lm_id, 4 * P * WK},     {(void**)&b.keep, P * WK},
         {(void**)&b.camobs, 4 * P * W * WK}, {(void**)&b.obs_Vg, 8 * P * WK * 9}, {(void**)&b.obs_cam, 4 * P * WK},
         {(void**)&b.obs_k, 4 * P * WK},      {(void**)&b.obs_id, 4 * P * WK},    {(void**)&b.cam_off, 4 * P * (W + 1)},
-        {(void**)&b.counts, 4 * 4 * P},      {(void**)&b.tiles, 4 * P * 2 * TS_BA_TILES},
+        {(void**)&b.counts, 4 * 4 * P},      {(void**)&b.tiles, 4 * P * 2 * TS_BA_TILES}, {(void**)&b.done, 4 * P},
         {(void**)&b.lo_o, 4 * P * WK * M},   {(void**)&b.lo_uvd, 32 * P * WK * M}, {(void**)&b.lo_W, 8 * 18 * P * WK * M},
         {(void**)&b.Xc, 8 * P * WK * 3},
         {(void**)&b.lm_L, 8 * P * WK * 6},   {(void**)&b.lm_gp, 8 * P * WK * 3}, {(void**)&b.C, 8 * P * 64 * 64},

@@ -52,6 +52,7 @@ struct BaStore {
     int32_t* cam_off;  // [W+1]
     int32_t* counts;   // [P][4] n_obs, L, solve ok, pad
     int32_t* tiles;    // [2][TS_BA_TILES] tile counts, tile offsets
+    int32_t* done;     // [P] blocks of k_ba_reduce_solve counted in (zero between launches)
     // per (compact landmark r, window camera ci) slot s = r * TS_BA_MAXW + ci (k_ba_slots): the
     // observation index or -1, its (u, v, d), and W_o of the last linearisation — every per-
     // iteration read of the Schur pass is one level of indexing
@@ -102,7 +103,7 @@ struct BaPair {
     double* X;
     uint32_t* kf_desc;
     int64_t* gid;
-    int32_t *remap, *cnt, *li, *lm_id, *camobs, *obs_cam, *obs_k, *obs_id, *cam_off, *counts, *tiles, *lo_o;
+    int32_t *remap, *cnt, *li, *lm_id, *camobs, *obs_cam, *obs_k, *obs_id, *cam_off, *counts, *tiles, *lo_o, *done;
     uint8_t* keep;
     double *lo_uvd, *lo_W, *Xc, *obs_Vg, *lm_L, *lm_gp, *part, *C, *cam_U, *dc, *flops;
     double* imu;
@@ -128,6 +129,7 @@ __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, in
     q.cam_off = s.cam_off + p * (W + 1);
     q.counts = s.counts + 4 * p;
     q.tiles = s.tiles + p * 2 * TS_BA_TILES;
+    q.done = s.done + p;
     q.lo_o = s.lo_o + p * WK * M; q.lo_uvd = s.lo_uvd + p * WK * M * 4; q.lo_W = s.lo_W + p * WK * M * 18;
     q.Xc = s.Xc + p * WK * 3; q.obs_Vg = s.obs_Vg + p * WK * 9;
     q.lm_L = s.lm_L + p * WK * 6; q.lm_gp = s.lm_gp + p * WK * 3;
