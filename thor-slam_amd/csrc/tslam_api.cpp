@@ -173,6 +173,7 @@ struct tslam_handle {
     // asynchronous host boundary (tslam_submit_host / tslam_poll_*): the handle's own front/back
     // streams, pinned staging + device input per batch parity, pinned result slots per parity
     hipStream_t as_front = nullptr, as_back = nullptr;
+    hipStream_t as_ba = nullptr;      // local BA (ba_window > 0): its own stream on every CU
     uint8_t* as_stage[2] = {nullptr, nullptr};   // pinned host
     uint8_t* as_input[2] = {nullptr, nullptr};   // device
     hipEvent_t as_staged[2] = {nullptr, nullptr};   // DMA out of as_stage[k] done
@@ -814,7 +815,7 @@ int tslam_destroy(tslam_handle* h) {
                          h->ev_prior[1],
                          h->as_staged[0], h->as_staged[1], h->as_res[0].ev, h->as_res[1].ev})
         if (e) (void)hipEventDestroy(e);
-    for (hipStream_t st : {h->as_front, h->as_back})
+    for (hipStream_t st : {h->as_front, h->as_back, h->as_ba})
         if (st) (void)hipStreamDestroy(st);
     free_all(h);
     delete h;
@@ -890,8 +891,23 @@ static int ensure_async(tslam_handle* h) {
     if (rc != TSLAM_OK) return rc;
     int lo = 0, hi = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HIPCHK(hipStreamCreateWithPriority(&h->as_front, hipStreamNonBlocking, hi));   // front = critical path
-    HIPCHK(hipStreamCreateWithFlags(&h->as_back, hipStreamNonBlocking));
+    if (h->prm.ba_window) {
+        // local BA: its chain of small dependent launches (one-block solves, ~135-block Schur
+        // passes) runs on a stream of its own, and the front / back kernels stay off the last
+        // TS_BA_CU_RESERVE CUs so those launches find free CUs beside the next batch's front end
+        // (C4: 15.1k -> 16.2k frames/s, bench.py --front-cu-reserve sweep)
+        int n_cu = 0;
+        HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, h->device));
+        const int keep = n_cu > 2 * TS_BA_CU_RESERVE ? n_cu - TS_BA_CU_RESERVE : n_cu;
+        std::vector<uint32_t> mask((size_t)(n_cu + 31) / 32, 0u);
+        for (int cu = 0; cu < keep; ++cu) mask[(size_t)cu / 32] |= 1u << (cu % 32);
+        HIPCHK(hipExtStreamCreateWithCUMask(&h->as_front, (uint32_t)mask.size(), mask.data()));
+        HIPCHK(hipExtStreamCreateWithCUMask(&h->as_back, (uint32_t)mask.size(), mask.data()));
+        HIPCHK(hipStreamCreateWithPriority(&h->as_ba, hipStreamNonBlocking, hi));
+    } else {
+        HIPCHK(hipStreamCreateWithPriority(&h->as_front, hipStreamNonBlocking, hi));   // front = critical path
+        HIPCHK(hipStreamCreateWithFlags(&h->as_back, hipStreamNonBlocking));
+    }
     const size_t in_bytes = (size_t)h->B * host_frame_bytes(h);
     for (int k = 0; k < 2; ++k) {
         void* p = nullptr;
@@ -948,9 +964,10 @@ int tslam_submit_host(tslam_handle* h, const uint8_t* host_images, const double*
     if ((rc = tslam_begin_batch(h, h->as_input[k], n_frames)) != TSLAM_OK) return rc;
     const int stages[5] = {TSLAM_STAGE_RECTIFY, TSLAM_STAGE_DETECT, TSLAM_STAGE_DESCRIBE, TSLAM_STAGE_MATCH, TSLAM_STAGE_POSE};
     for (int i = 0; i < 5 && rc == TSLAM_OK; ++i) rc = tslam_run_stage(h, stages[i], i < 3 ? h->as_front : h->as_back);
-    if (rc == TSLAM_OK && h->prm.ba_window) rc = tslam_run_stage(h, TSLAM_STAGE_BA, h->as_back);
-    // results of this batch into the pinned slot of its parity
-    if (rc == TSLAM_OK) rc = stash_results(h, timestamps, h->as_back);
+    if (rc == TSLAM_OK && h->prm.ba_window) rc = tslam_run_stage(h, TSLAM_STAGE_BA, h->as_ba);
+    // results of this batch into the pinned slot of its parity (after its BA: the caller reads
+    // the window once the slot is polled)
+    if (rc == TSLAM_OK) rc = stash_results(h, timestamps, h->prm.ba_window ? h->as_ba : h->as_back);
     const int rc2 = tslam_end_batch(h);
     return rc != TSLAM_OK ? rc : rc2;
 }

@@ -45,6 +45,7 @@
 #define TS_MAX_SPLITS 32   // RANSAC blocks per frame
 #define TS_RANSAC_WORDS 26 // per split: key + pad + 12 doubles
 #define TS_PRIOR_DOUBLES 16 // per (frame, pair): IMU prior R (row-major 3x3), W_r, t[3], W_t, 0, 0
+#define TS_BA_CU_RESERVE 64   // CUs the front / back streams leave to the BA stream (tslam_submit_host)
 #define TS_BA_MAXW 10      // keyframes per BA window (6 camera rows each in the 64-wide system)
 
 struct LevelGeom {
