@@ -216,7 +216,9 @@ int tslam_sync(tslam_handle* h);
  *   [n][n_pairs][5*H*W]) into the handle's pinned staging buffer of the batch's parity (waiting
  *   only for that buffer's previous DMA), enqueue the DMA and the whole hot path on the handle's
  *   own streams (front stages on a high-priority stream overlapping the previous batch's back
- *   stages) and the batch's results into a pinned slot; returns without waiting for the device.
+ *   stages; with local BA, the BA on a third stream and the front / back streams CU-masked off
+ *   64 CUs so its small dependent launches find free CUs) and the batch's results into a pinned
+ *   slot (after its BA); returns without waiting for the device.
  *   timestamps[n] (seconds, the frames' SynchronizedFrameSet.timestamp) may be NULL.  At most two
  *   batches' results are held: an unread batch s-2 is dropped when batch s is submitted.
  * tslam_poll_batch: results of the oldest unread submitted batch: returns 1 and fills the outputs
