@@ -365,7 +365,7 @@ def test_ransac_bounded_scoring_with_outliers(splits, mode):
 
 
 def test_refine_block_128_parity():
-    """k_refine<128> (the automatic choice from 512 frames per launch) forced on a small batch:
+    """k_refine<128> (the automatic choice from 1024 problems per launch) forced on a small batch:
     the oracle's pose within 1e-9, and bit-identical to k_refine<256> — both follow the same
     256-virtual-thread summation partition (k_pose.hip, RF_VIRT)."""
     sc, a = hip_run(refine_block=128)
@@ -381,8 +381,8 @@ def test_refine_block_128_parity():
 
 
 def test_refine_512_frame_launch_invariance():
-    """One launch of 512 frames (auto: k_refine<128>, the bounded RANSAC) against the same launch with
-    k_refine<256> forced, and against launches of 64 frames: stats, poses and covariances
+    """One launch of 512 frames (auto: k_refine<256>, the bounded RANSAC) against the same launch with
+    k_refine<128> forced, and against launches of 64 frames: stats, poses and covariances
     bit-identical on every frame; the first frames also equal the oracle."""
     import torch
 
@@ -399,7 +399,7 @@ def test_refine_512_frame_launch_invariance():
     dev = torch.from_numpy(frames).cuda()
     s = torch.cuda.current_stream().cuda_stream
     out = {}
-    for name, batch, rb in (("auto", n, 0), ("256", n, 256), ("b64", 64, 0)):
+    for name, batch, rb in (("auto", n, 0), ("128", n, 128), ("b64", 64, 0)):
         h = Handle([rect], cfg, max_batch=batch, refine_block=rb)
         recs = {k: [] for k in ("stats", "T_rel", "T_abs", "cov")}
         for b0 in range(0, n, batch):
@@ -409,7 +409,7 @@ def test_refine_512_frame_launch_invariance():
                 recs[k].append(np.array(res[k][:, 0], copy=True))
         h.close()
         out[name] = {k: np.concatenate(v) for k, v in recs.items()}
-    for other in ("256", "b64"):
+    for other in ("128", "b64"):
         for k in ("stats", "T_rel", "T_abs", "cov"):
             np.testing.assert_array_equal(out["auto"][k], out[other][k], err_msg=f"{other}: {k}")
     assert (out["auto"]["stats"][1:, 0] == 0).mean() > 0.95   # tracked

@@ -1397,8 +1397,10 @@ int ransac_splits(const BatchCtx& c) {
 }
 
 static void launch_refine(const BatchCtx& c, int S, hipStream_t s) {
-    // the block size changes only the speed (RF_VIRT partition above), never the results
-    if (c.pp.refine_block == 128 || (c.pp.refine_block == 0 && c.n * c.npair >= 512))
+    // the block size changes only the speed (RF_VIRT partition above), never the results: 128
+    // threads from 1024 problems up (the C2 step: its VGPR-heavy waves then finish in one round
+    // beside detect), 256 below (a sharded rank's 512-problem range: pose 305 -> 269 us, probe r4w)
+    if (c.pp.refine_block == 128 || (c.pp.refine_block == 0 && c.n * c.npair >= 1024))
         hipLaunchKernelGGL(k_refine<128>, dim3(c.n * c.npair), dim3(128), 0, s, c, S);
     else
         hipLaunchKernelGGL(k_refine<256>, dim3(c.n * c.npair), dim3(256), 0, s, c, S);

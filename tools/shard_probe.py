@@ -36,6 +36,7 @@ def main() -> None:
     ap.add_argument("--names", type=int, default=4, help="stereo sources of the bracket rig (2 streams each)")
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--one-gpu", action="store_true", help="also time the one-GPU pipelined step (bench run_single)")
+    ap.add_argument("--refine-block", type=int, default=0, help="tslam_params.refine_block (0 = the library's choice)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     import torch
@@ -52,7 +53,7 @@ def main() -> None:
     uniq = render_rig_frames(names, 24, 0, C, 8)
     seq = torch.from_numpy(uniq[triangle_indices((args.steps + 1) * B, 24)]).cuda()
     parts = [seq[:, r * S:(r + 1) * S].contiguous() for r in range(W)]
-    hs = [Handle(rects, cfg, max_batch=B) for _ in range(W)]
+    hs = [Handle(rects, cfg, max_batch=B, refine_block=args.refine_block) for _ in range(W)]
     for h in hs:
         if len(rects) > 1:
             h.set_rig(E)
