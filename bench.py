@@ -626,7 +626,7 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     back_done = [torch.cuda.Event(), torch.cuda.Event()]
     back_issued = [False, False]
     # C4: local BA runs on a third stream, overlapping the next batches
-    ba_stream = torch.cuda.Stream() if c4 else None
+    ba_stream = torch.cuda.Stream(priority=-1 if args.ba_priority else 0) if c4 else None
     ba_done = [torch.cuda.Event(), torch.cuda.Event()] if c4 else None
     ba_issued = [False, False]
 
@@ -1236,6 +1236,7 @@ def main() -> None:
                          "15.6k / 15.7k / 16.2k / 15.9k / 16.2k / 16.0k frames/s)")
     ap.add_argument("--back-cu", type=int, default=0,
                     help="experiment (c2/c3): the back kernels on a stream restricted to N CUs spread over the chip")
+    ap.add_argument("--ba-priority", type=int, default=0, help="C4: the BA stream at high priority")
     ap.add_argument("--front-priority", type=int, default=1,
                     help="1: run the front kernels on a high-priority stream (pipelined mode)")
     ap.add_argument("--tsdf", type=int, default=0,
