@@ -208,3 +208,19 @@ def test_sharded_decomposition_matches_sequential_oracle(tmp_path):
                 assert rows[b, f, -1, 52] == st
                 np.testing.assert_array_equal(rows[b, f, -1, :16].reshape(4, 4), T)
                 np.testing.assert_allclose(t_abs[b, f, -1].reshape(4, 4), T_abs, rtol=0, atol=1e-12)
+
+
+def test_sharded_config_validation():
+    """HipSlamConfig(devices=...): local BA and batches of any length are allowed on a sharded rig
+    (rank 0 solves the window after the state gather; ranges may be uneven), the dense map is not
+    (the TSDF integrates on one device), and the transport is checked."""
+    import pytest
+
+    from thor_slam_amd.params import HipSlamConfig
+
+    HipSlamConfig(devices=(0, 1, 2, 3), ba_window=10, batch_size=6).validate()
+    HipSlamConfig(devices=(0, 1), enable_loop_closure=True, batch_size=1).validate()
+    with pytest.raises(ValueError, match="dense map"):
+        HipSlamConfig(devices=(0, 1), rgbd=True, dense_map=True).validate()
+    with pytest.raises(ValueError, match="shard_transport"):
+        HipSlamConfig(devices=(0, 1), shard_transport="tcp").validate()
