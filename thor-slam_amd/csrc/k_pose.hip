@@ -705,6 +705,7 @@ __global__ __launch_bounds__(RF_THREADS) void k_refine(BatchCtx c, int S) {
     static_assert(RF_VIRT % RF_THREADS == 0, "virtual partition");
     __shared__ int s_scan[RF_THREADS / 64];
     __shared__ double s_red[RF_VIRT / 64][N_ACC];
+    __shared__ double s_tot[N_ACC];
     __shared__ double s_R[9], s_t[3], s_H[36], s_misc[4];
     __shared__ int s_flag, s_best;
     const int p = c.pair0 + (int)blockIdx.x % c.npair;
@@ -788,12 +789,20 @@ __global__ __launch_bounds__(RF_THREADS) void k_refine(BatchCtx c, int S) {
         }
         }
         __syncthreads();
+        // lanes 0..28 of wave 0 add the virtual waves' sums of one accumulator each (the order the
+        // single thread used), then thread 0 reads the 29 totals
+        if (tid < N_ACC) {
+            double v = s_red[0][tid];
+#pragma unroll
+            for (int w = 1; w < RF_VIRT / 64; ++w) v += s_red[w][tid];
+            s_tot[tid] = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (tid == 0) {
             double tot[N_ACC];
-            for (int k = 0; k < N_ACC; ++k) {
-                tot[k] = s_red[0][k];
-                for (int w = 1; w < RF_VIRT / 64; ++w) tot[k] += s_red[w][k];
-            }
+            for (int k = 0; k < N_ACC; ++k) tot[k] = s_tot[k];
             const int n_in = (int)tot[28];
             s_flag = 0;
             if (n_in < 6) {
@@ -1077,6 +1086,7 @@ __global__ __launch_bounds__(RIG_THREADS) void k_rig_pose(BatchCtx c) {
     __shared__ double s_T[TS_RIG_MAXP][TS_RIG_MAXP][12];     // [candidate][pair] R | t
     __shared__ int s_cnt[RIG_WAVES][TS_RIG_MAXP];
     __shared__ double s_red[RIG_WAVES][N_ACC];
+    __shared__ double s_tot[N_ACC];
     __shared__ double s_H[36], s_misc[2];
     __shared__ int s_nc, s_flag, s_best;
     const int f = blockIdx.x;
@@ -1240,12 +1250,20 @@ __global__ __launch_bounds__(RIG_THREADS) void k_rig_pose(BatchCtx c) {
         }
         __syncthreads();
         RSTAMP(5);
+        // lanes 0..28 of wave 0 add the 8 wave sums of one accumulator each (the same order the
+        // single thread used), then thread 0 reads the 29 totals
+        if (tid < N_ACC) {
+            double v = s_red[0][tid];
+#pragma unroll
+            for (int w = 1; w < RIG_WAVES; ++w) v += s_red[w][tid];
+            s_tot[tid] = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (tid == 0) {
             double tot[N_ACC];
-            for (int k = 0; k < N_ACC; ++k) {
-                tot[k] = s_red[0][k];
-                for (int w = 1; w < RIG_WAVES; ++w) tot[k] += s_red[w][k];
-            }
+            for (int k = 0; k < N_ACC; ++k) tot[k] = s_tot[k];
             s_flag = 0;
             double Hm[36], gv[6], x[6], L[36];
             int k = 0;
