@@ -211,30 +211,14 @@ __global__ __launch_bounds__(TS_DT_THREADS) void k_describe(BatchCtx c) {
             const int x = rec[g].x & 0xFFFF, y = rec[g].x >> 16;
             // BRIEF: patch origin (x - 18, y - 18) in the smoothed tile
             const uint8_t* pbase = s_smo + (y - y0) * TS_DT_P + (x - 18 - c0);
-            // slot j of this lane runs test 64 w_j + lane (w_j: bits 14-15 of the entry, the
-            // per-lane read order chosen by the host to spread the LDS banks)
-            bool res[4];
-            int wd[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-#ifdef TS_DT_EXP_NOCONFLICT   // experiment builds only: conflict-free byte addresses (wrong descriptors)
-                const int a = pbase[(t[g][j] & 0x3u) + 4 * lane];
-                const int b = pbase[((t[g][j] >> 16) & 0x3u) + 4 * lane + 256];
-#else
-                const int a = pbase[t[g][j] & 0x3FFFu];
-                const int b = pbase[(t[g][j] >> 16) & 0x3FFFu];
-#endif
-                res[j] = a < b;
-                wd[j] = (int)((t[g][j] >> 14) & 3u);
-            }
             uint32_t words[8];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const bool bit = (res[0] && wd[0] == k) || (res[1] && wd[1] == k) || (res[2] && wd[2] == k) ||
-                                 (res[3] && wd[3] == k);
-                const uint64_t bm = __ballot(bit);
-                words[2 * k] = (uint32_t)bm;
-                words[2 * k + 1] = (uint32_t)(bm >> 32);
+            for (int j = 0; j < 4; ++j) {
+                const int a = pbase[t[g][j] & 0xFFFFu];
+                const int b = pbase[t[g][j] >> 16];
+                const uint64_t bm = __ballot(a < b);
+                words[2 * j] = (uint32_t)bm;
+                words[2 * j + 1] = (uint32_t)(bm >> 32);
             }
             const int kidx = (int)rec[g].z;
             // word j (wave-uniform) into lane j: 8 v_writelane

@@ -648,84 +648,6 @@ static int run_sharded_stage(tslam_handle* h, const BatchCtx& c, int stage, hipS
     return TSLAM_OK;
 }
 
-// The describe kernel's rotated-pattern table (k_describe.hip): per angle bin, slot j of lane L
-// (j < 4, L < 64) holds both points of one test as byte offsets from the patch origin in the LDS
-// tile, (py + 18) * TS_DT_P + px + 18, low | high << 16, and in bits 14-15 the descriptor word
-// (of the four 64-bit words) the test belongs to.  Lane L always runs tests L, 64 + L, 128 + L,
-// 192 + L (its ballot bit), but which of its four LDS reads runs which test is chosen per lane and
-// bin to spread each read instruction's 64 byte addresses over the LDS banks (a local search
-// over the per-lane orders: fewer bank conflicts, the same descriptor bits).
-static int brief_slot_cost(const uint16_t* off) {   // 64 byte offsets of one read instruction
-    int cost = 0;
-    for (int align = 0; align < 4; ++align)
-        for (int nb : {32, 64}) {   // both bank models: two half-waves x 32 banks, one wave x 64 banks
-            const int passes = nb == 32 ? 2 : 1;
-            for (int half = 0; half < passes; ++half) {
-                const int l0 = 64 / passes * half, l1 = l0 + 64 / passes;
-                int worst = 0;
-                int cnt[64] = {0};
-                uint32_t seen[64][8];
-                for (int l = l0; l < l1; ++l) {
-                    const uint32_t dw = (uint32_t)(off[l] + align) >> 2, b = dw % (uint32_t)nb;
-                    bool dup = false;
-                    for (int k = 0; k < cnt[b] && !dup; ++k) dup = seen[b][k] == dw;
-                    if (!dup && cnt[b] < 8) seen[b][cnt[b]++] = dw;
-                }
-                for (int b = 0; b < nb; ++b) worst = std::max(worst, cnt[b]);
-                cost += worst;   // cycles of this pass
-            }
-        }
-    return cost;
-}
-
-static void build_brief_offsets(uint32_t* out) {
-    for (int bin = 0; bin < 30; ++bin) {
-        uint16_t a[256], b[256];
-        for (int t = 0; t < 256; ++t) {
-            const uint32_t v = TSLAM_BRIEF_TABLE[bin * 256 + t];
-            const int px = (int8_t)(v & 0xFF), py = (int8_t)((v >> 8) & 0xFF);
-            const int qx = (int8_t)((v >> 16) & 0xFF), qy = (int8_t)(v >> 24);
-            a[t] = (uint16_t)((py + 18) * TS_DT_P + px + 18);
-            b[t] = (uint16_t)((qy + 18) * TS_DT_P + qx + 18);
-        }
-        int word[64][4];   // word[L][j]: the test word lane L runs in read slot j
-        for (int l = 0; l < 64; ++l)
-            for (int j = 0; j < 4; ++j) word[l][j] = j;
-        auto slot_cost = [&](int j) {
-            uint16_t oa[64], ob[64];
-            for (int l = 0; l < 64; ++l) {
-                oa[l] = a[64 * word[l][j] + l];
-                ob[l] = b[64 * word[l][j] + l];
-            }
-            return brief_slot_cost(oa) + brief_slot_cost(ob);
-        };
-        int cost[4];
-        for (int j = 0; j < 4; ++j) cost[j] = slot_cost(j);
-        for (int pass = 0; pass < 4; ++pass) {
-            bool improved = false;
-            for (int l = 0; l < 64; ++l)
-                for (int j0 = 0; j0 < 4; ++j0)
-                    for (int j1 = j0 + 1; j1 < 4; ++j1) {
-                        std::swap(word[l][j0], word[l][j1]);
-                        const int c0 = slot_cost(j0), c1 = slot_cost(j1);
-                        if (c0 + c1 < cost[j0] + cost[j1]) {
-                            cost[j0] = c0;
-                            cost[j1] = c1;
-                            improved = true;
-                        } else {
-                            std::swap(word[l][j0], word[l][j1]);
-                        }
-                    }
-            if (!improved) break;
-        }
-        for (int j = 0; j < 4; ++j)
-            for (int l = 0; l < 64; ++l) {
-                const int t = 64 * word[l][j] + l;
-                out[bin * 256 + 64 * j + l] = (uint32_t)a[t] | ((uint32_t)word[l][j] << 14) | ((uint32_t)b[t] << 16);
-            }
-    }
-}
-
 extern "C" {
 
 const char* tslam_last_error(void) { return g_err.c_str(); }
@@ -851,12 +773,13 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     // the describe kernel reads the rotated pattern as byte offsets from the patch origin
     // (x - 18, y - 18) in its LDS tile: (py + 18) * TS_DT_P + px + 18 for both points, packed
     // low | high << 16
-    // the table depends on compile-time constants only: searched once per process
-    static const std::vector<uint32_t> brief_off = [] {
-        std::vector<uint32_t> v(30 * 256);
-        build_brief_offsets(v.data());
-        return v;
-    }();
+    std::vector<uint32_t> brief_off(30 * 256);
+    for (int i = 0; i < 30 * 256; ++i) {
+        const uint32_t t = TSLAM_BRIEF_TABLE[i];
+        const int px = (int8_t)(t & 0xFF), py = (int8_t)((t >> 8) & 0xFF);
+        const int qx = (int8_t)((t >> 16) & 0xFF), qy = (int8_t)(t >> 24);
+        brief_off[i] = (uint32_t)((py + 18) * TS_DT_P + px + 18) | ((uint32_t)((qy + 18) * TS_DT_P + qx + 18) << 16);
+    }
     bool ok = hipMemcpy(h->d_brief, brief_off.data(), sizeof(uint32_t) * brief_off.size(), hipMemcpyHostToDevice) == hipSuccess &&
               hipMemcpy(h->d_wedges, TSLAM_WEDGES, sizeof(TSLAM_WEDGES), hipMemcpyHostToDevice) == hipSuccess;
     for (int i = 0; i < h->P && ok; ++i) {
