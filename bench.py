@@ -809,7 +809,9 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
         avg_us, flops = schur["us"], schur["flops"]
         mfma = {"bound": "mfma", "kernel": "k_ba_schur", "achieved": flops / (avg_us * 1e-6) / 1e12,
                 "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s", "traffic": None, "dtype": "f64",
-                "algorithmic_flops_per_launch": flops, "avg_launch_us": avg_us, "launches_timed": schur["reps"],
+                "algorithmic_flops_per_launch": flops,
+                "flop_count": "symmetric product C = Q^T Q: rows (rows + 1) 3L, rows = 6 n + 1 (lower triangle only)",
+                "avg_launch_us": avg_us, "launches_timed": schur["reps"],
                 "timing": "HIP events around back-to-back replays on the last solved window",
                 # launches per step: keyframes x Gauss-Newton iterations x pairs
                 "time_per_step_us": avg_us * (B // cfg.ba_kf_interval) * cfg.ba_iters * P}

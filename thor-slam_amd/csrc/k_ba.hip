@@ -384,7 +384,8 @@ __device__ __forceinline__ void ba_obs_jac(const double* T, const double* X, dou
     const double xc = ((T[0] * X[0] + T[1] * X[1]) + T[2] * X[2]) + T[3];
     const double yc = ((T[4] * X[0] + T[5] * X[1]) + T[6] * X[2]) + T[7];
     const double zc = ((T[8] * X[0] + T[9] * X[1]) + T[10] * X[2]) + T[11];
-    const double iz = 1.0 / zc;
+    double iz = __builtin_amdgcn_rcp(zc);   // + one Newton step (~1 ulp) instead of the division chain
+    iz = iz * (2.0 - zc * iz);
     const double base = cal.fxb / cal.fx;
     const bool st = __builtin_isfinite(d);
     double dpi[3][3] = {{cal.fx * iz, 0.0, -cal.fx * xc * iz * iz},
@@ -473,8 +474,13 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
     const int kk = lane >> 4, rc = lane & 15;
     BST_DECL;
     for (int i = threadIdx.x; i < n * 12; i += blockDim.x) s_T[i / 12][i % 12] = q.T[(size_t)a.order[i / 12] * 16 + i % 12];
-    d4v acc[4];
-    for (int t = 0; t < 4; ++t) acc[t] = (d4v){0.0, 0.0, 0.0, 0.0};
+    // wave w's two tiles (row block, column block) of the lower triangle of C, as the first rows /
+    // columns: (0,0) (3,0) | (1,0) (3,1) | (1,1) (3,2) | (2,0) (3,3) | (2,1) (2,2)
+    static_assert(BA_SCHUR_THREADS == 5 * 64, "five waves share the ten lower tiles");
+    const int ta[4] = {16 * ((0x22110 >> (4 * wave)) & 15), 16 * ((0x10100 >> (4 * wave)) & 15),
+                       16 * ((0x23333 >> (4 * wave)) & 15), 16 * ((0x23210 >> (4 * wave)) & 15)};
+    d4v acc[2];
+    for (int t = 0; t < 2; ++t) acc[t] = (d4v){0.0, 0.0, 0.0, 0.0};
     const bool bsub = a.fused_backsub && q.counts[2];   // the previous solve succeeded
     const int cu_item = (int)threadIdx.x - BA_CHUNK;     // (camera, element) of the camera sums
     double cam_acc = 0.0;
@@ -600,14 +606,20 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
                 if (s_has[li][ci])
 #pragma unroll
                     for (int e = 0; e < 9; ++e) vg[e] += s_Vg[li][ci][e];
-            // one reciprocal per pivot, multiplications after it (the chain had 9 divisions)
-            const double i00 = 1.0 / sqrt(vg[0] > 1e-300 ? vg[0] : 1e-300);
+            // one reciprocal square root per pivot, multiplications after it (the chain had 9
+            // divisions, then 3 sqrt + division pairs): v_rsq_f64 + one Newton step, ~1 ulp
+            auto rsqrt_nr = [](double x) {
+                x = x > 1e-300 ? x : 1e-300;
+                const double y = __builtin_amdgcn_rsq(x);
+                return y * (1.5 - (0.5 * x) * (y * y));
+            };
+            const double i00 = rsqrt_nr(vg[0]);
             const double l10 = vg[1] * i00, l20 = vg[2] * i00;
             const double d11 = vg[3] - l10 * l10;
-            const double i11 = 1.0 / sqrt(d11 > 1e-300 ? d11 : 1e-300);
+            const double i11 = rsqrt_nr(d11);
             const double l21 = (vg[4] - l20 * l10) * i11;
             const double d22 = (vg[5] - l20 * l20) - l21 * l21;
-            const double i22 = 1.0 / sqrt(d22 > 1e-300 ? d22 : 1e-300);
+            const double i22 = rsqrt_nr(d22);
             const double y0 = vg[6] * i00, y1 = (vg[7] - l10 * y0) * i11, y2 = ((vg[8] - l20 * y0) - l21 * y1) * i22;
             s_L[li][0] = i00; s_L[li][1] = l10; s_L[li][2] = i11; s_L[li][3] = l20; s_L[li][4] = l21;
             s_L[li][5] = i22;
@@ -656,43 +668,46 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
         }
         lds_barrier();
         BST(4);
-        // 4. C += Q^T Q over the chunk's columns (zero columns past nl contribute nothing)
-        if (wave < 4) {
+        // 4. C += Q^T Q over the chunk's columns (zero columns past nl contribute nothing): only
+        //    the 10 lower-triangle 16 x 16 tiles, two per wave (the upper ones are their transposes)
+        {
             const int ksteps = (3 * nl + 3) >> 2;
-            // the next k-step's operands load while this one's four MFMAs run
+            // the next k-step's operands load while this one's two MFMAs run
             const double* col = s_Q + kk * BA_QPITCH + rc;
-            double n0 = col[0], n1 = col[16], n2 = col[32], n3 = col[48];
+            double n0 = col[ta[0]], n1 = col[ta[1]], n2 = col[ta[2]], n3 = col[ta[3]];
             for (int st = 0; st < ksteps; ++st) {
-                const double b0 = n0, b1 = n1, b2 = n2, b3 = n3;
+                const double a0v = n0, b0v = n1, a1v = n2, b1v = n3;
                 const double* nx = col + 4 * min(st + 1, ksteps - 1) * BA_QPITCH;
-                n0 = nx[0];
-                n1 = nx[16];
-                n2 = nx[32];
-                n3 = nx[48];
-                const double av = wave == 0 ? b0 : wave == 1 ? b1 : wave == 2 ? b2 : b3;
-                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b0, acc[0], 0, 0, 0);
-                acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b1, acc[1], 0, 0, 0);
-                acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b2, acc[2], 0, 0, 0);
-                acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b3, acc[3], 0, 0, 0);
+                n0 = nx[ta[0]];
+                n1 = nx[ta[1]];
+                n2 = nx[ta[2]];
+                n3 = nx[ta[3]];
+                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0v, b0v, acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1v, b1v, acc[1], 0, 0, 0);
             }
         }
         BST(5);
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {   // algorithmic flops of the dense Schur product
-        const double rows = 6.0 * n + 1.0;
-        q.flops[0] += 2.0 * rows * rows * 3.0 * L;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {   // algorithmic flops of the symmetric Schur product
+        const double rows = 6.0 * n + 1.0;          // (SYRK: the lower triangle with its diagonal)
+        q.flops[0] += rows * (rows + 1.0) * 3.0 * L;
     }
     BST_PRINT("schur b0: stage+T, lm update, jacobians, factor, columns, mfma, -, -", blockIdx.x == 0 && threadIdx.x == 0);
     if (blockIdx.x * BA_CHUNK >= L) return;   // no chunk: no partial
     if (cu_item >= 0 && cu_item < n * 27) q.part[(size_t)blockIdx.x * TS_BA_PART + 4096 + cu_item] = cam_acc;
-    if (wave >= 4) return;
     double* out = q.part + (size_t)blockIdx.x * TS_BA_PART;
-    const int a0 = 16 * wave;
-    // C/D layout of v_mfma_f64_16x16x4f64: col = lane & 15, row = (lane >> 4) + 4 * reg
+    // C/D layout of v_mfma_f64_16x16x4f64: col = lane & 15, row = (lane >> 4) + 4 * reg; an
+    // off-diagonal tile is stored twice, as itself and as its transpose (the symmetric partner;
+    // a diagonal tile is symmetric bit for bit)
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 2; ++t) {
+        const int r0 = ta[2 * t], c0 = ta[2 * t + 1];
 #pragma unroll
-        for (int rg = 0; rg < 4; ++rg) out[(size_t)(a0 + kk + 4 * rg) * 64 + 16 * t + rc] = acc[t][rg];
+        for (int rg = 0; rg < 4; ++rg) {
+            out[(size_t)(r0 + kk + 4 * rg) * 64 + c0 + rc] = acc[t][rg];
+            if (r0 != c0) out[(size_t)(c0 + rc) * 64 + r0 + kk + 4 * rg] = acc[t][rg];
+        }
+    }
 }
 
 // Fixed-order sum of the partials of the blocks that had a chunk: block = 64 elements of a
