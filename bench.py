@@ -627,6 +627,9 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     back_issued = [False, False]
     # C4: local BA runs on a third stream, overlapping the next batches
     ba_stream = torch.cuda.Stream(priority=-1 if args.ba_priority else 0) if c4 else None
+    if c4 and args.ba_cus > 0:   # experiment: the BA chain only on the last N CUs (the front / back keep off them)
+        n_cu = torch.cuda.get_device_properties(dev_index).multi_processor_count
+        ba_stream = cu_masked_stream(dev_index, 0, 0, list(range(n_cu - args.ba_cus, n_cu)))
     ba_done = [torch.cuda.Event(), torch.cuda.Event()] if c4 else None
     ba_issued = [False, False]
 
@@ -904,7 +907,8 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
             "parallelism": (f"one stereo source per GPU x{world}" + (" (independent replicas)" if world > 1 else ""))
                            if not (c3 or c5) else "the whole rig on 1 GPU",
             **({"streams": "front + back kernels CU-masked off the last "
-                           f"{args.front_cu_reserve} CUs, local BA on a third stream on every CU"} if masked else {}),
+                           f"{args.front_cu_reserve} CUs, local BA on a third stream on "
+                           + (f"the last {args.ba_cus} CUs only" if args.ba_cus > 0 else "every CU")} if masked else {}),
         },
         "roofline": roofline,
         "latency_b1_ms": lat_ms,
@@ -1239,6 +1243,9 @@ def main() -> None:
     ap.add_argument("--back-cu", type=int, default=0,
                     help="experiment (c2/c3): the back kernels on a stream restricted to N CUs spread over the chip")
     ap.add_argument("--ba-priority", type=int, default=0, help="C4: the BA stream at high priority")
+    ap.add_argument("--ba-cus", type=int, default=0,
+                    help="C4 experiment: the BA stream CU-masked to the last N CUs (with --front-cu-reserve N "
+                         "the front / back kernels keep off them)")
     ap.add_argument("--front-priority", type=int, default=1,
                     help="1: run the front kernels on a high-priority stream (pipelined mode)")
     ap.add_argument("--tsdf", type=int, default=0,

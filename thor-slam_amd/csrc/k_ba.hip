@@ -41,6 +41,11 @@ __device__ __forceinline__ void mul4(const double* A, const double* B, double* o
             out[4 * i + j] = ((A[4 * i] * B[j] + A[4 * i + 1] * B[4 + j]) + A[4 * i + 2] * B[8 + j]) + A[4 * i + 3] * B[12 + j];
 }
 
+// The BA chain is latency-bound (small grids, dependent launches) and shares the SIMDs with the
+// next batches' front-end waves: its waves raise their issue priority (s_setprio) so the SIMD
+// arbiter serves them first.
+#define BA_PRIO __builtin_amdgcn_s_setprio(3)
+
 // Level-0 observation and validity of keypoint k of image (slot, cam); mirrors oracle.level0_coords.
 __device__ __forceinline__ bool kp_obs(const BatchCtx& c, int slot, int cam, int k, double* u, double* v) {
     const uint32_t* kp = c.kps + (((size_t)slot * c.C + cam) * c.g.K + k) * 2;
@@ -60,6 +65,7 @@ __device__ __forceinline__ bool kp_obs(const BatchCtx& c, int slot, int cam, int
 // remaining keyframe (a.order, oldest first).  Pass 1 takes the minimum (rank, keypoint) key per
 // landmark (remap pre-filled with a large value), pass 2 rewrites the ids and copies the position.
 __global__ __launch_bounds__(256) void k_ba_evict_min(BatchCtx c, BaArgs a) {
+    BA_PRIO;
     const int K = c.g.K;
     BaPair q = ba_pair(c, a, a.pair);
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -70,6 +76,7 @@ __global__ __launch_bounds__(256) void k_ba_evict_min(BatchCtx c, BaArgs a) {
 }
 
 __global__ __launch_bounds__(256) void k_ba_evict_move(BatchCtx c, BaArgs a) {
+    BA_PRIO;
     const int K = c.g.K;
     BaPair q = ba_pair(c, a, a.pair);
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -90,6 +97,7 @@ __global__ __launch_bounds__(256) void k_ba_evict_move(BatchCtx c, BaArgs a) {
 
 // Insertion of frame a.frame into slot a.slot (every block derives the pose; block 0 stores it).
 __global__ __launch_bounds__(256) void k_ba_insert(BatchCtx c, BaArgs a) {
+    BA_PRIO;
     __shared__ double s_T[16];   // new keyframe's cam_T_world
     const int K = c.g.K, p = a.pair;
     BaPair q = ba_pair(c, a, p);
@@ -195,6 +203,7 @@ __device__ int block_scan_excl(int v, int* s_tmp, int* total) {
 // Gate every observation of the window at the current estimate (positive depth, reprojection
 // error <= outlier_px); count the gated observations per landmark (cnt pre-zeroed).
 __global__ __launch_bounds__(256) void k_ba_gate(BatchCtx c, BaArgs a) {
+    BA_PRIO;
     __shared__ double s_T[TS_BA_MAXW][12];
     const int K = c.g.K, p = a.pair, n = a.n_order;
     BaPair q = ba_pair(c, a, p);
@@ -273,6 +282,7 @@ __device__ __forceinline__ void ba_tile_flags(const BatchCtx& c, const BaArgs& a
 }
 
 __global__ __launch_bounds__(256) void k_ba_tilecount(BatchCtx c, BaArgs a) {
+    BA_PRIO;
     __shared__ int s_tmp[32];
     BaPair q = ba_pair(c, a, a.pair);
     int fl[BA_SCAN_ITEMS], ids[BA_SCAN_ITEMS], ci, k0, cnt = 0;
@@ -288,6 +298,7 @@ __global__ __launch_bounds__(256) void k_ba_tilecount(BatchCtx c, BaArgs a) {
 // before it (landmark tiles and observation tiles are scanned separately), and block 0 also
 // publishes the totals and the per-camera observation ranges (no separate scan launch).
 __global__ __launch_bounds__(256) void k_ba_tilescatter(BatchCtx c, BaArgs a) {
+    BA_PRIO;
     __shared__ int s_tmp[32];
     __shared__ int s_cnt[TS_BA_TILES];
     BaPair q = ba_pair(c, a, a.pair);
@@ -336,6 +347,7 @@ __global__ __launch_bounds__(256) void k_ba_tilescatter(BatchCtx c, BaArgs a) {
 }
 
 __global__ __launch_bounds__(256) void k_ba_camobs(BatchCtx c, BaArgs a) {
+    BA_PRIO;
     BaPair q = ba_pair(c, a, a.pair);
     const int o = blockIdx.x * blockDim.x + threadIdx.x;
     if (o >= q.counts[0]) return;
@@ -346,6 +358,7 @@ __global__ __launch_bounds__(256) void k_ba_camobs(BatchCtx c, BaArgs a) {
 // camera ci gets its observation index (or -1) and (u, v, d); Xc[r] = X[lm_id[r]].  Resets the
 // camobs entries it reads and the gate counts, so neither needs a memset before the next solve.
 __global__ __launch_bounds__(256) void k_ba_slots(BatchCtx c, BaArgs a) {
+    BA_PRIO;
     BaPair q = ba_pair(c, a, a.pair);
     const int K = c.g.K, WK = a.W * K;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -455,6 +468,7 @@ __device__ __forceinline__ void lds_barrier() {
 // order.  The camera sums stay in the block instead of 27 scattered 8-byte stores per observation.
 __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArgs a) {
 #pragma clang fp contract(fast)   // single FMAs in the landmark chains (held to 1e-9, as k_ba_solve)
+    BA_PRIO;
     // the Schur tile Q (phases 3-4) and the observations' camera blocks (phases 1-2) share LDS
     constexpr int QN = 3 * BA_CHUNK * BA_QPITCH, CN = BA_CHUNK * TS_BA_MAXW * 27;
     __shared__ double s_buf[QN > CN ? QN : CN];
@@ -714,6 +728,7 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
 // partial, 4 waves each summing every 4th partial, then the 4 wave sums in order.  Elements 0..4095
 // are C, 4096.. the camera blocks U_c, g_c ([camera][27]).
 __global__ __launch_bounds__(256) void k_ba_reduce(BatchCtx c, BaArgs a) {
+    BA_PRIO;
     __shared__ double s_p[4][64];
     BaPair q = ba_pair(c, a, a.pair);
     const int L = q.counts[1];
@@ -997,7 +1012,10 @@ __device__ __forceinline__ void ba_solve_block(const BatchCtx& c, const BaArgs& 
 #endif
 }
 
-__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, BaArgs a) { ba_solve_block<false>(c, a); }
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, BaArgs a) {
+    BA_PRIO;
+    ba_solve_block<false>(c, a);
+}
 
 // k_ba_reduce and k_ba_solve in one launch (a stereo pair's own solve): the reduction's blocks
 // (k_ba_reduce's fixed order, waves 0-3) publish their sums with write-through (agent-scope)
@@ -1006,6 +1024,7 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, Ba
 // writes back the whole L2 of the XCD (the iteration's Schur partials and Jacobian blocks), which
 // cost more than the launch it saves (measured: 0.300 against 0.260 ms per keyframe).
 __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_solve(BatchCtx c, BaArgs a) {
+    BA_PRIO;
     __shared__ double s_p[4][64];
     __shared__ int s_last;
     BaPair q = ba_pair(c, a, a.pair);
@@ -1044,6 +1063,7 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_solve(BatchCt
 // the stored Cholesky factor and stores X[lm_id[r]] = Xc[r] + dp (Xc[r] alone when the last
 // solve failed).
 __global__ __launch_bounds__(256) void k_ba_backsub(BatchCtx c, BaArgs a) {
+    BA_PRIO;
     const int WK = a.W * c.g.K;
     BaPair q = ba_pair(c, a, a.pair);
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
