@@ -57,6 +57,7 @@ __device__ __forceinline__ uint32_t key_dist(uint32_t key) {   // distance of a 
 }
 
 __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
+    TS_BACK_PRIO;
     // per wave: the compacted-train ring during the walk, then the (best, second) reduction
     __shared__ __attribute__((aligned(16))) uint2 s_red[4][32 * TS_MRED_PITCH];
     __shared__ __attribute__((aligned(16))) uint32_t s_key[2][TS_MQ];  // temporal: (x, thread) sort keys, then the dealt positions
@@ -397,6 +398,7 @@ __device__ __forceinline__ int match_lookup(const BatchCtx& c, size_t mbase, int
 // grid xcd_grid(n*P, ceil(K/32)), block 256.
 #define TS_RS_QPB 32   // queries per block
 __global__ __launch_bounds__(256) void k_refine_stereo(BatchCtx c) {
+    TS_BACK_PRIO;
     __shared__ uint4 s_a[TS_RS_QPB][11];   // left patch rows: 11 bytes used
     __shared__ uint4 s_b[TS_RS_QPB][11];   // right window rows: 15 bytes used
     __shared__ int s_cost[TS_RS_QPB][5];
@@ -503,6 +505,7 @@ __global__ __launch_bounds__(256) void k_refine_stereo(BatchCtx c) {
 #define TS_RT_BROWS 15
 #define TS_RT_QPB 32   // queries per block
 __global__ __launch_bounds__(256) void k_refine_temporal(BatchCtx c) {
+    TS_BACK_PRIO;
     __shared__ uint4 s_a[TS_RT_QPB][TS_RT_AROWS];   // [query slot][row]: 11 bytes used (+ zero pad)
     __shared__ uint4 s_b[TS_RT_QPB][TS_RT_BROWS];   // 15 bytes used
     __shared__ int s_cost[TS_RT_QPB][25];

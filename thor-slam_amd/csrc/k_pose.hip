@@ -257,6 +257,7 @@ __device__ __forceinline__ void write_stats(int32_t* so, int status, int n, int 
 
 // ---- k_corr: correspondences of one (frame, pair), ordered by the current keypoint index ------
 __global__ __launch_bounds__(POSE_THREADS) void k_corr(BatchCtx c) {
+    TS_BACK_PRIO;
     __shared__ int s_scan[2 * (POSE_THREADS / 64)];
     const int p = c.pair0 + (int)blockIdx.x % c.npair;   // (frame, pair) of the pair view
     const int f = (int)blockIdx.x / c.npair;
@@ -332,6 +333,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_corr(BatchCtx c) {
 // its 4 candidate poses to c.hyp ([R 9 | t 3] f64 + their f32 scoring copies, TS_HYP_DOUBLES;
 // first element NaN = no solution).
 __global__ __launch_bounds__(POSE_THREADS) void k_p3p(BatchCtx c) {
+    TS_BACK_PRIO;
     const int H = c.pp.n_hyp;
     const int gid = blockIdx.x * POSE_THREADS + threadIdx.x;
     if (gid >= c.n * c.npair * H) return;
@@ -404,6 +406,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_p3p(BatchCtx c) {
 // launch (B = 1 latency, C4's 50) the per-pose latency of k_ransac's one-wave scans would be the
 // launch's critical path, so those launches take this kernel (same keys, same winner).
 __global__ __launch_bounds__(POSE_THREADS) void k_ransac_all(BatchCtx c, int S) {
+    TS_BACK_PRIO;
     __shared__ int s_cnt[4 * TS_MAX_HYP_SPLIT];
     __shared__ uint32_t s_wbest[4];
     const int fl = blockIdx.x / S;
@@ -523,6 +526,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_ransac_all(BatchCtx c, int S) 
 #define TS_RS_UNROLL 4
 #endif
 __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
+    TS_BACK_PRIO;
     extern __shared__ float4 s_corr[];   // [cap] (X, Y, Z, du) then [cap] float2 (dv, S)
     __shared__ uint32_t s_best;
     __shared__ int s_wout[POSE_THREADS / 64][64];   // a wave's misses of the pose it is scanning
@@ -702,6 +706,7 @@ __global__ __launch_bounds__(POSE_THREADS) void k_ransac(BatchCtx c, int S) {
 #define RF_VIRT 256
 template <int RF_THREADS>
 __global__ __launch_bounds__(RF_THREADS) void k_refine(BatchCtx c, int S) {
+    TS_BACK_PRIO;
     static_assert(RF_VIRT % RF_THREADS == 0, "virtual partition");
     __shared__ int s_scan[RF_THREADS / 64];
     __shared__ double s_red[RF_VIRT / 64][N_ACC];
@@ -935,6 +940,7 @@ __device__ __forceinline__ double mul4_elem(const double* a, const double* b, in
 }
 
 __global__ __launch_bounds__(256) void k_chain(BatchCtx c) {
+    TS_BACK_PRIO;
     __shared__ double s_f[TS_CHAIN_ROUND][16];   // the round's factors, then its prefixes Q(f)
     __shared__ int s_keep[TS_CHAIN_ROUND];        // 1: the frame does not move the chain
     __shared__ double s_A[TS_CHAIN_SEGS + 1][16];  // A of each segment of the round (+ the next)
@@ -1082,6 +1088,7 @@ __device__ __forceinline__ void mul4_fixed(const double* A, const double* B, dou
 #define RIG_THREADS 512
 #define RIG_WAVES (RIG_THREADS / 64)
 __global__ __launch_bounds__(RIG_THREADS) void k_rig_pose(BatchCtx c) {
+    TS_BACK_PRIO;
     __shared__ double s_M[TS_RIG_MAXP][16];                  // candidates (body motions)
     __shared__ double s_T[TS_RIG_MAXP][TS_RIG_MAXP][12];     // [candidate][pair] R | t
     __shared__ int s_cnt[RIG_WAVES][TS_RIG_MAXP];

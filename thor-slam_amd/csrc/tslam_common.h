@@ -46,6 +46,11 @@
 #define TS_RANSAC_WORDS 26 // per split: key + pad + 12 doubles
 #define TS_PRIOR_DOUBLES 16 // per (frame, pair): IMU prior R (row-major 3x3), W_r, t[3], W_t, 0, 0
 #define TS_BA_CU_RESERVE 64   // CUs the front / back streams leave to the BA stream (tslam_submit_host)
+// Wave issue priority of the back kernels (match .. chain, rig pose): latency-bound waves that share
+// the SIMDs with the next batch's front-end waves (detect, describe: throughput-bound) get served
+// first (C2 234.7-235.3k -> 235.6-235.9k frames/s, C3 59.75k -> 60.05k; the front kernels at
+// priority 1 or 2 instead were 1 % slower).  The local BA's kernels use 3 (k_ba.hip).
+#define TS_BACK_PRIO __builtin_amdgcn_s_setprio(2)
 #define TS_BA_MAXW 10      // keyframes per BA window (6 camera rows each in the 64-wide system)
 
 struct LevelGeom {
