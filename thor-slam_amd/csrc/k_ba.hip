@@ -1025,7 +1025,9 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, Ba
 // cost more than the launch it saves (measured: 0.300 against 0.260 ms per keyframe).
 __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_solve(BatchCtx c, BaArgs a) {
     BA_PRIO;
-    __shared__ double s_p[4][64];
+    // all BA_SOLVE_WAVES waves sum (every 8th partial each: half the dependent chain of k_ba_reduce's
+    // four), then the 8 wave sums in order
+    __shared__ double s_p[BA_SOLVE_WAVES][64];
     __shared__ int s_last;
     BaPair q = ba_pair(c, a, a.pair);
     const int L = q.counts[1];
@@ -1033,17 +1035,19 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_solve(BatchCt
     const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
     const int e = blockIdx.x * 64 + lane;
     const bool live = e < 4096 + a.n_order * 27;
-    if (grp < 4) {
+    {
         double sum = 0.0;
         if (live) {
 #pragma unroll 8
-            for (int b = grp; b < np; b += 4) sum += q.part[(size_t)b * TS_BA_PART + e];
+            for (int b = grp; b < np; b += BA_SOLVE_WAVES) sum += q.part[(size_t)b * TS_BA_PART + e];
         }
         s_p[grp][lane] = sum;
     }
     __syncthreads();
     if (grp == 0 && live) {
-        const double v = ((s_p[0][lane] + s_p[1][lane]) + s_p[2][lane]) + s_p[3][lane];
+        double v = s_p[0][lane];
+#pragma unroll
+        for (int g = 1; g < BA_SOLVE_WAVES; ++g) v += s_p[g][lane];
         __hip_atomic_store(e < 4096 ? q.C + e : q.cam_U + (e - 4096), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the write-through stores have landed
