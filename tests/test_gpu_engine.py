@@ -221,6 +221,40 @@ def test_submit_host_async_matches_device_submit():
     h.close()
 
 
+def test_submit_host_ba_batches_in_flight():
+    """With local BA on (its own stream) two batches submitted back to back before any poll
+    each return their own poses: the result copies run on the back stream right after the
+    batch's pose stage, so the next batch's pose stage cannot overwrite them."""
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    items = (("ba_window", 4), ("ba_kf_interval", 2), ("ba_iters", 3))
+    sc = scenario(seed=0, n=8, cfg_items=items)
+    cfg, rect = sc["cfg"], sc["rect"]
+    frames = np.ascontiguousarray(sc["frames"])
+    ref = Handle([rect], cfg, max_batch=2)
+    dev = torch.from_numpy(frames).cuda()
+    want = []
+    for b in range(4):
+        ref.submit(dev[2 * b].data_ptr(), 2, torch.cuda.current_stream().cuda_stream)
+        want.append(ref.read_poses(2))
+    ref.close()
+    h = Handle([rect], cfg, max_batch=2)
+    got = []
+    for pair in range(2):
+        for b in (2 * pair, 2 * pair + 1):
+            h.submit_host(frames[2 * b:2 * b + 2])
+        got += [h.poll_batch(block=True), h.poll_batch(block=True)]
+    assert h.poll_batch(block=True) is None
+    for b, (g, w) in enumerate(zip(got, want)):
+        assert g["first_frame"] == 2 * b and g["n"] == 2
+        np.testing.assert_array_equal(g["T_rel"], w["T_rel"])
+        np.testing.assert_array_equal(g["T_abs"], w["T_abs"])
+        np.testing.assert_array_equal(g["stats"], w["stats"])
+    h.close()
+
+
 def test_engine_async_equals_sync():
     """HipSlamEngine with batches in flight (loop closure off) publishes the same poses as the
     synchronous mode (loop closure on, which waits for every batch)."""

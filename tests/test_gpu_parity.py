@@ -421,3 +421,50 @@ def test_refine_512_frame_launch_invariance():
             assert out["auto"]["stats"][i, 4] == o["best_hyp"] and out["auto"]["stats"][i, 2] == o["n_inliers"]
             assert rel_frobenius(out["auto"]["T_rel"][i], o["T"]) < 1e-9
 
+
+
+def test_blocked_chain_equals_serial_chain_over_300_frames():
+    """k_chain's blocked product (T_abs(g) = A(j) Q(g) over global 64-frame blocks, k_pose.hip)
+    against the oracle's serial left-to-right chain T_abs(t) = T_abs(t-1) inv(T_rel(t))
+    (numpy_slam.py OracleTracker._advance) over 300 frames, so the comparison crosses four block
+    boundaries: in batches of 37 (every batch but the first starts mid-block), of 300 (one launch,
+    more than four blocks per round) and of 64.  Within 1e-9 relative Frobenius at every frame, and
+    bit-identical across the three batchings."""
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    n, unique = 300, 16
+    k = np.arange(n) % (2 * (unique - 1))
+    tri = np.where(k < unique, k, 2 * (unique - 1) - k)   # consecutive frames stay consecutive
+    sc = scenario(seed=0, n=4)
+    cfg, rect = sc["cfg"], sc["rect"]
+    frames = np.ascontiguousarray(sc["src"].render_stereo_sequence(unique)[tri])
+    dev = torch.from_numpy(frames).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    out = {}
+    for batch in (37, 300, 64):
+        h = Handle([rect], cfg, max_batch=batch)
+        recs = {k: [] for k in ("stats", "T_rel", "T_abs")}
+        for b0 in range(0, n, batch):
+            m = min(batch, n - b0)
+            h.submit(dev[b0:].data_ptr(), m, s)
+            res = h.read_poses(m)
+            for key in recs:
+                recs[key].append(np.array(res[key][:m, 0], copy=True))
+        h.close()
+        out[batch] = {key: np.concatenate(v) for key, v in recs.items()}
+    for other in (300, 64):
+        for key in ("stats", "T_rel", "T_abs"):
+            np.testing.assert_array_equal(out[37][key], out[other][key], err_msg=f"batch {other}: {key}")
+    st, t_rel, t_abs = out[37]["stats"], out[37]["T_rel"], out[37]["T_abs"]
+    assert (st[1:, 0] == 0).mean() > 0.95
+    serial = np.eye(4)
+    for g in range(n):
+        if g and st[g, 0] <= 0:
+            t = t_rel[g]
+            inv = np.eye(4)
+            inv[:3, :3] = t[:3, :3].T
+            inv[:3, 3] = -(t[:3, :3].T @ t[:3, 3])
+            serial = serial @ inv
+        assert rel_frobenius(t_abs[g], serial) < 1e-9, f"frame {g}: blocked chain vs serial chain"

@@ -82,3 +82,71 @@ def test_guard_flags_mfma_destination_over_a_source(tmp_path):
     assert not any(("k_ref" in e) or ("k_mac" in e) for e in errors), errors
     spill1 = [e for e in errors if "k_spill1" in e][0]
     assert "srcA" in spill1 and "srcC (partial)" in spill1
+
+
+# rule 3: in-launch hand-offs (k_ba_reduce_solve's pattern and three ways to break it)
+HANDOFF_SRC = r"""
+#include <hip/hip_runtime.h>
+#define AGENT __HIP_MEMORY_SCOPE_AGENT
+__device__ void tail(const double* C, double* out, int last) {
+    if (!last) return;
+    out[threadIdx.x] = __hip_atomic_load(C + threadIdx.x, __ATOMIC_RELAXED, AGENT) +
+                       __hip_atomic_load(C + 256 + threadIdx.x, __ATOMIC_RELAXED, AGENT);
+}
+__global__ void k_handoff_ok(double* C, int* done, double* out, double v) {
+    __shared__ int s_last;
+    __hip_atomic_store(C + blockIdx.x * 256 + threadIdx.x, v, __ATOMIC_RELAXED, AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, AGENT) == (int)gridDim.x - 1;
+    __syncthreads();
+    tail(C, out, s_last);
+}
+__global__ void k_handoff_plain_store(double* C, int* done, double* out, double v) {
+    __shared__ int s_last;
+    C[blockIdx.x * 256 + threadIdx.x] = v;   // cached in this XCD's L2: the last block may not see it
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, AGENT) == (int)gridDim.x - 1;
+    __syncthreads();
+    tail(C, out, s_last);
+}
+__global__ void k_handoff_no_wait(double* C, int* done, double* out, double v) {
+    __shared__ int s_last;
+    __hip_atomic_store(C + blockIdx.x * 256 + threadIdx.x, v, __ATOMIC_RELAXED, AGENT);
+    if (threadIdx.x == 0) s_last = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, AGENT) == (int)gridDim.x - 1;
+    __syncthreads();
+    tail(C, out, s_last);
+}
+__global__ void k_handoff_plain_load(double* C, int* done, double* out, double v) {
+    __shared__ int s_last;
+    __hip_atomic_store(C + blockIdx.x * 256 + threadIdx.x, v, __ATOMIC_RELAXED, AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, AGENT) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (s_last) out[threadIdx.x] = C[threadIdx.x] + C[256 + threadIdx.x];
+}
+"""
+
+
+@needs_hipcc
+def test_guard_checks_the_in_launch_handoff(tmp_path):
+    """Rule 3 (the BA hand-off): published stores with sc1, drained before the
+    counter, and sc1 loads in the last block.  The shipped k_ba_reduce_solve passes (the first
+    test); each broken variant trips."""
+    src = tmp_path / "handoff.hip"
+    src.write_text(HANDOFF_SRC)
+    obj = tmp_path / "handoff.o"
+    _compile(src, obj)
+    names = ("k_handoff_ok", "k_handoff_plain_store", "k_handoff_no_wait", "k_handoff_plain_load")
+    errors = isa_guard.check([obj], handoff={n: 2 for n in names})
+    by = {n: [e for e in errors if f"{n}" in e] for n in names}
+    assert by["k_handoff_ok"] == [], errors
+    assert any("without sc1" in e for e in by["k_handoff_plain_store"]), errors
+    assert any("vmcnt(0)" in e for e in by["k_handoff_no_wait"]), errors
+    assert any("sc1 (agent-scope) loads" in e for e in by["k_handoff_plain_load"]), errors
+    # the library's own hand-off kernel is checked by default and must exist in k_ba's object
+    objs = sorted((CSRC / "build").glob("*.o"))
+    if objs:
+        assert isa_guard.check([o for o in objs if o.name == "k_ba.hip.o"]) == []

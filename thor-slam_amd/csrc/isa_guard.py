@@ -4,7 +4,15 @@
 1. spills VGPRs (``.vgpr_spill_count`` > 0) or uses private (scratch) memory at all
    (``.private_segment_fixed_size`` > 0: spills, and private arrays indexed at run time), or
 2. contains an MFMA whose destination shares registers with a source other than an exact
-   accumulate (srcC == vdst): vdst overlapping srcA / srcB, or srcC partially overlapping vdst.
+   accumulate (srcC == vdst): vdst overlapping srcA / srcB, or srcC partially overlapping vdst, or
+3. is an in-launch hand-off kernel (``HANDOFF``: blocks publish data, count themselves in, the last
+   block to arrive reads everything) whose machine code does not follow the hardware rule the
+   hand-off relies on instead of an agent-scope release / acquire pair ("the BA
+   hand-off and the memory model"): every global store before the counter atomic carries ``sc1``
+   (agent scope: written through the XCD's L2), an ``s_waitcnt vmcnt(0)`` separates the last of
+   them from the counter atomic (the stores have reached memory before the count is visible), and
+   the last block reads the published data with at least the listed number of ``sc1`` loads
+   (agent scope: not served from a stale line of its own XCD's L2).
 
 Why ("k_match and the MFMA operand rule"): the toolchain keeps the destination of a
 >128-bit MFMA apart from its sources by an early-clobber constraint, and its assembler rejects a
@@ -37,6 +45,11 @@ LLVM = Path(os.environ.get("ROCM_LLVM_BIN", "/opt/rocm/lib/llvm/bin"))
 TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
 _REG = re.compile(r"^([va])(?:\[(\d+):(\d+)\]|(\d+))$")
 _FUNC = re.compile(r"^[0-9a-f]+ <(.+)>:$")
+_BASE = re.compile(r"^_Z(\d+)")
+
+# hand-off kernel -> the agent-scope loads its last block must issue for the published data
+# (k_ba_reduce_solve: C as 4096 / 512 threads = 8 loads per thread, and the camera blocks: 1)
+HANDOFF = {"k_ba_reduce_solve": 9}
 
 
 def _run(*args: str) -> str:
@@ -110,10 +123,61 @@ def mfma_violations(co: Path) -> list[str]:
     return bad
 
 
-def check(paths: list[Path], notes: list[str] | None = None) -> list[str]:
+def _base_name(mangled: str) -> str:
+    m = _BASE.match(mangled)
+    return mangled[m.end():m.end() + int(m.group(1))] if m else mangled
+
+
+def _functions(co: Path) -> dict[str, list[str]]:
+    """Instruction lines (comments stripped) per function of the code object's disassembly."""
+    funcs: dict[str, list[str]] = {}
+    cur: list[str] | None = None
+    for line in _run(str(LLVM / "llvm-objdump"), "-d", "--mcpu=gfx950", "--no-show-raw-insn", str(co)).splitlines():
+        m = _FUNC.match(line.strip())
+        if m:
+            cur = funcs.setdefault(m.group(1), [])
+            continue
+        s = line.split("//")[0].strip()
+        if cur is not None and s:
+            cur.append(s)
+    return funcs
+
+
+def handoff_violations(co: Path, table: dict[str, int] | None = None, found: set | None = None) -> list[str]:
+    """Rule 3 over every kernel of ``table`` (default ``HANDOFF``) found in the code object (their
+    names are added to ``found``)."""
+    table = HANDOFF if table is None else table
+    bad = []
+    for func, ins in _functions(co).items():
+        name = _base_name(func)
+        if name not in table:
+            continue
+        if found is not None:
+            found.add(name)
+        # the counter: the first returning (sc0) global atomic
+        at = next((i for i, s in enumerate(ins) if s.startswith("global_atomic") and " sc0" in f" {s} "), None)
+        if at is None:
+            bad.append(f"{func}: hand-off kernel without a returning counter atomic")
+            continue
+        stores = [i for i in range(at) if ins[i].startswith("global_store")]
+        if not stores:
+            bad.append(f"{func}: hand-off kernel publishes nothing before its counter atomic")
+        for i in stores:
+            if "sc1" not in ins[i].split():
+                bad.append(f"{func}: {ins[i]}  [published store without sc1 (agent scope) before the counter]")
+        if stores and not any(s.startswith("s_waitcnt") and "vmcnt(0)" in s for s in ins[stores[-1] + 1:at]):
+            bad.append(f"{func}: no s_waitcnt vmcnt(0) between the last published store and the counter atomic")
+        loads = sum(1 for s in ins[at + 1:] if s.startswith("global_load") and "sc1" in s.split())
+        if loads < table[name]:
+            bad.append(f"{func}: {loads} sc1 (agent-scope) loads after the counter, the hand-off needs {table[name]}")
+    return bad
+
+
+def check(paths: list[Path], notes: list[str] | None = None, handoff: dict[str, int] | None = None) -> list[str]:
     """Every violation of the two rules over the given objects, as printable lines (SGPR spills
     into VGPR lanes go to ``notes`` when given)."""
     errors: list[str] = []
+    found: set = set()
     with tempfile.TemporaryDirectory() as d:
         for p in paths:
             co = code_object(Path(p), Path(d))
@@ -128,6 +192,12 @@ def check(paths: list[Path], notes: list[str] | None = None) -> list[str]:
                 if k.get("private_segment_fixed_size", 0):
                     errors.append(f"{Path(p).name}: {name} uses {k['private_segment_fixed_size']} B/lane of scratch")
             errors += [f"{Path(p).name}: {v}" for v in mfma_violations(co)]
+            errors += [f"{Path(p).name}: {v}" for v in handoff_violations(co, handoff, found)]
+    # a hand-off kernel that vanished from the library (renamed, or the objects incomplete) would
+    # pass unchecked: the library's own objects must hold every HANDOFF kernel
+    table = HANDOFF if handoff is None else handoff
+    if any(Path(p).name == "k_ba.hip.o" for p in paths) or handoff is not None:
+        errors += [f"{m}: hand-off kernel not found in the checked objects" for m in sorted(set(table) - found)]
     return errors
 
 

@@ -397,7 +397,7 @@ __device__ __forceinline__ void ba_obs_jac(const double* T, const double* X, dou
     const double xc = ((T[0] * X[0] + T[1] * X[1]) + T[2] * X[2]) + T[3];
     const double yc = ((T[4] * X[0] + T[5] * X[1]) + T[6] * X[2]) + T[7];
     const double zc = ((T[8] * X[0] + T[9] * X[1]) + T[10] * X[2]) + T[11];
-    double iz = __builtin_amdgcn_rcp(zc);   // + one Newton step (~1 ulp) instead of the division chain
+    double iz = __builtin_amdgcn_rcp(zc);   // + one Newton step instead of the division chain (error ~e0^2, e0 the estimate's)
     iz = iz * (2.0 - zc * iz);
     const double base = cal.fxb / cal.fx;
     const bool st = __builtin_isfinite(d);
@@ -621,7 +621,9 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
 #pragma unroll
                     for (int e = 0; e < 9; ++e) vg[e] += s_Vg[li][ci][e];
             // one reciprocal square root per pivot, multiplications after it (the chain had 9
-            // divisions, then 3 sqrt + division pairs): v_rsq_f64 + one Newton step, ~1 ulp
+            // divisions, then 3 sqrt + division pairs): v_rsq_f64 + one Newton step; the hardware estimate is
+            // good to roughly 2^-22..2^-26, so the result is within ~2^-44..2^-52 relative (not correctly
+            // rounded; the oracle bar is 1e-9)
             auto rsqrt_nr = [](double x) {
                 x = x > 1e-300 ? x : 1e-300;
                 const double y = __builtin_amdgcn_rsq(x);
@@ -872,7 +874,7 @@ __device__ __forceinline__ void ba_solve_block(const BatchCtx& c, const BaArgs& 
             const int jj = b6 + j;
             const double d = readlane_f64(col[j], jj);
             good = good && d > 0.0;
-            double inv = __builtin_amdgcn_rcp(d);   // + one Newton step: ~1 ulp, off the division chain
+            double inv = __builtin_amdgcn_rcp(d);   // + one Newton step (~2^-44..2^-52 relative), off the division chain
             inv = inv * (2.0 - d * inv);
             const double pre = col[j];
             const double l = lane > jj ? pre * inv : 0.0;

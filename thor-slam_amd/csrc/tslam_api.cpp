@@ -964,10 +964,16 @@ int tslam_submit_host(tslam_handle* h, const uint8_t* host_images, const double*
     if ((rc = tslam_begin_batch(h, h->as_input[k], n_frames)) != TSLAM_OK) return rc;
     const int stages[5] = {TSLAM_STAGE_RECTIFY, TSLAM_STAGE_DETECT, TSLAM_STAGE_DESCRIBE, TSLAM_STAGE_MATCH, TSLAM_STAGE_POSE};
     for (int i = 0; i < 5 && rc == TSLAM_OK; ++i) rc = tslam_run_stage(h, stages[i], i < 3 ? h->as_front : h->as_back);
-    if (rc == TSLAM_OK && h->prm.ba_window) rc = tslam_run_stage(h, TSLAM_STAGE_BA, h->as_ba);
-    // results of this batch into the pinned slot of its parity (after its BA: the caller reads
-    // the window once the slot is polled)
-    if (rc == TSLAM_OK) rc = stash_results(h, timestamps, h->prm.ba_window ? h->as_ba : h->as_back);
+    // results of this batch into the pinned slot of its parity, copied on the back stream right
+    // after its pose stage: the next batch's back stages overwrite the pose buffers in that
+    // stream's order, so the copies read this batch's records whatever the BA stream does
+    if (rc == TSLAM_OK) rc = stash_results(h, timestamps, h->as_back);
+    if (rc == TSLAM_OK && h->prm.ba_window) {
+        // the BA stream waits for the back stream (ba_stage's event is recorded after the copies),
+        // and the slot is ready once this batch's BA ran: the caller reads the window after polling
+        rc = tslam_run_stage(h, TSLAM_STAGE_BA, h->as_ba);
+        if (rc == TSLAM_OK) HIPCHK(hipEventRecord(h->as_res[(h->as_batches - 1) & 1].ev, h->as_ba));
+    }
     const int rc2 = tslam_end_batch(h);
     return rc != TSLAM_OK ? rc : rc2;
 }

@@ -150,7 +150,7 @@ struct BatchCtx {
     const double* rig_Einv;
     double* rig_pose;      // [B][68]  body T_rel, T_abs, cov
     int32_t* rig_stats;    // [B][8]
-    double* rig_state;     // [16]
+    double* rig_state;     // [32]: the rig chain's (A, Q), two row-major 4x4 (k_pose.hip blocked chain)
     double* rig_prior;     // [B][16] body-frame IMU prior (k_rig_prior, from the pairs' priors) or null
     // A4 speculative FAST threshold (DESIGN.md §5 "detect"): te[cam][l] in use, its running
     // minimum for the next batch, per (frame, cam, level) fallback flags, launch mode
