@@ -544,6 +544,101 @@ def boundary_bench(uniq: np.ndarray, src, n_frames: int, batch_sizes=(1, 64)) ->
     return out
 
 
+# ---- the reference's default drop-in path ----------------------------------
+LAP = 240          # one full turn of the 45 deg/s circle at 30 fps: the trajectory repeats
+C3_NAMES = ("192.168.2.21", "192.168.2.22", "192.168.2.23", "192.168.2.25")   # run_slam.py:45-50
+
+
+def _lap_sources(names, frames=None):
+    """Stereo sources on the bracket joints along one repeating turn (IMU on the first, with the
+    noise of an OAK-class MEMS IMU); with `frames` ({name: [LAP][2][H][W]}) they replay them."""
+    from thor_slam_amd.synthetic import CachedStereoSource, RoomScene, SyntheticStereoSource, circle_trajectory
+
+    joints = json.loads(JOINTS.read_text())
+    scene, traj = RoomScene(seed=0), circle_trajectory(LAP, yaw_rate_deg=45.0)
+    out = []
+    for k, nm in enumerate(names):
+        kw = dict(name=nm, scene=scene, trajectory=traj, rig_T_source=np.array(joints[nm]), seed=k, imu=(k == 0),
+                  gyro_noise=1e-4, accel_noise=0.01)
+        out.append(CachedStereoSource(frames[nm], **kw) if frames is not None else SyntheticStereoSource(**kw))
+    return out
+
+
+def _render_lap_chunk(args):
+    names, items = args   # items: (source index, frame, camera)
+    srcs = _lap_sources(names)
+    return [srcs[q].render_image(i, c) for q, i, c in items]
+
+
+def default_config_bench(kind: str, n_frames: int, workers: int) -> dict:
+    """SlamEngine.process_frames exactly as the reference deploys it after the two-line swap
+    (scripts/run_slam.py:299-300): HipSlamEngine(num_cameras=N) + initialize(rig.calibration), no
+    config — batch 1, loop closure on (SlamConfig.enable_loop_closure, interface.py:156), IMU fusion
+    on because the rig carries the IMU (Makefile:81, run_slam.py:249-283).  The rig replays one
+    rendered turn of a 45 deg/s circle with its IMU samples, so from the second lap on every
+    keyframe finds the previous lap: the worst case for loop closure (a search, a verification and
+    a span solve per keyframe).  Frame sets are built before timing."""
+    from thor_slam_amd.camera import CameraRig, Extrinsics
+    from thor_slam_amd.camera.types import IMUExtrinsics
+    from thor_slam_amd.slam.hip_engine import HipSlamEngine
+    from thor_slam_amd.synthetic import DRB_TO_RDF
+
+    names = C3_NAMES if kind == "c3" else C3_NAMES[:1]
+    t0 = time.perf_counter()
+    items = [(q, i, c) for q in range(len(names)) for i in range(LAP) for c in (0, 1)]
+    chunks = [items[k::workers] for k in range(workers) if items[k::workers]]
+    frames = {nm: np.empty((LAP, 2, 400, 640), np.uint8) for nm in names}
+    with ProcessPoolExecutor(max_workers=max(1, len(chunks))) as ex:
+        for ch, imgs in zip(chunks, ex.map(_render_lap_chunk, [(names, ch) for ch in chunks])):
+            for (q, i, c), img in zip(ch, imgs):
+                frames[names[q]][i, c] = img
+    t_render = time.perf_counter() - t0
+    joints = json.loads(JOINTS.read_text())
+    srcs = _lap_sources(names, frames)
+    base_T_imu = np.array(joints[names[0]]) @ DRB_TO_RDF
+    rig = CameraRig(srcs, rig_extrinsics={nm: Extrinsics.from_4x4_matrix(np.array(joints[nm])) for nm in names},
+                    imu_source=names[0], imu_extrinsics=IMUExtrinsics(names[0], Extrinsics.from_4x4_matrix(base_T_imu)))
+    rig.start()
+    warm = 64
+    sets = []
+    while len(sets) < warm + n_frames:
+        fs = rig.get_synchronized_frames()
+        if fs is not None:
+            sets.append(fs)
+    out = {"cameras": 2 * len(names), "frames": n_frames, "render_s": t_render}
+    for mode in ("default", "sync"):
+        from thor_slam_amd.params import HipSlamConfig
+
+        eng = HipSlamEngine(num_cameras=2 * len(names))
+        if mode == "default":
+            eng.initialize(rig.calibration)   # the reference's call: no config
+        else:   # the same with every batch waited for (the round-4 behaviour of this configuration)
+            eng.initialize(rig.calibration, HipSlamConfig(num_cameras=2 * len(names), sync=True))
+        cfg = eng._config
+        for fs in sets[:warm]:   # kernels, loop jobs and the pose-graph scratch warm up
+            eng.process_frames(fs)
+        eng.settle()
+        eng.reset()
+        t1 = time.perf_counter()
+        for fs in sets[warm:]:
+            eng.process_frames(fs)
+        eng.flush()
+        dt = time.perf_counter() - t1
+        lp = eng._loop
+        rec = {"fps": n_frames / dt, "batch_size": cfg.batch_size, "loop_closure": lp is not None,
+               "imu_fusion": eng._imu is not None, "imu_prior_lag": cfg.imu_prior_lag,
+               "loop_latency_frames": cfg.loop_latency, "asynchronous": bool(eng._async),
+               "keyframes": len(lp.frames) if lp is not None else 0,
+               "loops_closed": len(lp.loops) if lp is not None else 0,
+               "state": eng.get_tracking_state().name}
+        eng.shutdown()
+        if mode == "default":
+            out.update(rec)
+        else:
+            out["sync_fps"] = rec["fps"]
+    return out
+
+
 # ---- single handle (N = 1, and c5 replicas) ---------------------------------------------------
 def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     import torch
@@ -931,6 +1026,11 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     h.close()
     if rank == 0 and world == 1 and args.boundary_frames > 0 and args.config == "c2":
         out["boundary"] = boundary_bench(uniq, src, args.boundary_frames)
+        if args.default_frames > 0:
+            workers = usable_cpus()
+            out["boundary"]["default_config"] = {
+                "c2": default_config_bench("c2", args.default_frames, workers),
+                "c3": default_config_bench("c3", max(args.default_frames // 2, 1), workers)}
     if rank == 0 and world == 1 and args.cpu_budget > 0:
         procs = args.cpu_procs or usable_cpus()
         if c5:
@@ -1220,6 +1320,9 @@ def main() -> None:
     ap.add_argument("--latency-frames", type=int, default=20, help="B=1 submissions timed for latency_b1_ms")
     ap.add_argument("--boundary-frames", type=int, default=1024,
                     help="c2: frames timed through HipSlamEngine.process_frames (0 = skip)")
+    ap.add_argument("--default-frames", type=int, default=1024,
+                    help="c2: frames timed through the reference's default construction (batch 1, loop closure + "
+                         "IMU on) for C2 and (half as many) the C3 rig, in boundary.default_config (0 = skip)")
     ap.add_argument("--out", type=str, default="", help="also write the JSON line to this file")
     ap.add_argument("--outliers", type=int, default=35,
                     help="c2/c3: also time --outlier-steps pipelined steps with this %% of the refined temporal "

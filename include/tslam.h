@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 14
+#define TSLAM_ABI_VERSION 15
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -570,6 +570,41 @@ int tslam_loop_query(tslam_handle* h, int slot, int n_candidates, int32_t* votes
 int tslam_loop_verify(tslam_handle* h, int pair, int64_t frame, int slot, double* T_qc, double* cov, int32_t* stats);
 int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_edges, const int32_t* edges,
                      const double* meas, const double* info, int iters, double* cost);
+
+/* Asynchronous loop closure (ABI 15): the reference's default deployment path runs with loop
+ * closure on at batch 1 (HipSlamEngine(num_cameras=N) + initialize, scripts/run_slam.py:299-300;
+ * SlamConfig.enable_loop_closure defaults to True, interface.py:156), so nothing of it may wait on
+ * the host per frame.  Spec of the policy on top: oracle/numpy_loop.py LoopPolicy.
+ *
+ * tslam_loop_auto: with interval > 0 every tracked keyframe of every later batch (frame g with
+ *   g % interval == 0 and pose status 0: the rig's after tslam_set_rig, pair 0's otherwise) is
+ *   stored by the submit path itself, on the batch's back stream right after its pose stage (no
+ *   host round trip, no ring-residency condition).  The i-th tracked keyframe since the call (or
+ *   tslam_reset) takes database position i, entry (i mod cap_k) * P + p for each pair p, cap_k =
+ *   max_keyframes / P of tslam_loop_init: the database is a ring over tracked keyframes, so a
+ *   session of any length keeps the newest cap_k, and untracked stretches take no entries.  Each
+ *   entry also holds a snapshot of its image's keypoint records, level counts and descriptors (the
+ *   query side of a later verification).  interval 0 turns it off.  tslam_loop_add_keyframe (the
+ *   manual slot counter) is refused while it is on.  Unsharded handles only.
+ * Jobs: run in submission order on the handle's loop stream (beside the tracking streams), results
+ * in pinned memory; at most 64 jobs may be unreturned.  Each returns a job id (> 0).
+ * tslam_loop_job_vote: votes of entry `query` against the entries of database positions
+ *   [k0, k0 + n_kf): votes[(k - k0) * P + p] for pair p's entry of position k (tslam_loop_query's
+ *   rule).
+ * tslam_loop_job_verify: cam_q_T_cam_c of entry `query`'s snapshot (its pair's left image, the
+ *   RANSAC seeded by `frame`, the keyframe's frame index) against entry `cand`'s landmarks, as
+ *   tslam_loop_verify on the resident frame.
+ * tslam_loop_job_pose_graph: tslam_pose_graph's solve (inputs copied at the call).
+ * tslam_loop_job_poll: 0 while job `id` runs (block = 0), else 1 and its results once:
+ *   vote -> votes[n_kf * P]; verify -> T_qc[16], cov[36], stats[8]; pose graph -> world_T_node
+ *   [n_nodes][16] and *cost (NULL skips any output).  TSLAM_ESTATE for an unknown or returned id. */
+int tslam_loop_auto(tslam_handle* h, int interval);
+int tslam_loop_job_vote(tslam_handle* h, int query, int64_t k0, int n_kf, int64_t* job);
+int tslam_loop_job_verify(tslam_handle* h, int pair, int64_t frame, int query, int cand, int64_t* job);
+int tslam_loop_job_pose_graph(tslam_handle* h, int n_nodes, const double* world_T_node, int n_edges, const int32_t* edges,
+                              const double* meas, const double* info, int iters, int64_t* job);
+int tslam_loop_job_poll(tslam_handle* h, int64_t job, int block, int32_t* votes, double* T_qc, double* cov,
+                        int32_t* stats, double* world_T_node, double* cost);
 
 /* RGB-D dense mapping (the reference runs nvblox on the RGB + u16 depth
  * topics, scripts/run_pipeline.py:218-256, voxel 0.05 m / truncation 4 voxels / 10 m,

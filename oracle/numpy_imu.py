@@ -212,25 +212,44 @@ def batch_priors(filt: ImuFilter, samples: list) -> list:
     return out
 
 
-def run_sequence(tracker, frames: np.ndarray, samples: list, batch: int, filt: ImuFilter | None) -> list:
+def _absorb(filt: ImuFilter, items: list, samples: list) -> None:
+    """The filter absorbs a tracked batch: per frame (index, tracker result, prior)."""
+    for i, r, pr in items:
+        dt, gy, ac = samples[i]
+        if dt is None:
+            continue
+        T, C = r["T"], r["cov"]
+        if int(r["status"]) == 0 and pr is not None:
+            T, C = vision_only(T, C, r["sigma2"], pr)
+        filt.update(filt.predict(dt, gy, ac), int(r["status"]), T, C)
+
+
+def lagged_priors(filt: ImuFilter, pending: list, batch_samples: list) -> list:
+    """A batch's priors when the vision of the ``pending`` batches (tracked, not yet absorbed:
+    lists of (index, ...) items, their samples first) is not in the filter yet: the state is
+    coasted over their samples, then the batch's frames are predicted (HipSlamEngine with
+    ``imu_prior_lag`` > 0: the prior of batch s uses the vision of batches <= s - 1 - lag)."""
+    coast = [c for _, items, smp in pending for c in smp]
+    return batch_priors(filt, coast + list(batch_samples))[len(coast):]
+
+
+def run_sequence(tracker, frames: np.ndarray, samples: list, batch: int, filt: ImuFilter | None, lag: int = 0) -> list:
     """The engine's batch flow on the oracle tracker: ``samples[i]`` = (dt, gyro, accel) of frame
-    i (dt None for the first).  Returns the tracker's per-frame results."""
+    i (dt None for the first).  With ``lag`` (``HipSlamConfig.imu_prior_lag``) the prior of batch
+    s is computed before the vision of batches s - lag .. s - 1 is absorbed (they are coasted
+    over), so that many batches may be in flight.  Returns the tracker's per-frame results."""
     results = []
-    for b0 in range(0, len(frames), batch):
+    pending = []   # (batch number, [(i, result, prior)], [samples]) tracked, not yet absorbed
+    for bi, b0 in enumerate(range(0, len(frames), batch)):
         idx = range(b0, min(b0 + batch, len(frames)))
+        while filt is not None and pending and pending[0][0] <= bi - 1 - lag:
+            _absorb(filt, pending.pop(0)[1], samples)
         if filt is not None and not filt.ready:
             filt.start(samples[b0][2])
-        priors = batch_priors(filt, [samples[i] for i in idx]) if filt is not None else [None] * len(idx)
+        smp = [samples[i] for i in idx]
+        priors = lagged_priors(filt, pending, smp) if filt is not None else [None] * len(idx)
         res = [tracker.step(frames[i, 0], frames[i, 1], prior=pr) for i, pr in zip(idx, priors)]
-        if filt is not None:
-            for i, r, pr in zip(idx, res, priors):
-                dt, gy, ac = samples[i]
-                if dt is None:
-                    continue
-                T, C = r["T"], r["cov"]
-                if int(r["status"]) == 0 and pr is not None:
-                    T, C = vision_only(T, C, r["sigma2"], pr)
-                filt.update(filt.predict(dt, gy, ac), int(r["status"]), T, C)
+        pending.append((bi, list(zip(idx, res, priors)), smp))
         results += res
     return results
 
@@ -262,7 +281,7 @@ def pair_prior(prior: tuple, E: list, p: int) -> tuple:
 
 
 def run_rig_sequence(trackers: list, frames: np.ndarray, samples: list, batch: int, filt: ImuFilter, E: list,
-                     cfg) -> list:
+                     cfg, lag: int = 0) -> list:
     """A multi-pair rig in the engine's batch flow: per batch the filter's pair-0 priors for every
     pair, each pair tracked, the rig pose over all pairs (``numpy_rig.rig_pose``), the rig chained
     (an untracked body frame with the first pair's W_t > 0 follows its prediction), and the filter
@@ -272,11 +291,29 @@ def run_rig_sequence(trackers: list, frames: np.ndarray, samples: list, batch: i
     Einv = [inv_rigid(e) for e in E]
     T_abs = np.eye(4)
     out = []
-    for b0 in range(0, len(frames), batch):
+    pending = []   # (batch number, [(i, rig result)], [samples]) tracked, not yet absorbed
+
+    def absorb(items):
+        for i, res in items:
+            dt, gy, ac = samples[i]
+            if dt is None:
+                continue
+            st = int(res["status"])
+            t0 = c0 = None
+            if st == 0:
+                t0 = _inv(E[0]) @ res["T"] @ E[0]
+                ad = _adjoint(_inv(E[0]))
+                c0 = ad @ res["cov"] @ ad.T
+            filt.update(filt.predict(dt, gy, ac), st, t0, c0)
+
+    for bi, b0 in enumerate(range(0, len(frames), batch)):
         idx = range(b0, min(b0 + batch, len(frames)))
+        while pending and pending[0][0] <= bi - 1 - lag:
+            absorb(pending.pop(0)[1])
         if not filt.ready:
             filt.start(samples[b0][2])
-        priors = batch_priors(filt, [samples[i] for i in idx])
+        smp = [samples[i] for i in idx]
+        priors = lagged_priors(filt, pending, smp)
         results = []
         for i, pr in zip(idx, priors):
             outs = [trk.step(frames[i, 2 * q], frames[i, 2 * q + 1], prior=None if pr is None else pair_prior(pr, E, q))
@@ -296,15 +333,5 @@ def run_rig_sequence(trackers: list, frames: np.ndarray, samples: list, batch: i
                 T_abs = T_abs @ inv_rigid(mul4(mul4(E[0], T), Einv[0]))
             results.append(res)
             out.append({"status": int(res["status"]), "T_abs": T_abs.copy()})
-        for i, res in zip(idx, results):
-            dt, gy, ac = samples[i]
-            if dt is None:
-                continue
-            st = int(res["status"])
-            t0 = c0 = None
-            if st == 0:
-                t0 = _inv(E[0]) @ res["T"] @ E[0]
-                ad = _adjoint(_inv(E[0]))
-                c0 = ad @ res["cov"] @ ad.T
-            filt.update(filt.predict(dt, gy, ac), st, t0, c0)
+        pending.append((bi, list(zip(idx, results)), smp))
     return out

@@ -234,3 +234,135 @@ def best_candidate(votes: np.ndarray, n_allowed: int, min_votes: int) -> int:
     v = np.asarray(votes[:n_allowed])
     j = int(np.argmax(v))
     return j if v[j] >= min_votes else -1
+
+
+# --------------------------------------------------------------------------------------------
+# the asynchronous loop-closure policy (HipSlamEngine with tslam_loop_auto follows it frame by
+# frame)
+# --------------------------------------------------------------------------------------------
+
+
+def candidate_window(idx: int, cap_k: int, min_gap: int, latency: int, batch: int, interval: int) -> tuple[int, int]:
+    """Database positions (= node indices: the i-th tracked keyframe takes position i) [lo, hi]
+    the search of node ``idx`` votes against: at least ``min_gap`` nodes older, and still in the
+    ring of cap_k positions while the search runs — which may be until frame g + latency, with up
+    to two batches submitted past it whose tracked keyframes overwrite the oldest positions:
+    margin M = (latency + 2 * batch - 1) // interval + 1."""
+    margin = (latency + 2 * batch - 1) // interval + 1
+    return max(0, idx - cap_k + margin), idx - min_gap
+
+
+def best_vote(votes: list, n_pairs: int) -> tuple[int, int, int]:
+    """(best votes, query pair q, candidate index j) over every query pair's votes [n * P]
+    (candidate j = position lo + j // P, pair j % P): the most votes; ties go to the lower query
+    pair, then the NEWEST position (the smallest loop span), then the lower pair."""
+    best, q, j = -1, 0, 0
+    for qq, v in enumerate(votes):
+        v = np.asarray(v).reshape(-1, n_pairs)
+        n = v.shape[0]
+        r = int(np.argmax(v[::-1].reshape(-1)))   # newest position first, lower pair first within it
+        jj = (n - 1 - r // n_pairs) * n_pairs + r % n_pairs
+        if int(v.reshape(-1)[jj]) > best:
+            best, q, j = int(v.reshape(-1)[jj]), qq, jj
+    return best, q, j
+
+
+def span_edges(edges: list, a: int, b: int) -> list[int]:
+    """Indices of the edges (x, y), x < y, with both ends in the span [a, b], in the canonical
+    order (y, x) — the solve's summation order does not depend on when a loop edge was recorded."""
+    return sorted((e for e, (x, y) in enumerate(edges) if a <= x and y <= b), key=lambda e: (edges[e][1], edges[e][0]))
+
+
+class LoopPolicy:
+    """Keyframe pose graph + loop closure with a fixed latency.
+
+    Frames are published in order; for frame g (status, raw = pair 0's rectified-left world_T_cam
+    before loop correction):
+
+    1. a tracked (status 0) frame with g % interval == 0 is a keyframe: node idx (T = T_prev @ Z
+       with Z = raw_prev^-1 raw and the odometry edge (idx - 1, idx), or corr @ raw for the first),
+       database position idx (entry (idx mod cap_k) * P + p per pair), and a search item due at
+       frame g + latency;
+    2. every item due at or before g completes, oldest first:
+       * votes of pair q's entry of node idx against every pair's entry of the positions of
+         ``candidate_window``; ``best_vote`` picks; below ``loop_min_votes`` nothing follows;
+       * verification of the best candidate (node c, pair pc) on pair q's view (RANSAC seeded by
+         g); a loop needs status 0 and ``loop_min_inliers``;
+       * the loop edge (c, idx) with Z = M_pc T_qc^-1 M_q^-1 (M_p = rect0_T_rect_p), and the span
+         solve: Gauss-Newton (``pg_iters``) on the nodes [c, idx] with node c fixed and the edges
+         with both ends in the span (``span_edges``); the span takes the solution, later nodes
+         are re-chained by their odometry (T_i = T_{i-1} Z_i), and corr = T_last raw_last^-1;
+    3. the frame's corrected pose is corr @ raw.
+
+    A session of any length keeps the newest cap_k keyframes searchable, and the span solve bounds
+    a loop's cost by the ring (<= cap_k nodes).  ``vote(idx, q, lo, n)`` -> votes [n * P],
+    ``verify(idx, g, q, c, pc)`` -> {"T", "stats"}, ``solve(T, edges, meas, info, iters)`` ->
+    {"T", "cost"} are the device's operations (``vote`` / ``verify`` / ``optimize`` above restate
+    them)."""
+
+    def __init__(self, cfg, n_pairs: int, rect0_T_rect: list, vote, verify, solve):
+        self.cfg, self.P = cfg, int(n_pairs)
+        self.m = [np.asarray(x, dtype=np.float64) for x in rect0_T_rect]
+        self.vote, self.verify, self.solve = vote, verify, solve
+        self.cap_k = int(cfg.loop_max_keyframes)
+        self.info = loop_information(cfg.pg_sigma_t, cfg.pg_sigma_r)
+        self.frames, self.raw, self.T, self.odo = [], [], [], []
+        self.edges, self.meas = [], []
+        self.loops, self.loop_pairs = [], []
+        self.items = []   # [idx, g, due]
+        self.corr = np.eye(4)
+        self.cost = 0.0
+
+    def step(self, g: int, status: int, raw: np.ndarray) -> np.ndarray:
+        """Frame g -> its corrected pose (rect-left world_T_cam)."""
+        if status == 0 and g % self.cfg.loop_kf_interval == 0:
+            self._node(g, raw)
+        while self.items and self.items[0][2] <= g:
+            self._complete(*self.items.pop(0)[:2])
+        return self.corr @ raw
+
+    def finish(self) -> None:
+        """Complete every pending item now (HipSlamEngine.settle)."""
+        while self.items:
+            self._complete(*self.items.pop(0)[:2])
+
+    def _node(self, g: int, raw: np.ndarray) -> None:
+        idx = len(self.frames)
+        if idx == 0:
+            T, Z = self.corr @ raw, None
+        else:
+            Z = inv_se3(self.raw[-1]) @ raw
+            T = self.T[-1] @ Z
+            self.edges.append((idx - 1, idx))
+            self.meas.append(Z)
+        self.frames.append(g)
+        self.raw.append(np.array(raw, dtype=np.float64, copy=True))
+        self.T.append(T)
+        self.odo.append(Z)
+        self.items.append([idx, g, g + int(self.cfg.loop_latency)])
+
+    def _complete(self, idx: int, g: int) -> None:
+        cfg, P = self.cfg, self.P
+        lo, hi = candidate_window(idx, self.cap_k, cfg.loop_min_gap, cfg.loop_latency, cfg.batch_size,
+                                  cfg.loop_kf_interval)
+        if hi < lo:
+            return
+        best, q, j = best_vote([self.vote(idx, qq, lo, hi - lo + 1) for qq in range(P)], P)
+        if best < cfg.loop_min_votes:
+            return
+        c, pc = lo + j // P, j % P
+        ver = self.verify(idx, g, q, c, pc)
+        if int(ver["stats"][0]) != 0 or int(ver["stats"][2]) < cfg.loop_min_inliers:
+            return
+        self.edges.append((c, idx))
+        self.meas.append(self.m[pc] @ inv_se3(ver["T"]) @ inv_se3(self.m[q]))
+        self.loops.append((self.frames[c], g, int(ver["stats"][2])))
+        self.loop_pairs.append((pc, q))
+        sel = span_edges(self.edges, c, idx)
+        sol = self.solve(np.stack(self.T[c:idx + 1]), np.array([self.edges[e] for e in sel]) - c,
+                         np.stack([self.meas[e] for e in sel]), np.stack([self.info] * len(sel)), cfg.pg_iters)
+        self.T[c:idx + 1] = list(sol["T"])
+        for i in range(idx + 1, len(self.T)):
+            self.T[i] = self.T[i - 1] @ self.odo[i]
+        self.corr = self.T[-1] @ inv_se3(self.raw[-1])
+        self.cost = float(sol["cost"])

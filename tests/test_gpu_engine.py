@@ -65,7 +65,9 @@ def _engine_poses(cfg, n, batch):
     src = make_source(0)
     rig = CameraRig([src], rig_extrinsics={src.name: Extrinsics.from_4x4_matrix(src.rig_T_source)})
     rig.start()
-    eng = HipSlamEngine(num_cameras=2, config=HipSlamConfig(batch_size=batch))
+    # sync: every call returns its own frame's pose (the asynchronous default returns the newest
+    # completed one, which may lag)
+    eng = HipSlamEngine(num_cameras=2, config=HipSlamConfig(batch_size=batch, sync=True))
     eng.initialize(rig.calibration)
     poses, states = [], []
     for _ in range(n):
@@ -256,8 +258,8 @@ def test_submit_host_ba_batches_in_flight():
 
 
 def test_engine_async_equals_sync():
-    """HipSlamEngine with batches in flight (loop closure off) publishes the same poses as the
-    synchronous mode (loop closure on, which waits for every batch)."""
+    """HipSlamEngine with batches in flight publishes the same poses as the synchronous mode
+    (``sync``: every batch waited for)."""
     from thor_slam_amd.camera.rig import CameraRig
     from thor_slam_amd.params import HipSlamConfig
     from thor_slam_amd.slam.hip_engine import HipSlamEngine
@@ -265,11 +267,11 @@ def test_engine_async_equals_sync():
     from helpers import make_source
 
     poses = {}
-    for mode, loop in (("async", False), ("sync", True)):
+    for mode, sync in (("async", False), ("sync", True)):
         src = make_source(seed=1, n_frames=40)
         rig = CameraRig([src])
         rig.start()
-        eng = HipSlamEngine(num_cameras=2, config=HipSlamConfig(batch_size=3, enable_loop_closure=loop))
+        eng = HipSlamEngine(num_cameras=2, config=HipSlamConfig(batch_size=3, sync=sync))
         eng.initialize(rig.calibration)
         out = []
         for _ in range(10):

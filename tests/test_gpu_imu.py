@@ -146,17 +146,19 @@ def _run_engine(rig, n, cfg, num_cameras=2, keep=None):
     return cat, rects
 
 
-def test_accelerometer_prior_and_dropout_match_oracle():
+@pytest.mark.parametrize("batch,lag", [(4, 1), (1, 1), (4, 0)])
+def test_accelerometer_prior_and_dropout_match_oracle(batch, lag):
     """The engine's gyro + accelerometer leg (host filter -> tslam_set_motion_prior -> k_refine's
     translation prior and k_chain's IMU chaining) against oracle/numpy_imu.run_sequence on the same
     frames and samples, across a 3-frame visual dropout: statuses and RANSAC winners identical,
-    T_abs within 1e-9."""
+    T_abs within 1e-9.  With imu_prior_lag 1 (the default) the prior of batch s lacks the vision of
+    batch s - 1 (lagged_priors), so batches stay in flight; batch 1 is the default drop-in path."""
     from oracle import numpy_imu as OI
     from thor_slam_amd.params import HipSlamConfig
 
-    n, batch = 20, 4
+    n = 20
     src, rig = _imu_rig(blackout=(9, 12), accel_noise=0.01, gyro_noise=1e-4)
-    cfg = HipSlamConfig(imu_fusion=True, imu_accel=True, batch_size=batch)
+    cfg = HipSlamConfig(imu_fusion=True, imu_accel=True, batch_size=batch, imu_prior_lag=lag)
     res, rects = _run_engine(rig, n, cfg)
     rect = rects[0]
     cal = rig.calibration
@@ -174,7 +176,7 @@ def test_accelerometer_prior_and_dropout_match_oracle():
                                     map_l=rect.map_left, map_r=rect.map_right))
     frames = np.stack([np.stack([src.render_image(i, 0), src.render_image(i, 1)]) for i in range(n)])
     filt = oracle_filter(cfg, rect_T_imu)
-    want = OI.run_sequence(trk, frames, samples, batch, filt)
+    want = OI.run_sequence(trk, frames, samples, batch, filt, lag=cfg.imu_prior_lag)
     status = [int(w["status"]) for w in want]
     assert status[9:13] == [1, 1, 1, 1] and status[13:] == [0] * (n - 13)   # the dropout, then tracking
     for g in range(n):
@@ -278,7 +280,7 @@ def test_rig_imu_dropout_matches_oracle():
     trks = [O.OracleTracker(cfg, dict(fx=r.fx, fy=r.fy, cx=r.cx, cy=r.cy, baseline=r.baseline, map_l=r.map_left,
                                       map_r=r.map_right)) for r in rects]
     filt = oracle_filter(cfg, np.linalg.inv(E[0]) @ base_T_imu)
-    want = OI.run_rig_sequence(trks, frames, samples, batch, filt, E, cfg)
+    want = OI.run_rig_sequence(trks, frames, samples, batch, filt, E, cfg, lag=cfg.imu_prior_lag)
     status = [w["status"] for w in want]
     assert status[9:13] == [1] * 4 and status[13:] == [0] * (n - 13)   # frame 12 has no frame 11 to match
     for g in range(n):

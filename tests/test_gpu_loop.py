@@ -157,6 +157,7 @@ def test_engine_closes_the_loop():
     dev = torch.from_numpy(frames).cuda()
     for b0 in range(0, LOOP_FRAMES, 30):
         eng.process_batch(dev[b0:b0 + 30], [src.timestamp(i) for i in range(b0, b0 + 30)])
+    eng.settle()   # the searches of the last keyframes (due loop_latency frames later)
     loops = eng.loop_closures
     assert loops, "no loop closed"
     assert all(c <= 40 and q >= 225 for c, q, _ in loops), loops
@@ -237,6 +238,7 @@ def test_engine_closes_the_loop_on_a_two_source_rig():
     dev = torch.from_numpy(frames).cuda()
     for b0 in range(0, LOOP_FRAMES, 30):
         eng.process_batch(dev[b0:b0 + 30], [srcs[0].timestamp(i) for i in range(b0, b0 + 30)])
+    eng.settle()
     loops = eng.loop_closures
     assert loops, "no loop closed"
     pg, lp, bt = eng.pose_graph, eng._loop, eng._base_T_rect
@@ -286,6 +288,7 @@ def test_rig_loop_seen_only_by_pair_1():
     dev = torch.from_numpy(frames).cuda()
     for b0 in range(0, LOOP_FRAMES, 30):
         eng.process_batch(dev[b0:b0 + 30], [srcs[0].timestamp(i) for i in range(b0, b0 + 30)])
+    eng.settle()
     loops = eng.loop_closures
     assert loops, "no loop closed"
     assert all(c <= 40 and q >= 225 for c, q, _ in loops), loops

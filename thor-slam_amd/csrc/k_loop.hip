@@ -8,6 +8,10 @@
 // The first S landmarks are the keyframe's signature (the strongest level-0 corners with depth).
 //
 //   k_loop_store  one block: valid keypoints with a disparity d > 0 -> compacted landmarks;
+//   k_loop_store_auto  the same for every keyframe of a batch (grid keyframes x pairs, on the
+//                 batch's back stream after its pose stage; tslam_loop_auto), plus a snapshot of
+//                 the keyframe image's keypoint records, level counts and descriptors, so a later
+//                 verification needs no ring slot;
 //   k_loop_vote   block per candidate keyframe: each of the query's S signature descriptors is
 //                 matched by brute-force Hamming against the candidate's signature (LDS
 //                 broadcasts, best / second by (distance, index)); ratio + max_hamming votes;
@@ -17,8 +21,8 @@
 
 #define LP_THREADS 256
 
-__global__ __launch_bounds__(LP_THREADS) void k_loop_store(BatchCtx c, int pair, int rslot, double* xyz, uint32_t* desc,
-                                                           int32_t* n_out) {
+__device__ __forceinline__ void loop_store_block(const BatchCtx& c, int pair, int rslot, double* xyz, uint32_t* desc,
+                                                 int32_t* n_out) {
     __shared__ int s_tmp[LP_THREADS / 64];
     const int K = c.g.K, cam = c.cpp * pair;
     const size_t ib = (size_t)rslot * c.C + cam;
@@ -70,12 +74,66 @@ __global__ __launch_bounds__(LP_THREADS) void k_loop_store(BatchCtx c, int pair,
     if (threadIdx.x == 0) *n_out = n;
 }
 
+__global__ __launch_bounds__(LP_THREADS) void k_loop_store(BatchCtx c, int pair, int rslot, double* xyz, uint32_t* desc,
+                                                           int32_t* n_out) {
+    loop_store_block(c, pair, rslot, xyz, desc, n_out);
+}
+
+// Tracked keyframes of a batch (tslam_loop_auto): keyframe frames g = k * interval of the batch
+// whose pose status is 0 (the rig's with `rig`, pair 0's otherwise) take the next database
+// positions in frame order, position i -> entry (i mod capk) * P + pair; *count holds the
+// positions taken by earlier batches (k_loop_count_commit adds this batch's after the stores).
+__device__ __forceinline__ bool kf_tracked(const BatchCtx& c, int64_t g, bool rig) {
+    const int64_t f = g - c.g0;
+    return (rig ? c.rig_stats[f * TS_STATS_INTS] : c.stats[f * c.P * TS_STATS_INTS]) == 0;
+}
+
+// grid (keyframes of the batch, pairs): keyframe k_first + x is frame (k_first + x) * interval
+__global__ __launch_bounds__(LP_THREADS) void k_loop_store_auto(BatchCtx c, int interval, int64_t k_first, int capk,
+                                                                bool rig, const int64_t* count, LoopDb db) {
+    __shared__ int s_before;
+    const int x = blockIdx.x;
+    const int pair = blockIdx.y, K = c.g.K, L = c.g.n_levels;
+    if (!kf_tracked(c, (k_first + x) * interval, rig)) return;
+    if (threadIdx.x == 0) s_before = 0;
+    __syncthreads();
+    int mine = 0;   // tracked keyframes of this batch before x
+    for (int i = threadIdx.x; i < x; i += LP_THREADS) mine += kf_tracked(c, (k_first + i) * interval, rig);
+    if (mine) atomicAdd(&s_before, mine);   // integer count: order-free
+    __syncthreads();
+    const int64_t pos = *count + s_before;
+    const int rslot = ring_slot(c, (k_first + x) * interval);
+    const size_t e = (size_t)(pos % capk) * c.P + pair;
+    loop_store_block(c, pair, rslot, db.xyz + e * K * 3, db.desc + e * K * 8, db.n + e);
+    const size_t ib = (size_t)rslot * c.C + c.cpp * pair;
+    const uint2* kp = reinterpret_cast<const uint2*>(c.kps + ib * K * 2);   // one 8-byte record per keypoint
+    uint2* skp = reinterpret_cast<uint2*>(db.snap_kps + e * K * 2);
+    for (int i = threadIdx.x; i < K; i += LP_THREADS) skp[i] = kp[i];
+    const uint4* dsrc = reinterpret_cast<const uint4*>(c.desc + ib * K * 8);
+    uint4* ddst = reinterpret_cast<uint4*>(db.snap_desc + e * K * 8);
+    for (int i = threadIdx.x; i < K * 2; i += LP_THREADS) ddst[i] = dsrc[i];
+    if ((int)threadIdx.x < L) db.snap_kcount[e * TS_MAX_LEVELS + threadIdx.x] = c.kcount[ib * L + threadIdx.x];
+}
+
+// one wave: *count += the batch's tracked keyframes (after the stores read it)
+__global__ __launch_bounds__(64) void k_loop_count_commit(BatchCtx c, int interval, int64_t k_first, int nkf, bool rig,
+                                                          int64_t* count) {
+    int n = 0;
+    for (int i = threadIdx.x; i < nkf; i += 64) n += kf_tracked(c, (k_first + i) * interval, rig);
+    for (int o = 32; o; o >>= 1) n += __shfl_xor(n, o, 64);
+    if (threadIdx.x == 0) *count += n;
+}
+
 // grid = candidates, block = LP_THREADS (S <= LP_THREADS): thread t owns query signature entry t.
+// Candidate b is entry ((k0 + b / P) mod capk) * P + b mod P (keyframe-major, every pair's entry;
+// the manual database passes k0 = 0, P = 1 and a capk above the count: entry b).
 __global__ __launch_bounds__(LP_THREADS) void k_loop_vote(const uint32_t* db_desc, const int32_t* db_n, int K, int S,
-                                                          int q_slot, int max_hamming, int ratio_pct, int32_t* votes) {
+                                                          int q_slot, int64_t k0, int capk, int P, int max_hamming,
+                                                          int ratio_pct, int32_t* votes) {
     __shared__ uint4 s_d[LP_THREADS][2];
     __shared__ int s_votes;
-    const int cand = blockIdx.x, t = threadIdx.x;
+    const int t = threadIdx.x;
+    const int cand = (int)(((k0 + blockIdx.x / P) % capk) * P + blockIdx.x % P);
     const int nc = min(S, db_n[cand]), nq = min(S, db_n[q_slot]);
     if (t == 0) s_votes = 0;
     for (int i = t; i < 2 * nc; i += LP_THREADS)
@@ -104,7 +162,7 @@ __global__ __launch_bounds__(LP_THREADS) void k_loop_vote(const uint32_t* db_des
             atomicAdd(&s_votes, 1);   // integer count: order-free
     }
     __syncthreads();
-    if (t == 0) votes[cand] = s_votes;
+    if (t == 0) votes[blockIdx.x] = s_votes;
 }
 
 void launch_loop_store(const BatchCtx& c, int pair, int64_t frame, double* xyz, uint32_t* desc, int32_t* n_out,
@@ -112,8 +170,18 @@ void launch_loop_store(const BatchCtx& c, int pair, int64_t frame, double* xyz, 
     hipLaunchKernelGGL(k_loop_store, dim3(1), dim3(LP_THREADS), 0, s, c, pair, ring_slot(c, frame), xyz, desc, n_out);
 }
 
-void launch_loop_vote(const uint32_t* db_desc, const int32_t* db_n, int K, int S, int q_slot, int n_cand,
-                      int max_hamming, int ratio_pct, int32_t* votes, hipStream_t s) {
-    hipLaunchKernelGGL(k_loop_vote, dim3(n_cand), dim3(LP_THREADS), 0, s, db_desc, db_n, K, S, q_slot, max_hamming,
-                       ratio_pct, votes);
+void launch_loop_store_auto(const BatchCtx& c, int interval, const LoopDb& db, int capk, bool rig, int64_t* count,
+                            hipStream_t s) {
+    const int64_t k_first = (c.g0 + interval - 1) / interval, k_last = (c.g0 + c.n - 1) / interval;
+    if (k_last < k_first) return;
+    const int nkf = (int)(k_last - k_first + 1);
+    hipLaunchKernelGGL(k_loop_store_auto, dim3(nkf, c.P), dim3(LP_THREADS), 0, s, c, interval, k_first, capk, rig,
+                       (const int64_t*)count, db);
+    hipLaunchKernelGGL(k_loop_count_commit, dim3(1), dim3(64), 0, s, c, interval, k_first, nkf, rig, count);
+}
+
+void launch_loop_vote(const uint32_t* db_desc, const int32_t* db_n, int K, int S, int q_slot, int64_t k0, int capk, int P,
+                      int n_cand, int max_hamming, int ratio_pct, int32_t* votes, hipStream_t s) {
+    hipLaunchKernelGGL(k_loop_vote, dim3(n_cand), dim3(LP_THREADS), 0, s, db_desc, db_n, K, S, q_slot, k0, capk, P,
+                       max_hamming, ratio_pct, votes);
 }

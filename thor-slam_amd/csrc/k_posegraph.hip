@@ -11,8 +11,12 @@
 //                  multiple of 32 with identity): fixed-order sums over the node's incident edges
 //                  (CSR built on the host, sorted by edge) — deterministic, no atomics;
 //   k_pg_potrf     right-looking blocked Cholesky, panel k: every block factors the 32x32 diagonal
-//                  tile in registers (block 0 writes it), blocks 1.. solve their tile row of the
-//                  panel; tiles outside the matrix profile (zero, no fill-in) are skipped;
+//                  tile in registers from its lower triangle, blocks 1.. solve their tile row of the
+//                  panel, and block 0 stores L_kk where no block of the launch reads: the strict
+//                  lower part transposed into the tile's upper triangle, the diagonal into Ld (the
+//                  blocks of one launch need not be resident together, so L_kk written in place
+//                  would race with a late block's read of A_kk); tiles outside the matrix profile
+//                  (zero, no fill-in) are skipped;
 //   k_pg_syrk      trailing update A_IJ -= L_Ik L_Jk^T, one 32x32 tile per block, four waves of
 //                  v_mfma_f64_16x16x4f64 (the dense J^T J work on the FP64 matrix cores);
 //   k_pg_trsv      one block: blocked forward / backward substitution (wave 0 solves the 32x32
@@ -279,9 +283,10 @@ __device__ __forceinline__ void pg_factor_tile(const double* H, int np, size_t d
     }
 }
 
-// panel k: block 0 writes L_kk; block b >= 1 solves tile row I = k + b (X L_kk^T = A_Ik), unless
-// that tile row is outside the profile of column k.
-__global__ __launch_bounds__(64) void k_pg_potrf(double* H, int np, int k, const int32_t* ftile) {
+// panel k: block 0 stores L_kk (strict lower part as the tile's upper triangle, L^T, the diagonal
+// in Ld); block b >= 1 solves tile row I = k + b (X L_kk^T = A_Ik), unless that tile row is
+// outside the profile of column k.
+__global__ __launch_bounds__(64) void k_pg_potrf(double* H, int np, int k, const int32_t* ftile, double* Ld) {
     __shared__ double s_L[PG_TILE][PG_TILE + 1];
     const int I = k + blockIdx.x;
     if (blockIdx.x > 0 && ftile[I] > k) return;
@@ -290,10 +295,15 @@ __global__ __launch_bounds__(64) void k_pg_potrf(double* H, int np, int k, const
     double r[PG_TILE];
     pg_factor_tile(H, np, d0, t, r);
     if (blockIdx.x == 0) {
-        if (threadIdx.x < PG_TILE)
+        if (threadIdx.x < PG_TILE) {
+            double dg = 0.0;
 #pragma unroll
-            for (int c = 0; c < PG_TILE; ++c)
-                if (c <= t) H[(d0 + t) * np + d0 + c] = r[c];
+            for (int c = 0; c < PG_TILE; ++c) {
+                if (c < t) H[(d0 + c) * np + d0 + t] = r[c];   // L[t][c] at (c, t): coalesced over t
+                if (c == t) dg = r[c];   // (a run-time index into r would put it in scratch)
+            }
+            Ld[d0 + t] = dg;
+        }
         return;
     }
     if (threadIdx.x < PG_TILE)
@@ -347,7 +357,7 @@ __global__ __launch_bounds__(256) void k_pg_syrk(double* H, int np, int k, const
 // 32-lane sum), backward one column element per thread (consecutive threads, consecutive bytes).
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(PG_TRSV_THREADS) void k_pg_trsv(const double* H, int np, const double* g, double* delta,
-                                                             const int32_t* ftile) {
+                                                             const int32_t* ftile, const double* Ld) {
     __shared__ double s_r[PG_MAX_N];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int nt = np / PG_TILE;
@@ -357,9 +367,9 @@ __global__ __launch_bounds__(PG_TRSV_THREADS) void k_pg_trsv(const double* H, in
     for (int k = 0; k < nt; ++k) {   // forward: L y = -g
         const int d0 = k * PG_TILE;
         if (wave == 0) {
-            double l[PG_TILE];
+            double l[PG_TILE];   // row tl of L_kk: L[tl][c] is stored at (c, tl), the diagonal in Ld
 #pragma unroll
-            for (int c = 0; c < PG_TILE; ++c) l[c] = H[(size_t)(d0 + tl) * np + d0 + c];
+            for (int c = 0; c < PG_TILE; ++c) l[c] = c == tl ? Ld[d0 + tl] : H[(size_t)(d0 + c) * np + d0 + tl];
             double y = s_r[d0 + tl];
 #pragma unroll
             for (int c = 0; c < PG_TILE; ++c) {
@@ -386,9 +396,9 @@ __global__ __launch_bounds__(PG_TRSV_THREADS) void k_pg_trsv(const double* H, in
     for (int k = nt - 1; k >= 0; --k) {   // backward: L^T x = y
         const int d0 = k * PG_TILE;
         if (wave == 0) {
-            double lc[PG_TILE];   // column tl of the diagonal tile: lc[c] = L[d0 + c][d0 + tl]
+            double lc[PG_TILE];   // column tl of L_kk: lc[c] = L[c][tl], stored at (tl, c)
 #pragma unroll
-            for (int c = 0; c < PG_TILE; ++c) lc[c] = H[(size_t)(d0 + c) * np + d0 + tl];
+            for (int c = 0; c < PG_TILE; ++c) lc[c] = c == tl ? Ld[d0 + tl] : H[(size_t)(d0 + tl) * np + d0 + c];
             double x = s_r[d0 + tl];
 #pragma unroll
             for (int c = PG_TILE - 1; c >= 0; --c) {
@@ -421,20 +431,29 @@ __global__ __launch_bounds__(64) void k_pg_update(double* T, const double* delta
 
 void launch_pose_graph_iteration(double* T, const int32_t* edges, const double* Z, const double* info, int N, int E,
                                  const int32_t* adj_off, const int32_t* adj, const int32_t* ftile, double* terms,
-                                 double* H, double* g, double* delta, hipStream_t s) {
+                                 double* H, double* g, double* delta, double* Ld, hipStream_t s) {
     const int n = 6 * (N - 1), np = (n + PG_TILE - 1) / PG_TILE * PG_TILE, nt = np / PG_TILE;
     hipLaunchKernelGGL(k_pg_edges, dim3((E + 63) / 64), dim3(64), 0, s, T, edges, Z, info, E, terms);
     hipLaunchKernelGGL(k_pg_assemble, dim3((np + 255) / 256, np), dim3(256), 0, s, terms, edges, adj_off, adj, n, np, H, g);
     for (int k = 0; k < nt; ++k) {
-        hipLaunchKernelGGL(k_pg_potrf, dim3(nt - k), dim3(64), 0, s, H, np, k, ftile);
+        hipLaunchKernelGGL(k_pg_potrf, dim3(nt - k), dim3(64), 0, s, H, np, k, ftile, Ld);
         const int m = nt - k - 1;
         if (m > 0) hipLaunchKernelGGL(k_pg_syrk, dim3(m * (m + 1) / 2), dim3(256), 0, s, H, np, k, ftile);
     }
-    hipLaunchKernelGGL(k_pg_trsv, dim3(1), dim3(PG_TRSV_THREADS), 0, s, H, np, g, delta, ftile);
+    hipLaunchKernelGGL(k_pg_trsv, dim3(1), dim3(PG_TRSV_THREADS), 0, s, H, np, g, delta, ftile, Ld);
     hipLaunchKernelGGL(k_pg_update, dim3((N + 62) / 64), dim3(64), 0, s, T, delta, N);
 }
 
+// the cost sum_k e_k^T info_k e_k in edge order (one lane: the order the host summed in before)
+__global__ __launch_bounds__(64) void k_pg_cost_sum(const double* terms, int E, double* cost) {
+    if (threadIdx.x) return;
+    double cs = 0.0;
+    for (int k = 0; k < E; ++k) cs += terms[(size_t)128 * k + 120];
+    *cost = cs;
+}
+
 void launch_pose_graph_cost(const double* T, const int32_t* edges, const double* Z, const double* info, int E,
-                            double* terms, hipStream_t s) {
-    hipLaunchKernelGGL(k_pg_edges, dim3((E + 63) / 64), dim3(64), 0, s, T, edges, Z, info, E, terms);
+                            double* terms, double* cost, hipStream_t s) {
+    if (E > 0) hipLaunchKernelGGL(k_pg_edges, dim3((E + 63) / 64), dim3(64), 0, s, T, edges, Z, info, E, terms);
+    hipLaunchKernelGGL(k_pg_cost_sum, dim3(1), dim3(64), 0, s, terms, E, cost);
 }

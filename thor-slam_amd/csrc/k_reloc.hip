@@ -13,19 +13,19 @@
 
 // One thread per query keypoint; the block stages the map descriptors chunk by chunk (LDS
 // broadcasts: every thread reads the same descriptor) and keeps best / second per query.
-__global__ __launch_bounds__(256) void k_reloc_match(BatchCtx c, int cam, int slot, const uint32_t* map_desc, int M,
-                                                     int32_t* match) {
+__global__ __launch_bounds__(256) void k_reloc_match(BatchCtx c, RelocQuery qi, const uint32_t* map_desc, int M_arg,
+                                                     const int32_t* dM, int32_t* match) {
     __shared__ uint4 s_d[RL_CHUNK][2];
     const int K = c.g.K;
+    const int M = dM ? *dM : M_arg;
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t ib = (size_t)slot * c.C + cam;
     bool valid = false;
     uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (q < K) {
-        const uint32_t meta = c.kps[(ib * K + q) * 2 + 1];
+        const uint32_t meta = qi.kps[(size_t)q * 2 + 1];
         const int l = (int)(meta & 0xFF);
-        valid = q - c.g.koff[l] < c.kcount[ib * c.g.n_levels + l];
-        const uint4* src = reinterpret_cast<const uint4*>(c.desc + (ib * K + q) * 8);
+        valid = q - c.g.koff[l] < qi.kcount[l];
+        const uint4* src = reinterpret_cast<const uint4*>(qi.desc + (size_t)q * 8);
         const uint4 a = src[0], b = src[1];
         d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
     }
@@ -64,7 +64,7 @@ __global__ __launch_bounds__(256) void k_reloc_match(BatchCtx c, int cam, int sl
 
 // One block: the matches in keypoint order -> correspondence rows (A7 layout) + stats.  `xf`
 // (row-major 3x4, or null): the map point enters as xf * X (the rig's per-pair frame E_p^-1).
-__global__ __launch_bounds__(256) void k_reloc_corr(BatchCtx c, int cam, int slot, int pair, const double* map_xyz,
+__global__ __launch_bounds__(256) void k_reloc_corr(BatchCtx c, RelocQuery qi, int pair, const double* map_xyz,
                                                     const double* xf, const int32_t* match, double* corr, int32_t* stats,
                                                     double* pose, int64_t frame) {
     __shared__ int s_tmp[32];
@@ -72,7 +72,6 @@ __global__ __launch_bounds__(256) void k_reloc_corr(BatchCtx c, int cam, int slo
     // the pose record starts as k_corr leaves it (identity T_rel, zeros): k_refine writes the 3x4
     // part only, and k_rig_pose reads the whole 4x4
     for (int i = threadIdx.x; i < TS_POSE_DOUBLES; i += blockDim.x) pose[i] = (i < 16 && (i % 5) == 0) ? 1.0 : 0.0;
-    const size_t ib = (size_t)slot * c.C + cam;
     const PairCalib cal = c.calib[pair];
     const double fx = cal.fx, fy = cal.fy, cx = cal.cx, cy = cal.cy;
     int n = 0;
@@ -95,7 +94,7 @@ __global__ __launch_bounds__(256) void k_reloc_corr(BatchCtx c, int cam, int slo
             tot += s_tmp[w];
         }
         if (flag) {
-            const uint32_t xy = c.kps[(ib * K + q) * 2], meta = c.kps[(ib * K + q) * 2 + 1];
+            const uint32_t xy = qi.kps[(size_t)q * 2], meta = qi.kps[(size_t)q * 2 + 1];
             const double sc = (double)(1 << (meta & 0xFF));
             const double u = ((double)(xy & 0xFFFF) + 0.5) * sc - 0.5;
             const double v = ((double)(xy >> 16) + 0.5) * sc - 0.5;
@@ -131,9 +130,17 @@ __global__ __launch_bounds__(256) void k_reloc_corr(BatchCtx c, int cam, int slo
 
 void launch_reloc(const BatchCtx& c, int pair, int64_t frame, const double* map_xyz, const uint32_t* map_desc, int M,
                   int32_t* match, double* corr, int32_t* stats, double* pose, double* ransac, double* hyp, hipStream_t s) {
-    const int slot = ring_slot(c, frame), cam = c.cpp * pair;
-    hipLaunchKernelGGL(k_reloc_match, dim3((c.g.K + 255) / 256), dim3(256), 0, s, c, cam, slot, map_desc, M, match);
-    hipLaunchKernelGGL(k_reloc_corr, dim3(1), dim3(256), 0, s, c, cam, slot, pair, map_xyz, (const double*)nullptr, match,
+    launch_reloc_query(c, pair, frame, reloc_query_ring(c, c.cpp * pair, frame), map_xyz, map_desc, M, nullptr, match, corr,
+                       stats, pose, ransac, hyp, s);
+}
+
+// The same from an explicit query image (a keyframe database snapshot: loop verification jobs
+// that run after the frame's ring slot was reused); frame = the RANSAC seed.
+void launch_reloc_query(const BatchCtx& c, int pair, int64_t frame, RelocQuery q, const double* map_xyz,
+                        const uint32_t* map_desc, int M, const int32_t* dM, int32_t* match, double* corr, int32_t* stats,
+                        double* pose, double* ransac, double* hyp, hipStream_t s) {
+    hipLaunchKernelGGL(k_reloc_match, dim3((c.g.K + 255) / 256), dim3(256), 0, s, c, q, map_desc, M, dM, match);
+    hipLaunchKernelGGL(k_reloc_corr, dim3(1), dim3(256), 0, s, c, q, pair, map_xyz, (const double*)nullptr, match,
                        corr, stats, pose, frame);
     BatchCtx r = c;   // A7's RANSAC + refinement on the relocalisation scratch: one frame, one "pair"
     r.n = 1;
@@ -141,6 +148,8 @@ void launch_reloc(const BatchCtx& c, int pair, int64_t frame, const double* map_
     r.pair0 = 0;
     r.npair = 1;
     r.g0 = frame;
+    r.prior = nullptr;   // no IMU prior: the solve is the map's alone
+    r.rig_prior = nullptr;
     r.calib[0] = c.calib[pair];
     r.corr = corr;
     r.stats = stats;
@@ -159,11 +168,13 @@ void launch_reloc(const BatchCtx& c, int pair, int64_t frame, const double* map_
 void launch_reloc_rig(const BatchCtx& c, int64_t frame, const double* map_xyz, const uint32_t* map_desc, int M,
                       int32_t* match, double* corr, int32_t* stats, double* pose, double* ransac, double* hyp,
                       double* rig_pose, int32_t* rig_stats, hipStream_t s) {
-    const int slot = ring_slot(c, frame), K = c.g.K;
+    const int K = c.g.K;
     for (int p = 0; p < c.P; ++p) {
         int32_t* mp = match + (size_t)p * K;
-        hipLaunchKernelGGL(k_reloc_match, dim3((K + 255) / 256), dim3(256), 0, s, c, c.cpp * p, slot, map_desc, M, mp);
-        hipLaunchKernelGGL(k_reloc_corr, dim3(1), dim3(256), 0, s, c, c.cpp * p, slot, p, map_xyz, c.rig_Einv + 16 * p, mp,
+        const RelocQuery q = reloc_query_ring(c, c.cpp * p, frame);
+        hipLaunchKernelGGL(k_reloc_match, dim3((K + 255) / 256), dim3(256), 0, s, c, q, map_desc, M, (const int32_t*)nullptr,
+                           mp);
+        hipLaunchKernelGGL(k_reloc_corr, dim3(1), dim3(256), 0, s, c, q, p, map_xyz, c.rig_Einv + 16 * p, mp,
                            corr + (size_t)p * K * TS_CORR_DOUBLES, stats + (size_t)p * TS_STATS_INTS,
                            pose + (size_t)p * TS_POSE_DOUBLES, frame);
     }

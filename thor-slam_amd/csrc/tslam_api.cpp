@@ -7,6 +7,11 @@
 
 #include <algorithm>
 #include <array>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <limits>
 #include <map>
 #include <cmath>
@@ -93,12 +98,47 @@ struct tslam_handle {
     uint32_t* d_lp_desc = nullptr;   // [cap][K][8]
     int32_t* d_lp_n = nullptr;       // [cap]
     int32_t* d_lp_votes = nullptr;   // [cap]
-    std::vector<int32_t> lp_n;       // host mirror of d_lp_n
+    // asynchronous loop closure (tslam_loop_auto / tslam_loop_job_*): keyframes stored by the
+    // submit path into entry (k mod cap_k) * P + p with a snapshot of their image; jobs (vote,
+    // verify, pose graph) in order on the loop stream, results in pinned memory
+    int lp_auto = 0;                       // keyframe interval (0: off)
+    int64_t* d_lp_pos = nullptr;           // database positions taken so far (device counter)
+    uint32_t* d_lp_snap_kps = nullptr;     // [cap][K][2]
+    int32_t* d_lp_snap_kcount = nullptr;   // [cap][TS_MAX_LEVELS]
+    uint32_t* d_lp_snap_desc = nullptr;    // [cap][K][8]
+    hipStream_t lp_stream = nullptr;
+    hipEvent_t lp_ev_store = nullptr;      // the newest batch's keyframe stores (back stream)
+    bool lp_store_armed = false;
+    struct LoopJob {
+        int kind = 0;                      // 0 free, 1 vote, 2 verify, 3 pose graph
+        int64_t id = 0;
+        hipEvent_t ev = nullptr;
+        int n_out = 0, n_edges = 0;        // votes / nodes; pose-graph edges
+        void* out = nullptr;               // pinned results
+        size_t out_cap = 0;
+        void* in = nullptr;                // pinned pose-graph inputs
+        size_t in_cap = 0;
+        int posted = 0;                    // (worker mutex) 0 queued, 1 on the loop stream, -1 failed
+        std::string err;
+    } lp_jobs[64];
+    int64_t lp_job_next = 1;
+    // the loop worker: a host thread that issues the jobs' copies and launches on the loop stream,
+    // so a job call returns once its inputs are staged (the caller's frame loop does not pay the
+    // ~10-200 launches of a verification or a span solve)
+    struct LoopWorker {
+        std::thread th;
+        std::mutex mu;
+        std::condition_variable cv;
+        std::deque<std::function<void()>> q;
+        int pending = 0;
+        bool stop = false;
+    }* lp_worker = nullptr;
     // pose graph (tslam_pose_graph) scratch, grown on demand
     int pg_nodes = 0, pg_edges = 0, pg_np = 0;
     double *d_pg_T = nullptr, *d_pg_Z = nullptr, *d_pg_info = nullptr, *d_pg_terms = nullptr;
-    double *d_pg_H = nullptr, *d_pg_g = nullptr, *d_pg_delta = nullptr;
+    double *d_pg_H = nullptr, *d_pg_g = nullptr, *d_pg_delta = nullptr, *d_pg_Ld = nullptr;
     int32_t *d_pg_edges = nullptr, *d_pg_adj_off = nullptr, *d_pg_adj = nullptr, *d_pg_ftile = nullptr;
+    double* d_pg_cost = nullptr;   // the solve's cost (k_pg_cost_sum), one double
     // RGB-D dense mapping (tslam_tsdf_*): dense TSDF volume + per-launch pose scratch
     bool tsdf_on = false;
     bool tsdf_color = false;          // colour layer (tslam_tsdf_color)
@@ -223,6 +263,60 @@ static void free_all(tslam_handle* h) {
     h->allocs.clear();
     for (void* p : h->host_allocs) (void)hipHostFree(p);
     h->host_allocs.clear();
+}
+
+// -- the loop worker (tslam_loop_job_*) -----------------------------------------------------------
+static void loop_worker_run(tslam_handle* h) {
+    auto* w = h->lp_worker;
+    (void)hipSetDevice(h->device);
+    for (;;) {
+        std::function<void()> f;
+        {
+            std::unique_lock<std::mutex> lk(w->mu);
+            w->cv.wait(lk, [&] { return w->stop || !w->q.empty(); });
+            if (w->q.empty()) return;
+            f = std::move(w->q.front());
+            w->q.pop_front();
+        }
+        f();
+        {
+            std::lock_guard<std::mutex> lk(w->mu);
+            --w->pending;
+        }
+        w->cv.notify_all();
+    }
+}
+
+static void loop_worker_post(tslam_handle* h, std::function<void()> f) {
+    if (!h->lp_worker) {
+        h->lp_worker = new tslam_handle::LoopWorker();
+        h->lp_worker->th = std::thread(loop_worker_run, h);
+    }
+    {
+        std::lock_guard<std::mutex> lk(h->lp_worker->mu);
+        h->lp_worker->q.push_back(std::move(f));
+        ++h->lp_worker->pending;
+    }
+    h->lp_worker->cv.notify_all();
+}
+
+// every posted job is on the loop stream
+static void loop_worker_drain(tslam_handle* h) {
+    if (!h->lp_worker) return;
+    std::unique_lock<std::mutex> lk(h->lp_worker->mu);
+    h->lp_worker->cv.wait(lk, [&] { return h->lp_worker->pending == 0; });
+}
+
+static void loop_worker_stop(tslam_handle* h) {
+    if (!h->lp_worker) return;
+    {
+        std::lock_guard<std::mutex> lk(h->lp_worker->mu);
+        h->lp_worker->stop = true;
+    }
+    h->lp_worker->cv.notify_all();
+    h->lp_worker->th.join();   // the queue is drained first (the thread exits on an empty queue)
+    delete h->lp_worker;
+    h->lp_worker = nullptr;
 }
 
 static void build_geometry(tslam_handle* h) {
@@ -808,9 +902,14 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
 
 int tslam_destroy(tslam_handle* h) {
     if (!h) return TSLAM_OK;
+    loop_worker_stop(h);   // its queued jobs reach the loop stream before the device is drained
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();
     for (hipEvent_t e : h->ba_events) (void)hipEventDestroy(e);
+    for (auto& j : h->lp_jobs)
+        if (j.ev) (void)hipEventDestroy(j.ev);
+    if (h->lp_ev_store) (void)hipEventDestroy(h->lp_ev_store);
+    if (h->lp_stream) (void)hipStreamDestroy(h->lp_stream);
     for (hipEvent_t e : {h->ev_fe, h->ev_ba[0], h->ev_ba[1], h->ev_front, h->ev_back[0], h->ev_back[1], h->ev_prior[0],
                          h->ev_prior[1],
                          h->as_staged[0], h->as_staged[1], h->as_res[0].ev, h->as_res[1].ev})
@@ -824,6 +923,7 @@ int tslam_destroy(tslam_handle* h) {
 
 int tslam_reset(tslam_handle* h) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
+    loop_worker_drain(h);
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
     std::vector<double> eye(32 * (size_t)h->P, 0.0);   // every chain's (A, Q) = (I, I)
@@ -849,7 +949,10 @@ int tslam_reset(tslam_handle* h) {
         }
     }
     h->lp_count = 0;   // the keyframe database belongs to the session
-    std::fill(h->lp_n.begin(), h->lp_n.end(), 0);
+    if (h->d_lp_n) HIPCHK(hipMemset(h->d_lp_n, 0, sizeof(int32_t) * (size_t)h->lp_cap));   // every entry empty
+    if (h->d_lp_pos) HIPCHK(hipMemset(h->d_lp_pos, 0, sizeof(int64_t)));
+    for (auto& j : h->lp_jobs) j.kind = 0;   // jobs of the old session are dropped
+    h->lp_store_armed = false;
     h->ba_pending[0] = h->ba_pending[1] = false;
     h->back_pending[0] = h->back_pending[1] = false;
     h->in_batch = false;
@@ -1087,6 +1190,14 @@ int tslam_end_batch(tslam_handle* h) {
     return TSLAM_OK;
 }
 
+// tslam_loop_auto: the batch's keyframes into the database, right after its pose stage
+static void loop_auto_store(tslam_handle* h, const BatchCtx& c, hipStream_t s) {
+    if (!h->lp_auto) return;
+    const LoopDb db{h->d_lp_xyz, h->d_lp_desc, h->d_lp_n, h->d_lp_snap_kps, h->d_lp_snap_kcount, h->d_lp_snap_desc};
+    launch_loop_store_auto(c, h->lp_auto, db, h->lp_cap / h->P, h->rig, h->d_lp_pos, s);
+    if (hipEventRecord(h->lp_ev_store, s) == hipSuccess) h->lp_store_armed = true;
+}
+
 int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
     if (!h->in_batch) return fail(TSLAM_ESTATE, "tslam_begin_batch first");
@@ -1142,6 +1253,7 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
             launch_pose(c, s);
             if (h->rig) launch_rig_pose(c, s);
             launch_chains(c, h->rig, s);
+            loop_auto_store(h, c, s);
             break;
         case TSLAM_STAGE_ALL:
             launch_rectify_pyramid(c, s);
@@ -1153,6 +1265,7 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
             launch_pose(c, s);
             if (h->rig) launch_rig_pose(c, s);
             launch_chains(c, h->rig, s);
+            loop_auto_store(h, c, s);
             if (h->prm.ba_window) {
                 double* snap = h->ba.fe_pose + (size_t)(h->batch_idx & 1) * h->B * h->P * 16;
                 double* snap_body = h->ba.fe_body + (size_t)(h->batch_idx & 1) * h->B * 16;
@@ -1647,8 +1760,16 @@ static int ensure_reloc_scratch(tslam_handle* h) {
 }
 
 // reloc-path solve of `frame` (pair) against M landmarks; result copied to the host
+// loop jobs share the relocalisation scratch and the vote buffer: the synchronous users wait for them
+static int loop_quiesce(tslam_handle* h) {
+    loop_worker_drain(h);
+    if (h->lp_stream) HIPCHK(hipStreamSynchronize(h->lp_stream));
+    return TSLAM_OK;
+}
+
 static int reloc_solve(tslam_handle* h, int pair, int64_t frame, const double* map_xyz, const uint32_t* map_desc,
                        int64_t M, double* T_out, double* cov, int32_t* stats) {
+    if (loop_quiesce(h) != TSLAM_OK) return TSLAM_EHIP;
     const BatchCtx c = make_ctx(h);
     hipStream_t s = h->last_stream;
     if (M == 0) {
@@ -1723,6 +1844,7 @@ int tslam_relocalize_rig(tslam_handle* h, int64_t frame, double* body_T_world, d
     if (frame < 0 || frame >= h->frames_done || frame < h->frames_done - h->R)
         return fail(TSLAM_EINVAL, "frame is not resident in the ring");
     HIPCHK(hipSetDevice(h->device));
+    if (loop_quiesce(h) != TSLAM_OK) return TSLAM_EHIP;
     const BatchCtx c = make_ctx(h);
     hipStream_t s = h->last_stream;
     const int P = h->P;
@@ -1762,6 +1884,7 @@ int tslam_loop_init(tslam_handle* h, int max_keyframes, int signature) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
     if (max_keyframes < 1 || max_keyframes > (1 << 16)) return fail(TSLAM_EINVAL, "max_keyframes must be in [1, 65536]");
     if (signature < 1 || signature > 256) return fail(TSLAM_EINVAL, "signature must be in [1, 256]");
+    loop_worker_drain(h);
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
     const size_t K = h->g.K, cap = max_keyframes;
@@ -1771,30 +1894,44 @@ int tslam_loop_init(tslam_handle* h, int max_keyframes, int signature) {
     if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_lp_votes, sizeof(int32_t) * cap);
     if (rc == TSLAM_OK) rc = ensure_reloc_scratch(h);
     if (rc != TSLAM_OK) return rc;
+    for (void** p : {(void**)&h->d_lp_snap_kps, (void**)&h->d_lp_snap_kcount, (void**)&h->d_lp_snap_desc})
+        if (*p) {   // snapshots follow the capacity: tslam_loop_auto allocates them again
+            (void)hipFree(*p);
+            h->allocs.erase(std::remove(h->allocs.begin(), h->allocs.end(), *p), h->allocs.end());
+            *p = nullptr;
+        }
+    h->lp_auto = 0;
     h->lp_cap = max_keyframes;
     h->lp_S = signature;
     h->lp_count = 0;
-    h->lp_n.assign(cap, 0);
+    for (auto& j : h->lp_jobs) j.kind = 0;
+    h->lp_store_armed = false;
+    return TSLAM_OK;
+}
+
+static int loop_count(tslam_handle* h, int slot, int32_t* n) {
+    HIPCHK(hipMemcpy(n, h->d_lp_n + slot, sizeof(int32_t), hipMemcpyDeviceToHost));
     return TSLAM_OK;
 }
 
 int tslam_loop_add_keyframe(tslam_handle* h, int pair, int64_t frame, int* slot, int* n_landmarks) {
     if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
     if (!h->lp_cap) return fail(TSLAM_ESTATE, "loop database not initialised (tslam_loop_init)");
+    if (h->lp_auto) return fail(TSLAM_ESTATE, "the submit path stores the keyframes (tslam_loop_auto)");
     if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_loop_add_keyframe inside a batch");
     if (frame < 0 || frame >= h->frames_done || frame < h->frames_done - h->R)
         return fail(TSLAM_EINVAL, "frame is not resident in the ring");
     HIPCHK(hipSetDevice(h->device));
+    if (loop_quiesce(h) != TSLAM_OK) return TSLAM_EHIP;
     const int sl = (int)(h->lp_count % h->lp_cap);
     const size_t K = h->g.K;
     const BatchCtx c = make_ctx(h);
     hipStream_t s = h->last_stream;
     launch_loop_store(c, pair, frame, h->d_lp_xyz + (size_t)sl * K * 3, h->d_lp_desc + (size_t)sl * K * 8, h->d_lp_n + sl, s);
     HIPCHK(hipGetLastError());
-    int32_t n = 0;
-    HIPCHK(hipMemcpyAsync(&n, h->d_lp_n + sl, sizeof(n), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    h->lp_n[sl] = n;
+    int32_t n = 0;
+    if (loop_count(h, sl, &n) != TSLAM_OK) return TSLAM_EHIP;
     ++h->lp_count;
     if (slot) *slot = sl;
     if (n_landmarks) *n_landmarks = n;
@@ -1805,8 +1942,10 @@ int tslam_loop_read_keyframe(tslam_handle* h, int slot, double* xyz, uint32_t* d
     if (!h || !h->lp_cap) return fail(TSLAM_ESTATE, "loop database not initialised (tslam_loop_init)");
     if (slot < 0 || slot >= h->lp_cap) return fail(TSLAM_EINVAL, "slot out of range");
     HIPCHK(hipSetDevice(h->device));
-    HIPCHK(hipStreamSynchronize(h->last_stream));
-    const size_t K = h->g.K, m = h->lp_n[slot];
+    HIPCHK(hipDeviceSynchronize());   // the stores of every stream (tslam_loop_auto: the back stream)
+    int32_t m = 0;
+    if (loop_count(h, slot, &m) != TSLAM_OK) return TSLAM_EHIP;
+    const size_t K = h->g.K;
     if (xyz && m) HIPCHK(hipMemcpy(xyz, h->d_lp_xyz + (size_t)slot * K * 3, sizeof(double) * 3 * m, hipMemcpyDeviceToHost));
     if (desc && m) HIPCHK(hipMemcpy(desc, h->d_lp_desc + (size_t)slot * K * 8, sizeof(uint32_t) * 8 * m, hipMemcpyDeviceToHost));
     if (n) *n = (int)m;
@@ -1819,9 +1958,10 @@ int tslam_loop_query(tslam_handle* h, int slot, int n_candidates, int32_t* votes
     if (n_candidates < 0 || n_candidates > h->lp_cap) return fail(TSLAM_EINVAL, "n_candidates out of range");
     if (n_candidates == 0) return TSLAM_OK;
     HIPCHK(hipSetDevice(h->device));
+    if (loop_quiesce(h) != TSLAM_OK) return TSLAM_EHIP;
     hipStream_t s = h->last_stream;
-    launch_loop_vote(h->d_lp_desc, h->d_lp_n, h->g.K, h->lp_S, slot, n_candidates, h->prm.max_hamming, h->prm.ratio_pct,
-                     h->d_lp_votes, s);
+    launch_loop_vote(h->d_lp_desc, h->d_lp_n, h->g.K, h->lp_S, slot, 0, std::numeric_limits<int>::max(), 1, n_candidates,
+                     h->prm.max_hamming, h->prm.ratio_pct, h->d_lp_votes, s);
     HIPCHK(hipGetLastError());
     if (votes) HIPCHK(hipMemcpyAsync(votes, h->d_lp_votes, sizeof(int32_t) * n_candidates, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -1836,9 +1976,151 @@ int tslam_loop_verify(tslam_handle* h, int pair, int64_t frame, int slot, double
     if (frame < 0 || frame >= h->frames_done || frame < h->frames_done - h->R)
         return fail(TSLAM_EINVAL, "frame is not resident in the ring");
     HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    int32_t m = 0;
+    if (loop_count(h, slot, &m) != TSLAM_OK) return TSLAM_EHIP;
     const size_t K = h->g.K;
-    return reloc_solve(h, pair, frame, h->d_lp_xyz + (size_t)slot * K * 3, h->d_lp_desc + (size_t)slot * K * 8,
-                       h->lp_n[slot], T_qc, cov, stats);
+    return reloc_solve(h, pair, frame, h->d_lp_xyz + (size_t)slot * K * 3, h->d_lp_desc + (size_t)slot * K * 8, m, T_qc,
+                       cov, stats);
+}
+
+// -- asynchronous loop closure (tslam_loop_auto / tslam_loop_job_*) ------------------------------
+static int pose_graph_reserve(tslam_handle* h, int n_nodes, int n_edges);
+
+int tslam_loop_auto(tslam_handle* h, int interval) {
+    if (!h || interval < 0) return fail(TSLAM_EINVAL, "bad handle or interval");
+    if (!h->lp_cap) return fail(TSLAM_ESTATE, "loop database not initialised (tslam_loop_init)");
+    if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_loop_auto inside a batch");
+    if (h->sh_world > 1 || h->sh_comm) return fail(TSLAM_ESTATE, "tslam_loop_auto takes an unsharded handle");
+    if (h->lp_cap % h->P) return fail(TSLAM_EINVAL, "max_keyframes of tslam_loop_init must be a multiple of the pairs");
+    HIPCHK(hipSetDevice(h->device));
+    if (interval && !h->d_lp_snap_kps) {
+        const size_t K = h->g.K, cap = h->lp_cap;
+        int rc = dev_alloc(h, (void**)&h->d_lp_snap_kps, sizeof(uint32_t) * 2 * K * cap);
+        if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_lp_snap_kcount, sizeof(int32_t) * TS_MAX_LEVELS * cap);
+        if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_lp_snap_desc, sizeof(uint32_t) * 8 * K * cap);
+        if (rc != TSLAM_OK) return rc;
+    }
+    if (interval && !h->d_lp_pos) {
+        const int rc = dev_alloc(h, (void**)&h->d_lp_pos, sizeof(int64_t));
+        if (rc != TSLAM_OK) return rc;
+    }
+    if (interval && h->d_lp_pos) HIPCHK(hipMemset(h->d_lp_pos, 0, sizeof(int64_t)));   // (dev_alloc synchronised)
+    if (interval) {   // a span solve covers at most the ring's cap_k nodes (and one loop edge per node)
+        const int nn = std::min(1024, h->lp_cap / h->P);
+        const int rc = pose_graph_reserve(h, std::max(nn, 2), 2 * std::max(nn, 2));
+        if (rc != TSLAM_OK) return rc;
+    }
+    HIPCHK(hipDeviceSynchronize());
+    if (interval && !h->lp_ev_store) HIPCHK(hipEventCreateWithFlags(&h->lp_ev_store, hipEventDisableTiming));
+    h->lp_auto = interval;
+    return TSLAM_OK;
+}
+
+static int pinned_reserve(tslam_handle* h, void** p, size_t* cap, size_t bytes) {
+    if (bytes <= *cap) return TSLAM_OK;
+    if (*p) {
+        (void)hipHostFree(*p);
+        h->host_allocs.erase(std::remove(h->host_allocs.begin(), h->host_allocs.end(), *p), h->host_allocs.end());
+        *p = nullptr;
+        *cap = 0;
+    }
+    HIPCHK(hipHostMalloc(p, bytes, hipHostMallocDefault));
+    h->host_allocs.push_back(*p);
+    *cap = bytes;
+    return TSLAM_OK;
+}
+
+// A job slot (the loop stream created on first use).  The caller stages the inputs; the worker
+// makes the loop stream wait for the newest batch's keyframe stores (so a job sees every entry of
+// every batch submitted before it), runs `work` and records the job's event.
+static int job_begin(tslam_handle* h, int kind, tslam_handle::LoopJob** out) {
+    if (!h->lp_stream) HIPCHK(hipStreamCreateWithFlags(&h->lp_stream, hipStreamNonBlocking));
+    auto& j = h->lp_jobs[h->lp_job_next % 64];
+    if (j.kind) return fail(TSLAM_ESTATE, "64 loop jobs are unreturned (tslam_loop_job_poll)");
+    if (!j.ev) HIPCHK(hipEventCreateWithFlags(&j.ev, hipEventDisableTiming));
+    j.kind = kind;
+    j.id = h->lp_job_next;
+    j.posted = 0;
+    j.err.clear();
+    *out = &j;
+    return TSLAM_OK;
+}
+
+static int job_post(tslam_handle* h, tslam_handle::LoopJob& j, std::function<hipError_t()> work, int64_t* id) {
+    const bool wait_store = h->lp_store_armed;
+    tslam_handle::LoopJob* jp = &j;
+    loop_worker_post(h, [h, jp, wait_store, work = std::move(work)] {
+        hipError_t e = wait_store ? hipStreamWaitEvent(h->lp_stream, h->lp_ev_store, 0) : hipSuccess;
+        if (e == hipSuccess) e = work();
+        if (e == hipSuccess) e = hipGetLastError();
+        if (e == hipSuccess) e = hipEventRecord(jp->ev, h->lp_stream);
+        std::lock_guard<std::mutex> lk(h->lp_worker->mu);
+        jp->posted = e == hipSuccess ? 1 : -1;
+        if (e != hipSuccess) jp->err = std::string("loop job: ") + hipGetErrorString(e);
+    });
+    ++h->lp_job_next;
+    if (id) *id = j.id;
+    return TSLAM_OK;
+}
+
+int tslam_loop_job_vote(tslam_handle* h, int query, int64_t k0, int n_kf, int64_t* job) {
+    if (!h || !h->lp_cap) return fail(TSLAM_ESTATE, "loop database not initialised (tslam_loop_init)");
+    if (h->lp_cap % h->P) return fail(TSLAM_ESTATE, "the database is not keyframe-major over the pairs");
+    const int capk = h->lp_cap / h->P;
+    if (query < 0 || query >= h->lp_cap || k0 < 0 || n_kf < 0 || n_kf > capk)
+        return fail(TSLAM_EINVAL, "query entry or keyframe range out of range");
+    HIPCHK(hipSetDevice(h->device));
+    tslam_handle::LoopJob* j = nullptr;
+    int rc = job_begin(h, 1, &j);
+    if (rc != TSLAM_OK) return rc;
+    const int n = n_kf * h->P;
+    j->n_out = n;
+    if ((rc = pinned_reserve(h, &j->out, &j->out_cap, sizeof(int32_t) * std::max(n, 1))) != TSLAM_OK) {
+        j->kind = 0;
+        return rc;
+    }
+    const int K = h->g.K, S = h->lp_S, P = h->P, mh = h->prm.max_hamming, rp = h->prm.ratio_pct;
+    const uint32_t* desc = h->d_lp_desc;
+    const int32_t* cnt = h->d_lp_n;
+    int32_t* votes = h->d_lp_votes;
+    void* out = j->out;
+    return job_post(h, *j, [=]() -> hipError_t {
+        if (!n) return hipSuccess;
+        launch_loop_vote(desc, cnt, K, S, query, k0, capk, P, n, mh, rp, votes, h->lp_stream);
+        return hipMemcpyAsync(out, votes, sizeof(int32_t) * n, hipMemcpyDeviceToHost, h->lp_stream);
+    }, job);
+}
+
+int tslam_loop_job_verify(tslam_handle* h, int pair, int64_t frame, int query, int cand, int64_t* job) {
+    if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
+    if (!h->lp_cap || !h->d_lp_snap_kps) return fail(TSLAM_ESTATE, "no keyframe snapshots (tslam_loop_auto)");
+    if (query < 0 || query >= h->lp_cap || cand < 0 || cand >= h->lp_cap || frame < 0)
+        return fail(TSLAM_EINVAL, "entry or frame out of range");
+    HIPCHK(hipSetDevice(h->device));
+    tslam_handle::LoopJob* j = nullptr;
+    int rc = job_begin(h, 2, &j);
+    if (rc != TSLAM_OK) return rc;
+    const size_t pose_b = sizeof(double) * TS_POSE_DOUBLES, stat_b = sizeof(int32_t) * TS_STATS_INTS;
+    if ((rc = pinned_reserve(h, &j->out, &j->out_cap, pose_b + stat_b)) != TSLAM_OK) {
+        j->kind = 0;
+        return rc;
+    }
+    const size_t K = h->g.K;
+    const RelocQuery q{h->d_lp_snap_kps + (size_t)query * K * 2, h->d_lp_snap_kcount + (size_t)query * TS_MAX_LEVELS,
+                       h->d_lp_snap_desc + (size_t)query * K * 8};
+    const BatchCtx c = make_ctx(h);   // built here: the worker must not read the handle's batch state
+    const double* xyz = h->d_lp_xyz + (size_t)cand * K * 3;
+    const uint32_t* desc = h->d_lp_desc + (size_t)cand * K * 8;
+    const int32_t* dM = h->d_lp_n + cand;
+    void* out = j->out;
+    return job_post(h, *j, [=]() -> hipError_t {
+        launch_reloc_query(c, pair, frame, q, xyz, desc, 0, dM, h->d_rl_match, h->d_rl_corr, h->d_rl_stats, h->d_rl_pose,
+                           h->d_rl_ransac, h->d_rl_hyp, h->lp_stream);
+        hipError_t e = hipMemcpyAsync(out, h->d_rl_pose, pose_b, hipMemcpyDeviceToHost, h->lp_stream);
+        if (e == hipSuccess) e = hipMemcpyAsync((char*)out + pose_b, h->d_rl_stats, stat_b, hipMemcpyDeviceToHost, h->lp_stream);
+        return e;
+    }, job);
 }
 
 // -- RGB-D dense mapping: TSDF integration -------------------------------------------------------
@@ -2159,8 +2441,44 @@ int tslam_esdf_slice(tslam_handle* h, int y0, int y1, double max_dist, double si
     return TSLAM_OK;
 }
 
-int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_edges, const int32_t* edges,
-                     const double* meas, const double* info, int iters, double* cost) {
+// Pose-graph scratch for n_nodes / n_edges.  Growth reallocates (and synchronises the device), so
+// tslam_loop_auto reserves the largest span solve up front.
+static int pose_graph_reserve(tslam_handle* h, int n_nodes, int n_edges) {
+    const int np = (6 * (n_nodes - 1) + 31) / 32 * 32;
+    int rc = TSLAM_OK;
+    if (!h->d_pg_cost && (rc = dev_alloc(h, (void**)&h->d_pg_cost, sizeof(double))) != TSLAM_OK) return rc;
+    if (n_nodes > h->pg_nodes) {
+        rc = dev_realloc(h, (void**)&h->d_pg_T, sizeof(double) * 16 * n_nodes);
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_adj_off, sizeof(int32_t) * (n_nodes + 1));
+        if (rc != TSLAM_OK) return rc;
+        h->pg_nodes = n_nodes;
+    }
+    if (n_edges > h->pg_edges) {
+        rc = dev_realloc(h, (void**)&h->d_pg_Z, sizeof(double) * 16 * n_edges);
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_info, sizeof(double) * 36 * n_edges);
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_terms, sizeof(double) * 128 * n_edges);
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_edges, sizeof(int32_t) * 2 * n_edges);
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_adj, sizeof(int32_t) * 2 * n_edges);
+        if (rc != TSLAM_OK) return rc;
+        h->pg_edges = n_edges;
+    }
+    if (np > h->pg_np) {
+        rc = dev_realloc(h, (void**)&h->d_pg_H, sizeof(double) * (size_t)np * np);
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_ftile, sizeof(int32_t) * (np / 32));
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_g, sizeof(double) * np);
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_delta, sizeof(double) * np);
+        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_Ld, sizeof(double) * np);
+        if (rc != TSLAM_OK) return rc;
+        h->pg_np = np;
+    }
+    return TSLAM_OK;
+}
+
+// The pose-graph solve as a loop job: validation, the CSR incidence and the matrix profile on the
+// host, every input copied into the job's pinned staging at the call, the iterations on the loop
+// stream, the poses and the per-edge cost terms back into pinned memory.
+int tslam_loop_job_pose_graph(tslam_handle* h, int n_nodes, const double* world_T_node, int n_edges, const int32_t* edges,
+                              const double* meas, const double* info, int iters, int64_t* job) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
     if (n_nodes < 1 || n_nodes > 1024) return fail(TSLAM_EINVAL, "n_nodes must be in [1, 1024]");
     if (n_edges < 0 || (n_edges && (!edges || !meas || !info)) || !world_T_node || iters < 0)
@@ -2198,61 +2516,114 @@ int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_e
         const int col = 6 * (lo - 1) / 32;
         for (int r = 6 * (p - 1); r < 6 * p; ++r) ftile[r / 32] = std::min(ftile[r / 32], col);
     }
-    int rc = TSLAM_OK;
-    if (n_nodes > h->pg_nodes) {
-        rc = dev_realloc(h, (void**)&h->d_pg_T, sizeof(double) * 16 * n_nodes);
-        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_adj_off, sizeof(int32_t) * (n_nodes + 1));
-        if (rc != TSLAM_OK) return rc;
-        h->pg_nodes = n_nodes;
+    int rc = pose_graph_reserve(h, n_nodes, n_edges);
+    if (rc != TSLAM_OK) return rc;
+    tslam_handle::LoopJob* j = nullptr;
+    if ((rc = job_begin(h, 3, &j)) != TSLAM_OK) return rc;
+    j->n_out = n_nodes;
+    j->n_edges = n_edges;
+    // staging: T | Z | info | off | ftile | edges | adj (doubles first, 8-byte aligned)
+    const size_t bT = sizeof(double) * 16 * n_nodes, bZ = sizeof(double) * 16 * n_edges, bI = sizeof(double) * 36 * n_edges;
+    const size_t bO = sizeof(int32_t) * (n_nodes + 1), bF = sizeof(int32_t) * nt, bE = sizeof(int32_t) * 2 * n_edges;
+    const size_t out_b = bT + sizeof(double);
+    if ((rc = pinned_reserve(h, &j->in, &j->in_cap, bT + bZ + bI + bO + bF + 2 * bE)) != TSLAM_OK ||
+        (rc = pinned_reserve(h, &j->out, &j->out_cap, out_b)) != TSLAM_OK) {
+        j->kind = 0;
+        return rc;
     }
-    if (n_edges > h->pg_edges) {
-        rc = dev_realloc(h, (void**)&h->d_pg_Z, sizeof(double) * 16 * n_edges);
-        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_info, sizeof(double) * 36 * n_edges);
-        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_terms, sizeof(double) * 128 * n_edges);
-        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_edges, sizeof(int32_t) * 2 * n_edges);
-        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_adj, sizeof(int32_t) * 2 * n_edges);
-        if (rc != TSLAM_OK) return rc;
-        h->pg_edges = n_edges;
-    }
-    if (np > h->pg_np) {
-        rc = dev_realloc(h, (void**)&h->d_pg_H, sizeof(double) * (size_t)np * np);
-        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_ftile, sizeof(int32_t) * (np / 32));
-        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_g, sizeof(double) * np);
-        if (rc == TSLAM_OK) rc = dev_realloc(h, (void**)&h->d_pg_delta, sizeof(double) * np);
-        if (rc != TSLAM_OK) return rc;
-        h->pg_np = np;
-    }
-    hipStream_t s = h->last_stream;
-    HIPCHK(hipMemcpyAsync(h->d_pg_T, world_T_node, sizeof(double) * 16 * n_nodes, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(h->d_pg_adj_off, off.data(), sizeof(int32_t) * (n_nodes + 1), hipMemcpyHostToDevice, s));
-    if (nt) HIPCHK(hipMemcpyAsync(h->d_pg_ftile, ftile.data(), sizeof(int32_t) * nt, hipMemcpyHostToDevice, s));
+    char* st = (char*)j->in;
+    memcpy(st, world_T_node, bT);
     if (n_edges) {
-        HIPCHK(hipMemcpyAsync(h->d_pg_Z, meas, sizeof(double) * 16 * n_edges, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(h->d_pg_info, info, sizeof(double) * 36 * n_edges, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(h->d_pg_edges, edges, sizeof(int32_t) * 2 * n_edges, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(h->d_pg_adj, adj.data(), sizeof(int32_t) * 2 * n_edges, hipMemcpyHostToDevice, s));
+        memcpy(st + bT, meas, bZ);
+        memcpy(st + bT + bZ, info, bI);
+        memcpy(st + bT + bZ + bI + bO + bF, edges, bE);
+        memcpy(st + bT + bZ + bI + bO + bF + bE, adj.data(), bE);
     }
-    if (n > 0)
-        for (int it = 0; it < iters; ++it)
-            launch_pose_graph_iteration(h->d_pg_T, h->d_pg_edges, h->d_pg_Z, h->d_pg_info, n_nodes, n_edges, h->d_pg_adj_off,
-                                        h->d_pg_adj, h->d_pg_ftile, h->d_pg_terms, h->d_pg_H, h->d_pg_g, h->d_pg_delta, s);
-    std::vector<double> terms;
-    if (cost && n_edges) {
-        launch_pose_graph_cost(h->d_pg_T, h->d_pg_edges, h->d_pg_Z, h->d_pg_info, n_edges, h->d_pg_terms, s);
-        terms.resize((size_t)128 * n_edges);
-        HIPCHK(hipMemcpyAsync(terms.data(), h->d_pg_terms, sizeof(double) * terms.size(), hipMemcpyDeviceToHost, s));
+    memcpy(st + bT + bZ + bI, off.data(), bO);
+    if (nt) memcpy(st + bT + bZ + bI + bO, ftile.data(), bF);
+    void* out = j->out;
+    return job_post(h, *j, [=]() -> hipError_t {
+        hipStream_t s = h->lp_stream;
+        hipError_t e = hipMemcpyAsync(h->d_pg_T, st, bT, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(h->d_pg_adj_off, st + bT + bZ + bI, bO, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess && nt) e = hipMemcpyAsync(h->d_pg_ftile, st + bT + bZ + bI + bO, bF, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess && n_edges) {
+            e = hipMemcpyAsync(h->d_pg_Z, st + bT, bZ, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(h->d_pg_info, st + bT + bZ, bI, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(h->d_pg_edges, st + bT + bZ + bI + bO + bF, bE, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(h->d_pg_adj, st + bT + bZ + bI + bO + bF + bE, bE, hipMemcpyHostToDevice, s);
+        }
+        if (e != hipSuccess) return e;
+        if (n > 0)
+            for (int it = 0; it < iters; ++it)
+                launch_pose_graph_iteration(h->d_pg_T, h->d_pg_edges, h->d_pg_Z, h->d_pg_info, n_nodes, n_edges,
+                                            h->d_pg_adj_off, h->d_pg_adj, h->d_pg_ftile, h->d_pg_terms, h->d_pg_H, h->d_pg_g,
+                                            h->d_pg_delta, h->d_pg_Ld, s);
+        // the cost (sum of the edges' e^T info e in edge order) reduced on the device: 8 bytes back
+        launch_pose_graph_cost(h->d_pg_T, h->d_pg_edges, h->d_pg_Z, h->d_pg_info, n_edges, h->d_pg_terms, h->d_pg_cost, s);
+        e = hipMemcpyAsync((char*)out + bT, h->d_pg_cost, sizeof(double), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(out, h->d_pg_T, bT, hipMemcpyDeviceToHost, s);
+        return e;
+    }, job);
+}
+
+int tslam_loop_job_poll(tslam_handle* h, int64_t id, int block, int32_t* votes, double* T_qc, double* cov,
+                        int32_t* stats, double* world_T_node, double* cost) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    auto& j = h->lp_jobs[(size_t)(id > 0 ? id : 0) % 64];
+    if (id <= 0 || !j.kind || j.id != id) return fail(TSLAM_ESTATE, "unknown or already returned loop job");
+    HIPCHK(hipSetDevice(h->device));
+    {   // the worker may not have issued it yet
+        std::unique_lock<std::mutex> lk(h->lp_worker->mu);
+        if (j.posted == 0) {
+            if (!block) return 0;
+            h->lp_worker->cv.wait(lk, [&] { return j.posted != 0; });
+        }
+        if (j.posted < 0) {
+            j.kind = 0;
+            return fail(TSLAM_EHIP, j.err);
+        }
     }
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(world_T_node, h->d_pg_T, sizeof(double) * 16 * n_nodes, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    if (cost) {
-        double cs = 0.0;
-        for (int k = 0; k < n_edges; ++k) cs += terms[(size_t)128 * k + 120];
-        *cost = cs;
+    if (block) {
+        HIPCHK(hipEventSynchronize(j.ev));
+    } else {
+        const hipError_t q = hipEventQuery(j.ev);
+        if (q == hipErrorNotReady) return 0;
+        if (q != hipSuccess) return fail(TSLAM_EHIP, std::string("hipEventQuery: ") + hipGetErrorString(q));
     }
-    for (int i = 0; i < 16 * n_nodes; ++i)
-        if (!std::isfinite(world_T_node[i])) return fail(TSLAM_ESTATE, "pose graph: normal matrix not positive definite");
-    return TSLAM_OK;
+    const int kind = j.kind;
+    j.kind = 0;   // returned: the slot is free whatever follows
+    if (kind == 1) {
+        if (votes && j.n_out) memcpy(votes, j.out, sizeof(int32_t) * j.n_out);
+    } else if (kind == 2) {
+        double pose[TS_POSE_DOUBLES];
+        int32_t st[TS_STATS_INTS];
+        memcpy(pose, j.out, sizeof(pose));
+        memcpy(st, (const char*)j.out + sizeof(pose), sizeof(st));
+        if (st[0] != 0)   // as reloc_solve: identity when the verification failed
+            for (int i = 0; i < 16; ++i) pose[i] = (i % 5) == 0 ? 1.0 : 0.0;
+        pose[12] = pose[13] = pose[14] = 0.0;   // k_refine writes the 3x4 part only
+        pose[15] = 1.0;
+        if (T_qc) memcpy(T_qc, pose, 16 * sizeof(double));
+        if (cov) memcpy(cov, pose + 32, 36 * sizeof(double));
+        if (stats) memcpy(stats, st, sizeof(st));
+    } else {
+        const double* T = (const double*)j.out;
+        for (int i = 0; i < 16 * j.n_out; ++i)
+            if (!std::isfinite(T[i])) return fail(TSLAM_ESTATE, "pose graph: normal matrix not positive definite");
+        if (world_T_node) memcpy(world_T_node, T, sizeof(double) * 16 * j.n_out);
+        if (cost) *cost = T[16 * (size_t)j.n_out];
+    }
+    return 1;
+}
+
+int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_edges, const int32_t* edges,
+                     const double* meas, const double* info, int iters, double* cost) {
+    int64_t id = 0;
+    int rc = tslam_loop_job_pose_graph(h, n_nodes, world_T_node, n_edges, edges, meas, info, iters, &id);
+    if (rc != TSLAM_OK) return rc;
+    rc = tslam_loop_job_poll(h, id, 1, nullptr, nullptr, nullptr, nullptr, world_T_node, cost);
+    return rc < 0 ? rc : TSLAM_OK;
 }
 
 int tslam_ba_imu_factor(tslam_handle* h, int pair, int64_t frame, const double* M, double weight) {

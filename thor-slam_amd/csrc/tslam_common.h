@@ -238,15 +238,42 @@ void launch_reloc(const BatchCtx& c, int pair, int64_t frame, const double* map_
 void launch_reloc_rig(const BatchCtx& c, int64_t frame, const double* map_xyz, const uint32_t* map_desc, int M,
                       int32_t* match, double* corr, int32_t* stats, double* pose, double* ransac, double* hyp,
                       double* rig_pose, int32_t* rig_stats, hipStream_t s);
+// relocalisation query image: keypoint records [K][2], level counts [L], descriptors [K][8] of one
+// camera image (a ring slot's, or a keyframe database entry's snapshot)
+struct RelocQuery {
+    const uint32_t* kps;
+    const int32_t* kcount;
+    const uint32_t* desc;
+};
+static inline RelocQuery reloc_query_ring(const BatchCtx& c, int cam, int64_t frame) {
+    const size_t ib = (size_t)ring_slot(c, frame) * c.C + cam;
+    return {c.kps + ib * c.g.K * 2, c.kcount + ib * c.g.n_levels, c.desc + ib * c.g.K * 8};
+}
+// `dM` (device, may be null): the map size read on the device instead of M
+void launch_reloc_query(const BatchCtx& c, int pair, int64_t frame, RelocQuery q, const double* map_xyz,
+                        const uint32_t* map_desc, int M, const int32_t* dM, int32_t* match, double* corr, int32_t* stats,
+                        double* pose, double* ransac, double* hyp, hipStream_t s);
+// keyframe database (tslam_loop_*): entry e holds landmarks xyz [K][3] + desc [K][8] + count, and
+// the snapshot of its image (kps [K][2], kcount [TS_MAX_LEVELS], desc [K][8])
+struct LoopDb {
+    double* xyz;
+    uint32_t* desc;
+    int32_t* n;
+    uint32_t* snap_kps;
+    int32_t* snap_kcount;
+    uint32_t* snap_desc;
+};
 void launch_loop_store(const BatchCtx& c, int pair, int64_t frame, double* xyz, uint32_t* desc, int32_t* n_out,
                        hipStream_t s);
-void launch_loop_vote(const uint32_t* db_desc, const int32_t* db_n, int K, int S, int q_slot, int n_cand,
-                      int max_hamming, int ratio_pct, int32_t* votes, hipStream_t s);
+void launch_loop_store_auto(const BatchCtx& c, int interval, const LoopDb& db, int capk, bool rig, int64_t* count,
+                            hipStream_t s);
+void launch_loop_vote(const uint32_t* db_desc, const int32_t* db_n, int K, int S, int q_slot, int64_t k0, int capk, int P,
+                      int n_cand, int max_hamming, int ratio_pct, int32_t* votes, hipStream_t s);
 void launch_pose_graph_iteration(double* T, const int32_t* edges, const double* Z, const double* info, int N, int E,
                                  const int32_t* adj_off, const int32_t* adj, const int32_t* ftile, double* terms,
-                                 double* H, double* g, double* delta, hipStream_t s);
+                                 double* H, double* g, double* delta, double* Ld, hipStream_t s);
 void launch_pose_graph_cost(const double* T, const int32_t* edges, const double* Z, const double* info, int E,
-                            double* terms, hipStream_t s);
+                            double* terms, double* cost, hipStream_t s);
 // TSDF volume + one integration launch (k_tsdf.hip)
 #define TSDF_MAX_FRAMES 256
 #define TSDF_POSE 13   // cam_T_world R (9), t (3), use flag

@@ -225,6 +225,17 @@ _SIGNATURES = {
                                         ctypes.c_double, ctypes.c_void_p]),
     "tslam_pose_graph": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
+    "tslam_loop_auto": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "tslam_loop_job_vote": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_int64)]),
+    "tslam_loop_job_verify": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_int64)]),
+    "tslam_loop_job_pose_graph": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                                 ctypes.POINTER(ctypes.c_int64)]),
+    "tslam_loop_job_poll": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.POINTER(ctypes.c_double)]),
 }
 
 
@@ -709,6 +720,33 @@ class Handle:
                                           st.ctypes.data))
         return {"T": T, "cov": cov, "stats": st}
 
+    # -- asynchronous loop closure (tslam_loop_auto / tslam_loop_job_*) -----------------------
+    def loop_auto(self, interval: int) -> None:
+        """Keyframes (g % interval == 0) stored by the submit path itself; 0 turns it off."""
+        _check(self.lib.tslam_loop_auto(self.h, int(interval)))
+
+    def loop_job_vote(self, query: int, k0: int, n_kf: int) -> "LoopJob":
+        job = ctypes.c_int64()
+        _check(self.lib.tslam_loop_job_vote(self.h, int(query), int(k0), int(n_kf), ctypes.byref(job)))
+        return LoopJob(self, job.value, "vote", n=int(n_kf) * self.n_pairs)
+
+    def loop_job_verify(self, frame: int, query: int, cand: int, pair: int = 0) -> "LoopJob":
+        job = ctypes.c_int64()
+        _check(self.lib.tslam_loop_job_verify(self.h, int(pair), int(frame), int(query), int(cand), ctypes.byref(job)))
+        return LoopJob(self, job.value, "verify")
+
+    def loop_job_pose_graph(self, T: np.ndarray, edges: np.ndarray, meas: np.ndarray, info: np.ndarray,
+                            iters: int) -> "LoopJob":
+        T = np.ascontiguousarray(np.array(T, dtype=np.float64).reshape(-1, 4, 4))
+        edges = np.ascontiguousarray(np.asarray(edges, dtype=np.int32).reshape(-1, 2))
+        meas = np.ascontiguousarray(np.asarray(meas, dtype=np.float64).reshape(-1, 4, 4))
+        info = np.ascontiguousarray(np.asarray(info, dtype=np.float64).reshape(-1, 6, 6))
+        job = ctypes.c_int64()
+        _check(self.lib.tslam_loop_job_pose_graph(self.h, int(T.shape[0]), T.ctypes.data, int(edges.shape[0]),
+                                                  edges.ctypes.data, meas.ctypes.data, info.ctypes.data, int(iters),
+                                                  ctypes.byref(job)))
+        return LoopJob(self, job.value, "pose_graph", n=int(T.shape[0]))
+
     def pose_graph(self, T: np.ndarray, edges: np.ndarray, meas: np.ndarray, info: np.ndarray, iters: int) -> dict:
         """Gauss-Newton on a keyframe pose graph (node 0 fixed) on the device -> poses, cost."""
         T = np.ascontiguousarray(np.array(T, dtype=np.float64).reshape(-1, 4, 4))
@@ -857,6 +895,40 @@ class Handle:
             "level": (kp[:, 1] & 0xFF).astype(np.int64), "angle": ((kp[:, 1] >> 8) & 0xFF).astype(np.int64),
             "score": (kp[:, 1] >> 16).astype(np.int64), "counts": cnt.astype(np.int64), "desc": desc,
         }
+
+
+class LoopJob:
+    """One ``tslam_loop_job_*`` on the handle's loop stream; ``result(block)`` returns its outputs
+    once (None while it runs and ``block`` is False)."""
+
+    def __init__(self, handle: Handle, job_id: int, kind: str, n: int = 0):
+        self.handle, self.id, self.kind, self.n = handle, int(job_id), kind, int(n)
+        self._res = None
+
+    def result(self, block: bool = False):
+        if self._res is not None:
+            return self._res
+        h = self.handle
+        if self.kind == "vote":
+            votes = np.zeros(max(self.n, 1), dtype=np.int32)
+            rc = h.lib.tslam_loop_job_poll(h.h, self.id, int(block), votes.ctypes.data, None, None, None, None, None)
+            out = votes[:self.n]
+        elif self.kind == "verify":
+            T, cov, st = np.zeros((4, 4)), np.zeros((6, 6)), np.zeros(8, dtype=np.int32)
+            rc = h.lib.tslam_loop_job_poll(h.h, self.id, int(block), None, T.ctypes.data, cov.ctypes.data, st.ctypes.data,
+                                           None, None)
+            out = {"T": T, "cov": cov, "stats": st}
+        else:
+            T, cost = np.zeros((self.n, 4, 4)), ctypes.c_double()
+            rc = h.lib.tslam_loop_job_poll(h.h, self.id, int(block), None, None, None, None, T.ctypes.data,
+                                           ctypes.byref(cost))
+            out = {"T": T, "cost": cost.value}
+        if rc < 0:
+            _check(rc)
+        if rc == 0:
+            return None
+        self._res = out
+        return out
 
 
 class HandleGroup:

@@ -64,6 +64,11 @@ class HipSlamConfig(SlamConfig):
     imu_trans_floor: float = 1e-3   # m, added in quadrature to the predicted translation's std
     imu_gyro_bias_sigma: float = 0.01   # rad/s, initial gyroscope-bias std
     imu_accel_bias_sigma: float = 0.05  # m/s^2, initial accelerometer-bias std
+    # batches whose vision the prior of the next batch may lack (oracle/numpy_imu.py lagged_priors):
+    # the prior of batch s comes from the filter with the vision of batches <= s - 1 - lag absorbed,
+    # coasted over the rest, so up to `lag` batches stay in flight; 0 = synchronous (each batch
+    # waits for the previous one's vision)
+    imu_prior_lag: int = 1
     # loop closure + keyframe pose graph; on when the reference's
     # SlamConfig.enable_loop_closure is (interface.py:155-156; single stereo pair / RGB-D camera)
     loop_kf_interval: int = 5       # frame g is a loop-closure keyframe iff g % loop_kf_interval == 0
@@ -75,6 +80,10 @@ class HipSlamConfig(SlamConfig):
     pg_iters: int = 8               # Gauss-Newton iterations per pose-graph solve
     pg_sigma_t: float = 0.01        # m, std of an edge's translation
     pg_sigma_r: float = 0.005       # rad, std of an edge's rotation
+    # asynchronous loop closure (oracle/numpy_loop.py LoopPolicy): the search a keyframe g starts
+    # (signature votes, verification, the pose-graph solve of the loop's span) runs on the device
+    # beside tracking, and its correction applies from frame g + loop_latency on; 0 = at g itself
+    loop_latency: int = 30
     # input kind: RGB-D (BASELINE configs[4]) = per source a colour camera (cam_idx 0, BGR) and a
     # depth image aligned to it (cam_idx 1, u16 mm); depth replaces stereo matching
     rgbd: bool = False
@@ -102,7 +111,8 @@ class HipSlamConfig(SlamConfig):
     esdf_slice_min_height: float = -0.5
     esdf_slice_max_height: float = 0.5
     # pipeline
-    batch_size: int = 1             # frames per submission (1 = synchronous latency mode)
+    batch_size: int = 1             # frames per submission
+    sync: bool = False              # wait for every batch before process_frames returns (latency mode)
     # one camera stream per GPU from one process (the rig cuVSLAM's multicam mode
     # takes, launch/thor_visual_slam.launch.py:49,81): the rig's cameras sharded over these devices,
     # rank r on devices[r] (empty = the engine's one device, unsharded).  shard_transport "rccl" =
@@ -139,6 +149,8 @@ class HipSlamConfig(SlamConfig):
             raise ValueError("ba_kf_interval and ba_iters must be >= 1")
         if not (1 <= self.loop_max_keyframes <= 1024 and 1 <= self.loop_signature <= 256 and self.loop_kf_interval >= 1):
             raise ValueError("loop_max_keyframes must be in [1, 1024], loop_signature in [1, 256], loop_kf_interval >= 1")
+        if self.loop_latency < 0 or self.imu_prior_lag < 0:
+            raise ValueError("loop_latency and imu_prior_lag must be >= 0")
         if self.devices:
             if self.dense_map:   # the TSDF integrates on one device; local BA runs on rank 0 (state gather)
                 raise ValueError("a sharded rig (devices) runs without the dense map")

@@ -58,6 +58,7 @@ from .._lib import POSE_INIT, POSE_LOST, POSE_OK, Handle, HandleGroup
 from ..calib import (StereoRectification, confidence_from_covariance, extract_cameras, rgbd_pairs, rgbd_undistort,
                      stereo_pairs, stereo_rectify)
 from ..camera.rig import RigCalibration
+from ..loop import span_edges
 from ..camera.types import SynchronizedFrameSet
 from ..imu import ImuNoise, ImuPropagator, vision_only
 from ..params import HipSlamConfig
@@ -119,6 +120,168 @@ class _LoopGraph:
         return np.diag([1.0 / cfg.pg_sigma_t ** 2] * 3 + [1.0 / cfg.pg_sigma_r ** 2] * 3)
 
 
+class _AsyncLoop(_LoopGraph):
+    """Loop closure without host waits (one device, ``tslam_loop_auto``): the policy of
+    ``oracle/numpy_loop.py`` ``LoopPolicy`` on the device's loop jobs.  The submit path stores every
+    keyframe in the database in stream order; a tracked keyframe becomes a node whose search
+    (signature votes -> verification -> span solve) runs as jobs on the handle's loop stream while
+    tracking goes on; items progress at every call without waiting and complete, oldest first, at
+    the latest when their due frame (keyframe + ``loop_latency``) is published — so the published
+    poses are a function of the data alone, whatever the timing."""
+
+    MAX_JOBS = 48   # of the library's 64 unreturned job slots
+
+    def __init__(self, handle: Handle, cfg: HipSlamConfig, n_pairs: int, rect0_T_rect: list) -> None:
+        super().__init__()
+        self.h, self.cfg, self.P = handle, cfg, n_pairs
+        self.m = rect0_T_rect
+        self.info_m = self.information(cfg)
+        self.odo: list = []
+        self.items: collections.deque = collections.deque()
+        self.jobs = 0   # submitted, not yet returned
+        self.trace: dict | None = None   # set to {} to record every job's inputs and results (tests)
+        self.failures: list = []
+
+    # -- oracle LoopPolicy._node: node idx = database position idx (tslam_loop_auto) ----------
+    def node(self, g: int, raw: np.ndarray, ts: float) -> None:
+        idx = len(self.frames)
+        if idx == 0:
+            T, Z = self.corr @ raw, None
+        else:
+            Z = _invert(self.raw[-1]) @ raw
+            T = self.T[-1] @ Z
+            self.edges.append((idx - 1, idx))
+            self.meas.append(Z)
+            self.info.append(self.info_m)
+        self.frames.append(g)
+        self.stamps.append(ts)
+        self.raw.append(raw.copy())
+        self.T.append(T)
+        self.odo.append(Z)
+        cfg = self.cfg
+        lo, hi = self._window(idx)
+        it = {"idx": idx, "g": g, "due": g + cfg.loop_latency, "lo": lo, "n_kf": hi - lo + 1,
+              "stage": "new" if hi >= lo else "done"}
+        self.items.append(it)
+        self._progress(it, False, len(self.items) == 1)
+
+    def _window(self, idx: int) -> tuple[int, int]:   # oracle numpy_loop.candidate_window
+        cfg = self.cfg
+        margin = (cfg.loop_latency + 2 * cfg.batch_size - 1) // cfg.loop_kf_interval + 1
+        return max(0, idx - cfg.loop_max_keyframes + margin), idx - cfg.loop_min_gap
+
+    def _entry(self, pos: int, p: int) -> int:
+        return (pos % self.cfg.loop_max_keyframes) * self.P + p
+
+    def _result(self, job, block: bool):
+        r = job.result(block)
+        if r is not None:
+            self.jobs -= 1
+        return r
+
+    # -- progress without waiting; `block`: complete it (its due frame is being published) --------
+    def advance(self, until: int | None = None) -> None:
+        first = True
+        for it in list(self.items):
+            must = until is not None and it["due"] <= until
+            self._progress(it, must, first)
+            if it["stage"] != "done":
+                if must:
+                    raise RuntimeError("loop closure: a due item did not complete")
+                first = False
+                continue
+            if first:
+                self.items.popleft()
+
+    def _progress(self, it: dict, block: bool, head: bool) -> None:
+        cfg, P, h = self.cfg, self.P, self.h
+        if it["stage"] == "new":
+            if self.jobs + P > self.MAX_JOBS and not block:
+                return
+            it["votes"] = [h.loop_job_vote(self._entry(it["idx"], q), it["lo"], it["n_kf"]) for q in range(P)]
+            self.jobs += P
+            it["stage"] = "vote"
+        if it["stage"] == "vote":
+            got = it.setdefault("got", [None] * P)
+            for q, job in enumerate(it["votes"]):
+                if got[q] is None:
+                    got[q] = self._result(job, block)
+            if any(v is None for v in got):
+                return
+            if self.trace is not None:
+                for q, v in enumerate(got):
+                    self.trace[("vote", it["idx"], q)] = (it["lo"], it["n_kf"], v.copy())
+            # oracle numpy_loop.best_vote: most votes; ties to the lower query pair, then the newest
+            # position (the smallest span), then the lower pair
+            best, q, j = -1, 0, 0
+            for qq in range(P):
+                v = got[qq].reshape(-1, P)
+                r = int(np.argmax(v[::-1].reshape(-1)))
+                jj = (v.shape[0] - 1 - r // P) * P + r % P
+                if int(got[qq][jj]) > best:
+                    best, q, j = int(got[qq][jj]), qq, jj
+            if best < cfg.loop_min_votes:
+                it["stage"] = "done"
+                return
+            c, pc = it["lo"] + j // P, j % P
+            it.update(q=q, c=c, pc=pc, stage="verify")
+            it["job"] = h.loop_job_verify(it["g"], self._entry(it["idx"], q), self._entry(c, pc), pair=q)
+            self.jobs += 1
+        if it["stage"] == "verify":
+            ver = self._result(it["job"], block)
+            if ver is None:
+                return
+            if self.trace is not None:
+                self.trace[("verify", it["idx"])] = (it["q"], it["c"], it["pc"], ver)
+            if int(ver["stats"][0]) != POSE_OK or int(ver["stats"][2]) < cfg.loop_min_inliers:
+                it["stage"] = "done"
+                return
+            it.update(ver=ver, stage="verified")
+        if it["stage"] == "verified" and head:
+            # the span solve starts once every older item is applied, so its inputs (the span's
+            # poses and edges, with this loop's edge) are what they are at the due frame
+            a, idx, q, pc = it["c"], it["idx"], it["q"], it["pc"]
+            ver = it["ver"]
+            it["edge"] = (a, idx, self.m[pc] @ _invert(ver["T"]) @ _invert(self.m[q]))
+            edges = self.edges + [(a, idx)]
+            meas = self.meas + [it["edge"][2]]
+            sel = span_edges(edges, a, idx)
+            args = (np.stack(self.T[a:idx + 1]), np.array([edges[e] for e in sel]) - a, np.stack([meas[e] for e in sel]),
+                    np.stack([self.info_m] * len(sel)))
+            it["job"] = h.loop_job_pose_graph(*args, cfg.pg_iters)
+            it["args"] = args
+            self.jobs += 1
+            it.update(a=a, stage="solve")
+        if it["stage"] == "solve":
+            try:
+                sol = self._result(it["job"], block)
+            except RuntimeError as exc:   # a diverged solve: keep the failing inputs for diagnosis
+                self.jobs -= 1
+                self.failures.append({"idx": it["idx"], "g": it["g"], "args": it["args"], "ver": it["ver"],
+                                      "q": it["q"], "c": it["c"], "pc": it["pc"], "error": str(exc)})
+                raise
+            if sol is None:
+                return
+            it.update(sol=sol, stage="solved")
+        if it["stage"] == "solved" and block:   # applied at the due frame, as LoopPolicy does
+            a, idx, sol, ver = it["a"], it["idx"], it["sol"], it["ver"]
+            if self.trace is not None:
+                self.trace[("solve", idx)] = (it["args"], sol)
+            self.edges.append((a, idx))
+            self.meas.append(it["edge"][2])
+            self.info.append(self.info_m)
+            self.loops.append((self.frames[a], it["g"], int(ver["stats"][2])))
+            self.pairs.append((it["pc"], it["q"]))
+            self.T[a:idx + 1] = list(sol["T"])
+            for i in range(idx + 1, len(self.T)):
+                self.T[i] = self.T[i - 1] @ self.odo[i]
+            self.corr = self.T[-1] @ _invert(self.raw[-1])
+            self.cost = sol["cost"]
+            it["stage"] = "done"
+            logger.info("loop closure: keyframe %d -> %d (%d inliers), span of %d nodes, cost %.3g",
+                        self.frames[a], it["g"], int(it["ver"]["stats"][2]), idx - a + 1, sol["cost"])
+
+
 class HipSlamEngine(SlamEngine):
     """Stereo visual odometry front end (detect -> match -> pose) running on one MI355X."""
 
@@ -142,7 +305,10 @@ class HipSlamEngine(SlamEngine):
         self._staged: list[tuple[np.ndarray, float]] = []
         self._staged_imu: list[tuple | None] = []    # (gyro, accel) per staged frame
         self._imu: ImuPropagator | None = None       # IMU filter (gyro bias; accelerometer leg with imu_accel)
-        self._imu_batches: list = []                  # IMU samples of submitted, unpublished batches (None: no data)
+        # submitted batches whose vision the IMU filter has not absorbed yet, in order: {"n": batch
+        # number, "samples", "steps", "res": the absorb inputs once published} (no "samples": no data)
+        self._imu_batches: list = []
+        self._imu_seq = 0                            # batches submitted (numbers the entries)
         self._kf_imu: tuple | None = None             # gyro rotation since the last BA keyframe (R, var, first frame)
         self._prev_stamp: float | None = None      # timestamp of the last submitted frame (IMU dt)
         self._base_R_imu = np.eye(3)
@@ -233,7 +399,12 @@ class HipSlamEngine(SlamEngine):
                 if cap > 1 << 16:
                     raise ValueError(f"loop_max_keyframes * pairs = {cap} exceeds the 65536-entry database")
                 self._handle.loop_init(cap, cfg.loop_signature)
-                self._loop = _LoopGraph()
+                if self._shard is None:   # the submit path stores the keyframes; searches run as loop jobs
+                    self._handle.loop_auto(cfg.loop_kf_interval)
+                    m = [_invert(self._base_T_rects[0]) @ e for e in self._base_T_rects]
+                    self._loop = _AsyncLoop(self._handle, cfg, len(self._pairs), m)
+                else:
+                    self._loop = _LoopGraph()
         except RuntimeError:
             raise
         except Exception as exc:  # per interface.py:187-188
@@ -350,6 +521,9 @@ class HipSlamEngine(SlamEngine):
         if len(self._staged) >= self._config.batch_size:
             self._submit_staged()
         self._drain(block=False)
+        if isinstance(self._loop, _AsyncLoop) and self._loop.items:
+            with self._map_lock:
+                self._loop.advance()   # submit / collect loop jobs without waiting
         with self._pose_lock:
             return self._latest_pose
 
@@ -359,8 +533,8 @@ class HipSlamEngine(SlamEngine):
         filter that has seen no sample yet predicts nothing, so a rig whose calibration names an
         IMU that sends no data keeps the asynchronous path)."""
         cfg = self._config
-        return (cfg.ba_window <= 0 and self._loop is None and not cfg.dense_map
-                and (self._imu is None or not self._imu.ready))
+        return (not cfg.sync and cfg.ba_window <= 0 and (self._loop is None or isinstance(self._loop, _AsyncLoop)) and not cfg.dense_map
+                and (self._imu is None or not self._imu.ready or cfg.imu_prior_lag > 0))
 
     def _submit_staged(self) -> None:
         n = len(self._staged)
@@ -415,6 +589,14 @@ class HipSlamEngine(SlamEngine):
         self._submit_staged()
         self._drain(block=True)
 
+    def settle(self) -> None:
+        """``flush`` and complete every pending loop-closure search now (oracle LoopPolicy.finish):
+        the pose graph, ``loop_closures`` and the next published poses then include them."""
+        self.flush()
+        if isinstance(self._loop, _AsyncLoop):
+            with self._map_lock:
+                self._loop.advance(until=1 << 62)
+
     # -- IMU fusion (SURVEY.md §8f item 2) -------------------------------------------------------
     @staticmethod
     def _imu_of(frame_set: SynchronizedFrameSet) -> tuple | None:
@@ -436,8 +618,11 @@ class HipSlamEngine(SlamEngine):
         — moved into every other pair's camera through the rig, inv(E_p) E_0 T inv(E_0) E_p.  The
         samples are kept for the filter's update when the batch's results come back."""
         imu, prev = self._imu, self._prev_stamp
+        seq = self._imu_seq
+        self._imu_seq += 1
+        self._imu_absorb_due(seq)
         if not imu.ready and all(s is None for s in imus):   # no IMU sample yet: nothing to predict,
-            self._imu_batches.append(None)                    # and the batch may stay in flight
+            self._imu_batches.append({"n": seq, "res": None})  # and the batch may stay in flight
             return
         samples = []
         for ts, s in zip(stamps, imus):
@@ -450,7 +635,10 @@ class HipSlamEngine(SlamEngine):
             else:
                 samples.append((None, None, None))
             prev = ts
-        steps = imu.batch_priors(samples)
+        # the vision of the batches still pending (at most imu_prior_lag of them) is not in the
+        # filter yet: the state coasts over their samples (oracle/numpy_imu.py lagged_priors)
+        coast = [c for e in self._imu_batches if "samples" in e for c in e["samples"]]
+        steps = imu.batch_priors(coast + samples)[len(coast):]
         self._ba_imu_factors(steps)
         P, n = len(self._pairs), len(stamps)
         rot = np.tile(np.eye(3), (n, P, 1, 1))
@@ -467,7 +655,21 @@ class HipSlamEngine(SlamEngine):
                 rot[k, p], trn[k, p] = tp[:3, :3], tp[:3, 3]
                 wr[k, p], wt[k, p] = st.w_rot, st.w_trans
         self._set_motion_prior(rot, wr, trn, wt)
-        self._imu_batches.append((samples, steps))
+        self._imu_batches.append({"n": seq, "samples": samples, "steps": steps, "res": None})
+
+    def _imu_absorb_due(self, seq: int) -> None:
+        """Before batch ``seq``'s priors: the filter absorbs the vision of every batch numbered
+        <= seq - 1 - imu_prior_lag (waiting for its results if needed), in order, and no other —
+        whatever has already come back — so the priors are a function of the data alone."""
+        lag = max(int(self._config.imu_prior_lag), 0)
+        while self._imu_batches and self._imu_batches[0]["n"] <= seq - 1 - lag:
+            while self._imu_batches[0]["res"] is None:
+                if self._in_flight == 0:
+                    raise RuntimeError("IMU filter: a batch to absorb was never published")
+                self._drain(block=True, limit=1)
+            e = self._imu_batches.pop(0)
+            if "samples" in e:
+                self._imu.absorb(e["samples"], *e["res"])
 
     def _ba_imu_factors(self, steps: list) -> None:
         """The local BA's IMU rotation factors (one stereo pair): the per-frame gyro rotations of
@@ -674,9 +876,11 @@ class HipSlamEngine(SlamEngine):
             self._publish_locked(res, stamps, g0)
 
     def _publish_locked(self, res: dict, stamps: list[float], g0: int) -> None:
-        entry = self._imu_batches.pop(0) if self._imu is not None and self._imu_batches else None
-        if entry is not None:   # the filter absorbs the tracked motions
-            samples, steps = entry
+        entry = next((e for e in self._imu_batches if e["res"] is None), None) if self._imu is not None else None
+        if entry is not None and "samples" not in entry:
+            entry["res"] = ()
+        elif entry is not None:   # what the filter absorbs of the tracked motions (at the next prior that may use it)
+            steps = entry["steps"]
             if len(self._pairs) == 1:   # the vision-only motion behind each prior-weighted solution
                 st = res["stats"][:, 0]
                 sig = np.ascontiguousarray(st[:, 6:8]).view(np.float64)[:, 0]   # sigma^2 (tslam.h)
@@ -684,14 +888,14 @@ class HipSlamEngine(SlamEngine):
                 for k, step in enumerate(steps[:len(st)]):
                     if step is not None and int(st[k, 0]) == POSE_OK:
                         t_rel[k], cov[k] = vision_only(t_rel[k], cov[k], float(sig[k]), step)
-                self._imu.absorb(samples, st[:, 0], t_rel, cov)
+                entry["res"] = (st[:, 0].copy(), t_rel, cov)
             else:   # the rig's body motion, moved into pair 0's camera (the filter's frame)
                 e0 = self._base_T_rects[0]
                 ie0, ad = _invert(e0), adjoint(_invert(e0))
                 rig = res["rig"]
                 t_rel = np.stack([ie0 @ m @ e0 for m in rig["T_rel"]])
                 cov = np.stack([ad @ c @ ad.T for c in rig["cov"]])
-                self._imu.absorb(samples, rig["stats"][:, 0], t_rel, cov)
+                entry["res"] = (rig["stats"][:, 0].copy(), t_rel, cov)
         latest = None
         state = self._state
         corr = self._ba_corrections(res, len(stamps), g0)
@@ -700,7 +904,14 @@ class HipSlamEngine(SlamEngine):
             status, body, cov = self._body_pose(res, k)
             if corr is not None and status != POSE_LOST:   # a rig's correction is in body terms
                 body = corr[k] @ body if len(self._pairs) > 1 else bt @ corr[k] @ res["T_abs"][k, 0] @ _invert(bt)
-            if self._loop is not None and status != POSE_LOST:
+            if isinstance(self._loop, _AsyncLoop):   # oracle/numpy_loop.py LoopPolicy.step
+                g = g0 + k
+                raw = _invert(bt) @ body @ bt                      # rect-left world_T_cam before loop correction
+                if status == POSE_OK and g % self._config.loop_kf_interval == 0:
+                    self._loop.node(g, raw, ts)
+                self._loop.advance(until=g)
+                body = bt @ self._loop.corr @ raw @ _invert(bt)
+            elif self._loop is not None and status != POSE_LOST:
                 g = g0 + k
                 raw = _invert(bt) @ body @ bt                      # rect-left world_T_cam before loop correction
                 if status == POSE_OK and g % self._config.loop_kf_interval == 0:
@@ -931,13 +1142,16 @@ class HipSlamEngine(SlamEngine):
             self._latest_pose = None
         self._staged, self._staged_imu, self._prev_stamp = [], [], None
         self._imu_batches = []
+        self._imu_seq = 0
         self._kf_imu = None
         if self._imu is not None:
             self._imu.reset()
         self._keyframe_poses = []
         self._fe_at, self._kf_final, self._kf_stamp, self._ba_window, self._ba_pairs = {}, {}, {}, None, []
         self._map_points, self._map_offset = {}, np.eye(4)
-        if self._loop is not None:
+        if isinstance(self._loop, _AsyncLoop):
+            self._loop = _AsyncLoop(self._handle, self._config, self._loop.P, self._loop.m)
+        elif self._loop is not None:
             self._loop = _LoopGraph()
         if self._shard is not None:
             self._shard["stamps"].clear()

@@ -343,6 +343,19 @@ def synthetic_rig(joints: dict, names: list[str] | tuple[str, ...], width: int =
     return srcs, rig
 
 
+class CachedStereoSource(SyntheticStereoSource):
+    """A ``SyntheticStereoSource`` whose frames come from a pre-rendered cycle: frame i is
+    ``frames[i % len(frames)]`` ([n][2][H][W] u8) — a trajectory that repeats with that period
+    (``circle_trajectory`` of one full turn) replays without rendering, IMU samples included."""
+
+    def __init__(self, frames: np.ndarray, **kw) -> None:
+        super().__init__(**kw)
+        self.frames = frames
+
+    def render_image(self, i: int, cam: int) -> np.ndarray:
+        return self.frames[i % len(self.frames), cam]
+
+
 class SyntheticRGBDSource(SyntheticStereoSource):
     """An RGB-D source (BASELINE configs[4]): frames are [colour BGR u8, depth u16 mm] from one
     camera, the depth aligned to the colour image (same K and D, as Luxonis ``depth_align_to_rgb``,
