@@ -287,7 +287,8 @@ class LoopPolicy:
        * votes of pair q's entry of node idx against every pair's entry of the positions of
          ``candidate_window``; ``best_vote`` picks; below ``loop_min_votes`` nothing follows;
        * verification of the best candidate (node c, pair pc) on pair q's view (RANSAC seeded by
-         g); a loop needs status 0 and ``loop_min_inliers``;
+         g); a loop needs status 0 and ``loop_min_inliers``, and is not closed when the last
+         closed loop's newer node is within ``loop_cooldown`` nodes of idx;
        * the loop edge (c, idx) with Z = M_pc T_qc^-1 M_q^-1 (M_p = rect0_T_rect_p), and the span
          solve: Gauss-Newton (``pg_iters``) on the nodes [c, idx] with node c fixed and the edges
          with both ends in the span (``span_edges``); the span takes the solution, later nodes
@@ -312,6 +313,7 @@ class LoopPolicy:
         self.items = []   # [idx, g, due]
         self.corr = np.eye(4)
         self.cost = 0.0
+        self.last_loop = None   # node of the last closed loop
 
     def step(self, g: int, status: int, raw: np.ndarray) -> np.ndarray:
         """Frame g -> its corrected pose (rect-left world_T_cam)."""
@@ -354,6 +356,9 @@ class LoopPolicy:
         ver = self.verify(idx, g, q, c, pc)
         if int(ver["stats"][0]) != 0 or int(ver["stats"][2]) < cfg.loop_min_inliers:
             return
+        if self.last_loop is not None and idx - self.last_loop <= int(getattr(cfg, "loop_cooldown", 0)):
+            return
+        self.last_loop = idx
         self.edges.append((c, idx))
         self.meas.append(self.m[pc] @ inv_se3(ver["T"]) @ inv_se3(self.m[q]))
         self.loops.append((self.frames[c], g, int(ver["stats"][2])))

@@ -281,12 +281,12 @@ def test_default_path_equals_loop_policy():
 
 @pytest.mark.slow
 def test_long_session_keeps_closing_loops():
-    """6,050 frames = 25 laps of the loop at batch 1 (default configuration): more tracked
+    """6,100 frames = 25 laps of the loop at batch 1 (default configuration): more tracked
     keyframes than the database holds (1,024), so its ring wraps, and the searches keep finding
     the previous lap: a loop with its keyframe past frame 6,000 is detected, verified and closed,
     every published pose equals LoopPolicy's, and every span solve stays within the ring."""
     frames = _lap_frames()
-    n = 6050
+    n = 6100   # a loop at keyframe 6,000+ is applied loop_latency frames later
     published, recs, eng = _run_default(frames, n)
     lp = eng._loop
     assert len(lp.frames) > 1100   # > 1,024 database positions: the ring wrapped

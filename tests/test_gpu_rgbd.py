@@ -105,7 +105,8 @@ def test_engine_rgbd_matches_oracle():
     src = SyntheticRGBDSource(width=640, height=400)
     rig = CameraRig([src], rig_extrinsics={src.name: Extrinsics.from_4x4_matrix(src.rig_T_source)})
     rig.start()
-    eng = HipSlamEngine(num_cameras=2, config=HipSlamConfig(rgbd=True))
+    # sync: each call returns its own frame's pose (the asynchronous default may lag)
+    eng = HipSlamEngine(num_cameras=2, config=HipSlamConfig(rgbd=True, sync=True))
     eng.initialize(rig.calibration)
     bt = src.rig_T_source @ src.get_extrinsics()[0].to_4x4_matrix() @ sc["rect"].left_optical_T_rect()
     for i in range(4):

@@ -1,0 +1,115 @@
+"""oracle/numpy_loop.py LoopPolicy (the asynchronous loop closure HipSlamEngine follows) on
+synthetic laps with scripted place recognition: the candidate window over the database ring, the
+newest-first tie rule, the cooldown, the due frame of a correction and the span solve.  CPU only."""
+
+from __future__ import annotations
+
+import numpy as np
+
+from oracle import numpy_loop as L
+from thor_slam_amd.params import HipSlamConfig
+
+
+def _lap_pose(i: int, lap: int = 100) -> np.ndarray:
+    th = 2.0 * np.pi * (i % lap) / lap
+    T = np.eye(4)
+    T[:3, :3] = [[np.cos(th), 0.0, np.sin(th)], [0.0, 1.0, 0.0], [-np.sin(th), 0.0, np.cos(th)]]
+    T[:3, 3] = [2.0 * np.sin(th), 0.0, 2.0 * (1.0 - np.cos(th))]
+    return T
+
+
+def _drift(i: int) -> np.ndarray:
+    """Odometry that drifts: a slow yaw / translation error growing with the frame index."""
+    return L.se3_exp(np.r_[1e-4 * i, 0.0, 0.0, 0.0, 2e-5 * i, 0.0])
+
+
+class _Scripted:
+    """Votes: a candidate at the same place of an earlier lap gets 100 votes (all other 0);
+    verification returns the true relative pose; the solve is the oracle's Gauss-Newton."""
+
+    def __init__(self, lap: int, interval: int):
+        self.lap, self.I = lap, interval
+        self.frames: list[int] = []   # node -> frame (tracked keyframes)
+        self.votes, self.verifies, self.solves = [], [], []
+
+    def vote(self, idx, q, lo, n):
+        g = self.frames[idx]
+        v = np.array([100 if (self.frames[c] - g) % self.lap == 0 else 0 for c in range(lo, lo + n)])
+        self.votes.append((idx, lo, n))
+        return v
+
+    def verify(self, idx, g, q, c, pc):
+        self.verifies.append((idx, c))
+        T = L.inv_se3(_lap_pose(g, self.lap)) @ _lap_pose(self.frames[c], self.lap)   # cam_q_T_cam_c
+        return {"T": T, "stats": np.array([0, 200, 150, 0, 0, 0, 0, 0])}
+
+    def solve(self, T, edges, meas, info, iters):
+        self.solves.append(len(T))
+        return L.optimize(T, edges, meas, info, iters)
+
+
+def _run(n_frames, lap=100, **cfg_items):
+    cfg = HipSlamConfig(**cfg_items)
+    sc = _Scripted(lap, cfg.loop_kf_interval)
+    pol = L.LoopPolicy(cfg, 1, [np.eye(4)], sc.vote, sc.verify, sc.solve)
+    out, raw_all = [], []
+    for g in range(n_frames):
+        raw = _lap_pose(g, lap) @ _drift(g)
+        status = 2 if g == 0 else 0
+        if status == 0 and g % cfg.loop_kf_interval == 0:
+            sc.frames.append(g)
+        out.append(pol.step(g, status, raw))
+        raw_all.append(raw)
+    return pol, sc, out, raw_all
+
+
+def test_window_and_tie_rules():
+    assert L.candidate_window(100, 1024, 20, 30, 1, 5) == (0, 80)
+    assert L.candidate_window(2000, 1024, 20, 30, 1, 5) == (2000 - 1024 + 7, 1980)   # margin (30 + 1) // 5 + 1
+    assert L.candidate_window(2000, 1024, 20, 0, 30, 5) == (2000 - 1024 + 12, 1980)
+    # ties: newest position first; across query pairs the first strictly best wins
+    assert L.best_vote([np.array([7, 7, 7])], 1) == (7, 0, 2)
+    assert L.best_vote([np.array([1, 9, 9, 2])], 2) == (9, 0, 2)
+    assert L.best_vote([np.array([5, 0]), np.array([0, 6])], 2) == (6, 1, 1)
+
+
+def test_corrections_apply_at_the_due_frame_and_pull_drift_back():
+    lap, latency = 100, 30
+    pol, sc, out, raw = _run(260, lap=lap, loop_latency=latency, loop_cooldown=0)
+    assert pol.loops, "no loop closed"
+    first_g = pol.loops[0][1]
+    assert first_g >= lap and (first_g - pol.loops[0][0]) % lap == 0
+    # the correction is the identity before the first loop's due frame and not after it
+    for g in range(first_g + latency):
+        np.testing.assert_array_equal(out[g], raw[g])
+    assert not np.array_equal(out[first_g + latency], raw[first_g + latency])
+    # the last span solve honours its loop edge far better than the drifting odometry did (a
+    # span solve only sees the edges inside its span: older loop edges that cross its start are
+    # not re-balanced, the price of a bounded solve)
+    (a, b), Z = pol.edges[-1], pol.meas[-1]
+    assert b != a + 1
+    e_raw = np.linalg.norm(L.se3_log(L.inv_se3(Z) @ L.inv_se3(pol.raw[a]) @ pol.raw[b]))
+    e_opt = np.linalg.norm(L.se3_log(L.inv_se3(Z) @ L.inv_se3(pol.T[a]) @ pol.T[b]))
+    assert e_opt < 0.1 * e_raw, (a, b, e_raw, e_opt)
+    # every span solve covered [candidate, keyframe]: one lap of keyframes (newest candidate wins)
+    assert set(sc.solves) == {lap // 5 + 1}
+
+
+def test_cooldown_and_latency_zero():
+    pol0, sc0, _, _ = _run(400, loop_latency=0, loop_cooldown=0)
+    pol5, sc5, _, _ = _run(400, loop_latency=0, loop_cooldown=5)
+    assert len(pol0.loops) > 4 * len(pol5.loops) > 0
+    idx = [pol5.frames.index(q) for _, q, _ in pol5.loops]
+    assert all(b - a > 5 for a, b in zip(idx, idx[1:]))
+    # latency 0: the loop's own keyframe is already corrected
+    assert pol0.loops[0][1] in pol0.frames
+
+
+def test_ring_wrap_keeps_searching():
+    """More tracked keyframes than the ring (cap 64): candidates stay inside the newest
+    cap - margin positions, and loops keep closing after the wrap."""
+    pol, sc, _, _ = _run(1200, loop_max_keyframes=64, loop_latency=30, loop_cooldown=0)
+    assert len(pol.frames) > 200
+    for idx, lo, n in sc.votes:
+        assert lo >= idx - 64 + 7 and lo + n - 1 == idx - 20
+    assert pol.loops[-1][1] > 1100

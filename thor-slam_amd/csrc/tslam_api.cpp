@@ -78,6 +78,8 @@ struct tslam_handle {
     hipEvent_t ev_prior[2] = {nullptr, nullptr};   // the last reader of each prior slot is done
     bool prior_read_armed[2] = {false, false};
     bool prior_armed = false;
+    double* h_prior_pin[2] = {nullptr, nullptr};   // pinned staging of each parity's prior slot
+    bool prior_copy_pending = false;               // copied on the batch's back stream at its first back stage
     // relocalisation map (tslam_map_upload) and scratch
     double* d_map_xyz = nullptr;
     uint32_t* d_map_desc = nullptr;
@@ -1181,6 +1183,7 @@ int tslam_end_batch(tslam_handle* h) {
         h->prior_read_armed[par] = true;
     }
     h->prior_armed = false;   // a prior applies to one batch
+    h->prior_copy_pending = false;
     if (h->back_started && h->front_started && h->back_stream != h->front_stream) {
         const int par = (int)(h->batch_idx & 1);
         HIPCHK(hipEventRecord(h->ev_back[par], h->back_stream));
@@ -1234,6 +1237,12 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
         }
         h->back_started = true;
         h->back_stream = s;
+    }
+    if (back && h->prior_copy_pending) {   // this batch's prior (tslam_set_motion_prior), before its pose stage
+        const size_t slot = (size_t)TS_PRIOR_DOUBLES * h->P * h->B;
+        HIPCHK(hipMemcpyAsync(h->d_prior + (size_t)par * slot, h->h_prior_pin[par], sizeof(double) * slot,
+                              hipMemcpyHostToDevice, s));
+        h->prior_copy_pending = false;
     }
     if (front && h->front_started && s != h->front_stream && !back)
         return fail(TSLAM_ESTATE, "all front stages of a batch must use one stream");
@@ -1421,10 +1430,17 @@ int tslam_set_motion_prior(tslam_handle* h, const double* prior, int n_frames) {
         HIPCHK(hipEventSynchronize(h->ev_prior[par]));
         h->prior_read_armed[par] = false;
     }
-    std::vector<double> buf(slot, 0.0);   // frames past n: weight 0
-    memcpy(buf.data(), prior, sizeof(double) * TS_PRIOR_DOUBLES * h->P * n_frames);
-    HIPCHK(hipMemcpy(h->d_prior + par * slot, buf.data(), sizeof(double) * buf.size(), hipMemcpyHostToDevice));
+    if (!h->h_prior_pin[par]) {
+        HIPCHK(hipHostMalloc((void**)&h->h_prior_pin[par], sizeof(double) * slot, hipHostMallocDefault));
+        h->host_allocs.push_back(h->h_prior_pin[par]);
+    }
+    // pinned staging (its previous DMA, batch s-2's, is covered by the event above); the copy is
+    // enqueued on the batch's own back stream, so no host wait and no null-stream ordering
+    const size_t nb = (size_t)TS_PRIOR_DOUBLES * h->P * n_frames;
+    memcpy(h->h_prior_pin[par], prior, sizeof(double) * nb);
+    std::fill(h->h_prior_pin[par] + nb, h->h_prior_pin[par] + slot, 0.0);   // frames past n: weight 0
     h->prior_armed = true;
+    h->prior_copy_pending = true;
     return TSLAM_OK;
 }
 

@@ -84,6 +84,9 @@ class HipSlamConfig(SlamConfig):
     # (signature votes, verification, the pose-graph solve of the loop's span) runs on the device
     # beside tracking, and its correction applies from frame g + loop_latency on; 0 = at g itself
     loop_latency: int = 30
+    # a verified loop is not closed (no edge, no solve) within this many keyframes after the last
+    # closed loop: revisiting a known place would otherwise re-solve the span at every keyframe
+    loop_cooldown: int = 5
     # input kind: RGB-D (BASELINE configs[4]) = per source a colour camera (cam_idx 0, BGR) and a
     # depth image aligned to it (cam_idx 1, u16 mm); depth replaces stereo matching
     rgbd: bool = False
@@ -149,8 +152,8 @@ class HipSlamConfig(SlamConfig):
             raise ValueError("ba_kf_interval and ba_iters must be >= 1")
         if not (1 <= self.loop_max_keyframes <= 1024 and 1 <= self.loop_signature <= 256 and self.loop_kf_interval >= 1):
             raise ValueError("loop_max_keyframes must be in [1, 1024], loop_signature in [1, 256], loop_kf_interval >= 1")
-        if self.loop_latency < 0 or self.imu_prior_lag < 0:
-            raise ValueError("loop_latency and imu_prior_lag must be >= 0")
+        if self.loop_latency < 0 or self.imu_prior_lag < 0 or self.loop_cooldown < 0:
+            raise ValueError("loop_latency, loop_cooldown and imu_prior_lag must be >= 0")
         if self.devices:
             if self.dense_map:   # the TSDF integrates on one device; local BA runs on rank 0 (state gather)
                 raise ValueError("a sharded rig (devices) runs without the dense map")

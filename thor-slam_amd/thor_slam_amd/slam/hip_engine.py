@@ -139,6 +139,8 @@ class _AsyncLoop(_LoopGraph):
         self.odo: list = []
         self.items: collections.deque = collections.deque()
         self.jobs = 0   # submitted, not yet returned
+        self._busy = False
+        self.last_loop: int | None = None   # node of the last closed loop (loop_cooldown)
         self.trace: dict | None = None   # set to {} to record every job's inputs and results (tests)
         self.failures: list = []
 
@@ -174,14 +176,21 @@ class _AsyncLoop(_LoopGraph):
         return (pos % self.cfg.loop_max_keyframes) * self.P + p
 
     def _result(self, job, block: bool):
+        # jobs finish in submission order on the loop stream: once one is still running, a later
+        # one is too, so this pass polls no further (each poll is an event query)
+        if not block and self._busy:
+            return None
         r = job.result(block)
         if r is not None:
             self.jobs -= 1
+        elif not block:
+            self._busy = True
         return r
 
     # -- progress without waiting; `block`: complete it (its due frame is being published) --------
     def advance(self, until: int | None = None) -> None:
         first = True
+        self._busy = False
         for it in list(self.items):
             must = until is not None and it["due"] <= until
             self._progress(it, must, first)
@@ -241,6 +250,10 @@ class _AsyncLoop(_LoopGraph):
             # the span solve starts once every older item is applied, so its inputs (the span's
             # poses and edges, with this loop's edge) are what they are at the due frame
             a, idx, q, pc = it["c"], it["idx"], it["q"], it["pc"]
+            if self.last_loop is not None and idx - self.last_loop <= cfg.loop_cooldown:
+                it["stage"] = "done"   # within the cooldown of the last closed loop
+                return
+            self.last_loop = idx
             ver = it["ver"]
             it["edge"] = (a, idx, self.m[pc] @ _invert(ver["T"]) @ _invert(self.m[q]))
             edges = self.edges + [(a, idx)]
