@@ -218,7 +218,13 @@ int tslam_sync(tslam_handle* h);
  *   own streams (front stages on a high-priority stream overlapping the previous batch's back
  *   stages; with local BA, the BA on a third stream and the front / back streams CU-masked off
  *   64 CUs so its small dependent launches find free CUs) and the batch's results into a pinned
- *   slot (after its BA); returns without waiting for the device.
+ *   slot (copied on the back stream right after the pose stage; with BA the slot completes after
+ *   the BA, so the caller reads the window once it is polled); returns without waiting for the
+ *   device.  Note: with local BA the CU-masked front / back streams come from
+ *   hipExtStreamCreateWithCUMask, which gives default-flag, default-priority streams: they
+ *   synchronise with the legacy null stream (null-stream work of the caller, e.g. a hipMemset or
+ *   torch's default stream, serialises against the pipeline) and the front stream loses its high
+ *   priority in that mode (the C4 bench runs in it).
  *   timestamps[n] (seconds, the frames' SynchronizedFrameSet.timestamp) may be NULL.  At most two
  *   batches' results are held: an unread batch s-2 is dropped when batch s is submitted.
  * tslam_poll_batch: results of the oldest unread submitted batch: returns 1 and fills the outputs

@@ -293,7 +293,7 @@ def test_long_session_keeps_closing_loops():
     late = [(c, q) for c, q, _ in lp.loops if q >= 6000]
     assert late, lp.loops[-3:]
     assert all(q - c <= 5 * 1024 for c, q, _ in lp.loops)
-    pol, want, checked = _policy_from_trace(eng, recs, solve_check_every=97)
+    pol, want, checked = _policy_from_trace(eng, recs, solve_check_every=17)
     assert lp.loops == pol.loops and len(checked) >= 10
     _compare(published, want, n)
     eng.shutdown()
