@@ -276,21 +276,25 @@ def _oracle_worker(args):
                            "intr": (r["fx"], r["fy"], r["cx"], r["cy"])} for o, r in zip(outs, rects)], E, cfg)
             n += 1
         return n, time.perf_counter() - t0
-    trk = O.OracleTracker(cfg, rect_d)
-    bat = None
-    if cfg.ba_window > 0:
-        from oracle.numpy_ba import BAParams, BATracker
+    # one stereo pair: the CPU SlamEngine (oracle/numpy_engine.py, BASELINE configs[0]) through the
+    # reference's loop (run_slam.py:299-328): a CameraRig replaying the chunk, initialize with the
+    # rig's calibration, process_frames per synchronised set (sets built before timing)
+    from oracle.numpy_engine import NumpySlamEngine
+    from thor_slam_amd.camera.rig import CameraRig
+    from thor_slam_amd.synthetic import CachedStereoSource
 
-        bat = BATracker(cfg.n_features, (rect_d["fx"], rect_d["fy"], rect_d["cx"], rect_d["cy"],
-                                         rect_d["fx"] * rect_d["baseline"]),
-                        BAParams(cfg.ba_window, cfg.ba_kf_interval, cfg.ba_iters, cfg.ba_lambda, cfg.ba_outlier_px))
+    src = CachedStereoSource(np.asarray(frames), width=frames.shape[-1], height=frames.shape[-2],
+                             n_frames=len(frames))
+    rig = CameraRig([src])
+    rig.start()
+    sets = [rig.get_synchronized_frames() for _ in range(256)]
+    eng = NumpySlamEngine(num_cameras=2, config=cfg)
+    eng.initialize(rig.calibration)
     n = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
-        i = n % len(frames)
-        res = trk.step(frames[i, 0], frames[i, 1])
-        if bat is not None:
-            bat.step(res)
+        eng.process_frames(sets[n % len(sets)])
+        eng.results.clear()   # the per-frame records are for tests
         n += 1
     return n, time.perf_counter() - t0
 
@@ -350,7 +354,10 @@ def cpu_baseline(frames, rect_d, cfg, budget_s: float, procs: int, what: str) ->
     rate = n / wall
     return {"value": rate, "unit": "frames/s", "cores": len(parts), "kind": "port",
             "sample": f"{n} {what} ({len(parts)} process(es) x {budget_s:.0f} s, each replaying a contiguous chunk), "
-                      f"NumPy oracle{' + local BA' if cfg.ba_window else ''}",
+                      + ("NumpySlamEngine.process_frames (oracle/numpy_engine.py: the NumPy CPU SlamEngine of "
+                         "BASELINE configs[0], through CameraRig sets as run_slam.py:299-328; this config's "
+                         "loop closure / IMU / BA settings)" if not isinstance(rect_d, list) and not cfg.rgbd
+                         else "NumPy oracle per pair + rig pose"),
             "single_core": {"value": n1 / wall1, "cores": 1, "sample": f"{n1} frames, 1 process x {wall1:.0f} s"},
             # the cores used are the per-GPU share of the node (pool rule: worker pools sized to
             # it); the whole node's figure is the linear extrapolation of the measured per-process
