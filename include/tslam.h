@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 15
+#define TSLAM_ABI_VERSION 16
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -522,6 +522,11 @@ int tslam_ba_read(tslam_handle* h, int pair, int64_t* frames, double* cam_T_worl
  * (2 (6n+1)^2 3L per launch, n keyframes, L landmarks), then re-arms timing for up to
  * `max_launches` further launches (0 = off). */
 int tslam_ba_profile(tslam_handle* h, int max_launches, double* schur_ms, int64_t* schur_launches, double* schur_flops);
+/* Verification of the in-launch hand-off: split = 1 runs every later pair-window
+ * Gauss-Newton step as k_ba_reduce + k_ba_solve (a kernel boundary between the reduction and the
+ * solve) instead of k_ba_reduce_solve; both sum in the same order, so the windows agree bit for
+ * bit.  0 (default) restores the fused launch. */
+int tslam_ba_split_solve(tslam_handle* h, int split);
 /* Measurement: `reps` back-to-back k_ba_schur launches on pair `pair`'s last solved window (the
  * kernel only rewrites its own outputs), between two HIP events on `stream`: the average launch
  * duration and the algorithmic flops per launch (for the FP64 MFMA roofline, without per-launch

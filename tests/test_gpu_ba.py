@@ -96,6 +96,42 @@ def test_ba_window_parity(batch):
     assert want[-1]["solve"]["n_lm"] > 50
 
 
+def test_ba_split_solve_equals_fused_handoff():
+    """The in-launch hand-off of k_ba_reduce_solve (write-through stores + agent-scope loads, no
+    kernel boundary) against the same reduction and solve split across a kernel
+    boundary (tslam_ba_split_solve): windows, poses and landmarks bit-identical, and the IMU
+    factor path (it reads the window poses in the solve block) too."""
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    n, batch = 12, 3
+    sc, _ = _scenario_and_oracle(n)
+    imu = _imu_factors(sc, n)
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    runs = {}
+    for split in (False, True):
+        h = Handle([sc["rect"]], sc["cfg"], max_batch=batch)
+        try:
+            h.ba_split_solve(split)
+            for g, (M, w) in imu.items():
+                h.ba_imu_factor(g, M, w)
+            snaps = []
+            for b0 in range(0, n, batch):
+                h.submit(dev[b0:].data_ptr(), batch, torch.cuda.current_stream().cuda_stream)
+                snaps.append(h.ba_read(0))
+            runs[split] = (snaps, h.read_poses(batch))
+        finally:
+            h.close()
+    for k, (a, b) in enumerate(zip(runs[False][0], runs[True][0])):
+        for key in ("frames", "lm", "T_cw", "X"):
+            np.testing.assert_array_equal(np.asarray(a[key]).view(np.uint8), np.asarray(b[key]).view(np.uint8),
+                                          err_msg=f"batch {k} {key}")
+        assert a["ok"] and b["ok"] and a["n_lm"] == b["n_lm"] > 50
+    for key, a in runs[False][1].items():   # the last batch's published poses
+        np.testing.assert_array_equal(a, runs[True][1][key], err_msg=key)
+
+
 def test_ba_imu_rotation_factors_parity():
     """IMU rotation factors between window-consecutive keyframes (tslam_ba_imu_factor) against the
     oracle's imu_terms: same windows to 1e-9, through evictions, in batches of 3 — and the factors

@@ -237,3 +237,40 @@ def test_engine_dense_map():
     eng.reset()
     assert not eng.get_dense_map()["weight"].any()
     eng.shutdown()
+
+
+def test_sharded_rgbd_rig_dense_map_equals_one_device():
+    """C5 over 4 ranks behind SlamEngine: HipSlamConfig(rgbd, dense_map,
+    devices=(0,)*4, copy transport) integrates pair 0's depth and colour on rank 0 with the device
+    poses and gives a TSDF, weight and colour layer bit-identical to the one-device engine's."""
+    import json
+    from pathlib import Path
+
+    from thor_slam_amd.slam.hip_engine import HipSlamEngine
+    from thor_slam_amd.synthetic import synthetic_rgbd_rig
+
+    names = ("192.168.2.21", "192.168.2.22", "192.168.2.23", "192.168.2.25")
+    joints = json.loads((Path(__file__).parent / "golden" / "brackets_joints.json").read_text())
+    n, batch = 8, 4
+    sets = None
+    out = {}
+    for mode, devices in (("one", ()), ("four", (0, 0, 0, 0))):
+        srcs, rig = synthetic_rgbd_rig(joints, names, 320, 240)
+        rig.start()
+        if sets is None:
+            sets = [rig.get_synchronized_frames() for _ in range(n)]
+        cfg = HipSlamConfig(rgbd=True, n_features=1000, n_levels=3, batch_size=batch, dense_map=True,
+                            tsdf_origin=(-7.2, -1.8, -4.4), tsdf_dims=(88, 36, 88), voxel_size=0.1,
+                            devices=devices, shard_transport="copy", enable_loop_closure=False)
+        eng = HipSlamEngine(num_cameras=8, config=cfg)
+        eng.initialize(rig.calibration)
+        for fs in sets:
+            eng.process_frames(fs)
+        dm = eng.get_dense_map()
+        out[mode] = (dm, eng._latest_pose.to_4x4_matrix())
+        eng.shutdown()
+    one, four = out["one"][0], out["four"][0]
+    assert (one["weight"] > 0).sum() > 5000
+    for key in ("tsdf", "weight", "color", "color_weight"):
+        np.testing.assert_array_equal(four[key].view(np.uint32), one[key].view(np.uint32), err_msg=key)
+    np.testing.assert_array_equal(out["four"][1], out["one"][1])

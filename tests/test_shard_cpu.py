@@ -212,15 +212,16 @@ def test_sharded_decomposition_matches_sequential_oracle(tmp_path):
 
 def test_sharded_config_validation():
     """HipSlamConfig(devices=...): local BA and batches of any length are allowed on a sharded rig
-    (rank 0 solves the window after the state gather; ranges may be uneven), the dense map is not
-    (the TSDF integrates on one device), and the transport is checked."""
+    (rank 0 solves the window after the state gather; ranges may be uneven), so is the dense map of
+    an RGB-D rig (the TSDF lives on rank 0, whose camera is pair 0), and the transport is checked."""
     import pytest
 
     from thor_slam_amd.params import HipSlamConfig
 
     HipSlamConfig(devices=(0, 1, 2, 3), ba_window=10, batch_size=6).validate()
     HipSlamConfig(devices=(0, 1), enable_loop_closure=True, batch_size=1).validate()
-    with pytest.raises(ValueError, match="dense map"):
-        HipSlamConfig(devices=(0, 1), rgbd=True, dense_map=True).validate()
+    HipSlamConfig(devices=(0, 1), rgbd=True, dense_map=True).validate()
+    with pytest.raises(ValueError, match="without local BA"):
+        HipSlamConfig(devices=(0, 1), rgbd=True, ba_window=4).validate()
     with pytest.raises(ValueError, match="shard_transport"):
         HipSlamConfig(devices=(0, 1), shard_transport="tcp").validate()

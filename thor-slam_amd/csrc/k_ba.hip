@@ -727,26 +727,36 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
 }
 
 // Fixed-order sum of the partials of the blocks that had a chunk: block = 64 elements of a
-// partial, 4 waves each summing every 4th partial, then the 4 wave sums in order.  Elements 0..4095
-// are C, 4096.. the camera blocks U_c, g_c ([camera][27]).
-__global__ __launch_bounds__(256) void k_ba_reduce(BatchCtx c, BaArgs a) {
-    BA_PRIO;
-    __shared__ double s_p[4][64];
-    BaPair q = ba_pair(c, a, a.pair);
+// partial, BA_SOLVE_WAVES waves each summing every BA_SOLVE_WAVES-th partial, then the wave sums
+// in order (k_ba_reduce_solve sums in the same order: the split and the fused launch agree bit for
+// bit).  Elements 0..4095 are C, 4096.. the camera blocks U_c, g_c ([camera][27]).
+#define BA_SOLVE_WAVES 8
+__device__ __forceinline__ double ba_reduce_elem(const BaPair& q, const BaArgs& a, int e, bool live,
+                                                 double (*s_p)[64]) {
     const int L = q.counts[1];
     const int np = min(a.nsplit, (L + BA_CHUNK - 1) / BA_CHUNK);
     const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-    const int e = blockIdx.x * 64 + lane;
-    const bool live = e < 4096 + a.n_order * 27;
-    double s = 0.0;
+    double sum = 0.0;
     if (live) {
 #pragma unroll 8
-        for (int b = grp; b < np; b += 4) s += q.part[(size_t)b * TS_BA_PART + e];
+        for (int b = grp; b < np; b += BA_SOLVE_WAVES) sum += q.part[(size_t)b * TS_BA_PART + e];
     }
-    s_p[grp][lane] = s;
+    s_p[grp][lane] = sum;
     __syncthreads();
-    if (grp != 0 || !live) return;
-    const double v = ((s_p[0][lane] + s_p[1][lane]) + s_p[2][lane]) + s_p[3][lane];
+    double v = s_p[0][lane];
+#pragma unroll
+    for (int g = 1; g < BA_SOLVE_WAVES; ++g) v += s_p[g][lane];
+    return v;   // meaningful in wave 0
+}
+
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce(BatchCtx c, BaArgs a) {
+    BA_PRIO;
+    __shared__ double s_p[BA_SOLVE_WAVES][64];
+    BaPair q = ba_pair(c, a, a.pair);
+    const int e = blockIdx.x * 64 + (threadIdx.x & 63);
+    const bool live = e < 4096 + a.n_order * 27;
+    const double v = ba_reduce_elem(q, a, e, live, s_p);
+    if ((threadIdx.x >> 6) != 0 || !live) return;
     if (e < 4096) q.C[e] = v;
     else q.cam_U[e - 4096] = v;
 }
@@ -765,7 +775,6 @@ __global__ __launch_bounds__(256) void k_ba_reduce(BatchCtx c, BaArgs a) {
 //   * wave 0 then solves D L^T x = y (x_i by readlane, l_ki from the upper triangle, where the
 //     panel wave left them).
 // Camera updates R <- cayley(w) R, t <- ... + rho follow.
-#define BA_SOLVE_WAVES 8
 #define BA_SP 65   // LDS row pitch of S (doubles)
 // `handoff`: C and the camera blocks were published by other workgroups of this launch with
 // write-through stores (k_ba_reduce_solve), so they are read with agent-scope loads that bypass
@@ -1027,31 +1036,15 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, Ba
 // cost more than the launch it saves (measured: 0.300 against 0.260 ms per keyframe).
 __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_solve(BatchCtx c, BaArgs a) {
     BA_PRIO;
-    // all BA_SOLVE_WAVES waves sum (every 8th partial each: half the dependent chain of k_ba_reduce's
-    // four), then the 8 wave sums in order
+    // all BA_SOLVE_WAVES waves sum (every 8th partial each), then the 8 wave sums in order
     __shared__ double s_p[BA_SOLVE_WAVES][64];
     __shared__ int s_last;
     BaPair q = ba_pair(c, a, a.pair);
-    const int L = q.counts[1];
-    const int np = min(a.nsplit, (L + BA_CHUNK - 1) / BA_CHUNK);
-    const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-    const int e = blockIdx.x * 64 + lane;
+    const int e = blockIdx.x * 64 + (threadIdx.x & 63);
     const bool live = e < 4096 + a.n_order * 27;
-    {
-        double sum = 0.0;
-        if (live) {
-#pragma unroll 8
-            for (int b = grp; b < np; b += BA_SOLVE_WAVES) sum += q.part[(size_t)b * TS_BA_PART + e];
-        }
-        s_p[grp][lane] = sum;
-    }
-    __syncthreads();
-    if (grp == 0 && live) {
-        double v = s_p[0][lane];
-#pragma unroll
-        for (int g = 1; g < BA_SOLVE_WAVES; ++g) v += s_p[g][lane];
+    const double v = ba_reduce_elem(q, a, e, live, s_p);
+    if ((threadIdx.x >> 6) == 0 && live)
         __hip_atomic_store(e < 4096 ? q.C + e : q.cam_U + (e - 4096), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the write-through stores have landed
     __syncthreads();
     if (threadIdx.x == 0)
@@ -1176,7 +1169,7 @@ static void launch_ba_linearize(const BatchCtx& c, const BaArgs& a, int it, hipS
     hipLaunchKernelGGL(k_ba_schur, dim3(a.nsplit), dim3(BA_SCHUR_THREADS), 0, s, c, ai);
     if (rec) (void)hipEventRecord(timing->ev[2 * timing->used++ + 1], s);
     if (!reduce) return;   // k_ba_reduce_solve follows
-    hipLaunchKernelGGL(k_ba_reduce, dim3(64 + (a.n_order * 27 + 63) / 64), dim3(256), 0, s, c, a);
+    hipLaunchKernelGGL(k_ba_reduce, dim3(64 + (a.n_order * 27 + 63) / 64), dim3(64 * BA_SOLVE_WAVES), 0, s, c, a);
 }
 
 static void launch_ba_backsub(const BatchCtx& c, const BaArgs& a, hipStream_t s) {
@@ -1184,11 +1177,14 @@ static void launch_ba_backsub(const BatchCtx& c, const BaArgs& a, hipStream_t s)
     hipLaunchKernelGGL(k_ba_backsub, dim3(16 * nb), dim3(256), 0, s, c, a);   // the last iteration's
 }
 
-void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing) {
+void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing, bool split) {
     launch_ba_prepare(c, a, s);
     for (int it = 0; it < a.iters; ++it) {
-        launch_ba_linearize(c, a, it, s, timing, false);
-        hipLaunchKernelGGL(k_ba_reduce_solve, dim3(64 + (a.n_order * 27 + 63) / 64), dim3(64 * BA_SOLVE_WAVES), 0, s, c, a);
+        launch_ba_linearize(c, a, it, s, timing, split);
+        if (split)   // the kernel boundary instead of the in-launch hand-off (tslam_ba_split_solve)
+            hipLaunchKernelGGL(k_ba_solve, dim3(1), dim3(64 * BA_SOLVE_WAVES), 0, s, c, a);
+        else
+            hipLaunchKernelGGL(k_ba_reduce_solve, dim3(64 + (a.n_order * 27 + 63) / 64), dim3(64 * BA_SOLVE_WAVES), 0, s, c, a);
     }
     launch_ba_backsub(c, a, s);
 }

@@ -188,6 +188,7 @@ struct tslam_handle {
     int64_t ba_nkf = 0;
     int64_t ba_last = -1;    // newest frame inserted
     BaTiming ba_timing{};    // k_ba_schur events while profiling is on
+    bool ba_split = false;   // tslam_ba_split_solve: k_ba_reduce + k_ba_solve instead of k_ba_reduce_solve
     std::map<std::pair<int, int64_t>, std::array<double, 10>> ba_imu;   // (pair, keyframe) -> IMU factor
     std::vector<BaArgs> ba_solved;   // per pair: the arguments of its last window solve (replays)
     // BA on its own stream (overlapping the next batch): events and the batch parity
@@ -502,7 +503,7 @@ static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const doub
         }
         for (int p = 0; p < h->P; ++p) {
             a.pair = p;
-            launch_ba_solve(c, a, s, h->ba_timing.ev ? &h->ba_timing : nullptr);
+            launch_ba_solve(c, a, s, h->ba_timing.ev ? &h->ba_timing : nullptr, h->ba_split);
             h->ba_solved[p] = a;
         }
     }
@@ -2713,6 +2714,12 @@ int tslam_ba_replay_schur(tslam_handle* h, int pair, int reps, void* stream, dou
     HIPCHK(hipMemcpy(&fl, h->ba.flops, sizeof(double), hipMemcpyDeviceToHost));
     if (us_per_launch) *us_per_launch = 1e3 * ms / reps;
     if (flops_per_launch) *flops_per_launch = fl / reps;
+    return TSLAM_OK;
+}
+
+int tslam_ba_split_solve(tslam_handle* h, int split) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    h->ba_split = split != 0;
     return TSLAM_OK;
 }
 

@@ -146,7 +146,8 @@ struct BaTiming {
     hipEvent_t* ev;   // 2 * cap events
     int cap, used;
 };
-void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing);
+// split: k_ba_reduce + k_ba_solve per iteration instead of k_ba_reduce_solve (same sums, bit for bit)
+void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing, bool split = false);
 // rig-level A8: the body snapshot of the batch, a keyframe's body pose (and every pair's camera at
 // E_p^-1 B), and the joint solve over all pairs (storage pair c.P = the body window)
 void launch_ba_snapshot_rig(const BatchCtx& c, double* dst, hipStream_t s);

@@ -194,6 +194,7 @@ _SIGNATURES = {
     "tslam_ba_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6),
     "tslam_ba_replay_schur": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+    "tslam_ba_split_solve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "tslam_ba_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
     "tslam_loop_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
@@ -874,6 +875,10 @@ class Handle:
         _check(self.lib.tslam_ba_replay_schur(self.h, int(pair), int(reps), ctypes.c_void_p(stream), ctypes.byref(us),
                                               ctypes.byref(fl)))
         return {"us": us.value, "flops": fl.value, "reps": int(reps)}
+
+    def ba_split_solve(self, split: bool) -> None:
+        """k_ba_reduce + k_ba_solve (kernel boundary) instead of k_ba_reduce_solve (tslam.h)."""
+        _check(self.lib.tslam_ba_split_solve(self.h, int(bool(split))))
 
     def ba_profile(self, max_launches: int = 0) -> dict:
         """Schur-kernel HIP-event time / launches / algorithmic flops since the last call; re-arms

@@ -155,8 +155,10 @@ class HipSlamConfig(SlamConfig):
         if self.loop_latency < 0 or self.imu_prior_lag < 0 or self.loop_cooldown < 0:
             raise ValueError("loop_latency, loop_cooldown and imu_prior_lag must be >= 0")
         if self.devices:
-            if self.dense_map:   # the TSDF integrates on one device; local BA runs on rank 0 (state gather)
-                raise ValueError("a sharded rig (devices) runs without the dense map")
+            # local BA runs on rank 0 (state gather of a stereo rig); a camera-sharded RGB-D rig keeps
+            # the TSDF on rank 0 (pair 0 is rank 0's camera) and has no local BA or loop closure
+            if self.rgbd and self.ba_window:
+                raise ValueError("a camera-sharded RGB-D rig (devices) runs without local BA")
             if self.shard_transport not in ("rccl", "copy"):
                 raise ValueError("shard_transport must be 'rccl' or 'copy'")
         if not 0 <= self.max_hamming <= 253:

@@ -403,7 +403,11 @@ class HipSlamEngine(SlamEngine):
                                        cfg.tsdf_integrator_truncation_distance_vox,
                                        cfg.tsdf_integrator_max_integration_distance_m, cfg.tsdf_max_weight)
             self._loop = None
-            if cfg.enable_loop_closure:
+            if cfg.enable_loop_closure and cfg.devices and cfg.rgbd:
+                # rank 0's ring holds only its own cameras' features (no state gather): no rig-wide
+                # place recognition
+                logger.warning("loop closure is off on a camera-sharded RGB-D rig")
+            elif cfg.enable_loop_closure:
                 # place recognition over every pair's camera (P database entries per keyframe,
                 # keyframe-major) and verification on the pair that voted best; the keyframe nodes
                 # are pair 0's rectified-left poses (on a multi-pair rig taken from the rig's body
@@ -431,8 +435,6 @@ class HipSlamEngine(SlamEngine):
         closure and relocalisation run on rank 0's handle) and pinned result slots (asynchronous
         polling); pinned staging + device input per rank and batch parity."""
         torch, cfg = self._torch, self._config
-        if cfg.dense_map:
-            raise RuntimeError("the dense map runs on one device (devices=[] with dense_map)")
         devs = [int(d) for d in cfg.devices]
         world = len(devs)
         n_cams = shape[1]
@@ -446,7 +448,9 @@ class HipSlamEngine(SlamEngine):
                            for (l, _), r in zip(self._pairs, self._rects)])
             handles.append(h)
         group = HandleGroup(handles, cfg.shard_transport)
-        handles[0].shard_options(gather=True, results=True, pipeline=True)   # results through the slots
+        # results through the slots; the state gather (rank 0's ring as the one-handle path's) is the
+        # stereo rig's: a camera-sharded RGB-D rig moves pair blocks and keeps no rig-wide ring
+        handles[0].shard_options(gather=not cfg.rgbd, results=True, pipeline=True)
         S = n_cams // world
         part = (cfg.batch_size, S) + tuple(shape[2:])
         self._shard = {"handles": handles, "group": group, "world": world, "S": S, "devices": devs, "batches": 0,
@@ -491,6 +495,13 @@ class HipSlamEngine(SlamEngine):
         self._prev_stamp = stamps[-1]
         if not self._async:
             self._drain(block=True)
+        if self._config.dense_map:
+            # camera-sharded RGB-D: pair 0 is rank 0's first camera, and rank 0 ends the batch with
+            # every pair's chained poses (the pose records' all-gather), so the volume lives on rank
+            # 0 and integrates its own input with the device poses — no extra exchange (the batch
+            # was waited for: the dense map keeps the engine synchronous)
+            self._integrate_depth(sh["dev"][0][k].data_ptr(), n, torch.cuda.current_stream(sh["devices"][0]).cuda_stream,
+                                  cams_per_frame=S)
 
     # ------------------------------------------------------------------------------------------
     def _frame_images(self, frame_set: SynchronizedFrameSet) -> np.ndarray | None:
@@ -730,18 +741,20 @@ class HipSlamEngine(SlamEngine):
         return res
 
     # -- RGB-D dense mapping ----------------------------------------------
-    def _integrate_depth(self, records_ptr: int, n: int, stream: int) -> None:
+    def _integrate_depth(self, records_ptr: int, n: int, stream: int, cams_per_frame: int | None = None) -> None:
         """The batch's depth images of pair 0 into the TSDF volume, with the batch's device-resident
-        tracked poses (untracked frames are skipped), on the batch's stream."""
+        tracked poses (untracked frames are skipped), on the batch's stream.  ``cams_per_frame``: the
+        records per frame of the buffer (a sharded rig: rank 0's cameras, pair 0 first)."""
         if not self._config.dense_map:
             return
         r = self._rects[0]
         hw = r.width * r.height
+        stride = 5 * hw * (cams_per_frame or len(self._pairs))
         if self._config.dense_color:   # the record's BGR part with its depth part
-            self._handle.tsdf_integrate_rgbd(records_ptr, records_ptr + 3 * hw, 5 * hw * len(self._pairs), n,
+            self._handle.tsdf_integrate_rgbd(records_ptr, records_ptr + 3 * hw, stride, n,
                                              first_frame=self._handle.frames_done - n, pair=0, stream=stream)
         else:
-            self._handle.tsdf_integrate(records_ptr + 3 * hw, 5 * hw * len(self._pairs), n,
+            self._handle.tsdf_integrate(records_ptr + 3 * hw, stride, n,
                                         first_frame=self._handle.frames_done - n, pair=0, stream=stream)
 
     def get_dense_map(self) -> dict | None:
