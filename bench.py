@@ -723,7 +723,12 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     bstream = (cu_masked_stream(dev_index, args.front_cu_reserve, 0) if masked else torch.cuda.Stream()) if args.pipeline else stream
     if args.back_cu and args.pipeline and not masked:   # experiment: the back kernels on N CUs spread over the chip
         n_cu = torch.cuda.get_device_properties(dev_index).multi_processor_count
-        bstream = cu_masked_stream(dev_index, 0, 0, [i * n_cu // args.back_cu for i in range(args.back_cu)])
+        back_set = [i * n_cu // args.back_cu for i in range(args.back_cu)]
+        bstream = cu_masked_stream(dev_index, 0, 0, back_set)
+        if args.split_cu:   # and the front kernels on the other CUs (disjoint)
+            stream = cu_masked_stream(dev_index, 0, 0, sorted(set(range(n_cu)) - set(back_set)))
+            torch.cuda.set_stream(stream)
+            sp = stream.cuda_stream
     bsp = bstream.cuda_stream
     back_done = [torch.cuda.Event(), torch.cuda.Event()]
     back_issued = [False, False]
@@ -1352,6 +1357,8 @@ def main() -> None:
                          "15.6k / 15.7k / 16.2k / 15.9k / 16.2k / 16.0k frames/s)")
     ap.add_argument("--back-cu", type=int, default=0,
                     help="experiment (c2/c3): the back kernels on a stream restricted to N CUs spread over the chip")
+    ap.add_argument("--split-cu", type=int, default=0,
+                    help="experiment (c2/c3, with --back-cu N): the front kernels on the other CUs, disjoint from the back's")
     ap.add_argument("--ba-priority", type=int, default=0, help="C4: the BA stream at high priority")
     ap.add_argument("--ba-cus", type=int, default=0,
                     help="C4 experiment: the BA stream CU-masked to the last N CUs (with --front-cu-reserve N "
