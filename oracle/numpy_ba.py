@@ -38,6 +38,25 @@ Spec (shared with ``thor-slam_amd/csrc/k_ba.hip``):
   residual e has Jacobians ``Q^T`` on camera c's rotation and ``-I`` on camera c - 1's (left
   updates), so ``S_cc += w I``, ``S_{c-1,c-1} += w I``, ``S_{c,c-1} += -w Q`` (rotation blocks),
   ``b_c -= w Q e``, ``b_{c-1} += w e``; camera 0's rows drop with the gauge.
+* Inertial factors (tightly coupled, optional; the accelerometer leg of SURVEY.md §8f item 2):
+  keyframe g may carry the accelerometer preintegration from the previous keyframe
+  (``preintegrate``: dv, dp in the previous keyframe's camera axes, their Jacobians Jv, Jp with
+  respect to the accelerometer bias, the bias ba_lin they were integrated with, dt, and the
+  weights wv, wp in 1 / (m/s)^2 and 1 / m^2) and an initial world velocity of its camera.  The
+  window then carries one velocity v_c per keyframe and one accelerometer bias ba for the window
+  (``set_inertial``: world gravity gw, the bias prior ba0 with weight wb).  Between window-
+  consecutive keyframes (i, j) = (c - 1, c) whose later one carries a factor, with R_i the
+  world_T_cam rotation (R_cw,i^T), p the camera centres and dba = ba - ba_lin:
+      r_v = R_cw,i (v_j - v_i - gw dt) - (dv + Jv dba)
+      r_p = R_cw,i (p_j - p_i - v_i dt - gw dt^2 / 2) - (dp + Jp dba)
+  weighted wv, wp; under the left camera update (rho, omega): d(R_cw,i u)/d omega_i =
+  -[R_cw,i u]x, dp/d rho = -R_wc, so dr_p/d rho_i = I, dr_p/d rho_j = -R_cw,i R_wc,j,
+  dr_v/d v_i = -R_cw,i, dr_v/d v_j = R_cw,i, dr_p/d v_i = -R_cw,i dt, dr/d ba = -(Jv; Jp).
+  With y = (v_0 .. v_{n-1}, ba) the normal equations [[S + lam I, Hxy], [Hyx, Hyy]] (Hyy with
+  lam I and the prior wb I on ba) are reduced to the cameras, S' = S - Hxy Hyy^-1 Hyx,
+  b' = b - Hxy Hyy^-1 b_y (camera 0's rows dropped first), and after the camera solve
+  dy = Hyy^-1 (b_y - Hyx dc): v_c += dv_c, ba += dba.  A window with no inertial factor skips
+  all of it (the solve is the visual one, bit for bit).
 """
 
 from __future__ import annotations
@@ -47,6 +66,89 @@ from dataclasses import dataclass
 import numpy as np
 
 from .numpy_slam import cayley, level0_coords
+
+# inertial factor record per slot (k_ba.hip TS_BA_INE): dv 0-2, dp 3-5, Jv 6-14 and Jp 15-23
+# (row-major 3x3), ba_lin 24-26, dt 27, wv 28, wp 29 (0 = no factor), 30-31 unused
+INE_N = 32
+
+
+def _exp_so3(w: np.ndarray) -> np.ndarray:
+    th = float(np.linalg.norm(w))
+    K = np.array([[0.0, -w[2], w[1]], [w[2], 0.0, -w[0]], [-w[1], w[0], 0.0]])
+    if th < 1e-12:
+        return np.eye(3) + K
+    return np.eye(3) + np.sin(th) / th * K + (1.0 - np.cos(th)) / (th * th) * (K @ K)
+
+
+def preintegrate(samples: list, rect_R_imu: np.ndarray, bg: np.ndarray, ba: np.ndarray,
+                 lever: np.ndarray | None = None, w_prev: np.ndarray | None = None,
+                 acc_density: float = 2.553e-3, v_floor: float = 1e-2, p_floor: float = 1e-3) -> np.ndarray:
+    """The inertial factor record (INE_N doubles) of the frame intervals ``samples`` = [(dt, gyro,
+    accel)] (IMU axes) from one keyframe to the next, in the first keyframe's camera axes: per
+    interval w = Ri (gyro - bg) (camera axes), alpha = (w - w_prev) / dt (0 for the first interval
+    without ``w_prev``), the camera's specific force a = Ri (accel - ba) - w x (w x r) - alpha x r
+    (r = the IMU's position in the camera, as ``numpy_imu.ImuFilter``), then
+        dp += dv dt + dR a dt^2 / 2,   Jp += Jv dt - dR Ri dt^2 / 2,
+        dv += dR a dt,                 Jv += -dR Ri dt,
+        dR <- dR exp([w dt]x);
+    weights wv = 1 / (n_a^2 T + v_floor^2), wp = 1 / (n_a^2 T^3 / 3 + p_floor^2) over the total T."""
+    Ri = np.asarray(rect_R_imu, dtype=np.float64)
+    r = np.zeros(3) if lever is None else np.asarray(lever, dtype=np.float64)
+    dR, dv, dp = np.eye(3), np.zeros(3), np.zeros(3)
+    Jv, Jp = np.zeros((3, 3)), np.zeros((3, 3))
+    T = 0.0
+    wp = None if w_prev is None else np.asarray(w_prev, dtype=np.float64)
+    for dt, gyro, accel in samples:
+        w = Ri @ (np.asarray(gyro, dtype=np.float64) - bg)
+        al = np.zeros(3) if wp is None else (w - wp) / dt
+        a = Ri @ (np.asarray(accel, dtype=np.float64) - ba) - np.cross(w, np.cross(w, r)) - np.cross(al, r)
+        dp = dp + dv * dt + 0.5 * (dR @ a) * dt * dt
+        Jp = Jp + Jv * dt - 0.5 * (dR @ Ri) * dt * dt
+        dv = dv + (dR @ a) * dt
+        Jv = Jv - (dR @ Ri) * dt
+        dR = dR @ _exp_so3(w * dt)
+        T += dt
+        wp = w
+    out = np.zeros(INE_N)
+    out[0:3], out[3:6], out[6:15], out[15:24], out[24:27] = dv, dp, Jv.reshape(9), Jp.reshape(9), ba
+    out[27] = T
+    out[28] = 1.0 / (acc_density ** 2 * T + v_floor ** 2)
+    out[29] = 1.0 / (acc_density ** 2 * T ** 3 / 3.0 + p_floor ** 2)
+    return out
+
+
+def inertial_residual(f: np.ndarray, Rcw_i: np.ndarray, tcw_i: np.ndarray, Rcw_j: np.ndarray, tcw_j: np.ndarray,
+                      v_i: np.ndarray, v_j: np.ndarray, ba: np.ndarray, gw: np.ndarray) -> np.ndarray:
+    """(r_v, r_p) of one inertial factor record at the cameras cam_T_world i, j."""
+    dt = f[27]
+    dba = ba - f[24:27]
+    p_i, p_j = -Rcw_i.T @ tcw_i, -Rcw_j.T @ tcw_j
+    uv = v_j - v_i - gw * dt
+    up = p_j - p_i - v_i * dt - 0.5 * gw * dt * dt
+    rv = Rcw_i @ uv - (f[0:3] + f[6:15].reshape(3, 3) @ dba)
+    rp = Rcw_i @ up - (f[3:6] + f[15:24].reshape(3, 3) @ dba)
+    return np.concatenate([rv, rp])
+
+
+def inertial_jacobian(f: np.ndarray, Rcw_i: np.ndarray, tcw_i: np.ndarray, Rcw_j: np.ndarray, tcw_j: np.ndarray,
+                      v_i: np.ndarray, v_j: np.ndarray, gw: np.ndarray) -> np.ndarray:
+    """6 x 21 Jacobian of (r_v, r_p): columns rho_i, omega_i, rho_j, omega_j (left camera
+    updates), v_i, v_j, ba."""
+    dt = f[27]
+    p_i, p_j = -Rcw_i.T @ tcw_i, -Rcw_j.T @ tcw_j
+    uv = v_j - v_i - gw * dt
+    up = p_j - p_i - v_i * dt - 0.5 * gw * dt * dt
+    J = np.zeros((6, 21))
+    J[0:3, 3:6] = -_skew(Rcw_i @ uv)
+    J[0:3, 12:15] = -Rcw_i
+    J[0:3, 15:18] = Rcw_i
+    J[0:3, 18:21] = -f[6:15].reshape(3, 3)
+    J[3:6, 0:3] = np.eye(3)
+    J[3:6, 3:6] = -_skew(Rcw_i @ up)
+    J[3:6, 6:9] = -Rcw_i @ Rcw_j.T
+    J[3:6, 12:15] = -Rcw_i * dt
+    J[3:6, 18:21] = -f[15:24].reshape(3, 3)
+    return J
 
 
 @dataclass
@@ -86,6 +188,10 @@ class KeyframeWindow:
         self.X = np.zeros((W * K, 3))
         self.imu_M = np.tile(np.eye(3), (W, 1, 1))   # IMU rotation from the previous keyframe
         self.imu_w = np.zeros(W)                     # its weight (0 = no factor)
+        self.ine = np.zeros((W, INE_N))              # inertial factor from the previous keyframe
+        self.vel = np.zeros((W, 3))                  # world velocity of the keyframe's camera
+        self.ba = np.zeros(3)                        # the window's accelerometer bias (IMU axes)
+        self.ine_cfg = (np.zeros(3), np.zeros(3), 0.0)   # gravity (world), bias prior, its weight
         self.n_kf = 0
 
     # -- window bookkeeping --------------------------------------------------------------------
@@ -115,10 +221,12 @@ class KeyframeWindow:
         self.frame[slot] = -1
 
     def add_keyframe(self, g: int, T_cw: np.ndarray, u: np.ndarray, v: np.ndarray, disp: np.ndarray,
-                     link: np.ndarray | None, imu: tuple | None = None) -> int:
+                     link: np.ndarray | None, imu: tuple | None = None, ine: tuple | None = None) -> int:
         """Insert keyframe g (u, v level-0 observations, NaN = invalid; disp refined, NaN = none;
         link into the previous keyframe or None for the first; imu = (M, w) the IMU rotation
-        factor from the previous keyframe, or None)."""
+        factor from the previous keyframe, or None; ine = (record, v0) the inertial factor from
+        the previous keyframe (``preintegrate``) and the camera's initial world velocity, or
+        None: no factor, velocity 0)."""
         K = self.K
         slot = self.n_kf % self.p.window
         prev = self.order()[-1] if self.n_kf else -1
@@ -127,6 +235,8 @@ class KeyframeWindow:
         self.frame[slot] = g
         self.T_cw[slot] = T_cw
         self.imu_M[slot], self.imu_w[slot] = (np.eye(3), 0.0) if imu is None else (np.asarray(imu[0], float), float(imu[1]))
+        self.ine[slot] = 0.0 if ine is None else np.asarray(ine[0], dtype=np.float64)
+        self.vel[slot] = 0.0 if ine is None else np.asarray(ine[1], dtype=np.float64)
         self.u[slot], self.v[slot] = u, v
         self.d[slot] = np.where(np.isfinite(disp) & (disp > 0), disp, np.nan)
         valid = np.isfinite(u)
@@ -261,6 +371,45 @@ class KeyframeWindow:
             b[rc:rc + 3] -= w * (Q @ e)
             b[rp:rp + 3] += w * e
 
+    def set_inertial(self, gw: np.ndarray, ba0: np.ndarray, wb: float) -> None:
+        """World gravity and the accelerometer-bias prior (value, weight) for the next solves."""
+        self.ine_cfg = (np.asarray(gw, dtype=np.float64).copy(), np.asarray(ba0, dtype=np.float64).copy(), float(wb))
+
+    def inertial_terms(self, slots: list[int], Rs: np.ndarray, ts: np.ndarray, S: np.ndarray,
+                       b: np.ndarray) -> tuple | None:
+        """The inertial factors into S and b (camera-camera parts, in place) and the velocity /
+        bias system (Hxy 6n x (3n+3), Hyy with lam I and the bias prior, b_y); None without
+        factors."""
+        n = len(slots)
+        fs = [c for c in range(1, n) if self.ine[slots[c]][28] > 0.0]
+        if not fs:
+            return None
+        gw, ba0, wb = self.ine_cfg
+        my = 3 * n + 3
+        Hxy = np.zeros((6 * n, my))
+        Hyy = np.zeros((my, my))
+        by = np.zeros(my)
+        for c in fs:
+            f = self.ine[slots[c]]
+            i, j = c - 1, c
+            vi, vj = self.vel[slots[i]], self.vel[slots[j]]
+            r = inertial_residual(f, Rs[i], ts[i], Rs[j], ts[j], vi, vj, self.ba, gw)
+            J = inertial_jacobian(f, Rs[i], ts[i], Rs[j], ts[j], vi, vj, gw)
+            Wd = np.array([f[28]] * 3 + [f[29]] * 3)
+            xc = list(range(6 * i, 6 * i + 6)) + list(range(6 * j, 6 * j + 6))
+            yc = list(range(3 * i, 3 * i + 3)) + list(range(3 * j, 3 * j + 3)) + list(range(3 * n, 3 * n + 3))
+            Jx, Jy = J[:, :12], J[:, 12:]
+            WJx, WJy = Wd[:, None] * Jx, Wd[:, None] * Jy
+            S[np.ix_(xc, xc)] += Jx.T @ WJx
+            b[xc] -= Jx.T @ (Wd * r)
+            Hxy[np.ix_(xc, yc)] += Jx.T @ WJy
+            Hyy[np.ix_(yc, yc)] += Jy.T @ WJy
+            by[yc] -= Jy.T @ (Wd * r)
+        Hyy[3 * n:, 3 * n:] += wb * np.eye(3)
+        by[3 * n:] -= wb * (self.ba - ba0)
+        Hyy += self.p.lam * np.eye(my)
+        return Hxy, Hyy, by
+
     def solve(self) -> dict:
         p = self.p
         slots = self.order()
@@ -273,9 +422,21 @@ class KeyframeWindow:
         for _ in range(p.iters):
             lin = self.linearize(ob, Rs, ts)
             self.imu_terms(slots, Rs, lin["S"], lin["b"])
+            ine = self.inertial_terms(slots, Rs, ts, lin["S"], lin["b"])
             S = lin["S"] + p.lam * np.eye(6 * n)
             dc = np.zeros(6 * n)
-            dc[6:] = np.linalg.solve(S[6:, 6:], lin["b"][6:])
+            if ine is None:
+                dc[6:] = np.linalg.solve(S[6:, 6:], lin["b"][6:])
+            else:
+                Hxy, Hyy, by = ine
+                Hx = Hxy[6:]
+                Z = np.linalg.solve(Hyy, Hx.T)          # Hyy^-1 Hyx
+                zb = np.linalg.solve(Hyy, by)
+                dc[6:] = np.linalg.solve(S[6:, 6:] - Hx @ Z, lin["b"][6:] - Hx @ zb)
+                dy = zb - Z @ dc[6:]
+                for c in range(n):
+                    self.vel[slots[c]] = self.vel[slots[c]] + dy[3 * c:3 * c + 3]
+                self.ba = self.ba + dy[3 * n:]
             dcc = dc.reshape(n, 6)
             dp = self.landmark_update(ob, lin, dcc)
             for c in range(1, n):
@@ -427,8 +588,9 @@ class BATracker:
         self.temporal: list[np.ndarray] = []   # newest first, the last kf_interval frames
         self.last_solve: dict | None = None
 
-    def step(self, res: dict, imu: tuple | None = None) -> dict | None:
-        """One frame's tracker result; ``imu`` = (M, w), the keyframe's IMU rotation factor."""
+    def step(self, res: dict, imu: tuple | None = None, ine: tuple | None = None) -> dict | None:
+        """One frame's tracker result; ``imu`` = (M, w), the keyframe's IMU rotation factor;
+        ``ine`` = (record, v0), its inertial factor and initial velocity."""
         g = int(res["frame"])
         cur = res["cur"]
         self.temporal.insert(0, np.asarray(cur["temporal"], dtype=np.int64))
@@ -445,7 +607,8 @@ class BATracker:
             T_wc = _inv_rigid(w.T_cw[prev]) @ _inv_rigid(self.Tfe[prev]) @ W_fe
             link = chain_links(self.temporal[: self.p.kf_interval])
         u, v = keyframe_observations(cur["left"], self.K)
-        slot = w.add_keyframe(g, _inv_rigid(T_wc), u, v, np.asarray(cur["disp"], dtype=np.float64), link, imu=imu)
+        slot = w.add_keyframe(g, _inv_rigid(T_wc), u, v, np.asarray(cur["disp"], dtype=np.float64), link, imu=imu,
+                              ine=ine)
         self.Tfe[slot] = W_fe
         self.last_solve = w.solve()
         return self.last_solve
