@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 16
+#define TSLAM_ABI_VERSION 17
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -339,6 +339,17 @@ int tslam_imu_absorb(tslam_imu* f, int n, const double* dt, const double* gyro, 
                      const int32_t* status, const double* t_rel, const double* cov);
 int tslam_imu_vision_only(const double* T, const double* cov, double sigma2, const tslam_imu_step* s, double* T_out,
                           double* cov_out);
+/* The filter's world gravity (zero before tslam_imu_begin / for the gyro-only filter). */
+int tslam_imu_gravity(const tslam_imu* f, double* gravity);
+/* The inertial factor record of tslam_ba_inertial_factor (record[32], layout there) from the n
+ * frame intervals between two keyframes: dt[n], gyro[n][3], accel[n][3] (IMU axes), the filter's
+ * biases bg[3], ba[3] (ba becomes ba_lin), w_prev[3] = the camera-axes rate of the interval before
+ * the first (NULL: none), and the weights' floors (m/s, m):
+ * wv = 1 / (n_a^2 T + v_floor^2), wp = 1 / (n_a^2 T^3 / 3 + p_floor^2).  Spec:
+ * oracle/numpy_ba.py preintegrate. */
+int tslam_imu_preintegrate(const tslam_imu* f, int n, const double* dt, const double* gyro, const double* accel,
+                           const double* bg, const double* ba, const double* w_prev, double v_floor, double p_floor,
+                           double* record);
 
 /* Rig pose (replaces the multi-camera fusion cuVSLAM does for the rig of
  * isaac_ros.py:364-411): base_T_rect[P][16] = the rectified-left frame of each pair in the rig's
@@ -514,6 +525,21 @@ int tslam_group_destroy(tslam_group* g);
  * residual vee((M^T R_c R_{c-1}^T - ...) / 2) between window-consecutive keyframes (spec:
  * oracle/numpy_ba.py imu_terms).  Pair windows only (a rig's body window ignores it). */
 int tslam_ba_imu_factor(tslam_handle* h, int pair, int64_t frame, const double* M, double weight);
+/* Tightly coupled inertial factors (spec: oracle/numpy_ba.py inertial_terms; pair windows only).
+ * tslam_ba_inertial: world gravity [3] (the tracking world: pair 0's rectified-left camera at frame
+ *   0), the accelerometer-bias prior [3] (IMU axes) and its weight (1 / (m/s^2)^2) for the next
+ *   solves of `pair`'s window.
+ * tslam_ba_inertial_factor: keyframe `frame`'s accelerometer preintegration from the previous
+ *   keyframe (before the batch holding it is submitted): record[30] = dv[3], dp[3] (previous
+ *   keyframe's camera axes), Jv[9], Jp[9] (row-major, d/d ba), ba_lin[3], dt, wv (1 / (m/s)^2),
+ *   wp (1 / m^2), and v0[3], the keyframe camera's initial world velocity.  The window then
+ *   carries a velocity per keyframe and one accelerometer bias; every Gauss-Newton step eliminates
+ *   them into the reduced camera system (k_ba_reduce_solve_ine) and updates them after the camera
+ *   solve.  A window with no factor between two of its keyframes solves as before.
+ * tslam_ba_read_inertial (synchronises): velocity[W][3] by slot, ba[3]. */
+int tslam_ba_inertial(tslam_handle* h, int pair, const double* gravity, const double* ba_prior, double ba_weight);
+int tslam_ba_inertial_factor(tslam_handle* h, int pair, int64_t frame, const double* record, const double* v0);
+int tslam_ba_read_inertial(tslam_handle* h, int pair, double* velocity, double* ba);
 int tslam_ba_read(tslam_handle* h, int pair, int64_t* frames, double* cam_T_world, int32_t* landmark,
                   double* points, double* obs_uvd, int32_t* counts);
 

@@ -41,19 +41,55 @@ def _imu_factors(sc, n: int, angle: float = 3e-3, weight: float = 1e5) -> dict:
     return out
 
 
-def _oracle_windows(sc, imu: dict | None = None):
+INE_CFG = (np.array([0.4, 9.7, 1.2]), np.array([0.01, 0.0, -0.01]), 10.0)   # gravity, bias prior, weight
+
+
+def _inertial_factors(sc, n: int) -> dict:
+    """Per keyframe g > 0: an inertial factor whose residual vanishes at the oracle front end's
+    cameras, central-difference velocities and a bias of (0.02, -0.01, 0.03) (the BA's visual
+    window disagrees slightly, so the factors pull), with the initial velocity off by 0.05 m/s."""
+    from oracle.numpy_ba import INE_N
+
+    rng = np.random.default_rng(7)
+    iv = sc["cfg"].ba_kf_interval
+    dt = iv / 30.0
+    gw = INE_CFG[0]
+    ba_true = np.array([0.02, -0.01, 0.03])
+    Tcw = [np.linalg.inv(r["world_T_cam"]) for r in sc["oracle"]]
+    pos = [r["world_T_cam"][:3, 3] for r in sc["oracle"]]
+    vel = {g: (pos[min(g + 1, n - 1)] - pos[max(g - 1, 0)]) / (dt / iv * (min(g + 1, n - 1) - max(g - 1, 0)))
+           for g in range(0, n, iv)}
+    out = {}
+    for g in range(iv, n, iv):
+        Ti, Tj = Tcw[g - iv], Tcw[g]
+        vi, vj = vel[g - iv], vel[g]
+        pi, pj = pos[g - iv], pos[g]
+        Jv, Jp = rng.normal(0, 0.2, (3, 3)) * dt, rng.normal(0, 0.02, (3, 3)) * dt
+        f = np.zeros(INE_N)
+        f[0:3] = Ti[:3, :3] @ (vj - vi - gw * dt) - Jv @ ba_true
+        f[3:6] = Ti[:3, :3] @ (pj - pi - vi * dt - 0.5 * gw * dt * dt) - Jp @ ba_true
+        f[6:15], f[15:24] = Jv.reshape(9), Jp.reshape(9)
+        f[27], f[28], f[29] = dt, 1e3, 1e5
+        out[g] = (f, vj + rng.normal(0, 0.05, 3))
+    return out
+
+
+def _oracle_windows(sc, imu: dict | None = None, ine: dict | None = None):
     from oracle.numpy_ba import BAParams, BATracker
 
     cfg, rect = sc["cfg"], sc["rect"]
     bp = BAParams(window=cfg.ba_window, kf_interval=cfg.ba_kf_interval, iters=cfg.ba_iters, lam=cfg.ba_lambda,
                   outlier_px=cfg.ba_outlier_px)
     trk = BATracker(cfg.n_features, (rect.fx, rect.fy, rect.cx, rect.cy, rect.fx * rect.baseline), bp)
+    if ine is not None:
+        trk.win.set_inertial(*INE_CFG)
     snaps = []
     for g, res in enumerate(sc["oracle"]):
-        trk.step(res, imu=None if imu is None else imu.get(g))
+        trk.step(res, imu=None if imu is None else imu.get(g), ine=None if ine is None else ine.get(g))
         w = trk.win
         snaps.append({"frames": w.frame.copy(), "T_cw": w.T_cw.copy(), "lm": w.lm.copy(), "X": w.X.copy(),
-                      "u": w.u.copy(), "v": w.v.copy(), "d": w.d.copy(), "solve": trk.last_solve})
+                      "u": w.u.copy(), "v": w.v.copy(), "d": w.d.copy(), "solve": trk.last_solve,
+                      "vel": w.vel.copy(), "ba": w.ba.copy()})
     return snaps
 
 
@@ -157,6 +193,57 @@ def test_ba_imu_rotation_factors_parity():
     occ = want[-1]["frames"] >= 0
     moved = max(rel_frobenius(want[-1]["T_cw"][s_], plain[-1]["T_cw"][s_]) for s_ in np.nonzero(occ)[0])
     assert moved > 1e-6, moved
+
+
+def test_ba_inertial_factors_parity():
+    """Tightly coupled inertial factors (tslam_ba_inertial / _inertial_factor: velocities per
+    keyframe and the window's accelerometer bias eliminated into the camera system,
+    k_ba_reduce_solve_ine) against the oracle's inertial_terms: windows, velocities and bias to
+    1e-9 through evictions, in batches of 3, with the IMU rotation factors on too; the factors
+    move the solution; the split (kernel-boundary) solve agrees bit for bit."""
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    n, batch = 12, 3
+    sc, plain = _scenario_and_oracle(n)
+    imu = _imu_factors(sc, n)
+    ine = _inertial_factors(sc, n)
+    want = _oracle_windows(sc, imu, ine)
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    runs = []
+    for split in (False, True):
+        h = Handle([sc["rect"]], sc["cfg"], max_batch=batch)
+        try:
+            h.ba_split_solve(split)
+            h.ba_inertial(*INE_CFG)
+            for g, (M, w) in imu.items():
+                h.ba_imu_factor(g, M, w)
+            for g, (f, v0) in ine.items():
+                h.ba_inertial_factor(g, f, v0)
+            snaps = []
+            for b0 in range(0, n, batch):
+                h.submit(dev[b0:].data_ptr(), batch, torch.cuda.current_stream().cuda_stream)
+                got = h.ba_read(0)
+                want_k = want[b0 + batch - 1]
+                _compare(got, want_k, f"inertial, after frame {b0 + batch - 1}")
+                gi = h.ba_read_inertial(0)
+                occ = want_k["frames"] >= 0
+                err_v = np.abs(gi["vel"][occ] - want_k["vel"][occ]).max() / np.abs(want_k["vel"][occ]).max()
+                assert err_v < 1e-9, (b0, err_v)
+                assert np.abs(gi["ba"] - want_k["ba"]).max() < 1e-9 * max(np.abs(want_k["ba"]).max(), 1e-3), (b0, gi["ba"])
+                snaps.append((got, gi))
+            runs.append(snaps)
+        finally:
+            h.close()
+    for (a, ai), (b, bi) in zip(*runs):
+        np.testing.assert_array_equal(a["T_cw"], b["T_cw"])
+        np.testing.assert_array_equal(ai["vel"], bi["vel"])
+        np.testing.assert_array_equal(ai["ba"], bi["ba"])
+    occ = want[-1]["frames"] >= 0
+    moved = max(rel_frobenius(want[-1]["T_cw"][s_], plain[-1]["T_cw"][s_]) for s_ in np.nonzero(occ)[0])
+    assert moved > 1e-7, moved
+    assert np.abs(want[-1]["ba"]).max() > 1e-4   # the bias moved off zero
 
 
 def test_ba_imu_factor_rejects_non_finite():

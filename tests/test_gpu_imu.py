@@ -331,3 +331,61 @@ def test_engine_ba_imu_rotation_factors():
     _, err_off = run(False)
     assert len(err_on) == len(err_off) == 8
     assert max(err_on) < max(err_off) + 5e-4, (err_on, err_off)
+
+
+def test_engine_ba_inertial_factors():
+    """IMU fusion (accelerometer leg) with local BA on one stereo pair: each keyframe interval's
+    samples are preintegrated on the host (tslam_imu_preintegrate) and enter the window as
+    tightly coupled inertial factors (tslam_ba_inertial_factor) — one per keyframe after the
+    first; the window's velocities follow the camera's true velocity and the keyframe positions
+    stay on the ground truth (no worse than without the factors by more than 5 mm)."""
+    from thor_slam_amd.camera import CameraRig, Extrinsics
+    from thor_slam_amd.camera.types import IMUExtrinsics
+    from thor_slam_amd.params import HipSlamConfig
+    from thor_slam_amd.slam.hip_engine import HipSlamEngine
+    from thor_slam_amd.synthetic import DRB_TO_RDF, SyntheticStereoSource
+
+    def run(inertial: bool):
+        src = SyntheticStereoSource(seed=0, imu=True)
+        rig_T = src.rig_T_source
+        rig = CameraRig([src], rig_extrinsics={src.name: Extrinsics.from_4x4_matrix(rig_T)}, imu_source=src.name,
+                        imu_extrinsics=IMUExtrinsics(src.name, Extrinsics.from_4x4_matrix(rig_T @ DRB_TO_RDF)))
+        rig.start()
+        eng = HipSlamEngine(num_cameras=2, config=HipSlamConfig(batch_size=4, ba_window=4, ba_kf_interval=2, ba_iters=3,
+                                                                enable_loop_closure=False, ba_inertial=inertial))
+        eng.initialize(rig.calibration)
+        calls = []
+        inner = eng._handle.ba_inertial_factor
+        eng._handle.ba_inertial_factor = lambda g, rec, v0, pair=0: (calls.append(g), inner(g, rec, v0, pair))
+        for _ in range(16):
+            eng.process_frames(rig.get_synchronized_frames())
+        eng.flush()
+        smap = eng.get_map()
+        ine = eng._handle.ba_read_inertial(0)
+        frames = eng._handle.ba_read(0)["frames"]
+        rects = eng._rects
+        eng.shutdown()
+        gt0 = src.ground_truth_body(0)
+        pos_err = []
+        for kf in smap.keyframe_poses:
+            k = min(range(16), key=lambda i: abs(src.timestamp(i) - kf.timestamp))
+            gt = np.linalg.inv(gt0) @ src.ground_truth_body(k)
+            pos_err.append(np.linalg.norm(kf.to_4x4_matrix()[:3, 3] - gt[:3, 3]))
+        return calls, pos_err, ine, frames, src
+
+    calls, err_on, ine, frames, src = run(True)
+    assert calls == [2, 4, 6, 8, 10, 12, 14], calls
+    assert np.isfinite(ine["vel"]).all() and np.isfinite(ine["ba"]).all()
+    # the camera's true speed at the window's keyframes (central differences of the left camera)
+    c0 = src.camera_pose(0, 0)
+    dt = 1.0 / src.fps
+    for s, g in enumerate(frames):
+        if g <= 0:
+            continue
+        p = [(np.linalg.inv(c0) @ src.camera_pose(int(g) + d, 0))[:3, 3] for d in (-1, 1)]
+        v_true = (p[1] - p[0]) / (2 * dt)
+        assert abs(np.linalg.norm(ine["vel"][s]) - np.linalg.norm(v_true)) < 0.05, (g, ine["vel"][s], v_true)
+    calls_off, err_off, _, _, _ = run(False)
+    assert calls_off == []
+    assert len(err_on) == len(err_off) == 8
+    assert max(err_on) < max(err_off) + 5e-3, (err_on, err_off)

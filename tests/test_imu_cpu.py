@@ -165,3 +165,24 @@ def test_vision_only_matches_oracle():
     big = type(s)(s.dt, s.gyro, s.w, s.R_rel, s.t_rel, 1e12, 1e12, s.v1, s.var_v1)
     got_T, got_C = vision_only(T, cov, 1.0, big)
     np.testing.assert_array_equal(got_T, T)
+
+
+def test_preintegration_matches_oracle():
+    """tslam_imu_preintegrate (the product's inertial factor record) against the spec
+    oracle/numpy_ba.py preintegrate on the synthetic IMU, with biases and w_prev, to 1e-12."""
+    from oracle.numpy_ba import preintegrate
+
+    src = SyntheticStereoSource(seed=0, imu=True, n_frames=60, gyro_bias=np.array([0.01, -0.02, 0.005]))
+    ri = _rect_R_imu(src)
+    noise = ImuNoise()
+    prod = ImuPropagator(ri, noise, lever=LEVER)
+    dt = 1.0 / src.fps
+    bg, ba = np.array([0.004, -0.01, 0.002]), np.array([0.03, 0.01, -0.02])
+    for i0, wp in ((5, None), (12, np.array([0.1, -0.2, 0.05]))):
+        smp = [(dt, src.imu_sample(k)["gyroscope"], src.imu_sample(k)["accelerometer"]) for k in range(i0 + 1, i0 + 6)]
+        got = prod.preintegrate(smp, bg, ba, wp)
+        want = preintegrate(smp, ri, bg, ba, LEVER, w_prev=wp, acc_density=noise.acc_density)
+        np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-14)
+    prod.begin(src.imu_sample(0)["accelerometer"])
+    g = prod.gravity()
+    assert abs(np.linalg.norm(g) - 9.81) < 1e-12

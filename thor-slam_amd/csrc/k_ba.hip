@@ -131,6 +131,8 @@ __global__ __launch_bounds__(256) void k_ba_insert(BatchCtx c, BaArgs a) {
             }
     }
     if (blockIdx.x == 0 && threadIdx.x < 10) q.imu[(size_t)a.slot * 10 + threadIdx.x] = a.imu[threadIdx.x];
+    if (blockIdx.x == 0 && threadIdx.x < TS_BA_INE) q.ine[(size_t)a.slot * TS_BA_INE + threadIdx.x] = a.ine[threadIdx.x];
+    if (blockIdx.x == 0 && threadIdx.x < 3) q.vel[(size_t)a.slot * 3 + threadIdx.x] = a.vel0[threadIdx.x];
     __syncthreads();
     const PairCalib cal = c.calib[p];
     const double* disp = c.disp + ((size_t)rslot * c.P + p) * K;
@@ -776,10 +778,241 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce(BatchCtx c, B
 //     panel wave left them).
 // Camera updates R <- cayley(w) R, t <- ... + rho follow.
 #define BA_SP 65   // LDS row pitch of S (doubles)
+// ---------------------------------------------------------------------------------------------
+// Inertial factors (oracle/numpy_ba.py inertial_terms): per window-consecutive pair (c - 1, c)
+// whose later keyframe carries a factor, the velocity and position residuals of the accelerometer
+// preintegration against the cameras, the two velocities and the window's accelerometer bias.
+// The velocity / bias unknowns y (3n + 3) are eliminated into the camera system in LDS:
+//   phase 0: factor t (= c - 1) on thread t: r (6), J (6 x 21: rho_i, omega_i, rho_j, omega_j,
+//            v_i, v_j, ba), weights;
+//   phase 1: per factor (in order, a barrier each), thread (a, b) of J^T W J scatters into S
+//            (lower triangle), Hxy or Hyy and 21 threads the gradient into b_x or b_y; then the
+//            bias prior and lam I on Hyy;
+//   phase 2: wave 0 factors Hyy = L L^T (lane = row);
+//   phase 3: thread i < m: Z_i = L^-1 Hxy_i (in place); thread m: zb = L^-1 b_y;
+//   phase 4: S -= Z Z^T (lower), b_x -= Z zb;
+//   after the camera solve (ba_inertial_update): dy = L^-T (zb - Z^T dc), v_c += dv_c, ba += dba.
+// ---------------------------------------------------------------------------------------------
+struct BaIneLds {
+    double J[TS_BA_MAXW - 1][6][21];
+    double r[TS_BA_MAXW - 1][6];
+    double w[TS_BA_MAXW - 1][2];
+    double Y[TS_BA_MAXY][TS_BA_MAXY + 1];   // Hyy, then its Cholesky factor (lower)
+    double X[TS_BA_MAXD][TS_BA_MAXY + 1];   // row i: Hxy_i, then Z_i = (L^-1 Hyx)^T_i
+    double by[TS_BA_MAXY];                  // b_y, then zb = L^-1 b_y, then zb - Z^T dc
+    double ld[TS_BA_MAXY];                  // 1 / L_yy
+    int any, good;
+};
+template <bool INE>
+__device__ __forceinline__ BaIneLds* ine_lds() {
+    return nullptr;
+}
+template <>
+__device__ __forceinline__ BaIneLds* ine_lds<true>() {
+    __shared__ BaIneLds s;
+    return &s;
+}
+
+// global unknown of factor t's column col: x index (camera rows without the gauge, -1 = camera 0)
+// for col < 12, else y index
+__device__ __forceinline__ int ine_col(int t, int col, int n) {
+    const int c = t + 1;
+    if (col < 6) return c - 1 >= 1 ? 6 * (c - 2) + col : -1;
+    if (col < 12) return 6 * (c - 1) + col - 6;
+    if (col < 15) return 3 * (c - 1) + col - 12;
+    if (col < 18) return 3 * c + col - 15;
+    return 3 * n + col - 18;
+}
+
+// phases 0-4; returns whether any factor acts (block-uniform)
+__device__ bool ba_inertial_reduce(const BaPair& q, const BaArgs& a, int n, int m, double* s_S, double* s_x, BaIneLds* L) {
+#pragma clang fp contract(fast)
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const int nf = n - 1, my = 3 * n + 3;
+    if (tid < nf) {   // phase 0
+        const int t = tid, c = t + 1;
+        const double* f = q.ine + (size_t)a.order[c] * TS_BA_INE;
+        const double wv = f[28], wp = f[29];
+        double (*J)[21] = L->J[t];
+        for (int r = 0; r < 6; ++r) {
+            L->r[t][r] = 0.0;
+            for (int k = 0; k < 21; ++k) J[r][k] = 0.0;
+        }
+        L->w[t][0] = wv > 0.0 ? wv : 0.0;
+        L->w[t][1] = wv > 0.0 ? wp : 0.0;
+        if (wv > 0.0) {
+            const double* Ti = q.T + (size_t)a.order[c - 1] * 16;
+            const double* Tj = q.T + (size_t)a.order[c] * 16;
+            const double* vi = q.vel + (size_t)a.order[c - 1] * 3;
+            const double* vj = q.vel + (size_t)a.order[c] * 3;
+            const double dt = f[27];
+            double pi[3], pj[3], uv[3], up[3], dba[3];
+            for (int k = 0; k < 3; ++k) {
+                pi[k] = -((Ti[k] * Ti[3] + Ti[4 + k] * Ti[7]) + Ti[8 + k] * Ti[11]);
+                pj[k] = -((Tj[k] * Tj[3] + Tj[4 + k] * Tj[7]) + Tj[8 + k] * Tj[11]);
+                dba[k] = q.ine_ba[k] - f[24 + k];
+            }
+            for (int k = 0; k < 3; ++k) {
+                const double g = a.icfg[k];
+                uv[k] = ((vj[k] - vi[k]) - g * dt);
+                up[k] = (((pj[k] - pi[k]) - vi[k] * dt) - 0.5 * g * dt * dt);
+            }
+            double ruv[3], rup[3];
+            for (int r = 0; r < 3; ++r) {
+                ruv[r] = (Ti[4 * r] * uv[0] + Ti[4 * r + 1] * uv[1]) + Ti[4 * r + 2] * uv[2];
+                rup[r] = (Ti[4 * r] * up[0] + Ti[4 * r + 1] * up[1]) + Ti[4 * r + 2] * up[2];
+            }
+            for (int r = 0; r < 3; ++r) {
+                const double jv = (f[6 + 3 * r] * dba[0] + f[7 + 3 * r] * dba[1]) + f[8 + 3 * r] * dba[2];
+                const double jp = (f[15 + 3 * r] * dba[0] + f[16 + 3 * r] * dba[1]) + f[17 + 3 * r] * dba[2];
+                L->r[t][r] = ruv[r] - (f[r] + jv);
+                L->r[t][3 + r] = rup[r] - (f[3 + r] + jp);
+            }
+            // -[a]x rows: (0, a2, -a1), (-a2, 0, a0), (a1, -a0, 0)
+            const double sv[3][3] = {{0.0, ruv[2], -ruv[1]}, {-ruv[2], 0.0, ruv[0]}, {ruv[1], -ruv[0], 0.0}};
+            const double sp[3][3] = {{0.0, rup[2], -rup[1]}, {-rup[2], 0.0, rup[0]}, {rup[1], -rup[0], 0.0}};
+            for (int r = 0; r < 3; ++r)
+                for (int k = 0; k < 3; ++k) {
+                    const double Rrk = Ti[4 * r + k];
+                    J[r][3 + k] = sv[r][k];
+                    J[r][12 + k] = -Rrk;
+                    J[r][15 + k] = Rrk;
+                    J[r][18 + k] = -f[6 + 3 * r + k];
+                    J[3 + r][k] = r == k ? 1.0 : 0.0;
+                    J[3 + r][3 + k] = sp[r][k];
+                    // -R_cw,i R_cw,j^T
+                    J[3 + r][6 + k] = -((Ti[4 * r] * Tj[4 * k] + Ti[4 * r + 1] * Tj[4 * k + 1]) + Ti[4 * r + 2] * Tj[4 * k + 2]);
+                    J[3 + r][12 + k] = -Rrk * dt;
+                    J[3 + r][18 + k] = -f[15 + 3 * r + k];
+                }
+        }
+    }
+    for (int e = tid; e < TS_BA_MAXY * (TS_BA_MAXY + 1); e += nthr) (&L->Y[0][0])[e] = 0.0;
+    for (int e = tid; e < TS_BA_MAXD * (TS_BA_MAXY + 1); e += nthr) (&L->X[0][0])[e] = 0.0;
+    if (tid < TS_BA_MAXY) L->by[tid] = 0.0;
+    __syncthreads();
+    if (tid == 0) {
+        int any = 0;
+        for (int t = 0; t < nf; ++t) any |= L->w[t][0] > 0.0;
+        L->any = any;
+    }
+    __syncthreads();
+    if (!L->any) return false;
+    for (int t = 0; t < nf; ++t) {   // phase 1, one factor at a time
+        if (!(L->w[t][0] > 0.0)) continue;   // (uniform)
+        const double w0 = L->w[t][0], w1 = L->w[t][1];
+        const double (*J)[21] = L->J[t];
+        for (int e = tid; e < 21 * 21 + 21; e += nthr) {
+            if (e < 441) {
+                const int ca = e / 21, cb = e - 21 * ca;
+                const int ga = ine_col(t, ca, n), gb = ine_col(t, cb, n);
+                const bool xa = ca < 12, xb = cb < 12;
+                if (ga < 0 || gb < 0) continue;        // the gauge camera's columns
+                if (xa && xb && ga < gb) continue;     // S: lower triangle
+                if (!xa && xb) continue;               // Hyx: from (b, a)
+                const double h = ((w0 * (J[0][ca] * J[0][cb]) + w0 * (J[1][ca] * J[1][cb])) + w0 * (J[2][ca] * J[2][cb])) +
+                                 ((w1 * (J[3][ca] * J[3][cb]) + w1 * (J[4][ca] * J[4][cb])) + w1 * (J[5][ca] * J[5][cb]));
+                if (xa && xb) s_S[ga * BA_SP + gb] += h;
+                else if (xa) L->X[ga][gb] += h;
+                else L->Y[ga][gb] += h;
+            } else {
+                const int ca = e - 441;
+                const int ga = ine_col(t, ca, n);
+                if (ga < 0) continue;
+                const double gsum = ((w0 * (J[0][ca] * L->r[t][0]) + w0 * (J[1][ca] * L->r[t][1])) + w0 * (J[2][ca] * L->r[t][2])) +
+                                    ((w1 * (J[3][ca] * L->r[t][3]) + w1 * (J[4][ca] * L->r[t][4])) + w1 * (J[5][ca] * L->r[t][5]));
+                if (ca < 12) s_x[ga] -= gsum;
+                else L->by[ga] -= gsum;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid < my) {   // bias prior on ba, lam on every velocity / bias unknown
+        L->Y[tid][tid] += a.lam;
+        if (tid >= 3 * n) {
+            const int k = tid - 3 * n;
+            L->Y[tid][tid] += a.icfg[6];
+            L->by[tid] -= a.icfg[6] * (q.ine_ba[k] - a.icfg[3 + k]);
+        }
+    }
+    __syncthreads();
+    if (tid < 64) {   // phase 2: wave 0, lane = row
+        const int i = tid;
+        bool good = true;
+        for (int j = 0; j < my; ++j) {
+            const double d = L->Y[j][j];
+            good = good && d > 0.0;
+            const double l = sqrt(d), inv = 1.0 / l;
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            if (i > j && i < my) L->Y[i][j] *= inv;
+            if (i == j) {
+                L->Y[j][j] = l;
+                L->ld[j] = inv;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            if (i > j && i < my) {
+                const double lij = L->Y[i][j];
+                for (int k = j + 1; k <= i; ++k) L->Y[i][k] -= lij * L->Y[k][j];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        }
+        if (i == 0) L->good = good;
+    }
+    __syncthreads();
+    if (tid <= m) {   // phase 3: forward substitutions (thread m: the right-hand side)
+        double* z = tid < m ? L->X[tid] : L->by;
+        for (int y = 0; y < my; ++y) {
+            double v = z[y];
+            for (int k = 0; k < y; ++k) v -= L->Y[y][k] * z[k];
+            z[y] = v * L->ld[y];
+        }
+    }
+    __syncthreads();
+    for (int e = tid; e < m * m + m; e += nthr) {   // phase 4
+        if (e < m * m) {
+            const int i = e / m, k = e - m * i;
+            if (k > i) continue;
+            double sum = 0.0;
+            for (int y = 0; y < my; ++y) sum += L->X[i][y] * L->X[k][y];
+            s_S[i * BA_SP + k] -= sum;
+        } else {
+            const int i = e - m * m;
+            double sum = 0.0;
+            for (int y = 0; y < my; ++y) sum += L->X[i][y] * L->by[y];
+            s_x[i] -= sum;
+        }
+    }
+    __syncthreads();
+    return true;
+}
+
+// after the camera solve (dc = s_x[0 .. m)): dy = L^-T (zb - Z^T dc); v_c += dv_c, ba += dba
+__device__ void ba_inertial_update(const BaPair& q, const BaArgs& a, int n, int m, const double* s_x, BaIneLds* L) {
+#pragma clang fp contract(fast)
+    const int tid = threadIdx.x, my = 3 * n + 3;
+    if (tid < my) {
+        double v = L->by[tid];
+        for (int i = 0; i < m; ++i) v -= L->X[i][tid] * s_x[i];
+        L->by[tid] = v;
+    }
+    __syncthreads();
+    if (tid < 64) {
+        const int y = tid;
+        double val = y < my ? L->by[y] : 0.0, x = 0.0;
+        for (int i2 = my - 1; i2 >= 0; --i2) {
+            const double xi = readlane_f64(val, i2) * L->ld[i2];
+            if (y == i2) x = xi;
+            if (y < i2) val -= L->Y[i2][y] * xi;
+        }
+        if (y < 3 * n) q.vel[(size_t)a.order[y / 3] * 3 + y % 3] += x;
+        else if (y < my) q.ine_ba[y - 3 * n] += x;
+    }
+}
+
 // `handoff`: C and the camera blocks were published by other workgroups of this launch with
 // write-through stores (k_ba_reduce_solve), so they are read with agent-scope loads that bypass
 // this CU's caches.
-template <bool handoff>
+template <bool handoff, bool INE>
 __device__ __forceinline__ void ba_solve_block(const BatchCtx& c, const BaArgs& a) {
     // the elimination's a - l * b updates as single FMAs (the library builds with contraction off
     // for the bit-exact pose kernels; this solve is only held to 1e-9 against the oracle's LU)
@@ -871,6 +1104,9 @@ __device__ __forceinline__ void ba_solve_block(const BatchCtx& c, const BaArgs& 
         }
     }
     if (any_imu) __syncthreads();
+    BaIneLds* ine = ine_lds<INE>();
+    bool ine_on = false;
+    if constexpr (INE) ine_on = ba_inertial_reduce(q, a, n, m, s_S, s_x, ine);
     const bool live = lane < m;
     double rhs = (w == 0 && live) ? s_x[lane] : 0.0;   // wave 0: right-hand side of row `lane`
     bool good = true;   // wave 0: every pivot positive
@@ -989,7 +1225,7 @@ __device__ __forceinline__ void ba_solve_block(const BatchCtx& c, const BaArgs& 
     __syncthreads();
     BST(4);
     const bool good_all = s_ok != 0;
-    const bool ok = good_all;
+    const bool ok = good_all && (!ine_on || ine->good);
     if (threadIdx.x == 0) q.counts[2] = ok;
     for (int e = threadIdx.x; e < 6 * n; e += blockDim.x) q.dc[e] = (e < 6 || !ok) ? 0.0 : s_x[e - 6];
     if (ok && (int)threadIdx.x >= 1 && (int)threadIdx.x < n) {
@@ -1015,6 +1251,8 @@ __device__ __forceinline__ void ba_solve_block(const BatchCtx& c, const BaArgs& 
             T[4 * ii + 3] = tn[ii];
         }
     }
+    if constexpr (INE)
+        if (ine_on && ok) ba_inertial_update(q, a, n, m, s_x, ine);
     BST(5);
     BST_PRINT("solve: stage C, build S, panel 0, block steps, backsub, update, -, -", threadIdx.x == 1);
 #ifdef TS_BA_STAMPS
@@ -1025,7 +1263,12 @@ __device__ __forceinline__ void ba_solve_block(const BatchCtx& c, const BaArgs& 
 
 __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, BaArgs a) {
     BA_PRIO;
-    ba_solve_block<false>(c, a);
+    ba_solve_block<false, false>(c, a);
+}
+
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve_ine(BatchCtx c, BaArgs a) {
+    BA_PRIO;
+    ba_solve_block<false, true>(c, a);
 }
 
 // k_ba_reduce and k_ba_solve in one launch (a stereo pair's own solve): the reduction's blocks
@@ -1034,8 +1277,8 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, Ba
 // solve, reading the sums with agent-scope loads.  No agent-scope release fence: on this GPU it
 // writes back the whole L2 of the XCD (the iteration's Schur partials and Jacobian blocks), which
 // cost more than the launch it saves (measured: 0.300 against 0.260 ms per keyframe).
-__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_solve(BatchCtx c, BaArgs a) {
-    BA_PRIO;
+template <bool INE>
+__device__ __forceinline__ void ba_reduce_solve_body(const BatchCtx& c, const BaArgs& a) {
     // all BA_SOLVE_WAVES waves sum (every 8th partial each), then the 8 wave sums in order
     __shared__ double s_p[BA_SOLVE_WAVES][64];
     __shared__ int s_last;
@@ -1052,7 +1295,18 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_solve(BatchCt
     __syncthreads();
     if (!s_last) return;
     if (threadIdx.x == 0) __hip_atomic_store(q.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
-    ba_solve_block<true>(c, a);
+    ba_solve_block<true, INE>(c, a);
+}
+
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_solve(BatchCtx c, BaArgs a) {
+    BA_PRIO;
+    ba_reduce_solve_body<false>(c, a);
+}
+
+// with the window's inertial factors (velocities + accelerometer bias eliminated into S)
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_solve_ine(BatchCtx c, BaArgs a) {
+    BA_PRIO;
+    ba_reduce_solve_body<true>(c, a);
 }
 
 
@@ -1177,14 +1431,15 @@ static void launch_ba_backsub(const BatchCtx& c, const BaArgs& a, hipStream_t s)
     hipLaunchKernelGGL(k_ba_backsub, dim3(16 * nb), dim3(256), 0, s, c, a);   // the last iteration's
 }
 
-void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing, bool split) {
+void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing, bool split, bool inertial) {
     launch_ba_prepare(c, a, s);
+    const dim3 grid(64 + (a.n_order * 27 + 63) / 64), block(64 * BA_SOLVE_WAVES);
     for (int it = 0; it < a.iters; ++it) {
         launch_ba_linearize(c, a, it, s, timing, split);
         if (split)   // the kernel boundary instead of the in-launch hand-off (tslam_ba_split_solve)
-            hipLaunchKernelGGL(k_ba_solve, dim3(1), dim3(64 * BA_SOLVE_WAVES), 0, s, c, a);
+            hipLaunchKernelGGL(inertial ? k_ba_solve_ine : k_ba_solve, dim3(1), block, 0, s, c, a);
         else
-            hipLaunchKernelGGL(k_ba_reduce_solve, dim3(64 + (a.n_order * 27 + 63) / 64), dim3(64 * BA_SOLVE_WAVES), 0, s, c, a);
+            hipLaunchKernelGGL(inertial ? k_ba_reduce_solve_ine : k_ba_reduce_solve, grid, block, 0, s, c, a);
     }
     launch_ba_backsub(c, a, s);
 }

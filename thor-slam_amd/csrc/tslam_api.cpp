@@ -190,6 +190,10 @@ struct tslam_handle {
     BaTiming ba_timing{};    // k_ba_schur events while profiling is on
     bool ba_split = false;   // tslam_ba_split_solve: k_ba_reduce + k_ba_solve instead of k_ba_reduce_solve
     std::map<std::pair<int, int64_t>, std::array<double, 10>> ba_imu;   // (pair, keyframe) -> IMU factor
+    // (pair, keyframe) -> inertial factor record + initial velocity (tslam_ba_inertial_factor)
+    std::map<std::pair<int, int64_t>, std::array<double, TS_BA_INE + 3>> ba_ine;
+    std::vector<std::array<double, 8>> ba_icfg;             // per pair: gravity, bias prior, its weight
+    std::vector<std::array<uint8_t, TS_BA_MAXW>> ba_ine_slot;   // per pair and slot: carries a factor
     std::vector<BaArgs> ba_solved;   // per pair: the arguments of its last window solve (replays)
     // BA on its own stream (overlapping the next batch): events and the batch parity
     int64_t batch_idx = 0;
@@ -414,6 +418,7 @@ static int alloc_ba(tslam_handle* h) {
         {(void**)&b.part, 8 * P * (size_t)TS_BA_SPLIT * TS_BA_PART}, {(void**)&b.cam_U, 8 * P * W * 27}, {(void**)&b.dc, 8 * P * W * 6},
         {(void**)&b.flops, 8},               {(void**)&b.fe_pose, 8 * 2 * (size_t)h->B * h->P * 16},
         {(void**)&b.fe_body, 8 * 2 * (size_t)h->B * 16}, {(void**)&b.imu, 8 * P * W * 10},
+        {(void**)&b.ine, 8 * P * W * TS_BA_INE}, {(void**)&b.vel, 8 * P * W * 3}, {(void**)&b.ine_ba, 8 * P * 4},
     };
     for (const A& a : list) {
         const int rc = dev_alloc(h, a.p, a.bytes);
@@ -425,6 +430,8 @@ static int alloc_ba(tslam_handle* h) {
     HIPCHK(hipMemset(b.camobs, 0xFF, 4 * P * W * WK));
     HIPCHK(hipMemset(b.remap, 0x7F, 4 * P * K));
     HIPCHK(hipDeviceSynchronize());
+    h->ba_icfg.assign(h->P, std::array<double, 8>{});
+    h->ba_ine_slot.assign(h->P, std::array<uint8_t, TS_BA_MAXW>{});
     return TSLAM_OK;
 }
 
@@ -483,11 +490,20 @@ static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const doub
             auto it = h->ba_imu.find({p, g});   // the keyframe's IMU rotation factor (if given)
             for (int e = 0; e < 10; ++e) a.imu[e] = (!rig && it != h->ba_imu.end()) ? it->second[e] : 0.0;
             if (it != h->ba_imu.end()) h->ba_imu.erase(it);
+            auto jt = h->ba_ine.find({p, g});   // and its inertial factor + initial velocity
+            const bool has = !rig && jt != h->ba_ine.end();
+            for (int e = 0; e < TS_BA_INE; ++e) a.ine[e] = has ? jt->second[e] : 0.0;
+            for (int e = 0; e < 3; ++e) a.vel0[e] = has ? jt->second[TS_BA_INE + e] : 0.0;
+            if (jt != h->ba_ine.end()) h->ba_ine.erase(jt);
+            h->ba_ine_slot[p][a.slot] = has && a.ine[28] > 0.0;
             launch_ba_keyframe(c, a, evict, s);
         }
         for (int e = 0; e < 10; ++e) a.imu[e] = 0.0;
+        for (int e = 0; e < TS_BA_INE; ++e) a.ine[e] = 0.0;
         for (auto it = h->ba_imu.begin(); it != h->ba_imu.end();)   // factors of frames already past
             it = it->first.second < g ? h->ba_imu.erase(it) : std::next(it);
+        for (auto it = h->ba_ine.begin(); it != h->ba_ine.end();)
+            it = it->first.second < g ? h->ba_ine.erase(it) : std::next(it);
         h->ba_frame[a.slot] = g;
         h->ba_nkf += 1;
         h->ba_last = g;
@@ -503,7 +519,12 @@ static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const doub
         }
         for (int p = 0; p < h->P; ++p) {
             a.pair = p;
-            launch_ba_solve(c, a, s, h->ba_timing.ev ? &h->ba_timing : nullptr, h->ba_split);
+            for (int e = 0; e < 8; ++e) a.icfg[e] = h->ba_icfg[p][e];
+            // the inertial kernels when a factor links two keyframes of the window (the oldest
+            // keyframe's factor points out of it)
+            bool ine = false;
+            for (int k = 1; k < a.n_order; ++k) ine = ine || h->ba_ine_slot[p][a.order[k]];
+            launch_ba_solve(c, a, s, h->ba_timing.ev ? &h->ba_timing : nullptr, h->ba_split, ine);
             h->ba_solved[p] = a;
         }
     }
@@ -942,6 +963,15 @@ int tslam_reset(tslam_handle* h) {
     h->ba_nkf = 0;
     h->ba_last = -1;
     h->ba_solved.clear();
+    if (h->prm.ba_window) {   // the inertial state of the window belongs to the session
+        const size_t P = h->P + 1, W = h->prm.ba_window;
+        HIPCHK(hipMemset(h->ba.ine, 0, 8 * P * W * TS_BA_INE));
+        HIPCHK(hipMemset(h->ba.vel, 0, 8 * P * W * 3));
+        HIPCHK(hipMemset(h->ba.ine_ba, 0, 8 * P * 4));
+        h->ba_ine.clear();
+        h->ba_imu.clear();
+        for (auto& f : h->ba_ine_slot) f.fill(0);
+    }
     if (h->tsdf_on) {   // so does the dense map
         const size_t nv = (size_t)h->tsdf.nx * h->tsdf.ny * h->tsdf.nz;
         HIPCHK(hipMemset(h->tsdf.tsdf, 0, sizeof(float) * nv));
@@ -2655,6 +2685,50 @@ int tslam_ba_imu_factor(tslam_handle* h, int pair, int64_t frame, const double* 
     for (int e = 0; e < 9; ++e) f[e] = M[e];
     f[9] = weight;
     h->ba_imu[{pair, frame}] = f;
+    return TSLAM_OK;
+}
+
+int tslam_ba_inertial(tslam_handle* h, int pair, const double* gravity, const double* ba_prior, double ba_weight) {
+    if (!h || !gravity || !ba_prior || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad argument");
+    if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
+    if (!(ba_weight >= 0.0) || !std::isfinite(ba_weight)) return fail(TSLAM_EINVAL, "ba_weight must be finite and >= 0");
+    for (int e = 0; e < 3; ++e)
+        if (!std::isfinite(gravity[e]) || !std::isfinite(ba_prior[e])) return fail(TSLAM_EINVAL, "non-finite input");
+    auto& f = h->ba_icfg[pair];
+    for (int e = 0; e < 3; ++e) {
+        f[e] = gravity[e];
+        f[3 + e] = ba_prior[e];
+    }
+    f[6] = ba_weight;
+    return TSLAM_OK;
+}
+
+int tslam_ba_inertial_factor(tslam_handle* h, int pair, int64_t frame, const double* record, const double* v0) {
+    if (!h || !record || !v0 || pair < 0 || pair >= h->P || frame < 0) return fail(TSLAM_EINVAL, "bad argument");
+    if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
+    if (ba_rig(h)) return fail(TSLAM_ESTATE, "inertial factors act on pair windows (not a rig's body window)");
+    std::array<double, TS_BA_INE + 3> f{};
+    for (int e = 0; e < 30; ++e) {
+        if (!std::isfinite(record[e])) return fail(TSLAM_EINVAL, "non-finite factor record");
+        f[e] = record[e];
+    }
+    if (!(f[27] > 0.0) || !(f[28] >= 0.0) || !(f[29] >= 0.0)) return fail(TSLAM_EINVAL, "dt must be > 0, weights >= 0");
+    for (int e = 0; e < 3; ++e) {
+        if (!std::isfinite(v0[e])) return fail(TSLAM_EINVAL, "non-finite velocity");
+        f[TS_BA_INE + e] = v0[e];
+    }
+    h->ba_ine[{pair, frame}] = f;
+    return TSLAM_OK;
+}
+
+int tslam_ba_read_inertial(tslam_handle* h, int pair, double* velocity, double* ba) {
+    if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
+    if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
+    int rc = tslam_sync(h);
+    if (rc != TSLAM_OK) return rc;
+    const size_t W = h->prm.ba_window;
+    if (velocity) HIPCHK(hipMemcpy(velocity, h->ba.vel + pair * W * 3, 8 * W * 3, hipMemcpyDeviceToHost));
+    if (ba) HIPCHK(hipMemcpy(ba, h->ba.ine_ba + 4 * pair, 8 * 3, hipMemcpyDeviceToHost));
     return TSLAM_OK;
 }
 

@@ -20,6 +20,10 @@
 #include "tslam_common.h"
 
 #define TS_BA_MAXD 54   // 6 * (TS_BA_MAXW - 1): the reduced camera system without the gauge
+// inertial factor record per slot (oracle/numpy_ba.py INE_N): dv 0-2, dp 3-5, Jv 6-14, Jp 15-23
+// (row-major), ba_lin 24-26, dt 27, wv 28, wp 29 (0 = no factor)
+#define TS_BA_INE 32
+#define TS_BA_MAXY (3 * TS_BA_MAXW + 3)   // velocity + bias unknowns of a window: v_0 .. v_{n-1}, ba
 #define TS_BA_SPLIT 256 // blocks of the Schur product (32-landmark chunks dealt over them; 8192 landmarks in one round)
 #define TS_BA_TILES 128 // scan tiles of a solve's compaction (landmark + observation tiles)
 #define TS_BA_PART (4096 + 288) // doubles per Schur block partial: C [64][64], then the camera blocks [MAXW][27]
@@ -71,6 +75,9 @@ struct BaStore {
     double* fe_pose;   // [2][B][P][16] front-end world_T_cam of the batch (snapshot per batch parity)
     double* fe_body;   // [2][B][16] rig front end's world_T_body of the batch (rig-level A8)
     double* imu;       // [P][W][10] IMU rotation factor per slot: M (row-major 9), weight (0 = none)
+    double* ine;       // [P][W][TS_BA_INE] inertial factor per slot (from the previous keyframe)
+    double* vel;       // [P][W][3] world velocity of each slot's camera
+    double* ine_ba;    // [P][4] the window's accelerometer bias (IMU axes)
 };
 
 struct BaArgs {
@@ -90,6 +97,9 @@ struct BaArgs {
     const double* fe;           // insert: this batch's front-end pose snapshot [B][P][16]
     const double* fe_body;      // rig insert: the rig front end's snapshot [B][16]
     double imu[10];             // insert: the keyframe's IMU rotation factor (M 9, weight; 0 = none)
+    double ine[TS_BA_INE];      // insert: the keyframe's inertial factor (wv = 0: none)
+    double vel0[3];             // insert: its camera's initial world velocity
+    double icfg[8];             // solve: world gravity 0-2, accelerometer-bias prior 3-5, its weight 6
 };
 
 // Per-pair view (the scratch pointers are shared).
@@ -107,6 +117,7 @@ struct BaPair {
     uint8_t* keep;
     double *lo_uvd, *lo_W, *Xc, *obs_Vg, *lm_L, *lm_gp, *part, *C, *cam_U, *dc, *flops;
     double* imu;
+    double *ine, *vel, *ine_ba;
 };
 
 __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, int p) {
@@ -136,6 +147,9 @@ __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, in
     q.part = s.part + p * (size_t)TS_BA_SPLIT * TS_BA_PART; q.C = s.C + p * 4096;
     q.cam_U = s.cam_U + p * W * 27; q.dc = s.dc + p * W * 6; q.flops = s.flops;
     q.imu = s.imu + p * W * 10;
+    q.ine = s.ine + p * W * TS_BA_INE;
+    q.vel = s.vel + p * W * 3;
+    q.ine_ba = s.ine_ba + 4 * p;
     return q;
 }
 
@@ -146,8 +160,10 @@ struct BaTiming {
     hipEvent_t* ev;   // 2 * cap events
     int cap, used;
 };
-// split: k_ba_reduce + k_ba_solve per iteration instead of k_ba_reduce_solve (same sums, bit for bit)
-void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing, bool split = false);
+// split: k_ba_reduce + k_ba_solve per iteration instead of k_ba_reduce_solve (same sums, bit for bit);
+// inertial: the solve kernels with the window's inertial factors (velocities + accelerometer bias)
+void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing, bool split = false,
+                     bool inertial = false);
 // rig-level A8: the body snapshot of the batch, a keyframe's body pose (and every pair's camera at
 // E_p^-1 B), and the joint solve over all pairs (storage pair c.P = the body window)
 void launch_ba_snapshot_rig(const BatchCtx& c, double* dst, hipStream_t s);

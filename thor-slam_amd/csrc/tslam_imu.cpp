@@ -423,4 +423,59 @@ int tslam_imu_vision_only(const double* T, const double* cov, double sigma2, con
     return TSLAM_OK;
 }
 
+int tslam_imu_gravity(const tslam_imu* f, double* g) {
+    if (!f || !g) return tslam_internal_fail(TSLAM_EINVAL, "null argument");
+    std::memcpy(g, f->g, sizeof f->g);
+    return TSLAM_OK;
+}
+
+// Accelerometer preintegration between two keyframes (spec: oracle/numpy_ba.py preintegrate), in
+// the first keyframe's camera axes, with the filter's Ri and lever arm: per interval k the rate
+// w = Ri (gyro - bg), alpha = (w - w_prev) / dt, the camera's specific force
+// a = Ri (accel - ba) - w x (w x r) - alpha x r; dp += dv dt + dR a dt^2 / 2,
+// Jp += Jv dt - dR Ri dt^2 / 2, dv += dR a dt, Jv -= dR Ri dt, dR <- dR exp([w dt]x).
+int tslam_imu_preintegrate(const tslam_imu* f, int n, const double* dt, const double* gyro, const double* accel,
+                           const double* bg, const double* ba, const double* w_prev, double v_floor, double p_floor,
+                           double* record) {
+    if (!f || n < 1 || !dt || !gyro || !accel || !bg || !ba || !record)
+        return tslam_internal_fail(TSLAM_EINVAL, "tslam_imu_preintegrate: null argument or n < 1");
+    double dR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, Jv[9] = {}, Jp[9] = {};
+    V3 dv{0, 0, 0}, dp{0, 0, 0};
+    double T = 0.0;
+    bool have_prev = w_prev != nullptr;
+    V3 wp = have_prev ? v3(w_prev) : V3{0, 0, 0};
+    const V3 r = v3(f->r), bgv = v3(bg), bav = v3(ba);
+    double dRRi[9];
+    for (int k = 0; k < n; ++k) {
+        const double h = dt[k];
+        if (!(h > 0.0)) return tslam_internal_fail(TSLAM_EINVAL, "tslam_imu_preintegrate: dt must be > 0");
+        const V3 w = mv(f->Ri, v3(gyro + 3 * k) - bgv);
+        const V3 al = have_prev ? (w - wp) / h : V3{0, 0, 0};
+        const V3 a = mv(f->Ri, v3(accel + 3 * k) - bav) - cross(w, cross(w, r)) - cross(al, r);
+        const V3 Ra = mv(dR, a);
+        mm(dR, f->Ri, dRRi);
+        dp = dp + dv * h + 0.5 * Ra * h * h;
+        for (int e = 0; e < 9; ++e) Jp[e] = Jp[e] + Jv[e] * h - 0.5 * dRRi[e] * h * h;
+        dv = dv + Ra * h;
+        for (int e = 0; e < 9; ++e) Jv[e] = Jv[e] - dRRi[e] * h;
+        double E[9], nR[9];
+        rotvec_to_matrix(w * h, E);
+        mm(dR, E, nR);
+        std::memcpy(dR, nR, sizeof dR);
+        T += h;
+        wp = w;
+        have_prev = true;
+    }
+    std::memset(record, 0, 32 * sizeof(double));
+    put(dv, record);
+    put(dp, record + 3);
+    std::memcpy(record + 6, Jv, sizeof Jv);
+    std::memcpy(record + 15, Jp, sizeof Jp);
+    put(bav, record + 24);
+    record[27] = T;
+    record[28] = 1.0 / (f->na * f->na * T + v_floor * v_floor);
+    record[29] = 1.0 / (f->na * f->na * T * T * T / 3.0 + p_floor * p_floor);
+    return TSLAM_OK;
+}
+
 }   // extern "C"

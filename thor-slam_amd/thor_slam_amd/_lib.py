@@ -123,6 +123,9 @@ _SIGNATURES = {
     "tslam_imu_batch_priors": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P]),
     "tslam_imu_absorb": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P, _P]),
     "tslam_imu_vision_only": (ctypes.c_int, [_P, _P, ctypes.c_double, _P, _P, _P]),
+    "tslam_imu_gravity": (ctypes.c_int, [_P, _P]),
+    "tslam_imu_preintegrate": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P, _P, ctypes.c_double, ctypes.c_double,
+                                              _P]),
     "tslam_last_error": (ctypes.c_char_p, []),
     "tslam_abi_version": (ctypes.c_int, []),
     "tslam_create": (ctypes.c_int, [ctypes.POINTER(StereoDesc), ctypes.POINTER(Params), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
@@ -195,6 +198,10 @@ _SIGNATURES = {
     "tslam_ba_replay_schur": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "tslam_ba_split_solve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "tslam_ba_inertial": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double]),
+    "tslam_ba_inertial_factor": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
+                                                ctypes.c_void_p]),
+    "tslam_ba_read_inertial": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_ba_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
     "tslam_loop_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
@@ -875,6 +882,26 @@ class Handle:
         _check(self.lib.tslam_ba_replay_schur(self.h, int(pair), int(reps), ctypes.c_void_p(stream), ctypes.byref(us),
                                               ctypes.byref(fl)))
         return {"us": us.value, "flops": fl.value, "reps": int(reps)}
+
+    def ba_inertial(self, gravity, ba_prior, ba_weight: float, pair: int = 0) -> None:
+        """World gravity, accelerometer-bias prior and its weight for pair's window (tslam.h)."""
+        g = np.ascontiguousarray(gravity, dtype=np.float64).reshape(3)
+        b = np.ascontiguousarray(ba_prior, dtype=np.float64).reshape(3)
+        _check(self.lib.tslam_ba_inertial(self.h, int(pair), g.ctypes.data, b.ctypes.data, float(ba_weight)))
+
+    def ba_inertial_factor(self, frame: int, record, v0, pair: int = 0) -> None:
+        """Keyframe ``frame``'s inertial factor record (30 doubles, oracle INE_N layout) and initial
+        velocity, before its batch is submitted."""
+        r = np.ascontiguousarray(np.asarray(record, dtype=np.float64).reshape(-1)[:30])
+        v = np.ascontiguousarray(v0, dtype=np.float64).reshape(3)
+        _check(self.lib.tslam_ba_inertial_factor(self.h, int(pair), int(frame), r.ctypes.data, v.ctypes.data))
+
+    def ba_read_inertial(self, pair: int = 0) -> dict:
+        """Velocities by slot [W][3] and the window's accelerometer bias [3] (synchronises)."""
+        vel = np.zeros((self.cfg.ba_window, 3))
+        ba = np.zeros(3)
+        _check(self.lib.tslam_ba_read_inertial(self.h, int(pair), vel.ctypes.data, ba.ctypes.data))
+        return {"vel": vel, "ba": ba}
 
     def ba_split_solve(self, split: bool) -> None:
         """k_ba_reduce + k_ba_solve (kernel boundary) instead of k_ba_reduce_solve (tslam.h)."""

@@ -210,6 +210,30 @@ class ImuPropagator:
                                                     None if ac is None else ac.ctypes.data, out, valid.ctypes.data))
         return [_py_step(out[k]) if valid[k] else None for k in range(n)]
 
+    def gravity(self) -> np.ndarray:
+        """World gravity of the accelerometer filter (its camera-0 world; zeros before ``begin``)."""
+        g = np.zeros(3)
+        _lib._check(self.lib.tslam_imu_gravity(self._f, g.ctypes.data))
+        return g
+
+    def preintegrate(self, samples: list, bg: np.ndarray, ba: np.ndarray, w_prev: np.ndarray | None = None,
+                     v_floor: float = 1e-2, p_floor: float = 1e-3) -> np.ndarray:
+        """The local BA's inertial factor record (32 doubles, tslam_ba_inertial_factor) of the
+        frame intervals ``samples`` = [(dt, gyro, accel)] between two keyframes
+        (tslam_imu_preintegrate)."""
+        n = len(samples)
+        dt = np.ascontiguousarray([float(d) for d, _, _ in samples], dtype=np.float64)
+        gy = np.ascontiguousarray([np.asarray(g, dtype=np.float64).reshape(3) for _, g, _ in samples])
+        ac = np.ascontiguousarray([np.asarray(a, dtype=np.float64).reshape(3) for _, _, a in samples])
+        bgv = np.ascontiguousarray(bg, dtype=np.float64).reshape(3)
+        bav = np.ascontiguousarray(ba, dtype=np.float64).reshape(3)
+        wp = None if w_prev is None else np.ascontiguousarray(w_prev, dtype=np.float64).reshape(3)
+        out = np.zeros(32)
+        _lib._check(self.lib.tslam_imu_preintegrate(self._f, n, dt.ctypes.data, gy.ctypes.data, ac.ctypes.data,
+                                                    bgv.ctypes.data, bav.ctypes.data, None if wp is None else wp.ctypes.data,
+                                                    float(v_floor), float(p_floor), out.ctypes.data))
+        return out
+
     def absorb(self, samples: list, status: np.ndarray, t_rel: np.ndarray, cov: np.ndarray) -> None:
         """The batch's results in the filter's camera: status [n], T_rel [n][4][4], cov [n][6][6]
         (tslam_imu_absorb)."""

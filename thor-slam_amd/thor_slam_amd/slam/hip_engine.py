@@ -323,6 +323,7 @@ class HipSlamEngine(SlamEngine):
         self._imu_batches: list = []
         self._imu_seq = 0                            # batches submitted (numbers the entries)
         self._kf_imu: tuple | None = None             # gyro rotation since the last BA keyframe (R, var, first frame)
+        self._kf_ine: tuple | None = None             # samples since the last BA keyframe (list, first frame, w_prev)
         self._prev_stamp: float | None = None      # timestamp of the last submitted frame (IMU dt)
         self._base_R_imu = np.eye(3)
         self._torch = None
@@ -664,6 +665,7 @@ class HipSlamEngine(SlamEngine):
         coast = [c for e in self._imu_batches if "samples" in e for c in e["samples"]]
         steps = imu.batch_priors(coast + samples)[len(coast):]
         self._ba_imu_factors(steps)
+        self._ba_inertial_factors(steps, samples)
         P, n = len(self._pairs), len(stamps)
         rot = np.tile(np.eye(3), (n, P, 1, 1))
         trn = np.zeros((n, P, 3))
@@ -717,6 +719,34 @@ class HipSlamEngine(SlamEngine):
                 if acc is not None and acc[2] == gk - cfg.ba_kf_interval + 1 and acc[1] > 0.0:
                     self._handle.ba_imu_factor(gk, acc[0], 1.0 / acc[1])
                 self._kf_imu = (np.eye(3), 0.0, gk + 1)
+
+    def _ba_inertial_factors(self, steps: list, samples: list) -> None:
+        """The local BA's tightly coupled inertial factors (one stereo pair, accelerometer leg):
+        the frame intervals' samples since the last BA keyframe are preintegrated with the
+        filter's current biases (tslam_imu_preintegrate); at each keyframe whose whole interval had
+        samples the record and the keyframe camera's predicted world velocity go to
+        tslam_ba_inertial_factor, and the window gets the filter's gravity and accelerometer-bias
+        prior (tslam_ba_inertial) before the batch is submitted."""
+        cfg, imu = self._config, self._imu
+        if cfg.ba_window <= 0 or len(self._pairs) != 1 or not cfg.ba_inertial or not imu.accel or not imu.ready:
+            return
+        st = imu.st
+        self._handle.ba_inertial(imu.gravity(), st.ba, 1.0 / max(st.var_b, 1e-12))
+        g = self._handle.frames_done
+        for k, (step, smp) in enumerate(zip(steps, samples)):
+            gk = g + k
+            if step is None or step.v1 is None or smp[0] is None:
+                self._kf_ine = None
+            else:
+                if self._kf_ine is None:
+                    self._kf_ine = ([], gk, None)
+                self._kf_ine[0].append(smp)
+            if gk % cfg.ba_kf_interval == 0:
+                acc = self._kf_ine
+                if acc is not None and acc[1] == gk - cfg.ba_kf_interval + 1 and len(acc[0]) == cfg.ba_kf_interval:
+                    rec = imu.preintegrate(acc[0], st.bg, st.ba, acc[2], cfg.ba_inertial_v_floor, cfg.ba_inertial_p_floor)
+                    self._handle.ba_inertial_factor(gk, rec, step.v1)
+                self._kf_ine = ([], gk + 1, None if step is None else step.w.copy())
 
     def _set_motion_prior(self, *args) -> None:
         """The batch's priors on the handle (every rank's handle on a sharded rig: each refines its
@@ -1170,6 +1200,7 @@ class HipSlamEngine(SlamEngine):
         self._imu_batches = []
         self._imu_seq = 0
         self._kf_imu = None
+        self._kf_ine = None
         if self._imu is not None:
             self._imu.reset()
         self._keyframe_poses = []
