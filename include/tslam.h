@@ -343,13 +343,16 @@ int tslam_imu_vision_only(const double* T, const double* cov, double sigma2, con
 int tslam_imu_gravity(const tslam_imu* f, double* gravity);
 /* The inertial factor record of tslam_ba_inertial_factor (record[32], layout there) from the n
  * frame intervals between two keyframes: dt[n], gyro[n][3], accel[n][3] (IMU axes), the filter's
- * biases bg[3], ba[3] (ba becomes ba_lin), w_prev[3] = the camera-axes rate of the interval before
- * the first (NULL: none), and the weights' floors (m/s, m):
+ * biases bg[3], ba[3] (ba becomes ba_lin), w_prev[3] = the factor frame's rate over the interval
+ * before the first (NULL: none), the factor's frame: frame_R_imu[9] (row-major; NULL = the
+ * filter's rect_R_imu, i.e. pair 0's rectified-left camera; a rig's body window passes
+ * base_R_imu) and lever[3] (the IMU's position in that frame; NULL = the filter's), and the
+ * weights' floors (m/s, m):
  * wv = 1 / (n_a^2 T + v_floor^2), wp = 1 / (n_a^2 T^3 / 3 + p_floor^2).  Spec:
  * oracle/numpy_ba.py preintegrate. */
 int tslam_imu_preintegrate(const tslam_imu* f, int n, const double* dt, const double* gyro, const double* accel,
-                           const double* bg, const double* ba, const double* w_prev, double v_floor, double p_floor,
-                           double* record);
+                           const double* bg, const double* ba, const double* w_prev, const double* frame_R_imu,
+                           const double* lever, double v_floor, double p_floor, double* record);
 
 /* Rig pose (replaces the multi-camera fusion cuVSLAM does for the rig of
  * isaac_ros.py:364-411): base_T_rect[P][16] = the rectified-left frame of each pair in the rig's
@@ -536,7 +539,10 @@ int tslam_ba_imu_factor(tslam_handle* h, int pair, int64_t frame, const double* 
  *   carries a velocity per keyframe and one accelerometer bias; every Gauss-Newton step eliminates
  *   them into the reduced camera system (k_ba_reduce_solve_ine) and updates them after the camera
  *   solve.  A window with no factor between two of its keyframes solves as before.
- * tslam_ba_read_inertial (synchronises): velocity[W][3] by slot, ba[3]. */
+ * tslam_ba_read_inertial (synchronises): velocity[W][3] by slot, ba[3].
+ * On a rig (tslam_set_rig over several pairs, rig-level A8) the factors act on the body window:
+ * pair = n_pairs, record in the earlier keyframe's body (base_link) axes, velocities of the body
+ * origin, gravity in the body window's world (base_link at frame 0); pair windows are refused. */
 int tslam_ba_inertial(tslam_handle* h, int pair, const double* gravity, const double* ba_prior, double ba_weight);
 int tslam_ba_inertial_factor(tslam_handle* h, int pair, int64_t frame, const double* record, const double* v0);
 int tslam_ba_read_inertial(tslam_handle* h, int pair, double* velocity, double* ba);

@@ -130,6 +130,59 @@ def inertial_residual(f: np.ndarray, Rcw_i: np.ndarray, tcw_i: np.ndarray, Rcw_j
     return np.concatenate([rv, rp])
 
 
+def inertial_system(st, slots: list[int], Rs: np.ndarray, ts: np.ndarray, S: np.ndarray, b: np.ndarray) -> tuple | None:
+    """``KeyframeWindow.inertial_terms`` for any window state ``st`` carrying ``ine``, ``vel``,
+    ``ba``, ``ine_cfg`` and ``p.lam`` (a pair window, or a rig's body window with the body poses
+    as the cameras)."""
+    n = len(slots)
+    fs = [c for c in range(1, n) if st.ine[slots[c]][28] > 0.0]
+    if not fs:
+        return None
+    gw, ba0, wb = st.ine_cfg
+    my = 3 * n + 3
+    Hxy = np.zeros((6 * n, my))
+    Hyy = np.zeros((my, my))
+    by = np.zeros(my)
+    for c in fs:
+        f = st.ine[slots[c]]
+        i, j = c - 1, c
+        vi, vj = st.vel[slots[i]], st.vel[slots[j]]
+        r = inertial_residual(f, Rs[i], ts[i], Rs[j], ts[j], vi, vj, st.ba, gw)
+        J = inertial_jacobian(f, Rs[i], ts[i], Rs[j], ts[j], vi, vj, gw)
+        Wd = np.array([f[28]] * 3 + [f[29]] * 3)
+        xc = list(range(6 * i, 6 * i + 6)) + list(range(6 * j, 6 * j + 6))
+        yc = list(range(3 * i, 3 * i + 3)) + list(range(3 * j, 3 * j + 3)) + list(range(3 * n, 3 * n + 3))
+        Jx, Jy = J[:, :12], J[:, 12:]
+        WJx, WJy = Wd[:, None] * Jx, Wd[:, None] * Jy
+        S[np.ix_(xc, xc)] += Jx.T @ WJx
+        b[xc] -= Jx.T @ (Wd * r)
+        Hxy[np.ix_(xc, yc)] += Jx.T @ WJy
+        Hyy[np.ix_(yc, yc)] += Jy.T @ WJy
+        by[yc] -= Jy.T @ (Wd * r)
+    Hyy[3 * n:, 3 * n:] += wb * np.eye(3)
+    by[3 * n:] -= wb * (st.ba - ba0)
+    Hyy += st.p.lam * np.eye(my)
+    return Hxy, Hyy, by
+
+
+def inertial_step(st, slots: list[int], S: np.ndarray, b: np.ndarray, ine: tuple) -> np.ndarray:
+    """Solve the damped camera system ``S`` (6n, lam included), ``b`` with the velocity / bias
+    unknowns of ``ine`` = (Hxy, Hyy, b_y) eliminated (camera 0 = gauge); apply dy to ``st``'s
+    velocities and bias; return the 6n camera step (zeros for camera 0)."""
+    n = len(slots)
+    Hxy, Hyy, by = ine
+    Hx = Hxy[6:]
+    Z = np.linalg.solve(Hyy, Hx.T)          # Hyy^-1 Hyx
+    zb = np.linalg.solve(Hyy, by)
+    dc = np.zeros(6 * n)
+    dc[6:] = np.linalg.solve(S[6:, 6:] - Hx @ Z, b[6:] - Hx @ zb)
+    dy = zb - Z @ dc[6:]
+    for c in range(n):
+        st.vel[slots[c]] = st.vel[slots[c]] + dy[3 * c:3 * c + 3]
+    st.ba = st.ba + dy[3 * n:]
+    return dc
+
+
 def inertial_jacobian(f: np.ndarray, Rcw_i: np.ndarray, tcw_i: np.ndarray, Rcw_j: np.ndarray, tcw_j: np.ndarray,
                       v_i: np.ndarray, v_j: np.ndarray, gw: np.ndarray) -> np.ndarray:
     """6 x 21 Jacobian of (r_v, r_p): columns rho_i, omega_i, rho_j, omega_j (left camera
@@ -380,35 +433,12 @@ class KeyframeWindow:
         """The inertial factors into S and b (camera-camera parts, in place) and the velocity /
         bias system (Hxy 6n x (3n+3), Hyy with lam I and the bias prior, b_y); None without
         factors."""
-        n = len(slots)
-        fs = [c for c in range(1, n) if self.ine[slots[c]][28] > 0.0]
-        if not fs:
-            return None
-        gw, ba0, wb = self.ine_cfg
-        my = 3 * n + 3
-        Hxy = np.zeros((6 * n, my))
-        Hyy = np.zeros((my, my))
-        by = np.zeros(my)
-        for c in fs:
-            f = self.ine[slots[c]]
-            i, j = c - 1, c
-            vi, vj = self.vel[slots[i]], self.vel[slots[j]]
-            r = inertial_residual(f, Rs[i], ts[i], Rs[j], ts[j], vi, vj, self.ba, gw)
-            J = inertial_jacobian(f, Rs[i], ts[i], Rs[j], ts[j], vi, vj, gw)
-            Wd = np.array([f[28]] * 3 + [f[29]] * 3)
-            xc = list(range(6 * i, 6 * i + 6)) + list(range(6 * j, 6 * j + 6))
-            yc = list(range(3 * i, 3 * i + 3)) + list(range(3 * j, 3 * j + 3)) + list(range(3 * n, 3 * n + 3))
-            Jx, Jy = J[:, :12], J[:, 12:]
-            WJx, WJy = Wd[:, None] * Jx, Wd[:, None] * Jy
-            S[np.ix_(xc, xc)] += Jx.T @ WJx
-            b[xc] -= Jx.T @ (Wd * r)
-            Hxy[np.ix_(xc, yc)] += Jx.T @ WJy
-            Hyy[np.ix_(yc, yc)] += Jy.T @ WJy
-            by[yc] -= Jy.T @ (Wd * r)
-        Hyy[3 * n:, 3 * n:] += wb * np.eye(3)
-        by[3 * n:] -= wb * (self.ba - ba0)
-        Hyy += self.p.lam * np.eye(my)
-        return Hxy, Hyy, by
+        return inertial_system(self, slots, Rs, ts, S, b)
+
+    def inertial_solve(self, slots: list[int], S: np.ndarray, b: np.ndarray, ine: tuple) -> np.ndarray:
+        """The camera step (gauge camera 0 dropped) with the velocity / bias unknowns eliminated,
+        and their own step applied to the window's velocities and bias."""
+        return inertial_step(self, slots, S, b, ine)
 
     def solve(self) -> dict:
         p = self.p
@@ -428,15 +458,7 @@ class KeyframeWindow:
             if ine is None:
                 dc[6:] = np.linalg.solve(S[6:, 6:], lin["b"][6:])
             else:
-                Hxy, Hyy, by = ine
-                Hx = Hxy[6:]
-                Z = np.linalg.solve(Hyy, Hx.T)          # Hyy^-1 Hyx
-                zb = np.linalg.solve(Hyy, by)
-                dc[6:] = np.linalg.solve(S[6:, 6:] - Hx @ Z, lin["b"][6:] - Hx @ zb)
-                dy = zb - Z @ dc[6:]
-                for c in range(n):
-                    self.vel[slots[c]] = self.vel[slots[c]] + dy[3 * c:3 * c + 3]
-                self.ba = self.ba + dy[3 * n:]
+                dc = self.inertial_solve(slots, S, lin["b"], ine)
             dcc = dc.reshape(n, 6)
             dp = self.landmark_update(ob, lin, dcc)
             for c in range(1, n):
@@ -483,7 +505,12 @@ class RigKeyframeWindow:
         S = sum_p Ad_p^T S_p Ad_p (6x6 blocks, pairs in order) + lam I,   b = sum_p Ad_p^T b_p;
     body 0 (oldest keyframe) is the gauge; S' dB = b' by Cholesky; each pair's landmarks move by
     its back substitution with dc_p = Ad_p dB; bodies R <- cayley(w) R, t <- cayley(w) t + rho, then
-    every pair's cameras are recomputed as E_p^-1 B."""
+    every pair's cameras are recomputed as E_p^-1 B.
+
+    Inertial factors on the body window (``add_keyframe(..., ine=(record, v0))``, ``set_inertial``):
+    ``inertial_terms`` with the body poses as the cameras (record in the earlier keyframe's body
+    axes, velocities of the body origin, gravity in the body window's world = base_link at frame
+    0), added to the combined S and b and eliminated as in the pair window."""
 
     def __init__(self, K: int, intrs: list, E: list[np.ndarray], params: BAParams):
         from .numpy_rig import inv_rigid, mul4
@@ -495,6 +522,13 @@ class RigKeyframeWindow:
         self.Ad = [adjoint_rl(ei) for ei in self.Einv]
         self.p = params
         self.B = np.tile(np.eye(4), (params.window, 1, 1))   # body_T_world per slot
+        self.ine = np.zeros((params.window, INE_N))
+        self.vel = np.zeros((params.window, 3))
+        self.ba = np.zeros(3)
+        self.ine_cfg = (np.zeros(3), np.zeros(3), 0.0)
+
+    def set_inertial(self, gw: np.ndarray, ba0: np.ndarray, wb: float) -> None:
+        self.ine_cfg = (np.asarray(gw, dtype=np.float64).copy(), np.asarray(ba0, dtype=np.float64).copy(), float(wb))
 
     @property
     def frame(self) -> np.ndarray:
@@ -506,13 +540,16 @@ class RigKeyframeWindow:
     def cams(self, p: int, B: np.ndarray) -> np.ndarray:
         return np.stack([self._mul4(self.Einv[p], b) for b in B])
 
-    def add_keyframe(self, g: int, B_new: np.ndarray, obs: list[tuple]) -> int:
+    def add_keyframe(self, g: int, B_new: np.ndarray, obs: list[tuple], ine: tuple | None = None) -> int:
         """Keyframe g with body pose ``B_new`` (body_T_world); ``obs[p]`` = (u, v, disp, link) of
-        pair p as for ``KeyframeWindow.add_keyframe``."""
+        pair p as for ``KeyframeWindow.add_keyframe``; ``ine`` = (record, v0) the body's inertial
+        factor from the previous keyframe and its initial velocity."""
         slot = -1
         for p, (w, (u, v, disp, link)) in enumerate(zip(self.pairs, obs)):
             slot = w.add_keyframe(g, self._mul4(self.Einv[p], B_new), u, v, disp, link)
         self.B[slot] = B_new
+        self.ine[slot] = 0.0 if ine is None else np.asarray(ine[0], dtype=np.float64)
+        self.vel[slot] = 0.0 if ine is None else np.asarray(ine[1], dtype=np.float64)
         return slot
 
     def solve(self) -> dict:
@@ -534,8 +571,12 @@ class RigKeyframeWindow:
                 A = np.kron(np.eye(n), self.Ad[q])
                 S = S + A.T @ lin["S"] @ A
                 b = b + A.T @ lin["b"]
-            dB = np.zeros(6 * n)
-            dB[6:] = np.linalg.solve(S[6:, 6:], b[6:])
+            ine = inertial_system(self, slots, B[:, :3, :3], B[:, :3, 3], S, b)
+            if ine is None:
+                dB = np.zeros(6 * n)
+                dB[6:] = np.linalg.solve(S[6:, 6:], b[6:])
+            else:
+                dB = inertial_step(self, slots, S, b, ine)
             dBB = dB.reshape(n, 6)
             for q, w in enumerate(self.pairs):
                 dcc = dBB @ self.Ad[q].T                   # dc_p = Ad_p dB per camera
@@ -628,7 +669,7 @@ class RigBATracker:
         self.temporal: list[list[np.ndarray]] = [[] for _ in intrs]
         self.last_solve: dict | None = None
 
-    def step(self, g: int, results: list[dict], world_T_body: np.ndarray) -> dict | None:
+    def step(self, g: int, results: list[dict], world_T_body: np.ndarray, ine: tuple | None = None) -> dict | None:
         for q, res in enumerate(results):
             self.temporal[q].insert(0, np.asarray(res["cur"]["temporal"], dtype=np.int64))
             del self.temporal[q][self.p.kf_interval:]
@@ -646,7 +687,7 @@ class RigBATracker:
             u, v = keyframe_observations(res["cur"]["left"], self.K)
             link = None if first else chain_links(self.temporal[q][: self.p.kf_interval])
             obs.append((u, v, np.asarray(res["cur"]["disp"], dtype=np.float64), link))
-        slot = w.add_keyframe(g, _inv_rigid(T_wb), obs)
+        slot = w.add_keyframe(g, _inv_rigid(T_wb), obs, ine=ine)
         self.Tfe[slot] = world_T_body
         self.last_solve = w.solve()
         return self.last_solve

@@ -26,8 +26,41 @@ BA_ITEMS = dict(ba_window=4, ba_kf_interval=2, ba_iters=3, ba_lambda=1.0, ba_out
 N = 10
 
 
-@functools.lru_cache(maxsize=1)
-def rig_ba_scenario():
+RIG_INE_CFG = (np.array([0.3, -9.75, 0.9]), np.array([0.0, 0.01, 0.0]), 10.0)   # gravity, bias prior, weight
+
+
+def _body_inertial_factors(T_abs: list) -> dict:
+    """Per body keyframe g > 0: an inertial factor (body axes) whose residual vanishes at the rig
+    chain's body poses, central-difference velocities and a bias (0.02, -0.01, 0.03); initial
+    velocities off by 0.05 m/s (the BA's visual window disagrees slightly: the factors pull)."""
+    from oracle.numpy_ba import INE_N
+
+    rng = np.random.default_rng(11)
+    iv = BA_ITEMS["ba_kf_interval"]
+    dt = 1.0 / 30.0
+    gw = RIG_INE_CFG[0]
+    ba_true = np.array([0.02, -0.01, 0.03])
+    Tbw = [inv_rigid(t) for t in T_abs]
+    pos = [t[:3, 3] for t in T_abs]
+    vel = {g: (pos[min(g + 1, N - 1)] - pos[max(g - 1, 0)]) / (dt * (min(g + 1, N - 1) - max(g - 1, 0)))
+           for g in range(0, N, iv)}
+    out = {}
+    for g in range(iv, N, iv):
+        Ti, vi, vj = Tbw[g - iv], vel[g - iv], vel[g]
+        Jv, Jp = rng.normal(0, 0.2, (3, 3)) * iv * dt, rng.normal(0, 0.02, (3, 3)) * iv * dt
+        f = np.zeros(INE_N)
+        T = iv * dt
+        f[0:3] = Ti[:3, :3] @ (vj - vi - gw * T) - Jv @ ba_true
+        f[3:6] = Ti[:3, :3] @ (pos[g] - pos[g - iv] - vi * T - 0.5 * gw * T * T) - Jp @ ba_true
+        f[6:15], f[15:24] = Jv.reshape(9), Jp.reshape(9)
+        f[27], f[28], f[29] = T, 1e3, 1e5
+        out[g] = (f, vj + rng.normal(0, 0.05, 3))
+    return out
+
+
+@functools.lru_cache(maxsize=2)
+def rig_ba_scenario(inertial: bool = False):
+    ine = _body_inertial_factors(rig_ba_scenario()["T_abs"]) if inertial else None
     sc = dict(rig_scene(NAMES, N))
     frames, rects, E = sc["frames"], sc["rects"], sc["E"]
     cfg = HipSlamConfig(**BA_ITEMS)
@@ -37,8 +70,10 @@ def rig_ba_scenario():
                   outlier_px=cfg.ba_outlier_px)
     intrs = [(r.fx, r.fy, r.cx, r.cy, r.fx * r.baseline) for r in rects]
     ba = RigBATracker(cfg.n_features, intrs, E, bp)
+    if ine is not None:
+        ba.win.set_inertial(*RIG_INE_CFG)
     chain = RigChain()
-    snaps = []
+    snaps, T_seq = [], []
     for i in range(N):
         outs = [trk.step(frames[i, 2 * q], frames[i, 2 * q + 1]) for q, trk in enumerate(trks)]
         if i == 0:
@@ -47,12 +82,15 @@ def rig_ba_scenario():
             items = [{"status": o["status"], "T": o["T"], "corr": o.get("corr"), "intr": (r.fx, r.fy, r.cx, r.cy)}
                      for o, r in zip(outs, rects)]
             T_abs = chain.step(rig_pose(items, E, cfg))
-        ba.step(i, outs, T_abs)
+        T_seq.append(T_abs.copy())
+        ba.step(i, outs, T_abs, ine=None if ine is None else ine.get(i))
         w = ba.win
         snaps.append({"frames": w.frame.copy(), "B": w.B.copy(), "solve": ba.last_solve,
+                      "vel": w.vel.copy(), "ba": w.ba.copy(),
                       "pairs": [{"T_cw": pw.T_cw.copy(), "lm": pw.lm.copy(), "X": pw.X.copy(), "u": pw.u.copy(),
                                  "v": pw.v.copy(), "d": pw.d.copy()} for pw in w.pairs]})
-    return {"frames": frames, "rects": rects, "E": E, "cfg": cfg, "snaps": snaps, "traj": sc["traj"]}
+    return {"frames": frames, "rects": rects, "E": E, "cfg": cfg, "snaps": snaps, "traj": sc["traj"], "T_abs": T_seq,
+            "ine": ine}
 
 
 def _compare(h, want: dict, E, where: str):
@@ -96,6 +134,44 @@ def test_rig_ba_matches_oracle(batch):
         h.read_poses(nb)
         _compare(h, sc["snaps"][b0 + nb - 1], sc["E"], f"after frame {b0 + nb - 1}")
     h.close()
+
+
+def test_rig_ba_body_inertial_factors_match_oracle():
+    """Inertial factors on the rig's body window (tslam_ba_inertial_factor with pair = n_pairs):
+    body poses, every pair's cameras and landmarks, body velocities and the window's bias within
+    1e-9 of RigKeyframeWindow's inertial solve, in batches of 3; pair windows are refused."""
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    sc = rig_ba_scenario(True)
+    plain = rig_ba_scenario()
+    P, batch = len(sc["E"]), 3
+    h = Handle(sc["rects"], sc["cfg"], max_batch=batch)
+    try:
+        h.set_rig(sc["E"])
+        with pytest.raises(RuntimeError, match="body window"):
+            h.ba_inertial(*RIG_INE_CFG, pair=0)
+        h.ba_inertial(*RIG_INE_CFG, pair=P)
+        for g, (f, v0) in sc["ine"].items():
+            h.ba_inertial_factor(g, f, v0, pair=P)
+        dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+        for b0 in range(0, N, batch):
+            nb = min(batch, N - b0)
+            h.submit(dev[b0:].data_ptr(), nb, torch.cuda.current_stream().cuda_stream)
+            want = sc["snaps"][b0 + nb - 1]
+            _compare(h, want, sc["E"], f"inertial, after frame {b0 + nb - 1}")
+            gi = h.ba_read_inertial(P)
+            occ = want["frames"] >= 0
+            err_v = np.abs(gi["vel"][occ] - want["vel"][occ]).max() / max(np.abs(want["vel"][occ]).max(), 1e-3)
+            assert err_v < 1e-9, (b0, err_v)
+            assert np.abs(gi["ba"] - want["ba"]).max() < 1e-9 * max(np.abs(want["ba"]).max(), 1e-3), (b0, gi["ba"])
+    finally:
+        h.close()
+    last, base = sc["snaps"][-1], plain["snaps"][-1]
+    occ = last["frames"] >= 0
+    assert max(rel_frobenius(last["B"][s], base["B"][s]) for s in np.nonzero(occ)[0]) > 1e-7
+    assert np.abs(last["ba"]).max() > 1e-4
 
 
 def test_rig_ba_every_pair_contributes():

@@ -1497,6 +1497,8 @@ __global__ void k_ba_rig_insert(BatchCtx c, BaArgs a) {
         qb.Tfe[(size_t)a.slot * 16 + e] = fe[e];
     }
     for (int p = 0; p < c.P; ++p) mul4(c.rig_Einv + 16 * p, Tbw, a.st.T + ((size_t)p * a.W + a.slot) * 16);
+    for (int e = 0; e < TS_BA_INE; ++e) qb.ine[(size_t)a.slot * TS_BA_INE + e] = a.ine[e];   // the body's inertial factor
+    for (int e = 0; e < 3; ++e) qb.vel[(size_t)a.slot * 3 + e] = a.vel0[e];
 }
 
 // The body system of an iteration from every pair's reduced system (block r = row, thread = column):
@@ -1591,7 +1593,7 @@ void launch_ba_rig_keyframe(const BatchCtx& c, const BaArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_ba_rig_insert, dim3(1), dim3(64), 0, s, c, a);
 }
 
-void launch_ba_rig_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing) {
+void launch_ba_rig_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing, bool inertial) {
     BaArgs ap = a, ab = a;
     ab.pair = c.P;
     for (int p = 0; p < c.P; ++p) {
@@ -1604,7 +1606,7 @@ void launch_ba_rig_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTi
             launch_ba_linearize(c, ap, it, s, timing);
         }
         hipLaunchKernelGGL(k_ba_rig_combine, dim3(64), dim3(64), 0, s, c, ab);
-        hipLaunchKernelGGL(k_ba_solve, dim3(1), dim3(64 * BA_SOLVE_WAVES), 0, s, c, ab);
+        hipLaunchKernelGGL(inertial ? k_ba_solve_ine : k_ba_solve, dim3(1), dim3(64 * BA_SOLVE_WAVES), 0, s, c, ab);
         hipLaunchKernelGGL(k_ba_rig_expand, dim3(c.P), dim3(64), 0, s, c, ab);
     }
     for (int p = 0; p < c.P; ++p) {

@@ -430,8 +430,8 @@ static int alloc_ba(tslam_handle* h) {
     HIPCHK(hipMemset(b.camobs, 0xFF, 4 * P * W * WK));
     HIPCHK(hipMemset(b.remap, 0x7F, 4 * P * K));
     HIPCHK(hipDeviceSynchronize());
-    h->ba_icfg.assign(h->P, std::array<double, 8>{});
-    h->ba_ine_slot.assign(h->P, std::array<uint8_t, TS_BA_MAXW>{});
+    h->ba_icfg.assign(h->P + 1, std::array<double, 8>{});   // pair windows + a rig's body window
+    h->ba_ine_slot.assign(h->P + 1, std::array<uint8_t, TS_BA_MAXW>{});
     return TSLAM_OK;
 }
 
@@ -480,9 +480,15 @@ static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const doub
         const bool evict = h->ba_frame[a.slot] >= 0;
         if (evict) a.n_order = ba_order(h, a.slot, a.order);
         const bool rig = ba_rig(h);
-        if (rig) {   // the body pose first, every pair's camera E_p^-1 B
+        if (rig) {   // the body pose first, every pair's camera E_p^-1 B (and the body's inertial factor)
             a.fe_body = fe_body;
             a.pose_given = 1;
+            auto jt = h->ba_ine.find({h->P, g});
+            const bool has = jt != h->ba_ine.end();
+            for (int e = 0; e < TS_BA_INE; ++e) a.ine[e] = has ? jt->second[e] : 0.0;
+            for (int e = 0; e < 3; ++e) a.vel0[e] = has ? jt->second[TS_BA_INE + e] : 0.0;
+            if (has) h->ba_ine.erase(jt);
+            h->ba_ine_slot[h->P][a.slot] = has && a.ine[28] > 0.0;
             launch_ba_rig_keyframe(c, a, s);
         }
         for (int p = 0; p < h->P; ++p) {
@@ -510,7 +516,10 @@ static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const doub
         a.n_order = ba_order(h, -1, a.order);
         h->ba_solved.resize(h->P);
         if (rig) {
-            launch_ba_rig_solve(c, a, s, h->ba_timing.ev ? &h->ba_timing : nullptr);
+            for (int e = 0; e < 8; ++e) a.icfg[e] = h->ba_icfg[h->P][e];
+            bool ine = false;
+            for (int k = 1; k < a.n_order; ++k) ine = ine || h->ba_ine_slot[h->P][a.order[k]];
+            launch_ba_rig_solve(c, a, s, h->ba_timing.ev ? &h->ba_timing : nullptr, ine);
             for (int p = 0; p < h->P; ++p) {
                 h->ba_solved[p] = a;
                 h->ba_solved[p].pair = p;
@@ -2688,9 +2697,18 @@ int tslam_ba_imu_factor(tslam_handle* h, int pair, int64_t frame, const double* 
     return TSLAM_OK;
 }
 
-int tslam_ba_inertial(tslam_handle* h, int pair, const double* gravity, const double* ba_prior, double ba_weight) {
-    if (!h || !gravity || !ba_prior || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad argument");
+// A rig's inertial factors act on its body window (pair = n_pairs); a stereo pair's on its own.
+static int ine_pair_check(tslam_handle* h, int pair) {
     if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
+    if (ba_rig(h) ? pair != h->P : (pair < 0 || pair >= h->P))
+        return fail(TSLAM_EINVAL, ba_rig(h) ? "a rig's inertial factors go to its body window (pair = n_pairs)"
+                                            : "bad pair");
+    return TSLAM_OK;
+}
+
+int tslam_ba_inertial(tslam_handle* h, int pair, const double* gravity, const double* ba_prior, double ba_weight) {
+    if (!h || !gravity || !ba_prior) return fail(TSLAM_EINVAL, "bad argument");
+    if (int rc = ine_pair_check(h, pair); rc != TSLAM_OK) return rc;
     if (!(ba_weight >= 0.0) || !std::isfinite(ba_weight)) return fail(TSLAM_EINVAL, "ba_weight must be finite and >= 0");
     for (int e = 0; e < 3; ++e)
         if (!std::isfinite(gravity[e]) || !std::isfinite(ba_prior[e])) return fail(TSLAM_EINVAL, "non-finite input");
@@ -2704,9 +2722,8 @@ int tslam_ba_inertial(tslam_handle* h, int pair, const double* gravity, const do
 }
 
 int tslam_ba_inertial_factor(tslam_handle* h, int pair, int64_t frame, const double* record, const double* v0) {
-    if (!h || !record || !v0 || pair < 0 || pair >= h->P || frame < 0) return fail(TSLAM_EINVAL, "bad argument");
-    if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
-    if (ba_rig(h)) return fail(TSLAM_ESTATE, "inertial factors act on pair windows (not a rig's body window)");
+    if (!h || !record || !v0 || frame < 0) return fail(TSLAM_EINVAL, "bad argument");
+    if (int rc = ine_pair_check(h, pair); rc != TSLAM_OK) return rc;
     std::array<double, TS_BA_INE + 3> f{};
     for (int e = 0; e < 30; ++e) {
         if (!std::isfinite(record[e])) return fail(TSLAM_EINVAL, "non-finite factor record");
@@ -2722,8 +2739,8 @@ int tslam_ba_inertial_factor(tslam_handle* h, int pair, int64_t frame, const dou
 }
 
 int tslam_ba_read_inertial(tslam_handle* h, int pair, double* velocity, double* ba) {
-    if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
-    if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (int rc = ine_pair_check(h, pair); rc != TSLAM_OK) return rc;
     int rc = tslam_sync(h);
     if (rc != TSLAM_OK) return rc;
     const size_t W = h->prm.ba_window;

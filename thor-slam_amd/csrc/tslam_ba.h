@@ -168,6 +168,6 @@ void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming
 // E_p^-1 B), and the joint solve over all pairs (storage pair c.P = the body window)
 void launch_ba_snapshot_rig(const BatchCtx& c, double* dst, hipStream_t s);
 void launch_ba_rig_keyframe(const BatchCtx& c, const BaArgs& a, hipStream_t s);
-void launch_ba_rig_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing);
+void launch_ba_rig_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing, bool inertial = false);
 // one k_ba_schur launch on the window state `a` (measurement replays)
 void launch_ba_schur(const BatchCtx& c, const BaArgs& a, hipStream_t s);

@@ -435,8 +435,8 @@ int tslam_imu_gravity(const tslam_imu* f, double* g) {
 // a = Ri (accel - ba) - w x (w x r) - alpha x r; dp += dv dt + dR a dt^2 / 2,
 // Jp += Jv dt - dR Ri dt^2 / 2, dv += dR a dt, Jv -= dR Ri dt, dR <- dR exp([w dt]x).
 int tslam_imu_preintegrate(const tslam_imu* f, int n, const double* dt, const double* gyro, const double* accel,
-                           const double* bg, const double* ba, const double* w_prev, double v_floor, double p_floor,
-                           double* record) {
+                           const double* bg, const double* ba, const double* w_prev, const double* frame_R_imu,
+                           const double* lever, double v_floor, double p_floor, double* record) {
     if (!f || n < 1 || !dt || !gyro || !accel || !bg || !ba || !record)
         return tslam_internal_fail(TSLAM_EINVAL, "tslam_imu_preintegrate: null argument or n < 1");
     double dR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, Jv[9] = {}, Jp[9] = {};
@@ -444,16 +444,17 @@ int tslam_imu_preintegrate(const tslam_imu* f, int n, const double* dt, const do
     double T = 0.0;
     bool have_prev = w_prev != nullptr;
     V3 wp = have_prev ? v3(w_prev) : V3{0, 0, 0};
-    const V3 r = v3(f->r), bgv = v3(bg), bav = v3(ba);
+    const double* Ri = frame_R_imu ? frame_R_imu : f->Ri;   // the factor's frame (default: the filter's camera)
+    const V3 r = v3(lever ? lever : f->r), bgv = v3(bg), bav = v3(ba);
     double dRRi[9];
     for (int k = 0; k < n; ++k) {
         const double h = dt[k];
         if (!(h > 0.0)) return tslam_internal_fail(TSLAM_EINVAL, "tslam_imu_preintegrate: dt must be > 0");
-        const V3 w = mv(f->Ri, v3(gyro + 3 * k) - bgv);
+        const V3 w = mv(Ri, v3(gyro + 3 * k) - bgv);
         const V3 al = have_prev ? (w - wp) / h : V3{0, 0, 0};
-        const V3 a = mv(f->Ri, v3(accel + 3 * k) - bav) - cross(w, cross(w, r)) - cross(al, r);
+        const V3 a = mv(Ri, v3(accel + 3 * k) - bav) - cross(w, cross(w, r)) - cross(al, r);
         const V3 Ra = mv(dR, a);
-        mm(dR, f->Ri, dRRi);
+        mm(dR, Ri, dRRi);
         dp = dp + dv * h + 0.5 * Ra * h * h;
         for (int e = 0; e < 9; ++e) Jp[e] = Jp[e] + Jv[e] * h - 0.5 * dRRi[e] * h * h;
         dv = dv + Ra * h;

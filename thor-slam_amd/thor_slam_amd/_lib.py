@@ -124,8 +124,8 @@ _SIGNATURES = {
     "tslam_imu_absorb": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P, _P]),
     "tslam_imu_vision_only": (ctypes.c_int, [_P, _P, ctypes.c_double, _P, _P, _P]),
     "tslam_imu_gravity": (ctypes.c_int, [_P, _P]),
-    "tslam_imu_preintegrate": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P, _P, ctypes.c_double, ctypes.c_double,
-                                              _P]),
+    "tslam_imu_preintegrate": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, ctypes.c_double,
+                                              ctypes.c_double, _P]),
     "tslam_last_error": (ctypes.c_char_p, []),
     "tslam_abi_version": (ctypes.c_int, []),
     "tslam_create": (ctypes.c_int, [ctypes.POINTER(StereoDesc), ctypes.POINTER(Params), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),

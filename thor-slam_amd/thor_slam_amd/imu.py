@@ -217,10 +217,11 @@ class ImuPropagator:
         return g
 
     def preintegrate(self, samples: list, bg: np.ndarray, ba: np.ndarray, w_prev: np.ndarray | None = None,
-                     v_floor: float = 1e-2, p_floor: float = 1e-3) -> np.ndarray:
+                     v_floor: float = 1e-2, p_floor: float = 1e-3, frame_R_imu: np.ndarray | None = None,
+                     lever: np.ndarray | None = None) -> np.ndarray:
         """The local BA's inertial factor record (32 doubles, tslam_ba_inertial_factor) of the
-        frame intervals ``samples`` = [(dt, gyro, accel)] between two keyframes
-        (tslam_imu_preintegrate)."""
+        frame intervals ``samples`` = [(dt, gyro, accel)] between two keyframes, in the filter's
+        camera or (``frame_R_imu``, ``lever``) another rigid frame (tslam_imu_preintegrate)."""
         n = len(samples)
         dt = np.ascontiguousarray([float(d) for d, _, _ in samples], dtype=np.float64)
         gy = np.ascontiguousarray([np.asarray(g, dtype=np.float64).reshape(3) for _, g, _ in samples])
@@ -228,9 +229,13 @@ class ImuPropagator:
         bgv = np.ascontiguousarray(bg, dtype=np.float64).reshape(3)
         bav = np.ascontiguousarray(ba, dtype=np.float64).reshape(3)
         wp = None if w_prev is None else np.ascontiguousarray(w_prev, dtype=np.float64).reshape(3)
+        fr = None if frame_R_imu is None else np.ascontiguousarray(frame_R_imu, dtype=np.float64).reshape(9)
+        lv = None if lever is None else np.ascontiguousarray(lever, dtype=np.float64).reshape(3)
         out = np.zeros(32)
         _lib._check(self.lib.tslam_imu_preintegrate(self._f, n, dt.ctypes.data, gy.ctypes.data, ac.ctypes.data,
                                                     bgv.ctypes.data, bav.ctypes.data, None if wp is None else wp.ctypes.data,
+                                                    None if fr is None else fr.ctypes.data,
+                                                    None if lv is None else lv.ctypes.data,
                                                     float(v_floor), float(p_floor), out.ctypes.data))
         return out
 
