@@ -514,6 +514,30 @@ __device__ __forceinline__ void hsum4(const uint8_t* row, int x0, int W, u16x2* 
     *od = __builtin_bit_cast(u16x2, hj[1] | (hj[3] << 16));
 }
 
+// Horizontal 1-4-6-4-1 of an interior quad (4 <= x0, x0 + 8 <= W: no column clamp), `p` = row + x0.
+__device__ __forceinline__ void hsum4_in(const uint8_t* p, u16x2* ev, u16x2* od) {
+    const uint32_t a = *(const uint32_t*)(p - 4), b = *(const uint32_t*)p, c2 = *(const uint32_t*)(p + 4);
+    const uint32_t D0 = __builtin_amdgcn_alignbyte(b, a, 2), D1 = __builtin_amdgcn_alignbyte(b, a, 3);
+    const uint32_t D3 = __builtin_amdgcn_alignbyte(c2, b, 1), D4 = __builtin_amdgcn_alignbyte(c2, b, 2);
+    const uint32_t h0 = __builtin_amdgcn_udot4(D0, 0x04060401u, D1 >> 24, false);
+    const uint32_t h1 = __builtin_amdgcn_udot4(D1, 0x04060401u, b >> 24, false);
+    const uint32_t h2 = __builtin_amdgcn_udot4(b, 0x04060401u, D3 >> 24, false);
+    const uint32_t h3 = __builtin_amdgcn_udot4(D3, 0x04060401u, D4 >> 24, false);
+    *ev = __builtin_bit_cast(u16x2, h0 | (h2 << 16));
+    *od = __builtin_bit_cast(u16x2, h1 | (h3 << 16));
+}
+
+// Vertical 1-4-6-4-1 of five horizontal sums (rows o-2 .. o+2) + rounding, packed to 4 bytes: the
+// rounded sums stay below 2^16, so byte 1 of each u16 lane is the result (one v_perm picks the
+// four: ev lanes -> bytes 0 / 2, od lanes -> bytes 1 / 3).
+__device__ __forceinline__ uint32_t vsum4(u16x2 e0, u16x2 e1, u16x2 e2, u16x2 e3, u16x2 e4, u16x2 d0, u16x2 d1,
+                                          u16x2 d2, u16x2 d3, u16x2 d4) {
+    const u16x2 four = {4, 4}, six = {6, 6}, rnd = {128, 128};
+    const u16x2 ve = six * e2 + (four * (e1 + e3) + ((e0 + e4) + rnd));
+    const u16x2 vo = six * d2 + (four * (d1 + d3) + ((d0 + d4) + rnd));
+    return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, vo), __builtin_bit_cast(uint32_t, ve), 0x07030501u);
+}
+
 // MODE 0: speculative threshold (k_detect); MODE 1: exact fallback at t + 1 for the flagged
 // images (k_detect_fallback, its own symbol so profiles keep the two launches apart)
 // (bx: the band over all levels, img: the view image; the fallback runs only flagged image-levels)
@@ -576,26 +600,54 @@ __device__ __forceinline__ void detect_body(const BatchCtx& c, int bx, int img) 
 
     // 5x5 binomial smoothing of the band rows (column clamp; rows already clamped in LDS).
     if (wide) {
-        // item = (4-pixel quad, 8-row group): 12 horizontal sums (3 dword LDS reads each) slide
-        // through 5 registers; u16 pairs cannot overflow (16 * 16 * 255 + 128 < 2^16)
+        // item = (4-pixel quad, row group): the horizontal sums (3 dword LDS reads + 4 v_dot4
+        // each) slide through 5 register pairs, rotated by unrolling 5 rows (no moves); u16 pairs
+        // cannot overflow (16 * 16 * 255 + 128 < 2^16).  Interior quads (1 .. W4 - 2) need no
+        // column clamp and run without divergence; the two edge quads of each row group follow.
         const int W4 = W >> 2;
-        const u16x2 four = {4, 4}, six = {6, 6}, rnd = {128, 128};
         const int groups = c.g.smooth_groups[l];
         const int SR = (BR + groups - 1) / groups;
-        for (int it = threadIdx.x; it < groups * W4; it += TS_DET_THREADS) {
-            const int half = it / W4, q = it - half * W4, x0 = 4 * q;
+        const int NQ = W4 - 2;
+        for (int it = threadIdx.x; it < groups * NQ; it += TS_DET_THREADS) {
+            const int half = it / NQ, q = 1 + (it - half * NQ), x0 = 4 * q;
             const int o0 = SR * half, o1 = min(o0 + SR, rows_here);   // output rows (band-relative)
+            if (o0 >= o1) continue;
+            const uint8_t* rp = tile + (TS_DET_HALO - 2 + o0) * W + x0;
+            u16x2 e0, e1, e2, e3, e4, d0, d1, d2, d3, d4;
+            hsum4_in(rp, &e0, &d0);
+            hsum4_in(rp + W, &e1, &d1);
+            hsum4_in(rp + 2 * W, &e2, &d2);
+            hsum4_in(rp + 3 * W, &e3, &d3);
+            rp += 4 * W;
+            uint32_t off = (uint32_t)((y0 + o0) * W + x0);
+            int o = o0;
+#define TS_SMOOTH_ROW(A, B, C, D, N, a, b, cc, d, n)                            \
+    {                                                                         \
+        hsum4_in(rp, &N, &n);                                                 \
+        *(uint32_t*)(smo + off) = vsum4(A, B, C, D, N, a, b, cc, d, n);       \
+        rp += W;                                                              \
+        off += (uint32_t)W;                                                   \
+        if (++o == o1) break;                                                 \
+    }
+            for (;;) {
+                TS_SMOOTH_ROW(e0, e1, e2, e3, e4, d0, d1, d2, d3, d4)
+                TS_SMOOTH_ROW(e1, e2, e3, e4, e0, d1, d2, d3, d4, d0)
+                TS_SMOOTH_ROW(e2, e3, e4, e0, e1, d2, d3, d4, d0, d1)
+                TS_SMOOTH_ROW(e3, e4, e0, e1, e2, d3, d4, d0, d1, d2)
+                TS_SMOOTH_ROW(e4, e0, e1, e2, e3, d4, d0, d1, d2, d3)
+            }
+#undef TS_SMOOTH_ROW
+        }
+        for (int it = threadIdx.x; it < groups * 2; it += TS_DET_THREADS) {   // the edge quads (clamped)
+            const int half = it >> 1, x0 = (it & 1) ? 4 * (W4 - 1) : 0;
+            const int o0 = SR * half, o1 = min(o0 + SR, rows_here);
             if (o0 >= o1) continue;
             u16x2 e[5], d[5];
 #pragma unroll
             for (int k = 0; k < 4; ++k) hsum4(tile + (TS_DET_HALO - 2 + o0 + k) * W, x0, W, &e[k], &d[k]);
-#pragma unroll 2   // two rows' LDS reads in flight (528 -> 512 us)
             for (int o = o0; o < o1; ++o) {
                 hsum4(tile + (TS_DET_HALO + 2 + o) * W, x0, W, &e[4], &d[4]);
-                const u16x2 ve = (e[0] + four * e[1] + six * e[2] + four * e[3] + e[4] + rnd) >> 8;
-                const u16x2 vo = (d[0] + four * d[1] + six * d[2] + four * d[3] + d[4] + rnd) >> 8;
-                *(uint32_t*)(smo + (size_t)(y0 + o) * W + x0) =
-                    (uint32_t)ve.x | ((uint32_t)vo.x << 8) | ((uint32_t)ve.y << 16) | ((uint32_t)vo.y << 24);
+                *(uint32_t*)(smo + (size_t)(y0 + o) * W + x0) = vsum4(e[0], e[1], e[2], e[3], e[4], d[0], d[1], d[2], d[3], d[4]);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     e[k] = e[k + 1];
