@@ -389,3 +389,65 @@ def test_engine_ba_inertial_factors():
     assert calls_off == []
     assert len(err_on) == len(err_off) == 8
     assert max(err_on) < max(err_off) + 5e-3, (err_on, err_off)
+
+
+def test_engine_rig_ba_inertial_factors():
+    """A two-source rig with the IMU on source 0 and local BA (the rig's body window): the host
+    preintegrates each keyframe interval in the body frame (tslam_imu_preintegrate with base_R_imu
+    and the IMU's body position) and hands the body window its inertial factors (pair = n_pairs);
+    the body velocities follow the rig's true speed and the keyframe positions stay on the ground
+    truth (no worse than without the factors by more than 5 mm)."""
+    import json
+    from pathlib import Path
+
+    from thor_slam_amd.camera import CameraRig, Extrinsics
+    from thor_slam_amd.camera.types import IMUExtrinsics
+    from thor_slam_amd.params import HipSlamConfig
+    from thor_slam_amd.slam.hip_engine import HipSlamEngine
+    from thor_slam_amd.synthetic import DRB_TO_RDF, RoomScene, SyntheticStereoSource, circle_trajectory
+
+    n = 16
+    names = ("192.168.2.21", "192.168.2.25")
+    mats = json.loads((Path(__file__).parent / "golden" / "brackets_joints.json").read_text())
+
+    def run(inertial: bool):
+        scene, traj = RoomScene(seed=0), circle_trajectory(40)
+        srcs = [SyntheticStereoSource(name=nm, scene=scene, trajectory=traj, rig_T_source=np.array(mats[nm]), seed=k,
+                                      imu=(k == 0)) for k, nm in enumerate(names)]
+        base_T_imu = np.array(mats[names[0]]) @ DRB_TO_RDF
+        rig = CameraRig(srcs, rig_extrinsics={nm: Extrinsics.from_4x4_matrix(np.array(mats[nm])) for nm in names},
+                        imu_source=names[0], imu_extrinsics=IMUExtrinsics(names[0], Extrinsics.from_4x4_matrix(base_T_imu)))
+        rig.start()
+        eng = HipSlamEngine(num_cameras=4, config=HipSlamConfig(batch_size=4, ba_window=4, ba_kf_interval=2, ba_iters=3,
+                                                                enable_loop_closure=False, ba_inertial=inertial))
+        eng.initialize(rig.calibration)
+        calls = []
+        inner = eng._handle.ba_inertial_factor
+        eng._handle.ba_inertial_factor = lambda g, rec, v0, pair=0: (calls.append((g, pair)), inner(g, rec, v0, pair))
+        for _ in range(n):
+            eng.process_frames(rig.get_synchronized_frames())
+        eng.flush()
+        smap = eng.get_map()
+        ine = eng._handle.ba_read_inertial(2) if inertial else None
+        frames = eng._handle.ba_read(2)["frames"]
+        eng.shutdown()
+        pos_err = []
+        for kf in smap.keyframe_poses:
+            k = min(range(n), key=lambda i: abs(srcs[0].timestamp(i) - kf.timestamp))
+            gt = np.linalg.inv(traj[0]) @ traj[k]
+            pos_err.append(np.linalg.norm(kf.to_4x4_matrix()[:3, 3] - gt[:3, 3]))
+        return calls, pos_err, ine, frames, traj, srcs[0]
+
+    calls, err_on, ine, frames, traj, src = run(True)
+    assert calls == [(g, 2) for g in (2, 4, 6, 8, 10, 12, 14)], calls
+    assert np.isfinite(ine["vel"]).all() and np.isfinite(ine["ba"]).all()
+    dt = 1.0 / src.fps
+    for s, g in enumerate(frames):
+        if g <= 0:
+            continue
+        v_true = (traj[int(g) + 1][:3, 3] - traj[int(g) - 1][:3, 3]) / (2 * dt)
+        assert abs(np.linalg.norm(ine["vel"][s]) - np.linalg.norm(v_true)) < 0.05, (g, ine["vel"][s], v_true)
+    calls_off, err_off, _, _, _, _ = run(False)
+    assert calls_off == []
+    assert len(err_on) == len(err_off) > 0
+    assert max(err_on) < max(err_off) + 5e-3, (err_on, err_off)

@@ -326,6 +326,7 @@ class HipSlamEngine(SlamEngine):
         self._kf_ine: tuple | None = None             # samples since the last BA keyframe (list, first frame, w_prev)
         self._prev_stamp: float | None = None      # timestamp of the last submitted frame (IMU dt)
         self._base_R_imu = np.eye(3)
+        self._base_T_imu = np.eye(4)
         self._torch = None
         self._dev_images = None
         self._host_images = None
@@ -384,6 +385,7 @@ class HipSlamEngine(SlamEngine):
             imu = getattr(calibration, "imu_extrinsics", None)   # world(base)_T_imu, RDF-converted by the caller
             base_T_imu = imu.to_4x4_matrix() if imu is not None else np.eye(4)
             self._base_R_imu = base_T_imu[:3, :3]
+            self._base_T_imu = base_T_imu
             self._imu = None
             # the reference fuses the IMU whenever it has one (enable_imu_fusion:=true, Makefile:81)
             fusion = cfg.imu_fusion if cfg.imu_fusion is not None else imu is not None
@@ -721,17 +723,23 @@ class HipSlamEngine(SlamEngine):
                 self._kf_imu = (np.eye(3), 0.0, gk + 1)
 
     def _ba_inertial_factors(self, steps: list, samples: list) -> None:
-        """The local BA's tightly coupled inertial factors (one stereo pair, accelerometer leg):
-        the frame intervals' samples since the last BA keyframe are preintegrated with the
-        filter's current biases (tslam_imu_preintegrate); at each keyframe whose whole interval had
-        samples the record and the keyframe camera's predicted world velocity go to
-        tslam_ba_inertial_factor, and the window gets the filter's gravity and accelerometer-bias
-        prior (tslam_ba_inertial) before the batch is submitted."""
+        """The local BA's tightly coupled inertial factors (accelerometer leg): the frame
+        intervals' samples since the last BA keyframe are preintegrated with the filter's current
+        biases (tslam_imu_preintegrate); at each keyframe whose whole interval had samples the
+        record and the keyframe's predicted world velocity go to tslam_ba_inertial_factor, and the
+        window gets the filter's gravity and accelerometer-bias prior (tslam_ba_inertial) before
+        the batch is submitted.  One stereo pair: in pair 0's rectified-left camera; a rig: in the
+        body (base_link) frame of its body window (pair = n_pairs), the filter's camera-0 vectors
+        rotated into it (the velocity only seeds the solve)."""
         cfg, imu = self._config, self._imu
-        if cfg.ba_window <= 0 or len(self._pairs) != 1 or not cfg.ba_inertial or not imu.accel or not imu.ready:
+        if cfg.ba_window <= 0 or not cfg.ba_inertial or not imu.accel or not imu.ready:
             return
+        rig = len(self._pairs) > 1
+        pair = len(self._pairs) if rig else 0
+        R0 = self._base_T_rects[0][:3, :3]   # base_R_rect0: camera-0 vectors into the body world
         st = imu.st
-        self._handle.ba_inertial(imu.gravity(), st.ba, 1.0 / max(st.var_b, 1e-12))
+        g = imu.gravity()
+        self._handle.ba_inertial(R0 @ g if rig else g, st.ba, 1.0 / max(st.var_b, 1e-12), pair=pair)
         g = self._handle.frames_done
         for k, (step, smp) in enumerate(zip(steps, samples)):
             gk = g + k
@@ -744,8 +752,15 @@ class HipSlamEngine(SlamEngine):
             if gk % cfg.ba_kf_interval == 0:
                 acc = self._kf_ine
                 if acc is not None and acc[1] == gk - cfg.ba_kf_interval + 1 and len(acc[0]) == cfg.ba_kf_interval:
-                    rec = imu.preintegrate(acc[0], st.bg, st.ba, acc[2], cfg.ba_inertial_v_floor, cfg.ba_inertial_p_floor)
-                    self._handle.ba_inertial_factor(gk, rec, step.v1)
+                    if rig:
+                        rec = imu.preintegrate(acc[0], st.bg, st.ba, None if acc[2] is None else R0 @ acc[2],
+                                               cfg.ba_inertial_v_floor, cfg.ba_inertial_p_floor,
+                                               frame_R_imu=self._base_T_imu[:3, :3], lever=self._base_T_imu[:3, 3])
+                        self._handle.ba_inertial_factor(gk, rec, R0 @ step.v1, pair=pair)
+                    else:
+                        rec = imu.preintegrate(acc[0], st.bg, st.ba, acc[2], cfg.ba_inertial_v_floor,
+                                               cfg.ba_inertial_p_floor)
+                        self._handle.ba_inertial_factor(gk, rec, step.v1)
                 self._kf_ine = ([], gk + 1, None if step is None else step.w.copy())
 
     def _set_motion_prior(self, *args) -> None:
