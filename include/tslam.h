@@ -236,6 +236,10 @@ int tslam_sync(tslam_handle* h);
  *   pose), cov[36], ts, state (TSLAM_POSE_*), conf = clamp(1 / (1 + tr(cov[:3,:3])), 0, 1)
  *   (isaac_ros.py:312; 1 when not tracked).  Returns 1 when a newer pose was written, else 0. */
 int tslam_submit_host(tslam_handle* h, const uint8_t* host_images, const double* timestamps, int n_frames);
+/* The pinned staging buffer the next tslam_submit_host copies from (max_batch frames of
+ * frame_bytes each), after waiting until its previous DMA finished: a caller that assembles the
+ * batch's frames there and passes this pointer as host_images saves the staging copy. */
+int tslam_host_stage(tslam_handle* h, uint8_t** stage, int64_t* frame_bytes);
 int tslam_poll_batch(tslam_handle* h, int block, int max_frames, double* T_rel, double* T_abs, double* cov, int32_t* stats,
                      double* rig_T_rel, double* rig_T_abs, double* rig_cov, int32_t* rig_stats, double* ts,
                      int64_t* first_frame, int* n_frames);

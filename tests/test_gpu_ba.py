@@ -246,6 +246,41 @@ def test_ba_inertial_factors_parity():
     assert np.abs(want[-1]["ba"]).max() > 1e-4   # the bias moved off zero
 
 
+def test_ba_inertial_state_resets_and_rejects_bad_input():
+    """tslam_reset clears the window's velocities and accelerometer bias (a new session), and
+    tslam_ba_inertial_factor refuses a non-finite record, dt <= 0 or a negative weight."""
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    n, batch = 12, 3
+    sc, _ = _scenario_and_oracle(n)
+    ine = _inertial_factors(sc, n)
+    h = Handle([sc["rect"]], sc["cfg"], max_batch=batch)
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    try:
+        f, v0 = ine[2]
+        for bad in (np.where(np.arange(f.size) == 3, np.nan, f), np.where(np.arange(f.size) == 27, 0.0, f),
+                    np.where(np.arange(f.size) == 29, -1.0, f)):
+            with pytest.raises(RuntimeError, match="tslam error"):
+                h.ba_inertial_factor(2, bad, v0)
+        with pytest.raises(RuntimeError, match="tslam error"):
+            h.ba_inertial_factor(2, f, np.array([np.inf, 0.0, 0.0]))
+        h.ba_inertial(*INE_CFG)
+        for g, (rec, v) in ine.items():
+            h.ba_inertial_factor(g, rec, v)
+        for b0 in range(0, n, batch):
+            h.submit(dev[b0:].data_ptr(), batch, torch.cuda.current_stream().cuda_stream)
+        got = h.ba_read_inertial(0)
+        assert np.abs(got["ba"]).max() > 0 and np.abs(got["vel"]).max() > 0
+        h.reset()
+        got = h.ba_read_inertial(0)
+        np.testing.assert_array_equal(got["vel"], 0.0)
+        np.testing.assert_array_equal(got["ba"], 0.0)
+    finally:
+        h.close()
+
+
 def test_ba_imu_factor_rejects_non_finite():
     """tslam_ba_imu_factor refuses an infinite / NaN weight or rotation entry (they would poison the
     window's whole Schur system) and leaves the window unchanged."""

@@ -1090,6 +1090,22 @@ static int stash_results(tslam_handle* h, const double* ts, hipStream_t s) {
     return TSLAM_OK;
 }
 
+int tslam_host_stage(tslam_handle* h, uint8_t** stage, int64_t* frame_bytes) {
+    if (!h || !stage) return fail(TSLAM_EINVAL, "bad argument");
+    if (h->sh_world > 1 || h->sh_comm) return fail(TSLAM_ESTATE, "a sharded handle is driven stage by stage");
+    HIPCHK(hipSetDevice(h->device));
+    int rc = ensure_async(h);
+    if (rc != TSLAM_OK) return rc;
+    const int k = (int)(h->as_batches & 1);
+    if (h->as_staged_armed[k]) {
+        HIPCHK(hipEventSynchronize(h->as_staged[k]));
+        h->as_staged_armed[k] = false;
+    }
+    *stage = (uint8_t*)h->as_stage[k];
+    if (frame_bytes) *frame_bytes = host_frame_bytes(h);
+    return TSLAM_OK;
+}
+
 int tslam_submit_host(tslam_handle* h, const uint8_t* host_images, const double* timestamps, int n_frames) {
     if (!h || !host_images) return fail(TSLAM_EINVAL, "bad argument");
     if (n_frames < 1 || n_frames > h->B) return fail(TSLAM_EINVAL, "n_frames must be in [1, max_batch]");
@@ -1101,7 +1117,7 @@ int tslam_submit_host(tslam_handle* h, const uint8_t* host_images, const double*
     const size_t bytes = (size_t)n_frames * host_frame_bytes(h);
     // the staging buffer of this parity is free once the DMA of batch s-2 out of it finished
     if (h->as_staged_armed[k]) HIPCHK(hipEventSynchronize(h->as_staged[k]));
-    memcpy(h->as_stage[k], host_images, bytes);
+    if (host_images != h->as_stage[k]) memcpy(h->as_stage[k], host_images, bytes);   // (tslam_host_stage: in place)
     // the device input of this parity: batch s-2's rectify read it earlier on the same stream
     HIPCHK(hipMemcpyAsync(h->as_input[k], h->as_stage[k], bytes, hipMemcpyHostToDevice, h->as_front));
     HIPCHK(hipEventRecord(h->as_staged[k], h->as_front));
@@ -2073,8 +2089,12 @@ int tslam_loop_auto(tslam_handle* h, int interval) {
     return TSLAM_OK;
 }
 
+// Grows geometrically (and to at least 4 KiB): a job slot's buffer is reallocated O(log) times as
+// the vote window or the pose-graph span grows, not on every job (a pinned allocation and free
+// cost ~0.2 ms of the submitting thread).
 static int pinned_reserve(tslam_handle* h, void** p, size_t* cap, size_t bytes) {
     if (bytes <= *cap) return TSLAM_OK;
+    bytes = std::max({bytes, 2 * *cap, (size_t)4096});
     if (*p) {
         (void)hipHostFree(*p);
         h->host_allocs.erase(std::remove(h->host_allocs.begin(), h->host_allocs.end(), *p), h->host_allocs.end());
@@ -2132,7 +2152,8 @@ int tslam_loop_job_vote(tslam_handle* h, int query, int64_t k0, int n_kf, int64_
     if (rc != TSLAM_OK) return rc;
     const int n = n_kf * h->P;
     j->n_out = n;
-    if ((rc = pinned_reserve(h, &j->out, &j->out_cap, sizeof(int32_t) * std::max(n, 1))) != TSLAM_OK) {
+    // sized for the whole database at once: the vote window grows with every keyframe
+    if ((rc = pinned_reserve(h, &j->out, &j->out_cap, sizeof(int32_t) * std::max(n, h->lp_cap))) != TSLAM_OK) {
         j->kind = 0;
         return rc;
     }

@@ -164,6 +164,7 @@ _SIGNATURES = {
     "tslam_set_rig": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "tslam_set_motion_prior": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "tslam_read_rig_poses": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 4),
+    "tslam_host_stage": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64)]),
     "tslam_submit_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "tslam_poll_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 9
                          + [ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int)]),
@@ -500,6 +501,21 @@ class Handle:
         n = int(images.shape[0])
         ts = None if timestamps is None else np.ascontiguousarray(timestamps, dtype=np.float64)
         _check(self.lib.tslam_submit_host(self.h, images.ctypes.data, None if ts is None else ts.ctypes.data, n))
+
+    def host_stage(self) -> np.ndarray:
+        """The pinned staging buffer of the next submit_host as a [max_batch][frame_bytes] u8 view
+        (tslam_host_stage: waits until its previous DMA finished); frames written there and passed
+        back to submit_host skip the staging copy."""
+        p, fb = ctypes.c_void_p(), ctypes.c_int64()
+        _check(self.lib.tslam_host_stage(self.h, ctypes.byref(p), ctypes.byref(fb)))
+        key = (p.value, fb.value)
+        views = getattr(self, "_stage_views", None)
+        if views is None:
+            views = self._stage_views = {}
+        if key not in views:
+            buf = (ctypes.c_uint8 * (self.max_batch * fb.value)).from_address(p.value)
+            views[key] = np.frombuffer(buf, dtype=np.uint8).reshape(self.max_batch, fb.value)
+        return views[key]
 
     def _poll_buffers(self) -> tuple:
         """Result arrays of tslam_poll_batch, allocated once with their pointers (a non-blocking poll

@@ -507,7 +507,11 @@ class HipSlamEngine(SlamEngine):
                                   cams_per_frame=S)
 
     # ------------------------------------------------------------------------------------------
-    def _frame_images(self, frame_set: SynchronizedFrameSet) -> np.ndarray | None:
+    def _frame_images(self, frame_set: SynchronizedFrameSet, out: np.ndarray | None = None) -> np.ndarray | None:
+        """The frame's input record ([2P][H][W] gray stereo, or [P][5HW] RGB-D), written into
+        ``out`` (one flat row of the library's pinned staging, tslam_host_stage) when given — the
+        batch then needs no stacking or staging copy — else stacked into a new array.  None when a
+        camera of the rig is missing from the set."""
         imgs = []
         if self._config.rgbd:
             for c, d in self._pairs:
@@ -522,7 +526,7 @@ class HipSlamEngine(SlamEngine):
                 if bgr.shape[:2] != (self._rects[0].height, self._rects[0].width) or depth.shape != bgr.shape[:2]:
                     raise ValueError(f"RGB-D camera {c}: colour {bgr.shape} / depth {depth.shape} do not match its calibration")
                 imgs.append(pack_rgbd(bgr, depth.astype(np.uint16, copy=False)))
-            return np.stack(imgs)
+            return np.stack(imgs) if out is None else self._fill(out, imgs)
         for l, r in self._pairs:
             for gi in (l, r):
                 cam = self._cameras[gi]
@@ -533,13 +537,25 @@ class HipSlamEngine(SlamEngine):
                 if img.shape != (self._rects[0].height, self._rects[0].width):
                     raise ValueError(f"camera {gi} image shape {img.shape} does not match its calibration")
                 imgs.append(img)
-        return np.stack(imgs)
+        return np.stack(imgs) if out is None else self._fill(out, imgs)
+
+    @staticmethod
+    def _fill(out: np.ndarray, imgs: list) -> np.ndarray:
+        rows = out.reshape(len(imgs), -1)
+        for i, im in enumerate(imgs):
+            np.copyto(rows[i], np.asarray(im, dtype=np.uint8).reshape(-1))
+        return out
 
     def process_frames(self, frame_set: SynchronizedFrameSet) -> SlamPose | None:
         if self._handle is None:
             raise RuntimeError("Not initialized")
         self._frame_count += 1
-        imgs = self._frame_images(frame_set)
+        if self._shard is None and not self._config.dense_map:   # straight into the pinned staging
+            if not self._staged:
+                self._stage = self._handle.host_stage()
+            imgs = self._frame_images(frame_set, out=self._stage[len(self._staged)])
+        else:
+            imgs = self._frame_images(frame_set)
         if imgs is None:
             with self._pose_lock:
                 return self._latest_pose
@@ -586,7 +602,7 @@ class HipSlamEngine(SlamEngine):
             self._prev_stamp = stamps[-1]
             self._publish(self._read(n), stamps, self._handle.frames_done - n)
             return
-        imgs = self._staged[0][0][None] if n == 1 else np.stack([im for im, _ in self._staged])
+        imgs = self._stage[:n]   # the frames were written there as they were staged (host_stage)
         if self._in_flight >= 2:   # the handle keeps two batches' results: publish the older first
             self._drain(block=True, limit=1)
         self._handle.submit_host(imgs, stamps)
