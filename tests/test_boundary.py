@@ -158,3 +158,17 @@ def test_live_reference_slampose_random(ref_mods):
         b = SlamPose.from_4x4_matrix(m, 1.0)
         np.testing.assert_array_equal(a.rotation, b.rotation)
         np.testing.assert_array_equal(a.to_4x4_matrix(), b.to_4x4_matrix())
+
+
+def test_fast_quaternion_equals_scipy():
+    """The publish path's quaternion (hip_engine._quat_xyzw) is scipy's from_matrix(...).as_quat(),
+    bit for bit, on rotations of every branch (trace and each diagonal element the largest)."""
+    from scipy.spatial.transform import Rotation
+
+    from thor_slam_amd.slam.hip_engine import _quat_xyzw
+
+    rng = np.random.default_rng(0)
+    mats = [Rotation.from_rotvec(rng.normal(0, 1.5, 3)).as_matrix() for _ in range(3000)]
+    mats += [Rotation.from_rotvec(np.pi * np.eye(3)[a] * 0.999).as_matrix() for a in range(3)] + [np.eye(3)]
+    for m in mats:
+        np.testing.assert_array_equal(_quat_xyzw(m), Rotation.from_matrix(m).as_quat())

@@ -49,6 +49,7 @@ from __future__ import annotations
 
 import collections
 import logging
+import math
 import threading
 
 import numpy as np
@@ -88,6 +89,33 @@ def adjoint(t: np.ndarray) -> np.ndarray:
     ad[:3, :3] = ad[3:, 3:] = r
     ad[:3, 3:] = tx @ r
     return ad
+
+
+def _quat_xyzw(m: np.ndarray) -> np.ndarray:
+    """(x, y, z, w) of a rotation matrix — scipy's ``Rotation.from_matrix(m).as_quat()`` formula
+    (the largest of the diagonal and the trace picks the branch; bit-identical on orthonormal input,
+    checked in tests/test_boundary.py) in plain floats: the per-frame publish path avoids scipy's
+    ~30-60 us of validation per call."""
+    m00, m01, m02 = float(m[0, 0]), float(m[0, 1]), float(m[0, 2])
+    m10, m11, m12 = float(m[1, 0]), float(m[1, 1]), float(m[1, 2])
+    m20, m21, m22 = float(m[2, 0]), float(m[2, 1]), float(m[2, 2])
+    tr = m00 + m11 + m22
+    d = (m00, m11, m22, tr)
+    c = max(range(4), key=d.__getitem__)
+    if c == 3:
+        q = [m21 - m12, m02 - m20, m10 - m01, 1.0 + tr]
+    else:
+        M = ((m00, m01, m02), (m10, m11, m12), (m20, m21, m22))
+        i = c
+        j = (i + 1) % 3
+        k = (j + 1) % 3
+        q = [0.0, 0.0, 0.0, 0.0]
+        q[i] = 1.0 - tr + 2.0 * M[i][i]
+        q[j] = M[j][i] + M[i][j]
+        q[k] = M[k][i] + M[i][k]
+        q[3] = M[k][j] - M[j][k]
+    n = math.sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3])
+    return np.array([q[0] / n, q[1] / n, q[2] / n, q[3] / n])
 
 
 def _invert(t: np.ndarray) -> np.ndarray:
@@ -382,6 +410,9 @@ class HipSlamEngine(SlamEngine):
             self._base_T_rects = [self._cameras[l].extrinsics.to_4x4_matrix() @ r.left_optical_T_rect()
                                   for (l, _), r in zip(self._pairs, self._rects)]
             self._base_T_rect = self._base_T_rects[0]
+            self._bt_inv = _invert(self._base_T_rect)        # cached for the per-frame publish path
+            self._prior_moves = None
+            self._bt_ad = adjoint(self._base_T_rect)
             imu = getattr(calibration, "imu_extrinsics", None)   # world(base)_T_imu, RDF-converted by the caller
             base_T_imu = imu.to_4x4_matrix() if imu is not None else np.eye(4)
             self._base_R_imu = base_T_imu[:3, :3]
@@ -688,14 +719,16 @@ class HipSlamEngine(SlamEngine):
         rot = np.tile(np.eye(3), (n, P, 1, 1))
         trn = np.zeros((n, P, 3))
         wr, wt = np.zeros((n, P)), np.zeros((n, P))
-        e0 = self._base_T_rects[0]
+        if getattr(self, "_prior_moves", None) is None:   # (inv(E_p) E_0, inv(E_0), E_p) per pair, once
+            e0 = self._base_T_rects[0]
+            self._prior_moves = [(_invert(ep) @ e0, _invert(e0), ep) for ep in self._base_T_rects]
         for k, st in enumerate(steps):
             if st is None:
                 continue
             t0 = np.eye(4)
             t0[:3, :3], t0[:3, 3] = st.R_rel, st.t_rel
-            for p, ep in enumerate(self._base_T_rects):
-                tp = t0 if p == 0 else _invert(ep) @ e0 @ t0 @ _invert(e0) @ ep
+            for p, (a, ie0, ep) in enumerate(self._prior_moves):
+                tp = t0 if p == 0 else a @ t0 @ ie0 @ ep   # the same products, in the same order, as before
                 rot[k, p], trn[k, p] = tp[:3, :3], tp[:3, 3]
                 wr[k, p], wt[k, p] = st.w_rot, st.w_trans
         self._set_motion_prior(rot, wr, trn, wt)
@@ -892,8 +925,8 @@ class HipSlamEngine(SlamEngine):
         stats = res["stats"][k, :, 0]
         if len(self._pairs) == 1:
             status = int(stats[0])
-            body = bt @ res["T_abs"][k, 0] @ _invert(bt)
-            ad = adjoint(bt)   # camera-frame twist -> base-frame twist (rotation and lever arm)
+            body = bt @ res["T_abs"][k, 0] @ self._bt_inv
+            ad = self._bt_ad   # camera-frame twist -> base-frame twist (rotation and lever arm)
             cov = ad @ res["cov"][k, 0] @ ad.T if status == POSE_OK else np.zeros((6, 6))
             return status, body, cov
         # multi-pair rig: the device's generalised PnP over all pairs (k_rig_pose), already in the
@@ -986,24 +1019,24 @@ class HipSlamEngine(SlamEngine):
         latest = None
         state = self._state
         corr = self._ba_corrections(res, len(stamps), g0)
-        bt = self._base_T_rect
+        bt, bt_inv = self._base_T_rect, self._bt_inv
         for k, ts in enumerate(stamps):
             status, body, cov = self._body_pose(res, k)
             if corr is not None and status != POSE_LOST:   # a rig's correction is in body terms
-                body = corr[k] @ body if len(self._pairs) > 1 else bt @ corr[k] @ res["T_abs"][k, 0] @ _invert(bt)
+                body = corr[k] @ body if len(self._pairs) > 1 else bt @ corr[k] @ res["T_abs"][k, 0] @ bt_inv
             if isinstance(self._loop, _AsyncLoop):   # oracle/numpy_loop.py LoopPolicy.step
                 g = g0 + k
-                raw = _invert(bt) @ body @ bt                      # rect-left world_T_cam before loop correction
+                raw = bt_inv @ body @ bt                           # rect-left world_T_cam before loop correction
                 if status == POSE_OK and g % self._config.loop_kf_interval == 0:
                     self._loop.node(g, raw, ts)
                 self._loop.advance(until=g)
-                body = bt @ self._loop.corr @ raw @ _invert(bt)
+                body = bt @ self._loop.corr @ raw @ bt_inv
             elif self._loop is not None and status != POSE_LOST:
                 g = g0 + k
-                raw = _invert(bt) @ body @ bt                      # rect-left world_T_cam before loop correction
+                raw = bt_inv @ body @ bt                           # rect-left world_T_cam before loop correction
                 if status == POSE_OK and g % self._config.loop_kf_interval == 0:
                     self._loop_keyframe(g, raw, ts)
-                body = bt @ self._loop.corr @ raw @ _invert(bt)
+                body = bt @ self._loop.corr @ raw @ bt_inv
             body = self._map_offset @ body
             if status == POSE_LOST:
                 state = TrackingState.LOST
@@ -1012,7 +1045,7 @@ class HipSlamEngine(SlamEngine):
             state = TrackingState.TRACKING if status == POSE_OK else TrackingState.INITIALIZING
             latest = SlamPose(
                 position=body[:3, 3].copy(),
-                rotation=Rotation.from_matrix(body[:3, :3]).as_quat(),
+                rotation=_quat_xyzw(body),
                 timestamp=ts,
                 tracking_state=state,
                 confidence=confidence_from_covariance(cov) if status == POSE_OK else 1.0,
