@@ -56,18 +56,22 @@ __device__ __forceinline__ uint32_t key_dist(uint32_t key) {   // distance of a 
     return (uint32_t)__uint_as_float(key & 0xFFFF8000u);
 }
 
-__global__ __launch_bounds__(256) void k_match(BatchCtx c) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_match(BatchCtx c) {
     TS_BACK_PRIO;
     // per wave: the compacted-train ring during the walk, then the (best, second) reduction
     __shared__ __attribute__((aligned(16))) uint2 s_red[4][32 * TS_MRED_PITCH];
     __shared__ __attribute__((aligned(16))) uint32_t s_key[2][TS_MQ];  // temporal: (x, thread) sort keys, then the dealt positions
     __shared__ __attribute__((aligned(16))) uint32_t s_wk[4][32];   // per wave: query-index sort keys
-    __shared__ uint4 s_qrec[TS_MQ];       // the block's query records and descriptors (one load round)
-    __shared__ uint4 s_qdesc[2 * TS_MQ];
+    // the block's query records and descriptors (one load round), in the ring's LDS: they are dead
+    // once every wave has built its A operand (the barrier before the walk)
+    uint4* const s_qrec = reinterpret_cast<uint4*>(&s_red[0][0]);
+    uint4* const s_qdesc = s_qrec + TS_MQ;
     __shared__ uint32_t s_sq[4][32];      // per wave slot: query keypoint index (~0: empty slot)
     __shared__ uint32_t s_si[4][32];      // ... its block-local index
-    __shared__ uint32_t s_sg[4][32];      // ... gate word (qy + gy_tol) << 16 | (qx - gx_lo)
-    __shared__ float s_spc[4][32];        // ... |q| (popcount of the descriptor)
+    // ... gate word (qy + gy_tol) << 16 | (qx - gx_lo) and |q| (popcount of the descriptor), by
+    // [wave][slot & 1][slot >> 1]: lane half h reads its 16 accumulator rows as four 16-byte words
+    __shared__ __attribute__((aligned(16))) uint32_t s_sg[4][2][16];
+    __shared__ __attribute__((aligned(16))) float s_spc[4][2][16];
     // blockIdx.y: the temporal blocks (the heavy ones: a window of rows, not a row band) of every
     // frame first, then the stereo blocks, so the short stereo blocks fill the launch's tail
     // (stereo-only launches, match_modes == 1: blockIdx.y = f * P + p, all stereo)
@@ -185,8 +189,8 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
             s_sq[wave][rank] = active ? qi : 0xFFFFFFFFu;
             s_si[wave][rank] = (uint32_t)bi;
             // inactive: 0xFFFF halves fail every gate
-            s_sg[wave][rank] = active ? ((uint32_t)(qy + gy_tol) << 16 | ((uint32_t)(qx - gx_lo) & 0xFFFFu)) : 0xFFFFFFFFu;
-            s_spc[wave][rank] = (float)pc;
+            s_sg[wave][rank & 1][rank >> 1] = active ? ((uint32_t)(qy + gy_tol) << 16 | ((uint32_t)(qx - gx_lo) & 0xFFFFu)) : 0xFFFFFFFFu;
+            s_spc[wave][rank & 1][rank >> 1] = (float)pc;
         }
     }
     // the columns of this wave's queries
@@ -221,14 +225,11 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) qa[s][j] = 0x22222222u | (((w4[j] >> s) & 0x11111111u) << 3);
     }
-    // per accumulator register: the slot's |q| (the MFMA's C) and gate word
-    v16f_t cinit;
-    uint32_t qgate[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        cinit[r] = s_spc[wave][2 * r + h];
-        qgate[r] = s_sg[wave][2 * r + h];
-    }
+    __syncthreads();   // every wave's A operand is built: s_qrec / s_qdesc become ring space
+    // per accumulator register: the slot's |q| (the MFMA's C) and gate word, re-read from LDS per
+    // tile (32 VGPRs fewer across the walk: 4 waves per SIMD instead of 3)
+    const float4* const spc4 = reinterpret_cast<const float4*>(s_spc[wave][h]);
+    const uint4* const sg4 = reinterpret_cast<const uint4*>(s_sg[wave][h]);
     uint32_t best[16], second[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) best[r] = second[r] = 0xFFFFFFFFu;
@@ -245,7 +246,15 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
     uint2* ring = s_red[wave];   // {txy, tidx << 16 | position}; after scoring {tmin, ...}
     auto score = [&](const uint4& d, const uint2& e, uint32_t k, uint32_t n) {
         const uint32_t w4[4] = {d.x, d.y, d.z, d.w};
-        v16f_t acc = cinit;
+        v16f_t acc;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float4 v = spc4[i];
+            acc[4 * i] = v.x;
+            acc[4 * i + 1] = v.y;
+            acc[4 * i + 2] = v.z;
+            acc[4 * i + 3] = v.w;
+        }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             v8i_t a, b;
@@ -266,6 +275,15 @@ __global__ __launch_bounds__(256) void k_match(BatchCtx c) {
         const uint32_t txy = k < n ? e.x : 0x80008000u;   // padding fails every gate
         const uint32_t tidx = e.y >> 16;
         uint32_t tmin = 0xFFFFFFFFu;
+        uint32_t qgate[16];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint4 v = sg4[i];
+            qgate[4 * i] = v.x;
+            qgate[4 * i + 1] = v.y;
+            qgate[4 * i + 2] = v.z;
+            qgate[4 * i + 3] = v.w;
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const uint32_t hb = gate_ok(qgate[r], txy, span) ? __float_as_uint(acc[r]) : 0x7F800000u;
