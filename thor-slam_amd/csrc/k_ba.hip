@@ -6,9 +6,9 @@
 //
 // Per window solve: k_ba_gate gates the observations at the current estimate and counts them per
 // landmark; a tiled scan (k_ba_tilecount, k_ba_tilescatter) keeps landmarks seen >= 2 times,
-// ranks them (compact index) and builds the observation list; k_ba_camobs scatters the camera x
-// landmark table and k_ba_slots turns it into the dense (landmark, camera) slot table that every
-// iteration reads with one level of indexing (and resets the scratch for the next solve).
+// ranks them (compact index) and writes the dense (landmark, camera) slot table that every
+// iteration reads with one level of indexing (k_ba_gate clears the last solve's rows, k_ba_backsub
+// re-zeroes the gate counts).
 // Then per Gauss-Newton iteration:
 //   k_ba_schur   per chunk of 32 landmarks: the previous iteration's landmark update (fused back
 //                substitution), then J_c, J_p, r per observation -> W_o, J_c^T J_c | J_c^T r;
@@ -210,6 +210,9 @@ __global__ __launch_bounds__(256) void k_ba_gate(BatchCtx c, BaArgs a) {
     const int K = c.g.K, p = a.pair, n = a.n_order;
     BaPair q = ba_pair(c, a, p);
     for (int i = threadIdx.x; i < n * 12; i += blockDim.x) s_T[i / 12][i % 12] = q.T[(size_t)a.order[i / 12] * 16 + i % 12];
+    // the slot table back to all -1: the rows the last solve filled (k_ba_tilescatter fills this one's)
+    const int Lp = q.counts[1];
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < Lp * TS_BA_MAXW; t += gridDim.x * blockDim.x) q.lo_o[t] = -1;
     __syncthreads();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n * K) return;
@@ -237,8 +240,10 @@ __global__ __launch_bounds__(256) void k_ba_gate(BatchCtx c, BaArgs a) {
 //   landmark tiles over the ids (flag: >= 2 gated observations) -> compact index li = rank of the
 //   id, lm_id = its inverse;  observation tiles per window camera over its keypoints (flag: gated
 //   and its landmark kept) -> the observation list in (camera, keypoint) order.
-// k_ba_tilecount counts every tile, k_ba_tilescatter scans the counts and writes, k_ba_camobs
-// fills the camera x landmark table.
+// k_ba_tilecount counts every tile (and keeps each landmark tile's flag words), k_ba_tilescatter
+// scans the counts and writes the compact landmarks and the dense slot table directly: an
+// observation's compact landmark index is its id's tile offset + the flagged ids before its word +
+// a popcount in the word.
 #define BA_TILE (256 * BA_SCAN_ITEMS)
 
 struct BaTiles {
@@ -260,9 +265,10 @@ __device__ __forceinline__ void ba_tile_flags(const BatchCtx& c, const BaArgs& a
         *ci_out = -1;
         *k0_out = i0;
 #pragma unroll
-        for (int it = 0; it < BA_SCAN_ITEMS; ++it) {
+        for (int it = 0; it < BA_SCAN_ITEMS; ++it) {   // unconditional (clamped) loads, no branches
             ids[it] = i0 + it;
-            fl[it] = i0 + it < NID && q.cnt[i0 + it] >= 2;
+            const int cn = q.cnt[min(i0 + it, NID - 1)];
+            fl[it] = i0 + it < NID && cn >= 2;
         }
     } else {
         const int bb = b - t.n_lm_tiles, ci = bb / t.per_cam;
@@ -270,15 +276,20 @@ __device__ __forceinline__ void ba_tile_flags(const BatchCtx& c, const BaArgs& a
         *ci_out = ci;
         *k0_out = k0;
         const size_t base = (size_t)a.order[ci] * K;
+        // the items' gate bytes and ids first, then the count gathers (a kept observation has an id)
+        uint32_t kp[BA_SCAN_ITEMS];
+        int lmv[BA_SCAN_ITEMS];
 #pragma unroll
         for (int it = 0; it < BA_SCAN_ITEMS; ++it) {
-            const int k = k0 + it;
-            ids[it] = -1;
-            fl[it] = 0;
-            if (k < K && q.keep[ci * K + k]) {
-                ids[it] = q.lm[base + k];
-                fl[it] = q.cnt[ids[it]] >= 2;
-            }
+            const int k = min(k0 + it, K - 1);
+            kp[it] = k0 + it < K ? q.keep[ci * K + k] : 0u;
+            lmv[it] = q.lm[base + k];
+        }
+#pragma unroll
+        for (int it = 0; it < BA_SCAN_ITEMS; ++it) {
+            const int cn = q.cnt[kp[it] ? lmv[it] : 0];
+            ids[it] = kp[it] ? lmv[it] : -1;
+            fl[it] = kp[it] && cn >= 2;
         }
     }
 }
@@ -286,14 +297,33 @@ __device__ __forceinline__ void ba_tile_flags(const BatchCtx& c, const BaArgs& a
 __global__ __launch_bounds__(256) void k_ba_tilecount(BatchCtx c, BaArgs a) {
     BA_PRIO;
     __shared__ int s_tmp[32];
+    __shared__ __attribute__((aligned(4))) uint8_t s_fl[256];   // thread t's flags: bits 8t .. 8t+7 of the tile
     BaPair q = ba_pair(c, a, a.pair);
     int fl[BA_SCAN_ITEMS], ids[BA_SCAN_ITEMS], ci, k0, cnt = 0;
     ba_tile_flags(c, a, q, blockIdx.x, fl, ids, &ci, &k0);
+    uint32_t bits = 0;
 #pragma unroll
-    for (int it = 0; it < BA_SCAN_ITEMS; ++it) cnt += fl[it];
+    for (int it = 0; it < BA_SCAN_ITEMS; ++it) {
+        cnt += fl[it];
+        bits |= (uint32_t)fl[it] << it;
+    }
+    s_fl[threadIdx.x] = (uint8_t)bits;
     int tot;
-    block_scan_excl(cnt, s_tmp, &tot);
+    block_scan_excl(cnt, s_tmp, &tot);   // its barriers order the s_fl stores
     if (threadIdx.x == 0) q.tiles[blockIdx.x] = tot;
+    // a landmark tile's 64 flag words and the flagged ids before each (wave 0: a word per lane)
+    if (ci < 0 && threadIdx.x < 64) {
+        const uint32_t w = reinterpret_cast<const uint32_t*>(s_fl)[threadIdx.x];
+        const int pc = __popc(w);
+        int x = pc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if ((int)threadIdx.x >= o) x += y;
+        }
+        q.lmask[blockIdx.x * 64 + threadIdx.x] = w;
+        q.lpre[blockIdx.x * 64 + threadIdx.x] = x - pc;
+    }
 }
 
 // Scatter after the tile counts; each block takes its tile's offset from the counts of the tiles
@@ -303,16 +333,25 @@ __global__ __launch_bounds__(256) void k_ba_tilescatter(BatchCtx c, BaArgs a) {
     BA_PRIO;
     __shared__ int s_tmp[32];
     __shared__ int s_cnt[TS_BA_TILES];
+    __shared__ int s_lbase[TS_BA_TILES];   // compact index of each landmark tile's first flagged id
     BaPair q = ba_pair(c, a, a.pair);
     const BaTiles t = ba_tiles(c, a);
     const int ntiles = t.n_lm_tiles + a.n_order * t.per_cam;
     for (int j = threadIdx.x; j < ntiles; j += blockDim.x) s_cnt[j] = q.tiles[j];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int run = 0;
+        for (int b = 0; b < t.n_lm_tiles; ++b) {
+            s_lbase[b] = run;
+            run += s_cnt[b];
+        }
+    }
     int fl[BA_SCAN_ITEMS], ids[BA_SCAN_ITEMS], ci, k0, cnt = 0;
     ba_tile_flags(c, a, q, blockIdx.x, fl, ids, &ci, &k0);
 #pragma unroll
     for (int it = 0; it < BA_SCAN_ITEMS; ++it) cnt += fl[it];
     int tot;
-    const int within = block_scan_excl(cnt, s_tmp, &tot);   // its barriers order the s_cnt stores
+    const int within = block_scan_excl(cnt, s_tmp, &tot);   // its barriers order the s_lbase stores
     const int first = (int)blockIdx.x < t.n_lm_tiles ? 0 : t.n_lm_tiles;
     int base = 0;
     for (int j = first; j < (int)blockIdx.x; ++j) base += s_cnt[j];   // LDS broadcast reads
@@ -329,64 +368,54 @@ __global__ __launch_bounds__(256) void k_ba_tilescatter(BatchCtx c, BaArgs a) {
         q.counts[0] = run;
     }
     int pos = base + within;
-    if (ci < 0) {
-        const int NID = a.W * c.g.K;
+    // every item's loads are issued before the first store (indices clamped for the unflagged
+    // ones), so a thread waits on one round of gathers instead of one per item
+    if (ci < 0) {   // compact landmark pos: its id and its position during the solve
+        double x[BA_SCAN_ITEMS][3];
 #pragma unroll
         for (int it = 0; it < BA_SCAN_ITEMS; ++it) {
-            if (k0 + it < NID) q.li[k0 + it] = fl[it] ? pos : -1;
-            if (fl[it]) q.lm_id[pos++] = k0 + it;
+            const size_t id = fl[it] ? (size_t)(k0 + it) : 0;
+#pragma unroll
+            for (int e = 0; e < 3; ++e) x[it][e] = q.X[id * 3 + e];
         }
-    } else {
 #pragma unroll
         for (int it = 0; it < BA_SCAN_ITEMS; ++it)
             if (fl[it]) {
-                q.obs_cam[pos] = ci;
-                q.obs_k[pos] = k0 + it;
-                q.obs_id[pos] = ids[it];
+                q.lm_id[pos] = k0 + it;
+#pragma unroll
+                for (int e = 0; e < 3; ++e) q.Xc[(size_t)pos * 3 + e] = x[it][e];
                 ++pos;
             }
-    }
-}
-
-__global__ __launch_bounds__(256) void k_ba_camobs(BatchCtx c, BaArgs a) {
-    BA_PRIO;
-    BaPair q = ba_pair(c, a, a.pair);
-    const int o = blockIdx.x * blockDim.x + threadIdx.x;
-    if (o >= q.counts[0]) return;
-    q.camobs[(size_t)q.obs_cam[o] * a.W * c.g.K + q.li[q.obs_id[o]]] = o;
-}
-
-// The solve's dense slot table: slot s = r * TS_BA_MAXW + ci of compact landmark r and window
-// camera ci gets its observation index (or -1) and (u, v, d); Xc[r] = X[lm_id[r]].  Resets the
-// camobs entries it reads and the gate counts, so neither needs a memset before the next solve.
-__global__ __launch_bounds__(256) void k_ba_slots(BatchCtx c, BaArgs a) {
-    BA_PRIO;
-    BaPair q = ba_pair(c, a, a.pair);
-    const int K = c.g.K, WK = a.W * K;
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < WK) q.cnt[t] = 0;   // read by the tile kernels only, which have run
-    const int L = q.counts[1];
-    const int r = t / TS_BA_MAXW, ci = t - r * TS_BA_MAXW;
-    if (r >= L) return;
-    int o = -1;
-    if (ci < a.n_order) {
-        int32_t* e = q.camobs + (size_t)ci * WK + r;
-        o = *e;
-        if (o >= 0) *e = -1;
-    }
-    q.lo_o[t] = o;
-    if (o >= 0) {
-        const size_t so = (size_t)a.order[ci] * K + q.obs_k[o];
-        double* uvd = q.lo_uvd + (size_t)t * 4;
-        uvd[0] = q.u[so];
-        uvd[1] = q.v[so];
-        uvd[2] = q.d[so];
-        uvd[3] = 0.0;
-    }
-    if (ci == 0) {
-        const int id = q.lm_id[r];
+    } else {   // observation pos of window camera ci: its slot (compact landmark r, ci) and (u, v, d)
+        const size_t ob = (size_t)a.order[ci] * c.g.K;
+        uint32_t mw[BA_SCAN_ITEMS];
+        int pw[BA_SCAN_ITEMS], rb[BA_SCAN_ITEMS];
+        double uvd[BA_SCAN_ITEMS][3];
 #pragma unroll
-        for (int e = 0; e < 3; ++e) q.Xc[(size_t)r * 3 + e] = q.X[(size_t)id * 3 + e];
+        for (int it = 0; it < BA_SCAN_ITEMS; ++it) {
+            const int id = fl[it] ? ids[it] : 0;
+            const int tl = id / BA_TILE, item = id - tl * BA_TILE, w = tl * 64 + (item >> 5);
+            mw[it] = q.lmask[w] & ((1u << (item & 31)) - 1u);
+            pw[it] = q.lpre[w];
+            rb[it] = s_lbase[tl];
+            const size_t so = fl[it] ? ob + k0 + it : ob;
+            uvd[it][0] = q.u[so];
+            uvd[it][1] = q.v[so];
+            uvd[it][2] = q.d[so];
+        }
+#pragma unroll
+        for (int it = 0; it < BA_SCAN_ITEMS; ++it)
+            if (fl[it]) {
+                const int r = rb[it] + pw[it] + __popc(mw[it]);
+                const size_t sl = (size_t)r * TS_BA_MAXW + ci;
+                q.lo_o[sl] = pos;
+                double* d = q.lo_uvd + sl * 4;
+                d[0] = uvd[it][0];
+                d[1] = uvd[it][1];
+                d[2] = uvd[it][2];
+                d[3] = 0.0;
+                ++pos;
+            }
     }
 }
 
@@ -504,7 +533,7 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
         const int nl = min(BA_CHUNK, L - l0);
         lds_barrier();
         BST(0);
-        // every global read of the chunk is one level of indexing (the k_ba_slots table), issued
+        // every global read of the chunk is one level of indexing (the slot table of k_ba_tilescatter), issued
         // up front: slot (li, ci) = thread / TS_BA_MAXW, thread % TS_BA_MAXW; landmark li = thread
         const int li = threadIdx.x / TS_BA_MAXW, ci = threadIdx.x - li * TS_BA_MAXW;
         const int r = l0 + li;
@@ -1320,6 +1349,7 @@ __global__ __launch_bounds__(256) void k_ba_backsub(BatchCtx c, BaArgs a) {
     const int WK = a.W * c.g.K;
     BaPair q = ba_pair(c, a, a.pair);
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid < WK) q.cnt[gid] = 0;   // the gate counts, for the next solve (the tile kernels have run)
     const int r = gid >> 4, ci = gid & 15;
     const int L = q.counts[1];
     if ((r & ~15) >= L) return;   // whole 16-landmark groups exit together
@@ -1403,13 +1433,10 @@ void launch_ba_schur(const BatchCtx& c, const BaArgs& a, hipStream_t s) {
 static void launch_ba_prepare(const BatchCtx& c, const BaArgs& a, hipStream_t s) {
     // grids sized for the window's maximum (counts live on the device; threads past them exit)
     const int WK = a.W * c.g.K;
-    const int nb = (WK + 255) / 256;
     hipLaunchKernelGGL(k_ba_gate, dim3((a.n_order * c.g.K + 255) / 256), dim3(256), 0, s, c, a);
     const int ntiles = (WK + BA_TILE - 1) / BA_TILE + a.n_order * ((c.g.K + BA_TILE - 1) / BA_TILE);
     hipLaunchKernelGGL(k_ba_tilecount, dim3(ntiles), dim3(256), 0, s, c, a);
     hipLaunchKernelGGL(k_ba_tilescatter, dim3(ntiles), dim3(256), 0, s, c, a);
-    hipLaunchKernelGGL(k_ba_camobs, dim3(nb), dim3(256), 0, s, c, a);
-    hipLaunchKernelGGL(k_ba_slots, dim3((WK * TS_BA_MAXW + 255) / 256), dim3(256), 0, s, c, a);
 }
 
 // One linearisation of pair a.pair: the Schur pass (+ iteration it - 1's landmark update when

@@ -408,9 +408,9 @@ static int alloc_ba(tslam_handle* h) {
         {(void**)&b.v, 8 * P * WK},          {(void**)&b.d, 8 * P * WK},         {(void**)&b.lm, 4 * P * WK},
         {(void**)&b.X, 8 * P * WK * 3},      {(void**)&b.kf_desc, 32 * P * WK},  {(void**)&b.gid, 8 * P * WK},
         {(void**)&b.remap, 4 * P * K},       {(void**)&b.cnt, 4 * P * WK},
-        {(void**)&b.li, 4 * P * WK},         {(void**)&b.lm_id, 4 * P * WK},     {(void**)&b.keep, P * WK},
-        {(void**)&b.camobs, 4 * P * W * WK}, {(void**)&b.obs_Vg, 8 * P * WK * 9}, {(void**)&b.obs_cam, 4 * P * WK},
-        {(void**)&b.obs_k, 4 * P * WK},      {(void**)&b.obs_id, 4 * P * WK},    {(void**)&b.cam_off, 4 * P * (W + 1)},
+        {(void**)&b.lm_id, 4 * P * WK},      {(void**)&b.keep, P * WK},          {(void**)&b.obs_Vg, 8 * P * WK * 9},
+        {(void**)&b.lmask, 4 * P * (WK / 32 + 64)}, {(void**)&b.lpre, 4 * P * (WK / 32 + 64)},
+        {(void**)&b.cam_off, 4 * P * (W + 1)},
         {(void**)&b.counts, 4 * 4 * P},      {(void**)&b.tiles, 4 * P * 2 * TS_BA_TILES}, {(void**)&b.done, 4 * P},
         {(void**)&b.lo_o, 4 * P * WK * M},   {(void**)&b.lo_uvd, 32 * P * WK * M}, {(void**)&b.lo_W, 8 * 18 * P * WK * M},
         {(void**)&b.Xc, 8 * P * WK * 3},
@@ -425,9 +425,10 @@ static int alloc_ba(tslam_handle* h) {
         if (rc != TSLAM_OK) return rc;
     }
     // scratch kept in its between-solves state by the kernels themselves (no per-solve memsets):
-    // camobs all -1 (k_ba_slots resets the entries k_ba_camobs set), remap all 0x7F7F7F7F
-    // (k_ba_insert refills it after an eviction), cnt zero (dev_alloc; k_ba_slots re-zeroes it)
-    HIPCHK(hipMemset(b.camobs, 0xFF, 4 * P * W * WK));
+    // the slot table all -1 (k_ba_gate clears the rows the last solve filled), remap all
+    // 0x7F7F7F7F (k_ba_insert refills it after an eviction), cnt zero (dev_alloc; k_ba_backsub
+    // re-zeroes it)
+    HIPCHK(hipMemset(b.lo_o, 0xFF, 4 * P * WK * M));
     HIPCHK(hipMemset(b.remap, 0x7F, 4 * P * K));
     HIPCHK(hipDeviceSynchronize());
     h->ba_icfg.assign(h->P + 1, std::array<double, 8>{});   // pair windows + a rig's body window

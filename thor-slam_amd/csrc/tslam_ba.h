@@ -45,22 +45,20 @@ struct BaStore {
     // scratch (sizes for W*K landmarks/observations)
     int32_t* remap;    // [K] (0x7F7F7F7F between evictions: k_ba_insert refills it)
     int32_t* cnt;      // [WK] observations per landmark id (after the gate; zero between solves)
-    int32_t* li;       // [WK] compact index per id or -1
     int32_t* lm_id;    // [WK] id per compact index
     uint8_t* keep;     // [W*K] gate result per (window camera, keypoint)
-    int32_t* camobs;   // [W][WK] observation index of (window camera, compact landmark) or -1
-                       // (all -1 between solves: k_ba_slots resets what k_ba_camobs set)
-    int32_t* obs_cam;  // [WK] window position of the observing keyframe (0 = oldest)
-    int32_t* obs_k;    // [WK]
-    int32_t* obs_id;   // [WK]
+    // per landmark tile (k_ba_tilecount): the ids' flags (>= 2 gated observations), 32 per word,
+    // and the flagged ids of the tile before each word — the compact index of any id in O(1)
+    uint32_t* lmask;   // [WK / 32 + 64]
+    int32_t* lpre;     // [WK / 32 + 64]
     int32_t* cam_off;  // [W+1]
     int32_t* counts;   // [P][4] n_obs, L, solve ok, pad
     int32_t* tiles;    // [2][TS_BA_TILES] tile counts, tile offsets
     int32_t* done;     // [P] blocks of k_ba_reduce_solve counted in (zero between launches)
-    // per (compact landmark r, window camera ci) slot s = r * TS_BA_MAXW + ci (k_ba_slots): the
-    // observation index or -1, its (u, v, d), and W_o of the last linearisation — every per-
+    // per (compact landmark r, window camera ci) slot s = r * TS_BA_MAXW + ci (k_ba_tilescatter):
+    // the observation index or -1, its (u, v, d), and W_o of the last linearisation — every per-
     // iteration read of the Schur pass is one level of indexing
-    int32_t* lo_o;     // [WK * MAXW]
+    int32_t* lo_o;     // [WK * MAXW] (all -1 outside a solve's rows: k_ba_gate clears the last solve's)
     double* lo_uvd;    // [WK * MAXW][4]  u, v, d, 0
     double* lo_W;      // [WK * MAXW][18] W_o = J_c^T J_p (6x3, row-major)
     double* Xc;        // [WK][3] position of compact landmark r during the solve (X[lm_id[r]] after it)
@@ -113,7 +111,8 @@ struct BaPair {
     double* X;
     uint32_t* kf_desc;
     int64_t* gid;
-    int32_t *remap, *cnt, *li, *lm_id, *camobs, *obs_cam, *obs_k, *obs_id, *cam_off, *counts, *tiles, *lo_o, *done;
+    int32_t *remap, *cnt, *lm_id, *lpre, *cam_off, *counts, *tiles, *lo_o, *done;
+    uint32_t* lmask;
     uint8_t* keep;
     double *lo_uvd, *lo_W, *Xc, *obs_Vg, *lm_L, *lm_gp, *part, *C, *cam_U, *dc, *flops;
     double* imu;
@@ -134,9 +133,9 @@ __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, in
     q.kf_desc = s.kf_desc + p * WK * 8;
     q.gid = s.gid + p * WK;
     // per-pair scratch (strides: ba_scratch_sizes in tslam_api.cpp)
-    q.remap = s.remap + p * K; q.cnt = s.cnt + p * WK; q.li = s.li + p * WK; q.lm_id = s.lm_id + p * WK;
-    q.keep = s.keep + p * WK; q.camobs = s.camobs + p * W * WK;
-    q.obs_cam = s.obs_cam + p * WK; q.obs_k = s.obs_k + p * WK; q.obs_id = s.obs_id + p * WK;
+    q.remap = s.remap + p * K; q.cnt = s.cnt + p * WK; q.lm_id = s.lm_id + p * WK;
+    q.keep = s.keep + p * WK;
+    q.lmask = s.lmask + p * (WK / 32 + 64); q.lpre = s.lpre + p * (WK / 32 + 64);
     q.cam_off = s.cam_off + p * (W + 1);
     q.counts = s.counts + 4 * p;
     q.tiles = s.tiles + p * 2 * TS_BA_TILES;
