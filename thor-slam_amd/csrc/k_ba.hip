@@ -4,10 +4,11 @@
 // landmark homes slot*K + k with re-homing on eviction, stereo reprojection residuals, Schur
 // complement on the cameras, Gauss-Newton with Levenberg damping, gauge = oldest keyframe).
 //
-// Per window solve: k_ba_gate gates the observations at the current estimate and counts them per
+// Per window solve: k_ba_insert_gate inserts the new keyframe (after k_ba_evict_* re-homed the
+// evicted slot's landmarks), gates the observations at the current estimate and counts them per
 // landmark; a tiled scan (k_ba_tilecount, k_ba_tilescatter) keeps landmarks seen >= 2 times,
 // ranks them (compact index) and writes the dense (landmark, camera) slot table that every
-// iteration reads with one level of indexing (k_ba_gate clears the last solve's rows, k_ba_backsub
+// iteration reads with one level of indexing (k_ba_insert_gate clears the last solve's rows, k_ba_backsub
 // re-zeroes the gate counts).
 // Then per Gauss-Newton iteration:
 //   k_ba_schur   per chunk of 32 landmarks: the previous iteration's landmark update (fused back
@@ -95,80 +96,6 @@ __global__ __launch_bounds__(256) void k_ba_evict_move(BatchCtx c, BaArgs a) {
     }
 }
 
-// Insertion of frame a.frame into slot a.slot (every block derives the pose; block 0 stores it).
-__global__ __launch_bounds__(256) void k_ba_insert(BatchCtx c, BaArgs a) {
-    BA_PRIO;
-    __shared__ double s_T[16];   // new keyframe's cam_T_world
-    const int K = c.g.K, p = a.pair;
-    BaPair q = ba_pair(c, a, p);
-    const int64_t g = a.frame;
-    const int f = (int)(g - c.g0);                  // frame of the current batch
-    const int rslot = ring_slot(c, g);
-    if (threadIdx.x == 0 && a.pose_given) {   // rig-level A8: E_p^-1 B set by k_ba_rig_insert
-        for (int e = 0; e < 16; ++e) s_T[e] = q.T[(size_t)a.slot * 16 + e];
-        if (blockIdx.x == 0)
-            for (int e = 0; e < 16; ++e) q.Tfe[(size_t)a.slot * 16 + e] = a.fe[(size_t)(f * c.P + p) * 16 + e];
-    } else if (threadIdx.x == 0) {
-        const double* Tfe = a.fe + (size_t)(f * c.P + p) * 16;   // world_T_cam (front-end snapshot)
-        double Twc[16];
-        if (a.prev < 0) {
-            for (int e = 0; e < 16; ++e) Twc[e] = Tfe[e];
-        } else {
-            // W_ba(prev) * inv(W_fe(prev)) * W_fe(g)
-            double Wba[16], ifp[16], tmp[16];
-            inv_rigid(q.T + (size_t)a.prev * 16, Wba);
-            inv_rigid(q.Tfe + (size_t)a.prev * 16, ifp);
-            mul4(Wba, ifp, tmp);
-            mul4(tmp, Tfe, Twc);
-        }
-        double Tcw[16];
-        inv_rigid(Twc, Tcw);
-        for (int e = 0; e < 16; ++e) s_T[e] = Tcw[e];
-        if (blockIdx.x == 0)
-            for (int e = 0; e < 16; ++e) {
-                q.Tfe[(size_t)a.slot * 16 + e] = Tfe[e];
-                q.T[(size_t)a.slot * 16 + e] = Tcw[e];
-            }
-    }
-    if (blockIdx.x == 0 && threadIdx.x < 10) q.imu[(size_t)a.slot * 10 + threadIdx.x] = a.imu[threadIdx.x];
-    if (blockIdx.x == 0 && threadIdx.x < TS_BA_INE) q.ine[(size_t)a.slot * TS_BA_INE + threadIdx.x] = a.ine[threadIdx.x];
-    if (blockIdx.x == 0 && threadIdx.x < 3) q.vel[(size_t)a.slot * 3 + threadIdx.x] = a.vel0[threadIdx.x];
-    __syncthreads();
-    const PairCalib cal = c.calib[p];
-    const double* disp = c.disp + ((size_t)rslot * c.P + p) * K;
-    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x) {
-        q.remap[k] = 0x7F7F7F7F;   // for the next eviction (k_ba_evict_* have run)
-        double u = __builtin_nan(""), v = __builtin_nan("");
-        const bool valid = kp_obs(c, rslot, c.cpp * p, k, &u, &v);
-        const double dd = disp[k];
-        const bool has_d = __builtin_isfinite(dd) && dd > 0.0;
-        int lm = -1;
-        if (valid && a.prev >= 0) {
-            int j = k;   // chain the temporal matches back to the previous keyframe
-            for (int st = 0; st < a.interval && j >= 0; ++st)
-                j = c.temporal[((size_t)ring_slot(c, g - st) * c.P + p) * K + j];
-            if (j >= 0) lm = q.lm[(size_t)a.prev * K + j];
-        }
-        if (valid && lm < 0 && has_d) {
-            lm = a.slot * K + k;
-            q.gid[lm] = g * K + k;
-            const double z = cal.fxb / dd;
-            const double xc[3] = {(u - cal.cx) * z / cal.fx, (v - cal.cy) * z / cal.fy, z};
-            for (int e = 0; e < 3; ++e)   // R^T (xc - t)
-                q.X[(size_t)lm * 3 + e] = ((s_T[e] * (xc[0] - s_T[3]) + s_T[4 + e] * (xc[1] - s_T[7])) + s_T[8 + e] * (xc[2] - s_T[11]));
-        }
-        const size_t o = (size_t)a.slot * K + k;
-        const uint4* dsrc = reinterpret_cast<const uint4*>(c.desc + (((size_t)rslot * c.C + c.cpp * p) * K + k) * 8);
-        uint4* ddst = reinterpret_cast<uint4*>(q.kf_desc + o * 8);
-        ddst[0] = dsrc[0];
-        ddst[1] = dsrc[1];
-        q.u[o] = valid ? u : __builtin_nan("");
-        q.v[o] = valid ? v : __builtin_nan("");
-        q.d[o] = has_d ? dd : __builtin_nan("");
-        q.lm[o] = lm;
-    }
-}
-
 // ---------------------------------------------------------------------------------------------
 // observation set of a solve (one block): gate at the current estimate, >= 2 observations per
 // landmark, compact landmark index (= rank of the id), camera x landmark observation table
@@ -202,34 +129,121 @@ __device__ int block_scan_excl(int v, int* s_tmp, int* total) {
     return r;
 }
 
-// Gate every observation of the window at the current estimate (positive depth, reprojection
-// error <= outlier_px); count the gated observations per landmark (cnt pre-zeroed).
-__global__ __launch_bounds__(256) void k_ba_gate(BatchCtx c, BaArgs a) {
+// Insertion of frame a.frame into slot a.slot, fused with the gate of the solve that follows (one
+// launch instead of two).  a.order is the solve's window (the new slot is in it).  Every block
+// derives the new keyframe's pose (block 0 stores it); a thread of the new slot's items inserts its
+// keypoint — landmark by the chained temporal matches to the previous keyframe, else a new one from
+// the disparity — and gates that observation from its registers; the other items are gated as
+// stored (positive depth, reprojection error <= outlier_px) and every gated observation counts
+// towards its landmark (cnt pre-zeroed).  No other item reads what an inserting thread writes: the
+// new slot's landmarks are observed by the new keyframe only (eviction re-homed the slot's old ones).
+__global__ __launch_bounds__(256) void k_ba_insert_gate(BatchCtx c, BaArgs a) {
     BA_PRIO;
-    __shared__ double s_T[TS_BA_MAXW][12];
+    __shared__ double s_T[TS_BA_MAXW][12];   // cam_T_world of the window
+    __shared__ double s_Tn[16];              // the new keyframe's
     const int K = c.g.K, p = a.pair, n = a.n_order;
     BaPair q = ba_pair(c, a, p);
-    for (int i = threadIdx.x; i < n * 12; i += blockDim.x) s_T[i / 12][i % 12] = q.T[(size_t)a.order[i / 12] * 16 + i % 12];
+    const int64_t g = a.frame;
+    const int f = (int)(g - c.g0);   // frame of the current batch
+    const int rslot = ring_slot(c, g);
+    if (threadIdx.x == 0 && a.pose_given) {   // rig-level A8: E_p^-1 B set by k_ba_rig_insert
+        for (int e = 0; e < 16; ++e) s_Tn[e] = q.T[(size_t)a.slot * 16 + e];
+        if (blockIdx.x == 0)
+            for (int e = 0; e < 16; ++e) q.Tfe[(size_t)a.slot * 16 + e] = a.fe[(size_t)(f * c.P + p) * 16 + e];
+    } else if (threadIdx.x == 0) {
+        const double* Tfe = a.fe + (size_t)(f * c.P + p) * 16;   // world_T_cam (front-end snapshot)
+        double Twc[16];
+        if (a.prev < 0) {
+            for (int e = 0; e < 16; ++e) Twc[e] = Tfe[e];
+        } else {
+            // W_ba(prev) * inv(W_fe(prev)) * W_fe(g)
+            double Wba[16], ifp[16], tmp[16];
+            inv_rigid(q.T + (size_t)a.prev * 16, Wba);
+            inv_rigid(q.Tfe + (size_t)a.prev * 16, ifp);
+            mul4(Wba, ifp, tmp);
+            mul4(tmp, Tfe, Twc);
+        }
+        double Tcw[16];
+        inv_rigid(Twc, Tcw);
+        for (int e = 0; e < 16; ++e) s_Tn[e] = Tcw[e];
+        if (blockIdx.x == 0)
+            for (int e = 0; e < 16; ++e) {
+                q.Tfe[(size_t)a.slot * 16 + e] = Tfe[e];
+                q.T[(size_t)a.slot * 16 + e] = Tcw[e];
+            }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 10) q.imu[(size_t)a.slot * 10 + threadIdx.x] = a.imu[threadIdx.x];
+    if (blockIdx.x == 0 && threadIdx.x < TS_BA_INE) q.ine[(size_t)a.slot * TS_BA_INE + threadIdx.x] = a.ine[threadIdx.x];
+    if (blockIdx.x == 0 && threadIdx.x < 3) q.vel[(size_t)a.slot * 3 + threadIdx.x] = a.vel0[threadIdx.x];
     // the slot table back to all -1: the rows the last solve filled (k_ba_tilescatter fills this one's)
     const int Lp = q.counts[1];
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < Lp * TS_BA_MAXW; t += gridDim.x * blockDim.x) q.lo_o[t] = -1;
     __syncthreads();
+    for (int i = threadIdx.x; i < n * 12; i += blockDim.x)
+        s_T[i / 12][i % 12] = a.order[i / 12] == a.slot ? s_Tn[i % 12] : q.T[(size_t)a.order[i / 12] * 16 + i % 12];
+    __syncthreads();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n * K) return;
     const PairCalib cal = c.calib[p];
-    const double lim = a.outlier_px * a.outlier_px;
     const int ci = i / K, k = i - ci * K;
     const size_t o = (size_t)a.order[ci] * K + k;
-    const int id = q.lm[o];
+    int id;
+    double u, v, X[3];
+    if (a.order[ci] == a.slot) {   // insert keypoint k of the new keyframe
+        q.remap[k] = 0x7F7F7F7F;   // for the next eviction (k_ba_evict_* have run)
+        u = __builtin_nan("");
+        v = __builtin_nan("");
+        const bool valid = kp_obs(c, rslot, c.cpp * p, k, &u, &v);
+        const double dd = c.disp[((size_t)rslot * c.P + p) * K + k];
+        const bool has_d = __builtin_isfinite(dd) && dd > 0.0;
+        int lm = -1;
+        if (valid && a.prev >= 0) {
+            int j = k;   // chain the temporal matches back to the previous keyframe
+            for (int st = 0; st < a.interval && j >= 0; ++st)
+                j = c.temporal[((size_t)ring_slot(c, g - st) * c.P + p) * K + j];
+            if (j >= 0) lm = q.lm[(size_t)a.prev * K + j];
+        }
+        if (valid && lm < 0 && has_d) {
+            lm = a.slot * K + k;
+            q.gid[lm] = g * K + k;
+            const double z = cal.fxb / dd;
+            const double xc[3] = {(u - cal.cx) * z / cal.fx, (v - cal.cy) * z / cal.fy, z};
+            for (int e = 0; e < 3; ++e) {   // R^T (xc - t)
+                X[e] = ((s_Tn[e] * (xc[0] - s_Tn[3]) + s_Tn[4 + e] * (xc[1] - s_Tn[7])) + s_Tn[8 + e] * (xc[2] - s_Tn[11]));
+                q.X[(size_t)lm * 3 + e] = X[e];
+            }
+        } else if (lm >= 0) {
+            for (int e = 0; e < 3; ++e) X[e] = q.X[(size_t)lm * 3 + e];
+        }
+        const uint4* dsrc = reinterpret_cast<const uint4*>(c.desc + (((size_t)rslot * c.C + c.cpp * p) * K + k) * 8);
+        uint4* ddst = reinterpret_cast<uint4*>(q.kf_desc + o * 8);
+        ddst[0] = dsrc[0];
+        ddst[1] = dsrc[1];
+        if (!valid) {
+            u = __builtin_nan("");
+            v = __builtin_nan("");
+        }
+        q.u[o] = u;
+        q.v[o] = v;
+        q.d[o] = has_d ? dd : __builtin_nan("");
+        q.lm[o] = lm;
+        id = lm;
+    } else {
+        id = q.lm[o];
+        u = q.u[o];
+        v = q.v[o];
+        if (id >= 0)
+            for (int e = 0; e < 3; ++e) X[e] = q.X[(size_t)id * 3 + e];
+    }
     int keep = 0;
     if (id >= 0) {
         const double* T = s_T[ci];
-        const double* X = q.X + (size_t)id * 3;
+        const double lim = a.outlier_px * a.outlier_px;
         const double xc = ((T[0] * X[0] + T[1] * X[1]) + T[2] * X[2]) + T[3];
         const double yc = ((T[4] * X[0] + T[5] * X[1]) + T[6] * X[2]) + T[7];
         const double zc = ((T[8] * X[0] + T[9] * X[1]) + T[10] * X[2]) + T[11];
         const double pu = cal.fx * xc / zc + cal.cx, pv = cal.fy * yc / zc + cal.cy;
-        const double du = pu - q.u[o], dv = pv - q.v[o];
+        const double du = pu - u, dv = pv - v;
         keep = zc > 0.0 && du * du + dv * dv <= lim;
         if (keep) atomicAdd(&q.cnt[id], 1);
     }
@@ -1415,12 +1429,11 @@ void launch_ba_snapshot(const BatchCtx& c, double* dst, hipStream_t s) {
 
 void launch_ba_keyframe(const BatchCtx& c, const BaArgs& a, bool evict, hipStream_t s) {
     const int K = c.g.K;
-    if (evict) {
+    if (evict) {   // the insertion itself is the first launch of the solve (k_ba_insert_gate)
         const int nb = (a.n_order * K + 255) / 256;
         hipLaunchKernelGGL(k_ba_evict_min, dim3(nb), dim3(256), 0, s, c, a);
         hipLaunchKernelGGL(k_ba_evict_move, dim3(nb), dim3(256), 0, s, c, a);
     }
-    hipLaunchKernelGGL(k_ba_insert, dim3((K + 255) / 256), dim3(256), 0, s, c, a);
 }
 
 void launch_ba_schur(const BatchCtx& c, const BaArgs& a, hipStream_t s) {
@@ -1433,7 +1446,7 @@ void launch_ba_schur(const BatchCtx& c, const BaArgs& a, hipStream_t s) {
 static void launch_ba_prepare(const BatchCtx& c, const BaArgs& a, hipStream_t s) {
     // grids sized for the window's maximum (counts live on the device; threads past them exit)
     const int WK = a.W * c.g.K;
-    hipLaunchKernelGGL(k_ba_gate, dim3((a.n_order * c.g.K + 255) / 256), dim3(256), 0, s, c, a);
+    hipLaunchKernelGGL(k_ba_insert_gate, dim3((a.n_order * c.g.K + 255) / 256), dim3(256), 0, s, c, a);
     const int ntiles = (WK + BA_TILE - 1) / BA_TILE + a.n_order * ((c.g.K + BA_TILE - 1) / BA_TILE);
     hipLaunchKernelGGL(k_ba_tilecount, dim3(ntiles), dim3(256), 0, s, c, a);
     hipLaunchKernelGGL(k_ba_tilescatter, dim3(ntiles), dim3(256), 0, s, c, a);

@@ -425,7 +425,7 @@ static int alloc_ba(tslam_handle* h) {
         if (rc != TSLAM_OK) return rc;
     }
     // scratch kept in its between-solves state by the kernels themselves (no per-solve memsets):
-    // the slot table all -1 (k_ba_gate clears the rows the last solve filled), remap all
+    // the slot table all -1 (k_ba_insert_gate clears the rows the last solve filled), remap all
     // 0x7F7F7F7F (k_ba_insert refills it after an eviction), cnt zero (dev_alloc; k_ba_backsub
     // re-zeroes it)
     HIPCHK(hipMemset(b.lo_o, 0xFF, 4 * P * WK * M));
@@ -492,21 +492,25 @@ static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const doub
             h->ba_ine_slot[h->P][a.slot] = has && a.ine[28] > 0.0;
             launch_ba_rig_keyframe(c, a, s);
         }
+        // per pair: the keyframe's IMU rotation factor, inertial factor and initial velocity (zero
+        // for a rig's pairs), inserted by the solve's first launch (k_ba_insert_gate)
+        std::vector<std::array<double, 10 + TS_BA_INE + 3>> kfi((size_t)h->P);
         for (int p = 0; p < h->P; ++p) {
             a.pair = p;
+            auto& v = kfi[(size_t)p];
             auto it = h->ba_imu.find({p, g});   // the keyframe's IMU rotation factor (if given)
-            for (int e = 0; e < 10; ++e) a.imu[e] = (!rig && it != h->ba_imu.end()) ? it->second[e] : 0.0;
+            for (int e = 0; e < 10; ++e) v[e] = (!rig && it != h->ba_imu.end()) ? it->second[e] : 0.0;
             if (it != h->ba_imu.end()) h->ba_imu.erase(it);
             auto jt = h->ba_ine.find({p, g});   // and its inertial factor + initial velocity
             const bool has = !rig && jt != h->ba_ine.end();
-            for (int e = 0; e < TS_BA_INE; ++e) a.ine[e] = has ? jt->second[e] : 0.0;
-            for (int e = 0; e < 3; ++e) a.vel0[e] = has ? jt->second[TS_BA_INE + e] : 0.0;
+            for (int e = 0; e < TS_BA_INE + 3; ++e) v[10 + e] = has ? jt->second[e] : 0.0;
             if (jt != h->ba_ine.end()) h->ba_ine.erase(jt);
-            h->ba_ine_slot[p][a.slot] = has && a.ine[28] > 0.0;
-            launch_ba_keyframe(c, a, evict, s);
+            h->ba_ine_slot[p][a.slot] = has && v[10 + 28] > 0.0;
+            launch_ba_keyframe(c, a, evict, s);   // eviction only
         }
         for (int e = 0; e < 10; ++e) a.imu[e] = 0.0;
         for (int e = 0; e < TS_BA_INE; ++e) a.ine[e] = 0.0;
+        for (int e = 0; e < 3; ++e) a.vel0[e] = 0.0;
         for (auto it = h->ba_imu.begin(); it != h->ba_imu.end();)   // factors of frames already past
             it = it->first.second < g ? h->ba_imu.erase(it) : std::next(it);
         for (auto it = h->ba_ine.begin(); it != h->ba_ine.end();)
@@ -529,6 +533,10 @@ static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const doub
         }
         for (int p = 0; p < h->P; ++p) {
             a.pair = p;
+            const auto& v = kfi[(size_t)p];
+            for (int e = 0; e < 10; ++e) a.imu[e] = v[e];
+            for (int e = 0; e < TS_BA_INE; ++e) a.ine[e] = v[10 + e];
+            for (int e = 0; e < 3; ++e) a.vel0[e] = v[10 + TS_BA_INE + e];
             for (int e = 0; e < 8; ++e) a.icfg[e] = h->ba_icfg[p][e];
             // the inertial kernels when a factor links two keyframes of the window (the oldest
             // keyframe's factor points out of it)

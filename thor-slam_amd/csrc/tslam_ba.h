@@ -58,7 +58,7 @@ struct BaStore {
     // per (compact landmark r, window camera ci) slot s = r * TS_BA_MAXW + ci (k_ba_tilescatter):
     // the observation index or -1, its (u, v, d), and W_o of the last linearisation — every per-
     // iteration read of the Schur pass is one level of indexing
-    int32_t* lo_o;     // [WK * MAXW] (all -1 outside a solve's rows: k_ba_gate clears the last solve's)
+    int32_t* lo_o;     // [WK * MAXW] (all -1 outside a solve's rows: k_ba_insert_gate clears the last solve's)
     double* lo_uvd;    // [WK * MAXW][4]  u, v, d, 0
     double* lo_W;      // [WK * MAXW][18] W_o = J_c^T J_p (6x3, row-major)
     double* Xc;        // [WK][3] position of compact landmark r during the solve (X[lm_id[r]] after it)
