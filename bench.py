@@ -704,7 +704,7 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     # --front-priority 1 it is a high-priority stream, so the back kernels fill the gaps around it
     stream = (torch.cuda.Stream(priority=-1) if args.front_priority and args.pipeline else torch.cuda.current_stream())
     if args.front_cu_reserve < 0:
-        args.front_cu_reserve = 64 if c4 else 0
+        args.front_cu_reserve = 96 if c4 else 0
     masked = c4 and args.front_cu_reserve > 0 and args.pipeline
     if masked:   # C4: the front / back kernels kept off the last CUs, which stay free for the BA chain
         stream = cu_masked_stream(dev_index, args.front_cu_reserve, -1 if args.front_priority else 0)
@@ -1353,8 +1353,9 @@ def main() -> None:
                     help="1: front and back kernels on two streams (batch s+1's front overlaps batch s's back)")
     ap.add_argument("--front-cu-reserve", type=int, default=-1,
                     help="C4: keep the front / back kernels off the last N CUs (left to the BA chain); "
-                         "-1 = the C4 default, 64 (round 4 sweep: 0 / 32 / 48 / 64 / 80 / 96 / 128 CUs -> 15.1k / "
-                         "15.6k / 15.7k / 16.2k / 15.9k / 16.2k / 16.0k frames/s)")
+                         "-1 = the C4 default, 96 (round 5 sweep after the BA preparation changes: 32 / 64 / 96 / "
+                         "128 CUs -> 16.9k / 17.55k / 17.66k / 17.48k frames/s; round 4: 0 / 32 / 48 / 64 / 80 / 96 / "
+                         "128 -> 15.1k / 15.6k / 15.7k / 16.2k / 15.9k / 16.2k / 16.0k)")
     ap.add_argument("--back-cu", type=int, default=0,
                     help="experiment (c2/c3): the back kernels on a stream restricted to N CUs spread over the chip")
     ap.add_argument("--split-cu", type=int, default=0,

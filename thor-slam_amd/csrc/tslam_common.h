@@ -45,7 +45,8 @@
 #define TS_MAX_SPLITS 32   // RANSAC blocks per frame
 #define TS_RANSAC_WORDS 26 // per split: key + pad + 12 doubles
 #define TS_PRIOR_DOUBLES 16 // per (frame, pair): IMU prior R (row-major 3x3), W_r, t[3], W_t, 0, 0
-#define TS_BA_CU_RESERVE 64   // CUs the front / back streams leave to the BA stream (tslam_submit_host)
+#define TS_BA_CU_RESERVE 96   // CUs the front / back streams leave to the BA stream (tslam_submit_host;
+                              // bench.py --front-cu-reserve sweep)
 // Wave issue priority of the back kernels (match .. chain, rig pose): latency-bound waves that share
 // the SIMDs with the next batch's front-end waves (detect, describe: throughput-bound) get served
 // first (C2 234.7-235.3k -> 235.6-235.9k frames/s, C3 59.75k -> 60.05k; the front kernels at
