@@ -246,6 +246,46 @@ def test_ba_inertial_factors_parity():
     assert np.abs(want[-1]["ba"]).max() > 1e-4   # the bias moved off zero
 
 
+def test_ba_two_pairs_own_factors_parity():
+    """Two independent stereo pairs (no rig) fed the same frames, each window with its own
+    keyframe factors — pair 0 IMU rotation + inertial factors, pair 1 other rotation factors only —
+    each against its own oracle window to 1e-9 through evictions.  The keyframe insertion runs in
+    each pair's solve launch (k_ba_insert_gate), so this pins that every pair's factors reach its
+    own window and nothing leaks from one pair into the other."""
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    n, batch = 12, 3
+    sc, _ = _scenario_and_oracle(n)
+    imu0, imu1 = _imu_factors(sc, n), _imu_factors(sc, n, angle=-2e-3, weight=5e4)
+    ine = _inertial_factors(sc, n)
+    want = (_oracle_windows(sc, imu0, ine), _oracle_windows(sc, imu1))
+    frames = np.ascontiguousarray(np.concatenate([sc["frames"], sc["frames"]], axis=1))   # [n][4][H][W]
+    dev = torch.from_numpy(frames).cuda()
+    h = Handle([sc["rect"], sc["rect"]], sc["cfg"], max_batch=batch)
+    try:
+        h.ba_inertial(*INE_CFG, pair=0)
+        for g, (M, w) in imu0.items():
+            h.ba_imu_factor(g, M, w, pair=0)
+        for g, (M, w) in imu1.items():
+            h.ba_imu_factor(g, M, w, pair=1)
+        for g, (f, v0) in ine.items():
+            h.ba_inertial_factor(g, f, v0, pair=0)
+        for b0 in range(0, n, batch):
+            h.submit(dev[b0:].data_ptr(), batch, torch.cuda.current_stream().cuda_stream)
+            for p in (0, 1):
+                _compare(h.ba_read(p), want[p][b0 + batch - 1], f"pair {p}, after frame {b0 + batch - 1}")
+            gi, wk = h.ba_read_inertial(0), want[0][b0 + batch - 1]
+            occ = wk["frames"] >= 0
+            assert np.abs(gi["vel"][occ] - wk["vel"][occ]).max() < 1e-9 * np.abs(wk["vel"][occ]).max()
+    finally:
+        h.close()
+    a0, a1 = want[0][-1], want[1][-1]
+    occ = a0["frames"] >= 0
+    assert max(rel_frobenius(a0["T_cw"][s_], a1["T_cw"][s_]) for s_ in np.nonzero(occ)[0]) > 1e-7   # the windows differ
+
+
 def test_ba_inertial_state_resets_and_rejects_bad_input():
     """tslam_reset clears the window's velocities and accelerometer bias (a new session), and
     tslam_ba_inertial_factor refuses a non-finite record, dt <= 0 or a negative weight."""
