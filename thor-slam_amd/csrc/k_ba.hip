@@ -197,10 +197,8 @@ __global__ __launch_bounds__(256) void k_ba_insert_gate(BatchCtx c, BaArgs a) {
         const double dd = c.disp[((size_t)rslot * c.P + p) * K + k];
         const bool has_d = __builtin_isfinite(dd) && dd > 0.0;
         int lm = -1;
-        if (valid && a.prev >= 0) {
-            int j = k;   // chain the temporal matches back to the previous keyframe
-            for (int st = 0; st < a.interval && j >= 0; ++st)
-                j = c.temporal[((size_t)ring_slot(c, g - st) * c.P + p) * K + j];
+        if (valid && a.prev >= 0) {   // the temporal matches chained back to the previous keyframe
+            const int j = a.kf_assoc[((size_t)f * c.P + p) * K + k];
             if (j >= 0) lm = q.lm[(size_t)a.prev * K + j];
         }
         if (valid && lm < 0 && has_d) {
@@ -1425,6 +1423,26 @@ __global__ __launch_bounds__(256) void k_ba_snapshot(BatchCtx c, double* dst) {
 
 void launch_ba_snapshot(const BatchCtx& c, double* dst, hipStream_t s) {
     hipLaunchKernelGGL(k_ba_snapshot, dim3((c.n * c.P * 16 + 255) / 256), dim3(256), 0, s, c, dst);
+}
+
+// Keypoint k of every keyframe g (g % iv == 0) of the batch chained through the temporal matches
+// of frames g, g - 1, .., g - iv + 1 to its keypoint in frame g - iv (-1 where a link is missing):
+// the association k_ba_insert_gate needs, computed on the stream of the batch's last stage beside
+// the pose snapshot, so the BA chain itself starts from one load instead of iv dependent ones.
+__global__ __launch_bounds__(256) void k_ba_kf_assoc(BatchCtx c, int32_t* dst, int iv) {
+    const int K = c.g.K;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= c.n * c.P * K) return;
+    const int f = i / (c.P * K), r = i - f * c.P * K, p = r / K, k = r - p * K;
+    const int64_t g = c.g0 + f;
+    if (g % iv != 0) return;
+    int j = k;
+    for (int st = 0; st < iv && j >= 0; ++st) j = c.temporal[((size_t)ring_slot(c, g - st) * c.P + p) * K + j];
+    dst[i] = j;
+}
+
+void launch_ba_kf_assoc(const BatchCtx& c, int32_t* dst, int iv, hipStream_t s) {
+    hipLaunchKernelGGL(k_ba_kf_assoc, dim3((c.n * c.P * c.g.K + 255) / 256), dim3(256), 0, s, c, dst, iv);
 }
 
 void launch_ba_keyframe(const BatchCtx& c, const BaArgs& a, bool evict, hipStream_t s) {

@@ -418,6 +418,7 @@ static int alloc_ba(tslam_handle* h) {
         {(void**)&b.part, 8 * P * (size_t)TS_BA_SPLIT * TS_BA_PART}, {(void**)&b.cam_U, 8 * P * W * 27}, {(void**)&b.dc, 8 * P * W * 6},
         {(void**)&b.flops, 8},               {(void**)&b.fe_pose, 8 * 2 * (size_t)h->B * h->P * 16},
         {(void**)&b.fe_body, 8 * 2 * (size_t)h->B * 16}, {(void**)&b.imu, 8 * P * W * 10},
+        {(void**)&b.kf_assoc, 4 * 2 * (size_t)h->B * h->P * K},
         {(void**)&b.ine, 8 * P * W * TS_BA_INE}, {(void**)&b.vel, 8 * P * W * 3}, {(void**)&b.ine_ba, 8 * P * 4},
     };
     for (const A& a : list) {
@@ -467,12 +468,14 @@ static bool ba_rig(const tslam_handle* h) { return h->rig && h->P > 1 && h->prm.
 // evicting the oldest when the window is full, and the window is solved (per pair, or for a rig
 // one joint body solve: launch_ba_rig_solve).  Host bookkeeping of the slots only; nothing
 // synchronises.  `fe_body`: the rig front end's snapshot of the batch (rig-level A8).
-static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const double* fe, const double* fe_body) {
+static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const double* fe, const double* fe_body,
+                   const int32_t* kf_assoc) {
     const int W = h->prm.ba_window, iv = h->prm.ba_kf_interval;
     for (int64_t g = c.g0; g < c.g0 + c.n; ++g) {
         if (g % iv != 0 || g <= h->ba_last) continue;
         BaArgs a = ba_args(h);
         a.fe = fe;
+        a.kf_assoc = kf_assoc;
         a.frame = g;
         a.slot = (int)(h->ba_nkf % W);
         int ord[TS_BA_MAXW];
@@ -663,8 +666,10 @@ static int ba_stage(tslam_handle* h, const BatchCtx& c, hipStream_t s) {
     const int par = (int)(h->batch_idx & 1);
     double* snap = h->ba.fe_pose + (size_t)par * h->B * h->P * 16;
     double* snap_body = h->ba.fe_body + (size_t)par * h->B * 16;
+    int32_t* assoc = h->ba.kf_assoc + (size_t)par * h->B * h->P * h->g.K;
     hipStream_t fs = h->last_stream;
     launch_ba_snapshot(c, snap, fs);
+    launch_ba_kf_assoc(c, assoc, h->prm.ba_kf_interval, fs);
     if (ba_rig(h)) launch_ba_snapshot_rig(c, snap_body, fs);
     const bool other = s != fs;
     if (other) {
@@ -676,7 +681,7 @@ static int ba_stage(tslam_handle* h, const BatchCtx& c, hipStream_t s) {
         HIPCHK(hipEventRecord(h->ev_fe, fs));
         HIPCHK(hipStreamWaitEvent(s, h->ev_fe, 0));
     }
-    run_ba(h, c, s, snap, snap_body);
+    run_ba(h, c, s, snap, snap_body, assoc);
     if (other) {
         HIPCHK(hipEventRecord(h->ev_ba[par], s));
         h->ba_pending[par] = true;
@@ -1343,9 +1348,11 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
             if (h->prm.ba_window) {
                 double* snap = h->ba.fe_pose + (size_t)(h->batch_idx & 1) * h->B * h->P * 16;
                 double* snap_body = h->ba.fe_body + (size_t)(h->batch_idx & 1) * h->B * 16;
+                int32_t* assoc = h->ba.kf_assoc + (size_t)(h->batch_idx & 1) * h->B * h->P * h->g.K;
                 launch_ba_snapshot(c, snap, s);
+                launch_ba_kf_assoc(c, assoc, h->prm.ba_kf_interval, s);
                 if (ba_rig(h)) launch_ba_snapshot_rig(c, snap_body, s);
-                run_ba(h, c, s, snap, snap_body);
+                run_ba(h, c, s, snap, snap_body, assoc);
             }
             break;
         case TSLAM_KERNEL_RIG:

@@ -72,6 +72,8 @@ struct BaStore {
     double* flops;     // [1] algorithmic Schur-product flops accumulated (profiling)
     double* fe_pose;   // [2][B][P][16] front-end world_T_cam of the batch (snapshot per batch parity)
     double* fe_body;   // [2][B][16] rig front end's world_T_body of the batch (rig-level A8)
+    int32_t* kf_assoc; // [2][B][P][K] a keyframe's keypoint chained by the temporal matches back to
+                       // frame g - interval (or -1), written beside the pose snapshot (k_ba_kf_assoc)
     double* imu;       // [P][W][10] IMU rotation factor per slot: M (row-major 9), weight (0 = none)
     double* ine;       // [P][W][TS_BA_INE] inertial factor per slot (from the previous keyframe)
     double* vel;       // [P][W][3] world velocity of each slot's camera
@@ -94,6 +96,7 @@ struct BaArgs {
     double lam, outlier_px;
     const double* fe;           // insert: this batch's front-end pose snapshot [B][P][16]
     const double* fe_body;      // rig insert: the rig front end's snapshot [B][16]
+    const int32_t* kf_assoc;    // insert: this batch's chained temporal matches [B][P][K]
     double imu[10];             // insert: the keyframe's IMU rotation factor (M 9, weight; 0 = none)
     double ine[TS_BA_INE];      // insert: the keyframe's inertial factor (wv = 0: none)
     double vel0[3];             // insert: its camera's initial world velocity
@@ -153,6 +156,8 @@ __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, in
 }
 
 void launch_ba_snapshot(const BatchCtx& c, double* dst, hipStream_t s);
+// the batch's keyframes' temporal-match chains back to the previous keyframe frame (interval iv)
+void launch_ba_kf_assoc(const BatchCtx& c, int32_t* dst, int iv, hipStream_t s);
 void launch_ba_keyframe(const BatchCtx& c, const BaArgs& a, bool evict, hipStream_t s);
 // timing: when non-null, an event pair is recorded around every k_ba_schur launch (profiling)
 struct BaTiming {
