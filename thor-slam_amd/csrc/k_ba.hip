@@ -257,6 +257,7 @@ __global__ __launch_bounds__(256) void k_ba_insert_gate(BatchCtx c, BaArgs a) {
 // observation's compact landmark index is its id's tile offset + the flagged ids before its word +
 // a popcount in the word.
 #define BA_TILE (256 * BA_SCAN_ITEMS)
+static_assert(BA_TILE == 2048 && BA_SCAN_ITEMS == 8, "tc_ids / tc_fl layout (tslam_ba.h)");
 
 struct BaTiles {
     int n_lm_tiles, per_cam;   // landmark tiles; observation tiles per camera
@@ -320,6 +321,13 @@ __global__ __launch_bounds__(256) void k_ba_tilecount(BatchCtx c, BaArgs a) {
         bits |= (uint32_t)fl[it] << it;
     }
     s_fl[threadIdx.x] = (uint8_t)bits;
+    // this thread's flags and (observation tiles) ids for the scatter
+    q.tc_fl[blockIdx.x * 256 + threadIdx.x] = (uint8_t)bits;
+    if (ci >= 0) {
+        int4* dst = reinterpret_cast<int4*>(q.tc_ids + (size_t)blockIdx.x * BA_TILE + threadIdx.x * BA_SCAN_ITEMS);
+        dst[0] = int4{ids[0], ids[1], ids[2], ids[3]};
+        dst[1] = int4{ids[4], ids[5], ids[6], ids[7]};
+    }
     int tot;
     block_scan_excl(cnt, s_tmp, &tot);   // its barriers order the s_fl stores
     if (threadIdx.x == 0) q.tiles[blockIdx.x] = tot;
@@ -358,8 +366,28 @@ __global__ __launch_bounds__(256) void k_ba_tilescatter(BatchCtx c, BaArgs a) {
             run += s_cnt[b];
         }
     }
+    // the tile count's flags and ids (k_ba_tilecount stored them; same tiles, same threads)
     int fl[BA_SCAN_ITEMS], ids[BA_SCAN_ITEMS], ci, k0, cnt = 0;
-    ba_tile_flags(c, a, q, blockIdx.x, fl, ids, &ci, &k0);
+    {
+        const int b = blockIdx.x;
+        if (b < t.n_lm_tiles) {
+            ci = -1;
+            k0 = b * BA_TILE + threadIdx.x * BA_SCAN_ITEMS;
+#pragma unroll
+            for (int it = 0; it < BA_SCAN_ITEMS; ++it) ids[it] = k0 + it;
+        } else {
+            const int bb = b - t.n_lm_tiles;
+            ci = bb / t.per_cam;
+            k0 = (bb - ci * t.per_cam) * BA_TILE + threadIdx.x * BA_SCAN_ITEMS;
+            const int4* src = reinterpret_cast<const int4*>(q.tc_ids + (size_t)b * BA_TILE + threadIdx.x * BA_SCAN_ITEMS);
+            const int4 u0 = src[0], u1 = src[1];
+            ids[0] = u0.x; ids[1] = u0.y; ids[2] = u0.z; ids[3] = u0.w;
+            ids[4] = u1.x; ids[5] = u1.y; ids[6] = u1.z; ids[7] = u1.w;
+        }
+        const uint32_t bits = q.tc_fl[b * 256 + threadIdx.x];
+#pragma unroll
+        for (int it = 0; it < BA_SCAN_ITEMS; ++it) fl[it] = (bits >> it) & 1u;
+    }
 #pragma unroll
     for (int it = 0; it < BA_SCAN_ITEMS; ++it) cnt += fl[it];
     int tot;

@@ -410,6 +410,7 @@ static int alloc_ba(tslam_handle* h) {
         {(void**)&b.remap, 4 * P * K},       {(void**)&b.cnt, 4 * P * WK},
         {(void**)&b.lm_id, 4 * P * WK},      {(void**)&b.keep, P * WK},          {(void**)&b.obs_Vg, 8 * P * WK * 9},
         {(void**)&b.lmask, 4 * P * (WK / 32 + 64)}, {(void**)&b.lpre, 4 * P * (WK / 32 + 64)},
+        {(void**)&b.tc_fl, P * TS_BA_TILES * 256},  {(void**)&b.tc_ids, 4 * P * TS_BA_TILES * 2048},
         {(void**)&b.cam_off, 4 * P * (W + 1)},
         {(void**)&b.counts, 4 * 4 * P},      {(void**)&b.tiles, 4 * P * 2 * TS_BA_TILES}, {(void**)&b.done, 4 * P},
         {(void**)&b.lo_o, 4 * P * WK * M},   {(void**)&b.lo_uvd, 32 * P * WK * M}, {(void**)&b.lo_W, 8 * 18 * P * WK * M},

@@ -51,6 +51,10 @@ struct BaStore {
     // and the flagged ids of the tile before each word — the compact index of any id in O(1)
     uint32_t* lmask;   // [WK / 32 + 64]
     int32_t* lpre;     // [WK / 32 + 64]
+    // k_ba_tilecount's per-thread results for k_ba_tilescatter: each thread's 8 flags (a byte) and,
+    // in observation tiles, its 8 landmark ids — the scatter reads them instead of re-deriving them
+    uint8_t* tc_fl;    // [TS_BA_TILES][256]
+    int32_t* tc_ids;   // [TS_BA_TILES][2048]
     int32_t* cam_off;  // [W+1]
     int32_t* counts;   // [P][4] n_obs, L, solve ok, pad
     int32_t* tiles;    // [2][TS_BA_TILES] tile counts, tile offsets
@@ -116,6 +120,8 @@ struct BaPair {
     int64_t* gid;
     int32_t *remap, *cnt, *lm_id, *lpre, *cam_off, *counts, *tiles, *lo_o, *done;
     uint32_t* lmask;
+    uint8_t* tc_fl;
+    int32_t* tc_ids;
     uint8_t* keep;
     double *lo_uvd, *lo_W, *Xc, *obs_Vg, *lm_L, *lm_gp, *part, *C, *cam_U, *dc, *flops;
     double* imu;
@@ -139,6 +145,7 @@ __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, in
     q.remap = s.remap + p * K; q.cnt = s.cnt + p * WK; q.lm_id = s.lm_id + p * WK;
     q.keep = s.keep + p * WK;
     q.lmask = s.lmask + p * (WK / 32 + 64); q.lpre = s.lpre + p * (WK / 32 + 64);
+    q.tc_fl = s.tc_fl + p * (size_t)TS_BA_TILES * 256; q.tc_ids = s.tc_ids + p * (size_t)TS_BA_TILES * 2048;
     q.cam_off = s.cam_off + p * (W + 1);
     q.counts = s.counts + 4 * p;
     q.tiles = s.tiles + p * 2 * TS_BA_TILES;
