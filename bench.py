@@ -63,9 +63,11 @@ METRIC_C5 = "RGB-D rig frames/sec (4 cameras, BGR+depth, detect+match+pose+rig p
 HBM_PEAK_GBS = 8000.0
 # VALU issue: 256 CUs x 4 SIMD-32, a wave64 instruction every 2 cycles per SIMD at 2.4 GHz
 VALU_PEAK_WINST = 256 * 4 * 2.4e9 / 2
-# C2 frames per step: 1024 amortises each launch's ramp and drain (measured on one MI355X, round 2:
-# 147.3k / 153.3k / 154.0k / 155.3k frames/s at B = 256 / 512 / 768 / 1024)
-C2_BATCH = 1024
+# C2 frames per step: larger batches amortise each launch's ramp and drain (measured on one MI355X,
+# round 2: 147.3k / 153.3k / 154.0k / 155.3k frames/s at B = 256 / 512 / 768 / 1024; round 5, two
+# runs each: 239.1k / 242.1k / 243.9k at B = 1024 / 2048 / 4096 — 2048 takes most of the gain at
+# half the step latency of 4096)
+C2_BATCH = 2048
 # C5 rig frames per step: 4 periods of the 24-frame triangle wave (the resident batch is replayed)
 C5_BATCH = 184
 # C3 rig frames per step (one GPU, and each step of the sharded rig): 1024, as C2 — at 8 ranks a

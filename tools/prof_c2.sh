@@ -17,5 +17,5 @@ for c in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_WAVES"; do
   n=${c%% *}
   timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d "$out/pmc_$n" -o run -- python3 bench.py "${args[@]}" --steps 2 --warmup 1 > "$out/pmc_$n.log" 2>&1
 done
-python3 tools/pmc_summary.py "$out/pmc_FETCH_SIZE" "$out/pmc_WRITE_SIZE" "$out/pmc.json" --batch "${BATCH:-1024}" --sq "$out/pmc_SQ_INSTS_VALU" > /dev/null
+python3 tools/pmc_summary.py "$out/pmc_FETCH_SIZE" "$out/pmc_WRITE_SIZE" "$out/pmc.json" --batch "${BATCH:-2048}" --sq "$out/pmc_SQ_INSTS_VALU" > /dev/null
 timeout -k 10 240 python3 -u bench.py "${args[@]}" --latency-frames 20 --cpu-budget 12 --boundary-frames 1024 --default-frames 1024 --pmc "$out/pmc.json" --out "$out/bench.json"
