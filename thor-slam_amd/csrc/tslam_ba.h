@@ -26,6 +26,9 @@
 #define TS_BA_MAXY (3 * TS_BA_MAXW + 3)   // velocity + bias unknowns of a window: v_0 .. v_{n-1}, ba
 #define TS_BA_SPLIT 256 // blocks of the Schur product (32-landmark chunks dealt over them; 8192 landmarks in one round)
 #define TS_BA_TILES 128 // scan tiles of a solve's compaction (landmark + observation tiles)
+// at the largest window and K (n_features <= 8192, tslam_create): landmark tiles W K / 2048 plus
+// W K / 2048 observation tiles fit (k_ba_tilescatter's LDS counts, tc_fl / tc_ids)
+static_assert(2 * TS_BA_MAXW * (8192 / 2048) <= TS_BA_TILES, "compaction tiles at W = 10, K = 8192");
 #define TS_BA_PART (4096 + 288) // doubles per Schur block partial: C [64][64], then the camera blocks [MAXW][27]
 
 static_assert(6 * TS_BA_MAXW + 1 <= 64, "the BA camera system (6 rows per keyframe + rhs) is 64 wide");
