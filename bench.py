@@ -747,11 +747,16 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     back_issued = [False, False]
     # C4: local BA runs on a third stream, overlapping the next batches
     ba_stream = torch.cuda.Stream(priority=-1 if args.ba_priority else 0) if c4 else None
+    if c4 and args.pipeline and args.ba_defer:
+        # the BA's ~160 host launches per batch enqueued after the next batch's front stages
+        # (tslam_ba_defer), so the front end of batch s+1 overlaps the BA of batch s on the GPU
+        h.ba_defer(True)
     if c4 and args.ba_cus > 0:   # experiment: the BA chain only on the last N CUs (the front / back keep off them)
         n_cu = torch.cuda.get_device_properties(dev_index).multi_processor_count
         ba_stream = cu_masked_stream(dev_index, 0, 0, list(range(n_cu - args.ba_cus, n_cu)))
     ba_done = [torch.cuda.Event(), torch.cuda.Event()] if c4 else None
     ba_issued = [False, False]
+    ba_host = [0.0, 0]   # C4: host seconds spent enqueuing the BA stage, calls
 
     # kernels bracketed by HIP events inside the timed steps: every event pair is a marker on the
     # GPU timeline, so by default only the dominant kernel's (detect; the roofline's live launch
@@ -784,7 +789,10 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
                 ba_stream.wait_stream(bstream)
                 if evs is not None:
                     evs[i][0].record(ba_stream)
+                t_ba = time.perf_counter()
                 h.run_stage("ba", ba_stream.cuda_stream)
+                ba_host[0] += time.perf_counter() - t_ba
+                ba_host[1] += 1
                 ba_done[s % 2].record(ba_stream)
                 ba_issued[s % 2] = True
                 if evs is not None:
@@ -827,6 +835,7 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(args.warmup + k, events[k])
+    t_issue = time.perf_counter() - t0   # host time to issue the steps (launches are asynchronous)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -1013,6 +1022,8 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
+        "host_issue_ms_per_step": t_issue / args.steps * 1e3,   # host time to enqueue a step
+        "host_ba_issue_ms_per_call": (ba_host[0] / ba_host[1] * 1e3) if c4 and ba_host[1] else None,
         "higher_is_better": True,
         "scaling": "strong" if (c3 or c5) else "weak",
         "vs_baseline": None,
@@ -1380,6 +1391,8 @@ def main() -> None:
     ap.add_argument("--split-cu", type=int, default=0,
                     help="experiment (c2/c3, with --back-cu N): the front kernels on the other CUs, disjoint from the back's")
     ap.add_argument("--ba-priority", type=int, default=0, help="C4: the BA stream at high priority")
+    ap.add_argument("--ba-defer", type=int, default=1,
+                    help="C4: enqueue each batch's BA launches at the next batch's first back stage (tslam_ba_defer)")
     ap.add_argument("--ba-cus", type=int, default=0,
                     help="C4 experiment: the BA stream CU-masked to the last N CUs (with --front-cu-reserve N "
                          "the front / back kernels keep off them)")

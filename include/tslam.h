@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 17
+#define TSLAM_ABI_VERSION 18
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -563,6 +563,15 @@ int tslam_ba_profile(tslam_handle* h, int max_launches, double* schur_ms, int64_
  * solve) instead of k_ba_reduce_solve; both sum in the same order, so the windows agree bit for
  * bit.  0 (default) restores the fused launch. */
 int tslam_ba_split_solve(tslam_handle* h, int split);
+/* Deferred BA issue for stage-API callers that pipeline batches (defer = 1; 0, the default,
+ * issues the BA inside tslam_run_stage(TSLAM_STAGE_BA)).  With a BA stage on a stream of its own,
+ * the stage call only takes the pose snapshot and makes that stream wait for the batch's back end;
+ * the ~16 launches per keyframe are enqueued at the next flush point: the next batch's first back
+ * stage (so its front stages are already on the GPU), the next BA stage, or any call that reads or
+ * changes BA, pose or map state (tslam_sync, tslam_poll_*, tslam_read_*, tslam_ba_*, tslam_copy_*,
+ * loop / relocalisation / map / TSDF calls, tslam_reset, tslam_destroy).  tslam_submit_host never
+ * defers.  Results are identical; only the host's enqueue order changes. */
+int tslam_ba_defer(tslam_handle* h, int defer);
 /* Measurement: `reps` back-to-back k_ba_schur launches on pair `pair`'s last solved window (the
  * kernel only rewrites its own outputs), between two HIP events on `stream`: the average launch
  * duration and the algorithmic flops per launch (for the FP64 MFMA roofline, without per-launch

@@ -286,6 +286,43 @@ def test_ba_two_pairs_own_factors_parity():
     assert max(rel_frobenius(a0["T_cw"][s_], a1["T_cw"][s_]) for s_ in np.nonzero(occ)[0]) > 1e-7   # the windows differ
 
 
+def test_ba_deferred_issue_equals_immediate():
+    """tslam_ba_defer: the stage API pipelined as bench.py --config c4 drives it (front stages on
+    one stream, back stages on a second, the BA stage on a third) with each batch's BA launches
+    enqueued at the next batch's first back stage instead of inside the BA stage call.  Windows,
+    landmarks and the last batch's poses are bit-identical to the immediate issue, and equal the
+    oracle's windows."""
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    n, batch = 12, 3
+    sc, want = _scenario_and_oracle(n)
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    front, back, bas = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    runs = {}
+    for defer in (False, True):
+        h = Handle([sc["rect"]], sc["cfg"], max_batch=batch)
+        try:
+            h.ba_defer(defer)
+            for b0 in range(0, n, batch):
+                h.begin_batch(dev[b0:].data_ptr(), batch)
+                for st, stream in (("rectify", front), ("detect", front), ("describe", front), ("match", back), ("pose", back)):
+                    h.run_stage(st, stream.cuda_stream)
+                h.run_stage("ba", bas.cuda_stream)
+                h.end_batch()
+            got = h.ba_read(0)   # flushes a deferred BA, then synchronises
+            runs[defer] = (got, h.read_poses(batch))
+        finally:
+            h.close()
+    for key in ("frames", "lm", "T_cw", "X"):
+        np.testing.assert_array_equal(np.asarray(runs[False][0][key]).view(np.uint8),
+                                      np.asarray(runs[True][0][key]).view(np.uint8), err_msg=key)
+    for key, a in runs[False][1].items():
+        np.testing.assert_array_equal(a, runs[True][1][key], err_msg=key)
+    _compare(runs[True][0], want[n - 1], "deferred, last batch")
+
+
 def test_ba_inertial_state_resets_and_rejects_bad_input():
     """tslam_reset clears the window's velocities and accelerometer bias (a new session), and
     tslam_ba_inertial_factor refuses a non-finite record, dt <= 0 or a negative weight."""

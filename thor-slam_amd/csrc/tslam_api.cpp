@@ -189,6 +189,19 @@ struct tslam_handle {
     int64_t ba_last = -1;    // newest frame inserted
     BaTiming ba_timing{};    // k_ba_schur events while profiling is on
     bool ba_split = false;   // tslam_ba_split_solve: k_ba_reduce + k_ba_solve instead of k_ba_reduce_solve
+    // tslam_ba_defer: a BA stage on its own stream is enqueued later (the next batch's first back
+    // stage, or any call that reads or changes BA state), so the caller's next front stages are on
+    // the GPU before this batch's ~160 BA launches are issued from the host
+    bool ba_defer = false;
+    struct {
+        bool pending = false;
+        BatchCtx c{};
+        hipStream_t s = nullptr;
+        double* snap = nullptr;
+        double* snap_body = nullptr;
+        int32_t* assoc = nullptr;
+        int par = 0;
+    } ba_job;
     std::map<std::pair<int, int64_t>, std::array<double, 10>> ba_imu;   // (pair, keyframe) -> IMU factor
     // (pair, keyframe) -> inertial factor record + initial velocity (tslam_ba_inertial_factor)
     std::map<std::pair<int, int64_t>, std::array<double, TS_BA_INE + 3>> ba_ine;
@@ -662,8 +675,23 @@ static void shard_range(const tslam_handle* h, int n, int* lo, int* hi) { peer_r
 // on the stream of the last stage) and only reads ring buffers plus a snapshot of the batch's
 // poses, so the next batch can start.  A sharded rank runs it once its ring holds every pair's
 // keyframe data (rank 0 after the state gather, tslam_shard.cpp).
+// The deferred BA job (tslam_ba_defer): its stream already waits for its batch's back end, so
+// issuing it later only moves the host work.
+static void ba_flush(tslam_handle* h) {
+    if (!h->ba_job.pending) return;
+    h->ba_job.pending = false;
+    auto& j = h->ba_job;
+    run_ba(h, j.c, j.s, j.snap, j.snap_body, j.assoc);
+    (void)hipEventRecord(h->ev_ba[j.par], j.s);
+}
+#define BA_FLUSH(h)                                \
+    do {                                           \
+        if ((h) && (h)->ba_job.pending) ba_flush(h); \
+    } while (0)
+
 static int ba_stage(tslam_handle* h, const BatchCtx& c, hipStream_t s) {
     if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
+    BA_FLUSH(h);   // the previous batch's deferred BA comes first (host state, event order)
     const int par = (int)(h->batch_idx & 1);
     double* snap = h->ba.fe_pose + (size_t)par * h->B * h->P * 16;
     double* snap_body = h->ba.fe_body + (size_t)par * h->B * 16;
@@ -681,6 +709,17 @@ static int ba_stage(tslam_handle* h, const BatchCtx& c, hipStream_t s) {
         }
         HIPCHK(hipEventRecord(h->ev_fe, fs));
         HIPCHK(hipStreamWaitEvent(s, h->ev_fe, 0));
+        if (h->ba_defer) {   // enqueued at the next flush point (BA_FLUSH)
+            h->ba_job.pending = true;
+            h->ba_job.c = c;
+            h->ba_job.s = s;
+            h->ba_job.snap = snap;
+            h->ba_job.snap_body = snap_body;
+            h->ba_job.assoc = assoc;
+            h->ba_job.par = par;
+            h->ba_pending[par] = true;
+            return TSLAM_OK;
+        }
     }
     run_ba(h, c, s, snap, snap_body, assoc);
     if (other) {
@@ -950,6 +989,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
 
 int tslam_destroy(tslam_handle* h) {
     if (!h) return TSLAM_OK;
+    BA_FLUSH(h);
     loop_worker_stop(h);   // its queued jobs reach the loop stream before the device is drained
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();
@@ -971,6 +1011,7 @@ int tslam_destroy(tslam_handle* h) {
 
 int tslam_reset(tslam_handle* h) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
+    BA_FLUSH(h);
     loop_worker_drain(h);
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
@@ -1148,6 +1189,7 @@ int tslam_submit_host(tslam_handle* h, const uint8_t* host_images, const double*
         // the BA stream waits for the back stream (ba_stage's event is recorded after the copies),
         // and the slot is ready once this batch's BA ran: the caller reads the window after polling
         rc = tslam_run_stage(h, TSLAM_STAGE_BA, h->as_ba);
+        BA_FLUSH(h);   // the slot event below follows the BA's launches
         if (rc == TSLAM_OK) HIPCHK(hipEventRecord(h->as_res[(h->as_batches - 1) & 1].ev, h->as_ba));
     }
     const int rc2 = tslam_end_batch(h);
@@ -1167,6 +1209,7 @@ int tslam_poll_batch(tslam_handle* h, int block, int max_frames, double* T_rel, 
                      double* rig_T_rel, double* rig_T_abs, double* rig_cov, int32_t* rig_stats, double* ts,
                      int64_t* first_frame, int* n_frames) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
+    BA_FLUSH(h);
     HIPCHK(hipSetDevice(h->device));
     // the oldest unread batch
     int k = -1;
@@ -1198,6 +1241,7 @@ int tslam_poll_batch(tslam_handle* h, int block, int max_frames, double* T_rel, 
 
 int tslam_poll_pose(tslam_handle* h, double* T, double* cov, double* ts, int32_t* state, float* conf) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
+    BA_FLUSH(h);
     HIPCHK(hipSetDevice(h->device));
     int k = -1;   // the newest completed batch
     for (int i = 0; i < 2; ++i) {
@@ -1287,7 +1331,9 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
         HIPCHK(hipEventCreateWithFlags(&h->ev_back[1], hipEventDisableTiming));
     }
     const int par = (int)(h->batch_idx & 1);
+    if (back && !h->back_started) BA_FLUSH(h);   // a deferred BA of the previous batch: now, behind this batch's front
     if (stage != TSLAM_STAGE_BA && !h->batch_started) {
+        if (h->ba_job.pending && h->ba_job.par == par) ba_flush(h);   // (that BA's event is recorded before this wait)
         // the first work of a batch: the BA of the batch two back (same ring slots) must be done
         if (h->ba_pending[par]) HIPCHK(hipStreamWaitEvent(s, h->ev_ba[par], 0));
         h->ba_pending[par] = false;
@@ -1397,6 +1443,7 @@ int tslam_pose(tslam_handle* h, void* stream) { return tslam_run_stage(h, TSLAM_
 
 int tslam_sync(tslam_handle* h) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
+    BA_FLUSH(h);
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
     return TSLAM_OK;
@@ -1418,6 +1465,7 @@ static int copy_pose_records(const double* dev_pose, const int32_t* dev_stats, i
 
 int tslam_read_poses(tslam_handle* h, int max_frames, double* T_rel, double* T_abs, double* cov, int32_t* stats) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
+    BA_FLUSH(h);
     if (h->cur_n == 0) return fail(TSLAM_ESTATE, "no batch has run since tslam_create / tslam_reset");
     if (max_frames < h->cur_n) return fail(TSLAM_EINVAL, "output capacity (max_frames) is smaller than the last batch");
     int rc = tslam_sync(h);
@@ -1428,6 +1476,7 @@ int tslam_read_poses(tslam_handle* h, int max_frames, double* T_rel, double* T_a
 
 int tslam_buffer_info(tslam_handle* h, int which, void** device_ptr, int64_t* bytes_total, int64_t* bytes_per_frame) {
     if (!h || which < 0 || which >= TSLAM_BUF_COUNT) return fail(TSLAM_EINVAL, "bad handle or buffer id");
+    BA_FLUSH(h);
     if (device_ptr) *device_ptr = h->buf[which].ptr;
     if (bytes_total) *bytes_total = h->buf[which].bytes;
     if (bytes_per_frame) *bytes_per_frame = h->buf[which].per_frame;
@@ -1436,6 +1485,7 @@ int tslam_buffer_info(tslam_handle* h, int which, void** device_ptr, int64_t* by
 
 int tslam_copy_out(tslam_handle* h, int which, int64_t offset, void* host_dst, int64_t bytes) {
     if (!h || which < 0 || which >= TSLAM_BUF_COUNT || !host_dst) return fail(TSLAM_EINVAL, "bad argument");
+    BA_FLUSH(h);
     if (offset < 0 || bytes < 0 || offset + bytes > h->buf[which].bytes) return fail(TSLAM_EINVAL, "range outside buffer");
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
@@ -1445,6 +1495,7 @@ int tslam_copy_out(tslam_handle* h, int which, int64_t offset, void* host_dst, i
 
 int tslam_copy_in(tslam_handle* h, int which, int64_t offset, const void* host_src, int64_t bytes) {
     if (!h || which < 0 || which >= TSLAM_BUF_COUNT || !host_src) return fail(TSLAM_EINVAL, "bad argument");
+    BA_FLUSH(h);
     if (offset < 0 || bytes < 0 || offset + bytes > h->buf[which].bytes) return fail(TSLAM_EINVAL, "range outside buffer");
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
@@ -1484,6 +1535,7 @@ int tslam_layout(tslam_handle* h, int64_t* out16, int32_t* level_info18) {
 
 int tslam_set_motion_prior(tslam_handle* h, const double* prior, int n_frames) {
     if (!h || !prior) return fail(TSLAM_EINVAL, "bad argument");
+    BA_FLUSH(h);
     if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_set_motion_prior inside a batch");
     if (n_frames < 1 || n_frames > h->B) return fail(TSLAM_EINVAL, "n_frames must be in [1, max_batch]");
     HIPCHK(hipSetDevice(h->device));
@@ -1556,6 +1608,7 @@ static int set_rig_E(tslam_handle* h, int q_total, const double* base_T_rect) {
 
 int tslam_set_rig(tslam_handle* h, const double* base_T_rect) {
     if (!h || !base_T_rect) return fail(TSLAM_EINVAL, "bad argument");
+    BA_FLUSH(h);
     if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_set_rig inside a batch");
     const int rc = set_rig_E(h, h->P, base_T_rect);
     if (rc != TSLAM_OK) return rc;
@@ -1565,6 +1618,7 @@ int tslam_set_rig(tslam_handle* h, const double* base_T_rect) {
 
 int tslam_read_rig_poses(tslam_handle* h, int max_frames, double* T_rel, double* T_abs, double* cov, int32_t* stats) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
+    BA_FLUSH(h);
     if (!h->rig) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig)");
     if (h->cur_n == 0) return fail(TSLAM_ESTATE, "no batch has run since tslam_create / tslam_reset");
     if (max_frames < h->cur_n) return fail(TSLAM_EINVAL, "output capacity (max_frames) is smaller than the last batch");
@@ -1576,6 +1630,7 @@ int tslam_read_rig_poses(tslam_handle* h, int max_frames, double* T_rel, double*
 // -- sharded rig ------------------------------------------------------------------
 int tslam_set_shard(tslam_handle* h, int cam_lo, int cam_hi, int rank, int world) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
+    BA_FLUSH(h);
     if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_set_shard inside a batch");
     if (cam_lo < 0 || cam_hi > h->C || cam_lo >= cam_hi) return fail(TSLAM_EINVAL, "camera range outside [0, cameras)");
     if (world < 1 || rank < 0 || rank >= world || world > h->B) return fail(TSLAM_EINVAL, "need 0 <= rank < world <= max_batch");
@@ -1721,6 +1776,7 @@ int tslam_internal_state_blocks(tslam_handle* h, int pack, int rank, int cam_lo,
 
 int tslam_perturb_temporal(tslam_handle* h, int percent, uint64_t seed, void* stream) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
+    BA_FLUSH(h);
     if (!h->in_batch) return fail(TSLAM_ESTATE, "tslam_perturb_temporal inside a batch (after MATCH_REFINE)");
     if (percent < 0 || percent > 100) return fail(TSLAM_EINVAL, "percent must be in [0, 100]");
     if (h->sh_world > 1 || h->sh_comm) return fail(TSLAM_ESTATE, "tslam_perturb_temporal takes an unsharded handle");
@@ -1822,6 +1878,7 @@ int tslam_unpack_poses(tslam_handle* h, const void* src, void* stream) {
 
 int tslam_ba_read_map(tslam_handle* h, int pair, int64_t* gid, uint32_t* desc) {
     if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
+    BA_FLUSH(h);
     if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
     int rc = tslam_sync(h);
     if (rc != TSLAM_OK) return rc;
@@ -1886,6 +1943,7 @@ static int reloc_solve(tslam_handle* h, int pair, int64_t frame, const double* m
 
 int tslam_map_upload(tslam_handle* h, const double* xyz, const uint32_t* desc, int64_t n) {
     if (!h || n < 0 || (n && (!xyz || !desc))) return fail(TSLAM_EINVAL, "bad argument");
+    BA_FLUSH(h);
     if (n > (1 << 20) - 1) return fail(TSLAM_EINVAL, "at most 2^20 - 1 map points");
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
@@ -1915,6 +1973,7 @@ int tslam_map_upload(tslam_handle* h, const double* xyz, const uint32_t* desc, i
 
 int tslam_relocalize(tslam_handle* h, int pair, int64_t frame, double* cam_T_world, double* cov, int32_t* stats) {
     if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
+    BA_FLUSH(h);
     if (!h->d_rl_match) return fail(TSLAM_ESTATE, "no map uploaded (tslam_map_upload)");
     if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_relocalize inside a batch");
     if (frame < 0 || frame >= h->frames_done || frame < h->frames_done - h->R)
@@ -1926,6 +1985,7 @@ int tslam_relocalize(tslam_handle* h, int pair, int64_t frame, double* cam_T_wor
 int tslam_relocalize_rig(tslam_handle* h, int64_t frame, double* body_T_world, double* cov, int32_t* stats,
                          int32_t* pair_stats) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
+    BA_FLUSH(h);
     if (!h->rig || h->rig_q != h->P) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig)");
     if (h->prm.rgbd) return fail(TSLAM_ESTATE, "tslam_relocalize_rig takes a stereo rig");
     if (!h->d_rl_match) return fail(TSLAM_ESTATE, "no map uploaded (tslam_map_upload)");
@@ -1971,6 +2031,7 @@ int tslam_relocalize_rig(tslam_handle* h, int64_t frame, double* body_T_world, d
 // -- loop closure: keyframe database, place recognition, verification, pose graph ---------------
 int tslam_loop_init(tslam_handle* h, int max_keyframes, int signature) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
+    BA_FLUSH(h);
     if (max_keyframes < 1 || max_keyframes > (1 << 16)) return fail(TSLAM_EINVAL, "max_keyframes must be in [1, 65536]");
     if (signature < 1 || signature > 256) return fail(TSLAM_EINVAL, "signature must be in [1, 256]");
     loop_worker_drain(h);
@@ -2005,6 +2066,7 @@ static int loop_count(tslam_handle* h, int slot, int32_t* n) {
 
 int tslam_loop_add_keyframe(tslam_handle* h, int pair, int64_t frame, int* slot, int* n_landmarks) {
     if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
+    BA_FLUSH(h);
     if (!h->lp_cap) return fail(TSLAM_ESTATE, "loop database not initialised (tslam_loop_init)");
     if (h->lp_auto) return fail(TSLAM_ESTATE, "the submit path stores the keyframes (tslam_loop_auto)");
     if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_loop_add_keyframe inside a batch");
@@ -2029,6 +2091,7 @@ int tslam_loop_add_keyframe(tslam_handle* h, int pair, int64_t frame, int* slot,
 
 int tslam_loop_read_keyframe(tslam_handle* h, int slot, double* xyz, uint32_t* desc, int* n) {
     if (!h || !h->lp_cap) return fail(TSLAM_ESTATE, "loop database not initialised (tslam_loop_init)");
+    BA_FLUSH(h);
     if (slot < 0 || slot >= h->lp_cap) return fail(TSLAM_EINVAL, "slot out of range");
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());   // the stores of every stream (tslam_loop_auto: the back stream)
@@ -2043,6 +2106,7 @@ int tslam_loop_read_keyframe(tslam_handle* h, int slot, double* xyz, uint32_t* d
 
 int tslam_loop_query(tslam_handle* h, int slot, int n_candidates, int32_t* votes) {
     if (!h || !h->lp_cap) return fail(TSLAM_ESTATE, "loop database not initialised (tslam_loop_init)");
+    BA_FLUSH(h);
     if (slot < 0 || slot >= h->lp_cap) return fail(TSLAM_EINVAL, "slot out of range");
     if (n_candidates < 0 || n_candidates > h->lp_cap) return fail(TSLAM_EINVAL, "n_candidates out of range");
     if (n_candidates == 0) return TSLAM_OK;
@@ -2059,6 +2123,7 @@ int tslam_loop_query(tslam_handle* h, int slot, int n_candidates, int32_t* votes
 
 int tslam_loop_verify(tslam_handle* h, int pair, int64_t frame, int slot, double* T_qc, double* cov, int32_t* stats) {
     if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
+    BA_FLUSH(h);
     if (!h->lp_cap) return fail(TSLAM_ESTATE, "loop database not initialised (tslam_loop_init)");
     if (slot < 0 || slot >= h->lp_cap) return fail(TSLAM_EINVAL, "slot out of range");
     if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_loop_verify inside a batch");
@@ -2078,6 +2143,7 @@ static int pose_graph_reserve(tslam_handle* h, int n_nodes, int n_edges);
 
 int tslam_loop_auto(tslam_handle* h, int interval) {
     if (!h || interval < 0) return fail(TSLAM_EINVAL, "bad handle or interval");
+    BA_FLUSH(h);
     if (!h->lp_cap) return fail(TSLAM_ESTATE, "loop database not initialised (tslam_loop_init)");
     if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_loop_auto inside a batch");
     if (h->sh_world > 1 || h->sh_comm) return fail(TSLAM_ESTATE, "tslam_loop_auto takes an unsharded handle");
@@ -2159,6 +2225,7 @@ static int job_post(tslam_handle* h, tslam_handle::LoopJob& j, std::function<hip
 
 int tslam_loop_job_vote(tslam_handle* h, int query, int64_t k0, int n_kf, int64_t* job) {
     if (!h || !h->lp_cap) return fail(TSLAM_ESTATE, "loop database not initialised (tslam_loop_init)");
+    BA_FLUSH(h);
     if (h->lp_cap % h->P) return fail(TSLAM_ESTATE, "the database is not keyframe-major over the pairs");
     const int capk = h->lp_cap / h->P;
     if (query < 0 || query >= h->lp_cap || k0 < 0 || n_kf < 0 || n_kf > capk)
@@ -2188,6 +2255,7 @@ int tslam_loop_job_vote(tslam_handle* h, int query, int64_t k0, int n_kf, int64_
 
 int tslam_loop_job_verify(tslam_handle* h, int pair, int64_t frame, int query, int cand, int64_t* job) {
     if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
+    BA_FLUSH(h);
     if (!h->lp_cap || !h->d_lp_snap_kps) return fail(TSLAM_ESTATE, "no keyframe snapshots (tslam_loop_auto)");
     if (query < 0 || query >= h->lp_cap || cand < 0 || cand >= h->lp_cap || frame < 0)
         return fail(TSLAM_EINVAL, "entry or frame out of range");
@@ -2221,6 +2289,7 @@ int tslam_loop_job_verify(tslam_handle* h, int pair, int64_t frame, int query, i
 int tslam_tsdf_init(tslam_handle* h, const double* origin, const int32_t* dims, double voxel_size, double trunc_vox,
                     double max_dist, double max_weight) {
     if (!h || !origin || !dims) return fail(TSLAM_EINVAL, "bad argument");
+    BA_FLUSH(h);
     if (dims[0] < 1 || dims[1] < 1 || dims[2] < 1 || (int64_t)dims[0] * dims[1] * dims[2] > ((int64_t)1 << 31))
         return fail(TSLAM_EINVAL, "dims must be >= 1 with at most 2^31 voxels");
     if (!(voxel_size > 0.0) || !(trunc_vox > 0.0) || !(max_dist > 0.0) || !(max_weight >= 1.0))
@@ -2279,6 +2348,7 @@ int tslam_tsdf_color(tslam_handle* h, int enable) {
 static int tsdf_integrate(tslam_handle* h, int pair, const void* color, const void* depth, int64_t stride_bytes,
                           int n_frames, int64_t first_frame, const double* world_T_cam, void* stream) {
     if (!h || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad handle or pair");
+    BA_FLUSH(h);
     if (!h->tsdf_on) return fail(TSLAM_ESTATE, "no TSDF volume (tslam_tsdf_init)");
     if (!depth || n_frames < 0 || (n_frames > 1 && stride_bytes < 2LL * h->W * h->H)) return fail(TSLAM_EINVAL, "bad depth / stride");
     if (h->in_batch) return fail(TSLAM_ESTATE, "tslam_tsdf_integrate inside a batch");
@@ -2321,6 +2391,7 @@ static int tsdf_integrate(tslam_handle* h, int pair, const void* color, const vo
 
 int tslam_tsdf_read(tslam_handle* h, float* tsdf, float* weight) {
     if (!h || !h->tsdf_on) return fail(TSLAM_ESTATE, "no TSDF volume (tslam_tsdf_init)");
+    BA_FLUSH(h);
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
     const size_t nv = (size_t)h->tsdf.nx * h->tsdf.ny * h->tsdf.nz;
@@ -2352,6 +2423,7 @@ int tslam_tsdf_write_color(tslam_handle* h, const float* rgb, const float* weigh
 
 int tslam_tsdf_write(tslam_handle* h, const float* tsdf, const float* weight) {
     if (!h || !h->tsdf_on) return fail(TSLAM_ESTATE, "no TSDF volume (tslam_tsdf_init)");
+    BA_FLUSH(h);
     if (!tsdf || !weight) return fail(TSLAM_EINVAL, "null volume");
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
@@ -2392,6 +2464,7 @@ static int grow(tslam_handle* h, void** p, size_t* cap, size_t need) {
 
 int tslam_mesh_extract(tslam_handle* h, double min_weight, int64_t* n_tris, void* stream) {
     if (!h || !h->tsdf_on) return fail(TSLAM_ESTATE, "no TSDF volume (tslam_tsdf_init)");
+    BA_FLUSH(h);
     if (!(min_weight >= 0.0)) return fail(TSLAM_EINVAL, "min_weight must be >= 0");
     HIPCHK(hipSetDevice(h->device));
     hipStream_t s = stream ? (hipStream_t)stream : h->last_stream;
@@ -2574,6 +2647,7 @@ static int pose_graph_reserve(tslam_handle* h, int n_nodes, int n_edges) {
 int tslam_loop_job_pose_graph(tslam_handle* h, int n_nodes, const double* world_T_node, int n_edges, const int32_t* edges,
                               const double* meas, const double* info, int iters, int64_t* job) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
+    BA_FLUSH(h);
     if (n_nodes < 1 || n_nodes > 1024) return fail(TSLAM_EINVAL, "n_nodes must be in [1, 1024]");
     if (n_edges < 0 || (n_edges && (!edges || !meas || !info)) || !world_T_node || iters < 0)
         return fail(TSLAM_EINVAL, "bad argument");
@@ -2664,6 +2738,7 @@ int tslam_loop_job_pose_graph(tslam_handle* h, int n_nodes, const double* world_
 int tslam_loop_job_poll(tslam_handle* h, int64_t id, int block, int32_t* votes, double* T_qc, double* cov,
                         int32_t* stats, double* world_T_node, double* cost) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
+    BA_FLUSH(h);
     auto& j = h->lp_jobs[(size_t)(id > 0 ? id : 0) % 64];
     if (id <= 0 || !j.kind || j.id != id) return fail(TSLAM_ESTATE, "unknown or already returned loop job");
     HIPCHK(hipSetDevice(h->device));
@@ -2722,6 +2797,7 @@ int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_e
 
 int tslam_ba_imu_factor(tslam_handle* h, int pair, int64_t frame, const double* M, double weight) {
     if (!h || !M || pair < 0 || pair >= h->P) return fail(TSLAM_EINVAL, "bad argument");
+    BA_FLUSH(h);
     if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
     // non-finite inputs would poison the whole window's Schur system (k_ba_solve adds them to S, b)
     if (!(weight >= 0.0) || !std::isfinite(weight) || frame < 0)
@@ -2746,6 +2822,7 @@ static int ine_pair_check(tslam_handle* h, int pair) {
 
 int tslam_ba_inertial(tslam_handle* h, int pair, const double* gravity, const double* ba_prior, double ba_weight) {
     if (!h || !gravity || !ba_prior) return fail(TSLAM_EINVAL, "bad argument");
+    BA_FLUSH(h);
     if (int rc = ine_pair_check(h, pair); rc != TSLAM_OK) return rc;
     if (!(ba_weight >= 0.0) || !std::isfinite(ba_weight)) return fail(TSLAM_EINVAL, "ba_weight must be finite and >= 0");
     for (int e = 0; e < 3; ++e)
@@ -2761,6 +2838,7 @@ int tslam_ba_inertial(tslam_handle* h, int pair, const double* gravity, const do
 
 int tslam_ba_inertial_factor(tslam_handle* h, int pair, int64_t frame, const double* record, const double* v0) {
     if (!h || !record || !v0 || frame < 0) return fail(TSLAM_EINVAL, "bad argument");
+    BA_FLUSH(h);
     if (int rc = ine_pair_check(h, pair); rc != TSLAM_OK) return rc;
     std::array<double, TS_BA_INE + 3> f{};
     for (int e = 0; e < 30; ++e) {
@@ -2778,6 +2856,7 @@ int tslam_ba_inertial_factor(tslam_handle* h, int pair, int64_t frame, const dou
 
 int tslam_ba_read_inertial(tslam_handle* h, int pair, double* velocity, double* ba) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
+    BA_FLUSH(h);
     if (int rc = ine_pair_check(h, pair); rc != TSLAM_OK) return rc;
     int rc = tslam_sync(h);
     if (rc != TSLAM_OK) return rc;
@@ -2790,6 +2869,7 @@ int tslam_ba_read_inertial(tslam_handle* h, int pair, double* velocity, double* 
 int tslam_ba_read(tslam_handle* h, int pair, int64_t* frames, double* cam_T_world, int32_t* landmark,
                   double* points, double* obs_uvd, int32_t* counts) {
     if (!h || pair < 0 || pair > h->P || (pair == h->P && !ba_rig(h))) return fail(TSLAM_EINVAL, "bad handle or pair");
+    BA_FLUSH(h);
     if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
     int rc = tslam_sync(h);
     if (rc != TSLAM_OK) return rc;
@@ -2820,6 +2900,7 @@ int tslam_ba_read(tslam_handle* h, int pair, int64_t* frames, double* cam_T_worl
 int tslam_ba_replay_schur(tslam_handle* h, int pair, int reps, void* stream, double* us_per_launch,
                           double* flops_per_launch) {
     if (!h || pair < 0 || pair >= h->P || reps < 1) return fail(TSLAM_EINVAL, "bad argument");
+    BA_FLUSH(h);
     if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
     if ((int)h->ba_solved.size() <= pair) return fail(TSLAM_ESTATE, "no window solved yet");
     HIPCHK(hipSetDevice(h->device));
@@ -2846,14 +2927,23 @@ int tslam_ba_replay_schur(tslam_handle* h, int pair, int reps, void* stream, dou
     return TSLAM_OK;
 }
 
+int tslam_ba_defer(tslam_handle* h, int defer) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    BA_FLUSH(h);
+    h->ba_defer = defer != 0;
+    return TSLAM_OK;
+}
+
 int tslam_ba_split_solve(tslam_handle* h, int split) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
+    BA_FLUSH(h);
     h->ba_split = split != 0;
     return TSLAM_OK;
 }
 
 int tslam_ba_profile(tslam_handle* h, int max_launches, double* schur_ms, int64_t* schur_launches, double* schur_flops) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
+    BA_FLUSH(h);
     if (!h->prm.ba_window) return fail(TSLAM_ESTATE, "local BA is off (ba_window = 0)");
     int rc = tslam_sync(h);
     if (rc != TSLAM_OK) return rc;

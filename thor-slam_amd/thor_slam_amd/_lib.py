@@ -199,6 +199,7 @@ _SIGNATURES = {
     "tslam_ba_replay_schur": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "tslam_ba_split_solve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "tslam_ba_defer": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "tslam_ba_inertial": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double]),
     "tslam_ba_inertial_factor": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
                                                 ctypes.c_void_p]),
@@ -918,6 +919,11 @@ class Handle:
         ba = np.zeros(3)
         _check(self.lib.tslam_ba_read_inertial(self.h, int(pair), vel.ctypes.data, ba.ctypes.data))
         return {"vel": vel, "ba": ba}
+
+    def ba_defer(self, defer: bool) -> None:
+        """``tslam_ba_defer``: a BA stage on its own stream is enqueued at the next flush point
+        (the next batch's first back stage, or any state read) instead of inside the stage call."""
+        _check(self.lib.tslam_ba_defer(self.h, int(bool(defer))))
 
     def ba_split_solve(self, split: bool) -> None:
         """k_ba_reduce + k_ba_solve (kernel boundary) instead of k_ba_reduce_solve (tslam.h)."""
