@@ -393,9 +393,30 @@ def tsdf_report(h, us: float, B: int, width: int, height: int) -> dict:
                          "frac": alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": alg}}
 
 
+_MASKED_STREAMS: list = []   # (hip library, hipStream_t) created by cu_masked_stream
+
+
+def destroy_masked_streams() -> None:
+    """hipStreamDestroy every stream cu_masked_stream created, after the device is idle and torch's
+    current stream is back on the default one.  Streams left to the process exit were torn down by
+    the HIP runtime's static destructors after rocprofv3's tool finalisation, which segfaulted
+    there (__cxa_finalize) on the C4 profile of round 5."""
+    import torch
+
+    if not _MASKED_STREAMS:
+        return
+    torch.cuda.synchronize()
+    torch.cuda.set_stream(torch.cuda.default_stream())
+    while _MASKED_STREAMS:
+        hip, st = _MASKED_STREAMS.pop()
+        rc = hip.hipStreamDestroy(st)
+        if rc != 0:
+            raise RuntimeError(f"hipStreamDestroy failed ({rc})")
+
+
 def cu_masked_stream(dev_index: int, reserve: int, priority: int, cus: list | None = None):
     """A torch stream whose kernels may use every CU but the last `reserve`, or only the CUs `cus`
-    (hipExtStreamCreateWithCUMask)."""
+    (hipExtStreamCreateWithCUMask); destroyed by destroy_masked_streams."""
     import ctypes
 
     import torch
@@ -411,6 +432,8 @@ def cu_masked_stream(dev_index: int, reserve: int, priority: int, cus: list | No
     rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words), mask)
     if rc != 0:
         raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    _MASKED_STREAMS.append((hip, st.value))
     if priority:
         pass   # CU-masked streams take the default priority
     return torch.cuda.ExternalStream(st.value, device=torch.device("cuda", dev_index))
@@ -1060,6 +1083,7 @@ def run_single(args, world: int, rank: int, dev_index: int) -> dict:
         out["dense_map"] = tsdf_report(h, per_kernel_us["tsdf"], B, width, height)
         out["dense_map"]["outputs"] = dense_outputs_report(h)
     h.close()
+    destroy_masked_streams()
     if rank == 0 and world == 1 and args.boundary_frames > 0 and args.config == "c2":
         out["boundary"] = boundary_bench(uniq, src, args.boundary_frames)
         if args.default_frames > 0:

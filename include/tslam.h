@@ -41,13 +41,14 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 18
+#define TSLAM_ABI_VERSION 19
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
 #define TSLAM_EHIP (-2)
 #define TSLAM_ENOMEM (-3)
 #define TSLAM_ESTATE (-4)
+#define TSLAM_ESINGULAR (-5)   /* a pose-graph solve whose normal matrix is not positive definite */
 
 /* pose status per frame (tslam_read_poses stats[4*i + 0]) */
 #define TSLAM_POSE_OK 0
@@ -139,7 +140,9 @@ enum tslam_buffer {
     TSLAM_BUF_DESC_YS = 17,  /* u32 [ring][cams][K][8]           descriptors in the y-sorted order */
     TSLAM_BUF_DET_THR = 18,  /* u32 [1][cams][levels]            speculative FAST threshold te in use (0 = t + 1) */
     TSLAM_BUF_DET_FAIL = 19, /* u32 [batch][cams][levels]        1 = the last batch's image-level took the fallback */
-    TSLAM_BUF_COUNT = 20
+    TSLAM_BUF_HYP = 20,      /* f64 [batch][pairs][n_hyp][4][20] P3P candidates of each RANSAC hypothesis, by
+                                ascending root: R[9] t[3] (f64; R[0] NaN = no solution), then f32 copies */
+    TSLAM_BUF_COUNT = 21
 };
 
 enum tslam_stage {
@@ -159,8 +162,11 @@ enum tslam_stage {
     TSLAM_KERNEL_MATCH_REFINE = 15,
     TSLAM_KERNEL_POSE = 16,
     TSLAM_KERNEL_CHAIN = 17,        /* every pair's chain, and the rig's after tslam_set_rig (one block each) */
-    TSLAM_KERNEL_RIG = 18           /* rig pose (after tslam_set_rig; sharded: the range's); run it before
+    TSLAM_KERNEL_RIG = 18,          /* rig pose (after tslam_set_rig; sharded: the range's); run it before
                                        KERNEL_CHAIN */
+    TSLAM_KERNEL_POSE_SOLVE = 19    /* parity tests: P3P + RANSAC + refinement alone, on the correspondences
+                                       and counts in TSLAM_BUF_CORR / TSLAM_BUF_STATS (status 3 = to be
+                                       solved, stats[1] = n) — crafted sets injected with tslam_copy_in */
 };
 
 /* Benchmark hook, never on the tracking path: inside a batch, after MATCH_REFINE, move `percent` %
@@ -563,6 +569,12 @@ int tslam_ba_profile(tslam_handle* h, int max_launches, double* schur_ms, int64_
  * solve) instead of k_ba_reduce_solve; both sum in the same order, so the windows agree bit for
  * bit.  0 (default) restores the fused launch. */
 int tslam_ba_split_solve(tslam_handle* h, int split);
+/* Issue of a stereo pair window's keyframe chain (ABI 19).  enable = 1 (default): each keyframe's
+ * ~16 BA launches replay a captured hipGraph of that chain shape whose kernels read the keyframe's
+ * arguments from a device record (one node update + one graph launch per keyframe and pair);
+ * 0: direct launches with by-value arguments.  Same kernels, same sums: the windows agree bit for
+ * bit.  Rig body windows and BA profiling (tslam_ba_profile) always launch directly. */
+int tslam_ba_graph(tslam_handle* h, int enable);
 /* Deferred BA issue for stage-API callers that pipeline batches (defer = 1; 0, the default,
  * issues the BA inside tslam_run_stage(TSLAM_STAGE_BA)).  With a BA stage on a stream of its own,
  * the stage call only takes the pose snapshot and makes that stream wait for the batch's back end;
@@ -626,6 +638,10 @@ int tslam_loop_query(tslam_handle* h, int slot, int n_candidates, int32_t* votes
 int tslam_loop_verify(tslam_handle* h, int pair, int64_t frame, int slot, double* T_qc, double* cov, int32_t* stats);
 int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_edges, const int32_t* edges,
                      const double* meas, const double* info, int iters, double* cost);
+/* Test hook (process-wide, 0 = off, the default): every later k_pg_potrf launch holds its blocks
+ * >= 1 back by `spins` x 127 x 64 cycles before they read the diagonal tile, forcing the read
+ * order of a late block (the panel's stores of block 0 have landed).  Results never change. */
+int tslam_test_potrf_delay(int spins);
 
 /* Asynchronous loop closure (ABI 15): the reference's default deployment path runs with loop
  * closure on at batch 1 (HipSlamEngine(num_cameras=N) + initialize, scripts/run_slam.py:299-300;
@@ -653,7 +669,10 @@ int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_e
  * tslam_loop_job_pose_graph: tslam_pose_graph's solve (inputs copied at the call).
  * tslam_loop_job_poll: 0 while job `id` runs (block = 0), else 1 and its results once:
  *   vote -> votes[n_kf * P]; verify -> T_qc[16], cov[36], stats[8]; pose graph -> world_T_node
- *   [n_nodes][16] and *cost (NULL skips any output).  TSLAM_ESTATE for an unknown or returned id. */
+ *   [n_nodes][16] and *cost (NULL skips any output).  TSLAM_ESTATE for an unknown or returned id;
+ *   TSLAM_ESINGULAR (also from tslam_pose_graph) when the solve's normal matrix was not positive
+ *   definite (a pivot <= 0 or NaN: some pose came back non-finite) — the loop policy then rejects
+ *   that loop (oracle/numpy_loop.py LoopPolicy). */
 int tslam_loop_auto(tslam_handle* h, int interval);
 int tslam_loop_job_vote(tslam_handle* h, int query, int64_t k0, int n_kf, int64_t* job);
 int tslam_loop_job_verify(tslam_handle* h, int pair, int64_t frame, int query, int cand, int64_t* job);

@@ -273,6 +273,11 @@ def span_edges(edges: list, a: int, b: int) -> list[int]:
     return sorted((e for e, (x, y) in enumerate(edges) if a <= x and y <= b), key=lambda e: (edges[e][1], edges[e][0]))
 
 
+class SpanSolveFailed(Exception):
+    """Raised by a LoopPolicy ``solve`` callable for a span solve that failed (the device's
+    TSLAM_ESINGULAR); ``optimize``'s own failure is ``np.linalg.LinAlgError``."""
+
+
 class LoopPolicy:
     """Keyframe pose graph + loop closure with a fixed latency.
 
@@ -293,7 +298,37 @@ class LoopPolicy:
          solve: Gauss-Newton (``pg_iters``) on the nodes [c, idx] with node c fixed and the edges
          with both ends in the span (``span_edges``); the span takes the solution, later nodes
          are re-chained by their odometry (T_i = T_{i-1} Z_i), and corr = T_last raw_last^-1;
+       * rejection: a span solve whose normal matrix is not positive definite (Cholesky fails: a
+         pivot <= 0 or NaN — ``optimize`` raises ``LinAlgError``, the device returns
+         TSLAM_ESINGULAR) or that returns a non-finite pose drops the loop: no edge, no
+         correction, ``last_loop`` unchanged (the cooldown counts closed loops only), and
+         (frame of c, g) goes to ``rejected``.  The session goes on: the reference's contract is
+         a pose or None from ``process_frames`` (``interface.py:192-200``), and
+         ``run_slam.py:314-321`` has no handler for an exception;
     3. the frame's corrected pose is corr @ raw.
+
+    Relocalisation after a LOST run (``reloc_after_lost`` > 0; the reference's
+    ``TrackingState.RELOCALIZING``, ``interface.py:16-23``, and cuVSLAM's
+    ``enable_localization_n_mapping``, ``launch/thor_visual_slam.launch.py:42,74``): the device
+    keeps chaining through LOST frames without their motion, so the poses after a long gap are
+    off by whatever happened in it.
+
+    * the ``reloc_after_lost``-th consecutive LOST frame (with at least one node) breaks the graph:
+      state RELOCALIZING, ``anchor_end`` = the node count at the first break of the episode,
+      ``seg_start`` = the next node (a later long LOST run inside the episode moves it again);
+    * the first node of a segment gets no odometry edge (T = corr @ raw, provisional); nodes
+      created while RELOCALIZING get a relocalisation item instead of a loop item, due at
+      g + ``reloc_latency`` (items stay in order: an item is never due before the one before it);
+    * a relocalisation item of node idx (skipped unless still RELOCALIZING and idx >= seg_start)
+      votes against the positions [max(0, idx - cap_k + M), anchor_end - 1] (M of
+      ``candidate_window``: still in the ring) with ``best_vote``, needs ``loop_min_votes`` and a
+      verification with status 0 and ``loop_min_inliers``; then Z = M_pc T_qc^-1 M_q^-1, the
+      segment's nodes move rigidly by D = T_c Z T_idx^-1 (T_i <- D T_i for i >= seg_start), the
+      edge (c, idx) joins the graph, corr <- D corr, ``last_loop`` = idx, and tracking resumes
+      (``relocs`` gets (frame of c, g, inliers));
+    * span solves re-chain later nodes by odometry only up to a segment break; ``state`` is
+      "relocalizing" for every frame of the episode (the engine publishes None), "lost" for other
+      LOST frames, "tracking" otherwise.
 
     A session of any length keeps the newest cap_k keyframes searchable, and the span solve bounds
     a loop's cost by the ring (<= cap_k nodes).  ``vote(idx, q, lo, n)`` -> votes [n * P],
@@ -310,27 +345,52 @@ class LoopPolicy:
         self.frames, self.raw, self.T, self.odo = [], [], [], []
         self.edges, self.meas = [], []
         self.loops, self.loop_pairs = [], []
-        self.items = []   # [idx, g, due]
+        self.rejected = []   # (frame of c, g) of loops whose span solve failed
+        self.items = []   # [idx, g, due, kind] (kind "loop" or "reloc")
         self.corr = np.eye(4)
         self.cost = 0.0
         self.last_loop = None   # node of the last closed loop
+        # relocalisation after a LOST run
+        self.reloc_after = int(getattr(cfg, "reloc_after_lost", 0))
+        self.reloc_latency = int(getattr(cfg, "reloc_latency", 0))
+        self.lost_run = 0
+        self.reloc = False        # RELOCALIZING
+        self.anchor_end = 0       # candidates of the episode: nodes < anchor_end
+        self.seg_start = 0        # first node of the unanchored segment
+        self.relocs = []          # (frame of c, g, inliers)
+        self.last_due = -1
+        self.state = "tracking"
+
+    def observe(self, g: int, status: int) -> None:
+        """The LOST-run bookkeeping of frame g (first part of ``step``)."""
+        if status == 1:
+            self.lost_run += 1
+            if self.reloc_after > 0 and self.lost_run == self.reloc_after and self.frames:
+                if not self.reloc:
+                    self.reloc = True
+                    self.anchor_end = len(self.frames)
+                self.seg_start = len(self.frames)
+        else:
+            self.lost_run = 0
 
     def step(self, g: int, status: int, raw: np.ndarray) -> np.ndarray:
-        """Frame g -> its corrected pose (rect-left world_T_cam)."""
+        """Frame g -> its corrected pose (rect-left world_T_cam); ``state`` says how to publish it."""
+        self.observe(g, status)
         if status == 0 and g % self.cfg.loop_kf_interval == 0:
             self._node(g, raw)
         while self.items and self.items[0][2] <= g:
-            self._complete(*self.items.pop(0)[:2])
+            self._complete(*self.items.pop(0))
+        self.state = "relocalizing" if self.reloc else "lost" if status == 1 else "tracking"
         return self.corr @ raw
 
     def finish(self) -> None:
         """Complete every pending item now (HipSlamEngine.settle)."""
         while self.items:
-            self._complete(*self.items.pop(0)[:2])
+            self._complete(*self.items.pop(0))
 
     def _node(self, g: int, raw: np.ndarray) -> None:
         idx = len(self.frames)
-        if idx == 0:
+        if idx == 0 or (self.reloc and idx == self.seg_start):   # the first node of a segment
             T, Z = self.corr @ raw, None
         else:
             Z = inv_se3(self.raw[-1]) @ raw
@@ -341,9 +401,15 @@ class LoopPolicy:
         self.raw.append(np.array(raw, dtype=np.float64, copy=True))
         self.T.append(T)
         self.odo.append(Z)
-        self.items.append([idx, g, g + int(self.cfg.loop_latency)])
+        kind = "reloc" if self.reloc else "loop"
+        due = max(g + (self.reloc_latency if self.reloc else int(self.cfg.loop_latency)), self.last_due)
+        self.last_due = due
+        self.items.append([idx, g, due, kind])
 
-    def _complete(self, idx: int, g: int) -> None:
+    def _complete(self, idx: int, g: int, due: int = 0, kind: str = "loop") -> None:
+        if kind == "reloc":
+            self._relocate(idx, g)
+            return
         cfg, P = self.cfg, self.P
         lo, hi = candidate_window(idx, self.cap_k, cfg.loop_min_gap, cfg.loop_latency, cfg.batch_size,
                                   cfg.loop_kf_interval)
@@ -358,16 +424,57 @@ class LoopPolicy:
             return
         if self.last_loop is not None and idx - self.last_loop <= int(getattr(cfg, "loop_cooldown", 0)):
             return
+        edges = self.edges + [(c, idx)]
+        meas = self.meas + [self.m[pc] @ inv_se3(ver["T"]) @ inv_se3(self.m[q])]
+        sel = span_edges(edges, c, idx)
+        try:
+            sol = self.solve(np.stack(self.T[c:idx + 1]), np.array([edges[e] for e in sel]) - c,
+                             np.stack([meas[e] for e in sel]), np.stack([self.info] * len(sel)), cfg.pg_iters)
+            ok = bool(np.all(np.isfinite(sol["T"])))
+        except (np.linalg.LinAlgError, SpanSolveFailed):
+            ok = False
+        if not ok:
+            self.rejected.append((self.frames[c], g))
+            return
         self.last_loop = idx
-        self.edges.append((c, idx))
-        self.meas.append(self.m[pc] @ inv_se3(ver["T"]) @ inv_se3(self.m[q]))
+        self.edges, self.meas = edges, meas
         self.loops.append((self.frames[c], g, int(ver["stats"][2])))
         self.loop_pairs.append((pc, q))
-        sel = span_edges(self.edges, c, idx)
-        sol = self.solve(np.stack(self.T[c:idx + 1]), np.array([self.edges[e] for e in sel]) - c,
-                         np.stack([self.meas[e] for e in sel]), np.stack([self.info] * len(sel)), cfg.pg_iters)
         self.T[c:idx + 1] = list(sol["T"])
         for i in range(idx + 1, len(self.T)):
+            if self.odo[i] is None:   # a segment break: the nodes after it are anchored otherwise
+                break
             self.T[i] = self.T[i - 1] @ self.odo[i]
         self.corr = self.T[-1] @ inv_se3(self.raw[-1])
         self.cost = float(sol["cost"])
+
+    def reloc_window(self, idx: int) -> tuple[int, int]:
+        """Database positions [lo, hi] a relocalisation item of node idx votes against."""
+        cfg = self.cfg
+        margin = (cfg.loop_latency + 2 * cfg.batch_size - 1) // cfg.loop_kf_interval + 1
+        return max(0, idx - self.cap_k + margin), self.anchor_end - 1
+
+    def _relocate(self, idx: int, g: int) -> None:
+        cfg, P = self.cfg, self.P
+        if not self.reloc or idx < self.seg_start:
+            return
+        lo, hi = self.reloc_window(idx)
+        if hi < lo:
+            return
+        best, q, j = best_vote([self.vote(idx, qq, lo, hi - lo + 1) for qq in range(P)], P)
+        if best < cfg.loop_min_votes:
+            return
+        c, pc = lo + j // P, j % P
+        ver = self.verify(idx, g, q, c, pc)
+        if int(ver["stats"][0]) != 0 or int(ver["stats"][2]) < cfg.loop_min_inliers:
+            return
+        Z = self.m[pc] @ inv_se3(ver["T"]) @ inv_se3(self.m[q])
+        D = self.T[c] @ Z @ inv_se3(self.T[idx])
+        for i in range(self.seg_start, len(self.T)):
+            self.T[i] = D @ self.T[i]
+        self.edges.append((c, idx))
+        self.meas.append(Z)
+        self.corr = D @ self.corr
+        self.relocs.append((self.frames[c], g, int(ver["stats"][2])))
+        self.reloc = False
+        self.last_loop = idx

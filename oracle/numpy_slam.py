@@ -480,8 +480,15 @@ def p3p(pw: list, f: list):
 
     pw[k], f[k]: world points / unit bearings of the 3 samples, each a list of 3 arrays (H,).
     Returns R (H, 4, 3, 3), t (H, 4, 3) and a validity mask (H, 4), solutions ordered by the
-    ascending root v = s3 / s1.
+    ascending root v = s3 / s1.  Degenerate samples (coincident or collinear points, coincident
+    bearings) divide by zero and produce NaN / inf on purpose, as the kernel does: those
+    solutions fail the finiteness tests (IEEE semantics, no warnings).
     """
+    with np.errstate(all="ignore"):
+        return _p3p(pw, f)
+
+
+def _p3p(pw: list, f: list):
     a2 = _dot(_sub(pw[1], pw[2]), _sub(pw[1], pw[2]))
     b2 = _dot(_sub(pw[0], pw[2]), _sub(pw[0], pw[2]))
     c2 = _dot(_sub(pw[0], pw[1]), _sub(pw[0], pw[1]))
@@ -512,34 +519,32 @@ def p3p(pw: list, f: list):
     q2 = q2 + 4.0 * ((e0 * g2 + e1 * g1) + e2 * g0)
     q1 = q1 + 4.0 * (e0 * g1 + e1 * g0)
     q0 = q0 + 4.0 * (e0 * g0)
-    with np.errstate(all="ignore"):
-        roots = _roots([q0, q1, q2, q3, q4], 0.0, P3P_VMAX)
+    roots = _roots([q0, q1, q2, q3, q4], 0.0, P3P_VMAX)
     nh = q0.shape[0]
     rot = np.full((nh, 4, 3, 3), np.nan)
     trn = np.full((nh, 4, 3), np.nan)
     ok = np.zeros((nh, 4), dtype=bool)
     fw = _frame(pw[0], pw[1], pw[2])
-    with np.errstate(all="ignore"):
-        for s in range(4):
-            v = roots[:, s]
-            num = (n0 + n1 * v) + n2 * (v * v)
-            den = 2.0 * (cg - ca * v)
-            u = num / den
-            s1sq = b2 / ((1.0 + v * v) - 2.0 * cb * v)
-            good = np.isfinite(v) & (u > 0) & (s1sq > 0) & np.isfinite(u) & np.isfinite(s1sq)
-            s1 = np.sqrt(np.where(good, s1sq, 1.0))
-            s2 = u * s1
-            s3 = v * s1
-            pc = [[f[0][k] * s1 for k in range(3)], [f[1][k] * s2 for k in range(3)], [f[2][k] * s3 for k in range(3)]]
-            fc = _frame(pc[0], pc[1], pc[2])
-            for i in range(3):
-                for j in range(3):
-                    rot[:, s, i, j] = (fc[0][i] * fw[0][j] + fc[1][i] * fw[1][j]) + fc[2][i] * fw[2][j]
-            for i in range(3):
-                rp = (rot[:, s, i, 0] * pw[0][0] + rot[:, s, i, 1] * pw[0][1]) + rot[:, s, i, 2] * pw[0][2]
-                trn[:, s, i] = pc[0][i] - rp
-            good &= np.isfinite(rot[:, s]).all((1, 2)) & np.isfinite(trn[:, s]).all(1)
-            ok[:, s] = good
+    for s in range(4):
+        v = roots[:, s]
+        num = (n0 + n1 * v) + n2 * (v * v)
+        den = 2.0 * (cg - ca * v)
+        u = num / den
+        s1sq = b2 / ((1.0 + v * v) - 2.0 * cb * v)
+        good = np.isfinite(v) & (u > 0) & (s1sq > 0) & np.isfinite(u) & np.isfinite(s1sq)
+        s1 = np.sqrt(np.where(good, s1sq, 1.0))
+        s2 = u * s1
+        s3 = v * s1
+        pc = [[f[0][k] * s1 for k in range(3)], [f[1][k] * s2 for k in range(3)], [f[2][k] * s3 for k in range(3)]]
+        fc = _frame(pc[0], pc[1], pc[2])
+        for i in range(3):
+            for j in range(3):
+                rot[:, s, i, j] = (fc[0][i] * fw[0][j] + fc[1][i] * fw[1][j]) + fc[2][i] * fw[2][j]
+        for i in range(3):
+            rp = (rot[:, s, i, 0] * pw[0][0] + rot[:, s, i, 1] * pw[0][1]) + rot[:, s, i, 2] * pw[0][2]
+            trn[:, s, i] = pc[0][i] - rp
+        good &= np.isfinite(rot[:, s]).all((1, 2)) & np.isfinite(trn[:, s]).all(1)
+        ok[:, s] = good
     return rot, trn, ok
 
 

@@ -168,6 +168,50 @@ def test_ba_split_solve_equals_fused_handoff():
         np.testing.assert_array_equal(a, runs[True][1][key], err_msg=key)
 
 
+@pytest.mark.parametrize("split", [False, True])
+def test_ba_graph_replay_equals_direct_launches(split):
+    """tslam_ba_graph: each keyframe's chain replayed from a captured hipGraph
+    whose kernels read the keyframe's record (the default) against the direct by-value launches:
+    30 keyframes through the 4-slot window in batches of 6 with IMU rotation and inertial factors
+    on — more replays of the steady-state chain than an instance ring holds (24), so instances are
+    re-pointed at new records — windows, velocities, bias and poses bit-identical."""
+    import torch
+
+    from thor_slam_amd._lib import Handle
+
+    n, batch = 60, 6
+    sc = scenario(seed=0, n=n, cfg_items=BA_ITEMS)
+    imu, ine = _imu_factors(sc, n), _inertial_factors(sc, n)
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    runs = {}
+    for graph in (False, True):
+        h = Handle([sc["rect"]], sc["cfg"], max_batch=batch)
+        try:
+            h.ba_graph(graph)
+            h.ba_split_solve(split)
+            h.ba_inertial(*INE_CFG)
+            for g, (M, w) in imu.items():
+                h.ba_imu_factor(g, M, w)
+            for g, (f, v0) in ine.items():
+                h.ba_inertial_factor(g, f, v0)
+            snaps = []
+            for b0 in range(0, n, batch):
+                h.submit(dev[b0:].data_ptr(), batch, torch.cuda.current_stream().cuda_stream)
+                snaps.append((h.ba_read(0), h.ba_read_inertial(0)))
+            runs[graph] = (snaps, h.read_poses(batch))
+        finally:
+            h.close()
+    for k, ((a, ai), (b, bi)) in enumerate(zip(runs[False][0], runs[True][0])):
+        for key in ("frames", "lm", "T_cw", "X"):
+            np.testing.assert_array_equal(np.asarray(a[key]).view(np.uint8), np.asarray(b[key]).view(np.uint8),
+                                          err_msg=f"batch {k} {key}")
+        np.testing.assert_array_equal(ai["vel"], bi["vel"])
+        np.testing.assert_array_equal(ai["ba"], bi["ba"])
+        assert a["ok"] and a["n_lm"] == b["n_lm"] > 50
+    for key, a in runs[False][1].items():
+        np.testing.assert_array_equal(a, runs[True][1][key], err_msg=key)
+
+
 def test_ba_imu_rotation_factors_parity():
     """IMU rotation factors between window-consecutive keyframes (tslam_ba_imu_factor) against the
     oracle's imu_terms: same windows to 1e-9, through evictions, in batches of 3 — and the factors

@@ -99,6 +99,56 @@ def test_pose_graph_rejects_bad_graphs():
     h.close()
 
 
+def test_degenerate_span_is_singular_on_the_device():
+    """A span with a free gauge direction (test_oracle_loop_policy.degenerate_span: zero residuals,
+    the last edge informs translation only) fails the device's Cholesky exactly where the oracle's
+    does: TSLAM_ESINGULAR (SingularSystemError) from the synchronous solve and from a loop job,
+    after which the handle solves a well-posed graph as before."""
+    from test_oracle_loop_policy import degenerate_span
+    from thor_slam_amd._lib import Handle, SingularSystemError
+
+    T, edges, Z, info = degenerate_span()
+    with pytest.raises(np.linalg.LinAlgError):
+        L.optimize(T, edges, Z, info, 3)
+    h = Handle([_rect(_loop_source())], HipSlamConfig(), max_batch=1)
+    with pytest.raises(SingularSystemError, match="not positive definite"):
+        h.pose_graph(T, edges, Z, info, 3)
+    h.loop_init(64, 256)
+    job = h.loop_job_pose_graph(T, edges, Z, info, 3)
+    with pytest.raises(SingularSystemError):
+        job.result(block=True)
+    T0, e0, Z0, i0 = _random_graph(np.random.default_rng(30), 30, [(0, 29), (4, 21)])
+    got = h.pose_graph(T0, e0, Z0, i0, 6)
+    want = L.optimize(T0, e0, Z0, i0, 6)
+    assert max(rel_frobenius(a, b) for a, b in zip(got["T"], want["T"])) < 1e-9
+    h.close()
+
+
+def test_potrf_late_blocks_read_the_unfactored_tile():
+    """Regression for the k_pg_potrf diagonal-tile race (fixed in round 5): with
+    tslam_test_potrf_delay every block >= 1 of each panel launch reads A_kk only after block 0
+    has stored its factor (~100 us late), the read order under which the former in-place store of
+    L_kk handed late blocks a factored tile.  The solve must be bit-identical to the undelayed
+    one and equal the oracle's Gauss-Newton (a 200-node graph: 38 tile panels)."""
+    from thor_slam_amd._lib import Handle, load_library
+
+    lib = load_library()
+    rng = np.random.default_rng(200)
+    T0, edges, Z, info = _random_graph(rng, 200, [(0, 199), (10, 150), (50, 120), (3, 90)])
+    h = Handle([_rect(_loop_source())], HipSlamConfig(), max_batch=1)
+    base = h.pose_graph(T0, edges, Z, info, 4)
+    assert lib.tslam_test_potrf_delay(30) == 0
+    try:
+        late = h.pose_graph(T0, edges, Z, info, 4)
+    finally:
+        assert lib.tslam_test_potrf_delay(0) == 0
+    h.close()
+    np.testing.assert_array_equal(late["T"], base["T"])
+    assert late["cost"] == base["cost"]
+    want = L.optimize(T0, edges, Z, info, 4)
+    assert max(rel_frobenius(a, b) for a, b in zip(late["T"], want["T"])) < 1e-9
+
+
 def test_keyframe_database_votes_and_verification():
     import torch
 
@@ -306,3 +356,22 @@ def test_rig_loop_seen_only_by_pair_1():
     print("pair-1-only loop: %s; keyframe error raw max %.4f m, optimised max %.4f m"
           % (loops, max(err_raw), max(err_opt)))
     eng.shutdown()
+
+
+def test_growing_pose_graph_jobs_without_polling():
+    """a small pose-graph job, then larger ones, submitted back to back without a poll
+    in between — the scratch grows under the queued jobs (the reserve drains the loop worker and
+    stream first) — and every job returns the oracle's solve."""
+    from thor_slam_amd._lib import Handle
+
+    h = Handle([_rect(_loop_source())], HipSlamConfig(), max_batch=1)
+    graphs, jobs = [], []
+    for N, loops in ((6, [(0, 5)]), (40, [(0, 39), (5, 30)]), (120, [(0, 119), (7, 80), (40, 100)])):
+        g = _random_graph(np.random.default_rng(N), N, loops)
+        graphs.append(g)
+        jobs.append(h.loop_job_pose_graph(*g, 5))
+    for g, job in zip(graphs, jobs):
+        got = job.result(block=True)
+        want = L.optimize(*g, 5)
+        assert max(rel_frobenius(a, b) for a, b in zip(got["T"], want["T"])) < 1e-9
+    h.close()

@@ -164,7 +164,7 @@ def test_loop_jobs_equal_synchronous_calls():
     man.close()
 
 
-def _run_default(frames, n_frames, settle=False):
+def _run_default(frames, n_frames, settle=False, hook=None):
     """The reference's default drop-in construction (scripts/run_slam.py:299-300 after the swap):
     HipSlamEngine(num_cameras=2) + initialize(rig.calibration), no config — batch 1, loop closure
     on (SlamConfig.enable_loop_closure), the rig's identity IMU idle.  Returns per frame the
@@ -178,6 +178,8 @@ def _run_default(frames, n_frames, settle=False):
     eng.initialize(rig.calibration)
     assert eng._config.batch_size == 1 and eng._config.enable_loop_closure and eng._async
     eng._loop.trace = {}
+    if hook is not None:
+        hook(eng)
     recs, published = [], {}
     orig = eng._publish
 
@@ -197,7 +199,7 @@ def _run_default(frames, n_frames, settle=False):
     return published, recs, eng
 
 
-def _policy_from_trace(eng, recs, solve_check_every=0):
+def _policy_from_trace(eng, recs, solve_check_every=0, finish=False):
     """oracle LoopPolicy on the engine's tracked poses, with the device's votes / verifications
     (the trace) and — for the solves — the device's results after asserting the policy built the
     same inputs (every ``solve_check_every``-th solve, and the last, re-solved by the oracle's
@@ -227,6 +229,8 @@ def _policy_from_trace(eng, recs, solve_check_every=0):
         np.testing.assert_array_equal(T, t_in)
         np.testing.assert_array_equal(edges, e_in)
         np.testing.assert_array_equal(meas, m_in)
+        if sol is None:   # the device rejected this span solve (TSLAM_ESINGULAR)
+            raise L.SpanSolveFailed(str(idx))
         if (solve_check_every and state["i"] % solve_check_every == 1) or state["i"] == len(solves) or len(solves) < 8:
             ora = L.optimize(T, edges, meas, info, iters)
             err = max(np.linalg.norm(a - b) / np.linalg.norm(b) for a, b in zip(sol["T"], ora["T"]))
@@ -243,6 +247,8 @@ def _policy_from_trace(eng, recs, solve_check_every=0):
             raw = _invert(bt) @ body @ bt   # the engine's rect-left pose before loop correction
             corr = pol.step(g0 + k, int(st[k]), raw)
             out[g0 + k] = None if int(st[k]) == 1 else bt @ corr @ _invert(bt)
+    if finish:   # HipSlamEngine.settle
+        pol.finish()
     return pol, out, checked
 
 
@@ -296,4 +302,44 @@ def test_long_session_keeps_closing_loops():
     pol, want, checked = _policy_from_trace(eng, recs, solve_check_every=17)
     assert lp.loops == pol.loops and len(checked) >= 10
     _compare(published, want, n)
+    eng.shutdown()
+
+
+def test_rejected_loop_solve_keeps_the_session_running():
+    """the first loop's span solve is handed an uninformative span (every
+    edge's information zeroed — every direction of the span is a free gauge, the normal matrix is
+    0).  The device's Cholesky fails (TSLAM_ESINGULAR) where the oracle's does (LinAlgError); the
+    engine rejects that loop as LoopPolicy defines — no edge, no correction, the cooldown not
+    armed — and process_frames keeps returning poses: every published pose equals the policy's,
+    and the next keyframe's loop is closed."""
+    frames = _render_many(list(range(LOOP_FRAMES)))
+    zeroed = []
+
+    def hook(eng):
+        h = eng._loop.h
+        orig = h.loop_job_pose_graph
+
+        def degenerate_first(T, edges, meas, info, iters):
+            if not zeroed:
+                info = np.zeros_like(info)
+                zeroed.append((np.array(T), np.array(edges), np.array(meas), info))
+            return orig(T, edges, meas, info, iters)
+
+        h.loop_job_pose_graph = degenerate_first
+
+    # settle: the searches still pending at the end (the keyframes after the rejected one) complete
+    published, recs, eng = _run_default(frames, LOOP_FRAMES, settle=True, hook=hook)
+    assert zeroed
+    with pytest.raises(np.linalg.LinAlgError):   # the oracle fails the same span
+        L.optimize(*zeroed[0], eng._config.pg_iters)
+    lp = eng._loop
+    pol, want, _ = _policy_from_trace(eng, recs, finish=True)
+    assert len(lp.rejected) == 1 and lp.rejected == pol.rejected, (lp.rejected, pol.rejected)
+    assert "not positive definite" in lp.failures[0]["error"]
+    assert lp.loops and lp.loops == pol.loops
+    assert lp.loops[0][1] > lp.rejected[0][1]   # a later keyframe closed its loop
+    a_node, b_node = (lp.frames.index(f) for f in lp.rejected[0])
+    assert (a_node, b_node) not in lp.edges
+    _compare(published, want, LOOP_FRAMES)
+    assert sum(p is not None for p in published.values()) >= LOOP_FRAMES - 2
     eng.shutdown()

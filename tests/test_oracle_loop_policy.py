@@ -113,3 +113,84 @@ def test_ring_wrap_keeps_searching():
     for idx, lo, n in sc.votes:
         assert lo >= idx - 64 + 7 and lo + n - 1 == idx - 20
     assert pol.loops[-1][1] > 1100
+
+
+def degenerate_span(n: int = 4) -> tuple:
+    """A span whose normal matrix is singular: a chain of ``n`` nodes whose edge measurements equal
+    the poses exactly (every residual 0, so every Jacobian is the adjoint alone) and whose last
+    edge carries translation information only — the last node's rotation is a free gauge
+    direction, its diagonal block diag(1, 1, 1, 0, 0, 0) gives an exactly zero Cholesky pivot."""
+    T = np.stack([_lap_pose(5 * i) for i in range(n)])
+    edges = np.array([(i, i + 1) for i in range(n - 1)])
+    Z = np.stack([L.inv_se3(T[a]) @ T[b] for a, b in edges])
+    info = np.stack([L.loop_information(0.01, 0.005)] * (n - 2) + [np.diag([1.0, 1.0, 1.0, 0.0, 0.0, 0.0])])
+    return T, edges, Z, info
+
+
+def test_degenerate_span_fails_the_oracle_solve():
+    T, edges, Z, info = degenerate_span()
+    try:
+        L.optimize(T, edges, Z, info, 3)
+    except np.linalg.LinAlgError:
+        pass
+    else:
+        raise AssertionError("a span with a free gauge direction solved")
+    # the well-posed chain (full information everywhere) solves and stays put (zero residuals)
+    ok = L.optimize(T, edges, Z, np.stack([L.loop_information(0.01, 0.005)] * len(edges)), 3)
+    np.testing.assert_allclose(ok["T"], T, atol=1e-12)
+
+
+def test_rejected_span_solve_leaves_poses_uncorrected_and_the_session_running():
+    """A span solve that fails (LinAlgError from the oracle, SpanSolveFailed from a device
+    callable) drops that loop: no edge, no correction, the cooldown not armed; the next loop is
+    closed as usual, and every frame still gets a pose."""
+    lap = 100
+    for exc in (np.linalg.LinAlgError, L.SpanSolveFailed):
+        cfg = HipSlamConfig(loop_latency=0, loop_cooldown=50)
+        sc = _Scripted(lap, cfg.loop_kf_interval)
+        calls = {"n": 0}
+
+        def solve(T, edges, meas, info, iters, exc=exc):
+            calls["n"] += 1
+            if calls["n"] == 1:
+                raise exc("normal matrix not positive definite")
+            return L.optimize(T, edges, meas, info, iters)
+
+        pol = L.LoopPolicy(cfg, 1, [np.eye(4)], sc.vote, sc.verify, solve)
+        ref = L.LoopPolicy(cfg, 1, [np.eye(4)], sc.vote, sc.verify, sc.solve)
+        out = []
+        for g in range(260):
+            raw = _lap_pose(g, lap) @ _drift(g)
+            status = 2 if g == 0 else 0
+            if status == 0 and g % cfg.loop_kf_interval == 0:
+                sc.frames.append(g)
+            out.append(pol.step(g, status, raw))
+            ref.step(g, status, raw)
+            if not pol.loops:
+                np.testing.assert_array_equal(out[-1], raw)   # uncorrected until a loop is closed
+        assert len(pol.rejected) == 1 and ref.loops and not ref.rejected
+        rej_c, rej_g = pol.rejected[0]
+        assert rej_g == ref.loops[0][1]   # the first loop found is the rejected one
+        # the cooldown counts closed loops only: the keyframe after the rejected one closes its loop
+        assert pol.loops[0][1] == rej_g + cfg.loop_kf_interval, (pol.loops[:2], rej_g)
+        assert (pol.frames.index(rej_c), pol.frames.index(rej_g)) not in pol.edges
+        assert len(pol.edges) == len(pol.frames) - 1 + len(pol.loops)
+
+
+def test_non_finite_solution_is_rejected():
+    """A solve that returns a non-finite pose (the device's NaN propagation) is rejected too."""
+    cfg = HipSlamConfig(loop_latency=0, loop_cooldown=0)
+    sc = _Scripted(100, cfg.loop_kf_interval)
+
+    def solve(T, edges, meas, info, iters):
+        sol = L.optimize(T, edges, meas, info, iters)
+        sol["T"][-1, 0, 0] = np.nan
+        return sol
+
+    pol = L.LoopPolicy(cfg, 1, [np.eye(4)], sc.vote, sc.verify, solve)
+    for g in range(160):
+        raw = _lap_pose(g, 100) @ _drift(g)
+        if g and g % cfg.loop_kf_interval == 0:
+            sc.frames.append(g)
+        np.testing.assert_array_equal(pol.step(g, 2 if g == 0 else 0, raw), raw)
+    assert pol.rejected and not pol.loops

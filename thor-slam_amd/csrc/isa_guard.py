@@ -49,7 +49,7 @@ _BASE = re.compile(r"^_Z(\d+)")
 
 # hand-off kernel -> the agent-scope loads its last block must issue for the published data
 # (k_ba_reduce_solve: C as 4096 / 512 threads = 8 loads per thread, and the camera blocks: 1)
-HANDOFF = {"k_ba_reduce_solve": 9, "k_ba_reduce_solve_ine": 9}
+HANDOFF = {"k_ba_reduce_solve": 9, "k_ba_reduce_solve_ine": 9, "k_ba_reduce_solve_rec": 9, "k_ba_reduce_solve_ine_rec": 9}
 
 
 def _run(*args: str) -> str:

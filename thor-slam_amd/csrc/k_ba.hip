@@ -24,6 +24,7 @@
 // Every reduction has a fixed order, so a solve is deterministic run to run.  Floating-point
 // results differ from the oracle's (LU solves, numpy summation order) at the 1e-14 level.
 #include "tslam_ba.h"
+#include <cstring>
 
 // ---------------------------------------------------------------------------------------------
 // small dense helpers (f64)
@@ -59,13 +60,20 @@ __device__ __forceinline__ bool kp_obs(const BatchCtx& c, int slot, int cam, int
     return true;
 }
 
+// The *_rec entry points read the batch context and the arguments from a device record
+// (BaRec, graph replays) through constant-address-space pointers: the record is immutable during
+// the launch, so its fields come in through scalar loads and the pointers loaded from it stay
+// global (a generic pointer to the record would turn every access through them into flat ones).
+typedef const __attribute__((address_space(4))) BatchCtx* __restrict__ BaCtxRef;
+typedef const __attribute__((address_space(4))) BaArgs* __restrict__ BaArgsRef;
+
 // ---------------------------------------------------------------------------------------------
 // keyframe insertion (after the batch that contains frame g) and eviction
 // ---------------------------------------------------------------------------------------------
 // Eviction of slot a.slot: each landmark homed there moves to its observation in the oldest
 // remaining keyframe (a.order, oldest first).  Pass 1 takes the minimum (rank, keypoint) key per
 // landmark (remap pre-filled with a large value), pass 2 rewrites the ids and copies the position.
-__global__ __launch_bounds__(256) void k_ba_evict_min(BatchCtx c, BaArgs a) {
+__device__ __forceinline__ void d_ba_evict_min(const BatchCtx& c, const BaArgs& a) {
     BA_PRIO;
     const int K = c.g.K;
     BaPair q = ba_pair(c, a, a.pair);
@@ -75,8 +83,12 @@ __global__ __launch_bounds__(256) void k_ba_evict_min(BatchCtx c, BaArgs a) {
     const int id = q.lm[(size_t)a.order[r] * K + k], lo = a.slot * K;
     if (id >= lo && id < lo + K) atomicMin(&q.remap[id - lo], i);
 }
+__global__ __launch_bounds__(256) void k_ba_evict_min(BatchCtx c, BaArgs a) { d_ba_evict_min(c, a); }
+__global__ __launch_bounds__(256) void k_ba_evict_min_rec(BaCtxRef c, BaArgsRef a) {
+    d_ba_evict_min(*(const BatchCtx*)c, *(const BaArgs*)a);
+}
 
-__global__ __launch_bounds__(256) void k_ba_evict_move(BatchCtx c, BaArgs a) {
+__device__ __forceinline__ void d_ba_evict_move(const BatchCtx& c, const BaArgs& a) {
     BA_PRIO;
     const int K = c.g.K;
     BaPair q = ba_pair(c, a, a.pair);
@@ -94,6 +106,10 @@ __global__ __launch_bounds__(256) void k_ba_evict_move(BatchCtx c, BaArgs a) {
         for (int e = 0; e < 3; ++e) q.X[(size_t)nid * 3 + e] = q.X[(size_t)id * 3 + e];
         q.gid[nid] = q.gid[id];
     }
+}
+__global__ __launch_bounds__(256) void k_ba_evict_move(BatchCtx c, BaArgs a) { d_ba_evict_move(c, a); }
+__global__ __launch_bounds__(256) void k_ba_evict_move_rec(BaCtxRef c, BaArgsRef a) {
+    d_ba_evict_move(*(const BatchCtx*)c, *(const BaArgs*)a);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -137,7 +153,7 @@ __device__ int block_scan_excl(int v, int* s_tmp, int* total) {
 // stored (positive depth, reprojection error <= outlier_px) and every gated observation counts
 // towards its landmark (cnt pre-zeroed).  No other item reads what an inserting thread writes: the
 // new slot's landmarks are observed by the new keyframe only (eviction re-homed the slot's old ones).
-__global__ __launch_bounds__(256) void k_ba_insert_gate(BatchCtx c, BaArgs a) {
+__device__ __forceinline__ void d_ba_insert_gate(const BatchCtx& c, const BaArgs& a) {
     BA_PRIO;
     __shared__ double s_T[TS_BA_MAXW][12];   // cam_T_world of the window
     __shared__ double s_Tn[16];              // the new keyframe's
@@ -247,6 +263,10 @@ __global__ __launch_bounds__(256) void k_ba_insert_gate(BatchCtx c, BaArgs a) {
     }
     q.keep[i] = (uint8_t)keep;
 }
+__global__ __launch_bounds__(256) void k_ba_insert_gate(BatchCtx c, BaArgs a) { d_ba_insert_gate(c, a); }
+__global__ __launch_bounds__(256) void k_ba_insert_gate_rec(BaCtxRef c, BaArgsRef a) {
+    d_ba_insert_gate(*(const BatchCtx*)c, *(const BaArgs*)a);
+}
 
 // Compaction after the gate, as a deterministic tiled scan (tiles of BA_TILE items):
 //   landmark tiles over the ids (flag: >= 2 gated observations) -> compact index li = rank of the
@@ -307,7 +327,7 @@ __device__ __forceinline__ void ba_tile_flags(const BatchCtx& c, const BaArgs& a
     }
 }
 
-__global__ __launch_bounds__(256) void k_ba_tilecount(BatchCtx c, BaArgs a) {
+__device__ __forceinline__ void d_ba_tilecount(const BatchCtx& c, const BaArgs& a) {
     BA_PRIO;
     __shared__ int s_tmp[32];
     __shared__ __attribute__((aligned(4))) uint8_t s_fl[256];   // thread t's flags: bits 8t .. 8t+7 of the tile
@@ -345,11 +365,15 @@ __global__ __launch_bounds__(256) void k_ba_tilecount(BatchCtx c, BaArgs a) {
         q.lpre[blockIdx.x * 64 + threadIdx.x] = x - pc;
     }
 }
+__global__ __launch_bounds__(256) void k_ba_tilecount(BatchCtx c, BaArgs a) { d_ba_tilecount(c, a); }
+__global__ __launch_bounds__(256) void k_ba_tilecount_rec(BaCtxRef c, BaArgsRef a) {
+    d_ba_tilecount(*(const BatchCtx*)c, *(const BaArgs*)a);
+}
 
 // Scatter after the tile counts; each block takes its tile's offset from the counts of the tiles
 // before it (landmark tiles and observation tiles are scanned separately), and block 0 also
 // publishes the totals and the per-camera observation ranges (no separate scan launch).
-__global__ __launch_bounds__(256) void k_ba_tilescatter(BatchCtx c, BaArgs a) {
+__device__ __forceinline__ void d_ba_tilescatter(const BatchCtx& c, const BaArgs& a) {
     BA_PRIO;
     __shared__ int s_tmp[32];
     __shared__ int s_cnt[TS_BA_TILES];
@@ -458,6 +482,10 @@ __global__ __launch_bounds__(256) void k_ba_tilescatter(BatchCtx c, BaArgs a) {
             }
     }
 }
+__global__ __launch_bounds__(256) void k_ba_tilescatter(BatchCtx c, BaArgs a) { d_ba_tilescatter(c, a); }
+__global__ __launch_bounds__(256) void k_ba_tilescatter_rec(BaCtxRef c, BaArgsRef a) {
+    d_ba_tilescatter(*(const BatchCtx*)c, *(const BaArgs*)a);
+}
 
 // ---------------------------------------------------------------------------------------------
 // one Gauss-Newton step
@@ -537,7 +565,7 @@ __device__ __forceinline__ void lds_barrier() {
 // Blocks stride the chunks; each block that had a chunk writes its 64 x 64 partial and its camera
 // partial (TS_BA_PART doubles per block: C, then [camera][27]), which k_ba_reduce sums in a fixed
 // order.  The camera sums stay in the block instead of 27 scattered 8-byte stores per observation.
-__global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArgs a) {
+__device__ __forceinline__ void d_ba_schur(const BatchCtx& c, const BaArgs& a, int fused) {
 #pragma clang fp contract(fast)   // single FMAs in the landmark chains (held to 1e-9, as k_ba_solve)
     BA_PRIO;
     // the Schur tile Q (phases 3-4) and the observations' camera blocks (phases 1-2) share LDS
@@ -566,7 +594,7 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
                        16 * ((0x23333 >> (4 * wave)) & 15), 16 * ((0x23210 >> (4 * wave)) & 15)};
     d4v acc[2];
     for (int t = 0; t < 2; ++t) acc[t] = (d4v){0.0, 0.0, 0.0, 0.0};
-    const bool bsub = a.fused_backsub && q.counts[2];   // the previous solve succeeded
+    const bool bsub = fused && q.counts[2];   // the previous solve succeeded
     const int cu_item = (int)threadIdx.x - BA_CHUNK;     // (camera, element) of the camera sums
     double cam_acc = 0.0;
     for (int l0 = blockIdx.x * BA_CHUNK; l0 < L; l0 += gridDim.x * BA_CHUNK) {
@@ -796,6 +824,11 @@ __global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArg
         }
     }
 }
+__global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur(BatchCtx c, BaArgs a) { d_ba_schur(c, a, a.fused_backsub); }
+__global__ __launch_bounds__(BA_SCHUR_THREADS) void k_ba_schur_rec(BaCtxRef c, BaArgsRef a,
+    int fused) {
+    d_ba_schur(*(const BatchCtx*)c, *(const BaArgs*)a, fused);
+}
 
 // Fixed-order sum of the partials of the blocks that had a chunk: block = 64 elements of a
 // partial, BA_SOLVE_WAVES waves each summing every BA_SOLVE_WAVES-th partial, then the wave sums
@@ -820,7 +853,7 @@ __device__ __forceinline__ double ba_reduce_elem(const BaPair& q, const BaArgs& 
     return v;   // meaningful in wave 0
 }
 
-__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce(BatchCtx c, BaArgs a) {
+__device__ __forceinline__ void d_ba_reduce(const BatchCtx& c, const BaArgs& a) {
     BA_PRIO;
     __shared__ double s_p[BA_SOLVE_WAVES][64];
     BaPair q = ba_pair(c, a, a.pair);
@@ -830,6 +863,10 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce(BatchCtx c, B
     if ((threadIdx.x >> 6) != 0 || !live) return;
     if (e < 4096) q.C[e] = v;
     else q.cam_U[e - 4096] = v;
+}
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce(BatchCtx c, BaArgs a) { d_ba_reduce(c, a); }
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_rec(BaCtxRef c, BaArgsRef a) {
+    d_ba_reduce(*(const BatchCtx*)c, *(const BaArgs*)a);
 }
 
 // Reduced camera system (camera 0 = gauge): S = blockdiag(U + lam) - C, b = -g_c + C[:, 60].
@@ -1330,14 +1367,22 @@ __device__ __forceinline__ void ba_solve_block(const BatchCtx& c, const BaArgs& 
 #endif
 }
 
-__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, BaArgs a) {
+__device__ __forceinline__ void d_ba_solve(const BatchCtx& c, const BaArgs& a) {
     BA_PRIO;
     ba_solve_block<false, false>(c, a);
 }
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve(BatchCtx c, BaArgs a) { d_ba_solve(c, a); }
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve_rec(BaCtxRef c, BaArgsRef a) {
+    d_ba_solve(*(const BatchCtx*)c, *(const BaArgs*)a);
+}
 
-__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve_ine(BatchCtx c, BaArgs a) {
+__device__ __forceinline__ void d_ba_solve_ine(const BatchCtx& c, const BaArgs& a) {
     BA_PRIO;
     ba_solve_block<false, true>(c, a);
+}
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve_ine(BatchCtx c, BaArgs a) { d_ba_solve_ine(c, a); }
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_solve_ine_rec(BaCtxRef c, BaArgsRef a) {
+    d_ba_solve_ine(*(const BatchCtx*)c, *(const BaArgs*)a);
 }
 
 // k_ba_reduce and k_ba_solve in one launch (a stereo pair's own solve): the reduction's blocks
@@ -1367,15 +1412,23 @@ __device__ __forceinline__ void ba_reduce_solve_body(const BatchCtx& c, const Ba
     ba_solve_block<true, INE>(c, a);
 }
 
-__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_solve(BatchCtx c, BaArgs a) {
+__device__ __forceinline__ void d_ba_reduce_solve(const BatchCtx& c, const BaArgs& a) {
     BA_PRIO;
     ba_reduce_solve_body<false>(c, a);
 }
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_solve(BatchCtx c, BaArgs a) { d_ba_reduce_solve(c, a); }
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_solve_rec(BaCtxRef c, BaArgsRef a) {
+    d_ba_reduce_solve(*(const BatchCtx*)c, *(const BaArgs*)a);
+}
 
 // with the window's inertial factors (velocities + accelerometer bias eliminated into S)
-__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_solve_ine(BatchCtx c, BaArgs a) {
+__device__ __forceinline__ void d_ba_reduce_solve_ine(const BatchCtx& c, const BaArgs& a) {
     BA_PRIO;
     ba_reduce_solve_body<true>(c, a);
+}
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_solve_ine(BatchCtx c, BaArgs a) { d_ba_reduce_solve_ine(c, a); }
+__global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_solve_ine_rec(BaCtxRef c, BaArgsRef a) {
+    d_ba_reduce_solve_ine(*(const BatchCtx*)c, *(const BaArgs*)a);
 }
 
 
@@ -1384,7 +1437,7 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_solve_ine(Bat
 // the 16 lanes by a fixed xor-butterfly; the first lane then solves dp = V^-1 (-g_p - sum) with
 // the stored Cholesky factor and stores X[lm_id[r]] = Xc[r] + dp (Xc[r] alone when the last
 // solve failed).
-__global__ __launch_bounds__(256) void k_ba_backsub(BatchCtx c, BaArgs a) {
+__device__ __forceinline__ void d_ba_backsub(const BatchCtx& c, const BaArgs& a) {
     BA_PRIO;
     const int WK = a.W * c.g.K;
     BaPair q = ba_pair(c, a, a.pair);
@@ -1436,6 +1489,10 @@ __global__ __launch_bounds__(256) void k_ba_backsub(BatchCtx c, BaArgs a) {
     }
     const int id = q.lm_id[r];
     for (int i = 0; i < 3; ++i) q.X[(size_t)id * 3 + i] = upd ? q.Xc[(size_t)r * 3 + i] + x[i] : q.Xc[(size_t)r * 3 + i];
+}
+__global__ __launch_bounds__(256) void k_ba_backsub(BatchCtx c, BaArgs a) { d_ba_backsub(c, a); }
+__global__ __launch_bounds__(256) void k_ba_backsub_rec(BaCtxRef c, BaArgsRef a) {
+    d_ba_backsub(*(const BatchCtx*)c, *(const BaArgs*)a);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1528,6 +1585,68 @@ void launch_ba_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming
             hipLaunchKernelGGL(inertial ? k_ba_reduce_solve_ine : k_ba_reduce_solve, grid, block, 0, s, c, a);
     }
     launch_ba_backsub(c, a, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+// the keyframe chain by record (graph replays, tslam_api.cpp ba_chain)
+// ---------------------------------------------------------------------------------------------
+struct BaRecWords {
+    uint64_t w[(sizeof(BaRec) + 7) / 8];
+};
+static_assert(sizeof(BaRecWords) + sizeof(void*) <= 4096, "k_ba_setrec's record must fit the kernel arguments");
+
+__global__ __launch_bounds__(64) void k_ba_setrec(BaRecWords r, BaRecWords* d) {
+    for (int i = threadIdx.x; i < (int)(sizeof(BaRecWords) / 8); i += 64) d->w[i] = r.w[i];
+}
+
+void launch_ba_setrec(const BaRec& r, BaRec* d, hipStream_t s) {
+    BaRecWords w{};
+    memcpy(&w, &r, sizeof(BaRec));
+    hipLaunchKernelGGL(k_ba_setrec, dim3(1), dim3(64), 0, s, w, reinterpret_cast<BaRecWords*>(d));
+}
+
+hipError_t ba_graph_set_record(hipGraphExec_t exec, hipGraphNode_t node, const BaRec& r, BaRec* d) {
+    BaRecWords w{};
+    memcpy(&w, &r, sizeof(BaRec));
+    BaRecWords* dw = reinterpret_cast<BaRecWords*>(d);
+    void* args[] = {&w, &dw};
+    hipKernelNodeParams p{};
+    p.func = reinterpret_cast<void*>(k_ba_setrec);
+    p.gridDim = dim3(1);
+    p.blockDim = dim3(64);
+    p.sharedMemBytes = 0;
+    p.kernelParams = args;
+    p.extra = nullptr;
+    return hipGraphExecKernelNodeSetParams(exec, node, &p);
+}
+
+void launch_ba_chain_rec(const BaRec& r, const BaRec* d, bool evict, bool split, bool inertial, hipStream_t s) {
+    const BaCtxRef c = (BaCtxRef)&d->c;
+    const BaArgsRef a = (BaArgsRef)&d->a;
+    const BaArgsRef ev = (BaArgsRef)&d->evict;
+    const int K = r.c.g.K;
+    if (evict) {
+        const int nb = (r.evict.n_order * K + 255) / 256;
+        hipLaunchKernelGGL(k_ba_evict_min_rec, dim3(nb), dim3(256), 0, s, c, ev);
+        hipLaunchKernelGGL(k_ba_evict_move_rec, dim3(nb), dim3(256), 0, s, c, ev);
+    }
+    const BaArgs& ha = r.a;
+    const int WK = ha.W * K;
+    hipLaunchKernelGGL(k_ba_insert_gate_rec, dim3((ha.n_order * K + 255) / 256), dim3(256), 0, s, c, a);
+    const int ntiles = (WK + BA_TILE - 1) / BA_TILE + ha.n_order * ((K + BA_TILE - 1) / BA_TILE);
+    hipLaunchKernelGGL(k_ba_tilecount_rec, dim3(ntiles), dim3(256), 0, s, c, a);
+    hipLaunchKernelGGL(k_ba_tilescatter_rec, dim3(ntiles), dim3(256), 0, s, c, a);
+    const dim3 grid(64 + (ha.n_order * 27 + 63) / 64), block(64 * BA_SOLVE_WAVES);
+    for (int it = 0; it < ha.iters; ++it) {
+        hipLaunchKernelGGL(k_ba_schur_rec, dim3(ha.nsplit), dim3(BA_SCHUR_THREADS), 0, s, c, a, it > 0 ? 1 : 0);
+        if (split) {
+            hipLaunchKernelGGL(k_ba_reduce_rec, grid, block, 0, s, c, a);
+            hipLaunchKernelGGL(inertial ? k_ba_solve_ine_rec : k_ba_solve_rec, dim3(1), block, 0, s, c, a);
+        } else {
+            hipLaunchKernelGGL(inertial ? k_ba_reduce_solve_ine_rec : k_ba_reduce_solve_rec, grid, block, 0, s, c, a);
+        }
+    }
+    hipLaunchKernelGGL(k_ba_backsub_rec, dim3(16 * ((WK + 255) / 256)), dim3(256), 0, s, c, a);
 }
 
 // ---------------------------------------------------------------------------------------------

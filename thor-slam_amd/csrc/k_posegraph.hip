@@ -23,6 +23,7 @@
 //                  diagonal systems with lane broadcasts, the block updates the rest);
 //   k_pg_update    thread per free node: T_i <- T_i Exp(delta_i).
 #include "tslam_common.h"
+#include <atomic>
 
 #define PG_TILE 32
 #define PG_TERMS 128   // doubles per edge: H_aa 36, H_ab 36, H_bb 36, g_a 6, g_b 6, cost 1
@@ -286,10 +287,15 @@ __device__ __forceinline__ void pg_factor_tile(const double* H, int np, size_t d
 // panel k: block 0 stores L_kk (strict lower part as the tile's upper triangle, L^T, the diagonal
 // in Ld); block b >= 1 solves tile row I = k + b (X L_kk^T = A_Ik), unless that tile row is
 // outside the profile of column k.
-__global__ __launch_bounds__(64) void k_pg_potrf(double* H, int np, int k, const int32_t* ftile, double* Ld) {
+// `delay` (0 on every product path; tslam_test_potrf_delay) holds blocks >= 1 back by delay x
+// 127 x 64 cycles before they read A_kk, so block 0's stores have landed by then: the read order
+// that made the pre-round-5 in-place store of L_kk fail, forced (tests/test_gpu_loop.py).
+__global__ __launch_bounds__(64) void k_pg_potrf(double* H, int np, int k, const int32_t* ftile, double* Ld, int delay) {
     __shared__ double s_L[PG_TILE][PG_TILE + 1];
     const int I = k + blockIdx.x;
     if (blockIdx.x > 0 && ftile[I] > k) return;
+    if (blockIdx.x > 0)
+        for (int i = 0; i < delay; ++i) __builtin_amdgcn_s_sleep(127);
     const int t = threadIdx.x & (PG_TILE - 1);
     const size_t d0 = (size_t)k * PG_TILE;
     double r[PG_TILE];
@@ -429,6 +435,9 @@ __global__ __launch_bounds__(64) void k_pg_update(double* T, const double* delta
     for (int i = 0; i < 16; ++i) Ta[i] = O[i];
 }
 
+static std::atomic<int> g_potrf_delay{0};
+void pose_graph_test_delay(int spins) { g_potrf_delay.store(spins < 0 ? 0 : spins); }
+
 void launch_pose_graph_iteration(double* T, const int32_t* edges, const double* Z, const double* info, int N, int E,
                                  const int32_t* adj_off, const int32_t* adj, const int32_t* ftile, double* terms,
                                  double* H, double* g, double* delta, double* Ld, hipStream_t s) {
@@ -436,7 +445,7 @@ void launch_pose_graph_iteration(double* T, const int32_t* edges, const double* 
     hipLaunchKernelGGL(k_pg_edges, dim3((E + 63) / 64), dim3(64), 0, s, T, edges, Z, info, E, terms);
     hipLaunchKernelGGL(k_pg_assemble, dim3((np + 255) / 256, np), dim3(256), 0, s, terms, edges, adj_off, adj, n, np, H, g);
     for (int k = 0; k < nt; ++k) {
-        hipLaunchKernelGGL(k_pg_potrf, dim3(nt - k), dim3(64), 0, s, H, np, k, ftile, Ld);
+        hipLaunchKernelGGL(k_pg_potrf, dim3(nt - k), dim3(64), 0, s, H, np, k, ftile, Ld, g_potrf_delay.load());
         const int m = nt - k - 1;
         if (m > 0) hipLaunchKernelGGL(k_pg_syrk, dim3(m * (m + 1) / 2), dim3(256), 0, s, H, np, k, ftile);
     }

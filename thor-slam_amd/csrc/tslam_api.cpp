@@ -208,6 +208,28 @@ struct tslam_handle {
     std::vector<std::array<double, 8>> ba_icfg;             // per pair: gravity, bias prior, its weight
     std::vector<std::array<uint8_t, TS_BA_MAXW>> ba_ine_slot;   // per pair and slot: carries a factor
     std::vector<BaArgs> ba_solved;   // per pair: the arguments of its last window solve (replays)
+    // A pair window's keyframe chain (eviction, gate, tiles, iters x (Schur, reduce-and-solve),
+    // back substitution: ~16 launches) replayed from a captured hipGraph per chain shape: the
+    // kernels read a device record (BaRec) written by the graph's first node, so a replay costs one
+    // node update and one graph launch instead of ~16 launches with 2 KB of by-value arguments.
+    // Each shape keeps a ring of instances (own record, event of its last replay), so an instance
+    // is updated only once its previous replay has run.
+    struct BaGraphInst {
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+        hipGraphNode_t setrec = nullptr;
+        hipEvent_t done = nullptr;
+        bool armed = false;
+        BaRec* d_rec = nullptr;
+    };
+    struct BaGraphSet {
+        std::array<int, 6> key{};   // evict, eviction n_order, n_order, inertial, split, iters
+        std::vector<BaGraphInst> inst;
+        int next = 0;
+    };
+    bool ba_graph = true;            // tslam_ba_graph (0: direct launches, the reference for tests)
+    std::vector<BaGraphSet> ba_graphs;
+    hipStream_t ba_cap_stream = nullptr;
     // BA on its own stream (overlapping the next batch): events and the batch parity
     int64_t batch_idx = 0;
     bool batch_started = false;
@@ -478,13 +500,90 @@ static BatchCtx make_ctx(tslam_handle* h);
 // Rig-level A8: a handle with tslam_set_rig over several pairs solves one body window.
 static bool ba_rig(const tslam_handle* h) { return h->rig && h->P > 1 && h->prm.ba_window; }
 
+static constexpr int BA_GRAPH_MAX = 32;   // instances per chain shape (keyframes of that shape in flight)
+
+// One pair window's keyframe chain through the graph cache (see BaGraphInst): a finished instance
+// of the chain's shape is re-pointed at this keyframe's record, a new one is captured only while
+// every instance still has a replay in flight (the steady state needs two or three per shape).
+static hipError_t ba_chain_graph(tslam_handle* h, const BaRec& r, bool evict, bool split, bool ine, hipStream_t s) {
+    const std::array<int, 6> key{evict ? 1 : 0, evict ? r.evict.n_order : 0, r.a.n_order, ine ? 1 : 0, split ? 1 : 0,
+                                 r.a.iters};
+    tslam_handle::BaGraphSet* set = nullptr;
+    for (auto& g : h->ba_graphs)
+        if (g.key == key) set = &g;
+    if (!set) {
+        h->ba_graphs.emplace_back();
+        set = &h->ba_graphs.back();
+        set->key = key;
+    }
+    hipError_t e = hipSuccess;
+    const int n = (int)set->inst.size();
+    int pick = -1;
+    for (int k = 0; k < n && pick < 0; ++k) {   // round robin from the oldest replay
+        const int i = (set->next + k) % n;
+        tslam_handle::BaGraphInst& in = set->inst[(size_t)i];
+        if (!in.armed) {
+            pick = i;
+        } else {
+            e = hipEventQuery(in.done);
+            if (e == hipSuccess) pick = i;
+            else if (e != hipErrorNotReady) return e;
+        }
+    }
+    if (pick < 0 && n == BA_GRAPH_MAX) {   // every instance busy: wait for the oldest replay
+        pick = set->next % n;
+        if ((e = hipEventSynchronize(set->inst[(size_t)pick].done)) != hipSuccess) return e;
+    }
+    if (pick < 0) {   // a new instance: capture the chain on a private stream (nothing runs), instantiate it
+        tslam_handle::BaGraphInst in;
+        if (dev_alloc(h, (void**)&in.d_rec, sizeof(BaRec)) != TSLAM_OK) return hipErrorOutOfMemory;
+        if (!h->ba_cap_stream && (e = hipStreamCreateWithFlags(&h->ba_cap_stream, hipStreamNonBlocking)) != hipSuccess)
+            return e;
+        if ((e = hipStreamBeginCapture(h->ba_cap_stream, hipStreamCaptureModeThreadLocal)) != hipSuccess) return e;
+        launch_ba_setrec(r, in.d_rec, h->ba_cap_stream);
+        launch_ba_chain_rec(r, in.d_rec, evict, split, ine, h->ba_cap_stream);
+        if ((e = hipStreamEndCapture(h->ba_cap_stream, &in.graph)) != hipSuccess) return e;
+        size_t n_root = 1;
+        if ((e = hipGraphGetRootNodes(in.graph, &in.setrec, &n_root)) != hipSuccess) return e;
+        if (n_root != 1) return hipErrorInvalidValue;
+        if ((e = hipGraphInstantiate(&in.exec, in.graph, nullptr, nullptr, 0)) != hipSuccess) return e;
+        if ((e = hipEventCreateWithFlags(&in.done, hipEventDisableTiming)) != hipSuccess) return e;
+        set->inst.push_back(in);
+        pick = n;
+    } else if ((e = ba_graph_set_record(set->inst[(size_t)pick].exec, set->inst[(size_t)pick].setrec, r,
+                                        set->inst[(size_t)pick].d_rec)) != hipSuccess) {
+        return e;
+    }
+    tslam_handle::BaGraphInst& in = set->inst[(size_t)pick];
+    set->next = (pick + 1) % (int)set->inst.size();
+    if ((e = hipGraphLaunch(in.exec, s)) != hipSuccess) return e;
+    if ((e = hipEventRecord(in.done, s)) != hipSuccess) return e;
+    in.armed = true;
+    return hipSuccess;
+}
+
+static void ba_graphs_destroy(tslam_handle* h) {
+    for (auto& g : h->ba_graphs)
+        for (auto& in : g.inst) {
+            if (in.exec) (void)hipGraphExecDestroy(in.exec);
+            if (in.graph) (void)hipGraphDestroy(in.graph);
+            if (in.done) (void)hipEventDestroy(in.done);
+        }
+    h->ba_graphs.clear();
+    if (h->ba_cap_stream) (void)hipStreamDestroy(h->ba_cap_stream);
+    h->ba_cap_stream = nullptr;
+}
+
 // A8: every keyframe of the current batch (g % ba_kf_interval == 0) enters each pair's window,
 // evicting the oldest when the window is full, and the window is solved (per pair, or for a rig
 // one joint body solve: launch_ba_rig_solve).  Host bookkeeping of the slots only; nothing
 // synchronises.  `fe_body`: the rig front end's snapshot of the batch (rig-level A8).
-static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const double* fe, const double* fe_body,
-                   const int32_t* kf_assoc) {
+static hipError_t run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const double* fe, const double* fe_body,
+                         const int32_t* kf_assoc) {
     const int W = h->prm.ba_window, iv = h->prm.ba_kf_interval;
+    // pair windows replay their keyframe chains from graphs (not while Schur launches are timed)
+    const bool graph = h->ba_graph && !ba_rig(h) && !h->ba_timing.ev;
+    std::vector<BaArgs> ev_args;
     for (int64_t g = c.g0; g < c.g0 + c.n; ++g) {
         if (g % iv != 0 || g <= h->ba_last) continue;
         BaArgs a = ba_args(h);
@@ -523,7 +622,10 @@ static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const doub
             for (int e = 0; e < TS_BA_INE + 3; ++e) v[10 + e] = has ? jt->second[e] : 0.0;
             if (jt != h->ba_ine.end()) h->ba_ine.erase(jt);
             h->ba_ine_slot[p][a.slot] = has && v[10 + 28] > 0.0;
-            launch_ba_keyframe(c, a, evict, s);   // eviction only
+            if (graph)
+                ev_args.push_back(a);   // the eviction runs first in the pair's chain below
+            else
+                launch_ba_keyframe(c, a, evict, s);   // eviction only
         }
         for (int e = 0; e < 10; ++e) a.imu[e] = 0.0;
         for (int e = 0; e < TS_BA_INE; ++e) a.ine[e] = 0.0;
@@ -559,10 +661,18 @@ static void run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, const doub
             // keyframe's factor points out of it)
             bool ine = false;
             for (int k = 1; k < a.n_order; ++k) ine = ine || h->ba_ine_slot[p][a.order[k]];
-            launch_ba_solve(c, a, s, h->ba_timing.ev ? &h->ba_timing : nullptr, h->ba_split, ine);
+            if (graph) {
+                const BaRec r{c, ev_args[(size_t)p], a};
+                const hipError_t e = ba_chain_graph(h, r, evict, h->ba_split, ine, s);
+                if (e != hipSuccess) return e;
+            } else {
+                launch_ba_solve(c, a, s, h->ba_timing.ev ? &h->ba_timing : nullptr, h->ba_split, ine);
+            }
             h->ba_solved[p] = a;
         }
+        if (graph) ev_args.clear();
     }
+    return hipSuccess;
 }
 
 static BatchCtx make_ctx(tslam_handle* h) {
@@ -677,16 +787,26 @@ static void shard_range(const tslam_handle* h, int n, int* lo, int* hi) { peer_r
 // keyframe data (rank 0 after the state gather, tslam_shard.cpp).
 // The deferred BA job (tslam_ba_defer): its stream already waits for its batch's back end, so
 // issuing it later only moves the host work.
-static void ba_flush(tslam_handle* h) {
-    if (!h->ba_job.pending) return;
+static int ba_flush(tslam_handle* h) {
+    if (!h->ba_job.pending) return TSLAM_OK;
     h->ba_job.pending = false;
     auto& j = h->ba_job;
-    run_ba(h, j.c, j.s, j.snap, j.snap_body, j.assoc);
-    (void)hipEventRecord(h->ev_ba[j.par], j.s);
+    HIPCHK(hipSetDevice(h->device));   // flushed from any entry point, before it sets the device
+    hipError_t e = run_ba(h, j.c, j.s, j.snap, j.snap_body, j.assoc);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e == hipSuccess) e = hipEventRecord(h->ev_ba[j.par], j.s);
+    if (e != hipSuccess) {   // no event to wait for: the window's state is unknown, say so now
+        h->ba_pending[j.par] = false;
+        return fail(TSLAM_EHIP, std::string("deferred BA: ") + hipGetErrorString(e));
+    }
+    return TSLAM_OK;
 }
-#define BA_FLUSH(h)                                \
-    do {                                           \
-        if ((h) && (h)->ba_job.pending) ba_flush(h); \
+#define BA_FLUSH(h)                                    \
+    do {                                               \
+        if ((h) && (h)->ba_job.pending) {              \
+            const int rc_flush__ = ba_flush(h);        \
+            if (rc_flush__ != TSLAM_OK) return rc_flush__; \
+        }                                              \
     } while (0)
 
 static int ba_stage(tslam_handle* h, const BatchCtx& c, hipStream_t s) {
@@ -721,7 +841,8 @@ static int ba_stage(tslam_handle* h, const BatchCtx& c, hipStream_t s) {
             return TSLAM_OK;
         }
     }
-    run_ba(h, c, s, snap, snap_body, assoc);
+    if (const hipError_t e = run_ba(h, c, s, snap, snap_body, assoc); e != hipSuccess)
+        return fail(TSLAM_EHIP, std::string("BA: ") + hipGetErrorString(e));
     if (other) {
         HIPCHK(hipEventRecord(h->ev_ba[par], s));
         h->ba_pending[par] = true;
@@ -926,6 +1047,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
         {TSLAM_BUF_ROWSTART, R, C * (int64_t)h->g.rs_total * 2},
         {TSLAM_BUF_DET_THR, 1, C * L * 4},
         {TSLAM_BUF_DET_FAIL, B, C * L * 4},
+        {TSLAM_BUF_HYP, B, P * 4 * (int64_t)p.ransac_hypotheses * TS_HYP_DOUBLES * 8},
     };
     int rc = TSLAM_OK;
     for (const Spec& s : specs) {
@@ -940,7 +1062,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_det_thr_acc, sizeof(uint32_t) * (size_t)C * L);
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_state, sizeof(double) * 32 * (size_t)P);   // chain (A, Q) per pair
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_ransac, sizeof(uint32_t) * TS_RANSAC_WORDS * TS_MAX_SPLITS * (size_t)B * P);
-    if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_hyp, sizeof(double) * TS_HYP_DOUBLES * 4 * (size_t)p.ransac_hypotheses * B * P);
+    if (rc == TSLAM_OK) h->d_hyp = (double*)h->buf[TSLAM_BUF_HYP].ptr;
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_brief, sizeof(TSLAM_BRIEF_TABLE));
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_wedges, sizeof(TSLAM_WEDGES));
     if (rc == TSLAM_OK) rc = dev_alloc(h, (void**)&h->d_maps, sizeof(int32_t) * (size_t)C * W * H * 2);
@@ -989,7 +1111,7 @@ int tslam_create(const tslam_stereo_desc* pairs, const tslam_params* params, int
 
 int tslam_destroy(tslam_handle* h) {
     if (!h) return TSLAM_OK;
-    BA_FLUSH(h);
+    (void)ba_flush(h);   // destroyed whatever the deferred BA reports
     loop_worker_stop(h);   // its queued jobs reach the loop stream before the device is drained
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();
@@ -1004,6 +1126,7 @@ int tslam_destroy(tslam_handle* h) {
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t st : {h->as_front, h->as_back, h->as_ba})
         if (st) (void)hipStreamDestroy(st);
+    ba_graphs_destroy(h);
     free_all(h);
     delete h;
     return TSLAM_OK;
@@ -1324,7 +1447,7 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
     const bool front = stage == TSLAM_STAGE_ALL || stage == TSLAM_STAGE_RECTIFY || stage == TSLAM_STAGE_DETECT ||
                        stage == TSLAM_STAGE_DESCRIBE || (stage >= TSLAM_KERNEL_RECTIFY_PYRAMID && stage <= TSLAM_KERNEL_DESCRIBE);
     const bool back = stage == TSLAM_STAGE_ALL || stage == TSLAM_STAGE_MATCH || stage == TSLAM_STAGE_POSE ||
-                      (stage >= TSLAM_KERNEL_MATCH && stage <= TSLAM_KERNEL_RIG);
+                      (stage >= TSLAM_KERNEL_MATCH && stage <= TSLAM_KERNEL_POSE_SOLVE);
     if (!h->ev_front) {
         HIPCHK(hipEventCreateWithFlags(&h->ev_front, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&h->ev_back[0], hipEventDisableTiming));
@@ -1399,7 +1522,8 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
                 launch_ba_snapshot(c, snap, s);
                 launch_ba_kf_assoc(c, assoc, h->prm.ba_kf_interval, s);
                 if (ba_rig(h)) launch_ba_snapshot_rig(c, snap_body, s);
-                run_ba(h, c, s, snap, snap_body, assoc);
+                if (const hipError_t e = run_ba(h, c, s, snap, snap_body, assoc); e != hipSuccess)
+                    return fail(TSLAM_EHIP, std::string("BA: ") + hipGetErrorString(e));
             }
             break;
         case TSLAM_KERNEL_RIG:
@@ -1418,6 +1542,7 @@ int tslam_run_stage(tslam_handle* h, int stage, void* stream) {
         case TSLAM_KERNEL_MATCH: launch_match(c, s); break;
         case TSLAM_KERNEL_MATCH_REFINE: launch_match_refine(c, s); break;
         case TSLAM_KERNEL_POSE: launch_pose(c, s); break;
+        case TSLAM_KERNEL_POSE_SOLVE: launch_pose_solve(c, s); break;
         case TSLAM_KERNEL_CHAIN: launch_chains(c, h->rig, s); break;
         default: return fail(TSLAM_EINVAL, "unknown stage");
     }
@@ -2259,6 +2384,9 @@ int tslam_loop_job_verify(tslam_handle* h, int pair, int64_t frame, int query, i
     if (!h->lp_cap || !h->d_lp_snap_kps) return fail(TSLAM_ESTATE, "no keyframe snapshots (tslam_loop_auto)");
     if (query < 0 || query >= h->lp_cap || cand < 0 || cand >= h->lp_cap || frame < 0)
         return fail(TSLAM_EINVAL, "entry or frame out of range");
+    // entry (position mod cap_k) * P + p holds pair p's view: its snapshot must be solved with
+    // that pair's calibration
+    if (query % h->P != pair) return fail(TSLAM_EINVAL, "query entry is not a view of `pair` (entry % n_pairs)");
     HIPCHK(hipSetDevice(h->device));
     tslam_handle::LoopJob* j = nullptr;
     int rc = job_begin(h, 2, &j);
@@ -2613,6 +2741,13 @@ int tslam_esdf_slice(tslam_handle* h, int y0, int y1, double max_dist, double si
 static int pose_graph_reserve(tslam_handle* h, int n_nodes, int n_edges) {
     const int np = (6 * (n_nodes - 1) + 31) / 32 * 32;
     int rc = TSLAM_OK;
+    if (n_nodes > h->pg_nodes || n_edges > h->pg_edges || np > h->pg_np) {
+        // growth frees the d_pg_* buffers that queued pose-graph jobs read when the worker issues
+        // them (and their kernels on the loop stream): drain the worker and the stream first, so
+        // no job holds an old pointer and no other thread reads the fields being replaced
+        loop_worker_drain(h);
+        if (h->lp_stream) HIPCHK(hipStreamSynchronize(h->lp_stream));
+    }
     if (!h->d_pg_cost && (rc = dev_alloc(h, (void**)&h->d_pg_cost, sizeof(double))) != TSLAM_OK) return rc;
     if (n_nodes > h->pg_nodes) {
         rc = dev_realloc(h, (void**)&h->d_pg_T, sizeof(double) * 16 * n_nodes);
@@ -2779,11 +2914,17 @@ int tslam_loop_job_poll(tslam_handle* h, int64_t id, int block, int32_t* votes, 
     } else {
         const double* T = (const double*)j.out;
         for (int i = 0; i < 16 * j.n_out; ++i)
-            if (!std::isfinite(T[i])) return fail(TSLAM_ESTATE, "pose graph: normal matrix not positive definite");
+            if (!std::isfinite(T[i])) return fail(TSLAM_ESINGULAR, "pose graph: normal matrix not positive definite");
         if (world_T_node) memcpy(world_T_node, T, sizeof(double) * 16 * j.n_out);
         if (cost) *cost = T[16 * (size_t)j.n_out];
     }
     return 1;
+}
+
+int tslam_test_potrf_delay(int spins) {
+    if (spins < 0 || spins > 100000) return fail(TSLAM_EINVAL, "spins must be in [0, 100000]");
+    pose_graph_test_delay(spins);
+    return TSLAM_OK;
 }
 
 int tslam_pose_graph(tslam_handle* h, int n_nodes, double* world_T_node, int n_edges, const int32_t* edges,
@@ -2931,6 +3072,13 @@ int tslam_ba_defer(tslam_handle* h, int defer) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
     BA_FLUSH(h);
     h->ba_defer = defer != 0;
+    return TSLAM_OK;
+}
+
+int tslam_ba_graph(tslam_handle* h, int enable) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    BA_FLUSH(h);
+    h->ba_graph = enable != 0;
     return TSLAM_OK;
 }
 

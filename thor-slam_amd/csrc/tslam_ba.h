@@ -185,3 +185,21 @@ void launch_ba_rig_keyframe(const BatchCtx& c, const BaArgs& a, hipStream_t s);
 void launch_ba_rig_solve(const BatchCtx& c, const BaArgs& a, hipStream_t s, BaTiming* timing, bool inertial = false);
 // one k_ba_schur launch on the window state `a` (measurement replays)
 void launch_ba_schur(const BatchCtx& c, const BaArgs& a, hipStream_t s);
+
+// A pair window's keyframe as a device-resident record: the batch context, the eviction's
+// arguments (remaining slots) and the solve's.  The *_rec kernels read it through two pointers,
+// so one captured hipGraph per chain shape replays every keyframe of that shape: its first node
+// (k_ba_setrec, the record by value) is the only one whose parameters change per replay.
+struct BaRec {
+    BatchCtx c;
+    BaArgs evict;
+    BaArgs a;
+};
+// The keyframe's chain on the record d (grids from the host copy `r`): eviction (when `evict`),
+// gate / tile count / scatter, a.iters x (Schur + reduce-and-solve, or reduce + solve when
+// `split`), back substitution — the launches of launch_ba_keyframe + launch_ba_solve, by pointer.
+void launch_ba_chain_rec(const BaRec& r, const BaRec* d, bool evict, bool split, bool inertial, hipStream_t s);
+// k_ba_setrec: copies the record (by value) to d
+void launch_ba_setrec(const BaRec& r, BaRec* d, hipStream_t s);
+// points graph node `node` (a captured k_ba_setrec) of `exec` at record r / destination d
+hipError_t ba_graph_set_record(hipGraphExec_t exec, hipGraphNode_t node, const BaRec& r, BaRec* d);

@@ -273,6 +273,8 @@ void launch_loop_vote(const uint32_t* db_desc, const int32_t* db_n, int K, int S
 void launch_pose_graph_iteration(double* T, const int32_t* edges, const double* Z, const double* info, int N, int E,
                                  const int32_t* adj_off, const int32_t* adj, const int32_t* ftile, double* terms,
                                  double* H, double* g, double* delta, double* Ld, hipStream_t s);
+// test hook: blocks >= 1 of every k_pg_potrf launch sleep `spins` x 127 x 64 cycles first
+void pose_graph_test_delay(int spins);
 void launch_pose_graph_cost(const double* T, const int32_t* edges, const double* Z, const double* info, int E,
                             double* terms, double* cost, hipStream_t s);
 // TSDF volume + one integration launch (k_tsdf.hip)

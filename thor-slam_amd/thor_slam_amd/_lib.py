@@ -23,6 +23,7 @@ BUF = {
     "pyramid": 0, "smooth": 1, "keypoints": 2, "kcount": 3, "desc": 4, "stereo": 5, "disp": 6,
     "temporal": 7, "temporal_uv": 8, "corr": 9, "pose": 10, "stats": 11, "qbest": 12,
     "qsecond": 13, "tbest": 14, "ysorted": 15, "rowstart": 16, "desc_ys": 17, "det_thr": 18, "det_fail": 19,
+    "hyp": 20,
 }
 STAGE = {"rectify": 0, "detect": 1, "describe": 2, "match": 3, "pose": 4, "all": 5, "ba": 6}
 # single kernels, in pipeline order (bench.py times each with HIP events)
@@ -31,6 +32,7 @@ KERNELS = {
     "match": 14, "match_refine": 15, "pose": 16, "chain": 17,
 }
 RIG_KERNEL = 18   # rig pose (+ chain; sharded: the range's rig pose only)
+POSE_SOLVE_KERNEL = 19   # P3P + RANSAC + refine on injected correspondences (parity tests)
 TRANSPORT = {"rccl": 0, "copy": 1}   # tslam_group_create
 SHARD_GATHER, SHARD_RESULTS, SHARD_PROFILE, SHARD_SERIAL, SHARD_PIPELINE, SHARD_SOLO = 1, 2, 4, 8, 16, 32   # tslam_shard_options
 # tslam_shard_timing segments (enum tslam_segment), in order
@@ -235,6 +237,8 @@ _SIGNATURES = {
                                         ctypes.c_double, ctypes.c_void_p]),
     "tslam_pose_graph": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
+    "tslam_test_potrf_delay": (ctypes.c_int, [ctypes.c_int]),
+    "tslam_ba_graph": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "tslam_loop_auto": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "tslam_loop_job_vote": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
                                            ctypes.POINTER(ctypes.c_int64)]),
@@ -287,10 +291,18 @@ def exported_symbols() -> list[str]:
     return list(_SIGNATURES)
 
 
+TSLAM_ESINGULAR = -5
+
+
+class SingularSystemError(RuntimeError):
+    """A pose-graph solve whose normal matrix was not positive definite (TSLAM_ESINGULAR)."""
+
+
 def _check(rc: int) -> None:
     if rc != 0:
         msg = load_library().tslam_last_error()
-        raise RuntimeError(f"tslam error {rc}: {msg.decode() if msg else ''}")
+        text = f"tslam error {rc}: {msg.decode() if msg else ''}"
+        raise SingularSystemError(text) if rc == TSLAM_ESINGULAR else RuntimeError(text)
 
 
 RANSAC_MODE = {"auto": 0, "exhaustive": 1, "bounded": 2}   # tslam_params.ransac_mode
@@ -434,6 +446,11 @@ class Handle:
 
     def run_kernel(self, name: str, stream: int = 0) -> None:
         _check(self.lib.tslam_run_stage(self.h, KERNELS[name], ctypes.c_void_p(stream)))
+
+    def run_pose_solve(self, stream: int = 0) -> None:
+        """``TSLAM_KERNEL_POSE_SOLVE`` (parity tests): P3P + RANSAC + refinement on the
+        correspondences and counts already in the ``corr`` / ``stats`` buffers."""
+        _check(self.lib.tslam_run_stage(self.h, POSE_SOLVE_KERNEL, ctypes.c_void_p(stream)))
 
     def perturb_temporal(self, percent: int, seed: int = 11, stream: int = 0) -> None:
         """``tslam_perturb_temporal`` (benchmark hook): outliers into the batch's refined temporal
@@ -924,6 +941,10 @@ class Handle:
         """``tslam_ba_defer``: a BA stage on its own stream is enqueued at the next flush point
         (the next batch's first back stage, or any state read) instead of inside the stage call."""
         _check(self.lib.tslam_ba_defer(self.h, int(bool(defer))))
+
+    def ba_graph(self, enable: bool) -> None:
+        """Pair windows' keyframe chains from captured hipGraphs (default) or direct launches (tslam.h)."""
+        _check(self.lib.tslam_ba_graph(self.h, int(bool(enable))))
 
     def ba_split_solve(self, split: bool) -> None:
         """k_ba_reduce + k_ba_solve (kernel boundary) instead of k_ba_reduce_solve (tslam.h)."""

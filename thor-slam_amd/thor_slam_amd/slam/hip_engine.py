@@ -55,7 +55,7 @@ import threading
 import numpy as np
 from scipy.spatial.transform import Rotation
 
-from .._lib import POSE_INIT, POSE_LOST, POSE_OK, Handle, HandleGroup
+from .._lib import POSE_INIT, POSE_LOST, POSE_OK, Handle, HandleGroup, SingularSystemError
 from ..calib import (StereoRectification, confidence_from_covariance, extract_cameras, rgbd_pairs, rgbd_undistort,
                      stereo_pairs, stereo_rectify)
 from ..camera.rig import RigCalibration
@@ -171,6 +171,7 @@ class _AsyncLoop(_LoopGraph):
         self.last_loop: int | None = None   # node of the last closed loop (loop_cooldown)
         self.trace: dict | None = None   # set to {} to record every job's inputs and results (tests)
         self.failures: list = []
+        self.rejected: list = []   # (keyframe of c, g) of loops whose span solve was rejected
 
     # -- oracle LoopPolicy._node: node idx = database position idx (tslam_loop_auto) ----------
     def node(self, g: int, raw: np.ndarray, ts: float) -> None:
@@ -208,7 +209,11 @@ class _AsyncLoop(_LoopGraph):
         # one is too, so this pass polls no further (each poll is an event query)
         if not block and self._busy:
             return None
-        r = job.result(block)
+        try:
+            r = job.result(block)
+        except RuntimeError:   # a failed job is returned too (its slot is free): count it out
+            self.jobs -= 1
+            raise
         if r is not None:
             self.jobs -= 1
         elif not block:
@@ -242,7 +247,11 @@ class _AsyncLoop(_LoopGraph):
             got = it.setdefault("got", [None] * P)
             for q, job in enumerate(it["votes"]):
                 if got[q] is None:
-                    got[q] = self._result(job, block)
+                    try:
+                        got[q] = self._result(job, block)
+                    except RuntimeError:   # a failed job (a device error): the item ends here (its
+                        it["stage"] = "done"  # other vote jobs stay counted: their slots are unreturned
+                        raise
             if any(v is None for v in got):
                 return
             if self.trace is not None:
@@ -265,7 +274,11 @@ class _AsyncLoop(_LoopGraph):
             it["job"] = h.loop_job_verify(it["g"], self._entry(it["idx"], q), self._entry(c, pc), pair=q)
             self.jobs += 1
         if it["stage"] == "verify":
-            ver = self._result(it["job"], block)
+            try:
+                ver = self._result(it["job"], block)
+            except RuntimeError:   # a failed job (a device error): the item ends here
+                it["stage"] = "done"
+                raise
             if ver is None:
                 return
             if self.trace is not None:
@@ -281,6 +294,7 @@ class _AsyncLoop(_LoopGraph):
             if self.last_loop is not None and idx - self.last_loop <= cfg.loop_cooldown:
                 it["stage"] = "done"   # within the cooldown of the last closed loop
                 return
+            it["last_loop"] = self.last_loop   # restored when the span solve is rejected
             self.last_loop = idx
             ver = it["ver"]
             it["edge"] = (a, idx, self.m[pc] @ _invert(ver["T"]) @ _invert(self.m[q]))
@@ -296,11 +310,19 @@ class _AsyncLoop(_LoopGraph):
         if it["stage"] == "solve":
             try:
                 sol = self._result(it["job"], block)
-            except RuntimeError as exc:   # a diverged solve: keep the failing inputs for diagnosis
-                self.jobs -= 1
+            except SingularSystemError as exc:
+                # LoopPolicy's rejection: the span's normal matrix is not positive definite, so the
+                # loop is dropped (no edge, no correction, the cooldown unchanged) and tracking goes
+                # on — process_frames keeps the reference's contract (interface.py:192-200)
                 self.failures.append({"idx": it["idx"], "g": it["g"], "args": it["args"], "ver": it["ver"],
                                       "q": it["q"], "c": it["c"], "pc": it["pc"], "error": str(exc)})
-                raise
+                self.rejected.append((self.frames[it["a"]], it["g"]))
+                self.last_loop = it["last_loop"]
+                if self.trace is not None:
+                    self.trace[("solve", it["idx"])] = (it["args"], None)
+                it["stage"] = "done"
+                logger.warning("loop closure: keyframe %d -> %d rejected (%s)", self.frames[it["a"]], it["g"], exc)
+                return
             if sol is None:
                 return
             it.update(sol=sol, stage="solved")
@@ -1108,12 +1130,18 @@ class HipSlamEngine(SlamEngine):
             return
         j, p = divmod(e, P)
         m = [_invert(self._base_T_rects[0]) @ self._base_T_rects[k] for k in (p, q)]
+        meas = m[0] @ _invert(ver["T"]) @ _invert(m[1])
+        try:
+            sol = h.pose_graph(np.stack(lp.T), np.array(lp.edges + [(j, idx)]), np.stack(lp.meas + [meas]),
+                               np.stack(lp.info + [info]), cfg.pg_iters)
+        except SingularSystemError as exc:   # LoopPolicy's rejection: the loop is dropped, tracking goes on
+            logger.warning("loop closure: keyframe %d -> %d rejected (%s)", lp.frames[j], g, exc)
+            return
         lp.edges.append((j, idx))
-        lp.meas.append(m[0] @ _invert(ver["T"]) @ _invert(m[1]))
+        lp.meas.append(meas)
         lp.info.append(info)
         lp.loops.append((lp.frames[j], g, int(ver["stats"][2])))
         lp.pairs.append((p, q))
-        sol = h.pose_graph(np.stack(lp.T), np.array(lp.edges), np.stack(lp.meas), np.stack(lp.info), cfg.pg_iters)
         lp.T = list(sol["T"])
         lp.cost = sol["cost"]
         lp.corr = lp.T[-1] @ _invert(raw)
