@@ -569,11 +569,12 @@ int tslam_ba_profile(tslam_handle* h, int max_launches, double* schur_ms, int64_
  * solve) instead of k_ba_reduce_solve; both sum in the same order, so the windows agree bit for
  * bit.  0 (default) restores the fused launch. */
 int tslam_ba_split_solve(tslam_handle* h, int split);
-/* Issue of a stereo pair window's keyframe chain (ABI 19).  enable = 1 (default): each keyframe's
- * ~16 BA launches replay a captured hipGraph of that chain shape whose kernels read the keyframe's
+/* Issue of a stereo pair window's keyframe chain (ABI 19).  enable = 1: each keyframe's ~16 BA
+ * launches replay a captured hipGraph of that chain shape whose kernels read the keyframe's
  * arguments from a device record (one node update + one graph launch per keyframe and pair);
- * 0: direct launches with by-value arguments.  Same kernels, same sums: the windows agree bit for
- * bit.  Rig body windows and BA profiling (tslam_ba_profile) always launch directly. */
+ * 0 (default): direct launches with by-value arguments — on this ROCm the replay is the slower
+ * issue (162 against 80 us of host time per keyframe).  Same kernels, same sums:
+ * the windows agree bit for bit.  Rig body windows and BA profiling always launch directly. */
 int tslam_ba_graph(tslam_handle* h, int enable);
 /* Deferred BA issue for stage-API callers that pipeline batches (defer = 1; 0, the default,
  * issues the BA inside tslam_run_stage(TSLAM_STAGE_BA)).  With a BA stage on a stream of its own,

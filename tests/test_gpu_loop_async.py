@@ -246,7 +246,7 @@ def _policy_from_trace(eng, recs, solve_check_every=0, finish=False):
             body = bt @ T_abs[k] @ _invert(bt)
             raw = _invert(bt) @ body @ bt   # the engine's rect-left pose before loop correction
             corr = pol.step(g0 + k, int(st[k]), raw)
-            out[g0 + k] = None if int(st[k]) == 1 else bt @ corr @ _invert(bt)
+            out[g0 + k] = None if pol.state != "tracking" else bt @ corr @ _invert(bt)
     if finish:   # HipSlamEngine.settle
         pol.finish()
     return pol, out, checked
@@ -343,3 +343,50 @@ def test_rejected_loop_solve_keeps_the_session_running():
     _compare(published, want, LOOP_FRAMES)
     assert sum(p is not None for p in published.values()) >= LOOP_FRAMES - 2
     eng.shutdown()
+
+
+def test_relocalisation_after_a_blank_gap():
+    """20 blank frames (a covered lens) in the reference's default drop-in
+    path.  The device reports LOST through the gap (and for the first frame after it); the third
+    LOST frame moves the engine to RELOCALIZING (published pose None, get_tracking_state
+    RELOCALIZING); the tracked keyframes after the gap search the keyframes from before it until
+    one is verified; then tracking resumes in the map's frame.  Every published pose and state
+    equals oracle LoopPolicy's on the same tracked poses and search results, and after the
+    relocalisation the poses are back on the gap-free run's (the gap's 30 degrees of motion,
+    which the device's chain misses, are recovered)."""
+    from thor_slam_amd.slam.interface import TrackingState
+
+    frames = _render_many(list(range(LOOP_FRAMES)))
+    gap = frames.copy()
+    gap[100:120] = 0
+    states = {}
+
+    def hook(eng):
+        orig = eng._publish
+
+        def record(res, stamps, g0):
+            orig(res, stamps, g0)
+            states[g0 + len(stamps) - 1] = eng.get_tracking_state()
+
+        eng._publish = record
+
+    published, recs, eng = _run_default(gap, LOOP_FRAMES, hook=hook)
+    lp = eng._loop
+    pol, want, _ = _policy_from_trace(eng, recs)
+    stats = np.concatenate([r[2] for r in recs])
+    assert (stats[100:121] == 1).all() and stats[121] == 0
+    assert lp.relocs and lp.relocs == pol.relocs, (lp.relocs, pol.relocs)
+    _compare(published, want, LOOP_FRAMES)
+    g_rel = lp.relocs[0][1]
+    back = g_rel + eng._config.reloc_latency
+    assert states[100] == TrackingState.LOST and states[102] == TrackingState.RELOCALIZING
+    assert all(published[g] is None and states[g] == TrackingState.RELOCALIZING for g in range(102, back))
+    assert all(published[g] is not None and states[g] == TrackingState.TRACKING for g in range(back, LOOP_FRAMES))
+    eng.shutdown()
+    ref, _, eng0 = _run_default(frames, LOOP_FRAMES)   # the same lap without the gap
+    eng0.shutdown()
+    end = 230 if back < 225 else LOOP_FRAMES   # before the loop closures of frame 235 (they differ by run)
+    err = max(np.linalg.norm(published[g][:3, 3] - ref[g][:3, 3]) for g in range(back, end))
+    assert err < 0.05, err
+    print(f"relocalised at frame {g_rel} against keyframe {lp.relocs[0][0]}; position error vs the gap-free "
+          f"run after it: max {err:.4f} m")

@@ -194,3 +194,59 @@ def test_non_finite_solution_is_rejected():
             sc.frames.append(g)
         np.testing.assert_array_equal(pol.step(g, 2 if g == 0 else 0, raw), raw)
     assert pol.rejected and not pol.loops
+
+
+def _run_gap(gap=(150, 170), after=3, n_frames=260, lap=100, **cfg_items):
+    """A drift-free lap sequence whose frames in [gap) are LOST; the device's chain then misses the
+    gap's motion, so every raw pose after it is off by the rigid error E = raw_{g0-1} raw_{g1-1}^-1
+    (the LOST frames keep the last tracked pose, the first frame after the gap chains from it)."""
+    cfg = HipSlamConfig(reloc_after_lost=after, **cfg_items)
+    sc = _Scripted(lap, cfg.loop_kf_interval)
+    pol = L.LoopPolicy(cfg, 1, [np.eye(4)], sc.vote, sc.verify, sc.solve)
+    g0, g1 = gap
+    E = _lap_pose(g0 - 1, lap) @ L.inv_se3(_lap_pose(g1, lap))   # first frame after the gap is LOST too
+    out, states = [], []
+    for g in range(n_frames):
+        if g0 <= g <= g1:
+            status, raw = 1, _lap_pose(g0 - 1, lap)
+        else:
+            status = 2 if g == 0 else 0
+            raw = _lap_pose(g, lap) if g < g0 else E @ _lap_pose(g, lap)
+        if status == 0 and g % cfg.loop_kf_interval == 0:
+            sc.frames.append(g)
+        out.append(pol.step(g, status, raw))
+        states.append(pol.state)
+    return pol, sc, out, states
+
+
+def test_relocalisation_after_a_lost_run_reanchors_the_new_segment():
+    """reloc_after_lost = 3: the third LOST frame breaks the graph (RELOCALIZING), the first
+    tracked keyframe after the gap starts an unanchored segment without an odometry edge, its
+    relocalisation item (due reloc_latency frames later) finds the place seen a lap earlier, and
+    from then on the published poses are the true ones again; loop closure goes on afterwards."""
+    lap, (g0, g1) = 100, (150, 170)
+    pol, sc, out, states = _run_gap(loop_latency=30, loop_cooldown=0, reloc_latency=5)
+    assert states[g0] == states[g0 + 1] == "lost" and states[g0 + 2] == "relocalizing"
+    assert pol.relocs, "not relocalised"
+    c_frame, g_rel, inl = pol.relocs[0]
+    assert g_rel == 175 and (g_rel - c_frame) % lap == 0 and inl == 150   # the first keyframe after the gap
+    first_back = g_rel + 5   # its item is due reloc_latency frames later
+    assert all(s_ == "relocalizing" for s_ in states[g0 + 2:first_back])
+    assert all(s_ == "tracking" for s_ in states[first_back:])
+    for g in range(first_back, 260):   # the drift-free sequence: exact poses again
+        np.testing.assert_allclose(out[g], _lap_pose(g, lap), atol=1e-9)
+    # the segment's first node has no odometry edge to the node before the gap; the
+    # relocalisation edge joins it to its candidate
+    idx = pol.frames.index(g_rel)
+    assert (idx - 1, idx) not in pol.edges and (pol.frames.index(c_frame), idx) in pol.edges
+    assert pol.loops and pol.loops[-1][1] > first_back   # loop closure afterwards
+
+
+def test_short_lost_run_and_reloc_off_do_not_break_the_graph():
+    # a LOST run shorter than reloc_after_lost: no episode, the offset stays (the device's chain)
+    pol, _, out, states = _run_gap(gap=(150, 151), after=3, loop_latency=30, loop_cooldown=0)
+    assert "relocalizing" not in states and not pol.relocs
+    # relocalisation off: the 21-frame gap leaves the later poses off by its motion
+    pol0, _, out0, states0 = _run_gap(after=0, loop_latency=30, loop_cooldown=0)
+    assert "relocalizing" not in states0 and not pol0.relocs
+    assert np.abs(out0[200][:3, 3] - _lap_pose(200)[:3, 3]).max() > 0.1

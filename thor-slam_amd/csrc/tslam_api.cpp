@@ -227,7 +227,10 @@ struct tslam_handle {
         std::vector<BaGraphInst> inst;
         int next = 0;
     };
-    bool ba_graph = true;            // tslam_ba_graph (0: direct launches, the reference for tests)
+    // tslam_ba_graph: off by default — measured on MI355X (tools/ba_probe.py), a
+    // replay (one node update + the graph launch) costs the host 162 us per keyframe against 80 us
+    // for the 16 direct launches, and the chain's GPU time 0.240 against 0.222 ms
+    bool ba_graph = false;
     std::vector<BaGraphSet> ba_graphs;
     hipStream_t ba_cap_stream = nullptr;
     // BA on its own stream (overlapping the next batch): events and the batch parity

@@ -94,6 +94,15 @@ class HipSlamConfig(SlamConfig):
     # a verified loop is not closed (no edge, no solve) within this many keyframes after the last
     # closed loop: revisiting a known place would otherwise re-solve the span at every keyframe
     loop_cooldown: int = 5
+    # relocalisation after a LOST run (the reference's TrackingState.RELOCALIZING, interface.py:16-23;
+    # cuVSLAM's enable_localization_n_mapping, launch/thor_visual_slam.launch.py:42,74): the
+    # reloc_after_lost-th consecutive LOST frame breaks the keyframe graph; each tracked keyframe
+    # after it searches the keyframes from before the gap (loop-closure votes + verification,
+    # due reloc_latency frames later) until one re-anchors the new segment; meanwhile the published
+    # pose is None and the state RELOCALIZING (oracle/numpy_loop.py LoopPolicy).  0 = off.  Needs
+    # the keyframe database of loop closure.
+    reloc_after_lost: int = 3
+    reloc_latency: int = 5
     # input kind: RGB-D (BASELINE configs[4]) = per source a colour camera (cam_idx 0, BGR) and a
     # depth image aligned to it (cam_idx 1, u16 mm); depth replaces stereo matching
     rgbd: bool = False
@@ -161,6 +170,8 @@ class HipSlamConfig(SlamConfig):
             raise ValueError("loop_max_keyframes must be in [1, 1024], loop_signature in [1, 256], loop_kf_interval >= 1")
         if self.loop_latency < 0 or self.imu_prior_lag < 0 or self.loop_cooldown < 0:
             raise ValueError("loop_latency, loop_cooldown and imu_prior_lag must be >= 0")
+        if self.reloc_after_lost < 0 or self.reloc_latency < 0:
+            raise ValueError("reloc_after_lost and reloc_latency must be >= 0")
         if self.devices:
             # local BA runs on rank 0 (state gather of a stereo rig); a camera-sharded RGB-D rig keeps
             # the TSDF on rank 0 (pair 0 is rank 0's camera) and has no local BA or loop closure

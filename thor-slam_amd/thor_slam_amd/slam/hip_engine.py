@@ -172,11 +172,31 @@ class _AsyncLoop(_LoopGraph):
         self.trace: dict | None = None   # set to {} to record every job's inputs and results (tests)
         self.failures: list = []
         self.rejected: list = []   # (keyframe of c, g) of loops whose span solve was rejected
+        # relocalisation after a LOST run (LoopPolicy.observe / _relocate)
+        self.lost_run = 0
+        self.reloc = False          # RELOCALIZING
+        self.anchor_end = 0         # candidates of the episode: nodes < anchor_end
+        self.seg_start = 0          # first node of the unanchored segment
+        self.relocs: list = []      # (keyframe of c, g, inliers)
+        self.last_due = -1
+
+    def observe(self, g: int, status: int) -> None:
+        """oracle LoopPolicy.observe: the LOST-run bookkeeping of frame g."""
+        if status == POSE_LOST:
+            self.lost_run += 1
+            after = self.cfg.reloc_after_lost
+            if after > 0 and self.lost_run == after and self.frames:
+                if not self.reloc:
+                    self.reloc = True
+                    self.anchor_end = len(self.frames)
+                self.seg_start = len(self.frames)
+        else:
+            self.lost_run = 0
 
     # -- oracle LoopPolicy._node: node idx = database position idx (tslam_loop_auto) ----------
     def node(self, g: int, raw: np.ndarray, ts: float) -> None:
         idx = len(self.frames)
-        if idx == 0:
+        if idx == 0 or (self.reloc and idx == self.seg_start):   # the first node of a segment
             T, Z = self.corr @ raw, None
         else:
             Z = _invert(self.raw[-1]) @ raw
@@ -190,8 +210,11 @@ class _AsyncLoop(_LoopGraph):
         self.T.append(T)
         self.odo.append(Z)
         cfg = self.cfg
-        lo, hi = self._window(idx)
-        it = {"idx": idx, "g": g, "due": g + cfg.loop_latency, "lo": lo, "n_kf": hi - lo + 1,
+        kind = "reloc" if self.reloc else "loop"
+        lo, hi = self._reloc_window(idx) if self.reloc else self._window(idx)
+        due = max(g + (cfg.reloc_latency if self.reloc else cfg.loop_latency), self.last_due)
+        self.last_due = due
+        it = {"idx": idx, "g": g, "due": due, "lo": lo, "n_kf": hi - lo + 1, "kind": kind,
               "stage": "new" if hi >= lo else "done"}
         self.items.append(it)
         self._progress(it, False, len(self.items) == 1)
@@ -200,6 +223,11 @@ class _AsyncLoop(_LoopGraph):
         cfg = self.cfg
         margin = (cfg.loop_latency + 2 * cfg.batch_size - 1) // cfg.loop_kf_interval + 1
         return max(0, idx - cfg.loop_max_keyframes + margin), idx - cfg.loop_min_gap
+
+    def _reloc_window(self, idx: int) -> tuple[int, int]:   # oracle LoopPolicy.reloc_window
+        cfg = self.cfg
+        margin = (cfg.loop_latency + 2 * cfg.batch_size - 1) // cfg.loop_kf_interval + 1
+        return max(0, idx - cfg.loop_max_keyframes + margin), self.anchor_end - 1
 
     def _entry(self, pos: int, p: int) -> int:
         return (pos % self.cfg.loop_max_keyframes) * self.P + p
@@ -287,6 +315,11 @@ class _AsyncLoop(_LoopGraph):
                 it["stage"] = "done"
                 return
             it.update(ver=ver, stage="verified")
+        if it["kind"] == "reloc":
+            if it["stage"] == "verified" and block:   # applied at the due frame (LoopPolicy._relocate)
+                self._relocate(it)
+                it["stage"] = "done"
+            return
         if it["stage"] == "verified" and head:
             # the span solve starts once every older item is applied, so its inputs (the span's
             # poses and edges, with this loop's edge) are what they are at the due frame
@@ -337,12 +370,35 @@ class _AsyncLoop(_LoopGraph):
             self.pairs.append((it["pc"], it["q"]))
             self.T[a:idx + 1] = list(sol["T"])
             for i in range(idx + 1, len(self.T)):
+                if self.odo[i] is None:   # a segment break: the nodes after it are anchored otherwise
+                    break
                 self.T[i] = self.T[i - 1] @ self.odo[i]
             self.corr = self.T[-1] @ _invert(self.raw[-1])
             self.cost = sol["cost"]
             it["stage"] = "done"
             logger.info("loop closure: keyframe %d -> %d (%d inliers), span of %d nodes, cost %.3g",
                         self.frames[a], it["g"], int(it["ver"]["stats"][2]), idx - a + 1, sol["cost"])
+
+
+    def _relocate(self, it: dict) -> None:
+        """oracle LoopPolicy._relocate, from the item's verified candidate: the unanchored
+        segment moves rigidly onto the candidate keyframe's pose and tracking resumes."""
+        idx, c, q, pc, ver = it["idx"], it["c"], it["q"], it["pc"], it["ver"]
+        if not self.reloc or idx < self.seg_start:
+            return
+        Z = self.m[pc] @ _invert(ver["T"]) @ _invert(self.m[q])
+        D = self.T[c] @ Z @ _invert(self.T[idx])
+        for i in range(self.seg_start, len(self.T)):
+            self.T[i] = D @ self.T[i]
+        self.edges.append((c, idx))
+        self.meas.append(Z)
+        self.info.append(self.info_m)
+        self.corr = D @ self.corr
+        self.relocs.append((self.frames[c], it["g"], int(ver["stats"][2])))
+        self.reloc = False
+        self.last_loop = idx
+        logger.info("relocalised: keyframe %d against keyframe %d (%d inliers)", it["g"], self.frames[c],
+                    int(ver["stats"][2]))
 
 
 class HipSlamEngine(SlamEngine):
@@ -1049,10 +1105,15 @@ class HipSlamEngine(SlamEngine):
             if isinstance(self._loop, _AsyncLoop):   # oracle/numpy_loop.py LoopPolicy.step
                 g = g0 + k
                 raw = bt_inv @ body @ bt                           # rect-left world_T_cam before loop correction
+                self._loop.observe(g, status)
                 if status == POSE_OK and g % self._config.loop_kf_interval == 0:
                     self._loop.node(g, raw, ts)
                 self._loop.advance(until=g)
                 body = bt @ self._loop.corr @ raw @ bt_inv
+                if self._loop.reloc:   # no pose until the new segment is anchored in the map
+                    state = TrackingState.RELOCALIZING
+                    latest = None
+                    continue
             elif self._loop is not None and status != POSE_LOST:
                 g = g0 + k
                 raw = bt_inv @ body @ bt                           # rect-left world_T_cam before loop correction
