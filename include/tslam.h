@@ -351,18 +351,22 @@ int tslam_imu_vision_only(const double* T, const double* cov, double sigma2, con
                           double* cov_out);
 /* The filter's world gravity (zero before tslam_imu_begin / for the gyro-only filter). */
 int tslam_imu_gravity(const tslam_imu* f, double* gravity);
-/* The inertial factor record of tslam_ba_inertial_factor (record[32], layout there) from the n
- * frame intervals between two keyframes: dt[n], gyro[n][3], accel[n][3] (IMU axes), the filter's
- * biases bg[3], ba[3] (ba becomes ba_lin), w_prev[3] = the factor frame's rate over the interval
- * before the first (NULL: none), the factor's frame: frame_R_imu[9] (row-major; NULL = the
- * filter's rect_R_imu, i.e. pair 0's rectified-left camera; a rig's body window passes
- * base_R_imu) and lever[3] (the IMU's position in that frame; NULL = the filter's), and the
- * weights' floors (m/s, m):
- * wv = 1 / (n_a^2 T + v_floor^2), wp = 1 / (n_a^2 T^3 / 3 + p_floor^2).  Spec:
+/* The inertial factor record of tslam_ba_inertial_factor (record[TSLAM_BA_INE_RECORD], layout
+ * there) from the n frame intervals between two keyframes: dt[n], gyro[n][3], accel[n][3] (IMU
+ * axes), the filter's biases bg[3], ba[3] (they become bg_lin, ba_lin), w_prev[3] = the factor
+ * frame's rate over the interval before the first (NULL: none), the factor's frame: frame_R_imu[9]
+ * (row-major; NULL = the filter's rect_R_imu, i.e. pair 0's rectified-left camera; a rig's body
+ * window passes base_R_imu) and lever[3] (the IMU's position in that frame; NULL = the filter's),
+ * and the weights' floors: wv = 1 / (n_a^2 T + v_floor^2), wp = 1 / (n_a^2 T^3 / 3 + p_floor^2),
+ * wR = 1 / (n_g^2 T + r_floor^2), the bias random walks w_ra = 1 / (s_a^2 T + ba_floor^2),
+ * w_rg = 1 / (s_g^2 T + bg_floor^2) (n_a, n_g, s_a, s_g: the filter's noise densities and random
+ * walks, launch/thor_visual_slam.launch.py:82-93; a zero density or walk gives weight 0).  Spec:
  * oracle/numpy_ba.py preintegrate. */
+#define TSLAM_BA_INE_RECORD 80
 int tslam_imu_preintegrate(const tslam_imu* f, int n, const double* dt, const double* gyro, const double* accel,
                            const double* bg, const double* ba, const double* w_prev, const double* frame_R_imu,
-                           const double* lever, double v_floor, double p_floor, double* record);
+                           const double* lever, double v_floor, double p_floor, double r_floor, double ba_floor,
+                           double bg_floor, double* record);
 
 /* Rig pose (replaces the multi-camera fusion cuVSLAM does for the rig of
  * isaac_ros.py:364-411): base_T_rect[P][16] = the rectified-left frame of each pair in the rig's
@@ -538,24 +542,33 @@ int tslam_group_destroy(tslam_group* g);
  * residual vee((M^T R_c R_{c-1}^T - ...) / 2) between window-consecutive keyframes (spec:
  * oracle/numpy_ba.py imu_terms).  Pair windows only (a rig's body window ignores it). */
 int tslam_ba_imu_factor(tslam_handle* h, int pair, int64_t frame, const double* M, double weight);
-/* Tightly coupled inertial factors (spec: oracle/numpy_ba.py inertial_terms; pair windows only).
+/* Tightly coupled inertial factors (spec: oracle/numpy_ba.py inertial_system; ABI 19: gyroscope
+ * bias and bias random walks, the noise model of launch/thor_visual_slam.launch.py:50-53,88-93).
  * tslam_ba_inertial: world gravity [3] (the tracking world: pair 0's rectified-left camera at frame
- *   0), the accelerometer-bias prior [3] (IMU axes) and its weight (1 / (m/s^2)^2) for the next
- *   solves of `pair`'s window.
- * tslam_ba_inertial_factor: keyframe `frame`'s accelerometer preintegration from the previous
- *   keyframe (before the batch holding it is submitted): record[30] = dv[3], dp[3] (previous
- *   keyframe's camera axes), Jv[9], Jp[9] (row-major, d/d ba), ba_lin[3], dt, wv (1 / (m/s)^2),
- *   wp (1 / m^2), and v0[3], the keyframe camera's initial world velocity.  The window then
- *   carries a velocity per keyframe and one accelerometer bias; every Gauss-Newton step eliminates
- *   them into the reduced camera system (k_ba_reduce_solve_ine) and updates them after the camera
- *   solve.  A window with no factor between two of its keyframes solves as before.
- * tslam_ba_read_inertial (synchronises): velocity[W][3] by slot, ba[3].
+ *   0) and priors on the oldest window keyframe's biases: accelerometer [3] with its weight
+ *   (1 / (m/s^2)^2), gyroscope [3] with its weight (1 / (rad/s)^2), for the next solves of `pair`'s
+ *   window.
+ * tslam_ba_inertial_factor: keyframe `frame`'s IMU preintegration from the previous keyframe
+ *   (before the batch holding it is submitted): record[TSLAM_BA_INE_RECORD] = dv[3], dp[3]
+ *   (previous keyframe's camera axes), Jv[9], Jp[9] (row-major, d/d ba), ba_lin[3], dt, wv
+ *   (1 / (m/s)^2, 0 = no factor), wp (1 / m^2), wR (1 / rad^2: the gyro rotation rows), w_ra
+ *   (accelerometer-bias random walk), M[9] (the gyro rotation, previous camera points -> this
+ *   camera), JRe[9] (d r_R / d bg), Jvg[9], Jpg[9] (d/d bg), bg_lin[3], w_rg (gyroscope-bias random
+ *   walk), 8 unused — tslam_imu_preintegrate writes it — and v0[3], the keyframe camera's initial
+ *   world velocity.  Every window keyframe then carries a velocity and accelerometer / gyroscope
+ *   biases (a new keyframe's start at its record's linearisation point, or the previous keyframe's);
+ *   every Gauss-Newton step eliminates these 9 unknowns per keyframe into the reduced camera system
+ *   (k_ba_reduce_solve_ine) and updates them after the camera solve.  A window with no factor
+ *   between two of its keyframes solves as before.  A factor's rotation rows replace the separate
+ *   tslam_ba_imu_factor of that keyframe: give one or the other.
+ * tslam_ba_read_inertial (synchronises): velocity[W][3] and bias[W][6] (accelerometer, gyroscope) by slot.
  * On a rig (tslam_set_rig over several pairs, rig-level A8) the factors act on the body window:
  * pair = n_pairs, record in the earlier keyframe's body (base_link) axes, velocities of the body
  * origin, gravity in the body window's world (base_link at frame 0); pair windows are refused. */
-int tslam_ba_inertial(tslam_handle* h, int pair, const double* gravity, const double* ba_prior, double ba_weight);
+int tslam_ba_inertial(tslam_handle* h, int pair, const double* gravity, const double* ba_prior, double ba_weight,
+                      const double* bg_prior, double bg_weight);
 int tslam_ba_inertial_factor(tslam_handle* h, int pair, int64_t frame, const double* record, const double* v0);
-int tslam_ba_read_inertial(tslam_handle* h, int pair, double* velocity, double* ba);
+int tslam_ba_read_inertial(tslam_handle* h, int pair, double* velocity, double* bias);
 int tslam_ba_read(tslam_handle* h, int pair, int64_t* frames, double* cam_T_world, int32_t* landmark,
                   double* points, double* obs_uvd, int32_t* counts);
 

@@ -38,25 +38,27 @@ Spec (shared with ``thor-slam_amd/csrc/k_ba.hip``):
   residual e has Jacobians ``Q^T`` on camera c's rotation and ``-I`` on camera c - 1's (left
   updates), so ``S_cc += w I``, ``S_{c-1,c-1} += w I``, ``S_{c,c-1} += -w Q`` (rotation blocks),
   ``b_c -= w Q e``, ``b_{c-1} += w e``; camera 0's rows drop with the gauge.
-* Inertial factors (tightly coupled, optional; the accelerometer leg of SURVEY.md §8f item 2):
-  keyframe g may carry the accelerometer preintegration from the previous keyframe
-  (``preintegrate``: dv, dp in the previous keyframe's camera axes, their Jacobians Jv, Jp with
-  respect to the accelerometer bias, the bias ba_lin they were integrated with, dt, and the
-  weights wv, wp in 1 / (m/s)^2 and 1 / m^2) and an initial world velocity of its camera.  The
-  window then carries one velocity v_c per keyframe and one accelerometer bias ba for the window
-  (``set_inertial``: world gravity gw, the bias prior ba0 with weight wb).  Between window-
-  consecutive keyframes (i, j) = (c - 1, c) whose later one carries a factor, with R_i the
-  world_T_cam rotation (R_cw,i^T), p the camera centres and dba = ba - ba_lin:
-      r_v = R_cw,i (v_j - v_i - gw dt) - (dv + Jv dba)
-      r_p = R_cw,i (p_j - p_i - v_i dt - gw dt^2 / 2) - (dp + Jp dba)
-  weighted wv, wp; under the left camera update (rho, omega): d(R_cw,i u)/d omega_i =
-  -[R_cw,i u]x, dp/d rho = -R_wc, so dr_p/d rho_i = I, dr_p/d rho_j = -R_cw,i R_wc,j,
-  dr_v/d v_i = -R_cw,i, dr_v/d v_j = R_cw,i, dr_p/d v_i = -R_cw,i dt, dr/d ba = -(Jv; Jp).
-  With y = (v_0 .. v_{n-1}, ba) the normal equations [[S + lam I, Hxy], [Hyx, Hyy]] (Hyy with
-  lam I and the prior wb I on ba) are reduced to the cameras, S' = S - Hxy Hyy^-1 Hyx,
-  b' = b - Hxy Hyy^-1 b_y (camera 0's rows dropped first), and after the camera solve
-  dy = Hyy^-1 (b_y - Hyx dc): v_c += dv_c, ba += dba.  A window with no inertial factor skips
-  all of it (the solve is the visual one, bit for bit).
+* Inertial factors (tightly coupled, optional; SURVEY.md §8f item 2 with the biases and random
+  walks of ``launch/thor_visual_slam.launch.py:50-53,88-93``): keyframe g may carry the IMU
+  preintegration from the previous keyframe (``preintegrate``, record layout at ``INE_N``) and an
+  initial world velocity of its camera.  Every window keyframe c carries the states y_c = (v_c,
+  ba_c, bg_c): its camera's world velocity and the accelerometer / gyroscope biases (IMU axes)
+  over the interval that starts at it.  ``set_inertial``: world gravity gw and priors (ba0, wb),
+  (bg0, wg) on the oldest keyframe's biases.  Between window-consecutive keyframes (i, j) =
+  (c - 1, c) whose later one carries a factor, with R_i the cam_T_world rotation, p the camera
+  centres, dba = ba_i - ba_lin, dbg = bg_i - bg_lin, Q = R_j R_i^T and A = M^T Q:
+      r_v  = R_i (v_j - v_i - gw dt) - (dv + Jv dba + Jvg dbg)            weight wv
+      r_p  = R_i (p_j - p_i - v_i dt - gw dt^2 / 2) - (dp + Jp dba + Jpg dbg)   wp
+      r_R  = vee((A - A^T) / 2) + JRe dbg                                 wR (0: no rotation rows)
+      r_ba = ba_j - ba_i,   r_bg = bg_j - bg_i                            w_ra, w_rg (random walks)
+  with the Jacobians of ``inertial_jacobian`` (left camera updates (rho, omega): d(R_i u)/d omega_i
+  = -[R_i u]x, dp/d rho = -R_wc; the rotation rows take the IMU rotation factor's Q^T / -I).  With
+  y = (y_0 .. y_{n-1}) (9 per keyframe) the normal equations [[S + lam I, Hxy], [Hyx, Hyy]] (Hyy
+  with lam I and the priors on y_0's biases) are reduced to the cameras, S' = S - Hxy Hyy^-1 Hyx,
+  b' = b - Hxy Hyy^-1 b_y (camera 0's rows dropped first); after the camera solve
+  dy = Hyy^-1 (b_y - Hyx dc) updates every keyframe's velocity and biases.  A new keyframe's biases
+  start at its record's (ba_lin, bg_lin), or the previous keyframe's without a record.  A window
+  with no inertial factor skips all of it (the solve is the visual one, bit for bit).
 """
 
 from __future__ import annotations
@@ -68,8 +70,12 @@ import numpy as np
 from .numpy_slam import cayley, level0_coords
 
 # inertial factor record per slot (k_ba.hip TS_BA_INE): dv 0-2, dp 3-5, Jv 6-14 and Jp 15-23
-# (row-major 3x3), ba_lin 24-26, dt 27, wv 28, wp 29 (0 = no factor), 30-31 unused
-INE_N = 32
+# (d/d ba, row-major 3x3), ba_lin 24-26, dt 27, wv 28 (0 = no factor), wp 29, wR 30 (rotation
+# rows), w_ra 31 (accelerometer-bias random walk), M 32-40 (the gyro rotation, camera i points ->
+# camera j), JRe 41-49 (d r_R / d bg), Jvg 50-58 and Jpg 59-67 (d/d bg), bg_lin 68-70, w_rg 71
+# (gyroscope-bias random walk), 72-79 unused
+INE_N = 80
+INE_Y = 9   # states per keyframe: v, ba, bg
 
 
 def _exp_so3(w: np.ndarray) -> np.ndarray:
@@ -80,9 +86,21 @@ def _exp_so3(w: np.ndarray) -> np.ndarray:
     return np.eye(3) + np.sin(th) / th * K + (1.0 - np.cos(th)) / (th * th) * (K @ K)
 
 
+def _jr_so3(w: np.ndarray) -> np.ndarray:
+    """Right Jacobian of SO(3): I - (1 - cos t) / t^2 [w]x + (t - sin t) / t^3 [w]x^2 (series
+    below t = 1e-4)."""
+    th = float(np.linalg.norm(w))
+    K = np.array([[0.0, -w[2], w[1]], [w[2], 0.0, -w[0]], [-w[1], w[0], 0.0]])
+    if th < 1e-4:
+        return np.eye(3) - 0.5 * K + (K @ K) / 6.0
+    return np.eye(3) - (1.0 - np.cos(th)) / (th * th) * K + (th - np.sin(th)) / (th * th * th) * (K @ K)
+
+
 def preintegrate(samples: list, rect_R_imu: np.ndarray, bg: np.ndarray, ba: np.ndarray,
                  lever: np.ndarray | None = None, w_prev: np.ndarray | None = None,
-                 acc_density: float = 2.553e-3, v_floor: float = 1e-2, p_floor: float = 1e-3) -> np.ndarray:
+                 acc_density: float = 2.553e-3, v_floor: float = 1e-2, p_floor: float = 1e-3,
+                 gyro_density: float = 0.0, r_floor: float = 0.0, acc_rw: float = 0.0, gyro_rw: float = 0.0,
+                 ba_floor: float = 1e-3, bg_floor: float = 1e-3) -> np.ndarray:
     """The inertial factor record (INE_N doubles) of the frame intervals ``samples`` = [(dt, gyro,
     accel)] (IMU axes) from one keyframe to the next, in the first keyframe's camera axes: per
     interval w = Ri (gyro - bg) (camera axes), alpha = (w - w_prev) / dt (0 for the first interval
@@ -90,23 +108,35 @@ def preintegrate(samples: list, rect_R_imu: np.ndarray, bg: np.ndarray, ba: np.n
     (r = the IMU's position in the camera, as ``numpy_imu.ImuFilter``), then
         dp += dv dt + dR a dt^2 / 2,   Jp += Jv dt - dR Ri dt^2 / 2,
         dv += dR a dt,                 Jv += -dR Ri dt,
-        dR <- dR exp([w dt]x);
-    weights wv = 1 / (n_a^2 T + v_floor^2), wp = 1 / (n_a^2 T^3 / 3 + p_floor^2) over the total T."""
+        Jpg += Jvg dt - dR [a]x JR dt^2 / 2,   Jvg += -dR [a]x JR dt,
+        JR <- exp(w dt)^T JR - Jr(w dt) Ri dt,   dR <- dR exp([w dt]x)
+    (the gyroscope bias enters through the rotation; the lever-arm terms' own dependence on it is
+    left out), M = dR^T, JRe = dR JR; weights over the total T: wv = 1 / (n_a^2 T + v_floor^2),
+    wp = 1 / (n_a^2 T^3 / 3 + p_floor^2), wR = 1 / (n_g^2 T + r_floor^2) (0 when n_g = 0), the
+    bias random walks w_ra = 1 / (s_a^2 T + ba_floor^2), w_rg = 1 / (s_g^2 T + bg_floor^2) (0 when
+    s = 0)."""
     Ri = np.asarray(rect_R_imu, dtype=np.float64)
     r = np.zeros(3) if lever is None else np.asarray(lever, dtype=np.float64)
+    bg = np.asarray(bg, dtype=np.float64)
+    ba = np.asarray(ba, dtype=np.float64)
     dR, dv, dp = np.eye(3), np.zeros(3), np.zeros(3)
-    Jv, Jp = np.zeros((3, 3)), np.zeros((3, 3))
+    Jv, Jp, Jvg, Jpg, JR = (np.zeros((3, 3)) for _ in range(5))
     T = 0.0
     wp = None if w_prev is None else np.asarray(w_prev, dtype=np.float64)
     for dt, gyro, accel in samples:
         w = Ri @ (np.asarray(gyro, dtype=np.float64) - bg)
         al = np.zeros(3) if wp is None else (w - wp) / dt
         a = Ri @ (np.asarray(accel, dtype=np.float64) - ba) - np.cross(w, np.cross(w, r)) - np.cross(al, r)
+        Ra = dR @ _skew(a) @ JR
         dp = dp + dv * dt + 0.5 * (dR @ a) * dt * dt
         Jp = Jp + Jv * dt - 0.5 * (dR @ Ri) * dt * dt
+        Jpg = Jpg + Jvg * dt - 0.5 * Ra * dt * dt
         dv = dv + (dR @ a) * dt
         Jv = Jv - (dR @ Ri) * dt
-        dR = dR @ _exp_so3(w * dt)
+        Jvg = Jvg - Ra * dt
+        E = _exp_so3(w * dt)
+        JR = E.T @ JR - _jr_so3(w * dt) @ Ri * dt
+        dR = dR @ E
         T += dt
         wp = w
     out = np.zeros(INE_N)
@@ -114,32 +144,47 @@ def preintegrate(samples: list, rect_R_imu: np.ndarray, bg: np.ndarray, ba: np.n
     out[27] = T
     out[28] = 1.0 / (acc_density ** 2 * T + v_floor ** 2)
     out[29] = 1.0 / (acc_density ** 2 * T ** 3 / 3.0 + p_floor ** 2)
+    out[30] = 1.0 / (gyro_density ** 2 * T + r_floor ** 2) if gyro_density > 0.0 else 0.0
+    out[31] = 1.0 / (acc_rw ** 2 * T + ba_floor ** 2) if acc_rw > 0.0 else 0.0
+    out[32:41] = dR.T.reshape(9)
+    out[41:50] = (dR @ JR).reshape(9)
+    out[50:59], out[59:68], out[68:71] = Jvg.reshape(9), Jpg.reshape(9), bg
+    out[71] = 1.0 / (gyro_rw ** 2 * T + bg_floor ** 2) if gyro_rw > 0.0 else 0.0
     return out
 
 
 def inertial_residual(f: np.ndarray, Rcw_i: np.ndarray, tcw_i: np.ndarray, Rcw_j: np.ndarray, tcw_j: np.ndarray,
-                      v_i: np.ndarray, v_j: np.ndarray, ba: np.ndarray, gw: np.ndarray) -> np.ndarray:
-    """(r_v, r_p) of one inertial factor record at the cameras cam_T_world i, j."""
+                      v_i: np.ndarray, v_j: np.ndarray, bias_i: np.ndarray, bias_j: np.ndarray,
+                      gw: np.ndarray) -> np.ndarray:
+    """(r_v, r_p, r_R, r_ba, r_bg) (15) of one inertial factor record at the cameras cam_T_world
+    i, j, velocities and biases (ba, bg) = bias[0:3], bias[3:6]."""
     dt = f[27]
-    dba = ba - f[24:27]
+    dba = bias_i[0:3] - f[24:27]
+    dbg = bias_i[3:6] - f[68:71]
     p_i, p_j = -Rcw_i.T @ tcw_i, -Rcw_j.T @ tcw_j
     uv = v_j - v_i - gw * dt
     up = p_j - p_i - v_i * dt - 0.5 * gw * dt * dt
-    rv = Rcw_i @ uv - (f[0:3] + f[6:15].reshape(3, 3) @ dba)
-    rp = Rcw_i @ up - (f[3:6] + f[15:24].reshape(3, 3) @ dba)
-    return np.concatenate([rv, rp])
+    rv = Rcw_i @ uv - (f[0:3] + f[6:15].reshape(3, 3) @ dba + f[50:59].reshape(3, 3) @ dbg)
+    rp = Rcw_i @ up - (f[3:6] + f[15:24].reshape(3, 3) @ dba + f[59:68].reshape(3, 3) @ dbg)
+    A = f[32:41].reshape(3, 3).T @ (Rcw_j @ Rcw_i.T)
+    rR = 0.5 * np.array([A[2, 1] - A[1, 2], A[0, 2] - A[2, 0], A[1, 0] - A[0, 1]]) + f[41:50].reshape(3, 3) @ dbg
+    return np.concatenate([rv, rp, rR, bias_j[0:3] - bias_i[0:3], bias_j[3:6] - bias_i[3:6]])
+
+
+def inertial_weights(f: np.ndarray) -> np.ndarray:
+    return np.array([f[28]] * 3 + [f[29]] * 3 + [f[30]] * 3 + [f[31]] * 3 + [f[71]] * 3)
 
 
 def inertial_system(st, slots: list[int], Rs: np.ndarray, ts: np.ndarray, S: np.ndarray, b: np.ndarray) -> tuple | None:
     """``KeyframeWindow.inertial_terms`` for any window state ``st`` carrying ``ine``, ``vel``,
-    ``ba``, ``ine_cfg`` and ``p.lam`` (a pair window, or a rig's body window with the body poses
+    ``bias``, ``ine_cfg`` and ``p.lam`` (a pair window, or a rig's body window with the body poses
     as the cameras)."""
     n = len(slots)
     fs = [c for c in range(1, n) if st.ine[slots[c]][28] > 0.0]
     if not fs:
         return None
-    gw, ba0, wb = st.ine_cfg
-    my = 3 * n + 3
+    gw, ba0, wb, bg0, wg = st.ine_cfg
+    my = INE_Y * n
     Hxy = np.zeros((6 * n, my))
     Hyy = np.zeros((my, my))
     by = np.zeros(my)
@@ -147,11 +192,12 @@ def inertial_system(st, slots: list[int], Rs: np.ndarray, ts: np.ndarray, S: np.
         f = st.ine[slots[c]]
         i, j = c - 1, c
         vi, vj = st.vel[slots[i]], st.vel[slots[j]]
-        r = inertial_residual(f, Rs[i], ts[i], Rs[j], ts[j], vi, vj, st.ba, gw)
+        bi, bj = st.bias[slots[i]], st.bias[slots[j]]
+        r = inertial_residual(f, Rs[i], ts[i], Rs[j], ts[j], vi, vj, bi, bj, gw)
         J = inertial_jacobian(f, Rs[i], ts[i], Rs[j], ts[j], vi, vj, gw)
-        Wd = np.array([f[28]] * 3 + [f[29]] * 3)
+        Wd = inertial_weights(f)
         xc = list(range(6 * i, 6 * i + 6)) + list(range(6 * j, 6 * j + 6))
-        yc = list(range(3 * i, 3 * i + 3)) + list(range(3 * j, 3 * j + 3)) + list(range(3 * n, 3 * n + 3))
+        yc = list(range(INE_Y * i, INE_Y * i + INE_Y)) + list(range(INE_Y * j, INE_Y * j + INE_Y))
         Jx, Jy = J[:, :12], J[:, 12:]
         WJx, WJy = Wd[:, None] * Jx, Wd[:, None] * Jy
         S[np.ix_(xc, xc)] += Jx.T @ WJx
@@ -159,8 +205,11 @@ def inertial_system(st, slots: list[int], Rs: np.ndarray, ts: np.ndarray, S: np.
         Hxy[np.ix_(xc, yc)] += Jx.T @ WJy
         Hyy[np.ix_(yc, yc)] += Jy.T @ WJy
         by[yc] -= Jy.T @ (Wd * r)
-    Hyy[3 * n:, 3 * n:] += wb * np.eye(3)
-    by[3 * n:] -= wb * (st.ba - ba0)
+    b0 = st.bias[slots[0]]   # the priors on the oldest keyframe's biases
+    Hyy[3:6, 3:6] += wb * np.eye(3)
+    by[3:6] -= wb * (b0[0:3] - ba0)
+    Hyy[6:9, 6:9] += wg * np.eye(3)
+    by[6:9] -= wg * (b0[3:6] - bg0)
     Hyy += st.p.lam * np.eye(my)
     return Hxy, Hyy, by
 
@@ -168,7 +217,7 @@ def inertial_system(st, slots: list[int], Rs: np.ndarray, ts: np.ndarray, S: np.
 def inertial_step(st, slots: list[int], S: np.ndarray, b: np.ndarray, ine: tuple) -> np.ndarray:
     """Solve the damped camera system ``S`` (6n, lam included), ``b`` with the velocity / bias
     unknowns of ``ine`` = (Hxy, Hyy, b_y) eliminated (camera 0 = gauge); apply dy to ``st``'s
-    velocities and bias; return the 6n camera step (zeros for camera 0)."""
+    velocities and biases; return the 6n camera step (zeros for camera 0)."""
     n = len(slots)
     Hxy, Hyy, by = ine
     Hx = Hxy[6:]
@@ -178,29 +227,37 @@ def inertial_step(st, slots: list[int], S: np.ndarray, b: np.ndarray, ine: tuple
     dc[6:] = np.linalg.solve(S[6:, 6:] - Hx @ Z, b[6:] - Hx @ zb)
     dy = zb - Z @ dc[6:]
     for c in range(n):
-        st.vel[slots[c]] = st.vel[slots[c]] + dy[3 * c:3 * c + 3]
-    st.ba = st.ba + dy[3 * n:]
+        y = dy[INE_Y * c:INE_Y * c + INE_Y]
+        st.vel[slots[c]] = st.vel[slots[c]] + y[0:3]
+        st.bias[slots[c]] = st.bias[slots[c]] + y[3:9]
     return dc
 
 
 def inertial_jacobian(f: np.ndarray, Rcw_i: np.ndarray, tcw_i: np.ndarray, Rcw_j: np.ndarray, tcw_j: np.ndarray,
                       v_i: np.ndarray, v_j: np.ndarray, gw: np.ndarray) -> np.ndarray:
-    """6 x 21 Jacobian of (r_v, r_p): columns rho_i, omega_i, rho_j, omega_j (left camera
-    updates), v_i, v_j, ba."""
+    """15 x 30 Jacobian of ``inertial_residual``: columns rho_i, omega_i, rho_j, omega_j (left
+    camera updates), then y_i = (v_i, ba_i, bg_i), y_j = (v_j, ba_j, bg_j)."""
     dt = f[27]
     p_i, p_j = -Rcw_i.T @ tcw_i, -Rcw_j.T @ tcw_j
     uv = v_j - v_i - gw * dt
     up = p_j - p_i - v_i * dt - 0.5 * gw * dt * dt
-    J = np.zeros((6, 21))
+    J = np.zeros((15, 30))
     J[0:3, 3:6] = -_skew(Rcw_i @ uv)
     J[0:3, 12:15] = -Rcw_i
-    J[0:3, 15:18] = Rcw_i
-    J[0:3, 18:21] = -f[6:15].reshape(3, 3)
+    J[0:3, 15:18] = -f[6:15].reshape(3, 3)
+    J[0:3, 18:21] = -f[50:59].reshape(3, 3)
+    J[0:3, 21:24] = Rcw_i
     J[3:6, 0:3] = np.eye(3)
     J[3:6, 3:6] = -_skew(Rcw_i @ up)
     J[3:6, 6:9] = -Rcw_i @ Rcw_j.T
     J[3:6, 12:15] = -Rcw_i * dt
-    J[3:6, 18:21] = -f[15:24].reshape(3, 3)
+    J[3:6, 15:18] = -f[15:24].reshape(3, 3)
+    J[3:6, 18:21] = -f[59:68].reshape(3, 3)
+    J[6:9, 3:6] = -np.eye(3)
+    J[6:9, 9:12] = (Rcw_j @ Rcw_i.T).T
+    J[6:9, 18:21] = f[41:50].reshape(3, 3)
+    J[9:12, 15:18], J[9:12, 24:27] = -np.eye(3), np.eye(3)
+    J[12:15, 18:21], J[12:15, 27:30] = -np.eye(3), np.eye(3)
     return J
 
 
@@ -243,8 +300,9 @@ class KeyframeWindow:
         self.imu_w = np.zeros(W)                     # its weight (0 = no factor)
         self.ine = np.zeros((W, INE_N))              # inertial factor from the previous keyframe
         self.vel = np.zeros((W, 3))                  # world velocity of the keyframe's camera
-        self.ba = np.zeros(3)                        # the window's accelerometer bias (IMU axes)
-        self.ine_cfg = (np.zeros(3), np.zeros(3), 0.0)   # gravity (world), bias prior, its weight
+        self.bias = np.zeros((W, 6))                 # its accelerometer and gyroscope biases (IMU axes)
+        # gravity (world), accelerometer-bias prior and weight, gyroscope-bias prior and weight
+        self.ine_cfg = (np.zeros(3), np.zeros(3), 0.0, np.zeros(3), 0.0)
         self.n_kf = 0
 
     # -- window bookkeeping --------------------------------------------------------------------
@@ -290,6 +348,7 @@ class KeyframeWindow:
         self.imu_M[slot], self.imu_w[slot] = (np.eye(3), 0.0) if imu is None else (np.asarray(imu[0], float), float(imu[1]))
         self.ine[slot] = 0.0 if ine is None else np.asarray(ine[0], dtype=np.float64)
         self.vel[slot] = 0.0 if ine is None else np.asarray(ine[1], dtype=np.float64)
+        self.bias[slot] = new_keyframe_bias(self.ine[slot], self.bias, prev)
         self.u[slot], self.v[slot] = u, v
         self.d[slot] = np.where(np.isfinite(disp) & (disp > 0), disp, np.nan)
         valid = np.isfinite(u)
@@ -424,9 +483,11 @@ class KeyframeWindow:
             b[rc:rc + 3] -= w * (Q @ e)
             b[rp:rp + 3] += w * e
 
-    def set_inertial(self, gw: np.ndarray, ba0: np.ndarray, wb: float) -> None:
-        """World gravity and the accelerometer-bias prior (value, weight) for the next solves."""
-        self.ine_cfg = (np.asarray(gw, dtype=np.float64).copy(), np.asarray(ba0, dtype=np.float64).copy(), float(wb))
+    def set_inertial(self, gw: np.ndarray, ba0: np.ndarray, wb: float, bg0: np.ndarray | None = None,
+                     wg: float = 0.0) -> None:
+        """World gravity and the priors (value, weight) on the oldest keyframe's accelerometer and
+        gyroscope biases for the next solves."""
+        self.ine_cfg = _ine_cfg(gw, ba0, wb, bg0, wg)
 
     def inertial_terms(self, slots: list[int], Rs: np.ndarray, ts: np.ndarray, S: np.ndarray,
                        b: np.ndarray) -> tuple | None:
@@ -478,6 +539,19 @@ class KeyframeWindow:
         return {"n_obs": int(cam.size), "n_lm": int(ob["ids"].size), "rms_px": rms}
 
 
+def _ine_cfg(gw, ba0, wb, bg0, wg) -> tuple:
+    return (np.asarray(gw, dtype=np.float64).copy(), np.asarray(ba0, dtype=np.float64).copy(), float(wb),
+            np.zeros(3) if bg0 is None else np.asarray(bg0, dtype=np.float64).copy(), float(wg))
+
+
+def new_keyframe_bias(record: np.ndarray, bias: np.ndarray, prev: int) -> np.ndarray:
+    """A new keyframe's (ba, bg): its record's linearisation point, or the previous keyframe's
+    biases without a record (zeros for the first keyframe)."""
+    if record[28] > 0.0:
+        return np.concatenate([record[24:27], record[68:71]])
+    return bias[prev].copy() if prev >= 0 else np.zeros(6)
+
+
 def _skew(t: np.ndarray) -> np.ndarray:
     return np.array([[0.0, -t[2], t[1]], [t[2], 0.0, -t[0]], [-t[1], t[0], 0.0]])
 
@@ -524,11 +598,12 @@ class RigKeyframeWindow:
         self.B = np.tile(np.eye(4), (params.window, 1, 1))   # body_T_world per slot
         self.ine = np.zeros((params.window, INE_N))
         self.vel = np.zeros((params.window, 3))
-        self.ba = np.zeros(3)
-        self.ine_cfg = (np.zeros(3), np.zeros(3), 0.0)
+        self.bias = np.zeros((params.window, 6))
+        self.ine_cfg = (np.zeros(3), np.zeros(3), 0.0, np.zeros(3), 0.0)
 
-    def set_inertial(self, gw: np.ndarray, ba0: np.ndarray, wb: float) -> None:
-        self.ine_cfg = (np.asarray(gw, dtype=np.float64).copy(), np.asarray(ba0, dtype=np.float64).copy(), float(wb))
+    def set_inertial(self, gw: np.ndarray, ba0: np.ndarray, wb: float, bg0: np.ndarray | None = None,
+                     wg: float = 0.0) -> None:
+        self.ine_cfg = _ine_cfg(gw, ba0, wb, bg0, wg)
 
     @property
     def frame(self) -> np.ndarray:
@@ -545,11 +620,13 @@ class RigKeyframeWindow:
         pair p as for ``KeyframeWindow.add_keyframe``; ``ine`` = (record, v0) the body's inertial
         factor from the previous keyframe and its initial velocity."""
         slot = -1
+        prev = self.order()[-1] if self.pairs[0].n_kf else -1
         for p, (w, (u, v, disp, link)) in enumerate(zip(self.pairs, obs)):
             slot = w.add_keyframe(g, self._mul4(self.Einv[p], B_new), u, v, disp, link)
         self.B[slot] = B_new
         self.ine[slot] = 0.0 if ine is None else np.asarray(ine[0], dtype=np.float64)
         self.vel[slot] = 0.0 if ine is None else np.asarray(ine[1], dtype=np.float64)
+        self.bias[slot] = new_keyframe_bias(self.ine[slot], self.bias, prev)
         return slot
 
     def solve(self) -> dict:

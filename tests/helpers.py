@@ -176,3 +176,29 @@ def rgbd_rig_scene(names: tuple = ("192.168.2.21", "192.168.2.22", "192.168.2.23
     records = np.stack([np.stack([pack_rgbd(b, d) for b, d in fr]) for fr in raw])
     return {"raw": raw, "records": records, "rects": rects, "E": E, "traj": srcs[0].trajectory,
             "cams": cams, "pairs": pairs, "sources": srcs}
+
+
+def exact_inertial_record(Ti, vi, Tj, vj, gw, dt, b_true, rng, weights=(1e3, 1e5, 1e4, 1e2, 1e3), b_lin=None):
+    """An inertial factor record (oracle/numpy_ba.py INE_N layout) between cameras cam_T_world Ti
+    and Tj whose velocity, position and gyro-rotation residuals vanish at velocities vi, vj and the
+    biases b_true = (ba, bg) of the earlier keyframe (linearised at b_lin, default 0), with random
+    bias Jacobians; weights = (wv, wp, wR, w_ra, w_rg)."""
+    from oracle import numpy_ba as B
+
+    b_lin = np.zeros(6) if b_lin is None else np.asarray(b_lin, dtype=np.float64)
+    f = np.zeros(B.INE_N)
+    Jv, Jp = rng.normal(0, 0.2, (3, 3)) * dt, rng.normal(0, 0.02, (3, 3)) * dt
+    Jvg, Jpg = rng.normal(0, 0.2, (3, 3)) * dt, rng.normal(0, 0.02, (3, 3)) * dt
+    JRe = -np.eye(3) * dt + rng.normal(0, 0.01, (3, 3)) * dt
+    dba, dbg = b_true[0:3] - b_lin[0:3], b_true[3:6] - b_lin[3:6]
+    pi, pj = -Ti[:3, :3].T @ Ti[:3, 3], -Tj[:3, :3].T @ Tj[:3, 3]
+    f[0:3] = Ti[:3, :3] @ (vj - vi - gw * dt) - Jv @ dba - Jvg @ dbg
+    f[3:6] = Ti[:3, :3] @ (pj - pi - vi * dt - 0.5 * gw * dt * dt) - Jp @ dba - Jpg @ dbg
+    t = -JRe @ dbg   # the gyro rotation M with vee-asym(M^T Q) = t
+    nt = float(np.linalg.norm(t))
+    A = B._exp_so3(t / max(nt, 1e-300) * np.arcsin(min(nt, 1.0)))
+    M = (Tj[:3, :3] @ Ti[:3, :3].T) @ A.T
+    f[6:15], f[15:24], f[24:27], f[27] = Jv.reshape(9), Jp.reshape(9), b_lin[0:3], dt
+    f[28], f[29], f[30], f[31], f[71] = weights
+    f[32:41], f[41:50], f[50:59], f[59:68], f[68:71] = M.reshape(9), JRe.reshape(9), Jvg.reshape(9), Jpg.reshape(9), b_lin[3:6]
+    return f

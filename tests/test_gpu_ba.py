@@ -41,36 +41,30 @@ def _imu_factors(sc, n: int, angle: float = 3e-3, weight: float = 1e5) -> dict:
     return out
 
 
-INE_CFG = (np.array([0.4, 9.7, 1.2]), np.array([0.01, 0.0, -0.01]), 10.0)   # gravity, bias prior, weight
+# gravity, accelerometer-bias prior and weight, gyroscope-bias prior and weight (oldest keyframe)
+INE_CFG = (np.array([0.4, 9.7, 1.2]), np.array([0.01, 0.0, -0.01]), 10.0, np.array([0.0, 0.002, 0.0]), 100.0)
+B_TRUE = np.array([0.02, -0.01, 0.03, 0.004, -0.003, 0.002])   # accelerometer, gyroscope biases
 
 
 def _inertial_factors(sc, n: int) -> dict:
-    """Per keyframe g > 0: an inertial factor whose residual vanishes at the oracle front end's
-    cameras, central-difference velocities and a bias of (0.02, -0.01, 0.03) (the BA's visual
-    window disagrees slightly, so the factors pull), with the initial velocity off by 0.05 m/s."""
-    from oracle.numpy_ba import INE_N
+    """Per keyframe g > 0: an inertial factor whose velocity, position and gyro-rotation residuals
+    vanish at the oracle front end's cameras, central-difference velocities and the biases B_TRUE
+    (the BA's visual window disagrees slightly, so the factors pull), with the initial velocity
+    off by 0.05 m/s."""
+    from helpers import exact_inertial_record
 
     rng = np.random.default_rng(7)
     iv = sc["cfg"].ba_kf_interval
     dt = iv / 30.0
     gw = INE_CFG[0]
-    ba_true = np.array([0.02, -0.01, 0.03])
     Tcw = [np.linalg.inv(r["world_T_cam"]) for r in sc["oracle"]]
     pos = [r["world_T_cam"][:3, 3] for r in sc["oracle"]]
     vel = {g: (pos[min(g + 1, n - 1)] - pos[max(g - 1, 0)]) / (dt / iv * (min(g + 1, n - 1) - max(g - 1, 0)))
            for g in range(0, n, iv)}
     out = {}
     for g in range(iv, n, iv):
-        Ti, Tj = Tcw[g - iv], Tcw[g]
-        vi, vj = vel[g - iv], vel[g]
-        pi, pj = pos[g - iv], pos[g]
-        Jv, Jp = rng.normal(0, 0.2, (3, 3)) * dt, rng.normal(0, 0.02, (3, 3)) * dt
-        f = np.zeros(INE_N)
-        f[0:3] = Ti[:3, :3] @ (vj - vi - gw * dt) - Jv @ ba_true
-        f[3:6] = Ti[:3, :3] @ (pj - pi - vi * dt - 0.5 * gw * dt * dt) - Jp @ ba_true
-        f[6:15], f[15:24] = Jv.reshape(9), Jp.reshape(9)
-        f[27], f[28], f[29] = dt, 1e3, 1e5
-        out[g] = (f, vj + rng.normal(0, 0.05, 3))
+        f = exact_inertial_record(Tcw[g - iv], vel[g - iv], Tcw[g], vel[g], gw, dt, B_TRUE, rng)
+        out[g] = (f, vel[g] + rng.normal(0, 0.05, 3))
     return out
 
 
@@ -89,7 +83,7 @@ def _oracle_windows(sc, imu: dict | None = None, ine: dict | None = None):
         w = trk.win
         snaps.append({"frames": w.frame.copy(), "T_cw": w.T_cw.copy(), "lm": w.lm.copy(), "X": w.X.copy(),
                       "u": w.u.copy(), "v": w.v.copy(), "d": w.d.copy(), "solve": trk.last_solve,
-                      "vel": w.vel.copy(), "ba": w.ba.copy()})
+                      "vel": w.vel.copy(), "bias": w.bias.copy()})
     return snaps
 
 
@@ -206,7 +200,7 @@ def test_ba_graph_replay_equals_direct_launches(split):
             np.testing.assert_array_equal(np.asarray(a[key]).view(np.uint8), np.asarray(b[key]).view(np.uint8),
                                           err_msg=f"batch {k} {key}")
         np.testing.assert_array_equal(ai["vel"], bi["vel"])
-        np.testing.assert_array_equal(ai["ba"], bi["ba"])
+        np.testing.assert_array_equal(ai["bias"], bi["bias"])
         assert a["ok"] and a["n_lm"] == b["n_lm"] > 50
     for key, a in runs[False][1].items():
         np.testing.assert_array_equal(a, runs[True][1][key], err_msg=key)
@@ -275,7 +269,8 @@ def test_ba_inertial_factors_parity():
                 occ = want_k["frames"] >= 0
                 err_v = np.abs(gi["vel"][occ] - want_k["vel"][occ]).max() / np.abs(want_k["vel"][occ]).max()
                 assert err_v < 1e-9, (b0, err_v)
-                assert np.abs(gi["ba"] - want_k["ba"]).max() < 1e-9 * max(np.abs(want_k["ba"]).max(), 1e-3), (b0, gi["ba"])
+                err_b = np.abs(gi["bias"][occ] - want_k["bias"][occ]).max()
+                assert err_b < 1e-9 * max(np.abs(want_k["bias"][occ]).max(), 1e-3), (b0, err_b)
                 snaps.append((got, gi))
             runs.append(snaps)
         finally:
@@ -283,11 +278,12 @@ def test_ba_inertial_factors_parity():
     for (a, ai), (b, bi) in zip(*runs):
         np.testing.assert_array_equal(a["T_cw"], b["T_cw"])
         np.testing.assert_array_equal(ai["vel"], bi["vel"])
-        np.testing.assert_array_equal(ai["ba"], bi["ba"])
+        np.testing.assert_array_equal(ai["bias"], bi["bias"])
     occ = want[-1]["frames"] >= 0
     moved = max(rel_frobenius(want[-1]["T_cw"][s_], plain[-1]["T_cw"][s_]) for s_ in np.nonzero(occ)[0])
     assert moved > 1e-7, moved
-    assert np.abs(want[-1]["ba"]).max() > 1e-4   # the bias moved off zero
+    occ = want[-1]["frames"] >= 0
+    assert np.abs(want[-1]["bias"][occ][:, 3:6]).max() > 1e-4   # the gyroscope biases moved off zero
 
 
 def test_ba_two_pairs_own_factors_parity():
@@ -382,7 +378,8 @@ def test_ba_inertial_state_resets_and_rejects_bad_input():
     try:
         f, v0 = ine[2]
         for bad in (np.where(np.arange(f.size) == 3, np.nan, f), np.where(np.arange(f.size) == 27, 0.0, f),
-                    np.where(np.arange(f.size) == 29, -1.0, f)):
+                    np.where(np.arange(f.size) == 29, -1.0, f), np.where(np.arange(f.size) == 71, -1.0, f),
+                    np.where(np.arange(f.size) == 45, np.inf, f)):
             with pytest.raises(RuntimeError, match="tslam error"):
                 h.ba_inertial_factor(2, bad, v0)
         with pytest.raises(RuntimeError, match="tslam error"):
@@ -393,11 +390,11 @@ def test_ba_inertial_state_resets_and_rejects_bad_input():
         for b0 in range(0, n, batch):
             h.submit(dev[b0:].data_ptr(), batch, torch.cuda.current_stream().cuda_stream)
         got = h.ba_read_inertial(0)
-        assert np.abs(got["ba"]).max() > 0 and np.abs(got["vel"]).max() > 0
+        assert np.abs(got["bias"]).max() > 0 and np.abs(got["vel"]).max() > 0
         h.reset()
         got = h.ba_read_inertial(0)
         np.testing.assert_array_equal(got["vel"], 0.0)
-        np.testing.assert_array_equal(got["ba"], 0.0)
+        np.testing.assert_array_equal(got["bias"], 0.0)
     finally:
         h.close()
 

@@ -26,35 +26,30 @@ BA_ITEMS = dict(ba_window=4, ba_kf_interval=2, ba_iters=3, ba_lambda=1.0, ba_out
 N = 10
 
 
-RIG_INE_CFG = (np.array([0.3, -9.75, 0.9]), np.array([0.0, 0.01, 0.0]), 10.0)   # gravity, bias prior, weight
+# gravity, accelerometer-bias prior and weight, gyroscope-bias prior and weight (oldest keyframe)
+RIG_INE_CFG = (np.array([0.3, -9.75, 0.9]), np.array([0.0, 0.01, 0.0]), 10.0, np.array([0.001, 0.0, 0.0]), 100.0)
 
 
 def _body_inertial_factors(T_abs: list) -> dict:
-    """Per body keyframe g > 0: an inertial factor (body axes) whose residual vanishes at the rig
-    chain's body poses, central-difference velocities and a bias (0.02, -0.01, 0.03); initial
-    velocities off by 0.05 m/s (the BA's visual window disagrees slightly: the factors pull)."""
-    from oracle.numpy_ba import INE_N
+    """Per body keyframe g > 0: an inertial factor (body axes) whose velocity, position and
+    gyro-rotation residuals vanish at the rig chain's body poses, central-difference velocities and
+    biases (0.02, -0.01, 0.03 | 0.003, 0.002, -0.004); initial velocities off by 0.05 m/s (the BA's
+    visual window disagrees slightly: the factors pull)."""
+    from helpers import exact_inertial_record
 
     rng = np.random.default_rng(11)
     iv = BA_ITEMS["ba_kf_interval"]
     dt = 1.0 / 30.0
     gw = RIG_INE_CFG[0]
-    ba_true = np.array([0.02, -0.01, 0.03])
+    b_true = np.array([0.02, -0.01, 0.03, 0.003, 0.002, -0.004])
     Tbw = [inv_rigid(t) for t in T_abs]
     pos = [t[:3, 3] for t in T_abs]
     vel = {g: (pos[min(g + 1, N - 1)] - pos[max(g - 1, 0)]) / (dt * (min(g + 1, N - 1) - max(g - 1, 0)))
            for g in range(0, N, iv)}
     out = {}
     for g in range(iv, N, iv):
-        Ti, vi, vj = Tbw[g - iv], vel[g - iv], vel[g]
-        Jv, Jp = rng.normal(0, 0.2, (3, 3)) * iv * dt, rng.normal(0, 0.02, (3, 3)) * iv * dt
-        f = np.zeros(INE_N)
-        T = iv * dt
-        f[0:3] = Ti[:3, :3] @ (vj - vi - gw * T) - Jv @ ba_true
-        f[3:6] = Ti[:3, :3] @ (pos[g] - pos[g - iv] - vi * T - 0.5 * gw * T * T) - Jp @ ba_true
-        f[6:15], f[15:24] = Jv.reshape(9), Jp.reshape(9)
-        f[27], f[28], f[29] = T, 1e3, 1e5
-        out[g] = (f, vj + rng.normal(0, 0.05, 3))
+        f = exact_inertial_record(Tbw[g - iv], vel[g - iv], Tbw[g], vel[g], gw, iv * dt, b_true, rng)
+        out[g] = (f, vel[g] + rng.normal(0, 0.05, 3))
     return out
 
 
@@ -86,7 +81,7 @@ def rig_ba_scenario(inertial: bool = False):
         ba.step(i, outs, T_abs, ine=None if ine is None else ine.get(i))
         w = ba.win
         snaps.append({"frames": w.frame.copy(), "B": w.B.copy(), "solve": ba.last_solve,
-                      "vel": w.vel.copy(), "ba": w.ba.copy(),
+                      "vel": w.vel.copy(), "bias": w.bias.copy(),
                       "pairs": [{"T_cw": pw.T_cw.copy(), "lm": pw.lm.copy(), "X": pw.X.copy(), "u": pw.u.copy(),
                                  "v": pw.v.copy(), "d": pw.d.copy()} for pw in w.pairs]})
     return {"frames": frames, "rects": rects, "E": E, "cfg": cfg, "snaps": snaps, "traj": sc["traj"], "T_abs": T_seq,
@@ -165,13 +160,14 @@ def test_rig_ba_body_inertial_factors_match_oracle():
             occ = want["frames"] >= 0
             err_v = np.abs(gi["vel"][occ] - want["vel"][occ]).max() / max(np.abs(want["vel"][occ]).max(), 1e-3)
             assert err_v < 1e-9, (b0, err_v)
-            assert np.abs(gi["ba"] - want["ba"]).max() < 1e-9 * max(np.abs(want["ba"]).max(), 1e-3), (b0, gi["ba"])
+            err_b = np.abs(gi["bias"][occ] - want["bias"][occ]).max()
+            assert err_b < 1e-9 * max(np.abs(want["bias"][occ]).max(), 1e-3), (b0, err_b)
     finally:
         h.close()
     last, base = sc["snaps"][-1], plain["snaps"][-1]
     occ = last["frames"] >= 0
     assert max(rel_frobenius(last["B"][s], base["B"][s]) for s in np.nonzero(occ)[0]) > 1e-7
-    assert np.abs(last["ba"]).max() > 1e-4
+    assert np.abs(last["bias"][last["frames"] >= 0]).max() > 1e-4
 
 
 def test_rig_ba_every_pair_contributes():

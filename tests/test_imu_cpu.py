@@ -181,7 +181,10 @@ def test_preintegration_matches_oracle():
     for i0, wp in ((5, None), (12, np.array([0.1, -0.2, 0.05]))):
         smp = [(dt, src.imu_sample(k)["gyroscope"], src.imu_sample(k)["accelerometer"]) for k in range(i0 + 1, i0 + 6)]
         got = prod.preintegrate(smp, bg, ba, wp)
-        want = preintegrate(smp, ri, bg, ba, LEVER, w_prev=wp, acc_density=noise.acc_density)
+        want = preintegrate(smp, ri, bg, ba, LEVER, w_prev=wp, acc_density=noise.acc_density,
+                            gyro_density=noise.gyro_density, r_floor=1e-3, acc_rw=noise.acc_random_walk,
+                            gyro_rw=noise.gyro_random_walk, ba_floor=1e-3, bg_floor=1e-3)
+        assert got.size == want.size == 80 and got[30] > 0 and got[31] > 0 and got[71] > 0
         np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-14)
     prod.begin(src.imu_sample(0)["accelerometer"])
     g = prod.gravity()

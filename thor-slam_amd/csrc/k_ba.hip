@@ -153,6 +153,13 @@ __device__ int block_scan_excl(int v, int* s_tmp, int* total) {
 // stored (positive depth, reprojection error <= outlier_px) and every gated observation counts
 // towards its landmark (cnt pre-zeroed).  No other item reads what an inserting thread writes: the
 // new slot's landmarks are observed by the new keyframe only (eviction re-homed the slot's old ones).
+// A new keyframe's bias component k (accelerometer 0-2, gyroscope 3-5; oracle new_keyframe_bias):
+// its inertial record's linearisation point, else the previous keyframe's, else 0.
+__device__ __forceinline__ double ba_new_bias(const BaArgs& a, const double* bias, int k) {
+    if (a.ine[28] > 0.0) return k < 3 ? a.ine[24 + k] : a.ine[68 + k - 3];
+    return a.prev >= 0 ? bias[(size_t)a.prev * 6 + k] : 0.0;
+}
+
 __device__ __forceinline__ void d_ba_insert_gate(const BatchCtx& c, const BaArgs& a) {
     BA_PRIO;
     __shared__ double s_T[TS_BA_MAXW][12];   // cam_T_world of the window
@@ -191,6 +198,7 @@ __device__ __forceinline__ void d_ba_insert_gate(const BatchCtx& c, const BaArgs
     if (blockIdx.x == 0 && threadIdx.x < 10) q.imu[(size_t)a.slot * 10 + threadIdx.x] = a.imu[threadIdx.x];
     if (blockIdx.x == 0 && threadIdx.x < TS_BA_INE) q.ine[(size_t)a.slot * TS_BA_INE + threadIdx.x] = a.ine[threadIdx.x];
     if (blockIdx.x == 0 && threadIdx.x < 3) q.vel[(size_t)a.slot * 3 + threadIdx.x] = a.vel0[threadIdx.x];
+    if (blockIdx.x == 0 && threadIdx.x < 6) q.bias[(size_t)a.slot * 6 + threadIdx.x] = ba_new_bias(a, q.bias, threadIdx.x);
     // the slot table back to all -1: the rows the last solve filled (k_ba_tilescatter fills this one's)
     const int Lp = q.counts[1];
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < Lp * TS_BA_MAXW; t += gridDim.x * blockDim.x) q.lo_o[t] = -1;
@@ -885,30 +893,42 @@ __global__ __launch_bounds__(64 * BA_SOLVE_WAVES) void k_ba_reduce_rec(BaCtxRef 
 // Camera updates R <- cayley(w) R, t <- ... + rho follow.
 #define BA_SP 65   // LDS row pitch of S (doubles)
 // ---------------------------------------------------------------------------------------------
-// Inertial factors (oracle/numpy_ba.py inertial_terms): per window-consecutive pair (c - 1, c)
-// whose later keyframe carries a factor, the velocity and position residuals of the accelerometer
-// preintegration against the cameras, the two velocities and the window's accelerometer bias.
-// The velocity / bias unknowns y (3n + 3) are eliminated into the camera system in LDS:
-//   phase 0: factor t (= c - 1) on thread t: r (6), J (6 x 21: rho_i, omega_i, rho_j, omega_j,
-//            v_i, v_j, ba), weights;
+// Inertial factors (oracle/numpy_ba.py inertial_system): per window-consecutive pair (i, j) =
+// (c - 1, c) whose later keyframe carries a factor, the velocity, position and gyro-rotation
+// residuals of the IMU preintegration against the cameras, the velocities and the earlier
+// keyframe's biases, plus the random walks of both biases between the two keyframes.  Every
+// keyframe c has TS_BA_INEY unknowns y_c = (v_c, ba_c, bg_c) (9n in all, block tridiagonal Hyy),
+// eliminated into the camera system in LDS:
+//   phase 0: factor t (= c - 1) on thread t: r (15), J (15 x 30: rho_i, omega_i, rho_j, omega_j,
+//            y_i, y_j), the five row weights;
 //   phase 1: per factor (in order, a barrier each), thread (a, b) of J^T W J scatters into S
-//            (lower triangle), Hxy or Hyy and 21 threads the gradient into b_x or b_y; then the
-//            bias prior and lam I on Hyy;
-//   phase 2: wave 0 factors Hyy = L L^T (lane = row);
-//   phase 3: thread i < m: Z_i = L^-1 Hxy_i (in place); thread m: zb = L^-1 b_y;
+//            (lower triangle), Hxy or Hyy (packed lower) and 30 threads the gradient into b_x or
+//            b_y; then the priors on y_0's biases and lam I on Hyy;
+//   phase 2: wave 0 factors Hyy = L L^T (two rows per lane; fill-in stays in the block band);
+//   phase 3: thread i < m: Z_i = L^-1 Hxy_i (in place, banded forward substitution); thread m:
+//            zb = L^-1 b_y;
 //   phase 4: S -= Z Z^T (lower), b_x -= Z zb;
-//   after the camera solve (ba_inertial_update): dy = L^-T (zb - Z^T dc), v_c += dv_c, ba += dba.
+//   after the camera solve (ba_inertial_update): dy = L^-T (zb - Z^T dc) (banded), then every
+//   keyframe's velocity and biases move by its dy.
 // ---------------------------------------------------------------------------------------------
+#define BA_INE_R 15   // residual rows: r_v, r_p, r_R, r_ba, r_bg
+#define BA_INE_C 30   // Jacobian columns: rho_i, omega_i, rho_j, omega_j, y_i, y_j
 struct BaIneLds {
-    double J[TS_BA_MAXW - 1][6][21];
-    double r[TS_BA_MAXW - 1][6];
-    double w[TS_BA_MAXW - 1][2];
-    double Y[TS_BA_MAXY][TS_BA_MAXY + 1];   // Hyy, then its Cholesky factor (lower)
-    double X[TS_BA_MAXD][TS_BA_MAXY + 1];   // row i: Hxy_i, then Z_i = (L^-1 Hyx)^T_i
-    double by[TS_BA_MAXY];                  // b_y, then zb = L^-1 b_y, then zb - Z^T dc
-    double ld[TS_BA_MAXY];                  // 1 / L_yy
+    double J[TS_BA_MAXW - 1][BA_INE_R][BA_INE_C];
+    double r[TS_BA_MAXW - 1][BA_INE_R];
+    double w[TS_BA_MAXW - 1][5];
+    double Y[TS_BA_MAXY * (TS_BA_MAXY + 1) / 2];   // Hyy (lower, packed by rows), then its Cholesky factor
+    double X[TS_BA_MAXD][TS_BA_MAXY + 1];           // row i: Hxy_i, then Z_i = (L^-1 Hyx)^T_i
+    double by[TS_BA_MAXY];                          // b_y, then zb = L^-1 b_y, then dy
+    double ld[TS_BA_MAXY];                          // 1 / L_yy
     int any, good;
 };
+__device__ __forceinline__ int ine_yi(int i, int k) { return i * (i + 1) / 2 + k; }   // (i, k <= i)
+// last row + 1 of the band of column j (L_ij = 0 for i >= this: Hyy is block tridiagonal)
+__device__ __forceinline__ int ine_band_end(int j, int my) { return min(my, TS_BA_INEY * (j / TS_BA_INEY + 2)); }
+// first column of the band of row y
+__device__ __forceinline__ int ine_band_start(int y) { return max(0, TS_BA_INEY * (y / TS_BA_INEY - 1)); }
+
 template <bool INE>
 __device__ __forceinline__ BaIneLds* ine_lds() {
     return nullptr;
@@ -921,79 +941,113 @@ __device__ __forceinline__ BaIneLds* ine_lds<true>() {
 
 // global unknown of factor t's column col: x index (camera rows without the gauge, -1 = camera 0)
 // for col < 12, else y index
-__device__ __forceinline__ int ine_col(int t, int col, int n) {
+__device__ __forceinline__ int ine_col(int t, int col) {
     const int c = t + 1;
     if (col < 6) return c - 1 >= 1 ? 6 * (c - 2) + col : -1;
     if (col < 12) return 6 * (c - 1) + col - 6;
-    if (col < 15) return 3 * (c - 1) + col - 12;
-    if (col < 18) return 3 * c + col - 15;
-    return 3 * n + col - 18;
+    if (col < 21) return TS_BA_INEY * (c - 1) + col - 12;
+    return TS_BA_INEY * c + col - 21;
+}
+
+// 3x3 row-major helpers (in-kernel: registers)
+__device__ __forceinline__ void ine_mv(const double* M, const double* x, double* y) {
+    for (int r = 0; r < 3; ++r) y[r] = (M[3 * r] * x[0] + M[3 * r + 1] * x[1]) + M[3 * r + 2] * x[2];
 }
 
 // phases 0-4; returns whether any factor acts (block-uniform)
 __device__ bool ba_inertial_reduce(const BaPair& q, const BaArgs& a, int n, int m, double* s_S, double* s_x, BaIneLds* L) {
 #pragma clang fp contract(fast)
     const int tid = threadIdx.x, nthr = blockDim.x;
-    const int nf = n - 1, my = 3 * n + 3;
-    if (tid < nf) {   // phase 0
-        const int t = tid, c = t + 1;
+    const int nf = n - 1, my = TS_BA_INEY * n;
+    if (tid < 5 * nf) {   // phase 0: thread (t, grp) = factor t's row group grp (r_v, r_p, r_R, r_ba, r_bg)
+        const int t = tid / 5, grp = tid - 5 * t, c = t + 1;
         const double* f = q.ine + (size_t)a.order[c] * TS_BA_INE;
-        const double wv = f[28], wp = f[29];
-        double (*J)[21] = L->J[t];
-        for (int r = 0; r < 6; ++r) {
-            L->r[t][r] = 0.0;
-            for (int k = 0; k < 21; ++k) J[r][k] = 0.0;
+        const bool on = f[28] > 0.0;
+        double (*J)[BA_INE_C] = L->J[t] + 3 * grp;   // this group's 3 rows
+        double* rr = L->r[t] + 3 * grp;
+        for (int r = 0; r < 3; ++r) {
+            rr[r] = 0.0;
+            for (int k = 0; k < BA_INE_C; ++k) J[r][k] = 0.0;
         }
-        L->w[t][0] = wv > 0.0 ? wv : 0.0;
-        L->w[t][1] = wv > 0.0 ? wp : 0.0;
-        if (wv > 0.0) {
+        const int wi[5] = {28, 29, 30, 31, 71};
+        L->w[t][grp] = on ? f[wi[grp]] : 0.0;
+        if (on) {
             const double* Ti = q.T + (size_t)a.order[c - 1] * 16;
             const double* Tj = q.T + (size_t)a.order[c] * 16;
-            const double* vi = q.vel + (size_t)a.order[c - 1] * 3;
-            const double* vj = q.vel + (size_t)a.order[c] * 3;
+            const double* bi = q.bias + (size_t)a.order[c - 1] * 6;
+            const double* bj = q.bias + (size_t)a.order[c] * 6;
             const double dt = f[27];
-            double pi[3], pj[3], uv[3], up[3], dba[3];
-            for (int k = 0; k < 3; ++k) {
-                pi[k] = -((Ti[k] * Ti[3] + Ti[4 + k] * Ti[7]) + Ti[8 + k] * Ti[11]);
-                pj[k] = -((Tj[k] * Tj[3] + Tj[4 + k] * Tj[7]) + Tj[8 + k] * Tj[11]);
-                dba[k] = q.ine_ba[k] - f[24 + k];
-            }
-            for (int k = 0; k < 3; ++k) {
-                const double g = a.icfg[k];
-                uv[k] = ((vj[k] - vi[k]) - g * dt);
-                up[k] = (((pj[k] - pi[k]) - vi[k] * dt) - 0.5 * g * dt * dt);
-            }
-            double ruv[3], rup[3];
-            for (int r = 0; r < 3; ++r) {
-                ruv[r] = (Ti[4 * r] * uv[0] + Ti[4 * r + 1] * uv[1]) + Ti[4 * r + 2] * uv[2];
-                rup[r] = (Ti[4 * r] * up[0] + Ti[4 * r + 1] * up[1]) + Ti[4 * r + 2] * up[2];
-            }
-            for (int r = 0; r < 3; ++r) {
-                const double jv = (f[6 + 3 * r] * dba[0] + f[7 + 3 * r] * dba[1]) + f[8 + 3 * r] * dba[2];
-                const double jp = (f[15 + 3 * r] * dba[0] + f[16 + 3 * r] * dba[1]) + f[17 + 3 * r] * dba[2];
-                L->r[t][r] = ruv[r] - (f[r] + jv);
-                L->r[t][3 + r] = rup[r] - (f[3 + r] + jp);
-            }
-            // -[a]x rows: (0, a2, -a1), (-a2, 0, a0), (a1, -a0, 0)
-            const double sv[3][3] = {{0.0, ruv[2], -ruv[1]}, {-ruv[2], 0.0, ruv[0]}, {ruv[1], -ruv[0], 0.0}};
-            const double sp[3][3] = {{0.0, rup[2], -rup[1]}, {-rup[2], 0.0, rup[0]}, {rup[1], -rup[0], 0.0}};
-            for (int r = 0; r < 3; ++r)
+            double dbg[3];
+            for (int k = 0; k < 3; ++k) dbg[k] = bi[3 + k] - f[68 + k];
+            if (grp <= 1) {   // r_v / r_p: R_i u - (d + J_a dba + J_g dbg)
+                const double* vi = q.vel + (size_t)a.order[c - 1] * 3;
+                const double* vj = q.vel + (size_t)a.order[c] * 3;
+                double dba[3], u[3];
+                for (int k = 0; k < 3; ++k) dba[k] = bi[k] - f[24 + k];
                 for (int k = 0; k < 3; ++k) {
-                    const double Rrk = Ti[4 * r + k];
-                    J[r][3 + k] = sv[r][k];
-                    J[r][12 + k] = -Rrk;
-                    J[r][15 + k] = Rrk;
-                    J[r][18 + k] = -f[6 + 3 * r + k];
-                    J[3 + r][k] = r == k ? 1.0 : 0.0;
-                    J[3 + r][3 + k] = sp[r][k];
-                    // -R_cw,i R_cw,j^T
-                    J[3 + r][6 + k] = -((Ti[4 * r] * Tj[4 * k] + Ti[4 * r + 1] * Tj[4 * k + 1]) + Ti[4 * r + 2] * Tj[4 * k + 2]);
-                    J[3 + r][12 + k] = -Rrk * dt;
-                    J[3 + r][18 + k] = -f[15 + 3 * r + k];
+                    const double g = a.icfg[k];
+                    if (grp == 0) {
+                        u[k] = ((vj[k] - vi[k]) - g * dt);
+                    } else {
+                        const double pik = -((Ti[k] * Ti[3] + Ti[4 + k] * Ti[7]) + Ti[8 + k] * Ti[11]);
+                        const double pjk = -((Tj[k] * Tj[3] + Tj[4 + k] * Tj[7]) + Tj[8 + k] * Tj[11]);
+                        u[k] = (((pjk - pik) - vi[k] * dt) - 0.5 * g * dt * dt);
+                    }
                 }
+                double ru[3], ja[3], jg[3];
+                for (int r = 0; r < 3; ++r) ru[r] = (Ti[4 * r] * u[0] + Ti[4 * r + 1] * u[1]) + Ti[4 * r + 2] * u[2];
+                const double* Ja = f + (grp == 0 ? 6 : 15);
+                const double* Jg = f + (grp == 0 ? 50 : 59);
+                ine_mv(Ja, dba, ja);
+                ine_mv(Jg, dbg, jg);
+                for (int r = 0; r < 3; ++r) rr[r] = ru[r] - ((f[3 * grp + r] + ja[r]) + jg[r]);
+                // -[ru]x rows: (0, a2, -a1), (-a2, 0, a0), (a1, -a0, 0)
+                const double sk[3][3] = {{0.0, ru[2], -ru[1]}, {-ru[2], 0.0, ru[0]}, {ru[1], -ru[0], 0.0}};
+                for (int r = 0; r < 3; ++r)
+                    for (int k = 0; k < 3; ++k) {
+                        const double Rrk = Ti[4 * r + k];
+                        J[r][3 + k] = sk[r][k];
+                        J[r][15 + k] = -Ja[3 * r + k];
+                        J[r][18 + k] = -Jg[3 * r + k];
+                        if (grp == 0) {
+                            J[r][12 + k] = -Rrk;
+                            J[r][21 + k] = Rrk;
+                        } else {
+                            J[r][k] = r == k ? 1.0 : 0.0;
+                            // -R_cw,i R_cw,j^T
+                            J[r][6 + k] = -((Ti[4 * r] * Tj[4 * k] + Ti[4 * r + 1] * Tj[4 * k + 1]) + Ti[4 * r + 2] * Tj[4 * k + 2]);
+                            J[r][12 + k] = -Rrk * dt;
+                        }
+                    }
+            } else if (grp == 2) {   // r_R = vee-asym(M^T Q) + JRe dbg, Q = R_j R_i^T
+                double Qm[9], A[9], jr[3];
+                for (int r = 0; r < 3; ++r)
+                    for (int k = 0; k < 3; ++k)
+                        Qm[3 * r + k] = (Tj[4 * r] * Ti[4 * k] + Tj[4 * r + 1] * Ti[4 * k + 1]) + Tj[4 * r + 2] * Ti[4 * k + 2];
+                for (int r = 0; r < 3; ++r)
+                    for (int k = 0; k < 3; ++k)
+                        A[3 * r + k] = (f[32 + r] * Qm[k] + f[35 + r] * Qm[3 + k]) + f[38 + r] * Qm[6 + k];
+                ine_mv(f + 41, dbg, jr);
+                rr[0] = 0.5 * (A[7] - A[5]) + jr[0];
+                rr[1] = 0.5 * (A[2] - A[6]) + jr[1];
+                rr[2] = 0.5 * (A[3] - A[1]) + jr[2];
+                for (int r = 0; r < 3; ++r)
+                    for (int k = 0; k < 3; ++k) {
+                        J[r][3 + k] = r == k ? -1.0 : 0.0;
+                        J[r][9 + k] = Qm[3 * k + r];   // Q^T
+                        J[r][18 + k] = f[41 + 3 * r + k];
+                    }
+            } else {   // random walk of the accelerometer (grp 3) / gyroscope (grp 4) bias
+                const int o = grp == 3 ? 0 : 3, col = grp == 3 ? 15 : 18;
+                for (int r = 0; r < 3; ++r) {
+                    rr[r] = bj[o + r] - bi[o + r];
+                    J[r][col + r] = -1.0;
+                    J[r][col + 9 + r] = 1.0;
+                }
+            }
         }
     }
-    for (int e = tid; e < TS_BA_MAXY * (TS_BA_MAXY + 1); e += nthr) (&L->Y[0][0])[e] = 0.0;
+    for (int e = tid; e < TS_BA_MAXY * (TS_BA_MAXY + 1) / 2; e += nthr) L->Y[e] = 0.0;
     for (int e = tid; e < TS_BA_MAXD * (TS_BA_MAXY + 1); e += nthr) (&L->X[0][0])[e] = 0.0;
     if (tid < TS_BA_MAXY) L->by[tid] = 0.0;
     __syncthreads();
@@ -1006,70 +1060,84 @@ __device__ bool ba_inertial_reduce(const BaPair& q, const BaArgs& a, int n, int 
     if (!L->any) return false;
     for (int t = 0; t < nf; ++t) {   // phase 1, one factor at a time
         if (!(L->w[t][0] > 0.0)) continue;   // (uniform)
-        const double w0 = L->w[t][0], w1 = L->w[t][1];
-        const double (*J)[21] = L->J[t];
-        for (int e = tid; e < 21 * 21 + 21; e += nthr) {
-            if (e < 441) {
-                const int ca = e / 21, cb = e - 21 * ca;
-                const int ga = ine_col(t, ca, n), gb = ine_col(t, cb, n);
+        const double (*J)[BA_INE_C] = L->J[t];
+        const double* wt = L->w[t];
+        for (int e = tid; e < BA_INE_C * BA_INE_C + BA_INE_C; e += nthr) {
+            if (e < BA_INE_C * BA_INE_C) {
+                const int ca = e / BA_INE_C, cb = e - BA_INE_C * ca;
+                const int ga = ine_col(t, ca), gb = ine_col(t, cb);
                 const bool xa = ca < 12, xb = cb < 12;
                 if (ga < 0 || gb < 0) continue;        // the gauge camera's columns
                 if (xa && xb && ga < gb) continue;     // S: lower triangle
                 if (!xa && xb) continue;               // Hyx: from (b, a)
-                const double h = ((w0 * (J[0][ca] * J[0][cb]) + w0 * (J[1][ca] * J[1][cb])) + w0 * (J[2][ca] * J[2][cb])) +
-                                 ((w1 * (J[3][ca] * J[3][cb]) + w1 * (J[4][ca] * J[4][cb])) + w1 * (J[5][ca] * J[5][cb]));
+                if (!xa && !xb && ga < gb) continue;   // Hyy: lower triangle
+                double h = 0.0;
+#pragma unroll
+                for (int g5 = 0; g5 < 5; ++g5) {
+                    const double wg = wt[g5];
+                    h += (wg * (J[3 * g5][ca] * J[3 * g5][cb]) + wg * (J[3 * g5 + 1][ca] * J[3 * g5 + 1][cb])) +
+                         wg * (J[3 * g5 + 2][ca] * J[3 * g5 + 2][cb]);
+                }
                 if (xa && xb) s_S[ga * BA_SP + gb] += h;
                 else if (xa) L->X[ga][gb] += h;
-                else L->Y[ga][gb] += h;
+                else L->Y[ine_yi(ga, gb)] += h;
             } else {
-                const int ca = e - 441;
-                const int ga = ine_col(t, ca, n);
+                const int ca = e - BA_INE_C * BA_INE_C;
+                const int ga = ine_col(t, ca);
                 if (ga < 0) continue;
-                const double gsum = ((w0 * (J[0][ca] * L->r[t][0]) + w0 * (J[1][ca] * L->r[t][1])) + w0 * (J[2][ca] * L->r[t][2])) +
-                                    ((w1 * (J[3][ca] * L->r[t][3]) + w1 * (J[4][ca] * L->r[t][4])) + w1 * (J[5][ca] * L->r[t][5]));
+                double gsum = 0.0;
+#pragma unroll
+                for (int rr = 0; rr < BA_INE_R; ++rr) gsum += wt[rr / 3] * (J[rr][ca] * L->r[t][rr]);
                 if (ca < 12) s_x[ga] -= gsum;
                 else L->by[ga] -= gsum;
             }
         }
         __syncthreads();
     }
-    if (tid < my) {   // bias prior on ba, lam on every velocity / bias unknown
-        L->Y[tid][tid] += a.lam;
-        if (tid >= 3 * n) {
-            const int k = tid - 3 * n;
-            L->Y[tid][tid] += a.icfg[6];
-            L->by[tid] -= a.icfg[6] * (q.ine_ba[k] - a.icfg[3 + k]);
+    if (tid < my) {   // the priors on the oldest keyframe's biases, lam on every y unknown
+        L->Y[ine_yi(tid, tid)] += a.lam;
+        const double* b0 = q.bias + (size_t)a.order[0] * 6;
+        if (tid >= 3 && tid < 6) {
+            L->Y[ine_yi(tid, tid)] += a.icfg[6];
+            L->by[tid] -= a.icfg[6] * (b0[tid - 3] - a.icfg[tid]);
+        } else if (tid >= 6 && tid < 9) {
+            L->Y[ine_yi(tid, tid)] += a.icfg[10];
+            L->by[tid] -= a.icfg[10] * (b0[tid - 3] - a.icfg[tid + 1]);
         }
     }
     __syncthreads();
-    if (tid < 64) {   // phase 2: wave 0, lane = row
-        const int i = tid;
+    if (tid < 64) {   // phase 2: wave 0, rows lane and lane + 64
         bool good = true;
         for (int j = 0; j < my; ++j) {
-            const double d = L->Y[j][j];
+            const int iend = ine_band_end(j, my);
+            const double d = L->Y[ine_yi(j, j)];
             good = good && d > 0.0;
             const double l = sqrt(d), inv = 1.0 / l;
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            if (i > j && i < my) L->Y[i][j] *= inv;
-            if (i == j) {
-                L->Y[j][j] = l;
-                L->ld[j] = inv;
+            for (int i = tid; i < TS_BA_MAXY; i += 64) {
+                if (i > j && i < iend) L->Y[ine_yi(i, j)] *= inv;
+                if (i == j) {
+                    L->Y[ine_yi(j, j)] = l;
+                    L->ld[j] = inv;
+                }
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            if (i > j && i < my) {
-                const double lij = L->Y[i][j];
-                for (int k = j + 1; k <= i; ++k) L->Y[i][k] -= lij * L->Y[k][j];
+            for (int i = tid; i < TS_BA_MAXY; i += 64) {
+                if (i > j && i < iend) {
+                    const double lij = L->Y[ine_yi(i, j)];
+                    for (int k = j + 1; k <= i; ++k) L->Y[ine_yi(i, k)] -= lij * L->Y[ine_yi(k, j)];
+                }
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         }
-        if (i == 0) L->good = good;
+        if (tid == 0) L->good = good;
     }
     __syncthreads();
-    if (tid <= m) {   // phase 3: forward substitutions (thread m: the right-hand side)
+    if (tid <= m) {   // phase 3: banded forward substitutions (thread m: the right-hand side)
         double* z = tid < m ? L->X[tid] : L->by;
         for (int y = 0; y < my; ++y) {
             double v = z[y];
-            for (int k = 0; k < y; ++k) v -= L->Y[y][k] * z[k];
+            for (int k = ine_band_start(y); k < y; ++k) v -= L->Y[ine_yi(y, k)] * z[k];
             z[y] = v * L->ld[y];
         }
     }
@@ -1092,26 +1160,30 @@ __device__ bool ba_inertial_reduce(const BaPair& q, const BaArgs& a, int n, int 
     return true;
 }
 
-// after the camera solve (dc = s_x[0 .. m)): dy = L^-T (zb - Z^T dc); v_c += dv_c, ba += dba
+// after the camera solve (dc = s_x[0 .. m)): dy = L^-T (zb - Z^T dc); every keyframe's velocity
+// and biases move by its dy
 __device__ void ba_inertial_update(const BaPair& q, const BaArgs& a, int n, int m, const double* s_x, BaIneLds* L) {
 #pragma clang fp contract(fast)
-    const int tid = threadIdx.x, my = 3 * n + 3;
+    const int tid = threadIdx.x, my = TS_BA_INEY * n;
     if (tid < my) {
         double v = L->by[tid];
         for (int i = 0; i < m; ++i) v -= L->X[i][tid] * s_x[i];
         L->by[tid] = v;
     }
     __syncthreads();
-    if (tid < 64) {
-        const int y = tid;
-        double val = y < my ? L->by[y] : 0.0, x = 0.0;
-        for (int i2 = my - 1; i2 >= 0; --i2) {
-            const double xi = readlane_f64(val, i2) * L->ld[i2];
-            if (y == i2) x = xi;
-            if (y < i2) val -= L->Y[i2][y] * xi;
+    if (tid == 0)   // banded back substitution L^T x = by, in place
+        for (int y = my - 1; y >= 0; --y) {
+            double v = L->by[y];
+            const int kend = ine_band_end(y, my);
+            for (int k = y + 1; k < kend; ++k) v -= L->Y[ine_yi(k, y)] * L->by[k];
+            L->by[y] = v * L->ld[y];
         }
-        if (y < 3 * n) q.vel[(size_t)a.order[y / 3] * 3 + y % 3] += x;
-        else if (y < my) q.ine_ba[y - 3 * n] += x;
+    __syncthreads();
+    if (tid < my) {
+        const int c = tid / TS_BA_INEY, k = tid - TS_BA_INEY * c;
+        const int s = a.order[c];
+        if (k < 3) q.vel[(size_t)s * 3 + k] += L->by[tid];
+        else q.bias[(size_t)s * 6 + k - 3] += L->by[tid];
     }
 }
 
@@ -1704,6 +1776,7 @@ __global__ void k_ba_rig_insert(BatchCtx c, BaArgs a) {
     for (int p = 0; p < c.P; ++p) mul4(c.rig_Einv + 16 * p, Tbw, a.st.T + ((size_t)p * a.W + a.slot) * 16);
     for (int e = 0; e < TS_BA_INE; ++e) qb.ine[(size_t)a.slot * TS_BA_INE + e] = a.ine[e];   // the body's inertial factor
     for (int e = 0; e < 3; ++e) qb.vel[(size_t)a.slot * 3 + e] = a.vel0[e];
+    for (int e = 0; e < 6; ++e) qb.bias[(size_t)a.slot * 6 + e] = ba_new_bias(a, qb.bias, e);
 }
 
 // The body system of an iteration from every pair's reduced system (block r = row, thread = column):

@@ -205,7 +205,7 @@ struct tslam_handle {
     std::map<std::pair<int, int64_t>, std::array<double, 10>> ba_imu;   // (pair, keyframe) -> IMU factor
     // (pair, keyframe) -> inertial factor record + initial velocity (tslam_ba_inertial_factor)
     std::map<std::pair<int, int64_t>, std::array<double, TS_BA_INE + 3>> ba_ine;
-    std::vector<std::array<double, 8>> ba_icfg;             // per pair: gravity, bias prior, its weight
+    std::vector<std::array<double, 12>> ba_icfg;            // per pair: gravity, bias priors and weights (BaArgs.icfg)
     std::vector<std::array<uint8_t, TS_BA_MAXW>> ba_ine_slot;   // per pair and slot: carries a factor
     std::vector<BaArgs> ba_solved;   // per pair: the arguments of its last window solve (replays)
     // A pair window's keyframe chain (eviction, gate, tiles, iters x (Schur, reduce-and-solve),
@@ -458,7 +458,7 @@ static int alloc_ba(tslam_handle* h) {
         {(void**)&b.flops, 8},               {(void**)&b.fe_pose, 8 * 2 * (size_t)h->B * h->P * 16},
         {(void**)&b.fe_body, 8 * 2 * (size_t)h->B * 16}, {(void**)&b.imu, 8 * P * W * 10},
         {(void**)&b.kf_assoc, 4 * 2 * (size_t)h->B * h->P * K},
-        {(void**)&b.ine, 8 * P * W * TS_BA_INE}, {(void**)&b.vel, 8 * P * W * 3}, {(void**)&b.ine_ba, 8 * P * 4},
+        {(void**)&b.ine, 8 * P * W * TS_BA_INE}, {(void**)&b.vel, 8 * P * W * 3}, {(void**)&b.bias, 8 * P * W * 6},
     };
     for (const A& a : list) {
         const int rc = dev_alloc(h, a.p, a.bytes);
@@ -471,7 +471,7 @@ static int alloc_ba(tslam_handle* h) {
     HIPCHK(hipMemset(b.lo_o, 0xFF, 4 * P * WK * M));
     HIPCHK(hipMemset(b.remap, 0x7F, 4 * P * K));
     HIPCHK(hipDeviceSynchronize());
-    h->ba_icfg.assign(h->P + 1, std::array<double, 8>{});   // pair windows + a rig's body window
+    h->ba_icfg.assign(h->P + 1, std::array<double, 12>{});   // pair windows + a rig's body window
     h->ba_ine_slot.assign(h->P + 1, std::array<uint8_t, TS_BA_MAXW>{});
     return TSLAM_OK;
 }
@@ -643,7 +643,7 @@ static hipError_t run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, cons
         a.n_order = ba_order(h, -1, a.order);
         h->ba_solved.resize(h->P);
         if (rig) {
-            for (int e = 0; e < 8; ++e) a.icfg[e] = h->ba_icfg[h->P][e];
+            for (int e = 0; e < 12; ++e) a.icfg[e] = h->ba_icfg[h->P][e];
             bool ine = false;
             for (int k = 1; k < a.n_order; ++k) ine = ine || h->ba_ine_slot[h->P][a.order[k]];
             launch_ba_rig_solve(c, a, s, h->ba_timing.ev ? &h->ba_timing : nullptr, ine);
@@ -659,7 +659,7 @@ static hipError_t run_ba(tslam_handle* h, const BatchCtx& c, hipStream_t s, cons
             for (int e = 0; e < 10; ++e) a.imu[e] = v[e];
             for (int e = 0; e < TS_BA_INE; ++e) a.ine[e] = v[10 + e];
             for (int e = 0; e < 3; ++e) a.vel0[e] = v[10 + TS_BA_INE + e];
-            for (int e = 0; e < 8; ++e) a.icfg[e] = h->ba_icfg[p][e];
+            for (int e = 0; e < 12; ++e) a.icfg[e] = h->ba_icfg[p][e];
             // the inertial kernels when a factor links two keyframes of the window (the oldest
             // keyframe's factor points out of it)
             bool ine = false;
@@ -1158,7 +1158,7 @@ int tslam_reset(tslam_handle* h) {
         const size_t P = h->P + 1, W = h->prm.ba_window;
         HIPCHK(hipMemset(h->ba.ine, 0, 8 * P * W * TS_BA_INE));
         HIPCHK(hipMemset(h->ba.vel, 0, 8 * P * W * 3));
-        HIPCHK(hipMemset(h->ba.ine_ba, 0, 8 * P * 4));
+        HIPCHK(hipMemset(h->ba.bias, 0, 8 * P * W * 6));
         h->ba_ine.clear();
         h->ba_imu.clear();
         for (auto& f : h->ba_ine_slot) f.fill(0);
@@ -2964,19 +2964,24 @@ static int ine_pair_check(tslam_handle* h, int pair) {
     return TSLAM_OK;
 }
 
-int tslam_ba_inertial(tslam_handle* h, int pair, const double* gravity, const double* ba_prior, double ba_weight) {
-    if (!h || !gravity || !ba_prior) return fail(TSLAM_EINVAL, "bad argument");
+int tslam_ba_inertial(tslam_handle* h, int pair, const double* gravity, const double* ba_prior, double ba_weight,
+                      const double* bg_prior, double bg_weight) {
+    if (!h || !gravity || !ba_prior || !bg_prior) return fail(TSLAM_EINVAL, "bad argument");
     BA_FLUSH(h);
     if (int rc = ine_pair_check(h, pair); rc != TSLAM_OK) return rc;
-    if (!(ba_weight >= 0.0) || !std::isfinite(ba_weight)) return fail(TSLAM_EINVAL, "ba_weight must be finite and >= 0");
+    if (!(ba_weight >= 0.0) || !std::isfinite(ba_weight) || !(bg_weight >= 0.0) || !std::isfinite(bg_weight))
+        return fail(TSLAM_EINVAL, "bias weights must be finite and >= 0");
     for (int e = 0; e < 3; ++e)
-        if (!std::isfinite(gravity[e]) || !std::isfinite(ba_prior[e])) return fail(TSLAM_EINVAL, "non-finite input");
+        if (!std::isfinite(gravity[e]) || !std::isfinite(ba_prior[e]) || !std::isfinite(bg_prior[e]))
+            return fail(TSLAM_EINVAL, "non-finite input");
     auto& f = h->ba_icfg[pair];
     for (int e = 0; e < 3; ++e) {
         f[e] = gravity[e];
         f[3 + e] = ba_prior[e];
+        f[7 + e] = bg_prior[e];
     }
     f[6] = ba_weight;
+    f[10] = bg_weight;
     return TSLAM_OK;
 }
 
@@ -2985,11 +2990,13 @@ int tslam_ba_inertial_factor(tslam_handle* h, int pair, int64_t frame, const dou
     BA_FLUSH(h);
     if (int rc = ine_pair_check(h, pair); rc != TSLAM_OK) return rc;
     std::array<double, TS_BA_INE + 3> f{};
-    for (int e = 0; e < 30; ++e) {
+    for (int e = 0; e < TS_BA_INE; ++e) {
         if (!std::isfinite(record[e])) return fail(TSLAM_EINVAL, "non-finite factor record");
         f[e] = record[e];
     }
-    if (!(f[27] > 0.0) || !(f[28] >= 0.0) || !(f[29] >= 0.0)) return fail(TSLAM_EINVAL, "dt must be > 0, weights >= 0");
+    if (!(f[27] > 0.0)) return fail(TSLAM_EINVAL, "dt must be > 0");
+    for (int e : {28, 29, 30, 31, 71})
+        if (!(f[e] >= 0.0)) return fail(TSLAM_EINVAL, "weights must be >= 0");
     for (int e = 0; e < 3; ++e) {
         if (!std::isfinite(v0[e])) return fail(TSLAM_EINVAL, "non-finite velocity");
         f[TS_BA_INE + e] = v0[e];
@@ -2998,7 +3005,7 @@ int tslam_ba_inertial_factor(tslam_handle* h, int pair, int64_t frame, const dou
     return TSLAM_OK;
 }
 
-int tslam_ba_read_inertial(tslam_handle* h, int pair, double* velocity, double* ba) {
+int tslam_ba_read_inertial(tslam_handle* h, int pair, double* velocity, double* bias) {
     if (!h) return fail(TSLAM_EINVAL, "null handle");
     BA_FLUSH(h);
     if (int rc = ine_pair_check(h, pair); rc != TSLAM_OK) return rc;
@@ -3006,7 +3013,7 @@ int tslam_ba_read_inertial(tslam_handle* h, int pair, double* velocity, double* 
     if (rc != TSLAM_OK) return rc;
     const size_t W = h->prm.ba_window;
     if (velocity) HIPCHK(hipMemcpy(velocity, h->ba.vel + pair * W * 3, 8 * W * 3, hipMemcpyDeviceToHost));
-    if (ba) HIPCHK(hipMemcpy(ba, h->ba.ine_ba + 4 * pair, 8 * 3, hipMemcpyDeviceToHost));
+    if (bias) HIPCHK(hipMemcpy(bias, h->ba.bias + pair * W * 6, 8 * W * 6, hipMemcpyDeviceToHost));
     return TSLAM_OK;
 }
 

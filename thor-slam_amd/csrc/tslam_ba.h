@@ -21,9 +21,12 @@
 
 #define TS_BA_MAXD 54   // 6 * (TS_BA_MAXW - 1): the reduced camera system without the gauge
 // inertial factor record per slot (oracle/numpy_ba.py INE_N): dv 0-2, dp 3-5, Jv 6-14, Jp 15-23
-// (row-major), ba_lin 24-26, dt 27, wv 28, wp 29 (0 = no factor)
-#define TS_BA_INE 32
-#define TS_BA_MAXY (3 * TS_BA_MAXW + 3)   // velocity + bias unknowns of a window: v_0 .. v_{n-1}, ba
+// (d/d ba, row-major), ba_lin 24-26, dt 27, wv 28 (0 = no factor), wp 29, wR 30, w_ra 31, M 32-40
+// (gyro rotation, camera i points -> camera j), JRe 41-49 (d r_R / d bg), Jvg 50-58, Jpg 59-67
+// (d/d bg), bg_lin 68-70, w_rg 71, 72-79 unused
+#define TS_BA_INE 80
+#define TS_BA_INEY 9   // inertial unknowns per keyframe: velocity, accelerometer bias, gyroscope bias
+#define TS_BA_MAXY (TS_BA_INEY * TS_BA_MAXW)
 #define TS_BA_SPLIT 256 // blocks of the Schur product (32-landmark chunks dealt over them; 8192 landmarks in one round)
 #define TS_BA_TILES 128 // scan tiles of a solve's compaction (landmark + observation tiles)
 // at the largest window and K (n_features <= 8192, tslam_create): landmark tiles W K / 2048 plus
@@ -84,7 +87,7 @@ struct BaStore {
     double* imu;       // [P][W][10] IMU rotation factor per slot: M (row-major 9), weight (0 = none)
     double* ine;       // [P][W][TS_BA_INE] inertial factor per slot (from the previous keyframe)
     double* vel;       // [P][W][3] world velocity of each slot's camera
-    double* ine_ba;    // [P][4] the window's accelerometer bias (IMU axes)
+    double* bias;      // [P][W][6] accelerometer and gyroscope biases (IMU axes) per slot
 };
 
 struct BaArgs {
@@ -107,7 +110,8 @@ struct BaArgs {
     double imu[10];             // insert: the keyframe's IMU rotation factor (M 9, weight; 0 = none)
     double ine[TS_BA_INE];      // insert: the keyframe's inertial factor (wv = 0: none)
     double vel0[3];             // insert: its camera's initial world velocity
-    double icfg[8];             // solve: world gravity 0-2, accelerometer-bias prior 3-5, its weight 6
+    double icfg[12];            // solve: world gravity 0-2, priors on the oldest keyframe's biases:
+                                // accelerometer 3-5 with weight 6, gyroscope 7-9 with weight 10
 };
 
 // Per-pair view (the scratch pointers are shared).
@@ -128,7 +132,7 @@ struct BaPair {
     uint8_t* keep;
     double *lo_uvd, *lo_W, *Xc, *obs_Vg, *lm_L, *lm_gp, *part, *C, *cam_U, *dc, *flops;
     double* imu;
-    double *ine, *vel, *ine_ba;
+    double *ine, *vel, *bias;
 };
 
 __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, int p) {
@@ -161,7 +165,7 @@ __device__ __forceinline__ BaPair ba_pair(const BatchCtx& c, const BaArgs& a, in
     q.imu = s.imu + p * W * 10;
     q.ine = s.ine + p * W * TS_BA_INE;
     q.vel = s.vel + p * W * 3;
-    q.ine_ba = s.ine_ba + 4 * p;
+    q.bias = s.bias + p * W * 6;
     return q;
 }
 

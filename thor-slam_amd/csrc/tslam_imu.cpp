@@ -434,12 +434,30 @@ int tslam_imu_gravity(const tslam_imu* f, double* g) {
 // w = Ri (gyro - bg), alpha = (w - w_prev) / dt, the camera's specific force
 // a = Ri (accel - ba) - w x (w x r) - alpha x r; dp += dv dt + dR a dt^2 / 2,
 // Jp += Jv dt - dR Ri dt^2 / 2, dv += dR a dt, Jv -= dR Ri dt, dR <- dR exp([w dt]x).
+// right Jacobian of SO(3) (oracle numpy_ba._jr_so3): I - (1 - cos t) / t^2 [w]x + (t - sin t) / t^3 [w]x^2
+static void jr_so3(V3 w, double* J) {
+    const double t2 = w.x * w.x + w.y * w.y + w.z * w.z, th = std::sqrt(t2);
+    double a, b;
+    if (th < 1e-4) {
+        a = 0.5;
+        b = 1.0 / 6.0;
+    } else {
+        a = (1.0 - std::cos(th)) / t2;
+        b = (th - std::sin(th)) / (t2 * th);
+    }
+    const double K[9] = {0.0, -w.z, w.y, w.z, 0.0, -w.x, -w.y, w.x, 0.0};
+    double K2[9];
+    mm(K, K, K2);
+    for (int e = 0; e < 9; ++e) J[e] = ((e % 4) == 0 ? 1.0 : 0.0) - a * K[e] + b * K2[e];
+}
+
 int tslam_imu_preintegrate(const tslam_imu* f, int n, const double* dt, const double* gyro, const double* accel,
                            const double* bg, const double* ba, const double* w_prev, const double* frame_R_imu,
-                           const double* lever, double v_floor, double p_floor, double* record) {
+                           const double* lever, double v_floor, double p_floor, double r_floor, double ba_floor,
+                           double bg_floor, double* record) {
     if (!f || n < 1 || !dt || !gyro || !accel || !bg || !ba || !record)
         return tslam_internal_fail(TSLAM_EINVAL, "tslam_imu_preintegrate: null argument or n < 1");
-    double dR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, Jv[9] = {}, Jp[9] = {};
+    double dR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, Jv[9] = {}, Jp[9] = {}, Jvg[9] = {}, Jpg[9] = {}, JR[9] = {};
     V3 dv{0, 0, 0}, dp{0, 0, 0};
     double T = 0.0;
     bool have_prev = w_prev != nullptr;
@@ -455,19 +473,32 @@ int tslam_imu_preintegrate(const tslam_imu* f, int n, const double* dt, const do
         const V3 a = mv(Ri, v3(accel + 3 * k) - bav) - cross(w, cross(w, r)) - cross(al, r);
         const V3 Ra = mv(dR, a);
         mm(dR, Ri, dRRi);
+        // dR [a]x JR: the gyroscope bias's first-order effect on the specific force's rotation
+        const double Ka[9] = {0.0, -a.z, a.y, a.z, 0.0, -a.x, -a.y, a.x, 0.0};
+        double KJ[9], RaJ[9];
+        mm(Ka, JR, KJ);
+        mm(dR, KJ, RaJ);
         dp = dp + dv * h + 0.5 * Ra * h * h;
         for (int e = 0; e < 9; ++e) Jp[e] = Jp[e] + Jv[e] * h - 0.5 * dRRi[e] * h * h;
+        for (int e = 0; e < 9; ++e) Jpg[e] = Jpg[e] + Jvg[e] * h - 0.5 * RaJ[e] * h * h;
         dv = dv + Ra * h;
         for (int e = 0; e < 9; ++e) Jv[e] = Jv[e] - dRRi[e] * h;
-        double E[9], nR[9];
+        for (int e = 0; e < 9; ++e) Jvg[e] = Jvg[e] - RaJ[e] * h;
+        double E[9], nR[9], Jr[9], JrRi[9], nJ[9];
         rotvec_to_matrix(w * h, E);
+        jr_so3(w * h, Jr);
+        mm(Jr, Ri, JrRi);
+        for (int i = 0; i < 3; ++i)   // JR <- E^T JR - Jr Ri h
+            for (int j = 0; j < 3; ++j)
+                nJ[3 * i + j] = (E[i] * JR[j] + E[3 + i] * JR[3 + j] + E[6 + i] * JR[6 + j]) - JrRi[3 * i + j] * h;
+        std::memcpy(JR, nJ, sizeof JR);
         mm(dR, E, nR);
         std::memcpy(dR, nR, sizeof dR);
         T += h;
         wp = w;
         have_prev = true;
     }
-    std::memset(record, 0, 32 * sizeof(double));
+    std::memset(record, 0, TSLAM_BA_INE_RECORD * sizeof(double));
     put(dv, record);
     put(dp, record + 3);
     std::memcpy(record + 6, Jv, sizeof Jv);
@@ -476,6 +507,15 @@ int tslam_imu_preintegrate(const tslam_imu* f, int n, const double* dt, const do
     record[27] = T;
     record[28] = 1.0 / (f->na * f->na * T + v_floor * v_floor);
     record[29] = 1.0 / (f->na * f->na * T * T * T / 3.0 + p_floor * p_floor);
+    record[30] = f->ng > 0.0 ? 1.0 / (f->ng * f->ng * T + r_floor * r_floor) : 0.0;
+    record[31] = f->rw > 0.0 ? 1.0 / (f->rw * f->rw * T + ba_floor * ba_floor) : 0.0;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) record[32 + 3 * i + j] = dR[3 * j + i];   // M = dR^T
+    mm(dR, JR, record + 41);                                                  // JRe = dR JR
+    std::memcpy(record + 50, Jvg, sizeof Jvg);
+    std::memcpy(record + 59, Jpg, sizeof Jpg);
+    put(bgv, record + 68);
+    record[71] = f->rwg > 0.0 ? 1.0 / (f->rwg * f->rwg * T + bg_floor * bg_floor) : 0.0;
     return TSLAM_OK;
 }
 

@@ -31,6 +31,7 @@ KERNELS = {
     "rectify_pyramid": 10, "detect": 11, "select": 12, "describe": 13,
     "match": 14, "match_refine": 15, "pose": 16, "chain": 17,
 }
+INE_RECORD = 80   # TSLAM_BA_INE_RECORD: doubles of an inertial factor record
 RIG_KERNEL = 18   # rig pose (+ chain; sharded: the range's rig pose only)
 POSE_SOLVE_KERNEL = 19   # P3P + RANSAC + refine on injected correspondences (parity tests)
 TRANSPORT = {"rccl": 0, "copy": 1}   # tslam_group_create
@@ -127,7 +128,7 @@ _SIGNATURES = {
     "tslam_imu_vision_only": (ctypes.c_int, [_P, _P, ctypes.c_double, _P, _P, _P]),
     "tslam_imu_gravity": (ctypes.c_int, [_P, _P]),
     "tslam_imu_preintegrate": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, ctypes.c_double,
-                                              ctypes.c_double, _P]),
+                                              ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, _P]),
     "tslam_last_error": (ctypes.c_char_p, []),
     "tslam_abi_version": (ctypes.c_int, []),
     "tslam_create": (ctypes.c_int, [ctypes.POINTER(StereoDesc), ctypes.POINTER(Params), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
@@ -202,7 +203,8 @@ _SIGNATURES = {
                                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "tslam_ba_split_solve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "tslam_ba_defer": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
-    "tslam_ba_inertial": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double]),
+    "tslam_ba_inertial": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double,
+                                         ctypes.c_void_p, ctypes.c_double]),
     "tslam_ba_inertial_factor": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
                                                 ctypes.c_void_p]),
     "tslam_ba_read_inertial": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
@@ -917,25 +919,31 @@ class Handle:
                                               ctypes.byref(fl)))
         return {"us": us.value, "flops": fl.value, "reps": int(reps)}
 
-    def ba_inertial(self, gravity, ba_prior, ba_weight: float, pair: int = 0) -> None:
-        """World gravity, accelerometer-bias prior and its weight for pair's window (tslam.h)."""
+    def ba_inertial(self, gravity, ba_prior, ba_weight: float, bg_prior=None, bg_weight: float = 0.0,
+                    pair: int = 0) -> None:
+        """World gravity and the priors (value, weight) on the oldest window keyframe's
+        accelerometer and gyroscope biases for pair's window (tslam.h)."""
         g = np.ascontiguousarray(gravity, dtype=np.float64).reshape(3)
         b = np.ascontiguousarray(ba_prior, dtype=np.float64).reshape(3)
-        _check(self.lib.tslam_ba_inertial(self.h, int(pair), g.ctypes.data, b.ctypes.data, float(ba_weight)))
+        bg = np.ascontiguousarray(np.zeros(3) if bg_prior is None else bg_prior, dtype=np.float64).reshape(3)
+        _check(self.lib.tslam_ba_inertial(self.h, int(pair), g.ctypes.data, b.ctypes.data, float(ba_weight),
+                                          bg.ctypes.data, float(bg_weight)))
 
     def ba_inertial_factor(self, frame: int, record, v0, pair: int = 0) -> None:
-        """Keyframe ``frame``'s inertial factor record (30 doubles, oracle INE_N layout) and initial
-        velocity, before its batch is submitted."""
-        r = np.ascontiguousarray(np.asarray(record, dtype=np.float64).reshape(-1)[:30])
+        """Keyframe ``frame``'s inertial factor record (INE_RECORD doubles, oracle INE_N layout) and
+        initial velocity, before its batch is submitted."""
+        r = np.zeros(INE_RECORD)
+        src = np.asarray(record, dtype=np.float64).reshape(-1)[:INE_RECORD]
+        r[:src.size] = src
         v = np.ascontiguousarray(v0, dtype=np.float64).reshape(3)
         _check(self.lib.tslam_ba_inertial_factor(self.h, int(pair), int(frame), r.ctypes.data, v.ctypes.data))
 
     def ba_read_inertial(self, pair: int = 0) -> dict:
-        """Velocities by slot [W][3] and the window's accelerometer bias [3] (synchronises)."""
+        """Velocities [W][3] and accelerometer / gyroscope biases [W][6] by slot (synchronises)."""
         vel = np.zeros((self.cfg.ba_window, 3))
-        ba = np.zeros(3)
-        _check(self.lib.tslam_ba_read_inertial(self.h, int(pair), vel.ctypes.data, ba.ctypes.data))
-        return {"vel": vel, "ba": ba}
+        bias = np.zeros((self.cfg.ba_window, 6))
+        _check(self.lib.tslam_ba_read_inertial(self.h, int(pair), vel.ctypes.data, bias.ctypes.data))
+        return {"vel": vel, "bias": bias}
 
     def ba_defer(self, defer: bool) -> None:
         """``tslam_ba_defer``: a BA stage on its own stream is enqueued at the next flush point

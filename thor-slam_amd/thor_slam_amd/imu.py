@@ -218,9 +218,10 @@ class ImuPropagator:
 
     def preintegrate(self, samples: list, bg: np.ndarray, ba: np.ndarray, w_prev: np.ndarray | None = None,
                      v_floor: float = 1e-2, p_floor: float = 1e-3, frame_R_imu: np.ndarray | None = None,
-                     lever: np.ndarray | None = None) -> np.ndarray:
-        """The local BA's inertial factor record (32 doubles, tslam_ba_inertial_factor) of the
-        frame intervals ``samples`` = [(dt, gyro, accel)] between two keyframes, in the filter's
+                     lever: np.ndarray | None = None, r_floor: float = 1e-3, ba_floor: float = 1e-3,
+                     bg_floor: float = 1e-3) -> np.ndarray:
+        """The local BA's inertial factor record (INE_RECORD doubles, tslam_ba_inertial_factor) of
+        the frame intervals ``samples`` = [(dt, gyro, accel)] between two keyframes, in the filter's
         camera or (``frame_R_imu``, ``lever``) another rigid frame (tslam_imu_preintegrate)."""
         n = len(samples)
         dt = np.ascontiguousarray([float(d) for d, _, _ in samples], dtype=np.float64)
@@ -231,12 +232,13 @@ class ImuPropagator:
         wp = None if w_prev is None else np.ascontiguousarray(w_prev, dtype=np.float64).reshape(3)
         fr = None if frame_R_imu is None else np.ascontiguousarray(frame_R_imu, dtype=np.float64).reshape(9)
         lv = None if lever is None else np.ascontiguousarray(lever, dtype=np.float64).reshape(3)
-        out = np.zeros(32)
+        out = np.zeros(_lib.INE_RECORD)
         _lib._check(self.lib.tslam_imu_preintegrate(self._f, n, dt.ctypes.data, gy.ctypes.data, ac.ctypes.data,
                                                     bgv.ctypes.data, bav.ctypes.data, None if wp is None else wp.ctypes.data,
                                                     None if fr is None else fr.ctypes.data,
                                                     None if lv is None else lv.ctypes.data,
-                                                    float(v_floor), float(p_floor), out.ctypes.data))
+                                                    float(v_floor), float(p_floor), float(r_floor), float(ba_floor),
+                                                    float(bg_floor), out.ctypes.data))
         return out
 
     def absorb(self, samples: list, status: np.ndarray, t_rel: np.ndarray, cov: np.ndarray) -> None:

@@ -54,13 +54,19 @@ class HipSlamConfig(SlamConfig):
     # lever arm, a translation prior, and IMU chaining through visual dropouts (None = with
     # imu_fusion)
     imu_accel: bool | None = None
-    # ... and, with local BA on one stereo pair, the tightly coupled inertial factors: the
-    # accelerometer preintegrated between BA keyframes, a velocity per keyframe and the window's
-    # accelerometer bias inside the BA (oracle/numpy_ba.py inertial_terms); floors of their
-    # weights' standard deviations (m/s, m)
+    # ... and, with local BA, the tightly coupled inertial factors: the IMU preintegrated between
+    # BA keyframes, a velocity and accelerometer / gyroscope biases per keyframe (tied by the bias
+    # random walks) inside the BA (oracle/numpy_ba.py inertial_system); floors of the velocity and
+    # position weights' standard deviations (m/s, m)
     ba_inertial: bool = True
     ba_inertial_v_floor: float = 1e-2
     ba_inertial_p_floor: float = 1e-3
+    # the record's gyro-rotation rows and the bias random walks between window keyframes (weights
+    # from the gyroscope noise density and both random walks of launch/thor_visual_slam.launch.py:
+    # 50-53,88-93, floored: rad, m/s^2, rad/s)
+    ba_inertial_r_floor: float = 1e-3
+    ba_inertial_ba_floor: float = 1e-3
+    ba_inertial_bg_floor: float = 1e-3
     # noise model, launch/thor_visual_slam.launch.py:82-93 (calibrated on a 2.5 h rosbag, :97-104)
     gyroscope_noise_density: float = 8.27e-5        # rad/s/sqrt(Hz)   (launch:82)
     accelerometer_noise_density: float = 2.553e-3   # m/s^2/sqrt(Hz)   (launch:85)

@@ -835,6 +835,8 @@ class HipSlamEngine(SlamEngine):
         cfg = self._config
         if cfg.ba_window <= 0 or len(self._pairs) != 1:
             return
+        if self._ine_on():   # the inertial records carry the gyro rotation (and the gyroscope bias)
+            return
         g = self._handle.frames_done
         for k, st in enumerate(steps):
             gk = g + k
@@ -849,6 +851,12 @@ class HipSlamEngine(SlamEngine):
                     self._handle.ba_imu_factor(gk, acc[0], 1.0 / acc[1])
                 self._kf_imu = (np.eye(3), 0.0, gk + 1)
 
+    def _ine_on(self) -> bool:
+        """The local BA takes tightly coupled inertial factors (accelerometer leg, filter started)."""
+        imu = self._imu
+        return (self._config.ba_window > 0 and bool(self._config.ba_inertial) and imu is not None and bool(imu.accel)
+                and bool(imu.ready))
+
     def _ba_inertial_factors(self, steps: list, samples: list) -> None:
         """The local BA's tightly coupled inertial factors (accelerometer leg): the frame
         intervals' samples since the last BA keyframe are preintegrated with the filter's current
@@ -859,14 +867,16 @@ class HipSlamEngine(SlamEngine):
         body (base_link) frame of its body window (pair = n_pairs), the filter's camera-0 vectors
         rotated into it (the velocity only seeds the solve)."""
         cfg, imu = self._config, self._imu
-        if cfg.ba_window <= 0 or not cfg.ba_inertial or not imu.accel or not imu.ready:
+        if not self._ine_on():
             return
         rig = len(self._pairs) > 1
         pair = len(self._pairs) if rig else 0
         R0 = self._base_T_rects[0][:3, :3]   # base_R_rect0: camera-0 vectors into the body world
         st = imu.st
         g = imu.gravity()
-        self._handle.ba_inertial(R0 @ g if rig else g, st.ba, 1.0 / max(st.var_b, 1e-12), pair=pair)
+        self._handle.ba_inertial(R0 @ g if rig else g, st.ba, 1.0 / max(st.var_b, 1e-12), st.bg,
+                                 1.0 / max(st.var_g, 1e-12), pair=pair)
+        floors = dict(r_floor=cfg.ba_inertial_r_floor, ba_floor=cfg.ba_inertial_ba_floor, bg_floor=cfg.ba_inertial_bg_floor)
         g = self._handle.frames_done
         for k, (step, smp) in enumerate(zip(steps, samples)):
             gk = g + k
@@ -882,11 +892,12 @@ class HipSlamEngine(SlamEngine):
                     if rig:
                         rec = imu.preintegrate(acc[0], st.bg, st.ba, None if acc[2] is None else R0 @ acc[2],
                                                cfg.ba_inertial_v_floor, cfg.ba_inertial_p_floor,
-                                               frame_R_imu=self._base_T_imu[:3, :3], lever=self._base_T_imu[:3, 3])
+                                               frame_R_imu=self._base_T_imu[:3, :3], lever=self._base_T_imu[:3, 3],
+                                               **floors)
                         self._handle.ba_inertial_factor(gk, rec, R0 @ step.v1, pair=pair)
                     else:
                         rec = imu.preintegrate(acc[0], st.bg, st.ba, acc[2], cfg.ba_inertial_v_floor,
-                                               cfg.ba_inertial_p_floor)
+                                               cfg.ba_inertial_p_floor, **floors)
                         self._handle.ba_inertial_factor(gk, rec, step.v1)
                 self._kf_ine = ([], gk + 1, None if step is None else step.w.copy())
 
