@@ -1190,9 +1190,12 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
         for h in hs:
             if P > 1:
                 h.set_rig(E)
+        pairs = bool(args.pair_split)
+        if pairs and (c5 or S != 1):
+            raise SystemExit("--pair-split shards a stereo rig with one camera stream per GPU")
         if rehearse:
             grp = HandleGroup(hs, "copy")
-            hs[0].shard_options(pipeline=True)
+            hs[0].shard_options(pipeline=True, pairs=pairs)
             step = lambda s, timer=None: grp.submit([batch_of(q, s).data_ptr() for q in range(world)], B,  # noqa: E731
                                                     [stream.cuda_stream] * world)
         else:
@@ -1200,7 +1203,7 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
             if world > 1:
                 dist.broadcast_object_list(uid, src=0)
             hs[0].comm_init(uid[0], rank, world)
-            hs[0].shard_options(pipeline=True)   # batch s+1's front end beside batch s's back end
+            hs[0].shard_options(pipeline=True, pairs=pairs)   # batch s+1's front end beside batch s's back end
             step = lambda s, timer=None: hs[0].submit_sharded(batch_of(0, s).data_ptr(), B, stream.cuda_stream)  # noqa: E731
         drain = torch.cuda.synchronize
     for s in range(args.warmup):
@@ -1211,7 +1214,7 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
     torch.cuda.synchronize()
     timer = StageTimer()
     if args.driver == "library":
-        hs[0].shard_options(profile=True, pipeline=True)
+        hs[0].shard_options(profile=True, pipeline=True, pairs=bool(args.pair_split))
     t0 = time.perf_counter()
     for k in range(args.steps):
         s = args.warmup + k
@@ -1232,7 +1235,7 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
         if P > 1:
             res["rig"] = hs[0].read_rig_poses(B)
         sb, pr = hs[0].exchange_sizes()
-        pb = hs[0].pair_block_bytes() if c5 else 0
+        pb = hs[0].pair_block_bytes() if (c5 or args.pair_split) else 0
     else:
         res = rig.read()
         per_kernel_us = timer.mean_us()
@@ -1258,6 +1261,22 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
     if c5:
         xbytes = {"pair_blocks": (world - 1) * plan.frames_per_rank * S * pb, "pose_records": plan.frames_per_rank * pr,
                   "pair_block_bytes": pb, "pose_record_bytes": pr}
+        xbytes["largest_to_one_peer"] = plan.frames_per_rank * S * pb
+    elif args.driver == "library" and args.pair_split:
+        # rank 0 (pair 0, first half) sends its camera of the partner's half + the frame before it
+        # to the partner, and its pair's blocks of each rig range of the same half to that range's
+        # owner (world / 2 - 1 ranks)
+        half = B - B // 2
+        xbytes = {
+            "raw_images": (half + 1) * width * height,
+            "stream_blocks": (half + 1) * sb,
+            "pair_blocks": (world // 2 - 1) * plan.frames_per_rank * pb if P > 1 else 0,
+            "pose_records": plan.frames_per_rank * pr,
+            "stream_block_bytes": sb,
+            "pair_block_bytes": pb,
+            "pose_record_bytes": pr,
+        }
+        xbytes["largest_to_one_peer"] = (half + 1) * (width * height + sb)   # the partner link
     else:
         xbytes = {  # what one rank sends per step
             "raw_images": ((world - 1) * plan.recv_frames if alltoall else (B + 1)) * S * width * height,
@@ -1266,7 +1285,9 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
             "stream_block_bytes": sb,
             "pose_record_bytes": pr,
         }
-    xbytes["total_sent"] = sum(v for k_, v in xbytes.items() if not k_.endswith("_bytes"))
+        if alltoall:
+            xbytes["largest_to_one_peer"] = plan.recv_frames * S * (width * height + sb)
+    xbytes["total_sent"] = sum(v for k_, v in xbytes.items() if not k_.endswith("_bytes") and k_ != "largest_to_one_peer")
     if args.driver == "library":
         if rehearse:
             grp.close()
@@ -1306,6 +1327,11 @@ def run_sharded(args, world: int, rank: int, dev_index: int) -> dict:
             "parallelism": (f"{S} RGB-D camera(s) per GPU x{world}: each GPU tracks its cameras over the batch, "
                             f"RCCL all-to-all of pair blocks (pose + correspondences), rig pose on each GPU's "
                             f"{plan.frames_per_rank}-frame range, RCCL all-gather of pose records" if c5 else
+                            f"1 camera stream per GPU x{world}, pair split: front end per stream, RCCL send/recv of "
+                            f"raw images + keypoint/descriptor stream blocks to the pair partner only, the pair's back "
+                            f"end on each GPU's half of the batch, pair blocks to the rig-range owners of the same "
+                            f"half, rig pose on each GPU's {plan.frames_per_rank}-frame range, RCCL all-gather of "
+                            f"pose records" if (args.driver == "library" and args.pair_split) else
                             f"{S} camera stream(s) per GPU x{world}: front end per stream, RCCL "
                             f"{'all-to-all' if alltoall else 'all-gather'} of raw images + keypoint/descriptor "
                             f"stream blocks, per-pair back end + rig pose on each GPU's {plan.frames_per_rank}-frame "
@@ -1403,6 +1429,9 @@ def main() -> None:
     ap.add_argument("--transport", choices=["rccl", "copy"], default="rccl",
                     help="copy: all --gpus ranks in this process on one GPU with device copies (tslam_group_create; "
                          "a rehearsal of the library driver's exchange on a one-GPU box)")
+    ap.add_argument("--pair-split", type=int, default=0,
+                    help="sharded stereo rig, one camera per GPU: TSLAM_SHARD_PAIRS (each rank solves its camera's "
+                         "pair over half the batch; images go to the partner only, pair blocks to the rig ranges)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="1: front and back kernels on two streams (batch s+1's front overlaps batch s's back)")
     ap.add_argument("--front-cu-reserve", type=int, default=-1,

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define TSLAM_ABI_VERSION 19
+#define TSLAM_ABI_VERSION 20
 
 #define TSLAM_OK 0
 #define TSLAM_EINVAL (-1)
@@ -407,8 +407,9 @@ int tslam_read_rig_poses(tslam_handle* h, int max_frames, double* T_rel, double*
  * all-to-all -> tslam_unpack_pairs (the peers' cameras, its own range); KERNEL_RIG solves the rig
  * pose of its range; then pack_poses -> all-gather -> unpack_poses -> KERNEL_CHAIN as above. */
 int tslam_set_shard(tslam_handle* h, int cam_lo, int cam_hi, int rank, int world);
-/* Bytes of one pair block (RGB-D sharding; per batch frame and camera: pose f64[68], stats i32[8],
- * correspondences f64[K][8]). */
+/* Bytes of one pair block (RGB-D sharding and the stereo pair split; per batch frame and pair:
+ * pose f64[68], stats i32[8], correspondences f64[K][5] — the columns the rig pose reads:
+ * X, Y, Z, cx - u, cy - v; rows past stats[1] are not copied). */
 int tslam_pair_block_bytes(tslam_handle* h, int64_t* bytes);
 /* Pair blocks of batch frames f0 .. f0+n_frames-1 x pairs [pair_lo, pair_hi) (frame-major) to / from
  * device memory, inside a batch (pack after POSE, unpack before KERNEL_RIG). */
@@ -488,7 +489,14 @@ int tslam_submit_sharded(tslam_handle* h, const uint8_t* images, int n_frames, v
  *   TSLAM_SHARD_SOLO     (profiling aid, groups only) rank 0 alone runs its work and every exchange
  *                        is skipped (its receive buffers keep the last full batch's data): the
  *                        per-GPU step of one rank of an N-GPU node with the exchange hidden, timed
- *                        on one GPU.  Results are not meaningful; reset the handles afterwards.
+ *                        on one GPU.  Results are not meaningful; reset the handles afterwards;
+ *   TSLAM_SHARD_PAIRS    pair split of a stereo rig with one camera per rank (world = cameras, no
+ *                        local BA / gather): rank r's back end solves pair r/2 over half r&1 of
+ *                        the batch, so its raw images and stream blocks go to its partner r^1
+ *                        only, and rank r's rig range (range (r&1)*world/2 + r/2 of the world-way
+ *                        split, inside its half) collects the other pairs' pair blocks (pose,
+ *                        stats, correspondences) from the ranks of its half before the rig pose.
+ *                        Every rank of the rig must set it alike.  Results are identical.
  * Setting options waits for the work enqueued so far. */
 #define TSLAM_SHARD_GATHER 1
 #define TSLAM_SHARD_RESULTS 2
@@ -496,12 +504,14 @@ int tslam_submit_sharded(tslam_handle* h, const uint8_t* images, int n_frames, v
 #define TSLAM_SHARD_SERIAL 8
 #define TSLAM_SHARD_PIPELINE 16
 #define TSLAM_SHARD_SOLO 32
+#define TSLAM_SHARD_PAIRS 64
 enum tslam_segment {
     TSLAM_SEG_RECTIFY = 0, TSLAM_SEG_DETECT, TSLAM_SEG_SELECT, TSLAM_SEG_DESCRIBE, TSLAM_SEG_PACK,
     TSLAM_SEG_EXCHANGE_WAIT,   /* front end done -> the peers' images and stream blocks landed */
     TSLAM_SEG_IMPORT, TSLAM_SEG_MATCH, TSLAM_SEG_MATCH_REFINE, TSLAM_SEG_POSE, TSLAM_SEG_RIG,
     TSLAM_SEG_STATE,           /* state blocks packed (senders) / unpacked (rank 0) */
     TSLAM_SEG_POSE_GATHER, TSLAM_SEG_CHAIN, TSLAM_SEG_BA,
+    TSLAM_SEG_PAIR_BLOCKS,     /* pair split: pair blocks packed, exchanged, unpacked */
     TSLAM_SEG_COUNT
 };
 int tslam_shard_options(tslam_handle* h, int flags);

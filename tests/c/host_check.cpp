@@ -183,6 +183,19 @@ static int cmd_ranges() {
                     ++checked;
                 }
                 if (prev_hi != n || mx - mn > 1) return die("ranges: uneven", n);
+                // pair split (even world = cameras): rig_rank inverts rig_slot, and every rank's rig
+                // range lies inside its pair's half, which fits the stereo receive buffers
+                if (world % 2 || world < 2) continue;
+                for (int r = 0; r < world; ++r) {
+                    const int sl = rig_slot(r, world, 1);
+                    if (sl < 0 || sl >= world || rig_rank(sl, world, 1) != r) return die("pairs: slot", r);
+                    int lo, hi, hlo, hhi;
+                    peer_range(sl, n, world, &lo, &hi);
+                    peer_range(r & 1, n, 2, &hlo, &hhi);
+                    if (hi > lo && (lo < hlo || hi > hhi)) return die("pairs: rig range outside the half", r);
+                    if ((hhi > hlo ? hhi - hlo + 1 : 0) > world * cap) return die("pairs: half vs receive slots", r);
+                    ++checked;
+                }
             }
         }
     }

@@ -6,7 +6,9 @@
   disparities, left keypoints and descriptors as one handle's does, and rank 0 solves the local
   BA window — bit-identical to one handle fed all cameras;
 * pinned result slots (TSLAM_SHARD_RESULTS: tslam_poll_batch on a sharded handle) and the
-  per-segment HIP-event timing (TSLAM_SHARD_PROFILE).
+  per-segment HIP-event timing (TSLAM_SHARD_PROFILE);
+* the pair split (TSLAM_SHARD_PAIRS): each rank solves its camera's pair over half the batch with
+  the partner's images only, and the rig ranges gather pair blocks — identical results.
 
 Ranks share this GPU through the COPY transport (the same packing, ordering and buffers as RCCL);
 the RCCL transport runs at world 1 (one device on the test box)."""
@@ -46,17 +48,17 @@ def _ring(h, g, K, P):
     return out
 
 
-def _run(sc, cfg, sizes, world, transport="copy", max_batch=8, options=None, check=None):
+def _run(sc, cfg, sizes, world, transport="copy", max_batch=8, options=None, check=None, rig=True):
     """The unsharded handle and a `world`-rank group fed the same batches; check(b, h1, hs, n)."""
     import torch
 
     from thor_slam_amd._lib import Handle, HandleGroup
 
     h1 = Handle(sc["rects"], cfg, max_batch=max_batch)
-    h1.set_rig(sc["E"])
     hs = [Handle(sc["rects"], cfg, max_batch=max_batch) for _ in range(world)]
-    for h in hs:
-        h.set_rig(sc["E"])
+    if rig:
+        for h in hs + [h1]:
+            h.set_rig(sc["E"])
     grp = HandleGroup(hs, transport)
     if options:
         hs[0].shard_options(**options)
@@ -274,6 +276,95 @@ def test_solo_profiles_rank0_only():
         t0, nb0 = hs[0].shard_timing()
         assert nb0 == 2 and t0["detect"] > 0.0 and t0["pose"] > 0.0 and t0["pose_gather"] >= 0.0
         assert hs[1].shard_timing()[1] == 0
+    finally:
+        grp.close()
+        for h in hs:
+            h.close()
+
+
+def _pair_split_identical(names, world, sizes, rig=True, options=None):
+    sc = rig_scene(names, sum(sizes))
+
+    def check(b, h1, hs, n):
+        import torch
+
+        torch.cuda.synchronize()   # every rank on this device: pipelined batches have finished
+        if options and options.get("results"):
+            for r, h in enumerate(hs):
+                res = h.poll_batch(block=True)
+                assert res is not None and res["n"] == n, (b, r)
+        want = _poses(h1, n) if rig else {"pairs": h1.read_poses(n)}
+        for r, h in enumerate(hs):
+            got = _poses(h, n) if rig else {"pairs": h.read_poses(n)}
+            for part in want:
+                for k in ("T_rel", "T_abs", "cov", "stats"):
+                    np.testing.assert_array_equal(got[part][k], want[part][k],
+                                                  err_msg=f"batch {b} ({n} frames) rank {r} {part}.{k}")
+
+    _run(sc, HipSlamConfig(), sizes, world, options={"pairs": True, **(options or {})}, check=check, rig=rig)
+
+
+@pytest.mark.parametrize("names,world,rig", [(TWO[:1], 2, False), (TWO[:1], 2, True), (TWO, 4, True)])
+def test_pair_split_identical(names, world, rig):
+    """TSLAM_SHARD_PAIRS: rank r solves pair r/2 over half r&1 of each batch from its partner's
+    images and stream blocks only, the rig ranges gather the other pairs' pair blocks (pose,
+    stats, the 5 correspondence columns the rig pose reads).  Batches of 3, 8, 1, 2, 5 frames
+    (uneven and empty halves, frame -1 from the previous batch): every rank's pair and rig poses,
+    covariances and statistics equal the unsharded handle's, bit for bit."""
+    _pair_split_identical(names, world, [3, 8, 1, 2, 5], rig=rig)
+
+
+def test_pair_split_pipelined_results_identical():
+    """The pair split with TSLAM_SHARD_PIPELINE + TSLAM_SHARD_RESULTS (4 ranks, 2 pairs): batches
+    polled from the result slots equal the unsharded handle's."""
+    _pair_split_identical(TWO, 4, [8, 8, 3], options={"pipeline": True, "results": True})
+
+
+@pytest.mark.slow
+def test_pair_split_c3_eight_ranks_identical():
+    """C3 (4 pairs, 8 streams) over 8 ranks with the pair split: rig poses identical."""
+    _pair_split_identical(C3_SOURCES, 8, [8, 5, 8])
+
+
+def test_pair_split_options_checked():
+    """TSLAM_SHARD_PAIRS needs one camera per rank and no state gather / local BA; the profile
+    reports the pair-block segment."""
+    import torch
+
+    from thor_slam_amd._lib import Handle, HandleGroup
+
+    sc = rig_scene(TWO, 8)
+    hs = [Handle(sc["rects"], HipSlamConfig(), max_batch=8) for _ in range(2)]   # 2 cameras per rank
+    grp = HandleGroup(hs, "copy")
+    try:
+        with pytest.raises(RuntimeError, match="one camera per rank"):
+            hs[0].shard_options(pairs=True)
+    finally:
+        grp.close()
+        for h in hs:
+            h.close()
+    hs = [Handle(sc["rects"], HipSlamConfig(ba_window=10), max_batch=8) for _ in range(4)]
+    grp = HandleGroup(hs, "copy")
+    try:
+        with pytest.raises(RuntimeError, match="without the state gather"):
+            hs[0].shard_options(pairs=True)
+    finally:
+        grp.close()
+        for h in hs:
+            h.close()
+    hs = [Handle(sc["rects"], HipSlamConfig(), max_batch=8) for _ in range(4)]
+    for h in hs:
+        h.set_rig(sc["E"])
+    grp = HandleGroup(hs, "copy")
+    dev = torch.from_numpy(np.ascontiguousarray(sc["frames"])).cuda()
+    parts = [dev[:, r:r + 1].contiguous() for r in range(4)]
+    try:
+        hs[0].shard_options(pairs=True, profile=True)
+        grp.submit([p[0].data_ptr() for p in parts], 8)
+        torch.cuda.synchronize()
+        for r in range(4):
+            t, nb = hs[r].shard_timing()
+            assert nb == 1 and t["pair_blocks"] > 0.0 and t["rig"] > 0.0 and t["import"] > 0.0, (r, t)
     finally:
         grp.close()
         for h in hs:

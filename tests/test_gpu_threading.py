@@ -7,6 +7,7 @@ main thread gets back never go backwards, and the tracking result equals a run w
 from __future__ import annotations
 
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -41,6 +42,10 @@ def _run(cfg, n, reader: bool, tmp_path=None):
                     eng.save_map(str(tmp_path / f"map{k % 2}.npz"))
                 reads[0] += 1
                 k += 1
+                # a poller, not a spinner: a thread that never blocks holds the GIL for whole
+                # switch intervals (5 ms) after each of the main thread's ctypes calls returns,
+                # which stretched this test to ~90 s per case without changing what it checks
+                time.sleep(0.002)
             except Exception as exc:   # noqa: BLE001 - collected and reported by the main thread
                 errors.append(repr(exc))
                 return

@@ -151,9 +151,10 @@ __global__ __launch_bounds__(256) void k_pose_records(BatchCtx c, int f0, uint8_
     }
 }
 
-// unpack of the all-gather's padded layout: frame f of the batch is record (f - lo_q) of rank q's
-// slot (peer_records(n, world) records per rank), q the owner of f
-__global__ __launch_bounds__(256) void k_pose_records_gathered(BatchCtx c, int world, const uint8_t* rec) {
+// unpack of the all-gather's padded layout: frame f of the batch is record (f - lo) of range q's
+// owner's slot (peer_records(n, world) records per rank), [lo, hi) = range q the one holding f
+// (the owner of range q is rank q, or rig_rank(q) under the pair split)
+__global__ __launch_bounds__(256) void k_pose_records_gathered(BatchCtx c, int world, int pairs, const uint8_t* rec) {
     const int f = blockIdx.x, per = peer_records(c.n, world);
     int q = 0, lo = 0, hi = 0;
     for (; q < world; ++q) {
@@ -161,7 +162,7 @@ __global__ __launch_bounds__(256) void k_pose_records_gathered(BatchCtx c, int w
         if (f < hi) break;
     }
     const int P = c.P;
-    const uint8_t* r = rec + ((int64_t)q * per + (f - lo)) * pose_record_size(P);
+    const uint8_t* r = rec + ((int64_t)rig_rank(q, world, pairs) * per + (f - lo)) * pose_record_size(P);
     const double* rd = reinterpret_cast<const double*>(r);
     const int32_t* ri = reinterpret_cast<const int32_t*>(r + (int64_t)(P + 1) * TS_POSE_DOUBLES * 8);
     for (int i = threadIdx.x; i < (P + 1) * TS_POSE_DOUBLES; i += blockDim.x) {
@@ -178,8 +179,8 @@ __global__ __launch_bounds__(256) void k_pose_records_gathered(BatchCtx c, int w
     }
 }
 
-void launch_pose_records_gathered(const BatchCtx& c, int world, const uint8_t* rec, hipStream_t s) {
-    hipLaunchKernelGGL(k_pose_records_gathered, dim3(c.n), dim3(256), 0, s, c, world, rec);
+void launch_pose_records_gathered(const BatchCtx& c, int world, bool pairs, const uint8_t* rec, hipStream_t s) {
+    hipLaunchKernelGGL(k_pose_records_gathered, dim3(c.n), dim3(256), 0, s, c, world, pairs ? 1 : 0, rec);
 }
 
 void launch_pose_records(const BatchCtx& c, bool pack, int f0, int n, uint8_t* rec, hipStream_t s) {
@@ -188,12 +189,14 @@ void launch_pose_records(const BatchCtx& c, bool pack, int f0, int n, uint8_t* r
     else hipLaunchKernelGGL(k_pose_records<false>, dim3(n), dim3(256), 0, s, c, f0, rec);
 }
 
-// pair block, per (batch frame, pair) of a camera-sharded RGB-D rig (each rank tracks its own
-// cameras over the whole batch; the rig pose of a frame range needs every camera's
-// correspondences): pose f64[68] | stats i32[8] | corr f64[K][8] (rows past stats[1] are not
-// copied).  The rig pose reads nothing else of a pair (k_rig_pose).
+// pair block, per (batch frame, pair), for the rig pose of a frame range on another rank (a
+// camera-sharded RGB-D rig, or the pair split of a stereo rig): pose f64[68] | stats i32[8] |
+// corr f64[K][5] — the columns k_rig_pose reads of a correspondence (X, Y, Z, cx - u, cy - v; the
+// bearing columns 5..7 serve P3P on the pair's own rank), rows past stats[1] not copied.  The rig
+// pose reads nothing else of a pair.
+#define TS_PAIR_CORR 5
 static inline __host__ __device__ int64_t pair_block_size(int K) {
-    return (int64_t)TS_POSE_DOUBLES * 8 + TS_STATS_INTS * 4 + (int64_t)K * TS_CORR_DOUBLES * 8;
+    return (int64_t)TS_POSE_DOUBLES * 8 + TS_STATS_INTS * 4 + (int64_t)K * TS_PAIR_CORR * 8;
 }
 int64_t pair_block_bytes(const LevelGeom& g) { return pair_block_size(g.K); }
 
@@ -207,18 +210,25 @@ __global__ __launch_bounds__(256) void k_pair_blocks(BatchCtx c, int f0, int p0,
     const size_t fp = (size_t)f * c.P + p;
     uint8_t* pose = reinterpret_cast<uint8_t*>(c.pose + fp * TS_POSE_DOUBLES);
     uint8_t* stats = reinterpret_cast<uint8_t*>(c.stats + fp * TS_STATS_INTS);
-    uint8_t* corr = reinterpret_cast<uint8_t*>(c.corr + fp * K * TS_CORR_DOUBLES);
+    double* corr = c.corr + fp * K * TS_CORR_DOUBLES;
     const int64_t so = (int64_t)TS_POSE_DOUBLES * 8, co = so + TS_STATS_INTS * 4;
+    double* bc = reinterpret_cast<double*>(b + co);   // 16-byte aligned: 544 + 32 bytes in
     if (PACK) {
         copy_piece(b, pose, so);
         copy_piece(b + so, stats, TS_STATS_INTS * 4);
         const int n = min(max(c.stats[fp * TS_STATS_INTS + 1], 0), (int)K);
-        copy_piece(b + co, corr, (int64_t)n * TS_CORR_DOUBLES * 8);
+        for (int i = threadIdx.x; i < n * TS_PAIR_CORR; i += blockDim.x) {
+            const int row = i / TS_PAIR_CORR, col = i - row * TS_PAIR_CORR;
+            bc[i] = corr[(size_t)row * TS_CORR_DOUBLES + col];
+        }
     } else {
         copy_piece(pose, b, so);
         copy_piece(stats, b + so, TS_STATS_INTS * 4);
         const int n = min(max(reinterpret_cast<const int32_t*>(b + so)[1], 0), (int)K);
-        copy_piece(corr, b + co, (int64_t)n * TS_CORR_DOUBLES * 8);
+        for (int i = threadIdx.x; i < n * TS_PAIR_CORR; i += blockDim.x) {
+            const int row = i / TS_PAIR_CORR, col = i - row * TS_PAIR_CORR;
+            corr[(size_t)row * TS_CORR_DOUBLES + col] = bc[i];
+        }
     }
 }
 

@@ -249,6 +249,9 @@ struct tslam_handle {
     // sharded rig (tslam_set_shard): front-end cameras [sh_cam_lo, sh_cam_hi) and back-end frames
     // [rank * n / world, (rank + 1) * n / world) of every batch
     int sh_cam_lo = 0, sh_cam_hi = 0, sh_rank = 0, sh_world = 1;
+    // pair split (TSLAM_SHARD_PAIRS, one camera per rank): the back end solves this camera's pair
+    // over half of the batch and the rig pose covers range rig_slot (tslam_ranges.h)
+    bool sh_pairs = false;
     // library-driven sharding (tslam_comm_init / tslam_group_create, tslam_shard.cpp): the driver
     // that owns this rank's communicators, streams and exchange buffers (owned here after
     // tslam_comm_init; a group owns it otherwise)
@@ -782,7 +785,12 @@ static BatchCtx range_ctx(const BatchCtx& c, int lo, int hi) {
     return r;
 }
 
-static void shard_range(const tslam_handle* h, int n, int* lo, int* hi) { peer_range(h->sh_rank, n, h->sh_world, lo, hi); }
+// the rank's rig range: rig pose, pose records (and, without the pair split, its whole back end)
+static void shard_range(const tslam_handle* h, int n, int* lo, int* hi) {
+    peer_range(rig_slot(h->sh_rank, h->sh_world, h->sh_pairs), n, h->sh_world, lo, hi);
+}
+// pair split: the half of the batch whose frames this rank's pair back end solves
+static void pair_half(const tslam_handle* h, int n, int* lo, int* hi) { peer_range(h->sh_cam_lo & 1, n, 2, lo, hi); }
 
 // A8 of the current batch.  It may run on its own stream: it depends on this batch's poses (event
 // on the stream of the last stage) and only reads ring buffers plus a snapshot of the batch's
@@ -903,13 +911,33 @@ static int run_sharded_rgbd_stage(tslam_handle* h, const BatchCtx& c, int stage,
 static int run_sharded_stage(tslam_handle* h, const BatchCtx& c, int stage, hipStream_t s) {
     if (h->prm.rgbd) return run_sharded_rgbd_stage(h, c, stage, s);
     int lo, hi;
-    shard_range(h, c.n, &lo, &hi);
-    const BatchCtx cb = range_ctx(c, lo, hi);
+    if (h->sh_pairs) pair_half(h, c.n, &lo, &hi);
+    else shard_range(h, c.n, &lo, &hi);
+    BatchCtx cb = range_ctx(c, lo, hi);
     const bool empty = hi <= lo;           // a short batch leaves this rank no frames
     const bool pre = !empty && c.g0 + lo - 1 >= 0;   // frame lo - 1 exists
     BatchCtx cp = c;                        // the pre-pass: frame lo - 1, batch scratch at frame 0
     cp.g0 = c.g0 + lo - 1;
     cp.n = 1;
+    if (h->sh_pairs) {   // pair split: this camera's pair only; the rig pose is its own step (KERNEL_RIG)
+        cb.pair0 = cp.pair0 = h->sh_cam_lo / 2;
+        cb.npair = cp.npair = 1;
+        switch (stage) {
+            case TSLAM_STAGE_POSE:
+                if (!empty) launch_pose(cb, s);
+                HIPCHK(hipGetLastError());
+                return TSLAM_OK;
+            case TSLAM_KERNEL_RIG: {
+                if (!h->rig) return fail(TSLAM_ESTATE, "no rig set (tslam_set_rig)");
+                int rl, rh;
+                shard_range(h, c.n, &rl, &rh);   // every pair's blocks of the rig range are here (tslam_shard.cpp)
+                if (rh > rl) launch_rig_pose(range_ctx(c, rl, rh), s);
+                HIPCHK(hipGetLastError());
+                return TSLAM_OK;
+            }
+            default: break;
+        }
+    }
     switch (stage) {
         case TSLAM_STAGE_RECTIFY: launch_rectify_pyramid(c, s); break;
         case TSLAM_STAGE_DETECT: launch_detect(c, s); launch_select(c, s); break;
@@ -1768,6 +1796,7 @@ int tslam_set_shard(tslam_handle* h, int cam_lo, int cam_hi, int rank, int world
     h->sh_cam_hi = cam_hi;
     h->sh_rank = rank;
     h->sh_world = world;
+    h->sh_pairs = false;   // the driver sets the pair split after (tslam_shard_options)
     return TSLAM_OK;
 }
 
@@ -1982,6 +2011,64 @@ int tslam_import_peers(tslam_handle* h, const uint8_t* raw, const void* streams,
     return TSLAM_OK;
 }
 
+// -- pair split (TSLAM_SHARD_PAIRS): the partner camera's frames of this rank's half -------------
+int tslam_internal_set_pairs(tslam_handle* h, int on) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (h->in_batch) return fail(TSLAM_ESTATE, "the pair split is set outside a batch");
+    if (on) {
+        if (h->prm.rgbd) return fail(TSLAM_EINVAL, "the pair split shards a stereo rig");
+        if (h->sh_world < 2 || h->sh_world != h->C || h->sh_cam_hi - h->sh_cam_lo != 1 || h->sh_cam_lo != h->sh_rank)
+            return fail(TSLAM_EINVAL, "the pair split needs one camera per rank (world = cameras)");
+        if (h->prm.ba_window) return fail(TSLAM_EINVAL, "the pair split runs without local BA (no state gather)");
+    }
+    h->sh_pairs = on != 0;
+    return TSLAM_OK;
+}
+
+static int check_partner(tslam_handle* h) {
+    if (!h) return fail(TSLAM_EINVAL, "null handle");
+    if (!h->in_batch) return fail(TSLAM_ESTATE, "partner blocks are packed / imported inside a batch");
+    if (!h->sh_pairs) return fail(TSLAM_ESTATE, "the handle is not pair-split (TSLAM_SHARD_PAIRS)");
+    return TSLAM_OK;
+}
+
+int tslam_internal_pack_partner(tslam_handle* h, void* dst, void* stream) {
+    int rc = check_partner(h);
+    if (rc != TSLAM_OK) return rc;
+    if (!dst) return fail(TSLAM_EINVAL, "null buffer");
+    HIPCHK(hipSetDevice(h->device));
+    int lo, hi;
+    peer_range((h->sh_cam_lo & 1) ^ 1, h->cur_n, 2, &lo, &hi);   // the partner's half
+    if (hi > lo)   // frames lo - 1 .. hi - 1 of this camera (zeros before the sequence start)
+        launch_stream_blocks(make_ctx(h), true, h->cur_g0 + lo - 1, hi - lo + 1, h->sh_cam_lo, 1, (uint8_t*)dst,
+                             (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return TSLAM_OK;
+}
+
+int tslam_internal_import_partner(tslam_handle* h, const uint8_t* raw, const void* streams, void* stream) {
+    int rc = check_partner(h);
+    if (rc != TSLAM_OK) return rc;
+    if (!raw || !streams) return fail(TSLAM_EINVAL, "null buffer");
+    HIPCHK(hipSetDevice(h->device));
+    int lo, hi;
+    pair_half(h, h->cur_n, &lo, &hi);
+    if (hi <= lo) return TSLAM_OK;   // an empty half: this rank's back end has nothing to do
+    const int partner = h->sh_cam_lo ^ 1, nf = hi - lo + 1;
+    const int64_t first = h->cur_g0 + lo - 1;
+    const int skip = first < 0 ? 1 : 0;   // frame -1 (before the sequence start) is not imported
+    BatchCtx c = make_ctx(h);
+    c.images = raw + (size_t)skip * h->W * h->H;
+    c.g0 = first + skip;
+    c.n = nf - skip;
+    c.cam0 = partner;
+    c.ncam = 1;
+    if (c.n > 0) launch_rectify_pyramid(c, (hipStream_t)stream);
+    launch_stream_blocks(make_ctx(h), false, first, nf, partner, 1, (uint8_t*)streams, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return TSLAM_OK;
+}
+
 int tslam_pack_poses(tslam_handle* h, void* dst, void* stream) {
     if (!h || !dst) return fail(TSLAM_EINVAL, "bad argument");
     if (!h->in_batch) return fail(TSLAM_ESTATE, "tslam_pack_poses inside a batch (after its POSE stage)");
@@ -1997,9 +2084,9 @@ int tslam_unpack_poses(tslam_handle* h, const void* src, void* stream) {
     if (!h || !src) return fail(TSLAM_EINVAL, "bad argument");
     if (!h->in_batch) return fail(TSLAM_ESTATE, "tslam_unpack_poses inside a batch (before its CHAIN stage)");
     HIPCHK(hipSetDevice(h->device));
-    // rank q's records start at q * peer_records(n, world) (the all-gather pads every range to the
-    // longest); with equal ranges that is the contiguous batch order
-    launch_pose_records_gathered(make_ctx(h), h->sh_world, (const uint8_t*)src, (hipStream_t)stream);
+    // rank q's records (its rig range) start at q * peer_records(n, world) (the all-gather pads
+    // every range to the longest); with equal ranges, and no pair split, that is the batch order
+    launch_pose_records_gathered(make_ctx(h), h->sh_world, h->sh_pairs, (const uint8_t*)src, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
     return TSLAM_OK;
 }

@@ -220,7 +220,8 @@ void launch_stage_raw_peers(const uint8_t* images, const uint8_t* prev, uint8_t*
                             int S, int64_t img_bytes, hipStream_t s);
 void launch_pose_records(const BatchCtx& c, bool pack, int f0, int n, uint8_t* rec, hipStream_t s);
 // every frame of the batch from the all-gather's padded layout [world][peer_records][record]
-void launch_pose_records_gathered(const BatchCtx& c, int world, const uint8_t* rec, hipStream_t s);
+// (`pairs`: rank q's slot holds rig range rig_slot(q), tslam_ranges.h)
+void launch_pose_records_gathered(const BatchCtx& c, int world, bool pairs, const uint8_t* rec, hipStream_t s);
 // state blocks a sharded rank sends to rank 0 so that rank 0's ring holds what local BA, loop
 // closure and relocalisation read (k_exchange.hip): per (frame of the sender's range, pair) the
 // temporal matches + refined disparities, per (batch frame, left camera of the sender's streams)

@@ -38,4 +38,13 @@ TSLAM_INTERNAL int tslam_internal_state_blocks(tslam_handle* h, int pack, int ra
                                                void* stream);
 // the current batch's poses / stats into the handle's pinned result slots (tslam_poll_batch)
 TSLAM_INTERNAL int tslam_internal_stash(tslam_handle* h, void* stream);
+
+// Pair split (TSLAM_SHARD_PAIRS, tslam_ranges.h rig_slot): set / clear it on a sharded stereo
+// handle with one camera per rank (outside a batch).  Inside a batch: pack this camera's stream
+// blocks of the partner's half (frames lo' - 1 .. hi' - 1, the partner = the pair's other camera)
+// -> dst; import the partner's raw images + stream blocks of this rank's half (as received) into
+// the ring.  Pair blocks of the rig ranges move with tslam_pack_pairs / tslam_unpack_pairs.
+TSLAM_INTERNAL int tslam_internal_set_pairs(tslam_handle* h, int on);
+TSLAM_INTERNAL int tslam_internal_pack_partner(tslam_handle* h, void* dst, void* stream);
+TSLAM_INTERNAL int tslam_internal_import_partner(tslam_handle* h, const uint8_t* raw, const void* streams, void* stream);
 }  // extern "C"

@@ -27,3 +27,16 @@ static inline TS_RANGE_HD int peer_frames(int q, int n, int world) {
 }
 static inline TS_RANGE_HD int peer_cap(int max_batch, int world) { return (max_batch + world - 1) / world + 1; }
 static inline TS_RANGE_HD int peer_records(int n, int world) { return (n + world - 1) / world; }
+
+// Pair split (TSLAM_SHARD_PAIRS; one camera per rank, world = cameras): rank r holds camera r of
+// pair r / 2 and its back end solves that pair over half of the batch, side r & 1 =
+// peer_range(r & 1, n, 2).  Its rig range (rig pose + pose records) is range `rig_slot` of the
+// world-way split: the even ranks take the first half's world/2 ranges in pair order, the odd
+// ranks the second half's, so a rank's rig range lies inside its own half (floor ranges nest:
+// peer_range(s, n, world) for s < world/2 ends by n/2) and its pair's blocks never leave it.
+static inline TS_RANGE_HD int rig_slot(int rank, int world, int pairs) {
+    return pairs ? (rank & 1) * (world / 2) + (rank >> 1) : rank;
+}
+static inline TS_RANGE_HD int rig_rank(int slot, int world, int pairs) {   // inverse of rig_slot
+    return !pairs ? slot : slot < world / 2 ? 2 * slot : 2 * (slot - world / 2) + 1;
+}

@@ -24,6 +24,13 @@
 // the pose all-gather pads every range to peer_records(n, N) records.  Raw images go straight from
 // the caller's input (and the previous batch's last frame) to the peers: no staging copy.
 //
+// Pair split (TSLAM_SHARD_PAIRS, one camera per rank): rank r's back end solves pair r / 2 over
+// half r & 1 of the batch, so the raw images and stream blocks go to the partner (r ^ 1) only —
+// half a batch + 1 frame instead of a range + 1 frame to each of world - 1 peers; the rig pose of a
+// rank's rig range (tslam_ranges.h rig_slot, inside its half) then takes the other pairs' pair
+// blocks (pose, stats, the 5 correspondence columns it reads) from the ranks of the same half.
+// Fewer bytes per rank, all of the image traffic on the one partner link.
+//
 // State gather (TSLAM_SHARD_GATHER, implied by local BA): every rank sends rank 0 the temporal
 // matches and disparities of its range and the keypoints + descriptors of its left cameras, so
 // rank 0's ring holds what the one-handle path's local BA, loop closure and relocalisation read;
@@ -87,6 +94,8 @@ struct Rank {
     uint8_t* pose_send[2] = {nullptr, nullptr};
     uint8_t* pose_recv[2] = {nullptr, nullptr};
     uint8_t* state_buf[2] = {nullptr, nullptr};    // gather: the payload (sender) / all payloads (rank 0)
+    uint8_t* pb_send[2] = {nullptr, nullptr};      // pair split: pair blocks per rig-range owner
+    uint8_t* pb_recv[2] = {nullptr, nullptr};
     uint8_t* prev_raw = nullptr;   // the previous batch's last frame of this rank's cameras
     std::vector<void*> allocs;
     // profiling
@@ -97,7 +106,7 @@ struct Rank {
     int64_t timed_batches = 0;
 };
 
-enum Which { RAW = 0, FEAT = 1, POSE = 2, STATE = 3 };
+enum Which { RAW = 0, FEAT = 1, POSE = 2, STATE = 3, PAIRB = 4 };
 }  // namespace
 
 struct tslam_shard_driver {
@@ -105,12 +114,17 @@ struct tslam_shard_driver {
     bool rgbd = false, rig = false, ba = false;
     int flags = 0;                       // TSLAM_SHARD_* options
     int S = 0, B = 0, cap = 0;           // cameras per rank, max_batch, frames per peer slot
+    int P = 0;                           // stereo pairs (RGB-D: cameras)
     int n = 0, maxr = 0;                 // this batch: frames, pose records per rank in the all-gather
     size_t img = 0, rec = 0, sblk = 0, pblk = 0;   // bytes: image, pose record, stream block, pair block
     size_t state_cap = 0;                // bytes of one sender's state payload slot (full batch)
+    bool pb_ready = false;               // pair split: pair-block buffers allocated
     int64_t batches = 0;
     std::vector<Rank> ranks;   // local ranks: all of a group, one after tslam_comm_init
     bool gather() const { return world > 1 && !rgbd && (ba || (flags & TSLAM_SHARD_GATHER)); }
+    // TSLAM_SHARD_PAIRS: rank r's back end solves pair r / 2 over half r & 1 of the batch; the
+    // stereo exchange goes to the partner (r ^ 1) only, the rig pose gathers pair blocks
+    bool pairs() const { return (flags & TSLAM_SHARD_PAIRS) != 0; }
 };
 
 // The rank's streams: its own three, or with TSLAM_SHARD_SERIAL one stream per device shared by
@@ -163,6 +177,7 @@ static int plan(tslam_shard_driver* d, tslam_handle* h, int world) {
     d->rig = in.rig != 0;
     d->ba = in.ba != 0;
     d->S = in.C / world;
+    d->P = in.P;
     d->B = in.B;
     d->cap = peer_cap(in.B, world);
     d->img = (size_t)in.W * in.H;
@@ -172,11 +187,25 @@ static int plan(tslam_shard_driver* d, tslam_handle* h, int world) {
     return TSLAM_OK;
 }
 
+// The frames rank q's stereo back end solves: its frame range, or under the pair split its pair's
+// half of the batch; it reads the other cameras of frames lo - 1 .. hi - 1 (none when empty).
+static void back_range(const tslam_shard_driver* d, int q, int* lo, int* hi) {
+    if (d->pairs()) peer_range(q & 1, d->n, 2, lo, hi);
+    else peer_range(q, d->n, d->world, lo, hi);
+}
+static int back_frames(const tslam_shard_driver* d, int q) {
+    int lo, hi;
+    back_range(d, q, &lo, &hi);
+    return hi > lo ? hi - lo + 1 : 0;
+}
+// does rank src send rank dst its raw images and stream blocks (pair split: the partner only)
+static bool stereo_peer(const tslam_shard_driver* d, int src, int dst) { return src != dst && (!d->pairs() || dst == (src ^ 1)); }
+
 // bytes rank `q`'s slot carries for this batch: raw images / stream blocks of the frames q's back end
 // reads (lo_q - 1 .. hi_q - 1) of S cameras; pair blocks (RGB-D) of q's range; slot capacities
-static size_t raw_bytes(const tslam_shard_driver* d, int q) { return (size_t)peer_frames(q, d->n, d->world) * d->S * d->img; }
+static size_t raw_bytes(const tslam_shard_driver* d, int q) { return (size_t)back_frames(d, q) * d->S * d->img; }
 static size_t feat_bytes(const tslam_shard_driver* d, int q) {
-    if (!d->rgbd) return (size_t)peer_frames(q, d->n, d->world) * d->S * d->sblk;
+    if (!d->rgbd) return (size_t)back_frames(d, q) * d->S * d->sblk;
     int lo, hi;
     peer_range(q, d->n, d->world, &lo, &hi);
     return (size_t)(hi - lo) * d->S * d->pblk;
@@ -227,6 +256,37 @@ static int setup_gather(tslam_shard_driver* d) {
     return TSLAM_OK;
 }
 
+// The pair split's pair-block buffers (allocated when first needed): a slot per rank of the rig
+// range it owns (peer_records(max_batch, world) frames), sent to / received from the ranks of the
+// same half.  The stereo receive buffers need no change: world slots of peer_cap frames hold the
+// partner's half (max_batch / 2 + 1 frames) from offset 0.
+static int setup_pairs(tslam_shard_driver* d) {
+    if (!d->pairs() || d->pb_ready) return TSLAM_OK;
+    const size_t bytes = (size_t)d->world * peer_records(d->B, d->world) * d->pblk;
+    for (Rank& r : d->ranks) {
+        SHCHK(hipSetDevice(r.device));
+        for (int k = 0; k < 2; ++k) {
+            RC(alloc(r, &r.pb_send[k], bytes));
+            RC(alloc(r, &r.pb_recv[k], bytes));
+        }
+        SHCHK(hipDeviceSynchronize());
+    }
+    d->pb_ready = true;
+    return TSLAM_OK;
+}
+// pair split: rank q's rig range (rig pose + pose records), inside its pair's half
+static void rig_range(const tslam_shard_driver* d, int q, int* lo, int* hi) {
+    peer_range(rig_slot(q, d->world, 1), d->n, d->world, lo, hi);
+}
+static size_t pb_slot(const tslam_shard_driver* d) { return (size_t)peer_records(d->B, d->world) * d->pblk; }
+// does rank src send rank dst pair blocks (pair split: the other ranks of the same half)
+static bool pair_peer(const tslam_shard_driver* d, int src, int dst) { return src != dst && ((src ^ dst) & 1) == 0; }
+static size_t pb_bytes(const tslam_shard_driver* d, int dst) {   // one pair's blocks of dst's rig range
+    int lo, hi;
+    rig_range(d, dst, &lo, &hi);
+    return (size_t)(hi - lo) * d->pblk;
+}
+
 // ---- profiling (TSLAM_SHARD_PROFILE) ------------------------------------------------------------
 static int span_begin(tslam_shard_driver* d, Rank& r, int seg, hipStream_t s) {
     if (!(d->flags & TSLAM_SHARD_PROFILE)) return TSLAM_OK;
@@ -262,7 +322,7 @@ static int run_timed(tslam_shard_driver* d, Rank& r, int seg, int stage, hipStre
 // The stream an exchange runs on (sender and receiver side): stereo raw images and stream blocks
 // on the exchange stream, pair blocks, state blocks and pose records on the back stream.
 static hipStream_t xstream(const tslam_shard_driver* d, const Rank& r, Which w) {
-    return (w == POSE || w == STATE || d->rgbd) ? BS(d, r) : XS(d, r);
+    return (w == POSE || w == STATE || w == PAIRB || d->rgbd) ? BS(d, r) : XS(d, r);
 }
 
 // The pieces rank `src` sends rank `dst` for exchange w (at most two: a raw image slot of peer 0
@@ -277,7 +337,7 @@ static int pieces(const tslam_shard_driver* d, const Rank& src, int dst, Which w
         const size_t frame = (size_t)d->S * d->img, total = raw_bytes(d, dst);
         if (total == 0) return 0;
         int lo, hi;
-        peer_range(dst, d->n, d->world, &lo, &hi);
+        back_range(d, dst, &lo, &hi);
         if (lo > 0) {   // frames lo-1 .. hi-1 are contiguous in the input
             out[0] = {images + (size_t)(lo - 1) * frame, 0, total};
             return 1;
@@ -289,7 +349,13 @@ static int pieces(const tslam_shard_driver* d, const Rank& src, int dst, Which w
     if (w == FEAT) {
         const size_t b = feat_bytes(d, dst);
         if (b == 0) return 0;
-        out[0] = {src.feat_send[k] + (size_t)dst * feat_cap(d), 0, b};
+        out[0] = {src.feat_send[k] + (d->pairs() ? 0 : (size_t)dst * feat_cap(d)), 0, b};   // pair split: one slot
+        return 1;
+    }
+    if (w == PAIRB) {
+        const size_t b = pb_bytes(d, dst);
+        if (b == 0) return 0;
+        out[0] = {src.pb_send[k] + (size_t)dst * pb_slot(d), 0, b};
         return 1;
     }
     return 0;
@@ -298,15 +364,24 @@ static int pieces(const tslam_shard_driver* d, const Rank& src, int dst, Which w
 static int exchange(tslam_shard_driver* d, Which w, int k, const uint8_t* const* images) {
     const int N = d->world;
     if (w == STATE && !d->gather()) return TSLAM_OK;
+    const bool pairs = d->pairs();
     auto recv_buf = [&](Rank& r, int src) -> uint8_t* {   // where src's data lands in r's buffers
-        if (w == RAW) return r.raw_recv[k] + (size_t)src * raw_cap(d);
-        if (w == FEAT) return r.feat_recv[k] + (size_t)src * feat_cap(d);
+        if (w == RAW) return r.raw_recv[k] + (pairs ? 0 : (size_t)src * raw_cap(d));   // pair split: the partner's
+        if (w == FEAT) return r.feat_recv[k] + (pairs ? 0 : (size_t)src * feat_cap(d));
+        if (w == PAIRB) return r.pb_recv[k] + (size_t)src * pb_slot(d);
         return r.state_buf[k] + (size_t)src * d->state_cap;
     };
     auto recv_bytes = [&](const Rank& r, int src) -> size_t {   // what r receives from src
         if (w == RAW) return raw_bytes(d, r.rank);
         if (w == FEAT) return feat_bytes(d, r.rank);
+        if (w == PAIRB) return pb_bytes(d, r.rank);
         return (size_t)tslam_internal_state_bytes(r.h, d->n, src, src * d->S, (src + 1) * d->S);
+    };
+    // the (src, dst) pairs exchange w connects
+    auto linked = [&](int src, int dst) -> bool {
+        if (w == PAIRB) return pair_peer(d, src, dst);
+        if (w == RAW || (w == FEAT && !d->rgbd)) return stereo_peer(d, src, dst);
+        return src != dst;
     };
     if (d->transport == TSLAM_TRANSPORT_RCCL) {
         NCCLCHK(ncclGroupStart());
@@ -329,22 +404,23 @@ static int exchange(tslam_shard_driver* d, Which w, int k, const uint8_t* const*
                 }
                 continue;
             }
+            ncclComm_t comm = w == PAIRB ? r.comm_p : r.comm_x;   // PAIRB: the back stream's communicator
             for (int q = 0; q < N; ++q) {
-                if (q == r.rank) continue;
+                if (!linked(r.rank, q)) continue;
                 Piece pc[2];
                 const int np = pieces(d, r, q, w, k, images ? images[i] : nullptr, pc);
-                for (int j = 0; j < np; ++j) NCCLCHK(ncclSend(pc[j].p, pc[j].bytes, ncclUint8, q, r.comm_x, s));
+                for (int j = 0; j < np; ++j) NCCLCHK(ncclSend(pc[j].p, pc[j].bytes, ncclUint8, q, comm, s));
                 // what q sends me, in the same pieces (q's view of my range)
                 const size_t b = recv_bytes(r, q);
                 if (b == 0) continue;
                 int lo, hi;
-                peer_range(r.rank, d->n, N, &lo, &hi);
+                back_range(d, r.rank, &lo, &hi);
                 if (w == RAW && lo == 0) {
                     const size_t frame = (size_t)d->S * d->img;
-                    NCCLCHK(ncclRecv(recv_buf(r, q), frame, ncclUint8, q, r.comm_x, s));
-                    NCCLCHK(ncclRecv(recv_buf(r, q) + frame, b - frame, ncclUint8, q, r.comm_x, s));
+                    NCCLCHK(ncclRecv(recv_buf(r, q), frame, ncclUint8, q, comm, s));
+                    NCCLCHK(ncclRecv(recv_buf(r, q) + frame, b - frame, ncclUint8, q, comm, s));
                 } else {
-                    NCCLCHK(ncclRecv(recv_buf(r, q), b, ncclUint8, q, r.comm_x, s));
+                    NCCLCHK(ncclRecv(recv_buf(r, q), b, ncclUint8, q, comm, s));
                 }
             }
         }
@@ -372,6 +448,14 @@ static int exchange(tslam_shard_driver* d, Which w, int k, const uint8_t* const*
                 if (b) SHCHK(hipMemcpyAsync(recv_buf(dst, src.rank), src.state_buf[k], b, hipMemcpyDeviceToDevice, s));
                 continue;
             }
+            if (!linked(src.rank, dst.rank)) continue;
+            if (w == PAIRB) {   // dst's back stream unpacked this parity's blocks (batch s-2) before its batch s-1 ended
+                if (dst.done_armed) SHCHK(hipStreamWaitEvent(s, dst.ev_done, 0));
+                Piece pc[2];
+                if (pieces(d, src, dst.rank, w, k, nullptr, pc))
+                    SHCHK(hipMemcpyAsync(recv_buf(dst, src.rank), pc[0].p, pc[0].bytes, hipMemcpyDeviceToDevice, s));
+                continue;
+            }
             if (dst.consumed_armed[k]) SHCHK(hipStreamWaitEvent(s, dst.consumed[k], 0));
             Piece pc[2];
             const int np = pieces(d, src, dst.rank, w, k, images ? images[i] : nullptr, pc);
@@ -393,6 +477,7 @@ static int exchange(tslam_shard_driver* d, Which w, int k, const uint8_t* const*
 static int submit(tslam_shard_driver* d, const uint8_t* const* images, int n, void* const* streams) {
     if (n < 1 || n > d->B) return tslam_internal_fail(TSLAM_EINVAL, "a sharded batch needs 1 <= n_frames <= max_batch");
     RC(setup_gather(d));
+    RC(setup_pairs(d));
     d->n = n;
     d->maxr = peer_records(n, d->world);
     const int k = (int)(d->batches & 1), N = d->world, S = d->S;
@@ -433,7 +518,8 @@ static int submit(tslam_shard_driver* d, const uint8_t* const* images, int n, vo
         if (d->rgbd) continue;
         if (N > 1) {
             RC(span_begin(d, r, TSLAM_SEG_PACK, FS(d, r)));
-            RC(tslam_pack_streams_peers(r.h, r.feat_send[k], FS(d, r)));   // every peer's frames, one launch
+            if (d->pairs()) RC(tslam_internal_pack_partner(r.h, r.feat_send[k], FS(d, r)));   // the partner's half
+            else RC(tslam_pack_streams_peers(r.h, r.feat_send[k], FS(d, r)));   // every peer's frames, one launch
             RC(span_end(d, r, FS(d, r)));
         }
         SHCHK(hipSetDevice(r.device));
@@ -451,7 +537,8 @@ static int submit(tslam_shard_driver* d, const uint8_t* const* images, int n, vo
             if (prof && N > 1) RC(span_between(d, r, TSLAM_SEG_EXCHANGE_WAIT, FS(d, r), BS(d, r)));   // front done -> data landed
             if (N > 1) {
                 RC(span_begin(d, r, TSLAM_SEG_IMPORT, BS(d, r)));
-                RC(tslam_import_peers(r.h, r.raw_recv[k], r.feat_recv[k], BS(d, r)));
+                if (d->pairs()) RC(tslam_internal_import_partner(r.h, r.raw_recv[k], r.feat_recv[k], BS(d, r)));
+                else RC(tslam_import_peers(r.h, r.raw_recv[k], r.feat_recv[k], BS(d, r)));
                 RC(span_end(d, r, BS(d, r)));
             }
             SHCHK(hipEventRecord(r.consumed[k], BS(d, r)));
@@ -461,7 +548,7 @@ static int submit(tslam_shard_driver* d, const uint8_t* const* images, int n, vo
             RC(run_timed(d, r, TSLAM_SEG_MATCH, TSLAM_KERNEL_MATCH, BS(d, r)));
             RC(run_timed(d, r, TSLAM_SEG_MATCH_REFINE, TSLAM_KERNEL_MATCH_REFINE, BS(d, r)));
             RC(run_timed(d, r, TSLAM_SEG_POSE, TSLAM_KERNEL_POSE, BS(d, r)));
-            if (d->rig && !d->rgbd) RC(run_timed(d, r, TSLAM_SEG_RIG, TSLAM_KERNEL_RIG, BS(d, r)));
+            if (d->rig && !d->rgbd && !d->pairs()) RC(run_timed(d, r, TSLAM_SEG_RIG, TSLAM_KERNEL_RIG, BS(d, r)));
         } else {
             RC(tslam_run_stage(r.h, TSLAM_STAGE_MATCH, BS(d, r)));
             RC(tslam_run_stage(r.h, TSLAM_STAGE_POSE, BS(d, r)));
@@ -489,6 +576,34 @@ static int submit(tslam_shard_driver* d, const uint8_t* const* images, int n, vo
             r.consumed_armed[k] = true;
             if (d->rig) RC(run_timed(d, r, TSLAM_SEG_RIG, TSLAM_KERNEL_RIG, BS(d, r)));
         }
+    }
+    if (d->pairs()) {   // every pair's blocks of a rank's rig range from the ranks of its half, then the rig pose
+        const size_t slot = pb_slot(d);
+        if (d->P > 1) {
+            for (Rank& r : d->ranks) {
+                if (idle(r)) continue;
+                RC(span_begin(d, r, TSLAM_SEG_PAIR_BLOCKS, BS(d, r)));
+                for (int q = 0; q < N; ++q) {
+                    int lo, hi;
+                    rig_range(d, q, &lo, &hi);
+                    if (pair_peer(d, r.rank, q) && hi > lo)
+                        RC(tslam_pack_pairs(r.h, lo, hi - lo, r.rank / 2, r.rank / 2 + 1, r.pb_send[k] + (size_t)q * slot, BS(d, r)));
+                }
+            }
+            if (!solo) RC(exchange(d, PAIRB, k, images));
+            for (Rank& r : d->ranks) {
+                if (idle(r)) continue;
+                int lo, hi;
+                rig_range(d, r.rank, &lo, &hi);
+                for (int q = 0; q < N; ++q)
+                    if (pair_peer(d, q, r.rank) && hi > lo)
+                        RC(tslam_unpack_pairs(r.h, lo, hi - lo, q / 2, q / 2 + 1, r.pb_recv[k] + (size_t)q * slot, BS(d, r)));
+                RC(span_end(d, r, BS(d, r)));
+            }
+        }
+        if (d->rig)
+            for (Rank& r : d->ranks)
+                if (!idle(r)) RC(run_timed(d, r, TSLAM_SEG_RIG, TSLAM_KERNEL_RIG, BS(d, r)));
     }
     if (d->gather()) {   // every rank's share of the pairs' state into rank 0's ring
         for (Rank& r : d->ranks) {
@@ -616,12 +731,16 @@ int tslam_shard_options(tslam_handle* h, int flags) {
     tslam_shard_driver* d = tslam_internal_driver(h);
     if (!d) return tslam_internal_fail(TSLAM_ESTATE, "the handle is not driven (tslam_comm_init / tslam_group_create)");
     if (flags & ~(TSLAM_SHARD_GATHER | TSLAM_SHARD_RESULTS | TSLAM_SHARD_PROFILE | TSLAM_SHARD_SERIAL |
-                  TSLAM_SHARD_PIPELINE | TSLAM_SHARD_SOLO))
+                  TSLAM_SHARD_PIPELINE | TSLAM_SHARD_SOLO | TSLAM_SHARD_PAIRS))
         return tslam_internal_fail(TSLAM_EINVAL, "unknown TSLAM_SHARD_* flag");
     if ((flags & TSLAM_SHARD_SOLO) && (int)d->ranks.size() != d->world)
         return tslam_internal_fail(TSLAM_EINVAL, "TSLAM_SHARD_SOLO needs every rank in this process (tslam_group_create)");
     if ((flags & TSLAM_SHARD_GATHER) && d->rgbd)
         return tslam_internal_fail(TSLAM_EINVAL, "the state gather describes a stereo rig");
+    if ((flags & TSLAM_SHARD_PAIRS) && (d->rgbd || d->S != 1 || d->world < 2))
+        return tslam_internal_fail(TSLAM_EINVAL, "the pair split shards a stereo rig with one camera per rank");
+    if ((flags & TSLAM_SHARD_PAIRS) && (d->ba || (flags & TSLAM_SHARD_GATHER)))
+        return tslam_internal_fail(TSLAM_EINVAL, "the pair split runs without the state gather (no local BA)");
     // the streams may change (TSLAM_SHARD_SERIAL): everything enqueued so far finishes first
     for (Rank& r : d->ranks) {
         SHCHK(hipSetDevice(r.device));
@@ -639,6 +758,7 @@ int tslam_shard_options(tslam_handle* h, int flags) {
                 r.serial_owner = true;
             }
         }
+    for (Rank& r : d->ranks) RC(tslam_internal_set_pairs(r.h, (flags & TSLAM_SHARD_PAIRS) ? 1 : 0));
     d->flags = flags;
     return TSLAM_OK;
 }

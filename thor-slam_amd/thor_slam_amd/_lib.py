@@ -35,10 +35,10 @@ INE_RECORD = 80   # TSLAM_BA_INE_RECORD: doubles of an inertial factor record
 RIG_KERNEL = 18   # rig pose (+ chain; sharded: the range's rig pose only)
 POSE_SOLVE_KERNEL = 19   # P3P + RANSAC + refine on injected correspondences (parity tests)
 TRANSPORT = {"rccl": 0, "copy": 1}   # tslam_group_create
-SHARD_GATHER, SHARD_RESULTS, SHARD_PROFILE, SHARD_SERIAL, SHARD_PIPELINE, SHARD_SOLO = 1, 2, 4, 8, 16, 32   # tslam_shard_options
+SHARD_GATHER, SHARD_RESULTS, SHARD_PROFILE, SHARD_SERIAL, SHARD_PIPELINE, SHARD_SOLO, SHARD_PAIRS = 1, 2, 4, 8, 16, 32, 64   # tslam_shard_options
 # tslam_shard_timing segments (enum tslam_segment), in order
 SHARD_SEGMENTS = ("rectify_pyramid", "detect", "select", "describe", "pack", "exchange_wait", "import", "match",
-                  "match_refine", "pose", "rig", "state", "pose_gather", "chain", "local_ba")
+                  "match_refine", "pose", "rig", "state", "pose_gather", "chain", "local_ba", "pair_blocks")
 POSE_OK, POSE_LOST, POSE_INIT = 0, 1, 2
 
 
@@ -590,10 +590,12 @@ class Handle:
         _check(self.lib.tslam_submit_sharded(self.h, ctypes.c_void_p(images_dev_ptr), n, ctypes.c_void_p(stream)))
 
     def shard_options(self, gather: bool = False, results: bool = False, profile: bool = False,
-                      serial: bool = False, pipeline: bool = False, solo: bool = False) -> None:
-        """``tslam_shard_options`` of the driver behind this (sharded) handle."""
+                      serial: bool = False, pipeline: bool = False, solo: bool = False, pairs: bool = False) -> None:
+        """``tslam_shard_options`` of the driver behind this (sharded) handle (``pairs``:
+        TSLAM_SHARD_PAIRS, the pair split of a one-camera-per-rank stereo rig)."""
         flags = ((SHARD_GATHER if gather else 0) | (SHARD_RESULTS if results else 0) | (SHARD_PROFILE if profile else 0)
-                 | (SHARD_SERIAL if serial else 0) | (SHARD_PIPELINE if pipeline else 0) | (SHARD_SOLO if solo else 0))
+                 | (SHARD_SERIAL if serial else 0) | (SHARD_PIPELINE if pipeline else 0) | (SHARD_SOLO if solo else 0)
+                 | (SHARD_PAIRS if pairs else 0))
         _check(self.lib.tslam_shard_options(self.h, flags))
 
     def shard_timing(self) -> tuple[dict, int]:

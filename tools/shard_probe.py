@@ -1,6 +1,6 @@
 """The sharded rig's per-rank work in a one-GPU rehearsal of the library driver (profiling aid).
 
-    python tools/shard_probe.py [--world 8] [--batch 256] [--names 4] [--steps 4] [--one-gpu]
+    python tools/shard_probe.py [--world 8] [--batch 256] [--names 4] [--steps 4] [--one-gpu] [--pairs]
 
 All `world` ranks of a tslam_group (copy transport) on this GPU with TSLAM_SHARD_SERIAL |
 TSLAM_SHARD_PROFILE: every kernel and copy of every rank runs alone on one stream and is timed
@@ -11,7 +11,8 @@ without the device copies standing in for RCCL, run one after another), then ran
 step alone on the GPU (TSLAM_SHARD_SOLO | TSLAM_SHARD_PIPELINE: front end of batch s+1 beside the
 back end of batch s, exchanges skipped) — the N-GPU step when the exchange is hidden —
 the bytes one rank sends per step, and (--one-gpu) the one-GPU step of the same rig and batch
-through the pipelined single handle for the ratio.
+through the pipelined single handle for the ratio.  --pairs runs the pair split (TSLAM_SHARD_PAIRS:
+one camera per rank, the partner's images only, pair blocks to the rig ranges).
 """
 
 from __future__ import annotations
@@ -37,6 +38,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--one-gpu", action="store_true", help="also time the one-GPU pipelined step (bench run_single)")
     ap.add_argument("--refine-block", type=int, default=0, help="tslam_params.refine_block (0 = the library's choice)")
+    ap.add_argument("--pairs", action="store_true", help="TSLAM_SHARD_PAIRS (world = 2 x names)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     import torch
@@ -58,10 +60,11 @@ def main() -> None:
         if len(rects) > 1:
             h.set_rig(E)
     grp = HandleGroup(hs, "copy")
-    hs[0].shard_options(serial=True)
+    pairs = args.pairs
+    hs[0].shard_options(serial=True, pairs=pairs)
     grp.submit([p[0].data_ptr() for p in parts], B)   # warm-up
     torch.cuda.synchronize()
-    hs[0].shard_options(serial=True, profile=True)
+    hs[0].shard_options(serial=True, profile=True, pairs=pairs)
     for s in range(1, args.steps + 1):
         grp.submit([p[s * B].data_ptr() for p in parts], B)
     torch.cuda.synchronize()
@@ -70,7 +73,7 @@ def main() -> None:
     # rank 0 alone on the GPU, pipelined (TSLAM_SHARD_SOLO | TSLAM_SHARD_PIPELINE): its front end
     # of batch s + 1 beside its back end of batch s on the driver's own streams, no exchange — the
     # per-GPU step of an N-GPU node whose exchange is hidden
-    hs[0].shard_options(solo=True, pipeline=True)
+    hs[0].shard_options(solo=True, pipeline=True, pairs=pairs)
     stream = torch.cuda.current_stream().cuda_stream
     grp.submit([p[0].data_ptr() for p in parts], B, [stream] * W)
     torch.cuda.synchronize()
@@ -80,13 +83,23 @@ def main() -> None:
     torch.cuda.synchronize()
     solo_us = (time.perf_counter() - t0) / args.steps * 1e6
     sb, pr = hs[0].exchange_sizes()
-    fr = B // W + 1   # frames a rank reads of each peer's cameras
-    sent = {"raw_images": (W - 1) * fr * S * 640 * 400, "stream_blocks": (W - 1) * fr * S * sb,
-            "pose_records": (B // W) * pr}
+    if pairs:   # rank 0: its camera of the partner's half + 1 frame; its pair's blocks of the other rig ranges of its half
+        pb, hf = hs[0].pair_block_bytes(), B - B // 2 + 1
+        sent = {"raw_images": hf * 640 * 400, "stream_blocks": hf * sb,
+                "pair_blocks": (W // 2 - 1) * (B // W) * pb if len(rects) > 1 else 0, "pose_records": (B // W) * pr}
+        largest = hf * (640 * 400 + sb)
+    else:
+        fr = B // W + 1   # frames a rank reads of each peer's cameras
+        sent = {"raw_images": (W - 1) * fr * S * 640 * 400, "stream_blocks": (W - 1) * fr * S * sb,
+                "pose_records": (B // W) * pr}
+        largest = fr * S * (640 * 400 + sb)
+    sent["total"] = sum(sent.values())
+    sent["largest_to_one_peer"] = largest
     grp.close()
     for h in hs:
         h.close()
     out = {"world": W, "batch": B, "streams": C, "stereo_pairs": len(rects), "driver": "library (copy, serial)",
+           "layout": "pair split (TSLAM_SHARD_PAIRS)" if pairs else "frame ranges",
            "us_per_step_per_rank": per_rank, "per_gpu_compute_us": max(compute),
            "per_gpu_compute_us_by_rank": compute, "bytes_sent_per_rank_per_step": sent,
            "rank0_pipelined_step_us": solo_us}
