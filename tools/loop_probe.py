@@ -22,6 +22,8 @@ def main() -> None:
     ap.add_argument("--kind", default="c2")
     ap.add_argument("--profile", action="store_true", help="cProfile the timed loop (top entries by own time)")
     ap.add_argument("--trace", type=int, default=1, help="record the loop trace (0: as deployed)")
+    ap.add_argument("--sort", default="tottime", help="cProfile sort key (tottime, cumulative)")
+    ap.add_argument("--callees", default="", help="also print the callees of functions matching this name")
     args = ap.parse_args()
     import bench
     from thor_slam_amd.camera import CameraRig, Extrinsics
@@ -94,7 +96,10 @@ def main() -> None:
         import pstats
 
         prof.disable()
-        pstats.Stats(prof).sort_stats("tottime").print_stats(30)
+        st = pstats.Stats(prof).sort_stats(args.sort)
+        st.print_stats(30)
+        if args.callees:
+            st.print_callees(args.callees)
     lp = eng._loop
     print(f"{args.kind}: {args.frames / dt:.0f} frames/s, {len(lp.frames)} keyframes, {len(lp.loops)} loops, "
           f"state {eng.get_tracking_state().name}, async {eng._async}, imu {eng._imu is not None}")
